@@ -1,0 +1,259 @@
+#!/usr/bin/env python3
+"""Benchmark of the YA_VO front-end hot path on MI355X (BASELINE.json configs[1]).
+
+A step = one pass of the hot path over one resident batch of B synthetic 1241x376 stereo frames per GPU:
+for every frame, FAST-12 + Harris + top-2000 and blur + BRIEF on the left and right images, Hamming
+matching L_{k-1} -> L_k (the reference's temporal matchFeatures, src/LoopHandler.cc:189,534) and L_k -> R_k
+(stereo), and removeOutliers(20) on both match lists.  `value` = stereo frames per second over all GPUs
+(max-over-ranks wall time).  One process per GPU; frames shard across ranks (weak scaling, no collective
+in the data path).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames B]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+H, W = 376, 1241
+MAX_KP = 2000
+METRIC = "frames/sec (detect+describe+match+PnP) on 1241×376 KITTI stereo; RMSE vs CPU ref"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-op/s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=64, help="stereo frames per step per GPU")
+    ap.add_argument("--cpu-baseline", choices=["both", "literal", "efficient", "none"], default="both")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-timing", action="store_true", help="do not record per-stage HIP events")
+    return ap.parse_args()
+
+
+def stage_bytes(counts, B):
+    """Algorithmic HBM bytes per launch of each stage (DESIGN.md 'Algorithmic bytes')."""
+    img = H * W
+    n_img = 2 * B
+    cand = float(np.sum(counts["cand"][:n_img]))
+    det = float(np.sum(counts["det"][:n_img]))
+    kp = float(np.sum(counts["kp"][:n_img]))
+    nq = float(np.sum(counts["match"]))
+    nf = float(np.sum(counts["filt"]))
+    return {
+        # image read once, candidate keys (8 B) appended
+        "fast_harris": n_img * img + 8 * cand,
+        # image read once, blurred image written once
+        "blur": 2 * n_img * img,
+        # candidate keys read once; (row, col) + response + kp_src written
+        "topk": 8 * cand + 12 * det + 16 * kp,
+        # blurred image read once; 48-B KeyPoint + 32-B descriptor written per keypoint
+        "brief": n_img * img + 80 * kp,
+        # query + train descriptors read, 4-B match key written per query
+        "match": 2 * 32 * nq + 4 * nq,
+        # keys + query records read, 100-B Matches written (all + filtered)
+        "finalize": (4 + 48) * nq + 100 * (nq + nf),
+    }
+
+
+def stage_valu_ops(counts, B):
+    """Algorithmic lane-operations of the VALU-bound stages (for the VALU roofline in DESIGN.md)."""
+    n_img = 2 * B
+    px = n_img * (H - 8) * (W - 8)
+    kq = counts["match"].astype(np.float64)
+    # matcher: per (query, train) pair 8 xor + 8 popcount-accumulate + key build + min = 18 ops
+    kt = counts["train"].astype(np.float64)
+    return {"fast_harris": px * 60.0, "match": float(np.sum(kq * kt)) * 18.0}
+
+
+def cpu_baseline(kind, threads, offsets):
+    """Oracle (CPU restatement of the reference) on the GPU box's host cores, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind
+    from ya_vo_amd.synth import synth_stereo_batch
+    orc = oracle_bind.Oracle()
+
+    def one_frame(imgs, prev_left_kp, mode):
+        kps = []
+        for img in imgs:
+            rc, _, _ = orc.fast(img, MAX_KP, mode=mode)
+            kps.append(orc.brief(img, rc, offsets))
+        for q, t in ((prev_left_kp, kps[0]), (kps[0], kps[1])):
+            orc.remove_outliers(orc.match(q, t), 20)
+        return kps[0]
+
+    res = {}
+    if kind in ("both", "literal"):
+        imgs = synth_stereo_batch(4242, 2)
+        prev = orc.brief(imgs[0], orc.fast(imgs[0], MAX_KP)[0], offsets)
+        t0 = time.perf_counter()
+        one_frame(imgs[2:4], prev, 0)
+        dt = time.perf_counter() - t0
+        res["literal"] = {"value": 1.0 / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+                          "sample": "1 synthetic 1241x376 stereo frame (detect+describe L,R; match L0->L1, "
+                                    "L1->R1; removeOutliers), ref-literal costs: per-pixel ring rebuild, three "
+                                    "whole-image products per corner (src/FastDetector.cc:249-251), bit-loop "
+                                    "popcount; single thread", "seconds": dt}
+    if kind in ("both", "efficient"):
+        from concurrent.futures import ThreadPoolExecutor
+        nfr = 2 * threads
+        imgs = synth_stereo_batch(4243, nfr + 1)
+        lefts = [orc.brief(imgs[2 * k], orc.fast(imgs[2 * k], MAX_KP)[0], offsets) for k in range(nfr)]
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL inside the oracle
+            list(ex.map(lambda k: one_frame(imgs[2 * k + 2:2 * k + 4], lefts[k], 1), range(nfr)))
+        dt = time.perf_counter() - t0
+        res["efficient"] = {"value": nfr / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+                            "sample": f"{nfr} synthetic stereo frames, same outputs with local Harris sums "
+                                      f"and a precomputed ring, {threads} threads over frames", "seconds": dt}
+    return res
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import ya_vo_amd as yv
+    from ya_vo_amd.synth import synth_stereo_batch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    offsets = np.fromfile(os.path.join(ROOT, "tests", "golden", "brief_offsets_mt19937_42.bin"), np.int8)
+    ctx = yv.Context(local_rank)
+    ctx.set_brief_offsets(offsets)
+    B = args.frames
+    n_img = 2 * B
+    # each rank owns a contiguous chunk of the sequence (frame sharding)
+    frames = synth_stereo_batch(1234 + rank, B, start=rank * B)
+    d_frames = torch.from_numpy(frames).to(dev)
+    batch = yv.Batch(ctx, n_img, H, W, MAX_KP, n_img)
+    carry = n_img
+    pairs = []
+    for k in range(B):
+        pairs.append((carry if k == 0 else 2 * (k - 1), 2 * k))  # temporal L_{k-1} -> L_k
+        pairs.append((2 * k, 2 * k + 1))                          # stereo L_k -> R_k
+    batch.set_pairs(pairs)
+
+    def step():
+        batch.run(d_frames.data_ptr(), n_img, W, H * W, 20, carry_from=2 * (B - 1))
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    if not args.no_timing:
+        batch.enable_timing(True)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    v = batch.view()
+    counts = {
+        "cand": ctx.download(v.cand_count, np.uint32, n_img + 1).astype(np.int64),
+        "det": ctx.download(v.det_count, np.int32, n_img + 1).astype(np.int64),
+        "kp": ctx.download(v.kp_count, np.int32, n_img + 1).astype(np.int64),
+        "match": ctx.download(v.match_count, np.int32, len(pairs)).astype(np.int64),
+        "filt": ctx.download(v.filt_count, np.int32, len(pairs)).astype(np.int64),
+    }
+    counts["train"] = np.array([counts["kp"][t] for _, t in pairs], np.int64)
+
+    stages = {}
+    roofline = None
+    if not args.no_timing:
+        ms, nruns = batch.stage_times()
+        per_launch_ms = {name: float(ms[i]) / max(nruns, 1) for i, name in enumerate(yv.STAGE_NAMES)}
+        stages = {k: round(x, 4) for k, x in per_launch_ms.items()}
+        nbytes = stage_bytes(counts, B)
+        dom = max(per_launch_ms, key=per_launch_ms.get)
+        dur_s = per_launch_ms[dom] / 1e3
+        achieved = nbytes[dom] / dur_s / 1e9
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            try:
+                pmc = json.load(open(pmc_path))
+                if pmc.get("frames_per_step") == B:
+                    traffic = pmc.get("per_launch_bytes", {}).get(dom)
+            except (OSError, ValueError):
+                traffic = None
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "algorithmic_bytes_per_launch": int(nbytes[dom]), "launch_ms": round(per_launch_ms[dom], 4)}
+        ops = stage_valu_ops(counts, B)
+        if dom in ops:
+            tops = ops[dom] / dur_s / 1e12
+            roofline["valu"] = {"achieved": round(tops, 3), "peak": round(VALU_PEAK_TOPS, 1), "unit": "T lane-op/s",
+                                "frac": round(tops / VALU_PEAK_TOPS, 4)}
+
+    frames_total = B * world * args.steps
+    value = frames_total / elapsed
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": "configs[1]: FAST+BRIEF+Hamming match, 1241x376 synthetic stereo, 2000 kp/image "
+                               "(no PnP stage: that is configs[2])",
+                   "H": H, "W": W, "max_kp": MAX_KP, "frames_per_step_per_gpu": B, "images_per_frame": 2,
+                   "match_pairs_per_frame": 2, "parallelism": f"frame-sharded x{world}, no collective",
+                   "mean_candidates_per_image": round(float(np.mean(counts["cand"][:n_img])), 1),
+                   "mean_keypoints_per_image": round(float(np.mean(counts["kp"][:n_img])), 1),
+                   "mean_filtered_matches_per_pair": round(float(np.mean(counts["filt"])), 1)},
+        "stages_ms_per_launch": stages,
+        "roofline": roofline,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline != "none":
+        cb = cpu_baseline(args.cpu_baseline, args.cpu_threads, offsets.reshape(256, 4))
+        main_cb = cb.get("literal") or cb.get("efficient")
+        out["cpu_baseline"] = main_cb
+        if "efficient" in cb and main_cb is not cb["efficient"]:
+            out["cpu_baseline_efficient"] = cb["efficient"]
+        out["cpu_baseline_host_cpus"] = os.cpu_count()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    batch.close()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,133 @@
+/*
+ * yavo.h -- C ABI of the MI355X-native YA_VO front end (libyavo.so, gfx950).
+ *
+ * Drop-in boundary for the reference's per-frame hot path.  Each host-pointer entry point replaces one
+ * reference member function (cited below) with the same argument meaning; results are bit-identical
+ * to the reference's integer arithmetic (FAST indices, BRIEF bits, Hamming matches) and follow the
+ * reference's float arithmetic operation-for-operation where it has one.
+ *
+ * Conventions:
+ *   - plain C, no exceptions cross the boundary; every call returns YV_OK (0) or a negative status;
+ *   - caller-allocated output buffers, capacities passed in, counts returned through out-pointers;
+ *   - one yv_ctx per thread and per GPU (not thread-shared); all work is issued on the ctx's HIP stream
+ *     unless a stream is passed explicitly;
+ *   - coordinates follow the reference: x / rc[2i] = ROW, y / rc[2i+1] = COLUMN.
+ *
+ * There is no CPU fallback: without a usable gfx950 device every compute entry point returns
+ * YV_ERR_NODEVICE.
+ */
+#ifndef YAVO_H
+#define YAVO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "yavo_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YV_OK 0
+#define YV_ERR_INVALID (-1)   /* bad argument (null pointer, bad size, capacity too small) */
+#define YV_ERR_HIP (-2)       /* HIP runtime error */
+#define YV_ERR_NODEVICE (-3)  /* no usable GPU */
+#define YV_ERR_CAPACITY (-4)  /* request exceeds the batch / context capacity */
+
+#define YV_ABI_VERSION 1
+
+typedef struct yv_ctx yv_ctx;
+typedef struct yv_batch yv_batch;
+
+/* ---- library / context ------------------------------------------------------------------------ */
+int yv_abi_version(void);
+const char* yv_status_string(int status);
+/* Number of visible HIP devices (0 when none); never fails. */
+int yv_device_count(void);
+/* Create a context on `device`: a HIP stream, default parameters (FAST threshold 40, 2000 corners,
+ * the 9x9/sigma 2.5 fixed-point blur kernel, an all-zero BRIEF offset table until set). */
+int yv_create(int device, yv_ctx** out);
+void yv_destroy(yv_ctx* ctx);
+/* The stream all yv_* calls on this context use (hipStream_t as void*). */
+void* yv_stream(yv_ctx* ctx);
+/* Block until all work queued on the context stream has finished. */
+int yv_sync(yv_ctx* ctx);
+/* Synchronous copies between host memory and device memory (e.g. a yv_batch_view array) on the
+ * context stream. */
+int yv_download(yv_ctx* ctx, void* host_dst, const void* dev_src, size_t bytes);
+int yv_upload(yv_ctx* ctx, void* dev_dst, const void* host_src, size_t bytes);
+
+/* FastDetector constructor constants (include/FastDetector.hpp:32-38): intensityThreshold (40) and
+ * fastCornerNumThreshold (2000). */
+int yv_set_fast_params(yv_ctx* ctx, int intensity_threshold, int max_corners);
+/* Brief offsets table (src/BriefDescriptor.cc:4-20): 256 rows of {drow1, dcol1, drow2, dcol2},
+ * each in [-8, 8]. */
+int yv_set_brief_offsets(yv_ctx* ctx, const int8_t* offsets /* [256*4] */);
+/* 9-tap fixed-point Gaussian (8 fractional bits, sum 256) used in place of cv::GaussianBlur
+ * (src/BriefDescriptor.cc:90).  Default = OpenCV's bit-exact 9 / 2.5 kernel {12,22,31,41,44,...}. */
+int yv_set_blur_kernel(yv_ctx* ctx, const uint16_t* k9);
+
+/* ---- host-pointer drop-in entry points (synchronous) --------------------------------------------- */
+/* FastDetector::getFastFeatures (src/FastDetector.cc:277-369; include/FastDetector.hpp:48).
+ * img: H x W u8, row stride `stride` bytes.  Writes up to max_kp (row, col) pairs into rc[2*max_kp] in
+ * response-descending order (ties: row-major index ascending) and their Harris responses into resp
+ * (may be NULL).  *n = number written, *n_candidates (may be NULL) = corners before the top-K cut. */
+int yv_detect(yv_ctx* ctx, const uint8_t* img, int H, int W, int stride, int max_kp, int32_t* rc,
+              float* resp, int* n, int* n_candidates);
+/* Brief::computeBrief (src/BriefDescriptor.cc:86-124; include/BriefDescriptor.hpp:61): blur, keep the
+ * points inside checkBoundry (:128-136), emit KeyPoint records (id = input index).  out capacity n. */
+int yv_describe(yv_ctx* ctx, const uint8_t* img, int H, int W, int stride, const int32_t* rc, int n,
+                yv_keypoint* out, int* n_out);
+/* Brief::matchFeatures (src/BriefDescriptor.cc:163-183; include/BriefDescriptor.hpp:62): for every
+ * query the first train point at minimum Hamming distance.  out capacity nq. */
+int yv_match_features(yv_ctx* ctx, const yv_keypoint* q, int nq, const yv_keypoint* t, int nt, yv_match* out);
+/* Brief::removeOutliers (src/BriefDescriptor.cc:213-231; include/BriefDescriptor.hpp:64). */
+int yv_filter_matches(yv_ctx* ctx, const yv_match* in, int n, int thr, yv_match* out, int* n_out);
+
+/* ---- batched device pipeline (inputs resident in HBM) ---------------------------------------------- */
+/* A batch owns device workspace for up to max_images images of H x W and max_pairs match pairs.  Slot
+ * index max_images is the "carry" slot: it holds the keypoints / descriptors of one image of the
+ * previous run (see yv_batch_run's carry_from), so consecutive runs chain frame k-1 -> k. */
+int yv_batch_create(yv_ctx* ctx, int max_images, int H, int W, int max_kp, int max_pairs,
+                    yv_batch** out);
+void yv_batch_destroy(yv_batch* b);
+/* Match pairs (query image, train image) for subsequent runs; indices in [0, max_images] (max_images =
+ * carry slot).  Copied to the device once. */
+int yv_batch_set_pairs(yv_batch* b, const int32_t* pairs /* [2*n_pairs] */, int n_pairs);
+/* Run detect -> describe -> match -> removeOutliers for n_images device images
+ *   image i at d_images + i*image_pitch, rows `stride` bytes apart,
+ * then copy image carry_from's keypoints into the carry slot (carry_from < 0: no copy).  Asynchronous
+ * on `stream` (NULL = the context stream).  match_thr is removeOutliers' threshold (20 in
+ * src/LoopHandler.cc:192,537). */
+int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride, int64_t image_pitch,
+                 int match_thr, int carry_from, void* stream);
+/* Per-stage device time of the runs since the last reset, when timing is enabled (HIP events recorded
+ * on the run stream around every stage).  Stages: 0 fast+harris, 1 blur, 2 top-K, 3 brief, 4 match,
+ * 5 finalize+filter.  ms[i] = summed milliseconds, *n_runs = runs accumulated. */
+int yv_batch_enable_timing(yv_batch* b, int on);
+int yv_batch_stage_times(yv_batch* b, float* ms /* [8] */, int* n_runs);
+#define YV_NUM_STAGES 6
+
+/* Device views of the batch results (valid until the next run / destroy).  All arrays are indexed
+ * [slot][...] with the per-slot strides given. */
+typedef struct yv_batch_view {
+    int max_images, max_kp, max_pairs, H, W;
+    int64_t cand_cap;                 /* candidate capacity per image = (H-8)*(W-8) */
+    const uint32_t* cand_count;       /* [max_images+1]: FAST corners before the cut */
+    const int32_t* det_count;         /* [max_images+1]: min(corners, max_kp) */
+    const int32_t* det_rc;            /* [max_images+1][max_kp][2] (row, col), response order */
+    const float* det_resp;            /* [max_images+1][max_kp] */
+    const int32_t* kp_count;          /* [max_images+1]: keypoints that passed checkBoundry */
+    const yv_keypoint* keypoints;     /* [max_images+1][max_kp] */
+    const uint8_t* blurred;           /* [max_images][H*W] */
+    const int32_t* match_count;       /* [max_pairs]: = kp_count of the query image */
+    const yv_match* matches;          /* [max_pairs][max_kp] */
+    const int32_t* filt_count;        /* [max_pairs] */
+    const yv_match* filtered;         /* [max_pairs][max_kp] */
+} yv_batch_view;
+int yv_batch_view_get(yv_batch* b, yv_batch_view* view);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YAVO_H */

@@ -1,0 +1,83 @@
+/*
+ * yavo_oracle.h -- CPU restatement of the YA_VO per-frame hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the parity checker for the HIP path: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.  The product library
+ * (ya_vo_amd/lib/libyavo.so) never links, calls or falls back to it.
+ *
+ * Every function restates the reference's arithmetic literally (file:line cited at each definition in
+ * yavo_oracle.c / yavo_oracle_geom.c).  The reference itself cannot be compiled here (OpenCV, Eigen,
+ * Sophus, g2o, jsoncpp, Boost, Pangolin absent), so the third-party arithmetic it calls
+ * (cv::eigen, cv::GaussianBlur, cv::SVD, Eigen JacobiSVD/LDLT, Sophus exp, g2o LM) is restated from the
+ * published algorithms and named per function.  Pinned by: the reference's ring fixture
+ * (tests/testBresenham.png), the contiguity tests (tests/FastDetectorTest.cc:38-80) and the calib parser
+ * test (tests/UtilsTest.cc:4-15).  Everything past the FAST candidate test is "parity unpinned" against
+ * the real reference binary (no fixtures exist for it); see DESIGN.md.
+ */
+#ifndef YAVO_ORACLE_H
+#define YAVO_ORACLE_H
+
+#include <stdint.h>
+#include "../include/yavo/yavo_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- FAST ring / candidate test (src/FastDetector.cc) ---- */
+/* Literal Bresenham ring with the reference's two std::set orderings (src/FastDetector.cc:50-112).
+ * out[k][0] = row, out[k][1] = col (absolute), k = 0..15. */
+void or_bresenham_ring(int xc, int yc, int out[16][2]);
+/* checkContiguousPixels (src/FastDetector.cc:135-153) with checkInBetween (:155-161). */
+int or_check_contiguous(uint8_t cent, const int ring[16][2], const uint8_t* img, int stride, int thr);
+
+/* getFastFeatures (src/FastDetector.cc:277-369).  mode 0 = literal costs (per-pixel ring rebuild, three
+ * full-image products per corner); mode 1 = same outputs, local arithmetic.  Writes up to max_kp
+ * (row, col) pairs + responses in output order, *n = count, *n_cand = corners before the cut.
+ * cand_idx/cand_resp (optional, may be NULL, capacity cand_cap) receive the unsorted candidate list in
+ * scan order. */
+int or_fast_detect(const uint8_t* img, int H, int W, int stride, int thr, int max_kp, int mode,
+                   int32_t* rc, float* resp, int* n, int* n_cand,
+                   int32_t* cand_idx, float* cand_resp, int cand_cap);
+
+/* Harris response from the 3x3-summed structure tensor (src/FastDetector.cc:244-273). */
+float or_harris_response(float m00, float m01, float m11);
+/* OpenCV JacobiImpl_<float> eigenvalues (descending), the cv::eigen path without HAVE_EIGEN. */
+void or_eigen_jacobi_f32(const float* A, int n, float* w);
+
+/* ---- Gaussian blur (cv::GaussianBlur(img, out, Size(9,9), 2.5, 2.5): src/BriefDescriptor.cc:90) ---- */
+/* Bit-exact 8U fixed-point kernel: error-diffusion rounding (ed=1, OpenCV >= 3.4 bit-exact path) or
+ * plain rounding (ed=0).  out has n entries summing to 256. */
+void or_gauss_kernel_fixed(int n, double sigma, int ed, uint16_t* out);
+/* Separable 8U fixed-point blur with BORDER_REFLECT_101; out is H x W contiguous. */
+void or_gaussian_blur_u8(const uint8_t* img, int H, int W, int stride, const uint16_t* k, int n,
+                         uint8_t* out);
+
+/* ---- BRIEF (src/BriefDescriptor.cc) ---- */
+/* Brief::computeBrief (:86-124) on an already blurred H x W contiguous image.  offsets: 256 x 4 int8
+ * (o0=drow1, o1=dcol1, o2=drow2, o3=dcol2).  Reads past the buffer end return 0 (reference: UB). */
+int or_compute_brief_blurred(const uint8_t* blur, int H, int W, const int8_t* offsets,
+                             const int32_t* rc, int n, yv_keypoint* out, int* n_out);
+/* Blur + describe, i.e. the whole computeBrief call. */
+int or_compute_brief(const uint8_t* img, int H, int W, int stride, const uint16_t* k9,
+                     const int8_t* offsets, const int32_t* rc, int n, yv_keypoint* out, int* n_out);
+/* Brief::preComputeOffsets (:4-20) with an explicit seed instead of std::random_device:
+ * std::mt19937(seed) + uniform_int_distribution<int>(-8, 8) (libstdc++ algorithm). */
+void or_brief_offsets_mt19937(uint32_t seed, int8_t* out /* 1024 */);
+
+/* Brief::popCount (:151-160) / hammingDistance (:139-146). */
+int or_hamming(const uint8_t* a, const uint8_t* b);
+/* Brief::matchFeatures (:163-183).  out has nq records. */
+int or_match(const yv_keypoint* q, int nq, const yv_keypoint* t, int nt, yv_match* out);
+/* Brief::removeOutliers (:213-231). */
+int or_remove_outliers(const yv_match* in, int n, int thr, yv_match* out, int* n_out);
+
+/* ---- utils ---- */
+/* parseCalibString (src/Utils.cc:4-28): reads the numbers after the "Pn:" tag into a row-major
+ * 4x4 (missing values -> 0; the reference reads past a 12-value vector). returns #values parsed. */
+int or_parse_calib_string(const char* s, double out[16]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

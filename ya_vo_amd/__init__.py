@@ -1,0 +1,245 @@
+"""ya_vo_amd -- MI355X-native YA_VO visual-odometry front end (detect / describe / match hot path).
+
+The product is libyavo.so (gfx950 HIP kernels behind the C ABI in include/yavo/yavo.h).  This module is
+a thin ctypes binding plus a Python mirror of the reference's operator classes (FastDetector, Brief; see
+ya_vo_amd/frontend.py).  There is no CPU fallback: if the library or a GPU is missing, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libyavo.so")
+
+YV_OK = 0
+YV_ERR_INVALID = -1
+YV_ERR_HIP = -2
+YV_ERR_NODEVICE = -3
+YV_ERR_CAPACITY = -4
+YV_NUM_STAGES = 6
+STAGE_NAMES = ("fast_harris", "blur", "topk", "brief", "match", "finalize")
+
+# byte-identical to KeyPoint (48 B) / Matches (100 B), /root/reference/include/BriefDescriptor.hpp:11-39
+KEYPOINT_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("id", "<i4"), ("matched", "u1"),
+                           ("featVec", "u1", (32,)), ("_pad", "u1", (3,))])
+MATCH_DTYPE = np.dtype([("pt1", KEYPOINT_DTYPE), ("pt2", KEYPOINT_DTYPE), ("distance", "<i4")])
+assert KEYPOINT_DTYPE.itemsize == 48 and MATCH_DTYPE.itemsize == 100
+
+# cv::GaussianBlur(Size(9, 9), 2.5) 8U fixed-point kernel (src/BriefDescriptor.cc:90)
+DEFAULT_BLUR_KERNEL = np.array([12, 22, 31, 41, 44, 41, 31, 22, 12], dtype=np.uint16)
+
+
+class YavoError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"{what}: yavo status {status}")
+
+
+class _BatchView(ctypes.Structure):
+    _fields_ = [("max_images", ctypes.c_int), ("max_kp", ctypes.c_int), ("max_pairs", ctypes.c_int),
+                ("H", ctypes.c_int), ("W", ctypes.c_int), ("cand_cap", ctypes.c_int64),
+                ("cand_count", ctypes.c_void_p), ("det_count", ctypes.c_void_p), ("det_rc", ctypes.c_void_p),
+                ("det_resp", ctypes.c_void_p), ("kp_count", ctypes.c_void_p), ("keypoints", ctypes.c_void_p),
+                ("blurred", ctypes.c_void_p), ("match_count", ctypes.c_void_p), ("matches", ctypes.c_void_p),
+                ("filt_count", ctypes.c_void_p), ("filtered", ctypes.c_void_p)]
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+# symbol -> (restype, argtypes); the same list the C header declares (tests check they all resolve)
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+SIGNATURES = {
+    "yv_abi_version": (_I, []),
+    "yv_status_string": (ctypes.c_char_p, [_I]),
+    "yv_device_count": (_I, []),
+    "yv_create": (_I, [_I, ctypes.POINTER(_P)]),
+    "yv_destroy": (None, [_P]),
+    "yv_stream": (_P, [_P]),
+    "yv_sync": (_I, [_P]),
+    "yv_download": (_I, [_P, _P, _P, ctypes.c_size_t]),
+    "yv_upload": (_I, [_P, _P, _P, ctypes.c_size_t]),
+    "yv_set_fast_params": (_I, [_P, _I, _I]),
+    "yv_set_brief_offsets": (_I, [_P, _P]),
+    "yv_set_blur_kernel": (_I, [_P, _P]),
+    "yv_detect": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "yv_describe": (_I, [_P, _P, _I, _I, _I, _P, _I, _P, ctypes.POINTER(_I)]),
+    "yv_match_features": (_I, [_P, _P, _I, _P, _I, _P]),
+    "yv_filter_matches": (_I, [_P, _P, _I, _I, _P, ctypes.POINTER(_I)]),
+    "yv_batch_create": (_I, [_P, _I, _I, _I, _I, _I, ctypes.POINTER(_P)]),
+    "yv_batch_destroy": (None, [_P]),
+    "yv_batch_set_pairs": (_I, [_P, _P, _I]),
+    "yv_batch_run": (_I, [_P, _P, _I, _I, ctypes.c_int64, _I, _I, _P]),
+    "yv_batch_enable_timing": (_I, [_P, _I]),
+    "yv_batch_stage_times": (_I, [_P, _P, ctypes.POINTER(_I)]),
+    "yv_batch_view_get": (_I, [_P, ctypes.POINTER(_BatchView)]),
+}
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libyavo.so (built by __graft_entry__.build()).  Raises if it is missing: no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(status: int, what: str) -> None:
+    if status != YV_OK:
+        raise YavoError(status, what)
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class Context:
+    """One yv_ctx: a GPU, a HIP stream and the algorithm constants."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        _check(self.lib.yv_create(device, ctypes.byref(h)), f"yv_create(device={device})")
+        self.handle = h
+        self.device = device
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.yv_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return self.lib.yv_stream(self.handle) or 0
+
+    def sync(self) -> None:
+        _check(self.lib.yv_sync(self.handle), "yv_sync")
+
+    def download(self, dev_ptr: int, dtype, count: int) -> np.ndarray:
+        """Copy `count` elements of `dtype` from device memory to a new host array."""
+        out = np.zeros(max(count, 1), dtype=dtype)
+        nbytes = out.dtype.itemsize * count
+        _check(self.lib.yv_download(self.handle, _ptr(out), ctypes.c_void_p(dev_ptr), nbytes), "yv_download")
+        return out[:count]
+
+    def upload(self, dev_ptr: int, host: np.ndarray) -> None:
+        h = np.ascontiguousarray(host)
+        _check(self.lib.yv_upload(self.handle, ctypes.c_void_p(dev_ptr), _ptr(h), h.nbytes), "yv_upload")
+
+    def set_fast_params(self, intensity_threshold: int = 40, max_corners: int = 2000) -> None:
+        _check(self.lib.yv_set_fast_params(self.handle, intensity_threshold, max_corners), "yv_set_fast_params")
+
+    def set_brief_offsets(self, offsets: np.ndarray) -> None:
+        o = np.ascontiguousarray(offsets, dtype=np.int8).reshape(256, 4)
+        _check(self.lib.yv_set_brief_offsets(self.handle, _ptr(o)), "yv_set_brief_offsets")
+
+    def set_blur_kernel(self, k9: np.ndarray) -> None:
+        k = np.ascontiguousarray(k9, dtype=np.uint16).reshape(9)
+        _check(self.lib.yv_set_blur_kernel(self.handle, _ptr(k)), "yv_set_blur_kernel")
+
+    # ---- host-pointer drop-in calls ----
+    def detect(self, img: np.ndarray, max_kp: int = 2000) -> Tuple[np.ndarray, np.ndarray, int]:
+        """FastDetector::getFastFeatures -> (rc [n,2] int32 (row, col), resp [n] float32, n_candidates)."""
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        H, W = img.shape
+        rc = np.zeros((max(max_kp, 1), 2), np.int32)
+        resp = np.zeros(max(max_kp, 1), np.float32)
+        n, nc = ctypes.c_int(), ctypes.c_int()
+        _check(self.lib.yv_detect(self.handle, _ptr(img), H, W, W, max_kp, _ptr(rc), _ptr(resp), ctypes.byref(n),
+                                  ctypes.byref(nc)), "yv_detect")
+        return rc[:n.value].copy(), resp[:n.value].copy(), nc.value
+
+    def describe(self, img: np.ndarray, rc: np.ndarray) -> np.ndarray:
+        """Brief::computeBrief -> KEYPOINT_DTYPE array (points inside checkBoundry)."""
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        H, W = img.shape
+        rc = np.ascontiguousarray(rc, dtype=np.int32).reshape(-1, 2)
+        out = np.zeros(max(len(rc), 1), KEYPOINT_DTYPE)
+        m = ctypes.c_int()
+        _check(self.lib.yv_describe(self.handle, _ptr(img), H, W, W, _ptr(rc), len(rc), _ptr(out), ctypes.byref(m)),
+               "yv_describe")
+        return out[:m.value].copy()
+
+    def match_features(self, q: np.ndarray, t: np.ndarray) -> np.ndarray:
+        """Brief::matchFeatures -> MATCH_DTYPE array (one per query)."""
+        q = np.ascontiguousarray(q, dtype=KEYPOINT_DTYPE)
+        t = np.ascontiguousarray(t, dtype=KEYPOINT_DTYPE)
+        out = np.zeros(max(len(q), 1), MATCH_DTYPE)
+        _check(self.lib.yv_match_features(self.handle, _ptr(q), len(q), _ptr(t), len(t), _ptr(out)),
+               "yv_match_features")
+        return out[:len(q)].copy()
+
+    def filter_matches(self, matches: np.ndarray, thr: int = 20) -> np.ndarray:
+        """Brief::removeOutliers -> MATCH_DTYPE array."""
+        m = np.ascontiguousarray(matches, dtype=MATCH_DTYPE)
+        out = np.zeros(max(len(m), 1), MATCH_DTYPE)
+        n = ctypes.c_int()
+        _check(self.lib.yv_filter_matches(self.handle, _ptr(m), len(m), thr, _ptr(out), ctypes.byref(n)),
+               "yv_filter_matches")
+        return out[:n.value].copy()
+
+
+class Batch:
+    """Device-resident batched pipeline (yv_batch): detect -> describe -> match -> removeOutliers."""
+
+    def __init__(self, ctx: Context, max_images: int, H: int, W: int, max_kp: int = 2000, max_pairs: int = 0):
+        self.ctx = ctx
+        self.lib = ctx.lib
+        h = ctypes.c_void_p()
+        _check(self.lib.yv_batch_create(ctx.handle, max_images, H, W, max_kp, max_pairs, ctypes.byref(h)),
+               "yv_batch_create")
+        self.handle = h
+        self.max_images, self.H, self.W, self.max_kp, self.max_pairs = max_images, H, W, max_kp, max_pairs
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.yv_batch_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_pairs(self, pairs) -> None:
+        p = np.ascontiguousarray(np.asarray(pairs, dtype=np.int32).reshape(-1, 2))
+        _check(self.lib.yv_batch_set_pairs(self.handle, _ptr(p), len(p)), "yv_batch_set_pairs")
+        self.n_pairs = len(p)
+
+    def run(self, d_images: int, n_images: int, stride: int, pitch: int, match_thr: int = 20, carry_from: int = -1,
+            stream: int = 0) -> None:
+        _check(self.lib.yv_batch_run(self.handle, ctypes.c_void_p(d_images), n_images, stride, pitch, match_thr,
+                                     carry_from, ctypes.c_void_p(stream) if stream else None), "yv_batch_run")
+
+    def enable_timing(self, on: bool = True) -> None:
+        _check(self.lib.yv_batch_enable_timing(self.handle, 1 if on else 0), "yv_batch_enable_timing")
+
+    def stage_times(self) -> Tuple[np.ndarray, int]:
+        ms = np.zeros(8, np.float32)
+        n = ctypes.c_int()
+        _check(self.lib.yv_batch_stage_times(self.handle, _ptr(ms), ctypes.byref(n)), "yv_batch_stage_times")
+        return ms[:YV_NUM_STAGES].copy(), n.value
+
+    def view(self) -> _BatchView:
+        v = _BatchView()
+        _check(self.lib.yv_batch_view_get(self.handle, ctypes.byref(v)), "yv_batch_view_get")
+        return v

@@ -1,0 +1,537 @@
+// yavo_api.hip -- the C ABI of libyavo.so (include/yavo/yavo.h): contexts, batches, the host-pointer
+// drop-in entry points and the batched device pipeline.  Host code only; kernels live in
+// yavo_kernels.hip.  No CPU fallback exists: every compute path runs the gfx950 kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/yavo/yavo.h"
+#include "yavo_internal.h"
+
+using yavo::Desc;
+
+struct yv_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int fast_thr = 40;         // include/FastDetector.hpp:35
+    int max_corners = 2000;    // include/FastDetector.hpp:36
+    uint16_t k9[9] = {12, 22, 31, 41, 44, 41, 31, 22, 12};  // cv::GaussianBlur 9x9, sigma 2.5, 8U
+    int8_t* d_offsets = nullptr;                              // [256*4]
+    yv_batch* single = nullptr;                               // workspace of the host-pointer API
+    int32_t* h_pinned = nullptr;                              // small pinned scratch for counts
+};
+
+struct yv_batch {
+    yv_ctx* ctx = nullptr;
+    int max_images = 0, H = 0, W = 0, max_kp = 0, max_pairs = 0, n_pairs = 0;
+    int64_t cap = 0;
+    int nslots = 0;
+    uint64_t* cand_keys = nullptr;
+    uint32_t* cand_count = nullptr;
+    uint32_t* cand_seen = nullptr;
+    int32_t* det_rc = nullptr;
+    float* det_resp = nullptr;
+    int32_t* det_count = nullptr;
+    int32_t* kp_src = nullptr;
+    int32_t* kp_count = nullptr;
+    yv_keypoint* keypoints = nullptr;
+    Desc* desc = nullptr;
+    uint8_t* blur = nullptr;
+    int32_t* pairs = nullptr;
+    uint32_t* match_key = nullptr;
+    yv_match* matches = nullptr;
+    int32_t* match_count = nullptr;
+    yv_match* filtered = nullptr;
+    int32_t* filt_count = nullptr;
+    uint8_t* staging = nullptr;  // one H x W input image (host-pointer API)
+    // stage timing
+    bool timing = false;
+    std::vector<hipEvent_t> events;  // (YV_NUM_STAGES + 1) per recorded run
+    int runs_recorded = 0;
+};
+
+namespace {
+
+constexpr int kEvPerRun = YV_NUM_STAGES + 1;
+constexpr int kMaxTimedRuns = 4096;
+
+#define YV_HIP(call)                                                                           \
+    do {                                                                                       \
+        hipError_t e_ = (call);                                                                \
+        if (e_ != hipSuccess) {                                                                \
+            std::fprintf(stderr, "yavo: %s failed: %s (%s:%d)\n", #call, hipGetErrorString(e_), \
+                         __FILE__, __LINE__);                                                  \
+            return YV_ERR_HIP;                                                                 \
+        }                                                                                      \
+    } while (0)
+
+int check_launch() {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "yavo: kernel launch failed: %s\n", hipGetErrorString(e));
+        return YV_ERR_HIP;
+    }
+    return YV_OK;
+}
+
+template <class T>
+int dalloc(T** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "yavo: hipMalloc(%zu B) failed: %s\n", count * sizeof(T), hipGetErrorString(e));
+        return YV_ERR_HIP;
+    }
+    return YV_OK;
+}
+
+void batch_free(yv_batch* b) {
+    if (!b) return;
+    void* ptrs[] = {b->cand_keys, b->cand_count, b->cand_seen, b->det_rc,   b->det_resp,    b->det_count, b->kp_src,
+                    b->kp_count,  b->keypoints,  b->desc,     b->blur,        b->pairs,     b->match_key,
+                    b->matches,   b->match_count, b->filtered, b->filt_count, b->staging};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (hipEvent_t e : b->events) (void)hipEventDestroy(e);
+    delete b;
+}
+
+int set_device(yv_ctx* ctx) {
+    YV_HIP(hipSetDevice(ctx->device));
+    return YV_OK;
+}
+
+// The host-pointer entry points share one single-image workspace per context.
+int ensure_single(yv_ctx* ctx, int H, int W) {
+    if (ctx->single && ctx->single->H == H && ctx->single->W == W) return YV_OK;
+    if (ctx->single) {
+        batch_free(ctx->single);
+        ctx->single = nullptr;
+    }
+    yv_batch* b = nullptr;
+    int rc = yv_batch_create(ctx, 1, H, W, yavo::kMaxKp, 1, &b);
+    if (rc != YV_OK) return rc;
+    const int32_t pair[2] = {0, 1};  // query = slot 0, train = slot 1 (the carry slot)
+    rc = yv_batch_set_pairs(b, pair, 1);
+    if (rc != YV_OK) {
+        batch_free(b);
+        return rc;
+    }
+    ctx->single = b;
+    return YV_OK;
+}
+
+int record_stage(yv_batch* b, hipStream_t s, int run, int stage) {
+    if (!b->timing || run < 0) return YV_OK;
+    YV_HIP(hipEventRecord(b->events[(size_t)run * kEvPerRun + stage], s));
+    return YV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int yv_abi_version(void) { return YV_ABI_VERSION; }
+
+const char* yv_status_string(int status) {
+    switch (status) {
+        case YV_OK: return "ok";
+        case YV_ERR_INVALID: return "invalid argument";
+        case YV_ERR_HIP: return "HIP runtime error";
+        case YV_ERR_NODEVICE: return "no usable GPU";
+        case YV_ERR_CAPACITY: return "capacity exceeded";
+        default: return "unknown status";
+    }
+}
+
+int yv_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int yv_create(int device, yv_ctx** out) {
+    if (!out) return YV_ERR_INVALID;
+    *out = nullptr;
+    int n = yv_device_count();
+    if (n <= 0) return YV_ERR_NODEVICE;
+    if (device < 0 || device >= n) return YV_ERR_INVALID;
+    yv_ctx* ctx = new (std::nothrow) yv_ctx();
+    if (!ctx) return YV_ERR_INVALID;
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return YV_ERR_HIP;
+    }
+    if (dalloc(&ctx->d_offsets, 1024) != YV_OK || hipMemset(ctx->d_offsets, 0, 1024) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&ctx->h_pinned), 64 * sizeof(int32_t)) != hipSuccess) {
+        yv_destroy(ctx);
+        return YV_ERR_HIP;
+    }
+    *out = ctx;
+    return YV_OK;
+}
+
+void yv_destroy(yv_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    batch_free(ctx->single);
+    if (ctx->d_offsets) (void)hipFree(ctx->d_offsets);
+    if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+void* yv_stream(yv_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
+
+int yv_sync(yv_ctx* ctx) {
+    if (!ctx) return YV_ERR_INVALID;
+    YV_HIP(hipStreamSynchronize(ctx->stream));
+    return YV_OK;
+}
+
+int yv_download(yv_ctx* ctx, void* host_dst, const void* dev_src, size_t bytes) {
+    if (!ctx || (bytes > 0 && (!host_dst || !dev_src))) return YV_ERR_INVALID;
+    if (bytes == 0) return YV_OK;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMemcpyAsync(host_dst, dev_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    YV_HIP(hipStreamSynchronize(ctx->stream));
+    return YV_OK;
+}
+
+int yv_upload(yv_ctx* ctx, void* dev_dst, const void* host_src, size_t bytes) {
+    if (!ctx || (bytes > 0 && (!host_src || !dev_dst))) return YV_ERR_INVALID;
+    if (bytes == 0) return YV_OK;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMemcpyAsync(dev_dst, host_src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    YV_HIP(hipStreamSynchronize(ctx->stream));
+    return YV_OK;
+}
+
+int yv_set_fast_params(yv_ctx* ctx, int intensity_threshold, int max_corners) {
+    if (!ctx || intensity_threshold < 0 || intensity_threshold > 255 || max_corners < 0 ||
+        max_corners > yavo::kMaxKp)
+        return YV_ERR_INVALID;
+    ctx->fast_thr = intensity_threshold;
+    ctx->max_corners = max_corners;
+    return YV_OK;
+}
+
+int yv_set_brief_offsets(yv_ctx* ctx, const int8_t* offsets) {
+    if (!ctx || !offsets) return YV_ERR_INVALID;
+    for (int i = 0; i < 1024; ++i)
+        if (offsets[i] < -8 || offsets[i] > 8) return YV_ERR_INVALID;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMemcpyAsync(ctx->d_offsets, offsets, 1024, hipMemcpyHostToDevice, ctx->stream));
+    YV_HIP(hipStreamSynchronize(ctx->stream));
+    return YV_OK;
+}
+
+int yv_set_blur_kernel(yv_ctx* ctx, const uint16_t* k9) {
+    if (!ctx || !k9) return YV_ERR_INVALID;
+    uint32_t sum = 0;
+    for (int i = 0; i < 9; ++i) sum += k9[i];
+    if (sum != 256u) return YV_ERR_INVALID;  // 8 fractional bits: the kernel must sum to 1.0
+    std::memcpy(ctx->k9, k9, sizeof(ctx->k9));
+    return YV_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// batches
+// ------------------------------------------------------------------------------------------------
+int yv_batch_create(yv_ctx* ctx, int max_images, int H, int W, int max_kp, int max_pairs, yv_batch** out) {
+    if (!ctx || !out || max_images <= 0 || H < 9 || W < 9 || max_kp <= 0 || max_kp > yavo::kMaxKp ||
+        max_pairs < 0 || (int64_t)H * W >= (1ll << 31))
+        return YV_ERR_INVALID;
+    *out = nullptr;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    yv_batch* b = new (std::nothrow) yv_batch();
+    if (!b) return YV_ERR_INVALID;
+    b->ctx = ctx;
+    b->max_images = max_images;
+    b->H = H;
+    b->W = W;
+    b->max_kp = max_kp;
+    b->max_pairs = max_pairs;
+    b->nslots = max_images + 1;
+    b->cap = (int64_t)(H - 8) * (W - 8);  // every pixel FAST can test: no candidate is ever dropped
+    const size_t ns = (size_t)b->nslots, nk = (size_t)max_kp, np = (size_t)std::max(max_pairs, 1);
+    int rc = YV_OK;
+    rc |= dalloc(&b->cand_keys, (size_t)max_images * (size_t)b->cap);
+    rc |= dalloc(&b->cand_count, ns);
+    rc |= dalloc(&b->cand_seen, ns);
+    rc |= dalloc(&b->det_rc, ns * nk * 2);
+    rc |= dalloc(&b->det_resp, ns * nk);
+    rc |= dalloc(&b->det_count, ns);
+    rc |= dalloc(&b->kp_src, ns * nk * 4);
+    rc |= dalloc(&b->kp_count, ns);
+    rc |= dalloc(&b->keypoints, ns * nk);
+    rc |= dalloc(&b->desc, ns * nk);
+    rc |= dalloc(&b->blur, (size_t)max_images * (size_t)H * W);
+    rc |= dalloc(&b->pairs, np * 2);
+    rc |= dalloc(&b->match_key, np * nk);
+    rc |= dalloc(&b->matches, np * nk);
+    rc |= dalloc(&b->match_count, np);
+    rc |= dalloc(&b->filtered, np * nk);
+    rc |= dalloc(&b->filt_count, np);
+    rc |= dalloc(&b->staging, (size_t)H * W);
+    if (rc != YV_OK) {
+        batch_free(b);
+        return YV_ERR_HIP;
+    }
+    hipStream_t s = ctx->stream;
+    bool ok = hipMemsetAsync(b->cand_count, 0, ns * sizeof(uint32_t), s) == hipSuccess &&
+              hipMemsetAsync(b->cand_seen, 0, ns * sizeof(uint32_t), s) == hipSuccess &&
+              hipMemsetAsync(b->kp_count, 0, ns * sizeof(int32_t), s) == hipSuccess &&
+              hipMemsetAsync(b->det_count, 0, ns * sizeof(int32_t), s) == hipSuccess &&
+              hipMemsetAsync(b->match_key, 0xFF, np * nk * sizeof(uint32_t), s) == hipSuccess &&
+              hipMemsetAsync(b->keypoints, 0, ns * nk * sizeof(yv_keypoint), s) == hipSuccess &&
+              hipMemsetAsync(b->match_count, 0, np * sizeof(int32_t), s) == hipSuccess &&
+              hipMemsetAsync(b->filt_count, 0, np * sizeof(int32_t), s) == hipSuccess &&
+              hipStreamSynchronize(s) == hipSuccess;
+    if (!ok) {
+        batch_free(b);
+        return YV_ERR_HIP;
+    }
+    *out = b;
+    return YV_OK;
+}
+
+void yv_batch_destroy(yv_batch* b) {
+    if (!b) return;
+    (void)hipSetDevice(b->ctx->device);
+    (void)hipStreamSynchronize(b->ctx->stream);
+    batch_free(b);
+}
+
+int yv_batch_set_pairs(yv_batch* b, const int32_t* pairs, int n_pairs) {
+    if (!b || n_pairs < 0 || n_pairs > b->max_pairs || (n_pairs > 0 && !pairs)) return YV_ERR_INVALID;
+    for (int i = 0; i < 2 * n_pairs; ++i)
+        if (pairs[i] < 0 || pairs[i] > b->max_images) return YV_ERR_INVALID;
+    if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+    if (n_pairs > 0) {
+        YV_HIP(hipMemcpyAsync(b->pairs, pairs, sizeof(int32_t) * 2 * (size_t)n_pairs, hipMemcpyHostToDevice,
+                              b->ctx->stream));
+        YV_HIP(hipStreamSynchronize(b->ctx->stream));
+    }
+    b->n_pairs = n_pairs;
+    return YV_OK;
+}
+
+int yv_batch_enable_timing(yv_batch* b, int on) {
+    if (!b) return YV_ERR_INVALID;
+    if (on && b->events.empty()) {
+        if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+        b->events.resize((size_t)kMaxTimedRuns * kEvPerRun);
+        for (auto& e : b->events) YV_HIP(hipEventCreate(&e));
+    }
+    b->timing = on != 0;
+    b->runs_recorded = 0;
+    return YV_OK;
+}
+
+int yv_batch_stage_times(yv_batch* b, float* ms, int* n_runs) {
+    if (!b || !ms) return YV_ERR_INVALID;
+    for (int i = 0; i < 8; ++i) ms[i] = 0.f;
+    const int runs = std::min(b->runs_recorded, kMaxTimedRuns);
+    if (n_runs) *n_runs = runs;
+    if (runs == 0) return YV_OK;
+    YV_HIP(hipEventSynchronize(b->events[(size_t)(runs - 1) * kEvPerRun + YV_NUM_STAGES]));
+    for (int r = 0; r < runs; ++r)
+        for (int st = 0; st < YV_NUM_STAGES; ++st) {
+            float t = 0.f;
+            YV_HIP(hipEventElapsedTime(&t, b->events[(size_t)r * kEvPerRun + st], b->events[(size_t)r * kEvPerRun + st + 1]));
+            ms[st] += t;
+        }
+    return YV_OK;
+}
+
+int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride, int64_t image_pitch, int match_thr,
+                 int carry_from, void* stream) {
+    if (!b || !d_images || n_images <= 0 || n_images > b->max_images || stride < b->W ||
+        image_pitch < (int64_t)stride * (b->H - 1) + b->W || carry_from >= n_images)
+        return YV_ERR_INVALID;
+    yv_ctx* ctx = b->ctx;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+    const int H = b->H, W = b->W, K = b->max_kp;
+    const int keep = std::min(ctx->max_corners, K);
+    int run = -1;
+    if (b->timing && b->runs_recorded < kMaxTimedRuns) run = b->runs_recorded++;
+    int rc = YV_OK;
+    rc |= record_stage(b, s, run, 0);
+    yavo::launch_fast_harris(d_images, n_images, H, W, stride, image_pitch, ctx->fast_thr, b->cand_keys, b->cap,
+                             b->cand_count, s);
+    rc |= record_stage(b, s, run, 1);
+    yavo::launch_blur9(d_images, n_images, H, W, stride, image_pitch, ctx->k9, b->blur, s);
+    rc |= record_stage(b, s, run, 2);
+    yavo::launch_topk(b->cand_keys, b->cap, b->cand_count, b->cand_seen, n_images, H, W, K, keep, b->det_rc, b->det_resp,
+                      b->det_count, b->kp_src, b->kp_count, s);
+    rc |= record_stage(b, s, run, 3);
+    yavo::launch_brief(b->blur, n_images, H, W, ctx->d_offsets, b->kp_src, b->kp_count, K, b->keypoints, b->desc, s);
+    rc |= record_stage(b, s, run, 4);
+    if (b->n_pairs > 0) {
+        yavo::launch_match(b->desc, b->kp_count, b->pairs, b->n_pairs, K, b->match_key, s);
+        rc |= record_stage(b, s, run, 5);
+        yavo::launch_match_finalize(b->match_key, b->keypoints, b->kp_count, b->pairs, b->n_pairs, K, match_thr,
+                                    b->matches, b->match_count, b->filtered, b->filt_count, s);
+    } else {
+        rc |= record_stage(b, s, run, 5);
+    }
+    rc |= record_stage(b, s, run, 6);
+    if (carry_from >= 0) {
+        const size_t c = (size_t)carry_from, dst = (size_t)b->max_images, nk = (size_t)K;
+        YV_HIP(hipMemcpyAsync(b->keypoints + dst * nk, b->keypoints + c * nk, nk * sizeof(yv_keypoint),
+                              hipMemcpyDeviceToDevice, s));
+        YV_HIP(hipMemcpyAsync(b->desc + dst * nk, b->desc + c * nk, nk * sizeof(Desc), hipMemcpyDeviceToDevice, s));
+        YV_HIP(hipMemcpyAsync(b->kp_count + dst, b->kp_count + c, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    }
+    if (rc != YV_OK) return YV_ERR_HIP;
+    return check_launch();
+}
+
+int yv_batch_view_get(yv_batch* b, yv_batch_view* v) {
+    if (!b || !v) return YV_ERR_INVALID;
+    v->max_images = b->max_images;
+    v->max_kp = b->max_kp;
+    v->max_pairs = b->max_pairs;
+    v->H = b->H;
+    v->W = b->W;
+    v->cand_cap = b->cap;
+    v->cand_count = b->cand_seen;
+    v->det_count = b->det_count;
+    v->det_rc = b->det_rc;
+    v->det_resp = b->det_resp;
+    v->kp_count = b->kp_count;
+    v->keypoints = b->keypoints;
+    v->blurred = b->blur;
+    v->match_count = b->match_count;
+    v->matches = b->matches;
+    v->filt_count = b->filt_count;
+    v->filtered = b->filtered;
+    return YV_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// host-pointer drop-in entry points
+// ------------------------------------------------------------------------------------------------
+static int upload_image(yv_batch* b, const uint8_t* img, int stride, hipStream_t s) {
+    YV_HIP(hipMemcpy2DAsync(b->staging, (size_t)b->W, img, (size_t)stride, (size_t)b->W, (size_t)b->H,
+                            hipMemcpyHostToDevice, s));
+    return YV_OK;
+}
+
+int yv_detect(yv_ctx* ctx, const uint8_t* img, int H, int W, int stride, int max_kp, int32_t* rc, float* resp,
+              int* n, int* n_candidates) {
+    if (!ctx || !img || !rc || !n || H < 9 || W < 9 || stride < W || max_kp < 0) return YV_ERR_INVALID;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    int st = ensure_single(ctx, H, W);
+    if (st != YV_OK) return st;
+    yv_batch* b = ctx->single;
+    hipStream_t s = ctx->stream;
+    const int keep = std::min(std::min(ctx->max_corners, max_kp), b->max_kp);
+    if (upload_image(b, img, stride, s) != YV_OK) return YV_ERR_HIP;
+    yavo::launch_fast_harris(b->staging, 1, H, W, W, (int64_t)H * W, ctx->fast_thr, b->cand_keys, b->cap,
+                             b->cand_count, s);
+    yavo::launch_topk(b->cand_keys, b->cap, b->cand_count, b->cand_seen, 1, H, W, b->max_kp, keep, b->det_rc, b->det_resp,
+                      b->det_count, b->kp_src, b->kp_count, s);
+    if (check_launch() != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMemcpyAsync(ctx->h_pinned, b->det_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    YV_HIP(hipMemcpyAsync(ctx->h_pinned + 1, b->cand_seen, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    YV_HIP(hipStreamSynchronize(s));
+    const int k = ctx->h_pinned[0];
+    if (k > 0) {
+        YV_HIP(hipMemcpyAsync(rc, b->det_rc, sizeof(int32_t) * 2 * (size_t)k, hipMemcpyDeviceToHost, s));
+        if (resp) YV_HIP(hipMemcpyAsync(resp, b->det_resp, sizeof(float) * (size_t)k, hipMemcpyDeviceToHost, s));
+        YV_HIP(hipStreamSynchronize(s));
+    }
+    *n = k;
+    if (n_candidates) *n_candidates = ctx->h_pinned[1];
+    return YV_OK;
+}
+
+int yv_describe(yv_ctx* ctx, const uint8_t* img, int H, int W, int stride, const int32_t* rc, int n, yv_keypoint* out,
+                int* n_out) {
+    if (!ctx || !img || !out || !n_out || H < 9 || W < 9 || stride < W || n < 0 || (n > 0 && !rc)) return YV_ERR_INVALID;
+    if (n > yavo::kMaxKp) return YV_ERR_CAPACITY;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    int st = ensure_single(ctx, H, W);
+    if (st != YV_OK) return st;
+    yv_batch* b = ctx->single;
+    hipStream_t s = ctx->stream;
+    if (upload_image(b, img, stride, s) != YV_OK) return YV_ERR_HIP;
+    ctx->h_pinned[0] = n;
+    if (n > 0) YV_HIP(hipMemcpyAsync(b->det_rc, rc, sizeof(int32_t) * 2 * (size_t)n, hipMemcpyHostToDevice, s));
+    YV_HIP(hipMemcpyAsync(b->det_count, ctx->h_pinned, sizeof(int32_t), hipMemcpyHostToDevice, s));
+    yavo::launch_blur9(b->staging, 1, H, W, W, (int64_t)H * W, ctx->k9, b->blur, s);
+    yavo::launch_kp_boundary(b->det_rc, b->det_count, 1, H, W, b->max_kp, b->kp_src, b->kp_count, s);
+    yavo::launch_brief(b->blur, 1, H, W, ctx->d_offsets, b->kp_src, b->kp_count, b->max_kp, b->keypoints, b->desc, s);
+    if (check_launch() != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMemcpyAsync(ctx->h_pinned + 2, b->kp_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    YV_HIP(hipStreamSynchronize(s));
+    const int m = ctx->h_pinned[2];
+    if (m > 0) {
+        YV_HIP(hipMemcpyAsync(out, b->keypoints, sizeof(yv_keypoint) * (size_t)m, hipMemcpyDeviceToHost, s));
+        YV_HIP(hipStreamSynchronize(s));
+    }
+    *n_out = m;
+    return YV_OK;
+}
+
+int yv_match_features(yv_ctx* ctx, const yv_keypoint* q, int nq, const yv_keypoint* t, int nt, yv_match* out) {
+    if (!ctx || nq < 0 || nt < 0 || (nq > 0 && (!q || !out)) || (nt > 0 && !t)) return YV_ERR_INVALID;
+    if (nq > yavo::kMaxKp || nt > yavo::kMaxKp) return YV_ERR_CAPACITY;
+    if (nq == 0) return YV_OK;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    // the matcher does not look at the image size: reuse whatever workspace exists (or a minimal one)
+    int st = ctx->single ? YV_OK : ensure_single(ctx, 16, 16);
+    if (st != YV_OK) return st;
+    yv_batch* b = ctx->single;
+    hipStream_t s = ctx->stream;
+    const size_t nk = (size_t)b->max_kp;
+    YV_HIP(hipMemcpyAsync(b->keypoints, q, sizeof(yv_keypoint) * (size_t)nq, hipMemcpyHostToDevice, s));
+    if (nt > 0) YV_HIP(hipMemcpyAsync(b->keypoints + nk, t, sizeof(yv_keypoint) * (size_t)nt, hipMemcpyHostToDevice, s));
+    ctx->h_pinned[0] = nq;
+    ctx->h_pinned[1] = nt;
+    YV_HIP(hipMemcpyAsync(b->kp_count, ctx->h_pinned, 2 * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    yavo::launch_pack_desc(b->keypoints, b->kp_count, 2, b->max_kp, b->desc, s);
+    yavo::launch_match(b->desc, b->kp_count, b->pairs, 1, b->max_kp, b->match_key, s);
+    yavo::launch_match_finalize(b->match_key, b->keypoints, b->kp_count, b->pairs, 1, b->max_kp, 0, b->matches,
+                                b->match_count, b->filtered, b->filt_count, s);
+    if (check_launch() != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMemcpyAsync(out, b->matches, sizeof(yv_match) * (size_t)nq, hipMemcpyDeviceToHost, s));
+    YV_HIP(hipStreamSynchronize(s));
+    return YV_OK;
+}
+
+int yv_filter_matches(yv_ctx* ctx, const yv_match* in, int n, int thr, yv_match* out, int* n_out) {
+    if (!ctx || !n_out || n < 0 || (n > 0 && (!in || !out))) return YV_ERR_INVALID;
+    if (n > yavo::kMaxKp) return YV_ERR_CAPACITY;
+    *n_out = 0;
+    if (n == 0) return YV_OK;  // reference: minmax_element on an empty list is dereferenced (UB)
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    int st = ctx->single ? YV_OK : ensure_single(ctx, 16, 16);
+    if (st != YV_OK) return st;
+    yv_batch* b = ctx->single;
+    hipStream_t s = ctx->stream;
+    YV_HIP(hipMemcpyAsync(b->matches, in, sizeof(yv_match) * (size_t)n, hipMemcpyHostToDevice, s));
+    yavo::launch_filter_records(b->matches, n, thr, b->filtered, b->filt_count, s);
+    if (check_launch() != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMemcpyAsync(ctx->h_pinned, b->filt_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    YV_HIP(hipStreamSynchronize(s));
+    const int m = ctx->h_pinned[0];
+    if (m > 0) {
+        YV_HIP(hipMemcpyAsync(out, b->filtered, sizeof(yv_match) * (size_t)m, hipMemcpyDeviceToHost, s));
+        YV_HIP(hipStreamSynchronize(s));
+    }
+    *n_out = m;
+    return YV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,54 @@
+// yavo_internal.h -- launchers shared between the kernel translation unit and the C-ABI layer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/yavo/yavo_types.h"
+
+namespace yavo {
+
+constexpr int kMaxKp = 4096;       // per-image keypoint capacity supported by the top-K / scan kernels
+constexpr int kFastTileW = 64;     // FAST / blur output tile: one wave per tile row
+constexpr int kFastTileH = 32;
+
+struct Desc {                      // 256-bit BRIEF descriptor, test j -> bit j (LSB-first bytes)
+    uint32_t w[8];
+};
+
+// FAST-12 candidate test + Harris response, appends (response, index) keys per image.
+void launch_fast_harris(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,
+                        int thr, uint64_t* cand_keys, int64_t cap, uint32_t* cand_count,
+                        hipStream_t s);
+// 9-tap separable fixed-point Gaussian, BORDER_REFLECT_101; output H x W contiguous per image.
+void launch_blur9(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,
+                  const uint16_t* k9_host, uint8_t* blur, hipStream_t s);
+// Per-image top-K (response desc, index asc) + checkBoundry compaction.
+// cand_count is copied to cand_seen and reset to 0 after it is read (ready for the next detection).
+void launch_topk(const uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, uint32_t* cand_seen, int n_images,
+                 int H, int W, int max_kp, int keep, int32_t* det_rc, float* det_resp, int32_t* det_count,
+                 int32_t* kp_src, int32_t* kp_count, hipStream_t s);
+// checkBoundry compaction of externally supplied points (det_rc / det_count already on the device).
+void launch_kp_boundary(const int32_t* det_rc, const int32_t* det_count, int n_images, int H, int W,
+                        int max_kp, int32_t* kp_src, int32_t* kp_count, hipStream_t s);
+// BRIEF: one wave per keypoint, 256 tests -> 4 ballots; writes KeyPoint records + packed descriptors.
+void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t* offsets,
+                  const int32_t* kp_src, const int32_t* kp_count, int max_kp, yv_keypoint* keypoints,
+                  Desc* desc, hipStream_t s);
+// Pack KeyPoint records -> descriptors (host-supplied keypoints).
+void launch_pack_desc(const yv_keypoint* keypoints, const int32_t* kp_count, int n_slots, int max_kp,
+                      Desc* desc, hipStream_t s);
+// Brute-force Hamming NN: match_key[pair][q] = min over t of (dist << 16 | t).
+void launch_match(const Desc* desc, const int32_t* kp_count, const int32_t* pairs, int n_pairs,
+                  int max_kp, uint32_t* match_key, hipStream_t s);
+// Matches records (matchFeatures) + removeOutliers per pair.  match_key entries are reset to
+// 0xFFFFFFFF after they are read (ready for the next match).
+void launch_match_finalize(uint32_t* match_key, const yv_keypoint* keypoints,
+                           const int32_t* kp_count, const int32_t* pairs, int n_pairs, int max_kp,
+                           int thr, yv_match* matches, int32_t* match_count, yv_match* filtered,
+                           int32_t* filt_count, hipStream_t s);
+// removeOutliers on externally supplied Matches records (one list).
+void launch_filter_records(const yv_match* in, int n, int thr, yv_match* out, int32_t* out_count,
+                           hipStream_t s);
+
+}  // namespace yavo

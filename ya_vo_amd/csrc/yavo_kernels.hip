@@ -1,0 +1,789 @@
+// yavo_kernels.hip -- gfx950 (CDNA4) kernels for the YA_VO detect / describe / match hot path.
+//
+// Built with -ffp-contract=off: the Harris eigen solve and response must round operation-for-operation
+// like the reference's x86-64 build (no FMA contraction), see DESIGN.md "Float parity".
+//
+// Reference functions restated (file:line in /root/reference):
+//   fast_harris_kernel  FastDetector::getFastFeatures loop      src/FastDetector.cc:298-335
+//                       checkInBetween / checkContiguousPixels  src/FastDetector.cc:135-161
+//                       preComputeHarris + Harris response      src/FastDetector.cc:164-214, 244-273
+//   topk_kernel         std::sort + top-2000 cut                src/FastDetector.cc:343-368
+//                       Brief::checkBoundry                     src/BriefDescriptor.cc:128-136
+//   blur9_kernel        cv::GaussianBlur(9x9, 2.5) call         src/BriefDescriptor.cc:90
+//   brief_kernel        Brief::computeBrief                     src/BriefDescriptor.cc:86-124
+//   match_kernel        Brief::matchFeatures / hammingDistance  src/BriefDescriptor.cc:139-183
+//   match_finalize      Matches records + removeOutliers        src/BriefDescriptor.cc:163-231
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "yavo_internal.h"
+
+namespace yavo {
+
+// ------------------------------------------------------------------------------------------------
+// helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+// Inclusive scan across one 64-lane wave.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        int t = __shfl_up(v, off, 64);
+        if (lane >= off) v += t;
+    }
+    return v;
+}
+
+// Exclusive scan over the whole block (blockDim.x = NT, multiple of 64, <= 1024).  s_tmp >= 16 ints.
+template <int NT>
+__device__ __forceinline__ int block_excl_scan(int v, int* s_tmp, int* total) {
+    const int lane = lane_id();
+    const int wave = (int)threadIdx.x >> 6;
+    constexpr int NW = NT / 64;
+    int incl = wave_incl_scan(v);
+    if (lane == 63) s_tmp[wave] = incl;
+    __syncthreads();
+    if (wave == 0) {
+        int w = lane < NW ? s_tmp[lane] : 0;
+        int wi = wave_incl_scan(w);
+        if (lane < NW) s_tmp[lane] = wi - w;  // exclusive wave offsets
+        if (lane == NW - 1) s_tmp[NW] = wi;
+    }
+    __syncthreads();
+    int res = s_tmp[wave] + incl - v;
+    if (total) *total = s_tmp[NW];
+    __syncthreads();
+    return res;
+}
+
+// ------------------------------------------------------------------------------------------------
+// FAST-12 + Harris
+// ------------------------------------------------------------------------------------------------
+// Ring order of FastDetector::getBresenhamCirclePoints (src/FastDetector.cc:50-112) as (drow, dcol);
+// pinned by tests/test_oracle_fast.py against the reference's testBresenham.png fixture.
+#define YV_RING_DR {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1}
+#define YV_RING_DC {-3, -3, -2, -1, 0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3}
+
+// OpenCV lapack.cpp hypot<float>: a*sqrt(1+(b/a)^2) (used by JacobiImpl_).
+__device__ __forceinline__ float cv_hypotf(float a, float b) {
+    a = fabsf(a);
+    b = fabsf(b);
+    if (a > b) {
+        b /= a;
+        return a * sqrtf(1.0f + b * b);
+    }
+    if (b > 0.0f) {
+        a /= b;
+        return b * sqrtf(1.0f + a * a);
+    }
+    return 0.0f;
+}
+
+// cv::eigen on the 2x2 float structure tensor = JacobiImpl_<float>(n=2): one rotation unless
+// |m01| <= FLT_EPSILON, then a descending sort; followed by the response expression of
+// src/FastDetector.cc:270 evaluated in double and rounded to float.
+__device__ __forceinline__ float harris_response(float a, float b, float d) {
+    float w0 = a, w1 = d;
+    if (!(fabsf(b) <= 1.1920928955078125e-07f)) {
+        const float p = b;
+        const float y = (float)((double)(w1 - w0) * 0.5);
+        float t = fabsf(y) + cv_hypotf(p, y);
+        float s = cv_hypotf(p, t);
+        // c = t / s is only used to rotate off-diagonal entries, none remain for n = 2
+        s = p / s;
+        t = (p / t) * p;
+        if (y < 0.0f) { s = -s; t = -t; }
+        w0 -= t;
+        w1 += t;
+    }
+    if (w0 < w1) { float tmp = w0; w0 = w1; w1 = tmp; }
+    const float prod = w0 * w1;
+    const float sum = w1 + w0;
+    const double sq = (double)sum * (double)sum;
+    const double r = (double)prod - 0.04 * sq;
+    return (float)r;
+}
+
+// Order-preserving key: ascending key == (response descending, row-major index ascending).
+__device__ __forceinline__ uint64_t make_key(float resp, uint32_t idx) {
+    if (resp == 0.0f) resp = 0.0f;  // -0 and +0 compare equal in the reference's sort
+    uint32_t u = __float_as_uint(resp);
+    uint32_t ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((uint64_t)(~ord) << 32) | (uint64_t)idx;
+}
+__device__ __forceinline__ float key_resp(uint64_t key) {
+    uint32_t ord = ~(uint32_t)(key >> 32);
+    uint32_t u = (ord & 0x80000000u) ? (ord & 0x7fffffffu) : ~ord;
+    return __uint_as_float(u);
+}
+
+constexpr int FT_W = kFastTileW;        // 64 output columns per tile (one wave-row)
+constexpr int FT_H = kFastTileH;        // 32 output rows per tile
+constexpr int FT_R = 3;                 // halo: ring radius 3, Sobel+3x3 window radius 2
+constexpr int FT_LW = FT_W + 2 * FT_R;  // 70 bytes per LDS row
+constexpr int FT_LWP = 72;              // padded LDS row stride
+constexpr int FT_LH = FT_H + 2 * FT_R;  // 38 LDS rows
+
+__global__ __launch_bounds__(256) void fast_harris_kernel(const uint8_t* __restrict__ imgs, int H, int W,
+                                                          int stride, int64_t pitch, int thr,
+                                                          uint64_t* __restrict__ cand_keys, int64_t cap,
+                                                          uint32_t* __restrict__ cand_count) {
+    __shared__ uint8_t tile[FT_LH * FT_LWP];
+    const int img = blockIdx.z;
+    const int r0 = blockIdx.y * FT_H, c0 = blockIdx.x * FT_W;
+    const uint8_t* src = imgs + (int64_t)img * pitch;
+    const int tid = threadIdx.x;
+
+    // Stage the (FT_H + 6) x (FT_W + 6) tile; pixels outside the image are never read by a valid
+    // candidate (rows 4..H-5 / cols 4..W-5 with a radius-3 footprint) and are filled with 0.
+    for (int i = tid; i < FT_LH * FT_LW; i += 256) {
+        const int lr = i / FT_LW, lc = i - lr * FT_LW;
+        const int r = r0 - FT_R + lr, c = c0 - FT_R + lc;
+        uint8_t v = 0;
+        if (r >= 0 && r < H && c >= 0 && c < W) v = src[(int64_t)r * stride + c];
+        tile[lr * FT_LWP + lc] = v;
+    }
+    __syncthreads();
+
+    constexpr int ring_dr[16] = YV_RING_DR;
+    constexpr int ring_dc[16] = YV_RING_DC;
+    const int tx = tid & 63, ty = tid >> 6;
+    const int c = c0 + tx;
+    const int lane = lane_id();
+    for (int rr = ty; rr < FT_H; rr += 4) {
+        const int r = r0 + rr;
+        const bool inside = (r >= 4) && (r < H - 4) && (c >= 4) && (c < W - 4);
+        const uint8_t* t0 = &tile[(rr + FT_R) * FT_LWP + tx + FT_R];
+        const int cent = t0[0];
+        uint32_t mask = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int p = t0[ring_dr[k] * FT_LWP + ring_dc[k]];
+            // !checkInBetween(cent, p)  <=>  !(cent > p - thr && cent < p + thr)
+            const bool diff = !((cent > p - thr) && (cent < p + thr));
+            mask |= (uint32_t)diff << k;
+        }
+        // pretest on ring indices 0, 7 and (4 | 12) (src/FastDetector.cc:304-317)
+        const bool pre = (mask & 1u) && (mask & (1u << 7)) && ((mask & (1u << 4)) || (mask & (1u << 12)));
+        // >= 12 consecutive set bits in mask[0..15], no wrap (checkContiguousPixels)
+        const uint32_t a2 = mask & (mask >> 1);
+        const uint32_t a4 = a2 & (a2 >> 2);
+        const uint32_t a8 = a4 & (a4 >> 4);
+        const uint32_t a12 = a8 & (a4 >> 8);
+        const bool cand = inside && pre && (a12 != 0u);
+
+        uint64_t key = 0;
+        if (cand) {
+            // Sobel Ix / Iy (3x3 correlation) at the 3x3 window around the corner, from the 5x5 patch.
+            int sxx = 0, sxy = 0, syy = 0;
+#pragma unroll
+            for (int i = -1; i <= 1; ++i) {
+#pragma unroll
+                for (int j = -1; j <= 1; ++j) {
+                    const uint8_t* q = t0 + i * FT_LWP + j;
+                    const int pmm = q[-FT_LWP - 1], pm0 = q[-FT_LWP], pmp = q[-FT_LWP + 1];
+                    const int p0m = q[-1], p0p = q[1];
+                    const int ppm = q[FT_LWP - 1], pp0 = q[FT_LWP], ppp = q[FT_LWP + 1];
+                    const int gx = (pmp - pmm) + 2 * (p0p - p0m) + (ppp - ppm);
+                    const int gy = (ppm - pmm) + 2 * (pp0 - pm0) + (ppp - pmp);
+                    sxx += gx * gx;
+                    sxy += gx * gy;
+                    syy += gy * gy;
+                }
+            }
+            // all partial sums are integers < 2^24: exact in float, as in the reference
+            const float resp = harris_response((float)sxx, (float)sxy, (float)syy);
+            key = make_key(resp, (uint32_t)(r * W + c));
+        }
+        const uint64_t bal = __ballot(cand);
+        if (bal) {
+            const int leader = __ffsll((long long)bal) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&cand_count[img], (uint32_t)__popcll(bal));
+            base = __shfl(base, leader, 64);
+            if (cand) {
+                const uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+                if ((int64_t)pos < cap) cand_keys[(int64_t)img * cap + pos] = key;
+            }
+        }
+    }
+}
+
+void launch_fast_harris(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,
+                        int thr, uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, hipStream_t s) {
+    dim3 grid((W + FT_W - 1) / FT_W, (H + FT_H - 1) / FT_H, n_images);
+    hipLaunchKernelGGL(fast_harris_kernel, grid, dim3(256), 0, s, imgs, H, W, stride, pitch, thr, cand_keys,
+                       cap, cand_count);
+}
+
+// ------------------------------------------------------------------------------------------------
+// 9x9 fixed-point Gaussian blur (OpenCV GaussianBlurFixedPoint<uint8_t, ufixedpoint16>)
+// ------------------------------------------------------------------------------------------------
+struct K9 {
+    uint32_t k[9];
+};
+constexpr int BL_W = 64, BL_H = 32, BL_R = 4;
+constexpr int BL_LW = BL_W + 2 * BL_R;  // 72
+constexpr int BL_LH = BL_H + 2 * BL_R;  // 40
+
+__device__ __forceinline__ int reflect101(int p, int len) {
+    // cv::borderInterpolate(BORDER_REFLECT_101) for |p| < len
+    if (p < 0) p = -p;
+    if (p >= len) p = 2 * len - p - 2;
+    return p;
+}
+
+__global__ __launch_bounds__(256) void blur9_kernel(const uint8_t* __restrict__ imgs, int H, int W, int stride,
+                                                    int64_t pitch, K9 kw, uint8_t* __restrict__ blur) {
+    __shared__ uint8_t tin[BL_LH * BL_LW];
+    __shared__ uint32_t th[BL_LH * BL_W];
+    const int img = blockIdx.z;
+    const int r0 = blockIdx.y * BL_H, c0 = blockIdx.x * BL_W;
+    const uint8_t* src = imgs + (int64_t)img * pitch;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < BL_LH * BL_LW; i += 256) {
+        const int lr = i / BL_LW, lc = i - lr * BL_LW;
+        const int r = reflect101(min(max(r0 - BL_R + lr, -(H - 1)), 2 * H - 2), H);
+        const int c = reflect101(min(max(c0 - BL_R + lc, -(W - 1)), 2 * W - 2), W);
+        tin[i] = src[(int64_t)r * stride + c];
+    }
+    __syncthreads();
+    // horizontal: exact u32 sums (<= 255 * 256)
+    for (int i = tid; i < BL_LH * BL_W; i += 256) {
+        const int lr = i >> 6, lc = i & 63;
+        const uint8_t* q = &tin[lr * BL_LW + lc];
+        uint32_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) acc += kw.k[j] * (uint32_t)q[j];
+        th[i] = acc;
+    }
+    __syncthreads();
+    const int tx = tid & 63, ty = tid >> 6;
+    const int c = c0 + tx;
+    for (int rr = ty; rr < BL_H; rr += 4) {
+        const int r = r0 + rr;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) acc += kw.k[i] * th[(rr + i) * BL_W + tx];
+        uint32_t v = (acc + (1u << 15)) >> 16;
+        if (r < H && c < W) blur[(int64_t)img * H * W + (int64_t)r * W + c] = (uint8_t)(v > 255u ? 255u : v);
+    }
+}
+
+void launch_blur9(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,
+                  const uint16_t* k9_host, uint8_t* blur, hipStream_t s) {
+    K9 kw;
+    for (int i = 0; i < 9; ++i) kw.k[i] = k9_host[i];
+    dim3 grid((W + BL_W - 1) / BL_W, (H + BL_H - 1) / BL_H, n_images);
+    hipLaunchKernelGGL(blur9_kernel, grid, dim3(256), 0, s, imgs, H, W, stride, pitch, kw, blur);
+}
+
+// ------------------------------------------------------------------------------------------------
+// top-K selection + sort + checkBoundry compaction (one 1024-thread workgroup per image)
+// ------------------------------------------------------------------------------------------------
+constexpr int TK_NT = 1024;
+
+// checkBoundry(kp.y=col, kp.x=row, W, H): 8 <= col <= W-8 and 8 <= row <= H-8.
+__device__ __forceinline__ bool brief_boundary(int row, int col, int H, int W) {
+    return !(col - 8 < 0 || col + 8 > W) && !(row - 8 < 0 || row + 8 > H);
+}
+
+// Compacts points 0..K-1 (rc_at(i) -> int2 {row, col}) to those inside checkBoundry, keeping order;
+// kp_src[slot] = {row, col, id = input index, 0}.  Handles K <= 4 * TK_NT.
+template <class RcAt>
+__device__ void boundary_compact(RcAt rc_at, int K, int H, int W, int32_t* kp_src, int32_t* kp_count, int* s_tmp) {
+    const int tid = threadIdx.x;
+    int flags[4];
+    int2 rcs[4];
+    int cnt = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = tid * 4 + u;
+        flags[u] = 0;
+        rcs[u] = make_int2(0, 0);
+        if (i < K) {
+            rcs[u] = rc_at(i);
+            flags[u] = brief_boundary(rcs[u].x, rcs[u].y, H, W) ? 1 : 0;
+        }
+        cnt += flags[u];
+    }
+    int total = 0;
+    int off = block_excl_scan<TK_NT>(cnt, s_tmp, &total);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = tid * 4 + u;
+        if (flags[u]) {
+            reinterpret_cast<int4*>(kp_src)[off] = make_int4(rcs[u].x, rcs[u].y, i, 0);
+            off++;
+        }
+    }
+    if (tid == 0) *kp_count = total;
+}
+
+__global__ __launch_bounds__(TK_NT) void topk_kernel(const uint64_t* __restrict__ cand_keys, int64_t cap,
+                                                     uint32_t* __restrict__ cand_count, uint32_t* __restrict__ cand_seen,
+                                                     int H, int W, int max_kp, int keep, int32_t* __restrict__ det_rc,
+                                                     float* __restrict__ det_resp, int32_t* __restrict__ det_count,
+                                                     int32_t* __restrict__ kp_src, int32_t* __restrict__ kp_count) {
+    __shared__ uint64_t s_keys[kMaxKp];
+    __shared__ uint32_t s_hist[256];
+    __shared__ int s_tmp[40];
+    __shared__ uint64_t s_prefix, s_mask;
+    __shared__ int s_krem, s_done, s_n;
+
+    const int img = blockIdx.x;
+    const int tid = threadIdx.x;
+    const uint64_t* keys = cand_keys + (int64_t)img * cap;
+    int64_t C64 = (int64_t)cand_count[img];
+    if (C64 > cap) C64 = cap;
+    const int C = (int)C64;
+    const int K = C < keep ? C : keep;
+    __syncthreads();
+    if (tid == 0) {
+        cand_seen[img] = (uint32_t)C;  // corners before the cut, kept for the caller
+        cand_count[img] = 0;           // consumed: ready for the next detection into this slot
+    }
+    int32_t* rc_out = det_rc + (int64_t)img * max_kp * 2;
+    float* resp_out = det_resp + (int64_t)img * max_kp;
+
+    if (K == 0) {  // no corners (or max_kp == 0): nothing to select
+        if (tid == 0) { det_count[img] = 0; kp_count[img] = 0; }
+        return;
+    }
+    uint64_t sel_mask = 0, sel_prefix = ~0ull;  // selection: (key & sel_mask) <= sel_prefix
+    if (C > K) {
+        if (tid == 0) { s_prefix = 0; s_mask = 0; s_krem = K; s_done = 0; }
+        __syncthreads();
+        for (int shift = 56; shift >= 0; shift -= 8) {
+            // state of the previous pass is read before the barrier that precedes any rewrite of it
+            const uint64_t pm = s_mask, pp = s_prefix;
+            const int krem = s_krem;
+            if (tid < 256) s_hist[tid] = 0;
+            __syncthreads();
+            for (int i = tid; i < C; i += TK_NT) {
+                const uint64_t k = keys[i];
+                if ((k & pm) == pp) atomicAdd(&s_hist[(k >> shift) & 255u], 1u);
+            }
+            __syncthreads();
+            // find the bucket holding the krem-th smallest key (256-entry scan by the first 4 waves)
+            int h = 0, incl = 0;
+            if (tid < 256) {
+                h = (int)s_hist[tid];
+                incl = wave_incl_scan(h);
+                if ((tid & 63) == 63) s_tmp[tid >> 6] = incl;
+            }
+            __syncthreads();
+            if (tid < 256) {
+                int base = 0;
+                for (int w = 0; w < (tid >> 6); ++w) base += s_tmp[w];
+                incl += base;
+                if (incl >= krem && incl - h < krem) {
+                    const int nk = krem - (incl - h);
+                    s_prefix = pp | ((uint64_t)tid << shift);
+                    s_mask = pm | (0xFFull << shift);
+                    s_krem = nk;
+                    s_done = (h == nk);
+                }
+            }
+            __syncthreads();
+            if (s_done) break;
+        }
+        sel_mask = s_mask;
+        sel_prefix = s_prefix;
+    }
+    // collect the K selected keys into LDS (any order), pad to a power of two, bitonic sort
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    for (int i = tid; i < C; i += TK_NT) {
+        const uint64_t k = keys[i];
+        if ((k & sel_mask) <= sel_prefix) {
+            const int p = atomicAdd(&s_n, 1);
+            if (p < kMaxKp) s_keys[p] = k;
+        }
+    }
+    __syncthreads();
+    int P2 = 1;
+    while (P2 < K) P2 <<= 1;
+    for (int i = K + tid; i < P2; i += TK_NT) s_keys[i] = ~0ull;
+    __syncthreads();
+    for (int size = 2; size <= P2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = tid; t < (P2 >> 1); t += TK_NT) {
+                const int i = 2 * t - (t & (stride - 1));
+                const int j = i + stride;
+                const bool up = ((i & size) == 0);
+                const uint64_t a = s_keys[i], b = s_keys[j];
+                if ((a > b) == up) { s_keys[i] = b; s_keys[j] = a; }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = tid; i < K; i += TK_NT) {
+        const uint64_t k = s_keys[i];
+        const uint32_t idx = (uint32_t)k;
+        const int row = (int)(idx / (uint32_t)W), col = (int)(idx - (uint32_t)row * (uint32_t)W);
+        rc_out[2 * i] = row;
+        rc_out[2 * i + 1] = col;
+        resp_out[i] = key_resp(k);
+    }
+    if (tid == 0) det_count[img] = K;
+    const uint32_t Wu = (uint32_t)W;
+    auto rc_from_lds = [&](int i) -> int2 {
+        const uint32_t idx = (uint32_t)s_keys[i];
+        const uint32_t row = idx / Wu;
+        return make_int2((int)row, (int)(idx - row * Wu));
+    };
+    boundary_compact(rc_from_lds, K, H, W, kp_src + (int64_t)img * max_kp * 4, kp_count + img, s_tmp);
+}
+
+__global__ __launch_bounds__(TK_NT) void kp_boundary_kernel(const int32_t* __restrict__ det_rc,
+                                                            const int32_t* __restrict__ det_count, int H, int W,
+                                                            int max_kp, int32_t* __restrict__ kp_src,
+                                                            int32_t* __restrict__ kp_count) {
+    __shared__ int s_tmp[40];
+    const int img = blockIdx.x;
+    int K = det_count[img];
+    if (K > max_kp) K = max_kp;
+    const int32_t* rc = det_rc + (int64_t)img * max_kp * 2;
+    auto rc_from_global = [&](int i) -> int2 { return make_int2(rc[2 * i], rc[2 * i + 1]); };
+    boundary_compact(rc_from_global, K, H, W, kp_src + (int64_t)img * max_kp * 4, kp_count + img, s_tmp);
+}
+
+void launch_topk(const uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, uint32_t* cand_seen, int n_images,
+                 int H, int W, int max_kp, int keep, int32_t* det_rc, float* det_resp, int32_t* det_count, int32_t* kp_src,
+                 int32_t* kp_count, hipStream_t s) {
+    hipLaunchKernelGGL(topk_kernel, dim3(n_images), dim3(TK_NT), 0, s, cand_keys, cap, cand_count, cand_seen, H, W,
+                       max_kp, keep, det_rc, det_resp, det_count, kp_src, kp_count);
+}
+
+void launch_kp_boundary(const int32_t* det_rc, const int32_t* det_count, int n_images, int H, int W, int max_kp,
+                        int32_t* kp_src, int32_t* kp_count, hipStream_t s) {
+    hipLaunchKernelGGL(kp_boundary_kernel, dim3(n_images), dim3(TK_NT), 0, s, det_rc, det_count, H, W, max_kp,
+                       kp_src, kp_count);
+}
+
+// ------------------------------------------------------------------------------------------------
+// BRIEF: one wave per keypoint; lane l evaluates tests l, l+64, l+128, l+192 -> 4 ballots = 256 bits
+// ------------------------------------------------------------------------------------------------
+constexpr int BR_KP_PER_WAVE = 4;
+
+// v[idx] for a small register array without dynamic indexing (keeps it out of scratch).
+template <int N>
+__device__ __forceinline__ uint32_t reg_select(const uint32_t (&v)[N], int idx) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int q = 0; q < N; ++q) r = (q == idx) ? v[q] : r;
+    return r;
+}
+
+__device__ __forceinline__ int blur_pix(const uint8_t* b, int64_t n, int64_t idx) {
+    // getPixelVal(i, j) = data[i*cols + j]: the linear index may wrap into the next row (reproduced);
+    // past the buffer end the reference reads out of bounds (UB) -> 0 here.
+    return (idx >= 0 && idx < n) ? (int)b[idx] : 0;
+}
+
+__global__ __launch_bounds__(256) void brief_kernel(const uint8_t* __restrict__ blur, int H, int W,
+                                                    const int8_t* __restrict__ offsets,
+                                                    const int32_t* __restrict__ kp_src,
+                                                    const int32_t* __restrict__ kp_count, int max_kp,
+                                                    yv_keypoint* __restrict__ keypoints, Desc* __restrict__ desc) {
+    const int img = blockIdx.y;
+    const int lane = lane_id();
+    const int wave = (int)threadIdx.x >> 6;
+    const int n = kp_count[img];
+    const int first = (blockIdx.x * 4 + wave) * BR_KP_PER_WAVE;
+    if (first >= n) return;
+    const uint8_t* b = blur + (int64_t)img * H * W;
+    const int64_t npix = (int64_t)H * W;
+    // offsets of this lane's four tests: rows l, l+64, l+128, l+192 of the 256 x 4 table
+    int o[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const uint32_t packed = reinterpret_cast<const uint32_t*>(offsets)[lane + 64 * t];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[t][q] = (int)(int8_t)((packed >> (8 * q)) & 0xFFu);
+    }
+    const int4* src = reinterpret_cast<const int4*>(kp_src) + (int64_t)img * max_kp;
+    uint32_t* rec_base = reinterpret_cast<uint32_t*>(keypoints + (int64_t)img * max_kp);
+    Desc* d_base = desc + (int64_t)img * max_kp;
+    for (int kk = 0; kk < BR_KP_PER_WAVE; ++kk) {
+        const int i = first + kk;
+        if (i >= n) break;
+        const int4 kp = src[i];
+        const int row = kp.x, col = kp.y;
+        uint64_t w[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int64_t i1 = (int64_t)(row + o[t][0]) * W + (col + o[t][1]);
+            const int64_t i2 = (int64_t)(row + o[t][2]) * W + (col + o[t][3]);
+            const bool bit = blur_pix(b, npix, i1) > blur_pix(b, npix, i2);
+            w[t] = __ballot(bit);
+        }
+        // descriptor (32 B) and the 48-B KeyPoint record {x, y, id, matched=0, featVec[32], pad 0}
+        uint32_t bd[9];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) { bd[2 * t] = (uint32_t)w[t]; bd[2 * t + 1] = (uint32_t)(w[t] >> 32); }
+        bd[8] = 0;
+        if (lane < 8) d_base[i].w[lane] = reg_select(bd, lane);
+        if (lane < 12) {
+            uint32_t v;
+            if (lane == 0) v = (uint32_t)row;
+            else if (lane == 1) v = (uint32_t)col;
+            else if (lane == 2) v = (uint32_t)kp.z;
+            else {
+                const int m = lane - 3;  // record dword 3+m = featVec bytes shifted by one (matched byte first)
+                const uint32_t hi = reg_select(bd, m);
+                const uint32_t lo = m > 0 ? reg_select(bd, m - 1) : 0u;
+                v = (hi << 8) | (lo >> 24);
+            }
+            rec_base[(int64_t)i * 12 + lane] = v;
+        }
+    }
+}
+
+void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t* offsets, const int32_t* kp_src,
+                  const int32_t* kp_count, int max_kp, yv_keypoint* keypoints, Desc* desc, hipStream_t s) {
+    const int per_block = 4 * BR_KP_PER_WAVE;
+    dim3 grid((max_kp + per_block - 1) / per_block, n_images);
+    hipLaunchKernelGGL(brief_kernel, grid, dim3(256), 0, s, blur, H, W, offsets, kp_src, kp_count, max_kp,
+                       keypoints, desc);
+}
+
+__global__ void pack_desc_kernel(const yv_keypoint* __restrict__ keypoints, const int32_t* __restrict__ kp_count,
+                                 int max_kp, Desc* __restrict__ desc) {
+    const int slot = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= kp_count[slot] || i >= max_kp) return;
+    const uint8_t* rec = reinterpret_cast<const uint8_t*>(keypoints + (int64_t)slot * max_kp + i);
+    Desc d;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        d.w[q] = (uint32_t)rec[13 + 4 * q] | ((uint32_t)rec[14 + 4 * q] << 8) | ((uint32_t)rec[15 + 4 * q] << 16) |
+                 ((uint32_t)rec[16 + 4 * q] << 24);
+    }
+    desc[(int64_t)slot * max_kp + i] = d;
+}
+
+void launch_pack_desc(const yv_keypoint* keypoints, const int32_t* kp_count, int n_slots, int max_kp, Desc* desc,
+                      hipStream_t s) {
+    dim3 grid((max_kp + 255) / 256, n_slots);
+    hipLaunchKernelGGL(pack_desc_kernel, grid, dim3(256), 0, s, keypoints, kp_count, max_kp, desc);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Brute-force Hamming matcher
+// ------------------------------------------------------------------------------------------------
+constexpr int MT_QPT = 2;                 // queries per thread
+constexpr int MT_QB = 256 * MT_QPT;       // queries per workgroup
+constexpr int MT_TB = 512;                // train descriptors per LDS chunk (16 KB)
+
+__global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ desc, const int32_t* __restrict__ kp_count,
+                                                    const int32_t* __restrict__ pairs, int max_kp,
+                                                    uint32_t* __restrict__ match_key) {
+    __shared__ uint4 s_t[MT_TB * 2];
+    const int pair = blockIdx.z;
+    const int qi = pairs[2 * pair], ti = pairs[2 * pair + 1];
+    const int nq = kp_count[qi], nt = kp_count[ti];
+    const int q0 = blockIdx.x * MT_QB, t0 = blockIdx.y * MT_TB;
+    if (q0 >= nq || t0 >= nt) return;
+    const int tn = min(MT_TB, nt - t0);
+    const uint4* tsrc = reinterpret_cast<const uint4*>(desc + (int64_t)ti * max_kp + t0);
+    for (int i = threadIdx.x; i < tn * 2; i += 256) s_t[i] = tsrc[i];
+    uint32_t qd[MT_QPT][8];
+    uint32_t best[MT_QPT];
+#pragma unroll
+    for (int k = 0; k < MT_QPT; ++k) {
+        const int q = q0 + threadIdx.x + 256 * k;
+        best[k] = 0xFFFFFFFFu;
+        const Desc* qs = desc + (int64_t)qi * max_kp + (q < nq ? q : 0);
+        const uint4 a = reinterpret_cast<const uint4*>(qs)[0];
+        const uint4 bq = reinterpret_cast<const uint4*>(qs)[1];
+        qd[k][0] = a.x; qd[k][1] = a.y; qd[k][2] = a.z; qd[k][3] = a.w;
+        qd[k][4] = bq.x; qd[k][5] = bq.y; qd[k][6] = bq.z; qd[k][7] = bq.w;
+    }
+    __syncthreads();
+    for (int t = 0; t < tn; ++t) {
+        const uint4 a = s_t[2 * t], bq = s_t[2 * t + 1];
+        const uint32_t tag = (uint32_t)(t0 + t);
+#pragma unroll
+        for (int k = 0; k < MT_QPT; ++k) {
+            uint32_t d = __popc(qd[k][0] ^ a.x);
+            d += __popc(qd[k][1] ^ a.y);
+            d += __popc(qd[k][2] ^ a.z);
+            d += __popc(qd[k][3] ^ a.w);
+            d += __popc(qd[k][4] ^ bq.x);
+            d += __popc(qd[k][5] ^ bq.y);
+            d += __popc(qd[k][6] ^ bq.z);
+            d += __popc(qd[k][7] ^ bq.w);
+            const uint32_t key = (d << 16) | tag;  // min key = smallest distance, then first index
+            best[k] = min(best[k], key);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < MT_QPT; ++k) {
+        const int q = q0 + threadIdx.x + 256 * k;
+        if (q < nq) atomicMin(&match_key[(int64_t)pair * max_kp + q], best[k]);
+    }
+}
+
+void launch_match(const Desc* desc, const int32_t* kp_count, const int32_t* pairs, int n_pairs, int max_kp,
+                  uint32_t* match_key, hipStream_t s) {
+    dim3 grid((max_kp + MT_QB - 1) / MT_QB, (max_kp + MT_TB - 1) / MT_TB, n_pairs);
+    hipLaunchKernelGGL(match_kernel, grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Matches records + removeOutliers (one 1024-thread workgroup per pair)
+// ------------------------------------------------------------------------------------------------
+constexpr int FZ_NT = 1024;
+constexpr int REC_DW = 25;  // 100-B Matches record = 25 dwords
+
+__device__ __forceinline__ int block_min_int(int v, int* s_tmp) {
+    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+    const int wave = (int)threadIdx.x >> 6;
+    if (lane_id() == 0) s_tmp[wave] = v;
+    __syncthreads();
+    int r = s_tmp[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r = min(r, s_tmp[w]);
+    __syncthreads();
+    return r;
+}
+
+// removeOutliers limit: max(2*min_dist, thr) with the reference's int wrap-around.
+__device__ __forceinline__ int outlier_limit(int min_d, int thr) {
+    const int twice = (int)((uint32_t)min_d * 2u);
+    return twice > thr ? twice : thr;
+}
+
+__global__ __launch_bounds__(FZ_NT) void match_finalize_kernel(
+    uint32_t* __restrict__ match_key, const yv_keypoint* __restrict__ keypoints,
+    const int32_t* __restrict__ kp_count, const int32_t* __restrict__ pairs, int max_kp, int thr,
+    yv_match* __restrict__ matches, int32_t* __restrict__ match_count, yv_match* __restrict__ filtered,
+    int32_t* __restrict__ filt_count) {
+    __shared__ int s_dist[kMaxKp];
+    __shared__ int s_j[kMaxKp];
+    __shared__ int s_pos[kMaxKp];
+    __shared__ int s_tmp[40];
+    const int pair = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int qi = pairs[2 * pair], ti = pairs[2 * pair + 1];
+    const int nq = kp_count[qi];
+    uint32_t* keys = match_key + (int64_t)pair * max_kp;
+    int local_min = 0x7fffffff;
+    for (int i = tid; i < nq; i += FZ_NT) {
+        const uint32_t k = keys[i];
+        keys[i] = 0xFFFFFFFFu;  // consumed: ready for the next match into this pair slot
+        const int d = (k == 0xFFFFFFFFu) ? 0x7fffffff : (int)(k >> 16);
+        s_dist[i] = d;
+        s_j[i] = (k == 0xFFFFFFFFu) ? -1 : (int)(k & 0xFFFFu);
+        local_min = min(local_min, d);
+    }
+    const int min_d = block_min_int(local_min, s_tmp);
+    const int lim = outlier_limit(min_d, thr);
+    int flags[4], cnt = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = tid * 4 + u;
+        flags[u] = (i < nq && s_dist[i] < lim) ? 1 : 0;
+        cnt += flags[u];
+    }
+    int total = 0;
+    int off = block_excl_scan<FZ_NT>(cnt, s_tmp, &total);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = tid * 4 + u;
+        if (i < nq) s_pos[i] = flags[u] ? off : -1;
+        off += flags[u];
+    }
+    __syncthreads();
+    const uint32_t* qrec = reinterpret_cast<const uint32_t*>(keypoints + (int64_t)qi * max_kp);
+    const uint32_t* trec = reinterpret_cast<const uint32_t*>(keypoints + (int64_t)ti * max_kp);
+    uint32_t* out_all = reinterpret_cast<uint32_t*>(matches + (int64_t)pair * max_kp);
+    uint32_t* out_f = reinterpret_cast<uint32_t*>(filtered + (int64_t)pair * max_kp);
+    const int ndw = nq * REC_DW;
+    for (int dw = tid; dw < ndw; dw += FZ_NT) {
+        const int i = dw / REC_DW;
+        const int f = dw - i * REC_DW;
+        uint32_t v;
+        bool is_matched_dw = false;
+        if (f < 12) {
+            v = qrec[(int64_t)i * 12 + f];
+            if (f == 11) v &= 0xFFu;  // featVec[31]; the 3 pad bytes are always written as 0
+            is_matched_dw = (f == 3);
+        } else if (f < 24) {
+            const int g = f - 12;
+            const int j = s_j[i];
+            v = 0;
+            if (g < 3 && j >= 0) v = trec[(int64_t)j * 12 + g];
+            is_matched_dw = (g == 3);
+        } else {
+            v = (uint32_t)s_dist[i];
+        }
+        out_all[dw] = v;
+        const int p = s_pos[i];
+        if (p >= 0) {
+            if (is_matched_dw) v = (v & ~0xFFu) | 1u;  // matched = true on both copies
+            out_f[(int64_t)p * REC_DW + f] = v;
+        }
+    }
+    if (tid == 0) {
+        match_count[pair] = nq;
+        filt_count[pair] = total;
+    }
+}
+
+void launch_match_finalize(uint32_t* match_key, const yv_keypoint* keypoints, const int32_t* kp_count,
+                           const int32_t* pairs, int n_pairs, int max_kp, int thr, yv_match* matches,
+                           int32_t* match_count, yv_match* filtered, int32_t* filt_count, hipStream_t s) {
+    hipLaunchKernelGGL(match_finalize_kernel, dim3(n_pairs), dim3(FZ_NT), 0, s, match_key, keypoints, kp_count,
+                       pairs, max_kp, thr, matches, match_count, filtered, filt_count);
+}
+
+// removeOutliers over a caller-supplied Matches list (n <= kMaxKp), one workgroup.
+__global__ __launch_bounds__(FZ_NT) void filter_records_kernel(const yv_match* __restrict__ in, int n, int thr,
+                                                               yv_match* __restrict__ out,
+                                                               int32_t* __restrict__ out_count) {
+    __shared__ int s_pos[kMaxKp];
+    __shared__ int s_tmp[40];
+    const int tid = threadIdx.x;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(in);
+    int local_min = 0x7fffffff;
+    for (int i = tid; i < n; i += FZ_NT) local_min = min(local_min, (int)src[(int64_t)i * REC_DW + 24]);
+    const int min_d = block_min_int(local_min, s_tmp);
+    const int lim = outlier_limit(min_d, thr);
+    int flags[4], cnt = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = tid * 4 + u;
+        flags[u] = (i < n && (int)src[(int64_t)i * REC_DW + 24] < lim) ? 1 : 0;
+        cnt += flags[u];
+    }
+    int total = 0;
+    int off = block_excl_scan<FZ_NT>(cnt, s_tmp, &total);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = tid * 4 + u;
+        if (i < n) s_pos[i] = flags[u] ? off : -1;
+        off += flags[u];
+    }
+    __syncthreads();
+    uint32_t* dst = reinterpret_cast<uint32_t*>(out);
+    for (int dw = tid; dw < n * REC_DW; dw += FZ_NT) {
+        const int i = dw / REC_DW;
+        const int f = dw - i * REC_DW;
+        const int p = s_pos[i];
+        if (p < 0) continue;
+        uint32_t v = src[dw];
+        if (f == 3 || f == 15) v = (v & ~0xFFu) | 1u;
+        dst[(int64_t)p * REC_DW + f] = v;
+    }
+    if (tid == 0) *out_count = total;
+}
+
+void launch_filter_records(const yv_match* in, int n, int thr, yv_match* out, int32_t* out_count, hipStream_t s) {
+    hipLaunchKernelGGL(filter_records_kernel, dim3(1), dim3(FZ_NT), 0, s, in, n, thr, out, out_count);
+}
+
+}  // namespace yavo
