@@ -87,6 +87,15 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         return _lib
     if not os.path.exists(path):
         raise FileNotFoundError(f"{path} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process.  torch ships its own libamdhip64 (SONAME libamdhip64.so.7) and links it
+    # by the unversioned name; if libyavo.so were loaded first, /opt/rocm's copy would be mapped and torch
+    # would then map a second runtime (two HSA instances: "No HIP GPUs are available").  Loading torch first
+    # makes libyavo's NEEDED libamdhip64.so.7 resolve to the runtime already in the process.
+    if os.environ.get("YAVO_NO_TORCH", "0") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
