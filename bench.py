@@ -51,10 +51,8 @@ def stage_bytes(counts, B):
     nq = float(np.sum(counts["match"]))
     nf = float(np.sum(counts["filt"]))
     return {
-        # image read once, candidate keys (8 B) appended
-        "fast_harris": n_img * img + 8 * cand,
-        # image read once, blurred image written once
-        "blur": 2 * n_img * img,
+        # image read once, blurred image written once, candidate keys (8 B) appended
+        "detect": 2 * n_img * img + 8 * cand,
         # candidate keys read once; (row, col) + response + kp_src written
         "topk": 8 * cand + 12 * det + 16 * kp,
         # blurred image read once; 48-B KeyPoint + 32-B descriptor written per keypoint
@@ -73,7 +71,8 @@ def stage_valu_ops(counts, B):
     kq = counts["match"].astype(np.float64)
     # matcher: per (query, train) pair 8 xor + 8 popcount-accumulate + key build + min = 18 ops
     kt = counts["train"].astype(np.float64)
-    return {"fast_harris": px * 60.0, "match": float(np.sum(kq * kt)) * 18.0}
+    # detect: per tested pixel 17 LDS reads + 16 x (2 compares + and/or) + run test ~ 60 ops, blur 18 MACs
+    return {"detect": px * 78.0, "match": float(np.sum(kq * kt)) * 18.0}
 
 
 def cpu_baseline(kind, threads, offsets):

@@ -64,7 +64,8 @@ int yv_set_fast_params(yv_ctx* ctx, int intensity_threshold, int max_corners);
  * each in [-8, 8]. */
 int yv_set_brief_offsets(yv_ctx* ctx, const int8_t* offsets /* [256*4] */);
 /* 9-tap fixed-point Gaussian (8 fractional bits, sum 256) used in place of cv::GaussianBlur
- * (src/BriefDescriptor.cc:90).  Default = OpenCV's bit-exact 9 / 2.5 kernel {12,22,31,41,44,...}. */
+ * (src/BriefDescriptor.cc:90).  Default = OpenCV's bit-exact 9 / 2.5 kernel {12,22,31,41,44,...}.
+ * Each tap must be <= 255 (YV_ERR_INVALID otherwise). */
 int yv_set_blur_kernel(yv_ctx* ctx, const uint16_t* k9);
 
 /* ---- host-pointer drop-in entry points (synchronous) --------------------------------------------- */
@@ -102,11 +103,12 @@ int yv_batch_set_pairs(yv_batch* b, const int32_t* pairs /* [2*n_pairs] */, int 
 int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride, int64_t image_pitch,
                  int match_thr, int carry_from, void* stream);
 /* Per-stage device time of the runs since the last reset, when timing is enabled (HIP events recorded
- * on the run stream around every stage).  Stages: 0 fast+harris, 1 blur, 2 top-K, 3 brief, 4 match,
- * 5 finalize+filter.  ms[i] = summed milliseconds, *n_runs = runs accumulated. */
+ * on the run stream around every stage).  Stages: 0 detect (FAST + Harris + blur, one fused kernel),
+ * 1 top-K + checkBoundry, 2 BRIEF, 3 match, 4 Matches records + removeOutliers.  ms[i] = summed
+ * milliseconds, *n_runs = runs accumulated. */
 int yv_batch_enable_timing(yv_batch* b, int on);
 int yv_batch_stage_times(yv_batch* b, float* ms /* [8] */, int* n_runs);
-#define YV_NUM_STAGES 6
+#define YV_NUM_STAGES 5
 
 /* Device views of the batch results (valid until the next run / destroy).  All arrays are indexed
  * [slot][...] with the per-slot strides given. */

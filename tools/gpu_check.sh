@@ -21,9 +21,12 @@ run() {  # run NAME TIMEOUT CMD...
 }
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 
-run pytest_gpu 900 python -m pytest tests -m gpu -q -rf; st=$?; ok $st || exit $st
-run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; st=$?; ok $st || exit $st
+if [ "${SKIP_TESTS:-0}" != "1" ]; then
+    run pytest_gpu 900 python -m pytest tests -m gpu -q -rf; st=$?; ok $st || exit $st
+    run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; st=$?; ok $st || exit $st
+fi
 run bench 900 python bench.py "$@"; st=$?; ok $st || exit $st
+[ "${PROFILE:-1}" = "1" ] || exit 0
 export TMPDIR=/tmp
 run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
     python3 "$ROOT/bench.py" --steps 5 --warmup 1 --cpu-baseline none "$@"; st=$?; ok $st || exit $st

@@ -20,8 +20,8 @@ YV_ERR_INVALID = -1
 YV_ERR_HIP = -2
 YV_ERR_NODEVICE = -3
 YV_ERR_CAPACITY = -4
-YV_NUM_STAGES = 6
-STAGE_NAMES = ("fast_harris", "blur", "topk", "brief", "match", "finalize")
+YV_NUM_STAGES = 5
+STAGE_NAMES = ("detect", "topk", "brief", "match", "finalize")
 
 # byte-identical to KeyPoint (48 B) / Matches (100 B), /root/reference/include/BriefDescriptor.hpp:11-39
 KEYPOINT_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("id", "<i4"), ("matched", "u1"),

@@ -236,7 +236,10 @@ int yv_set_brief_offsets(yv_ctx* ctx, const int8_t* offsets) {
 int yv_set_blur_kernel(yv_ctx* ctx, const uint16_t* k9) {
     if (!ctx || !k9) return YV_ERR_INVALID;
     uint32_t sum = 0;
-    for (int i = 0; i < 9; ++i) sum += k9[i];
+    for (int i = 0; i < 9; ++i) {
+        if (k9[i] > 255u) return YV_ERR_INVALID;  // taps are packed as u8 for v_dot4_u32_u8
+        sum += k9[i];
+    }
     if (sum != 256u) return YV_ERR_INVALID;  // 8 fractional bits: the kernel must sum to 1.0
     std::memcpy(ctx->k9, k9, sizeof(ctx->k9));
     return YV_OK;
@@ -366,25 +369,23 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
     if (b->timing && b->runs_recorded < kMaxTimedRuns) run = b->runs_recorded++;
     int rc = YV_OK;
     rc |= record_stage(b, s, run, 0);
-    yavo::launch_fast_harris(d_images, n_images, H, W, stride, image_pitch, ctx->fast_thr, b->cand_keys, b->cap,
-                             b->cand_count, s);
+    yavo::launch_detect_blur(d_images, n_images, H, W, stride, image_pitch, ctx->fast_thr, b->cand_keys, b->cap,
+                             b->cand_count, ctx->k9, b->blur, s);
     rc |= record_stage(b, s, run, 1);
-    yavo::launch_blur9(d_images, n_images, H, W, stride, image_pitch, ctx->k9, b->blur, s);
+    yavo::launch_topk(b->cand_keys, b->cap, b->cand_count, b->cand_seen, n_images, H, W, K, keep, b->det_rc,
+                      b->det_resp, b->det_count, b->kp_src, b->kp_count, s);
     rc |= record_stage(b, s, run, 2);
-    yavo::launch_topk(b->cand_keys, b->cap, b->cand_count, b->cand_seen, n_images, H, W, K, keep, b->det_rc, b->det_resp,
-                      b->det_count, b->kp_src, b->kp_count, s);
-    rc |= record_stage(b, s, run, 3);
     yavo::launch_brief(b->blur, n_images, H, W, ctx->d_offsets, b->kp_src, b->kp_count, K, b->keypoints, b->desc, s);
-    rc |= record_stage(b, s, run, 4);
+    rc |= record_stage(b, s, run, 3);
     if (b->n_pairs > 0) {
         yavo::launch_match(b->desc, b->kp_count, b->pairs, b->n_pairs, K, b->match_key, s);
-        rc |= record_stage(b, s, run, 5);
+        rc |= record_stage(b, s, run, 4);
         yavo::launch_match_finalize(b->match_key, b->keypoints, b->kp_count, b->pairs, b->n_pairs, K, match_thr,
                                     b->matches, b->match_count, b->filtered, b->filt_count, s);
     } else {
-        rc |= record_stage(b, s, run, 5);
+        rc |= record_stage(b, s, run, 4);
     }
-    rc |= record_stage(b, s, run, 6);
+    rc |= record_stage(b, s, run, 5);
     if (carry_from >= 0) {
         const size_t c = (size_t)carry_from, dst = (size_t)b->max_images, nk = (size_t)K;
         YV_HIP(hipMemcpyAsync(b->keypoints + dst * nk, b->keypoints + c * nk, nk * sizeof(yv_keypoint),

@@ -20,6 +20,10 @@ struct Desc {                      // 256-bit BRIEF descriptor, test j -> bit j 
 void launch_fast_harris(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,
                         int thr, uint64_t* cand_keys, int64_t cap, uint32_t* cand_count,
                         hipStream_t s);
+// Fused FAST + Harris + 9x9 blur over the same LDS tile (the image is read once).
+void launch_detect_blur(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch, int thr,
+                        uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, const uint16_t* k9_host,
+                        uint8_t* blur, hipStream_t s);
 // 9-tap separable fixed-point Gaussian, BORDER_REFLECT_101; output H x W contiguous per image.
 void launch_blur9(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,
                   const uint16_t* k9_host, uint8_t* blur, hipStream_t s);

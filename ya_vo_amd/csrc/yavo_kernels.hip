@@ -119,52 +119,92 @@ __device__ __forceinline__ float key_resp(uint64_t key) {
     return __uint_as_float(u);
 }
 
+struct K9 {
+    uint32_t k[9];
+    uint32_t k4[2];   // taps 0..3 and 4..7 as packed u8 (v_dot4_u32_u8)
+    uint32_t k2e[4];  // (k0,k1) (k2,k3) (k4,k5) (k6,k7) as packed u16 (v_dot2_u32_u16), even output rows
+    uint32_t k2o[4];  // (k1,k2) (k3,k4) (k5,k6) (k7,k8), odd output rows
+};
+
+static K9 make_k9(const uint16_t* k9) {
+    K9 kw;
+    for (int i = 0; i < 9; ++i) kw.k[i] = k9[i];
+    for (int h = 0; h < 2; ++h)
+        kw.k4[h] = k9[4 * h] | (k9[4 * h + 1] << 8) | (k9[4 * h + 2] << 16) | ((uint32_t)k9[4 * h + 3] << 24);
+    for (int t = 0; t < 4; ++t) {
+        kw.k2e[t] = k9[2 * t] | ((uint32_t)k9[2 * t + 1] << 16);
+        kw.k2o[t] = k9[2 * t + 1] | ((uint32_t)k9[2 * t + 2] << 16);
+    }
+    return kw;
+}
+
+__device__ __forceinline__ int reflect101(int p, int len) {
+    // cv::borderInterpolate(BORDER_REFLECT_101); callers clamp p to [-(len-1), 2*len-2]
+    if (p < 0) p = -p;
+    if (p >= len) p = 2 * len - p - 2;
+    return p;
+}
+
+// Fused per-tile detector: FAST-12 candidate test + Harris response (src/FastDetector.cc:298-335) and the
+// 9x9 fixed-point Gaussian of the same tile (src/BriefDescriptor.cc:90), so the image is read from HBM
+// once.  One 256-thread workgroup per 64 x 32 output tile, the tile plus a 4-pixel halo staged in LDS
+// (BORDER_REFLECT_101 values outside the image: the blur needs them, no FAST candidate ever reads them).
+// Candidates are staged in LDS and appended with ONE global atomic per workgroup.
 constexpr int FT_W = kFastTileW;        // 64 output columns per tile (one wave-row)
 constexpr int FT_H = kFastTileH;        // 32 output rows per tile
-constexpr int FT_R = 3;                 // halo: ring radius 3, Sobel+3x3 window radius 2
-constexpr int FT_LW = FT_W + 2 * FT_R;  // 70 bytes per LDS row
-constexpr int FT_LWP = 72;              // padded LDS row stride
-constexpr int FT_LH = FT_H + 2 * FT_R;  // 38 LDS rows
+constexpr int FT_R = 4;                 // halo: blur radius 4 (ring radius 3, Sobel + 3x3 window radius 2)
+constexpr int FT_LW = FT_W + 2 * FT_R;  // 72 bytes per LDS row
+constexpr int FT_LH = FT_H + 2 * FT_R;  // 40 LDS rows
 
-__global__ __launch_bounds__(256) void fast_harris_kernel(const uint8_t* __restrict__ imgs, int H, int W,
-                                                          int stride, int64_t pitch, int thr,
-                                                          uint64_t* __restrict__ cand_keys, int64_t cap,
-                                                          uint32_t* __restrict__ cand_count) {
-    __shared__ uint8_t tile[FT_LH * FT_LWP];
+template <bool kBlur>
+__global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__ imgs, int H, int W, int stride,
+                                                     int64_t pitch, int thr, uint64_t* __restrict__ cand_keys,
+                                                     int64_t cap, uint32_t* __restrict__ cand_count, K9 kw,
+                                                     uint8_t* __restrict__ blur) {
+    __shared__ uint8_t tile[FT_LH * FT_LW];
+    __shared__ uint32_t hbuf[kBlur ? (FT_LH / 2) * FT_W : 1];
+    __shared__ uint16_t s_pos[FT_W * FT_H];
+    __shared__ uint32_t s_n, s_base;
     const int img = blockIdx.z;
     const int r0 = blockIdx.y * FT_H, c0 = blockIdx.x * FT_W;
     const uint8_t* src = imgs + (int64_t)img * pitch;
     const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int wave = tid >> 6;
+    if (tid == 0) s_n = 0;
 
-    // Stage the (FT_H + 6) x (FT_W + 6) tile; pixels outside the image are never read by a valid
-    // candidate (rows 4..H-5 / cols 4..W-5 with a radius-3 footprint) and are filled with 0.
-    for (int i = tid; i < FT_LH * FT_LW; i += 256) {
-        const int lr = i / FT_LW, lc = i - lr * FT_LW;
-        const int r = r0 - FT_R + lr, c = c0 - FT_R + lc;
-        uint8_t v = 0;
-        if (r >= 0 && r < H && c >= 0 && c < W) v = src[(int64_t)r * stride + c];
-        tile[lr * FT_LWP + lc] = v;
+    // stage (FT_H + 8) x (FT_W + 8): wave w loads rows w, w+4, ...; lanes 0..63 (+ 0..7) cover 72 columns
+    const int cA = reflect101(min(max(c0 - FT_R + lane, -(W - 1)), 2 * W - 2), W);
+    const int cB = reflect101(min(max(c0 - FT_R + 64 + (lane & 7), -(W - 1)), 2 * W - 2), W);
+    for (int lr = wave; lr < FT_LH; lr += 4) {
+        const int r = reflect101(min(max(r0 - FT_R + lr, -(H - 1)), 2 * H - 2), H);
+        const uint8_t* row = src + (int64_t)r * stride;
+        const uint8_t a = row[cA];
+        tile[lr * FT_LW + lane] = a;
+        if (lane < FT_LW - 64) tile[lr * FT_LW + 64 + lane] = row[cB];
     }
     __syncthreads();
 
     constexpr int ring_dr[16] = YV_RING_DR;
     constexpr int ring_dc[16] = YV_RING_DC;
-    const int tx = tid & 63, ty = tid >> 6;
+    const uint32_t neg_thr = (uint32_t)(-thr);
+    const int tx = lane, ty = wave;
     const int c = c0 + tx;
-    const int lane = lane_id();
     for (int rr = ty; rr < FT_H; rr += 4) {
         const int r = r0 + rr;
         const bool inside = (r >= 4) && (r < H - 4) && (c >= 4) && (c < W - 4);
-        const uint8_t* t0 = &tile[(rr + FT_R) * FT_LWP + tx + FT_R];
-        const int cent = t0[0];
-        uint32_t mask = 0;
+        const uint8_t* t0 = &tile[(rr + FT_R) * FT_LW + tx + FT_R];
+        const uint32_t cent = t0[0];
+        uint32_t sim = 0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            const int p = t0[ring_dr[k] * FT_LWP + ring_dc[k]];
-            // !checkInBetween(cent, p)  <=>  !(cent > p - thr && cent < p + thr)
-            const bool diff = !((cent > p - thr) && (cent < p + thr));
-            mask |= (uint32_t)diff << k;
+            const uint32_t p = t0[ring_dr[k] * FT_LW + ring_dc[k]];
+            // checkInBetween(cent, p) <=> cent > p - thr && cent < p + thr <=> |cent - p| - thr < 0:
+            // v_sad_u8 gives |cent - p| + (-thr) in one instruction; its sign bit is "similar"
+            const uint32_t t = __builtin_amdgcn_sad_u8(cent, p, neg_thr);
+            sim |= (t >> 31) << k;
         }
+        const uint32_t mask = ~sim & 0xFFFFu;  // "different" ring pixels
         // pretest on ring indices 0, 7 and (4 | 12) (src/FastDetector.cc:304-317)
         const bool pre = (mask & 1u) && (mask & (1u << 7)) && ((mask & (1u << 4)) || (mask & (1u << 12)));
         // >= 12 consecutive set bits in mask[0..15], no wrap (checkContiguousPixels)
@@ -173,19 +213,61 @@ __global__ __launch_bounds__(256) void fast_harris_kernel(const uint8_t* __restr
         const uint32_t a8 = a4 & (a4 >> 4);
         const uint32_t a12 = a8 & (a4 >> 8);
         const bool cand = inside && pre && (a12 != 0u);
-
-        uint64_t key = 0;
-        if (cand) {
+        const uint64_t bal = __ballot(cand);
+        if (bal == 0) continue;  // wave-uniform: no corner in this 64-pixel row segment
+        // stage the corner's tile position; Harris runs densely over the staged list below
+        const int leader = __ffsll((long long)bal) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&s_n, (uint32_t)__popcll(bal));
+        base = __shfl(base, leader, 64);
+        if (cand) s_pos[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(rr * FT_W + tx);
+    }
+    __syncthreads();
+    const uint32_t n = s_n;
+    // one global atomic per workgroup reserves the output range of this tile's corners
+    if (tid == 0 && n > 0) s_base = atomicAdd(&cand_count[img], n);
+    if (kBlur) {
+        // horizontal pass, exact: h = sum_j k_j * p[x + j] as two v_dot4_u32_u8 + one mad on the byte row
+        // (rows start 4-byte aligned: FT_LW = 72).  h <= 255 * 256 fits 16 bits; rows 2q and 2q+1 are
+        // packed into one dword so the vertical pass can use v_dot2_u32_u16.
+        const uint32_t* trow = reinterpret_cast<const uint32_t*>(tile);
+        for (int i = tid; i < (FT_LH / 2) * FT_W; i += 256) {
+            const int q = i >> 6, x = i & 63;
+            const int sh = x & 3;
+            uint32_t hv[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t* wr = trow + ((2 * q + h) * FT_LW >> 2) + (x >> 2);
+                const uint32_t d0 = wr[0], d1 = wr[1], d2 = wr[2];
+                const uint32_t b0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                const uint32_t b1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                const uint32_t b8 = (d2 >> (8 * sh)) & 0xFFu;
+                uint32_t acc = __builtin_amdgcn_udot4(b0, kw.k4[0], 0u, false);
+                acc = __builtin_amdgcn_udot4(b1, kw.k4[1], acc, false);
+                hv[h] = acc + kw.k[8] * b8;
+            }
+            hbuf[i] = hv[0] | (hv[1] << 16);
+        }
+    }
+    __syncthreads();
+    // Harris response of every staged corner, one lane per corner (no divergence across FAST lanes);
+    // consecutive lanes write consecutive keys
+    if (n > 0) {
+        uint64_t* out = cand_keys + (int64_t)img * cap + s_base;
+        for (uint32_t i = tid; i < n; i += 256) {
+            const int pos = s_pos[i];
+            const int prr = pos >> 6, ptx = pos & 63;
+            const uint8_t* t0 = &tile[(prr + FT_R) * FT_LW + ptx + FT_R];
             // Sobel Ix / Iy (3x3 correlation) at the 3x3 window around the corner, from the 5x5 patch.
             int sxx = 0, sxy = 0, syy = 0;
 #pragma unroll
-            for (int i = -1; i <= 1; ++i) {
+            for (int ii = -1; ii <= 1; ++ii) {
 #pragma unroll
                 for (int j = -1; j <= 1; ++j) {
-                    const uint8_t* q = t0 + i * FT_LWP + j;
-                    const int pmm = q[-FT_LWP - 1], pm0 = q[-FT_LWP], pmp = q[-FT_LWP + 1];
+                    const uint8_t* q = t0 + ii * FT_LW + j;
+                    const int pmm = q[-FT_LW - 1], pm0 = q[-FT_LW], pmp = q[-FT_LW + 1];
                     const int p0m = q[-1], p0p = q[1];
-                    const int ppm = q[FT_LWP - 1], pp0 = q[FT_LWP], ppp = q[FT_LWP + 1];
+                    const int ppm = q[FT_LW - 1], pp0 = q[FT_LW], ppp = q[FT_LW + 1];
                     const int gx = (pmp - pmm) + 2 * (p0p - p0m) + (ppp - ppm);
                     const int gy = (ppm - pmm) + 2 * (pp0 - pm0) + (ppp - pmp);
                     sxx += gx * gx;
@@ -195,17 +277,30 @@ __global__ __launch_bounds__(256) void fast_harris_kernel(const uint8_t* __restr
             }
             // all partial sums are integers < 2^24: exact in float, as in the reference
             const float resp = harris_response((float)sxx, (float)sxy, (float)syy);
-            key = make_key(resp, (uint32_t)(r * W + c));
+            out[i] = make_key(resp, (uint32_t)((r0 + prr) * W + (c0 + ptx)));  // cap >= every pixel: in range
         }
-        const uint64_t bal = __ballot(cand);
-        if (bal) {
-            const int leader = __ffsll((long long)bal) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&cand_count[img], (uint32_t)__popcll(bal));
-            base = __shfl(base, leader, 64);
-            if (cand) {
-                const uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-                if ((int64_t)pos < cap) cand_keys[(int64_t)img * cap + pos] = key;
+    }
+    if (kBlur) {
+        // vertical pass, exact u32: rows 2m and 2m+1 of column x from the row-pair dwords P_m .. P_{m+4}
+        typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+        uint8_t* dst = blur + (int64_t)img * H * W;
+        for (int i = tid; i < (FT_H / 2) * FT_W; i += 256) {
+            const int m = i >> 6, x = i & 63;
+            uint32_t P[5];
+#pragma unroll
+            for (int t = 0; t < 5; ++t) P[t] = hbuf[(m + t) * FT_W + x];
+            uint32_t ev = 0, od = kw.k[0] * (P[0] >> 16);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                ev = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, P[t]), __builtin_bit_cast(us2, kw.k2e[t]), ev, false);
+                od = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, P[t + 1]), __builtin_bit_cast(us2, kw.k2o[t]), od, false);
+            }
+            ev += kw.k[8] * (P[4] & 0xFFFFu);
+            const int r = r0 + 2 * m, c = c0 + x;
+            if (c < W) {
+                const uint32_t v0 = (ev + (1u << 15)) >> 16, v1 = (od + (1u << 15)) >> 16;
+                if (r < H) dst[(int64_t)r * W + c] = (uint8_t)(v0 > 255u ? 255u : v0);
+                if (r + 1 < H) dst[(int64_t)(r + 1) * W + c] = (uint8_t)(v1 > 255u ? 255u : v1);
             }
         }
     }
@@ -214,26 +309,26 @@ __global__ __launch_bounds__(256) void fast_harris_kernel(const uint8_t* __restr
 void launch_fast_harris(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,
                         int thr, uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, hipStream_t s) {
     dim3 grid((W + FT_W - 1) / FT_W, (H + FT_H - 1) / FT_H, n_images);
-    hipLaunchKernelGGL(fast_harris_kernel, grid, dim3(256), 0, s, imgs, H, W, stride, pitch, thr, cand_keys,
-                       cap, cand_count);
+    K9 kw = {};
+    hipLaunchKernelGGL(detect_kernel<false>, grid, dim3(256), 0, s, imgs, H, W, stride, pitch, thr, cand_keys,
+                       cap, cand_count, kw, (uint8_t*)nullptr);
+}
+
+void launch_detect_blur(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch, int thr,
+                        uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, const uint16_t* k9_host,
+                        uint8_t* blur, hipStream_t s) {
+    dim3 grid((W + FT_W - 1) / FT_W, (H + FT_H - 1) / FT_H, n_images);
+    const K9 kw = make_k9(k9_host);
+    hipLaunchKernelGGL(detect_kernel<true>, grid, dim3(256), 0, s, imgs, H, W, stride, pitch, thr, cand_keys, cap,
+                       cand_count, kw, blur);
 }
 
 // ------------------------------------------------------------------------------------------------
 // 9x9 fixed-point Gaussian blur (OpenCV GaussianBlurFixedPoint<uint8_t, ufixedpoint16>)
 // ------------------------------------------------------------------------------------------------
-struct K9 {
-    uint32_t k[9];
-};
 constexpr int BL_W = 64, BL_H = 32, BL_R = 4;
 constexpr int BL_LW = BL_W + 2 * BL_R;  // 72
 constexpr int BL_LH = BL_H + 2 * BL_R;  // 40
-
-__device__ __forceinline__ int reflect101(int p, int len) {
-    // cv::borderInterpolate(BORDER_REFLECT_101) for |p| < len
-    if (p < 0) p = -p;
-    if (p >= len) p = 2 * len - p - 2;
-    return p;
-}
 
 __global__ __launch_bounds__(256) void blur9_kernel(const uint8_t* __restrict__ imgs, int H, int W, int stride,
                                                     int64_t pitch, K9 kw, uint8_t* __restrict__ blur) {
@@ -274,8 +369,7 @@ __global__ __launch_bounds__(256) void blur9_kernel(const uint8_t* __restrict__ 
 
 void launch_blur9(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,
                   const uint16_t* k9_host, uint8_t* blur, hipStream_t s) {
-    K9 kw;
-    for (int i = 0; i < 9; ++i) kw.k[i] = k9_host[i];
+    const K9 kw = make_k9(k9_host);
     dim3 grid((W + BL_W - 1) / BL_W, (H + BL_H - 1) / BL_H, n_images);
     hipLaunchKernelGGL(blur9_kernel, grid, dim3(256), 0, s, imgs, H, W, stride, pitch, kw, blur);
 }
