@@ -228,3 +228,50 @@ def test_batch_is_deterministic_and_timed(ctx):
     ms, n = b.stage_times()
     assert n == 3 and np.all(ms > 0)
     b.close()
+
+
+def test_cpp_frontend_demo_matches_oracle(oracle, offsets, tmp_path):
+    """The C++ host side (ya_vo_amd/frontend: FastDetector / Brief over the C ABI, LoopHandler-shaped
+    driver) produces the oracle's keypoints and matches for a short synthetic sequence."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "ya_vo_amd", "bin", "yavo_frontend_demo")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(root, "ya_vo_amd", "frontend")], check=True)
+    H, W, n = 376, 1241, 3
+    frames = np.stack([synth_frame(555, k, 3 * k) for k in range(n)])
+    raw = tmp_path / "frames.raw"
+    with open(raw, "wb") as f:
+        f.write(np.array([n, H, W], np.int32).tobytes())
+        f.write(frames.tobytes())
+    out = tmp_path / "out.bin"
+    off = os.path.join(GOLDEN, "brief_offsets_mt19937_42.bin")
+    env = dict(os.environ)
+    r = subprocess.run([exe, str(raw), off, str(out)], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    buf = open(out, "rb").read()
+    pos = 0
+
+    def take(dtype, count):
+        nonlocal pos
+        a = np.frombuffer(buf, dtype, count, pos)
+        pos += a.nbytes
+        return a
+
+    prev = None
+    for k in range(n):
+        nk = int(take(np.int32, 1)[0])
+        kps = take(yv.KEYPOINT_DTYPE, nk)
+        orc, _, _ = oracle.fast(frames[k], 2000)
+        ok = oracle.brief(frames[k], orc, offsets)
+        np.testing.assert_array_equal(kps, ok)
+        if prev is not None:
+            nm = int(take(np.int32, 1)[0])
+            m = take(yv.MATCH_DTYPE, nm)
+            nf = int(take(np.int32, 1)[0])
+            f = take(yv.MATCH_DTYPE, nf)
+            om = oracle.match(prev, ok)
+            np.testing.assert_array_equal(m, om)
+            np.testing.assert_array_equal(f, oracle.remove_outliers(om, 20))
+        prev = ok
+    assert pos == len(buf)

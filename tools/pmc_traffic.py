@@ -1,0 +1,69 @@
+"""Parse the two rocprofv3 --pmc passes of tools/pmc_traffic.sh into per-launch HBM bytes per stage.
+
+gfx950 correction (MI355X_MICROARCH.md 'HBM'; cdna_hip_programming.md section 7): FETCH_SIZE and WRITE_SIZE
+are in KiB; FETCH_SIZE reports exactly half the bytes of a wide coalesced streaming read, so
+    traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
+The raw counters are kept next to the corrected figure (other access widths are uncalibrated)."""
+import csv
+import glob
+import json
+import os
+import sys
+
+STAGE_OF = {"detect_kernel": "detect", "topk_kernel": "topk", "brief_kernel": "brief",
+            "match_finalize_kernel": "finalize", "match_kernel": "match"}
+
+
+def stage(kernel_name):
+    for key, st in STAGE_OF.items():
+        if "yavo::" + key in kernel_name or key + "<" in kernel_name or kernel_name.startswith(key):
+            return st
+    return None
+
+
+def load(out_dir, counter):
+    files = glob.glob(os.path.join(out_dir, f"pmc_{counter}", "**", "*counter_collection*.csv"), recursive=True)
+    per = {}
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                name = row.get("Kernel_Name") or row.get("Kernel-Name") or ""
+                if (row.get("Counter_Name") or "") != counter:
+                    continue
+                st = stage(name)
+                if st is None:
+                    continue
+                per.setdefault(st, []).append(float(row.get("Counter_Value") or 0.0))
+    return per
+
+
+def main():
+    out_dir = sys.argv[1]
+    frames = 64
+    args = sys.argv[2:]
+    if "--frames" in args:
+        frames = int(args[args.index("--frames") + 1])
+    fetch = load(out_dir, "FETCH_SIZE")
+    write = load(out_dir, "WRITE_SIZE")
+    res = {"frames_per_step": frames, "units": "bytes per launch", "per_launch_bytes": {}, "raw_kib": {},
+           "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count correction)"}
+    for st in sorted(set(fetch) | set(write)):
+        f = fetch.get(st, [])
+        w = write.get(st, [])
+        # skip the warm-up launch: use the last three dispatches of each stage
+        f = f[-3:] if len(f) > 3 else f
+        w = w[-3:] if len(w) > 3 else w
+        fm = sum(f) / len(f) if f else 0.0
+        wm = sum(w) / len(w) if w else 0.0
+        res["raw_kib"][st] = {"FETCH_SIZE": fm, "WRITE_SIZE": wm, "dispatches": [len(f), len(w)]}
+        res["per_launch_bytes"][st] = int((2 * fm + wm) * 1024)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(root, "profiles", "pmc_traffic.json")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    json.dump(res, open(path, "w"), indent=1)
+    json.dump(res, open(os.path.join(out_dir, "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
