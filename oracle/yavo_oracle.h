@@ -77,6 +77,42 @@ int or_remove_outliers(const yv_match* in, int n, int thr, yv_match* out, int* n
  * 4x4 (missing values -> 0; the reference reads past a 12-value vector). returns #values parsed. */
 int or_parse_calib_string(const char* s, double out[16]);
 
+/* ---- geometry (yavo_oracle_geom.c) ---- */
+/* Poses are Sophus::SE3d::data(): {qx, qy, qz, qw, tx, ty, tz} (T_cw).  K is row-major 3x3. */
+/* OpenCV JacobiSVDImpl_<double> on At (n rows of m), as cv::SVD calls it. */
+void or_cv_jacobi_svd(double* At, int astep, double* W, double* Vt, int vstep, int m, int n, int n1);
+/* cv::SVD(src, FULL_UV) for square row-major n x n (n <= 9). */
+void or_cv_svd(const double* src, int n, double* w, double* u, double* vt);
+/* _3DHandler::getFundamentalMatrix (src/3DHandler.cc:50-142); pts [n][4] = (x1, y1, x2, y2). */
+int or_fundamental_8pt(const double* pts, int n, double F[9]);
+/* _3DHandler::getFRANSAC (src/3DHandler.cc:145-195) with explicit samples [iters][8]. */
+int or_f_ransac(const yv_match* m, int n, const int32_t* sample_idx, int iters, double thr, double F[9],
+                int* max_inliers);
+/* Eigen JacobiSVD (square, column-major): sv descending, V column-major. */
+int or_eigen_jacobi_svd(const double* A, int n, double* sv, double* V);
+/* LoopHandler::triangulation (src/LoopHandler.cc:867-885) for two poses and normalised points. */
+int or_triangulate_one(const double* Ta, const double* Tb, const double* pa, const double* pb, double* Xw);
+/* triangulate2View's per-match part (src/LoopHandler.cc:665-676): returns #ok. */
+int or_triangulate_matches(const double* Ta, const double* Tb, const double* K, const yv_match* m, int n,
+                           double* Xw, uint8_t* ok);
+/* Sophus pieces */
+void or_se3_exp(const double* a, double* out);
+void or_se3_mul(const double* A, const double* B, double* out);
+void or_se3_act(const double* T, const double* p, double* out);
+void or_quat_to_R(const double* q, double* R);
+double or_ksin(double x);
+double or_kcos(double x);
+/* Frame::world2Camera (src/Frame.cc:16-28): out [n][3] = K [R|t] [X; 1]. */
+void or_world2camera(const double* X, int n, const double* T, const double* K, double* out);
+/* Eigen LDLT solve of a 6x6 (variant 0: MatrixXd / g2o, 1: Matrix6d / test.cc). Returns isPositive. */
+int or_ldlt6_solve(const double* H, const double* b, double* x, int variant);
+/* LoopHandler::optimizePoseOnly (src/LoopHandler.cc:730-861); returns inliers.  sum_mode 0 = sequential
+ * edge sums (reference), 1 = the GPU's fixed tree order. */
+int or_pose_lm(const double* X, const double* uv, int n, const double* K, double* pose, uint8_t* outlier,
+               int sum_mode);
+/* bundleAdjustmentGaussNewton (src/test.cc:172-244); returns accepted iterations. */
+int or_pose_gn(const double* X, const double* uv, int n, const double* K, double* pose, int sum_mode);
+
 #ifdef __cplusplus
 }
 #endif

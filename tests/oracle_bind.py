@@ -39,6 +39,22 @@ class Oracle:
             "or_match": (_I, [_P, _I, _P, _I, _P]),
             "or_remove_outliers": (_I, [_P, _I, _I, _P, ctypes.POINTER(_I)]),
             "or_parse_calib_string": (_I, [ctypes.c_char_p, _P]),
+            "or_cv_svd": (None, [_P, _I, _P, _P, _P]),
+            "or_fundamental_8pt": (_I, [_P, _I, _P]),
+            "or_f_ransac": (_I, [_P, _I, _P, _I, ctypes.c_double, _P, ctypes.POINTER(_I)]),
+            "or_eigen_jacobi_svd": (_I, [_P, _I, _P, _P]),
+            "or_triangulate_one": (_I, [_P, _P, _P, _P, _P]),
+            "or_triangulate_matches": (_I, [_P, _P, _P, _P, _I, _P, _P]),
+            "or_se3_exp": (None, [_P, _P]),
+            "or_se3_mul": (None, [_P, _P, _P]),
+            "or_se3_act": (None, [_P, _P, _P]),
+            "or_quat_to_R": (None, [_P, _P]),
+            "or_ksin": (ctypes.c_double, [ctypes.c_double]),
+            "or_kcos": (ctypes.c_double, [ctypes.c_double]),
+            "or_world2camera": (None, [_P, _I, _P, _P, _P]),
+            "or_ldlt6_solve": (_I, [_P, _P, _P, _I]),
+            "or_pose_lm": (_I, [_P, _P, _I, _P, _P, _P, _I]),
+            "or_pose_gn": (_I, [_P, _P, _I, _P, _P, _I]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -134,3 +150,103 @@ class Oracle:
         out = np.zeros(16, np.float64)
         nv = self.lib.or_parse_calib_string(s.encode(), _p(out))
         return out.reshape(4, 4), nv
+
+    # ---- geometry ----
+    def cv_svd(self, A):
+        A = np.ascontiguousarray(A, np.float64)
+        n = A.shape[0]
+        w = np.zeros(n)
+        u = np.zeros((n, n))
+        vt = np.zeros((n, n))
+        self.lib.or_cv_svd(_p(A), n, _p(w), _p(u), _p(vt))
+        return w, u, vt
+
+    def fundamental(self, pts):
+        pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 4)
+        F = np.zeros(9)
+        ok = self.lib.or_fundamental_8pt(_p(pts), len(pts), _p(F))
+        return bool(ok), F.reshape(3, 3)
+
+    def f_ransac(self, matches, samples, thr=0.1):
+        m = np.ascontiguousarray(matches, MATCH_DTYPE)
+        smp = np.ascontiguousarray(samples, np.int32).reshape(-1, 8)
+        F = np.zeros(9)
+        mi = _I()
+        ok = self.lib.or_f_ransac(_p(m), len(m), _p(smp), len(smp), thr, _p(F), ctypes.byref(mi))
+        return bool(ok), F.reshape(3, 3), mi.value
+
+    def eigen_svd(self, A):
+        Acm = np.ascontiguousarray(np.asarray(A, np.float64).T)  # column-major
+        n = Acm.shape[0]
+        sv = np.zeros(n)
+        V = np.zeros(n * n)
+        ok = self.lib.or_eigen_jacobi_svd(_p(Acm), n, _p(sv), _p(V))
+        return bool(ok), sv, V.reshape(n, n).T
+
+    def triangulate_matches(self, Ta, Tb, K, matches):
+        Ta = np.ascontiguousarray(Ta, np.float64)
+        Tb = np.ascontiguousarray(Tb, np.float64)
+        K = np.ascontiguousarray(K, np.float64).reshape(9)
+        m = np.ascontiguousarray(matches, MATCH_DTYPE)
+        X = np.zeros((max(len(m), 1), 3))
+        ok = np.zeros(max(len(m), 1), np.uint8)
+        n = self.lib.or_triangulate_matches(_p(Ta), _p(Tb), _p(K), _p(m), len(m), _p(X), _p(ok))
+        return n, X[:len(m)], ok[:len(m)].astype(bool)
+
+    def se3_exp(self, a):
+        a = np.ascontiguousarray(a, np.float64)
+        out = np.zeros(7)
+        self.lib.or_se3_exp(_p(a), _p(out))
+        return out
+
+    def se3_mul(self, A, B):
+        A = np.ascontiguousarray(A, np.float64)
+        B = np.ascontiguousarray(B, np.float64)
+        out = np.zeros(7)
+        self.lib.or_se3_mul(_p(A), _p(B), _p(out))
+        return out
+
+    def se3_act(self, T, p):
+        T = np.ascontiguousarray(T, np.float64)
+        p = np.ascontiguousarray(p, np.float64)
+        out = np.zeros(3)
+        self.lib.or_se3_act(_p(T), _p(p), _p(out))
+        return out
+
+    def quat_to_R(self, q):
+        q = np.ascontiguousarray(q, np.float64)
+        R = np.zeros(9)
+        self.lib.or_quat_to_R(_p(q), _p(R))
+        return R.reshape(3, 3)
+
+    def world2camera(self, X, T, K):
+        X = np.ascontiguousarray(X, np.float64).reshape(-1, 3)
+        T = np.ascontiguousarray(T, np.float64)
+        K = np.ascontiguousarray(K, np.float64).reshape(9)
+        out = np.zeros_like(X)
+        self.lib.or_world2camera(_p(X), len(X), _p(T), _p(K), _p(out))
+        return out
+
+    def ldlt6(self, H, b, variant=0):
+        H = np.ascontiguousarray(H, np.float64).reshape(36)
+        b = np.ascontiguousarray(b, np.float64)
+        x = np.zeros(6)
+        pos = self.lib.or_ldlt6_solve(_p(H), _p(b), _p(x), variant)
+        return bool(pos), x
+
+    def pose_lm(self, X, uv, K, pose, sum_mode=0):
+        X = np.ascontiguousarray(X, np.float64).reshape(-1, 3)
+        uv = np.ascontiguousarray(uv, np.float64).reshape(-1, 2)
+        K = np.ascontiguousarray(K, np.float64).reshape(9)
+        T = np.array(pose, np.float64).copy()
+        out = np.zeros(max(len(X), 1), np.uint8)
+        inl = self.lib.or_pose_lm(_p(X), _p(uv), len(X), _p(K), _p(T), _p(out), sum_mode)
+        return T, out[:len(X)].astype(bool), inl
+
+    def pose_gn(self, X, uv, K, pose, sum_mode=0):
+        X = np.ascontiguousarray(X, np.float64).reshape(-1, 3)
+        uv = np.ascontiguousarray(uv, np.float64).reshape(-1, 2)
+        K = np.ascontiguousarray(K, np.float64).reshape(9)
+        T = np.array(pose, np.float64).copy()
+        it = self.lib.or_pose_gn(_p(X), _p(uv), len(X), _p(K), _p(T), sum_mode)
+        return T, it
