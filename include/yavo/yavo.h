@@ -132,4 +132,7 @@ int yv_batch_view_get(yv_batch* b, yv_batch_view* view);
 #ifdef __cplusplus
 }
 #endif
+
+#include "yavo_geom.h"
+
 #endif /* YAVO_H */

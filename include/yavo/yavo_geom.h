@@ -1,0 +1,69 @@
+/*
+ * yavo_geom.h -- geometry rows of the hot path behind the same C ABI as yavo.h.
+ *
+ * Poses are Sophus::SE3d (T_cw, world -> camera) in SE3d::data() layout:
+ *     pose[7] = {qx, qy, qz, qw, tx, ty, tz}
+ * so a reference Frame::pose (include/Frame.hpp:13) crosses as pose.data().  K is the row-major 3x3
+ * intrinsic matrix (Camera::K, include/Utils.hpp:30-70).  Image measurements are the reference's
+ * KeyPoint convention (x = row, y = column).  Conventions and errors as in yavo.h.
+ */
+#ifndef YAVO_GEOM_H
+#define YAVO_GEOM_H
+
+#include <stdint.h>
+
+#include "yavo_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct yv_ctx;
+
+/* _3DHandler::getFRANSAC (src/3DHandler.cc:145-195; include/3DHandler.hpp:58): `iters` hypotheses, each the
+ * normalised 8-point F (getFundamentalMatrix, :50-142) of samples[8*h .. 8*h+7] (indices into m, drawn with
+ * replacement -- the reference draws them from std::random_device), inliers |p2^T F p1| < thr in raw
+ * (row, col, 1) pixels; the first hypothesis with the most inliers wins.  *found = 0 (F untouched) when
+ * n < 8 (the reference returns false).  n <= 4096. */
+int yv_f_ransac(struct yv_ctx* ctx, const yv_match* m, int n, const int32_t* samples, int iters, double thr,
+                double F[9], int* max_inliers, int* found);
+
+/* triangulate2View's per-match work (src/LoopHandler.cc:658-726): pixel2camera of pt1 / pt2 (:908-915),
+ * LoopHandler::triangulation with the two poses (:867-885, DLT + SVD, success iff s4/s3 < 1e-2), accepted iff
+ * success and Z > 0.  Xw [n][3], ok [n], *n_ok = accepted count. */
+int yv_triangulate(struct yv_ctx* ctx, const double pose_a[7], const double pose_b[7], const double K[9],
+                   const yv_match* m, int n, double* Xw, uint8_t* ok, int* n_ok);
+
+/* Frame::world2Camera (src/Frame.cc:16-28): out[i] = K [R|t] [X_i; 1] (unnormalised). */
+int yv_world2camera(struct yv_ctx* ctx, const double* X, int n, const double pose[7], const double K[9],
+                    double* out);
+
+/* LoopHandler::optimizePoseOnly (src/LoopHandler.cc:730-861) with the g2o edge of include/Optimizer.hpp:40-135:
+ * pose-only Levenberg-Marquardt from the prior `pose`, 4 rounds x optimize(10), Huber(1) kernel (removed after
+ * round 3), chi2 > 5.991 -> outlier.  X [n][3] world points, uv [n][2] measurements (kp.x, kp.y).  pose is
+ * updated in place; outlier [n] = final flags; *inliers = n - outliers.  n <= 4096. */
+int yv_pose_lm(struct yv_ctx* ctx, const double* X, const double* uv, int n, const double K[9], double pose[7],
+               uint8_t* outlier, int* inliers);
+
+/* bundleAdjustmentGaussNewton (src/test.cc:172-244): 10 Gauss-Newton iterations, stop on cost increase or
+ * |dx| < 1e-6.  *iterations = accepted updates. */
+int yv_pose_gn(struct yv_ctx* ctx, const double* X, const double* uv, int n, const double K[9], double pose[7],
+               int* iterations);
+
+/* Batched device-pointer forms (asynchronous on `stream`, NULL = context stream).  Problem p owns edges
+ * [d_offsets[p], d_offsets[p+1]) of d_X [][3] / d_uv [][2]; d_K [p][9]; d_poses [p][7] in/out. */
+int yv_pose_lm_batch(struct yv_ctx* ctx, int n_problems, const int32_t* d_offsets, const double* d_X,
+                     const double* d_uv, const double* d_K, double* d_poses, uint8_t* d_outlier,
+                     int32_t* d_inliers, void* stream);
+int yv_pose_gn_batch(struct yv_ctx* ctx, int n_problems, const int32_t* d_offsets, const double* d_X,
+                     const double* d_uv, const double* d_K, double* d_poses, int32_t* d_iterations, void* stream);
+/* F-RANSAC over n_lists match lists: list l = d_matches + l*list_stride, d_counts[l] entries, samples
+ * d_samples + l*sample_stride ([iters][8]). */
+int yv_f_ransac_batch(struct yv_ctx* ctx, const yv_match* d_matches, int64_t list_stride, const int32_t* d_counts,
+                      int n_lists, const int32_t* d_samples, int64_t sample_stride, int iters, double thr,
+                      double* d_F, int32_t* d_max_inliers, int32_t* d_found, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YAVO_GEOM_H */

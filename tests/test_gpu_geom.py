@@ -1,0 +1,119 @@
+"""GPU parity of the geometry rows (F-RANSAC, triangulation, world2Camera, pose-only LM, GN) against the
+oracle.  The kernels evaluate every expression in the oracle's order with contraction off and sum edges in
+the oracle's tree order (sum_mode 1), so results are compared bit for bit; against the reference's
+sequential edge order (sum_mode 0) they agree within the stated tolerance (poses 1e-9 absolute)."""
+import numpy as np
+import pytest
+
+import ya_vo_amd as yv
+from ya_vo_amd import MATCH_DTYPE, scene
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-9  # |pose_gpu - pose_reference_order| (quaternion + translation), stated in DESIGN.md
+
+
+def _match_array(ua, ub):
+    m = np.zeros(len(ua), MATCH_DTYPE)
+    m["pt1"]["x"] = np.round(ua[:, 0])
+    m["pt1"]["y"] = np.round(ua[:, 1])
+    m["pt2"]["x"] = np.round(ub[:, 0])
+    m["pt2"]["y"] = np.round(ub[:, 1])
+    return m
+
+
+@pytest.mark.parametrize("n,iters,seed", [(200, 400, 2), (8, 50, 3), (1970, 400, 4), (50, 1, 5)])
+def test_f_ransac_matches_oracle(ctx, oracle, n, iters, seed):
+    Ta, Tb, X, ua, ub = scene.two_view_matches(n, seed=seed)
+    m = _match_array(ua, ub)
+    rng = np.random.default_rng(seed)
+    if seed == 4:  # add gross mismatches
+        bad = rng.choice(n, n // 5, replace=False)
+        m["pt2"]["x"][bad] = rng.integers(0, 376, len(bad))
+    samples = rng.integers(0, n, (iters, 8)).astype(np.int32)
+    found, F, inl = ctx.f_ransac(m, samples, 0.1)
+    ofound, oF, oinl = oracle.f_ransac(m, samples, 0.1)
+    assert found == ofound and inl == oinl
+    np.testing.assert_array_equal(F, oF)
+
+
+def test_f_ransac_too_few(ctx):
+    m = np.zeros(7, MATCH_DTYPE)
+    found, F, inl = ctx.f_ransac(m, np.zeros((4, 8), np.int32), 0.1)
+    assert not found
+
+
+def test_triangulate_matches_oracle(ctx, oracle):
+    Ta, Tb, X, ua, ub = scene.two_view_matches(1500, seed=6)
+    m = _match_array(ua, ub)
+    Tb2 = scene.perturb(Tb, np.random.default_rng(1), rot=0.003, trans=0.01)
+    for pa, pb in ((Ta, Tb), (Tb2, Ta)):
+        n, Xw, ok = ctx.triangulate(pa, pb, scene.K_KITTI, m)
+        on, oX, ook = oracle.triangulate_matches(pa, pb, scene.K_KITTI, m)
+        assert n == on
+        np.testing.assert_array_equal(ok, ook)
+        np.testing.assert_array_equal(Xw, oX)
+
+
+def test_world2camera_matches_oracle(ctx, oracle):
+    X, uv, T, _ = scene.random_scene(777, seed=7)
+    np.testing.assert_array_equal(ctx.world2camera(X, T, scene.K_KITTI), oracle.world2camera(X, T, scene.K_KITTI))
+
+
+@pytest.mark.parametrize("n,noise,outl,seed", [(300, 0.0, 0.0, 9), (1500, 0.5, 0.1, 10), (2000, 1.0, 0.3, 11),
+                                               (7, 0.3, 0.0, 12), (0, 0.0, 0.0, 13)])
+def test_pose_lm_matches_oracle(ctx, oracle, n, noise, outl, seed):
+    X, uv, T_true, _ = scene.random_scene(max(n, 1), seed=seed, noise_px=noise, outlier_frac=outl)
+    X, uv = X[:n], uv[:n]
+    prior = scene.perturb(T_true, np.random.default_rng(seed))
+    T, out, inl = ctx.pose_lm(X, uv, scene.K_KITTI, prior)
+    oT, oout, oinl = oracle.pose_lm(X, uv, scene.K_KITTI, prior, 1)
+    assert inl == oinl
+    np.testing.assert_array_equal(out, oout)
+    np.testing.assert_array_equal(T, oT)
+    rT, rout, rinl = oracle.pose_lm(X, uv, scene.K_KITTI, prior, 0)
+    assert rinl == inl
+    np.testing.assert_allclose(T, rT, rtol=0, atol=POSE_TOL)
+
+
+@pytest.mark.parametrize("n,seed", [(100, 12), (2000, 14)])
+def test_pose_gn_matches_oracle(ctx, oracle, n, seed):
+    X, uv, T_true, _ = scene.random_scene(n, seed=seed, noise_px=0.3)
+    prior = scene.perturb(T_true, np.random.default_rng(seed), rot=0.01, trans=0.05)
+    T, it = ctx.pose_gn(X, uv, scene.K_KITTI, prior)
+    oT, oit = oracle.pose_gn(X, uv, scene.K_KITTI, prior, 1)
+    assert it == oit
+    np.testing.assert_array_equal(T, oT)
+    rT, rit = oracle.pose_gn(X, uv, scene.K_KITTI, prior, 0)
+    np.testing.assert_allclose(T, rT, rtol=0, atol=POSE_TOL)
+
+
+def test_pose_lm_batch(ctx, oracle):
+    """Several pose problems in one launch (the batched frontend form)."""
+    import torch
+    probs = [scene.random_scene(n, seed=20 + i, noise_px=0.5, outlier_frac=0.1) for i, n in enumerate((50, 900, 1600))]
+    priors = [scene.perturb(p[2], np.random.default_rng(i)) for i, p in enumerate(probs)]
+    offs = np.cumsum([0] + [len(p[0]) for p in probs]).astype(np.int32)
+    Xall = np.concatenate([p[0] for p in probs])
+    uvall = np.concatenate([p[1] for p in probs])
+    dev = "cuda:0"
+    d_off = torch.from_numpy(offs).to(dev)
+    d_X = torch.from_numpy(Xall).to(dev)
+    d_uv = torch.from_numpy(uvall).to(dev)
+    d_K = torch.from_numpy(np.tile(scene.K_KITTI.reshape(1, 9), (len(probs), 1))).to(dev)
+    d_P = torch.from_numpy(np.stack(priors)).to(dev)
+    d_out = torch.zeros(len(Xall), dtype=torch.uint8, device=dev)
+    d_inl = torch.zeros(len(probs), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    st = ctx.lib.yv_pose_lm_batch(ctx.handle, len(probs), d_off.data_ptr(), d_X.data_ptr(), d_uv.data_ptr(),
+                                  d_K.data_ptr(), d_P.data_ptr(), d_out.data_ptr(), d_inl.data_ptr(), None)
+    assert st == 0
+    ctx.sync()
+    P = d_P.cpu().numpy()
+    out = d_out.cpu().numpy().astype(bool)
+    inl = d_inl.cpu().numpy()
+    for i, p in enumerate(probs):
+        oT, oout, oinl = oracle.pose_lm(p[0], p[1], scene.K_KITTI, priors[i], 1)
+        assert inl[i] == oinl
+        np.testing.assert_array_equal(P[i], oT)
+        np.testing.assert_array_equal(out[offs[i]:offs[i + 1]], oout)

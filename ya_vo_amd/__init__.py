@@ -80,6 +80,19 @@ SIGNATURES = {
 }
 
 
+_D = ctypes.c_double
+GEOM_SIGNATURES = {
+    "yv_f_ransac": (_I, [_P, _P, _I, _P, _I, _D, _P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "yv_triangulate": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, ctypes.POINTER(_I)]),
+    "yv_world2camera": (_I, [_P, _P, _I, _P, _P, _P]),
+    "yv_pose_lm": (_I, [_P, _P, _P, _I, _P, _P, _P, ctypes.POINTER(_I)]),
+    "yv_pose_gn": (_I, [_P, _P, _P, _I, _P, _P, ctypes.POINTER(_I)]),
+    "yv_pose_lm_batch": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "yv_pose_gn_batch": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "yv_f_ransac_batch": (_I, [_P, _P, ctypes.c_int64, _P, _I, _P, ctypes.c_int64, _I, _D, _P, _P, _P, _P]),
+}
+
+
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     """Load libyavo.so (built by __graft_entry__.build()).  Raises if it is missing: no fallback."""
     global _lib
@@ -97,7 +110,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         except ImportError:
             pass
     lib = ctypes.CDLL(path)
-    for name, (res, args) in SIGNATURES.items():
+    for name, (res, args) in list(SIGNATURES.items()) + list(GEOM_SIGNATURES.items()):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -114,7 +127,64 @@ def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data
 
 
-class Context:
+def _f64(a, shape=None) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a.reshape(shape) if shape is not None else a
+
+
+class _GeomMixin:
+    """Geometry rows (include/yavo/yavo_geom.h). Poses: Sophus SE3d::data() = {qx, qy, qz, qw, tx, ty, tz}."""
+
+    def f_ransac(self, matches: np.ndarray, samples: np.ndarray, thr: float = 0.1):
+        """_3DHandler::getFRANSAC -> (found, F [3,3], max_inliers)."""
+        m = np.ascontiguousarray(matches, dtype=MATCH_DTYPE)
+        smp = np.ascontiguousarray(samples, dtype=np.int32).reshape(-1, 8)
+        F = np.zeros(9)
+        mi, found = ctypes.c_int(), ctypes.c_int()
+        _check(self.lib.yv_f_ransac(self.handle, _ptr(m), len(m), _ptr(smp), len(smp), thr, _ptr(F),
+                                    ctypes.byref(mi), ctypes.byref(found)), "yv_f_ransac")
+        return bool(found.value), F.reshape(3, 3), mi.value
+
+    def triangulate(self, pose_a, pose_b, K, matches: np.ndarray):
+        """triangulate2View per-match part -> (n_ok, Xw [n,3], ok [n] bool)."""
+        m = np.ascontiguousarray(matches, dtype=MATCH_DTYPE)
+        pa, pb, k = _f64(pose_a, 7), _f64(pose_b, 7), _f64(K, 9)
+        X = np.zeros((max(len(m), 1), 3))
+        ok = np.zeros(max(len(m), 1), np.uint8)
+        n = ctypes.c_int()
+        _check(self.lib.yv_triangulate(self.handle, _ptr(pa), _ptr(pb), _ptr(k), _ptr(m), len(m), _ptr(X), _ptr(ok),
+                                       ctypes.byref(n)), "yv_triangulate")
+        return n.value, X[:len(m)], ok[:len(m)].astype(bool)
+
+    def world2camera(self, X, pose, K):
+        X = _f64(X, (-1, 3))
+        out = np.zeros_like(X)
+        _check(self.lib.yv_world2camera(self.handle, _ptr(X), len(X), _ptr(_f64(pose, 7)), _ptr(_f64(K, 9)),
+                                        _ptr(out)), "yv_world2camera")
+        return out
+
+    def pose_lm(self, X, uv, K, pose):
+        """LoopHandler::optimizePoseOnly -> (pose [7], outlier [n] bool, inliers)."""
+        X, uv = _f64(X, (-1, 3)), _f64(uv, (-1, 2))
+        T = _f64(pose, 7).copy()
+        out = np.zeros(max(len(X), 1), np.uint8)
+        inl = ctypes.c_int()
+        _check(self.lib.yv_pose_lm(self.handle, _ptr(X), _ptr(uv), len(X), _ptr(_f64(K, 9)), _ptr(T), _ptr(out),
+                                   ctypes.byref(inl)), "yv_pose_lm")
+        return T, out[:len(X)].astype(bool), inl.value
+
+    def pose_gn(self, X, uv, K, pose):
+        """bundleAdjustmentGaussNewton -> (pose [7], accepted iterations)."""
+        X, uv = _f64(X, (-1, 3)), _f64(uv, (-1, 2))
+        T = _f64(pose, 7).copy()
+        it = ctypes.c_int()
+        _check(self.lib.yv_pose_gn(self.handle, _ptr(X), _ptr(uv), len(X), _ptr(_f64(K, 9)), _ptr(T),
+                                   ctypes.byref(it)), "yv_pose_gn")
+        return T, it.value
+
+
+
+class Context(_GeomMixin):
     """One yv_ctx: a GPU, a HIP stream and the algorithm constants."""
 
     def __init__(self, device: int = 0):
@@ -204,6 +274,8 @@ class Context:
         _check(self.lib.yv_filter_matches(self.handle, _ptr(m), len(m), thr, _ptr(out), ctypes.byref(n)),
                "yv_filter_matches")
         return out[:n.value].copy()
+
+
 
 
 class Batch:

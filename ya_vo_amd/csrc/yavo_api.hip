@@ -23,6 +23,8 @@ struct yv_ctx {
     int8_t* d_offsets = nullptr;                              // [256*4]
     yv_batch* single = nullptr;                               // workspace of the host-pointer API
     int32_t* h_pinned = nullptr;                              // small pinned scratch for counts
+    void* scratch = nullptr;                                  // device arena of the geometry host calls
+    size_t scratch_cap = 0;
 };
 
 struct yv_batch {
@@ -182,6 +184,7 @@ void yv_destroy(yv_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     batch_free(ctx->single);
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->d_offsets) (void)hipFree(ctx->d_offsets);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -533,6 +536,235 @@ int yv_filter_matches(yv_ctx* ctx, const yv_match* in, int n, int thr, yv_match*
     }
     *n_out = m;
     return YV_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// geometry (include/yavo/yavo_geom.h)
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+// Carves 256-B aligned sub-buffers out of the context's device arena (grown on demand, outside any
+// timed loop: the host-pointer calls are synchronous anyway).
+struct Arena {
+    yv_ctx* ctx;
+    size_t need = 0;
+    std::vector<std::pair<void**, size_t>> reqs;
+    template <class T>
+    void add(T** p, size_t count) {
+        reqs.push_back({reinterpret_cast<void**>(p), count * sizeof(T)});
+        need += (count * sizeof(T) + 255) & ~(size_t)255;
+    }
+    int commit() {
+        if (need > ctx->scratch_cap) {
+            if (ctx->scratch) (void)hipFree(ctx->scratch);
+            ctx->scratch = nullptr;
+            ctx->scratch_cap = 0;
+            size_t cap = std::max(need, (size_t)1 << 20);
+            if (hipMalloc(&ctx->scratch, cap) != hipSuccess) return YV_ERR_HIP;
+            ctx->scratch_cap = cap;
+        }
+        char* base = reinterpret_cast<char*>(ctx->scratch);
+        size_t off = 0;
+        for (auto& r : reqs) {
+            *r.first = base + off;
+            off += (r.second + 255) & ~(size_t)255;
+        }
+        return YV_OK;
+    }
+};
+
+bool finite_pose(const double* p) {
+    for (int i = 0; i < 7; ++i)
+        if (!(p[i] == p[i])) return false;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int yv_f_ransac(yv_ctx* ctx, const yv_match* m, int n, const int32_t* samples, int iters, double thr, double F[9],
+                int* max_inliers, int* found) {
+    if (!ctx || !F || !max_inliers || !found || n < 0 || iters < 0 || (n > 0 && !m) || (iters > 0 && !samples))
+        return YV_ERR_INVALID;
+    if (n > yavo::kMaxKp) return YV_ERR_CAPACITY;
+    *found = 0;
+    if (n < 8) return YV_OK;  // "Not enough matches": false, F untouched (src/3DHandler.cc:154-156)
+    for (int i = 0; i < 8 * iters; ++i)
+        if (samples[i] < 0 || samples[i] >= n) return YV_ERR_INVALID;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = ctx->stream;
+    Arena a{ctx};
+    yv_match* dm;
+    int32_t *dcnt, *dsmp, *dmax, *dfound;
+    double* dF;
+    a.add(&dm, (size_t)n);
+    a.add(&dcnt, 1);
+    a.add(&dsmp, (size_t)std::max(8 * iters, 1));
+    a.add(&dF, 9);
+    a.add(&dmax, 1);
+    a.add(&dfound, 1);
+    if (a.commit() != YV_OK) return YV_ERR_HIP;
+    ctx->h_pinned[0] = n;
+    YV_HIP(hipMemcpyAsync(dm, m, sizeof(yv_match) * (size_t)n, hipMemcpyHostToDevice, s));
+    YV_HIP(hipMemcpyAsync(dcnt, ctx->h_pinned, sizeof(int32_t), hipMemcpyHostToDevice, s));
+    if (iters > 0) YV_HIP(hipMemcpyAsync(dsmp, samples, sizeof(int32_t) * 8 * (size_t)iters, hipMemcpyHostToDevice, s));
+    YV_HIP(hipMemcpyAsync(dF, F, sizeof(double) * 9, hipMemcpyHostToDevice, s));  // untouched if iters == 0
+    yavo::launch_f_ransac(dm, n, dcnt, 1, dsmp, 8 * (int64_t)iters, iters, thr, dF, dmax, dfound, s);
+    if (check_launch() != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMemcpyAsync(F, dF, sizeof(double) * 9, hipMemcpyDeviceToHost, s));
+    YV_HIP(hipMemcpyAsync(ctx->h_pinned + 1, dmax, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    YV_HIP(hipMemcpyAsync(ctx->h_pinned + 2, dfound, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    YV_HIP(hipStreamSynchronize(s));
+    *max_inliers = ctx->h_pinned[1];
+    *found = ctx->h_pinned[2];
+    return YV_OK;
+}
+
+int yv_triangulate(yv_ctx* ctx, const double pose_a[7], const double pose_b[7], const double K[9], const yv_match* m,
+                   int n, double* Xw, uint8_t* ok, int* n_ok) {
+    if (!ctx || !pose_a || !pose_b || !K || !n_ok || n < 0 || (n > 0 && (!m || !Xw || !ok))) return YV_ERR_INVALID;
+    *n_ok = 0;
+    if (n == 0) return YV_OK;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = ctx->stream;
+    Arena a{ctx};
+    yv_match* dm;
+    double *dposes, *dK, *dX;
+    uint8_t* dok;
+    int32_t* dn;
+    a.add(&dm, (size_t)n);
+    a.add(&dposes, 14);
+    a.add(&dK, 9);
+    a.add(&dX, 3 * (size_t)n);
+    a.add(&dok, (size_t)n);
+    a.add(&dn, 1);
+    if (a.commit() != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMemcpyAsync(dm, m, sizeof(yv_match) * (size_t)n, hipMemcpyHostToDevice, s));
+    YV_HIP(hipMemcpyAsync(dposes, pose_a, sizeof(double) * 7, hipMemcpyHostToDevice, s));
+    YV_HIP(hipMemcpyAsync(dposes + 7, pose_b, sizeof(double) * 7, hipMemcpyHostToDevice, s));
+    YV_HIP(hipMemcpyAsync(dK, K, sizeof(double) * 9, hipMemcpyHostToDevice, s));
+    YV_HIP(hipMemsetAsync(dn, 0, sizeof(int32_t), s));
+    yavo::launch_triangulate(dm, n, dposes, dK, dX, dok, dn, s);
+    if (check_launch() != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMemcpyAsync(Xw, dX, sizeof(double) * 3 * (size_t)n, hipMemcpyDeviceToHost, s));
+    YV_HIP(hipMemcpyAsync(ok, dok, (size_t)n, hipMemcpyDeviceToHost, s));
+    YV_HIP(hipMemcpyAsync(ctx->h_pinned, dn, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    YV_HIP(hipStreamSynchronize(s));
+    *n_ok = ctx->h_pinned[0];
+    return YV_OK;
+}
+
+int yv_world2camera(yv_ctx* ctx, const double* X, int n, const double pose[7], const double K[9], double* out) {
+    if (!ctx || !pose || !K || n < 0 || (n > 0 && (!X || !out))) return YV_ERR_INVALID;
+    if (n == 0) return YV_OK;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = ctx->stream;
+    Arena a{ctx};
+    double *dX, *dT, *dK, *dO;
+    a.add(&dX, 3 * (size_t)n);
+    a.add(&dT, 7);
+    a.add(&dK, 9);
+    a.add(&dO, 3 * (size_t)n);
+    if (a.commit() != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMemcpyAsync(dX, X, sizeof(double) * 3 * (size_t)n, hipMemcpyHostToDevice, s));
+    YV_HIP(hipMemcpyAsync(dT, pose, sizeof(double) * 7, hipMemcpyHostToDevice, s));
+    YV_HIP(hipMemcpyAsync(dK, K, sizeof(double) * 9, hipMemcpyHostToDevice, s));
+    yavo::launch_world2camera(dX, n, dT, dK, dO, s);
+    if (check_launch() != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMemcpyAsync(out, dO, sizeof(double) * 3 * (size_t)n, hipMemcpyDeviceToHost, s));
+    YV_HIP(hipStreamSynchronize(s));
+    return YV_OK;
+}
+
+static int pose_single(yv_ctx* ctx, const double* X, const double* uv, int n, const double* K, double* pose,
+                       uint8_t* outlier, int* result, bool lm) {
+    if (!ctx || !K || !pose || !result || n < 0 || (n > 0 && (!X || !uv)) || (lm && n > 0 && !outlier))
+        return YV_ERR_INVALID;
+    if (n > 4096) return YV_ERR_CAPACITY;
+    if (!finite_pose(pose)) return YV_ERR_INVALID;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = ctx->stream;
+    Arena a{ctx};
+    int32_t *doff, *dres;
+    double *dX, *duv, *dK, *dP;
+    uint8_t* dout;
+    a.add(&doff, 2);
+    a.add(&dX, 3 * (size_t)std::max(n, 1));
+    a.add(&duv, 2 * (size_t)std::max(n, 1));
+    a.add(&dK, 9);
+    a.add(&dP, 7);
+    a.add(&dout, (size_t)std::max(n, 1));
+    a.add(&dres, 1);
+    if (a.commit() != YV_OK) return YV_ERR_HIP;
+    ctx->h_pinned[0] = 0;
+    ctx->h_pinned[1] = n;
+    YV_HIP(hipMemcpyAsync(doff, ctx->h_pinned, 2 * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    if (n > 0) {
+        YV_HIP(hipMemcpyAsync(dX, X, sizeof(double) * 3 * (size_t)n, hipMemcpyHostToDevice, s));
+        YV_HIP(hipMemcpyAsync(duv, uv, sizeof(double) * 2 * (size_t)n, hipMemcpyHostToDevice, s));
+    }
+    YV_HIP(hipMemcpyAsync(dK, K, sizeof(double) * 9, hipMemcpyHostToDevice, s));
+    YV_HIP(hipMemcpyAsync(dP, pose, sizeof(double) * 7, hipMemcpyHostToDevice, s));
+    if (lm) yavo::launch_pose_lm(doff, 1, dX, duv, dK, dP, dout, dres, s);
+    else yavo::launch_pose_gn(doff, 1, dX, duv, dK, dP, dres, s);
+    if (check_launch() != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMemcpyAsync(pose, dP, sizeof(double) * 7, hipMemcpyDeviceToHost, s));
+    if (lm && n > 0) YV_HIP(hipMemcpyAsync(outlier, dout, (size_t)n, hipMemcpyDeviceToHost, s));
+    YV_HIP(hipMemcpyAsync(ctx->h_pinned + 2, dres, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    YV_HIP(hipStreamSynchronize(s));
+    *result = ctx->h_pinned[2];
+    return YV_OK;
+}
+
+int yv_pose_lm(yv_ctx* ctx, const double* X, const double* uv, int n, const double K[9], double pose[7],
+               uint8_t* outlier, int* inliers) {
+    return pose_single(ctx, X, uv, n, K, pose, outlier, inliers, true);
+}
+
+int yv_pose_gn(yv_ctx* ctx, const double* X, const double* uv, int n, const double K[9], double pose[7],
+               int* iterations) {
+    return pose_single(ctx, X, uv, n, K, pose, nullptr, iterations, false);
+}
+
+int yv_pose_lm_batch(yv_ctx* ctx, int n_problems, const int32_t* d_offsets, const double* d_X, const double* d_uv,
+                     const double* d_K, double* d_poses, uint8_t* d_outlier, int32_t* d_inliers, void* stream) {
+    if (!ctx || n_problems < 0 || (n_problems > 0 && (!d_offsets || !d_X || !d_uv || !d_K || !d_poses || !d_outlier ||
+                                                      !d_inliers)))
+        return YV_ERR_INVALID;
+    if (n_problems == 0) return YV_OK;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+    yavo::launch_pose_lm(d_offsets, n_problems, d_X, d_uv, d_K, d_poses, d_outlier, d_inliers, s);
+    return check_launch();
+}
+
+int yv_pose_gn_batch(yv_ctx* ctx, int n_problems, const int32_t* d_offsets, const double* d_X, const double* d_uv,
+                     const double* d_K, double* d_poses, int32_t* d_iterations, void* stream) {
+    if (!ctx || n_problems < 0 ||
+        (n_problems > 0 && (!d_offsets || !d_X || !d_uv || !d_K || !d_poses || !d_iterations)))
+        return YV_ERR_INVALID;
+    if (n_problems == 0) return YV_OK;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+    yavo::launch_pose_gn(d_offsets, n_problems, d_X, d_uv, d_K, d_poses, d_iterations, s);
+    return check_launch();
+}
+
+int yv_f_ransac_batch(yv_ctx* ctx, const yv_match* d_matches, int64_t list_stride, const int32_t* d_counts, int n_lists,
+                      const int32_t* d_samples, int64_t sample_stride, int iters, double thr, double* d_F,
+                      int32_t* d_max_inliers, int32_t* d_found, void* stream) {
+    if (!ctx || n_lists < 0 || iters < 0 ||
+        (n_lists > 0 && (!d_matches || !d_counts || !d_samples || !d_F || !d_max_inliers || !d_found)))
+        return YV_ERR_INVALID;
+    if (n_lists == 0) return YV_OK;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+    yavo::launch_f_ransac(d_matches, list_stride, d_counts, n_lists, d_samples, sample_stride, iters, thr, d_F,
+                          d_max_inliers, d_found, s);
+    return check_launch();
 }
 
 }  // extern "C"

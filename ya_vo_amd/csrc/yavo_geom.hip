@@ -1,0 +1,1114 @@
+// yavo_geom.hip -- gfx950 kernels for the geometry rows of the hot path.
+//
+//   f_ransac_kernel      _3DHandler::getFRANSAC / getFundamentalMatrix   src/3DHandler.cc:17-195
+//                        (cv::SVD = OpenCV JacobiSVDImpl_<double>), one workgroup per match list, one
+//                        hypothesis per lane, the match list staged in LDS for the inlier counts
+//   triangulate_kernel   LoopHandler::triangulation + pixel2camera        src/LoopHandler.cc:658-726, 867-915
+//                        (Eigen JacobiSVD on the 4x4 DLT system), one lane per match, all in registers
+//   world2camera_kernel  Frame::world2Camera                              src/Frame.cc:16-28
+//   pose_lm_kernel       LoopHandler::optimizePoseOnly + the g2o edge     src/LoopHandler.cc:730-861,
+//                        include/Optimizer.hpp:40-135; one workgroup per pose problem: edge terms
+//                        (residual, 2x6 Jacobian, Huber weight) per lane, J^T W J / J^T W e / chi2 as
+//                        fixed-order tree reductions in LDS, the 6x6 LDLT + LM control on lane 0
+//   pose_gn_kernel       bundleAdjustmentGaussNewton                      src/test.cc:172-244
+//
+// Every floating-point expression is written in the reference's operation order and the file is built
+// with -ffp-contract=off, so each kernel matches oracle/yavo_oracle_geom.c bit for bit (sums over edges
+// in the oracle's sum_mode 1 = this file's tree order).
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <stdint.h>
+
+#include "yavo_internal.h"
+
+namespace yavo {
+namespace geom {
+
+constexpr int kNT = 256;          // threads per workgroup of the reduction kernels
+constexpr int kMaxEdges = 4096;   // edges per pose problem held in LDS
+
+// exclusive scan over a 256-thread block; s_tmp >= 8 ints
+__device__ int block_excl_scan_geom(int v, int* s_tmp, int* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        int t = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += t;
+    }
+    if (lane == 63) s_tmp[wave] = incl;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int w = 0; w < kNT / 64; ++w) {
+        if (w < wave) base += s_tmp[w];
+        tot += s_tmp[w];
+    }
+    __syncthreads();
+    if (total) *total = tot;
+    return base + incl - v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// OpenCV JacobiSVDImpl_<double> (per lane, private arrays)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double cv_hypot(double a, double b) {
+    a = fabs(a);
+    b = fabs(b);
+    if (a > b) {
+        b /= a;
+        return a * sqrt(1 + b * b);
+    }
+    if (b > 0) {
+        a /= b;
+        return b * sqrt(1 + a * a);
+    }
+    return 0;
+}
+
+__device__ __forceinline__ uint32_t cv_rng_next(uint64_t* state) {
+    *state = (uint64_t)(uint32_t)*state * 4164903690ULL + (uint32_t)(*state >> 32);
+    return (uint32_t)*state;
+}
+
+template <int N>
+__device__ void cv_jacobi_svd(double* At, double* Wout, double* Vt) {
+    // square: m = n = N, astep = vstep = N, n1 = N
+    const double minval = DBL_MIN, eps = DBL_EPSILON * 10;
+    double W[N];
+    const int m = N, n = N, max_iter = m > 30 ? m : 30;
+    double c, s, sd;
+    for (int i = 0; i < n; i++) {
+        sd = 0;
+        for (int k = 0; k < m; k++) {
+            double t = At[i * N + k];
+            sd += t * t;
+        }
+        W[i] = sd;
+        for (int k = 0; k < n; k++) Vt[i * N + k] = 0;
+        Vt[i * N + i] = 1;
+    }
+    for (int iter = 0; iter < max_iter; iter++) {
+        bool changed = false;
+        for (int i = 0; i < n - 1; i++)
+            for (int j = i + 1; j < n; j++) {
+                double *Ai = At + i * N, *Aj = At + j * N;
+                double a = W[i], p = 0, b = W[j];
+                for (int k = 0; k < m; k++) p += Ai[k] * Aj[k];
+                if (fabs(p) <= eps * sqrt(a * b)) continue;
+                p *= 2;
+                double beta = a - b, gamma = cv_hypot(p, beta);
+                if (beta < 0) {
+                    double delta = (gamma - beta) * 0.5;
+                    s = sqrt(delta / gamma);
+                    c = p / (gamma * s * 2);
+                } else {
+                    c = sqrt((gamma + beta) / (gamma * 2));
+                    s = p / (gamma * c * 2);
+                }
+                a = b = 0;
+                for (int k = 0; k < m; k++) {
+                    double t0 = c * Ai[k] + s * Aj[k];
+                    double t1 = -s * Ai[k] + c * Aj[k];
+                    Ai[k] = t0;
+                    Aj[k] = t1;
+                    a += t0 * t0;
+                    b += t1 * t1;
+                }
+                W[i] = a;
+                W[j] = b;
+                changed = true;
+                double *Vi = Vt + i * N, *Vj = Vt + j * N;
+                for (int k = 0; k < n; k++) {
+                    double t0 = c * Vi[k] + s * Vj[k];
+                    double t1 = -s * Vi[k] + c * Vj[k];
+                    Vi[k] = t0;
+                    Vj[k] = t1;
+                }
+            }
+        if (!changed) break;
+    }
+    for (int i = 0; i < n; i++) {
+        sd = 0;
+        for (int k = 0; k < m; k++) {
+            double t = At[i * N + k];
+            sd += t * t;
+        }
+        W[i] = sqrt(sd);
+    }
+    for (int i = 0; i < n - 1; i++) {
+        int j = i;
+        for (int k = i + 1; k < n; k++)
+            if (W[j] < W[k]) j = k;
+        if (i != j) {
+            double t = W[i];
+            W[i] = W[j];
+            W[j] = t;
+            for (int k = 0; k < m; k++) { t = At[i * N + k]; At[i * N + k] = At[j * N + k]; At[j * N + k] = t; }
+            for (int k = 0; k < n; k++) { t = Vt[i * N + k]; Vt[i * N + k] = Vt[j * N + k]; Vt[j * N + k] = t; }
+        }
+    }
+    for (int i = 0; i < n; i++) Wout[i] = W[i];
+    uint64_t rng = 0x12345678;
+    for (int i = 0; i < n; i++) {
+        sd = W[i];
+        for (int ii = 0; ii < 100 && sd <= minval; ii++) {
+            const double val0 = 1. / m;
+            for (int k = 0; k < m; k++) At[i * N + k] = (cv_rng_next(&rng) & 256) != 0 ? val0 : -val0;
+            for (int it2 = 0; it2 < 2; it2++) {
+                for (int j = 0; j < i; j++) {
+                    sd = 0;
+                    for (int k = 0; k < m; k++) sd += At[i * N + k] * At[j * N + k];
+                    double asum = 0;
+                    for (int k = 0; k < m; k++) {
+                        double t = At[i * N + k] - sd * At[j * N + k];
+                        At[i * N + k] = t;
+                        asum += fabs(t);
+                    }
+                    asum = asum > eps * 100 ? 1 / asum : 0;
+                    for (int k = 0; k < m; k++) At[i * N + k] *= asum;
+                }
+            }
+            sd = 0;
+            for (int k = 0; k < m; k++) {
+                double t = At[i * N + k];
+                sd += t * t;
+            }
+            sd = sqrt(sd);
+        }
+        s = sd > minval ? 1 / sd : 0.;
+        for (int k = 0; k < m; k++) At[i * N + k] *= s;
+    }
+}
+
+__device__ __forceinline__ void mm3(const double* A, const double* B, double* C) {
+    double R[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) R[i * 3 + j] = A[i * 3 + 0] * B[0 * 3 + j] + A[i * 3 + 1] * B[1 * 3 + j] + A[i * 3 + 2] * B[2 * 3 + j];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) C[i] = R[i];
+}
+
+// getFundamentalMatrix (src/3DHandler.cc:50-142) on 8 correspondences pts[8][4] = (x1, y1, x2, y2)
+__device__ void fundamental_8pt(const double* pts, double* F) {
+    const int n = 8;
+    double xs[4][8];
+    for (int i = 0; i < n; ++i)
+        for (int q = 0; q < 4; ++q) xs[q][i] = pts[4 * i + q];
+    double N[2][9];
+    for (int v = 0; v < 2; ++v) {
+        const double* x = xs[2 * v];
+        const double* y = xs[2 * v + 1];
+        double mx = 0.0, my = 0.0;
+        for (int i = 0; i < n; ++i) mx += x[i];
+        mx /= n;
+        for (int i = 0; i < n; ++i) my += y[i];
+        my /= n;
+        double scaleDenom = 0.0;
+        for (int i = 0; i < n; i++) {
+            double xh = x[i] - mx, yh = y[i] - my;
+            scaleDenom += sqrt(xh * xh + yh * yh);
+        }
+        double scale = sqrt(2.0) / (scaleDenom / n);
+        double* M = N[v];
+        M[0] = scale; M[1] = 0; M[2] = -scale * mx;
+        M[3] = 0; M[4] = scale; M[5] = -scale * my;
+        M[6] = 0; M[7] = 0; M[8] = 1;
+    }
+    double A[8][9];
+    for (int i = 0; i < n; i++) {
+        const double* N1 = N[0];
+        const double* N2 = N[1];
+        double nx1 = N1[0] * xs[0][i] + N1[1] * xs[1][i] + N1[2] * 1.0;
+        double ny1 = N1[3] * xs[0][i] + N1[4] * xs[1][i] + N1[5] * 1.0;
+        double nx2 = N2[0] * xs[2][i] + N2[1] * xs[3][i] + N2[2] * 1.0;
+        double ny2 = N2[3] * xs[2][i] + N2[4] * xs[3][i] + N2[5] * 1.0;
+        A[i][0] = nx1 * nx2; A[i][1] = nx1 * ny2; A[i][2] = nx1;
+        A[i][3] = ny1 * nx2; A[i][4] = ny1 * ny2; A[i][5] = ny1;
+        A[i][6] = nx2; A[i][7] = ny2; A[i][8] = 1;
+    }
+    double At[81], V[81], w9[9];
+    // AtA = A^T A (symmetric); _SVDcompute transposes it into temp_a
+    for (int i = 0; i < 9; ++i)
+        for (int j = 0; j < 9; ++j) {
+            double s = 0;
+            for (int k = 0; k < n; ++k) s += A[k][i] * A[k][j];
+            At[j * 9 + i] = s;
+        }
+    cv_jacobi_svd<9>(At, w9, V);
+    double F0[9], A3[9], V3[9], w3[3];
+    for (int i = 0; i < 9; ++i) F0[i] = V[8 * 9 + i];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) A3[i * 3 + j] = F0[j * 3 + i];
+    cv_jacobi_svd<3>(A3, w3, V3);
+    double U[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) U[i * 3 + j] = A3[j * 3 + i];
+    w3[2] = 0;
+    double D[9] = {w3[0], 0, 0, 0, w3[1], 0, 0, 0, w3[2]};
+    double T[9];
+    mm3(U, D, T);
+    mm3(T, V3, F0);
+    const double* N1 = N[0];
+    const double* N2 = N[1];
+    double N2t[9] = {N2[0], N2[3], N2[6], N2[1], N2[4], N2[7], N2[2], N2[5], N2[8]};
+    mm3(N2t, F0, T);
+    mm3(T, N1, F0);
+    double inv = 1. / F0[8];
+    for (int i = 0; i < 9; ++i) F[i] = F0[i] * inv + 0.0;
+}
+
+__device__ __forceinline__ double epipolar_error(const double* F, double x1, double y1, double x2, double y2) {
+    double r0 = x2 * F[0] + y2 * F[3] + 1.0 * F[6];
+    double r1 = x2 * F[1] + y2 * F[4] + 1.0 * F[7];
+    double r2 = x2 * F[2] + y2 * F[5] + 1.0 * F[8];
+    return r0 * x1 + r1 * y1 + r2 * 1.0;
+}
+
+// One workgroup per match list; hypotheses h = tid, tid + 256, ... ; strict '>' keeps the first best.
+__global__ __launch_bounds__(kNT) void f_ransac_kernel(const yv_match* __restrict__ matches, int64_t list_stride,
+                                                       const int32_t* __restrict__ counts,
+                                                       const int32_t* __restrict__ samples, int64_t sample_stride,
+                                                       int iters, double thr, double* __restrict__ F_out,
+                                                       int32_t* __restrict__ max_inliers, int32_t* __restrict__ found) {
+    __shared__ int32_t s_pts[kMaxKp * 4];
+    __shared__ int s_best_cnt[kNT];
+    __shared__ int s_best_h[kNT];
+    const int list = blockIdx.x;
+    const int tid = threadIdx.x;
+    int n = counts[list];
+    if (n > kMaxKp) n = kMaxKp;
+    if (n < 8) {  // "Not enough matches": return false, F untouched
+        if (tid == 0) found[list] = 0;
+        return;
+    }
+    const yv_match* m = matches + (int64_t)list * list_stride;
+    for (int i = tid; i < n; i += kNT) {
+        s_pts[4 * i] = m[i].pt1.x;
+        s_pts[4 * i + 1] = m[i].pt1.y;
+        s_pts[4 * i + 2] = m[i].pt2.x;
+        s_pts[4 * i + 3] = m[i].pt2.y;
+    }
+    __syncthreads();
+    const int32_t* smp = samples + (int64_t)list * sample_stride;
+    int best_cnt = INT32_MIN, best_h = 0x7fffffff;
+    double best_F[9];
+    for (int q = 0; q < 9; ++q) best_F[q] = 0;
+    for (int h = tid; h < iters; h += kNT) {
+        double pts8[32];
+        for (int j = 0; j < 8; ++j) {
+            int idx = smp[8 * h + j];
+            idx = idx < 0 ? 0 : (idx >= n ? n - 1 : idx);
+            for (int q = 0; q < 4; ++q) pts8[4 * j + q] = (double)s_pts[4 * idx + q];
+        }
+        double Fh[9];
+        fundamental_8pt(pts8, Fh);
+        int cnt = 0;
+        for (int k = 0; k < n; ++k) {
+            const double e = epipolar_error(Fh, (double)s_pts[4 * k], (double)s_pts[4 * k + 1],
+                                            (double)s_pts[4 * k + 2], (double)s_pts[4 * k + 3]);
+            if (fabs(e) < thr) cnt++;
+        }
+        if (cnt > best_cnt) {  // h increases within a lane: the first best of this lane wins
+            best_cnt = cnt;
+            best_h = h;
+            for (int q = 0; q < 9; ++q) best_F[q] = Fh[q];
+        }
+    }
+    s_best_cnt[tid] = best_cnt;
+    s_best_h[tid] = best_h;
+    __syncthreads();
+    if (tid == 0) {
+        int bc = INT32_MIN, bh = 0x7fffffff, bt = -1;
+        for (int t = 0; t < kNT; ++t) {
+            const int c = s_best_cnt[t], hh = s_best_h[t];
+            if (c > bc || (c == bc && hh < bh)) { bc = c; bh = hh; bt = t; }
+        }
+        s_best_h[0] = bt;
+        max_inliers[list] = bc;
+        found[list] = 1;
+    }
+    __syncthreads();
+    if (tid == s_best_h[0] && iters > 0)
+        for (int q = 0; q < 9; ++q) F_out[(int64_t)list * 9 + q] = best_F[q];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Sophus SE3 (pose = {qx, qy, qz, qw, tx, ty, tz})
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double k_sin(double x) {
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03, S3 = -1.98412698298579493134e-04,
+                 S4 = 2.75573137070700676789e-06, S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    if (!(fabs(x) <= 0.78539816339744827900)) return sin(x);
+    double z = x * x, v = z * x;
+    double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    return x + v * (S1 + z * r);
+}
+
+__device__ __forceinline__ double k_cos(double x) {
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03, C3 = 2.48015872894767294178e-05,
+                 C4 = -2.75573143513906633035e-07, C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    if (!(fabs(x) <= 0.78539816339744827900)) return cos(x);
+    double z = x * x;
+    double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    double hz = 0.5 * z, w = 1.0 - hz;
+    return w + (((1.0 - w) - hz) + (z * r - x * 0.0));
+}
+
+__device__ __forceinline__ void quat_mul(const double* a, const double* b, double* r) {
+    double ax = a[0], ay = a[1], az = a[2], aw = a[3], bx = b[0], by = b[1], bz = b[2], bw = b[3];
+    r[3] = aw * bw - ax * bx - ay * by - az * bz;
+    r[0] = aw * bx + ax * bw + ay * bz - az * by;
+    r[1] = aw * by + ay * bw + az * bx - ax * bz;
+    r[2] = aw * bz + az * bw + ax * by - ay * bx;
+}
+
+__device__ __forceinline__ void quat_rotate(const double* q, const double* v, double* out) {
+    double uv0 = q[1] * v[2] - q[2] * v[1];
+    double uv1 = q[2] * v[0] - q[0] * v[2];
+    double uv2 = q[0] * v[1] - q[1] * v[0];
+    uv0 += uv0; uv1 += uv1; uv2 += uv2;
+    double c0 = q[1] * uv2 - q[2] * uv1;
+    double c1 = q[2] * uv0 - q[0] * uv2;
+    double c2 = q[0] * uv1 - q[1] * uv0;
+    out[0] = v[0] + q[3] * uv0 + c0;
+    out[1] = v[1] + q[3] * uv1 + c1;
+    out[2] = v[2] + q[3] * uv2 + c2;
+}
+
+__device__ __forceinline__ void quat_to_R(const double* q, double* R) {
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz; R[2] = txz + twy;
+    R[3] = txy + twz; R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy; R[7] = tyz + twx; R[8] = 1 - (txx + tyy);
+}
+
+__device__ __forceinline__ void se3_act(const double* T, const double* p, double* out) {
+    double r[3];
+    quat_rotate(T, p, r);
+    out[0] = r[0] + T[4];
+    out[1] = r[1] + T[5];
+    out[2] = r[2] + T[6];
+}
+
+__device__ __forceinline__ void se3_mul(const double* A, const double* B, double* out) {
+    double r[3], q[4];
+    quat_rotate(A, B + 4, r);
+    double t0 = A[4] + r[0], t1 = A[5] + r[1], t2 = A[6] + r[2];
+    quat_mul(A, B, q);
+    double sn = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
+    if (sn != 1.0) {
+        double sc = 2.0 / (1.0 + sn);
+        for (int i = 0; i < 4; ++i) q[i] *= sc;
+    }
+    out[0] = q[0]; out[1] = q[1]; out[2] = q[2]; out[3] = q[3];
+    out[4] = t0; out[5] = t1; out[6] = t2;
+}
+
+__device__ void se3_exp(const double* a, double* out) {
+    const double* om = a + 3;
+    const double eps = 1e-10;
+    double theta_sq = om[0] * om[0] + om[1] * om[1] + om[2] * om[2];
+    double theta, imag, real;
+    if (theta_sq < eps * eps) {
+        theta = 0;
+        double theta_po4 = theta_sq * theta_sq;
+        imag = 0.5 - (1.0 / 48.0) * theta_sq + (1.0 / 3840.0) * theta_po4;
+        real = 1 - (1.0 / 8.0) * theta_sq + (1.0 / 384.0) * theta_po4;
+    } else {
+        theta = sqrt(theta_sq);
+        double half = 0.5 * theta;
+        imag = k_sin(half) / theta;
+        real = k_cos(half);
+    }
+    double q[4] = {imag * om[0], imag * om[1], imag * om[2], real};
+    double O[9] = {0, -om[2], om[1], om[2], 0, -om[0], -om[1], om[0], 0};
+    double O2[9];
+    mm3(O, O, O2);
+    double V[9];
+    if (theta < eps) {
+        quat_to_R(q, V);
+    } else {
+        double theta_sq2 = theta * theta;
+        double a1 = (1 - k_cos(theta)) / theta_sq2;
+        double a2 = (theta - k_sin(theta)) / (theta_sq2 * theta);
+        for (int i = 0; i < 9; ++i) V[i] = ((i % 4 == 0) ? 1.0 : 0.0) + a1 * O[i] + a2 * O2[i];
+    }
+    out[0] = q[0]; out[1] = q[1]; out[2] = q[2]; out[3] = q[3];
+    for (int i = 0; i < 3; ++i) out[4 + i] = V[3 * i] * a[0] + V[3 * i + 1] * a[1] + V[3 * i + 2] * a[2];
+}
+
+// ------------------------------------------------------------------------------------------------
+// triangulation (Eigen JacobiSVD 4x4, registers) and world2Camera
+// ------------------------------------------------------------------------------------------------
+struct JRot {
+    double c, s;
+};
+
+__device__ __forceinline__ JRot make_jacobi(double x, double y, double z) {
+    JRot r;
+    double deno = 2 * fabs(y);
+    if (deno < DBL_MIN) {
+        r.c = 1; r.s = 0;
+        return r;
+    }
+    double tau = (x - z) / deno;
+    double w = sqrt(tau * tau + 1);
+    double t = tau > 0 ? 1 / (tau + w) : 1 / (tau - w);
+    double sign_t = t > 0 ? 1 : -1;
+    double nn = 1 / sqrt(t * t + 1);
+    r.s = -sign_t * (y / fabs(y)) * fabs(t) * nn;
+    r.c = nn;
+    return r;
+}
+
+// JacobiSVD<MatrixXd>(A 4x4 column-major): sv descending, V column-major.  false on non-finite input.
+__device__ bool eigen_jacobi_svd4(const double (&Ain)[16], double (&sv)[4], double (&V)[16]) {
+    constexpr int n = 4;
+    double Wk[16];
+    double scale = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        double a = fabs(Ain[i]);
+        if (a != a) return false;
+        if (a > scale) scale = a;
+    }
+    if (!isfinite(scale)) return false;
+    if (scale == 0) scale = 1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Wk[i] = Ain[i] / scale;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) V[i] = (i % 5 == 0) ? 1.0 : 0.0;
+    const double considerAsZero = DBL_MIN, precision = 2 * DBL_EPSILON;
+    double maxDiag = 0;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+        double a = fabs(Wk[i + i * n]);
+        if (a > maxDiag) maxDiag = a;
+    }
+    bool finished = false;
+    int guard = 0;
+    while (!finished && guard < 10000) {
+        finished = true;
+        ++guard;
+#pragma unroll
+        for (int p = 1; p < n; ++p)
+#pragma unroll
+            for (int q = 0; q < p; ++q) {
+                double threshold = considerAsZero > precision * maxDiag ? considerAsZero : precision * maxDiag;
+                if (fabs(Wk[p + q * n]) > threshold || fabs(Wk[q + p * n]) > threshold) {
+                    finished = false;
+                    // real_2x2_jacobi_svd
+                    double m00 = Wk[p + p * n], m01 = Wk[p + q * n], m10 = Wk[q + p * n], m11 = Wk[q + q * n];
+                    JRot rot1;
+                    double t = m00 + m11;
+                    double d = m10 - m01;
+                    if (fabs(d) < DBL_MIN) {
+                        rot1.s = 0; rot1.c = 1;
+                    } else {
+                        double u = t / d;
+                        double tmp = sqrt(1 + u * u);
+                        rot1.s = 1 / tmp;
+                        rot1.c = u / tmp;
+                    }
+                    if (!(rot1.c == 1 && rot1.s == 0)) {
+                        double a0 = m00, b0 = m10, a1 = m01, b1 = m11;
+                        m00 = rot1.c * a0 + rot1.s * b0;
+                        m10 = -rot1.s * a0 + rot1.c * b0;
+                        m01 = rot1.c * a1 + rot1.s * b1;
+                        m11 = -rot1.s * a1 + rot1.c * b1;
+                    }
+                    JRot jr = make_jacobi(m00, m01, m11);
+                    JRot jl;
+                    {
+                        const double jtc = jr.c, jts = -jr.s;
+                        jl.c = rot1.c * jtc - rot1.s * jts;
+                        jl.s = rot1.c * jts + rot1.s * jtc;
+                    }
+                    // work.applyOnTheLeft(p, q, jl): rows p, q
+                    if (!(jl.c == 1 && jl.s == 0)) {
+#pragma unroll
+                        for (int i = 0; i < n; ++i) {
+                            double xi = Wk[p + i * n], yi = Wk[q + i * n];
+                            Wk[p + i * n] = jl.c * xi + jl.s * yi;
+                            Wk[q + i * n] = -jl.s * xi + jl.c * yi;
+                        }
+                    }
+                    // work.applyOnTheRight(p, q, jr) and V.applyOnTheRight(p, q, jr): rotation by jr^T
+                    const double tc = jr.c, ts = -jr.s;
+                    if (!(tc == 1 && ts == 0)) {
+#pragma unroll
+                        for (int i = 0; i < n; ++i) {
+                            double xi = Wk[i + p * n], yi = Wk[i + q * n];
+                            Wk[i + p * n] = tc * xi + ts * yi;
+                            Wk[i + q * n] = -ts * xi + tc * yi;
+                        }
+#pragma unroll
+                        for (int i = 0; i < n; ++i) {
+                            double xi = V[i + p * n], yi = V[i + q * n];
+                            V[i + p * n] = tc * xi + ts * yi;
+                            V[i + q * n] = -ts * xi + tc * yi;
+                        }
+                    }
+                    double aa = fabs(Wk[p + p * n]), bb = fabs(Wk[q + q * n]);
+                    double mx = aa > bb ? aa : bb;
+                    if (mx > maxDiag) maxDiag = mx;
+                }
+            }
+    }
+#pragma unroll
+    for (int i = 0; i < n; ++i) sv[i] = fabs(Wk[i + i * n]) * scale;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+        int pos = i;
+        double mx = sv[i];
+#pragma unroll
+        for (int k = i + 1; k < n; ++k)
+            if (sv[k] > mx) { mx = sv[k]; pos = k; }
+        if (mx == 0) break;
+        if (pos != i) {
+            // swap sv[i] <-> sv[pos] and V columns, static indices only
+#pragma unroll
+            for (int k = i + 1; k < n; ++k)
+                if (k == pos) {
+                    double t = sv[i]; sv[i] = sv[k]; sv[k] = t;
+#pragma unroll
+                    for (int r = 0; r < n; ++r) { t = V[r + k * n]; V[r + k * n] = V[r + i * n]; V[r + i * n] = t; }
+                }
+        }
+    }
+    return true;
+}
+
+__global__ void triangulate_kernel(const yv_match* __restrict__ m, int n, const double* __restrict__ poses /*[2][7]*/,
+                                   const double* __restrict__ K, double* __restrict__ Xw, uint8_t* __restrict__ ok,
+                                   int32_t* __restrict__ n_ok) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool good = false;
+    if (i < n) {
+        const double K0 = K[0], K2 = K[2], K4 = K[4], K5 = K[5];
+        const double pa[2] = {((double)m[i].pt1.x - K2) * 1.0 / K0, ((double)m[i].pt1.y - K5) * 1.0 / K4};
+        const double pb[2] = {((double)m[i].pt2.x - K2) * 1.0 / K0, ((double)m[i].pt2.y - K5) * 1.0 / K4};
+        double A[16];
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            const double* T = poses + 7 * v;
+            const double* pp = v == 0 ? pa : pb;
+            double R[9];
+            quat_to_R(T, R);
+            double mm[12];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                mm[4 * r] = R[3 * r]; mm[4 * r + 1] = R[3 * r + 1]; mm[4 * r + 2] = R[3 * r + 2]; mm[4 * r + 3] = T[4 + r];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                A[(2 * v) + 4 * j] = pp[0] * mm[8 + j] - mm[j];
+                A[(2 * v + 1) + 4 * j] = pp[1] * mm[8 + j] - mm[4 + j];
+            }
+        }
+        double sv[4], V[16];
+        double X0 = NAN, X1 = NAN, X2 = NAN;
+        bool s = false;
+        if (eigen_jacobi_svd4(A, sv, V)) {
+            X0 = V[0 + 12] / V[3 + 12];
+            X1 = V[1 + 12] / V[3 + 12];
+            X2 = V[2 + 12] / V[3 + 12];
+            s = sv[3] / sv[2] < 1e-2;
+        }
+        Xw[3 * i] = X0;
+        Xw[3 * i + 1] = X1;
+        Xw[3 * i + 2] = X2;
+        good = s && X2 > 0;
+        ok[i] = good ? 1 : 0;
+    }
+    const uint64_t bal = __ballot(good);
+    if ((threadIdx.x & 63) == 0 && bal) atomicAdd(n_ok, (int32_t)__popcll(bal));
+}
+
+__global__ void world2camera_kernel(const double* __restrict__ X, int n, const double* __restrict__ T,
+                                    const double* __restrict__ K, double* __restrict__ out) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    double R[9], M[12], KM[12];
+    quat_to_R(T, R);
+    for (int i = 0; i < 3; ++i) {
+        M[4 * i] = R[3 * i]; M[4 * i + 1] = R[3 * i + 1]; M[4 * i + 2] = R[3 * i + 2]; M[4 * i + 3] = T[4 + i];
+    }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 4; ++j) KM[4 * i + j] = K[3 * i] * M[j] + K[3 * i + 1] * M[4 + j] + K[3 * i + 2] * M[8 + j];
+    for (int i = 0; i < 3; ++i)
+        out[3 * k + i] = KM[4 * i] * X[3 * k] + KM[4 * i + 1] * X[3 * k + 1] + KM[4 * i + 2] * X[3 * k + 2] + KM[4 * i + 3] * 1.0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Eigen LDLT 6x6 (lane 0)
+// ------------------------------------------------------------------------------------------------
+__device__ bool ldlt6_solve(const double* Hin, const double* b, double* x, int variant) {
+    double mat[36];
+    int tr[6];
+    for (int i = 0; i < 36; ++i) mat[i] = Hin[i];
+    const int n = 6;
+    int sign = 0;
+    int found_zero_pivot = 0, ret = 1;
+    double temp[6];
+#define L(i, j) mat[(i) * 6 + (j)]
+    for (int k = 0; k < n; ++k) {
+        int big = k;
+        double bv = fabs(L(k, k));
+        for (int i = k + 1; i < n; ++i)
+            if (fabs(L(i, i)) > bv) { bv = fabs(L(i, i)); big = i; }
+        tr[k] = big;
+        if (k != big) {
+            int s = n - big - 1;
+            for (int j = 0; j < k; ++j) { double t = L(k, j); L(k, j) = L(big, j); L(big, j) = t; }
+            for (int j = 0; j < s; ++j) { double t = L(big + 1 + j, k); L(big + 1 + j, k) = L(big + 1 + j, big); L(big + 1 + j, big) = t; }
+            { double t = L(k, k); L(k, k) = L(big, big); L(big, big) = t; }
+            for (int i = k + 1; i < big; ++i) { double t = L(i, k); L(i, k) = L(big, i); L(big, i) = t; }
+        }
+        int rs = n - k - 1;
+        if (k > 0) {
+            for (int j = 0; j < k; ++j) temp[j] = L(j, j) * L(k, j);
+            double dot = L(k, 0) * temp[0];
+            for (int j = 1; j < k; ++j) dot = dot + L(k, j) * temp[j];
+            L(k, k) -= dot;
+            for (int i = k + 1; i < n; ++i) {
+                if (variant == 0) {
+                    double acc = L(i, k);
+                    for (int j = 0; j < k; ++j) acc = acc - L(i, j) * temp[j];
+                    L(i, k) = acc;
+                } else {
+                    double d = L(i, 0) * temp[0];
+                    for (int j = 1; j < k; ++j) d = d + L(i, j) * temp[j];
+                    L(i, k) = L(i, k) - d;
+                }
+            }
+        }
+        double akk = L(k, k);
+        int valid = fabs(akk) > 0;
+        if (k == 0 && !valid) {
+            sign = 0;
+            for (int j = 0; j < n; ++j) tr[j] = j;
+            ret = 0;
+            break;
+        }
+        if (rs > 0 && valid) {
+            for (int i = k + 1; i < n; ++i) L(i, k) /= akk;
+        } else if (rs > 0) {
+            for (int i = k + 1; i < n; ++i) ret = ret && (L(i, k) == 0);
+        }
+        if (found_zero_pivot && valid) ret = 0;
+        else if (!valid) found_zero_pivot = 1;
+        if (sign == 1) { if (akk < 0) sign = 3; }
+        else if (sign == 2) { if (akk > 0) sign = 3; }
+        else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+    }
+    (void)ret;
+    const bool positive = (sign == 1 || sign == 0);
+    double v[6];
+    for (int i = 0; i < 6; ++i) v[i] = b[i];
+    for (int k = 0; k < n; ++k) { double t = v[k]; v[k] = v[tr[k]]; v[tr[k]] = t; }
+    for (int j = 0; j < n; ++j)
+        for (int i = j + 1; i < n; ++i) v[i] = v[i] - L(i, j) * v[j];
+    for (int i = 0; i < n; ++i) {
+        if (fabs(L(i, i)) > DBL_MIN) v[i] /= L(i, i);
+        else v[i] = 0;
+    }
+    for (int j = n - 1; j >= 0; --j)
+        for (int i = 0; i < j; ++i) v[i] = v[i] - L(j, i) * v[j];
+    for (int k = n - 1; k >= 0; --k) { double t = v[k]; v[k] = v[tr[k]]; v[tr[k]] = t; }
+#undef L
+    for (int i = 0; i < 6; ++i) x[i] = v[i];
+    return positive;
+}
+
+// ------------------------------------------------------------------------------------------------
+// pose-only LM (g2o semantics) and GN, one workgroup per problem
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void edge_error(const double* T, const double* K, const double* X, const double* meas,
+                                           double* e) {
+    double pc[3];
+    se3_act(T, X, pc);
+    double u0 = K[0] * pc[0] + K[1] * pc[1] + K[2] * pc[2];
+    double u1 = K[3] * pc[0] + K[4] * pc[1] + K[5] * pc[2];
+    double u2 = K[6] * pc[0] + K[7] * pc[1] + K[8] * pc[2];
+    e[0] = meas[0] - u0 / u2;
+    e[1] = meas[1] - u1 / u2;
+}
+
+__device__ __forceinline__ void edge_jacobian(const double* T, const double* K, const double* X, double* J) {
+    double pc[3];
+    se3_act(T, X, pc);
+    double fx = K[0], fy = K[4];
+    double x = pc[0], y = pc[1], z = pc[2];
+    double zinv = 1.0 / (z + 1e-18);
+    double zinv2 = zinv * zinv;
+    J[0] = -fx * zinv; J[1] = 0; J[2] = fx * x * zinv2; J[3] = fx * x * y * zinv2;
+    J[4] = -fx - fx * x * x * zinv2; J[5] = fx * y * zinv;
+    J[6] = 0; J[7] = -fy * zinv; J[8] = fy * y * zinv2; J[9] = fy + fy * y * y * zinv2;
+    J[10] = -fy * x * y * zinv2; J[11] = -fy * x * zinv;
+}
+
+__device__ __forceinline__ double huber_rho(double e2, double* rho1) {
+    const double delta = 1.0, dsqr = delta * delta;
+    if (e2 <= dsqr) {
+        *rho1 = 1.;
+        return e2;
+    }
+    double sqrte = sqrt(e2);
+    *rho1 = delta / sqrte;
+    return 2 * sqrte * delta - dsqr;
+}
+
+// Tree sum of per-thread partials: p[t] += p[t + off], off = 128 .. 1 (the oracle's sum_mode 1).
+// red: [nv][kNT] in LDS; each thread has written its partials; returns the totals into out[0..nv).
+__device__ void tree_reduce(double* red, int nv, double* out) {
+    const int tid = threadIdx.x;
+    __syncthreads();
+    for (int off = kNT / 2; off > 0; off >>= 1) {
+        if (tid < off)
+            for (int v = 0; v < nv; ++v) red[v * kNT + tid] = red[v * kNT + tid] + red[v * kNT + tid + off];
+        __syncthreads();
+    }
+    if (tid < nv) out[tid] = red[tid * kNT];
+    __syncthreads();
+}
+
+struct LMShared {
+    double T[7], Tbak[7], K[9];
+    double H[36], b[6], x[6], vals[32];
+    double lambda, ni, currentChi, tempChi, rho;
+    int flag;  // control broadcast from lane 0
+};
+
+constexpr int kLMVals = 28;  // 21 lower-triangle H entries + 6 b + 1 chi2
+
+__global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict__ offsets, const double* __restrict__ Xall,
+                                                      const double* __restrict__ uvall, const double* __restrict__ Kall,
+                                                      double* __restrict__ poses, uint8_t* __restrict__ outlier_all,
+                                                      int32_t* __restrict__ inliers) {
+    __shared__ double s_err[kMaxEdges * 2];
+    __shared__ uint8_t s_level[kMaxEdges], s_out[kMaxEdges], s_robust[kMaxEdges];
+    __shared__ int16_t s_active[kMaxEdges];
+    __shared__ double s_red[kLMVals * kNT];
+    __shared__ LMShared S;
+    __shared__ int s_tmp[40];
+    const int prob = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int e0 = offsets[prob];
+    int n = offsets[prob + 1] - e0;
+    if (n > kMaxEdges) n = kMaxEdges;
+    const double* X = Xall + 3 * (int64_t)e0;
+    const double* uv = uvall + 2 * (int64_t)e0;
+    if (tid < 9) S.K[tid] = Kall[9 * prob + tid];
+    if (tid < 7) S.T[tid] = poses[7 * prob + tid];
+    for (int i = tid; i < n; i += kNT) {
+        s_level[i] = 0;
+        s_out[i] = 0;
+        s_robust[i] = 1;
+        s_err[2 * i] = 0;
+        s_err[2 * i + 1] = 0;
+    }
+    __syncthreads();
+    double prior[7];
+    for (int q = 0; q < 7; ++q) prior[q] = S.T[q];
+    const double chi2th = 5.991;
+    const double tau = 1e-5, goodLower = 1.0 / 3.0, goodUpper = 2.0 / 3.0;
+    int outlierCount = 0;
+
+    for (int round = 0; round < 4; ++round) {
+        if (tid < 7) S.T[tid] = prior[tid];
+        // initializeOptimization(): active = level-0 edges in insertion order (block compaction)
+        int na = 0;
+        for (int base = 0; base < n; base += kNT) {
+            const int i = base + tid;
+            const int f = (i < n && s_level[i] == 0) ? 1 : 0;
+            int tot = 0;
+            const int off = block_excl_scan_geom(f, s_tmp, &tot);
+            if (f) s_active[na + off] = (int16_t)i;
+            na += tot;
+        }
+        __syncthreads();
+        if (na > 0) {
+            double lambda = 0, ni = 2;
+            for (int it = 0; it < 10; ++it) {
+                // computeActiveErrors + activeRobustChi2 + buildSystem at the current estimate
+                double part[kLMVals];
+                for (int v = 0; v < kLMVals; ++v) part[v] = 0.0;
+                double T[7], K[9];
+                for (int q = 0; q < 7; ++q) T[q] = S.T[q];
+                for (int q = 0; q < 9; ++q) K[q] = S.K[q];
+                for (int a = tid; a < na; a += kNT) {
+                    const int i = s_active[a];
+                    double e[2];
+                    edge_error(T, K, X + 3 * i, uv + 2 * i, e);
+                    s_err[2 * i] = e[0];
+                    s_err[2 * i + 1] = e[1];
+                    const double c2 = e[0] * e[0] + e[1] * e[1];
+                    double w = 1.0;
+                    double chi = c2;
+                    if (s_robust[i]) chi = huber_rho(c2, &w);
+                    part[27] = part[27] + chi;
+                    double J[12];
+                    edge_jacobian(T, K, X + 3 * i, J);
+                    int v = 0;
+                    for (int r = 0; r < 6; ++r) {
+                        double t0 = J[r] * w + J[6 + r] * 0.0;
+                        double t1 = J[r] * 0.0 + J[6 + r] * w;
+                        for (int c = 0; c <= r; ++c) {
+                            part[v] = part[v] + (t0 * J[c] + t1 * J[6 + c]);
+                            ++v;
+                        }
+                        double s0 = (w * J[r]) * 1.0 + (w * J[6 + r]) * 0.0;
+                        double s1 = (w * J[r]) * 0.0 + (w * J[6 + r]) * 1.0;
+                        part[21 + r] = part[21 + r] + (-(s0 * e[0] + s1 * e[1]));
+                    }
+                }
+                for (int v = 0; v < kLMVals; ++v) s_red[v * kNT + tid] = part[v];
+                tree_reduce(s_red, kLMVals, S.vals);
+                if (tid == 0) {
+                    int v = 0;
+                    for (int r = 0; r < 6; ++r)
+                        for (int c = 0; c <= r; ++c) {
+                            S.H[r * 6 + c] = S.vals[v];
+                            S.H[c * 6 + r] = S.vals[v];
+                            ++v;
+                        }
+                    for (int r = 0; r < 6; ++r) S.b[r] = S.vals[21 + r];
+                    S.currentChi = S.vals[27];
+                    if (it == 0) {
+                        double maxDiag = 0;
+                        for (int j = 0; j < 6; ++j) maxDiag = fabs(S.H[j * 7]) > maxDiag ? fabs(S.H[j * 7]) : maxDiag;
+                        lambda = tau * maxDiag;
+                        ni = 2;
+                    }
+                }
+                // trial loop (do ... while (rho < 0 && qmax < 10))
+                int qmax = 0;
+                bool terminate = false;
+                while (true) {
+                    int ok2 = 0;
+                    if (tid == 0) {
+                        for (int q = 0; q < 7; ++q) S.Tbak[q] = S.T[q];
+                        double Hl[36];
+                        for (int q = 0; q < 36; ++q) Hl[q] = S.H[q];
+                        for (int j = 0; j < 6; ++j) Hl[j * 7] += lambda;
+                        ok2 = ldlt6_solve(Hl, S.b, S.x, 0) ? 1 : 0;
+                        double Tn[7], Tnew[7];
+                        se3_exp(S.x, Tn);
+                        se3_mul(Tn, S.T, Tnew);
+                        for (int q = 0; q < 7; ++q) S.T[q] = Tnew[q];
+                        S.flag = ok2;
+                    }
+                    __syncthreads();
+                    ok2 = S.flag;
+                    for (int q = 0; q < 7; ++q) T[q] = S.T[q];
+                    double pc = 0.0;
+                    for (int a = tid; a < na; a += kNT) {
+                        const int i = s_active[a];
+                        double e[2];
+                        edge_error(T, K, X + 3 * i, uv + 2 * i, e);
+                        s_err[2 * i] = e[0];
+                        s_err[2 * i + 1] = e[1];
+                        const double c2 = e[0] * e[0] + e[1] * e[1];
+                        double w;
+                        pc = pc + (s_robust[i] ? huber_rho(c2, &w) : c2);
+                    }
+                    s_red[tid] = pc;
+                    tree_reduce(s_red, 1, S.vals);
+                    if (tid == 0) {
+                        double tempChi = S.vals[0];
+                        if (!ok2) tempChi = DBL_MAX;
+                        double rho = S.currentChi - tempChi;
+                        double scale = 1;
+                        if (ok2) {
+                            double sc = 0;
+                            for (int j = 0; j < 6; ++j) sc += S.x[j] * (lambda * S.x[j] + S.b[j]);
+                            scale = sc + 1e-3;
+                        }
+                        rho /= scale;
+                        int brk = 0;
+                        if (rho > 0 && isfinite(tempChi) && ok2) {
+                            double t = 2 * rho - 1;
+                            double alpha = 1. - t * t * t;
+                            alpha = alpha < goodUpper ? alpha : goodUpper;
+                            double sf = goodLower > alpha ? goodLower : alpha;
+                            lambda *= sf;
+                            ni = 2;
+                            S.currentChi = tempChi;
+                        } else {
+                            lambda *= ni;
+                            ni *= 2;
+                            for (int q = 0; q < 7; ++q) S.T[q] = S.Tbak[q];
+                            if (!isfinite(lambda)) brk = 1;
+                        }
+                        qmax++;
+                        const bool again = !brk && rho < 0 && qmax < 10;
+                        S.flag = again ? 1 : 0;
+                        if (!again) S.flag = (qmax == 10 || rho == 0 || !isfinite(lambda)) ? 2 : 0;
+                    }
+                    __syncthreads();
+                    const int f = S.flag;
+                    __syncthreads();
+                    if (f == 1) continue;
+                    terminate = (f == 2);
+                    break;
+                }
+                if (terminate) break;
+            }
+        }
+        __syncthreads();
+        // classify: outliers recomputed at the final estimate, others keep their last trial error
+        double T[7], K[9];
+        for (int q = 0; q < 7; ++q) T[q] = S.T[q];
+        for (int q = 0; q < 9; ++q) K[q] = S.K[q];
+        int cnt = 0;
+        for (int i = tid; i < n; i += kNT) {
+            if (s_out[i]) edge_error(T, K, X + 3 * i, uv + 2 * i, &s_err[2 * i]);
+            const double c2 = s_err[2 * i] * s_err[2 * i] + s_err[2 * i + 1] * s_err[2 * i + 1];
+            if (c2 > chi2th) {
+                s_out[i] = 1;
+                s_level[i] = 1;
+                cnt++;
+            } else {
+                s_out[i] = 0;
+                s_level[i] = 0;
+            }
+            if (round == 2) s_robust[i] = 0;
+        }
+        int tot = 0;
+        block_excl_scan_geom(cnt, s_tmp, &tot);
+        outlierCount = tot;
+        __syncthreads();
+    }
+    if (tid < 7) poses[7 * prob + tid] = S.T[tid];
+    for (int i = tid; i < n; i += kNT) outlier_all[e0 + i] = s_out[i];
+    if (tid == 0) inliers[prob] = n - outlierCount;
+}
+
+__global__ __launch_bounds__(kNT) void pose_gn_kernel(const int32_t* __restrict__ offsets, const double* __restrict__ Xall,
+                                                      const double* __restrict__ uvall, const double* __restrict__ Kall,
+                                                      double* __restrict__ poses, int32_t* __restrict__ iters_out) {
+    __shared__ double s_red[kLMVals * kNT];
+    __shared__ double s_vals[32];
+    __shared__ double s_T[7];
+    __shared__ int s_flag;
+    const int prob = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int e0 = offsets[prob];
+    const int n = offsets[prob + 1] - e0;
+    const double* X = Xall + 3 * (int64_t)e0;
+    const double* uv = uvall + 2 * (int64_t)e0;
+    double K[9];
+    for (int q = 0; q < 9; ++q) K[q] = Kall[9 * prob + q];
+    if (tid < 7) s_T[tid] = poses[7 * prob + tid];
+    __syncthreads();
+    const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
+    double lastCost = 0;
+    int acc = 0;
+    for (int iter = 0; iter < 10; iter++) {
+        double T[7];
+        for (int q = 0; q < 7; ++q) T[q] = s_T[q];
+        double part[kLMVals];
+        for (int v = 0; v < kLMVals; ++v) part[v] = 0.0;
+        for (int i = tid; i < n; i += kNT) {
+            double pc[3];
+            se3_act(T, X + 3 * i, pc);
+            double inv_z = 1.0 / pc[2];
+            double inv_z2 = inv_z * inv_z;
+            double proj0 = fx * pc[0] / pc[2] + cx, proj1 = fy * pc[1] / pc[2] + cy;
+            double ee0 = uv[2 * i] - proj0, ee1 = uv[2 * i + 1] - proj1;
+            part[27] = part[27] + (ee0 * ee0 + ee1 * ee1);
+            double J[12] = {-fx * inv_z, 0, fx * pc[0] * inv_z2, fx * pc[0] * pc[1] * inv_z2,
+                            -fx - fx * pc[0] * pc[0] * inv_z2, fx * pc[1] * inv_z,
+                            0, -fy * inv_z, fy * pc[1] * inv_z2, fy + fy * pc[1] * pc[1] * inv_z2,
+                            -fy * pc[0] * pc[1] * inv_z2, -fy * pc[0] * inv_z};
+            int v = 0;
+            for (int r = 0; r < 6; ++r) {
+                for (int c = 0; c <= r; ++c) {
+                    part[v] = part[v] + (J[r] * J[c] + J[6 + r] * J[6 + c]);
+                    ++v;
+                }
+                part[21 + r] = part[21 + r] + ((-J[r]) * ee0 + (-J[6 + r]) * ee1);
+            }
+        }
+        for (int v = 0; v < kLMVals; ++v) s_red[v * kNT + tid] = part[v];
+        tree_reduce(s_red, kLMVals, s_vals);
+        if (tid == 0) {
+            double H[36], b[6], dx[6];
+            int v = 0;
+            for (int r = 0; r < 6; ++r)
+                for (int c = 0; c <= r; ++c) {
+                    H[r * 6 + c] = s_vals[v];
+                    H[c * 6 + r] = s_vals[v];
+                    ++v;
+                }
+            for (int r = 0; r < 6; ++r) b[r] = s_vals[21 + r];
+            const double cost = s_vals[27];
+            ldlt6_solve(H, b, dx, 1);
+            int stop = 0;
+            if (isnan(dx[0])) stop = 1;
+            else if (iter > 0 && cost >= lastCost) stop = 1;
+            else {
+                double Tn[7], Tnew[7], Tc[7];
+                for (int q = 0; q < 7; ++q) Tc[q] = s_T[q];
+                se3_exp(dx, Tn);
+                se3_mul(Tn, Tc, Tnew);
+                for (int q = 0; q < 7; ++q) s_T[q] = Tnew[q];
+                lastCost = cost;
+                acc++;
+                double q0 = dx[0] * dx[0] + (dx[2] * dx[2] + dx[4] * dx[4]);
+                double q1 = dx[1] * dx[1] + (dx[3] * dx[3] + dx[5] * dx[5]);
+                if (sqrt(q0 + q1) < 1e-6) stop = 1;
+            }
+            s_flag = stop;
+        }
+        __syncthreads();
+        const int stop = s_flag;
+        __syncthreads();
+        if (stop) break;
+    }
+    if (tid < 7) poses[7 * prob + tid] = s_T[tid];
+    if (tid == 0) iters_out[prob] = acc;
+}
+
+}  // namespace geom
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+void launch_f_ransac(const yv_match* matches, int64_t list_stride, const int32_t* counts, int n_lists,
+                     const int32_t* samples, int64_t sample_stride, int iters, double thr, double* F_out,
+                     int32_t* max_inliers, int32_t* found, hipStream_t s) {
+    hipLaunchKernelGGL(geom::f_ransac_kernel, dim3(n_lists), dim3(geom::kNT), 0, s, matches, list_stride, counts,
+                       samples, sample_stride, iters, thr, F_out, max_inliers, found);
+}
+
+void launch_triangulate(const yv_match* m, int n, const double* poses2, const double* K, double* Xw, uint8_t* ok,
+                        int32_t* n_ok, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(geom::triangulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, m, n, poses2, K, Xw, ok, n_ok);
+}
+
+void launch_world2camera(const double* X, int n, const double* T, const double* K, double* out, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(geom::world2camera_kernel, dim3((n + 255) / 256), dim3(256), 0, s, X, n, T, K, out);
+}
+
+void launch_pose_lm(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
+                    double* poses, uint8_t* outlier, int32_t* inliers, hipStream_t s) {
+    hipLaunchKernelGGL(geom::pose_lm_kernel, dim3(n_problems), dim3(geom::kNT), 0, s, offsets, X, uv, K, poses,
+                       outlier, inliers);
+}
+
+void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
+                    double* poses, int32_t* iters, hipStream_t s) {
+    hipLaunchKernelGGL(geom::pose_gn_kernel, dim3(n_problems), dim3(geom::kNT), 0, s, offsets, X, uv, K, poses, iters);
+}
+
+}  // namespace yavo

@@ -55,4 +55,16 @@ void launch_match_finalize(uint32_t* match_key, const yv_keypoint* keypoints,
 void launch_filter_records(const yv_match* in, int n, int thr, yv_match* out, int32_t* out_count,
                            hipStream_t s);
 
+// ---- geometry (yavo_geom.hip) ----
+void launch_f_ransac(const yv_match* matches, int64_t list_stride, const int32_t* counts, int n_lists,
+                     const int32_t* samples, int64_t sample_stride, int iters, double thr, double* F_out,
+                     int32_t* max_inliers, int32_t* found, hipStream_t s);
+void launch_triangulate(const yv_match* m, int n, const double* poses2, const double* K, double* Xw, uint8_t* ok,
+                        int32_t* n_ok, hipStream_t s);
+void launch_world2camera(const double* X, int n, const double* T, const double* K, double* out, hipStream_t s);
+void launch_pose_lm(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
+                    double* poses, uint8_t* outlier, int32_t* inliers, hipStream_t s);
+void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
+                    double* poses, int32_t* iters, hipStream_t s);
+
 }  // namespace yavo
