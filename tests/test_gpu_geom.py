@@ -94,8 +94,10 @@ def test_pose_lm_batch(ctx, oracle):
     probs = [scene.random_scene(n, seed=20 + i, noise_px=0.5, outlier_frac=0.1) for i, n in enumerate((50, 900, 1600))]
     priors = [scene.perturb(p[2], np.random.default_rng(i)) for i, p in enumerate(probs)]
     offs = np.cumsum([0] + [len(p[0]) for p in probs]).astype(np.int32)
-    Xall = np.concatenate([p[0] for p in probs])
-    uvall = np.concatenate([p[1] for p in probs])
+    # random_scene's X is a transposed view; np.concatenate keeps its Fortran order and torch keeps strides,
+    # so force the row-major [n][3] / [n][2] layouts the ABI documents
+    Xall = np.ascontiguousarray(np.concatenate([p[0] for p in probs]))
+    uvall = np.ascontiguousarray(np.concatenate([p[1] for p in probs]))
     dev = "cuda:0"
     d_off = torch.from_numpy(offs).to(dev)
     d_X = torch.from_numpy(Xall).to(dev)
@@ -117,3 +119,57 @@ def test_pose_lm_batch(ctx, oracle):
         assert inl[i] == oinl
         np.testing.assert_array_equal(P[i], oT)
         np.testing.assert_array_equal(out[offs[i]:offs[i + 1]], oout)
+
+
+def test_pose_gn_batch(ctx, oracle):
+    import torch
+    probs = [scene.random_scene(n, seed=30 + i, noise_px=0.3) for i, n in enumerate((40, 700, 2000, 0))]
+    priors = [scene.perturb(p[2], np.random.default_rng(i), rot=0.01, trans=0.05) for i, p in enumerate(probs)]
+    offs = np.cumsum([0] + [len(p[0]) for p in probs]).astype(np.int32)
+    dev = "cuda:0"
+    d_off = torch.from_numpy(offs).to(dev)
+    d_X = torch.from_numpy(np.ascontiguousarray(np.concatenate([p[0] for p in probs]))).to(dev)
+    d_uv = torch.from_numpy(np.ascontiguousarray(np.concatenate([p[1] for p in probs]))).to(dev)
+    d_K = torch.from_numpy(np.tile(scene.K_KITTI.reshape(1, 9), (len(probs), 1))).to(dev)
+    d_P = torch.from_numpy(np.stack(priors)).to(dev)
+    d_it = torch.full((len(probs),), -1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    assert ctx.lib.yv_pose_gn_batch(ctx.handle, len(probs), d_off.data_ptr(), d_X.data_ptr(), d_uv.data_ptr(),
+                                    d_K.data_ptr(), d_P.data_ptr(), d_it.data_ptr(), None) == 0
+    ctx.sync()
+    P, it = d_P.cpu().numpy(), d_it.cpu().numpy()
+    for i, p in enumerate(probs):
+        oT, oit = oracle.pose_gn(p[0], p[1], scene.K_KITTI, priors[i], 1)
+        assert it[i] == oit
+        np.testing.assert_array_equal(P[i], oT)
+
+
+def test_f_ransac_batch(ctx, oracle):
+    """Several match lists (padded to a common stride) in one launch, incl. a list too short to fit."""
+    import torch
+    sizes, iters, stride = (300, 5, 1200, 60), 128, 1200
+    lists = np.zeros((len(sizes), stride), MATCH_DTYPE)
+    samples = np.zeros((len(sizes), iters, 8), np.int32)
+    for l, n in enumerate(sizes):
+        _, _, _, ua, ub = scene.two_view_matches(n, seed=40 + l)
+        lists[l, :n] = _match_array(ua, ub)
+        samples[l] = np.random.default_rng(l).integers(0, n, (iters, 8))
+    dev = "cuda:0"
+    d_m = torch.from_numpy(lists.view(np.uint8).reshape(-1)).to(dev)
+    d_cnt = torch.tensor(sizes, dtype=torch.int32, device=dev)
+    d_s = torch.from_numpy(samples.reshape(-1)).to(dev)
+    d_F = torch.zeros(len(sizes) * 9, dtype=torch.float64, device=dev)
+    d_inl = torch.zeros(len(sizes), dtype=torch.int32, device=dev)
+    d_found = torch.full((len(sizes),), -1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    assert ctx.lib.yv_f_ransac_batch(ctx.handle, d_m.data_ptr(), stride, d_cnt.data_ptr(), len(sizes), d_s.data_ptr(),
+                                     iters * 8, iters, 0.1, d_F.data_ptr(), d_inl.data_ptr(), d_found.data_ptr(),
+                                     None) == 0
+    ctx.sync()
+    F, inl, found = d_F.cpu().numpy().reshape(-1, 3, 3), d_inl.cpu().numpy(), d_found.cpu().numpy()
+    for l, n in enumerate(sizes):
+        ofound, oF, oinl = oracle.f_ransac(lists[l, :n], samples[l], 0.1)
+        assert bool(found[l]) == ofound
+        if ofound:
+            assert inl[l] == oinl
+            np.testing.assert_array_equal(F[l], oF)

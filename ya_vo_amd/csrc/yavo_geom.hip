@@ -272,7 +272,6 @@ __global__ __launch_bounds__(kNT) void f_ransac_kernel(const yv_match* __restric
                                                        const int32_t* __restrict__ samples, int64_t sample_stride,
                                                        int iters, double thr, double* __restrict__ F_out,
                                                        int32_t* __restrict__ max_inliers, int32_t* __restrict__ found) {
-    __shared__ int32_t s_pts[kMaxKp * 4];
     __shared__ int s_best_cnt[kNT];
     __shared__ int s_best_h[kNT];
     const int list = blockIdx.x;
@@ -284,13 +283,10 @@ __global__ __launch_bounds__(kNT) void f_ransac_kernel(const yv_match* __restric
         return;
     }
     const yv_match* m = matches + (int64_t)list * list_stride;
-    for (int i = tid; i < n; i += kNT) {
-        s_pts[4 * i] = m[i].pt1.x;
-        s_pts[4 * i + 1] = m[i].pt1.y;
-        s_pts[4 * i + 2] = m[i].pt2.x;
-        s_pts[4 * i + 3] = m[i].pt2.y;
-    }
-    __syncthreads();
+    // all lanes read the same match at the same time: one broadcast load per field
+    auto px = [&](int i, int q) -> int {
+        return q == 0 ? m[i].pt1.x : q == 1 ? m[i].pt1.y : q == 2 ? m[i].pt2.x : m[i].pt2.y;
+    };
     const int32_t* smp = samples + (int64_t)list * sample_stride;
     int best_cnt = INT32_MIN, best_h = 0x7fffffff;
     double best_F[9];
@@ -300,14 +296,14 @@ __global__ __launch_bounds__(kNT) void f_ransac_kernel(const yv_match* __restric
         for (int j = 0; j < 8; ++j) {
             int idx = smp[8 * h + j];
             idx = idx < 0 ? 0 : (idx >= n ? n - 1 : idx);
-            for (int q = 0; q < 4; ++q) pts8[4 * j + q] = (double)s_pts[4 * idx + q];
+            for (int q = 0; q < 4; ++q) pts8[4 * j + q] = (double)px(idx, q);
         }
         double Fh[9];
         fundamental_8pt(pts8, Fh);
         int cnt = 0;
         for (int k = 0; k < n; ++k) {
-            const double e = epipolar_error(Fh, (double)s_pts[4 * k], (double)s_pts[4 * k + 1],
-                                            (double)s_pts[4 * k + 2], (double)s_pts[4 * k + 3]);
+            const double e = epipolar_error(Fh, (double)m[k].pt1.x, (double)m[k].pt1.y, (double)m[k].pt2.x,
+                                            (double)m[k].pt2.y);
             if (fabs(e) < thr) cnt++;
         }
         if (cnt > best_cnt) {  // h increases within a lane: the first best of this lane wins
@@ -765,22 +761,36 @@ __device__ __forceinline__ double huber_rho(double e2, double* rho1) {
     return 2 * sqrte * delta - dsqr;
 }
 
-// Tree sum of per-thread partials: p[t] += p[t + off], off = 128 .. 1 (the oracle's sum_mode 1).
-// red: [nv][kNT] in LDS; each thread has written its partials; returns the totals into out[0..nv).
-__device__ void tree_reduce(double* red, int nv, double* out) {
+// Tree sum of per-thread partials in the oracle's order (sum_mode 1): p[t] += p[t + off] for
+// off = 128, 64 (across waves, through LDS), then 32 .. 1 inside wave 0 (shuffles).  part[] holds this
+// thread's nv partials; totals land in out[0..nv) (LDS), visible after the trailing barrier.
+// red: >= nv * 128 doubles of LDS.
+template <int NV>
+__device__ void tree_reduce(double (&part)[NV], double* red, double* out) {
     const int tid = threadIdx.x;
     __syncthreads();
-    for (int off = kNT / 2; off > 0; off >>= 1) {
-        if (tid < off)
-            for (int v = 0; v < nv; ++v) red[v * kNT + tid] = red[v * kNT + tid] + red[v * kNT + tid + off];
-        __syncthreads();
+    if (tid >= 128)
+        for (int v = 0; v < NV; ++v) red[v * 128 + (tid - 128)] = part[v];
+    __syncthreads();
+    if (tid < 128)
+        for (int v = 0; v < NV; ++v) part[v] = part[v] + red[v * 128 + tid];
+    __syncthreads();
+    if (tid >= 64 && tid < 128)
+        for (int v = 0; v < NV; ++v) red[v * 128 + (tid - 64)] = part[v];
+    __syncthreads();
+    if (tid < 64) {
+        for (int v = 0; v < NV; ++v) {
+            double x = part[v] + red[v * 128 + tid];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) x = x + __shfl_down(x, off, 64);
+            if (tid == 0) out[v] = x;
+        }
     }
-    if (tid < nv) out[tid] = red[tid * kNT];
     __syncthreads();
 }
 
 struct LMShared {
-    double T[7], Tbak[7], K[9];
+    double T[7], Tbak[7], Tlast[7], K[9];
     double H[36], b[6], x[6], vals[32];
     double lambda, ni, currentChi, tempChi, rho;
     int flag;  // control broadcast from lane 0
@@ -792,10 +802,9 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
                                                       const double* __restrict__ uvall, const double* __restrict__ Kall,
                                                       double* __restrict__ poses, uint8_t* __restrict__ outlier_all,
                                                       int32_t* __restrict__ inliers) {
-    __shared__ double s_err[kMaxEdges * 2];
     __shared__ uint8_t s_level[kMaxEdges], s_out[kMaxEdges], s_robust[kMaxEdges];
     __shared__ int16_t s_active[kMaxEdges];
-    __shared__ double s_red[kLMVals * kNT];
+    __shared__ double s_red[kLMVals * 128];
     __shared__ LMShared S;
     __shared__ int s_tmp[40];
     const int prob = blockIdx.x;
@@ -811,8 +820,6 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
         s_level[i] = 0;
         s_out[i] = 0;
         s_robust[i] = 1;
-        s_err[2 * i] = 0;
-        s_err[2 * i + 1] = 0;
     }
     __syncthreads();
     double prior[7];
@@ -843,12 +850,11 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
                 double T[7], K[9];
                 for (int q = 0; q < 7; ++q) T[q] = S.T[q];
                 for (int q = 0; q < 9; ++q) K[q] = S.K[q];
+                if (tid < 7) S.Tlast[tid] = T[tid];  // errors of the active edges are now at T
                 for (int a = tid; a < na; a += kNT) {
                     const int i = s_active[a];
                     double e[2];
                     edge_error(T, K, X + 3 * i, uv + 2 * i, e);
-                    s_err[2 * i] = e[0];
-                    s_err[2 * i + 1] = e[1];
                     const double c2 = e[0] * e[0] + e[1] * e[1];
                     double w = 1.0;
                     double chi = c2;
@@ -869,8 +875,7 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
                         part[21 + r] = part[21 + r] + (-(s0 * e[0] + s1 * e[1]));
                     }
                 }
-                for (int v = 0; v < kLMVals; ++v) s_red[v * kNT + tid] = part[v];
-                tree_reduce(s_red, kLMVals, S.vals);
+                tree_reduce<kLMVals>(part, s_red, S.vals);
                 if (tid == 0) {
                     int v = 0;
                     for (int r = 0; r < 6; ++r)
@@ -908,19 +913,17 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
                     __syncthreads();
                     ok2 = S.flag;
                     for (int q = 0; q < 7; ++q) T[q] = S.T[q];
-                    double pc = 0.0;
+                    if (tid < 7) S.Tlast[tid] = T[tid];
+                    double pc[1] = {0.0};
                     for (int a = tid; a < na; a += kNT) {
                         const int i = s_active[a];
                         double e[2];
                         edge_error(T, K, X + 3 * i, uv + 2 * i, e);
-                        s_err[2 * i] = e[0];
-                        s_err[2 * i + 1] = e[1];
                         const double c2 = e[0] * e[0] + e[1] * e[1];
                         double w;
-                        pc = pc + (s_robust[i] ? huber_rho(c2, &w) : c2);
+                        pc[0] = pc[0] + (s_robust[i] ? huber_rho(c2, &w) : c2);
                     }
-                    s_red[tid] = pc;
-                    tree_reduce(s_red, 1, S.vals);
+                    tree_reduce<1>(pc, s_red, S.vals);
                     if (tid == 0) {
                         double tempChi = S.vals[0];
                         if (!ok2) tempChi = DBL_MAX;
@@ -963,14 +966,18 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
             }
         }
         __syncthreads();
-        // classify: outliers recomputed at the final estimate, others keep their last trial error
-        double T[7], K[9];
+        // classify: previous outliers are recomputed at the final estimate (e->computeError()); the
+        // active edges keep the error of the last computeActiveErrors, i.e. at the last TRIAL estimate
+        // Tlast (possibly a rejected one) -- recomputed here from Tlast, bit-identical to the stored value
+        double T[7], Tl[7], K[9];
         for (int q = 0; q < 7; ++q) T[q] = S.T[q];
+        for (int q = 0; q < 7; ++q) Tl[q] = S.Tlast[q];
         for (int q = 0; q < 9; ++q) K[q] = S.K[q];
         int cnt = 0;
         for (int i = tid; i < n; i += kNT) {
-            if (s_out[i]) edge_error(T, K, X + 3 * i, uv + 2 * i, &s_err[2 * i]);
-            const double c2 = s_err[2 * i] * s_err[2 * i] + s_err[2 * i + 1] * s_err[2 * i + 1];
+            double ee[2];
+            edge_error(s_out[i] ? T : Tl, K, X + 3 * i, uv + 2 * i, ee);
+            const double c2 = ee[0] * ee[0] + ee[1] * ee[1];
             if (c2 > chi2th) {
                 s_out[i] = 1;
                 s_level[i] = 1;
@@ -994,7 +1001,7 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
 __global__ __launch_bounds__(kNT) void pose_gn_kernel(const int32_t* __restrict__ offsets, const double* __restrict__ Xall,
                                                       const double* __restrict__ uvall, const double* __restrict__ Kall,
                                                       double* __restrict__ poses, int32_t* __restrict__ iters_out) {
-    __shared__ double s_red[kLMVals * kNT];
+    __shared__ double s_red[kLMVals * 128];
     __shared__ double s_vals[32];
     __shared__ double s_T[7];
     __shared__ int s_flag;
@@ -1037,8 +1044,7 @@ __global__ __launch_bounds__(kNT) void pose_gn_kernel(const int32_t* __restrict_
                 part[21 + r] = part[21 + r] + ((-J[r]) * ee0 + (-J[6 + r]) * ee1);
             }
         }
-        for (int v = 0; v < kLMVals; ++v) s_red[v * kNT + tid] = part[v];
-        tree_reduce(s_red, kLMVals, s_vals);
+        tree_reduce<kLMVals>(part, s_red, s_vals);
         if (tid == 0) {
             double H[36], b[6], dx[6];
             int v = 0;

@@ -50,7 +50,7 @@ def random_scene(n: int, seed: int = 0, noise_px: float = 0.0, outlier_frac: flo
     ys = rng.uniform(-0.25, 0.25, n) * z
     pc = np.stack([xs, ys, z], 1)
     R = quat_to_R(T_true[:4])
-    X = (R.T @ (pc - T_true[4:]).T).T
+    X = np.ascontiguousarray((R.T @ (pc - T_true[4:]).T).T)
     uv = project(T_true, X, K)
     if noise_px > 0:
         uv = uv + rng.normal(scale=noise_px, size=uv.shape)
