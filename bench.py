@@ -4,9 +4,10 @@
 A step = one pass of the hot path over one resident batch of B synthetic 1241x376 stereo frames per GPU:
 for every frame, FAST-12 + Harris + top-2000 and blur + BRIEF on the left and right images, Hamming
 matching L_{k-1} -> L_k (the reference's temporal matchFeatures, src/LoopHandler.cc:189,534) and L_k -> R_k
-(stereo), and removeOutliers(20) on both match lists.  `value` = stereo frames per second over all GPUs
-(max-over-ranks wall time).  One process per GPU; frames shard across ranks (weak scaling, no collective
-in the data path).
+(stereo), removeOutliers(20) on both match lists, then PnP: the kept stereo matches are triangulated
+(LoopHandler::triangulation) and the pose-only LM (LoopHandler::optimizePoseOnly) solves every frame's pose
+from the kept temporal matches.  `value` = stereo frames per second over all GPUs (max-over-ranks wall
+time).  One process per GPU; frames shard across ranks (weak scaling, no collective in the data path).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--frames B]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -24,6 +25,7 @@ sys.path.insert(0, ROOT)
 
 H, W = 376, 1241
 MAX_KP = 2000
+T_RIGHT = np.array([0, 0, 0, 1, 0, -0.54, 0], np.float64)  # stereo right camera, KITTI baseline 0.54 m
 METRIC = "frames/sec (detect+describe+match+PnP) on 1241×376 KITTI stereo; RMSE vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-op/s
@@ -59,8 +61,12 @@ def stage_bytes(counts, B):
         "brief": n_img * img + 80 * kp,
         # query + train descriptors read, 4-B match key written per query
         "match": 2 * 32 * nq + 4 * nq,
-        # keys + query records read, 100-B Matches written (all + filtered)
-        "finalize": (4 + 48) * nq + 100 * (nq + nf),
+        # keys + query records read, 100-B Matches written (all + filtered) + 8-B {dist, j} per query
+        "finalize": (4 + 48) * nq + 100 * (nq + nf) + 8 * nq,
+        # per temporal query: 2 x {dist, j}; per edge: 3 keypoint (x, y) reads, X + uv + query index written
+        "track_edges": 16 * counts["tq"] + (24 + 44) * counts["edges"],
+        # per edge: X + uv read, outlier flag written (the LM iterates on these; it is latency bound)
+        "track_pose": 41 * counts["edges"],
     }
 
 
@@ -75,46 +81,57 @@ def stage_valu_ops(counts, B):
     return {"detect": px * 78.0, "match": float(np.sum(kq * kt)) * 18.0}
 
 
-def cpu_baseline(kind, threads, offsets):
-    """Oracle (CPU restatement of the reference) on the GPU box's host cores, bounded sample."""
+def cpu_baseline(kind, threads, offsets, frames, gpu_poses):
+    """Oracle (CPU restatement of the reference) on the GPU box's host cores, bounded sample of the SAME
+    frames the GPU processed; the CPU poses are compared with the GPU's (pose RMSE vs the CPU path)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bind
-    from ya_vo_amd.synth import synth_stereo_batch
+    from track_chain import track_pose
+    from ya_vo_amd import scene
     orc = oracle_bind.Oracle()
 
-    def one_frame(imgs, prev_left_kp, mode):
+    def one_frame(k, prev_left_kp, mode):
         kps = []
-        for img in imgs:
+        for img in frames[2 * k:2 * k + 2]:
             rc, _, _ = orc.fast(img, MAX_KP, mode=mode)
             kps.append(orc.brief(img, rc, offsets))
-        for q, t in ((prev_left_kp, kps[0]), (kps[0], kps[1])):
-            orc.remove_outliers(orc.match(q, t), 20)
-        return kps[0]
+        # temporal + stereo Matches, removeOutliers, triangulation, pose LM (tests/track_chain.py)
+        return kps[0], track_pose(orc, prev_left_kp, kps[0], kps[1], scene.K_KITTI, T_RIGHT)[3]
 
-    res = {}
+    def left_kp(k):
+        return orc.brief(frames[2 * k], orc.fast(frames[2 * k], MAX_KP)[0], offsets)
+
+    res, cpu_poses = {}, {}
     if kind in ("both", "literal"):
-        imgs = synth_stereo_batch(4242, 2)
-        prev = orc.brief(imgs[0], orc.fast(imgs[0], MAX_KP)[0], offsets)
+        prev = left_kp(0)
         t0 = time.perf_counter()
-        one_frame(imgs[2:4], prev, 0)
+        _, cpu_poses[1] = one_frame(1, prev, 0)
         dt = time.perf_counter() - t0
         res["literal"] = {"value": 1.0 / dt, "unit": "frames/s", "cores": 1, "kind": "port",
-                          "sample": "1 synthetic 1241x376 stereo frame (detect+describe L,R; match L0->L1, "
-                                    "L1->R1; removeOutliers), ref-literal costs: per-pixel ring rebuild, three "
-                                    "whole-image products per corner (src/FastDetector.cc:249-251), bit-loop "
-                                    "popcount; single thread", "seconds": dt}
+                          "sample": "frame 1 of the benchmarked batch (detect+describe L,R; match L0->L1, "
+                                    "L1->R1; removeOutliers; triangulation; pose LM), ref-literal costs: "
+                                    "per-pixel ring rebuild, three whole-image products per corner "
+                                    "(src/FastDetector.cc:249-251), bit-loop popcount; single thread",
+                          "seconds": dt}
     if kind in ("both", "efficient"):
         from concurrent.futures import ThreadPoolExecutor
-        nfr = 2 * threads
-        imgs = synth_stereo_batch(4243, nfr + 1)
-        lefts = [orc.brief(imgs[2 * k], orc.fast(imgs[2 * k], MAX_KP)[0], offsets) for k in range(nfr)]
+        nfr = min(2 * threads, len(frames) // 2 - 1)
+        lefts = [left_kp(k) for k in range(nfr)]
         t0 = time.perf_counter()
         with ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL inside the oracle
-            list(ex.map(lambda k: one_frame(imgs[2 * k + 2:2 * k + 4], lefts[k], 1), range(nfr)))
+            out = list(ex.map(lambda k: one_frame(k + 1, lefts[k], 1), range(nfr)))
         dt = time.perf_counter() - t0
+        for k, (_, T) in enumerate(out):
+            cpu_poses[k + 1] = T
         res["efficient"] = {"value": nfr / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-                            "sample": f"{nfr} synthetic stereo frames, same outputs with local Harris sums "
-                                      f"and a precomputed ring, {threads} threads over frames", "seconds": dt}
+                            "sample": f"frames 1..{nfr} of the benchmarked batch, same outputs with local Harris "
+                                      f"sums and a precomputed ring, {threads} threads over frames", "seconds": dt}
+    ks = sorted(cpu_poses)
+    d = np.array([gpu_poses[k] - cpu_poses[k] for k in ks])
+    res["pose_check"] = {"frames": len(ks), "pose_rmse_vs_cpu_ref": float(np.sqrt(np.mean(d[:, 4:] ** 2))),
+                         "max_abs_diff": float(np.abs(d).max()),
+                         "bit_identical": bool(np.array_equal(np.array([gpu_poses[k] for k in ks]),
+                                                              np.array([cpu_poses[k] for k in ks])))}
     return res
 
 
@@ -144,14 +161,21 @@ def main():
     d_frames = torch.from_numpy(frames).to(dev)
     batch = yv.Batch(ctx, n_img, H, W, MAX_KP, n_img)
     carry = n_img
-    pairs = []
+    pairs, tracks = [], []
     for k in range(B):
         pairs.append((carry if k == 0 else 2 * (k - 1), 2 * k))  # temporal L_{k-1} -> L_k
         pairs.append((2 * k, 2 * k + 1))                          # stereo L_k -> R_k
+        tracks.append((2 * k + 1, 2 * k))                         # PnP of frame k-1 against frame k's map
     batch.set_pairs(pairs)
+    from ya_vo_amd import scene
+    batch.set_tracks(tracks, scene.K_KITTI, T_RIGHT)
+    identity = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
+    d_prior = torch.from_numpy(np.tile(identity, (B, 1))).to(dev)
+    d_pose = torch.zeros((B, 7), dtype=torch.float64, device=dev)
 
     def step():
         batch.run(d_frames.data_ptr(), n_img, W, H * W, 20, carry_from=2 * (B - 1))
+        batch.track(d_prior.data_ptr(), d_pose.data_ptr())
 
     for _ in range(args.warmup):
         step()
@@ -184,6 +208,10 @@ def main():
         "filt": ctx.download(v.filt_count, np.int32, len(pairs)).astype(np.int64),
     }
     counts["train"] = np.array([counts["kp"][t] for _, t in pairs], np.int64)
+    counts["edges"] = float(np.sum(ctx.download(v.edge_count, np.int32, B)))
+    counts["tq"] = float(np.sum([counts["match"][tp] for _, tp in tracks]))
+    inliers = ctx.download(v.track_inliers, np.int32, B)
+    gpu_poses = d_pose.cpu().numpy()
 
     stages = {}
     roofline = None
@@ -228,24 +256,27 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": "configs[1]: FAST+BRIEF+Hamming match, 1241x376 synthetic stereo, 2000 kp/image "
-                               "(no PnP stage: that is configs[2])",
+        "config": {"workload": "configs[1] + PnP: FAST+BRIEF+Hamming match, 1241x376 synthetic stereo, 2000 "
+                               "kp/image, stereo triangulation + pose-only LM per frame",
                    "H": H, "W": W, "max_kp": MAX_KP, "frames_per_step_per_gpu": B, "images_per_frame": 2,
                    "match_pairs_per_frame": 2, "parallelism": f"frame-sharded x{world}, no collective",
                    "mean_candidates_per_image": round(float(np.mean(counts["cand"][:n_img])), 1),
                    "mean_keypoints_per_image": round(float(np.mean(counts["kp"][:n_img])), 1),
-                   "mean_filtered_matches_per_pair": round(float(np.mean(counts["filt"])), 1)},
+                   "mean_filtered_matches_per_pair": round(float(np.mean(counts["filt"])), 1),
+                   "mean_pnp_edges_per_frame": round(counts["edges"] / B, 1),
+                   "mean_pnp_inliers_per_frame": round(float(np.mean(inliers)), 1)},
         "stages_ms_per_launch": stages,
         "roofline": roofline,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and args.cpu_baseline != "none":
-        cb = cpu_baseline(args.cpu_baseline, args.cpu_threads, offsets.reshape(256, 4))
+        cb = cpu_baseline(args.cpu_baseline, args.cpu_threads, offsets.reshape(256, 4), frames, gpu_poses)
         main_cb = cb.get("literal") or cb.get("efficient")
         out["cpu_baseline"] = main_cb
         if "efficient" in cb and main_cb is not cb["efficient"]:
             out["cpu_baseline_efficient"] = cb["efficient"]
         out["cpu_baseline_host_cpus"] = os.cpu_count()
+        out["pose_check"] = cb["pose_check"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     batch.close()

@@ -34,7 +34,7 @@ extern "C" {
 #define YV_ERR_NODEVICE (-3)  /* no usable GPU */
 #define YV_ERR_CAPACITY (-4)  /* request exceeds the batch / context capacity */
 
-#define YV_ABI_VERSION 1
+#define YV_ABI_VERSION 2
 
 typedef struct yv_ctx yv_ctx;
 typedef struct yv_batch yv_batch;
@@ -102,13 +102,27 @@ int yv_batch_set_pairs(yv_batch* b, const int32_t* pairs /* [2*n_pairs] */, int 
  * src/LoopHandler.cc:192,537). */
 int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride, int64_t image_pitch,
                  int match_thr, int carry_from, void* stream);
+/* Tracking (PnP) over the last run's matches: track t = {stereo_pair, temporal_pair} (pair indices of
+ * yv_batch_set_pairs) where the stereo pair's query image (frame k left) is the temporal pair's train
+ * image.  Each frame-(k-1) keypoint kept by removeOutliers in the temporal pair whose frame-k keypoint is
+ * itself kept in the stereo pair becomes one pose edge: X = LoopHandler::triangulation of the stereo match
+ * (src/LoopHandler.cc:867-885, left camera = world, right camera pose T_right; accepted iff success and
+ * Z > 0 as in triangulate2View :658-726), measurement = the frame-(k-1) keypoint (x, y).  The pose of
+ * frame k-1 in frame k's camera is then LoopHandler::optimizePoseOnly (:730-861) from the prior.  K and
+ * T_right are copied once; tracks are validated against the pairs (YV_ERR_INVALID otherwise). */
+int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks /* [2*n_tracks] */, int n_tracks, const double K[9],
+                        const double T_right[7]);
+/* Build the track edges and solve every track's pose in one launch each (asynchronous on `stream`, NULL =
+ * context stream).  d_priors [n_tracks][7] in, d_poses [n_tracks][7] out (may alias d_priors). */
+int yv_batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stream);
 /* Per-stage device time of the runs since the last reset, when timing is enabled (HIP events recorded
  * on the run stream around every stage).  Stages: 0 detect (FAST + Harris + blur, one fused kernel),
- * 1 top-K + checkBoundry, 2 BRIEF, 3 match, 4 Matches records + removeOutliers.  ms[i] = summed
- * milliseconds, *n_runs = runs accumulated. */
+ * 1 top-K + checkBoundry, 2 BRIEF, 3 match, 4 Matches records + removeOutliers (+ carry copies),
+ * 5 track edges (stereo triangulation), 6 track poses (LM).  ms[i] = summed milliseconds, *n_runs = runs
+ * accumulated (stages 5-6 summed over the runs followed by yv_batch_track). */
 int yv_batch_enable_timing(yv_batch* b, int on);
 int yv_batch_stage_times(yv_batch* b, float* ms /* [8] */, int* n_runs);
-#define YV_NUM_STAGES 5
+#define YV_NUM_STAGES 7
 
 /* Device views of the batch results (valid until the next run / destroy).  All arrays are indexed
  * [slot][...] with the per-slot strides given. */
@@ -126,6 +140,18 @@ typedef struct yv_batch_view {
     const yv_match* matches;          /* [max_pairs][max_kp] */
     const int32_t* filt_count;        /* [max_pairs] */
     const yv_match* filtered;         /* [max_pairs][max_kp] */
+    /* per-query {distance, train keypoint index (-1: empty train)} and the removeOutliers limit
+     * (kept iff distance < limit) of every pair */
+    const int32_t* match_dj;          /* [max_pairs][max_kp][2] */
+    const int32_t* match_lim;         /* [max_pairs] */
+    /* tracks (yv_batch_set_tracks / yv_batch_track) */
+    int n_tracks;
+    const int32_t* edge_count;        /* [n_tracks] */
+    const double* edge_X;             /* [n_tracks][max_kp][3] */
+    const double* edge_uv;            /* [n_tracks][max_kp][2] */
+    const int32_t* edge_query;        /* [n_tracks][max_kp]: temporal query keypoint index */
+    const uint8_t* edge_outlier;      /* [n_tracks][max_kp] */
+    const int32_t* track_inliers;     /* [n_tracks] */
 } yv_batch_view;
 int yv_batch_view_get(yv_batch* b, yv_batch_view* view);
 

@@ -42,7 +42,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_abi_version_and_status_strings(lib):
-    assert lib.yv_abi_version() == 1
+    assert lib.yv_abi_version() == 2
     assert lib.yv_status_string(0) == b"ok"
     assert lib.yv_status_string(-3) == b"no usable GPU"
 
@@ -62,6 +62,20 @@ def test_record_layout_matches_reference_classes(tmp_path):
     kd, md = yv.KEYPOINT_DTYPE, yv.MATCH_DTYPE
     assert (kd.itemsize, kd.fields["id"][1], kd.fields["matched"][1], kd.fields["featVec"][1]) == (48, 8, 12, 13)
     assert (md.itemsize, md.fields["pt2"][1], md.fields["distance"][1]) == (100, 48, 96)
+
+
+def test_batch_view_layout_matches_ctypes(tmp_path):
+    # the ctypes mirror of yv_batch_view must agree with the C compiler field by field
+    fields = [f for f, _ in yv._BatchView._fields_]
+    src = tmp_path / "probe_view.c"
+    body = " ".join(f'printf("%zu ", offsetof(yv_batch_view, {f}));' for f in fields)
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "yavo/yavo.h"\n'
+                   f'int main(void){{{body} printf("%zu\\n", sizeof(yv_batch_view)); return 0;}}\n')
+    exe = tmp_path / "probe_view"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    expect = [getattr(yv._BatchView, f).offset for f in fields] + [ctypes.sizeof(yv._BatchView)]
+    assert vals == expect
 
 
 def test_no_device_means_error_not_fallback(lib):

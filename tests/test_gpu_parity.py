@@ -226,7 +226,7 @@ def test_batch_is_deterministic_and_timed(ctx):
     np.testing.assert_array_equal(outs[0], outs[1])
     np.testing.assert_array_equal(outs[0], outs[2])
     ms, n = b.stage_times()
-    assert n == 3 and np.all(ms > 0)
+    assert n == 3 and np.all(ms[:5] > 0) and np.all(ms[5:] == 0)  # no tracks set: stages 5-6 idle
     b.close()
 
 

@@ -1,0 +1,90 @@
+"""GPU parity of the batch's track stage (yv_batch_set_tracks / yv_batch_track): stereo triangulation of
+the kept matches and the per-frame pose LM, bit for bit against the oracle chain in tests/track_chain.py,
+over two chained runs (the first track of each run reads the carry slot)."""
+import numpy as np
+import pytest
+
+import ya_vo_amd as yv
+from ya_vo_amd import scene
+from ya_vo_amd.synth import synth_frame
+
+from track_chain import IDENTITY, track_pose
+
+pytestmark = pytest.mark.gpu
+
+H, W = 376, 1241
+T_RIGHT = np.array([0, 0, 0, 1, 0, -0.54, 0], np.float64)  # right camera 0.54 m along the column axis
+
+
+def _setup(ctx, n_frames):
+    b = yv.Batch(ctx, 2 * n_frames, H, W, 2000, 2 * n_frames)
+    carry = 2 * n_frames
+    pairs, tracks = [], []
+    for k in range(n_frames):
+        pairs.append((carry if k == 0 else 2 * (k - 1), 2 * k))  # temporal L_{k-1} -> L_k
+        pairs.append((2 * k, 2 * k + 1))                          # stereo L_k -> R_k
+        tracks.append((2 * k + 1, 2 * k))
+    b.set_pairs(pairs)
+    b.set_tracks(tracks, scene.K_KITTI, T_RIGHT)
+    return b, carry
+
+
+def test_track_matches_oracle(ctx, oracle, offsets):
+    import torch
+    n_frames = 3
+    b, carry = _setup(ctx, n_frames)
+    seq = [(synth_frame(51, k, 3 * k), synth_frame(51, k, 3 * k + 8)) for k in range(2 * n_frames)]
+    d_prior = torch.from_numpy(np.tile(IDENTITY, (n_frames, 1))).to("cuda:0")
+    d_pose = torch.zeros((n_frames, 7), dtype=torch.float64, device="cuda:0")
+    kps = {}
+    prev_left = None
+    b.enable_timing(True)
+    for run in range(2):
+        frames = np.stack([im for k in range(run * n_frames, (run + 1) * n_frames) for im in seq[k]])
+        d = torch.from_numpy(frames).to("cuda:0")
+        torch.cuda.synchronize()
+        b.run(d.data_ptr(), len(frames), W, H * W, 20, carry_from=2 * (n_frames - 1))
+        b.track(d_prior.data_ptr(), d_pose.data_ptr())
+        ctx.sync()
+        v = b.view()
+        assert v.n_tracks == n_frames
+        for i, img in enumerate(frames):
+            kps[i] = oracle.brief(img, oracle.fast(img, 2000)[0], offsets)
+        cnt = ctx.download(v.edge_count, np.int32, n_frames)
+        inl = ctx.download(v.track_inliers, np.int32, n_frames)
+        P = d_pose.cpu().numpy()
+        for k in range(n_frames):
+            kq = (prev_left if prev_left is not None else kps[0][:0]) if k == 0 else kps[2 * (k - 1)]
+            X, uv, q, T, out, oinl = track_pose(oracle, kq, kps[2 * k], kps[2 * k + 1], scene.K_KITTI, T_RIGHT)
+            assert cnt[k] == len(X), (run, k)
+            base = k * 2000
+            gX = ctx.download(v.edge_X + base * 24, np.float64, 3 * cnt[k]).reshape(-1, 3)
+            guv = ctx.download(v.edge_uv + base * 16, np.float64, 2 * cnt[k]).reshape(-1, 2)
+            gq = ctx.download(v.edge_query + base * 4, np.int32, cnt[k])
+            gout = ctx.download(v.edge_outlier + base, np.uint8, cnt[k]).astype(bool)
+            np.testing.assert_array_equal(gq, q)
+            np.testing.assert_array_equal(gX, X)
+            np.testing.assert_array_equal(guv, uv)
+            assert inl[k] == oinl
+            np.testing.assert_array_equal(gout, out)
+            np.testing.assert_array_equal(P[k], T)
+            if len(X) >= 100:
+                # the synthetic motion: frame k-1 is frame k's content shifted by (+1 row, +3 cols); the
+                # stereo disparity is 8 px, so every point lies at Z = 0.54 fy / 8 and the pose of frame
+                # k-1 in frame k is the translation (Z / fx, 3 Z / fy, 0) = (0.0675, 0.2025, 0)
+                np.testing.assert_allclose(T[4:], [0.0675, 0.2025, 0.0], atol=2e-3)
+                np.testing.assert_allclose(np.abs(T[3]), 1.0, atol=1e-4)
+        prev_left = kps[2 * (n_frames - 1)]
+    ms, nruns = b.stage_times()
+    assert nruns == 2 and np.all(ms > 0)  # every stage, incl. track_edges / track_pose, was timed
+    b.close()
+
+
+def test_track_rejects_inconsistent_pairs(ctx):
+    b = yv.Batch(ctx, 4, H, W, 2000, 4)
+    b.set_pairs([(0, 1), (2, 3)])
+    with pytest.raises(yv.YavoError):
+        b.set_tracks([(0, 1)], scene.K_KITTI, T_RIGHT)  # stereo query 0 != temporal train 3
+    with pytest.raises(yv.YavoError):
+        b.set_tracks([(0, 5)], scene.K_KITTI, T_RIGHT)  # pair index out of range
+    b.close()

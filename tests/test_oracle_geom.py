@@ -209,3 +209,17 @@ def test_pose_gn(oracle, sum_mode):
     T, it = oracle.pose_gn(X, uv, K, prior, sum_mode)
     assert it >= 2
     np.testing.assert_allclose(scene.project(T, X), uv, atol=1e-5)
+
+
+def test_track_chain_recovers_synthetic_motion(oracle, offsets):
+    """The CPU track chain (tests/track_chain.py) on a synthetic stereo pair of frames recovers the known
+    motion: frame k-1 is frame k shifted by (+1 row, +3 cols), disparity 8 px at baseline 0.54 m."""
+    from ya_vo_amd.synth import synth_frame
+    from track_chain import track_pose
+    imgs = [synth_frame(77, 0, 0), synth_frame(77, 1, 3), synth_frame(77, 1, 11)]
+    kp = [oracle.brief(im, oracle.fast(im, 2000)[0], offsets) for im in imgs]
+    T_right = np.array([0, 0, 0, 1, 0, -0.54, 0], np.float64)
+    X, uv, q, T, out, inl = track_pose(oracle, kp[0], kp[1], kp[2], scene.K_KITTI, T_right)
+    assert len(X) > 500 and inl > 0.8 * len(X)
+    np.testing.assert_allclose(X[:, 2], 0.54 * scene.K_KITTI[1, 1] / 8, rtol=1e-6)
+    np.testing.assert_allclose(T[4:], [0.0675, 0.2025, 0.0], atol=2e-3)

@@ -1,0 +1,53 @@
+"""CPU restatement of the batch's track stage (yv_batch_track) composed from oracle rows -- test
+infrastructure, used by tests/test_gpu_track.py and bench.py's cpu_baseline leg as the checker.
+
+Track for frame k: temporal Matches L_{k-1} -> L_k and stereo Matches L_k -> R_k (Brief::matchFeatures +
+removeOutliers, src/BriefDescriptor.cc:163-231), stereo triangulation with the left camera as world
+(LoopHandler::triangulation + triangulate2View's Z > 0, src/LoopHandler.cc:658-726, 867-885), then
+LoopHandler::optimizePoseOnly (src/LoopHandler.cc:730-861) of frame k-1's pose in frame k's camera from
+the frame-(k-1) measurements.
+"""
+import numpy as np
+
+from ya_vo_amd import MATCH_DTYPE
+
+IDENTITY = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
+
+
+def kept_flags(orc, m, thr=20):
+    """removeOutliers as per-record keep flags (pt1.id is unique within the query image)."""
+    if len(m) == 0:
+        return np.zeros(0, bool)
+    kept_ids = set(orc.remove_outliers(m, thr)["pt1"]["id"].tolist())
+    return np.array([i in kept_ids for i in m["pt1"]["id"].tolist()], bool)
+
+
+def track_edges(orc, kq, kl, kr, K, T_right, thr=20):
+    """Edges of one track -> (X [n,3], uv [n,2], query index [n])."""
+    if len(kq) == 0:
+        return np.zeros((0, 3)), np.zeros((0, 2)), np.zeros(0, np.int32)
+    mt = orc.match(kq, kl)
+    ms = orc.match(kl, kr) if len(kl) else np.zeros(0, MATCH_DTYPE)
+    kt, ks = kept_flags(orc, mt, thr), kept_flags(orc, ms, thr)
+    l_index = {int(i): j for j, i in enumerate(kl["id"].tolist())}
+    cand, recs = [], []
+    for i in range(len(kq)):
+        if not kt[i] or len(kl) == 0:
+            continue
+        j = l_index[int(mt[i]["pt2"]["id"])]
+        if not ks[j]:
+            continue
+        cand.append(i)
+        recs.append(ms[j])
+    if not cand:
+        return np.zeros((0, 3)), np.zeros((0, 2)), np.zeros(0, np.int32)
+    _, X, ok = orc.triangulate_matches(IDENTITY, T_right, K, np.array(recs, MATCH_DTYPE))
+    q = np.array(cand, np.int32)[ok]
+    uv = np.stack([kq["x"][q], kq["y"][q]], 1).astype(np.float64)
+    return X[ok], uv, q
+
+
+def track_pose(orc, kq, kl, kr, K, T_right, prior=IDENTITY, thr=20, sum_mode=1):
+    X, uv, q = track_edges(orc, kq, kl, kr, K, T_right, thr)
+    T, out, inl = orc.pose_lm(X, uv, K, prior, sum_mode)
+    return X, uv, q, T, out, inl

@@ -6,8 +6,10 @@ ya_vo_amd/frontend.py).  There is no CPU fallback: if the library or a GPU is mi
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
+import weakref
 from typing import Optional, Tuple
 
 import numpy as np
@@ -20,8 +22,8 @@ YV_ERR_INVALID = -1
 YV_ERR_HIP = -2
 YV_ERR_NODEVICE = -3
 YV_ERR_CAPACITY = -4
-YV_NUM_STAGES = 5
-STAGE_NAMES = ("detect", "topk", "brief", "match", "finalize")
+YV_NUM_STAGES = 7
+STAGE_NAMES = ("detect", "topk", "brief", "match", "finalize", "track_edges", "track_pose")
 
 # byte-identical to KeyPoint (48 B) / Matches (100 B), /root/reference/include/BriefDescriptor.hpp:11-39
 KEYPOINT_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("id", "<i4"), ("matched", "u1"),
@@ -45,7 +47,11 @@ class _BatchView(ctypes.Structure):
                 ("cand_count", ctypes.c_void_p), ("det_count", ctypes.c_void_p), ("det_rc", ctypes.c_void_p),
                 ("det_resp", ctypes.c_void_p), ("kp_count", ctypes.c_void_p), ("keypoints", ctypes.c_void_p),
                 ("blurred", ctypes.c_void_p), ("match_count", ctypes.c_void_p), ("matches", ctypes.c_void_p),
-                ("filt_count", ctypes.c_void_p), ("filtered", ctypes.c_void_p)]
+                ("filt_count", ctypes.c_void_p), ("filtered", ctypes.c_void_p),
+                ("match_dj", ctypes.c_void_p), ("match_lim", ctypes.c_void_p), ("n_tracks", ctypes.c_int),
+                ("edge_count", ctypes.c_void_p), ("edge_X", ctypes.c_void_p), ("edge_uv", ctypes.c_void_p),
+                ("edge_query", ctypes.c_void_p), ("edge_outlier", ctypes.c_void_p),
+                ("track_inliers", ctypes.c_void_p)]
 
 
 _lib: Optional[ctypes.CDLL] = None
@@ -77,6 +83,8 @@ SIGNATURES = {
     "yv_batch_enable_timing": (_I, [_P, _I]),
     "yv_batch_stage_times": (_I, [_P, _P, ctypes.POINTER(_I)]),
     "yv_batch_view_get": (_I, [_P, ctypes.POINTER(_BatchView)]),
+    "yv_batch_set_tracks": (_I, [_P, _P, _I, _P, _P]),
+    "yv_batch_track": (_I, [_P, _P, _P, _P]),
 }
 
 
@@ -184,6 +192,19 @@ class _GeomMixin:
 
 
 
+_live_contexts: "weakref.WeakSet" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_all() -> None:
+    """Release every context (and its batches) before torch / the HIP runtime tear down."""
+    for c in list(_live_contexts):
+        try:
+            c.close()
+        except Exception:
+            pass
+
+
 class Context(_GeomMixin):
     """One yv_ctx: a GPU, a HIP stream and the algorithm constants."""
 
@@ -193,9 +214,13 @@ class Context(_GeomMixin):
         _check(self.lib.yv_create(device, ctypes.byref(h)), f"yv_create(device={device})")
         self.handle = h
         self.device = device
+        _live_contexts.add(self)
 
     def close(self) -> None:
         if self.handle:
+            # a yv_batch holds its context: destroy the batches first (never a batch after its context)
+            for b in list(getattr(self, "_batches", ())):
+                b.close()
             self.lib.yv_destroy(self.handle)
             self.handle = None
 
@@ -289,6 +314,9 @@ class Batch:
                "yv_batch_create")
         self.handle = h
         self.max_images, self.H, self.W, self.max_kp, self.max_pairs = max_images, H, W, max_kp, max_pairs
+        if not hasattr(ctx, "_batches"):
+            ctx._batches = weakref.WeakSet()
+        ctx._batches.add(self)
 
     def close(self) -> None:
         if self.handle:
@@ -310,6 +338,17 @@ class Batch:
             stream: int = 0) -> None:
         _check(self.lib.yv_batch_run(self.handle, ctypes.c_void_p(d_images), n_images, stride, pitch, match_thr,
                                      carry_from, ctypes.c_void_p(stream) if stream else None), "yv_batch_run")
+
+    def set_tracks(self, tracks, K, T_right) -> None:
+        """tracks [n][2] = (stereo pair index, temporal pair index); K 3x3; T_right the right camera pose."""
+        t = np.ascontiguousarray(np.asarray(tracks, dtype=np.int32).reshape(-1, 2))
+        _check(self.lib.yv_batch_set_tracks(self.handle, _ptr(t), len(t), _ptr(_f64(K, 9)), _ptr(_f64(T_right, 7))),
+               "yv_batch_set_tracks")
+        self.n_tracks = len(t)
+
+    def track(self, d_priors: int, d_poses: int, stream: int = 0) -> None:
+        _check(self.lib.yv_batch_track(self.handle, ctypes.c_void_p(d_priors), ctypes.c_void_p(d_poses),
+                                       ctypes.c_void_p(stream) if stream else None), "yv_batch_track")
 
     def enable_timing(self, on: bool = True) -> None:
         _check(self.lib.yv_batch_enable_timing(self.handle, 1 if on else 0), "yv_batch_enable_timing")

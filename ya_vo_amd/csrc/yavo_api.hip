@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -49,16 +50,33 @@ struct yv_batch {
     int32_t* match_count = nullptr;
     yv_match* filtered = nullptr;
     int32_t* filt_count = nullptr;
+    int2* match_dj = nullptr;       // [max_pairs][max_kp] {distance, train index}
+    int32_t* match_lim = nullptr;   // [max_pairs] removeOutliers limit
     uint8_t* staging = nullptr;  // one H x W input image (host-pointer API)
-    // stage timing
+    std::vector<int32_t> h_pairs;   // host copy of the pairs (track validation)
+    // tracks (PnP over the matches)
+    int n_tracks = 0, max_tracks = 0;
+    int32_t* tracks = nullptr;      // [max_tracks][2] {stereo pair, temporal pair}
+    double* track_K = nullptr;      // [max_tracks][9]
+    double* T_right = nullptr;      // [7]
+    double* edge_X = nullptr;       // [max_tracks][max_kp][3]
+    double* edge_uv = nullptr;      // [max_tracks][max_kp][2]
+    int32_t* edge_query = nullptr;  // [max_tracks][max_kp]
+    int32_t* edge_count = nullptr;  // [max_tracks]
+    uint8_t* edge_outlier = nullptr;
+    int32_t* track_inliers = nullptr;
+    // stage timing: events 0..5 bracket the run's stages, 6..8 the track's
     bool timing = false;
-    std::vector<hipEvent_t> events;  // (YV_NUM_STAGES + 1) per recorded run
+    std::vector<hipEvent_t> events;  // kEvPerRun per recorded run
+    std::vector<uint8_t> tracked;    // run r was followed by a timed yv_batch_track
     int runs_recorded = 0;
+    int last_run = -1;
+    int pending_carry = -1;  // image whose keypoints enter the carry slot at the start of the next run
 };
 
 namespace {
 
-constexpr int kEvPerRun = YV_NUM_STAGES + 1;
+constexpr int kEvPerRun = 9;
 constexpr int kMaxTimedRuns = 4096;
 
 #define YV_HIP(call)                                                                           \
@@ -80,6 +98,12 @@ int check_launch() {
     return YV_OK;
 }
 
+bool finite_pose(const double* p) {
+    for (int i = 0; i < 7; ++i)
+        if (!(p[i] == p[i])) return false;
+    return true;
+}
+
 template <class T>
 int dalloc(T** p, size_t count) {
     *p = nullptr;
@@ -96,7 +120,9 @@ void batch_free(yv_batch* b) {
     if (!b) return;
     void* ptrs[] = {b->cand_keys, b->cand_count, b->cand_seen, b->det_rc,   b->det_resp,    b->det_count, b->kp_src,
                     b->kp_count,  b->keypoints,  b->desc,     b->blur,        b->pairs,     b->match_key,
-                    b->matches,   b->match_count, b->filtered, b->filt_count, b->staging};
+                    b->matches,   b->match_count, b->filtered, b->filt_count, b->staging,  b->match_dj,
+                    b->match_lim, b->tracks,     b->track_K,  b->T_right,    b->edge_X,    b->edge_uv,
+                    b->edge_query, b->edge_count, b->edge_outlier, b->track_inliers};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : b->events) (void)hipEventDestroy(e);
@@ -286,6 +312,8 @@ int yv_batch_create(yv_ctx* ctx, int max_images, int H, int W, int max_kp, int m
     rc |= dalloc(&b->match_count, np);
     rc |= dalloc(&b->filtered, np * nk);
     rc |= dalloc(&b->filt_count, np);
+    rc |= dalloc(&b->match_dj, np * nk);
+    rc |= dalloc(&b->match_lim, np);
     rc |= dalloc(&b->staging, (size_t)H * W);
     if (rc != YV_OK) {
         batch_free(b);
@@ -300,6 +328,7 @@ int yv_batch_create(yv_ctx* ctx, int max_images, int H, int W, int max_kp, int m
               hipMemsetAsync(b->keypoints, 0, ns * nk * sizeof(yv_keypoint), s) == hipSuccess &&
               hipMemsetAsync(b->match_count, 0, np * sizeof(int32_t), s) == hipSuccess &&
               hipMemsetAsync(b->filt_count, 0, np * sizeof(int32_t), s) == hipSuccess &&
+              hipMemsetAsync(b->match_lim, 0, np * sizeof(int32_t), s) == hipSuccess &&
               hipStreamSynchronize(s) == hipSuccess;
     if (!ok) {
         batch_free(b);
@@ -326,7 +355,9 @@ int yv_batch_set_pairs(yv_batch* b, const int32_t* pairs, int n_pairs) {
                               b->ctx->stream));
         YV_HIP(hipStreamSynchronize(b->ctx->stream));
     }
+    b->h_pairs.assign(pairs, pairs + 2 * (size_t)n_pairs);
     b->n_pairs = n_pairs;
+    b->n_tracks = 0;  // tracks refer to pair indices: set them again
     return YV_OK;
 }
 
@@ -336,9 +367,12 @@ int yv_batch_enable_timing(yv_batch* b, int on) {
         if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
         b->events.resize((size_t)kMaxTimedRuns * kEvPerRun);
         for (auto& e : b->events) YV_HIP(hipEventCreate(&e));
+        b->tracked.assign(kMaxTimedRuns, 0);
     }
     b->timing = on != 0;
     b->runs_recorded = 0;
+    b->last_run = -1;
+    std::fill(b->tracked.begin(), b->tracked.end(), 0);
     return YV_OK;
 }
 
@@ -348,13 +382,21 @@ int yv_batch_stage_times(yv_batch* b, float* ms, int* n_runs) {
     const int runs = std::min(b->runs_recorded, kMaxTimedRuns);
     if (n_runs) *n_runs = runs;
     if (runs == 0) return YV_OK;
-    YV_HIP(hipEventSynchronize(b->events[(size_t)(runs - 1) * kEvPerRun + YV_NUM_STAGES]));
-    for (int r = 0; r < runs; ++r)
-        for (int st = 0; st < YV_NUM_STAGES; ++st) {
+    for (int r = 0; r < runs; ++r) {
+        const hipEvent_t* ev = &b->events[(size_t)r * kEvPerRun];
+        YV_HIP(hipEventSynchronize(ev[b->tracked[r] ? 8 : 5]));
+        for (int st = 0; st < 5; ++st) {
             float t = 0.f;
-            YV_HIP(hipEventElapsedTime(&t, b->events[(size_t)r * kEvPerRun + st], b->events[(size_t)r * kEvPerRun + st + 1]));
+            YV_HIP(hipEventElapsedTime(&t, ev[st], ev[st + 1]));
             ms[st] += t;
         }
+        if (b->tracked[r])
+            for (int st = 5; st < 7; ++st) {
+                float t = 0.f;
+                YV_HIP(hipEventElapsedTime(&t, ev[st + 1], ev[st + 2]));
+                ms[st] += t;
+            }
+    }
     return YV_OK;
 }
 
@@ -368,8 +410,17 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
     const int H = b->H, W = b->W, K = b->max_kp;
     const int keep = std::min(ctx->max_corners, K);
+    if (b->pending_carry >= 0) {
+        const size_t c = (size_t)b->pending_carry, dst = (size_t)b->max_images, nk = (size_t)K;
+        YV_HIP(hipMemcpyAsync(b->keypoints + dst * nk, b->keypoints + c * nk, nk * sizeof(yv_keypoint),
+                              hipMemcpyDeviceToDevice, s));
+        YV_HIP(hipMemcpyAsync(b->desc + dst * nk, b->desc + c * nk, nk * sizeof(Desc), hipMemcpyDeviceToDevice, s));
+        YV_HIP(hipMemcpyAsync(b->kp_count + dst, b->kp_count + c, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+        b->pending_carry = -1;
+    }
     int run = -1;
     if (b->timing && b->runs_recorded < kMaxTimedRuns) run = b->runs_recorded++;
+    b->last_run = run;
     int rc = YV_OK;
     rc |= record_stage(b, s, run, 0);
     yavo::launch_detect_blur(d_images, n_images, H, W, stride, image_pitch, ctx->fast_thr, b->cand_keys, b->cap,
@@ -384,19 +435,16 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
         yavo::launch_match(b->desc, b->kp_count, b->pairs, b->n_pairs, K, b->match_key, s);
         rc |= record_stage(b, s, run, 4);
         yavo::launch_match_finalize(b->match_key, b->keypoints, b->kp_count, b->pairs, b->n_pairs, K, match_thr,
-                                    b->matches, b->match_count, b->filtered, b->filt_count, s);
+                                    b->matches, b->match_count, b->filtered, b->filt_count, b->match_dj,
+                                    b->match_lim, s);
     } else {
         rc |= record_stage(b, s, run, 4);
     }
     rc |= record_stage(b, s, run, 5);
-    if (carry_from >= 0) {
-        const size_t c = (size_t)carry_from, dst = (size_t)b->max_images, nk = (size_t)K;
-        YV_HIP(hipMemcpyAsync(b->keypoints + dst * nk, b->keypoints + c * nk, nk * sizeof(yv_keypoint),
-                              hipMemcpyDeviceToDevice, s));
-        YV_HIP(hipMemcpyAsync(b->desc + dst * nk, b->desc + c * nk, nk * sizeof(Desc), hipMemcpyDeviceToDevice, s));
-        YV_HIP(hipMemcpyAsync(b->kp_count + dst, b->kp_count + c, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-    }
     if (rc != YV_OK) return YV_ERR_HIP;
+    // The carry slot keeps this run's frame k-1 (the query of its first temporal pair) until the next run
+    // starts, so yv_batch_track and the view still see it; the copy of image carry_from is deferred.
+    b->pending_carry = carry_from;
     return check_launch();
 }
 
@@ -419,7 +467,87 @@ int yv_batch_view_get(yv_batch* b, yv_batch_view* v) {
     v->matches = b->matches;
     v->filt_count = b->filt_count;
     v->filtered = b->filtered;
+    v->match_dj = reinterpret_cast<const int32_t*>(b->match_dj);
+    v->match_lim = b->match_lim;
+    v->n_tracks = b->n_tracks;
+    v->edge_count = b->edge_count;
+    v->edge_X = b->edge_X;
+    v->edge_uv = b->edge_uv;
+    v->edge_query = b->edge_query;
+    v->edge_outlier = b->edge_outlier;
+    v->track_inliers = b->track_inliers;
     return YV_OK;
+}
+
+int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks, int n_tracks, const double K[9], const double T_right[7]) {
+    if (!b || n_tracks < 0 || (n_tracks > 0 && (!tracks || !K || !T_right))) return YV_ERR_INVALID;
+    for (int t = 0; t < n_tracks; ++t) {
+        const int sp = tracks[2 * t], tp = tracks[2 * t + 1];
+        if (sp < 0 || sp >= b->n_pairs || tp < 0 || tp >= b->n_pairs) return YV_ERR_INVALID;
+        if (b->h_pairs[2 * sp] != b->h_pairs[2 * tp + 1]) return YV_ERR_INVALID;  // stereo query = temporal train
+    }
+    for (int i = 0; i < 9 && n_tracks > 0; ++i)
+        if (!std::isfinite(K[i])) return YV_ERR_INVALID;
+    if (n_tracks > 0 && !finite_pose(T_right)) return YV_ERR_INVALID;
+    if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = b->ctx->stream;
+    if (n_tracks > b->max_tracks) {
+        void* old[] = {b->tracks, b->track_K, b->T_right, b->edge_X, b->edge_uv, b->edge_query, b->edge_count,
+                       b->edge_outlier, b->track_inliers};
+        YV_HIP(hipStreamSynchronize(s));
+        for (void* p : old)
+            if (p) (void)hipFree(p);
+        b->tracks = nullptr; b->track_K = nullptr; b->T_right = nullptr; b->edge_X = nullptr; b->edge_uv = nullptr;
+        b->edge_query = nullptr; b->edge_count = nullptr; b->edge_outlier = nullptr; b->track_inliers = nullptr;
+        b->max_tracks = 0;
+        b->n_tracks = 0;
+        const size_t nt = (size_t)n_tracks, nk = (size_t)b->max_kp;
+        int rc = YV_OK;
+        rc |= dalloc(&b->tracks, 2 * nt);
+        rc |= dalloc(&b->track_K, 9 * nt);
+        rc |= dalloc(&b->T_right, 7);
+        rc |= dalloc(&b->edge_X, 3 * nt * nk);
+        rc |= dalloc(&b->edge_uv, 2 * nt * nk);
+        rc |= dalloc(&b->edge_query, nt * nk);
+        rc |= dalloc(&b->edge_count, nt);
+        rc |= dalloc(&b->edge_outlier, nt * nk);
+        rc |= dalloc(&b->track_inliers, nt);
+        if (rc != YV_OK) return YV_ERR_HIP;
+        b->max_tracks = n_tracks;
+    }
+    if (n_tracks > 0) {
+        std::vector<double> Ks(9 * (size_t)n_tracks);
+        for (int t = 0; t < n_tracks; ++t) std::memcpy(&Ks[9 * (size_t)t], K, 9 * sizeof(double));
+        YV_HIP(hipMemcpyAsync(b->tracks, tracks, 2 * sizeof(int32_t) * (size_t)n_tracks, hipMemcpyHostToDevice, s));
+        YV_HIP(hipMemcpyAsync(b->track_K, Ks.data(), Ks.size() * sizeof(double), hipMemcpyHostToDevice, s));
+        YV_HIP(hipMemcpyAsync(b->T_right, T_right, 7 * sizeof(double), hipMemcpyHostToDevice, s));
+        YV_HIP(hipMemsetAsync(b->edge_count, 0, sizeof(int32_t) * (size_t)n_tracks, s));
+        YV_HIP(hipStreamSynchronize(s));
+    }
+    b->n_tracks = n_tracks;
+    return YV_OK;
+}
+
+int yv_batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stream) {
+    if (!b || (b->n_tracks > 0 && (!d_priors || !d_poses))) return YV_ERR_INVALID;
+    if (b->n_tracks == 0) return YV_OK;
+    if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->ctx->stream;
+    const int run = b->last_run;
+    const bool timed = b->timing && run >= 0 && !b->tracked[run];
+    hipEvent_t* ev = timed ? &b->events[(size_t)run * kEvPerRun] : nullptr;
+    if (timed) YV_HIP(hipEventRecord(ev[6], s));
+    yavo::launch_track_build(b->tracks, b->n_tracks, b->pairs, b->keypoints, b->kp_count, b->match_dj, b->match_lim,
+                             b->max_kp, b->track_K, b->T_right, b->edge_X, b->edge_uv, b->edge_query, b->edge_count,
+                             s);
+    if (timed) YV_HIP(hipEventRecord(ev[7], s));
+    yavo::launch_track_pose(b->n_tracks, b->edge_count, b->max_kp, b->edge_X, b->edge_uv, b->track_K, d_priors,
+                            d_poses, b->edge_outlier, b->track_inliers, s);
+    if (timed) {
+        YV_HIP(hipEventRecord(ev[8], s));
+        b->tracked[run] = 1;
+    }
+    return check_launch();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -507,7 +635,7 @@ int yv_match_features(yv_ctx* ctx, const yv_keypoint* q, int nq, const yv_keypoi
     yavo::launch_pack_desc(b->keypoints, b->kp_count, 2, b->max_kp, b->desc, s);
     yavo::launch_match(b->desc, b->kp_count, b->pairs, 1, b->max_kp, b->match_key, s);
     yavo::launch_match_finalize(b->match_key, b->keypoints, b->kp_count, b->pairs, 1, b->max_kp, 0, b->matches,
-                                b->match_count, b->filtered, b->filt_count, s);
+                                b->match_count, b->filtered, b->filt_count, b->match_dj, b->match_lim, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
     YV_HIP(hipMemcpyAsync(out, b->matches, sizeof(yv_match) * (size_t)nq, hipMemcpyDeviceToHost, s));
     YV_HIP(hipStreamSynchronize(s));
@@ -575,11 +703,6 @@ struct Arena {
     }
 };
 
-bool finite_pose(const double* p) {
-    for (int i = 0; i < 7; ++i)
-        if (!(p[i] == p[i])) return false;
-    return true;
-}
 
 }  // namespace
 

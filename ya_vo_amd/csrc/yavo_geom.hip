@@ -581,46 +581,53 @@ __device__ bool eigen_jacobi_svd4(const double (&Ain)[16], double (&sv)[4], doub
     return true;
 }
 
+// LoopHandler::triangulation of one match (pixel2camera of both integer pixels, DLT rows, Eigen JacobiSVD);
+// returns success (s4/s3 < 1e-2) && Z > 0, the triangulate2View acceptance test (src/LoopHandler.cc:676)
+__device__ bool triangulate_px(int x1, int y1, int x2, int y2, const double* Ta, const double* Tb,
+                               const double* K, double* Xo) {
+    const double K0 = K[0], K2 = K[2], K4 = K[4], K5 = K[5];
+    const double pa[2] = {((double)x1 - K2) * 1.0 / K0, ((double)y1 - K5) * 1.0 / K4};
+    const double pb[2] = {((double)x2 - K2) * 1.0 / K0, ((double)y2 - K5) * 1.0 / K4};
+    double A[16];
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+        const double* T = v == 0 ? Ta : Tb;
+        const double* pp = v == 0 ? pa : pb;
+        double R[9];
+        quat_to_R(T, R);
+        double mm[12];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            mm[4 * r] = R[3 * r]; mm[4 * r + 1] = R[3 * r + 1]; mm[4 * r + 2] = R[3 * r + 2]; mm[4 * r + 3] = T[4 + r];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            A[(2 * v) + 4 * j] = pp[0] * mm[8 + j] - mm[j];
+            A[(2 * v + 1) + 4 * j] = pp[1] * mm[8 + j] - mm[4 + j];
+        }
+    }
+    double sv[4], V[16];
+    double X0 = NAN, X1 = NAN, X2 = NAN;
+    bool s = false;
+    if (eigen_jacobi_svd4(A, sv, V)) {
+        X0 = V[0 + 12] / V[3 + 12];
+        X1 = V[1 + 12] / V[3 + 12];
+        X2 = V[2 + 12] / V[3 + 12];
+        s = sv[3] / sv[2] < 1e-2;
+    }
+    Xo[0] = X0;
+    Xo[1] = X1;
+    Xo[2] = X2;
+    return s && X2 > 0;
+}
+
 __global__ void triangulate_kernel(const yv_match* __restrict__ m, int n, const double* __restrict__ poses /*[2][7]*/,
                                    const double* __restrict__ K, double* __restrict__ Xw, uint8_t* __restrict__ ok,
                                    int32_t* __restrict__ n_ok) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     bool good = false;
     if (i < n) {
-        const double K0 = K[0], K2 = K[2], K4 = K[4], K5 = K[5];
-        const double pa[2] = {((double)m[i].pt1.x - K2) * 1.0 / K0, ((double)m[i].pt1.y - K5) * 1.0 / K4};
-        const double pb[2] = {((double)m[i].pt2.x - K2) * 1.0 / K0, ((double)m[i].pt2.y - K5) * 1.0 / K4};
-        double A[16];
-#pragma unroll
-        for (int v = 0; v < 2; ++v) {
-            const double* T = poses + 7 * v;
-            const double* pp = v == 0 ? pa : pb;
-            double R[9];
-            quat_to_R(T, R);
-            double mm[12];
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                mm[4 * r] = R[3 * r]; mm[4 * r + 1] = R[3 * r + 1]; mm[4 * r + 2] = R[3 * r + 2]; mm[4 * r + 3] = T[4 + r];
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                A[(2 * v) + 4 * j] = pp[0] * mm[8 + j] - mm[j];
-                A[(2 * v + 1) + 4 * j] = pp[1] * mm[8 + j] - mm[4 + j];
-            }
-        }
-        double sv[4], V[16];
-        double X0 = NAN, X1 = NAN, X2 = NAN;
-        bool s = false;
-        if (eigen_jacobi_svd4(A, sv, V)) {
-            X0 = V[0 + 12] / V[3 + 12];
-            X1 = V[1 + 12] / V[3 + 12];
-            X2 = V[2 + 12] / V[3 + 12];
-            s = sv[3] / sv[2] < 1e-2;
-        }
-        Xw[3 * i] = X0;
-        Xw[3 * i + 1] = X1;
-        Xw[3 * i + 2] = X2;
-        good = s && X2 > 0;
+        good = triangulate_px(m[i].pt1.x, m[i].pt1.y, m[i].pt2.x, m[i].pt2.y, poses, poses + 7, K, Xw + 3 * i);
         ok[i] = good ? 1 : 0;
     }
     const uint64_t bal = __ballot(good);
@@ -798,10 +805,14 @@ struct LMShared {
 
 constexpr int kLMVals = 28;  // 21 lower-triangle H entries + 6 b + 1 chi2
 
-__global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict__ offsets, const double* __restrict__ Xall,
+// Problem p owns edges [offsets[p], offsets[p+1]) (CSR) or, with counts != nullptr, [p*stride, p*stride +
+// counts[p]) (the batch's fixed-stride track layout).  The prior is read from priors[p] and the estimate
+// written to poses[p] (the two may alias).
+__global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
+                                                      int stride, const double* __restrict__ Xall,
                                                       const double* __restrict__ uvall, const double* __restrict__ Kall,
-                                                      double* __restrict__ poses, uint8_t* __restrict__ outlier_all,
-                                                      int32_t* __restrict__ inliers) {
+                                                      const double* priors, double* poses,
+                                                      uint8_t* __restrict__ outlier_all, int32_t* __restrict__ inliers) {
     __shared__ uint8_t s_level[kMaxEdges], s_out[kMaxEdges], s_robust[kMaxEdges];
     __shared__ int16_t s_active[kMaxEdges];
     __shared__ double s_red[kLMVals * 128];
@@ -809,13 +820,13 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
     __shared__ int s_tmp[40];
     const int prob = blockIdx.x;
     const int tid = threadIdx.x;
-    const int e0 = offsets[prob];
-    int n = offsets[prob + 1] - e0;
+    const int64_t e0 = counts ? (int64_t)prob * stride : (int64_t)offsets[prob];
+    int n = counts ? counts[prob] : (int)(offsets[prob + 1] - e0);
     if (n > kMaxEdges) n = kMaxEdges;
-    const double* X = Xall + 3 * (int64_t)e0;
-    const double* uv = uvall + 2 * (int64_t)e0;
+    const double* X = Xall + 3 * e0;
+    const double* uv = uvall + 2 * e0;
     if (tid < 9) S.K[tid] = Kall[9 * prob + tid];
-    if (tid < 7) S.T[tid] = poses[7 * prob + tid];
+    if (tid < 7) S.T[tid] = priors[7 * prob + tid];
     for (int i = tid; i < n; i += kNT) {
         s_level[i] = 0;
         s_out[i] = 0;
@@ -998,6 +1009,69 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
     if (tid == 0) inliers[prob] = n - outlierCount;
 }
 
+// Track edges of the batched frontend: track t = {stereo pair sp, temporal pair tp} with
+// pairs[sp].query == pairs[tp].train (frame k's left image).  For temporal query i (frame k-1 keypoint)
+// kept by removeOutliers with best train keypoint j of frame k, and j's stereo match kept with right-image
+// keypoint r: X = triangulate(kp_k[j], kp_right[r]) with the left camera as world (pose identity) and the
+// right camera at T_right; accepted iff triangulation succeeds and Z > 0 (triangulate2View,
+// src/LoopHandler.cc:658-726).  uv = (kp_{k-1}[i].x, kp_{k-1}[i].y) (the reference's measurement,
+// src/LoopHandler.cc:786).  Edges keep temporal query order.  One workgroup per track.
+__global__ __launch_bounds__(kNT) void track_build_kernel(
+    const int32_t* __restrict__ tracks, const int32_t* __restrict__ pairs, const yv_keypoint* __restrict__ keypoints,
+    const int32_t* __restrict__ kp_count, const int2* __restrict__ match_dj, const int32_t* __restrict__ match_lim,
+    int max_kp, const double* __restrict__ Kall, const double* __restrict__ T_right, double* __restrict__ edge_X,
+    double* __restrict__ edge_uv, int32_t* __restrict__ edge_query, int32_t* __restrict__ edge_count) {
+    __shared__ int s_tmp[40];
+    __shared__ double s_K[9], s_Ta[7], s_Tb[7];
+    const int t = blockIdx.x, tid = threadIdx.x;
+    const int sp = tracks[2 * t], tp = tracks[2 * t + 1];
+    const int qs = pairs[2 * sp], rs = pairs[2 * sp + 1];  // frame k left, frame k right
+    const int qt = pairs[2 * tp];                          // frame k-1 left
+    if (tid < 9) s_K[tid] = Kall[9 * t + tid];
+    if (tid < 7) {
+        s_Ta[tid] = tid == 3 ? 1.0 : 0.0;
+        s_Tb[tid] = T_right[tid];
+    }
+    __syncthreads();
+    const int nq = kp_count[qt];
+    const int lim_t = match_lim[tp], lim_s = match_lim[sp];
+    const int2* dj_t = match_dj + (int64_t)tp * max_kp;
+    const int2* dj_s = match_dj + (int64_t)sp * max_kp;
+    const yv_keypoint* kq = keypoints + (int64_t)qt * max_kp;
+    const yv_keypoint* kl = keypoints + (int64_t)qs * max_kp;
+    const yv_keypoint* kr = keypoints + (int64_t)rs * max_kp;
+    double* Xo = edge_X + 3 * (int64_t)t * max_kp;
+    double* uvo = edge_uv + 2 * (int64_t)t * max_kp;
+    int32_t* qo = edge_query + (int64_t)t * max_kp;
+    int ne = 0;
+    for (int base = 0; base < nq; base += kNT) {
+        const int i = base + tid;
+        bool good = false;
+        double X[3];
+        if (i < nq) {
+            const int2 a = dj_t[i];
+            if (a.x < lim_t && a.y >= 0) {
+                const int2 b = dj_s[a.y];
+                if (b.x < lim_s && b.y >= 0)
+                    good = triangulate_px(kl[a.y].x, kl[a.y].y, kr[b.y].x, kr[b.y].y, s_Ta, s_Tb, s_K, X);
+            }
+        }
+        int tot = 0;
+        const int off = block_excl_scan_geom(good ? 1 : 0, s_tmp, &tot);
+        if (good) {
+            const int e = ne + off;
+            Xo[3 * e] = X[0];
+            Xo[3 * e + 1] = X[1];
+            Xo[3 * e + 2] = X[2];
+            uvo[2 * e] = (double)kq[i].x;
+            uvo[2 * e + 1] = (double)kq[i].y;
+            qo[e] = i;
+        }
+        ne += tot;
+    }
+    if (tid == 0) edge_count[t] = ne;
+}
+
 __global__ __launch_bounds__(kNT) void pose_gn_kernel(const int32_t* __restrict__ offsets, const double* __restrict__ Xall,
                                                       const double* __restrict__ uvall, const double* __restrict__ Kall,
                                                       double* __restrict__ poses, int32_t* __restrict__ iters_out) {
@@ -1108,8 +1182,27 @@ void launch_world2camera(const double* X, int n, const double* T, const double* 
 
 void launch_pose_lm(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
                     double* poses, uint8_t* outlier, int32_t* inliers, hipStream_t s) {
-    hipLaunchKernelGGL(geom::pose_lm_kernel, dim3(n_problems), dim3(geom::kNT), 0, s, offsets, X, uv, K, poses,
+    hipLaunchKernelGGL(geom::pose_lm_kernel, dim3(n_problems), dim3(geom::kNT), 0, s, offsets,
+                       static_cast<const int32_t*>(nullptr), 0, X, uv, K, static_cast<const double*>(poses), poses,
                        outlier, inliers);
+}
+
+void launch_track_build(const int32_t* tracks, int n_tracks, const int32_t* pairs, const yv_keypoint* keypoints,
+                        const int32_t* kp_count, const int2* match_dj, const int32_t* match_lim, int max_kp,
+                        const double* K, const double* T_right, double* edge_X, double* edge_uv, int32_t* edge_query,
+                        int32_t* edge_count, hipStream_t s) {
+    if (n_tracks <= 0) return;
+    hipLaunchKernelGGL(geom::track_build_kernel, dim3(n_tracks), dim3(geom::kNT), 0, s, tracks, pairs, keypoints,
+                       kp_count, match_dj, match_lim, max_kp, K, T_right, edge_X, edge_uv, edge_query, edge_count);
+}
+
+void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, const double* edge_X,
+                       const double* edge_uv, const double* K, const double* priors, double* poses,
+                       uint8_t* edge_outlier, int32_t* inliers, hipStream_t s) {
+    if (n_tracks <= 0) return;
+    hipLaunchKernelGGL(geom::pose_lm_kernel, dim3(n_tracks), dim3(geom::kNT), 0, s,
+                       static_cast<const int32_t*>(nullptr), edge_count, stride, edge_X, edge_uv, K, priors, poses,
+                       edge_outlier, inliers);
 }
 
 void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,

@@ -50,7 +50,7 @@ void launch_match(const Desc* desc, const int32_t* kp_count, const int32_t* pair
 void launch_match_finalize(uint32_t* match_key, const yv_keypoint* keypoints,
                            const int32_t* kp_count, const int32_t* pairs, int n_pairs, int max_kp,
                            int thr, yv_match* matches, int32_t* match_count, yv_match* filtered,
-                           int32_t* filt_count, hipStream_t s);
+                           int32_t* filt_count, int2* match_dj, int32_t* match_lim, hipStream_t s);
 // removeOutliers on externally supplied Matches records (one list).
 void launch_filter_records(const yv_match* in, int n, int thr, yv_match* out, int32_t* out_count,
                            hipStream_t s);
@@ -66,5 +66,12 @@ void launch_pose_lm(const int32_t* offsets, int n_problems, const double* X, con
                     double* poses, uint8_t* outlier, int32_t* inliers, hipStream_t s);
 void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
                     double* poses, int32_t* iters, hipStream_t s);
+void launch_track_build(const int32_t* tracks, int n_tracks, const int32_t* pairs, const yv_keypoint* keypoints,
+                        const int32_t* kp_count, const int2* match_dj, const int32_t* match_lim, int max_kp,
+                        const double* K, const double* T_right, double* edge_X, double* edge_uv, int32_t* edge_query,
+                        int32_t* edge_count, hipStream_t s);
+void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, const double* edge_X,
+                       const double* edge_uv, const double* K, const double* priors, double* poses,
+                       uint8_t* edge_outlier, int32_t* inliers, hipStream_t s);
 
 }  // namespace yavo

@@ -755,7 +755,7 @@ __global__ __launch_bounds__(FZ_NT) void match_finalize_kernel(
     uint32_t* __restrict__ match_key, const yv_keypoint* __restrict__ keypoints,
     const int32_t* __restrict__ kp_count, const int32_t* __restrict__ pairs, int max_kp, int thr,
     yv_match* __restrict__ matches, int32_t* __restrict__ match_count, yv_match* __restrict__ filtered,
-    int32_t* __restrict__ filt_count) {
+    int32_t* __restrict__ filt_count, int2* __restrict__ match_dj, int32_t* __restrict__ match_lim) {
     __shared__ int s_dist[kMaxKp];
     __shared__ int s_j[kMaxKp];
     __shared__ int s_pos[kMaxKp];
@@ -777,11 +777,13 @@ __global__ __launch_bounds__(FZ_NT) void match_finalize_kernel(
     const int min_d = block_min_int(local_min, s_tmp);
     const int lim = outlier_limit(min_d, thr);
     int flags[4], cnt = 0;
+    int2* dj = match_dj + (int64_t)pair * max_kp;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int i = tid * 4 + u;
         flags[u] = (i < nq && s_dist[i] < lim) ? 1 : 0;
         cnt += flags[u];
+        if (i < nq) dj[i] = make_int2(s_dist[i], s_j[i]);
     }
     int total = 0;
     int off = block_excl_scan<FZ_NT>(cnt, s_tmp, &total);
@@ -825,14 +827,16 @@ __global__ __launch_bounds__(FZ_NT) void match_finalize_kernel(
     if (tid == 0) {
         match_count[pair] = nq;
         filt_count[pair] = total;
+        match_lim[pair] = lim;
     }
 }
 
 void launch_match_finalize(uint32_t* match_key, const yv_keypoint* keypoints, const int32_t* kp_count,
                            const int32_t* pairs, int n_pairs, int max_kp, int thr, yv_match* matches,
-                           int32_t* match_count, yv_match* filtered, int32_t* filt_count, hipStream_t s) {
+                           int32_t* match_count, yv_match* filtered, int32_t* filt_count, int2* match_dj,
+                           int32_t* match_lim, hipStream_t s) {
     hipLaunchKernelGGL(match_finalize_kernel, dim3(n_pairs), dim3(FZ_NT), 0, s, match_key, keypoints, kp_count,
-                       pairs, max_kp, thr, matches, match_count, filtered, filt_count);
+                       pairs, max_kp, thr, matches, match_count, filtered, filt_count, match_dj, match_lim);
 }
 
 // removeOutliers over a caller-supplied Matches list (n <= kMaxKp), one workgroup.
