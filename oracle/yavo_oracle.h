@@ -107,10 +107,12 @@ void or_world2camera(const double* X, int n, const double* T, const double* K, d
 /* Eigen LDLT solve of a 6x6 (variant 0: MatrixXd / g2o, 1: Matrix6d / test.cc). Returns isPositive. */
 int or_ldlt6_solve(const double* H, const double* b, double* x, int variant);
 /* LoopHandler::optimizePoseOnly (src/LoopHandler.cc:730-861); returns inliers.  sum_mode 0 = sequential
- * edge sums (reference), 1 = the GPU's fixed tree order. */
+ * edge sums (reference), m >= 1 = the GPU's fixed tree order over 128 << m threads (the LM kernel: 2). */
 int or_pose_lm(const double* X, const double* uv, int n, const double* K, double* pose, uint8_t* outlier,
                int sum_mode);
-/* bundleAdjustmentGaussNewton (src/test.cc:172-244); returns accepted iterations. */
+/* bundleAdjustmentGaussNewton (src/test.cc:172-244); returns accepted iterations (GPU order: sum_mode 1). */
+/* Pose-LM diagnostics: {builds, trials, accepted trials} since the last reset. */
+void or_lm_stats(long* out, int reset);
 int or_pose_gn(const double* X, const double* uv, int n, const double* K, double* pose, int sum_mode);
 
 #ifdef __cplusplus

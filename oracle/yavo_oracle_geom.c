@@ -17,8 +17,9 @@
  *   Gauss-Newton              src/test.cc:172-244
  *
  * Sums over edges (chi2, H, b) are done either sequentially in edge order (the reference) or in the fixed
- * tree order of the GPU kernel (sum_mode 1: per-thread strided partial sums over 256 threads, then a
- * halving tree), so GPU parity can be tested bit-for-bit and the two orders compared within tolerance.
+ * tree order of the GPU kernels (sum_mode m >= 1: per-thread strided partial sums over 128 << m threads --
+ * 512 for the pose LM (mode 2), 256 for GN (mode 1) -- then a halving tree), so GPU parity can be tested
+ * bit-for-bit and the two orders compared within tolerance.
  * sin / cos in SO3::exp use one fixed polynomial kernel (fdlibm's, |x| <= pi/4) on both sides; the
  * reference's std::sin / std::cos may differ by 1 ulp (unpinned).
  */
@@ -722,21 +723,28 @@ static void edge_jacobian(const double* T, const double* K, const double* X, dou
     J[10] = -fy * x * y * zinv2; J[11] = -fy * x * zinv;
 }
 
-/* ---- summation orders ---- */
-#define OR_NT 256
-typedef struct { int mode; double part[OR_NT]; } or_sum;
+/* ---- summation orders ----
+ * mode 0: sequential in edge order (the reference).  mode m >= 1: the GPU kernels' order over NT = 128 << m
+ * threads (1: 256 threads, 2: 512): edge k adds into thread k % NT's partial, then the pairwise tree
+ * p[t] += p[t + off] for off = NT/2 .. 1. */
+#define OR_NT_MAX 1024
+typedef struct { int mode, nt; double part[OR_NT_MAX]; } or_sum;
 
-static void sum_reset(or_sum* s, int mode) { s->mode = mode; memset(s->part, 0, sizeof s->part); }
+static void sum_reset(or_sum* s, int mode) {
+    s->mode = mode;
+    s->nt = mode >= 1 ? 128 << mode : 1;
+    memset(s->part, 0, sizeof(double) * (size_t)s->nt);
+}
 /* term of edge index k (in the active-edge order) */
 static void sum_add(or_sum* s, int k, double v) {
     if (s->mode == 0) s->part[0] = s->part[0] + v;
-    else s->part[k % OR_NT] = s->part[k % OR_NT] + v;
+    else s->part[k % s->nt] = s->part[k % s->nt] + v;
 }
 static double sum_total(or_sum* s) {
     if (s->mode == 0) return s->part[0];
-    double p[OR_NT];
-    memcpy(p, s->part, sizeof p);
-    for (int off = OR_NT / 2; off > 0; off >>= 1)
+    double p[OR_NT_MAX];
+    memcpy(p, s->part, sizeof(double) * (size_t)s->nt);
+    for (int off = s->nt / 2; off > 0; off >>= 1)
         for (int t = 0; t < off; ++t) p[t] = p[t] + p[t + off];
     return p[0];
 }
@@ -819,6 +827,15 @@ static void build_system(lm_problem* P, const double* T, double* H, double* b) {
     free(sH);
 }
 
+/* pass statistics (diagnostics for the kernel design: builds / trials / accepted trials) */
+static long g_lm_stats[3];
+void or_lm_stats(long* out, int reset) {
+    for (int i = 0; i < 3; ++i) {
+        out[i] = g_lm_stats[i];
+        if (reset) g_lm_stats[i] = 0;
+    }
+}
+
 /* SparseOptimizer::optimize(iterations) with OptimizationAlgorithmLevenberg::solve per iteration.
  * Returns the number of iterations run (-1 when there is no active edge). */
 static int lm_optimize(lm_problem* P, double* T, int iterations) {
@@ -831,6 +848,7 @@ static int lm_optimize(lm_problem* P, double* T, int iterations) {
         double currentChi = active_robust_chi2(P);
         double H[36], b[6];
         build_system(P, T, H, b);
+        g_lm_stats[0]++;
         if (it == 0) {
             double maxDiag = 0;
             for (int j = 0; j < 6; ++j) maxDiag = fabs(H[j * 7]) > maxDiag ? fabs(H[j * 7]) : maxDiag;
@@ -863,7 +881,9 @@ static int lm_optimize(lm_problem* P, double* T, int iterations) {
                 scale = sc + 1e-3;
             }
             rho /= scale;
+            g_lm_stats[1]++;
             if (rho > 0 && isfinite(tempChi) && ok2) {
+                g_lm_stats[2]++;
                 double t = 2 * rho - 1;
                 double alpha = 1. - t * t * t;
                 alpha = alpha < goodUpper ? alpha : goodUpper;

@@ -11,6 +11,8 @@ from ya_vo_amd import MATCH_DTYPE, scene
 pytestmark = pytest.mark.gpu
 
 POSE_TOL = 1e-9  # |pose_gpu - pose_reference_order| (quaternion + translation), stated in DESIGN.md
+LM_ORDER = 2     # the pose-LM kernel's edge-sum order: 512-thread tree (oracle sum_mode 2)
+GN_ORDER = 1     # the GN kernel's: 256-thread tree
 
 
 def _match_array(ua, ub):
@@ -67,7 +69,7 @@ def test_pose_lm_matches_oracle(ctx, oracle, n, noise, outl, seed):
     X, uv = X[:n], uv[:n]
     prior = scene.perturb(T_true, np.random.default_rng(seed))
     T, out, inl = ctx.pose_lm(X, uv, scene.K_KITTI, prior)
-    oT, oout, oinl = oracle.pose_lm(X, uv, scene.K_KITTI, prior, 1)
+    oT, oout, oinl = oracle.pose_lm(X, uv, scene.K_KITTI, prior, LM_ORDER)
     assert inl == oinl
     np.testing.assert_array_equal(out, oout)
     np.testing.assert_array_equal(T, oT)
@@ -81,7 +83,7 @@ def test_pose_gn_matches_oracle(ctx, oracle, n, seed):
     X, uv, T_true, _ = scene.random_scene(n, seed=seed, noise_px=0.3)
     prior = scene.perturb(T_true, np.random.default_rng(seed), rot=0.01, trans=0.05)
     T, it = ctx.pose_gn(X, uv, scene.K_KITTI, prior)
-    oT, oit = oracle.pose_gn(X, uv, scene.K_KITTI, prior, 1)
+    oT, oit = oracle.pose_gn(X, uv, scene.K_KITTI, prior, GN_ORDER)
     assert it == oit
     np.testing.assert_array_equal(T, oT)
     rT, rit = oracle.pose_gn(X, uv, scene.K_KITTI, prior, 0)
@@ -115,7 +117,7 @@ def test_pose_lm_batch(ctx, oracle):
     out = d_out.cpu().numpy().astype(bool)
     inl = d_inl.cpu().numpy()
     for i, p in enumerate(probs):
-        oT, oout, oinl = oracle.pose_lm(p[0], p[1], scene.K_KITTI, priors[i], 1)
+        oT, oout, oinl = oracle.pose_lm(p[0], p[1], scene.K_KITTI, priors[i], LM_ORDER)
         assert inl[i] == oinl
         np.testing.assert_array_equal(P[i], oT)
         np.testing.assert_array_equal(out[offs[i]:offs[i + 1]], oout)
@@ -139,7 +141,7 @@ def test_pose_gn_batch(ctx, oracle):
     ctx.sync()
     P, it = d_P.cpu().numpy(), d_it.cpu().numpy()
     for i, p in enumerate(probs):
-        oT, oit = oracle.pose_gn(p[0], p[1], scene.K_KITTI, priors[i], 1)
+        oT, oit = oracle.pose_gn(p[0], p[1], scene.K_KITTI, priors[i], GN_ORDER)
         assert it[i] == oit
         np.testing.assert_array_equal(P[i], oT)
 

@@ -25,9 +25,23 @@ namespace yavo {
 namespace geom {
 
 constexpr int kNT = 256;          // threads per workgroup of the reduction kernels
+constexpr int kLMNT = 512;        // threads per pose-LM workgroup: 2 waves per SIMD hide the FP64 latency
+
+// YAVO_LM_PROFILE builds (tools/lm_profile.py) time the pose-LM phases with the shader clock on lane 0
+#ifdef YAVO_LM_PROFILE
+__device__ unsigned long long g_lm_prof[1024][8];
+#define LMP_DECL unsigned long long lmp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long lmp_t = __builtin_readcyclecounter();
+#define LMP_MARK(slot) do { const unsigned long long t_ = __builtin_readcyclecounter(); lmp_acc[slot] += t_ - lmp_t; lmp_t = t_; } while (0)
+#define LMP_STORE() do { if (threadIdx.x == 0) for (int q_ = 0; q_ < 8; ++q_) g_lm_prof[blockIdx.x & 1023][q_] = lmp_acc[q_]; } while (0)
+#else
+#define LMP_DECL
+#define LMP_MARK(slot) do {} while (0)
+#define LMP_STORE() do {} while (0)
+#endif
 constexpr int kMaxEdges = 4096;   // edges per pose problem held in LDS
 
-// exclusive scan over a 256-thread block; s_tmp >= 8 ints
+// exclusive scan over an NT-thread block; s_tmp >= NT/64 ints
+template <int NT = kNT>
 __device__ int block_excl_scan_geom(int v, int* s_tmp, int* total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int incl = v;
@@ -39,7 +53,7 @@ __device__ int block_excl_scan_geom(int v, int* s_tmp, int* total) {
     if (lane == 63) s_tmp[wave] = incl;
     __syncthreads();
     int base = 0, tot = 0;
-    for (int w = 0; w < kNT / 64; ++w) {
+    for (int w = 0; w < NT / 64; ++w) {
         if (w < wave) base += s_tmp[w];
         tot += s_tmp[w];
     }
@@ -652,81 +666,267 @@ __global__ void world2camera_kernel(const double* __restrict__ X, int n, const d
 // ------------------------------------------------------------------------------------------------
 // Eigen LDLT 6x6 (lane 0)
 // ------------------------------------------------------------------------------------------------
-__device__ bool ldlt6_solve(const double* Hin, const double* b, double* x, int variant) {
-    double mat[36];
+// Eigen::LDLT<Matrix6d> (diagonal pivoting, Eigen's ldlt_inplace + solve) -- variant 0 subtracts the
+// GEMV update term by term (the dynamic-size path g2o's LinearSolverDense takes), variant 1 forms the dot
+// first (fixed-size path, test.cc's GN).  Fully unrolled: every index is a compile-time constant and the
+// pivot swaps are predicated swaps, so the 6x6 factor lives in registers (a runtime-indexed private array
+// would go to scratch memory, one dependent round trip per access).
+template <int A, int B>
+__device__ __forceinline__ void dswap(double (&m)[36]) {
+    const double t = m[A];
+    m[A] = m[B];
+    m[B] = t;
+}
+
+template <int variant>
+__device__ bool ldlt6_solve(const double* Hin, const double* b, double* x) {
+    double m[36];
+#pragma unroll
+    for (int i = 0; i < 36; ++i) m[i] = Hin[i];
+    constexpr int n = 6;
     int tr[6];
-    for (int i = 0; i < 36; ++i) mat[i] = Hin[i];
-    const int n = 6;
     int sign = 0;
-    int found_zero_pivot = 0, ret = 1;
-    double temp[6];
-#define L(i, j) mat[(i) * 6 + (j)]
+    int found_zero_pivot = 0;
+    bool stop = false;
+#pragma unroll
     for (int k = 0; k < n; ++k) {
-        int big = k;
-        double bv = fabs(L(k, k));
-        for (int i = k + 1; i < n; ++i)
-            if (fabs(L(i, i)) > bv) { bv = fabs(L(i, i)); big = i; }
-        tr[k] = big;
-        if (k != big) {
-            int s = n - big - 1;
-            for (int j = 0; j < k; ++j) { double t = L(k, j); L(k, j) = L(big, j); L(big, j) = t; }
-            for (int j = 0; j < s; ++j) { double t = L(big + 1 + j, k); L(big + 1 + j, k) = L(big + 1 + j, big); L(big + 1 + j, big) = t; }
-            { double t = L(k, k); L(k, k) = L(big, big); L(big, big) = t; }
-            for (int i = k + 1; i < big; ++i) { double t = L(i, k); L(i, k) = L(big, i); L(big, i) = t; }
-        }
-        int rs = n - k - 1;
-        if (k > 0) {
-            for (int j = 0; j < k; ++j) temp[j] = L(j, j) * L(k, j);
-            double dot = L(k, 0) * temp[0];
-            for (int j = 1; j < k; ++j) dot = dot + L(k, j) * temp[j];
-            L(k, k) -= dot;
-            for (int i = k + 1; i < n; ++i) {
-                if (variant == 0) {
-                    double acc = L(i, k);
-                    for (int j = 0; j < k; ++j) acc = acc - L(i, j) * temp[j];
-                    L(i, k) = acc;
-                } else {
-                    double d = L(i, 0) * temp[0];
-                    for (int j = 1; j < k; ++j) d = d + L(i, j) * temp[j];
-                    L(i, k) = L(i, k) - d;
+        if (!stop) {
+            int big = k;
+            double bv = fabs(m[k * 7]);
+#pragma unroll
+            for (int i = k + 1; i < n; ++i)
+                if (fabs(m[i * 7]) > bv) {
+                    bv = fabs(m[i * 7]);
+                    big = i;
+                }
+            tr[k] = big;
+#pragma unroll
+            for (int c = k + 1; c < n; ++c) {
+                if (c == big) {
+                    // rows/cols k <-> c of the lower triangle (Eigen's ldlt_inplace swap sequence)
+#pragma unroll
+                    for (int j = 0; j < k; ++j) {
+                        const double t = m[k * 6 + j]; m[k * 6 + j] = m[c * 6 + j]; m[c * 6 + j] = t;
+                    }
+#pragma unroll
+                    for (int j = 0; j < n - c - 1; ++j) {
+                        const double t = m[(c + 1 + j) * 6 + k]; m[(c + 1 + j) * 6 + k] = m[(c + 1 + j) * 6 + c];
+                        m[(c + 1 + j) * 6 + c] = t;
+                    }
+                    { const double t = m[k * 7]; m[k * 7] = m[c * 7]; m[c * 7] = t; }
+#pragma unroll
+                    for (int i = k + 1; i < c; ++i) {
+                        const double t = m[i * 6 + k]; m[i * 6 + k] = m[c * 6 + i]; m[c * 6 + i] = t;
+                    }
                 }
             }
+            if (k > 0) {
+                double temp[6];
+#pragma unroll
+                for (int j = 0; j < k; ++j) temp[j] = m[j * 7] * m[k * 6 + j];
+                double dot = m[k * 6 + 0] * temp[0];
+#pragma unroll
+                for (int j = 1; j < k; ++j) dot = dot + m[k * 6 + j] * temp[j];
+                m[k * 7] -= dot;
+#pragma unroll
+                for (int i = k + 1; i < n; ++i) {
+                    if (variant == 0) {
+                        double acc = m[i * 6 + k];
+#pragma unroll
+                        for (int j = 0; j < k; ++j) acc = acc - m[i * 6 + j] * temp[j];
+                        m[i * 6 + k] = acc;
+                    } else {
+                        double d = m[i * 6 + 0] * temp[0];
+#pragma unroll
+                        for (int j = 1; j < k; ++j) d = d + m[i * 6 + j] * temp[j];
+                        m[i * 6 + k] = m[i * 6 + k] - d;
+                    }
+                }
+            }
+            const double akk = m[k * 7];
+            const int valid = fabs(akk) > 0;
+            if (k == 0 && !valid) {
+                sign = 0;
+#pragma unroll
+                for (int j = 0; j < n; ++j) tr[j] = j;
+                stop = true;
+            } else {
+                if (k + 1 < n && valid) {
+#pragma unroll
+                    for (int i = k + 1; i < n; ++i) m[i * 6 + k] /= akk;
+                }
+                if (!(found_zero_pivot && valid) && !valid) found_zero_pivot = 1;
+                if (sign == 1) { if (akk < 0) sign = 3; }
+                else if (sign == 2) { if (akk > 0) sign = 3; }
+                else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+            }
+        } else {
+            tr[k] = k;
         }
-        double akk = L(k, k);
-        int valid = fabs(akk) > 0;
-        if (k == 0 && !valid) {
-            sign = 0;
-            for (int j = 0; j < n; ++j) tr[j] = j;
-            ret = 0;
-            break;
-        }
-        if (rs > 0 && valid) {
-            for (int i = k + 1; i < n; ++i) L(i, k) /= akk;
-        } else if (rs > 0) {
-            for (int i = k + 1; i < n; ++i) ret = ret && (L(i, k) == 0);
-        }
-        if (found_zero_pivot && valid) ret = 0;
-        else if (!valid) found_zero_pivot = 1;
-        if (sign == 1) { if (akk < 0) sign = 3; }
-        else if (sign == 2) { if (akk > 0) sign = 3; }
-        else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
     }
-    (void)ret;
     const bool positive = (sign == 1 || sign == 0);
     double v[6];
+#pragma unroll
     for (int i = 0; i < 6; ++i) v[i] = b[i];
-    for (int k = 0; k < n; ++k) { double t = v[k]; v[k] = v[tr[k]]; v[tr[k]] = t; }
+    // v = P b: transpositions applied in order, swap(v[k], v[tr[k]]) with tr[k] >= k
+#pragma unroll
+    for (int k = 0; k < n; ++k) {
+#pragma unroll
+        for (int c = k + 1; c < n; ++c)
+            if (tr[k] == c) { const double t = v[k]; v[k] = v[c]; v[c] = t; }
+    }
+#pragma unroll
     for (int j = 0; j < n; ++j)
-        for (int i = j + 1; i < n; ++i) v[i] = v[i] - L(i, j) * v[j];
+#pragma unroll
+        for (int i = j + 1; i < n; ++i) v[i] = v[i] - m[i * 6 + j] * v[j];
+#pragma unroll
     for (int i = 0; i < n; ++i) {
-        if (fabs(L(i, i)) > DBL_MIN) v[i] /= L(i, i);
+        if (fabs(m[i * 7]) > DBL_MIN) v[i] /= m[i * 7];
         else v[i] = 0;
     }
+#pragma unroll
     for (int j = n - 1; j >= 0; --j)
-        for (int i = 0; i < j; ++i) v[i] = v[i] - L(j, i) * v[j];
-    for (int k = n - 1; k >= 0; --k) { double t = v[k]; v[k] = v[tr[k]]; v[tr[k]] = t; }
-#undef L
+#pragma unroll
+        for (int i = 0; i < j; ++i) v[i] = v[i] - m[j * 6 + i] * v[j];
+#pragma unroll
+    for (int k = n - 1; k >= 0; --k) {
+#pragma unroll
+        for (int c = k + 1; c < n; ++c)
+            if (tr[k] == c) { const double t = v[k]; v[k] = v[c]; v[c] = t; }
+    }
+#pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = v[i];
+    return positive;
+}
+
+// The same Eigen LDLT for a symmetric system held in LDS (H + lambda I, the LM trial's damped matrix).
+// Eigen's pivot at step k is the largest |diagonal| among rows k..5, and those diagonal entries are still
+// the original ones (a row's diagonal is only updated at its own step), so the whole transposition
+// sequence follows from the six diagonal values alone.  Pivoted LDLT then performs exactly the arithmetic
+// of unpivoted LDLT on P H P^T: the permutation is resolved first, P H P^T's lower triangle is gathered
+// from LDS, and the factorization runs straight-line in registers.
+// Hp: the symmetric matrix's lower triangle packed by rows, (i, j <= i) at i (i + 1) / 2 + j.
+template <int variant>
+__device__ bool ldlt6_solve_perm(const double* Hp, double lambda, const double* b, double* x) {
+    constexpr int n = 6;
+    double dg[6];
+    int id[6];
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+        dg[i] = Hp[i * (i + 1) / 2 + i] + lambda;
+        id[i] = i;
+    }
+#pragma unroll
+    for (int k = 0; k < n; ++k) {
+        int big = k;
+        double bv = fabs(dg[k]);
+#pragma unroll
+        for (int i = k + 1; i < n; ++i)
+            if (fabs(dg[i]) > bv) {
+                bv = fabs(dg[i]);
+                big = i;
+            }
+        const double dk = dg[k];
+        const int ik = id[k];
+#pragma unroll
+        for (int c = k + 1; c < n; ++c) {
+            const bool sw = c == big;
+            dg[k] = sw ? dg[c] : dg[k];
+            id[k] = sw ? id[c] : id[k];
+            dg[c] = sw ? dk : dg[c];
+            id[c] = sw ? ik : id[c];
+        }
+    }
+    double m[36];
+    if (!(fabs(dg[0]) > 0)) {
+        // Eigen's k == 0 early exit (all diagonal entries 0, no transposition): the matrix stays as is
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            id[i] = i;
+#pragma unroll
+            for (int j = 0; j < i; ++j) m[i * 6 + j] = Hp[i * (i + 1) / 2 + j];
+            m[i * 7] = Hp[i * (i + 1) / 2 + i] + lambda;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+#pragma unroll
+            for (int j = 0; j < i; ++j) {
+                const int hi = id[i] > id[j] ? id[i] : id[j], lo = id[i] > id[j] ? id[j] : id[i];
+                m[i * 6 + j] = Hp[hi * (hi + 1) / 2 + lo];
+            }
+            m[i * 7] = dg[i];
+        }
+    }
+    int sign = 0;
+    int found_zero_pivot = 0;
+    if (fabs(dg[0]) > 0) {
+#pragma unroll
+        for (int k = 0; k < n; ++k) {
+            if (k > 0) {
+                double temp[6];
+#pragma unroll
+                for (int j = 0; j < k; ++j) temp[j] = m[j * 7] * m[k * 6 + j];
+                double dot = m[k * 6 + 0] * temp[0];
+#pragma unroll
+                for (int j = 1; j < k; ++j) dot = dot + m[k * 6 + j] * temp[j];
+                m[k * 7] -= dot;
+#pragma unroll
+                for (int i = k + 1; i < n; ++i) {
+                    if (variant == 0) {
+                        double acc = m[i * 6 + k];
+#pragma unroll
+                        for (int j = 0; j < k; ++j) acc = acc - m[i * 6 + j] * temp[j];
+                        m[i * 6 + k] = acc;
+                    } else {
+                        double d = m[i * 6 + 0] * temp[0];
+#pragma unroll
+                        for (int j = 1; j < k; ++j) d = d + m[i * 6 + j] * temp[j];
+                        m[i * 6 + k] = m[i * 6 + k] - d;
+                    }
+                }
+            }
+            const double akk = m[k * 7];
+            const int valid = fabs(akk) > 0;
+            if (k + 1 < n && valid) {
+#pragma unroll
+                for (int i = k + 1; i < n; ++i) m[i * 6 + k] /= akk;
+            }
+            if (!(found_zero_pivot && valid) && !valid) found_zero_pivot = 1;
+            if (sign == 1) { if (akk < 0) sign = 3; }
+            else if (sign == 2) { if (akk > 0) sign = 3; }
+            else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+        }
+    }
+    const bool positive = (sign == 1 || sign == 0);
+    double v[6];
+#pragma unroll
+    for (int i = 0; i < n; ++i) {  // v = P b
+        double t = b[0];
+#pragma unroll
+        for (int j = 1; j < n; ++j) t = id[i] == j ? b[j] : t;
+        v[i] = t;
+    }
+#pragma unroll
+    for (int j = 0; j < n; ++j)
+#pragma unroll
+        for (int i = j + 1; i < n; ++i) v[i] = v[i] - m[i * 6 + j] * v[j];
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+        if (fabs(m[i * 7]) > DBL_MIN) v[i] /= m[i * 7];
+        else v[i] = 0;
+    }
+#pragma unroll
+    for (int j = n - 1; j >= 0; --j)
+#pragma unroll
+        for (int i = 0; i < j; ++i) v[i] = v[i] - m[j * 6 + i] * v[j];
+#pragma unroll
+    for (int j = 0; j < n; ++j) {  // x = P^T v
+        double t = v[0];
+#pragma unroll
+        for (int i = 1; i < n; ++i) t = id[i] == j ? v[i] : t;
+        x[j] = t;
+    }
     return positive;
 }
 
@@ -768,29 +968,49 @@ __device__ __forceinline__ double huber_rho(double e2, double* rho1) {
     return 2 * sqrte * delta - dsqr;
 }
 
-// Tree sum of per-thread partials in the oracle's order (sum_mode 1): p[t] += p[t + off] for
-// off = 128, 64 (across waves, through LDS), then 32 .. 1 inside wave 0 (shuffles).  part[] holds this
+// Tree sum of per-thread partials in the oracle's order (sum_mode log2(NT) - 7): p[t] += p[t + off] for
+// off = NT/2 .. 64 (across waves, through LDS), then 32 .. 1 inside wave 0 (shuffles).  part[] holds this
 // thread's nv partials; totals land in out[0..nv) (LDS), visible after the trailing barrier.
-// red: >= nv * 128 doubles of LDS.
-template <int NV>
+// red: >= nv * NT/2 doubles of LDS.
+template <int NV, int NT = kNT>
 __device__ void tree_reduce(double (&part)[NV], double* red, double* out) {
     const int tid = threadIdx.x;
     __syncthreads();
-    if (tid >= 128)
-        for (int v = 0; v < NV; ++v) red[v * 128 + (tid - 128)] = part[v];
-    __syncthreads();
-    if (tid < 128)
-        for (int v = 0; v < NV; ++v) part[v] = part[v] + red[v * 128 + tid];
-    __syncthreads();
-    if (tid >= 64 && tid < 128)
-        for (int v = 0; v < NV; ++v) red[v * 128 + (tid - 64)] = part[v];
+#pragma unroll
+    for (int off = NT / 2; off >= 128; off >>= 1) {
+        if (tid >= off && tid < 2 * off) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) red[v * (NT / 2) + (tid - off)] = part[v];
+        }
+        __syncthreads();
+        if (tid < off) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) part[v] = part[v] + red[v * (NT / 2) + tid];
+        }
+        __syncthreads();
+    }
+    if (tid >= 64 && tid < 128) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) red[v * (NT / 2) + (tid - 64)] = part[v];
+    }
     __syncthreads();
     if (tid < 64) {
-        for (int v = 0; v < NV; ++v) {
-            double x = part[v] + red[v * 128 + tid];
+        // wave 0: the NV independent shuffle trees advance together (all NV shuffles of a level are issued
+        // before the adds), so one LDS-permute latency is paid per level instead of per value and level
+        double x[NV];
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) x = x + __shfl_down(x, off, 64);
-            if (tid == 0) out[v] = x;
+        for (int v = 0; v < NV; ++v) x[v] = part[v] + red[v * (NT / 2) + tid];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            double y[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) y[v] = __shfl_down(x[v], off, 64);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) x[v] = x[v] + y[v];
+        }
+        if (tid == 0) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) out[v] = x[v];
         }
     }
     __syncthreads();
@@ -798,26 +1018,127 @@ __device__ void tree_reduce(double (&part)[NV], double* red, double* out) {
 
 struct LMShared {
     double T[7], Tbak[7], Tlast[7], K[9];
-    double H[36], b[6], x[6], vals[32];
+    double sys[28], x[6], vals[32];  // sys: {H lower packed (21), b (6), chi2} of the current iteration
     double lambda, ni, currentChi, tempChi, rho;
     int flag;  // control broadcast from lane 0
 };
 
 constexpr int kLMVals = 28;  // 21 lower-triangle H entries + 6 b + 1 chi2
 
+// One pass over the active edges at S.T: computeActiveErrors + activeRobustChi2 + buildSystem of g2o's
+// BlockSolver (Huber-weighted J^T J lower triangle, -J^T W e, robust chi2), summed in the oracle's tree
+// order into S.vals[0..28).  Also records S.Tlast (the estimate the active edges' errors refer to).
+__device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, int na, const uint8_t* s_robust,
+                                        const double* X, const double* uv, double* s_red,
+                                        unsigned long long* lmp = nullptr) {
+    const int tid = threadIdx.x;
+    __syncthreads();  // S.T written by lane 0
+#ifdef YAVO_LM_PROFILE
+    const unsigned long long p0 = __builtin_readcyclecounter();
+#endif
+    double T[7], K[9];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) T[q] = S.T[q];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) K[q] = S.K[q];
+    if (tid < 7) S.Tlast[tid] = T[tid];
+    double part[kLMVals];
+#pragma unroll
+    for (int v = 0; v < kLMVals; ++v) part[v] = 0.0;
+    // the next edge's point / measurement / robust flag are loaded while this one is evaluated (the gathers
+    // hit L2: their latency would otherwise be paid once per edge)
+    double nx[5] = {0, 0, 0, 0, 0};
+    int nrob = 0;
+    if (tid < na) {
+        const int i = s_active[tid];
+        nx[0] = X[3 * i]; nx[1] = X[3 * i + 1]; nx[2] = X[3 * i + 2]; nx[3] = uv[2 * i]; nx[4] = uv[2 * i + 1];
+        nrob = s_robust[i];
+    }
+    for (int a = tid; a < na; a += kLMNT) {
+        const double xi[3] = {nx[0], nx[1], nx[2]}, mi[2] = {nx[3], nx[4]};
+        const int rob = nrob;
+        if (a + kLMNT < na) {
+            const int i = s_active[a + kLMNT];
+            nx[0] = X[3 * i]; nx[1] = X[3 * i + 1]; nx[2] = X[3 * i + 2]; nx[3] = uv[2 * i]; nx[4] = uv[2 * i + 1];
+            nrob = s_robust[i];
+        }
+        double e[2];
+        edge_error(T, K, xi, mi, e);
+        const double c2 = e[0] * e[0] + e[1] * e[1];
+        double w = 1.0;
+        double chi = c2;
+        if (rob) chi = huber_rho(c2, &w);
+        part[27] = part[27] + chi;
+        double J[12];
+        edge_jacobian(T, K, xi, J);
+        // g2o forms J^T (rho' Omega) J and -J^T (rho' Omega) e with Omega = I, i.e. products with the literal
+        // 0.0 / 1.0 of Omega, and J[1] = J[6] = 0 structurally.  With finite operands those products only
+        // contribute signed zeros, which cannot change a partial sum (a partial that starts at +0.0 never
+        // becomes -0.0, and p + (+-0) = p for p != 0), so the short form below gives bit-identical sums; an
+        // edge with a non-finite operand takes the literal form.
+        const double fin = J[0] + J[2] + J[3] + J[4] + J[5] + J[7] + J[8] + J[9] + J[10] + J[11] + w + e[0] + e[1];
+        if (__builtin_expect(isfinite(fin), 1)) {
+            double a[6], b[6];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+                a[r] = J[r] * w;
+                b[r] = J[6 + r] * w;
+            }
+            part[0] = part[0] + a[0] * J[0];
+            part[2] = part[2] + b[1] * J[7];
+#pragma unroll
+            for (int r = 2; r < 6; ++r) {
+                part[r * (r + 1) / 2 + 0] = part[r * (r + 1) / 2 + 0] + a[r] * J[0];
+                part[r * (r + 1) / 2 + 1] = part[r * (r + 1) / 2 + 1] + b[r] * J[7];
+#pragma unroll
+                for (int c = 2; c <= r; ++c)
+                    part[r * (r + 1) / 2 + c] = part[r * (r + 1) / 2 + c] + (a[r] * J[c] + b[r] * J[6 + c]);
+            }
+            part[21] = part[21] + (-(a[0] * e[0]));
+            part[22] = part[22] + (-(b[1] * e[1]));
+#pragma unroll
+            for (int r = 2; r < 6; ++r) part[21 + r] = part[21 + r] + (-(a[r] * e[0] + b[r] * e[1]));
+        } else {
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+                const double t0 = J[r] * w + J[6 + r] * 0.0;
+                const double t1 = J[r] * 0.0 + J[6 + r] * w;
+#pragma unroll
+                for (int c = 0; c <= r; ++c)
+                    part[r * (r + 1) / 2 + c] = part[r * (r + 1) / 2 + c] + (t0 * J[c] + t1 * J[6 + c]);
+                const double s0 = (w * J[r]) * 1.0 + (w * J[6 + r]) * 0.0;
+                const double s1 = (w * J[r]) * 0.0 + (w * J[6 + r]) * 1.0;
+                part[21 + r] = part[21 + r] + (-(s0 * e[0] + s1 * e[1]));
+            }
+        }
+    }
+#ifdef YAVO_LM_PROFILE
+    const unsigned long long p1 = __builtin_readcyclecounter();
+#endif
+    tree_reduce<kLMVals, kLMNT>(part, s_red, S.vals);
+#ifdef YAVO_LM_PROFILE
+    if (lmp) {
+        const unsigned long long p2 = __builtin_readcyclecounter();
+        lmp[0] += p1 - p0;
+        lmp[1] += p2 - p1;
+    }
+#endif
+}
+
 // Problem p owns edges [offsets[p], offsets[p+1]) (CSR) or, with counts != nullptr, [p*stride, p*stride +
 // counts[p]) (the batch's fixed-stride track layout).  The prior is read from priors[p] and the estimate
 // written to poses[p] (the two may alias).
-__global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
+__global__ __launch_bounds__(kLMNT) void pose_lm_kernel(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
                                                       int stride, const double* __restrict__ Xall,
                                                       const double* __restrict__ uvall, const double* __restrict__ Kall,
                                                       const double* priors, double* poses,
                                                       uint8_t* __restrict__ outlier_all, int32_t* __restrict__ inliers) {
     __shared__ uint8_t s_level[kMaxEdges], s_out[kMaxEdges], s_robust[kMaxEdges];
     __shared__ int16_t s_active[kMaxEdges];
-    __shared__ double s_red[kLMVals * 128];
+    __shared__ double s_red[kLMVals * (kLMNT / 2)];
     __shared__ LMShared S;
     __shared__ int s_tmp[40];
+    LMP_DECL
     const int prob = blockIdx.x;
     const int tid = threadIdx.x;
     const int64_t e0 = counts ? (int64_t)prob * stride : (int64_t)offsets[prob];
@@ -827,7 +1148,7 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
     const double* uv = uvall + 2 * e0;
     if (tid < 9) S.K[tid] = Kall[9 * prob + tid];
     if (tid < 7) S.T[tid] = priors[7 * prob + tid];
-    for (int i = tid; i < n; i += kNT) {
+    for (int i = tid; i < n; i += kLMNT) {
         s_level[i] = 0;
         s_out[i] = 0;
         s_robust[i] = 1;
@@ -843,110 +1164,88 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
         if (tid < 7) S.T[tid] = prior[tid];
         // initializeOptimization(): active = level-0 edges in insertion order (block compaction)
         int na = 0;
-        for (int base = 0; base < n; base += kNT) {
+        for (int base = 0; base < n; base += kLMNT) {
             const int i = base + tid;
             const int f = (i < n && s_level[i] == 0) ? 1 : 0;
             int tot = 0;
-            const int off = block_excl_scan_geom(f, s_tmp, &tot);
+            const int off = block_excl_scan_geom<kLMNT>(f, s_tmp, &tot);
             if (f) s_active[na + off] = (int16_t)i;
             na += tot;
         }
         __syncthreads();
         if (na > 0) {
             double lambda = 0, ni = 2;
+            // S.vals holds {H, b, chi2} at S.T when `have` (the last trial was accepted: g2o's next
+            // computeActiveErrors + buildSystem happen at exactly that estimate, so the trial pass builds the
+            // system along with its chi2 and the rebuild is skipped)
+            bool have = false;
             for (int it = 0; it < 10; ++it) {
-                // computeActiveErrors + activeRobustChi2 + buildSystem at the current estimate
-                double part[kLMVals];
-                for (int v = 0; v < kLMVals; ++v) part[v] = 0.0;
-                double T[7], K[9];
-                for (int q = 0; q < 7; ++q) T[q] = S.T[q];
-                for (int q = 0; q < 9; ++q) K[q] = S.K[q];
-                if (tid < 7) S.Tlast[tid] = T[tid];  // errors of the active edges are now at T
-                for (int a = tid; a < na; a += kNT) {
-                    const int i = s_active[a];
-                    double e[2];
-                    edge_error(T, K, X + 3 * i, uv + 2 * i, e);
-                    const double c2 = e[0] * e[0] + e[1] * e[1];
-                    double w = 1.0;
-                    double chi = c2;
-                    if (s_robust[i]) chi = huber_rho(c2, &w);
-                    part[27] = part[27] + chi;
-                    double J[12];
-                    edge_jacobian(T, K, X + 3 * i, J);
-                    int v = 0;
-                    for (int r = 0; r < 6; ++r) {
-                        double t0 = J[r] * w + J[6 + r] * 0.0;
-                        double t1 = J[r] * 0.0 + J[6 + r] * w;
-                        for (int c = 0; c <= r; ++c) {
-                            part[v] = part[v] + (t0 * J[c] + t1 * J[6 + c]);
-                            ++v;
-                        }
-                        double s0 = (w * J[r]) * 1.0 + (w * J[6 + r]) * 0.0;
-                        double s1 = (w * J[r]) * 0.0 + (w * J[6 + r]) * 1.0;
-                        part[21 + r] = part[21 + r] + (-(s0 * e[0] + s1 * e[1]));
-                    }
-                }
-                tree_reduce<kLMVals>(part, s_red, S.vals);
+#ifdef YAVO_LM_PROFILE
+                LMP_MARK(5);
+                if (!have) lm_pass(S, s_active, na, s_robust, X, uv, s_red, lmp_acc);
+                lmp_t = __builtin_readcyclecounter();
+#else
+                if (!have) lm_pass(S, s_active, na, s_robust, X, uv, s_red);
+#endif
                 if (tid == 0) {
-                    int v = 0;
-                    for (int r = 0; r < 6; ++r)
-                        for (int c = 0; c <= r; ++c) {
-                            S.H[r * 6 + c] = S.vals[v];
-                            S.H[c * 6 + r] = S.vals[v];
-                            ++v;
-                        }
-                    for (int r = 0; r < 6; ++r) S.b[r] = S.vals[21 + r];
-                    S.currentChi = S.vals[27];
+                    double sys[28];
+#pragma unroll
+                    for (int v = 0; v < 28; ++v) sys[v] = S.vals[v];
+#pragma unroll
+                    for (int v = 0; v < 28; ++v) S.sys[v] = sys[v];
+                    S.currentChi = sys[27];
                     if (it == 0) {
                         double maxDiag = 0;
-                        for (int j = 0; j < 6; ++j) maxDiag = fabs(S.H[j * 7]) > maxDiag ? fabs(S.H[j * 7]) : maxDiag;
+#pragma unroll
+                        for (int j = 0; j < 6; ++j) {
+                            const double d = fabs(sys[j * (j + 1) / 2 + j]);
+                            maxDiag = d > maxDiag ? d : maxDiag;
+                        }
                         lambda = tau * maxDiag;
                         ni = 2;
                     }
                 }
                 // trial loop (do ... while (rho < 0 && qmax < 10))
                 int qmax = 0;
-                bool terminate = false;
+                int f = 0;
                 while (true) {
-                    int ok2 = 0;
                     if (tid == 0) {
-                        for (int q = 0; q < 7; ++q) S.Tbak[q] = S.T[q];
-                        double Hl[36];
-                        for (int q = 0; q < 36; ++q) Hl[q] = S.H[q];
-                        for (int j = 0; j < 6; ++j) Hl[j * 7] += lambda;
-                        ok2 = ldlt6_solve(Hl, S.b, S.x, 0) ? 1 : 0;
+                        double Tc[7], xs[6];
+#pragma unroll
+                        for (int q = 0; q < 7; ++q) Tc[q] = S.T[q];
+#pragma unroll
+                        for (int q = 0; q < 7; ++q) S.Tbak[q] = Tc[q];
+                        const int ok2 = ldlt6_solve_perm<0>(S.sys, lambda, S.sys + 21, xs) ? 1 : 0;
+#pragma unroll
+                        for (int q = 0; q < 6; ++q) S.x[q] = xs[q];
+                        LMP_MARK(6);
                         double Tn[7], Tnew[7];
-                        se3_exp(S.x, Tn);
-                        se3_mul(Tn, S.T, Tnew);
+                        se3_exp(xs, Tn);
+                        se3_mul(Tn, Tc, Tnew);
+#pragma unroll
                         for (int q = 0; q < 7; ++q) S.T[q] = Tnew[q];
                         S.flag = ok2;
                     }
-                    __syncthreads();
-                    ok2 = S.flag;
-                    for (int q = 0; q < 7; ++q) T[q] = S.T[q];
-                    if (tid < 7) S.Tlast[tid] = T[tid];
-                    double pc[1] = {0.0};
-                    for (int a = tid; a < na; a += kNT) {
-                        const int i = s_active[a];
-                        double e[2];
-                        edge_error(T, K, X + 3 * i, uv + 2 * i, e);
-                        const double c2 = e[0] * e[0] + e[1] * e[1];
-                        double w;
-                        pc[0] = pc[0] + (s_robust[i] ? huber_rho(c2, &w) : c2);
-                    }
-                    tree_reduce<1>(pc, s_red, S.vals);
+                    LMP_MARK(2);
+#ifdef YAVO_LM_PROFILE
+                    lm_pass(S, s_active, na, s_robust, X, uv, s_red, lmp_acc);
+                    lmp_t = __builtin_readcyclecounter();
+#else
+                    lm_pass(S, s_active, na, s_robust, X, uv, s_red);  // errors + system at the trial estimate
+#endif
                     if (tid == 0) {
-                        double tempChi = S.vals[0];
+                        const int ok2 = S.flag;
+                        double tempChi = S.vals[27];
                         if (!ok2) tempChi = DBL_MAX;
                         double rho = S.currentChi - tempChi;
                         double scale = 1;
                         if (ok2) {
                             double sc = 0;
-                            for (int j = 0; j < 6; ++j) sc += S.x[j] * (lambda * S.x[j] + S.b[j]);
+                            for (int j = 0; j < 6; ++j) sc += S.x[j] * (lambda * S.x[j] + S.sys[21 + j]);
                             scale = sc + 1e-3;
                         }
                         rho /= scale;
-                        int brk = 0;
+                        int brk = 0, accepted = 0;
                         if (rho > 0 && isfinite(tempChi) && ok2) {
                             double t = 2 * rho - 1;
                             double alpha = 1. - t * t * t;
@@ -955,6 +1254,7 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
                             lambda *= sf;
                             ni = 2;
                             S.currentChi = tempChi;
+                            accepted = 1;
                         } else {
                             lambda *= ni;
                             ni *= 2;
@@ -963,17 +1263,19 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
                         }
                         qmax++;
                         const bool again = !brk && rho < 0 && qmax < 10;
-                        S.flag = again ? 1 : 0;
-                        if (!again) S.flag = (qmax == 10 || rho == 0 || !isfinite(lambda)) ? 2 : 0;
+                        int fl = again ? 1 : 0;
+                        if (!again) fl = (qmax == 10 || rho == 0 || !isfinite(lambda)) ? 2 : 0;
+                        S.flag = fl | (accepted << 2);
                     }
                     __syncthreads();
-                    const int f = S.flag;
+                    f = S.flag;
                     __syncthreads();
-                    if (f == 1) continue;
-                    terminate = (f == 2);
+                    LMP_MARK(3);
+                    if ((f & 3) == 1) continue;
                     break;
                 }
-                if (terminate) break;
+                if ((f & 3) == 2) break;
+                have = (f & 4) != 0;
             }
         }
         __syncthreads();
@@ -985,7 +1287,7 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
         for (int q = 0; q < 7; ++q) Tl[q] = S.Tlast[q];
         for (int q = 0; q < 9; ++q) K[q] = S.K[q];
         int cnt = 0;
-        for (int i = tid; i < n; i += kNT) {
+        for (int i = tid; i < n; i += kLMNT) {
             double ee[2];
             edge_error(s_out[i] ? T : Tl, K, X + 3 * i, uv + 2 * i, ee);
             const double c2 = ee[0] * ee[0] + ee[1] * ee[1];
@@ -1000,12 +1302,14 @@ __global__ __launch_bounds__(kNT) void pose_lm_kernel(const int32_t* __restrict_
             if (round == 2) s_robust[i] = 0;
         }
         int tot = 0;
-        block_excl_scan_geom(cnt, s_tmp, &tot);
+        block_excl_scan_geom<kLMNT>(cnt, s_tmp, &tot);
         outlierCount = tot;
         __syncthreads();
+        LMP_MARK(4);
     }
+    LMP_STORE();
     if (tid < 7) poses[7 * prob + tid] = S.T[tid];
-    for (int i = tid; i < n; i += kNT) outlier_all[e0 + i] = s_out[i];
+    for (int i = tid; i < n; i += kLMNT) outlier_all[e0 + i] = s_out[i];
     if (tid == 0) inliers[prob] = n - outlierCount;
 }
 
@@ -1130,7 +1434,7 @@ __global__ __launch_bounds__(kNT) void pose_gn_kernel(const int32_t* __restrict_
                 }
             for (int r = 0; r < 6; ++r) b[r] = s_vals[21 + r];
             const double cost = s_vals[27];
-            ldlt6_solve(H, b, dx, 1);
+            ldlt6_solve<1>(H, b, dx);
             int stop = 0;
             if (isnan(dx[0])) stop = 1;
             else if (iter > 0 && cost >= lastCost) stop = 1;
@@ -1182,7 +1486,7 @@ void launch_world2camera(const double* X, int n, const double* T, const double* 
 
 void launch_pose_lm(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
                     double* poses, uint8_t* outlier, int32_t* inliers, hipStream_t s) {
-    hipLaunchKernelGGL(geom::pose_lm_kernel, dim3(n_problems), dim3(geom::kNT), 0, s, offsets,
+    hipLaunchKernelGGL(geom::pose_lm_kernel, dim3(n_problems), dim3(geom::kLMNT), 0, s, offsets,
                        static_cast<const int32_t*>(nullptr), 0, X, uv, K, static_cast<const double*>(poses), poses,
                        outlier, inliers);
 }
@@ -1200,7 +1504,7 @@ void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, cons
                        const double* edge_uv, const double* K, const double* priors, double* poses,
                        uint8_t* edge_outlier, int32_t* inliers, hipStream_t s) {
     if (n_tracks <= 0) return;
-    hipLaunchKernelGGL(geom::pose_lm_kernel, dim3(n_tracks), dim3(geom::kNT), 0, s,
+    hipLaunchKernelGGL(geom::pose_lm_kernel, dim3(n_tracks), dim3(geom::kLMNT), 0, s,
                        static_cast<const int32_t*>(nullptr), edge_count, stride, edge_X, edge_uv, K, priors, poses,
                        edge_outlier, inliers);
 }
@@ -1211,3 +1515,11 @@ void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, con
 }
 
 }  // namespace yavo
+
+#ifdef YAVO_LM_PROFILE
+// profiling builds only (lib/libyavo_prof.so): per-workgroup pose-LM phase cycle counts of the last launch
+extern "C" int yv_debug_lm_prof(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(yavo::geom::g_lm_prof), sizeof(unsigned long long) * 1024 * 8) ==
+                   hipSuccess ? 0 : -2;
+}
+#endif
