@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=64, help="stereo frames per step per GPU")
+    ap.add_argument("--frames", type=int, default=256, help="stereo frames per step per GPU")
     ap.add_argument("--cpu-baseline", choices=["both", "literal", "efficient", "none"], default="both")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-timing", action="store_true", help="do not record per-stage HIP events")

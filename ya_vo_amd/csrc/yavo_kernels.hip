@@ -667,64 +667,150 @@ void launch_pack_desc(const yv_keypoint* keypoints, const int32_t* kp_count, int
 }
 
 // ------------------------------------------------------------------------------------------------
-// Brute-force Hamming matcher
+// Brute-force Hamming matcher on the int8 matrix cores
 // ------------------------------------------------------------------------------------------------
-constexpr int MT_QPT = 2;                 // queries per thread
-constexpr int MT_QB = 256 * MT_QPT;       // queries per workgroup
-constexpr int MT_TB = 512;                // train descriptors per LDS chunk (16 KB)
+// With every descriptor bit b mapped to the int8 value 2b - 1 (+1 / -1), the dot product of two 256-bit
+// descriptors is 256 - 2 * Hamming exactly, so a pair's whole distance matrix is an int8 GEMM
+// (queries x 256) . (256 x trains) with int32 accumulation: v_mfma_i32_16x16x64_i8 computes a 16 x 16
+// distance tile per K-step, four K-steps per tile.  Per query the first minimum (strict <, as
+// Brief::matchFeatures) is the maximum of the key (dot << 16) | (0xFFFF - j): larger dot, then smaller j.
+// A and B fragments place descriptor element k = 64 s + 16 (lane >> 4) + j in byte j of K-step s of
+// their lane, for both operands alike, so the products pair matching bits whatever the hardware's k
+// order inside an instruction is.
+typedef int mm_v4i __attribute__((ext_vector_type(4)));
+constexpr int MM_QT = 4;                  // 16-row query tiles per wave
+constexpr int MM_QB = 4 * MM_QT * 16;     // queries per workgroup (4 waves)
+constexpr int MM_TC = 64;                 // train descriptors per LDS chunk
+constexpr int MM_ROW = 17;                // uint4 per expanded train row (16 + 1 pad: conflict-free b128 reads)
+
+// 4 descriptor bits -> 4 bytes of +1 (bit set) / -1 (bit clear), bit i in byte i
+__device__ __forceinline__ uint32_t expand_pm1(uint32_t nib) {
+    const uint32_t spread = (nib * 0x00204081u) & 0x01010101u;
+    return ~(spread * 0xFEu);
+}
+
+__device__ __forceinline__ uint4 expand16_pm1(uint32_t bits) {
+    return make_uint4(expand_pm1(bits & 0xF), expand_pm1((bits >> 4) & 0xF), expand_pm1((bits >> 8) & 0xF),
+                      expand_pm1((bits >> 12) & 0xF));
+}
 
 __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ desc, const int32_t* __restrict__ kp_count,
                                                     const int32_t* __restrict__ pairs, int max_kp,
                                                     uint32_t* __restrict__ match_key) {
-    __shared__ uint4 s_t[MT_TB * 2];
-    const int pair = blockIdx.z;
+    __shared__ uint4 s_t[2][MM_TC * MM_ROW];
+    const int pair = blockIdx.y;
     const int qi = pairs[2 * pair], ti = pairs[2 * pair + 1];
     const int nq = kp_count[qi], nt = kp_count[ti];
-    const int q0 = blockIdx.x * MT_QB, t0 = blockIdx.y * MT_TB;
-    if (q0 >= nq || t0 >= nt) return;
-    const int tn = min(MT_TB, nt - t0);
-    const uint4* tsrc = reinterpret_cast<const uint4*>(desc + (int64_t)ti * max_kp + t0);
-    for (int i = threadIdx.x; i < tn * 2; i += 256) s_t[i] = tsrc[i];
-    uint32_t qd[MT_QPT][8];
-    uint32_t best[MT_QPT];
+    const int q0 = blockIdx.x * MM_QB;
+    if (q0 >= nq) return;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int col = lane & 15, g = lane >> 4;
+    const Desc* qd = desc + (int64_t)qi * max_kp;
+    const uint32_t* tw = reinterpret_cast<const uint32_t*>(desc + (int64_t)ti * max_kp);
+
+    // query fragments: tile qt row (lane & 15) = query q0 + 64 wave + 16 qt + (lane & 15)
+    mm_v4i A[MM_QT][4];
 #pragma unroll
-    for (int k = 0; k < MT_QPT; ++k) {
-        const int q = q0 + threadIdx.x + 256 * k;
-        best[k] = 0xFFFFFFFFu;
-        const Desc* qs = desc + (int64_t)qi * max_kp + (q < nq ? q : 0);
-        const uint4 a = reinterpret_cast<const uint4*>(qs)[0];
-        const uint4 bq = reinterpret_cast<const uint4*>(qs)[1];
-        qd[k][0] = a.x; qd[k][1] = a.y; qd[k][2] = a.z; qd[k][3] = a.w;
-        qd[k][4] = bq.x; qd[k][5] = bq.y; qd[k][6] = bq.z; qd[k][7] = bq.w;
-    }
-    __syncthreads();
-    for (int t = 0; t < tn; ++t) {
-        const uint4 a = s_t[2 * t], bq = s_t[2 * t + 1];
-        const uint32_t tag = (uint32_t)(t0 + t);
+    for (int qt = 0; qt < MM_QT; ++qt) {
+        const int q = q0 + 64 * wave + 16 * qt + col;
+        const Desc d = qd[q < nq ? q : 0];
 #pragma unroll
-        for (int k = 0; k < MT_QPT; ++k) {
-            uint32_t d = __popc(qd[k][0] ^ a.x);
-            d += __popc(qd[k][1] ^ a.y);
-            d += __popc(qd[k][2] ^ a.z);
-            d += __popc(qd[k][3] ^ a.w);
-            d += __popc(qd[k][4] ^ bq.x);
-            d += __popc(qd[k][5] ^ bq.y);
-            d += __popc(qd[k][6] ^ bq.z);
-            d += __popc(qd[k][7] ^ bq.w);
-            const uint32_t key = (d << 16) | tag;  // min key = smallest distance, then first index
-            best[k] = min(best[k], key);
+        for (int s = 0; s < 4; ++s) {
+            const uint32_t hi_mask = 0u - (uint32_t)(g >> 1);  // blend, not an index: keeps d in registers
+            const uint32_t w = d.w[2 * s] ^ ((d.w[2 * s] ^ d.w[2 * s + 1]) & hi_mask);
+            const uint32_t bits = (w >> (16 * (g & 1))) & 0xFFFFu;
+            const uint4 e = expand16_pm1(bits);
+            A[qt][s] = mm_v4i{(int)e.x, (int)e.y, (int)e.z, (int)e.w};
         }
     }
+    int best[MM_QT][4];
 #pragma unroll
-    for (int k = 0; k < MT_QPT; ++k) {
-        const int q = q0 + threadIdx.x + 256 * k;
-        if (q < nq) atomicMin(&match_key[(int64_t)pair * max_kp + q], best[k]);
+    for (int qt = 0; qt < MM_QT; ++qt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) best[qt][r] = INT_MIN;
+
+    // staging: thread -> (train tt = idx >> 4, 16-bit field u = idx & 15), 4 fields per thread per chunk
+    uint32_t pre[4];
+    auto fetch = [&](int t0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int idx = tid + 256 * k, tt = idx >> 4, u = idx & 15;
+            const int t = t0 + tt;
+            pre[k] = t < nt ? tw[(int64_t)t * 8 + (u >> 1)] : 0u;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int idx = tid + 256 * k, tt = idx >> 4, u = idx & 15;
+            s_t[buf][tt * MM_ROW + u] = expand16_pm1((pre[k] >> (16 * (u & 1))) & 0xFFFFu);
+        }
+    };
+    if (nt > 0) {
+        fetch(0);
+        store(0);
+    }
+    int buf = 0;
+    for (int t0 = 0; t0 < nt; t0 += MM_TC) {
+        const bool more = t0 + MM_TC < nt;
+        if (more) fetch(t0 + MM_TC);
+        __syncthreads();
+#pragma unroll
+        for (int tt0 = 0; tt0 < MM_TC; tt0 += 16) {
+            const int j = t0 + tt0 + col;
+            if (t0 + tt0 >= nt) break;
+            mm_v4i B[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const uint4 v = s_t[buf][(tt0 + col) * MM_ROW + 4 * s + g];
+                B[s] = mm_v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+            }
+            // key = (dot << 16) + bias: bias = 0xFFFF - j for a real train column; a column past nt gets
+            // -2^30, below every real key (>= -2^24) and above INT_MIN, so no per-element select is needed
+            const int bias = j < nt ? 0xFFFF - j : -(1 << 30);
+#pragma unroll
+            for (int qt = 0; qt < MM_QT; ++qt) {
+                mm_v4i acc = {0, 0, 0, 0};
+#pragma unroll
+                for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], B[s], acc, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = (int)(((uint32_t)acc[r] << 16) + (uint32_t)bias);
+                    best[qt][r] = max(best[qt][r], key);
+                }
+            }
+        }
+        if (more) {
+            store(buf ^ 1);  // the other buffer: last read before the barrier at the top of this chunk
+            buf ^= 1;
+        }
+    }
+    // per query row: max over the 16 lanes (train columns) of its lane group
+#pragma unroll
+    for (int qt = 0; qt < MM_QT; ++qt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            int v = best[qt][r];
+#pragma unroll
+            for (int m = 8; m > 0; m >>= 1) v = max(v, __shfl_xor(v, m, 16));
+            const int q = q0 + 64 * wave + 16 * qt + 4 * g + r;
+            if (col == r && q < nq) {
+                uint32_t key = 0xFFFFFFFFu;  // empty train set (nt >= 1 always leaves a real key in the row max)
+                if (v != INT_MIN) {
+                    const int dot = v >> 16;
+                    const uint32_t d = (uint32_t)((256 - dot) >> 1);
+                    const uint32_t jj = 0xFFFFu - ((uint32_t)v & 0xFFFFu);
+                    key = (d << 16) | jj;
+                }
+                match_key[(int64_t)pair * max_kp + q] = key;
+            }
+        }
     }
 }
 
 void launch_match(const Desc* desc, const int32_t* kp_count, const int32_t* pairs, int n_pairs, int max_kp,
                   uint32_t* match_key, hipStream_t s) {
-    dim3 grid((max_kp + MT_QB - 1) / MT_QB, (max_kp + MT_TB - 1) / MT_TB, n_pairs);
+    dim3 grid((max_kp + MM_QB - 1) / MM_QB, n_pairs);
     hipLaunchKernelGGL(match_kernel, grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
 }
 
