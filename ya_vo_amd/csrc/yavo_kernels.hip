@@ -678,7 +678,7 @@ void launch_pack_desc(const yv_keypoint* keypoints, const int32_t* kp_count, int
 // their lane, for both operands alike, so the products pair matching bits whatever the hardware's k
 // order inside an instruction is.
 typedef int mm_v4i __attribute__((ext_vector_type(4)));
-constexpr int MM_QT = 4;                  // 16-row query tiles per wave
+constexpr int MM_QT = 8;                  // 16-row query tiles per wave
 constexpr int MM_QB = 4 * MM_QT * 16;     // queries per workgroup (4 waves)
 constexpr int MM_TC = 64;                 // train descriptors per LDS chunk
 constexpr int MM_ROW = 17;                // uint4 per expanded train row (16 + 1 pad: conflict-free b128 reads)
@@ -708,11 +708,11 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
     const Desc* qd = desc + (int64_t)qi * max_kp;
     const uint32_t* tw = reinterpret_cast<const uint32_t*>(desc + (int64_t)ti * max_kp);
 
-    // query fragments: tile qt row (lane & 15) = query q0 + 64 wave + 16 qt + (lane & 15)
+    // query fragments: tile qt row (lane & 15) = query q0 + 16 MM_QT wave + 16 qt + (lane & 15)
     mm_v4i A[MM_QT][4];
 #pragma unroll
     for (int qt = 0; qt < MM_QT; ++qt) {
-        const int q = q0 + 64 * wave + 16 * qt + col;
+        const int q = q0 + 16 * MM_QT * wave + 16 * qt + col;
         const Desc d = qd[q < nq ? q : 0];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -768,15 +768,19 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
             // key = (dot << 16) + bias: bias = 0xFFFF - j for a real train column; a column past nt gets
             // -2^30, below every real key (>= -2^24) and above INT_MIN, so no per-element select is needed
             const int bias = j < nt ? 0xFFFF - j : -(1 << 30);
+            // two query tiles' K-chains interleaved: every MFMA has an independent one beside it
 #pragma unroll
-            for (int qt = 0; qt < MM_QT; ++qt) {
-                mm_v4i acc = {0, 0, 0, 0};
+            for (int qt = 0; qt < MM_QT; qt += 2) {
+                mm_v4i acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
-                for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], B[s], acc, 0, 0, 0);
+                for (int s = 0; s < 4; ++s) {
+                    acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], B[s], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][s], B[s], acc1, 0, 0, 0);
+                }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int key = (int)(((uint32_t)acc[r] << 16) + (uint32_t)bias);
-                    best[qt][r] = max(best[qt][r], key);
+                    best[qt][r] = max(best[qt][r], (int)(((uint32_t)acc0[r] << 16) + (uint32_t)bias));
+                    best[qt + 1][r] = max(best[qt + 1][r], (int)(((uint32_t)acc1[r] << 16) + (uint32_t)bias));
                 }
             }
         }
@@ -793,7 +797,7 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
             int v = best[qt][r];
 #pragma unroll
             for (int m = 8; m > 0; m >>= 1) v = max(v, __shfl_xor(v, m, 16));
-            const int q = q0 + 64 * wave + 16 * qt + 4 * g + r;
+            const int q = q0 + 16 * MM_QT * wave + 16 * qt + 4 * g + r;
             if (col == r && q < nq) {
                 uint32_t key = 0xFFFFFFFFu;  // empty train set (nt >= 1 always leaves a real key in the row max)
                 if (v != INT_MIN) {
