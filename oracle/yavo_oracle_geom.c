@@ -725,8 +725,10 @@ static void edge_jacobian(const double* T, const double* K, const double* X, dou
 
 /* ---- summation orders ----
  * mode 0: sequential in edge order (the reference).  mode m >= 1: the GPU kernels' order over NT = 128 << m
- * threads (1: 256 threads, 2: 512): edge k adds into thread k % NT's partial, then the pairwise tree
- * p[t] += p[t + off] for off = NT/2 .. 1. */
+ * threads (1: 256 threads, the GN kernel; 2: 512, the pose-LM kernel): edge k adds into thread k % NT's
+ * partial.  Mode 1 then sums the pairwise tree p[t] += p[t + off] for off = NT/2 .. 1.  Mode 2 halves once
+ * (p[t] += p[t + 256]), sums each run of 16 partials left to right (q[s] = p[16s] + p[16s+1] + ... + p[16s+15])
+ * and finishes with the tree q[s] += q[s + off], off = 8, 4, 2, 1. */
 #define OR_NT_MAX 1024
 typedef struct { int mode, nt; double part[OR_NT_MAX]; } or_sum;
 
@@ -744,6 +746,17 @@ static double sum_total(or_sum* s) {
     if (s->mode == 0) return s->part[0];
     double p[OR_NT_MAX];
     memcpy(p, s->part, sizeof(double) * (size_t)s->nt);
+    if (s->mode == 2) {
+        double q[16];
+        for (int t = 0; t < 256; ++t) p[t] = p[t] + p[t + 256];
+        for (int g = 0; g < 16; ++g) {
+            q[g] = p[16 * g];
+            for (int i = 1; i < 16; ++i) q[g] = q[g] + p[16 * g + i];
+        }
+        for (int off = 8; off > 0; off >>= 1)
+            for (int g = 0; g < off; ++g) q[g] = q[g] + q[g + off];
+        return q[0];
+    }
     for (int off = s->nt / 2; off > 0; off >>= 1)
         for (int t = 0; t < off; ++t) p[t] = p[t] + p[t + off];
     return p[0];

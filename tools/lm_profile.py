@@ -19,8 +19,8 @@ import ya_vo_amd as yv  # noqa: E402
 from ya_vo_amd import scene  # noqa: E402
 from ya_vo_amd.synth import synth_stereo_batch  # noqa: E402
 
-PHASES = ["edge compute (lane 0's share)", "tree reduce + wait", "lane-0 exp/mul", "accept + barriers",
-          "classify/compact", "iteration setup", "lane-0 H copy + LDLT", "-"]
+PHASES = ["edge compute (lane 0's share)", "tree reduce proper", "lane-0 exp/mul", "accept + barriers",
+          "classify/compact", "iteration setup", "lane-0 T backup + LDLT", "lane-0 system copy (iteration)", "wait for other waves' edges", "-"]
 
 
 def main():
@@ -55,12 +55,12 @@ def main():
     if args.plain:
         print(f"track_pose {ms[6]:.4f} ms, track_edges {ms[5]:.4f} ms, frames {B}")
         return
-    prof = np.zeros((1024, 8), np.uint64)
+    prof = np.zeros((1024, 10), np.uint64)
     assert lib.yv_debug_lm_prof(prof.ctypes.data) == 0
     p = prof[1:B].astype(np.float64)  # track 0 reads the carry slot
-    tot = p[:, :7].sum(1)
+    tot = p[:, :9].sum(1)
     print(f"track_pose {ms[6]:.4f} ms, frames {B}; mean cycles per workgroup: total {tot.mean():.0f}")
-    for i in range(7):
+    for i in range(9):
         print(f"  {PHASES[i]:32s} {p[:, i].mean():12.0f}  ({100 * p[:, i].mean() / tot.mean():5.1f}%)")
     b.close()
     ctx.close()

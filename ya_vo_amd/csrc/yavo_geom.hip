@@ -29,10 +29,10 @@ constexpr int kLMNT = 512;        // threads per pose-LM workgroup: 2 waves per 
 
 // YAVO_LM_PROFILE builds (tools/lm_profile.py) time the pose-LM phases with the shader clock on lane 0
 #ifdef YAVO_LM_PROFILE
-__device__ unsigned long long g_lm_prof[1024][8];
-#define LMP_DECL unsigned long long lmp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long lmp_t = __builtin_readcyclecounter();
+__device__ unsigned long long g_lm_prof[1024][10];
+#define LMP_DECL unsigned long long lmp_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long lmp_t = __builtin_readcyclecounter();
 #define LMP_MARK(slot) do { const unsigned long long t_ = __builtin_readcyclecounter(); lmp_acc[slot] += t_ - lmp_t; lmp_t = t_; } while (0)
-#define LMP_STORE() do { if (threadIdx.x == 0) for (int q_ = 0; q_ < 8; ++q_) g_lm_prof[blockIdx.x & 1023][q_] = lmp_acc[q_]; } while (0)
+#define LMP_STORE() do { if (threadIdx.x == 0) for (int q_ = 0; q_ < 10; ++q_) g_lm_prof[blockIdx.x & 1023][q_] = lmp_acc[q_]; } while (0)
 #else
 #define LMP_DECL
 #define LMP_MARK(slot) do {} while (0)
@@ -930,6 +930,117 @@ __device__ bool ldlt6_solve_perm(const double* Hp, double lambda, const double* 
     return positive;
 }
 
+// ldlt6_solve_perm for an LDS-resident system: Hf the full symmetric 6x6 (row-major), bs the right-hand
+// side, xs the solution (all LDS); P b and P^T v are indexed LDS accesses rather than select chains.
+template <int variant>
+__device__ bool ldlt6_solve_lds(const double* Hf, double lambda, const double* bs, double* xs) {
+    constexpr int n = 6;
+    double dg[6];
+    int id[6];
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+        dg[i] = Hf[i * 7] + lambda;
+        id[i] = i;
+    }
+#pragma unroll
+    for (int k = 0; k < n; ++k) {
+        int big = k;
+        double bv = fabs(dg[k]);
+#pragma unroll
+        for (int i = k + 1; i < n; ++i)
+            if (fabs(dg[i]) > bv) {
+                bv = fabs(dg[i]);
+                big = i;
+            }
+        const double dk = dg[k];
+        const int ik = id[k];
+#pragma unroll
+        for (int c = k + 1; c < n; ++c) {
+            const bool sw = c == big;
+            dg[k] = sw ? dg[c] : dg[k];
+            id[k] = sw ? id[c] : id[k];
+            dg[c] = sw ? dk : dg[c];
+            id[c] = sw ? ik : id[c];
+        }
+    }
+    const bool zero0 = !(fabs(dg[0]) > 0);  // Eigen's k == 0 early exit: no transposition, no factorization
+    if (zero0) {
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            id[i] = i;
+            dg[i] = Hf[i * 7] + lambda;
+        }
+    }
+    double m[36];
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+        const double* row = Hf + id[i] * 6;
+#pragma unroll
+        for (int j = 0; j < i; ++j) m[i * 6 + j] = row[id[j]];
+        m[i * 7] = dg[i];
+    }
+    int sign = 0;
+    int found_zero_pivot = 0;
+    if (!zero0) {
+#pragma unroll
+        for (int k = 0; k < n; ++k) {
+            if (k > 0) {
+                double temp[6];
+#pragma unroll
+                for (int j = 0; j < k; ++j) temp[j] = m[j * 7] * m[k * 6 + j];
+                double dot = m[k * 6 + 0] * temp[0];
+#pragma unroll
+                for (int j = 1; j < k; ++j) dot = dot + m[k * 6 + j] * temp[j];
+                m[k * 7] -= dot;
+#pragma unroll
+                for (int i = k + 1; i < n; ++i) {
+                    if (variant == 0) {
+                        double acc = m[i * 6 + k];
+#pragma unroll
+                        for (int j = 0; j < k; ++j) acc = acc - m[i * 6 + j] * temp[j];
+                        m[i * 6 + k] = acc;
+                    } else {
+                        double d = m[i * 6 + 0] * temp[0];
+#pragma unroll
+                        for (int j = 1; j < k; ++j) d = d + m[i * 6 + j] * temp[j];
+                        m[i * 6 + k] = m[i * 6 + k] - d;
+                    }
+                }
+            }
+            const double akk = m[k * 7];
+            const int valid = fabs(akk) > 0;
+            if (k + 1 < n && valid) {
+#pragma unroll
+                for (int i = k + 1; i < n; ++i) m[i * 6 + k] /= akk;
+            }
+            if (!(found_zero_pivot && valid) && !valid) found_zero_pivot = 1;
+            if (sign == 1) { if (akk < 0) sign = 3; }
+            else if (sign == 2) { if (akk > 0) sign = 3; }
+            else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+        }
+    }
+    const bool positive = (sign == 1 || sign == 0);
+    double v[6];
+#pragma unroll
+    for (int i = 0; i < n; ++i) v[i] = bs[id[i]];  // v = P b
+#pragma unroll
+    for (int j = 0; j < n; ++j)
+#pragma unroll
+        for (int i = j + 1; i < n; ++i) v[i] = v[i] - m[i * 6 + j] * v[j];
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+        if (fabs(m[i * 7]) > DBL_MIN) v[i] /= m[i * 7];
+        else v[i] = 0;
+    }
+#pragma unroll
+    for (int j = n - 1; j >= 0; --j)
+#pragma unroll
+        for (int i = 0; i < j; ++i) v[i] = v[i] - m[j * 6 + i] * v[j];
+#pragma unroll
+    for (int i = 0; i < n; ++i) xs[id[i]] = v[i];  // x = P^T v
+    return positive;
+}
+
 // ------------------------------------------------------------------------------------------------
 // pose-only LM (g2o semantics) and GN, one workgroup per problem
 // ------------------------------------------------------------------------------------------------
@@ -973,9 +1084,12 @@ __device__ __forceinline__ double huber_rho(double e2, double* rho1) {
 // thread's nv partials; totals land in out[0..nv) (LDS), visible after the trailing barrier.
 // red: >= nv * NT/2 doubles of LDS.
 template <int NV, int NT = kNT>
-__device__ void tree_reduce(double (&part)[NV], double* red, double* out) {
+__device__ void tree_reduce(double (&part)[NV], double* red, double* out, unsigned long long* t_sync = nullptr) {
     const int tid = threadIdx.x;
     __syncthreads();
+#ifdef YAVO_LM_PROFILE
+    if (t_sync) *t_sync = __builtin_readcyclecounter();
+#endif
 #pragma unroll
     for (int off = NT / 2; off >= 128; off >>= 1) {
         if (tid >= off && tid < 2 * off) {
@@ -1016,9 +1130,51 @@ __device__ void tree_reduce(double (&part)[NV], double* red, double* out) {
     __syncthreads();
 }
 
+// The pose LM's reduction of NV per-thread partials over kLMNT = 512 threads (oracle sum_mode 2):
+// p[t] += p[t + 256]; then thread (v, g) sums run g of 16 partials of value v left to right from a bank-padded
+// LDS image ([v][g][17]: conflict-free both when written by consecutive threads and when 16 threads read 16
+// runs); the 16 run sums of a value sit on 16 adjacent lanes and finish with the tree q[g] += q[g + off],
+// off = 8 .. 1.  Three barriers; one value per thread in the serial part instead of NV values in one wave.
+constexpr int kSegPad = 17;
+template <int NV>
+__device__ void seg_reduce(double (&part)[NV], double* red /* >= NV * 16 * kSegPad */, double* out,
+                           unsigned long long* t_sync = nullptr) {
+    static_assert(NV * 16 <= kLMNT, "one thread per (value, run)");
+    const int tid = threadIdx.x;
+    __syncthreads();
+#ifdef YAVO_LM_PROFILE
+    if (t_sync) *t_sync = __builtin_readcyclecounter();
+#endif
+    const int e = tid & 255;                         // partial index after the halving
+    const int slot = (e >> 4) * kSegPad + (e & 15);  // [g][i] with padded runs
+    if (tid >= 256) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) red[v * 16 * kSegPad + slot] = part[v];
+    }
+    __syncthreads();
+    if (tid < 256) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) red[v * 16 * kSegPad + slot] = part[v] + red[v * 16 * kSegPad + slot];
+    }
+    __syncthreads();
+    double q = 0.0;
+    const int v = tid >> 4, g = tid & 15;
+    if (tid < NV * 16) {
+        const double* r = red + v * 16 * kSegPad + g * kSegPad;
+        q = r[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) q = q + r[i];
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) q = q + __shfl_down(q, off, 16);
+    if (tid < NV * 16 && g == 0) out[v] = q;
+    __syncthreads();
+}
+
 struct LMShared {
     double T[7], Tbak[7], Tlast[7], K[9];
     double sys[28], x[6], vals[32];  // sys: {H lower packed (21), b (6), chi2} of the current iteration
+    double Hf[36];                     // the same H, full symmetric (the LDLT's gather source)
     double lambda, ni, currentChi, tempChi, rho;
     int flag;  // control broadcast from lane 0
 };
@@ -1115,13 +1271,17 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
 #ifdef YAVO_LM_PROFILE
     const unsigned long long p1 = __builtin_readcyclecounter();
 #endif
-    tree_reduce<kLMVals, kLMNT>(part, s_red, S.vals);
 #ifdef YAVO_LM_PROFILE
+    unsigned long long ps = 0;
+    seg_reduce<kLMVals>(part, s_red, S.vals, &ps);
     if (lmp) {
         const unsigned long long p2 = __builtin_readcyclecounter();
         lmp[0] += p1 - p0;
-        lmp[1] += p2 - p1;
+        lmp[1] += p2 - ps;  // the reduction proper
+        lmp[8] += ps - p1;  // waiting at the first barrier for the other waves' edges
     }
+#else
+    seg_reduce<kLMVals>(part, s_red, S.vals);
 #endif
 }
 
@@ -1135,7 +1295,7 @@ __global__ __launch_bounds__(kLMNT) void pose_lm_kernel(const int32_t* __restric
                                                       uint8_t* __restrict__ outlier_all, int32_t* __restrict__ inliers) {
     __shared__ uint8_t s_level[kMaxEdges], s_out[kMaxEdges], s_robust[kMaxEdges];
     __shared__ int16_t s_active[kMaxEdges];
-    __shared__ double s_red[kLMVals * (kLMNT / 2)];
+    __shared__ double s_red[kLMVals * 16 * kSegPad];
     __shared__ LMShared S;
     __shared__ int s_tmp[40];
     LMP_DECL
@@ -1193,6 +1353,13 @@ __global__ __launch_bounds__(kLMNT) void pose_lm_kernel(const int32_t* __restric
                     for (int v = 0; v < 28; ++v) sys[v] = S.vals[v];
 #pragma unroll
                     for (int v = 0; v < 28; ++v) S.sys[v] = sys[v];
+#pragma unroll
+                    for (int r = 0; r < 6; ++r)
+#pragma unroll
+                        for (int c = 0; c <= r; ++c) {
+                            S.Hf[r * 6 + c] = sys[r * (r + 1) / 2 + c];
+                            S.Hf[c * 6 + r] = sys[r * (r + 1) / 2 + c];
+                        }
                     S.currentChi = sys[27];
                     if (it == 0) {
                         double maxDiag = 0;
@@ -1205,6 +1372,7 @@ __global__ __launch_bounds__(kLMNT) void pose_lm_kernel(const int32_t* __restric
                         ni = 2;
                     }
                 }
+                LMP_MARK(7);
                 // trial loop (do ... while (rho < 0 && qmax < 10))
                 int qmax = 0;
                 int f = 0;
@@ -1215,9 +1383,9 @@ __global__ __launch_bounds__(kLMNT) void pose_lm_kernel(const int32_t* __restric
                         for (int q = 0; q < 7; ++q) Tc[q] = S.T[q];
 #pragma unroll
                         for (int q = 0; q < 7; ++q) S.Tbak[q] = Tc[q];
-                        const int ok2 = ldlt6_solve_perm<0>(S.sys, lambda, S.sys + 21, xs) ? 1 : 0;
+                        const int ok2 = ldlt6_solve_lds<0>(S.Hf, lambda, S.sys + 21, S.x) ? 1 : 0;
 #pragma unroll
-                        for (int q = 0; q < 6; ++q) S.x[q] = xs[q];
+                        for (int q = 0; q < 6; ++q) xs[q] = S.x[q];
                         LMP_MARK(6);
                         double Tn[7], Tnew[7];
                         se3_exp(xs, Tn);
@@ -1519,7 +1687,7 @@ void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, con
 #ifdef YAVO_LM_PROFILE
 // profiling builds only (lib/libyavo_prof.so): per-workgroup pose-LM phase cycle counts of the last launch
 extern "C" int yv_debug_lm_prof(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(yavo::geom::g_lm_prof), sizeof(unsigned long long) * 1024 * 8) ==
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(yavo::geom::g_lm_prof), sizeof(unsigned long long) * 1024 * 10) ==
                    hipSuccess ? 0 : -2;
 }
 #endif
