@@ -281,6 +281,7 @@ int yv_batch_create(yv_ctx* ctx, int max_images, int H, int W, int max_kp, int m
     if (!ctx || !out || max_images <= 0 || H < 9 || W < 9 || max_kp <= 0 || max_kp > yavo::kMaxKp ||
         max_pairs < 0 || (int64_t)H * W >= (1ll << 31))
         return YV_ERR_INVALID;
+    if (W > yavo::kMaxWidth) return YV_ERR_CAPACITY;  // BRIEF stages 49 image rows in LDS
     *out = nullptr;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
     yv_batch* b = new (std::nothrow) yv_batch();

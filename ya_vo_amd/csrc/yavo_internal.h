@@ -8,7 +8,8 @@
 
 namespace yavo {
 
-constexpr int kMaxKp = 4096;       // per-image keypoint capacity supported by the top-K / scan kernels
+constexpr int kMaxKp = 4096;
+constexpr int kMaxWidth = 2048;  // image width limit (BRIEF keeps 49 rows of the blurred image in LDS)       // per-image keypoint capacity supported by the top-K / scan kernels
 constexpr int kFastTileW = 64;     // FAST / blur output tile: one wave per tile row
 constexpr int kFastTileH = 32;
 

@@ -559,9 +559,8 @@ void launch_kp_boundary(const int32_t* det_rc, const int32_t* det_count, int n_i
 }
 
 // ------------------------------------------------------------------------------------------------
-// BRIEF: one wave per keypoint; lane l evaluates tests l, l+64, l+128, l+192 -> 4 ballots = 256 bits
+// BRIEF
 // ------------------------------------------------------------------------------------------------
-constexpr int BR_KP_PER_WAVE = 4;
 
 // v[idx] for a small register array without dynamic indexing (keeps it out of scratch).
 template <int N>
@@ -572,49 +571,94 @@ __device__ __forceinline__ uint32_t reg_select(const uint32_t (&v)[N], int idx) 
     return r;
 }
 
-__device__ __forceinline__ int blur_pix(const uint8_t* b, int64_t n, int64_t idx) {
-    // getPixelVal(i, j) = data[i*cols + j]: the linear index may wrap into the next row (reproduced);
-    // past the buffer end the reference reads out of bounds (UB) -> 0 here.
-    return (idx >= 0 && idx < n) ? (int)b[idx] : 0;
-}
+// One workgroup per (32-row band, image): the band's keypoints (rows [r0, r0 + 32)) read their 17 x 17
+// patches from an LDS copy of the blurred rows [r0 - 8, r0 + 41) -- stored with row stride W, so the
+// reference's linear index (row + dr) * W + (col + dc) (which wraps into the neighbouring row at the
+// image's left/right edge, src/BriefDescriptor.cc getPixelVal) addresses it unchanged.  One wave per
+// keypoint: lane l evaluates tests l, l + 64, l + 128, l + 192 -> 4 ballots = 256 bits.
+constexpr int BR_BAND = 32;
+constexpr int BR_ROWS = BR_BAND + 17;  // rows r0-8 .. r0+40 (the last one for the wrap of col + 8 == W)
 
 __global__ __launch_bounds__(256) void brief_kernel(const uint8_t* __restrict__ blur, int H, int W,
                                                     const int8_t* __restrict__ offsets,
                                                     const int32_t* __restrict__ kp_src,
                                                     const int32_t* __restrict__ kp_count, int max_kp,
                                                     yv_keypoint* __restrict__ keypoints, Desc* __restrict__ desc) {
+    extern __shared__ uint8_t s_band[];  // BR_ROWS * W + 32 bytes
+    __shared__ int16_t s_list[kMaxKp];
+    __shared__ int s_n;
     const int img = blockIdx.y;
-    const int lane = lane_id();
-    const int wave = (int)threadIdx.x >> 6;
+    const int r0 = blockIdx.x * BR_BAND;
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int n = kp_count[img];
-    const int first = (blockIdx.x * 4 + wave) * BR_KP_PER_WAVE;
-    if (first >= n) return;
+    const int4* src = reinterpret_cast<const int4*>(kp_src) + (int64_t)img * max_kp;
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    // 1. this band's keypoints (any order: each keypoint's outputs go to its own index); all row loads are
+    // issued before the first use
+    const int nscan = (n + 255) >> 8;
+    int next_row = tid < n ? src[tid].x : -1;  // software-pipelined: the next row load is in flight
+    for (int u = 0; u < nscan; ++u) {
+        const int i = u * 256 + tid;
+        const int row = next_row;
+        const int inext = i + 256;
+        next_row = inext < n ? src[inext].x : -1;
+        const bool mine = i < n && row >= r0 && row < r0 + BR_BAND;
+        const uint64_t bal = __ballot(mine);
+        int wbase = 0;
+        if (lane == 0 && bal) wbase = atomicAdd(&s_n, (int)__popcll(bal));
+        wbase = __shfl(wbase, 0, 64);
+        if (mine) s_list[wbase + (int)__popcll(bal & ((1ull << lane) - 1))] = (int16_t)i;
+    }
+    __syncthreads();
+    const int nb = s_n;
+    if (nb == 0) return;
+    // 2. stage the band: linear bytes [L0, L1) of the image, from a 16-B aligned global address; each
+    // thread's loads are all in flight before the LDS writes (H * W < 2^31: 32-bit indices)
     const uint8_t* b = blur + (int64_t)img * H * W;
-    const int64_t npix = (int64_t)H * W;
-    // offsets of this lane's four tests: rows l, l+64, l+128, l+192 of the 256 x 4 table
-    int o[4][4];
+    const int npix = H * W;
+    const int L0 = max(0, r0 - 8) * W;
+    const int L1 = min(npix, (r0 + BR_BAND + 9) * W);
+    const uintptr_t g0 = reinterpret_cast<uintptr_t>(b + L0);
+    const int sh = (int)(g0 & 15);
+    const uint4* gal = reinterpret_cast<const uint4*>(g0 - sh);
+    const int nbytes = (L1 - L0) + sh;  // bytes from gal to the end of the range
+    const int nfull = nbytes >> 4;
+    uint4* s4 = reinterpret_cast<uint4*>(s_band);
+    // 8 16-B words in flight per thread (written out: an array here is not kept in registers); indices are
+    // clamped so every load is a valid word inside [gal, b + L1)
+    for (int k0 = tid; k0 < nfull; k0 += 8 * 256) {
+        const int last = nfull - 1;
+        const uint4 v0 = gal[min(k0, last)], v1 = gal[min(k0 + 256, last)], v2 = gal[min(k0 + 512, last)],
+                    v3 = gal[min(k0 + 768, last)], v4 = gal[min(k0 + 1024, last)], v5 = gal[min(k0 + 1280, last)],
+                    v6 = gal[min(k0 + 1536, last)], v7 = gal[min(k0 + 1792, last)];
+        s4[k0] = v0;
+        if (k0 + 256 < nfull) s4[k0 + 256] = v1;
+        if (k0 + 512 < nfull) s4[k0 + 512] = v2;
+        if (k0 + 768 < nfull) s4[k0 + 768] = v3;
+        if (k0 + 1024 < nfull) s4[k0 + 1024] = v4;
+        if (k0 + 1280 < nfull) s4[k0 + 1280] = v5;
+        if (k0 + 1536 < nfull) s4[k0 + 1536] = v6;
+        if (k0 + 1792 < nfull) s4[k0 + 1792] = v7;
+    }
+    for (int k = nfull * 16 + tid; k < nbytes; k += 256)  // tail bytes
+        s_band[k] = reinterpret_cast<const uint8_t*>(gal)[k];
+    __syncthreads();
+    // 3. descriptors.  Each lane's 8 sample offsets as linear offsets dr * W + dc (the reference's index is
+    // (row + dr) * W + (col + dc) = row * W + col + (dr * W + dc)).
+    int ol[4][2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const uint32_t packed = reinterpret_cast<const uint32_t*>(offsets)[lane + 64 * t];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[t][q] = (int)(int8_t)((packed >> (8 * q)) & 0xFFu);
+        const int o0 = (int)(int8_t)(packed & 0xFFu), o1 = (int)(int8_t)((packed >> 8) & 0xFFu);
+        const int o2 = (int)(int8_t)((packed >> 16) & 0xFFu), o3 = (int)(int8_t)((packed >> 24) & 0xFFu);
+        ol[t][0] = o0 * W + o1;
+        ol[t][1] = o2 * W + o3;
     }
-    const int4* src = reinterpret_cast<const int4*>(kp_src) + (int64_t)img * max_kp;
     uint32_t* rec_base = reinterpret_cast<uint32_t*>(keypoints + (int64_t)img * max_kp);
     Desc* d_base = desc + (int64_t)img * max_kp;
-    for (int kk = 0; kk < BR_KP_PER_WAVE; ++kk) {
-        const int i = first + kk;
-        if (i >= n) break;
-        const int4 kp = src[i];
-        const int row = kp.x, col = kp.y;
-        uint64_t w[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int64_t i1 = (int64_t)(row + o[t][0]) * W + (col + o[t][1]);
-            const int64_t i2 = (int64_t)(row + o[t][2]) * W + (col + o[t][3]);
-            const bool bit = blur_pix(b, npix, i1) > blur_pix(b, npix, i2);
-            w[t] = __ballot(bit);
-        }
+    const int lds_off = sh - L0;  // LDS index of linear pixel L = L + lds_off
+    auto emit = [&](int i, const int4 kp, const uint64_t (&w)[4]) {
         // descriptor (32 B) and the 48-B KeyPoint record {x, y, id, matched=0, featVec[32], pad 0}
         uint32_t bd[9];
 #pragma unroll
@@ -623,8 +667,8 @@ __global__ __launch_bounds__(256) void brief_kernel(const uint8_t* __restrict__ 
         if (lane < 8) d_base[i].w[lane] = reg_select(bd, lane);
         if (lane < 12) {
             uint32_t v;
-            if (lane == 0) v = (uint32_t)row;
-            else if (lane == 1) v = (uint32_t)col;
+            if (lane == 0) v = (uint32_t)kp.x;
+            else if (lane == 1) v = (uint32_t)kp.y;
             else if (lane == 2) v = (uint32_t)kp.z;
             else {
                 const int m = lane - 3;  // record dword 3+m = featVec bytes shifted by one (matched byte first)
@@ -634,14 +678,35 @@ __global__ __launch_bounds__(256) void brief_kernel(const uint8_t* __restrict__ 
             }
             rec_base[(int64_t)i * 12 + lane] = v;
         }
+    };
+    // two keypoints per iteration: 16 LDS reads per lane in flight
+    for (int k = wave; k < nb; k += 8) {
+        const bool two = k + 4 < nb;
+        const int ia = s_list[k], ib = two ? s_list[k + 4] : ia;
+        const int4 kpa = src[ia], kpb = src[ib];
+        const int la = kpa.x * W + kpa.y, lb = kpb.x * W + kpb.y;
+        uint64_t wa[4], wb[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            // getPixelVal's linear index; past the image end the reference reads out of bounds -> 0
+            const int a1 = la + ol[t][0], a2 = la + ol[t][1], b1 = lb + ol[t][0], b2 = lb + ol[t][1];
+            const int pa1 = a1 < npix ? (int)s_band[a1 + lds_off] : 0;
+            const int pa2 = a2 < npix ? (int)s_band[a2 + lds_off] : 0;
+            const int pb1 = b1 < npix ? (int)s_band[b1 + lds_off] : 0;
+            const int pb2 = b2 < npix ? (int)s_band[b2 + lds_off] : 0;
+            wa[t] = __ballot(pa1 > pa2);
+            wb[t] = __ballot(pb1 > pb2);
+        }
+        emit(ia, kpa, wa);
+        if (two) emit(ib, kpb, wb);
     }
 }
 
 void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t* offsets, const int32_t* kp_src,
                   const int32_t* kp_count, int max_kp, yv_keypoint* keypoints, Desc* desc, hipStream_t s) {
-    const int per_block = 4 * BR_KP_PER_WAVE;
-    dim3 grid((max_kp + per_block - 1) / per_block, n_images);
-    hipLaunchKernelGGL(brief_kernel, grid, dim3(256), 0, s, blur, H, W, offsets, kp_src, kp_count, max_kp,
+    dim3 grid((H + BR_BAND - 1) / BR_BAND, n_images);
+    const size_t lds = (size_t)BR_ROWS * W + 32;
+    hipLaunchKernelGGL(brief_kernel, grid, dim3(256), lds, s, blur, H, W, offsets, kp_src, kp_count, max_kp,
                        keypoints, desc);
 }
 
