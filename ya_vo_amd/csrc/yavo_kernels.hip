@@ -164,30 +164,52 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
     __shared__ uint8_t tile[FT_LH * FT_LW];
     __shared__ uint32_t hbuf[kBlur ? (FT_LH / 2) * FT_W : 1];
     __shared__ uint16_t s_pos[FT_W * FT_H];
-    __shared__ uint32_t s_n, s_base;
+    __shared__ uint16_t s_pre[FT_W * FT_H];
+    __shared__ uint32_t s_n, s_npre, s_base;
     const int img = blockIdx.z;
     const int r0 = blockIdx.y * FT_H, c0 = blockIdx.x * FT_W;
     const uint8_t* src = imgs + (int64_t)img * pitch;
     const int tid = threadIdx.x;
     const int lane = lane_id();
     const int wave = tid >> 6;
-    if (tid == 0) s_n = 0;
+    if (tid == 0) {
+        s_n = 0;
+        s_npre = 0;
+    }
 
     // stage (FT_H + 8) x (FT_W + 8): wave w loads rows w, w+4, ...; lanes 0..63 (+ 0..7) cover 72 columns
     const int cA = reflect101(min(max(c0 - FT_R + lane, -(W - 1)), 2 * W - 2), W);
     const int cB = reflect101(min(max(c0 - FT_R + 64 + (lane & 7), -(W - 1)), 2 * W - 2), W);
-    for (int lr = wave; lr < FT_LH; lr += 4) {
+    // all of this wave's row loads are issued before the first LDS write (10 HBM round trips -> 1)
+    constexpr int kRowsPerWave = FT_LH / 4;
+    static_assert(FT_LH % 4 == 0, "rows split evenly over the 4 waves");
+    uint8_t va[kRowsPerWave], vb[kRowsPerWave];
+#pragma unroll
+    for (int u = 0; u < kRowsPerWave; ++u) {
+        const int lr = wave + 4 * u;
         const int r = reflect101(min(max(r0 - FT_R + lr, -(H - 1)), 2 * H - 2), H);
         const uint8_t* row = src + (int64_t)r * stride;
-        const uint8_t a = row[cA];
-        tile[lr * FT_LW + lane] = a;
-        if (lane < FT_LW - 64) tile[lr * FT_LW + 64 + lane] = row[cB];
+        va[u] = row[cA];
+        vb[u] = row[cB];
+    }
+#pragma unroll
+    for (int u = 0; u < kRowsPerWave; ++u) {
+        const int lr = wave + 4 * u;
+        tile[lr * FT_LW + lane] = va[u];
+        if (lane < FT_LW - 64) tile[lr * FT_LW + 64 + lane] = vb[u];
     }
     __syncthreads();
 
     constexpr int ring_dr[16] = YV_RING_DR;
     constexpr int ring_dc[16] = YV_RING_DC;
     const uint32_t neg_thr = (uint32_t)(-thr);
+    // checkInBetween(cent, p) <=> cent > p - thr && cent < p + thr <=> |cent - p| - thr < 0: v_sad_u8 gives
+    // |cent - p| + (-thr) in one instruction; its sign bit is "similar"
+    auto similar = [&](const uint8_t* t0, uint32_t cent, int k) -> uint32_t {
+        return __builtin_amdgcn_sad_u8(cent, (uint32_t)t0[ring_dr[k] * FT_LW + ring_dc[k]], neg_thr) >> 31;
+    };
+    // phase 1: the reference's pretest on ring pixels 0, 7 and (4 | 12) (src/FastDetector.cc:304-317) for
+    // every pixel; the few that pass are compacted into s_pre
     const int tx = lane, ty = wave;
     const int c = c0 + tx;
     for (int rr = ty; rr < FT_H; rr += 4) {
@@ -195,32 +217,46 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         const bool inside = (r >= 4) && (r < H - 4) && (c >= 4) && (c < W - 4);
         const uint8_t* t0 = &tile[(rr + FT_R) * FT_LW + tx + FT_R];
         const uint32_t cent = t0[0];
-        uint32_t sim = 0;
+        const uint32_t s0 = similar(t0, cent, 0), s7 = similar(t0, cent, 7);
+        const uint32_t s4 = similar(t0, cent, 4), s12 = similar(t0, cent, 12);
+        const bool pre = inside && !(s0 | s7) && !(s4 & s12);
+        const uint64_t bal = __ballot(pre);
+        if (bal == 0) continue;  // wave-uniform
+        const int leader = __ffsll((long long)bal) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&s_npre, (uint32_t)__popcll(bal));
+        base = __shfl(base, leader, 64);
+        if (pre) s_pre[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(rr * FT_W + tx);
+    }
+    __syncthreads();
+    // phase 2: the full 16-pixel test (>= 12 consecutive "different" ring pixels, no wrap:
+    // checkContiguousPixels) densely over the pretest survivors; corners are staged in s_pos
+    const uint32_t npre = s_npre;
+    for (uint32_t i0 = 0; i0 < npre; i0 += 256) {  // uniform trip count: the ballots below see whole waves
+        const uint32_t i = i0 + tid;
+        bool cand = false;
+        int pos = 0;
+        if (i < npre) {
+            pos = s_pre[i];
+            const uint8_t* t0 = &tile[((pos >> 6) + FT_R) * FT_LW + (pos & 63) + FT_R];
+            const uint32_t cent = t0[0];
+            uint32_t sim = 0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint32_t p = t0[ring_dr[k] * FT_LW + ring_dc[k]];
-            // checkInBetween(cent, p) <=> cent > p - thr && cent < p + thr <=> |cent - p| - thr < 0:
-            // v_sad_u8 gives |cent - p| + (-thr) in one instruction; its sign bit is "similar"
-            const uint32_t t = __builtin_amdgcn_sad_u8(cent, p, neg_thr);
-            sim |= (t >> 31) << k;
+            for (int k = 0; k < 16; ++k) sim |= similar(t0, cent, k) << k;
+            const uint32_t mask = ~sim & 0xFFFFu;  // "different" ring pixels
+            const uint32_t a2 = mask & (mask >> 1);
+            const uint32_t a4 = a2 & (a2 >> 2);
+            const uint32_t a8 = a4 & (a4 >> 4);
+            const uint32_t a12 = a8 & (a4 >> 8);
+            cand = a12 != 0u;
         }
-        const uint32_t mask = ~sim & 0xFFFFu;  // "different" ring pixels
-        // pretest on ring indices 0, 7 and (4 | 12) (src/FastDetector.cc:304-317)
-        const bool pre = (mask & 1u) && (mask & (1u << 7)) && ((mask & (1u << 4)) || (mask & (1u << 12)));
-        // >= 12 consecutive set bits in mask[0..15], no wrap (checkContiguousPixels)
-        const uint32_t a2 = mask & (mask >> 1);
-        const uint32_t a4 = a2 & (a2 >> 2);
-        const uint32_t a8 = a4 & (a4 >> 4);
-        const uint32_t a12 = a8 & (a4 >> 8);
-        const bool cand = inside && pre && (a12 != 0u);
         const uint64_t bal = __ballot(cand);
-        if (bal == 0) continue;  // wave-uniform: no corner in this 64-pixel row segment
-        // stage the corner's tile position; Harris runs densely over the staged list below
+        if (bal == 0) continue;
         const int leader = __ffsll((long long)bal) - 1;
         uint32_t base = 0;
         if (lane == leader) base = atomicAdd(&s_n, (uint32_t)__popcll(bal));
         base = __shfl(base, leader, 64);
-        if (cand) s_pos[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(rr * FT_W + tx);
+        if (cand) s_pos[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)pos;
     }
     __syncthreads();
     const uint32_t n = s_n;
