@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=["both", "literal", "efficient", "none"], default="both")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-timing", action="store_true", help="do not record per-stage HIP events")
+    ap.add_argument("--no-overlap", action="store_true", help="run the pose LM in order on the main stream")
     return ap.parse_args()
 
 
@@ -171,15 +172,21 @@ def main():
     batch.set_tracks(tracks, scene.K_KITTI, T_RIGHT)
     identity = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
     d_prior = torch.from_numpy(np.tile(identity, (B, 1))).to(dev)
-    d_pose = torch.zeros((B, 7), dtype=torch.float64, device=dev)
+    # the pose LM of step i runs on the batch's side stream beside step i + 1's image kernels; its output
+    # buffer alternates so step i + 1 never writes poses step i's LM is still producing
+    batch.set_track_overlap(not args.no_overlap)
+    d_poses = [torch.zeros((B, 7), dtype=torch.float64, device=dev) for _ in range(2)]
+    calls = [0]
 
     def step():
         batch.run(d_frames.data_ptr(), n_img, W, H * W, 20, carry_from=2 * (B - 1))
-        batch.track(d_prior.data_ptr(), d_pose.data_ptr())
+        batch.track(d_prior.data_ptr(), d_poses[calls[0] & 1].data_ptr())
+        calls[0] += 1
 
     for _ in range(args.warmup):
         step()
     ctx.sync()
+    batch.track_sync()
     torch.cuda.synchronize()
     if not args.no_timing:
         batch.enable_timing(True)
@@ -191,6 +198,7 @@ def main():
     for _ in range(args.steps):
         step()
     ctx.sync()
+    batch.track_sync()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -211,7 +219,7 @@ def main():
     counts["edges"] = float(np.sum(ctx.download(v.edge_count, np.int32, B)))
     counts["tq"] = float(np.sum([counts["match"][tp] for _, tp in tracks]))
     inliers = ctx.download(v.track_inliers, np.int32, B)
-    gpu_poses = d_pose.cpu().numpy()
+    gpu_poses = d_poses[(calls[0] - 1) & 1].cpu().numpy()
 
     stages = {}
     roofline = None

@@ -115,6 +115,12 @@ int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks /* [2*n_tracks] */, i
 /* Build the track edges and solve every track's pose in one launch each (asynchronous on `stream`, NULL =
  * context stream).  d_priors [n_tracks][7] in, d_poses [n_tracks][7] out (may alias d_priors). */
 int yv_batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stream);
+/* Overlap mode: the pose LM of each yv_batch_track runs on a stream of the batch, ordered after that call's
+ * edge build only, so it executes beside the next yv_batch_run's kernels (edge buffers alternate between
+ * two copies; the build of track i + 2 waits for the LM of track i).  d_priors / d_poses / the track views
+ * are then complete only after yv_batch_track_sync (or a device-wide synchronization). */
+int yv_batch_set_track_overlap(yv_batch* b, int on);
+int yv_batch_track_sync(yv_batch* b);
 /* Per-stage device time of the runs since the last reset, when timing is enabled (HIP events recorded
  * on the run stream around every stage).  Stages: 0 detect (FAST + Harris + blur, one fused kernel),
  * 1 top-K + checkBoundry, 2 BRIEF, 3 match, 4 Matches records + removeOutliers (+ carry copies),
@@ -144,7 +150,7 @@ typedef struct yv_batch_view {
      * (kept iff distance < limit) of every pair */
     const int32_t* match_dj;          /* [max_pairs][max_kp][2] */
     const int32_t* match_lim;         /* [max_pairs] */
-    /* tracks (yv_batch_set_tracks / yv_batch_track) */
+    /* tracks (yv_batch_set_tracks / yv_batch_track): the buffers of the last yv_batch_track call */
     int n_tracks;
     const int32_t* edge_count;        /* [n_tracks] */
     const double* edge_X;             /* [n_tracks][max_kp][3] */

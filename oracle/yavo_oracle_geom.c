@@ -726,15 +726,16 @@ static void edge_jacobian(const double* T, const double* K, const double* X, dou
 /* ---- summation orders ----
  * mode 0: sequential in edge order (the reference).  mode m >= 1: the GPU kernels' order over NT = 128 << m
  * threads (1: 256 threads, the GN kernel; 2: 512, the pose-LM kernel): edge k adds into thread k % NT's
- * partial.  Mode 1 then sums the pairwise tree p[t] += p[t + off] for off = NT/2 .. 1.  Mode 2 halves once
- * (p[t] += p[t + 256]), sums each run of 16 partials left to right (q[s] = p[16s] + p[16s+1] + ... + p[16s+15])
- * and finishes with the tree q[s] += q[s + off], off = 8, 4, 2, 1. */
+ * partial.  Mode 1 then sums the pairwise tree p[t] += p[t + off] for off = NT/2 .. 1.  Mode 2 (512 threads)
+ * and mode 3 (256 threads, the pose-LM kernel) halve once (p[t] += p[t + NT/2]), sum each of 16 runs of
+ * NT/32 partials left to right (q[s] = p[Rs] + p[Rs+1] + ... , R = NT/32) and finish with the tree
+ * q[s] += q[s + off], off = 8, 4, 2, 1. */
 #define OR_NT_MAX 1024
 typedef struct { int mode, nt; double part[OR_NT_MAX]; } or_sum;
 
 static void sum_reset(or_sum* s, int mode) {
     s->mode = mode;
-    s->nt = mode >= 1 ? 128 << mode : 1;
+    s->nt = mode == 3 ? 256 : mode >= 1 ? 128 << mode : 1;
     memset(s->part, 0, sizeof(double) * (size_t)s->nt);
 }
 /* term of edge index k (in the active-edge order) */
@@ -746,12 +747,14 @@ static double sum_total(or_sum* s) {
     if (s->mode == 0) return s->part[0];
     double p[OR_NT_MAX];
     memcpy(p, s->part, sizeof(double) * (size_t)s->nt);
-    if (s->mode == 2) {
+    if (s->mode == 2 || s->mode == 3) {
+        /* segmented: NT threads, halve once, 16 runs of NT/32 partials summed left to right, tree over runs */
+        const int half = s->nt / 2, run = half / 16;
         double q[16];
-        for (int t = 0; t < 256; ++t) p[t] = p[t] + p[t + 256];
+        for (int t = 0; t < half; ++t) p[t] = p[t] + p[t + half];
         for (int g = 0; g < 16; ++g) {
-            q[g] = p[16 * g];
-            for (int i = 1; i < 16; ++i) q[g] = q[g] + p[16 * g + i];
+            q[g] = p[run * g];
+            for (int i = 1; i < run; ++i) q[g] = q[g] + p[run * g + i];
         }
         for (int off = 8; off > 0; off >>= 1)
             for (int g = 0; g < off; ++g) q[g] = q[g] + q[g + off];

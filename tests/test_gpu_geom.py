@@ -11,7 +11,7 @@ from ya_vo_amd import MATCH_DTYPE, scene
 pytestmark = pytest.mark.gpu
 
 POSE_TOL = 1e-9  # |pose_gpu - pose_reference_order| (quaternion + translation), stated in DESIGN.md
-LM_ORDER = 2     # the pose-LM kernel's edge-sum order: 512-thread tree (oracle sum_mode 2)
+LM_ORDER = 3     # the pose-LM kernel's edge-sum order: 256-thread segmented (oracle sum_mode 3)
 GN_ORDER = 1     # the GN kernel's: 256-thread tree
 
 

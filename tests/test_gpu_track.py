@@ -29,10 +29,12 @@ def _setup(ctx, n_frames):
     return b, carry
 
 
-def test_track_matches_oracle(ctx, oracle, offsets):
+@pytest.mark.parametrize("overlap", [False, True])
+def test_track_matches_oracle(ctx, oracle, offsets, overlap):
     import torch
     n_frames = 3
     b, carry = _setup(ctx, n_frames)
+    b.set_track_overlap(overlap)
     seq = [(synth_frame(51, k, 3 * k), synth_frame(51, k, 3 * k + 8)) for k in range(2 * n_frames)]
     d_prior = torch.from_numpy(np.tile(IDENTITY, (n_frames, 1))).to("cuda:0")
     d_pose = torch.zeros((n_frames, 7), dtype=torch.float64, device="cuda:0")
@@ -46,6 +48,7 @@ def test_track_matches_oracle(ctx, oracle, offsets):
         b.run(d.data_ptr(), len(frames), W, H * W, 20, carry_from=2 * (n_frames - 1))
         b.track(d_prior.data_ptr(), d_pose.data_ptr())
         ctx.sync()
+        b.track_sync()
         v = b.view()
         assert v.n_tracks == n_frames
         for i, img in enumerate(frames):
@@ -87,4 +90,36 @@ def test_track_rejects_inconsistent_pairs(ctx):
         b.set_tracks([(0, 1)], scene.K_KITTI, T_RIGHT)  # stereo query 0 != temporal train 3
     with pytest.raises(yv.YavoError):
         b.set_tracks([(0, 5)], scene.K_KITTI, T_RIGHT)  # pair index out of range
+    b.close()
+
+
+def test_track_overlap_pipelined(ctx, oracle, offsets):
+    """Overlap mode without any host synchronization between steps: three run + track steps back to back
+    (the LM of step i beside the kernels of step i + 1, edge buffers alternating); every step's poses, read
+    after one final sync, equal the oracle chain's."""
+    import torch
+    n_frames, steps = 2, 3
+    b, carry = _setup(ctx, n_frames)
+    b.set_track_overlap(True)
+    seq = [(synth_frame(61, k, 3 * k), synth_frame(61, k, 3 * k + 8)) for k in range(n_frames * steps)]
+    d_prior = torch.from_numpy(np.tile(IDENTITY, (n_frames, 1))).to("cuda:0")
+    d_poses = [torch.zeros((n_frames, 7), dtype=torch.float64, device="cuda:0") for _ in range(steps)]
+    frames = [np.stack([im for k in range(i * n_frames, (i + 1) * n_frames) for im in seq[k]]) for i in range(steps)]
+    d_frames = [torch.from_numpy(f).to("cuda:0") for f in frames]
+    torch.cuda.synchronize()
+    for i in range(steps):
+        b.run(d_frames[i].data_ptr(), 2 * n_frames, W, H * W, 20, carry_from=2 * (n_frames - 1))
+        b.track(d_prior.data_ptr(), d_poses[i].data_ptr())
+    ctx.sync()
+    b.track_sync()
+    kp = [[oracle.brief(im, oracle.fast(im, 2000)[0], offsets) for im in f] for f in frames]
+    for i in range(steps):
+        P = d_poses[i].cpu().numpy()
+        for k in range(n_frames):
+            if k == 0:
+                kq = kp[i - 1][2 * (n_frames - 1)] if i > 0 else kp[0][0][:0]
+            else:
+                kq = kp[i][2 * (k - 1)]
+            T = track_pose(oracle, kq, kp[i][2 * k], kp[i][2 * k + 1], scene.K_KITTI, T_RIGHT)[3]
+            np.testing.assert_array_equal(P[k], T)
     b.close()

@@ -47,7 +47,7 @@ def track_edges(orc, kq, kl, kr, K, T_right, thr=20):
     return X[ok], uv, q
 
 
-def track_pose(orc, kq, kl, kr, K, T_right, prior=IDENTITY, thr=20, sum_mode=2):
+def track_pose(orc, kq, kl, kr, K, T_right, prior=IDENTITY, thr=20, sum_mode=3):
     X, uv, q = track_edges(orc, kq, kl, kr, K, T_right, thr)
     T, out, inl = orc.pose_lm(X, uv, K, prior, sum_mode)
     return X, uv, q, T, out, inl

@@ -85,6 +85,8 @@ SIGNATURES = {
     "yv_batch_view_get": (_I, [_P, ctypes.POINTER(_BatchView)]),
     "yv_batch_set_tracks": (_I, [_P, _P, _I, _P, _P]),
     "yv_batch_track": (_I, [_P, _P, _P, _P]),
+    "yv_batch_set_track_overlap": (_I, [_P, _I]),
+    "yv_batch_track_sync": (_I, [_P]),
 }
 
 
@@ -349,6 +351,13 @@ class Batch:
     def track(self, d_priors: int, d_poses: int, stream: int = 0) -> None:
         _check(self.lib.yv_batch_track(self.handle, ctypes.c_void_p(d_priors), ctypes.c_void_p(d_poses),
                                        ctypes.c_void_p(stream) if stream else None), "yv_batch_track")
+
+    def set_track_overlap(self, on: bool = True) -> None:
+        """Run each track's pose LM on the batch's own stream beside the next run (yv_batch_set_track_overlap)."""
+        _check(self.lib.yv_batch_set_track_overlap(self.handle, 1 if on else 0), "yv_batch_set_track_overlap")
+
+    def track_sync(self) -> None:
+        _check(self.lib.yv_batch_track_sync(self.handle), "yv_batch_track_sync")
 
     def enable_timing(self, on: bool = True) -> None:
         _check(self.lib.yv_batch_enable_timing(self.handle, 1 if on else 0), "yv_batch_enable_timing")

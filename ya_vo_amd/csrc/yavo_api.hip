@@ -59,12 +59,20 @@ struct yv_batch {
     int32_t* tracks = nullptr;      // [max_tracks][2] {stereo pair, temporal pair}
     double* track_K = nullptr;      // [max_tracks][9]
     double* T_right = nullptr;      // [7]
-    double* edge_X = nullptr;       // [max_tracks][max_kp][3]
-    double* edge_uv = nullptr;      // [max_tracks][max_kp][2]
-    int32_t* edge_query = nullptr;  // [max_tracks][max_kp]
-    int32_t* edge_count = nullptr;  // [max_tracks]
+    // edge / LM buffers, double-buffered ([2][...]): with the LM on the side stream, track i's LM reads
+    // buffer i % 2 while track i + 1 builds into the other one
+    double* edge_X = nullptr;       // [2][max_tracks][max_kp][3]
+    double* edge_uv = nullptr;      // [2][max_tracks][max_kp][2]
+    int32_t* edge_query = nullptr;  // [2][max_tracks][max_kp]
+    int32_t* edge_count = nullptr;  // [2][max_tracks]
     uint8_t* edge_outlier = nullptr;
     int32_t* track_inliers = nullptr;
+    int tbuf = 0;                   // buffer of the last yv_batch_track
+    int track_calls = 0;
+    bool overlap = false;           // LM on the side stream
+    hipStream_t side = nullptr;
+    hipEvent_t ev_edges[2] = {nullptr, nullptr}, ev_lm[2] = {nullptr, nullptr};
+    bool lm_pending[2] = {false, false};
     // stage timing: events 0..5 bracket the run's stages, 6..8 the track's
     bool timing = false;
     std::vector<hipEvent_t> events;  // kEvPerRun per recorded run
@@ -123,9 +131,15 @@ void batch_free(yv_batch* b) {
                     b->matches,   b->match_count, b->filtered, b->filt_count, b->staging,  b->match_dj,
                     b->match_lim, b->tracks,     b->track_K,  b->T_right,    b->edge_X,    b->edge_uv,
                     b->edge_query, b->edge_count, b->edge_outlier, b->track_inliers};
+    if (b->side) (void)hipStreamSynchronize(b->side);
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : b->events) (void)hipEventDestroy(e);
+    for (int k = 0; k < 2; ++k) {
+        if (b->ev_edges[k]) (void)hipEventDestroy(b->ev_edges[k]);
+        if (b->ev_lm[k]) (void)hipEventDestroy(b->ev_lm[k]);
+    }
+    if (b->side) (void)hipStreamDestroy(b->side);
     delete b;
 }
 
@@ -471,12 +485,13 @@ int yv_batch_view_get(yv_batch* b, yv_batch_view* v) {
     v->match_dj = reinterpret_cast<const int32_t*>(b->match_dj);
     v->match_lim = b->match_lim;
     v->n_tracks = b->n_tracks;
-    v->edge_count = b->edge_count;
-    v->edge_X = b->edge_X;
-    v->edge_uv = b->edge_uv;
-    v->edge_query = b->edge_query;
-    v->edge_outlier = b->edge_outlier;
-    v->track_inliers = b->track_inliers;
+    const size_t nt = (size_t)b->max_tracks, nk = (size_t)b->max_kp, k = (size_t)b->tbuf;
+    v->edge_count = b->edge_count ? b->edge_count + k * nt : nullptr;
+    v->edge_X = b->edge_X ? b->edge_X + k * nt * nk * 3 : nullptr;
+    v->edge_uv = b->edge_uv ? b->edge_uv + k * nt * nk * 2 : nullptr;
+    v->edge_query = b->edge_query ? b->edge_query + k * nt * nk : nullptr;
+    v->edge_outlier = b->edge_outlier ? b->edge_outlier + k * nt * nk : nullptr;
+    v->track_inliers = b->track_inliers ? b->track_inliers + k * nt : nullptr;
     return YV_OK;
 }
 
@@ -492,10 +507,12 @@ int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks, int n_tracks, const 
     if (n_tracks > 0 && !finite_pose(T_right)) return YV_ERR_INVALID;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
     hipStream_t s = b->ctx->stream;
+    if (b->side) YV_HIP(hipStreamSynchronize(b->side));  // an LM in flight reads tracks / K
     if (n_tracks > b->max_tracks) {
         void* old[] = {b->tracks, b->track_K, b->T_right, b->edge_X, b->edge_uv, b->edge_query, b->edge_count,
                        b->edge_outlier, b->track_inliers};
         YV_HIP(hipStreamSynchronize(s));
+        if (b->side) YV_HIP(hipStreamSynchronize(b->side));
         for (void* p : old)
             if (p) (void)hipFree(p);
         b->tracks = nullptr; b->track_K = nullptr; b->T_right = nullptr; b->edge_X = nullptr; b->edge_uv = nullptr;
@@ -507,12 +524,12 @@ int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks, int n_tracks, const 
         rc |= dalloc(&b->tracks, 2 * nt);
         rc |= dalloc(&b->track_K, 9 * nt);
         rc |= dalloc(&b->T_right, 7);
-        rc |= dalloc(&b->edge_X, 3 * nt * nk);
-        rc |= dalloc(&b->edge_uv, 2 * nt * nk);
-        rc |= dalloc(&b->edge_query, nt * nk);
-        rc |= dalloc(&b->edge_count, nt);
-        rc |= dalloc(&b->edge_outlier, nt * nk);
-        rc |= dalloc(&b->track_inliers, nt);
+        rc |= dalloc(&b->edge_X, 2 * 3 * nt * nk);
+        rc |= dalloc(&b->edge_uv, 2 * 2 * nt * nk);
+        rc |= dalloc(&b->edge_query, 2 * nt * nk);
+        rc |= dalloc(&b->edge_count, 2 * nt);
+        rc |= dalloc(&b->edge_outlier, 2 * nt * nk);
+        rc |= dalloc(&b->track_inliers, 2 * nt);
         if (rc != YV_OK) return YV_ERR_HIP;
         b->max_tracks = n_tracks;
     }
@@ -522,7 +539,7 @@ int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks, int n_tracks, const 
         YV_HIP(hipMemcpyAsync(b->tracks, tracks, 2 * sizeof(int32_t) * (size_t)n_tracks, hipMemcpyHostToDevice, s));
         YV_HIP(hipMemcpyAsync(b->track_K, Ks.data(), Ks.size() * sizeof(double), hipMemcpyHostToDevice, s));
         YV_HIP(hipMemcpyAsync(b->T_right, T_right, 7 * sizeof(double), hipMemcpyHostToDevice, s));
-        YV_HIP(hipMemsetAsync(b->edge_count, 0, sizeof(int32_t) * (size_t)n_tracks, s));
+        YV_HIP(hipMemsetAsync(b->edge_count, 0, 2 * sizeof(int32_t) * (size_t)b->max_tracks, s));
         YV_HIP(hipStreamSynchronize(s));
     }
     b->n_tracks = n_tracks;
@@ -534,21 +551,64 @@ int yv_batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* s
     if (b->n_tracks == 0) return YV_OK;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->ctx->stream;
+    const int k = b->track_calls++ & 1;
+    const size_t nt = (size_t)b->max_tracks, nk = (size_t)b->max_kp;
+    double* eX = b->edge_X + k * nt * nk * 3;
+    double* euv = b->edge_uv + k * nt * nk * 2;
+    int32_t* eq = b->edge_query + k * nt * nk;
+    int32_t* ec = b->edge_count + k * nt;
+    uint8_t* eo = b->edge_outlier + k * nt * nk;
+    int32_t* inl = b->track_inliers + k * nt;
     const int run = b->last_run;
     const bool timed = b->timing && run >= 0 && !b->tracked[run];
     hipEvent_t* ev = timed ? &b->events[(size_t)run * kEvPerRun] : nullptr;
+    // buffer k was last read by the LM two tracks ago (side stream): the build must not overwrite it early
+    if (b->lm_pending[k]) YV_HIP(hipStreamWaitEvent(s, b->ev_lm[k], 0));
     if (timed) YV_HIP(hipEventRecord(ev[6], s));
     yavo::launch_track_build(b->tracks, b->n_tracks, b->pairs, b->keypoints, b->kp_count, b->match_dj, b->match_lim,
-                             b->max_kp, b->track_K, b->T_right, b->edge_X, b->edge_uv, b->edge_query, b->edge_count,
-                             s);
-    if (timed) YV_HIP(hipEventRecord(ev[7], s));
-    yavo::launch_track_pose(b->n_tracks, b->edge_count, b->max_kp, b->edge_X, b->edge_uv, b->track_K, d_priors,
-                            d_poses, b->edge_outlier, b->track_inliers, s);
+                             b->max_kp, b->track_K, b->T_right, eX, euv, eq, ec, s);
+    hipStream_t ls = s;
+    if (b->overlap) {
+        // the LM reads only this track's edge buffer, priors and poses: it runs on the side stream beside the
+        // next batch's image kernels (which overwrite keypoints / matches, already consumed by the build)
+        YV_HIP(hipEventRecord(b->ev_edges[k], s));
+        YV_HIP(hipStreamWaitEvent(b->side, b->ev_edges[k], 0));
+        ls = b->side;
+    }
+    if (timed) YV_HIP(hipEventRecord(ev[7], ls));
+    yavo::launch_track_pose(b->n_tracks, ec, b->max_kp, eX, euv, b->track_K, d_priors, d_poses, eo, inl, ls);
     if (timed) {
-        YV_HIP(hipEventRecord(ev[8], s));
+        YV_HIP(hipEventRecord(ev[8], ls));
         b->tracked[run] = 1;
     }
+    if (b->overlap) {
+        YV_HIP(hipEventRecord(b->ev_lm[k], ls));
+        b->lm_pending[k] = true;
+    }
+    b->tbuf = k;
     return check_launch();
+}
+
+int yv_batch_set_track_overlap(yv_batch* b, int on) {
+    if (!b) return YV_ERR_INVALID;
+    if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+    if (on && !b->side) {
+        YV_HIP(hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking));
+        for (int k = 0; k < 2; ++k) {
+            YV_HIP(hipEventCreateWithFlags(&b->ev_edges[k], hipEventDisableTiming));
+            YV_HIP(hipEventCreateWithFlags(&b->ev_lm[k], hipEventDisableTiming));
+        }
+    }
+    if (!on && b->side) YV_HIP(hipStreamSynchronize(b->side));
+    b->overlap = on != 0;
+    return YV_OK;
+}
+
+int yv_batch_track_sync(yv_batch* b) {
+    if (!b) return YV_ERR_INVALID;
+    if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+    if (b->side) YV_HIP(hipStreamSynchronize(b->side));
+    return YV_OK;
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -25,7 +25,8 @@ namespace yavo {
 namespace geom {
 
 constexpr int kNT = 256;          // threads per workgroup of the reduction kernels
-constexpr int kLMNT = 512;        // threads per pose-LM workgroup: 2 waves per SIMD hide the FP64 latency
+constexpr int kLMNT = 256;        // threads per pose-LM workgroup (<= 256 VGPRs: half the register file, so the
+                                  // LM co-runs with the image kernels of the next batch)
 
 // YAVO_LM_PROFILE builds (tools/lm_profile.py) time the pose-LM phases with the shader clock on lane 0
 #ifdef YAVO_LM_PROFILE
@@ -1130,44 +1131,49 @@ __device__ void tree_reduce(double (&part)[NV], double* red, double* out, unsign
     __syncthreads();
 }
 
-// The pose LM's reduction of NV per-thread partials over kLMNT = 512 threads (oracle sum_mode 2):
-// p[t] += p[t + 256]; then thread (v, g) sums run g of 16 partials of value v left to right from a bank-padded
-// LDS image ([v][g][17]: conflict-free both when written by consecutive threads and when 16 threads read 16
-// runs); the 16 run sums of a value sit on 16 adjacent lanes and finish with the tree q[g] += q[g + off],
-// off = 8 .. 1.  Three barriers; one value per thread in the serial part instead of NV values in one wave.
-constexpr int kSegPad = 17;
+// The pose LM's reduction of NV per-thread partials over kLMNT threads (oracle sum_mode 3 for 256):
+// p[t] += p[t + NT/2]; then thread (v, g) sums run g of R = NT/32 partials of value v left to right from a
+// bank-padded LDS image ([v][g][R + 1]: conflict-free both when written by consecutive threads and when 16
+// threads read 16 runs); the 16 run sums of a value sit on 16 adjacent lanes and finish with the tree
+// q[g] += q[g + off], off = 8 .. 1.  Three barriers; one value per thread in the serial part.
+constexpr int kSegRun = kLMNT / 32;
+constexpr int kSegPad = kSegRun + 1;
 template <int NV>
 __device__ void seg_reduce(double (&part)[NV], double* red /* >= NV * 16 * kSegPad */, double* out,
                            unsigned long long* t_sync = nullptr) {
-    static_assert(NV * 16 <= kLMNT, "one thread per (value, run)");
+    constexpr int half = kLMNT / 2;
     const int tid = threadIdx.x;
     __syncthreads();
 #ifdef YAVO_LM_PROFILE
     if (t_sync) *t_sync = __builtin_readcyclecounter();
 #endif
-    const int e = tid & 255;                         // partial index after the halving
-    const int slot = (e >> 4) * kSegPad + (e & 15);  // [g][i] with padded runs
-    if (tid >= 256) {
+    const int e = tid & (half - 1);                             // partial index after the halving
+    const int slot = (e / kSegRun) * kSegPad + (e % kSegRun);  // [g][i] with padded runs
+    if (tid >= half) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) red[v * 16 * kSegPad + slot] = part[v];
     }
     __syncthreads();
-    if (tid < 256) {
+    if (tid < half) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) red[v * 16 * kSegPad + slot] = part[v] + red[v * 16 * kSegPad + slot];
     }
     __syncthreads();
-    double q = 0.0;
-    const int v = tid >> 4, g = tid & 15;
-    if (tid < NV * 16) {
-        const double* r = red + v * 16 * kSegPad + g * kSegPad;
-        q = r[0];
+    // (value, run) pairs over the block: NV * 16 of them, kLMNT threads
+    for (int w0 = 0; w0 < NV * 16; w0 += kLMNT) {
+        const int w = w0 + tid;
+        double q = 0.0;
+        const int v = w >> 4, g = w & 15;
+        if (w < NV * 16) {
+            const double* r = red + v * 16 * kSegPad + g * kSegPad;
+            q = r[0];
 #pragma unroll
-        for (int i = 1; i < 16; ++i) q = q + r[i];
+            for (int i = 1; i < kSegRun; ++i) q = q + r[i];
+        }
+#pragma unroll
+        for (int off = 8; off > 0; off >>= 1) q = q + __shfl_down(q, off, 16);
+        if (w < NV * 16 && g == 0) out[v] = q;
     }
-#pragma unroll
-    for (int off = 8; off > 0; off >>= 1) q = q + __shfl_down(q, off, 16);
-    if (tid < NV * 16 && g == 0) out[v] = q;
     __syncthreads();
 }
 

@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
                                                      int64_t cap, uint32_t* __restrict__ cand_count, K9 kw,
                                                      uint8_t* __restrict__ blur) {
     __shared__ uint8_t tile[FT_LH * FT_LW];
-    __shared__ uint32_t hbuf[kBlur ? (FT_LH / 2) * FT_W : 1];
+    __shared__ __align__(16) uint32_t hbuf[kBlur ? (FT_LH / 2) * FT_W : 4];
     __shared__ uint16_t s_pos[FT_W * FT_H];
     __shared__ uint16_t s_pre[FT_W * FT_H];
     __shared__ uint32_t s_n, s_npre, s_base;
@@ -265,24 +265,30 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
     if (kBlur) {
         // horizontal pass, exact: h = sum_j k_j * p[x + j] as two v_dot4_u32_u8 + one mad on the byte row
         // (rows start 4-byte aligned: FT_LW = 72).  h <= 255 * 256 fits 16 bits; rows 2q and 2q+1 are
-        // packed into one dword so the vertical pass can use v_dot2_u32_u16.
+        // packed into one dword so the vertical pass can use v_dot2_u32_u16.  One item = 4 adjacent
+        // columns of a row pair: 3 LDS dwords per row feed all 4 outputs, one 16-B LDS store.
         const uint32_t* trow = reinterpret_cast<const uint32_t*>(tile);
-        for (int i = tid; i < (FT_LH / 2) * FT_W; i += 256) {
-            const int q = i >> 6, x = i & 63;
-            const int sh = x & 3;
-            uint32_t hv[2];
+        constexpr int kItems = (FT_LH / 2) * (FT_W / 4);
+        for (int i = tid; i < kItems; i += 256) {
+            const int q = i >> 4, xq = (i & 15) * 4;
+            uint32_t hv[2][4];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const uint32_t* wr = trow + ((2 * q + h) * FT_LW >> 2) + (x >> 2);
+                const uint32_t* wr = trow + ((2 * q + h) * FT_LW >> 2) + (xq >> 2);
                 const uint32_t d0 = wr[0], d1 = wr[1], d2 = wr[2];
-                const uint32_t b0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-                const uint32_t b1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-                const uint32_t b8 = (d2 >> (8 * sh)) & 0xFFu;
-                uint32_t acc = __builtin_amdgcn_udot4(b0, kw.k4[0], 0u, false);
-                acc = __builtin_amdgcn_udot4(b1, kw.k4[1], acc, false);
-                hv[h] = acc + kw.k[8] * b8;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t b0 = j ? __builtin_amdgcn_alignbyte(d1, d0, j) : d0;
+                    const uint32_t b1 = j ? __builtin_amdgcn_alignbyte(d2, d1, j) : d1;
+                    const uint32_t b8 = (d2 >> (8 * j)) & 0xFFu;
+                    uint32_t acc = __builtin_amdgcn_udot4(b0, kw.k4[0], 0u, false);
+                    acc = __builtin_amdgcn_udot4(b1, kw.k4[1], acc, false);
+                    hv[h][j] = acc + kw.k[8] * b8;
+                }
             }
-            hbuf[i] = hv[0] | (hv[1] << 16);
+            *reinterpret_cast<uint4*>(&hbuf[q * FT_W + xq]) =
+                make_uint4(hv[0][0] | (hv[1][0] << 16), hv[0][1] | (hv[1][1] << 16), hv[0][2] | (hv[1][2] << 16),
+                           hv[0][3] | (hv[1][3] << 16));
         }
     }
     __syncthreads();
