@@ -207,6 +207,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # PCIe-inclusive rate: the same step's frames uploaded from pinned host memory, timed alone;
+    # reported beside `value` (which has the inputs resident in HBM), never as it
+    h_frames = torch.from_numpy(frames).pin_memory()
+    d_up = torch.empty_like(d_frames)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(3):
+        d_up.copy_(h_frames, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d_ms = (time.perf_counter() - t1) / 3 * 1e3
+    del d_up, h_frames
+
     v = batch.view()
     counts = {
         "cand": ctx.download(v.cand_count, np.uint32, n_img + 1).astype(np.int64),
@@ -274,6 +286,8 @@ def main():
                    "mean_pnp_edges_per_frame": round(counts["edges"] / B, 1),
                    "mean_pnp_inliers_per_frame": round(float(np.mean(inliers)), 1)},
         "stages_ms_per_launch": stages,
+        "h2d_upload_ms_per_step": round(h2d_ms, 4),
+        "pcie_inclusive_frames_per_s": round(frames_total / (elapsed + args.steps * h2d_ms / 1e3), 2),
         "roofline": roofline,
         "cpu_baseline": None,
     }

@@ -11,14 +11,15 @@ import os
 import sys
 
 STAGE_OF = {"detect_kernel": "detect", "topk_kernel": "topk", "brief_kernel": "brief",
-            "match_finalize_kernel": "finalize", "match_kernel": "match"}
+            "match_finalize_kernel": "finalize", "match_kernel": "match", "track_build_kernel": "track_edges",
+            "pose_lm_kernel": "track_pose"}
 
 
 def stage(kernel_name):
-    for key, st in STAGE_OF.items():
-        if "yavo::" + key in kernel_name or key + "<" in kernel_name or kernel_name.startswith(key):
-            return st
-    return None
+    # kernel names as rocprofv3 prints them: "yavo::match_kernel(...)", "void yavo::detect_kernel<true>(...)",
+    # "yavo::geom::pose_lm_kernel(...)"
+    base = kernel_name.split("(")[0].split("<")[0].split("::")[-1].strip()
+    return STAGE_OF.get(base)
 
 
 def load(out_dir, counter):
@@ -39,7 +40,7 @@ def load(out_dir, counter):
 
 def main():
     out_dir = sys.argv[1]
-    frames = 64
+    frames = 256  # bench.py's default
     args = sys.argv[2:]
     if "--frames" in args:
         frames = int(args[args.index("--frames") + 1])
