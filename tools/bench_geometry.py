@@ -1,0 +1,146 @@
+"""Throughput of the geometry rows on their own next to the oracle on the host, at the
+bench's shapes: 256 match lists / pose problems of ~1900 entries (one per stereo frame of a bench step).
+
+    python tools/bench_geometry.py [--lists 256] [--n 1900] [--iters 400]
+
+Prints one JSON object (committed as profiles/r01_geometry.json).  GPU times: HIP events around the batched
+launches, inputs resident in HBM.  CPU: the oracle (the reference's algorithms restated), single thread, on a
+bounded sample."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lists", type=int, default=256)
+    ap.add_argument("--n", type=int, default=1900)
+    ap.add_argument("--iters", type=int, default=400)
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+    import ya_vo_amd as yv
+    from ya_vo_amd import MATCH_DTYPE, scene
+    import oracle_bind
+
+    orc = oracle_bind.Oracle()
+    ctx = yv.Context(0)
+    dev = "cuda:0"
+    L, n, iters = args.lists, args.n, args.iters
+    out = {"lists": L, "entries_per_list": n, "ransac_iterations": iters}
+
+    # ---- F-RANSAC: L lists of n matches (two-view synthetic, 10% gross mismatches), iters hypotheses each
+    lists = np.zeros((L, n), MATCH_DTYPE)
+    samples = np.zeros((L, iters, 8), np.int32)
+    for l in range(L):
+        _, _, _, ua, ub = scene.two_view_matches(n, seed=100 + l)
+        m = lists[l]
+        m["pt1"]["x"], m["pt1"]["y"] = np.round(ua[:, 0]), np.round(ua[:, 1])
+        m["pt2"]["x"], m["pt2"]["y"] = np.round(ub[:, 0]), np.round(ub[:, 1])
+        rng = np.random.default_rng(l)
+        bad = rng.choice(n, n // 10, replace=False)
+        m["pt2"]["x"][bad] = rng.integers(0, 376, len(bad))
+        samples[l] = rng.integers(0, n, (iters, 8))
+    d_m = torch.from_numpy(lists.view(np.uint8).reshape(-1)).to(dev)
+    d_cnt = torch.full((L,), n, dtype=torch.int32, device=dev)
+    d_s = torch.from_numpy(samples.reshape(-1)).to(dev)
+    d_F = torch.zeros(L * 9, dtype=torch.float64, device=dev)
+    d_inl = torch.zeros(L, dtype=torch.int32, device=dev)
+    d_found = torch.zeros(L, dtype=torch.int32, device=dev)
+    # one explicit stream for the library launches, the copies and the events (the null stream would let the
+    # library fall back to its own non-blocking context stream, unordered with torch's work)
+    ts = torch.cuda.Stream()
+    torch.cuda.set_stream(ts)
+    stream = ts.cuda_stream
+    assert stream != 0
+
+    def ransac():
+        assert ctx.lib.yv_f_ransac_batch(ctx.handle, d_m.data_ptr(), n, d_cnt.data_ptr(), L, d_s.data_ptr(),
+                                         iters * 8, iters, 0.1, d_F.data_ptr(), d_inl.data_ptr(),
+                                         d_found.data_ptr(), stream) == 0
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / args.reps
+
+    ms = timed(ransac)
+    t0 = time.perf_counter()
+    ok, F, inl = orc.f_ransac(lists[0], samples[0], 0.1)
+    cpu = time.perf_counter() - t0
+    gpu_F = d_F[:9].cpu().numpy().reshape(3, 3)
+    out["f_ransac"] = {"gpu_ms_per_launch": round(ms, 4), "gpu_lists_per_s": round(L / ms * 1e3, 1),
+                       "gpu_hypotheses_per_s": round(L * iters / ms * 1e3, 1),
+                       "cpu_oracle_lists_per_s": round(1 / cpu, 3), "cpu_threads": 1,
+                       "list0_bit_identical": bool(np.array_equal(gpu_F, F) and int(d_inl[0]) == inl)}
+
+    # ---- pose LM / GN: L problems of n edges (0.5 px noise, 10% gross outliers)
+    probs = [scene.random_scene(n, seed=200 + i, noise_px=0.5, outlier_frac=0.1) for i in range(L)]
+    priors = np.stack([scene.perturb(p[2], np.random.default_rng(i)) for i, p in enumerate(probs)])
+    offs = (np.arange(L + 1) * n).astype(np.int32)
+    d_off = torch.from_numpy(offs).to(dev)
+    d_X = torch.from_numpy(np.ascontiguousarray(np.concatenate([p[0] for p in probs]))).to(dev)
+    d_uv = torch.from_numpy(np.ascontiguousarray(np.concatenate([p[1] for p in probs]))).to(dev)
+    d_K = torch.from_numpy(np.tile(scene.K_KITTI.reshape(1, 9), (L, 1))).to(dev)
+    d_prior = torch.from_numpy(priors).to(dev)
+    d_P = torch.empty_like(d_prior)
+    d_out = torch.zeros(L * n, dtype=torch.uint8, device=dev)
+    d_res = torch.zeros(L, dtype=torch.int32, device=dev)
+
+    def lm():
+        d_P.copy_(d_prior)
+        assert ctx.lib.yv_pose_lm_batch(ctx.handle, L, d_off.data_ptr(), d_X.data_ptr(), d_uv.data_ptr(),
+                                        d_K.data_ptr(), d_P.data_ptr(), d_out.data_ptr(), d_res.data_ptr(),
+                                        stream) == 0
+
+    def gn():
+        d_P.copy_(d_prior)
+        assert ctx.lib.yv_pose_gn_batch(ctx.handle, L, d_off.data_ptr(), d_X.data_ptr(), d_uv.data_ptr(),
+                                        d_K.data_ptr(), d_P.data_ptr(), d_res.data_ptr(), stream) == 0
+
+    for name, fn, cpu_fn in (("pose_lm", lm, lambda: orc.pose_lm(probs[0][0], probs[0][1], scene.K_KITTI, priors[0], 3)),
+                             ("pose_gn", gn, lambda: orc.pose_gn(probs[0][0], probs[0][1], scene.K_KITTI, priors[0], 1))):
+        ms = timed(fn)
+        torch.cuda.synchronize()
+        P0 = d_P[0].cpu().numpy()
+        t0 = time.perf_counter()
+        ref = cpu_fn()
+        cpu = time.perf_counter() - t0
+        out[name] = {"gpu_ms_per_launch": round(ms, 4), "gpu_problems_per_s": round(L / ms * 1e3, 1),
+                     "cpu_oracle_problems_per_s": round(1 / cpu, 2), "cpu_threads": 1,
+                     "problem0_bit_identical": bool(np.array_equal(P0, ref[0]))}
+
+    # ---- triangulation of n matches through the host-pointer entry point (includes the PCIe copies) and
+    # the oracle
+    Ta, Tb, _, ua, ub = scene.two_view_matches(n, seed=7)
+    m = lists[0]
+    t0 = time.perf_counter()
+    for _ in range(args.reps):
+        ctx.triangulate(Ta, Tb, scene.K_KITTI, m)
+    host_ms = (time.perf_counter() - t0) / args.reps * 1e3
+    t0 = time.perf_counter()
+    orc.triangulate_matches(Ta, Tb, scene.K_KITTI, m)
+    cpu = time.perf_counter() - t0
+    out["triangulate"] = {"host_api_ms_per_list": round(host_ms, 4), "cpu_oracle_ms_per_list": round(cpu * 1e3, 3),
+                          "note": "batched device-resident triangulation runs inside track_build_kernel "
+                                  "(bench.py stage track_edges)"}
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
