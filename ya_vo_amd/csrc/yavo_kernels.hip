@@ -150,6 +150,21 @@ __device__ __forceinline__ int reflect101(int p, int len) {
 // once.  One 256-thread workgroup per 64 x 32 output tile, the tile plus a 4-pixel halo staged in LDS
 // (BORDER_REFLECT_101 values outside the image: the blur needs them, no FAST candidate ever reads them).
 // Candidates are staged in LDS and appended with ONE global atomic per workgroup.
+// YAVO_LM_PROFILE builds (tools/det_profile.py): detect phase cycles of lane 0 of every workgroup, summed
+#ifdef YAVO_LM_PROFILE
+constexpr int kDetProfSlots = 131072;
+__device__ unsigned long long g_det_prof[kDetProfSlots][6];
+#define DP_DECL unsigned long long dp_acc[6] = {0, 0, 0, 0, 0, 0}; unsigned long long dp_t = __builtin_readcyclecounter();
+#define DP_MARK(k) do { const unsigned long long t_ = __builtin_readcyclecounter(); dp_acc[k] += t_ - dp_t; dp_t = t_; } while (0)
+#define DP_STORE() do { \
+        const unsigned slot_ = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; \
+        if (threadIdx.x == 0 && slot_ < kDetProfSlots) for (int q_ = 0; q_ < 6; ++q_) g_det_prof[slot_][q_] = dp_acc[q_]; \
+    } while (0)
+#else
+#define DP_DECL
+#define DP_MARK(k) do {} while (0)
+#define DP_STORE() do {} while (0)
+#endif
 constexpr int FT_W = kFastTileW;        // 64 output columns per tile (one wave-row)
 constexpr int FT_H = kFastTileH;        // 32 output rows per tile
 constexpr int FT_R = 4;                 // halo: blur radius 4 (ring radius 3, Sobel + 3x3 window radius 2)
@@ -166,6 +181,7 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
     __shared__ uint16_t s_pos[FT_W * FT_H];
     __shared__ uint16_t s_pre[FT_W * FT_H];
     __shared__ uint32_t s_n, s_npre, s_base;
+    DP_DECL
     const int img = blockIdx.z;
     const int r0 = blockIdx.y * FT_H, c0 = blockIdx.x * FT_W;
     const uint8_t* src = imgs + (int64_t)img * pitch;
@@ -177,28 +193,65 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         s_npre = 0;
     }
 
-    // stage (FT_H + 8) x (FT_W + 8): wave w loads rows w, w+4, ...; lanes 0..63 (+ 0..7) cover 72 columns
-    const int cA = reflect101(min(max(c0 - FT_R + lane, -(W - 1)), 2 * W - 2), W);
-    const int cB = reflect101(min(max(c0 - FT_R + 64 + (lane & 7), -(W - 1)), 2 * W - 2), W);
-    // all of this wave's row loads are issued before the first LDS write (10 HBM round trips -> 1)
-    constexpr int kRowsPerWave = FT_LH / 4;
-    static_assert(FT_LH % 4 == 0, "rows split evenly over the 4 waves");
-    uint8_t va[kRowsPerWave], vb[kRowsPerWave];
+    // stage (FT_H + 8) x (FT_W + 8) = 40 x 72 bytes.  Interior tiles (every source byte inside the image, and the
+    // last staged row not the image's last, so 3 bytes of alignment slack stay inside the image) load aligned
+    // dwords: 19 per row, 3 per thread, all in flight before the byte writes into LDS.  Border tiles take the
+    // REFLECT_101 byte path.
+    const bool interior = (c0 >= FT_R) && (c0 + FT_W + FT_R <= W) && (r0 >= FT_R) && (r0 + FT_H + FT_R < H);
+    if (interior) {
+        constexpr int kDw = 19;                      // dwords per row: 72 bytes + up to 3 of alignment
+        constexpr int kSlots = FT_LH * kDw;          // 760
+        constexpr int kPer = (kSlots + 255) / 256;   // 3
+        uint32_t v[kPer];
+        int sh[kPer];
 #pragma unroll
-    for (int u = 0; u < kRowsPerWave; ++u) {
-        const int lr = wave + 4 * u;
-        const int r = reflect101(min(max(r0 - FT_R + lr, -(H - 1)), 2 * H - 2), H);
-        const uint8_t* row = src + (int64_t)r * stride;
-        va[u] = row[cA];
-        vb[u] = row[cB];
-    }
+        for (int u = 0; u < kPer; ++u) {
+            const int t = tid + 256 * u;
+            const int lr = t / kDw, j = t - lr * kDw;
+            v[u] = 0;
+            sh[u] = 0;
+            if (t < kSlots) {
+                const uintptr_t a = reinterpret_cast<uintptr_t>(src + (int64_t)(r0 - FT_R + lr) * stride + (c0 - FT_R));
+                sh[u] = (int)(a & 3);
+                v[u] = reinterpret_cast<const uint32_t*>(a - sh[u])[j];
+            }
+        }
 #pragma unroll
-    for (int u = 0; u < kRowsPerWave; ++u) {
-        const int lr = wave + 4 * u;
-        tile[lr * FT_LW + lane] = va[u];
-        if (lane < FT_LW - 64) tile[lr * FT_LW + 64 + lane] = vb[u];
+        for (int u = 0; u < kPer; ++u) {
+            const int t = tid + 256 * u;
+            if (t >= kSlots) continue;
+            const int lr = t / kDw, j = t - lr * kDw;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int bcol = 4 * j + q - sh[u];  // tile column of byte q of this dword
+                if (bcol >= 0 && bcol < FT_LW) tile[lr * FT_LW + bcol] = (uint8_t)(v[u] >> (8 * q));
+            }
+        }
+    } else {
+        // wave w loads rows w, w+4, ...; lanes 0..63 (+ 0..7) cover 72 columns; all of this wave's row loads
+        // are issued before the first LDS write
+        const int cA = reflect101(min(max(c0 - FT_R + lane, -(W - 1)), 2 * W - 2), W);
+        const int cB = reflect101(min(max(c0 - FT_R + 64 + (lane & 7), -(W - 1)), 2 * W - 2), W);
+        constexpr int kRowsPerWave = FT_LH / 4;
+        static_assert(FT_LH % 4 == 0, "rows split evenly over the 4 waves");
+        uint8_t va[kRowsPerWave], vb[kRowsPerWave];
+#pragma unroll
+        for (int u = 0; u < kRowsPerWave; ++u) {
+            const int lr = wave + 4 * u;
+            const int r = reflect101(min(max(r0 - FT_R + lr, -(H - 1)), 2 * H - 2), H);
+            const uint8_t* row = src + (int64_t)r * stride;
+            va[u] = row[cA];
+            vb[u] = row[cB];
+        }
+#pragma unroll
+        for (int u = 0; u < kRowsPerWave; ++u) {
+            const int lr = wave + 4 * u;
+            tile[lr * FT_LW + lane] = va[u];
+            if (lane < FT_LW - 64) tile[lr * FT_LW + 64 + lane] = vb[u];
+        }
     }
     __syncthreads();
+    DP_MARK(0);
 
     constexpr int ring_dr[16] = YV_RING_DR;
     constexpr int ring_dc[16] = YV_RING_DC;
@@ -209,10 +262,15 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         return __builtin_amdgcn_sad_u8(cent, (uint32_t)t0[ring_dr[k] * FT_LW + ring_dc[k]], neg_thr) >> 31;
     };
     // phase 1: the reference's pretest on ring pixels 0, 7 and (4 | 12) (src/FastDetector.cc:304-317) for
-    // every pixel; the few that pass are compacted into s_pre
+    // every pixel; each lane keeps a mask of its passing rows and the survivors are compacted into s_pre
+    // once per wave (one scan, one LDS atomic)
     const int tx = lane, ty = wave;
     const int c = c0 + tx;
-    for (int rr = ty; rr < FT_H; rr += 4) {
+    constexpr int kRowIters = FT_H / 4;
+    uint32_t pmask = 0;
+#pragma unroll
+    for (int u = 0; u < kRowIters; ++u) {
+        const int rr = ty + 4 * u;
         const int r = r0 + rr;
         const bool inside = (r >= 4) && (r < H - 4) && (c >= 4) && (c < W - 4);
         const uint8_t* t0 = &tile[(rr + FT_R) * FT_LW + tx + FT_R];
@@ -220,15 +278,22 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         const uint32_t s0 = similar(t0, cent, 0), s7 = similar(t0, cent, 7);
         const uint32_t s4 = similar(t0, cent, 4), s12 = similar(t0, cent, 12);
         const bool pre = inside && !(s0 | s7) && !(s4 & s12);
-        const uint64_t bal = __ballot(pre);
-        if (bal == 0) continue;  // wave-uniform
-        const int leader = __ffsll((long long)bal) - 1;
+        pmask |= (uint32_t)pre << u;
+    }
+    {
+        const int cnt = __popc(pmask);
+        const int incl = wave_incl_scan(cnt);
+        const int total = __shfl(incl, 63, 64);
         uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&s_npre, (uint32_t)__popcll(bal));
-        base = __shfl(base, leader, 64);
-        if (pre) s_pre[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(rr * FT_W + tx);
+        if (lane == 0 && total > 0) base = atomicAdd(&s_npre, (uint32_t)total);
+        base = __shfl(base, 0, 64);
+        uint32_t off = base + (uint32_t)(incl - cnt);
+#pragma unroll
+        for (int u = 0; u < kRowIters; ++u)
+            if (pmask & (1u << u)) s_pre[off++] = (uint16_t)((ty + 4 * u) * FT_W + tx);
     }
     __syncthreads();
+    DP_MARK(1);
     // phase 2: the full 16-pixel test (>= 12 consecutive "different" ring pixels, no wrap:
     // checkContiguousPixels) densely over the pretest survivors; corners are staged in s_pos
     const uint32_t npre = s_npre;
@@ -259,6 +324,7 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         if (cand) s_pos[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)pos;
     }
     __syncthreads();
+    DP_MARK(2);
     const uint32_t n = s_n;
     // one global atomic per workgroup reserves the output range of this tile's corners
     if (tid == 0 && n > 0) s_base = atomicAdd(&cand_count[img], n);
@@ -292,6 +358,7 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         }
     }
     __syncthreads();
+    DP_MARK(3);
     // Harris response of every staged corner, one lane per corner (no divergence across FAST lanes);
     // consecutive lanes write consecutive keys
     if (n > 0) {
@@ -322,6 +389,7 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
             out[i] = make_key(resp, (uint32_t)((r0 + prr) * W + (c0 + ptx)));  // cap >= every pixel: in range
         }
     }
+    DP_MARK(4);
     if (kBlur) {
         // vertical pass, exact u32: rows 2m and 2m+1 of column x from the row-pair dwords P_m .. P_{m+4}
         typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -346,6 +414,8 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
             }
         }
     }
+    DP_MARK(5);
+    DP_STORE();
 }
 
 void launch_fast_harris(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,
@@ -1082,3 +1152,10 @@ void launch_filter_records(const yv_match* in, int n, int thr, yv_match* out, in
 }
 
 }  // namespace yavo
+
+#ifdef YAVO_LM_PROFILE
+extern "C" int yv_debug_det_prof(unsigned long long* out /* [131072][6] */) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(yavo::g_det_prof), sizeof(unsigned long long) * 131072 * 6) ==
+                   hipSuccess ? 0 : -2;
+}
+#endif
