@@ -115,6 +115,17 @@ int or_pose_lm(const double* X, const double* uv, int n, const double* K, double
 void or_lm_stats(long* out, int reset);
 int or_pose_gn(const double* X, const double* uv, int n, const double* K, double* pose, int sum_mode);
 
+/* ---- cv::calcOpticalFlowPyrLK (yavo_oracle_lk.c) ---- */
+/* cv::pyrDown, CV_8U, BORDER_REFLECT_101: dst [(H+1)/2][(W+1)/2]. */
+void or_pyr_down(const uint8_t* src, int H, int W, int sstride, uint8_t* dst);
+/* calcSharrDeriv: d [H][W][2] = (dx, dy) int16. */
+void or_scharr(const uint8_t* src, int H, int W, int sstride, int16_t* d);
+/* calcOpticalFlowPyrLK with flags 0 (src/LoopHandler.cc:372-375).  pts (x = col, y = row) float pairs.
+ * sum_mode 0 = OpenCV's scalar window-sum order, 1 = the GPU kernel's.  Returns the top level used. */
+int or_lk_pyr(const uint8_t* prev, const uint8_t* next, int H, int W, const float* prev_pts, int n, int win,
+              int max_level, int max_count, double eps, double min_eig, float* next_pts, uint8_t* status,
+              float* err, int sum_mode);
+
 #ifdef __cplusplus
 }
 #endif

@@ -55,6 +55,11 @@ class Oracle:
             "or_ldlt6_solve": (_I, [_P, _P, _P, _I]),
             "or_pose_lm": (_I, [_P, _P, _I, _P, _P, _P, _I]),
             "or_pose_gn": (_I, [_P, _P, _I, _P, _P, _I]),
+            "or_lm_stats": (None, [_P, _I]),
+            "or_pyr_down": (None, [_P, _I, _I, _I, _P]),
+            "or_scharr": (None, [_P, _I, _I, _I, _P]),
+            "or_lk_pyr": (_I, [_P, _P, _I, _I, _P, _I, _I, _I, _I, ctypes.c_double, ctypes.c_double, _P, _P, _P,
+                               _I]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -250,3 +255,31 @@ class Oracle:
         T = np.array(pose, np.float64).copy()
         it = self.lib.or_pose_gn(_p(X), _p(uv), len(X), _p(K), _p(T), sum_mode)
         return T, it
+
+    # ---- cv::calcOpticalFlowPyrLK ----
+    def pyr_down(self, img):
+        img = np.ascontiguousarray(img, np.uint8)
+        H, W = img.shape
+        out = np.zeros(((H + 1) // 2, (W + 1) // 2), np.uint8)
+        self.lib.or_pyr_down(_p(img), H, W, W, _p(out))
+        return out
+
+    def scharr(self, img):
+        img = np.ascontiguousarray(img, np.uint8)
+        H, W = img.shape
+        out = np.zeros((H, W, 2), np.int16)
+        self.lib.or_scharr(_p(img), H, W, W, _p(out))
+        return out
+
+    def lk(self, prev, nxt, pts, win=11, max_level=3, max_count=30, eps=0.01, min_eig=0.001, sum_mode=0):
+        """-> (next_pts [n, 2] (x = col, y = row), status [n] bool, err [n], top level used)."""
+        prev = np.ascontiguousarray(prev, np.uint8)
+        nxt = np.ascontiguousarray(nxt, np.uint8)
+        pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)
+        H, W = prev.shape
+        nextp = np.zeros_like(pts)
+        status = np.zeros(max(len(pts), 1), np.uint8)
+        err = np.zeros(max(len(pts), 1), np.float32)
+        lv = self.lib.or_lk_pyr(_p(prev), _p(nxt), H, W, _p(pts), len(pts), win, max_level, max_count, eps, min_eig,
+                                _p(nextp), _p(status), _p(err), sum_mode)
+        return nextp, status[:len(pts)].astype(bool), err[:len(pts)], lv
