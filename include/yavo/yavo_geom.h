@@ -63,6 +63,32 @@ int yv_f_ransac_batch(struct yv_ctx* ctx, const yv_match* d_matches, int64_t lis
                       int n_lists, const int32_t* d_samples, int64_t sample_stride, int iters, double thr,
                       double* d_F, int32_t* d_max_inliers, int32_t* d_found, void* stream);
 
+/* ---- cv::calcOpticalFlowPyrLK (src/LoopHandler.cc:372-375) ---------------------------
+ * Restates OpenCV's pyramidal LK (flags 0: no initial flow) -- pyrDown pyramid (levels stop when the next one
+ * would be <= win), Scharr derivatives, 14-bit bilinear windows, minEig test, Newton steps with the eps^2 and
+ * oscillation tests, the level-0 error.  Points are cv::Point2f (x = column, y = row).  Window sums use the
+ * GPU order of oracle/yavo_oracle_lk.c (sum_mode 1). */
+typedef struct yv_lk yv_lk;
+/* Workspace for up to max_images H x W images: pyramids and derivatives.  win <= 22, max_level <= 7. */
+int yv_lk_create(struct yv_ctx* ctx, int max_images, int H, int W, int win, int max_level, yv_lk** out);
+void yv_lk_destroy(yv_lk* lk);
+/* Levels actually used (buildOpticalFlowPyramid's return value). */
+int yv_lk_levels(const yv_lk* lk);
+/* Pyramids + derivatives of n_images device images (image i at d_images + i*image_pitch, rows `stride`
+ * apart).  The images must stay valid until the last yv_lk_track_batch that reads them has completed. */
+int yv_lk_build(yv_lk* lk, const uint8_t* d_images, int n_images, int stride, int64_t image_pitch, void* stream);
+/* Track d_counts[p] points of pair p (prev image d_pairs[2p], next image d_pairs[2p+1], indices into the
+ * last yv_lk_build): points d_pts + 2*(p*pts_stride + i); results at the same positions of d_next / d_status /
+ * d_err.  max_count, eps, min_eig: TermCriteria(COUNT+EPS, max_count, eps) and minEigThreshold. */
+int yv_lk_track_batch(yv_lk* lk, const int32_t* d_pairs, int n_pairs, const float* d_pts, const int32_t* d_counts,
+                      int pts_stride, int max_count, double eps, double min_eig, float* d_next, uint8_t* d_status,
+                      float* d_err, void* stream);
+/* Host-pointer drop-in for cv::calcOpticalFlowPyrLK(prev, next, prevPts, nextPts, status, err,
+ * Size(win, win), max_level, TermCriteria(COUNT+EPS, max_count, eps), 0, min_eig); n <= 65536. */
+int yv_calc_optical_flow_pyr_lk(struct yv_ctx* ctx, const uint8_t* prev, const uint8_t* next, int H, int W,
+                                int stride, const float* prev_pts, int n, int win, int max_level, int max_count,
+                                double eps, double min_eig, float* next_pts, uint8_t* status, float* err);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,77 @@
+"""GPU parity of the pyramidal LK row (cv::calcOpticalFlowPyrLK) against the oracle's
+restatement in the GPU window-sum order (sum_mode 1): tracked points, status and error bit for bit.  Against
+OpenCV's own scalar order (sum_mode 0) the points agree within LK_TOL px (the float window sums round
+differently)."""
+import numpy as np
+import pytest
+
+import ya_vo_amd as yv
+from ya_vo_amd.synth import synth_frame
+
+pytestmark = pytest.mark.gpu
+LK_TOL = 1e-2  # px, GPU vs OpenCV's scalar summation order
+
+
+def _pts(rng, n, H, W, margin=-20):
+    return np.stack([rng.uniform(margin, W - 1 - margin, n), rng.uniform(margin, H - 1 - margin, n)], 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("H,W,win,seed", [(376, 1241, 11, 0), (120, 200, 11, 1), (40, 60, 7, 2), (376, 1241, 21, 3)])
+def test_lk_matches_oracle(ctx, oracle, H, W, win, seed):
+    prev, nxt = synth_frame(20 + seed, 0, 0, H, W), synth_frame(20 + seed, 1, 3, H, W)
+    rng = np.random.default_rng(seed)
+    pts = _pts(rng, 500, H, W)
+    pts[:3] = [[-30, 5], [W + 40, 10], [5, H + 50]]  # rejected at level 0
+    g, gs, ge = ctx.calc_optical_flow_pyr_lk(prev, nxt, pts, win=win)
+    o, os_, oe, _ = oracle.lk(prev, nxt, pts, win=win, sum_mode=1)
+    np.testing.assert_array_equal(gs, os_)
+    np.testing.assert_array_equal(g, o)
+    np.testing.assert_array_equal(ge, oe)
+    r, rs, _, _ = oracle.lk(prev, nxt, pts, win=win, sum_mode=0)
+    both = gs & rs
+    assert np.mean(gs == rs) > 0.99
+    np.testing.assert_allclose(g[both], r[both], atol=LK_TOL)
+
+
+def test_lk_flat_image_fails_min_eig(ctx, oracle):
+    flat = np.full((64, 80), 128, np.uint8)
+    pts = np.array([[40.0, 30.0], [10.5, 12.25]], np.float32)
+    g, gs, ge = ctx.calc_optical_flow_pyr_lk(flat, flat, pts)
+    o, os_, oe, _ = oracle.lk(flat, flat, pts, sum_mode=1)
+    assert not gs.any() and not os_.any()
+    np.testing.assert_array_equal(g, o)
+
+
+def test_lk_batch_pairs(ctx, oracle):
+    """Several (prev, next) pairs with different point counts in one launch through yv_lk_build / track."""
+    import torch
+    H, W, n_img = 188, 300, 4
+    imgs = np.stack([synth_frame(40, k, 2 * k, H, W) for k in range(n_img)])
+    d_img = torch.from_numpy(imgs).to("cuda:0")
+    pairs = np.array([[0, 1], [1, 2], [3, 2]], np.int32)
+    counts = np.array([300, 17, 0], np.int32)
+    stride = 320
+    rng = np.random.default_rng(9)
+    pts = np.zeros((len(pairs), stride, 2), np.float32)
+    for p in range(len(pairs)):
+        pts[p, :counts[p]] = _pts(rng, counts[p], H, W, margin=5)
+    lk = yv.Lk(ctx, n_img, H, W)
+    dev = "cuda:0"
+    d_pairs, d_cnt = torch.from_numpy(pairs).to(dev), torch.from_numpy(counts).to(dev)
+    d_pts = torch.from_numpy(pts).to(dev)
+    d_next = torch.zeros_like(d_pts)
+    d_st = torch.zeros((len(pairs), stride), dtype=torch.uint8, device=dev)
+    d_err = torch.zeros((len(pairs), stride), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    lk.build(d_img.data_ptr(), n_img, W, H * W)
+    lk.track(d_pairs.data_ptr(), len(pairs), d_pts.data_ptr(), d_cnt.data_ptr(), stride, d_next.data_ptr(),
+             d_st.data_ptr(), d_err.data_ptr())
+    ctx.sync()
+    g, gs, ge = d_next.cpu().numpy(), d_st.cpu().numpy().astype(bool), d_err.cpu().numpy()
+    for p, (a, b) in enumerate(pairs):
+        n = counts[p]
+        o, os_, oe, _ = oracle.lk(imgs[a], imgs[b], pts[p, :n], sum_mode=1)
+        np.testing.assert_array_equal(gs[p, :n], os_)
+        np.testing.assert_array_equal(g[p, :n], o)
+        np.testing.assert_array_equal(ge[p, :n], oe)
+    lk.close()

@@ -100,6 +100,12 @@ GEOM_SIGNATURES = {
     "yv_pose_lm_batch": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "yv_pose_gn_batch": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P]),
     "yv_f_ransac_batch": (_I, [_P, _P, ctypes.c_int64, _P, _I, _P, ctypes.c_int64, _I, _D, _P, _P, _P, _P]),
+    "yv_lk_create": (_I, [_P, _I, _I, _I, _I, _I, ctypes.POINTER(_P)]),
+    "yv_lk_destroy": (None, [_P]),
+    "yv_lk_levels": (_I, [_P]),
+    "yv_lk_build": (_I, [_P, _P, _I, _I, ctypes.c_int64, _P]),
+    "yv_lk_track_batch": (_I, [_P, _P, _I, _P, _P, _I, _I, _D, _D, _P, _P, _P, _P]),
+    "yv_calc_optical_flow_pyr_lk": (_I, [_P, _P, _P, _I, _I, _I, _P, _I, _I, _I, _I, _D, _D, _P, _P, _P]),
 }
 
 
@@ -144,6 +150,20 @@ def _f64(a, shape=None) -> np.ndarray:
 
 class _GeomMixin:
     """Geometry rows (include/yavo/yavo_geom.h). Poses: Sophus SE3d::data() = {qx, qy, qz, qw, tx, ty, tz}."""
+
+    def calc_optical_flow_pyr_lk(self, prev, nxt, pts, win=11, max_level=3, max_count=30, eps=0.01, min_eig=0.001):
+        """cv::calcOpticalFlowPyrLK (flags 0) -> (next_pts [n, 2] (x = col, y = row), status [n] bool, err [n])."""
+        prev = np.ascontiguousarray(prev, np.uint8)
+        nxt = np.ascontiguousarray(nxt, np.uint8)
+        p = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)
+        H, W = prev.shape
+        out = np.zeros_like(p)
+        st = np.zeros(max(len(p), 1), np.uint8)
+        err = np.zeros(max(len(p), 1), np.float32)
+        _check(self.lib.yv_calc_optical_flow_pyr_lk(self.handle, _ptr(prev), _ptr(nxt), H, W, W, _ptr(p), len(p), win,
+                                                    max_level, max_count, eps, min_eig, _ptr(out), _ptr(st),
+                                                    _ptr(err)), "yv_calc_optical_flow_pyr_lk")
+        return out, st[:len(p)].astype(bool), err[:len(p)]
 
     def f_ransac(self, matches: np.ndarray, samples: np.ndarray, thr: float = 0.1):
         """_3DHandler::getFRANSAC -> (found, F [3,3], max_inliers)."""
@@ -372,3 +392,37 @@ class Batch:
         v = _BatchView()
         _check(self.lib.yv_batch_view_get(self.handle, ctypes.byref(v)), "yv_batch_view_get")
         return v
+
+
+class Lk:
+    """Batched pyramidal LK workspace (yv_lk): build pyramids of device images, track point lists per pair."""
+
+    def __init__(self, ctx: "Context", max_images: int, H: int, W: int, win: int = 11, max_level: int = 3):
+        self.ctx, self.lib = ctx, ctx.lib
+        h = ctypes.c_void_p()
+        _check(self.lib.yv_lk_create(ctx.handle, max_images, H, W, win, max_level, ctypes.byref(h)), "yv_lk_create")
+        self.handle = h
+        self.levels = self.lib.yv_lk_levels(h)
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.yv_lk_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def build(self, d_images: int, n_images: int, stride: int, pitch: int, stream: int = 0) -> None:
+        _check(self.lib.yv_lk_build(self.handle, ctypes.c_void_p(d_images), n_images, stride, pitch,
+                                    ctypes.c_void_p(stream) if stream else None), "yv_lk_build")
+
+    def track(self, d_pairs: int, n_pairs: int, d_pts: int, d_counts: int, pts_stride: int, d_next: int,
+              d_status: int, d_err: int, max_count: int = 30, eps: float = 0.01, min_eig: float = 0.001,
+              stream: int = 0) -> None:
+        _check(self.lib.yv_lk_track_batch(self.handle, ctypes.c_void_p(d_pairs), n_pairs, ctypes.c_void_p(d_pts),
+                                          ctypes.c_void_p(d_counts), pts_stride, max_count, eps, min_eig,
+                                          ctypes.c_void_p(d_next), ctypes.c_void_p(d_status), ctypes.c_void_p(d_err),
+                                          ctypes.c_void_p(stream) if stream else None), "yv_lk_track_batch")

@@ -951,4 +951,167 @@ int yv_f_ransac_batch(yv_ctx* ctx, const yv_match* d_matches, int64_t list_strid
     return check_launch();
 }
 
+// ------------------------------------------------------------------------------------------------
+// cv::calcOpticalFlowPyrLK
+// ------------------------------------------------------------------------------------------------
+}  // extern "C"
+
+struct yv_lk {
+    yv_ctx* ctx = nullptr;
+    int max_images = 0, H = 0, W = 0;
+    yavo::LkParams P;
+};
+
+extern "C" {
+
+int yv_lk_create(yv_ctx* ctx, int max_images, int H, int W, int win, int max_level, yv_lk** out) {
+    if (!ctx || !out || max_images <= 0 || H < 1 || W < 1 || win < 3 || win > 22 || max_level < 0 ||
+        max_level >= yavo::kLkMaxLevels || (int64_t)H * W >= (1ll << 31))
+        return YV_ERR_INVALID;
+    *out = nullptr;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    yv_lk* lk = new (std::nothrow) yv_lk();
+    if (!lk) return YV_ERR_INVALID;
+    lk->ctx = ctx;
+    lk->max_images = max_images;
+    lk->H = H;
+    lk->W = W;
+    yavo::LkParams& P = lk->P;
+    P.win = win;
+    P.h[0] = H;
+    P.w[0] = W;
+    // buildOpticalFlowPyramid: stop when the next level would be <= winSize in either dimension
+    int levels = 0;
+    for (int l = 0; l < max_level; ++l) {
+        const int h = (P.h[l] + 1) / 2, w = (P.w[l] + 1) / 2;
+        if (w <= win || h <= win) break;
+        P.h[l + 1] = h;
+        P.w[l + 1] = w;
+        levels = l + 1;
+    }
+    P.levels = levels;
+    int64_t off = 0, doff = 0;
+    for (int l = 0; l <= levels; ++l) {
+        if (l >= 1) {
+            P.off[l] = off;
+            off += ((int64_t)P.h[l] * P.w[l] + 255) & ~(int64_t)255;
+        }
+        P.der_off[l] = doff;
+        doff += ((int64_t)P.h[l] * P.w[l] * 2 + 127) & ~(int64_t)127;
+    }
+    P.pyr_pitch = std::max<int64_t>(off, 256);
+    P.der_pitch = doff;
+    if (dalloc(&P.pyr, (size_t)P.pyr_pitch * max_images) != YV_OK ||
+        dalloc(&P.der, (size_t)P.der_pitch * max_images) != YV_OK) {
+        if (P.pyr) (void)hipFree(P.pyr);
+        if (P.der) (void)hipFree(P.der);
+        delete lk;
+        return YV_ERR_HIP;
+    }
+    *out = lk;
+    return YV_OK;
+}
+
+void yv_lk_destroy(yv_lk* lk) {
+    if (!lk) return;
+    (void)hipSetDevice(lk->ctx->device);
+    (void)hipDeviceSynchronize();
+    if (lk->P.pyr) (void)hipFree(lk->P.pyr);
+    if (lk->P.der) (void)hipFree(lk->P.der);
+    delete lk;
+}
+
+int yv_lk_levels(const yv_lk* lk) { return lk ? lk->P.levels : YV_ERR_INVALID; }
+
+int yv_lk_build(yv_lk* lk, const uint8_t* d_images, int n_images, int stride, int64_t image_pitch, void* stream) {
+    if (!lk || !d_images || n_images <= 0 || n_images > lk->max_images || stride < lk->W ||
+        image_pitch < (int64_t)stride * (lk->H - 1) + lk->W)
+        return YV_ERR_INVALID;
+    if (set_device(lk->ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : lk->ctx->stream;
+    lk->P.img0 = d_images;
+    lk->P.stride0 = stride;
+    lk->P.pitch0 = image_pitch;
+    yavo::launch_lk_pyramid(lk->P, n_images, s);
+    return check_launch();
+}
+
+int yv_lk_track_batch(yv_lk* lk, const int32_t* d_pairs, int n_pairs, const float* d_pts, const int32_t* d_counts,
+                      int pts_stride, int max_count, double eps, double min_eig, float* d_next, uint8_t* d_status,
+                      float* d_err, void* stream) {
+    if (!lk || !lk->P.img0 || n_pairs < 0 || pts_stride < 0 ||
+        (n_pairs > 0 && (!d_pairs || !d_pts || !d_counts || !d_next || !d_status || !d_err)))
+        return YV_ERR_INVALID;
+    if (n_pairs == 0 || pts_stride == 0) return YV_OK;
+    if (set_device(lk->ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : lk->ctx->stream;
+    yavo::LkParams P = lk->P;
+    // TermCriteria handling of SparsePyrLKOpticalFlowImpl: maxCount clipped to [0, 100], eps to [0, 10], squared
+    P.max_count = std::min(std::max(max_count, 0), 100);
+    const double e = std::min(std::max(eps, 0.), 10.);
+    P.eps2 = e * e;
+    P.min_eig = min_eig;
+    yavo::launch_lk_track(P, d_pairs, n_pairs, d_pts, d_counts, pts_stride, pts_stride, d_next, d_status, d_err, s);
+    return check_launch();
+}
+
+int yv_calc_optical_flow_pyr_lk(yv_ctx* ctx, const uint8_t* prev, const uint8_t* next, int H, int W, int stride,
+                                const float* prev_pts, int n, int win, int max_level, int max_count, double eps,
+                                double min_eig, float* next_pts, uint8_t* status, float* err) {
+    if (!ctx || !prev || !next || n < 0 || (n > 0 && (!prev_pts || !next_pts || !status || !err)) || stride < W)
+        return YV_ERR_INVALID;
+    if (n > 65536) return YV_ERR_CAPACITY;
+    if (n == 0) return YV_OK;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    yv_lk* lk = nullptr;
+    int rc = yv_lk_create(ctx, 2, H, W, win, max_level, &lk);
+    if (rc != YV_OK) return rc;
+    hipStream_t s = ctx->stream;
+    Arena a{ctx};
+    uint8_t* dimg;
+    float *dpts, *dnext, *derr;
+    int32_t *dpair, *dcnt;
+    uint8_t* dst;
+    const int64_t pitch = (int64_t)H * W;
+    a.add(&dimg, (size_t)(2 * pitch + 64));
+    a.add(&dpts, 2 * (size_t)n);
+    a.add(&dnext, 2 * (size_t)n);
+    a.add(&derr, (size_t)n);
+    a.add(&dpair, 2);
+    a.add(&dcnt, 1);
+    a.add(&dst, (size_t)n);
+    if (a.commit() != YV_OK) {
+        yv_lk_destroy(lk);
+        return YV_ERR_HIP;
+    }
+    int status_rc = YV_OK;
+    do {
+        if (hipMemcpy2DAsync(dimg, W, prev, stride, W, H, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpy2DAsync(dimg + pitch, W, next, stride, W, H, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(dpts, prev_pts, sizeof(float) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess) {
+            status_rc = YV_ERR_HIP;
+            break;
+        }
+        ctx->h_pinned[0] = 0;
+        ctx->h_pinned[1] = 1;
+        ctx->h_pinned[2] = n;
+        if (hipMemcpyAsync(dpair, ctx->h_pinned, 2 * sizeof(int32_t), hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(dcnt, ctx->h_pinned + 2, sizeof(int32_t), hipMemcpyHostToDevice, s) != hipSuccess) {
+            status_rc = YV_ERR_HIP;
+            break;
+        }
+        status_rc = yv_lk_build(lk, dimg, 2, W, pitch, nullptr);
+        if (status_rc != YV_OK) break;
+        status_rc = yv_lk_track_batch(lk, dpair, 1, dpts, dcnt, n, max_count, eps, min_eig, dnext, dst, derr, nullptr);
+        if (status_rc != YV_OK) break;
+        if (hipMemcpyAsync(next_pts, dnext, sizeof(float) * 2 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(status, dst, (size_t)n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(err, derr, sizeof(float) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            status_rc = YV_ERR_HIP;
+    } while (0);
+    yv_lk_destroy(lk);
+    return status_rc;
+}
+
 }  // extern "C"

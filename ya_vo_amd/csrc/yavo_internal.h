@@ -67,6 +67,26 @@ void launch_pose_lm(const int32_t* offsets, int n_problems, const double* X, con
                     double* poses, uint8_t* outlier, int32_t* inliers, hipStream_t s);
 void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
                     double* poses, int32_t* iters, hipStream_t s);
+// cv::calcOpticalFlowPyrLK workspace view (yavo_lk.hip).  Level 0 is the caller's image; levels >= 1 live in
+// `pyr` ([image][pyr_pitch], level l at off[l], row stride w[l]); derivatives of every level in `der`
+// ([image][der_pitch] int16, level l at der_off[l], (dx, dy) interleaved, row stride 2 w[l]).
+constexpr int kLkMaxLevels = 8;
+struct LkParams {
+    int levels = 0, win = 11, max_count = 30;
+    double eps2 = 1e-4, min_eig = 1e-3;
+    int h[kLkMaxLevels] = {}, w[kLkMaxLevels] = {};
+    int64_t off[kLkMaxLevels] = {}, der_off[kLkMaxLevels] = {};
+    const uint8_t* img0 = nullptr;
+    int stride0 = 0;
+    int64_t pitch0 = 0;
+    uint8_t* pyr = nullptr;
+    int64_t pyr_pitch = 0;
+    int16_t* der = nullptr;
+    int64_t der_pitch = 0;
+};
+void launch_lk_pyramid(const LkParams& P, int n_images, hipStream_t s);
+void launch_lk_track(const LkParams& P, const int32_t* pairs, int n_pairs, const float* pts, const int32_t* counts,
+                     int pts_stride, int max_pts, float* next_pts, uint8_t* status, float* err, hipStream_t s);
 void launch_track_build(const int32_t* tracks, int n_tracks, const int32_t* pairs, const yv_keypoint* keypoints,
                         const int32_t* kp_count, const int2* match_dj, const int32_t* match_lim, int max_kp,
                         const double* K, const double* T_right, double* edge_X, double* edge_uv, int32_t* edge_query,
