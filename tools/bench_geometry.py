@@ -138,6 +138,47 @@ def main():
     out["triangulate"] = {"host_api_ms_per_list": round(host_ms, 4), "cpu_oracle_ms_per_list": round(cpu * 1e3, 3),
                           "note": "batched device-resident triangulation runs inside track_build_kernel "
                                   "(bench.py stage track_edges)"}
+    # ---- pyramidal LK: L frame pairs (synthetic 1241x376, frame k+1 = frame k shifted), 2000 points each --
+    from ya_vo_amd.synth import synth_stereo_batch
+    H, W = 376, 1241
+    imgs = synth_stereo_batch(77, L // 2 + 1)[::2]  # left images of consecutive frames
+    imgs = np.ascontiguousarray(imgs[: L // 2 + 1])
+    n_img = len(imgs)
+    n_pairs = n_img - 1
+    npts = 2000
+    rng = np.random.default_rng(3)
+    pts = np.stack([rng.uniform(20, W - 21, (n_pairs, npts)), rng.uniform(20, H - 21, (n_pairs, npts))], -1)
+    pts = pts.astype(np.float32)
+    d_img = torch.from_numpy(imgs).to(dev)
+    d_pairs = torch.from_numpy(np.stack([np.arange(n_pairs), np.arange(1, n_pairs + 1)], 1).astype(np.int32)).to(dev)
+    d_cnt = torch.full((n_pairs,), npts, dtype=torch.int32, device=dev)
+    d_pts = torch.from_numpy(pts).to(dev)
+    d_next = torch.zeros_like(d_pts)
+    d_st = torch.zeros((n_pairs, npts), dtype=torch.uint8, device=dev)
+    d_err = torch.zeros((n_pairs, npts), dtype=torch.float32, device=dev)
+    lk = yv.Lk(ctx, n_img, H, W)
+
+    def lk_build():
+        lk.build(d_img.data_ptr(), n_img, W, H * W, stream)
+
+    def lk_track():
+        lk.track(d_pairs.data_ptr(), n_pairs, d_pts.data_ptr(), d_cnt.data_ptr(), npts, d_next.data_ptr(),
+                 d_st.data_ptr(), d_err.data_ptr(), stream=stream)
+
+    ms_b = timed(lk_build)
+    ms_t = timed(lk_track)
+    torch.cuda.synchronize()
+    g = d_next[0].cpu().numpy()
+    t0 = time.perf_counter()
+    o, os_, oe, _ = orc.lk(imgs[0], imgs[1], pts[0], sum_mode=1)
+    cpu = time.perf_counter() - t0
+    out["lk"] = {"pairs": n_pairs, "points_per_pair": npts, "gpu_pyramid_ms": round(ms_b, 4),
+                 "gpu_track_ms": round(ms_t, 4),
+                 "gpu_points_per_s": round(n_pairs * npts / ((ms_b * n_img / n_img + ms_t) / 1e3), 1),
+                 "cpu_oracle_points_per_s": round(npts / cpu, 1), "cpu_threads": 1,
+                 "pair0_bit_identical": bool(np.array_equal(g, o)),
+                 "pair0_tracked": int(os_.sum())}
+    lk.close()
     print(json.dumps(out), flush=True)
     ctx.close()
 
