@@ -147,14 +147,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU over RCCL ("nccl"); YAVO_BENCH_BACKEND=gloo rehearses the multi-rank logic with
+    # several ranks sharing fewer GPUs (device = local rank modulo the visible devices)
+    backend = os.environ.get("YAVO_BENCH_BACKEND", "nccl")
+    dev_index = local_rank % max(torch.cuda.device_count(), 1)
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        dist.init_process_group(backend)
+    dev = torch.device("cuda", dev_index)
     torch.cuda.set_device(dev)
 
     offsets = np.fromfile(os.path.join(ROOT, "tests", "golden", "brief_offsets_mt19937_42.bin"), np.int8)
-    ctx = yv.Context(local_rank)
+    ctx = yv.Context(dev_index)
     ctx.set_brief_offsets(offsets)
     B = args.frames
     n_img = 2 * B
@@ -204,7 +208,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
