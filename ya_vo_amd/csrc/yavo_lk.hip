@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void scharr_kernel(const uint8_t* __restrict__
 // LK
 // ------------------------------------------------------------------------------------------------
 constexpr int kWBits = 14;
-constexpr int kMaxPix = 8;  // window pixels per lane: win <= 22
+// window pixels per lane (MP): ceil(win^2 / 64) rounded to 2, 4 or 8 (win <= 22); the launch picks the smallest
 
 __device__ __forceinline__ int descale(int x, int n) { return (x + (1 << (n - 1))) >> n; }
 
@@ -105,13 +105,24 @@ __device__ __forceinline__ void weights(float a, float b, int* iw) {
     iw[3] = (1 << kWBits) - iw[0] - iw[1] - iw[2];
 }
 
-// sum over the window in the oracle's sum_mode 1 order: lane partials from 0.0f, then p[l] += p[l + off]
+// Sum over the window in the oracle's sum_mode 1 order: lane partials from 0.0f, then p[l] += p[l + off] for
+// off = 32 .. 1, all in registers: v_permlane32_swap / v_permlane16_swap bring lane l + 32 / l + 16 to lane l
+// (the swapped second operand), DPP row_shl:off does l + off inside a 16-lane row; lane 0 holds the total.
 __device__ __forceinline__ float wave_sum(float part) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) part = part + __shfl_down(part, off, 64);
-    return __shfl(part, 0, 64);
+    float t = __uint_as_float(
+        __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part), false, false)[1]);
+    part = part + t;  // lanes 0..31: p[l] + p[l + 32]
+    t = __uint_as_float(
+        __builtin_amdgcn_permlane16_swap(__float_as_uint(part), __float_as_uint(part), false, false)[1]);
+    part = part + t;  // lanes 0..15 (of each half): + lane l + 16
+    part = part + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(part), 0x108, 0xF, 0xF, false));
+    part = part + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(part), 0x104, 0xF, 0xF, false));
+    part = part + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(part), 0x102, 0xF, 0xF, false));
+    part = part + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(part), 0x101, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(part)));
 }
 
+template <int kMaxPix>
 __global__ __launch_bounds__(256) void lk_kernel(LkParams P, const int32_t* __restrict__ pairs,
                                                  const float* __restrict__ pts, const int32_t* __restrict__ counts,
                                                  int pts_stride, float* __restrict__ next_out,
@@ -163,6 +174,8 @@ __global__ __launch_bounds__(256) void lk_kernel(LkParams P, const int32_t* __re
         // this lane's window pixels: I value and derivatives (IWinBuf / derivIWinBuf)
         int iv[kMaxPix], ixv[kMaxPix], iyv[kMaxPix];
         float a11 = 0.0f, a12 = 0.0f, a22 = 0.0f;
+        // the whole bilinear footprint inside the level image (wave-uniform): no border logic per sample
+        const bool inI = ipx >= 0 && ipy >= 0 && ipx + win < Wl && ipy + win < Hl;
 #pragma unroll
         for (int k = 0; k < kMaxPix; ++k) {
             const int p = lane + 64 * k;
@@ -170,19 +183,27 @@ __global__ __launch_bounds__(256) void lk_kernel(LkParams P, const int32_t* __re
             if (p < npix) {
                 const int y = p / win, x = p - y * win;
                 const int yy = ipy + y, xx = ipx + x;
-                const int r0 = refl(yy, Hl), r1 = refl(yy + 1, Hl), c0 = refl(xx, Wl), c1 = refl(xx + 1, Wl);
-                iv[k] = descale(I[(int64_t)r0 * sI + c0] * iw[0] + I[(int64_t)r0 * sI + c1] * iw[1] +
-                                    I[(int64_t)r1 * sI + c0] * iw[2] + I[(int64_t)r1 * sI + c1] * iw[3],
-                                kWBits - 5);
+                const int r0 = inI ? yy : refl(yy, Hl), r1 = inI ? yy + 1 : refl(yy + 1, Hl);
+                const int c0 = inI ? xx : refl(xx, Wl), c1 = inI ? xx + 1 : refl(xx + 1, Wl);
+                const uint8_t* i0 = I + r0 * sI;
+                const uint8_t* i1 = I + r1 * sI;
+                iv[k] = descale(i0[c0] * iw[0] + i0[c1] * iw[1] + i1[c0] * iw[2] + i1[c1] * iw[3], kWBits - 5);
                 // derivative image: zero outside [0, Hl) x [0, Wl)
                 int dxs[4], dys[4];
+                if (inI) {
+                    const int16_t* d0 = D + (yy * Wl + xx) * 2;
+                    const int16_t* d1 = d0 + Wl * 2;
+                    dxs[0] = d0[0]; dys[0] = d0[1]; dxs[1] = d0[2]; dys[1] = d0[3];
+                    dxs[2] = d1[0]; dys[2] = d1[1]; dxs[3] = d1[2]; dys[3] = d1[3];
+                } else {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int ry = yy + (q >> 1), rx = xx + (q & 1);
-                    const bool in = ry >= 0 && ry < Hl && rx >= 0 && rx < Wl;
-                    const int16_t* dp = D + ((int64_t)(in ? ry : 0) * Wl + (in ? rx : 0)) * 2;
-                    dxs[q] = in ? dp[0] : 0;
-                    dys[q] = in ? dp[1] : 0;
+                    for (int q = 0; q < 4; ++q) {
+                        const int ry = yy + (q >> 1), rx = xx + (q & 1);
+                        const bool in = ry >= 0 && ry < Hl && rx >= 0 && rx < Wl;
+                        const int16_t* dp = D + ((in ? ry : 0) * Wl + (in ? rx : 0)) * 2;
+                        dxs[q] = in ? dp[0] : 0;
+                        dys[q] = in ? dp[1] : 0;
+                    }
                 }
                 ixv[k] = descale(dxs[0] * iw[0] + dxs[1] * iw[1] + dxs[2] * iw[2] + dxs[3] * iw[3], kWBits);
                 iyv[k] = descale(dys[0] * iw[0] + dys[1] * iw[1] + dys[2] * iw[2] + dys[3] * iw[3], kWBits);
@@ -211,6 +232,7 @@ __global__ __launch_bounds__(256) void lk_kernel(LkParams P, const int32_t* __re
                 break;
             }
             weights(nx - (float)inx, ny - (float)iny, iw);
+            const bool inJ = inx >= 0 && iny >= 0 && inx + win < Wl && iny + win < Hl;
             float b1 = 0.0f, b2 = 0.0f;
 #pragma unroll
             for (int k = 0; k < kMaxPix; ++k) {
@@ -218,9 +240,11 @@ __global__ __launch_bounds__(256) void lk_kernel(LkParams P, const int32_t* __re
                 if (p < npix) {
                     const int y = p / win, x = p - y * win;
                     const int yy = iny + y, xx = inx + x;
-                    const int r0 = refl(yy, Hl), r1 = refl(yy + 1, Hl), c0 = refl(xx, Wl), c1 = refl(xx + 1, Wl);
-                    const int diff = descale(J[(int64_t)r0 * sI + c0] * iw[0] + J[(int64_t)r0 * sI + c1] * iw[1] +
-                                                 J[(int64_t)r1 * sI + c0] * iw[2] + J[(int64_t)r1 * sI + c1] * iw[3],
+                    const int r0 = inJ ? yy : refl(yy, Hl), r1 = inJ ? yy + 1 : refl(yy + 1, Hl);
+                    const int c0 = inJ ? xx : refl(xx, Wl), c1 = inJ ? xx + 1 : refl(xx + 1, Wl);
+                    const uint8_t* j0 = J + r0 * sI;
+                    const uint8_t* j1 = J + r1 * sI;
+                    const int diff = descale(j0[c0] * iw[0] + j0[c1] * iw[1] + j1[c0] * iw[2] + j1[c1] * iw[3],
                                              kWBits - 5) - iv[k];
                     b1 = b1 + (float)(diff * ixv[k]);
                     b2 = b2 + (float)(diff * iyv[k]);
@@ -303,7 +327,13 @@ void launch_lk_track(const LkParams& P, const int32_t* pairs, int n_pairs, const
                      int pts_stride, int max_pts, float* next_pts, uint8_t* status, float* err, hipStream_t s) {
     if (n_pairs <= 0 || max_pts <= 0) return;
     dim3 grid((max_pts + 3) / 4, n_pairs);
-    hipLaunchKernelGGL(lk::lk_kernel, grid, dim3(256), 0, s, P, pairs, pts, counts, pts_stride, next_pts, status, err);
+    const int npix = P.win * P.win;
+    if (npix <= 128)
+        hipLaunchKernelGGL(lk::lk_kernel<2>, grid, dim3(256), 0, s, P, pairs, pts, counts, pts_stride, next_pts, status, err);
+    else if (npix <= 256)
+        hipLaunchKernelGGL(lk::lk_kernel<4>, grid, dim3(256), 0, s, P, pairs, pts, counts, pts_stride, next_pts, status, err);
+    else
+        hipLaunchKernelGGL(lk::lk_kernel<8>, grid, dim3(256), 0, s, P, pairs, pts, counts, pts_stride, next_pts, status, err);
 }
 
 }  // namespace yavo
