@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-timing", action="store_true", help="do not record per-stage HIP events")
     ap.add_argument("--no-overlap", action="store_true", help="run the pose LM in order on the main stream")
+    ap.add_argument("--tracker", choices=["match", "lk"], default="match",
+                    help="PnP correspondences: BRIEF temporal matches (default) or calcOpticalFlowPyrLK of frame "
+                         "k-1's stereo map points (the reference's trackLastFrame)")
     return ap.parse_args()
 
 
@@ -171,16 +174,22 @@ def main():
     for k in range(B):
         pairs.append((carry if k == 0 else 2 * (k - 1), 2 * k))  # temporal L_{k-1} -> L_k
         pairs.append((2 * k, 2 * k + 1))                          # stereo L_k -> R_k
-        tracks.append((2 * k + 1, 2 * k))                         # PnP of frame k-1 against frame k's map
+        if args.tracker == "match":
+            tracks.append((2 * k + 1, 2 * k))                     # PnP of frame k-1 against frame k's map
+        elif k > 0:
+            tracks.append((2 * (k - 1) + 1, 2 * k))               # LK: frame k-1's stereo map -> L_k
     batch.set_pairs(pairs)
     from ya_vo_amd import scene
+    if args.tracker == "lk":
+        batch.set_track_lk(2)  # LK images = the left images 0, 2, 4, ...
     batch.set_tracks(tracks, scene.K_KITTI, T_RIGHT)
+    NT = len(tracks)
     identity = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
-    d_prior = torch.from_numpy(np.tile(identity, (B, 1))).to(dev)
+    d_prior = torch.from_numpy(np.tile(identity, (NT, 1))).to(dev)
     # the pose LM of step i runs on the batch's side stream beside step i + 1's image kernels; its output
     # buffer alternates so step i + 1 never writes poses step i's LM is still producing
     batch.set_track_overlap(not args.no_overlap)
-    d_poses = [torch.zeros((B, 7), dtype=torch.float64, device=dev) for _ in range(2)]
+    d_poses = [torch.zeros((NT, 7), dtype=torch.float64, device=dev) for _ in range(2)]
     calls = [0]
 
     def step():
@@ -233,9 +242,9 @@ def main():
         "filt": ctx.download(v.filt_count, np.int32, len(pairs)).astype(np.int64),
     }
     counts["train"] = np.array([counts["kp"][t] for _, t in pairs], np.int64)
-    counts["edges"] = float(np.sum(ctx.download(v.edge_count, np.int32, B)))
-    counts["tq"] = float(np.sum([counts["match"][tp] for _, tp in tracks]))
-    inliers = ctx.download(v.track_inliers, np.int32, B)
+    counts["edges"] = float(np.sum(ctx.download(v.edge_count, np.int32, NT)))
+    counts["tq"] = float(np.sum([counts["match"][tp] for _, tp in tracks])) if args.tracker == "match" else 0.0
+    inliers = ctx.download(v.track_inliers, np.int32, NT)
     gpu_poses = d_poses[(calls[0] - 1) & 1].cpu().numpy()
 
     stages = {}
@@ -314,7 +323,8 @@ def main():
                    "mean_candidates_per_image": round(float(np.mean(counts["cand"][:n_img])), 1),
                    "mean_keypoints_per_image": round(float(np.mean(counts["kp"][:n_img])), 1),
                    "mean_filtered_matches_per_pair": round(float(np.mean(counts["filt"])), 1),
-                   "mean_pnp_edges_per_frame": round(counts["edges"] / B, 1),
+                   "tracker": args.tracker, "pnp_frames_per_step": NT,
+                   "mean_pnp_edges_per_frame": round(counts["edges"] / max(NT, 1), 1),
                    "mean_pnp_inliers_per_frame": round(float(np.mean(inliers)), 1)},
         "stages_ms_per_launch": stages,
         "stage_rooflines": per_stage if not args.no_timing else None,
@@ -323,7 +333,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and args.cpu_baseline != "none":
+    if rank == 0 and world == 1 and args.cpu_baseline != "none" and args.tracker == "match":
         cb = cpu_baseline(args.cpu_baseline, args.cpu_threads, offsets.reshape(256, 4), frames, gpu_poses)
         main_cb = cb.get("literal") or cb.get("efficient")
         out["cpu_baseline"] = main_cb

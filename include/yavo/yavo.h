@@ -121,6 +121,15 @@ int yv_batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* s
  * are then complete only after yv_batch_track_sync (or a device-wide synchronization). */
 int yv_batch_set_track_overlap(yv_batch* b, int on);
 int yv_batch_track_sync(yv_batch* b);
+/* LK tracking mode, the reference's trackLastFrame (src/LoopHandler.cc:298-454): with image_step > 0 a track
+ * is {stereo pair of frame k-1, image index of frame k}.  Frame k-1's map points are its left keypoints whose
+ * stereo match survives removeOutliers and triangulates; they are tracked into frame k by
+ * calcOpticalFlowPyrLK(win, max_level, TermCriteria(COUNT+EPS, max_count, eps), flags 0, min_eig) on the last
+ * run's images 0, image_step, 2 image_step, ... (both images of a track must be among them), and every point
+ * with status 1 becomes an edge at cv::Point2i(next.y, next.x) (truncation).  image_step = 0: match mode.
+ * Clears the tracks (set them again).  Declared in yavo_geom.h: the LK workspace API it uses. */
+int yv_batch_set_track_lk(yv_batch* b, int image_step, int win, int max_level, int max_count, double eps,
+                          double min_eig);
 /* Per-stage device time of the runs since the last reset, when timing is enabled (HIP events recorded
  * on the run stream around every stage).  Stages: 0 detect (FAST + Harris + blur, one fused kernel),
  * 1 top-K + checkBoundry, 2 BRIEF, 3 match, 4 Matches records + removeOutliers (+ carry copies),

@@ -13,8 +13,10 @@
  *                            integer products, minEig test, Newton steps with the eps^2 test and the
  *                            oscillation check, the level-0 error (mean |diff| / 32)
  * Sums over the 11x11 window are taken either in OpenCV's scalar order (sum_mode 0, row-major) or in the
- * GPU kernel's order (sum_mode 1: window pixel p = 11y + x goes to lane p mod 64, each lane adds its terms
- * in order starting from 0.0f, then the 64 partials are reduced by p[l] += p[l + off], off = 32 .. 1).  The
+ * GPU kernel's order (sum_mode 1: 16 lanes per point, S = ceil(win / 4); lane g owns the S x S task at rows
+ * S (g >> 2) .., columns S (g & 3) .. of the window and adds its in-window terms row-major from 0.0f; the 16
+ * partials are then combined by the butterfly q[l] = q[l] + q[l ^ off], off = 8, 4, 2, 1, whose lane-0 value
+ * is the tree p[l] += p[l + off]).  The
  * reference's x86 OpenCV build runs a 4-lane SIMD path for x < 8 of each row, another float order: parity
  * with the reference binary is unpinned (no fixture holds LK outputs).
  */
@@ -92,19 +94,24 @@ static int der_at(const lk_level* L, int y, int x, int c) {
 #define LK_W_BITS 14
 #define LK_DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
 
-/* window sums in the requested order; terms[p] for p = 0 .. n-1 in row-major window order */
-static float lk_sum(const float* terms, int n, int sum_mode) {
+/* window sums in the requested order; terms[p] for p = 0 .. win^2 - 1 in row-major window order */
+static float lk_sum(const float* terms, int win, int sum_mode) {
     if (sum_mode == 0) {
         float s = 0.0f;
-        for (int p = 0; p < n; ++p) s = s + terms[p];
+        for (int p = 0; p < win * win; ++p) s = s + terms[p];
         return s;
     }
-    float part[64];
-    for (int l = 0; l < 64; ++l) {
-        part[l] = 0.0f;
-        for (int p = l; p < n; p += 64) part[l] = part[l] + terms[p];
+    const int S = (win + 3) / 4;
+    float part[16];
+    for (int g = 0; g < 16; ++g) {
+        part[g] = 0.0f;
+        for (int i = 0; i < S; ++i)
+            for (int j = 0; j < S; ++j) {
+                const int y = S * (g >> 2) + i, x = S * (g & 3) + j;
+                if (y < win && x < win) part[g] = part[g] + terms[y * win + x];
+            }
     }
-    for (int off = 32; off > 0; off >>= 1)
+    for (int off = 8; off > 0; off >>= 1)
         for (int l = 0; l < off; ++l) part[l] = part[l] + part[l + off];
     return part[0];
 }
@@ -169,9 +176,9 @@ static void lk_point(const lk_level* I, const lk_level* J, int level, int max_le
             t22[p] = (float)(iyv * iyv);
         }
     const float FLT_SCALE = 1.f / (1 << 20);
-    const float A11 = lk_sum(t11, n, sum_mode) * FLT_SCALE;
-    const float A12 = lk_sum(t12, n, sum_mode) * FLT_SCALE;
-    const float A22 = lk_sum(t22, n, sum_mode) * FLT_SCALE;
+    const float A11 = lk_sum(t11, win, sum_mode) * FLT_SCALE;
+    const float A12 = lk_sum(t12, win, sum_mode) * FLT_SCALE;
+    const float A22 = lk_sum(t22, win, sum_mode) * FLT_SCALE;
     float D = A11 * A22 - A12 * A12;
     const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * win * win);
     if (minEig < min_eig_thr || D < FLT_EPSILON) {
@@ -201,8 +208,8 @@ static void lk_point(const lk_level* I, const lk_level* J, int level, int max_le
                 tb[p] = (float)(diff * Iw[3 * p + 1]);
                 t12[p] = (float)(diff * Iw[3 * p + 2]);
             }
-        const float b1 = lk_sum(tb, n, sum_mode) * FLT_SCALE;
-        const float b2 = lk_sum(t12, n, sum_mode) * FLT_SCALE;
+        const float b1 = lk_sum(tb, win, sum_mode) * FLT_SCALE;
+        const float b2 = lk_sum(t12, win, sum_mode) * FLT_SCALE;
         const float dx = (float)((A12 * b2 - A22 * b1) * D);
         const float dy = (float)((A12 * b1 - A11 * b2) * D);
         nx += dx;
@@ -233,7 +240,7 @@ static void lk_point(const lk_level* I, const lk_level* J, int level, int max_le
                                                 LK_W_BITS - 5) - Iw[3 * p];
                     tb[p] = fabsf((float)diff);
                 }
-            *err = lk_sum(tb, n, sum_mode) * 1.f / (float)(32 * win * win);
+            *err = lk_sum(tb, win, sum_mode) * 1.f / (float)(32 * win * win);
         }
     }
     free(Iw);

@@ -123,3 +123,49 @@ def test_track_overlap_pipelined(ctx, oracle, offsets):
             T = track_pose(oracle, kq, kp[i][2 * k], kp[i][2 * k + 1], scene.K_KITTI, T_RIGHT)[3]
             np.testing.assert_array_equal(P[k], T)
     b.close()
+
+
+def test_track_lk_mode_matches_oracle(ctx, oracle, offsets):
+    """LK tracking mode (the reference's trackLastFrame): frame k-1's stereo map points tracked into frame k by
+    calcOpticalFlowPyrLK, then the pose LM; edges and poses bit for bit against tests/track_chain.py."""
+    import torch
+    from track_chain import lk_track_pose
+    n_frames = 3
+    b = yv.Batch(ctx, 2 * n_frames, H, W, 2000, 2 * n_frames)
+    carry = 2 * n_frames
+    pairs = []
+    for k in range(n_frames):
+        pairs.append((carry if k == 0 else 2 * (k - 1), 2 * k))
+        pairs.append((2 * k, 2 * k + 1))
+    b.set_pairs(pairs)
+    b.set_track_lk(2)
+    tracks = [(2 * (k - 1) + 1, 2 * k) for k in range(1, n_frames)]  # {stereo pair of k-1, image of L_k}
+    b.set_tracks(tracks, scene.K_KITTI, T_RIGHT)
+    frames = np.stack([im for k in range(n_frames) for im in (synth_frame(71, k, 3 * k), synth_frame(71, k, 3 * k + 8))])
+    d = torch.from_numpy(frames).to("cuda:0")
+    nt = len(tracks)
+    d_prior = torch.from_numpy(np.tile(IDENTITY, (nt, 1))).to("cuda:0")
+    d_pose = torch.zeros((nt, 7), dtype=torch.float64, device="cuda:0")
+    torch.cuda.synchronize()
+    b.run(d.data_ptr(), len(frames), W, H * W, 20)
+    b.track(d_prior.data_ptr(), d_pose.data_ptr())
+    ctx.sync()
+    v = b.view()
+    kps = [oracle.brief(im, oracle.fast(im, 2000)[0], offsets) for im in frames]
+    cnt = ctx.download(v.edge_count, np.int32, nt)
+    P = d_pose.cpu().numpy()
+    for t, k in enumerate(range(1, n_frames)):
+        X, uv, q, T, out, inl = lk_track_pose(oracle, frames[2 * (k - 1)], frames[2 * k], kps[2 * (k - 1)],
+                                              kps[2 * (k - 1) + 1], scene.K_KITTI, T_RIGHT)
+        assert cnt[t] == len(X) > 500
+        base = t * 2000
+        np.testing.assert_array_equal(ctx.download(v.edge_X + base * 24, np.float64, 3 * cnt[t]).reshape(-1, 3), X)
+        np.testing.assert_array_equal(ctx.download(v.edge_uv + base * 16, np.float64, 2 * cnt[t]).reshape(-1, 2), uv)
+        np.testing.assert_array_equal(ctx.download(v.edge_query + base * 4, np.int32, cnt[t]), q)
+        np.testing.assert_array_equal(P[t], T)
+        # frame k is frame k-1 shifted by (1, 3) px, the stereo points sit at Z = 0.54 fy / 8: the pose of frame
+        # k in frame k-1's camera is the translation (-Z/fx, -3 Z/fy, 0).  The reference truncates the LK points
+        # to int (cv::Point2i(float), src/LoopHandler.cc:395): LK lands within ~0.01 px of the integer truth, so
+        # truncation biases the measurements by up to 1 px = 0.07 m at this depth
+        np.testing.assert_allclose(T[4:], [-0.0675, -0.2025, 0.0], atol=0.07)
+    b.close()

@@ -51,3 +51,27 @@ def track_pose(orc, kq, kl, kr, K, T_right, prior=IDENTITY, thr=20, sum_mode=3):
     X, uv, q = track_edges(orc, kq, kl, kr, K, T_right, thr)
     T, out, inl = orc.pose_lm(X, uv, K, prior, sum_mode)
     return X, uv, q, T, out, inl
+
+
+def lk_track_pose(orc, img_prev, img_next, kl, kr, K, T_right, prior=IDENTITY, thr=20, lk_sum_mode=1, lm_sum_mode=3):
+    """The reference's trackLastFrame + optimizePoseOnly (src/LoopHandler.cc:298-454, 730-861) with frame k-1's
+    map points from its stereo pair: kept stereo matches triangulated (left camera = world), tracked by
+    calcOpticalFlowPyrLK into frame k, status-1 points at cv::Point2i(next.y, next.x) (truncation).
+    -> (X [n,3], uv [n,2], query index [n], T, outlier, inliers)."""
+    if len(kl) == 0:
+        e = np.zeros((0, 3)), np.zeros((0, 2)), np.zeros(0, np.int32)
+        return (*e, *orc.pose_lm(e[0], e[1], K, prior, lm_sum_mode))
+    ms = orc.match(kl, kr) if len(kr) else np.zeros(0, MATCH_DTYPE)
+    ks = kept_flags(orc, ms, thr) if len(kr) else np.zeros(len(kl), bool)
+    js = np.nonzero(ks)[0]
+    X = np.zeros((0, 3))
+    q = np.zeros(0, np.int32)
+    if len(js):
+        _, Xa, ok = orc.triangulate_matches(IDENTITY, T_right, K, ms[js])
+        X, q = Xa[ok], js[ok].astype(np.int32)
+    pts = np.stack([kl["y"][q], kl["x"][q]], 1).astype(np.float32)  # (x = column, y = row)
+    nxt, st, _, _ = orc.lk(img_prev, img_next, pts, sum_mode=lk_sum_mode)
+    uv = np.stack([np.trunc(nxt[st, 1]), np.trunc(nxt[st, 0])], 1).astype(np.float64)
+    X, q = X[st], q[st]
+    T, out, inl = orc.pose_lm(X, uv, K, prior, lm_sum_mode)
+    return X, uv, q, T, out, inl

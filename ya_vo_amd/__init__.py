@@ -87,6 +87,7 @@ SIGNATURES = {
     "yv_batch_track": (_I, [_P, _P, _P, _P]),
     "yv_batch_set_track_overlap": (_I, [_P, _I]),
     "yv_batch_track_sync": (_I, [_P]),
+    "yv_batch_set_track_lk": (_I, [_P, _I, _I, _I, _I, ctypes.c_double, ctypes.c_double]),
 }
 
 
@@ -375,6 +376,12 @@ class Batch:
     def set_track_overlap(self, on: bool = True) -> None:
         """Run each track's pose LM on the batch's own stream beside the next run (yv_batch_set_track_overlap)."""
         _check(self.lib.yv_batch_set_track_overlap(self.handle, 1 if on else 0), "yv_batch_set_track_overlap")
+
+    def set_track_lk(self, image_step: int, win: int = 11, max_level: int = 3, max_count: int = 30, eps: float = 0.01,
+                     min_eig: float = 0.001) -> None:
+        """LK tracking mode (yv_batch_set_track_lk): tracks become {stereo pair of frame k-1, image of frame k}."""
+        _check(self.lib.yv_batch_set_track_lk(self.handle, image_step, win, max_level, max_count, eps, min_eig),
+               "yv_batch_set_track_lk")
 
     def track_sync(self) -> None:
         _check(self.lib.yv_batch_track_sync(self.handle), "yv_batch_track_sync")

@@ -67,6 +67,23 @@ struct yv_batch {
     int32_t* edge_count = nullptr;  // [2][max_tracks]
     uint8_t* edge_outlier = nullptr;
     int32_t* track_inliers = nullptr;
+    // LK tracking mode (yv_batch_set_track_lk): tracks are {stereo pair of frame k-1, image index of frame k}
+    int lk_step = 0;                // > 0: LK mode, LK images are the run's images 0, lk_step, 2 lk_step, ...
+    yv_lk* lk = nullptr;
+    int lk_max_count = 30;
+    double lk_eps = 0.01, lk_min_eig = 1e-3;
+    int32_t* lk_sp = nullptr;       // [max_tracks] stereo pair per track
+    int32_t* lk_pairs = nullptr;    // [max_tracks][2] LK slots (prev, next)
+    double* lk_X = nullptr;         // [max_tracks][max_kp][3]
+    float* lk_pts = nullptr;        // [max_tracks][max_kp][2]
+    float* lk_next = nullptr;
+    float* lk_err = nullptr;
+    uint8_t* lk_status = nullptr;
+    int32_t* lk_q = nullptr;
+    int32_t* lk_count = nullptr;
+    const uint8_t* run_images = nullptr;  // the last yv_batch_run's images (LK reads them)
+    int run_n = 0, run_stride = 0;
+    int64_t run_pitch = 0;
     int tbuf = 0;                   // buffer of the last yv_batch_track
     int track_calls = 0;
     bool overlap = false;           // LM on the side stream
@@ -134,6 +151,11 @@ void batch_free(yv_batch* b) {
     if (b->side) (void)hipStreamSynchronize(b->side);
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    void* lk_ptrs[] = {b->lk_sp, b->lk_pairs, b->lk_X, b->lk_pts, b->lk_next, b->lk_err, b->lk_status, b->lk_q,
+                       b->lk_count};
+    for (void* p : lk_ptrs)
+        if (p) (void)hipFree(p);
+    if (b->lk) yv_lk_destroy(b->lk);
     for (hipEvent_t e : b->events) (void)hipEventDestroy(e);
     for (int k = 0; k < 2; ++k) {
         if (b->ev_edges[k]) (void)hipEventDestroy(b->ev_edges[k]);
@@ -460,6 +482,10 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
     // The carry slot keeps this run's frame k-1 (the query of its first temporal pair) until the next run
     // starts, so yv_batch_track and the view still see it; the copy of image carry_from is deferred.
     b->pending_carry = carry_from;
+    b->run_images = d_images;
+    b->run_n = n_images;
+    b->run_stride = stride;
+    b->run_pitch = image_pitch;
     return check_launch();
 }
 
@@ -499,8 +525,16 @@ int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks, int n_tracks, const 
     if (!b || n_tracks < 0 || (n_tracks > 0 && (!tracks || !K || !T_right))) return YV_ERR_INVALID;
     for (int t = 0; t < n_tracks; ++t) {
         const int sp = tracks[2 * t], tp = tracks[2 * t + 1];
-        if (sp < 0 || sp >= b->n_pairs || tp < 0 || tp >= b->n_pairs) return YV_ERR_INVALID;
-        if (b->h_pairs[2 * sp] != b->h_pairs[2 * tp + 1]) return YV_ERR_INVALID;  // stereo query = temporal train
+        if (sp < 0 || sp >= b->n_pairs) return YV_ERR_INVALID;
+        if (b->lk_step > 0) {
+            // LK mode: {stereo pair of frame k-1, image of frame k}, both LK images (multiples of the step)
+            const int prev = b->h_pairs[2 * sp];
+            if (prev % b->lk_step || prev >= b->max_images || tp < 0 || tp >= b->max_images || tp % b->lk_step)
+                return YV_ERR_INVALID;
+        } else {
+            if (tp < 0 || tp >= b->n_pairs) return YV_ERR_INVALID;
+            if (b->h_pairs[2 * sp] != b->h_pairs[2 * tp + 1]) return YV_ERR_INVALID;  // stereo query = temporal train
+        }
     }
     for (int i = 0; i < 9 && n_tracks > 0; ++i)
         if (!std::isfinite(K[i])) return YV_ERR_INVALID;
@@ -530,6 +564,23 @@ int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks, int n_tracks, const 
         rc |= dalloc(&b->edge_count, 2 * nt);
         rc |= dalloc(&b->edge_outlier, 2 * nt * nk);
         rc |= dalloc(&b->track_inliers, 2 * nt);
+        void* lk_old[] = {b->lk_sp, b->lk_pairs, b->lk_X, b->lk_pts, b->lk_next, b->lk_err, b->lk_status, b->lk_q,
+                          b->lk_count};
+        for (void* p : lk_old)
+            if (p) (void)hipFree(p);
+        b->lk_sp = b->lk_pairs = b->lk_q = b->lk_count = nullptr;
+        b->lk_X = nullptr;
+        b->lk_pts = b->lk_next = b->lk_err = nullptr;
+        b->lk_status = nullptr;
+        rc |= dalloc(&b->lk_sp, nt);
+        rc |= dalloc(&b->lk_pairs, 2 * nt);
+        rc |= dalloc(&b->lk_X, 3 * nt * nk);
+        rc |= dalloc(&b->lk_pts, 2 * nt * nk);
+        rc |= dalloc(&b->lk_next, 2 * nt * nk);
+        rc |= dalloc(&b->lk_err, nt * nk);
+        rc |= dalloc(&b->lk_status, nt * nk);
+        rc |= dalloc(&b->lk_q, nt * nk);
+        rc |= dalloc(&b->lk_count, nt);
         if (rc != YV_OK) return YV_ERR_HIP;
         b->max_tracks = n_tracks;
     }
@@ -540,6 +591,16 @@ int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks, int n_tracks, const 
         YV_HIP(hipMemcpyAsync(b->track_K, Ks.data(), Ks.size() * sizeof(double), hipMemcpyHostToDevice, s));
         YV_HIP(hipMemcpyAsync(b->T_right, T_right, 7 * sizeof(double), hipMemcpyHostToDevice, s));
         YV_HIP(hipMemsetAsync(b->edge_count, 0, 2 * sizeof(int32_t) * (size_t)b->max_tracks, s));
+        if (b->lk_step > 0) {
+            std::vector<int32_t> sp(n_tracks), lp(2 * (size_t)n_tracks);
+            for (int t = 0; t < n_tracks; ++t) {
+                sp[t] = tracks[2 * t];
+                lp[2 * t] = b->h_pairs[2 * sp[t]] / b->lk_step;
+                lp[2 * t + 1] = tracks[2 * t + 1] / b->lk_step;
+            }
+            YV_HIP(hipMemcpyAsync(b->lk_sp, sp.data(), sizeof(int32_t) * sp.size(), hipMemcpyHostToDevice, s));
+            YV_HIP(hipMemcpyAsync(b->lk_pairs, lp.data(), sizeof(int32_t) * lp.size(), hipMemcpyHostToDevice, s));
+        }
         YV_HIP(hipStreamSynchronize(s));
     }
     b->n_tracks = n_tracks;
@@ -565,8 +626,24 @@ int yv_batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* s
     // buffer k was last read by the LM two tracks ago (side stream): the build must not overwrite it early
     if (b->lm_pending[k]) YV_HIP(hipStreamWaitEvent(s, b->ev_lm[k], 0));
     if (timed) YV_HIP(hipEventRecord(ev[6], s));
-    yavo::launch_track_build(b->tracks, b->n_tracks, b->pairs, b->keypoints, b->kp_count, b->match_dj, b->match_lim,
-                             b->max_kp, b->track_K, b->T_right, eX, euv, eq, ec, s);
+    if (b->lk_step > 0) {
+        // trackLastFrame: frame k-1's stereo map points -> calcOpticalFlowPyrLK into frame k -> edges
+        if (!b->run_images || b->run_n < b->lk_step) return YV_ERR_INVALID;
+        yavo::launch_stereo_points(b->lk_sp, b->n_tracks, b->pairs, b->keypoints, b->kp_count, b->match_dj,
+                                   b->match_lim, b->max_kp, b->track_K, b->T_right, b->lk_X, b->lk_pts, b->lk_q,
+                                   b->lk_count, s);
+        const int n_lk = (b->run_n + b->lk_step - 1) / b->lk_step;
+        int rc = yv_lk_build(b->lk, b->run_images, n_lk, b->run_stride, b->run_pitch * b->lk_step, s);
+        if (rc != YV_OK) return rc;
+        rc = yv_lk_track_batch(b->lk, b->lk_pairs, b->n_tracks, b->lk_pts, b->lk_count, b->max_kp, b->lk_max_count,
+                               b->lk_eps, b->lk_min_eig, b->lk_next, b->lk_status, b->lk_err, s);
+        if (rc != YV_OK) return rc;
+        yavo::launch_lk_edges(b->n_tracks, b->lk_X, b->lk_next, b->lk_status, b->lk_q, b->lk_count, b->max_kp, eX,
+                              euv, eq, ec, s);
+    } else {
+        yavo::launch_track_build(b->tracks, b->n_tracks, b->pairs, b->keypoints, b->kp_count, b->match_dj,
+                                 b->match_lim, b->max_kp, b->track_K, b->T_right, eX, euv, eq, ec, s);
+    }
     hipStream_t ls = s;
     if (b->overlap) {
         // the LM reads only this track's edge buffer, priors and poses: it runs on the side stream beside the
@@ -608,6 +685,31 @@ int yv_batch_track_sync(yv_batch* b) {
     if (!b) return YV_ERR_INVALID;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
     if (b->side) YV_HIP(hipStreamSynchronize(b->side));
+    return YV_OK;
+}
+
+int yv_batch_set_track_lk(yv_batch* b, int image_step, int win, int max_level, int max_count, double eps,
+                          double min_eig) {
+    if (!b || image_step < 0 || (image_step > 0 && (win < 3 || win > 22 || max_level < 0))) return YV_ERR_INVALID;
+    if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+    if (b->side) YV_HIP(hipStreamSynchronize(b->side));
+    YV_HIP(hipStreamSynchronize(b->ctx->stream));
+    if (b->lk) {
+        yv_lk_destroy(b->lk);
+        b->lk = nullptr;
+    }
+    b->lk_step = image_step;
+    b->n_tracks = 0;  // tracks change meaning with the mode: set them again
+    if (image_step == 0) return YV_OK;
+    const int slots = (b->max_images + image_step - 1) / image_step;
+    const int rc = yv_lk_create(b->ctx, slots, b->H, b->W, win, max_level, &b->lk);
+    if (rc != YV_OK) {
+        b->lk_step = 0;
+        return rc;
+    }
+    b->lk_max_count = max_count;
+    b->lk_eps = eps;
+    b->lk_min_eig = min_eig;
     return YV_OK;
 }
 

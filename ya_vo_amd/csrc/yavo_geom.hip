@@ -1550,6 +1550,93 @@ __global__ __launch_bounds__(kNT) void track_build_kernel(
     if (tid == 0) edge_count[t] = ne;
 }
 
+// LK tracking mode (the reference's trackLastFrame, src/LoopHandler.cc:298-454).  Map points of frame k-1: its
+// left keypoints whose stereo match (pair sp) survives removeOutliers and triangulates (left camera = world).
+// Compacted in keypoint order: X, the LK start point (x = column, y = row as cv::Point2f, :344) and the
+// keypoint index.  One workgroup per track.
+__global__ __launch_bounds__(kNT) void stereo_points_kernel(
+    const int32_t* __restrict__ stereo_pairs, const int32_t* __restrict__ pairs,
+    const yv_keypoint* __restrict__ keypoints, const int32_t* __restrict__ kp_count, const int2* __restrict__ match_dj,
+    const int32_t* __restrict__ match_lim, int max_kp, const double* __restrict__ Kall,
+    const double* __restrict__ T_right, double* __restrict__ pX, float* __restrict__ pts, int32_t* __restrict__ pq,
+    int32_t* __restrict__ pcount) {
+    __shared__ int s_tmp[40];
+    __shared__ double s_K[9], s_Ta[7], s_Tb[7];
+    const int t = blockIdx.x, tid = threadIdx.x;
+    const int sp = stereo_pairs[t];
+    const int qs = pairs[2 * sp], rs = pairs[2 * sp + 1];
+    if (tid < 9) s_K[tid] = Kall[9 * t + tid];
+    if (tid < 7) {
+        s_Ta[tid] = tid == 3 ? 1.0 : 0.0;
+        s_Tb[tid] = T_right[tid];
+    }
+    __syncthreads();
+    const int nq = kp_count[qs];
+    const int lim = match_lim[sp];
+    const int2* dj = match_dj + (int64_t)sp * max_kp;
+    const yv_keypoint* kl = keypoints + (int64_t)qs * max_kp;
+    const yv_keypoint* kr = keypoints + (int64_t)rs * max_kp;
+    double* Xo = pX + 3 * (int64_t)t * max_kp;
+    float* po = pts + 2 * (int64_t)t * max_kp;
+    int32_t* qo = pq + (int64_t)t * max_kp;
+    int ne = 0;
+    for (int base = 0; base < nq; base += kNT) {
+        const int j = base + tid;
+        bool good = false;
+        double X[3];
+        if (j < nq) {
+            const int2 a = dj[j];
+            if (a.x < lim && a.y >= 0) good = triangulate_px(kl[j].x, kl[j].y, kr[a.y].x, kr[a.y].y, s_Ta, s_Tb, s_K, X);
+        }
+        int tot = 0;
+        const int off = block_excl_scan_geom(good ? 1 : 0, s_tmp, &tot);
+        if (good) {
+            const int e = ne + off;
+            Xo[3 * e] = X[0];
+            Xo[3 * e + 1] = X[1];
+            Xo[3 * e + 2] = X[2];
+            po[2 * e] = (float)kl[j].y;      // cv::Point2i(kp.y, kp.x) -> Point2f: x = column
+            po[2 * e + 1] = (float)kl[j].x;  // y = row
+            qo[e] = j;
+        }
+        ne += tot;
+    }
+    if (tid == 0) pcount[t] = ne;
+}
+
+// Pose edges from the LK result: points with status 1 become features at cv::Point2i(next.y, next.x), i.e. the
+// float coordinates truncated toward zero (src/LoopHandler.cc:395), measurement (kp.x, kp.y) = (row, col).
+__global__ __launch_bounds__(kNT) void lk_edges_kernel(const double* __restrict__ pX, const float* __restrict__ next,
+                                                       const uint8_t* __restrict__ status,
+                                                       const int32_t* __restrict__ pq,
+                                                       const int32_t* __restrict__ pcount, int max_kp,
+                                                       double* __restrict__ edge_X, double* __restrict__ edge_uv,
+                                                       int32_t* __restrict__ edge_query,
+                                                       int32_t* __restrict__ edge_count) {
+    __shared__ int s_tmp[40];
+    const int t = blockIdx.x, tid = threadIdx.x;
+    const int n = pcount[t];
+    const int64_t b = (int64_t)t * max_kp;
+    int ne = 0;
+    for (int base = 0; base < n; base += kNT) {
+        const int i = base + tid;
+        const bool good = i < n && status[b + i];
+        int tot = 0;
+        const int off = block_excl_scan_geom(good ? 1 : 0, s_tmp, &tot);
+        if (good) {
+            const int64_t e = b + ne + off;
+            edge_X[3 * e] = pX[3 * (b + i)];
+            edge_X[3 * e + 1] = pX[3 * (b + i) + 1];
+            edge_X[3 * e + 2] = pX[3 * (b + i) + 2];
+            edge_uv[2 * e] = (double)(int)next[2 * (b + i) + 1];  // kp.x = (int) row
+            edge_uv[2 * e + 1] = (double)(int)next[2 * (b + i)];  // kp.y = (int) column
+            edge_query[e] = pq[b + i];
+        }
+        ne += tot;
+    }
+    if (tid == 0) edge_count[t] = ne;
+}
+
 __global__ __launch_bounds__(kNT) void pose_gn_kernel(const int32_t* __restrict__ offsets, const double* __restrict__ Xall,
                                                       const double* __restrict__ uvall, const double* __restrict__ Kall,
                                                       double* __restrict__ poses, int32_t* __restrict__ iters_out) {
@@ -1672,6 +1759,23 @@ void launch_track_build(const int32_t* tracks, int n_tracks, const int32_t* pair
     if (n_tracks <= 0) return;
     hipLaunchKernelGGL(geom::track_build_kernel, dim3(n_tracks), dim3(geom::kNT), 0, s, tracks, pairs, keypoints,
                        kp_count, match_dj, match_lim, max_kp, K, T_right, edge_X, edge_uv, edge_query, edge_count);
+}
+
+void launch_stereo_points(const int32_t* stereo_pairs, int n_tracks, const int32_t* pairs,
+                          const yv_keypoint* keypoints, const int32_t* kp_count, const int2* match_dj,
+                          const int32_t* match_lim, int max_kp, const double* K, const double* T_right, double* pX,
+                          float* pts, int32_t* pq, int32_t* pcount, hipStream_t s) {
+    if (n_tracks <= 0) return;
+    hipLaunchKernelGGL(geom::stereo_points_kernel, dim3(n_tracks), dim3(geom::kNT), 0, s, stereo_pairs, pairs,
+                       keypoints, kp_count, match_dj, match_lim, max_kp, K, T_right, pX, pts, pq, pcount);
+}
+
+void launch_lk_edges(int n_tracks, const double* pX, const float* next, const uint8_t* status, const int32_t* pq,
+                     const int32_t* pcount, int max_kp, double* edge_X, double* edge_uv, int32_t* edge_query,
+                     int32_t* edge_count, hipStream_t s) {
+    if (n_tracks <= 0) return;
+    hipLaunchKernelGGL(geom::lk_edges_kernel, dim3(n_tracks), dim3(geom::kNT), 0, s, pX, next, status, pq, pcount,
+                       max_kp, edge_X, edge_uv, edge_query, edge_count);
 }
 
 void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, const double* edge_X,

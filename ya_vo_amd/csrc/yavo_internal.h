@@ -91,6 +91,13 @@ void launch_track_build(const int32_t* tracks, int n_tracks, const int32_t* pair
                         const int32_t* kp_count, const int2* match_dj, const int32_t* match_lim, int max_kp,
                         const double* K, const double* T_right, double* edge_X, double* edge_uv, int32_t* edge_query,
                         int32_t* edge_count, hipStream_t s);
+void launch_stereo_points(const int32_t* stereo_pairs, int n_tracks, const int32_t* pairs,
+                          const yv_keypoint* keypoints, const int32_t* kp_count, const int2* match_dj,
+                          const int32_t* match_lim, int max_kp, const double* K, const double* T_right, double* pX,
+                          float* pts, int32_t* pq, int32_t* pcount, hipStream_t s);
+void launch_lk_edges(int n_tracks, const double* pX, const float* next, const uint8_t* status, const int32_t* pq,
+                     const int32_t* pcount, int max_kp, double* edge_X, double* edge_uv, int32_t* edge_query,
+                     int32_t* edge_count, hipStream_t s);
 void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, const double* edge_X,
                        const double* edge_uv, const double* K, const double* priors, double* poses,
                        uint8_t* edge_outlier, int32_t* inliers, hipStream_t s);

@@ -5,11 +5,12 @@
 //   pyr_down_kernel   cv::pyrDown CV_8U, 5x5 [1 4 6 4 1]^2 / 256, BORDER_REFLECT_101 (exact integers); a
 //                     16 x 64 output tile per workgroup, its 35 x 131 source patch staged in LDS
 //   scharr_kernel     calcSharrDeriv: int16 (dx, dy), REFLECT_101 rows / columns
-//   lk_kernel         LKTrackerInvoker for every level of one point per wave: window pixel p = y * win + x
-//                     lives on lane p mod 64; bilinear samples (14-bit weights, CV_DESCALE) straight from the
-//                     level images (REFLECT_101 image border, zero derivative border); window sums as float
-//                     partials per lane then a wave tree (the oracle's sum_mode 1); every lane computes the
-//                     same Newton step from the broadcast sums
+//   lk_kernel         LKTrackerInvoker for every level of one point per 16-lane DPP row (4 points per wave):
+//                     each lane owns an S x S task of the window (S = ceil(win / 4)); bilinear samples (14-bit
+//                     weights, CV_DESCALE) straight from the level images (REFLECT_101 image border, zero
+//                     derivative border) with 24-bit multiply-adds; window sums as float partials per lane then
+//                     a row butterfly (the oracle's sum_mode 1) that leaves the sum in all 16 lanes, so every
+//                     lane computes the same Newton step
 //
 // Built with -ffp-contract=off like the rest: each float op rounds as the oracle's.
 #include <hip/hip_runtime.h>
@@ -94,7 +95,8 @@ __global__ __launch_bounds__(256) void scharr_kernel(const uint8_t* __restrict__
 // LK
 // ------------------------------------------------------------------------------------------------
 constexpr int kWBits = 14;
-// window pixels per lane (MP): ceil(win^2 / 64) rounded to 2, 4 or 8 (win <= 22); the launch picks the smallest
+constexpr int kLkLanes = 16;                   // lanes per point: one DPP row
+constexpr int kLkPtsPerBlock = 256 / kLkLanes;  // 16 points per 256-thread workgroup
 
 __device__ __forceinline__ int descale(int x, int n) { return (x + (1 << (n - 1))) >> n; }
 
@@ -105,38 +107,91 @@ __device__ __forceinline__ void weights(float a, float b, int* iw) {
     iw[3] = (1 << kWBits) - iw[0] - iw[1] - iw[2];
 }
 
-// Sum over the window in the oracle's sum_mode 1 order: lane partials from 0.0f, then p[l] += p[l + off] for
-// off = 32 .. 1, all in registers: v_permlane32_swap / v_permlane16_swap bring lane l + 32 / l + 16 to lane l
-// (the swapped second operand), DPP row_shl:off does l + off inside a 16-lane row; lane 0 holds the total.
-__device__ __forceinline__ float wave_sum(float part) {
-    float t = __uint_as_float(
-        __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part), false, false)[1]);
-    part = part + t;  // lanes 0..31: p[l] + p[l + 32]
-    t = __uint_as_float(
-        __builtin_amdgcn_permlane16_swap(__float_as_uint(part), __float_as_uint(part), false, false)[1]);
-    part = part + t;  // lanes 0..15 (of each half): + lane l + 16
-    part = part + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(part), 0x108, 0xF, 0xF, false));
-    part = part + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(part), 0x104, 0xF, 0xF, false));
-    part = part + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(part), 0x102, 0xF, 0xF, false));
-    part = part + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(part), 0x101, 0xF, 0xF, false));
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(part)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// a * b + c with |a|, |b| < 2^23 (v_mad_i32_i24): samples are u8 / int16, weights <= 2^14
+__device__ __forceinline__ int mad24(int a, int b, int c) { return __mul24(a, b) + c; }
+
+template <int kCtrl>
+__device__ __forceinline__ float row_dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, 0xF, 0xF, false));
 }
 
-template <int kMaxPix>
-__global__ __launch_bounds__(256) void lk_kernel(LkParams P, const int32_t* __restrict__ pairs,
+// Sum over a point's 16 lanes (one DPP row) in the oracle's sum_mode 1 order: the butterfly q[l] + q[l ^ off],
+// off = 8, 4, 2, 1, as row rotations (after the step with off the values have period off, so rotating by off / 2
+// brings lane l ^ (off / 2)).  Lane 0 follows the tree p[l] += p[l + off]; every lane ends with the same bits
+// (IEEE addition commutes), so the Newton step needs no broadcast.
+__device__ __forceinline__ float row_sum(float q) {
+    q = q + row_dpp<0x128>(q);  // row_ror:8
+    q = q + row_dpp<0x124>(q);  // row_ror:4
+    q = q + row_dpp<0x122>(q);  // row_ror:2
+    q = q + row_dpp<0x121>(q);  // row_ror:1
+    return q;
+}
+
+// REFLECT_101 then clamped: task pixels past the window (never summed) may lie beyond one reflection on a small
+// top level; their addresses stay in the image
+__device__ __forceinline__ int refl_c(int p, int len) { return min(max(refl(p, len), 0), len - 1); }
+
+// the (S + 1) x (S + 1) bilinear footprint of a lane's task, top-left (x0, y0), REFLECT_101 outside the image.
+// Inside the image each row's S + 1 <= 4 bytes come from one dword-aligned dwordx2 and one v_alignbyte (the aligned
+// 8 bytes stay inside the row: x0 + 7 < Wl); otherwise byte loads at reflected coordinates.
+template <int S>
+__device__ __forceinline__ void load_footprint(const uint8_t* __restrict__ J, int sJ, int Hl, int Wl, int x0, int y0,
+                                               int (&v)[S + 1][S + 1]) {
+    if (S <= 3 && x0 >= 0 && y0 >= 0 && x0 + 7 < Wl && y0 + S < Hl) {
+        const uint32_t off = (uint32_t)(y0 * sJ + x0);
+#pragma unroll
+        for (int i = 0; i <= S; ++i) {
+            const uint32_t o = off + (uint32_t)(i * sJ);
+            const uint32_t mis = (uint32_t)((uintptr_t)J + o) & 3u;
+            u32x2 a;  // one dwordx2 at 4-byte alignment
+            __builtin_memcpy(&a, __builtin_assume_aligned(J + (o - mis), 4), 8);
+            const uint32_t w = __builtin_amdgcn_alignbyte(a.y, a.x, mis);
+#pragma unroll
+            for (int j = 0; j <= S; ++j) v[i][j] = (w >> (8 * j)) & 0xFF;
+        }
+    } else if (x0 >= 0 && y0 >= 0 && x0 + S < Wl && y0 + S < Hl) {
+        uint32_t row = (uint32_t)(y0 * sJ + x0);
+#pragma unroll
+        for (int i = 0; i <= S; ++i, row += (uint32_t)sJ)
+#pragma unroll
+            for (int j = 0; j <= S; ++j) v[i][j] = J[row + (uint32_t)j];
+    } else {
+        int r[S + 1], c[S + 1];
+#pragma unroll
+        for (int i = 0; i <= S; ++i) {
+            r[i] = refl_c(y0 + i, Hl) * sJ;
+            c[i] = refl_c(x0 + i, Wl);
+        }
+#pragma unroll
+        for (int i = 0; i <= S; ++i)
+#pragma unroll
+            for (int j = 0; j <= S; ++j) v[i][j] = J[(uint32_t)(r[i] + c[j])];
+    }
+}
+
+// One point per 16-lane row, 4 per wave.  Lane g of the row owns the S x S task at window rows S (g >> 2) ..,
+// columns S (g & 3) .. (S = ceil(win / 4)); per level it keeps, for each task pixel, the I sample folded into the
+// rounding constant of the J interpolation (ck = 2^8 - 2^9 iv, so (ck + sum w J) >> 9 = descale(.) - iv) and the
+// derivatives as floats (zero for pixels past the window, which then add +0 to every sum).
+template <int S>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 : (S == 3 ? 6 : 1)))) void lk_kernel(LkParams P, const int32_t* __restrict__ pairs,
                                                  const float* __restrict__ pts, const int32_t* __restrict__ counts,
                                                  int pts_stride, float* __restrict__ next_out,
                                                  uint8_t* __restrict__ status_out, float* __restrict__ err_out) {
     const int pair = blockIdx.y;
-    const int lane = threadIdx.x & 63;
-    const int pi = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int g = threadIdx.x & (kLkLanes - 1);
+    const int pi = blockIdx.x * kLkPtsPerBlock + (threadIdx.x >> 4);
     const int n = counts[pair];
-    if (pi >= n) return;
+    if (pi >= n) return;  // whole rows leave together
     const int ia = pairs[2 * pair], ib = pairs[2 * pair + 1];
     const int64_t po = (int64_t)pair * pts_stride + pi;
-    const int win = P.win, npix = win * win;
+    const int win = P.win;
     const float halfw = (float)((win - 1) * 0.5f);
     const float px0 = pts[2 * po], py0 = pts[2 * po + 1];
+    const int r0 = S * (g >> 2), c0 = S * (g & 3);
     float nxo = 0.f, nyo = 0.f;  // nextPts[ptidx]
     uint8_t status = 1;
     float err = 0.f;
@@ -146,7 +201,7 @@ __global__ __launch_bounds__(256) void lk_kernel(LkParams P, const int32_t* __re
         const uint8_t* I = level == 0 ? P.img0 + (int64_t)ia * P.pitch0 : P.pyr + (int64_t)ia * P.pyr_pitch + P.off[level];
         const uint8_t* J = level == 0 ? P.img0 + (int64_t)ib * P.pitch0 : P.pyr + (int64_t)ib * P.pyr_pitch + P.off[level];
         const int sI = level == 0 ? P.stride0 : Wl;
-        const int16_t* D = P.der + (int64_t)ia * P.der_pitch + P.der_off[level];
+        const uint32_t* D = reinterpret_cast<const uint32_t*>(P.der + (int64_t)ia * P.der_pitch + P.der_off[level]);
         const float scale = (float)(1. / (1 << level));
         float px = px0 * scale, py = py0 * scale;
         float nx, ny;
@@ -171,50 +226,66 @@ __global__ __launch_bounds__(256) void lk_kernel(LkParams P, const int32_t* __re
         }
         int iw[4];
         weights(px - (float)ipx, py - (float)ipy, iw);
-        // this lane's window pixels: I value and derivatives (IWinBuf / derivIWinBuf)
-        int iv[kMaxPix], ixv[kMaxPix], iyv[kMaxPix];
-        float a11 = 0.0f, a12 = 0.0f, a22 = 0.0f;
-        // the whole bilinear footprint inside the level image (wave-uniform): no border logic per sample
-        const bool inI = ipx >= 0 && ipy >= 0 && ipx + win < Wl && ipy + win < Hl;
+        // I and (dx, dy) over the task footprint; the derivative image is zero outside [0, Hl) x [0, Wl)
+        int iv8[S + 1][S + 1];
+        load_footprint<S>(I, sI, Hl, Wl, ipx + c0, ipy + r0, iv8);
+        int dv[S + 1][S + 1];
+        if (S == 3 && ipx + c0 >= 0 && ipy + r0 >= 0 && ipx + c0 + S < Wl && ipy + r0 + S < Hl) {
+            // all inside: one dwordx4 per footprint row
 #pragma unroll
-        for (int k = 0; k < kMaxPix; ++k) {
-            const int p = lane + 64 * k;
-            iv[k] = ixv[k] = iyv[k] = 0;
-            if (p < npix) {
-                const int y = p / win, x = p - y * win;
-                const int yy = ipy + y, xx = ipx + x;
-                const int r0 = inI ? yy : refl(yy, Hl), r1 = inI ? yy + 1 : refl(yy + 1, Hl);
-                const int c0 = inI ? xx : refl(xx, Wl), c1 = inI ? xx + 1 : refl(xx + 1, Wl);
-                const uint8_t* i0 = I + r0 * sI;
-                const uint8_t* i1 = I + r1 * sI;
-                iv[k] = descale(i0[c0] * iw[0] + i0[c1] * iw[1] + i1[c0] * iw[2] + i1[c1] * iw[3], kWBits - 5);
-                // derivative image: zero outside [0, Hl) x [0, Wl)
-                int dxs[4], dys[4];
-                if (inI) {
-                    const int16_t* d0 = D + (yy * Wl + xx) * 2;
-                    const int16_t* d1 = d0 + Wl * 2;
-                    dxs[0] = d0[0]; dys[0] = d0[1]; dxs[1] = d0[2]; dys[1] = d0[3];
-                    dxs[2] = d1[0]; dys[2] = d1[1]; dxs[3] = d1[2]; dys[3] = d1[3];
-                } else {
+            for (int i = 0; i <= S; ++i) {
+                u32x4 d;
+                __builtin_memcpy(&d, __builtin_assume_aligned(D + (uint32_t)((ipy + r0 + i) * Wl + ipx + c0), 4), 16);
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int ry = yy + (q >> 1), rx = xx + (q & 1);
-                        const bool in = ry >= 0 && ry < Hl && rx >= 0 && rx < Wl;
-                        const int16_t* dp = D + ((in ? ry : 0) * Wl + (in ? rx : 0)) * 2;
-                        dxs[q] = in ? dp[0] : 0;
-                        dys[q] = in ? dp[1] : 0;
-                    }
-                }
-                ixv[k] = descale(dxs[0] * iw[0] + dxs[1] * iw[1] + dxs[2] * iw[2] + dxs[3] * iw[3], kWBits);
-                iyv[k] = descale(dys[0] * iw[0] + dys[1] * iw[1] + dys[2] * iw[2] + dys[3] * iw[3], kWBits);
-                a11 = a11 + (float)(ixv[k] * ixv[k]);
-                a12 = a12 + (float)(ixv[k] * iyv[k]);
-                a22 = a22 + (float)(iyv[k] * iyv[k]);
+                for (int j = 0; j <= S; ++j) dv[i][j] = (int)d[j & 3];
             }
+        } else {
+            int r[S + 1], c[S + 1];
+            bool rin[S + 1], cin[S + 1];
+#pragma unroll
+            for (int i = 0; i <= S; ++i) {
+                const int y = ipy + r0 + i, x = ipx + c0 + i;
+                rin[i] = y >= 0 && y < Hl;
+                cin[i] = x >= 0 && x < Wl;
+                r[i] = min(max(y, 0), Hl - 1) * Wl;
+                c[i] = min(max(x, 0), Wl - 1);
+            }
+#pragma unroll
+            for (int i = 0; i <= S; ++i)
+#pragma unroll
+                for (int j = 0; j <= S; ++j) {
+                    const uint32_t d = D[(uint32_t)(r[i] + c[j])];
+                    dv[i][j] = rin[i] && cin[j] ? (int)d : 0;
+                }
         }
-        const float A11 = wave_sum(a11) * FLT_SCALE;
-        const float A12 = wave_sum(a12) * FLT_SCALE;
-        const float A22 = wave_sum(a22) * FLT_SCALE;
+        int ck[S][S];
+        float fx[S][S], fy[S][S];
+        float a11 = 0.0f, a12 = 0.0f, a22 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                const int ival = descale(mad24(iv8[i][j], iw[0], mad24(iv8[i][j + 1], iw[1],
+                                         mad24(iv8[i + 1][j], iw[2], iv8[i + 1][j + 1] * iw[3]))), kWBits - 5);
+                // (int16) low / high halves of the interleaved (dx, dy) derivative
+                const int x00 = (int16_t)dv[i][j], x01 = (int16_t)dv[i][j + 1];
+                const int x10 = (int16_t)dv[i + 1][j], x11 = (int16_t)dv[i + 1][j + 1];
+                const int y00 = dv[i][j] >> 16, y01 = dv[i][j + 1] >> 16;
+                const int y10 = dv[i + 1][j] >> 16, y11 = dv[i + 1][j + 1] >> 16;
+                const int ixv = descale(mad24(x00, iw[0], mad24(x01, iw[1], mad24(x10, iw[2], __mul24(x11, iw[3])))), kWBits);
+                const int iyv = descale(mad24(y00, iw[0], mad24(y01, iw[1], mad24(y10, iw[2], __mul24(y11, iw[3])))), kWBits);
+                const bool in = r0 + i < win && c0 + j < win;
+                ck[i][j] = (1 << (kWBits - 6)) - (ival << (kWBits - 5));
+                fx[i][j] = in ? (float)ixv : 0.f;
+                fy[i][j] = in ? (float)iyv : 0.f;
+                // (float)(ixv * ixv) etc.: the products are < 2^24, exact as floats
+                a11 = a11 + fx[i][j] * fx[i][j];
+                a12 = a12 + fx[i][j] * fy[i][j];
+                a22 = a22 + fy[i][j] * fy[i][j];
+            }
+        const float A11 = row_sum(a11) * FLT_SCALE;
+        const float A12 = row_sum(a12) * FLT_SCALE;
+        const float A22 = row_sum(a22) * FLT_SCALE;
         float Dd = A11 * A22 - A12 * A12;
         const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * win * win);
         if (minEig < P.min_eig || Dd < FLT_EPSILON) {
@@ -225,33 +296,29 @@ __global__ __launch_bounds__(256) void lk_kernel(LkParams P, const int32_t* __re
         nx -= halfw;
         ny -= halfw;
         float pdx = 0.f, pdy = 0.f;
-        for (int j = 0; j < P.max_count; ++j) {
+        for (int it = 0; it < P.max_count; ++it) {
             const int inx = (int)floorf(nx), iny = (int)floorf(ny);
             if (inx < -win || inx >= Wl || iny < -win || iny >= Hl) {
                 if (level == 0) status = 0;
                 break;
             }
             weights(nx - (float)inx, ny - (float)iny, iw);
-            const bool inJ = inx >= 0 && iny >= 0 && inx + win < Wl && iny + win < Hl;
+            int jv[S + 1][S + 1];
+            load_footprint<S>(J, sI, Hl, Wl, inx + c0, iny + r0, jv);
             float b1 = 0.0f, b2 = 0.0f;
 #pragma unroll
-            for (int k = 0; k < kMaxPix; ++k) {
-                const int p = lane + 64 * k;
-                if (p < npix) {
-                    const int y = p / win, x = p - y * win;
-                    const int yy = iny + y, xx = inx + x;
-                    const int r0 = inJ ? yy : refl(yy, Hl), r1 = inJ ? yy + 1 : refl(yy + 1, Hl);
-                    const int c0 = inJ ? xx : refl(xx, Wl), c1 = inJ ? xx + 1 : refl(xx + 1, Wl);
-                    const uint8_t* j0 = J + r0 * sI;
-                    const uint8_t* j1 = J + r1 * sI;
-                    const int diff = descale(j0[c0] * iw[0] + j0[c1] * iw[1] + j1[c0] * iw[2] + j1[c1] * iw[3],
-                                             kWBits - 5) - iv[k];
-                    b1 = b1 + (float)(diff * ixv[k]);
-                    b2 = b2 + (float)(diff * iyv[k]);
+            for (int i = 0; i < S; ++i)
+#pragma unroll
+                for (int j = 0; j < S; ++j) {
+                    const int acc = mad24(jv[i][j], iw[0], mad24(jv[i][j + 1], iw[1],
+                                    mad24(jv[i + 1][j], iw[2], mad24(jv[i + 1][j + 1], iw[3], ck[i][j]))));
+                    // (float)(diff * ixv): |diff * ixv| < 2^27, one rounding either way
+                    const float d = (float)(acc >> (kWBits - 5));
+                    b1 = b1 + d * fx[i][j];
+                    b2 = b2 + d * fy[i][j];
                 }
-            }
-            const float B1 = wave_sum(b1) * FLT_SCALE;
-            const float B2 = wave_sum(b2) * FLT_SCALE;
+            const float B1 = row_sum(b1) * FLT_SCALE;
+            const float B2 = row_sum(b2) * FLT_SCALE;
             const float dx = (float)((A12 * B2 - A22 * B1) * Dd);
             const float dy = (float)((A12 * B1 - A11 * B2) * Dd);
             nx += dx;
@@ -259,7 +326,7 @@ __global__ __launch_bounds__(256) void lk_kernel(LkParams P, const int32_t* __re
             nxo = nx + halfw;
             nyo = ny + halfw;
             if ((double)dx * dx + (double)dy * dy <= P.eps2) break;
-            if (j > 0 && fabsf(dx + pdx) < 0.01 && fabsf(dy + pdy) < 0.01) {
+            if (it > 0 && fabsf(dx + pdx) < 0.01 && fabsf(dy + pdy) < 0.01) {
                 nxo -= dx * 0.5f;
                 nyo -= dy * 0.5f;
                 break;
@@ -274,25 +341,23 @@ __global__ __launch_bounds__(256) void lk_kernel(LkParams P, const int32_t* __re
                 status = 0;
             } else {
                 weights(ex - (float)inx, ey - (float)iny, iw);
+                int jv[S + 1][S + 1];
+                load_footprint<S>(J, sI, Hl, Wl, inx + c0, iny + r0, jv);
                 float e = 0.0f;
 #pragma unroll
-                for (int k = 0; k < kMaxPix; ++k) {
-                    const int p = lane + 64 * k;
-                    if (p < npix) {
-                        const int y = p / win, x = p - y * win;
-                        const int yy = iny + y, xx = inx + x;
-                        const int r0 = refl(yy, Hl), r1 = refl(yy + 1, Hl), c0 = refl(xx, Wl), c1 = refl(xx + 1, Wl);
-                        const int diff = descale(J[(int64_t)r0 * sI + c0] * iw[0] + J[(int64_t)r0 * sI + c1] * iw[1] +
-                                                     J[(int64_t)r1 * sI + c0] * iw[2] + J[(int64_t)r1 * sI + c1] * iw[3],
-                                                 kWBits - 5) - iv[k];
-                        e = e + fabsf((float)diff);
+                for (int i = 0; i < S; ++i)
+#pragma unroll
+                    for (int j = 0; j < S; ++j) {
+                        const int acc = mad24(jv[i][j], iw[0], mad24(jv[i][j + 1], iw[1],
+                                        mad24(jv[i + 1][j], iw[2], mad24(jv[i + 1][j + 1], iw[3], ck[i][j]))));
+                        const bool in = r0 + i < win && c0 + j < win;
+                        e = e + (in ? fabsf((float)(acc >> (kWBits - 5))) : 0.f);
                     }
-                }
-                err = wave_sum(e) * 1.f / (float)(32 * win * win);
+                err = row_sum(e) * 1.f / (float)(32 * win * win);
             }
         }
     }
-    if (lane == 0) {
+    if (g == 0) {
         next_out[2 * po] = nxo;
         next_out[2 * po + 1] = nyo;
         status_out[po] = status;
@@ -326,14 +391,24 @@ void launch_lk_pyramid(const LkParams& P, int n_images, hipStream_t s) {
 void launch_lk_track(const LkParams& P, const int32_t* pairs, int n_pairs, const float* pts, const int32_t* counts,
                      int pts_stride, int max_pts, float* next_pts, uint8_t* status, float* err, hipStream_t s) {
     if (n_pairs <= 0 || max_pts <= 0) return;
-    dim3 grid((max_pts + 3) / 4, n_pairs);
-    const int npix = P.win * P.win;
-    if (npix <= 128)
-        hipLaunchKernelGGL(lk::lk_kernel<2>, grid, dim3(256), 0, s, P, pairs, pts, counts, pts_stride, next_pts, status, err);
-    else if (npix <= 256)
-        hipLaunchKernelGGL(lk::lk_kernel<4>, grid, dim3(256), 0, s, P, pairs, pts, counts, pts_stride, next_pts, status, err);
-    else
-        hipLaunchKernelGGL(lk::lk_kernel<8>, grid, dim3(256), 0, s, P, pairs, pts, counts, pts_stride, next_pts, status, err);
+    dim3 grid((max_pts + lk::kLkPtsPerBlock - 1) / lk::kLkPtsPerBlock, n_pairs);
+    // S = ceil(win / 4) pixels per task side (win 3 .. 22)
+    switch ((P.win + 3) / 4) {
+#define YV_LK_CASE(S)                                                                                             \
+    case S:                                                                                                       \
+        hipLaunchKernelGGL(lk::lk_kernel<S>, grid, dim3(256), 0, s, P, pairs, pts, counts, pts_stride, next_pts, \
+                           status, err);                                                                          \
+        break;
+        YV_LK_CASE(1)
+        YV_LK_CASE(2)
+        YV_LK_CASE(3)
+        YV_LK_CASE(4)
+        YV_LK_CASE(5)
+        YV_LK_CASE(6)
+#undef YV_LK_CASE
+        default:
+            break;
+    }
 }
 
 }  // namespace yavo
