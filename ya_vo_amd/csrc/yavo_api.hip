@@ -670,7 +670,10 @@ int yv_batch_set_track_overlap(yv_batch* b, int on) {
     if (!b) return YV_ERR_INVALID;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
     if (on && !b->side) {
-        YV_HIP(hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking));
+        // lowest priority: the LM fills the CUs the next batch's detect / describe / match leave idle
+        int least = 0, greatest = 0;
+        YV_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        YV_HIP(hipStreamCreateWithPriority(&b->side, hipStreamNonBlocking, least));
         for (int k = 0; k < 2; ++k) {
             YV_HIP(hipEventCreateWithFlags(&b->ev_edges[k], hipEventDisableTiming));
             YV_HIP(hipEventCreateWithFlags(&b->ev_lm[k], hipEventDisableTiming));

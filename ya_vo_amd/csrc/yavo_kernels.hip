@@ -690,8 +690,12 @@ __device__ __forceinline__ uint32_t reg_select(const uint32_t (&v)[N], int idx) 
 // keypoint: lane l evaluates tests l, l + 64, l + 128, l + 192 -> 4 ballots = 256 bits.
 constexpr int BR_BAND = 32;
 constexpr int BR_ROWS = BR_BAND + 17;  // rows r0-8 .. r0+40 (the last one for the wrap of col + 8 == W)
+// 16 waves share one staged band: the ~61 KB band limits a CU to 2 workgroups, so the workgroup is as wide as
+// the 64-VGPR budget of 8 waves per SIMD allows
+constexpr int BR_NT = 1024;
+constexpr int BR_NW = BR_NT / 64;
 
-__global__ __launch_bounds__(256) void brief_kernel(const uint8_t* __restrict__ blur, int H, int W,
+__global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict__ blur, int H, int W,
                                                     const int8_t* __restrict__ offsets,
                                                     const int32_t* __restrict__ kp_src,
                                                     const int32_t* __restrict__ kp_count, int max_kp,
@@ -708,12 +712,12 @@ __global__ __launch_bounds__(256) void brief_kernel(const uint8_t* __restrict__ 
     __syncthreads();
     // 1. this band's keypoints (any order: each keypoint's outputs go to its own index); all row loads are
     // issued before the first use
-    const int nscan = (n + 255) >> 8;
+    const int nscan = (n + BR_NT - 1) / BR_NT;
     int next_row = tid < n ? src[tid].x : -1;  // software-pipelined: the next row load is in flight
     for (int u = 0; u < nscan; ++u) {
-        const int i = u * 256 + tid;
+        const int i = u * BR_NT + tid;
         const int row = next_row;
-        const int inext = i + 256;
+        const int inext = i + BR_NT;
         next_row = inext < n ? src[inext].x : -1;
         const bool mine = i < n && row >= r0 && row < r0 + BR_BAND;
         const uint64_t bal = __ballot(mine);
@@ -737,23 +741,18 @@ __global__ __launch_bounds__(256) void brief_kernel(const uint8_t* __restrict__ 
     const int nbytes = (L1 - L0) + sh;  // bytes from gal to the end of the range
     const int nfull = nbytes >> 4;
     uint4* s4 = reinterpret_cast<uint4*>(s_band);
-    // 8 16-B words in flight per thread (written out: an array here is not kept in registers); indices are
+    // 4 16-B words in flight per thread (written out: an array here is not kept in registers); indices are
     // clamped so every load is a valid word inside [gal, b + L1)
-    for (int k0 = tid; k0 < nfull; k0 += 8 * 256) {
+    for (int k0 = tid; k0 < nfull; k0 += 4 * BR_NT) {
         const int last = nfull - 1;
-        const uint4 v0 = gal[min(k0, last)], v1 = gal[min(k0 + 256, last)], v2 = gal[min(k0 + 512, last)],
-                    v3 = gal[min(k0 + 768, last)], v4 = gal[min(k0 + 1024, last)], v5 = gal[min(k0 + 1280, last)],
-                    v6 = gal[min(k0 + 1536, last)], v7 = gal[min(k0 + 1792, last)];
+        const uint4 v0 = gal[min(k0, last)], v1 = gal[min(k0 + BR_NT, last)], v2 = gal[min(k0 + 2 * BR_NT, last)],
+                    v3 = gal[min(k0 + 3 * BR_NT, last)];
         s4[k0] = v0;
-        if (k0 + 256 < nfull) s4[k0 + 256] = v1;
-        if (k0 + 512 < nfull) s4[k0 + 512] = v2;
-        if (k0 + 768 < nfull) s4[k0 + 768] = v3;
-        if (k0 + 1024 < nfull) s4[k0 + 1024] = v4;
-        if (k0 + 1280 < nfull) s4[k0 + 1280] = v5;
-        if (k0 + 1536 < nfull) s4[k0 + 1536] = v6;
-        if (k0 + 1792 < nfull) s4[k0 + 1792] = v7;
+        if (k0 + BR_NT < nfull) s4[k0 + BR_NT] = v1;
+        if (k0 + 2 * BR_NT < nfull) s4[k0 + 2 * BR_NT] = v2;
+        if (k0 + 3 * BR_NT < nfull) s4[k0 + 3 * BR_NT] = v3;
     }
-    for (int k = nfull * 16 + tid; k < nbytes; k += 256)  // tail bytes
+    for (int k = nfull * 16 + tid; k < nbytes; k += BR_NT)  // tail bytes
         s_band[k] = reinterpret_cast<const uint8_t*>(gal)[k];
     __syncthreads();
     // 3. descriptors.  Each lane's 8 sample offsets as linear offsets dr * W + dc (the reference's index is
@@ -792,9 +791,9 @@ __global__ __launch_bounds__(256) void brief_kernel(const uint8_t* __restrict__ 
         }
     };
     // two keypoints per iteration: 16 LDS reads per lane in flight
-    for (int k = wave; k < nb; k += 8) {
-        const bool two = k + 4 < nb;
-        const int ia = s_list[k], ib = two ? s_list[k + 4] : ia;
+    for (int k = wave; k < nb; k += 2 * BR_NW) {
+        const bool two = k + BR_NW < nb;
+        const int ia = s_list[k], ib = two ? s_list[k + BR_NW] : ia;
         const int4 kpa = src[ia], kpb = src[ib];
         const int la = kpa.x * W + kpa.y, lb = kpb.x * W + kpb.y;
         uint64_t wa[4], wb[4];
@@ -818,7 +817,7 @@ void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t*
                   const int32_t* kp_count, int max_kp, yv_keypoint* keypoints, Desc* desc, hipStream_t s) {
     dim3 grid((H + BR_BAND - 1) / BR_BAND, n_images);
     const size_t lds = (size_t)BR_ROWS * W + 32;
-    hipLaunchKernelGGL(brief_kernel, grid, dim3(256), lds, s, blur, H, W, offsets, kp_src, kp_count, max_kp,
+    hipLaunchKernelGGL(brief_kernel, grid, dim3(BR_NT), lds, s, blur, H, W, offsets, kp_src, kp_count, max_kp,
                        keypoints, desc);
 }
 
