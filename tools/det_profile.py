@@ -39,7 +39,7 @@ def main():
     ctx.sync()
     ms, _ = b.stage_times()
     assert lib.yv_debug_det_prof(buf.ctypes.data) == 0
-    wgs = ((W + 63) // 64) * ((H + 31) // 32) * 2 * B
+    wgs = ((W + 63) // 64) * ((H + 55) // 56) * 2 * B  # 64 x 56 tiles (kFastTileW x kFastTileH)
     per = buf[:min(wgs, 131072)].astype(np.float64).mean(0)
     print(f"detect {ms[0]:.4f} ms for {2 * B} images, {wgs} workgroups; mean cycles per workgroup (lane 0): "
           f"{per.sum():.0f}")

@@ -1294,7 +1294,7 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
 // Problem p owns edges [offsets[p], offsets[p+1]) (CSR) or, with counts != nullptr, [p*stride, p*stride +
 // counts[p]) (the batch's fixed-stride track layout).  The prior is read from priors[p] and the estimate
 // written to poses[p] (the two may alias).
-__global__ __launch_bounds__(kLMNT) __attribute__((amdgpu_waves_per_eu(4))) void pose_lm_kernel(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
+__global__ __launch_bounds__(kLMNT) void pose_lm_kernel(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
                                                       int stride, const double* __restrict__ Xall,
                                                       const double* __restrict__ uvall, const double* __restrict__ Kall,
                                                       const double* priors, double* poses,

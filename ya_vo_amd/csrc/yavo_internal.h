@@ -11,7 +11,7 @@ namespace yavo {
 constexpr int kMaxKp = 4096;
 constexpr int kMaxWidth = 2048;  // image width limit (BRIEF keeps 49 rows of the blurred image in LDS)       // per-image keypoint capacity supported by the top-K / scan kernels
 constexpr int kFastTileW = 64;     // FAST / blur output tile: one wave per tile row
-constexpr int kFastTileH = 32;
+constexpr int kFastTileH = 56;
 
 struct Desc {                      // 256-bit BRIEF descriptor, test j -> bit j (LSB-first bytes)
     uint32_t w[8];

@@ -166,20 +166,23 @@ __device__ unsigned long long g_det_prof[kDetProfSlots][6];
 #define DP_STORE() do {} while (0)
 #endif
 constexpr int FT_W = kFastTileW;        // 64 output columns per tile (one wave-row)
-constexpr int FT_H = kFastTileH;        // 32 output rows per tile
+constexpr int FT_H = kFastTileH;        // 56 output rows per tile
 constexpr int FT_R = 4;                 // halo: blur radius 4 (ring radius 3, Sobel + 3x3 window radius 2)
 constexpr int FT_LW = FT_W + 2 * FT_R;  // 72 bytes per LDS row
-constexpr int FT_LH = FT_H + 2 * FT_R;  // 40 LDS rows
+constexpr int FT_LH = FT_H + 2 * FT_R;  // 64 LDS rows
 
 template <bool kBlur>
 __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__ imgs, int H, int W, int stride,
                                                      int64_t pitch, int thr, uint64_t* __restrict__ cand_keys,
                                                      int64_t cap, uint32_t* __restrict__ cand_count, K9 kw,
                                                      uint8_t* __restrict__ blur) {
-    __shared__ uint8_t tile[FT_LH * FT_LW];
-    __shared__ __align__(16) uint32_t hbuf[kBlur ? (FT_LH / 2) * FT_W : 4];
+    __shared__ __align__(16) uint8_t tile[FT_LH * FT_LW];
+    // the pretest survivors (phases 1-2) and the horizontal blur (from the barrier after phase 2) share LDS
+    constexpr int kPreDw = FT_W * FT_H / 2, kHbufDw = kBlur ? (FT_LH / 2) * FT_W : 0;
+    __shared__ __align__(16) uint32_t s_share[kPreDw > kHbufDw ? kPreDw : kHbufDw];
+    uint16_t* s_pre = reinterpret_cast<uint16_t*>(s_share);
+    uint32_t* hbuf = s_share;
     __shared__ uint16_t s_pos[FT_W * FT_H];
-    __shared__ uint16_t s_pre[FT_W * FT_H];
     __shared__ uint32_t s_n, s_npre, s_base;
     DP_DECL
     const int img = blockIdx.z;
@@ -193,39 +196,31 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         s_npre = 0;
     }
 
-    // stage (FT_H + 8) x (FT_W + 8) = 40 x 72 bytes.  Interior tiles (every source byte inside the image, and the
-    // last staged row not the image's last, so 3 bytes of alignment slack stay inside the image) load aligned
-    // dwords: 19 per row, 3 per thread, all in flight before the byte writes into LDS.  Border tiles take the
-    // REFLECT_101 byte path.
+    // stage (FT_H + 8) x (FT_W + 8) = 64 x 72 bytes.  Interior tiles (every source byte inside the image, and the
+    // last staged row not the image's last, so the alignment slack past a row end stays inside the image): each
+    // LDS dword is one dword-aligned dwordx2 load funnel-shifted by the row's misalignment (v_alignbyte), 5 per
+    // thread, all in flight before the LDS writes.  Border tiles take the REFLECT_101 byte path.
     const bool interior = (c0 >= FT_R) && (c0 + FT_W + FT_R <= W) && (r0 >= FT_R) && (r0 + FT_H + FT_R < H);
     if (interior) {
-        constexpr int kDw = 19;                      // dwords per row: 72 bytes + up to 3 of alignment
-        constexpr int kSlots = FT_LH * kDw;          // 760
-        constexpr int kPer = (kSlots + 255) / 256;   // 3
-        uint32_t v[kPer];
-        int sh[kPer];
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        constexpr int kDw = FT_LW / 4;               // 18 LDS dwords per row
+        constexpr int kSlots = FT_LH * kDw;          // 1152
+        constexpr int kPer = (kSlots + 255) / 256;   // 5
+        u32x2 v[kPer];
+        uint32_t sh[kPer];
 #pragma unroll
         for (int u = 0; u < kPer; ++u) {
-            const int t = tid + 256 * u;
+            const int t = min(tid + 256 * u, kSlots - 1);
             const int lr = t / kDw, j = t - lr * kDw;
-            v[u] = 0;
-            sh[u] = 0;
-            if (t < kSlots) {
-                const uintptr_t a = reinterpret_cast<uintptr_t>(src + (int64_t)(r0 - FT_R + lr) * stride + (c0 - FT_R));
-                sh[u] = (int)(a & 3);
-                v[u] = reinterpret_cast<const uint32_t*>(a - sh[u])[j];
-            }
+            const uint8_t* a = src + (int64_t)(r0 - FT_R + lr) * stride + (c0 - FT_R) + 4 * j;
+            sh[u] = (uint32_t)reinterpret_cast<uintptr_t>(a) & 3u;
+            __builtin_memcpy(&v[u], __builtin_assume_aligned(a - sh[u], 4), 8);
         }
+        uint32_t* tile32 = reinterpret_cast<uint32_t*>(tile);
 #pragma unroll
         for (int u = 0; u < kPer; ++u) {
             const int t = tid + 256 * u;
-            if (t >= kSlots) continue;
-            const int lr = t / kDw, j = t - lr * kDw;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int bcol = 4 * j + q - sh[u];  // tile column of byte q of this dword
-                if (bcol >= 0 && bcol < FT_LW) tile[lr * FT_LW + bcol] = (uint8_t)(v[u] >> (8 * q));
-            }
+            if (t < kSlots) tile32[t] = __builtin_amdgcn_alignbyte(v[u].y, v[u].x, sh[u]);
         }
     } else {
         // wave w loads rows w, w+4, ...; lanes 0..63 (+ 0..7) cover 72 columns; all of this wave's row loads
@@ -258,28 +253,29 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
     const uint32_t neg_thr = (uint32_t)(-thr);
     // checkInBetween(cent, p) <=> cent > p - thr && cent < p + thr <=> |cent - p| - thr < 0: v_sad_u8 gives
     // |cent - p| + (-thr) in one instruction; its sign bit is "similar"
-    auto similar = [&](const uint8_t* t0, uint32_t cent, int k) -> uint32_t {
-        return __builtin_amdgcn_sad_u8(cent, (uint32_t)t0[ring_dr[k] * FT_LW + ring_dc[k]], neg_thr) >> 31;
-    };
     // phase 1: the reference's pretest on ring pixels 0, 7 and (4 | 12) (src/FastDetector.cc:304-317) for
     // every pixel; each lane keeps a mask of its passing rows and the survivors are compacted into s_pre
     // once per wave (one scan, one LDS atomic)
     const int tx = lane, ty = wave;
     const int c = c0 + tx;
     constexpr int kRowIters = FT_H / 4;
-    uint32_t pmask = 0;
+    // pixel (r, c) is tested iff 4 <= r < H - 4 and 4 <= c < W - 4: rows are wave-uniform, so the row test is one
+    // mask over the row iterations and the column test one compare
+    uint32_t row_ok = 0;
 #pragma unroll
-    for (int u = 0; u < kRowIters; ++u) {
-        const int rr = ty + 4 * u;
-        const int r = r0 + rr;
-        const bool inside = (r >= 4) && (r < H - 4) && (c >= 4) && (c < W - 4);
-        const uint8_t* t0 = &tile[(rr + FT_R) * FT_LW + tx + FT_R];
+    for (int u = 0; u < kRowIters; ++u) row_ok |= (uint32_t)((unsigned)(r0 + ty + 4 * u - 4) < (unsigned)(H - 8)) << u;
+    // "similar" is the sign bit of sad(c, p) - thr: pre <=> !(s0 | s7) && !(s4 & s12) <=> sign bit clear in
+    // (d0 | d7) | (d4 & d12); the sign bits are shifted into nmask (bit u = not pre) with v_alignbit
+    uint32_t nmask = 0;
+#pragma unroll
+    for (int u = kRowIters - 1; u >= 0; --u) {
+        const uint8_t* t0 = &tile[(ty + 4 * u + FT_R) * FT_LW + tx + FT_R];
         const uint32_t cent = t0[0];
-        const uint32_t s0 = similar(t0, cent, 0), s7 = similar(t0, cent, 7);
-        const uint32_t s4 = similar(t0, cent, 4), s12 = similar(t0, cent, 12);
-        const bool pre = inside && !(s0 | s7) && !(s4 & s12);
-        pmask |= (uint32_t)pre << u;
+        auto d = [&](int k) { return __builtin_amdgcn_sad_u8(cent, (uint32_t)t0[ring_dr[k] * FT_LW + ring_dc[k]], neg_thr); };
+        const uint32_t v = (d(0) | d(7)) | (d(4) & d(12));
+        nmask = __builtin_amdgcn_alignbit(nmask, v, 31);  // (nmask << 1) | (v >> 31)
     }
+    const uint32_t pmask = (unsigned)(c - 4) < (unsigned)(W - 8) ? (~nmask & row_ok) : 0u;
     {
         const int cnt = __popc(pmask);
         const int incl = wave_incl_scan(cnt);
@@ -305,9 +301,12 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
             pos = s_pre[i];
             const uint8_t* t0 = &tile[((pos >> 6) + FT_R) * FT_LW + (pos & 63) + FT_R];
             const uint32_t cent = t0[0];
+            // similar bits in reverse ring order (bit 15 - k for ring pixel k), one v_alignbit each; a run of
+            // 12 consecutive bits without wrap is the same test in either order
             uint32_t sim = 0;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) sim |= similar(t0, cent, k) << k;
+            for (int k = 0; k < 16; ++k)
+                sim = __builtin_amdgcn_alignbit(sim, __builtin_amdgcn_sad_u8(cent, (uint32_t)t0[ring_dr[k] * FT_LW + ring_dc[k]], neg_thr), 31);
             const uint32_t mask = ~sim & 0xFFFFu;  // "different" ring pixels
             const uint32_t a2 = mask & (mask >> 1);
             const uint32_t a4 = a2 & (a2 >> 2);
