@@ -89,6 +89,37 @@ int yv_calc_optical_flow_pyr_lk(struct yv_ctx* ctx, const uint8_t* prev, const u
                                 int stride, const float* prev_pts, int n, int win, int max_level, int max_count,
                                 double eps, double min_eig, float* next_pts, uint8_t* status, float* err);
 
+/* ---- cv::findEssentialMat (RANSAC) + cv::recoverPose ----
+ * Replaces, at the reference's (re)initialisation (src/LoopHandler.cc:239,256 and :581,598):
+ *     E = cv::findEssentialMat(currFeatures, prevFeatures, 718.8560, cv::Point2d(607.1928, 185.2157), cv::RANSAC,
+ *                              0.999, 1.0, mask);
+ *     cv::recoverPose(E, currFramePts, lastFramePts, K, R, t);
+ * Points are (x, y) pixel pairs exactly as the reference builds them (cv::Point2f(kp.x, kp.y), i.e. x = row,
+ * y = column, used literally with pp and K).  The classic OpenCV path is restated (oracle/yavo_oracle_essential.c):
+ * RANSAC with cv::RNG((uint64)-1) subsets, the five-point solver, float Sampson errors, maxIters 1000; recoverPose
+ * with distance threshold 50 and no input mask (as the reference calls it).  A workspace serves up to max_pairs
+ * lists of up to max_points correspondences. */
+typedef struct yv_essential yv_essential;
+int yv_essential_create(struct yv_ctx* ctx, int max_pairs, int max_points, int max_iters, yv_essential** out);
+void yv_essential_destroy(yv_essential* es);
+/* List p: d_pts1 / d_pts2 + 2*(p*pts_stride + i), i < d_counts[p] (5 <= n <= max_points to run; fewer -> not
+ * found).  Outputs: d_E [p][9] (row-major; 0 when not found), d_mask + p*pts_stride (inliers of E; may be NULL),
+ * d_found [p], d_stats [p][3] = {RANSAC iterations, models scored, best inlier count} (may be NULL). */
+int yv_find_essential_batch(yv_essential* es, const float* d_pts1, const float* d_pts2, const int32_t* d_counts,
+                            int n_pairs, int pts_stride, double focal, double ppx, double ppy, double prob,
+                            double threshold, double* d_E, uint8_t* d_mask, int32_t* d_found, int32_t* d_stats,
+                            void* stream);
+/* recoverPose(E_p, pts1_p, pts2_p, K, R_p, t_p): d_R [p][9], d_t [p][3], d_good [p] = cheirality count (may be
+ * NULL).  Lists as in yv_find_essential_batch. */
+int yv_recover_pose_batch(yv_essential* es, const double* d_E, const float* d_pts1, const float* d_pts2,
+                          const int32_t* d_counts, int n_pairs, int pts_stride, const double K[9], double* d_R,
+                          double* d_t, int32_t* d_good, void* stream);
+/* Host-pointer drop-ins for one list (n <= 65536): *found = 0 leaves E zero. */
+int yv_find_essential(struct yv_ctx* ctx, const float* pts1, const float* pts2, int n, double focal, double ppx,
+                      double ppy, double prob, double threshold, double E[9], uint8_t* mask, int* found);
+int yv_recover_pose(struct yv_ctx* ctx, const double E[9], const float* pts1, const float* pts2, int n,
+                    const double K[9], double R[9], double t[3], int* good);
+
 #ifdef __cplusplus
 }
 #endif

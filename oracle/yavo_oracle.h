@@ -126,6 +126,29 @@ int or_lk_pyr(const uint8_t* prev, const uint8_t* next, int H, int W, const floa
               int max_level, int max_count, double eps, double min_eig, float* next_pts, uint8_t* status,
               float* err, int sum_mode);
 
+/* ---- cv::findEssentialMat (RANSAC) + cv::recoverPose (yavo_oracle_essential.c) ---- */
+/* getSubset draws of RANSACPointSetRegistrator::run (cv::RNG((uint64)-1)): idx [iters][5] */
+void or_em_subsets(int count, int iters, int32_t* idx);
+/* the 10 x 20 cubic-constraint matrix from the null-space basis EE [4][9] */
+void or_em_coeff_mat(const double* EE, double* A);
+/* det B(z) of the 3 x 13 elimination matrix -> c[0..10] ascending */
+void or_em_det_poly(const double* B, double* c);
+/* cv::solvePoly (Durand-Kerner) on real c[0..n0] ascending; roots [n0][2] (re, im); returns iterations run */
+int or_solve_poly(const double* c, int n0, int max_iters, double* roots);
+/* EMEstimatorCallback::runKernel on 5 normalised correspondences; models [10][9]; returns the model count */
+int or_em_kernel(const double* q1, const double* q2, double* models);
+/* (p - c) / f as OpenCV's MatExpr evaluates it */
+void or_normalize_points(const double* pts, int n, double fx, double fy, double cx, double cy, double* out);
+/* findEssentialMat(pts1, pts2, focal, (ppx, ppy), RANSAC, prob, threshold, mask) with maxIters; pts [n][2] pixels.
+ * stats (optional) = {iterations run, models scored, best inlier count}.  Returns 1 when E was found. */
+int or_find_essential(const double* pts1, const double* pts2, int n, double focal, double ppx, double ppy, double prob,
+                      double threshold, int max_iters, double E[9], uint8_t* mask, int* stats);
+/* decomposeEssentialMat */
+void or_decompose_essential(const double E[9], double R1[9], double R2[9], double t[3]);
+/* recoverPose(E, pts1, pts2, K, R, t) (distanceThresh 50, no input mask); good[4] per candidate; returns the count */
+int or_recover_pose(const double E[9], const double* pts1, const double* pts2, int n, const double K[9], double R[9],
+                    double t[3], int good[4]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,16 @@ class Oracle:
             "or_scharr": (None, [_P, _I, _I, _I, _P]),
             "or_lk_pyr": (_I, [_P, _P, _I, _I, _P, _I, _I, _I, _I, ctypes.c_double, ctypes.c_double, _P, _P, _P,
                                _I]),
+            "or_em_subsets": (None, [_I, _I, _P]),
+            "or_em_coeff_mat": (None, [_P, _P]),
+            "or_em_det_poly": (None, [_P, _P]),
+            "or_solve_poly": (_I, [_P, _I, _I, _P]),
+            "or_em_kernel": (_I, [_P, _P, _P]),
+            "or_normalize_points": (None, [_P, _I, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, _P]),
+            "or_find_essential": (_I, [_P, _P, _I, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_double, _I, _P, _P, _P]),
+            "or_decompose_essential": (None, [_P, _P, _P, _P]),
+            "or_recover_pose": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -283,3 +293,48 @@ class Oracle:
         lv = self.lib.or_lk_pyr(_p(prev), _p(nxt), H, W, _p(pts), len(pts), win, max_level, max_count, eps, min_eig,
                                 _p(nextp), _p(status), _p(err), sum_mode)
         return nextp, status[:len(pts)].astype(bool), err[:len(pts)], lv
+
+    # ---- findEssentialMat / recoverPose ----
+    def em_subsets(self, count, iters):
+        idx = np.zeros((iters, 5), np.int32)
+        self.lib.or_em_subsets(count, iters, _p(idx))
+        return idx
+
+    def em_kernel(self, q1, q2):
+        q1 = np.ascontiguousarray(q1, np.float64).reshape(5, 2)
+        q2 = np.ascontiguousarray(q2, np.float64).reshape(5, 2)
+        models = np.zeros((10, 9), np.float64)
+        n = self.lib.or_em_kernel(_p(q1), _p(q2), _p(models))
+        return models[:n].reshape(-1, 3, 3)
+
+    def solve_poly(self, c, max_iters=300):
+        c = np.ascontiguousarray(c, np.float64)
+        roots = np.zeros((len(c) - 1, 2), np.float64)
+        it = self.lib.or_solve_poly(_p(c), len(c) - 1, max_iters, _p(roots))
+        return roots[:, 0] + 1j * roots[:, 1], it
+
+    def find_essential(self, pts1, pts2, focal=718.856, pp=(607.1928, 185.2157), prob=0.999, threshold=1.0,
+                       max_iters=1000):
+        """-> (ok, E [3, 3], mask [n] bool, stats {iters, models, best})."""
+        p1 = np.ascontiguousarray(pts1, np.float64).reshape(-1, 2)
+        p2 = np.ascontiguousarray(pts2, np.float64).reshape(-1, 2)
+        n = len(p1)
+        E = np.zeros(9, np.float64)
+        mask = np.zeros(max(n, 1), np.uint8)
+        st = np.zeros(3, np.int32)
+        ok = self.lib.or_find_essential(_p(p1), _p(p2), n, focal, pp[0], pp[1], prob, threshold, max_iters, _p(E),
+                                        _p(mask), _p(st))
+        return bool(ok), E.reshape(3, 3), mask[:n].astype(bool), dict(iters=int(st[0]), models=int(st[1]),
+                                                                        best=int(st[2]))
+
+    def recover_pose(self, E, pts1, pts2, K):
+        """-> (good, R [3, 3], t [3], good per candidate [4])."""
+        E = np.ascontiguousarray(E, np.float64).reshape(9)
+        p1 = np.ascontiguousarray(pts1, np.float64).reshape(-1, 2)
+        p2 = np.ascontiguousarray(pts2, np.float64).reshape(-1, 2)
+        K = np.ascontiguousarray(K, np.float64).reshape(9)
+        R = np.zeros(9, np.float64)
+        t = np.zeros(3, np.float64)
+        g = np.zeros(4, np.int32)
+        good = self.lib.or_recover_pose(_p(E), _p(p1), _p(p2), len(p1), _p(K), _p(R), _p(t), _p(g))
+        return good, R.reshape(3, 3), t, g

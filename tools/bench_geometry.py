@@ -179,6 +179,48 @@ def main():
                  "pair0_bit_identical": bool(np.array_equal(g, o)),
                  "pair0_tracked": int(os_.sum())}
     lk.close()
+    # ---- findEssentialMat (RANSAC) + recoverPose: L lists of n correspondences, 20% gross mismatches --------
+    from epipolar_scene import K_KITTI, two_view_scene
+    ne = n
+    e1 = np.zeros((L, ne, 2), np.float32)
+    e2 = np.zeros((L, ne, 2), np.float32)
+    for l in range(L):
+        a, b, _, _ = two_view_scene(ne, outlier_frac=0.2, seed=500 + l, angle=0.02 + 0.0001 * l)
+        e1[l], e2[l] = a, b
+    d_e1, d_e2 = torch.from_numpy(e1).to(dev), torch.from_numpy(e2).to(dev)
+    d_ecnt = torch.full((L,), ne, dtype=torch.int32, device=dev)
+    d_E = torch.zeros((L, 9), dtype=torch.float64, device=dev)
+    d_ef = torch.zeros(L, dtype=torch.int32, device=dev)
+    d_es = torch.zeros((L, 3), dtype=torch.int32, device=dev)
+    d_R = torch.zeros((L, 9), dtype=torch.float64, device=dev)
+    d_t = torch.zeros((L, 3), dtype=torch.float64, device=dev)
+    es = yv.Essential(ctx, L, ne)
+
+    def ess_find():
+        es.find(d_e1.data_ptr(), d_e2.data_ptr(), d_ecnt.data_ptr(), L, ne, d_E.data_ptr(), d_ef.data_ptr(),
+                d_stats=d_es.data_ptr(), stream=stream)
+
+    def ess_recover():
+        es.recover(d_E.data_ptr(), d_e1.data_ptr(), d_e2.data_ptr(), d_ecnt.data_ptr(), L, ne, K_KITTI,
+                   d_R.data_ptr(), d_t.data_ptr(), stream=stream)
+
+    ms_f = timed(ess_find)
+    ms_r = timed(ess_recover)
+    torch.cuda.synchronize()
+    gE = d_E[0].cpu().numpy().reshape(3, 3)
+    st = d_es.cpu().numpy()
+    t0 = time.perf_counter()
+    ok0, oE, _, _ = orc.find_essential(e1[0], e2[0])
+    og, oR, ot, _ = orc.recover_pose(oE, e1[0], e2[0], K_KITTI)
+    cpu = time.perf_counter() - t0
+    out["essential"] = {"pairs": L, "points_per_pair": ne, "outlier_frac": 0.2,
+                        "gpu_find_ms": round(ms_f, 4), "gpu_recover_ms": round(ms_r, 4),
+                        "gpu_pairs_per_s": round(L / ((ms_f + ms_r) / 1e3), 1),
+                        "mean_ransac_iterations": round(float(st[:, 0].mean()), 2),
+                        "cpu_oracle_pairs_per_s": round(1 / cpu, 2), "cpu_threads": 1,
+                        "pair0_bit_identical": bool(ok0 and np.array_equal(gE, oE) and
+                                                    np.array_equal(d_R[0].cpu().numpy().reshape(3, 3), oR))}
+    es.close()
     print(json.dumps(out), flush=True)
     ctx.close()
 

@@ -107,6 +107,12 @@ GEOM_SIGNATURES = {
     "yv_lk_build": (_I, [_P, _P, _I, _I, ctypes.c_int64, _P]),
     "yv_lk_track_batch": (_I, [_P, _P, _I, _P, _P, _I, _I, _D, _D, _P, _P, _P, _P]),
     "yv_calc_optical_flow_pyr_lk": (_I, [_P, _P, _P, _I, _I, _I, _P, _I, _I, _I, _I, _D, _D, _P, _P, _P]),
+    "yv_essential_create": (_I, [_P, _I, _I, _I, ctypes.POINTER(_P)]),
+    "yv_essential_destroy": (None, [_P]),
+    "yv_find_essential_batch": (_I, [_P, _P, _P, _P, _I, _I, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P]),
+    "yv_recover_pose_batch": (_I, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
+    "yv_find_essential": (_I, [_P, _P, _P, _I, _D, _D, _D, _D, _D, _P, _P, ctypes.POINTER(_I)]),
+    "yv_recover_pose": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, ctypes.POINTER(_I)]),
 }
 
 
@@ -165,6 +171,33 @@ class _GeomMixin:
                                                     max_level, max_count, eps, min_eig, _ptr(out), _ptr(st),
                                                     _ptr(err)), "yv_calc_optical_flow_pyr_lk")
         return out, st[:len(p)].astype(bool), err[:len(p)]
+
+    def find_essential(self, pts1, pts2, focal=718.8560, pp=(607.1928, 185.2157), prob=0.999, threshold=1.0):
+        """cv::findEssentialMat(pts1, pts2, focal, pp, RANSAC, prob, threshold, mask) (src/LoopHandler.cc:239)
+        -> (found, E [3, 3], mask [n] bool).  Points: (x, y) pixels as the reference passes them."""
+        p1 = np.ascontiguousarray(pts1, np.float32).reshape(-1, 2)
+        p2 = np.ascontiguousarray(pts2, np.float32).reshape(-1, 2)
+        if len(p1) != len(p2):
+            raise ValueError("pts1 and pts2 differ in length")
+        E = np.zeros(9, np.float64)
+        mask = np.zeros(max(len(p1), 1), np.uint8)
+        found = ctypes.c_int(0)
+        _check(self.lib.yv_find_essential(self.handle, _ptr(p1), _ptr(p2), len(p1), focal, pp[0], pp[1], prob,
+                                          threshold, _ptr(E), _ptr(mask), ctypes.byref(found)), "yv_find_essential")
+        return bool(found.value), E.reshape(3, 3), mask[:len(p1)].astype(bool)
+
+    def recover_pose(self, E, pts1, pts2, K):
+        """cv::recoverPose(E, pts1, pts2, K, R, t) (src/LoopHandler.cc:256) -> (good, R [3, 3], t [3])."""
+        E = np.ascontiguousarray(E, np.float64).reshape(9)
+        p1 = np.ascontiguousarray(pts1, np.float32).reshape(-1, 2)
+        p2 = np.ascontiguousarray(pts2, np.float32).reshape(-1, 2)
+        K = np.ascontiguousarray(K, np.float64).reshape(9)
+        R = np.zeros(9, np.float64)
+        t = np.zeros(3, np.float64)
+        good = ctypes.c_int(0)
+        _check(self.lib.yv_recover_pose(self.handle, _ptr(E), _ptr(p1), _ptr(p2), len(p1), _ptr(K), _ptr(R), _ptr(t),
+                                        ctypes.byref(good)), "yv_recover_pose")
+        return good.value, R.reshape(3, 3), t
 
     def f_ransac(self, matches: np.ndarray, samples: np.ndarray, thr: float = 0.1):
         """_3DHandler::getFRANSAC -> (found, F [3,3], max_inliers)."""
@@ -433,3 +466,44 @@ class Lk:
                                           ctypes.c_void_p(d_counts), pts_stride, max_count, eps, min_eig,
                                           ctypes.c_void_p(d_next), ctypes.c_void_p(d_status), ctypes.c_void_p(d_err),
                                           ctypes.c_void_p(stream) if stream else None), "yv_lk_track_batch")
+
+
+class Essential:
+    """Batched cv::findEssentialMat (RANSAC) + cv::recoverPose workspace (yv_essential)."""
+
+    def __init__(self, ctx: "Context", max_pairs: int, max_points: int, max_iters: int = 1000):
+        self.ctx, self.lib = ctx, ctx.lib
+        h = ctypes.c_void_p()
+        _check(self.lib.yv_essential_create(ctx.handle, max_pairs, max_points, max_iters, ctypes.byref(h)),
+               "yv_essential_create")
+        self.handle = h
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.yv_essential_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def find(self, d_pts1: int, d_pts2: int, d_counts: int, n_pairs: int, pts_stride: int, d_E: int, d_found: int,
+             d_mask: int = 0, d_stats: int = 0, focal: float = 718.8560, pp=(607.1928, 185.2157), prob: float = 0.999,
+             threshold: float = 1.0, stream: int = 0) -> None:
+        _check(self.lib.yv_find_essential_batch(self.handle, ctypes.c_void_p(d_pts1), ctypes.c_void_p(d_pts2),
+                                                ctypes.c_void_p(d_counts), n_pairs, pts_stride, focal, pp[0], pp[1],
+                                                prob, threshold, ctypes.c_void_p(d_E),
+                                                ctypes.c_void_p(d_mask) if d_mask else None, ctypes.c_void_p(d_found),
+                                                ctypes.c_void_p(d_stats) if d_stats else None,
+                                                ctypes.c_void_p(stream) if stream else None), "yv_find_essential_batch")
+
+    def recover(self, d_E: int, d_pts1: int, d_pts2: int, d_counts: int, n_pairs: int, pts_stride: int, K,
+                d_R: int, d_t: int, d_good: int = 0, stream: int = 0) -> None:
+        K = np.ascontiguousarray(K, np.float64).reshape(9)
+        _check(self.lib.yv_recover_pose_batch(self.handle, ctypes.c_void_p(d_E), ctypes.c_void_p(d_pts1),
+                                              ctypes.c_void_p(d_pts2), ctypes.c_void_p(d_counts), n_pairs, pts_stride,
+                                              _ptr(K), ctypes.c_void_p(d_R), ctypes.c_void_p(d_t),
+                                              ctypes.c_void_p(d_good) if d_good else None,
+                                              ctypes.c_void_p(stream) if stream else None), "yv_recover_pose_batch")

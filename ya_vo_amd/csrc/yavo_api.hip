@@ -1220,3 +1220,198 @@ int yv_calc_optical_flow_pyr_lk(yv_ctx* ctx, const uint8_t* prev, const uint8_t*
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// cv::findEssentialMat (RANSAC) + cv::recoverPose (yavo_geom.h)
+// ------------------------------------------------------------------------------------------------
+struct yv_essential {
+    yv_ctx* ctx = nullptr;
+    yavo::EssParams P;
+};
+
+namespace {
+void essential_free(yv_essential* es) {
+    if (!es) return;
+    yavo::EssParams& P = es->P;
+    void* ptrs[] = {P.m1, P.m2, P.idx, P.models, P.nmod, P.good, P.state, P.best, P.cand, P.cgood};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    delete es;
+}
+}  // namespace
+
+extern "C" {
+
+int yv_essential_create(yv_ctx* ctx, int max_pairs, int max_points, int max_iters, yv_essential** out) {
+    if (!ctx || !out || max_pairs <= 0 || max_points < 5 || max_points > (1 << 20) || max_iters <= 0 ||
+        max_iters > 100000)
+        return YV_ERR_INVALID;
+    *out = nullptr;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    yv_essential* es = new (std::nothrow) yv_essential();
+    if (!es) return YV_ERR_INVALID;
+    es->ctx = ctx;
+    yavo::EssParams& P = es->P;
+    P.max_pairs = max_pairs;
+    P.max_points = max_points;
+    P.max_iters = max_iters;
+    const size_t np = (size_t)max_pairs;
+    if (dalloc(&P.m1, np * max_points * 2) != YV_OK || dalloc(&P.m2, np * max_points * 2) != YV_OK ||
+        dalloc(&P.idx, np * max_iters * 5) != YV_OK || dalloc(&P.models, np * yavo::kEssChunk * 90) != YV_OK ||
+        dalloc(&P.nmod, np * yavo::kEssChunk) != YV_OK || dalloc(&P.good, np * yavo::kEssChunk * 10) != YV_OK ||
+        dalloc(&P.state, np * 8) != YV_OK || dalloc(&P.best, np * 9) != YV_OK || dalloc(&P.cand, np * 48) != YV_OK ||
+        dalloc(&P.cgood, np * 4) != YV_OK) {
+        essential_free(es);
+        return YV_ERR_HIP;
+    }
+    *out = es;
+    return YV_OK;
+}
+
+void yv_essential_destroy(yv_essential* es) {
+    if (!es) return;
+    (void)hipSetDevice(es->ctx->device);
+    (void)hipDeviceSynchronize();
+    essential_free(es);
+}
+
+int yv_find_essential_batch(yv_essential* es, const float* d_pts1, const float* d_pts2, const int32_t* d_counts,
+                            int n_pairs, int pts_stride, double focal, double ppx, double ppy, double prob,
+                            double threshold, double* d_E, uint8_t* d_mask, int32_t* d_found, int32_t* d_stats,
+                            void* stream) {
+    if (!es || n_pairs < 0 || n_pairs > es->P.max_pairs || pts_stride < 0 || pts_stride > es->P.max_points ||
+        (n_pairs > 0 && (!d_pts1 || !d_pts2 || !d_counts || !d_E || !d_found)) || !(focal != 0.0) ||
+        !(prob > 0.0 && prob < 1.0))
+        return YV_ERR_INVALID;
+    if (n_pairs == 0) return YV_OK;
+    if (set_device(es->ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : es->ctx->stream;
+    // a list holds at most pts_stride (<= max_points) points: longer counts are clipped on the device
+    yavo::EssRun r{focal, ppx, ppy, prob, threshold, es->P.max_iters};
+    yavo::launch_find_essential(es->P, r, d_pts1, d_pts2, d_counts, n_pairs, pts_stride, d_E, d_mask, d_found,
+                                d_stats, s);
+    return check_launch();
+}
+
+int yv_recover_pose_batch(yv_essential* es, const double* d_E, const float* d_pts1, const float* d_pts2,
+                          const int32_t* d_counts, int n_pairs, int pts_stride, const double K[9], double* d_R,
+                          double* d_t, int32_t* d_good, void* stream) {
+    if (!es || !K || n_pairs < 0 || n_pairs > es->P.max_pairs || pts_stride < 0 || pts_stride > es->P.max_points ||
+        (n_pairs > 0 && (!d_E || !d_pts1 || !d_pts2 || !d_counts || !d_R || !d_t)) || !(K[0] != 0.0) ||
+        !(K[4] != 0.0))
+        return YV_ERR_INVALID;
+    if (n_pairs == 0) return YV_OK;
+    if (set_device(es->ctx) != YV_OK) return YV_ERR_HIP;
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : es->ctx->stream;
+    yavo::Mat3 k;
+    for (int i = 0; i < 9; ++i) k.v[i] = K[i];
+    yavo::launch_recover_pose(es->P, d_E, d_pts1, d_pts2, d_counts, n_pairs, pts_stride, k, d_R, d_t, d_good, s);
+    return check_launch();
+}
+
+int yv_find_essential(yv_ctx* ctx, const float* pts1, const float* pts2, int n, double focal, double ppx, double ppy,
+                      double prob, double threshold, double E[9], uint8_t* mask, int* found) {
+    if (!ctx || !E || !found || n < 0 || (n > 0 && (!pts1 || !pts2))) return YV_ERR_INVALID;
+    if (n > 65536) return YV_ERR_CAPACITY;
+    *found = 0;
+    for (int i = 0; i < 9; ++i) E[i] = 0.0;
+    if (n < 5) {
+        if (mask)
+            for (int i = 0; i < n; ++i) mask[i] = 0;
+        return YV_OK;
+    }
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    yv_essential* es = nullptr;
+    int rc = yv_essential_create(ctx, 1, n, 1000, &es);
+    if (rc != YV_OK) return rc;
+    hipStream_t s = ctx->stream;
+    Arena a{ctx};
+    float *d1, *d2;
+    double* dE;
+    uint8_t* dm;
+    int32_t *dcnt, *dfound;
+    a.add(&d1, 2 * (size_t)n);
+    a.add(&d2, 2 * (size_t)n);
+    a.add(&dE, 9);
+    a.add(&dm, (size_t)n);
+    a.add(&dcnt, 1);
+    a.add(&dfound, 1);
+    if (a.commit() != YV_OK) {
+        yv_essential_destroy(es);
+        return YV_ERR_HIP;
+    }
+    int st = YV_OK;
+    do {
+        ctx->h_pinned[0] = n;
+        if (hipMemcpyAsync(d1, pts1, sizeof(float) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(d2, pts2, sizeof(float) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(dcnt, ctx->h_pinned, sizeof(int32_t), hipMemcpyHostToDevice, s) != hipSuccess) {
+            st = YV_ERR_HIP;
+            break;
+        }
+        st = yv_find_essential_batch(es, d1, d2, dcnt, 1, n, focal, ppx, ppy, prob, threshold, dE, dm, dfound,
+                                     nullptr, nullptr);
+        if (st != YV_OK) break;
+        if (hipMemcpyAsync(E, dE, sizeof(double) * 9, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(ctx->h_pinned + 1, dfound, sizeof(int32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            (mask && hipMemcpyAsync(mask, dm, (size_t)n, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            st = YV_ERR_HIP;
+            break;
+        }
+        *found = ctx->h_pinned[1];
+    } while (0);
+    yv_essential_destroy(es);
+    return st;
+}
+
+int yv_recover_pose(yv_ctx* ctx, const double E[9], const float* pts1, const float* pts2, int n, const double K[9],
+                    double R[9], double t[3], int* good) {
+    if (!ctx || !E || !K || !R || !t || !good || n < 0 || (n > 0 && (!pts1 || !pts2))) return YV_ERR_INVALID;
+    if (n > 65536) return YV_ERR_CAPACITY;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    yv_essential* es = nullptr;
+    int rc = yv_essential_create(ctx, 1, std::max(n, 5), 1, &es);
+    if (rc != YV_OK) return rc;
+    hipStream_t s = ctx->stream;
+    Arena a{ctx};
+    float *d1, *d2;
+    double *dE, *dR, *dt;
+    int32_t *dcnt, *dgood;
+    a.add(&d1, 2 * (size_t)std::max(n, 1));
+    a.add(&d2, 2 * (size_t)std::max(n, 1));
+    a.add(&dE, 9);
+    a.add(&dR, 9);
+    a.add(&dt, 3);
+    a.add(&dcnt, 1);
+    a.add(&dgood, 1);
+    if (a.commit() != YV_OK) {
+        yv_essential_destroy(es);
+        return YV_ERR_HIP;
+    }
+    int st = YV_OK;
+    do {
+        ctx->h_pinned[0] = n;
+        if ((n > 0 && (hipMemcpyAsync(d1, pts1, sizeof(float) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+                       hipMemcpyAsync(d2, pts2, sizeof(float) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess)) ||
+            hipMemcpyAsync(dE, E, sizeof(double) * 9, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(dcnt, ctx->h_pinned, sizeof(int32_t), hipMemcpyHostToDevice, s) != hipSuccess) {
+            st = YV_ERR_HIP;
+            break;
+        }
+        st = yv_recover_pose_batch(es, dE, d1, d2, dcnt, 1, std::max(n, 5), K, dR, dt, dgood, nullptr);
+        if (st != YV_OK) break;
+        if (hipMemcpyAsync(R, dR, sizeof(double) * 9, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(t, dt, sizeof(double) * 3, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(ctx->h_pinned + 1, dgood, sizeof(int32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            st = YV_ERR_HIP;
+            break;
+        }
+        *good = ctx->h_pinned[1];
+    } while (0);
+    yv_essential_destroy(es);
+    return st;
+}
+
+}  // extern "C"

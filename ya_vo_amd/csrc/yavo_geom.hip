@@ -20,9 +20,15 @@
 #include <stdint.h>
 
 #include "yavo_internal.h"
+#include "yavo_cvsvd.h"
 
 namespace yavo {
 namespace geom {
+
+using cv::cv_hypot;
+using cv::cv_rng_next;
+using cv::cv_jacobi_svd;
+using cv::cv_jacobi_svd_mn;
 
 constexpr int kNT = 256;          // threads per workgroup of the reduction kernels
 constexpr int kLMNT = 256;        // threads per pose-LM workgroup (<= 256 VGPRs: half the register file, so the
@@ -63,137 +69,7 @@ __device__ int block_excl_scan_geom(int v, int* s_tmp, int* total) {
     return base + incl - v;
 }
 
-// ------------------------------------------------------------------------------------------------
-// OpenCV JacobiSVDImpl_<double> (per lane, private arrays)
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ double cv_hypot(double a, double b) {
-    a = fabs(a);
-    b = fabs(b);
-    if (a > b) {
-        b /= a;
-        return a * sqrt(1 + b * b);
-    }
-    if (b > 0) {
-        a /= b;
-        return b * sqrt(1 + a * a);
-    }
-    return 0;
-}
-
-__device__ __forceinline__ uint32_t cv_rng_next(uint64_t* state) {
-    *state = (uint64_t)(uint32_t)*state * 4164903690ULL + (uint32_t)(*state >> 32);
-    return (uint32_t)*state;
-}
-
-template <int N>
-__device__ void cv_jacobi_svd(double* At, double* Wout, double* Vt) {
-    // square: m = n = N, astep = vstep = N, n1 = N
-    const double minval = DBL_MIN, eps = DBL_EPSILON * 10;
-    double W[N];
-    const int m = N, n = N, max_iter = m > 30 ? m : 30;
-    double c, s, sd;
-    for (int i = 0; i < n; i++) {
-        sd = 0;
-        for (int k = 0; k < m; k++) {
-            double t = At[i * N + k];
-            sd += t * t;
-        }
-        W[i] = sd;
-        for (int k = 0; k < n; k++) Vt[i * N + k] = 0;
-        Vt[i * N + i] = 1;
-    }
-    for (int iter = 0; iter < max_iter; iter++) {
-        bool changed = false;
-        for (int i = 0; i < n - 1; i++)
-            for (int j = i + 1; j < n; j++) {
-                double *Ai = At + i * N, *Aj = At + j * N;
-                double a = W[i], p = 0, b = W[j];
-                for (int k = 0; k < m; k++) p += Ai[k] * Aj[k];
-                if (fabs(p) <= eps * sqrt(a * b)) continue;
-                p *= 2;
-                double beta = a - b, gamma = cv_hypot(p, beta);
-                if (beta < 0) {
-                    double delta = (gamma - beta) * 0.5;
-                    s = sqrt(delta / gamma);
-                    c = p / (gamma * s * 2);
-                } else {
-                    c = sqrt((gamma + beta) / (gamma * 2));
-                    s = p / (gamma * c * 2);
-                }
-                a = b = 0;
-                for (int k = 0; k < m; k++) {
-                    double t0 = c * Ai[k] + s * Aj[k];
-                    double t1 = -s * Ai[k] + c * Aj[k];
-                    Ai[k] = t0;
-                    Aj[k] = t1;
-                    a += t0 * t0;
-                    b += t1 * t1;
-                }
-                W[i] = a;
-                W[j] = b;
-                changed = true;
-                double *Vi = Vt + i * N, *Vj = Vt + j * N;
-                for (int k = 0; k < n; k++) {
-                    double t0 = c * Vi[k] + s * Vj[k];
-                    double t1 = -s * Vi[k] + c * Vj[k];
-                    Vi[k] = t0;
-                    Vj[k] = t1;
-                }
-            }
-        if (!changed) break;
-    }
-    for (int i = 0; i < n; i++) {
-        sd = 0;
-        for (int k = 0; k < m; k++) {
-            double t = At[i * N + k];
-            sd += t * t;
-        }
-        W[i] = sqrt(sd);
-    }
-    for (int i = 0; i < n - 1; i++) {
-        int j = i;
-        for (int k = i + 1; k < n; k++)
-            if (W[j] < W[k]) j = k;
-        if (i != j) {
-            double t = W[i];
-            W[i] = W[j];
-            W[j] = t;
-            for (int k = 0; k < m; k++) { t = At[i * N + k]; At[i * N + k] = At[j * N + k]; At[j * N + k] = t; }
-            for (int k = 0; k < n; k++) { t = Vt[i * N + k]; Vt[i * N + k] = Vt[j * N + k]; Vt[j * N + k] = t; }
-        }
-    }
-    for (int i = 0; i < n; i++) Wout[i] = W[i];
-    uint64_t rng = 0x12345678;
-    for (int i = 0; i < n; i++) {
-        sd = W[i];
-        for (int ii = 0; ii < 100 && sd <= minval; ii++) {
-            const double val0 = 1. / m;
-            for (int k = 0; k < m; k++) At[i * N + k] = (cv_rng_next(&rng) & 256) != 0 ? val0 : -val0;
-            for (int it2 = 0; it2 < 2; it2++) {
-                for (int j = 0; j < i; j++) {
-                    sd = 0;
-                    for (int k = 0; k < m; k++) sd += At[i * N + k] * At[j * N + k];
-                    double asum = 0;
-                    for (int k = 0; k < m; k++) {
-                        double t = At[i * N + k] - sd * At[j * N + k];
-                        At[i * N + k] = t;
-                        asum += fabs(t);
-                    }
-                    asum = asum > eps * 100 ? 1 / asum : 0;
-                    for (int k = 0; k < m; k++) At[i * N + k] *= asum;
-                }
-            }
-            sd = 0;
-            for (int k = 0; k < m; k++) {
-                double t = At[i * N + k];
-                sd += t * t;
-            }
-            sd = sqrt(sd);
-        }
-        s = sd > minval ? 1 / sd : 0.;
-        for (int k = 0; k < m; k++) At[i * N + k] *= s;
-    }
-}
+// OpenCV JacobiSVDImpl_<double>, cv::RNG, hypot: yavo_cvsvd.h
 
 __device__ __forceinline__ void mm3(const double* A, const double* B, double* C) {
     double R[9];

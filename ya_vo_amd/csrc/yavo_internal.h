@@ -98,6 +98,35 @@ void launch_stereo_points(const int32_t* stereo_pairs, int n_tracks, const int32
 void launch_lk_edges(int n_tracks, const double* pX, const float* next, const uint8_t* status, const int32_t* pq,
                      const int32_t* pcount, int max_kp, double* edge_X, double* edge_uv, int32_t* edge_query,
                      int32_t* edge_count, hipStream_t s);
+
+// cv::findEssentialMat (RANSAC) + cv::recoverPose (yavo_essential.hip).  Workspace of a yv_essential.
+constexpr int kEssChunk = 64;  // RANSAC iterations evaluated per round (one lane each)
+struct EssParams {
+    int max_pairs = 0, max_points = 0, max_iters = 0;
+    double* m1 = nullptr;      // [max_pairs][max_points][2] normalised points1
+    double* m2 = nullptr;      // [max_pairs][max_points][2] normalised points2
+    int32_t* idx = nullptr;    // [max_pairs][max_iters][5] getSubset draws
+    double* models = nullptr;  // [max_pairs][kEssChunk][10][9]
+    int32_t* nmod = nullptr;   // [max_pairs][kEssChunk]
+    int32_t* good = nullptr;   // [max_pairs][kEssChunk][10]
+    int32_t* state = nullptr;  // [max_pairs][8]: niters, max_good, iterations run, models, found, n, -, -
+    double* best = nullptr;    // [max_pairs][9]
+    double* cand = nullptr;    // [max_pairs][4][12] recoverPose candidates P1..P4
+    int32_t* cgood = nullptr;  // [max_pairs][4]
+};
+struct EssRun {
+    double focal, ppx, ppy, prob, threshold;
+    int max_iters;
+};
+void launch_find_essential(const EssParams& P, const EssRun& r, const float* pts1, const float* pts2,
+                           const int32_t* counts, int n_pairs, int pts_stride, double* E, uint8_t* mask,
+                           int32_t* found, int32_t* stats, hipStream_t s);
+struct Mat3 {
+    double v[9];
+};
+void launch_recover_pose(const EssParams& P, const double* E, const float* pts1, const float* pts2,
+                         const int32_t* counts, int n_pairs, int pts_stride, const Mat3& K, double* R, double* t,
+                         int32_t* good, hipStream_t s);
 void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, const double* edge_X,
                        const double* edge_uv, const double* K, const double* priors, double* poses,
                        uint8_t* edge_outlier, int32_t* inliers, hipStream_t s);
