@@ -1,0 +1,65 @@
+/*
+ * yavo_io.h -- frame I/O and formats on either side of the hot path, behind the same C ABI as
+ * yavo.h (status codes, caller-owned buffers).  Replaces the reference's:
+ *   getFilesInFolder          src/Utils.cc:31-36       directory entries sorted as boost::filesystem::path
+ *   generatePathTrain         src/LoopHandler.cc:37-57  <seq>/image_0/ (and image_1/ for stereo)
+ *   getCalibParams            src/Utils.cc:39-62       first two lines of <seq>/calib.txt -> Camera Left / Right
+ *   parseCalibString          src/Utils.cc:4-28        ' '-separated std::stod, unparsable tokens skipped
+ *   cv::imread(path, 0)       src/LoopHandler.cc:919   PNG -> 8-bit grey
+ * and adds the KITTI odometry pose writer / reader the reference lacks (needed for trajectory RMSE).
+ */
+#ifndef YAVO_IO_H
+#define YAVO_IO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "yavo.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* PNG -> 8-bit grey as cv::imread(..., IMREAD_GRAYSCALE) does through libpng: grey 1/2/4-bit expanded to 8
+ * (v * 255 / (2^d - 1)), 16-bit stripped to the high byte, alpha dropped, RGB / palette converted with libpng's
+ * rgb_to_gray(0.299, 0.587) integer path (9797 R + 19234 G + 3737 B) >> 15 (R when R == G == B; no gAMA
+ * linearisation).  Interlaced and 16-bit colour PNGs return YV_ERR_INVALID. */
+int yv_png_info(const uint8_t* data, size_t len, int* H, int* W);
+int yv_png_decode_gray(const uint8_t* data, size_t len, uint8_t* dst, int stride, int H, int W);
+/* file variant: *H / *W receive the size; the image must fit cap_h x cap_w (row stride = stride) */
+int yv_imread_gray(const char* path, uint8_t* dst, int stride, int cap_h, int cap_w, int* H, int* W);
+
+/* parseCalibString: numbers of a "Pn: v0 v1 ..." line into a row-major 4x4 (missing values 0; the reference reads
+ * past a 12-value vector).  Returns the count parsed. */
+int yv_parse_calib_string(const char* line, double out[16]);
+
+/* A KITTI odometry sequence directory (basePath + sequence, src/LoopHandler.cc:12-24). */
+typedef struct yv_seq yv_seq;
+/* stereo != 0 also lists image_1/.  Fails (YV_ERR_INVALID) when image_0/ is missing or empty. */
+int yv_seq_open(const char* sequence_dir, int stereo, yv_seq** out);
+void yv_seq_close(yv_seq* seq);
+int yv_seq_frames(const yv_seq* seq);
+/* the path of frame i (side 0 = image_0, 1 = image_1); returns its length, or an error when cap is too small */
+int yv_seq_path(const yv_seq* seq, int frame, int side, char* buf, int cap);
+/* getCalibParams: P0 / P1 (4x4, row-major) and their top-left 3x3 K (Camera::K); YV_ERR_INVALID without calib.txt */
+int yv_seq_calib(const yv_seq* seq, double P0[16], double P1[16], double K0[9], double K1[9]);
+/* size of frame 0 of image_0 */
+int yv_seq_size(const yv_seq* seq, int* H, int* W);
+/* decode frames [first, first + n) into host memory, images of pitch bytes, rows of W bytes; stereo sequences
+ * store left, right per frame (2n images).  threads <= 0 picks the host's hardware concurrency (at most 64). */
+int yv_seq_read(yv_seq* seq, int first, int n, uint8_t* dst, int64_t pitch, int threads);
+/* the same decode into the sequence's pinned staging (two slots, reused once their copy completed) followed by an
+ * async copy to d_dst on stream (NULL: the context stream of ctx) -- PCIe overlapped with the caller's kernels */
+int yv_seq_upload(yv_seq* seq, struct yv_ctx* ctx, int first, int n, uint8_t* d_dst, int64_t pitch, int threads,
+                  void* stream);
+
+/* KITTI odometry poses: one line per frame, the 12 row-major numbers of the 3x4 [R | t] of T_wc = T_cw^-1, for
+ * poses given as Sophus SE3d::data() of T_cw ({qx, qy, qz, qw, tx, ty, tz}, yavo_geom.h). */
+int yv_write_kitti_poses(const char* path, const double* poses, int n);
+/* reads up to cap lines of 12 numbers (the same 3x4 layout) into out [cap][12] */
+int yv_read_kitti_poses(const char* path, double* out, int cap, int* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YAVO_IO_H */

@@ -12,7 +12,8 @@ import pytest
 import ya_vo_amd as yv
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", "yavo", h) for h in ("yavo.h", "yavo_types.h", "yavo_geom.h")]
+HEADERS = [os.path.join(ROOT, "include", "yavo", h) for h in ("yavo.h", "yavo_types.h", "yavo_geom.h",
+                                                                       "yavo_io.h")]
 
 
 def _declared_functions():
@@ -38,7 +39,8 @@ def test_every_declared_symbol_is_exported(lib):
     assert len(declared) >= 20
     for name in sorted(declared):
         assert hasattr(lib, name), f"{name} declared in include/yavo but not exported"
-        assert name in yv.SIGNATURES or name in getattr(yv, "GEOM_SIGNATURES", {}), f"{name} has no ctypes binding"
+        assert name in yv.SIGNATURES or name in yv.GEOM_SIGNATURES or name in yv.IO_SIGNATURES, \
+            f"{name} has no ctypes binding"
 
 
 def test_abi_version_and_status_strings(lib):

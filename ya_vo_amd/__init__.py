@@ -115,6 +115,24 @@ GEOM_SIGNATURES = {
     "yv_recover_pose": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, ctypes.POINTER(_I)]),
 }
 
+# include/yavo/yavo_io.h (frame I/O and formats; ya_vo_amd/io.py wraps them)
+IO_SIGNATURES = {
+    "yv_png_info": (_I, [_P, ctypes.c_size_t, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "yv_png_decode_gray": (_I, [_P, ctypes.c_size_t, _P, _I, _I, _I]),
+    "yv_imread_gray": (_I, [ctypes.c_char_p, _P, _I, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "yv_parse_calib_string": (_I, [ctypes.c_char_p, _P]),
+    "yv_seq_open": (_I, [ctypes.c_char_p, _I, ctypes.POINTER(_P)]),
+    "yv_seq_close": (None, [_P]),
+    "yv_seq_frames": (_I, [_P]),
+    "yv_seq_path": (_I, [_P, _I, _I, ctypes.c_char_p, _I]),
+    "yv_seq_calib": (_I, [_P, _P, _P, _P, _P]),
+    "yv_seq_size": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "yv_seq_read": (_I, [_P, _I, _I, _P, ctypes.c_int64, _I]),
+    "yv_seq_upload": (_I, [_P, _P, _I, _I, _P, ctypes.c_int64, _I, _P]),
+    "yv_write_kitti_poses": (_I, [ctypes.c_char_p, _P, _I]),
+    "yv_read_kitti_poses": (_I, [ctypes.c_char_p, _P, _I, ctypes.POINTER(_I)]),
+}
+
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     """Load libyavo.so (built by __graft_entry__.build()).  Raises if it is missing: no fallback."""
@@ -133,7 +151,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         except ImportError:
             pass
     lib = ctypes.CDLL(path)
-    for name, (res, args) in list(SIGNATURES.items()) + list(GEOM_SIGNATURES.items()):
+    for name, (res, args) in list(SIGNATURES.items()) + list(GEOM_SIGNATURES.items()) + list(IO_SIGNATURES.items()):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -28,6 +28,11 @@ struct yv_ctx {
     size_t scratch_cap = 0;
 };
 
+namespace yavo {
+int ctx_device(yv_ctx* ctx) { return ctx->device; }
+hipStream_t ctx_stream(yv_ctx* ctx) { return ctx->stream; }
+}  // namespace yavo
+
 struct yv_batch {
     yv_ctx* ctx = nullptr;
     int max_images = 0, H = 0, W = 0, max_kp = 0, max_pairs = 0, n_pairs = 0;

@@ -6,6 +6,8 @@
 
 #include "../../include/yavo/yavo_types.h"
 
+struct yv_ctx;
+
 namespace yavo {
 
 constexpr int kMaxKp = 4096;
@@ -124,6 +126,9 @@ void launch_find_essential(const EssParams& P, const EssRun& r, const float* pts
 struct Mat3 {
     double v[9];
 };
+// the context's device / stream for the host-side modules (yavo_io.hip); defined in yavo_api.hip
+int ctx_device(struct ::yv_ctx* ctx);
+hipStream_t ctx_stream(struct ::yv_ctx* ctx);
 void launch_recover_pose(const EssParams& P, const double* E, const float* pts1, const float* pts2,
                          const int32_t* counts, int n_pairs, int pts_stride, const Mat3& K, double* R, double* t,
                          int32_t* good, hipStream_t s);

@@ -1,0 +1,492 @@
+// yavo_io.hip -- host side of frame I/O (include/yavo/yavo_io.h): PNG -> 8-bit grey on zlib,
+// the sorted KITTI image listing, calib.txt, the KITTI pose format, and a threaded decoder feeding pinned staging
+// whose copies to HBM run asynchronously on the caller's stream.  Host code only (no kernels).
+#include <hip/hip_runtime.h>
+#include <dirent.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/yavo/yavo_io.h"
+#include "yavo_internal.h"
+
+namespace {
+
+uint32_t be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+
+struct PngHeader {
+    int W = 0, H = 0, depth = 0, ctype = 0, interlace = 0;
+};
+
+// chunk walk: IHDR, PLTE, the concatenated IDAT stream; stops at IEND
+int png_parse(const uint8_t* d, size_t len, PngHeader& h, std::vector<uint8_t>* idat, std::vector<uint8_t>* plte) {
+    static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+    if (!d || len < 8 + 25 || std::memcmp(d, sig, 8) != 0) return YV_ERR_INVALID;
+    size_t off = 8;
+    bool have_ihdr = false;
+    while (off + 12 <= len) {
+        const uint32_t n = be32(d + off);
+        const uint8_t* type = d + off + 4;
+        const uint8_t* body = d + off + 8;
+        if (n > len - off - 12) return YV_ERR_INVALID;
+        if (!std::memcmp(type, "IHDR", 4)) {
+            if (n != 13) return YV_ERR_INVALID;
+            h.W = (int)be32(body);
+            h.H = (int)be32(body + 4);
+            h.depth = body[8];
+            h.ctype = body[9];
+            if (body[10] != 0 || body[11] != 0) return YV_ERR_INVALID;  // compression / filter method
+            h.interlace = body[12];
+            have_ihdr = true;
+            if (!idat && !plte) return YV_OK;
+        } else if (!std::memcmp(type, "PLTE", 4)) {
+            if (plte) plte->assign(body, body + n);
+        } else if (!std::memcmp(type, "IDAT", 4)) {
+            if (idat) idat->insert(idat->end(), body, body + n);
+        } else if (!std::memcmp(type, "IEND", 4)) {
+            break;
+        }
+        off += 12 + n;
+    }
+    return have_ihdr ? YV_OK : YV_ERR_INVALID;
+}
+
+int png_channels(int ctype) {
+    switch (ctype) {
+        case 0: return 1;
+        case 2: return 3;
+        case 3: return 1;
+        case 4: return 2;
+        case 6: return 4;
+        default: return 0;
+    }
+}
+
+bool png_supported(const PngHeader& h) {
+    if (h.W <= 0 || h.H <= 0 || (int64_t)h.W * h.H > (1ll << 30) || h.interlace != 0) return false;
+    switch (h.ctype) {
+        case 0: return h.depth == 1 || h.depth == 2 || h.depth == 4 || h.depth == 8 || h.depth == 16;
+        case 3: return h.depth == 1 || h.depth == 2 || h.depth == 4 || h.depth == 8;
+        case 4: return h.depth == 8 || h.depth == 16;
+        case 2:
+        case 6: return h.depth == 8;
+        default: return false;
+    }
+}
+
+// libpng png_do_rgb_to_gray, 8-bit, no gamma table: coefficients (29900, 58700) / 100000 * 32768 truncated
+inline uint8_t rgb_to_gray(uint32_t r, uint32_t g, uint32_t b) {
+    constexpr uint32_t rc = 9797, gc = 19234, bc = 32768 - rc - gc;
+    if (r == g && r == b) return (uint8_t)r;
+    return (uint8_t)((rc * r + gc * g + bc * b) >> 15);
+}
+
+uint8_t paeth(int a, int b, int c) {
+    const int p = a + b - c, pa = std::abs(p - a), pb = std::abs(p - b), pc = std::abs(p - c);
+    if (pa <= pb && pa <= pc) return (uint8_t)a;
+    if (pb <= pc) return (uint8_t)b;
+    return (uint8_t)c;
+}
+
+int png_decode(const uint8_t* data, size_t len, uint8_t* dst, int stride, int H, int W) {
+    PngHeader h;
+    std::vector<uint8_t> idat, plte;
+    if (png_parse(data, len, h, &idat, &plte) != YV_OK) return YV_ERR_INVALID;
+    if (!png_supported(h) || h.H != H || h.W != W || stride < W) return YV_ERR_INVALID;
+    const int ch = png_channels(h.ctype);
+    const size_t bits = (size_t)ch * h.depth;
+    const size_t rowb = ((size_t)W * bits + 7) / 8;
+    const size_t fbpp = std::max<size_t>(1, bits / 8);
+    std::vector<uint8_t> raw((rowb + 1) * (size_t)H);
+    z_stream zs;
+    std::memset(&zs, 0, sizeof zs);
+    if (inflateInit(&zs) != Z_OK) return YV_ERR_INVALID;
+    zs.next_in = idat.data();
+    zs.avail_in = (uInt)idat.size();
+    zs.next_out = raw.data();
+    zs.avail_out = (uInt)raw.size();
+    const int zr = inflate(&zs, Z_FINISH);
+    const size_t produced = raw.size() - zs.avail_out;
+    inflateEnd(&zs);
+    if ((zr != Z_STREAM_END && zr != Z_BUF_ERROR && zr != Z_OK) || produced != raw.size()) return YV_ERR_INVALID;
+    // unfilter in place: row y = raw[y (rowb + 1) + 1 ..], filter byte first
+    for (int y = 0; y < H; ++y) {
+        uint8_t* row = raw.data() + (size_t)y * (rowb + 1);
+        const uint8_t f = row[0];
+        uint8_t* cur = row + 1;
+        const uint8_t* prev = y ? raw.data() + (size_t)(y - 1) * (rowb + 1) + 1 : nullptr;
+        switch (f) {
+            case 0: break;
+            case 1:
+                for (size_t i = fbpp; i < rowb; ++i) cur[i] = (uint8_t)(cur[i] + cur[i - fbpp]);
+                break;
+            case 2:
+                if (prev)
+                    for (size_t i = 0; i < rowb; ++i) cur[i] = (uint8_t)(cur[i] + prev[i]);
+                break;
+            case 3:
+                for (size_t i = 0; i < rowb; ++i) {
+                    const int a = i >= fbpp ? cur[i - fbpp] : 0, b = prev ? prev[i] : 0;
+                    cur[i] = (uint8_t)(cur[i] + ((a + b) >> 1));
+                }
+                break;
+            case 4:
+                for (size_t i = 0; i < rowb; ++i) {
+                    const int a = i >= fbpp ? cur[i - fbpp] : 0, b = prev ? prev[i] : 0;
+                    const int c = (prev && i >= fbpp) ? prev[i - fbpp] : 0;
+                    cur[i] = (uint8_t)(cur[i] + paeth(a, b, c));
+                }
+                break;
+            default: return YV_ERR_INVALID;
+        }
+    }
+    for (int y = 0; y < H; ++y) {
+        const uint8_t* s = raw.data() + (size_t)y * (rowb + 1) + 1;
+        uint8_t* o = dst + (size_t)y * stride;
+        if (h.ctype == 0 && h.depth == 8) {
+            std::memcpy(o, s, (size_t)W);
+        } else if (h.ctype == 0 && h.depth == 16) {
+            for (int x = 0; x < W; ++x) o[x] = s[2 * x];  // png_set_strip_16: the high byte
+        } else if (h.ctype == 0 || h.ctype == 3) {
+            const int d = h.depth, per = 8 / std::min(d, 8);
+            for (int x = 0; x < W; ++x) {
+                uint32_t v;
+                if (d == 8) {
+                    v = s[x];
+                } else {
+                    const int byte = x / per, shift = 8 - d * (x % per + 1);
+                    v = (s[byte] >> shift) & ((1u << d) - 1);
+                }
+                if (h.ctype == 0) {
+                    o[x] = (uint8_t)(d == 8 ? v : v * 255 / ((1u << d) - 1));  // expand_gray_1_2_4_to_8
+                } else {
+                    if (3 * v + 2 >= plte.size()) return YV_ERR_INVALID;
+                    o[x] = rgb_to_gray(plte[3 * v], plte[3 * v + 1], plte[3 * v + 2]);
+                }
+            }
+        } else if (h.ctype == 4) {
+            const int step = h.depth == 16 ? 4 : 2;
+            for (int x = 0; x < W; ++x) o[x] = s[step * x];  // grey (high byte), alpha dropped
+        } else {  // 2 / 6, 8-bit
+            for (int x = 0; x < W; ++x) {
+                const uint8_t* p = s + (size_t)ch * x;
+                o[x] = rgb_to_gray(p[0], p[1], p[2]);
+            }
+        }
+    }
+    return YV_OK;
+}
+
+bool read_file(const std::string& path, std::vector<uint8_t>& out) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    out.clear();
+    uint8_t buf[1 << 16];
+    size_t n;
+    while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) out.insert(out.end(), buf, buf + n);
+    const bool ok = !std::ferror(f);
+    std::fclose(f);
+    return ok;
+}
+
+// getFilesInFolder: every entry of the directory ('.' and '..' excluded), sorted as paths of one directory compare
+bool list_sorted(const std::string& dir, std::vector<std::string>& out) {
+    DIR* d = opendir(dir.c_str());
+    if (!d) return false;
+    std::vector<std::string> names;
+    while (dirent* e = readdir(d)) {
+        if (!std::strcmp(e->d_name, ".") || !std::strcmp(e->d_name, "..")) continue;
+        names.emplace_back(e->d_name);
+    }
+    closedir(d);
+    std::sort(names.begin(), names.end());
+    std::string base = dir;
+    if (!base.empty() && base.back() != '/') base += '/';
+    out.clear();
+    for (auto& n : names) out.push_back(base + n);
+    return true;
+}
+
+// parseCalibString: split on ' ', std::stod each token (leading blanks allowed, trailing text ignored), skip failures
+int parse_calib(const char* line, double out[16]) {
+    std::vector<double> v;
+    const std::string s(line ? line : "");
+    size_t pos = 0;
+    while (pos <= s.size()) {
+        size_t next = s.find(' ', pos);
+        if (next == std::string::npos) next = s.size();
+        const std::string tok = s.substr(pos, next - pos);
+        if (!tok.empty()) {
+            const char* c = tok.c_str();
+            char* end = nullptr;
+            errno = 0;
+            const double d = std::strtod(c, &end);
+            if (end != c && errno != ERANGE) v.push_back(d);
+        }
+        pos = next + 1;
+        if (next == s.size()) break;
+    }
+    for (int i = 0; i < 16; ++i) out[i] = i < (int)v.size() ? v[i] : 0.0;
+    return (int)v.size();
+}
+
+// Eigen::Quaterniond::toRotationMatrix
+void quat_to_R(const double* q, double* R) {
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz; R[2] = txz + twy;
+    R[3] = txy + twz; R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy; R[7] = tyz + twx; R[8] = 1 - (txx + tyy);
+}
+
+}  // namespace
+
+struct yv_seq {
+    std::string dir;
+    bool stereo = false;
+    std::vector<std::string> left, right;
+    int H = 0, W = 0;
+    // pinned staging for yv_seq_upload: two slots, each reused after its copy completed
+    uint8_t* stage[2] = {nullptr, nullptr};
+    size_t stage_cap[2] = {0, 0};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    bool pending[2] = {false, false};
+    int next = 0;
+};
+
+namespace {
+
+int decode_frames(yv_seq* s, int first, int n, uint8_t* dst, int64_t pitch, int threads) {
+    const int per = s->stereo ? 2 : 1;
+    const int total = n * per;
+    if (threads <= 0) threads = (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 64u);
+    threads = std::max(1, std::min(threads, total));
+    std::atomic<int> next{0}, status{YV_OK};
+    auto work = [&]() {
+        std::vector<uint8_t> file;
+        for (int k; (k = next.fetch_add(1)) < total;) {
+            const int frame = first + k / per, side = k % per;
+            const std::string& path = side ? s->right[frame] : s->left[frame];
+            if (!read_file(path, file)) {
+                status = YV_ERR_INVALID;
+                continue;
+            }
+            if (png_decode(file.data(), file.size(), dst + (int64_t)k * pitch, s->W, s->H, s->W) != YV_OK)
+                status = YV_ERR_INVALID;
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    return status.load();
+}
+
+}  // namespace
+
+extern "C" {
+
+int yv_png_info(const uint8_t* data, size_t len, int* H, int* W) {
+    if (!H || !W) return YV_ERR_INVALID;
+    PngHeader h;
+    if (png_parse(data, len, h, nullptr, nullptr) != YV_OK || !png_supported(h)) return YV_ERR_INVALID;
+    *H = h.H;
+    *W = h.W;
+    return YV_OK;
+}
+
+int yv_png_decode_gray(const uint8_t* data, size_t len, uint8_t* dst, int stride, int H, int W) {
+    if (!data || !dst) return YV_ERR_INVALID;
+    return png_decode(data, len, dst, stride, H, W);
+}
+
+int yv_imread_gray(const char* path, uint8_t* dst, int stride, int cap_h, int cap_w, int* H, int* W) {
+    if (!path || !dst || !H || !W) return YV_ERR_INVALID;
+    std::vector<uint8_t> file;
+    if (!read_file(path, file)) return YV_ERR_INVALID;
+    int h = 0, w = 0;
+    if (yv_png_info(file.data(), file.size(), &h, &w) != YV_OK) return YV_ERR_INVALID;
+    *H = h;
+    *W = w;
+    if (h > cap_h || w > cap_w || stride < w) return YV_ERR_CAPACITY;
+    return png_decode(file.data(), file.size(), dst, stride, h, w);
+}
+
+int yv_parse_calib_string(const char* line, double out[16]) {
+    if (!line || !out) return YV_ERR_INVALID;
+    return parse_calib(line, out);
+}
+
+int yv_seq_open(const char* sequence_dir, int stereo, yv_seq** out) {
+    if (!sequence_dir || !out) return YV_ERR_INVALID;
+    *out = nullptr;
+    yv_seq* s = new (std::nothrow) yv_seq();
+    if (!s) return YV_ERR_INVALID;
+    s->dir = sequence_dir;
+    if (!s->dir.empty() && s->dir.back() != '/') s->dir += '/';
+    s->stereo = stereo != 0;
+    if (!list_sorted(s->dir + "image_0/", s->left) || s->left.empty() ||
+        (s->stereo && (!list_sorted(s->dir + "image_1/", s->right) || s->right.size() < s->left.size()))) {
+        delete s;
+        return YV_ERR_INVALID;
+    }
+    std::vector<uint8_t> file;
+    if (!read_file(s->left[0], file) || yv_png_info(file.data(), file.size(), &s->H, &s->W) != YV_OK) {
+        delete s;
+        return YV_ERR_INVALID;
+    }
+    *out = s;
+    return YV_OK;
+}
+
+void yv_seq_close(yv_seq* s) {
+    if (!s) return;
+    for (int k = 0; k < 2; ++k) {
+        if (s->done[k]) {
+            (void)hipEventSynchronize(s->done[k]);
+            (void)hipEventDestroy(s->done[k]);
+        }
+        if (s->stage[k]) (void)hipHostFree(s->stage[k]);
+    }
+    delete s;
+}
+
+int yv_seq_frames(const yv_seq* s) { return s ? (int)s->left.size() : YV_ERR_INVALID; }
+
+int yv_seq_path(const yv_seq* s, int frame, int side, char* buf, int cap) {
+    if (!s || !buf || frame < 0 || frame >= (int)s->left.size() || side < 0 || side > (s->stereo ? 1 : 0))
+        return YV_ERR_INVALID;
+    const std::string& p = side ? s->right[frame] : s->left[frame];
+    if ((int)p.size() + 1 > cap) return YV_ERR_CAPACITY;
+    std::memcpy(buf, p.c_str(), p.size() + 1);
+    return (int)p.size();
+}
+
+int yv_seq_calib(const yv_seq* s, double P0[16], double P1[16], double K0[9], double K1[9]) {
+    if (!s) return YV_ERR_INVALID;
+    FILE* f = std::fopen((s->dir + "calib.txt").c_str(), "r");
+    if (!f) return YV_ERR_INVALID;
+    double P[2][16];
+    for (int i = 0; i < 2; ++i) {
+        std::string line;
+        int c;
+        while ((c = std::fgetc(f)) != EOF && c != '\n') line.push_back((char)c);
+        parse_calib(line.c_str(), P[i]);
+    }
+    std::fclose(f);
+    for (int i = 0; i < 16; ++i) {
+        if (P0) P0[i] = P[0][i];
+        if (P1) P1[i] = P[1][i];
+    }
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {  // Camera::K = fullMatrix(Range(0, 3), Range(0, 3))
+            if (K0) K0[r * 3 + c] = P[0][r * 4 + c];
+            if (K1) K1[r * 3 + c] = P[1][r * 4 + c];
+        }
+    return YV_OK;
+}
+
+int yv_seq_size(const yv_seq* s, int* H, int* W) {
+    if (!s || !H || !W) return YV_ERR_INVALID;
+    *H = s->H;
+    *W = s->W;
+    return YV_OK;
+}
+
+int yv_seq_read(yv_seq* s, int first, int n, uint8_t* dst, int64_t pitch, int threads) {
+    if (!s || !dst || first < 0 || n < 0 || first + n > (int)s->left.size() || pitch < (int64_t)s->H * s->W)
+        return YV_ERR_INVALID;
+    if (n == 0) return YV_OK;
+    return decode_frames(s, first, n, dst, pitch, threads);
+}
+
+int yv_seq_upload(yv_seq* s, yv_ctx* ctx, int first, int n, uint8_t* d_dst, int64_t pitch, int threads,
+                  void* stream) {
+    if (!s || !ctx || !d_dst || first < 0 || n < 0 || first + n > (int)s->left.size() ||
+        pitch < (int64_t)s->H * s->W)
+        return YV_ERR_INVALID;
+    if (n == 0) return YV_OK;
+    if (hipSetDevice(yavo::ctx_device(ctx)) != hipSuccess) return YV_ERR_HIP;
+    const int k = s->next;
+    s->next ^= 1;
+    if (s->pending[k] && hipEventSynchronize(s->done[k]) != hipSuccess) return YV_ERR_HIP;
+    s->pending[k] = false;
+    const size_t bytes = (size_t)pitch * n * (s->stereo ? 2 : 1);
+    if (bytes > s->stage_cap[k]) {
+        if (s->stage[k]) (void)hipHostFree(s->stage[k]);
+        s->stage[k] = nullptr;
+        s->stage_cap[k] = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&s->stage[k]), bytes) != hipSuccess) return YV_ERR_HIP;
+        s->stage_cap[k] = bytes;
+    }
+    if (!s->done[k] && hipEventCreateWithFlags(&s->done[k], hipEventDisableTiming) != hipSuccess) return YV_ERR_HIP;
+    const int rc = decode_frames(s, first, n, s->stage[k], pitch, threads);
+    if (rc != YV_OK) return rc;
+    hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : yavo::ctx_stream(ctx);
+    if (hipMemcpyAsync(d_dst, s->stage[k], bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipEventRecord(s->done[k], st) != hipSuccess)
+        return YV_ERR_HIP;
+    s->pending[k] = true;
+    return YV_OK;
+}
+
+int yv_write_kitti_poses(const char* path, const double* poses, int n) {
+    if (!path || n < 0 || (n > 0 && !poses)) return YV_ERR_INVALID;
+    FILE* f = std::fopen(path, "w");
+    if (!f) return YV_ERR_INVALID;
+    for (int i = 0; i < n; ++i) {
+        const double* p = poses + 7 * (size_t)i;
+        double R[9];
+        quat_to_R(p, R);
+        // T_wc = T_cw^-1: R^T, -R^T t
+        double M[12];
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) M[r * 4 + c] = R[c * 3 + r];
+            M[r * 4 + 3] = -(R[0 * 3 + r] * p[4] + R[1 * 3 + r] * p[5] + R[2 * 3 + r] * p[6]);
+        }
+        for (int q = 0; q < 12; ++q) std::fprintf(f, q ? " %.12e" : "%.12e", M[q]);
+        std::fputc('\n', f);
+    }
+    const bool ok = !std::ferror(f);
+    return std::fclose(f) == 0 && ok ? YV_OK : YV_ERR_INVALID;
+}
+
+int yv_read_kitti_poses(const char* path, double* out, int cap, int* n) {
+    if (!path || !n || cap < 0 || (cap > 0 && !out)) return YV_ERR_INVALID;
+    FILE* f = std::fopen(path, "r");
+    if (!f) return YV_ERR_INVALID;
+    int cnt = 0;
+    double v[12];
+    while (cnt < cap) {
+        int got = 0;
+        for (; got < 12; ++got)
+            if (std::fscanf(f, "%lf", &v[got]) != 1) break;
+        if (got == 0) break;
+        if (got != 12) {
+            std::fclose(f);
+            return YV_ERR_INVALID;
+        }
+        for (int q = 0; q < 12; ++q) out[12 * (size_t)cnt + q] = v[q];
+        ++cnt;
+    }
+    std::fclose(f);
+    *n = cnt;
+    return YV_OK;
+}
+
+}  // extern "C"
