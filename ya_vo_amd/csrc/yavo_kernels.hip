@@ -930,32 +930,41 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
         const bool more = t0 + MM_TC < nt;
         if (more) fetch(t0 + MM_TC);
         __syncthreads();
+        // two 16-column train tiles per pass: four independent MFMA chains, and one v_max3 folds both tiles' keys
+        // into the running maximum (1.5 VALU per distance)
 #pragma unroll
-        for (int tt0 = 0; tt0 < MM_TC; tt0 += 16) {
-            const int j = t0 + tt0 + col;
+        for (int tt0 = 0; tt0 < MM_TC; tt0 += 32) {
             if (t0 + tt0 >= nt) break;
-            mm_v4i B[4];
+            mm_v4i Ba[4], Bb[4];
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const uint4 v = s_t[buf][(tt0 + col) * MM_ROW + 4 * s + g];
-                B[s] = mm_v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+                const uint4 va = s_t[buf][(tt0 + col) * MM_ROW + 4 * s + g];
+                const uint4 vb = s_t[buf][(tt0 + 16 + col) * MM_ROW + 4 * s + g];
+                Ba[s] = mm_v4i{(int)va.x, (int)va.y, (int)va.z, (int)va.w};
+                Bb[s] = mm_v4i{(int)vb.x, (int)vb.y, (int)vb.z, (int)vb.w};
             }
-            // key = (dot << 16) + bias: bias = 0xFFFF - j for a real train column; a column past nt gets
-            // -2^30, below every real key (>= -2^24) and above INT_MIN, so no per-element select is needed
-            const int bias = j < nt ? 0xFFFF - j : -(1 << 30);
-            // two query tiles' K-chains interleaved: every MFMA has an independent one beside it
+            // key = (dot << 16) + bias: bias = 0xFFFF - j for a real train column; a column past nt (including the
+            // whole second tile at the end of the list) gets -2^30, below every real key (>= -2^24) and above
+            // INT_MIN, so no per-element select and no branch are needed
+            const int ja = t0 + tt0 + col, jb = ja + 16;
+            const int bias_a = ja < nt ? 0xFFFF - ja : -(1 << 30);
+            const int bias_b = jb < nt ? 0xFFFF - jb : -(1 << 30);
 #pragma unroll
             for (int qt = 0; qt < MM_QT; qt += 2) {
-                mm_v4i acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+                mm_v4i a0 = {0, 0, 0, 0}, b0 = {0, 0, 0, 0}, a1 = {0, 0, 0, 0}, b1 = {0, 0, 0, 0};
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
-                    acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], B[s], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][s], B[s], acc1, 0, 0, 0);
+                    a0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], Ba[s], a0, 0, 0, 0);
+                    b0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], Bb[s], b0, 0, 0, 0);
+                    a1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][s], Ba[s], a1, 0, 0, 0);
+                    b1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][s], Bb[s], b1, 0, 0, 0);
                 }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    best[qt][r] = max(best[qt][r], (int)(((uint32_t)acc0[r] << 16) + (uint32_t)bias));
-                    best[qt + 1][r] = max(best[qt + 1][r], (int)(((uint32_t)acc1[r] << 16) + (uint32_t)bias));
+                    best[qt][r] = max(best[qt][r], max((int)(((uint32_t)a0[r] << 16) + (uint32_t)bias_a),
+                                                       (int)(((uint32_t)b0[r] << 16) + (uint32_t)bias_b)));
+                    best[qt + 1][r] = max(best[qt + 1][r], max((int)(((uint32_t)a1[r] << 16) + (uint32_t)bias_a),
+                                                               (int)(((uint32_t)b1[r] << 16) + (uint32_t)bias_b)));
                 }
             }
         }
