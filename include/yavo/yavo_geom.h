@@ -120,6 +120,25 @@ int yv_find_essential(struct yv_ctx* ctx, const float* pts1, const float* pts2, 
 int yv_recover_pose(struct yv_ctx* ctx, const double E[9], const float* pts1, const float* pts2, int n,
                     const double K[9], double R[9], double t[3], int* good);
 
+/* ---- sliding-window bundle adjustment (BASELINE.json config 5) ----
+ * The reference's Optimizer (src/Optimizer.cc:17-60 partialBA, include/Optimizer.hpp:64-126 edge / vertex) widened
+ * to a keyframe window: poses (VertexPose, T_cw, SE3d::data()) and landmarks (3-vectors) joined by projection edges
+ * e = meas - (K (T X)).xy / z with the reference's pose Jacobian, solved by g2o's Levenberg-Marquardt over
+ * BlockSolver_6_3 (Schur complement on the landmarks, dense LDLT on the poses).  The first n_fixed poses are held
+ * fixed.  Restated in oracle/yavo_oracle_ba.c (or_ba_lm); results are bit-identical to it. */
+typedef struct yv_ba yv_ba;
+int yv_ba_create(struct yv_ctx* ctx, int max_poses, int max_landmarks, int max_edges, yv_ba** out);
+void yv_ba_destroy(yv_ba* ba);
+/* The graph: edge e joins pose edge_pose[e] and landmark edge_landmark[e] with measurement meas[e][2] (pixels, x
+ * along K's first row); K row-major.  Host arrays, copied; the block structure (edges per pose / landmark, landmarks
+ * shared by each pose pair) is built here, once per graph, as g2o's initializeOptimization does. */
+int yv_ba_set_problem(yv_ba* ba, int n_poses, int n_fixed, int n_landmarks, const int32_t* edge_pose,
+                      const int32_t* edge_landmark, const double* meas, int n_edges, const double K[9]);
+/* optimize(max_iters) from poses [n_poses][7] / landmarks [n_landmarks][3] (host, in / out).  chi2_log
+ * [max_iters + 1] (may be NULL): chi2 before the first iteration and after each; *iters = iterations run (may be
+ * NULL; an iteration whose 10 damping trials all fail ends the run). */
+int yv_ba_solve(yv_ba* ba, double* poses, double* landmarks, int max_iters, double* chi2_log, int* iters);
+
 #ifdef __cplusplus
 }
 #endif

@@ -149,6 +149,15 @@ void or_decompose_essential(const double E[9], double R1[9], double R2[9], doubl
 int or_recover_pose(const double E[9], const double* pts1, const double* pts2, int n, const double K[9], double R[9],
                     double t[3], int good[4]);
 
+/* ---- sliding-window bundle adjustment (BASELINE config 5; yavo_oracle_ba.c) ---- */
+/* Eigen LDLT (dynamic, g2o LinearSolverDense) on a symmetric n x n; returns isPositive */
+int or_ldlt_solve(const double* H, int n, const double* b, double* x);
+/* g2o LM + BlockSolver_6_3 (Schur) over P poses (first n_fixed fixed) and L landmarks with E pose-landmark
+ * edges (pose ep[e], landmark el[e], measurement meas[e][2] in the reference's (row, col) convention).
+ * poses [P][7] / X [L][3] in / out; chi2_log [max_iters + 1] optional.  Returns the iterations run. */
+int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t* ep, const int32_t* el,
+             const double* meas, int E, const double* K, int max_iters, double* chi2_log);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,425 @@
+/*
+ * yavo_oracle_ba.c -- CPU restatement of the sliding-window bundle adjustment of BASELINE.json config 5 / SURVEY.md
+ * 8d-8e (20 keyframe poses, ~10k landmarks, ~5 observations each).  TEST INFRASTRUCTURE ONLY (see yavo_oracle.h).
+ *
+ * The reference has no multi-pose BA: Optimizer::partialBA (src/Optimizer.cc:17-60) is a pose-only Gauss-Newton
+ * stub and src/test.cc:318-360 is pose-only too.  What it does have is the machinery such a BA is built from, and
+ * this restates that machinery:
+ *   edge            the reference's projection edge (include/Optimizer.hpp:64-126): e = meas - (K (T X)).xy / z,
+ *                   J_pose = its linearizeOplus (2 x 6, (rho, phi), no cx / cy); the landmark half of a binary
+ *                   pose-landmark edge is J_point = J_pose[:, 0:3] R (g2o EdgeProjectXYZ2UV's form)
+ *   vertices        VertexPose::oplusImpl T <- exp(dx) T (Optimizer.hpp:51-57); landmark X <- X + dx; the first
+ *                   n_fixed poses are fixed (gauge)
+ *   solver          g2o OptimizationAlgorithmLevenberg (as or_pose_lm: lambda init tau = 1e-5 times the largest
+ *                   Hessian diagonal, up to 10 trials, rho / scale with scale = x.(lambda x + b) + 1e-3, good-step
+ *                   factor max(1/3, min(2/3, 1 - (2 rho - 1)^3)), bad step lambda *= ni, ni *= 2) over
+ *                   BlockSolver_6_3: H_pp (block diagonal: no pose-pose edges), H_ll (3 x 3 per landmark), H_pl
+ *                   (6 x 3 per edge); lambda on every diagonal; Schur complement with explicit 3 x 3 inverses;
+ *                   LinearSolverDense = Eigen LDLT (unblocked, diagonal pivoting) on the reduced pose system;
+ *                   landmark back-substitution
+ * Summation orders (the GPU kernels, yavo_ba.hip, follow them bit for bit; g2o's own orders are not exposed, so
+ * parity with a g2o build is unpinned):
+ *   tree256   values indexed k = 0 .. n-1: partial[t] = sum of items k = t mod 256 in ascending k (from 0.0), then
+ *             p[t] += p[t + off], off = 128 .. 1; used for each pose's H_pp / b_p over its edges (edge order), for
+ *             chi2 over all edges and for the LM scale over all variables (poses, then landmarks)
+ *   sequential per landmark over its edges (edge order) for H_ll / b_l and the back-substitution; per Schur block
+ *             entry over the landmarks the two poses share (ascending); per pose for b_schur over its edges
+ */
+#include "yavo_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define BA_NT 256
+
+typedef struct {
+    double part[BA_NT];
+} tree256;
+static void t_reset(tree256* t) { memset(t->part, 0, sizeof t->part); }
+static void t_add(tree256* t, int k, double v) { t->part[k % BA_NT] = t->part[k % BA_NT] + v; }
+static double t_total(const tree256* t) {
+    double p[BA_NT];
+    memcpy(p, t->part, sizeof p);
+    for (int off = BA_NT / 2; off > 0; off >>= 1)
+        for (int i = 0; i < off; ++i) p[i] = p[i] + p[i + off];
+    return p[0];
+}
+
+/* e = meas - (K (T X)).xy / z  (or_se3_act = Sophus T * X) */
+static void ba_error(const double* T, const double* K, const double* X, const double* meas, double* e) {
+    double pc[3];
+    or_se3_act(T, X, pc);
+    const double u0 = K[0] * pc[0] + K[1] * pc[1] + K[2] * pc[2];
+    const double u1 = K[3] * pc[0] + K[4] * pc[1] + K[5] * pc[2];
+    const double u2 = K[6] * pc[0] + K[7] * pc[1] + K[8] * pc[2];
+    e[0] = meas[0] - u0 / u2;
+    e[1] = meas[1] - u1 / u2;
+}
+
+/* J_pose (2 x 6, the reference's linearizeOplus) and J_point = J_pose[:, 0:3] R (2 x 3) */
+static void ba_jacobians(const double* T, const double* K, const double* X, double* Jp, double* Jl) {
+    double pc[3], R[9];
+    or_se3_act(T, X, pc);
+    or_quat_to_R(T, R);
+    const double fx = K[0], fy = K[4];
+    const double x = pc[0], y = pc[1], z = pc[2];
+    const double zinv = 1.0 / (z + 1e-18);
+    const double zinv2 = zinv * zinv;
+    Jp[0] = -fx * zinv; Jp[1] = 0; Jp[2] = fx * x * zinv2; Jp[3] = fx * x * y * zinv2;
+    Jp[4] = -fx - fx * x * x * zinv2; Jp[5] = fx * y * zinv;
+    Jp[6] = 0; Jp[7] = -fy * zinv; Jp[8] = fy * y * zinv2; Jp[9] = fy + fy * y * y * zinv2;
+    Jp[10] = -fy * x * y * zinv2; Jp[11] = -fy * x * zinv;
+    for (int r = 0; r < 2; ++r)
+        for (int c = 0; c < 3; ++c)
+            Jl[r * 3 + c] = Jp[r * 6 + 0] * R[0 * 3 + c] + Jp[r * 6 + 1] * R[1 * 3 + c] + Jp[r * 6 + 2] * R[2 * 3 + c];
+}
+
+/* Eigen LDLT (dynamic size, g2o LinearSolverDense: column-wise GEMV subtraction) on a symmetric n x n (lower
+ * triangle read), solve in place.  Returns isPositive. */
+int or_ldlt_solve(const double* Hin, int n, const double* b, double* x) {
+    double* mat = (double*)malloc(sizeof(double) * (size_t)n * n);
+    double* temp = (double*)malloc(sizeof(double) * (size_t)n);
+    int* tr = (int*)malloc(sizeof(int) * (size_t)n);
+    memcpy(mat, Hin, sizeof(double) * (size_t)n * n);
+#define L(i, j) mat[(size_t)(i) * n + (j)]
+    int sign = 0, found_zero_pivot = 0;
+    for (int k = 0; k < n; ++k) {
+        int big = k;
+        double bv = fabs(L(k, k));
+        for (int i = k + 1; i < n; ++i)
+            if (fabs(L(i, i)) > bv) { bv = fabs(L(i, i)); big = i; }
+        tr[k] = big;
+        if (k != big) {
+            const int s = n - big - 1;
+            for (int j = 0; j < k; ++j) { double t = L(k, j); L(k, j) = L(big, j); L(big, j) = t; }
+            for (int j = 0; j < s; ++j) { double t = L(big + 1 + j, k); L(big + 1 + j, k) = L(big + 1 + j, big); L(big + 1 + j, big) = t; }
+            { double t = L(k, k); L(k, k) = L(big, big); L(big, big) = t; }
+            for (int i = k + 1; i < big; ++i) { double t = L(i, k); L(i, k) = L(big, i); L(big, i) = t; }
+        }
+        const int rs = n - k - 1;
+        if (k > 0) {
+            for (int j = 0; j < k; ++j) temp[j] = L(j, j) * L(k, j);
+            double dot = L(k, 0) * temp[0];
+            for (int j = 1; j < k; ++j) dot = dot + L(k, j) * temp[j];
+            L(k, k) -= dot;
+            for (int i = k + 1; i < n; ++i) {
+                double acc = L(i, k);
+                for (int j = 0; j < k; ++j) acc = acc - L(i, j) * temp[j];
+                L(i, k) = acc;
+            }
+        }
+        const double akk = L(k, k);
+        const int valid = fabs(akk) > 0;
+        if (k == 0 && !valid) {
+            sign = 0;
+            for (int j = 0; j < n; ++j) tr[j] = j;
+            break;
+        }
+        if (rs > 0 && valid)
+            for (int i = k + 1; i < n; ++i) L(i, k) /= akk;
+        if (!valid) found_zero_pivot = 1;
+        if (sign == 1) { if (akk < 0) sign = 3; }
+        else if (sign == 2) { if (akk > 0) sign = 3; }
+        else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+    }
+    (void)found_zero_pivot;
+    double* v = temp;
+    memcpy(v, b, sizeof(double) * (size_t)n);
+    for (int k = 0; k < n; ++k) { double t = v[k]; v[k] = v[tr[k]]; v[tr[k]] = t; }
+    for (int j = 0; j < n; ++j)
+        for (int i = j + 1; i < n; ++i) v[i] = v[i] - L(i, j) * v[j];
+    for (int i = 0; i < n; ++i) {
+        if (fabs(L(i, i)) > DBL_MIN) v[i] /= L(i, i);
+        else v[i] = 0;
+    }
+    for (int j = n - 1; j >= 0; --j)
+        for (int i = 0; i < j; ++i) v[i] = v[i] - L(j, i) * v[j];
+    for (int k = n - 1; k >= 0; --k) { double t = v[k]; v[k] = v[tr[k]]; v[tr[k]] = t; }
+#undef L
+    memcpy(x, v, sizeof(double) * (size_t)n);
+    free(mat);
+    free(temp);
+    free(tr);
+    return sign == 1 || sign == 0;
+}
+
+/* 3 x 3 inverse: adjugate / determinant (row-major) */
+static void inv3(const double* a, double* o) {
+    const double c00 = a[4] * a[8] - a[5] * a[7], c01 = a[5] * a[6] - a[3] * a[8], c02 = a[3] * a[7] - a[4] * a[6];
+    const double det = a[0] * c00 + a[1] * c01 + a[2] * c02;
+    const double id = 1.0 / det;
+    o[0] = c00 * id; o[1] = (a[2] * a[7] - a[1] * a[8]) * id; o[2] = (a[1] * a[5] - a[2] * a[4]) * id;
+    o[3] = c01 * id; o[4] = (a[0] * a[8] - a[2] * a[6]) * id; o[5] = (a[2] * a[3] - a[0] * a[5]) * id;
+    o[6] = c02 * id; o[7] = (a[1] * a[6] - a[0] * a[7]) * id; o[8] = (a[0] * a[4] - a[1] * a[3]) * id;
+}
+
+typedef struct {
+    int P, L, E, nf;
+    const double* K;
+    const int32_t* ep;
+    const int32_t* el;
+    const double* meas;
+    /* structure */
+    int* pe_off; int* pe;  /* edges per pose (edge order) */
+    int* le_off; int* le;  /* edges per landmark (edge order) */
+    int* cv_off; int* cv_l; int* cv_e1; int* cv_e2;  /* per pose pair (p1 <= p2, row-major upper): shared landmarks */
+} ba_struct;
+
+static void ba_build_struct(ba_struct* s) {
+    const int P = s->P, L = s->L, E = s->E;
+    s->pe_off = (int*)calloc((size_t)P + 1, sizeof(int));
+    s->le_off = (int*)calloc((size_t)L + 1, sizeof(int));
+    for (int e = 0; e < E; ++e) { s->pe_off[s->ep[e] + 1]++; s->le_off[s->el[e] + 1]++; }
+    for (int p = 0; p < P; ++p) s->pe_off[p + 1] += s->pe_off[p];
+    for (int l = 0; l < L; ++l) s->le_off[l + 1] += s->le_off[l];
+    s->pe = (int*)malloc(sizeof(int) * (size_t)(E > 0 ? E : 1));
+    s->le = (int*)malloc(sizeof(int) * (size_t)(E > 0 ? E : 1));
+    int* cp = (int*)calloc((size_t)P, sizeof(int));
+    int* cl = (int*)calloc((size_t)L, sizeof(int));
+    for (int e = 0; e < E; ++e) {
+        s->pe[s->pe_off[s->ep[e]] + cp[s->ep[e]]++] = e;
+        s->le[s->le_off[s->el[e]] + cl[s->el[e]]++] = e;
+    }
+    free(cp);
+    free(cl);
+    /* co-visibility: pairs (p1 <= p2) x landmarks ascending; for each landmark every ordered pair of its edges */
+    const int NB = P * P;
+    s->cv_off = (int*)calloc((size_t)NB + 1, sizeof(int));
+    for (int l = 0; l < L; ++l)
+        for (int a = s->le_off[l]; a < s->le_off[l + 1]; ++a)
+            for (int b = s->le_off[l]; b < s->le_off[l + 1]; ++b) {
+                const int p1 = s->ep[s->le[a]], p2 = s->ep[s->le[b]];
+                if (p1 <= p2) s->cv_off[p1 * P + p2 + 1]++;
+            }
+    for (int i = 0; i < NB; ++i) s->cv_off[i + 1] += s->cv_off[i];
+    const int nc = s->cv_off[NB];
+    s->cv_l = (int*)malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
+    s->cv_e1 = (int*)malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
+    s->cv_e2 = (int*)malloc(sizeof(int) * (size_t)(nc > 0 ? nc : 1));
+    int* fill = (int*)calloc((size_t)NB, sizeof(int));
+    for (int l = 0; l < L; ++l)
+        for (int a = s->le_off[l]; a < s->le_off[l + 1]; ++a)
+            for (int b = s->le_off[l]; b < s->le_off[l + 1]; ++b) {
+                const int p1 = s->ep[s->le[a]], p2 = s->ep[s->le[b]];
+                if (p1 > p2) continue;
+                const int k = s->cv_off[p1 * P + p2] + fill[p1 * P + p2]++;
+                s->cv_l[k] = l;
+                s->cv_e1[k] = s->le[a];
+                s->cv_e2[k] = s->le[b];
+            }
+    free(fill);
+}
+
+static void ba_free_struct(ba_struct* s) {
+    free(s->pe_off); free(s->pe); free(s->le_off); free(s->le);
+    free(s->cv_off); free(s->cv_l); free(s->cv_e1); free(s->cv_e2);
+}
+
+static double ba_chi2(const ba_struct* s, const double* poses, const double* X) {
+    tree256 t;
+    t_reset(&t);
+    for (int e = 0; e < s->E; ++e) {
+        double r[2];
+        ba_error(poses + 7 * s->ep[e], s->K, X + 3 * s->el[e], s->meas + 2 * e, r);
+        t_add(&t, e, r[0] * r[0] + r[1] * r[1]);
+    }
+    return t_total(&t);
+}
+
+/* or_ba_lm: g2o LM with BlockSolver_6_3 (see the header); poses [P][7] (T_cw, SE3d::data()), X [L][3] in / out.
+ * chi2_log [max_iters + 1] (may be NULL): chi2 before iteration 0 and after each iteration.  Returns the
+ * iterations run (an iteration that fails 10 trials ends the run, as g2o's Terminate). */
+int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t* ep, const int32_t* el,
+             const double* meas, int E, const double* K, int max_iters, double* chi2_log) {
+    ba_struct s = {P, L, E, n_fixed, K, ep, el, meas, 0, 0, 0, 0, 0, 0, 0, 0};
+    ba_build_struct(&s);
+    const int np = P - n_fixed, ns = 6 * np;
+    double* Jp = (double*)malloc(sizeof(double) * 12 * (size_t)E);
+    double* Jl = (double*)malloc(sizeof(double) * 6 * (size_t)E);
+    double* err = (double*)malloc(sizeof(double) * 2 * (size_t)E);
+    double* Hpl = (double*)malloc(sizeof(double) * 18 * (size_t)E);
+    double* W = (double*)malloc(sizeof(double) * 18 * (size_t)E);
+    double* Hpp = (double*)malloc(sizeof(double) * 36 * (size_t)P);
+    double* bp = (double*)malloc(sizeof(double) * 6 * (size_t)P);
+    double* Hll = (double*)malloc(sizeof(double) * 9 * (size_t)L);
+    double* bl = (double*)malloc(sizeof(double) * 3 * (size_t)L);
+    double* Dinv = (double*)malloc(sizeof(double) * 9 * (size_t)L);
+    double* S = (double*)malloc(sizeof(double) * (size_t)ns * ns + 1);
+    double* bs = (double*)malloc(sizeof(double) * (size_t)ns + 1);
+    double* xp = (double*)malloc(sizeof(double) * (size_t)ns + 1);
+    double* xl = (double*)malloc(sizeof(double) * 3 * (size_t)L);
+    double* bak_p = (double*)malloc(sizeof(double) * 7 * (size_t)P);
+    double* bak_X = (double*)malloc(sizeof(double) * 3 * (size_t)L);
+    double currentChi = ba_chi2(&s, poses, X);
+    if (chi2_log) chi2_log[0] = currentChi;
+    double lambda = 0, ni = 2;
+    int it;
+    for (it = 0; it < max_iters; ++it) {
+        /* buildSystem at the current estimate */
+        for (int e = 0; e < E; ++e) {
+            const double* T = poses + 7 * ep[e];
+            const double* Xe = X + 3 * el[e];
+            ba_error(T, K, Xe, meas + 2 * e, err + 2 * e);
+            ba_jacobians(T, K, Xe, Jp + 12 * e, Jl + 6 * e);
+            const double* jp = Jp + 12 * e;
+            const double* jl = Jl + 6 * e;
+            for (int a = 0; a < 6; ++a)
+                for (int c = 0; c < 3; ++c) Hpl[18 * e + 3 * a + c] = jp[a] * jl[c] + jp[6 + a] * jl[3 + c];
+        }
+        for (int p = n_fixed; p < P; ++p) {
+            for (int a = 0; a < 6; ++a)
+                for (int b = a; b < 6; ++b) {
+                    tree256 t;
+                    t_reset(&t);
+                    for (int k = s.pe_off[p]; k < s.pe_off[p + 1]; ++k) {
+                        const double* jp = Jp + 12 * s.pe[k];
+                        t_add(&t, k - s.pe_off[p], jp[a] * jp[b] + jp[6 + a] * jp[6 + b]);
+                    }
+                    Hpp[36 * p + 6 * a + b] = Hpp[36 * p + 6 * b + a] = t_total(&t);
+                }
+            for (int a = 0; a < 6; ++a) {
+                tree256 t;
+                t_reset(&t);
+                for (int k = s.pe_off[p]; k < s.pe_off[p + 1]; ++k) {
+                    const int e = s.pe[k];
+                    const double* jp = Jp + 12 * e;
+                    t_add(&t, k - s.pe_off[p], jp[a] * err[2 * e] + jp[6 + a] * err[2 * e + 1]);
+                }
+                bp[6 * p + a] = -t_total(&t);
+            }
+        }
+        for (int l = 0; l < L; ++l) {
+            double h[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+            for (int k = s.le_off[l]; k < s.le_off[l + 1]; ++k) {
+                const int e = s.le[k];
+                const double* jl = Jl + 6 * e;
+                for (int a = 0; a < 3; ++a) {
+                    for (int b = a; b < 3; ++b) h[3 * a + b] = h[3 * a + b] + (jl[a] * jl[b] + jl[3 + a] * jl[3 + b]);
+                    g[a] = g[a] + (jl[a] * err[2 * e] + jl[3 + a] * err[2 * e + 1]);
+                }
+            }
+            for (int a = 0; a < 3; ++a) {
+                for (int b = a; b < 3; ++b) Hll[9 * l + 3 * a + b] = Hll[9 * l + 3 * b + a] = h[3 * a + b];
+                bl[3 * l + a] = -g[a];
+            }
+        }
+        if (it == 0) {
+            double maxd = 0;
+            for (int p = n_fixed; p < P; ++p)
+                for (int a = 0; a < 6; ++a) maxd = fmax(maxd, fabs(Hpp[36 * p + 7 * a]));
+            for (int l = 0; l < L; ++l)
+                for (int a = 0; a < 3; ++a) maxd = fmax(maxd, fabs(Hll[9 * l + 4 * a]));
+            lambda = 1e-5 * maxd;
+            ni = 2;
+        }
+        double rho = 0;
+        int q = 0;
+        do {
+            memcpy(bak_p, poses, sizeof(double) * 7 * (size_t)P);
+            memcpy(bak_X, X, sizeof(double) * 3 * (size_t)L);
+            /* landmark blocks with lambda: Dinv, W_e = H_pl Dinv */
+            for (int l = 0; l < L; ++l) {
+                double d[9];
+                memcpy(d, Hll + 9 * l, sizeof d);
+                for (int a = 0; a < 3; ++a) d[4 * a] = d[4 * a] + lambda;
+                inv3(d, Dinv + 9 * l);
+                for (int k = s.le_off[l]; k < s.le_off[l + 1]; ++k) {
+                    const int e = s.le[k];
+                    for (int a = 0; a < 6; ++a)
+                        for (int c = 0; c < 3; ++c)
+                            W[18 * e + 3 * a + c] = Hpl[18 * e + 3 * a + 0] * Dinv[9 * l + 0 * 3 + c] +
+                                                    Hpl[18 * e + 3 * a + 1] * Dinv[9 * l + 1 * 3 + c] +
+                                                    Hpl[18 * e + 3 * a + 2] * Dinv[9 * l + 2 * 3 + c];
+                }
+            }
+            /* Schur: S(p1, p2) = [p1 == p2] (H_pp + lambda I) - sum_l W_e1 H_pl(e2)^T ; upper blocks, mirrored */
+            for (int p1 = n_fixed; p1 < P; ++p1)
+                for (int p2 = p1; p2 < P; ++p2)
+                    for (int a = 0; a < 6; ++a)
+                        for (int b = 0; b < 6; ++b) {
+                            double v = p1 == p2 ? Hpp[36 * p1 + 6 * a + b] + (a == b ? lambda : 0.0) : 0.0;
+                            for (int k = s.cv_off[p1 * P + p2]; k < s.cv_off[p1 * P + p2 + 1]; ++k) {
+                                const double* w = W + 18 * s.cv_e1[k] + 3 * a;
+                                const double* h = Hpl + 18 * s.cv_e2[k] + 3 * b;
+                                v = v - (w[0] * h[0] + w[1] * h[1] + w[2] * h[2]);
+                            }
+                            const int r = 6 * (p1 - n_fixed) + a, c = 6 * (p2 - n_fixed) + b;
+                            S[(size_t)r * ns + c] = v;
+                            S[(size_t)c * ns + r] = v;
+                        }
+            for (int p = n_fixed; p < P; ++p)
+                for (int a = 0; a < 6; ++a) {
+                    double v = bp[6 * p + a];
+                    for (int k = s.pe_off[p]; k < s.pe_off[p + 1]; ++k) {
+                        const int e = s.pe[k];
+                        const double* w = W + 18 * e + 3 * a;
+                        const double* g = bl + 3 * el[e];
+                        v = v - (w[0] * g[0] + w[1] * g[1] + w[2] * g[2]);
+                    }
+                    bs[6 * (p - n_fixed) + a] = v;
+                }
+            const int ok2 = ns > 0 ? or_ldlt_solve(S, ns, bs, xp) : 1;
+            /* landmarks: x_l = Dinv (b_l - sum_e H_pl(e)^T x_p(e)) */
+            for (int l = 0; l < L; ++l) {
+                double t[3] = {bl[3 * l], bl[3 * l + 1], bl[3 * l + 2]};
+                for (int k = s.le_off[l]; k < s.le_off[l + 1]; ++k) {
+                    const int e = s.le[k], p = ep[e];
+                    if (p < n_fixed) continue;
+                    const double* xpp = xp + 6 * (p - n_fixed);
+                    for (int c = 0; c < 3; ++c) {
+                        double d = Hpl[18 * e + c] * xpp[0];
+                        for (int a = 1; a < 6; ++a) d = d + Hpl[18 * e + 3 * a + c] * xpp[a];
+                        t[c] = t[c] - d;
+                    }
+                }
+                const double* D = Dinv + 9 * l;
+                for (int c = 0; c < 3; ++c) xl[3 * l + c] = D[3 * c] * t[0] + D[3 * c + 1] * t[1] + D[3 * c + 2] * t[2];
+            }
+            /* update */
+            for (int p = n_fixed; p < P; ++p) {
+                double dT[7], Tn[7];
+                or_se3_exp(xp + 6 * (p - n_fixed), dT);
+                or_se3_mul(dT, poses + 7 * p, Tn);
+                memcpy(poses + 7 * p, Tn, sizeof Tn);
+            }
+            for (int i = 0; i < 3 * L; ++i) X[i] = X[i] + xl[i];
+            double tempChi = ba_chi2(&s, poses, X);
+            if (!ok2) tempChi = DBL_MAX;
+            rho = currentChi - tempChi;
+            /* computeScale over the variables (poses, then landmarks), tree256 order */
+            tree256 t;
+            t_reset(&t);
+            for (int j = 0; j < ns; ++j) t_add(&t, j, xp[j] * (lambda * xp[j] + bp[6 * n_fixed + j]));
+            for (int j = 0; j < 3 * L; ++j) t_add(&t, ns + j, xl[j] * (lambda * xl[j] + bl[j]));
+            double scale = t_total(&t);
+            scale += 1e-3;
+            rho /= scale;
+            if (rho > 0 && isfinite(tempChi)) {
+                double alpha = 1. - pow((2 * rho - 1), 3);
+                alpha = fmin(alpha, 2. / 3.);
+                const double sf = fmax(1. / 3., alpha);
+                lambda *= sf;
+                ni = 2;
+                currentChi = tempChi;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                memcpy(poses, bak_p, sizeof(double) * 7 * (size_t)P);
+                memcpy(X, bak_X, sizeof(double) * 3 * (size_t)L);
+            }
+            q++;
+        } while (rho < 0 && q < 10);
+        if (chi2_log) chi2_log[it + 1] = currentChi;
+        if (q == 10 || rho == 0 || !isfinite(lambda)) {
+            ++it;
+            break;
+        }
+    }
+    free(Jp); free(Jl); free(err); free(Hpl); free(W); free(Hpp); free(bp); free(Hll); free(bl); free(Dinv);
+    free(S); free(bs); free(xp); free(xl); free(bak_p); free(bak_X);
+    ba_free_struct(&s);
+    return it;
+}

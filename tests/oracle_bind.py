@@ -70,6 +70,8 @@ class Oracle:
                                        ctypes.c_double, _I, _P, _P, _P]),
             "or_decompose_essential": (None, [_P, _P, _P, _P]),
             "or_recover_pose": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
+            "or_ldlt_solve": (_I, [_P, _I, _P, _P]),
+            "or_ba_lm": (_I, [_P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -338,3 +340,24 @@ class Oracle:
         g = np.zeros(4, np.int32)
         good = self.lib.or_recover_pose(_p(E), _p(p1), _p(p2), len(p1), _p(K), _p(R), _p(t), _p(g))
         return good, R.reshape(3, 3), t, g
+
+    # ---- sliding-window BA (BASELINE config 5) ----
+    def ldlt_solve(self, H, b):
+        H = np.ascontiguousarray(H, np.float64)
+        b = np.ascontiguousarray(b, np.float64)
+        x = np.zeros_like(b)
+        pos = self.lib.or_ldlt_solve(_p(H), len(b), _p(b), _p(x))
+        return x, bool(pos)
+
+    def ba_lm(self, poses, n_fixed, X, ep, el, meas, K, max_iters=10):
+        """-> (poses [P, 7], X [L, 3], iterations, chi2 log)."""
+        T = np.ascontiguousarray(poses, np.float64).copy()
+        Xo = np.ascontiguousarray(X, np.float64).copy()
+        ep = np.ascontiguousarray(ep, np.int32)
+        el = np.ascontiguousarray(el, np.int32)
+        meas = np.ascontiguousarray(meas, np.float64)
+        K = np.ascontiguousarray(K, np.float64).reshape(9)
+        log = np.zeros(max_iters + 1)
+        it = self.lib.or_ba_lm(_p(T), len(T), n_fixed, _p(Xo), len(Xo), _p(ep), _p(el), _p(meas), len(ep), _p(K),
+                               max_iters, _p(log))
+        return T, Xo, it, log[:it + 1]

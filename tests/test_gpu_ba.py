@@ -1,0 +1,74 @@
+"""GPU parity of the sliding-window bundle adjustment (yv_ba, ya_vo_amd/csrc/yavo_ba.hip; BASELINE.json config 5)
+with the CPU oracle (oracle/yavo_oracle_ba.c or_ba_lm): poses, landmarks, the chi2 log and the iteration count, bit
+for bit, from small windows to the config-5 size (20 keyframes, 10k landmarks, 5 observations each)."""
+import numpy as np
+import pytest
+
+import ya_vo_amd as yv
+from ya_vo_amd import scene
+
+pytestmark = pytest.mark.gpu
+
+
+def _both(ctx, oracle, w, n_fixed, iters, ba=None):
+    P, L, E = len(w["poses0"]), len(w["X0"]), len(w["ep"])
+    ba = ba or yv.BundleAdjuster(ctx, P, max(L, 1), max(E, 1))
+    ba.set_problem(P, n_fixed, L, w["ep"], w["el"], w["meas"], scene.K_KITTI)
+    T, X, log, it = ba.solve(w["poses0"], w["X0"], iters)
+    oT, oX, oit, olog = oracle.ba_lm(w["poses0"], n_fixed, w["X0"], w["ep"], w["el"], w["meas"], scene.K_KITTI, iters)
+    assert it == oit
+    np.testing.assert_array_equal(log, olog)
+    np.testing.assert_array_equal(T, oT)
+    np.testing.assert_array_equal(X, oX)
+    return T, X, log
+
+
+@pytest.mark.parametrize("P,L,obs,noise,nf,iters,seed", [
+    (5, 200, 3, 1.0, 1, 10, 0),
+    (6, 300, 4, 0.0, 2, 20, 1),
+    (10, 1000, 5, 1.0, 1, 10, 2),
+    (4, 150, 4, 0.3, 0, 8, 3),     # no fixed pose
+    (5, 200, 3, 0.5, 5, 10, 4),    # all poses fixed: landmarks only (no reduced system)
+    (44, 2000, 6, 1.0, 2, 6, 5),   # reduced system 252 x 252: more than one LDLT pass per thread
+])
+def test_ba_matches_oracle(ctx, oracle, P, L, obs, noise, nf, iters, seed):
+    w = scene.ba_window(n_poses=P, n_landmarks=L, obs=obs, noise_px=noise, seed=seed)
+    if noise == 0.0:
+        w["poses0"][:nf] = w["poses_true"][:nf]
+    _, _, log = _both(ctx, oracle, w, nf, iters)
+    assert log[-1] <= log[0]
+
+
+def test_ba_config5_matches_oracle(ctx, oracle):
+    """BASELINE.json config 5: 20-keyframe window, 10k landmarks, 5 observations each, 10 LM iterations."""
+    w = scene.ba_window(n_poses=20, n_landmarks=10000, obs=5, noise_px=1.0, seed=0)
+    _, _, log = _both(ctx, oracle, w, 1, 10)
+    assert log[-1] < 0.05 * log[0]
+
+
+def test_ba_reuse_and_shrink(ctx, oracle):
+    """One workspace, several graphs of different sizes (the structure rebuilt per set_problem)."""
+    ba = yv.BundleAdjuster(ctx, 20, 3000, 15000)
+    for P, L, obs, seed in [(20, 3000, 5, 10), (6, 100, 2, 11), (12, 2500, 6, 12)]:
+        w = scene.ba_window(n_poses=P, n_landmarks=L, obs=obs, noise_px=1.0, seed=seed)
+        _both(ctx, oracle, w, 1, 5, ba)
+
+
+def test_ba_empty_graph(ctx, oracle):
+    poses = scene.ba_window(n_poses=3, n_landmarks=1, obs=1, seed=5)["poses0"]
+    w = dict(poses0=poses, X0=np.zeros((0, 3)), ep=np.zeros(0, np.int32), el=np.zeros(0, np.int32),
+             meas=np.zeros((0, 2)))
+    T, _, log = _both(ctx, oracle, w, 1, 5)
+    np.testing.assert_array_equal(T, poses)
+
+
+def test_ba_rejects_bad_graph(ctx):
+    ba = yv.BundleAdjuster(ctx, 4, 10, 20)
+    ep = np.array([0, 4], np.int32)  # pose 4 out of range
+    el = np.array([0, 1], np.int32)
+    with pytest.raises(yv.YavoError):
+        ba.set_problem(4, 1, 10, ep, el, np.zeros((2, 2)), scene.K_KITTI)
+    with pytest.raises(yv.YavoError):
+        ba.set_problem(5, 1, 10, ep, el, np.zeros((2, 2)), scene.K_KITTI)  # more poses than the workspace
+    with pytest.raises(yv.YavoError):
+        ba.set_problem(4, 5, 10, np.array([0, 1], np.int32), el, np.zeros((2, 2)), scene.K_KITTI)

@@ -113,6 +113,10 @@ GEOM_SIGNATURES = {
     "yv_recover_pose_batch": (_I, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
     "yv_find_essential": (_I, [_P, _P, _P, _I, _D, _D, _D, _D, _D, _P, _P, ctypes.POINTER(_I)]),
     "yv_recover_pose": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, ctypes.POINTER(_I)]),
+    "yv_ba_create": (_I, [_P, _I, _I, _I, ctypes.POINTER(_P)]),
+    "yv_ba_destroy": (None, [_P]),
+    "yv_ba_set_problem": (_I, [_P, _I, _I, _I, _P, _P, _P, _I, _P]),
+    "yv_ba_solve": (_I, [_P, _P, _P, _I, _P, ctypes.POINTER(_I)]),
 }
 
 # include/yavo/yavo_io.h (frame I/O and formats; ya_vo_amd/io.py wraps them)
@@ -525,3 +529,49 @@ class Essential:
                                               _ptr(K), ctypes.c_void_p(d_R), ctypes.c_void_p(d_t),
                                               ctypes.c_void_p(d_good) if d_good else None,
                                               ctypes.c_void_p(stream) if stream else None), "yv_recover_pose_batch")
+
+
+class BundleAdjuster:
+    """Sliding-window bundle adjustment (yv_ba): g2o Levenberg-Marquardt over BlockSolver_6_3 with the reference's
+    projection edge (include/Optimizer.hpp:64-126) between keyframe poses and landmarks; poses SE3d::data() of T_cw,
+    the first n_fixed held fixed."""
+
+    def __init__(self, ctx: "Context", max_poses: int, max_landmarks: int, max_edges: int):
+        self.ctx, self.lib = ctx, ctx.lib
+        h = ctypes.c_void_p()
+        _check(self.lib.yv_ba_create(ctx.handle, max_poses, max_landmarks, max_edges, ctypes.byref(h)), "yv_ba_create")
+        self.handle = h
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.yv_ba_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_problem(self, n_poses: int, n_fixed: int, n_landmarks: int, edge_pose, edge_landmark, meas, K) -> None:
+        self._ep = np.ascontiguousarray(edge_pose, np.int32).reshape(-1)
+        self._el = np.ascontiguousarray(edge_landmark, np.int32).reshape(-1)
+        self._meas = _f64(meas, (-1, 2))
+        if not (len(self._ep) == len(self._el) == len(self._meas)):
+            raise ValueError("edge arrays differ in length")
+        K = _f64(K, (9,))
+        _check(self.lib.yv_ba_set_problem(self.handle, n_poses, n_fixed, n_landmarks, _ptr(self._ep), _ptr(self._el),
+                                          _ptr(self._meas), len(self._ep), _ptr(K)), "yv_ba_set_problem")
+        self.n_poses, self.n_landmarks = n_poses, n_landmarks
+
+    def solve(self, poses, landmarks, max_iters: int = 10):
+        """-> (poses [P, 7], landmarks [L, 3], chi2 log [iters + 1], iterations run)."""
+        poses = _f64(poses, (-1, 7)).copy()
+        X = _f64(landmarks, (-1, 3)).copy()
+        if len(poses) != self.n_poses or len(X) != self.n_landmarks:
+            raise ValueError("estimate does not match the problem")
+        log = np.zeros(max_iters + 1)
+        it = ctypes.c_int(0)
+        _check(self.lib.yv_ba_solve(self.handle, _ptr(poses), _ptr(X), max_iters, _ptr(log), ctypes.byref(it)),
+               "yv_ba_solve")
+        return poses, X, log[: it.value + 1], it.value

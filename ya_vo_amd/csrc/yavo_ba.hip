@@ -1,0 +1,780 @@
+// yavo_ba.hip -- gfx950 kernels for the sliding-window bundle adjustment (BASELINE.json config 5):
+// g2o's Levenberg-Marquardt over BlockSolver_6_3 with the reference's projection edge (include/Optimizer.hpp:64-126)
+// extended to pose-landmark edges, restated like oracle/yavo_oracle_ba.c, expression for expression, in its
+// summation orders (built with -ffp-contract=off):
+//
+//   ba_linearize_kernel   one lane per edge: e, J_pose (the reference's linearizeOplus), J_point = J_pose[:, :3] R,
+//                         H_pl = J_pose^T J_point (6 x 3)
+//   ba_pose_reduce_kernel one 256-thread workgroup per free pose: H_pp (21) and b_p (6) over the pose's edges,
+//                         strided partials then a halving tree (tree256)
+//   ba_landmark_kernel    one lane per landmark: H_ll, b_l (sequential over its edges); per trial the damped 3 x 3
+//                         inverse and W = H_pl Dinv for its edges
+//   ba_schur_kernel       one lane per entry of the upper Schur blocks (p1 <= p2) and of b_schur: sequential over
+//                         the landmarks the two poses share
+//   ba_ldlt_kernel        one workgroup: Eigen's LDLT (diagonal pivoting) on the reduced pose system, then the solve
+//   ba_backsub_kernel     one lane per landmark: x_l = Dinv (b_l - sum_e H_pl^T x_p)
+//   ba_update_kernel      T <- exp(x_p) T per free pose, X <- X + x_l per landmark
+//   ba_chi2_kernel        one workgroup: chi2 over all edges and the LM scale x.(lambda x + b), tree256
+// The LM control (lambda, rho, accept / reject, restore) runs on the host in the oracle's arithmetic.
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../include/yavo/yavo.h"
+#include "../../include/yavo/yavo_geom.h"
+#include "yavo_internal.h"
+#include "yavo_se3.h"
+
+namespace yavo {
+namespace ba {
+
+using se3::quat_to_R;
+using se3::se3_act;
+using se3::se3_exp;
+using se3::se3_mul;
+
+constexpr int kNT = 256;
+
+__device__ __forceinline__ void ba_error(const double* T, const double* K, const double* X, const double* meas,
+                                         double* e) {
+    double pc[3];
+    se3_act(T, X, pc);
+    const double u0 = K[0] * pc[0] + K[1] * pc[1] + K[2] * pc[2];
+    const double u1 = K[3] * pc[0] + K[4] * pc[1] + K[5] * pc[2];
+    const double u2 = K[6] * pc[0] + K[7] * pc[1] + K[8] * pc[2];
+    e[0] = meas[0] - u0 / u2;
+    e[1] = meas[1] - u1 / u2;
+}
+
+// the 256-lane halving tree over one value per thread (LDS), result valid in thread 0
+__device__ __forceinline__ double tree256(double v, double* red) {
+    const int t = threadIdx.x;
+    red[t] = v;
+    __syncthreads();
+    for (int off = kNT / 2; off > 0; off >>= 1) {
+        if (t < off) red[t] = red[t] + red[t + off];
+        __syncthreads();
+    }
+    const double r = red[0];
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(256) void ba_linearize_kernel(BaParams P, BaMat3 K) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= P.E) return;
+    const double* T = P.poses + 7 * P.ep[e];
+    const double* X = P.X + 3 * P.el[e];
+    double err[2];
+    ba_error(T, K.v, X, P.meas + 2 * e, err);
+    double pc[3], R[9], Jp[12], Jl[6];
+    se3_act(T, X, pc);
+    quat_to_R(T, R);
+    const double fx = K.v[0], fy = K.v[4];
+    const double x = pc[0], y = pc[1], z = pc[2];
+    const double zinv = 1.0 / (z + 1e-18);
+    const double zinv2 = zinv * zinv;
+    Jp[0] = -fx * zinv; Jp[1] = 0; Jp[2] = fx * x * zinv2; Jp[3] = fx * x * y * zinv2;
+    Jp[4] = -fx - fx * x * x * zinv2; Jp[5] = fx * y * zinv;
+    Jp[6] = 0; Jp[7] = -fy * zinv; Jp[8] = fy * y * zinv2; Jp[9] = fy + fy * y * y * zinv2;
+    Jp[10] = -fy * x * y * zinv2; Jp[11] = -fy * x * zinv;
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            Jl[r * 3 + c] = Jp[r * 6 + 0] * R[0 * 3 + c] + Jp[r * 6 + 1] * R[1 * 3 + c] + Jp[r * 6 + 2] * R[2 * 3 + c];
+    P.err[2 * e] = err[0];
+    P.err[2 * e + 1] = err[1];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) P.Jp[12 * (int64_t)e + i] = Jp[i];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) P.Jl[6 * (int64_t)e + i] = Jl[i];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) P.Hpl[18 * (int64_t)e + 3 * a + c] = Jp[a] * Jl[c] + Jp[6 + a] * Jl[3 + c];
+}
+
+// one workgroup per free pose (blockIdx.x + nf): 21 upper H entries + 6 b entries in tree256 order
+__global__ __launch_bounds__(256) void ba_pose_reduce_kernel(BaParams P) {
+    __shared__ double red[kNT];
+    const int p = P.nf + blockIdx.x;
+    const int k0 = P.pe_off[p], k1 = P.pe_off[p + 1];
+    const int t = threadIdx.x;
+    double h[21], g[6];
+#pragma unroll
+    for (int i = 0; i < 21; ++i) h[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) g[i] = 0.0;
+    for (int k = k0 + t; k < k1; k += kNT) {
+        const int e = P.pe[k];
+        const double* jp = P.Jp + 12 * (int64_t)e;
+        double J[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) J[i] = jp[i];
+        const double e0 = P.err[2 * e], e1 = P.err[2 * e + 1];
+        int q = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int b = a; b < 6; ++b, ++q) h[q] = h[q] + (J[a] * J[b] + J[6 + a] * J[6 + b]);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) g[a] = g[a] + (J[a] * e0 + J[6 + a] * e1);
+    }
+    double* H = P.Hpp + 36 * p;
+    int q = 0;
+    for (int a = 0; a < 6; ++a)
+        for (int b = a; b < 6; ++b, ++q) {
+            const double v = tree256(h[q], red);
+            if (t == 0) H[6 * a + b] = H[6 * b + a] = v;
+        }
+    for (int a = 0; a < 6; ++a) {
+        const double v = tree256(g[a], red);
+        if (t == 0) P.bp[6 * p + a] = -v;
+    }
+}
+
+// H_ll / b_l per landmark; maxdiag (|H| diagonal of free poses and landmarks) as uint64 bits of a non-negative double
+__global__ __launch_bounds__(256) void ba_landmark_reduce_kernel(BaParams P, unsigned long long* maxdiag) {
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    double m = 0.0;
+    if (l < P.L) {
+        double h[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+        for (int k = P.le_off[l]; k < P.le_off[l + 1]; ++k) {
+            const int e = P.le[k];
+            const double* jl = P.Jl + 6 * (int64_t)e;
+            const double e0 = P.err[2 * e], e1 = P.err[2 * e + 1];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+#pragma unroll
+                for (int b = a; b < 3; ++b) h[3 * a + b] = h[3 * a + b] + (jl[a] * jl[b] + jl[3 + a] * jl[3 + b]);
+                g[a] = g[a] + (jl[a] * e0 + jl[3 + a] * e1);
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+#pragma unroll
+            for (int b = a; b < 3; ++b) {
+                P.Hll[9 * l + 3 * a + b] = h[3 * a + b];
+                P.Hll[9 * l + 3 * b + a] = h[3 * a + b];
+            }
+            P.bl[3 * l + a] = -g[a];
+            m = fmax(m, fabs(h[4 * a]));
+        }
+    }
+    if (l < P.np) {  // the free poses' diagonals, lane l -> pose nf + l
+        const double* H = P.Hpp + 36 * (P.nf + l);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) m = fmax(m, fabs(H[7 * a]));
+    }
+    if (maxdiag && m > 0.0) atomicMax(maxdiag, (unsigned long long)__double_as_longlong(m));
+}
+
+__device__ __forceinline__ void inv3(const double* a, double* o) {
+    const double c00 = a[4] * a[8] - a[5] * a[7], c01 = a[5] * a[6] - a[3] * a[8], c02 = a[3] * a[7] - a[4] * a[6];
+    const double det = a[0] * c00 + a[1] * c01 + a[2] * c02;
+    const double id = 1.0 / det;
+    o[0] = c00 * id; o[1] = (a[2] * a[7] - a[1] * a[8]) * id; o[2] = (a[1] * a[5] - a[2] * a[4]) * id;
+    o[3] = c01 * id; o[4] = (a[0] * a[8] - a[2] * a[6]) * id; o[5] = (a[2] * a[3] - a[0] * a[5]) * id;
+    o[6] = c02 * id; o[7] = (a[1] * a[6] - a[0] * a[7]) * id; o[8] = (a[0] * a[4] - a[1] * a[3]) * id;
+}
+
+__global__ __launch_bounds__(256) void ba_landmark_trial_kernel(BaParams P, double lambda) {
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= P.L) return;
+    double d[9], Di[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) d[i] = P.Hll[9 * l + i];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) d[4 * a] = d[4 * a] + lambda;
+    inv3(d, Di);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) P.Dinv[9 * l + i] = Di[i];
+    for (int k = P.le_off[l]; k < P.le_off[l + 1]; ++k) {
+        const int e = P.le[k];
+        const double* h = P.Hpl + 18 * (int64_t)e;
+        double* w = P.W + 18 * (int64_t)e;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                w[3 * a + c] = h[3 * a + 0] * Di[0 * 3 + c] + h[3 * a + 1] * Di[1 * 3 + c] + h[3 * a + 2] * Di[2 * 3 + c];
+    }
+}
+
+// lanes [0, n_upper): upper Schur entries (block (p1 <= p2) x (a, b)); then [n_upper, n_upper + 6 np): b_schur
+__global__ __launch_bounds__(256) void ba_schur_kernel(BaParams P, double lambda) {
+    const int id = blockIdx.x * blockDim.x + threadIdx.x;
+    const int np = P.np, nb = np * (np + 1) / 2, n_upper = nb * 36;
+    if (id < n_upper) {
+        int blk = id / 36;
+        const int a = (id % 36) / 6, b = id % 6;
+        // blk -> (i1, i2), i1 <= i2, row-major over the upper triangle of the free-pose index
+        int i1 = 0;
+        while (blk >= np - i1) {
+            blk -= np - i1;
+            ++i1;
+        }
+        const int i2 = i1 + blk;
+        const int p1 = P.nf + i1, p2 = P.nf + i2;
+        double v = p1 == p2 ? P.Hpp[36 * p1 + 6 * a + b] + (a == b ? lambda : 0.0) : 0.0;
+        const int c0 = P.cv_off[p1 * P.P + p2], c1 = P.cv_off[p1 * P.P + p2 + 1];
+        for (int k = c0; k < c1; ++k) {
+            const double* w = P.W + 18 * (int64_t)P.cv_e1[k] + 3 * a;
+            const double* h = P.Hpl + 18 * (int64_t)P.cv_e2[k] + 3 * b;
+            v = v - (w[0] * h[0] + w[1] * h[1] + w[2] * h[2]);
+        }
+        const int r = 6 * i1 + a, c = 6 * i2 + b, ns = P.ns;
+        P.S[(int64_t)r * ns + c] = v;
+        P.S[(int64_t)c * ns + r] = v;
+    } else if (id < n_upper + 6 * np) {
+        const int j = id - n_upper, p = P.nf + j / 6, a = j % 6;
+        double v = P.bp[6 * p + a];
+        for (int k = P.pe_off[p]; k < P.pe_off[p + 1]; ++k) {
+            const int e = P.pe[k];
+            const double* w = P.W + 18 * (int64_t)e + 3 * a;
+            const double* g = P.bl + 3 * P.el[e];
+            v = v - (w[0] * g[0] + w[1] * g[1] + w[2] * g[2]);
+        }
+        P.bs[j] = v;
+    }
+}
+
+// Eigen LDLT (dynamic, column-wise GEMV subtraction) + solve, one workgroup; oracle or_ldlt_solve step for step
+__global__ __launch_bounds__(256) void ba_ldlt_kernel(BaParams P) {
+    extern __shared__ double s_dyn[];  // v [n], temp [n]
+    __shared__ double s_pv[kNT];
+    __shared__ int s_pi[kNT];
+    __shared__ int s_sign, s_break;
+    const int n = P.ns, t = threadIdx.x;
+    double* S = P.S;
+    int* tr = P.tr;
+    double* v = s_dyn;
+    double* temp = s_dyn + n;
+#define LL(i, j) S[(int64_t)(i) * n + (j)]
+    if (t == 0) {
+        s_sign = 0;
+        s_break = 0;
+    }
+    __syncthreads();
+    for (int k = 0; k < n; ++k) {
+        // pivot: the first index of the largest |L(i, i)|, i >= k (sequential strict '>' scan)
+        double bv = -1.0;
+        int bi = n;
+        for (int i = k + t; i < n; i += kNT) {
+            const double d = fabs(LL(i, i));
+            if (bi == n || d > bv) {
+                bv = d;
+                bi = i;
+            }
+        }
+        s_pv[t] = bv;
+        s_pi[t] = bi;
+        __syncthreads();
+        for (int off = kNT / 2; off > 0; off >>= 1) {
+            if (t < off) {
+                const double ov = s_pv[t + off];
+                const int oi = s_pi[t + off];
+                if (oi < n && (s_pi[t] == n || ov > s_pv[t] || (ov == s_pv[t] && oi < s_pi[t]))) {
+                    s_pv[t] = ov;
+                    s_pi[t] = oi;
+                }
+            }
+            __syncthreads();
+        }
+        // the sequential scan starts from bv = |L(k, k)| and only moves on a strict '>': ties keep the first index
+        const int big = s_pi[0];
+        __syncthreads();
+        if (t == 0) tr[k] = big;
+        if (k != big) {
+            const int s = n - big - 1;
+            for (int j = t; j < k; j += kNT) {
+                const double q = LL(k, j);
+                LL(k, j) = LL(big, j);
+                LL(big, j) = q;
+            }
+            for (int j = t; j < s; j += kNT) {
+                const double q = LL(big + 1 + j, k);
+                LL(big + 1 + j, k) = LL(big + 1 + j, big);
+                LL(big + 1 + j, big) = q;
+            }
+            if (t == 0) {
+                const double q = LL(k, k);
+                LL(k, k) = LL(big, big);
+                LL(big, big) = q;
+            }
+            for (int i = k + 1 + t; i < big; i += kNT) {
+                const double q = LL(i, k);
+                LL(i, k) = LL(big, i);
+                LL(big, i) = q;
+            }
+        }
+        __syncthreads();
+        if (k > 0) {
+            for (int j = t; j < k; j += kNT) temp[j] = LL(j, j) * LL(k, j);
+            __syncthreads();
+            for (int i = k + 1 + t; i < n; i += kNT) {
+                double acc = LL(i, k);
+                for (int j = 0; j < k; ++j) acc = acc - LL(i, j) * temp[j];
+                LL(i, k) = acc;
+            }
+            if (t == 0) {
+                double dot = LL(k, 0) * temp[0];
+                for (int j = 1; j < k; ++j) dot = dot + LL(k, j) * temp[j];
+                LL(k, k) -= dot;
+            }
+            __syncthreads();
+        }
+        const double akk = LL(k, k);
+        const bool valid = fabs(akk) > 0;
+        if (k == 0 && !valid) {
+            if (t == 0) s_break = 1;
+            for (int j = t; j < n; j += kNT) tr[j] = j;
+            __syncthreads();
+            break;
+        }
+        if (n - k - 1 > 0 && valid)
+            for (int i = k + 1 + t; i < n; i += kNT) LL(i, k) /= akk;
+        if (t == 0) {
+            int sign = s_sign;
+            if (sign == 1) { if (akk < 0) sign = 3; }
+            else if (sign == 2) { if (akk > 0) sign = 3; }
+            else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+            s_sign = sign;
+        }
+        __syncthreads();
+    }
+    if (s_break && t == 0) s_sign = 0;
+    for (int i = t; i < n; i += kNT) v[i] = P.bs[i];
+    __syncthreads();
+    if (t == 0)
+        for (int k = 0; k < n; ++k) {
+            const double q = v[k];
+            v[k] = v[tr[k]];
+            v[tr[k]] = q;
+        }
+    __syncthreads();
+    for (int j = 0; j < n; ++j) {
+        const double vj = v[j];
+        for (int i = j + 1 + t; i < n; i += kNT) v[i] = v[i] - LL(i, j) * vj;
+        __syncthreads();
+    }
+    for (int i = t; i < n; i += kNT) {
+        const double d = LL(i, i);
+        if (fabs(d) > DBL_MIN) v[i] /= d;
+        else v[i] = 0;
+    }
+    __syncthreads();
+    for (int j = n - 1; j >= 0; --j) {
+        const double vj = v[j];
+        for (int i = t; i < j; i += kNT) v[i] = v[i] - LL(j, i) * vj;
+        __syncthreads();
+    }
+    if (t == 0)
+        for (int k = n - 1; k >= 0; --k) {
+            const double q = v[k];
+            v[k] = v[tr[k]];
+            v[tr[k]] = q;
+        }
+    __syncthreads();
+    for (int i = t; i < n; i += kNT) P.xp[i] = v[i];
+    if (t == 0) P.scal[2] = (s_sign == 1 || s_sign == 0) ? 1.0 : 0.0;
+#undef LL
+}
+
+__global__ __launch_bounds__(256) void ba_backsub_kernel(BaParams P) {
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= P.L) return;
+    double tv[3] = {P.bl[3 * l], P.bl[3 * l + 1], P.bl[3 * l + 2]};
+    for (int k = P.le_off[l]; k < P.le_off[l + 1]; ++k) {
+        const int e = P.le[k], p = P.ep[e];
+        if (p < P.nf) continue;
+        const double* xpp = P.xp + 6 * (p - P.nf);
+        const double* h = P.Hpl + 18 * (int64_t)e;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double d = h[c] * xpp[0];
+#pragma unroll
+            for (int a = 1; a < 6; ++a) d = d + h[3 * a + c] * xpp[a];
+            tv[c] = tv[c] - d;
+        }
+    }
+    const double* D = P.Dinv + 9 * l;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) P.xl[3 * l + c] = D[3 * c] * tv[0] + D[3 * c + 1] * tv[1] + D[3 * c + 2] * tv[2];
+}
+
+// lanes [0, np): free poses; [np, np + 3 L): landmark coordinates
+__global__ __launch_bounds__(256) void ba_update_kernel(BaParams P) {
+    const int id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id < P.np) {
+        const int p = P.nf + id;
+        double dT[7], Tn[7];
+        se3_exp(P.xp + 6 * id, dT);
+        se3_mul(dT, P.poses + 7 * p, Tn);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) P.poses[7 * p + i] = Tn[i];
+    } else if (id < P.np + 3 * P.L) {
+        const int i = id - P.np;
+        P.X[i] = P.X[i] + P.xl[i];
+    }
+}
+
+// block 0: chi2 over the edges at the current estimate -> scal[0]; block 1 (when lambda >= 0): the LM scale
+// x.(lambda x + b) over the variables (free poses, then landmarks) -> scal[1]
+__global__ __launch_bounds__(256) void ba_chi2_kernel(BaParams P, BaMat3 K, double lambda, int with_scale) {
+    __shared__ double red[kNT];
+    const int t = threadIdx.x;
+    double acc = 0.0;
+    if (blockIdx.x == 0) {
+        for (int e = t; e < P.E; e += kNT) {
+            double r[2];
+            ba_error(P.poses + 7 * P.ep[e], K.v, P.X + 3 * P.el[e], P.meas + 2 * e, r);
+            acc = acc + (r[0] * r[0] + r[1] * r[1]);
+        }
+        const double v = tree256(acc, red);
+        if (t == 0) P.scal[0] = v;
+    } else if (with_scale) {
+        const int ns = P.ns, nv = ns + 3 * P.L;
+        for (int j = t; j < nv; j += kNT) {
+            double x, b;
+            if (j < ns) {
+                x = P.xp[j];
+                b = P.bp[6 * P.nf + j];
+            } else {
+                x = P.xl[j - ns];
+                b = P.bl[j - ns];
+            }
+            acc = acc + x * (lambda * x + b);
+        }
+        const double v = tree256(acc, red);
+        if (t == 0) P.scal[1] = v;
+    }
+}
+
+}  // namespace ba
+
+void launch_ba_linearize(const BaParams& P, const BaMat3& K, hipStream_t s) {
+    if (P.E > 0) hipLaunchKernelGGL(ba::ba_linearize_kernel, dim3((P.E + 255) / 256), dim3(256), 0, s, P, K);
+    if (P.np > 0) hipLaunchKernelGGL(ba::ba_pose_reduce_kernel, dim3(P.np), dim3(256), 0, s, P);
+}
+
+void launch_ba_landmark_reduce(const BaParams& P, unsigned long long* maxdiag, hipStream_t s) {
+    const int n = std::max(P.L, P.np);
+    if (n > 0) hipLaunchKernelGGL(ba::ba_landmark_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, P, maxdiag);
+}
+
+void launch_ba_trial(const BaParams& P, const BaMat3& K, double lambda, hipStream_t s) {
+    if (P.L > 0) hipLaunchKernelGGL(ba::ba_landmark_trial_kernel, dim3((P.L + 255) / 256), dim3(256), 0, s, P, lambda);
+    const int nb = P.np * (P.np + 1) / 2, nth = nb * 36 + 6 * P.np;
+    if (nth > 0) hipLaunchKernelGGL(ba::ba_schur_kernel, dim3((nth + 255) / 256), dim3(256), 0, s, P, lambda);
+    if (P.ns > 0)
+        hipLaunchKernelGGL(ba::ba_ldlt_kernel, dim3(1), dim3(256), sizeof(double) * 2 * P.ns, s, P);
+    if (P.L > 0) hipLaunchKernelGGL(ba::ba_backsub_kernel, dim3((P.L + 255) / 256), dim3(256), 0, s, P);
+    const int nu = P.np + 3 * P.L;
+    if (nu > 0) hipLaunchKernelGGL(ba::ba_update_kernel, dim3((nu + 255) / 256), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(2), dim3(256), 0, s, P, K, lambda, 1);
+}
+
+void launch_ba_chi2(const BaParams& P, const BaMat3& K, hipStream_t s) {
+    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(1), dim3(256), 0, s, P, K, 0.0, 0);
+}
+
+}  // namespace yavo
+
+// ---- C ABI (include/yavo/yavo_geom.h) ----
+
+struct yv_ba {
+    yv_ctx* ctx = nullptr;
+    int dev = 0;
+    hipStream_t st = nullptr;
+    int max_poses = 0, max_landmarks = 0, max_edges = 0;
+    int64_t cv_cap = 0;
+    yavo::BaParams P;
+    yavo::BaMat3 K{};
+    std::vector<void*> owned;
+    int32_t *d_ep = nullptr, *d_el = nullptr, *d_pe_off = nullptr, *d_pe = nullptr, *d_le_off = nullptr,
+            *d_le = nullptr, *d_cv_off = nullptr, *d_cv_e1 = nullptr, *d_cv_e2 = nullptr;
+    double* d_meas = nullptr;
+    double *bak_poses = nullptr, *bak_X = nullptr;
+    unsigned long long* d_maxdiag = nullptr;
+    double* h_scal = nullptr;  // pinned [4]
+    bool ready = false;
+};
+
+namespace {
+
+template <class T>
+int ba_alloc(yv_ba* b, T** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    if (hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)) != hipSuccess) {
+        std::fprintf(stderr, "yavo: hipMalloc(%zu B) failed in yv_ba\n", count * sizeof(T));
+        return YV_ERR_HIP;
+    }
+    b->owned.push_back(*p);
+    return YV_OK;
+}
+
+void ba_free_one(yv_ba* b, void* p) {
+    if (!p) return;
+    (void)hipFree(p);
+    b->owned.erase(std::remove(b->owned.begin(), b->owned.end(), p), b->owned.end());
+}
+
+int ba_sync_scal(yv_ba* b, int n) {
+    if (hipMemcpyAsync(b->h_scal, b->P.scal, sizeof(double) * n, hipMemcpyDeviceToHost, b->st) != hipSuccess ||
+        hipStreamSynchronize(b->st) != hipSuccess)
+        return YV_ERR_HIP;
+    return YV_OK;
+}
+
+}  // namespace
+
+extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int max_edges, yv_ba** out) {
+    if (!out) return YV_ERR_INVALID;
+    *out = nullptr;
+    // the reduced pose system (6 max_poses)^2 doubles is factorised by one workgroup with its vectors in LDS
+    if (!ctx || max_poses < 1 || max_poses > 1024 || max_landmarks < 0 || max_edges < 0) return YV_ERR_INVALID;
+    yv_ba* b = new yv_ba();
+    b->ctx = ctx;
+    b->dev = yavo::ctx_device(ctx);
+    b->st = yavo::ctx_stream(ctx);
+    b->max_poses = max_poses;
+    b->max_landmarks = max_landmarks;
+    b->max_edges = max_edges;
+    if (hipSetDevice(b->dev) != hipSuccess) {
+        delete b;
+        return YV_ERR_HIP;
+    }
+    const size_t P = max_poses, L = max_landmarks, E = max_edges, ns = 6 * P;
+    yavo::BaParams& Q = b->P;
+    int rc = YV_OK;
+    rc |= ba_alloc(b, &b->d_ep, E);
+    rc |= ba_alloc(b, &b->d_el, E);
+    rc |= ba_alloc(b, &b->d_meas, 2 * E);
+    rc |= ba_alloc(b, &b->d_pe_off, P + 1);
+    rc |= ba_alloc(b, &b->d_pe, E);
+    rc |= ba_alloc(b, &b->d_le_off, L + 1);
+    rc |= ba_alloc(b, &b->d_le, E);
+    rc |= ba_alloc(b, &b->d_cv_off, P * P + 1);
+    rc |= ba_alloc(b, &Q.poses, 7 * P);
+    rc |= ba_alloc(b, &Q.X, 3 * L);
+    rc |= ba_alloc(b, &b->bak_poses, 7 * P);
+    rc |= ba_alloc(b, &b->bak_X, 3 * L);
+    rc |= ba_alloc(b, &Q.err, 2 * E);
+    rc |= ba_alloc(b, &Q.Jp, 12 * E);
+    rc |= ba_alloc(b, &Q.Jl, 6 * E);
+    rc |= ba_alloc(b, &Q.Hpl, 18 * E);
+    rc |= ba_alloc(b, &Q.W, 18 * E);
+    rc |= ba_alloc(b, &Q.Hpp, 36 * P);
+    rc |= ba_alloc(b, &Q.bp, 6 * P);
+    rc |= ba_alloc(b, &Q.Hll, 9 * L);
+    rc |= ba_alloc(b, &Q.bl, 3 * L);
+    rc |= ba_alloc(b, &Q.Dinv, 9 * L);
+    rc |= ba_alloc(b, &Q.S, ns * ns);
+    rc |= ba_alloc(b, &Q.bs, ns);
+    rc |= ba_alloc(b, &Q.xp, ns);
+    rc |= ba_alloc(b, &Q.xl, 3 * L);
+    rc |= ba_alloc(b, &Q.tr, ns);
+    rc |= ba_alloc(b, &Q.scal, 4);
+    rc |= ba_alloc(b, &b->d_maxdiag, 1);
+    if (rc == YV_OK && hipHostMalloc(reinterpret_cast<void**>(&b->h_scal), 4 * sizeof(double)) != hipSuccess)
+        rc = YV_ERR_HIP;
+    if (rc != YV_OK) {
+        yv_ba_destroy(b);
+        return YV_ERR_HIP;
+    }
+    *out = b;
+    return YV_OK;
+}
+
+extern "C" void yv_ba_destroy(yv_ba* b) {
+    if (!b) return;
+    (void)hipSetDevice(b->dev);
+    (void)hipStreamSynchronize(b->st);
+    for (void* p : b->owned) (void)hipFree(p);
+    if (b->h_scal) (void)hipHostFree(b->h_scal);
+    delete b;
+}
+
+extern "C" int yv_ba_set_problem(yv_ba* b, int n_poses, int n_fixed, int n_landmarks, const int32_t* edge_pose,
+                                 const int32_t* edge_landmark, const double* meas, int n_edges, const double K[9]) {
+    if (!b || !K || n_poses < 1 || n_poses > b->max_poses || n_fixed < 0 || n_fixed > n_poses || n_landmarks < 0 ||
+        n_landmarks > b->max_landmarks || n_edges < 0 || n_edges > b->max_edges ||
+        (n_edges > 0 && (!edge_pose || !edge_landmark || !meas)))
+        return YV_ERR_INVALID;
+    for (int i = 0; i < 9; ++i)
+        if (!std::isfinite(K[i])) return YV_ERR_INVALID;
+    for (int e = 0; e < n_edges; ++e)
+        if (edge_pose[e] < 0 || edge_pose[e] >= n_poses || edge_landmark[e] < 0 || edge_landmark[e] >= n_landmarks)
+            return YV_ERR_INVALID;
+    if (hipSetDevice(b->dev) != hipSuccess) return YV_ERR_HIP;
+    b->ready = false;
+    const int P = n_poses, L = n_landmarks, E = n_edges;
+    // edges per pose / per landmark in edge order; co-visibility per pose pair (p1 <= p2), landmarks ascending
+    std::vector<int32_t> pe_off(P + 1, 0), le_off(L + 1, 0), pe(std::max(E, 1)), le(std::max(E, 1));
+    for (int e = 0; e < E; ++e) {
+        pe_off[edge_pose[e] + 1]++;
+        le_off[edge_landmark[e] + 1]++;
+    }
+    for (int p = 0; p < P; ++p) pe_off[p + 1] += pe_off[p];
+    for (int l = 0; l < L; ++l) le_off[l + 1] += le_off[l];
+    {
+        std::vector<int32_t> fp(pe_off.begin(), pe_off.end() - 1), fl(le_off.begin(), le_off.end() - 1);
+        for (int e = 0; e < E; ++e) {
+            pe[fp[edge_pose[e]]++] = e;
+            le[fl[edge_landmark[e]]++] = e;
+        }
+    }
+    const int64_t NB = (int64_t)P * P;
+    std::vector<int32_t> cv_off(NB + 1, 0);
+    for (int l = 0; l < L; ++l)
+        for (int a = le_off[l]; a < le_off[l + 1]; ++a)
+            for (int c = le_off[l]; c < le_off[l + 1]; ++c) {
+                const int p1 = edge_pose[le[a]], p2 = edge_pose[le[c]];
+                if (p1 <= p2) cv_off[(int64_t)p1 * P + p2 + 1]++;
+            }
+    int64_t nc = 0;
+    for (int64_t i = 0; i < NB; ++i) {
+        nc += cv_off[i + 1];
+        if (nc > INT32_MAX) return YV_ERR_CAPACITY;
+        cv_off[i + 1] = (int32_t)nc;
+    }
+    std::vector<int32_t> cv_e1(std::max<int64_t>(nc, 1)), cv_e2(std::max<int64_t>(nc, 1));
+    {
+        std::vector<int32_t> fill(cv_off.begin(), cv_off.end() - 1);
+        for (int l = 0; l < L; ++l)
+            for (int a = le_off[l]; a < le_off[l + 1]; ++a)
+                for (int c = le_off[l]; c < le_off[l + 1]; ++c) {
+                    const int p1 = edge_pose[le[a]], p2 = edge_pose[le[c]];
+                    if (p1 > p2) continue;
+                    const int32_t k = fill[(int64_t)p1 * P + p2]++;
+                    cv_e1[k] = le[a];
+                    cv_e2[k] = le[c];
+                }
+    }
+    if (nc > b->cv_cap) {
+        ba_free_one(b, b->d_cv_e1);
+        ba_free_one(b, b->d_cv_e2);
+        b->d_cv_e1 = b->d_cv_e2 = nullptr;
+        b->cv_cap = 0;
+        if (ba_alloc(b, &b->d_cv_e1, nc) != YV_OK || ba_alloc(b, &b->d_cv_e2, nc) != YV_OK) return YV_ERR_HIP;
+        b->cv_cap = nc;
+    }
+    auto h2d = [&](void* d, const void* h, size_t bytes) {
+        return bytes == 0 || hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, b->st) == hipSuccess;
+    };
+    bool ok = h2d(b->d_ep, edge_pose, sizeof(int32_t) * E) && h2d(b->d_el, edge_landmark, sizeof(int32_t) * E) &&
+              h2d(b->d_meas, meas, sizeof(double) * 2 * E) && h2d(b->d_pe_off, pe_off.data(), 4 * (P + 1)) &&
+              h2d(b->d_pe, pe.data(), 4 * (size_t)E) && h2d(b->d_le_off, le_off.data(), 4 * (size_t)(L + 1)) &&
+              h2d(b->d_le, le.data(), 4 * (size_t)E) && h2d(b->d_cv_off, cv_off.data(), 4 * (size_t)(NB + 1)) &&
+              h2d(b->d_cv_e1, cv_e1.data(), 4 * (size_t)nc) && h2d(b->d_cv_e2, cv_e2.data(), 4 * (size_t)nc);
+    // the pageable sources die with this call
+    if (!ok || hipStreamSynchronize(b->st) != hipSuccess) return YV_ERR_HIP;
+    yavo::BaParams& Q = b->P;
+    Q.P = P;
+    Q.nf = n_fixed;
+    Q.np = P - n_fixed;
+    Q.ns = 6 * Q.np;
+    Q.L = L;
+    Q.E = E;
+    Q.ep = b->d_ep;
+    Q.el = b->d_el;
+    Q.meas = b->d_meas;
+    Q.pe_off = b->d_pe_off;
+    Q.pe = b->d_pe;
+    Q.le_off = b->d_le_off;
+    Q.le = b->d_le;
+    Q.cv_off = b->d_cv_off;
+    Q.cv_e1 = b->d_cv_e1;
+    Q.cv_e2 = b->d_cv_e2;
+    std::memcpy(b->K.v, K, sizeof b->K.v);
+    b->ready = true;
+    return YV_OK;
+}
+
+// g2o OptimizationAlgorithmLevenberg::solve, as or_ba_lm: the host runs the damping control on the device's chi2
+// and scale (bit-identical double arithmetic), the device everything per edge / landmark / pose
+extern "C" int yv_ba_solve(yv_ba* b, double* poses, double* landmarks, int max_iters, double* chi2_log, int* iters) {
+    if (!b || !b->ready || !poses || (b->P.L > 0 && !landmarks) || max_iters < 0) return YV_ERR_INVALID;
+    if (hipSetDevice(b->dev) != hipSuccess) return YV_ERR_HIP;
+    yavo::BaParams& Q = b->P;
+    const size_t pb = sizeof(double) * 7 * Q.P, xb = sizeof(double) * 3 * Q.L;
+    hipStream_t st = b->st;
+    if (hipMemcpyAsync(Q.poses, poses, pb, hipMemcpyHostToDevice, st) != hipSuccess ||
+        (xb && hipMemcpyAsync(Q.X, landmarks, xb, hipMemcpyHostToDevice, st) != hipSuccess))
+        return YV_ERR_HIP;
+    yavo::launch_ba_chi2(Q, b->K, st);
+    if (ba_sync_scal(b, 1) != YV_OK) return YV_ERR_HIP;
+    double currentChi = b->h_scal[0];
+    if (chi2_log) chi2_log[0] = currentChi;
+    double lambda = 0, ni = 2;
+    int it;
+    for (it = 0; it < max_iters; ++it) {
+        yavo::launch_ba_linearize(Q, b->K, st);
+        if (it == 0) {
+            if (hipMemsetAsync(b->d_maxdiag, 0, sizeof(unsigned long long), st) != hipSuccess) return YV_ERR_HIP;
+            yavo::launch_ba_landmark_reduce(Q, b->d_maxdiag, st);
+            unsigned long long bits = 0;
+            if (hipMemcpyAsync(&bits, b->d_maxdiag, sizeof bits, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                return YV_ERR_HIP;
+            double maxd;
+            std::memcpy(&maxd, &bits, sizeof maxd);
+            lambda = 1e-5 * maxd;
+            ni = 2;
+        } else {
+            yavo::launch_ba_landmark_reduce(Q, nullptr, st);
+        }
+        double rho = 0;
+        int q = 0;
+        do {
+            if (hipMemcpyAsync(b->bak_poses, Q.poses, pb, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                (xb && hipMemcpyAsync(b->bak_X, Q.X, xb, hipMemcpyDeviceToDevice, st) != hipSuccess))
+                return YV_ERR_HIP;
+            yavo::launch_ba_trial(Q, b->K, lambda, st);
+            if (hipGetLastError() != hipSuccess || ba_sync_scal(b, 3) != YV_OK) return YV_ERR_HIP;
+            double tempChi = b->h_scal[0];
+            const bool ok2 = Q.ns > 0 ? b->h_scal[2] != 0.0 : true;
+            if (!ok2) tempChi = DBL_MAX;
+            rho = currentChi - tempChi;
+            double scale = b->h_scal[1];
+            scale += 1e-3;
+            rho /= scale;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - pow((2 * rho - 1), 3);
+                alpha = fmin(alpha, 2. / 3.);
+                const double sf = fmax(1. / 3., alpha);
+                lambda *= sf;
+                ni = 2;
+                currentChi = tempChi;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                if (hipMemcpyAsync(Q.poses, b->bak_poses, pb, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                    (xb && hipMemcpyAsync(Q.X, b->bak_X, xb, hipMemcpyDeviceToDevice, st) != hipSuccess))
+                    return YV_ERR_HIP;
+            }
+            q++;
+        } while (rho < 0 && q < 10);
+        if (chi2_log) chi2_log[it + 1] = currentChi;
+        if (q == 10 || rho == 0 || !std::isfinite(lambda)) {
+            ++it;
+            break;
+        }
+    }
+    if (hipMemcpyAsync(poses, Q.poses, pb, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        (xb && hipMemcpyAsync(landmarks, Q.X, xb, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return YV_ERR_HIP;
+    if (iters) *iters = it;
+    return YV_OK;
+}

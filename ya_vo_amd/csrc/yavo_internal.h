@@ -132,6 +132,46 @@ hipStream_t ctx_stream(struct ::yv_ctx* ctx);
 void launch_recover_pose(const EssParams& P, const double* E, const float* pts1, const float* pts2,
                          const int32_t* counts, int n_pairs, int pts_stride, const Mat3& K, double* R, double* t,
                          int32_t* good, hipStream_t s);
+// sliding-window BA (yavo_ba.hip): the device graph, workspace and estimate of a yv_ba
+struct BaParams {
+    int P = 0, nf = 0, np = 0, ns = 0, L = 0, E = 0;
+    const int32_t* ep = nullptr;      // [E]
+    const int32_t* el = nullptr;      // [E]
+    const double* meas = nullptr;     // [E][2]
+    const int32_t* pe_off = nullptr;  // [P + 1] edges per pose (edge order)
+    const int32_t* pe = nullptr;      // [E]
+    const int32_t* le_off = nullptr;  // [L + 1] edges per landmark (edge order)
+    const int32_t* le = nullptr;      // [E]
+    const int32_t* cv_off = nullptr;  // [P * P + 1] per pose pair (p1 <= p2): shared landmarks ascending
+    const int32_t* cv_e1 = nullptr;   // the p1 edge of each
+    const int32_t* cv_e2 = nullptr;   // the p2 edge of each
+    double* poses = nullptr;          // [P][7]
+    double* X = nullptr;              // [L][3]
+    double* err = nullptr;            // [E][2]
+    double* Jp = nullptr;             // [E][12]
+    double* Jl = nullptr;             // [E][6]
+    double* Hpl = nullptr;            // [E][18]
+    double* W = nullptr;              // [E][18]
+    double* Hpp = nullptr;            // [P][36]
+    double* bp = nullptr;             // [P][6]
+    double* Hll = nullptr;            // [L][9]
+    double* bl = nullptr;             // [L][3]
+    double* Dinv = nullptr;           // [L][9]
+    double* S = nullptr;              // [ns][ns]
+    double* bs = nullptr;             // [ns]
+    double* xp = nullptr;             // [ns]
+    double* xl = nullptr;             // [L][3]
+    int32_t* tr = nullptr;            // [ns] LDLT transpositions
+    double* scal = nullptr;           // [4]: chi2, scale, LDLT ok
+};
+struct BaMat3 {
+    double v[9];
+};
+void launch_ba_linearize(const BaParams& P, const BaMat3& K, hipStream_t s);
+void launch_ba_landmark_reduce(const BaParams& P, unsigned long long* maxdiag, hipStream_t s);
+void launch_ba_trial(const BaParams& P, const BaMat3& K, double lambda, hipStream_t s);
+void launch_ba_chi2(const BaParams& P, const BaMat3& K, hipStream_t s);
+
 void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, const double* edge_X,
                        const double* edge_uv, const double* K, const double* priors, double* poses,
                        uint8_t* edge_outlier, int32_t* inliers, hipStream_t s);

@@ -85,3 +85,40 @@ def two_view_matches(n: int, seed: int = 0, K=K_KITTI):
     ua = project(Ta, X, K)
     ub = project(Tb, X, K)
     return Ta, Tb, X, ua, ub
+
+
+def ba_window(n_poses: int = 20, n_landmarks: int = 10000, obs: int = 5, noise_px: float = 1.0, seed: int = 0,
+              K=K_KITTI, init_rot: float = 0.005, init_trans: float = 0.05, init_point: float = 0.1):
+    """Sliding-window BA problem: n_poses keyframes moving ~1 m forward per frame with a
+    slow yaw, n_landmarks points each observed by `obs` consecutive keyframes (pixel noise N(0, noise_px)), edges in
+    landmark order.  Returns dict(poses_true, X_true, poses0, X0 (perturbed initial estimates, the first pose
+    exact), ep, el, meas)."""
+    rng = np.random.default_rng(seed)
+    poses = []
+    for k in range(n_poses):
+        # camera k at world position c_k, looking along +z with yaw 0.01 k: T_cw = [R | -R c]
+        q = quat_from_axis_angle([0.0, 1.0, 0.0], 0.01 * k)
+        c = np.array([0.05 * np.sin(0.3 * k), 0.02 * k, 1.0 * k])
+        R = quat_to_R(q)
+        poses.append(pose(q, -R @ c))
+    poses = np.array(poses)
+    anchors = rng.integers(0, max(n_poses - obs + 1, 1), n_landmarks)
+    X = np.zeros((n_landmarks, 3))
+    for i, a in enumerate(anchors):
+        z = rng.uniform(8.0, 40.0)
+        pc = np.array([rng.uniform(-0.5, 0.5) * z, rng.uniform(-0.2, 0.2) * z, z])
+        T = poses[a]
+        X[i] = quat_to_R(T[:4]).T @ (pc - T[4:])
+    ep, el, meas = [], [], []
+    for i, a in enumerate(anchors):
+        for k in range(a, min(a + obs, n_poses)):
+            uv = project(poses[k], X[i:i + 1], K)[0] + rng.normal(scale=noise_px, size=2)
+            ep.append(k)
+            el.append(i)
+            meas.append(uv)
+    poses0 = poses.copy()
+    for k in range(1, n_poses):
+        poses0[k] = perturb(poses[k], rng, rot=init_rot, trans=init_trans)
+    X0 = X + rng.normal(scale=init_point, size=X.shape)
+    return dict(poses_true=poses, X_true=X, poses0=poses0, X0=X0, ep=np.array(ep, np.int32),
+                el=np.array(el, np.int32), meas=np.array(meas, np.float64))
