@@ -229,6 +229,15 @@ static double ba_chi2(const ba_struct* s, const double* poses, const double* X) 
     return t_total(&t);
 }
 
+/* diagnostics (tests only): when or_ba_dump_iter >= 0, the first damping trial of that iteration copies its
+ * buffers into or_ba_dump[which] (the order of yv_ba_debug_read; S before factorisation) where non-NULL */
+int or_ba_dump_iter = -1;
+double* or_ba_dump[16];
+
+static void ba_dump(int which, const double* src, size_t n) {
+    if (or_ba_dump[which]) memcpy(or_ba_dump[which], src, sizeof(double) * n);
+}
+
 /* or_ba_lm: g2o LM with BlockSolver_6_3 (see the header); poses [P][7] (T_cw, SE3d::data()), X [L][3] in / out.
  * chi2_log [max_iters + 1] (may be NULL): chi2 before iteration 0 and after each iteration.  Returns the
  * iterations run (an iteration that fails 10 trials ends the run, as g2o's Terminate). */
@@ -362,6 +371,14 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
                     bs[6 * (p - n_fixed) + a] = v;
                 }
             const int ok2 = ns > 0 ? or_ldlt_solve(S, ns, bs, xp) : 1;
+            const int dump = it == or_ba_dump_iter && q == 0;
+            if (dump) {
+                ba_dump(0, err, 2 * (size_t)E); ba_dump(1, Jp, 12 * (size_t)E); ba_dump(2, Jl, 6 * (size_t)E);
+                ba_dump(3, Hpl, 18 * (size_t)E); ba_dump(4, W, 18 * (size_t)E); ba_dump(5, Hpp, 36 * (size_t)P);
+                ba_dump(6, bp, 6 * (size_t)P); ba_dump(7, Hll, 9 * (size_t)L); ba_dump(8, bl, 3 * (size_t)L);
+                ba_dump(9, Dinv, 9 * (size_t)L); ba_dump(10, S, (size_t)ns * ns); ba_dump(11, bs, (size_t)ns);
+                ba_dump(12, xp, (size_t)ns);
+            }
             /* landmarks: x_l = Dinv (b_l - sum_e H_pl(e)^T x_p(e)) */
             for (int l = 0; l < L; ++l) {
                 double t[3] = {bl[3 * l], bl[3 * l + 1], bl[3 * l + 2]};
@@ -386,6 +403,9 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
                 memcpy(poses + 7 * p, Tn, sizeof Tn);
             }
             for (int i = 0; i < 3 * L; ++i) X[i] = X[i] + xl[i];
+            if (dump) {
+                ba_dump(13, xl, 3 * (size_t)L); ba_dump(14, poses, 7 * (size_t)P); ba_dump(15, X, 3 * (size_t)L);
+            }
             double tempChi = ba_chi2(&s, poses, X);
             if (!ok2) tempChi = DBL_MAX;
             rho = currentChi - tempChi;

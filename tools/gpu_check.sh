@@ -22,7 +22,7 @@ run() {  # run NAME TIMEOUT CMD...
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-    run pytest_gpu 900 python -m pytest tests -m gpu -q -rf; st=$?; ok $st || exit $st
+    run pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread; st=$?; ok $st || exit $st
     run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; st=$?; ok $st || exit $st
 fi
 run bench 900 python bench.py "$@"; st=$?; ok $st || exit $st

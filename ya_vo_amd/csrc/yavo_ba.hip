@@ -223,6 +223,10 @@ __global__ __launch_bounds__(256) void ba_schur_kernel(BaParams P, double lambda
             ++i1;
         }
         const int i2 = i1 + blk;
+        // a diagonal block's (a, b) and (b, a) are equal only in exact arithmetic; the oracle's loop leaves the
+        // one computed last, (max, min), in both mirrored entries, so the lane with a < b writes nothing (two
+        // lanes storing the same address in one wave would leave an unspecified one)
+        if (i1 == i2 && a < b) return;
         const int p1 = P.nf + i1, p2 = P.nf + i2;
         double v = p1 == p2 ? P.Hpp[36 * p1 + 6 * a + b] + (a == b ? lambda : 0.0) : 0.0;
         const int c0 = P.cv_off[p1 * P.P + p2], c1 = P.cv_off[p1 * P.P + p2 + 1];
@@ -776,5 +780,21 @@ extern "C" int yv_ba_solve(yv_ba* b, double* poses, double* landmarks, int max_i
         hipStreamSynchronize(st) != hipSuccess)
         return YV_ERR_HIP;
     if (iters) *iters = it;
+    return YV_OK;
+}
+
+// diagnostics: copy one of the workspace's device buffers (as left by the last yv_ba_solve) to the host
+extern "C" int yv_ba_debug_read(yv_ba* b, int which, double* dst, int64_t count) {
+    if (!b || !b->ready || !dst || count < 0) return YV_ERR_INVALID;
+    const yavo::BaParams& Q = b->P;
+    double* const bufs[] = {Q.err, Q.Jp, Q.Jl, Q.Hpl, Q.W, Q.Hpp, Q.bp, Q.Hll, Q.bl, Q.Dinv, Q.S, Q.bs, Q.xp, Q.xl,
+                            Q.poses, Q.X};
+    const int64_t sizes[] = {2LL * Q.E, 12LL * Q.E, 6LL * Q.E, 18LL * Q.E, 18LL * Q.E, 36LL * Q.P, 6LL * Q.P,
+                             9LL * Q.L, 3LL * Q.L, 9LL * Q.L, (int64_t)Q.ns * Q.ns, Q.ns, Q.ns, 3LL * Q.L,
+                             7LL * Q.P, 3LL * Q.L};
+    if (which < 0 || which >= (int)(sizeof sizes / sizeof sizes[0]) || count > sizes[which]) return YV_ERR_INVALID;
+    if (hipSetDevice(b->dev) != hipSuccess || hipStreamSynchronize(b->st) != hipSuccess) return YV_ERR_HIP;
+    if (count && hipMemcpy(dst, bufs[which], sizeof(double) * count, hipMemcpyDeviceToHost) != hipSuccess)
+        return YV_ERR_HIP;
     return YV_OK;
 }
