@@ -139,7 +139,7 @@ int yv_ba_set_problem(yv_ba* ba, int n_poses, int n_fixed, int n_landmarks, cons
  * NULL; an iteration whose 10 damping trials all fail ends the run). */
 int yv_ba_solve(yv_ba* ba, double* poses, double* landmarks, int max_iters, double* chi2_log, int* iters);
 /* Diagnostics: copy `count` doubles of workspace buffer `which` (0 err, 1 J_pose, 2 J_point, 3 H_pl, 4 W, 5 H_pp,
- * 6 b_p, 7 H_ll, 8 b_l, 9 D^-1, 10 S (LDLT-factorised in place), 11 b_schur, 12 x_p, 13 x_l, 14 poses, 15 landmarks)
+ * 6 b_p, 7 H_ll, 8 b_l, 9 D^-1, 10 S (as assembled for n <= 120; LDLT-factorised in place above), 11 b_schur, 12 x_p, 13 x_l, 14 poses, 15 landmarks)
  * as the last yv_ba_solve left it. */
 int yv_ba_debug_read(yv_ba* ba, int which, double* dst, int64_t count);
 

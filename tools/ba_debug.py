@@ -50,8 +50,6 @@ def main():
             if name in ("Hpp", "bp"):  # fixed poses are not assembled on the GPU
                 m = 36 if name == "Hpp" else 6
                 g, o = g[nf * m:], o[nf * m:]
-            if name == "S":
-                continue
             bad = np.flatnonzero(g != o)
             rel = np.max(np.abs(g - o) / np.maximum(np.abs(o), 1e-300)) if len(bad) else 0.0
             first = bad[:4].tolist()

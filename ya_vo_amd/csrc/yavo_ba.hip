@@ -7,13 +7,15 @@
 //                         H_pl = J_pose^T J_point (6 x 3)
 //   ba_pose_reduce_kernel one 256-thread workgroup per free pose: H_pp (21) and b_p (6) over the pose's edges,
 //                         strided partials then a halving tree (tree256)
-//   ba_landmark_kernel    one lane per landmark: H_ll, b_l (sequential over its edges); per trial the damped 3 x 3
-//                         inverse and W = H_pl Dinv for its edges
-//   ba_schur_kernel       one lane per entry of the upper Schur blocks (p1 <= p2) and of b_schur: sequential over
-//                         the landmarks the two poses share
-//   ba_ldlt_kernel        one workgroup: Eigen's LDLT (diagonal pivoting) on the reduced pose system, then the solve
+//   ba_landmark_*_kernel  one lane per landmark: H_ll, b_l (sequential over its edges); per trial the damped 3 x 3
+//                         inverse per landmark and W = H_pl Dinv per edge
+//   ba_schur_kernel       one 64-lane workgroup per upper Schur block (p1 <= p2), a lane per entry, and one per pose
+//                         for b_schur: sequential over the landmarks the two poses share, pairs staged in LDS
+//   ba_ldlt_lds_kernel    one workgroup: Eigen's LDLT (diagonal pivoting) on the reduced pose system with its lower
+//                         triangle in LDS (n <= 120; ba_ldlt_kernel on global memory above), then the solve
 //   ba_backsub_kernel     one lane per landmark: x_l = Dinv (b_l - sum_e H_pl^T x_p)
 //   ba_update_kernel      T <- exp(x_p) T per free pose, X <- X + x_l per landmark
+//   ba_edge_chi2_kernel   one lane per edge: |e|^2 at the current estimate
 //   ba_chi2_kernel        one workgroup: chi2 over all edges and the LM scale x.(lambda x + b), tree256
 // The LM control (lambda, rho, accept / reject, restore) runs on the host in the oracle's arithmetic.
 #include <hip/hip_runtime.h>
@@ -104,7 +106,7 @@ __global__ __launch_bounds__(256) void ba_linearize_kernel(BaParams P, BaMat3 K)
 
 // one workgroup per free pose (blockIdx.x + nf): 21 upper H entries + 6 b entries in tree256 order
 __global__ __launch_bounds__(256) void ba_pose_reduce_kernel(BaParams P) {
-    __shared__ double red[kNT];
+    __shared__ double red[27 * kNT];
     const int p = P.nf + blockIdx.x;
     const int k0 = P.pe_off[p], k1 = P.pe_off[p + 1];
     const int t = threadIdx.x;
@@ -128,16 +130,31 @@ __global__ __launch_bounds__(256) void ba_pose_reduce_kernel(BaParams P) {
 #pragma unroll
         for (int a = 0; a < 6; ++a) g[a] = g[a] + (J[a] * e0 + J[6 + a] * e1);
     }
-    double* H = P.Hpp + 36 * p;
-    int q = 0;
-    for (int a = 0; a < 6; ++a)
-        for (int b = a; b < 6; ++b, ++q) {
-            const double v = tree256(h[q], red);
-            if (t == 0) H[6 * a + b] = H[6 * b + a] = v;
+    // the 27 halving trees at once: level `off` has 27 * off independent additions p[t] = p[t] + p[t + off],
+    // spread over all 256 threads (each tree's order is the one tree256 uses)
+#pragma unroll
+    for (int i = 0; i < 21; ++i) red[i * kNT + t] = h[i];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) red[(21 + i) * kNT + t] = g[i];
+    __syncthreads();
+    for (int off = kNT / 2; off > 0; off >>= 1) {
+        for (int idx = t; idx < 27 * off; idx += kNT) {
+            const int q = idx / off, u = idx - q * off;
+            red[q * kNT + u] = red[q * kNT + u] + red[q * kNT + u + off];
         }
-    for (int a = 0; a < 6; ++a) {
-        const double v = tree256(g[a], red);
-        if (t == 0) P.bp[6 * p + a] = -v;
+        __syncthreads();
+    }
+    double* H = P.Hpp + 36 * p;
+    if (t < 21) {
+        int a = 0, q = t;
+        while (q >= 6 - a) {
+            q -= 6 - a;
+            ++a;
+        }
+        const int b = a + q;
+        H[6 * a + b] = H[6 * b + a] = red[t * kNT];
+    } else if (t < 27) {
+        P.bp[6 * p + t - 21] = -red[t * kNT];
     }
 }
 
@@ -186,72 +203,395 @@ __device__ __forceinline__ void inv3(const double* a, double* o) {
     o[6] = c02 * id; o[7] = (a[1] * a[6] - a[0] * a[7]) * id; o[8] = (a[0] * a[4] - a[1] * a[3]) * id;
 }
 
+// lanes [0, L): D^-1 of landmark l (H_ll + lambda I)^-1; lanes [0, E): W_e = H_pl(e) D^-1 of its landmark, with that
+// inverse recomputed in the lane (the same expressions, so the same bits as the landmark lane's)
 __global__ __launch_bounds__(256) void ba_landmark_trial_kernel(BaParams P, double lambda) {
-    const int l = blockIdx.x * blockDim.x + threadIdx.x;
-    if (l >= P.L) return;
-    double d[9], Di[9];
+    const int id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id < P.L) {
+        double d[9], Di[9];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) d[i] = P.Hll[9 * l + i];
+        for (int i = 0; i < 9; ++i) d[i] = P.Hll[9 * id + i];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) d[4 * a] = d[4 * a] + lambda;
-    inv3(d, Di);
+        for (int a = 0; a < 3; ++a) d[4 * a] = d[4 * a] + lambda;
+        inv3(d, Di);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) P.Dinv[9 * l + i] = Di[i];
-    for (int k = P.le_off[l]; k < P.le_off[l + 1]; ++k) {
-        const int e = P.le[k];
-        const double* h = P.Hpl + 18 * (int64_t)e;
-        double* w = P.W + 18 * (int64_t)e;
+        for (int i = 0; i < 9; ++i) P.Dinv[9 * id + i] = Di[i];
+    }
+    if (id < P.E) {
+        const int l = P.el[id];
+        double d[9], Di[9], h[18];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) d[i] = P.Hll[9 * l + i];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) d[4 * a] = d[4 * a] + lambda;
+        inv3(d, Di);
+        const double2* h2 = reinterpret_cast<const double2*>(P.Hpl + 18 * (int64_t)id);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const double2 v = h2[i];
+            h[2 * i] = v.x;
+            h[2 * i + 1] = v.y;
+        }
+        double w[18];
 #pragma unroll
         for (int a = 0; a < 6; ++a)
 #pragma unroll
             for (int c = 0; c < 3; ++c)
                 w[3 * a + c] = h[3 * a + 0] * Di[0 * 3 + c] + h[3 * a + 1] * Di[1 * 3 + c] + h[3 * a + 2] * Di[2 * 3 + c];
+        double2* w2 = reinterpret_cast<double2*>(P.W + 18 * (int64_t)id);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) w2[i] = make_double2(w[2 * i], w[2 * i + 1]);
     }
 }
 
-// lanes [0, n_upper): upper Schur entries (block (p1 <= p2) x (a, b)); then [n_upper, n_upper + 6 np): b_schur
-__global__ __launch_bounds__(256) void ba_schur_kernel(BaParams P, double lambda) {
-    const int id = blockIdx.x * blockDim.x + threadIdx.x;
-    const int np = P.np, nb = np * (np + 1) / 2, n_upper = nb * 36;
-    if (id < n_upper) {
-        int blk = id / 36;
-        const int a = (id % 36) / 6, b = id % 6;
-        // blk -> (i1, i2), i1 <= i2, row-major over the upper triangle of the free-pose index
-        int i1 = 0;
+constexpr int kSchurChunk = 128;  // pairs per pass = threads per workgroup
+constexpr int kSchurStride = 37;  // doubles per staged pair: 36 products + 1 (2-way instead of 8-way bank conflicts)
+
+// 18 doubles (one 6 x 3 block, 144 B, 16-B aligned) into registers
+__device__ __forceinline__ void load18(const double* src, double* r) {
+    const double2* s2 = reinterpret_cast<const double2*>(src);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const double2 v = s2[i];
+        r[2 * i] = v.x;
+        r[2 * i + 1] = v.y;
+    }
+}
+
+// the sequential chain v = v - d_0 - d_1 - ... over n staged products (LDS loads 8 ahead of the chain)
+__device__ __forceinline__ double schur_chain(double v, const double* sd, int n, int col) {
+    int j = 0;
+    for (; j + 8 <= n; j += 8) {
+        double d[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) d[u] = sd[(j + u) * kSchurStride + col];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v = v - d[u];
+    }
+    for (; j < n; ++j) v = v - sd[j * kSchurStride + col];
+    return v;
+}
+
+// One 128-lane workgroup per upper Schur block (p1 <= p2) of the free poses, then one per free pose for b_schur.
+// Block: entry (a, b) is the oracle's sequential chain over the landmarks the two poses share,
+// v = v - (W_e1[a] . H_pl(e2)[b]). Per pass of 128 pairs every lane forms one pair's 36 products from its registers
+// into LDS (the next pass's blocks already loading), then lane a * 6 + b (< 36) runs its chain over them: one LDS
+// load and one subtraction per pair. On a diagonal block only a >= b writes (the oracle's loop leaves the (max, min)
+// value in both mirrored entries). b_schur: lane a < 6 runs v = b_p[a] - sum_e W_e[a] . b_l(e) over the pose's edges.
+__global__ __launch_bounds__(kSchurChunk) void ba_schur_kernel(BaParams P, double lambda) {
+    __shared__ double sd[kSchurChunk * kSchurStride];
+    const int np = P.np, nb = np * (np + 1) / 2;
+    const int lane = threadIdx.x;
+    const int a = lane / 6, b = lane - 6 * (lane / 6);
+    if ((int)blockIdx.x < nb) {
+        int blk = blockIdx.x, i1 = 0;
         while (blk >= np - i1) {
             blk -= np - i1;
             ++i1;
         }
         const int i2 = i1 + blk;
-        // a diagonal block's (a, b) and (b, a) are equal only in exact arithmetic; the oracle's loop leaves the
-        // one computed last, (max, min), in both mirrored entries, so the lane with a < b writes nothing (two
-        // lanes storing the same address in one wave would leave an unspecified one)
-        if (i1 == i2 && a < b) return;
         const int p1 = P.nf + i1, p2 = P.nf + i2;
-        double v = p1 == p2 ? P.Hpp[36 * p1 + 6 * a + b] + (a == b ? lambda : 0.0) : 0.0;
+        const bool active = lane < 36 && !(i1 == i2 && a < b);
+        double v = 0.0;
+        if (active) v = p1 == p2 ? P.Hpp[36 * p1 + 6 * a + b] + (a == b ? lambda : 0.0) : 0.0;
         const int c0 = P.cv_off[p1 * P.P + p2], c1 = P.cv_off[p1 * P.P + p2 + 1];
-        for (int k = c0; k < c1; ++k) {
-            const double* w = P.W + 18 * (int64_t)P.cv_e1[k] + 3 * a;
-            const double* h = P.Hpl + 18 * (int64_t)P.cv_e2[k] + 3 * b;
-            v = v - (w[0] * h[0] + w[1] * h[1] + w[2] * h[2]);
+        double rw[18], rh[18];
+        if (c0 + lane < c1) {
+            load18(P.W + 18 * (int64_t)P.cv_e1[c0 + lane], rw);
+            load18(P.Hpl + 18 * (int64_t)P.cv_e2[c0 + lane], rh);
         }
-        const int r = 6 * i1 + a, c = 6 * i2 + b, ns = P.ns;
-        P.S[(int64_t)r * ns + c] = v;
-        P.S[(int64_t)c * ns + r] = v;
-    } else if (id < n_upper + 6 * np) {
-        const int j = id - n_upper, p = P.nf + j / 6, a = j % 6;
-        double v = P.bp[6 * p + a];
-        for (int k = P.pe_off[p]; k < P.pe_off[p + 1]; ++k) {
-            const int e = P.pe[k];
-            const double* w = P.W + 18 * (int64_t)e + 3 * a;
+        for (int base = c0; base < c1; base += kSchurChunk) {
+            const int n = min(kSchurChunk, c1 - base);
+            if (lane < n) {
+#pragma unroll
+                for (int x = 0; x < 6; ++x)
+#pragma unroll
+                    for (int y = 0; y < 6; ++y)
+                        sd[lane * kSchurStride + 6 * x + y] =
+                            rw[3 * x] * rh[3 * y] + rw[3 * x + 1] * rh[3 * y + 1] + rw[3 * x + 2] * rh[3 * y + 2];
+            }
+            const int nxt = base + kSchurChunk + lane;
+            if (nxt < c1) {
+                load18(P.W + 18 * (int64_t)P.cv_e1[nxt], rw);
+                load18(P.Hpl + 18 * (int64_t)P.cv_e2[nxt], rh);
+            }
+            __syncthreads();
+            if (active) v = schur_chain(v, sd, n, lane);
+            __syncthreads();
+        }
+        if (active) {
+            const int r = 6 * i1 + a, c = 6 * i2 + b, ns = P.ns;
+            P.S[(int64_t)r * ns + c] = v;
+            P.S[(int64_t)c * ns + r] = v;
+        }
+    } else {
+        const int j = blockIdx.x - nb, p = P.nf + j;
+        const bool active = lane < 6;
+        double v = active ? P.bp[6 * p + lane] : 0.0;
+        const int k0 = P.pe_off[p], k1 = P.pe_off[p + 1];
+        double rw[18], rg[3];
+        if (k0 + lane < k1) {
+            const int e = P.pe[k0 + lane];
+            load18(P.W + 18 * (int64_t)e, rw);
             const double* g = P.bl + 3 * P.el[e];
-            v = v - (w[0] * g[0] + w[1] * g[1] + w[2] * g[2]);
+            rg[0] = g[0]; rg[1] = g[1]; rg[2] = g[2];
         }
-        P.bs[j] = v;
+        for (int base = k0; base < k1; base += kSchurChunk) {
+            const int n = min(kSchurChunk, k1 - base);
+            if (lane < n) {
+#pragma unroll
+                for (int x = 0; x < 6; ++x)
+                    sd[lane * kSchurStride + x] = rw[3 * x] * rg[0] + rw[3 * x + 1] * rg[1] + rw[3 * x + 2] * rg[2];
+            }
+            const int nxt = base + kSchurChunk + lane;
+            if (nxt < k1) {
+                const int e = P.pe[nxt];
+                load18(P.W + 18 * (int64_t)e, rw);
+                const double* g = P.bl + 3 * P.el[e];
+                rg[0] = g[0]; rg[1] = g[1]; rg[2] = g[2];
+            }
+            __syncthreads();
+            if (active) v = schur_chain(v, sd, n, lane);
+            __syncthreads();
+        }
+        if (active) P.bs[6 * j + lane] = v;
     }
 }
 
-// Eigen LDLT (dynamic, column-wise GEMV subtraction) + solve, one workgroup; oracle or_ldlt_solve step for step
+// Eigen LDLT on the reduced system (n <= kLdltMaxN), bit-identical to the oracle's left-looking or_ldlt_solve
+// (diagonal pivoting), in three steps:
+//  1. The pivot sequence. At step k the oracle takes the first position of the largest |L(i, i)|, i >= k, and L(i, i)
+//     for i >= k still holds an original diagonal entry (it is only updated at its own step), so the sequence follows
+//     from the diagonal alone. Distinct values (the usual case): it is the descending order, by ranks. Any tie or NaN:
+//     wave 0 replays the oracle's scan-and-swap step by step.
+//  2. Pivoting commutes with the left-looking factorisation: the oracle swaps untouched original entries in the
+//     trailing part and the finished rows of L, so its result equals the unpivoted factorisation of P S P^T (S is
+//     bitwise symmetric: each Schur entry is stored to both halves from one value).
+//  3. The unpivoted factorisation runs right-looking with the matrix in registers: the oracle forms column k as
+//     acc = L(i, k) - L(i, 0) t_0 - L(i, 1) t_1 - ... (t_j = D(j) L(k, j)) and D(k) = L(k, k) - (L(k, 0) t_0 + ...);
+//     step j here applies term j of every such chain at once (L(i, c) -= L(i, j) (D(j) L(c, j)), i > c > j;
+//     dot_c += L(c, j) (D(j) L(c, j))), the same operations in the same order per entry. Thread = one 16-column
+//     segment of one row of the lower triangle (504 segments at n = 120); per step the owners of column k divide
+//     and publish L(i, k) and t_i through LDS, then every segment updates its entries in registers.
+// The triangular solves then run on wave 0 alone, the vector in registers, broadcasts by v_readlane.
+constexpr int kLdltMaxN = 120;
+constexpr int kLdltThreads = 512;
+constexpr int kLdltSeg = 16;
+
+__device__ __forceinline__ int tri(int i, int j) { return (i * (i + 1) >> 1) + j; }
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// makes one wave's LDS stores visible to its other lanes' later loads (wave-synchronous phases)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(kLdltThreads) void ba_ldlt_lds_kernel(BaParams P) {
+    __shared__ double Ls[kLdltMaxN * (kLdltMaxN + 1) / 2];  // the factor, for the solves
+    __shared__ double colk[kLdltMaxN];  // L(i, k) of the current step
+    __shared__ double tc[kLdltMaxN];    // t_i = D(k) L(i, k)
+    __shared__ double dg[kLdltMaxN];    // |diagonal|, permuted as the pivots are taken
+    __shared__ int perm[kLdltMaxN];     // position -> original index: (P S P^T)(i, j) = S(perm[i], perm[j])
+    __shared__ double s_akk;
+    __shared__ int s_slow;
+    const int n = P.ns, t = threadIdx.x;
+    if (t == 0) s_slow = 0;
+    for (int i = t; i < n; i += kLdltThreads) dg[i] = fabs(P.S[(int64_t)i * n + i]);
+    __syncthreads();
+    // 1. ranks by (|d| descending, index ascending); a tie or a NaN sends the sequence to the replay
+    if (t < n) {
+        const double d = dg[t];
+        int rank = 0;
+        bool tie = isnan(d);
+        for (int j = 0; j < n; ++j) {
+            const double o = dg[j];
+            rank += o > d;
+            tie |= (o == d && j != t);
+        }
+        perm[rank] = t;  // a permutation when there is no tie
+        if (tie) s_slow = 1;
+    }
+    __syncthreads();
+    if (s_slow) {
+        if (t < 64) {
+            for (int i = t; i < n; i += 64) perm[i] = i;
+            wave_lds_sync();
+            for (int k = 0; k < n; ++k) {
+                double bv = -1.0;
+                int bi = n;
+                for (int i = k + t; i < n; i += 64) {
+                    const double d = dg[i];
+                    if (isnan(d)) continue;
+                    if (bi == n || d > bv) {
+                        bv = d;
+                        bi = i;
+                    }
+                }
+#pragma unroll
+                for (int m = 1; m < 64; m <<= 1) {
+                    const double ov = __shfl_xor(bv, m);
+                    const int oi = __shfl_xor(bi, m);
+                    if (oi < n && (bi == n || ov > bv || (ov == bv && oi < bi))) {
+                        bv = ov;
+                        bi = oi;
+                    }
+                }
+                if (isnan(dg[k]) || bi == n) bi = k;
+                wave_lds_sync();
+                if (t == 0 && bi != k) {
+                    const double q = dg[k];
+                    dg[k] = dg[bi];
+                    dg[bi] = q;
+                    const int pq = perm[k];
+                    perm[k] = perm[bi];
+                    perm[bi] = pq;
+                }
+                wave_lds_sync();
+            }
+        }
+        __syncthreads();
+    }
+    // the oracle's first step: a zero (or NaN) pivot ends the factorisation with only its own transposition applied
+    // to the matrix and none to the vector
+    const int big0 = perm[0];
+    const double a00 = P.S[(int64_t)big0 * n + big0];
+    const bool brk = !(fabs(a00) > 0);
+    __syncthreads();
+    if (brk) {
+        for (int i = t; i < n; i += kLdltThreads) perm[i] = i == 0 ? big0 : (i == big0 ? 0 : i);
+        __syncthreads();
+    }
+    // 2. this thread's segment of P S P^T: row my_i, columns [cb, cb + 16) below the diagonal
+    int my_i = -1, cb = 0;
+    {
+        int r = t;
+        for (int i = 1; i < n; ++i) {
+            const int nsg = (i + kLdltSeg - 1) / kLdltSeg;
+            if (r < nsg) {
+                my_i = i;
+                cb = r * kLdltSeg;
+                break;
+            }
+            r -= nsg;
+        }
+    }
+    const bool owner = my_i >= 0;
+    const bool diag_owner = owner && (my_i - 1) / kLdltSeg == cb / kLdltSeg;  // holds the row's diagonal chain
+    double L[kLdltSeg];
+    double dorig = 0.0, dotv = 0.0;
+    if (owner) {
+        const int64_t pr = (int64_t)perm[my_i] * n;
+#pragma unroll
+        for (int u = 0; u < kLdltSeg; ++u) {
+            const int c = cb + u;
+            L[u] = c < my_i ? P.S[pr + perm[c < my_i ? c : 0]] : 0.0;
+        }
+        if (diag_owner) dorig = P.S[pr + perm[my_i]];
+    }
+    if (t == 0) {
+        s_akk = a00;
+        Ls[0] = a00;  // D(0) when the factorisation runs (with brk the solve reads the untouched diagonal)
+    }
+    // the row-0 diagonal is not in any segment: with brk the solves read the original entries
+    __syncthreads();
+    // 3. right-looking, unpivoted
+    int sign = 0;
+    for (int k = 0; k < n && !brk; ++k) {
+        const double akk = s_akk;
+        const bool valid = fabs(akk) > 0;
+        if (t == 0) {
+            Ls[tri(k, k)] = akk;
+            if (sign == 1) { if (akk < 0) sign = 3; }
+            else if (sign == 2) { if (akk > 0) sign = 3; }
+            else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+        }
+        // column k: divide, publish L(i, k) and t_i
+        if (owner && my_i > k && cb <= k && k < cb + kLdltSeg) {
+            const int uk = k - cb;
+            double lv = 0.0;
+#pragma unroll
+            for (int u = 0; u < kLdltSeg; ++u)
+                if (u == uk) lv = L[u];
+            const double l = valid ? lv / akk : lv;
+#pragma unroll
+            for (int u = 0; u < kLdltSeg; ++u)
+                if (u == uk) L[u] = l;
+            colk[my_i] = l;
+            tc[my_i] = akk * l;
+        }
+        __syncthreads();
+        // term k of every chain in this segment, and of the row's diagonal chain
+        if (owner && my_i > k) {
+            const double lik = colk[my_i];
+            if (cb + kLdltSeg - 1 > k) {
+#pragma unroll
+                for (int u = 0; u < kLdltSeg; ++u) {
+                    const int c = cb + u;
+                    if (c > k && c < my_i) L[u] = L[u] - lik * tc[c];
+                }
+            }
+            if (diag_owner) {
+                dotv = k > 0 ? dotv + lik * tc[my_i] : lik * tc[my_i];
+                if (my_i == k + 1) s_akk = dorig - dotv;
+            }
+        }
+        __syncthreads();
+    }
+    if (brk) sign = 0;
+    // the factor into LDS for the solves (with brk: the untouched P S P^T)
+    if (owner) {
+#pragma unroll
+        for (int u = 0; u < kLdltSeg; ++u)
+            if (cb + u < my_i) Ls[tri(my_i, cb + u)] = L[u];
+        if (brk && diag_owner) Ls[tri(my_i, my_i)] = dorig;
+    }
+    __syncthreads();
+    if (t >= 64) return;  // no barrier below
+    // the solves on wave 0: lane l holds positions l and l + 64
+    const int q0 = t, q1 = t + 64;
+    double v0 = 0.0, v1 = 0.0;
+    if (q0 < n) v0 = P.bs[brk ? q0 : perm[q0]];
+    if (q1 < n) v1 = P.bs[brk ? q1 : perm[q1]];
+#pragma unroll 4
+    for (int j = 0; j < n; ++j) {
+        const double vj = readlane_f64(j < 64 ? v0 : v1, j & 63);
+        const double a0 = q0 > j && q0 < n ? Ls[tri(q0, j)] : 0.0;
+        const double a1 = q1 > j && q1 < n ? Ls[tri(q1, j)] : 0.0;
+        if (q0 > j && q0 < n) v0 = v0 - a0 * vj;
+        if (q1 > j && q1 < n) v1 = v1 - a1 * vj;
+    }
+    if (q0 < n) {
+        const double d = Ls[tri(q0, q0)];
+        if (fabs(d) > DBL_MIN) v0 /= d;
+        else v0 = 0;
+    }
+    if (q1 < n) {
+        const double d = Ls[tri(q1, q1)];
+        if (fabs(d) > DBL_MIN) v1 /= d;
+        else v1 = 0;
+    }
+#pragma unroll 4
+    for (int j = n - 1; j >= 0; --j) {
+        const double vj = readlane_f64(j < 64 ? v0 : v1, j & 63);
+        const double a0 = q0 < j ? Ls[tri(j, q0)] : 0.0;
+        const double a1 = q1 < j ? Ls[tri(j, q1)] : 0.0;
+        if (q0 < j) v0 = v0 - a0 * vj;
+        if (q1 < j) v1 = v1 - a1 * vj;
+    }
+    if (q0 < n) P.xp[brk ? q0 : perm[q0]] = v0;
+    if (q1 < n) P.xp[brk ? q1 : perm[q1]] = v1;
+    if (t == 0) P.scal[2] = (sign == 1 || sign == 0) ? 1.0 : 0.0;
+}
+
+// larger systems: the same steps on S in global memory
 __global__ __launch_bounds__(256) void ba_ldlt_kernel(BaParams P) {
     extern __shared__ double s_dyn[];  // v [n], temp [n]
     __shared__ double s_pv[kNT];
@@ -431,6 +771,15 @@ __global__ __launch_bounds__(256) void ba_update_kernel(BaParams P) {
     }
 }
 
+// one lane per edge: its squared error at the current estimate (summed by ba_chi2_kernel)
+__global__ __launch_bounds__(256) void ba_edge_chi2_kernel(BaParams P, BaMat3 K) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= P.E) return;
+    double r[2];
+    ba_error(P.poses + 7 * P.ep[e], K.v, P.X + 3 * P.el[e], P.meas + 2 * e, r);
+    P.e2[e] = r[0] * r[0] + r[1] * r[1];
+}
+
 // block 0: chi2 over the edges at the current estimate -> scal[0]; block 1 (when lambda >= 0): the LM scale
 // x.(lambda x + b) over the variables (free poses, then landmarks) -> scal[1]
 __global__ __launch_bounds__(256) void ba_chi2_kernel(BaParams P, BaMat3 K, double lambda, int with_scale) {
@@ -438,11 +787,15 @@ __global__ __launch_bounds__(256) void ba_chi2_kernel(BaParams P, BaMat3 K, doub
     const int t = threadIdx.x;
     double acc = 0.0;
     if (blockIdx.x == 0) {
-        for (int e = t; e < P.E; e += kNT) {
-            double r[2];
-            ba_error(P.poses + 7 * P.ep[e], K.v, P.X + 3 * P.el[e], P.meas + 2 * e, r);
-            acc = acc + (r[0] * r[0] + r[1] * r[1]);
+        int e = t;
+        for (; e + 3 * kNT < P.E; e += 4 * kNT) {
+            const double v0 = P.e2[e], v1 = P.e2[e + kNT], v2 = P.e2[e + 2 * kNT], v3 = P.e2[e + 3 * kNT];
+            acc = acc + v0;
+            acc = acc + v1;
+            acc = acc + v2;
+            acc = acc + v3;
         }
+        for (; e < P.E; e += kNT) acc = acc + P.e2[e];
         const double v = tree256(acc, red);
         if (t == 0) P.scal[0] = v;
     } else if (with_scale) {
@@ -476,18 +829,23 @@ void launch_ba_landmark_reduce(const BaParams& P, unsigned long long* maxdiag, h
 }
 
 void launch_ba_trial(const BaParams& P, const BaMat3& K, double lambda, hipStream_t s) {
-    if (P.L > 0) hipLaunchKernelGGL(ba::ba_landmark_trial_kernel, dim3((P.L + 255) / 256), dim3(256), 0, s, P, lambda);
-    const int nb = P.np * (P.np + 1) / 2, nth = nb * 36 + 6 * P.np;
-    if (nth > 0) hipLaunchKernelGGL(ba::ba_schur_kernel, dim3((nth + 255) / 256), dim3(256), 0, s, P, lambda);
-    if (P.ns > 0)
+    const int nl = std::max(P.L, P.E);
+    if (nl > 0) hipLaunchKernelGGL(ba::ba_landmark_trial_kernel, dim3((nl + 255) / 256), dim3(256), 0, s, P, lambda);
+    const int nb = P.np * (P.np + 1) / 2;
+    if (nb > 0) hipLaunchKernelGGL(ba::ba_schur_kernel, dim3(nb + P.np), dim3(ba::kSchurChunk), 0, s, P, lambda);
+    if (P.ns > 0 && P.ns <= ba::kLdltMaxN)
+        hipLaunchKernelGGL(ba::ba_ldlt_lds_kernel, dim3(1), dim3(ba::kLdltThreads), 0, s, P);
+    else if (P.ns > 0)
         hipLaunchKernelGGL(ba::ba_ldlt_kernel, dim3(1), dim3(256), sizeof(double) * 2 * P.ns, s, P);
     if (P.L > 0) hipLaunchKernelGGL(ba::ba_backsub_kernel, dim3((P.L + 255) / 256), dim3(256), 0, s, P);
     const int nu = P.np + 3 * P.L;
     if (nu > 0) hipLaunchKernelGGL(ba::ba_update_kernel, dim3((nu + 255) / 256), dim3(256), 0, s, P);
+    if (P.E > 0) hipLaunchKernelGGL(ba::ba_edge_chi2_kernel, dim3((P.E + 255) / 256), dim3(256), 0, s, P, K);
     hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(2), dim3(256), 0, s, P, K, lambda, 1);
 }
 
 void launch_ba_chi2(const BaParams& P, const BaMat3& K, hipStream_t s) {
+    if (P.E > 0) hipLaunchKernelGGL(ba::ba_edge_chi2_kernel, dim3((P.E + 255) / 256), dim3(256), 0, s, P, K);
     hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(1), dim3(256), 0, s, P, K, 0.0, 0);
 }
 
@@ -588,7 +946,8 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
     rc |= ba_alloc(b, &Q.xp, ns);
     rc |= ba_alloc(b, &Q.xl, 3 * L);
     rc |= ba_alloc(b, &Q.tr, ns);
-    rc |= ba_alloc(b, &Q.scal, 4);
+    rc |= ba_alloc(b, &Q.scal, 16);
+    rc |= ba_alloc(b, &Q.e2, E);
     rc |= ba_alloc(b, &b->d_maxdiag, 1);
     if (rc == YV_OK && hipHostMalloc(reinterpret_cast<void**>(&b->h_scal), 4 * sizeof(double)) != hipSuccess)
         rc = YV_ERR_HIP;
@@ -788,10 +1147,10 @@ extern "C" int yv_ba_debug_read(yv_ba* b, int which, double* dst, int64_t count)
     if (!b || !b->ready || !dst || count < 0) return YV_ERR_INVALID;
     const yavo::BaParams& Q = b->P;
     double* const bufs[] = {Q.err, Q.Jp, Q.Jl, Q.Hpl, Q.W, Q.Hpp, Q.bp, Q.Hll, Q.bl, Q.Dinv, Q.S, Q.bs, Q.xp, Q.xl,
-                            Q.poses, Q.X};
+                            Q.poses, Q.X, Q.scal};
     const int64_t sizes[] = {2LL * Q.E, 12LL * Q.E, 6LL * Q.E, 18LL * Q.E, 18LL * Q.E, 36LL * Q.P, 6LL * Q.P,
                              9LL * Q.L, 3LL * Q.L, 9LL * Q.L, (int64_t)Q.ns * Q.ns, Q.ns, Q.ns, 3LL * Q.L,
-                             7LL * Q.P, 3LL * Q.L};
+                             7LL * Q.P, 3LL * Q.L, 16};
     if (which < 0 || which >= (int)(sizeof sizes / sizeof sizes[0]) || count > sizes[which]) return YV_ERR_INVALID;
     if (hipSetDevice(b->dev) != hipSuccess || hipStreamSynchronize(b->st) != hipSuccess) return YV_ERR_HIP;
     if (count && hipMemcpy(dst, bufs[which], sizeof(double) * count, hipMemcpyDeviceToHost) != hipSuccess)

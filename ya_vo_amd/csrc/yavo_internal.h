@@ -163,6 +163,7 @@ struct BaParams {
     double* xl = nullptr;             // [L][3]
     int32_t* tr = nullptr;            // [ns] LDLT transpositions
     double* scal = nullptr;           // [4]: chi2, scale, LDLT ok
+    double* e2 = nullptr;             // [E] squared error per edge
 };
 struct BaMat3 {
     double v[9];
