@@ -397,7 +397,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 __global__ __launch_bounds__(kLdltThreads) void ba_ldlt_lds_kernel(BaParams P) {
     __shared__ double Ls[kLdltMaxN * (kLdltMaxN + 1) / 2];  // the factor, for the solves
     __shared__ double colk[kLdltMaxN];  // L(i, k) of the current step
-    __shared__ double tc[kLdltMaxN];    // t_i = D(k) L(i, k)
+    __shared__ __attribute__((aligned(16))) double tc[kLdltMaxN];  // t_i = D(k) L(i, k)
     __shared__ double dg[kLdltMaxN];    // |diagonal|, permuted as the pivots are taken
     __shared__ int perm[kLdltMaxN];     // position -> original index: (P S P^T)(i, j) = S(perm[i], perm[j])
     __shared__ double s_akk;
@@ -531,11 +531,23 @@ __global__ __launch_bounds__(kLdltThreads) void ba_ldlt_lds_kernel(BaParams P) {
         // term k of every chain in this segment, and of the row's diagonal chain
         if (owner && my_i > k) {
             const double lik = colk[my_i];
-            if (cb + kLdltSeg - 1 > k) {
+            if (cb > k && cb + kLdltSeg <= my_i) {  // the whole segment is trailing: no per-column predicate
+                double tv[kLdltSeg];
+#pragma unroll
+                for (int u = 0; u < kLdltSeg; u += 2) {
+                    const double2 q = *reinterpret_cast<const double2*>(tc + cb + u);
+                    tv[u] = q.x;
+                    tv[u + 1] = q.y;
+                }
+#pragma unroll
+                for (int u = 0; u < kLdltSeg; ++u) L[u] = L[u] - lik * tv[u];
+            } else if (cb + kLdltSeg - 1 > k) {
 #pragma unroll
                 for (int u = 0; u < kLdltSeg; ++u) {
                     const int c = cb + u;
-                    if (c > k && c < my_i) L[u] = L[u] - lik * tc[c];
+                    const double tq = tc[c < kLdltMaxN ? c : 0];
+                    const double nv = L[u] - lik * tq;
+                    L[u] = (c > k && c < my_i) ? nv : L[u];
                 }
             }
             if (diag_owner) {
@@ -788,23 +800,36 @@ __global__ __launch_bounds__(256) void ba_chi2_kernel(BaParams P, BaMat3 K, doub
     double acc = 0.0;
     if (blockIdx.x == 0) {
         int e = t;
-        for (; e + 3 * kNT < P.E; e += 4 * kNT) {
-            const double v0 = P.e2[e], v1 = P.e2[e + kNT], v2 = P.e2[e + 2 * kNT], v3 = P.e2[e + 3 * kNT];
-            acc = acc + v0;
-            acc = acc + v1;
-            acc = acc + v2;
-            acc = acc + v3;
+        for (; e + 7 * kNT < P.E; e += 8 * kNT) {
+            double q[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) q[u] = P.e2[e + u * kNT];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc = acc + q[u];
         }
         for (; e < P.E; e += kNT) acc = acc + P.e2[e];
         const double v = tree256(acc, red);
         if (t == 0) P.scal[0] = v;
     } else if (with_scale) {
         const int ns = P.ns, nv = ns + 3 * P.L;
-        for (int j = t; j < nv; j += kNT) {
+        const double* bpf = P.bp + 6 * P.nf;
+        int j = t;
+        for (; j + 7 * kNT < nv; j += 8 * kNT) {
+            double x[8], b[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int q = j + u * kNT;
+                x[u] = q < ns ? P.xp[q] : P.xl[q - ns];
+                b[u] = q < ns ? bpf[q] : P.bl[q - ns];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc = acc + x[u] * (lambda * x[u] + b[u]);
+        }
+        for (; j < nv; j += kNT) {
             double x, b;
             if (j < ns) {
                 x = P.xp[j];
-                b = P.bp[6 * P.nf + j];
+                b = bpf[j];
             } else {
                 x = P.xl[j - ns];
                 b = P.bl[j - ns];
