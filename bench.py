@@ -6,8 +6,11 @@ for every frame, FAST-12 + Harris + top-2000 and blur + BRIEF on the left and ri
 matching L_{k-1} -> L_k (the reference's temporal matchFeatures, src/LoopHandler.cc:189,534) and L_k -> R_k
 (stereo), removeOutliers(20) on both match lists, then PnP: the kept stereo matches are triangulated
 (LoopHandler::triangulation) and the pose-only LM (LoopHandler::optimizePoseOnly) solves every frame's pose
-from the kept temporal matches.  `value` = stereo frames per second over all GPUs (max-over-ranks wall
-time).  One process per GPU; frames shard across ranks (weak scaling, no collective in the data path).
+from the kept temporal matches, and the chunk's shared-map block (keyframe poses + LM-inlier landmarks,
+include/yavo/yavo_map.h) is written after the LM.  `value` = stereo frames per second over all GPUs
+(max-over-ranks wall time).  One process per GPU; frames shard across ranks (weak scaling).  The only
+collective is the shared map's: every step the ranks all-gather their map blocks (RCCL over xGMI) on a
+communication stream and place them in world coordinates, overlapped with the next step's image kernels.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--frames B]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -45,6 +48,9 @@ def parse():
     ap.add_argument("--tracker", choices=["match", "lk"], default="match",
                     help="PnP correspondences: BRIEF temporal matches (default) or calcOpticalFlowPyrLK of frame "
                          "k-1's stereo map points (the reference's trackLastFrame)")
+    ap.add_argument("--kf-every", type=int, default=4,
+                    help="shared map: frames with global index %% kf_every == 0 are keyframes (their LM inliers "
+                         "become landmarks); 0 disables the map and its all-gather")
     return ap.parse_args()
 
 
@@ -192,9 +198,37 @@ def main():
     d_poses = [torch.zeros((NT, 7), dtype=torch.float64, device=dev) for _ in range(2)]
     calls = [0]
 
+    # shared map (include/yavo/yavo_map.h): this rank's chunk block after the LM, all-gathered over RCCL and
+    # placed in world coordinates on a communication stream; the next block write waits for the gather only
+    from ya_vo_amd import map as ymap
+    use_map = args.kf_every > 0 and args.tracker == "match"
+    first_frame = rank * B  # track k relates frame rank * B + k to its predecessor (the carry slot for k = 0)
+    if use_map:
+        max_kf = max(ymap.max_keyframes(NT, r * B, args.kf_every) for r in range(world))
+        max_kf = max(max_kf, 1)
+        bb = ymap.block_bytes(max_kf, MAX_KP)
+        d_block = torch.zeros(bb, dtype=torch.uint8, device=dev)
+        d_gathered = torch.zeros((world, bb), dtype=torch.uint8, device=dev) if world > 1 else d_block
+        d_base = torch.from_numpy(identity.copy()).to(dev)
+        d_anchors = torch.zeros((world, 7), dtype=torch.float64, device=dev)
+        comm = torch.cuda.Stream(device=dev)
+
     def step():
         batch.run(d_frames.data_ptr(), n_img, W, H * W, 20, carry_from=2 * (B - 1))
-        batch.track(d_prior.data_ptr(), d_poses[calls[0] & 1].data_ptr())
+        if not use_map:
+            batch.track(d_prior.data_ptr(), d_poses[calls[0] & 1].data_ptr())
+        else:
+            batch.track_map(d_prior.data_ptr(), d_poses[calls[0] & 1].data_ptr(), first_frame, args.kf_every,
+                            d_block.data_ptr(), max_kf)
+            batch.map_wait(comm.cuda_stream)
+            with torch.cuda.stream(comm):
+                if world > 1 and backend == "nccl":
+                    dist.all_gather_into_tensor(d_gathered, d_block)
+                elif world > 1:  # gloo rehearsal (YAVO_BENCH_BACKEND=gloo): list form
+                    dist.all_gather(list(d_gathered.unbind(0)), d_block)
+                ctx.map_place(d_gathered.data_ptr(), world, bb, d_base.data_ptr(), d_anchors.data_ptr(),
+                              stream=comm.cuda_stream)
+            batch.map_release(comm.cuda_stream)
         calls[0] += 1
 
     for _ in range(args.warmup):
@@ -319,7 +353,10 @@ def main():
         "config": {"workload": "configs[1] + PnP: FAST+BRIEF+Hamming match, 1241x376 synthetic stereo, 2000 "
                                "kp/image, stereo triangulation + pose-only LM per frame",
                    "H": H, "W": W, "max_kp": MAX_KP, "frames_per_step_per_gpu": B, "images_per_frame": 2,
-                   "match_pairs_per_frame": 2, "parallelism": f"frame-sharded x{world}, no collective",
+                   "match_pairs_per_frame": 2,
+                   "parallelism": f"frame-sharded x{world}" + (f", {'RCCL' if backend == 'nccl' else backend} "
+                                                                 "all-gather of shared-map blocks"
+                                                                 if use_map and world > 1 else ""),
                    "mean_candidates_per_image": round(float(np.mean(counts["cand"][:n_img])), 1),
                    "mean_keypoints_per_image": round(float(np.mean(counts["kp"][:n_img])), 1),
                    "mean_filtered_matches_per_pair": round(float(np.mean(counts["filt"])), 1),
@@ -333,6 +370,19 @@ def main():
         "roofline": roofline,
         "cpu_baseline": None,
     }
+    if use_map:
+        # the last placed map (rank 0's copy of every rank's block): its keyframes and landmarks per step
+        raw = d_gathered.cpu().numpy().reshape(world, bb)
+        n_kf = n_lm = 0
+        for r in range(world):
+            h, kfs, lms = ymap.parse_block(raw[r])
+            n_kf += int(h["n_kf"])
+            n_lm += sum(len(x) for x in lms)
+        out["shared_map"] = {"kf_every": args.kf_every, "block_bytes": bb, "keyframes_per_step": n_kf,
+                             "landmarks_per_step": n_lm, "allgather_bytes_per_rank_per_step": bb * world,
+                             "collective": ("none (1 rank)" if world == 1 else
+                                            "all_gather_into_tensor (RCCL)" if backend == "nccl" else
+                                            f"all_gather ({backend} rehearsal)")}
     if rank == 0 and world == 1 and args.cpu_baseline != "none" and args.tracker == "match":
         cb = cpu_baseline(args.cpu_baseline, args.cpu_threads, offsets.reshape(256, 4), frames, gpu_poses)
         main_cb = cb.get("literal") or cb.get("efficient")

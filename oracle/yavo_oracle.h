@@ -160,6 +160,12 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
 extern int or_ba_dump_iter;
 extern double* or_ba_dump[16];
 
+/* ---- shared map blocks (include/yavo/yavo_map.h; src/Map.cc:9-40) -- yavo_oracle_map.c ---- */
+int64_t or_map_block_bytes(int max_kf, int lm_stride);
+void or_map_chunk(const double* rel, int n, int64_t first_frame, int kf_every, const int32_t* edge_count,
+                  const double* edge_X, const uint8_t* edge_outlier, int max_kp, int max_kf, void* block);
+void or_map_place(void* blocks, int world, int64_t bb, double* base, double* anchors);
+
 #ifdef __cplusplus
 }
 #endif

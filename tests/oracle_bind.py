@@ -72,6 +72,9 @@ class Oracle:
             "or_recover_pose": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
             "or_ldlt_solve": (_I, [_P, _I, _P, _P]),
             "or_ba_lm": (_I, [_P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P]),
+            "or_map_block_bytes": (ctypes.c_int64, [_I, _I]),
+            "or_map_chunk": (None, [_P, _I, ctypes.c_int64, _I, _P, _P, _P, _I, _I, _P]),
+            "or_map_place": (None, [_P, _I, ctypes.c_int64, _P, _P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -361,3 +364,26 @@ class Oracle:
         it = self.lib.or_ba_lm(_p(T), len(T), n_fixed, _p(Xo), len(Xo), _p(ep), _p(el), _p(meas), len(ep), _p(K),
                                max_iters, _p(log))
         return T, Xo, it, log[:it + 1]
+
+    # ---- shared map blocks (include/yavo/yavo_map.h) ----
+    def map_block_bytes(self, max_kf, lm_stride):
+        return int(self.lib.or_map_block_bytes(max_kf, lm_stride))
+
+    def map_chunk(self, rel, first_frame, kf_every, edge_count, edge_X, edge_outlier, max_kp, max_kf):
+        """-> uint8 block. rel [n, 7]; edge_count [n]; edge_X [n, max_kp, 3]; edge_outlier [n, max_kp]."""
+        rel = np.ascontiguousarray(rel, np.float64).reshape(-1, 7)
+        n = len(rel)
+        ec = np.ascontiguousarray(edge_count, np.int32)
+        eX = np.ascontiguousarray(edge_X, np.float64).reshape(n, max_kp, 3)
+        eo = np.ascontiguousarray(edge_outlier, np.uint8).reshape(n, max_kp)
+        out = np.zeros(self.map_block_bytes(max_kf, max_kp), np.uint8)
+        self.lib.or_map_chunk(_p(rel), n, first_frame, kf_every, _p(ec), _p(eX), _p(eo), max_kp, max_kf, _p(out))
+        return out
+
+    def map_place(self, blocks, world, block_bytes, base):
+        """-> (placed blocks, new base, anchors [world, 7]); blocks = world blocks back to back (copied)."""
+        b = np.ascontiguousarray(blocks, np.uint8).reshape(-1).copy()
+        base = np.ascontiguousarray(base, np.float64).copy()
+        anchors = np.zeros((world, 7))
+        self.lib.or_map_place(_p(b), world, block_bytes, _p(base), _p(anchors))
+        return b, base, anchors

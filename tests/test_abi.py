@@ -13,7 +13,7 @@ import ya_vo_amd as yv
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADERS = [os.path.join(ROOT, "include", "yavo", h) for h in ("yavo.h", "yavo_types.h", "yavo_geom.h",
-                                                                       "yavo_io.h")]
+                                                                       "yavo_io.h", "yavo_map.h")]
 
 
 def _declared_functions():
@@ -39,7 +39,7 @@ def test_every_declared_symbol_is_exported(lib):
     assert len(declared) >= 20
     for name in sorted(declared):
         assert hasattr(lib, name), f"{name} declared in include/yavo but not exported"
-        assert name in yv.SIGNATURES or name in yv.GEOM_SIGNATURES or name in yv.IO_SIGNATURES, \
+        assert any(name in t for t in (yv.SIGNATURES, yv.GEOM_SIGNATURES, yv.IO_SIGNATURES, yv.MAP_SIGNATURES)), \
             f"{name} has no ctypes binding"
 
 

@@ -117,6 +117,16 @@ GEOM_SIGNATURES = {
     "yv_ba_destroy": (None, [_P]),
     "yv_ba_set_problem": (_I, [_P, _I, _I, _I, _P, _P, _P, _I, _P]),
     "yv_ba_solve": (_I, [_P, _P, _P, _I, _P, ctypes.POINTER(_I)]),
+    "yv_ba_debug_read": (_I, [_P, _I, _P, ctypes.c_int64]),
+}
+
+# include/yavo/yavo_map.h (the shared map; ya_vo_amd/map.py wraps the block layout)
+MAP_SIGNATURES = {
+    "yv_map_block_bytes": (ctypes.c_int64, [_I, _I]),
+    "yv_batch_track_map": (_I, [_P, _P, _P, ctypes.c_int64, _I, _P, _I, _P]),
+    "yv_batch_map_wait": (_I, [_P, _P]),
+    "yv_batch_map_release": (_I, [_P, _P]),
+    "yv_map_place": (_I, [_P, _P, _I, ctypes.c_int64, _P, _P, _P]),
 }
 
 # include/yavo/yavo_io.h (frame I/O and formats; ya_vo_amd/io.py wraps them)
@@ -155,7 +165,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         except ImportError:
             pass
     lib = ctypes.CDLL(path)
-    for name, (res, args) in list(SIGNATURES.items()) + list(GEOM_SIGNATURES.items()) + list(IO_SIGNATURES.items()):
+    tables = (SIGNATURES, GEOM_SIGNATURES, IO_SIGNATURES, MAP_SIGNATURES)
+    for name, (res, args) in [kv for t in tables for kv in t.items()]:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -178,6 +189,13 @@ def _f64(a, shape=None) -> np.ndarray:
 
 
 class _GeomMixin:
+    def map_place(self, d_blocks: int, world: int, block_bytes: int, d_base: int, d_anchors: int,
+                  stream: int = 0) -> None:
+        """Place gathered map blocks in world coordinates in place (yv_map_place)."""
+        _check(self.lib.yv_map_place(self.handle, ctypes.c_void_p(d_blocks), world, block_bytes,
+                                     ctypes.c_void_p(d_base), ctypes.c_void_p(d_anchors),
+                                     ctypes.c_void_p(stream) if stream else None), "yv_map_place")
+
     """Geometry rows (include/yavo/yavo_geom.h). Poses: Sophus SE3d::data() = {qx, qy, qz, qw, tx, ty, tz}."""
 
     def calc_optical_flow_pyr_lk(self, prev, nxt, pts, win=11, max_level=3, max_count=30, eps=0.01, min_eig=0.001):
@@ -427,6 +445,21 @@ class Batch:
     def track(self, d_priors: int, d_poses: int, stream: int = 0) -> None:
         _check(self.lib.yv_batch_track(self.handle, ctypes.c_void_p(d_priors), ctypes.c_void_p(d_poses),
                                        ctypes.c_void_p(stream) if stream else None), "yv_batch_track")
+
+    def track_map(self, d_priors: int, d_poses: int, first_frame: int, kf_every: int, d_block: int, max_kf: int,
+                  stream: int = 0) -> None:
+        """yv_batch_track + the chunk's shared-map block (yv_batch_track_map; layout in ya_vo_amd/map.py)."""
+        _check(self.lib.yv_batch_track_map(self.handle, ctypes.c_void_p(d_priors), ctypes.c_void_p(d_poses),
+                                           first_frame, kf_every, ctypes.c_void_p(d_block), max_kf,
+                                           ctypes.c_void_p(stream) if stream else None), "yv_batch_track_map")
+
+    def map_wait(self, stream: int) -> None:
+        """`stream` waits for the last map block (yv_batch_map_wait)."""
+        _check(self.lib.yv_batch_map_wait(self.handle, ctypes.c_void_p(stream)), "yv_batch_map_wait")
+
+    def map_release(self, stream: int) -> None:
+        """The next map block write waits for the work on `stream` so far (yv_batch_map_release)."""
+        _check(self.lib.yv_batch_map_release(self.handle, ctypes.c_void_p(stream)), "yv_batch_map_release")
 
     def set_track_overlap(self, on: bool = True) -> None:
         """Run each track's pose LM on the batch's own stream beside the next run (yv_batch_set_track_overlap)."""

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/yavo/yavo.h"
+#include "../../include/yavo/yavo_map.h"
 #include "yavo_internal.h"
 
 using yavo::Desc;
@@ -95,6 +96,10 @@ struct yv_batch {
     hipStream_t side = nullptr;
     hipEvent_t ev_edges[2] = {nullptr, nullptr}, ev_lm[2] = {nullptr, nullptr};
     bool lm_pending[2] = {false, false};
+    hipEvent_t ev_map = nullptr;    // after the last yv_batch_track_map's block (yv_batch_map_wait)
+    bool map_written = false;
+    hipEvent_t ev_map_release = nullptr;  // the block's readers (yv_batch_map_release): the next block write waits
+    bool map_release_pending = false;
     // stage timing: events 0..5 bracket the run's stages, 6..8 the track's
     bool timing = false;
     std::vector<hipEvent_t> events;  // kEvPerRun per recorded run
@@ -166,6 +171,8 @@ void batch_free(yv_batch* b) {
         if (b->ev_edges[k]) (void)hipEventDestroy(b->ev_edges[k]);
         if (b->ev_lm[k]) (void)hipEventDestroy(b->ev_lm[k]);
     }
+    if (b->ev_map) (void)hipEventDestroy(b->ev_map);
+    if (b->ev_map_release) (void)hipEventDestroy(b->ev_map_release);
     if (b->side) (void)hipStreamDestroy(b->side);
     delete b;
 }
@@ -612,7 +619,49 @@ int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks, int n_tracks, const 
     return YV_OK;
 }
 
+namespace {
+
+struct MapArgs {
+    int64_t first_frame;
+    int kf_every, max_kf;
+    void* block;
+};
+
+int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stream, const MapArgs* map);
+
+}  // namespace
+
 int yv_batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stream) {
+    return batch_track(b, d_priors, d_poses, stream, nullptr);
+}
+
+int yv_batch_track_map(yv_batch* b, const double* d_priors, double* d_poses, int64_t first_frame, int kf_every,
+                       void* d_block, int max_kf, void* stream) {
+    if (!b || !d_block || kf_every < 1 || max_kf < 1 || first_frame < 0) return YV_ERR_INVALID;
+    const MapArgs m{first_frame, kf_every, max_kf, d_block};
+    return batch_track(b, d_priors, d_poses, stream, &m);
+}
+
+int yv_batch_map_wait(yv_batch* b, void* stream) {
+    if (!b || !stream) return YV_ERR_INVALID;
+    if (!b->map_written) return YV_OK;
+    if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), b->ev_map, 0));
+    return YV_OK;
+}
+
+int yv_batch_map_release(yv_batch* b, void* stream) {
+    if (!b || !stream) return YV_ERR_INVALID;
+    if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+    if (!b->ev_map_release) YV_HIP(hipEventCreateWithFlags(&b->ev_map_release, hipEventDisableTiming));
+    YV_HIP(hipEventRecord(b->ev_map_release, reinterpret_cast<hipStream_t>(stream)));
+    b->map_release_pending = true;
+    return YV_OK;
+}
+
+namespace {
+
+int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stream, const MapArgs* map) {
     if (!b || (b->n_tracks > 0 && (!d_priors || !d_poses))) return YV_ERR_INVALID;
     if (b->n_tracks == 0) return YV_OK;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
@@ -663,6 +712,20 @@ int yv_batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* s
         YV_HIP(hipEventRecord(ev[8], ls));
         b->tracked[run] = 1;
     }
+    if (map) {
+        // the chunk's map block, after the LM on its stream: the build that next rewrites this edge buffer waits
+        // for ev_lm[k], recorded below, so it also waits for these reads. The block itself is rewritten only
+        // after its last reader released it (the all-gather of the previous chunk, yv_batch_map_release).
+        if (b->map_release_pending) {
+            YV_HIP(hipStreamWaitEvent(ls, b->ev_map_release, 0));
+            b->map_release_pending = false;
+        }
+        yavo::launch_map_chunk(d_poses, b->n_tracks, map->first_frame, map->kf_every, ec, eX, eo, b->max_kp,
+                               map->max_kf, map->block, ls);
+        if (!b->ev_map) YV_HIP(hipEventCreateWithFlags(&b->ev_map, hipEventDisableTiming));
+        YV_HIP(hipEventRecord(b->ev_map, ls));
+        b->map_written = true;
+    }
     if (b->overlap) {
         YV_HIP(hipEventRecord(b->ev_lm[k], ls));
         b->lm_pending[k] = true;
@@ -670,6 +733,8 @@ int yv_batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* s
     b->tbuf = k;
     return check_launch();
 }
+
+}  // namespace
 
 int yv_batch_set_track_overlap(yv_batch* b, int on) {
     if (!b) return YV_ERR_INVALID;

@@ -173,6 +173,11 @@ void launch_ba_landmark_reduce(const BaParams& P, unsigned long long* maxdiag, h
 void launch_ba_trial(const BaParams& P, const BaMat3& K, double lambda, hipStream_t s);
 void launch_ba_chi2(const BaParams& P, const BaMat3& K, hipStream_t s);
 
+// the shared map (yavo_map.hip): one chunk's block after its pose LM
+void launch_map_chunk(const double* rel, int n, int64_t first_frame, int kf_every, const int32_t* edge_count,
+                      const double* edge_X, const uint8_t* edge_outlier, int max_kp, int max_kf, void* block,
+                      hipStream_t s);
+
 void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, const double* edge_X,
                        const double* edge_uv, const double* K, const double* priors, double* poses,
                        uint8_t* edge_outlier, int32_t* inliers, hipStream_t s);
