@@ -1,0 +1,42 @@
+"""GPU parity of the full front end over a sequence (BASELINE configs[2] in miniature): detect / describe /
+match / PnP / shared map / local BA through libyavo (ya_vo_amd.sequence.SequenceFrontend) against the same loop
+over the CPU oracle (tests/sequence_chain.py): trajectories and refined landmarks bit for bit (the metric's "RMSE
+vs CPU ref" is 0), and the trajectory follows the synthetic ground truth."""
+import numpy as np
+import pytest
+
+from sequence_chain import ground_truth, oracle_sequence, rmse_translation
+from ya_vo_amd import scene
+from ya_vo_amd.sequence import SequenceFrontend, se3_inverse
+from ya_vo_amd.synth import synth_sequence
+
+pytestmark = pytest.mark.gpu
+
+T_RIGHT = np.array([0, 0, 0, 1, 0, -0.54, 0], np.float64)
+
+
+@pytest.mark.parametrize("n,chunk", [(8, 4), (12, 6)])
+def test_sequence_matches_oracle(ctx, oracle, offsets, n, chunk, tmp_path):
+    import torch
+    from ya_vo_amd import io as yio
+    frames = synth_sequence(71, n, stereo=True)  # [n, 2, H, W]
+    fe = SequenceFrontend(ctx, chunk, scene.K_KITTI, T_RIGHT)
+    d = torch.from_numpy(frames.reshape(2 * n, *frames.shape[2:])).to("cuda:0")
+    for c in range(n // chunk):
+        fe.process_chunk(d[2 * c * chunk:2 * (c + 1) * chunk])
+    traj = fe.trajectory()
+    ref, rec, log = oracle_sequence(oracle, frames, chunk, scene.K_KITTI, T_RIGHT, offsets, threads=8)
+    assert [x[:2] for x in fe.ba_log] == [x[:2] for x in log]
+    np.testing.assert_array_equal(np.array([x[2:] for x in fe.ba_log]), np.array([x[2:] for x in log]))
+    np.testing.assert_array_equal(traj, ref)
+    for g, r in rec.items():
+        np.testing.assert_array_equal(fe.records[g].edge, r.edge)
+        np.testing.assert_array_equal(fe.records[g].X, r.X)
+    assert rmse_translation(traj, ref) == 0.0
+    assert rmse_translation(traj, ground_truth(n, scene.K_KITTI)) < 0.02
+    # the KITTI pose file of the trajectory (T_wc rows) reads back
+    path = str(tmp_path / "poses.txt")
+    yio.write_kitti_poses(path, np.stack([se3_inverse(T) for T in traj]))
+    back = yio.read_kitti_poses(path)
+    np.testing.assert_allclose(back[:, :, 3], traj[:, 4:], atol=1e-9)
+    fe.close()

@@ -1,0 +1,71 @@
+"""CPU tests of the sequence front end's host logic (ya_vo_amd/sequence.py) and of its oracle restatement
+(tests/sequence_chain.py) on a short synthetic stereo sequence with a known trajectory (BASELINE configs[2]
+in miniature; the GPU run is tests/test_gpu_sequence.py)."""
+import numpy as np
+import pytest
+
+from sequence_chain import ground_truth, oracle_sequence, rmse_translation
+from ya_vo_amd import scene
+from ya_vo_amd.sequence import FrameRecord, apply_window, se3_inverse, window_problem
+from ya_vo_amd.synth import synth_frame
+
+T_RIGHT = np.array([0, 0, 0, 1, 0, -0.54, 0], np.float64)
+
+
+def test_se3_inverse(oracle):
+    rng = np.random.default_rng(0)
+    for _ in range(5):
+        T = oracle.se3_exp(rng.normal(0, 0.5, 6))
+        np.testing.assert_allclose(oracle.se3_mul(T, se3_inverse(T)), [0, 0, 0, 1, 0, 0, 0], atol=1e-12)
+        np.testing.assert_allclose(se3_inverse(se3_inverse(T)), T, atol=1e-12)
+
+
+def _records(oracle, n_frames, n_pts, noise, seed):
+    """Exact per-frame landmarks of a random scene seen by cameras moving along x, with noisy poses."""
+    rng = np.random.default_rng(seed)
+    K = scene.K_KITTI
+    truth = [np.concatenate([[0, 0, 0, 1.0], [0.5 * g, 0.0, 0.0]]) for g in range(n_frames)]  # T_wc
+    recs = {}
+    for g in range(n_frames):
+        pc = np.stack([rng.uniform(-8, 8, n_pts), rng.uniform(-3, 3, n_pts), rng.uniform(8, 30, n_pts)], 1)
+        Xw = np.array([oracle.se3_act(truth[g], p) for p in pc])
+        own = scene.project(se3_inverse(truth[g]), Xw, K)
+        prev = scene.project(se3_inverse(truth[g - 1]), Xw, K) if g else own
+        T0 = truth[g].copy()
+        if g >= 2:
+            T0[4:] += rng.normal(0, noise, 3)
+        recs[g] = FrameRecord(T0, np.arange(n_pts), Xw + rng.normal(0, noise, Xw.shape), prev, own)
+    return recs, truth
+
+
+def test_window_problem_layout(oracle):
+    recs, _ = _records(oracle, 4, 10, 0.0, 1)
+    poses, X, ep, el, meas, owners = window_problem(recs, [1, 2, 3], 1)
+    assert poses.shape == (3, 7) and X.shape == (20, 3)  # frame 1's predecessor is outside the window
+    assert owners == [(1, 0), (2, 10), (3, 10)]
+    assert list(ep[:10]) == [1] * 10 and list(ep[10:20]) == [0] * 10 and list(el[:10]) == list(range(10))
+    np.testing.assert_array_equal(meas[:10], recs[2].uv_own)
+    np.testing.assert_array_equal(meas[10:20], recs[2].uv_prev)
+
+
+def test_window_ba_recovers_truth(oracle):
+    recs, truth = _records(oracle, 6, 60, 0.02, 2)
+    frames = list(range(6))
+    poses, X, ep, el, meas, owners = window_problem(recs, frames, 2)
+    P, Xo, it, log = oracle.ba_lm(poses, 2, X, ep, el, meas, scene.K_KITTI, 20)
+    assert log[-1] < 1e-3 * log[0]
+    apply_window(recs, frames, P, Xo, owners)
+    for g in frames:
+        np.testing.assert_allclose(recs[g].T_wc[4:], truth[g][4:], atol=1e-3)
+
+
+def test_oracle_sequence_follows_ground_truth(oracle, offsets):
+    n, chunk = 8, 4
+    frames = np.stack([np.stack([synth_frame(61, k, 3 * k), synth_frame(61, k, 3 * k + 8)]) for k in range(n)])
+    traj, records, ba_log = oracle_sequence(oracle, frames, chunk, scene.K_KITTI, T_RIGHT,
+                                            offsets.reshape(256, 4), threads=8)
+    assert traj.shape == (n, 7) and len(ba_log) == 2
+    assert all(last_chi2 <= first_chi2 for _, _, first_chi2, last_chi2 in ba_log)
+    gt = ground_truth(n, scene.K_KITTI)
+    assert rmse_translation(traj, gt) < 0.02
+    assert sum(len(r.edge) for r in records.values()) > 1000

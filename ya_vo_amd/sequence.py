@@ -1,0 +1,186 @@
+"""The full front end over a stereo sequence (BASELINE configs[2]: "full Frontend incl. 3DHandler PnP + local-BA
+Optimizer, first 200 frames"), driven the way LoopHandler drives its loop (src/LoopHandler.cc:60-165):
+
+  per chunk of B stereo frames, on the device (one yv_batch, carry slot = the previous chunk's last frame):
+    detect + describe L / R, match L_{k-1} -> L_k and L_k -> R_k, removeOutliers(20)  (yv_batch_run)
+    stereo triangulation + pose-only LM per frame, the chunk's map block              (yv_batch_track_map)
+    placement of the block in world coordinates after the previous chunk             (yv_map_place)
+  then the local BA (the keyframe window the reference's Optimizer::partialBA stands for, src/Optimizer.cc:17-60,
+  solved as g2o's BlockSolver_6_3 LM would, yv_ba) over the chunk's frames plus the `n_fixed` frames before it
+  (held fixed: they were refined with the previous chunk and pin the gauge and the scale): every landmark of frame k
+  (its pose-LM inliers, X_w from the map) observed in frame k (its left keypoint) and frame k-1 (the PnP
+  measurement); the refined poses replace the trajectory's and the last one anchors the next chunk.
+
+Host logic only (the window assembly and SE3 inversion are numpy); every compute step is a libyavo kernel.
+tests/sequence_chain.py restates the same loop over the CPU oracle for the trajectory check.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+from . import map as ymap
+from .scene import quat_to_R
+
+IDENTITY = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
+
+
+def se3_inverse(T) -> np.ndarray:
+    """Sophus SE3d::inverse on data() = {qx, qy, qz, qw, tx, ty, tz}: q* and -R^T t."""
+    T = np.asarray(T, np.float64)
+    q = np.array([-T[0], -T[1], -T[2], T[3]])
+    t = -(quat_to_R(T[:4]).T @ T[4:])
+    return np.concatenate([q, t])
+
+
+@dataclass
+class FrameRecord:
+    """One frame's share of the map: T_wc, its landmarks (edge index, X_w) and their two observations."""
+    T_wc: np.ndarray
+    edge: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))
+    X: np.ndarray = field(default_factory=lambda: np.zeros((0, 3)))
+    uv_prev: np.ndarray = field(default_factory=lambda: np.zeros((0, 2)))  # in frame k-1 (the PnP measurement)
+    uv_own: np.ndarray = field(default_factory=lambda: np.zeros((0, 2)))   # in frame k (its left keypoint)
+
+
+def frame_records_from_block(block: np.ndarray, edge_uv: np.ndarray, edge_query: np.ndarray,
+                             own_px: np.ndarray) -> Dict[int, FrameRecord]:
+    """Placed map block + the chunk's edge arrays -> per-frame records. edge_uv [n, max_kp, 2] and edge_query
+    [n, max_kp] per track (track k = frame first_frame + k); own_px [n, max_kp, 2] = the frame-k keypoint the
+    query's temporal match selected (Matches::pt2, row / col)."""
+    h, kfs, lms = ymap.parse_block(block)
+    first = int(h["first_frame"])
+    out = {}
+    for kf, lm in zip(kfs, lms):
+        g = int(kf["frame_id"])
+        k = g - first
+        e = (lm["id"] & 0xFFFF).astype(np.int64)
+        q = edge_query[k, e]
+        out[g] = FrameRecord(np.array(kf["T"], np.float64), e, np.array(lm["X"], np.float64),
+                             edge_uv[k, e].astype(np.float64), own_px[k, q].astype(np.float64))
+    return out
+
+
+def window_problem(records: Dict[int, FrameRecord], frames: List[int], n_fixed: int):
+    """BA problem over consecutive `frames` (oldest first): poses T_cw, landmarks of frames whose predecessor is in
+    the window (two observations each), edges (pose index, landmark index, meas). -> (poses, X, ep, el, meas,
+    landmark owner [(frame, count)])."""
+    index = {g: i for i, g in enumerate(frames)}
+    poses = np.stack([se3_inverse(records[g].T_wc) for g in frames])
+    Xs, ep, el, meas, owners = [], [], [], [], []
+    base = 0
+    for g in frames:
+        r = records[g]
+        n = len(r.edge)
+        if g - 1 not in index or n == 0:
+            owners.append((g, 0))
+            continue
+        ids = np.arange(base, base + n, dtype=np.int32)
+        Xs.append(r.X)
+        ep += [np.full(n, index[g], np.int32), np.full(n, index[g - 1], np.int32)]
+        el += [ids, ids]
+        meas += [r.uv_own, r.uv_prev]
+        owners.append((g, n))
+        base += n
+    if not Xs:
+        return poses, np.zeros((0, 3)), np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros((0, 2)), owners
+    return (poses, np.concatenate(Xs), np.concatenate(ep), np.concatenate(el), np.concatenate(meas), owners)
+
+
+def apply_window(records: Dict[int, FrameRecord], frames: List[int], poses: np.ndarray, X: np.ndarray,
+                 owners) -> None:
+    """Write a solved window back: T_wc = inverse(T_cw) per frame, refined landmarks per owning frame."""
+    for g, T in zip(frames, poses):
+        records[g].T_wc = se3_inverse(T)
+    base = 0
+    for g, n in owners:
+        if n:
+            records[g].X = X[base:base + n].copy()
+            base += n
+
+
+class SequenceFrontend:
+    """The device front end over a stereo sequence in chunks of `chunk` frames (module docstring)."""
+
+    def __init__(self, ctx, chunk: int, K, T_right, n_fixed: int = 2, ba_iters: int = 10,
+                 H: int = 376, W: int = 1241, max_kp: int = 2000, match_thr: int = 20):
+        import torch
+        from . import Batch, BundleAdjuster
+        if chunk < 2 or n_fixed < 1:
+            raise ValueError("bad chunk / n_fixed")
+        window = chunk + n_fixed
+        self.ctx, self.chunk, self.H, self.W, self.max_kp = ctx, chunk, H, W, max_kp
+        self.K = np.asarray(K, np.float64)
+        self.window, self.n_fixed, self.ba_iters, self.match_thr = window, n_fixed, ba_iters, match_thr
+        self.batch = Batch(ctx, 2 * chunk, H, W, max_kp, 2 * chunk)
+        carry = 2 * chunk
+        pairs, tracks = [], []
+        for k in range(chunk):
+            pairs.append((carry if k == 0 else 2 * (k - 1), 2 * k))  # temporal L_{k-1} -> L_k
+            pairs.append((2 * k, 2 * k + 1))                          # stereo L_k -> R_k
+            tracks.append((2 * k + 1, 2 * k))
+        self.batch.set_pairs(pairs)
+        self.batch.set_tracks(tracks, self.K, T_right)
+        dev = torch.device("cuda", ctx.device)
+        self.bb = ymap.block_bytes(chunk, max_kp)
+        self.d_block = torch.zeros(self.bb, dtype=torch.uint8, device=dev)
+        self.d_base = torch.from_numpy(IDENTITY.copy()).to(dev)
+        self.d_anchors = torch.zeros((1, 7), dtype=torch.float64, device=dev)
+        self.d_prior = torch.from_numpy(np.tile(IDENTITY, (chunk, 1))).to(dev)
+        self.d_poses = torch.zeros((chunk, 7), dtype=torch.float64, device=dev)
+        self.ba = BundleAdjuster(ctx, window, window * max_kp, 2 * window * max_kp)
+        self.records: Dict[int, FrameRecord] = {}
+        self.next_frame = 0
+        self.ba_log: List[Tuple[int, int, float, float]] = []  # (last frame, iterations, chi2 first, chi2 last)
+
+    def close(self) -> None:
+        self.ba.close()
+        self.batch.close()
+
+    def process_chunk(self, d_images, seconds: Dict[str, float] = None) -> None:
+        """d_images: device uint8 [2 * chunk, H, W] (L_k, R_k interleaved) of frames next_frame ..."""
+        import time
+        ctx, n, kp = self.ctx, self.chunk, self.max_kp
+        t0 = time.perf_counter()
+        first = self.next_frame
+        self.batch.run(d_images.data_ptr(), 2 * n, self.W, self.H * self.W, self.match_thr,
+                       carry_from=2 * (n - 1))
+        self.batch.track_map(self.d_prior.data_ptr(), self.d_poses.data_ptr(), first, 1, self.d_block.data_ptr(), n)
+        ctx.map_place(self.d_block.data_ptr(), 1, self.bb, self.d_base.data_ptr(), self.d_anchors.data_ptr())
+        ctx.sync()
+        t1 = time.perf_counter()
+        v = self.batch.view()
+        block = ctx.download(self.d_block.data_ptr(), np.uint8, self.bb)
+        uv = ctx.download(v.edge_uv, np.float64, n * kp * 2).reshape(n, kp, 2)
+        q = ctx.download(v.edge_query, np.int32, n * kp).reshape(n, kp)
+        m = ctx.download(v.matches, np.uint8, 2 * n * kp * 100).reshape(2 * n, kp, 100)[0::2]
+        own = m[:, :, 48:56].copy().view(np.int32).reshape(n, kp, 2)  # Matches::pt2.{x, y}
+        t2 = time.perf_counter()
+        self.records.update(frame_records_from_block(block, uv, q, own))
+        self.next_frame = first + n
+        self._local_ba()
+        t3 = time.perf_counter()
+        if seconds is not None:
+            for key, dt in (("device", t1 - t0), ("download", t2 - t1), ("ba", t3 - t2)):
+                seconds[key] = seconds.get(key, 0.0) + dt
+
+    def _local_ba(self) -> None:
+        last = self.next_frame - 1
+        frames = list(range(max(0, last - self.window + 1), last + 1))
+        if len(frames) <= self.n_fixed:
+            return
+        poses, X, ep, el, meas, owners = window_problem(self.records, frames, self.n_fixed)
+        if len(ep) == 0:
+            return
+        self.ba.set_problem(len(frames), self.n_fixed, len(X), ep, el, meas, self.K)
+        poses, X, log, it = self.ba.solve(poses, X, self.ba_iters)
+        apply_window(self.records, frames, poses, X, owners)
+        self.ba_log.append((last, it, float(log[0]), float(log[-1])))
+        # the next chunk is placed after the refined last pose
+        self.ctx.upload(self.d_base.data_ptr(), self.records[last].T_wc)
+
+    def trajectory(self) -> np.ndarray:
+        """[n_frames, 7] T_wc in frame order."""
+        return np.stack([self.records[g].T_wc for g in sorted(self.records)])
