@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-timing", action="store_true", help="do not record per-stage HIP events")
     ap.add_argument("--no-overlap", action="store_true", help="run the pose LM in order on the main stream")
+    ap.add_argument("--overlap-mode", type=int, default=1, choices=[1, 2, 3],
+                    help="pose LM beside the next step: 1 after the edge build, 2 / 3 after the next detect / describe")
     ap.add_argument("--tracker", choices=["match", "lk"], default="match",
                     help="PnP correspondences: BRIEF temporal matches (default) or calcOpticalFlowPyrLK of frame "
                          "k-1's stereo map points (the reference's trackLastFrame)")
@@ -194,7 +196,7 @@ def main():
     d_prior = torch.from_numpy(np.tile(identity, (NT, 1))).to(dev)
     # the pose LM of step i runs on the batch's side stream beside step i + 1's image kernels; its output
     # buffer alternates so step i + 1 never writes poses step i's LM is still producing
-    batch.set_track_overlap(not args.no_overlap)
+    batch.set_track_overlap(0 if args.no_overlap else args.overlap_mode)
     d_poses = [torch.zeros((NT, 7), dtype=torch.float64, device=dev) for _ in range(2)]
     calls = [0]
 

@@ -118,7 +118,10 @@ int yv_batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* s
 /* Overlap mode: the pose LM of each yv_batch_track runs on a stream of the batch, ordered after that call's
  * edge build only, so it executes beside the next yv_batch_run's kernels (edge buffers alternate between
  * two copies; the build of track i + 2 waits for the LM of track i).  d_priors / d_poses / the track views
- * are then complete only after yv_batch_track_sync (or a device-wide synchronization). */
+ * are then complete only after yv_batch_track_sync (or a device-wide synchronization).  on = 2 / 3 defer each
+ * LM further: it is launched by the next yv_batch_run once that run's detect (2) / describe (3) stage is issued
+ * (so it runs beside the later, less occupancy-sensitive stages), or by yv_batch_track_sync /
+ * yv_batch_map_wait / the next yv_batch_track, whichever comes first. */
 int yv_batch_set_track_overlap(yv_batch* b, int on);
 int yv_batch_track_sync(yv_batch* b);
 /* LK tracking mode, the reference's trackLastFrame (src/LoopHandler.cc:298-454): with image_step > 0 a track

@@ -55,6 +55,10 @@ int yv_pose_gn(struct yv_ctx* ctx, const double* X, const double* uv, int n, con
 int yv_pose_lm_batch(struct yv_ctx* ctx, int n_problems, const int32_t* d_offsets, const double* d_X,
                      const double* d_uv, const double* d_K, double* d_poses, uint8_t* d_outlier,
                      int32_t* d_inliers, void* stream);
+/* The order in which the pose-LM kernel sums over edges, as the oracle's sum_mode (oracle/yavo_oracle.h:
+ * 4 / 5 / 6 = 64- / 128- / 256-thread workgroups; YAVO_LM_THREADS selects, default 256). Results are bit-identical
+ * to the oracle in that order and within 1e-9 of the reference's sequential order. */
+int yv_lm_sum_mode(void);
 int yv_pose_gn_batch(struct yv_ctx* ctx, int n_problems, const int32_t* d_offsets, const double* d_X,
                      const double* d_uv, const double* d_K, double* d_poses, int32_t* d_iterations, void* stream);
 /* F-RANSAC over n_lists match lists: list l = d_matches + l*list_stride, d_counts[l] entries, samples

@@ -729,13 +729,14 @@ static void edge_jacobian(const double* T, const double* K, const double* X, dou
  * partial.  Mode 1 then sums the pairwise tree p[t] += p[t + off] for off = NT/2 .. 1.  Mode 2 (512 threads)
  * and mode 3 (256 threads, the pose-LM kernel) halve once (p[t] += p[t + NT/2]), sum each of 16 runs of
  * NT/32 partials left to right (q[s] = p[Rs] + p[Rs+1] + ... , R = NT/32) and finish with the tree
- * q[s] += q[s + off], off = 8, 4, 2, 1. */
+ * q[s] += q[s + off], off = 8, 4, 2, 1.  Modes 4, 5, 6 (the pose-LM kernel at 64, 128, 256 threads): the halving
+ * tree p[l] += p[l + off], off = 32 .. 1, inside each 64-thread wave, then the wave totals left to right. */
 #define OR_NT_MAX 1024
 typedef struct { int mode, nt; double part[OR_NT_MAX]; } or_sum;
 
 static void sum_reset(or_sum* s, int mode) {
     s->mode = mode;
-    s->nt = mode == 3 ? 256 : mode >= 1 ? 128 << mode : 1;
+    s->nt = mode >= 4 ? 64 << (mode - 4) : mode == 3 ? 256 : mode >= 1 ? 128 << mode : 1;
     memset(s->part, 0, sizeof(double) * (size_t)s->nt);
 }
 /* term of edge index k (in the active-edge order) */
@@ -747,6 +748,16 @@ static double sum_total(or_sum* s) {
     if (s->mode == 0) return s->part[0];
     double p[OR_NT_MAX];
     memcpy(p, s->part, sizeof(double) * (size_t)s->nt);
+    if (s->mode >= 4) {
+        double tot = 0.0;
+        for (int w = 0; w < s->nt / 64; ++w) {
+            double* q = p + 64 * w;
+            for (int off = 32; off > 0; off >>= 1)
+                for (int t = 0; t < off; ++t) q[t] = q[t] + q[t + off];
+            tot = w == 0 ? q[0] : tot + q[0];
+        }
+        return tot;
+    }
     if (s->mode == 2 || s->mode == 3) {
         /* segmented: NT threads, halve once, 16 runs of NT/32 partials summed left to right, tree over runs */
         const int half = s->nt / 2, run = half / 16;

@@ -11,7 +11,7 @@ from ya_vo_amd import MATCH_DTYPE, scene
 pytestmark = pytest.mark.gpu
 
 POSE_TOL = 1e-9  # |pose_gpu - pose_reference_order| (quaternion + translation), stated in DESIGN.md
-LM_ORDER = 3     # the pose-LM kernel's edge-sum order: 256-thread segmented (oracle sum_mode 3)
+LM_ORDER = yv.lm_sum_mode()  # the pose-LM kernel's edge-sum order (oracle sum_mode 4 / 5 / 6, yv_lm_sum_mode)
 GN_ORDER = 1     # the GN kernel's: 256-thread tree
 
 

@@ -37,7 +37,7 @@ def _edges(ctx, b, n):
     return ec, eX, eo
 
 
-@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("overlap", [0, 1, 2, 3])
 def test_map_blocks_and_place_match_oracle(ctx, oracle, overlap):
     import torch
     n, every = 4, 2

@@ -171,7 +171,7 @@ def test_ldlt6(oracle):
         assert not pos
 
 
-@pytest.mark.parametrize("sum_mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("sum_mode", [0, 1, 2, 3, 4, 5, 6])
 def test_pose_lm_noise_free(oracle, sum_mode):
     X, uv, T_true, _ = scene.random_scene(300, seed=9)
     prior = scene.perturb(T_true, np.random.default_rng(1))
@@ -180,11 +180,12 @@ def test_pose_lm_noise_free(oracle, sum_mode):
     np.testing.assert_allclose(scene.project(T, X), uv, atol=1e-6)
 
 
-def test_pose_lm_outliers_and_sum_orders(oracle):
+@pytest.mark.parametrize("order", [3, 4, 5, 6])
+def test_pose_lm_outliers_and_sum_orders(oracle, order):
     X, uv, T_true, gross = scene.random_scene(800, seed=10, noise_px=0.5, outlier_frac=0.1)
     prior = scene.perturb(T_true, np.random.default_rng(2))
     T0, out0, inl0 = oracle.pose_lm(X, uv, scene.K_KITTI, prior, 0)
-    T1, out1, inl1 = oracle.pose_lm(X, uv, scene.K_KITTI, prior, 3)
+    T1, out1, inl1 = oracle.pose_lm(X, uv, scene.K_KITTI, prior, order)
     assert np.all(out0[gross])               # every gross outlier (>= 20 px) is flagged
     assert inl0 >= 800 - int(0.1 * 800) - 40  # chi2 > 5.991 also flags some 0.5-px noise tails
     np.testing.assert_array_equal(out0, out1)

@@ -9,7 +9,9 @@ the frame-(k-1) measurements.
 """
 import numpy as np
 
-from ya_vo_amd import MATCH_DTYPE
+from ya_vo_amd import MATCH_DTYPE, lm_sum_mode
+
+lm_sum_mode_default = lm_sum_mode  # the pose-LM kernel's edge-sum order (yv_lm_sum_mode)
 
 IDENTITY = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
 
@@ -47,17 +49,22 @@ def track_edges(orc, kq, kl, kr, K, T_right, thr=20):
     return X[ok], uv, q
 
 
-def track_pose(orc, kq, kl, kr, K, T_right, prior=IDENTITY, thr=20, sum_mode=3):
+def track_pose(orc, kq, kl, kr, K, T_right, prior=IDENTITY, thr=20, sum_mode=None):
+    if sum_mode is None:
+        sum_mode = lm_sum_mode()
     X, uv, q = track_edges(orc, kq, kl, kr, K, T_right, thr)
     T, out, inl = orc.pose_lm(X, uv, K, prior, sum_mode)
     return X, uv, q, T, out, inl
 
 
-def lk_track_pose(orc, img_prev, img_next, kl, kr, K, T_right, prior=IDENTITY, thr=20, lk_sum_mode=1, lm_sum_mode=3):
+def lk_track_pose(orc, img_prev, img_next, kl, kr, K, T_right, prior=IDENTITY, thr=20, lk_sum_mode=1,
+                  lm_sum_mode=None):
     """The reference's trackLastFrame + optimizePoseOnly (src/LoopHandler.cc:298-454, 730-861) with frame k-1's
     map points from its stereo pair: kept stereo matches triangulated (left camera = world), tracked by
     calcOpticalFlowPyrLK into frame k, status-1 points at cv::Point2i(next.y, next.x) (truncation).
     -> (X [n,3], uv [n,2], query index [n], T, outlier, inliers)."""
+    if lm_sum_mode is None:
+        lm_sum_mode = lm_sum_mode_default()
     if len(kl) == 0:
         e = np.zeros((0, 3)), np.zeros((0, 2)), np.zeros(0, np.int32)
         return (*e, *orc.pose_lm(e[0], e[1], K, prior, lm_sum_mode))

@@ -118,6 +118,7 @@ GEOM_SIGNATURES = {
     "yv_ba_set_problem": (_I, [_P, _I, _I, _I, _P, _P, _P, _I, _P]),
     "yv_ba_solve": (_I, [_P, _P, _P, _I, _P, ctypes.POINTER(_I)]),
     "yv_ba_debug_read": (_I, [_P, _I, _P, ctypes.c_int64]),
+    "yv_lm_sum_mode": (_I, []),
 }
 
 # include/yavo/yavo_map.h (the shared map; ya_vo_amd/map.py wraps the block layout)
@@ -172,6 +173,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def lm_sum_mode() -> int:
+    """The pose-LM kernel's edge-sum order as the oracle's sum_mode (yv_lm_sum_mode; parity tests use it)."""
+    return int(load_library().yv_lm_sum_mode())
 
 
 def _check(status: int, what: str) -> None:
@@ -461,9 +467,12 @@ class Batch:
         """The next map block write waits for the work on `stream` so far (yv_batch_map_release)."""
         _check(self.lib.yv_batch_map_release(self.handle, ctypes.c_void_p(stream)), "yv_batch_map_release")
 
-    def set_track_overlap(self, on: bool = True) -> None:
-        """Run each track's pose LM on the batch's own stream beside the next run (yv_batch_set_track_overlap)."""
-        _check(self.lib.yv_batch_set_track_overlap(self.handle, 1 if on else 0), "yv_batch_set_track_overlap")
+    def set_track_overlap(self, on=True) -> None:
+        """Run each track's pose LM on the batch's own stream beside the next run (yv_batch_set_track_overlap):
+        True / 1 after the edge build, 2 / 3 deferred until the next run's detect / describe stage, False / 0 in
+        order."""
+        mode = int(on) if not isinstance(on, bool) else (1 if on else 0)
+        _check(self.lib.yv_batch_set_track_overlap(self.handle, mode), "yv_batch_set_track_overlap")
 
     def set_track_lk(self, image_step: int, win: int = 11, max_level: int = 3, max_count: int = 30, eps: float = 0.01,
                      min_eig: float = 0.001) -> None:

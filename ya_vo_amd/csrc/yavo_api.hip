@@ -93,6 +93,19 @@ struct yv_batch {
     int tbuf = 0;                   // buffer of the last yv_batch_track
     int track_calls = 0;
     bool overlap = false;           // LM on the side stream
+    int overlap_mode = 0;           // 1: LM after the edge build; 2 / 3: after the next run's detect / describe
+    struct DeferredLM {              // overlap modes 2 / 3: an LM launch waiting for the next yv_batch_run
+        bool active = false;
+        int k = 0, run = -1;
+        const double* priors = nullptr;
+        double* poses = nullptr;
+        hipEvent_t* ev = nullptr;   // stage timing events of the run the track belongs to
+        bool has_map = false;
+        int64_t first_frame = 0;
+        int kf_every = 1, max_kf = 1;
+        void* block = nullptr;
+    } deferred;
+    hipEvent_t ev_defer = nullptr;
     hipStream_t side = nullptr;
     hipEvent_t ev_edges[2] = {nullptr, nullptr}, ev_lm[2] = {nullptr, nullptr};
     bool lm_pending[2] = {false, false};
@@ -172,6 +185,7 @@ void batch_free(yv_batch* b) {
         if (b->ev_lm[k]) (void)hipEventDestroy(b->ev_lm[k]);
     }
     if (b->ev_map) (void)hipEventDestroy(b->ev_map);
+    if (b->ev_defer) (void)hipEventDestroy(b->ev_defer);
     if (b->ev_map_release) (void)hipEventDestroy(b->ev_map_release);
     if (b->side) (void)hipStreamDestroy(b->side);
     delete b;
@@ -449,6 +463,11 @@ int yv_batch_stage_times(yv_batch* b, float* ms, int* n_runs) {
     return YV_OK;
 }
 
+namespace {
+int launch_deferred_after(yv_batch* b, hipStream_t s);
+int flush_deferred(yv_batch* b);
+}  // namespace
+
 int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride, int64_t image_pitch, int match_thr,
                  int carry_from, void* stream) {
     if (!b || !d_images || n_images <= 0 || n_images > b->max_images || stride < b->W ||
@@ -475,11 +494,13 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
     yavo::launch_detect_blur(d_images, n_images, H, W, stride, image_pitch, ctx->fast_thr, b->cand_keys, b->cap,
                              b->cand_count, ctx->k9, b->blur, s);
     rc |= record_stage(b, s, run, 1);
+    if (b->overlap_mode == 2) rc |= launch_deferred_after(b, s);
     yavo::launch_topk(b->cand_keys, b->cap, b->cand_count, b->cand_seen, n_images, H, W, K, keep, b->det_rc,
                       b->det_resp, b->det_count, b->kp_src, b->kp_count, s);
     rc |= record_stage(b, s, run, 2);
     yavo::launch_brief(b->blur, n_images, H, W, ctx->d_offsets, b->kp_src, b->kp_count, K, b->keypoints, b->desc, s);
     rc |= record_stage(b, s, run, 3);
+    if (b->overlap_mode == 3) rc |= launch_deferred_after(b, s);
     if (b->n_pairs > 0) {
         yavo::launch_match(b->desc, b->kp_count, b->pairs, b->n_pairs, K, b->match_key, s);
         rc |= record_stage(b, s, run, 4);
@@ -629,6 +650,67 @@ struct MapArgs {
 
 int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stream, const MapArgs* map);
 
+// The pose LM (and the map block) of one track. Overlap: on the side stream after the edge build (ev_edges[k]);
+// otherwise on `s`, in order.
+int launch_lm(yv_batch* b, const yv_batch::DeferredLM& L, hipStream_t s) {
+    const int k = L.k;
+    const size_t nt = (size_t)b->max_tracks, nk = (size_t)b->max_kp;
+    double* eX = b->edge_X + k * nt * nk * 3;
+    double* euv = b->edge_uv + k * nt * nk * 2;
+    int32_t* ec = b->edge_count + k * nt;
+    uint8_t* eo = b->edge_outlier + k * nt * nk;
+    int32_t* inl = b->track_inliers + k * nt;
+    hipStream_t ls = s;
+    if (b->overlap) {
+        // the LM reads only this track's edge buffer, priors and poses: it runs on the side stream beside the
+        // next batch's image kernels (which overwrite keypoints / matches, already consumed by the build)
+        YV_HIP(hipStreamWaitEvent(b->side, b->ev_edges[k], 0));
+        ls = b->side;
+    }
+    if (L.ev) YV_HIP(hipEventRecord(L.ev[7], ls));
+    yavo::launch_track_pose(b->n_tracks, ec, b->max_kp, eX, euv, b->track_K, L.priors, L.poses, eo, inl, ls);
+    if (L.ev) {
+        YV_HIP(hipEventRecord(L.ev[8], ls));
+        b->tracked[L.run] = 1;
+    }
+    if (L.has_map) {
+        // the chunk's map block, after the LM on its stream: the build that next rewrites this edge buffer waits
+        // for ev_lm[k], recorded below, so it also waits for these reads. The block itself is rewritten only
+        // after its last reader released it (the all-gather of the previous chunk, yv_batch_map_release).
+        if (b->map_release_pending) {
+            YV_HIP(hipStreamWaitEvent(ls, b->ev_map_release, 0));
+            b->map_release_pending = false;
+        }
+        yavo::launch_map_chunk(L.poses, b->n_tracks, L.first_frame, L.kf_every, ec, eX, eo, b->max_kp, L.max_kf,
+                               L.block, ls);
+        if (!b->ev_map) YV_HIP(hipEventCreateWithFlags(&b->ev_map, hipEventDisableTiming));
+        YV_HIP(hipEventRecord(b->ev_map, ls));
+        b->map_written = true;
+    }
+    if (b->overlap) {
+        YV_HIP(hipEventRecord(b->ev_lm[k], ls));
+        b->lm_pending[k] = true;
+    }
+    return YV_OK;
+}
+
+// The deferred LM of the previous track, ordered after the work issued on s so far (the stage it waits for).
+int launch_deferred_after(yv_batch* b, hipStream_t s) {
+    if (!b->deferred.active) return YV_OK;
+    if (!b->ev_defer) YV_HIP(hipEventCreateWithFlags(&b->ev_defer, hipEventDisableTiming));
+    YV_HIP(hipEventRecord(b->ev_defer, s));
+    YV_HIP(hipStreamWaitEvent(b->side, b->ev_defer, 0));
+    b->deferred.active = false;
+    return launch_lm(b, b->deferred, s) == YV_OK ? YV_OK : YV_ERR_HIP;
+}
+
+// Launch a deferred LM now (its inputs are complete once ev_edges was recorded).
+int flush_deferred(yv_batch* b) {
+    if (!b->deferred.active) return YV_OK;
+    b->deferred.active = false;
+    return launch_lm(b, b->deferred, b->ctx->stream);
+}
+
 }  // namespace
 
 int yv_batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stream) {
@@ -644,8 +726,9 @@ int yv_batch_track_map(yv_batch* b, const double* d_priors, double* d_poses, int
 
 int yv_batch_map_wait(yv_batch* b, void* stream) {
     if (!b || !stream) return YV_ERR_INVALID;
-    if (!b->map_written) return YV_OK;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+    if (flush_deferred(b) != YV_OK) return YV_ERR_HIP;  // the block is written after the LM
+    if (!b->map_written) return YV_OK;
     YV_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), b->ev_map, 0));
     return YV_OK;
 }
@@ -666,14 +749,13 @@ int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stre
     if (b->n_tracks == 0) return YV_OK;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->ctx->stream;
+    if (flush_deferred(b) != YV_OK) return YV_ERR_HIP;  // two tracks without a run between them
     const int k = b->track_calls++ & 1;
     const size_t nt = (size_t)b->max_tracks, nk = (size_t)b->max_kp;
     double* eX = b->edge_X + k * nt * nk * 3;
     double* euv = b->edge_uv + k * nt * nk * 2;
     int32_t* eq = b->edge_query + k * nt * nk;
     int32_t* ec = b->edge_count + k * nt;
-    uint8_t* eo = b->edge_outlier + k * nt * nk;
-    int32_t* inl = b->track_inliers + k * nt;
     const int run = b->last_run;
     const bool timed = b->timing && run >= 0 && !b->tracked[run];
     hipEvent_t* ev = timed ? &b->events[(size_t)run * kEvPerRun] : nullptr;
@@ -698,47 +780,38 @@ int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stre
         yavo::launch_track_build(b->tracks, b->n_tracks, b->pairs, b->keypoints, b->kp_count, b->match_dj,
                                  b->match_lim, b->max_kp, b->track_K, b->T_right, eX, euv, eq, ec, s);
     }
-    hipStream_t ls = s;
-    if (b->overlap) {
-        // the LM reads only this track's edge buffer, priors and poses: it runs on the side stream beside the
-        // next batch's image kernels (which overwrite keypoints / matches, already consumed by the build)
-        YV_HIP(hipEventRecord(b->ev_edges[k], s));
-        YV_HIP(hipStreamWaitEvent(b->side, b->ev_edges[k], 0));
-        ls = b->side;
-    }
-    if (timed) YV_HIP(hipEventRecord(ev[7], ls));
-    yavo::launch_track_pose(b->n_tracks, ec, b->max_kp, eX, euv, b->track_K, d_priors, d_poses, eo, inl, ls);
-    if (timed) {
-        YV_HIP(hipEventRecord(ev[8], ls));
-        b->tracked[run] = 1;
-    }
+    if (b->overlap) YV_HIP(hipEventRecord(b->ev_edges[k], s));
+    yv_batch::DeferredLM L;
+    L.active = true;
+    L.k = k;
+    L.run = timed ? run : -1;
+    L.priors = d_priors;
+    L.poses = d_poses;
+    L.ev = ev;
     if (map) {
-        // the chunk's map block, after the LM on its stream: the build that next rewrites this edge buffer waits
-        // for ev_lm[k], recorded below, so it also waits for these reads. The block itself is rewritten only
-        // after its last reader released it (the all-gather of the previous chunk, yv_batch_map_release).
-        if (b->map_release_pending) {
-            YV_HIP(hipStreamWaitEvent(ls, b->ev_map_release, 0));
-            b->map_release_pending = false;
-        }
-        yavo::launch_map_chunk(d_poses, b->n_tracks, map->first_frame, map->kf_every, ec, eX, eo, b->max_kp,
-                               map->max_kf, map->block, ls);
-        if (!b->ev_map) YV_HIP(hipEventCreateWithFlags(&b->ev_map, hipEventDisableTiming));
-        YV_HIP(hipEventRecord(b->ev_map, ls));
-        b->map_written = true;
-    }
-    if (b->overlap) {
-        YV_HIP(hipEventRecord(b->ev_lm[k], ls));
-        b->lm_pending[k] = true;
+        L.has_map = true;
+        L.first_frame = map->first_frame;
+        L.kf_every = map->kf_every;
+        L.max_kf = map->max_kf;
+        L.block = map->block;
     }
     b->tbuf = k;
+    if (b->overlap_mode >= 2) {
+        // launched by the next yv_batch_run after its detect (2) / describe (3) stage, or by a flush
+        b->deferred = L;
+        return check_launch();
+    }
+    const int rc = launch_lm(b, L, s);
+    if (rc != YV_OK) return rc;
     return check_launch();
 }
 
 }  // namespace
 
 int yv_batch_set_track_overlap(yv_batch* b, int on) {
-    if (!b) return YV_ERR_INVALID;
+    if (!b || on < 0 || on > 3) return YV_ERR_INVALID;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+    if (flush_deferred(b) != YV_OK) return YV_ERR_HIP;
     if (on && !b->side) {
         // lowest priority: the LM fills the CUs the next batch's detect / describe / match leave idle
         int least = 0, greatest = 0;
@@ -751,12 +824,14 @@ int yv_batch_set_track_overlap(yv_batch* b, int on) {
     }
     if (!on && b->side) YV_HIP(hipStreamSynchronize(b->side));
     b->overlap = on != 0;
+    b->overlap_mode = on;
     return YV_OK;
 }
 
 int yv_batch_track_sync(yv_batch* b) {
     if (!b) return YV_ERR_INVALID;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+    if (flush_deferred(b) != YV_OK) return YV_ERR_HIP;
     if (b->side) YV_HIP(hipStreamSynchronize(b->side));
     return YV_OK;
 }
@@ -765,6 +840,7 @@ int yv_batch_set_track_lk(yv_batch* b, int image_step, int win, int max_level, i
                           double min_eig) {
     if (!b || image_step < 0 || (image_step > 0 && (win < 3 || win > 22 || max_level < 0))) return YV_ERR_INVALID;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+    if (flush_deferred(b) != YV_OK) return YV_ERR_HIP;
     if (b->side) YV_HIP(hipStreamSynchronize(b->side));
     YV_HIP(hipStreamSynchronize(b->ctx->stream));
     if (b->lk) {

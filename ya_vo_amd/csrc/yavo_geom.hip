@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "yavo_internal.h"
 #include "yavo_cvsvd.h"
@@ -41,8 +42,6 @@ using se3::se3_exp;
 using se3::se3_mul;
 
 constexpr int kNT = 256;          // threads per workgroup of the reduction kernels
-constexpr int kLMNT = 256;        // threads per pose-LM workgroup (<= 256 VGPRs: half the register file, so the
-                                  // LM co-runs with the image kernels of the next batch)
 
 // YAVO_LM_PROFILE builds (tools/lm_profile.py) time the pose-LM phases with the shader clock on lane 0
 #ifdef YAVO_LM_PROFILE
@@ -901,48 +900,59 @@ __device__ void tree_reduce(double (&part)[NV], double* red, double* out, unsign
     __syncthreads();
 }
 
-// The pose LM's reduction of NV per-thread partials over kLMNT threads (oracle sum_mode 3 for 256):
-// p[t] += p[t + NT/2]; then thread (v, g) sums run g of R = NT/32 partials of value v left to right from a
-// bank-padded LDS image ([v][g][R + 1]: conflict-free both when written by consecutive threads and when 16
-// threads read 16 runs); the 16 run sums of a value sit on 16 adjacent lanes and finish with the tree
-// q[g] += q[g + off], off = 8 .. 1.  Three barriers; one value per thread in the serial part.
-constexpr int kSegRun = kLMNT / 32;
-constexpr int kSegPad = kSegRun + 1;
-template <int NV>
-__device__ void seg_reduce(double (&part)[NV], double* red /* >= NV * 16 * kSegPad */, double* out,
-                           unsigned long long* t_sync = nullptr) {
-    constexpr int half = kLMNT / 2;
-    const int tid = threadIdx.x;
-    __syncthreads();
+// The pose LM's reduction of NV per-thread partials over NT = 64 W threads (oracle sum_mode 4 + log2(W)): the
+// halving tree p[l] += p[l + off], off = 32 .. 1, inside each wave, then the W wave totals left to right.
+// Inside the wave it runs as a reduce-scatter: at the level with offset off the two lanes l, l ^ off split their
+// n live values, each keeping ceil(n / 2) of them (the lane with bit off clear the lower half) and adding its
+// partner's copy of those -- one shuffle per kept value instead of one per value, 29 instead of 168 exchanges for
+// 28 values. Each value's partials still meet in the tree's pairs and order (the kept sum is own + partner, and
+// IEEE addition commutes, so the lane with bit off set computes the lower lane's bits). After the six levels the
+// lane pair (l, l ^ 1) holds value v(l) = 14 b5 + 7 b4 + 4 b3 + 2 b2 + b1 (28 values: v < 28 is real, the rest
+// are padding slots).
+template <int N, int OFF>
+__device__ __forceinline__ void rs_level(const double* in, double* out, int lane, int& v) {
+    constexpr int h = (N + 1) / 2;
+    const bool up = (lane & OFF) != 0;
+#pragma unroll
+    for (int j = 0; j < h; ++j) {
+        const double lo = in[j];
+        const double hi = (h + j < N) ? in[h + j] : 0.0;
+        const double keep = up ? hi : lo;
+        out[j] = keep + __shfl_xor(up ? lo : hi, OFF, 64);
+    }
+    if (up) v += h;
+}
+
+template <int NV, int NT>
+__device__ void lm_reduce(double (&part)[NV], double* red /* >= NV * NT / 64 */, double* out,
+                          unsigned long long* t_sync = nullptr) {
+    static_assert(NV == 28, "the reduce-scatter schedule is written for 28 values");
+    constexpr int W = NT / 64;
 #ifdef YAVO_LM_PROFILE
     if (t_sync) *t_sync = __builtin_readcyclecounter();
 #endif
-    const int e = tid & (half - 1);                             // partial index after the halving
-    const int slot = (e / kSegRun) * kSegPad + (e % kSegRun);  // [g][i] with padded runs
-    if (tid >= half) {
-#pragma unroll
-        for (int v = 0; v < NV; ++v) red[v * 16 * kSegPad + slot] = part[v];
+    const int tid = threadIdx.x, lane = tid & 63;
+    int v = 0;
+    double a14[14], a7[7], a4[4], a2[2], a1[1];
+    rs_level<28, 32>(part, a14, lane, v);
+    rs_level<14, 16>(a14, a7, lane, v);
+    rs_level<7, 8>(a7, a4, lane, v);
+    rs_level<4, 4>(a4, a2, lane, v);
+    rs_level<2, 2>(a2, a1, lane, v);
+    const double tot = a1[0] + __shfl_xor(a1[0], 1, 64);
+    const bool owner = v < NV && (lane & 1) == 0;
+    if (W == 1) {
+        if (owner) out[v] = tot;
+        __syncthreads();
+        return;
     }
+    if (owner) red[(tid >> 6) * NV + v] = tot;
     __syncthreads();
-    if (tid < half) {
+    if (tid < NV) {
+        double q = red[tid];
 #pragma unroll
-        for (int v = 0; v < NV; ++v) red[v * 16 * kSegPad + slot] = part[v] + red[v * 16 * kSegPad + slot];
-    }
-    __syncthreads();
-    // (value, run) pairs over the block: NV * 16 of them, kLMNT threads
-    for (int w0 = 0; w0 < NV * 16; w0 += kLMNT) {
-        const int w = w0 + tid;
-        double q = 0.0;
-        const int v = w >> 4, g = w & 15;
-        if (w < NV * 16) {
-            const double* r = red + v * 16 * kSegPad + g * kSegPad;
-            q = r[0];
-#pragma unroll
-            for (int i = 1; i < kSegRun; ++i) q = q + r[i];
-        }
-#pragma unroll
-        for (int off = 8; off > 0; off >>= 1) q = q + __shfl_down(q, off, 16);
-        if (w < NV * 16 && g == 0) out[v] = q;
+        for (int w = 1; w < W; ++w) q = q + red[w * NV + tid];
+        out[tid] = q;
     }
     __syncthreads();
 }
@@ -960,6 +970,7 @@ constexpr int kLMVals = 28;  // 21 lower-triangle H entries + 6 b + 1 chi2
 // One pass over the active edges at S.T: computeActiveErrors + activeRobustChi2 + buildSystem of g2o's
 // BlockSolver (Huber-weighted J^T J lower triangle, -J^T W e, robust chi2), summed in the oracle's tree
 // order into S.vals[0..28).  Also records S.Tlast (the estimate the active edges' errors refer to).
+template <int NT>
 __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, int na, const uint8_t* s_robust,
                                         const double* X, const double* uv, double* s_red,
                                         unsigned long long* lmp = nullptr) {
@@ -986,11 +997,11 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
         nx[0] = X[3 * i]; nx[1] = X[3 * i + 1]; nx[2] = X[3 * i + 2]; nx[3] = uv[2 * i]; nx[4] = uv[2 * i + 1];
         nrob = s_robust[i];
     }
-    for (int a = tid; a < na; a += kLMNT) {
+    for (int a = tid; a < na; a += NT) {
         const double xi[3] = {nx[0], nx[1], nx[2]}, mi[2] = {nx[3], nx[4]};
         const int rob = nrob;
-        if (a + kLMNT < na) {
-            const int i = s_active[a + kLMNT];
+        if (a + NT < na) {
+            const int i = s_active[a + NT];
             nx[0] = X[3 * i]; nx[1] = X[3 * i + 1]; nx[2] = X[3 * i + 2]; nx[3] = uv[2 * i]; nx[4] = uv[2 * i + 1];
             nrob = s_robust[i];
         }
@@ -1049,7 +1060,7 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
 #endif
 #ifdef YAVO_LM_PROFILE
     unsigned long long ps = 0;
-    seg_reduce<kLMVals>(part, s_red, S.vals, &ps);
+    lm_reduce<kLMVals, NT>(part, s_red, S.vals, &ps);
     if (lmp) {
         const unsigned long long p2 = __builtin_readcyclecounter();
         lmp[0] += p1 - p0;
@@ -1057,21 +1068,22 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
         lmp[8] += ps - p1;  // waiting at the first barrier for the other waves' edges
     }
 #else
-    seg_reduce<kLMVals>(part, s_red, S.vals);
+    lm_reduce<kLMVals, NT>(part, s_red, S.vals);
 #endif
 }
 
 // Problem p owns edges [offsets[p], offsets[p+1]) (CSR) or, with counts != nullptr, [p*stride, p*stride +
 // counts[p]) (the batch's fixed-stride track layout).  The prior is read from priors[p] and the estimate
 // written to poses[p] (the two may alias).
-__global__ __launch_bounds__(kLMNT) void pose_lm_kernel(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
+template <int NT>
+__global__ __launch_bounds__(NT) void pose_lm_kernel(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
                                                       int stride, const double* __restrict__ Xall,
                                                       const double* __restrict__ uvall, const double* __restrict__ Kall,
                                                       const double* priors, double* poses,
                                                       uint8_t* __restrict__ outlier_all, int32_t* __restrict__ inliers) {
     __shared__ uint8_t s_level[kMaxEdges], s_out[kMaxEdges], s_robust[kMaxEdges];
     __shared__ int16_t s_active[kMaxEdges];
-    __shared__ double s_red[kLMVals * 16 * kSegPad];
+    __shared__ double s_red[NT > 64 ? kLMVals * (NT / 64) : 1];
     __shared__ LMShared S;
     __shared__ int s_tmp[40];
     LMP_DECL
@@ -1084,7 +1096,7 @@ __global__ __launch_bounds__(kLMNT) void pose_lm_kernel(const int32_t* __restric
     const double* uv = uvall + 2 * e0;
     if (tid < 9) S.K[tid] = Kall[9 * prob + tid];
     if (tid < 7) S.T[tid] = priors[7 * prob + tid];
-    for (int i = tid; i < n; i += kLMNT) {
+    for (int i = tid; i < n; i += NT) {
         s_level[i] = 0;
         s_out[i] = 0;
         s_robust[i] = 1;
@@ -1100,11 +1112,11 @@ __global__ __launch_bounds__(kLMNT) void pose_lm_kernel(const int32_t* __restric
         if (tid < 7) S.T[tid] = prior[tid];
         // initializeOptimization(): active = level-0 edges in insertion order (block compaction)
         int na = 0;
-        for (int base = 0; base < n; base += kLMNT) {
+        for (int base = 0; base < n; base += NT) {
             const int i = base + tid;
             const int f = (i < n && s_level[i] == 0) ? 1 : 0;
             int tot = 0;
-            const int off = block_excl_scan_geom<kLMNT>(f, s_tmp, &tot);
+            const int off = block_excl_scan_geom<NT>(f, s_tmp, &tot);
             if (f) s_active[na + off] = (int16_t)i;
             na += tot;
         }
@@ -1118,10 +1130,10 @@ __global__ __launch_bounds__(kLMNT) void pose_lm_kernel(const int32_t* __restric
             for (int it = 0; it < 10; ++it) {
 #ifdef YAVO_LM_PROFILE
                 LMP_MARK(5);
-                if (!have) lm_pass(S, s_active, na, s_robust, X, uv, s_red, lmp_acc);
+                if (!have) lm_pass<NT>(S, s_active, na, s_robust, X, uv, s_red, lmp_acc);
                 lmp_t = __builtin_readcyclecounter();
 #else
-                if (!have) lm_pass(S, s_active, na, s_robust, X, uv, s_red);
+                if (!have) lm_pass<NT>(S, s_active, na, s_robust, X, uv, s_red);
 #endif
                 if (tid == 0) {
                     double sys[28];
@@ -1172,10 +1184,10 @@ __global__ __launch_bounds__(kLMNT) void pose_lm_kernel(const int32_t* __restric
                     }
                     LMP_MARK(2);
 #ifdef YAVO_LM_PROFILE
-                    lm_pass(S, s_active, na, s_robust, X, uv, s_red, lmp_acc);
+                    lm_pass<NT>(S, s_active, na, s_robust, X, uv, s_red, lmp_acc);
                     lmp_t = __builtin_readcyclecounter();
 #else
-                    lm_pass(S, s_active, na, s_robust, X, uv, s_red);  // errors + system at the trial estimate
+                    lm_pass<NT>(S, s_active, na, s_robust, X, uv, s_red);  // errors + system at the trial estimate
 #endif
                     if (tid == 0) {
                         const int ok2 = S.flag;
@@ -1231,7 +1243,7 @@ __global__ __launch_bounds__(kLMNT) void pose_lm_kernel(const int32_t* __restric
         for (int q = 0; q < 7; ++q) Tl[q] = S.Tlast[q];
         for (int q = 0; q < 9; ++q) K[q] = S.K[q];
         int cnt = 0;
-        for (int i = tid; i < n; i += kLMNT) {
+        for (int i = tid; i < n; i += NT) {
             double ee[2];
             edge_error(s_out[i] ? T : Tl, K, X + 3 * i, uv + 2 * i, ee);
             const double c2 = ee[0] * ee[0] + ee[1] * ee[1];
@@ -1246,14 +1258,14 @@ __global__ __launch_bounds__(kLMNT) void pose_lm_kernel(const int32_t* __restric
             if (round == 2) s_robust[i] = 0;
         }
         int tot = 0;
-        block_excl_scan_geom<kLMNT>(cnt, s_tmp, &tot);
+        block_excl_scan_geom<NT>(cnt, s_tmp, &tot);
         outlierCount = tot;
         __syncthreads();
         LMP_MARK(4);
     }
     LMP_STORE();
     if (tid < 7) poses[7 * prob + tid] = S.T[tid];
-    for (int i = tid; i < n; i += kLMNT) outlier_all[e0 + i] = s_out[i];
+    for (int i = tid; i < n; i += NT) outlier_all[e0 + i] = s_out[i];
     if (tid == 0) inliers[prob] = n - outlierCount;
 }
 
@@ -1492,6 +1504,27 @@ __global__ __launch_bounds__(kNT) void pose_gn_kernel(const int32_t* __restrict_
     if (tid == 0) iters_out[prob] = acc;
 }
 
+// Threads per pose-LM workgroup: 256 by default (one wave per SIMD: the LM is latency-bound, and 64 / 128 threads
+// measured 2.1 / 1.5 ms against 1.0 ms per 256-frame batch); YAVO_LM_THREADS = 64 / 128 for experiments. The
+// summation order follows (yv_lm_sum_mode).
+inline int lm_threads() {
+    static const int nt = [] {
+        const char* e = getenv("YAVO_LM_THREADS");
+        const int v = e ? atoi(e) : 256;
+        return (v == 64 || v == 128) ? v : 256;
+    }();
+    return nt;
+}
+
+template <typename... A>
+void launch_lm(int n, hipStream_t s, A... args) {
+    switch (lm_threads()) {
+        case 256: hipLaunchKernelGGL(pose_lm_kernel<256>, dim3(n), dim3(256), 0, s, args...); break;
+        case 128: hipLaunchKernelGGL(pose_lm_kernel<128>, dim3(n), dim3(128), 0, s, args...); break;
+        default: hipLaunchKernelGGL(pose_lm_kernel<64>, dim3(n), dim3(64), 0, s, args...); break;
+    }
+}
+
 }  // namespace geom
 
 // ------------------------------------------------------------------------------------------------
@@ -1517,9 +1550,8 @@ void launch_world2camera(const double* X, int n, const double* T, const double* 
 
 void launch_pose_lm(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
                     double* poses, uint8_t* outlier, int32_t* inliers, hipStream_t s) {
-    hipLaunchKernelGGL(geom::pose_lm_kernel, dim3(n_problems), dim3(geom::kLMNT), 0, s, offsets,
-                       static_cast<const int32_t*>(nullptr), 0, X, uv, K, static_cast<const double*>(poses), poses,
-                       outlier, inliers);
+    geom::launch_lm(n_problems, s, offsets, static_cast<const int32_t*>(nullptr), 0, X, uv, K,
+                    static_cast<const double*>(poses), poses, outlier, inliers);
 }
 
 void launch_track_build(const int32_t* tracks, int n_tracks, const int32_t* pairs, const yv_keypoint* keypoints,
@@ -1552,9 +1584,8 @@ void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, cons
                        const double* edge_uv, const double* K, const double* priors, double* poses,
                        uint8_t* edge_outlier, int32_t* inliers, hipStream_t s) {
     if (n_tracks <= 0) return;
-    hipLaunchKernelGGL(geom::pose_lm_kernel, dim3(n_tracks), dim3(geom::kLMNT), 0, s,
-                       static_cast<const int32_t*>(nullptr), edge_count, stride, edge_X, edge_uv, K, priors, poses,
-                       edge_outlier, inliers);
+    geom::launch_lm(n_tracks, s, static_cast<const int32_t*>(nullptr), edge_count, stride, edge_X, edge_uv, K,
+                    priors, poses, edge_outlier, inliers);
 }
 
 void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
@@ -1563,6 +1594,11 @@ void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, con
 }
 
 }  // namespace yavo
+
+extern "C" int yv_lm_sum_mode(void) {
+    const int nt = yavo::geom::lm_threads();
+    return nt == 256 ? 6 : nt == 128 ? 5 : 4;
+}
 
 #ifdef YAVO_LM_PROFILE
 // profiling builds only (lib/libyavo_prof.so): per-workgroup pose-LM phase cycle counts of the last launch
