@@ -1276,7 +1276,8 @@ __global__ __launch_bounds__(NT) void pose_lm_kernel(const int32_t* __restrict__
 // right camera at T_right; accepted iff triangulation succeeds and Z > 0 (triangulate2View,
 // src/LoopHandler.cc:658-726).  uv = (kp_{k-1}[i].x, kp_{k-1}[i].y) (the reference's measurement,
 // src/LoopHandler.cc:786).  Edges keep temporal query order.  One workgroup per track.
-__global__ __launch_bounds__(kNT) void track_build_kernel(
+template <int NT>
+__global__ __launch_bounds__(NT) void track_build_kernel(
     const int32_t* __restrict__ tracks, const int32_t* __restrict__ pairs, const yv_keypoint* __restrict__ keypoints,
     const int32_t* __restrict__ kp_count, const int2* __restrict__ match_dj, const int32_t* __restrict__ match_lim,
     int max_kp, const double* __restrict__ Kall, const double* __restrict__ T_right, double* __restrict__ edge_X,
@@ -1304,7 +1305,7 @@ __global__ __launch_bounds__(kNT) void track_build_kernel(
     double* uvo = edge_uv + 2 * (int64_t)t * max_kp;
     int32_t* qo = edge_query + (int64_t)t * max_kp;
     int ne = 0;
-    for (int base = 0; base < nq; base += kNT) {
+    for (int base = 0; base < nq; base += NT) {
         const int i = base + tid;
         bool good = false;
         double X[3];
@@ -1317,7 +1318,7 @@ __global__ __launch_bounds__(kNT) void track_build_kernel(
             }
         }
         int tot = 0;
-        const int off = block_excl_scan_geom(good ? 1 : 0, s_tmp, &tot);
+        const int off = block_excl_scan_geom<NT>(good ? 1 : 0, s_tmp, &tot);
         if (good) {
             const int e = ne + off;
             Xo[3 * e] = X[0];
@@ -1559,7 +1560,8 @@ void launch_track_build(const int32_t* tracks, int n_tracks, const int32_t* pair
                         const double* K, const double* T_right, double* edge_X, double* edge_uv, int32_t* edge_query,
                         int32_t* edge_count, hipStream_t s) {
     if (n_tracks <= 0) return;
-    hipLaunchKernelGGL(geom::track_build_kernel, dim3(n_tracks), dim3(geom::kNT), 0, s, tracks, pairs, keypoints,
+    // 1024 threads: about one query keypoint per thread (the FP64 triangulations are latency-bound)
+    hipLaunchKernelGGL(geom::track_build_kernel<1024>, dim3(n_tracks), dim3(1024), 0, s, tracks, pairs, keypoints,
                        kp_count, match_dj, match_lim, max_kp, K, T_right, edge_X, edge_uv, edge_query, edge_count);
 }
 
