@@ -15,7 +15,7 @@ from typing import Optional, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libyavo.so")
+LIB_PATH = os.environ.get("YAVO_LIB") or os.path.join(_HERE, "lib", "libyavo.so")  # YAVO_LIB: experiment builds
 
 YV_OK = 0
 YV_ERR_INVALID = -1

@@ -1075,8 +1075,15 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
 // Problem p owns edges [offsets[p], offsets[p+1]) (CSR) or, with counts != nullptr, [p*stride, p*stride +
 // counts[p]) (the batch's fixed-stride track layout).  The prior is read from priors[p] and the estimate
 // written to poses[p] (the two may alias).
+// Register budget of the LM: 2 waves per SIMD = 256 VGPRs and no AGPRs (36 B of scratch), so a SIMD running an LM
+// wave keeps 256 registers for the image kernels beside it (4 detect waves instead of 3): 125k -> 131k frames/s.
+// 3 / 4 (168 / 128 VGPRs) spill 400-600 B per lane in the lane-0 LDLT and triple the LM's latency.
+#ifndef YAVO_LM_WAVES_PER_EU
+#define YAVO_LM_WAVES_PER_EU 2
+#endif
+#define YAVO_LM_ATTR __attribute__((amdgpu_waves_per_eu(YAVO_LM_WAVES_PER_EU)))
 template <int NT>
-__global__ __launch_bounds__(NT) void pose_lm_kernel(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
+__global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
                                                       int stride, const double* __restrict__ Xall,
                                                       const double* __restrict__ uvall, const double* __restrict__ Kall,
                                                       const double* priors, double* poses,
