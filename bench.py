@@ -215,26 +215,42 @@ def main():
         d_anchors = torch.zeros((world, 7), dtype=torch.float64, device=dev)
         comm = torch.cuda.Stream(device=dev)
 
+    pending = [False]
+
+    def exchange():
+        # the last track_map's block: all-gathered and placed on the communication stream once it is written
+        batch.map_wait(comm.cuda_stream)
+        with torch.cuda.stream(comm):
+            if world > 1 and backend == "nccl":
+                dist.all_gather_into_tensor(d_gathered, d_block)
+            elif world > 1:  # gloo rehearsal (YAVO_BENCH_BACKEND=gloo): list form
+                dist.all_gather(list(d_gathered.unbind(0)), d_block)
+            ctx.map_place(d_gathered.data_ptr(), world, bb, d_base.data_ptr(), d_anchors.data_ptr(),
+                          stream=comm.cuda_stream)
+        batch.map_release(comm.cuda_stream)
+        pending[0] = False
+
     def step():
+        # overlap modes 2 / 3 launch the previous step's pose LM (and its map block) inside this run, so the
+        # previous block is exchanged after it (one step behind: map_wait before the launch would force it early)
         batch.run(d_frames.data_ptr(), n_img, W, H * W, 20, carry_from=2 * (B - 1))
+        if pending[0]:
+            exchange()
         if not use_map:
             batch.track(d_prior.data_ptr(), d_poses[calls[0] & 1].data_ptr())
         else:
             batch.track_map(d_prior.data_ptr(), d_poses[calls[0] & 1].data_ptr(), first_frame, args.kf_every,
                             d_block.data_ptr(), max_kf)
-            batch.map_wait(comm.cuda_stream)
-            with torch.cuda.stream(comm):
-                if world > 1 and backend == "nccl":
-                    dist.all_gather_into_tensor(d_gathered, d_block)
-                elif world > 1:  # gloo rehearsal (YAVO_BENCH_BACKEND=gloo): list form
-                    dist.all_gather(list(d_gathered.unbind(0)), d_block)
-                ctx.map_place(d_gathered.data_ptr(), world, bb, d_base.data_ptr(), d_anchors.data_ptr(),
-                              stream=comm.cuda_stream)
-            batch.map_release(comm.cuda_stream)
+            pending[0] = True
         calls[0] += 1
+
+    def drain():
+        if pending[0]:
+            exchange()
 
     for _ in range(args.warmup):
         step()
+    drain()
     ctx.sync()
     batch.track_sync()
     torch.cuda.synchronize()
@@ -247,6 +263,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     ctx.sync()
     batch.track_sync()
     torch.cuda.synchronize()
