@@ -855,7 +855,7 @@ void launch_pack_desc(const yv_keypoint* keypoints, const int32_t* kp_count, int
 typedef int mm_v4i __attribute__((ext_vector_type(4)));
 constexpr int MM_QT = 8;                  // 16-row query tiles per wave
 constexpr int MM_QB = 4 * MM_QT * 16;     // queries per workgroup (4 waves)
-constexpr int MM_TC = 64;                 // train descriptors per LDS chunk
+constexpr int MM_TC = 128;                // train descriptors per LDS chunk
 constexpr int MM_ROW = 17;                // uint4 per expanded train row (16 + 1 pad: conflict-free b128 reads)
 
 // 4 descriptor bits -> 4 bytes of +1 (bit set) / -1 (bit clear), bit i in byte i
@@ -869,10 +869,40 @@ __device__ __forceinline__ uint4 expand16_pm1(uint32_t bits) {
                       expand_pm1((bits >> 12) & 0xF));
 }
 
+// 4 descriptor bits -> 4 bytes of 64 (bit set) / 0 (bit clear): the 0/64 encoding of the max_kp <= 2048 matcher
+__device__ __forceinline__ uint32_t expand_01x64(uint32_t nib) {
+    // v_mul_u32_u24 (full rate; nib <= 15) kept as written: LLVM would otherwise fold the shift into one
+    // quarter-rate v_mul_lo_u32 by 0x08102040
+    uint32_t spread;
+    asm("v_mul_u32_u24 %0, 0x204081, %1" : "=v"(spread) : "v"(nib));
+    return (spread & 0x01010101u) << 6;
+}
+
+__device__ __forceinline__ uint4 expand16_01x64(uint32_t bits) {
+    return make_uint4(expand_01x64(bits & 0xF), expand_01x64((bits >> 4) & 0xF), expand_01x64((bits >> 8) & 0xF),
+                      expand_01x64((bits >> 12) & 0xF));
+}
+
+__device__ __forceinline__ int desc_popcount(const Desc& d) {
+    int c = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) c += __popc(d.w[w]);
+    return c;
+}
+
+// kFast (max_kp <= 2048): bytes 0 / 64, so the MFMA's dot is 4096 * popcount(a & b) and, started from the
+// accumulator c_j = (2047 - j) - 2048 * popcount(b_j), a 4-step chain ends at the key itself:
+//   key = 2048 * (2 popcount(a & b_j) - popcount(b_j)) + (2047 - j) = 2048 * (pa - Hamming) + (2047 - j)
+// (pa - Hamming orders like -Hamming for one query; 2047 - j >= 0 breaks ties toward the first j). The epilogue is
+// one v_max3 per two distances, the train staging four full-rate ops per nibble, and the decode Hamming =
+// pa - (key >> 11), j = 2047 - (key & 2047). Otherwise (max_kp up to 4096): the +-1 encoding, dot = 256 - 2 Hamming,
+// key = (dot << 16) + 0xFFFF - j formed per element.
+template <bool kFast>
 __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ desc, const int32_t* __restrict__ kp_count,
                                                     const int32_t* __restrict__ pairs, int max_kp,
                                                     uint32_t* __restrict__ match_key) {
     __shared__ uint4 s_t[2][MM_TC * MM_ROW];
+    __shared__ int s_pb[2][MM_TC];
     const int pair = blockIdx.y;
     const int qi = pairs[2 * pair], ti = pairs[2 * pair + 1];
     const int nq = kp_count[qi], nt = kp_count[ti];
@@ -882,6 +912,7 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
     const int col = lane & 15, g = lane >> 4;
     const Desc* qd = desc + (int64_t)qi * max_kp;
     const uint32_t* tw = reinterpret_cast<const uint32_t*>(desc + (int64_t)ti * max_kp);
+    const Desc* td = desc + (int64_t)ti * max_kp;
 
     // query fragments: tile qt row (lane & 15) = query q0 + 16 MM_QT wave + 16 qt + (lane & 15)
     mm_v4i A[MM_QT][4];
@@ -894,7 +925,7 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
             const uint32_t hi_mask = 0u - (uint32_t)(g >> 1);  // blend, not an index: keeps d in registers
             const uint32_t w = d.w[2 * s] ^ ((d.w[2 * s] ^ d.w[2 * s + 1]) & hi_mask);
             const uint32_t bits = (w >> (16 * (g & 1))) & 0xFFFFu;
-            const uint4 e = expand16_pm1(bits);
+            const uint4 e = kFast ? expand16_01x64(bits) : expand16_pm1(bits);
             A[qt][s] = mm_v4i{(int)e.x, (int)e.y, (int)e.z, (int)e.w};
         }
     }
@@ -904,22 +935,28 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
 #pragma unroll
         for (int r = 0; r < 4; ++r) best[qt][r] = INT_MIN;
 
-    // staging: thread -> (train tt = idx >> 4, 16-bit field u = idx & 15), 4 fields per thread per chunk
-    uint32_t pre[4];
+    // staging: thread -> (train tt = idx >> 4, 16-bit field u = idx & 15), kF fields per thread per chunk; in kFast
+    // the first MM_TC threads also count the set bits of train tt = tid
+    constexpr int kF = MM_TC * 16 / 256;  // 16-bit fields per thread per chunk
+    uint32_t pre[kF];
+    int pre_pb = 0;
     auto fetch = [&](int t0) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kF; ++k) {
             const int idx = tid + 256 * k, tt = idx >> 4, u = idx & 15;
             const int t = t0 + tt;
             pre[k] = t < nt ? tw[(int64_t)t * 8 + (u >> 1)] : 0u;
         }
+        if (kFast && tid < MM_TC) pre_pb = t0 + tid < nt ? desc_popcount(td[t0 + tid]) : 0;
     };
     auto store = [&](int buf) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kF; ++k) {
             const int idx = tid + 256 * k, tt = idx >> 4, u = idx & 15;
-            s_t[buf][tt * MM_ROW + u] = expand16_pm1((pre[k] >> (16 * (u & 1))) & 0xFFFFu);
+            const uint32_t bits = (pre[k] >> (16 * (u & 1))) & 0xFFFFu;
+            s_t[buf][tt * MM_ROW + u] = kFast ? expand16_01x64(bits) : expand16_pm1(bits);
         }
+        if (kFast && tid < MM_TC) s_pb[buf][tid] = pre_pb;
     };
     if (nt > 0) {
         fetch(0);
@@ -931,7 +968,7 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
         if (more) fetch(t0 + MM_TC);
         __syncthreads();
         // two 16-column train tiles per pass: four independent MFMA chains, and one v_max3 folds both tiles' keys
-        // into the running maximum (1.5 VALU per distance)
+        // into the running maximum
 #pragma unroll
         for (int tt0 = 0; tt0 < MM_TC; tt0 += 32) {
             if (t0 + tt0 >= nt) break;
@@ -943,28 +980,54 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
                 Ba[s] = mm_v4i{(int)va.x, (int)va.y, (int)va.z, (int)va.w};
                 Bb[s] = mm_v4i{(int)vb.x, (int)vb.y, (int)vb.z, (int)vb.w};
             }
-            // key = (dot << 16) + bias: bias = 0xFFFF - j for a real train column; a column past nt (including the
-            // whole second tile at the end of the list) gets -2^30, below every real key (>= -2^24) and above
-            // INT_MIN, so no per-element select and no branch are needed
+            // a column past nt (including the whole second tile at the end of the list) gets -2^30, below every
+            // real key and above INT_MIN, so no per-element select and no branch are needed
             const int ja = t0 + tt0 + col, jb = ja + 16;
-            const int bias_a = ja < nt ? 0xFFFF - ja : -(1 << 30);
-            const int bias_b = jb < nt ? 0xFFFF - jb : -(1 << 30);
+            if (kFast) {
+                const int ca = ja < nt ? (2047 - ja) - 2048 * s_pb[buf][tt0 + col] : -(1 << 30);
+                const int cb = jb < nt ? (2047 - jb) - 2048 * s_pb[buf][tt0 + 16 + col] : -(1 << 30);
+                const mm_v4i Ca = {ca, ca, ca, ca}, Cb = {cb, cb, cb, cb};
 #pragma unroll
-            for (int qt = 0; qt < MM_QT; qt += 2) {
-                mm_v4i a0 = {0, 0, 0, 0}, b0 = {0, 0, 0, 0}, a1 = {0, 0, 0, 0}, b1 = {0, 0, 0, 0};
+                for (int qt = 0; qt < MM_QT; qt += 2) {
+                    mm_v4i a0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][0], Ba[0], Ca, 0, 0, 0);
+                    mm_v4i b0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][0], Bb[0], Cb, 0, 0, 0);
+                    mm_v4i a1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][0], Ba[0], Ca, 0, 0, 0);
+                    mm_v4i b1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][0], Bb[0], Cb, 0, 0, 0);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    a0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], Ba[s], a0, 0, 0, 0);
-                    b0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], Bb[s], b0, 0, 0, 0);
-                    a1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][s], Ba[s], a1, 0, 0, 0);
-                    b1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][s], Bb[s], b1, 0, 0, 0);
+                    for (int s = 1; s < 4; ++s) {
+                        a0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], Ba[s], a0, 0, 0, 0);
+                        b0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], Bb[s], b0, 0, 0, 0);
+                        a1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][s], Ba[s], a1, 0, 0, 0);
+                        b1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][s], Bb[s], b1, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        best[qt][r] = max(best[qt][r], max(a0[r], b0[r]));
+                        best[qt + 1][r] = max(best[qt + 1][r], max(a1[r], b1[r]));
+                    }
                 }
+            } else {
+                // key = (dot << 16) + bias: bias = 0xFFFF - j for a real train column
+                const int bias_a = ja < nt ? 0xFFFF - ja : -(1 << 30);
+                const int bias_b = jb < nt ? 0xFFFF - jb : -(1 << 30);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    best[qt][r] = max(best[qt][r], max((int)(((uint32_t)a0[r] << 16) + (uint32_t)bias_a),
-                                                       (int)(((uint32_t)b0[r] << 16) + (uint32_t)bias_b)));
-                    best[qt + 1][r] = max(best[qt + 1][r], max((int)(((uint32_t)a1[r] << 16) + (uint32_t)bias_a),
-                                                               (int)(((uint32_t)b1[r] << 16) + (uint32_t)bias_b)));
+                for (int qt = 0; qt < MM_QT; qt += 2) {
+                    mm_v4i a0 = {0, 0, 0, 0}, b0 = {0, 0, 0, 0}, a1 = {0, 0, 0, 0}, b1 = {0, 0, 0, 0};
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        a0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], Ba[s], a0, 0, 0, 0);
+                        b0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], Bb[s], b0, 0, 0, 0);
+                        a1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][s], Ba[s], a1, 0, 0, 0);
+                        b1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][s], Bb[s], b1, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        best[qt][r] = max(best[qt][r], max((int)(((uint32_t)a0[r] << 16) + (uint32_t)bias_a),
+                                                           (int)(((uint32_t)b0[r] << 16) + (uint32_t)bias_b)));
+                        best[qt + 1][r] = max(best[qt + 1][r],
+                                              max((int)(((uint32_t)a1[r] << 16) + (uint32_t)bias_a),
+                                                  (int)(((uint32_t)b1[r] << 16) + (uint32_t)bias_b)));
+                    }
                 }
             }
         }
@@ -985,10 +1048,17 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
             if (col == r && q < nq) {
                 uint32_t key = 0xFFFFFFFFu;  // empty train set (nt >= 1 always leaves a real key in the row max)
                 if (v != INT_MIN) {
-                    const int dot = v >> 16;
-                    const uint32_t d = (uint32_t)((256 - dot) >> 1);
-                    const uint32_t jj = 0xFFFFu - ((uint32_t)v & 0xFFFFu);
-                    key = (d << 16) | jj;
+                    if (kFast) {
+                        const int pa = desc_popcount(qd[q]);
+                        const uint32_t d = (uint32_t)(pa - (v >> 11));
+                        const uint32_t jj = 2047u - ((uint32_t)v & 2047u);
+                        key = (d << 16) | jj;
+                    } else {
+                        const int dot = v >> 16;
+                        const uint32_t d = (uint32_t)((256 - dot) >> 1);
+                        const uint32_t jj = 0xFFFFu - ((uint32_t)v & 0xFFFFu);
+                        key = (d << 16) | jj;
+                    }
                 }
                 match_key[(int64_t)pair * max_kp + q] = key;
             }
@@ -999,7 +1069,10 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
 void launch_match(const Desc* desc, const int32_t* kp_count, const int32_t* pairs, int n_pairs, int max_kp,
                   uint32_t* match_key, hipStream_t s) {
     dim3 grid((max_kp + MM_QB - 1) / MM_QB, n_pairs);
-    hipLaunchKernelGGL(match_kernel, grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
+    if (max_kp <= 2048)
+        hipLaunchKernelGGL(match_kernel<true>, grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
+    else
+        hipLaunchKernelGGL(match_kernel<false>, grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
 }
 
 // ------------------------------------------------------------------------------------------------
