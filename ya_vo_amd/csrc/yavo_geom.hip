@@ -967,6 +967,30 @@ struct LMShared {
 
 constexpr int kLMVals = 28;  // 21 lower-triangle H entries + 6 b + 1 chi2
 
+// The exact short form of one edge's J^T W J lower triangle and -J^T W e (see lm_pass), added to the partials.
+__device__ __forceinline__ void lm_accumulate_short(double (&part)[28], const double* J, double w, const double* e) {
+    double a[6], b[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        a[r] = J[r] * w;
+        b[r] = J[6 + r] * w;
+    }
+    part[0] = part[0] + a[0] * J[0];
+    part[2] = part[2] + b[1] * J[7];
+#pragma unroll
+    for (int r = 2; r < 6; ++r) {
+        part[r * (r + 1) / 2 + 0] = part[r * (r + 1) / 2 + 0] + a[r] * J[0];
+        part[r * (r + 1) / 2 + 1] = part[r * (r + 1) / 2 + 1] + b[r] * J[7];
+#pragma unroll
+        for (int c = 2; c <= r; ++c)
+            part[r * (r + 1) / 2 + c] = part[r * (r + 1) / 2 + c] + (a[r] * J[c] + b[r] * J[6 + c]);
+    }
+    part[21] = part[21] + (-(a[0] * e[0]));
+    part[22] = part[22] + (-(b[1] * e[1]));
+#pragma unroll
+    for (int r = 2; r < 6; ++r) part[21 + r] = part[21 + r] + (-(a[r] * e[0] + b[r] * e[1]));
+}
+
 // One pass over the active edges at S.T: computeActiveErrors + activeRobustChi2 + buildSystem of g2o's
 // BlockSolver (Huber-weighted J^T J lower triangle, -J^T W e, robust chi2), summed in the oracle's tree
 // order into S.vals[0..28).  Also records S.Tlast (the estimate the active edges' errors refer to).
@@ -1010,7 +1034,12 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
         const double c2 = e[0] * e[0] + e[1] * e[1];
         double w = 1.0;
         double chi = c2;
-        if (rob) chi = huber_rho(c2, &w);
+        // Huber only past delta: skipped by the whole wave when no lane needs it (a per-lane branch is if-converted
+        // into an unconditional sqrt + division)
+        const bool hub = rob && c2 > 1.0;
+        if (__any(hub)) {
+            if (rob) chi = huber_rho(c2, &w);
+        }
         part[27] = part[27] + chi;
         double J[12];
         edge_jacobian(T, K, xi, J);
@@ -1020,27 +1049,12 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
         // becomes -0.0, and p + (+-0) = p for p != 0), so the short form below gives bit-identical sums; an
         // edge with a non-finite operand takes the literal form.
         const double fin = J[0] + J[2] + J[3] + J[4] + J[5] + J[7] + J[8] + J[9] + J[10] + J[11] + w + e[0] + e[1];
-        if (__builtin_expect(isfinite(fin), 1)) {
-            double a[6], b[6];
-#pragma unroll
-            for (int r = 0; r < 6; ++r) {
-                a[r] = J[r] * w;
-                b[r] = J[6 + r] * w;
-            }
-            part[0] = part[0] + a[0] * J[0];
-            part[2] = part[2] + b[1] * J[7];
-#pragma unroll
-            for (int r = 2; r < 6; ++r) {
-                part[r * (r + 1) / 2 + 0] = part[r * (r + 1) / 2 + 0] + a[r] * J[0];
-                part[r * (r + 1) / 2 + 1] = part[r * (r + 1) / 2 + 1] + b[r] * J[7];
-#pragma unroll
-                for (int c = 2; c <= r; ++c)
-                    part[r * (r + 1) / 2 + c] = part[r * (r + 1) / 2 + c] + (a[r] * J[c] + b[r] * J[6 + c]);
-            }
-            part[21] = part[21] + (-(a[0] * e[0]));
-            part[22] = part[22] + (-(b[1] * e[1]));
-#pragma unroll
-            for (int r = 2; r < 6; ++r) part[21 + r] = part[21 + r] + (-(a[r] * e[0] + b[r] * e[1]));
+        const bool fin_ok = isfinite(fin);
+        // wave-uniform branch: a per-lane one is if-converted, i.e. both forms computed and selected (+100 FP64 ops)
+        if (__builtin_expect(__all(fin_ok), 1)) {
+            lm_accumulate_short(part, J, w, e);
+        } else if (fin_ok) {
+            lm_accumulate_short(part, J, w, e);
         } else {
 #pragma unroll
             for (int r = 0; r < 6; ++r) {
