@@ -1358,7 +1358,8 @@ __global__ __launch_bounds__(NT) void track_build_kernel(
 // left keypoints whose stereo match (pair sp) survives removeOutliers and triangulates (left camera = world).
 // Compacted in keypoint order: X, the LK start point (x = column, y = row as cv::Point2f, :344) and the
 // keypoint index.  One workgroup per track.
-__global__ __launch_bounds__(kNT) void stereo_points_kernel(
+template <int NT>
+__global__ __launch_bounds__(NT) void stereo_points_kernel(
     const int32_t* __restrict__ stereo_pairs, const int32_t* __restrict__ pairs,
     const yv_keypoint* __restrict__ keypoints, const int32_t* __restrict__ kp_count, const int2* __restrict__ match_dj,
     const int32_t* __restrict__ match_lim, int max_kp, const double* __restrict__ Kall,
@@ -1384,7 +1385,7 @@ __global__ __launch_bounds__(kNT) void stereo_points_kernel(
     float* po = pts + 2 * (int64_t)t * max_kp;
     int32_t* qo = pq + (int64_t)t * max_kp;
     int ne = 0;
-    for (int base = 0; base < nq; base += kNT) {
+    for (int base = 0; base < nq; base += NT) {
         const int j = base + tid;
         bool good = false;
         double X[3];
@@ -1393,7 +1394,7 @@ __global__ __launch_bounds__(kNT) void stereo_points_kernel(
             if (a.x < lim && a.y >= 0) good = triangulate_px(kl[j].x, kl[j].y, kr[a.y].x, kr[a.y].y, s_Ta, s_Tb, s_K, X);
         }
         int tot = 0;
-        const int off = block_excl_scan_geom(good ? 1 : 0, s_tmp, &tot);
+        const int off = block_excl_scan_geom<NT>(good ? 1 : 0, s_tmp, &tot);
         if (good) {
             const int e = ne + off;
             Xo[3 * e] = X[0];
@@ -1591,7 +1592,8 @@ void launch_stereo_points(const int32_t* stereo_pairs, int n_tracks, const int32
                           const int32_t* match_lim, int max_kp, const double* K, const double* T_right, double* pX,
                           float* pts, int32_t* pq, int32_t* pcount, hipStream_t s) {
     if (n_tracks <= 0) return;
-    hipLaunchKernelGGL(geom::stereo_points_kernel, dim3(n_tracks), dim3(geom::kNT), 0, s, stereo_pairs, pairs,
+    // 1024 threads: about one keypoint per thread (FP64 triangulations, latency-bound)
+    hipLaunchKernelGGL(geom::stereo_points_kernel<1024>, dim3(n_tracks), dim3(1024), 0, s, stereo_pairs, pairs,
                        keypoints, kp_count, match_dj, match_lim, max_kp, K, T_right, pX, pts, pq, pcount);
 }
 
