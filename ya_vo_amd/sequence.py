@@ -160,23 +160,34 @@ class SequenceFrontend:
         t2 = time.perf_counter()
         self.records.update(frame_records_from_block(block, uv, q, own))
         self.next_frame = first + n
-        self._local_ba()
+        ba_sec = {}
+        self._local_ba(ba_sec)
         t3 = time.perf_counter()
         if seconds is not None:
             for key, dt in (("device", t1 - t0), ("download", t2 - t1), ("ba", t3 - t2)):
                 seconds[key] = seconds.get(key, 0.0) + dt
+            for key, dt in ba_sec.items():
+                seconds[key] = seconds.get(key, 0.0) + dt
 
-    def _local_ba(self) -> None:
+    def _local_ba(self, sec) -> None:
+        import time
         last = self.next_frame - 1
         frames = list(range(max(0, last - self.window + 1), last + 1))
         if len(frames) <= self.n_fixed:
             return
+        t0 = time.perf_counter()
         poses, X, ep, el, meas, owners = window_problem(self.records, frames, self.n_fixed)
         if len(ep) == 0:
             return
+        t1 = time.perf_counter()
         self.ba.set_problem(len(frames), self.n_fixed, len(X), ep, el, meas, self.K)
+        t2 = time.perf_counter()
         poses, X, log, it = self.ba.solve(poses, X, self.ba_iters)
+        t3 = time.perf_counter()
         apply_window(self.records, frames, poses, X, owners)
+        sec["ba_assemble"] = t1 - t0 + time.perf_counter() - t3
+        sec["ba_set_problem"] = t2 - t1
+        sec["ba_solve"] = t3 - t2
         self.ba_log.append((last, it, float(log[0]), float(log[-1])))
         # the next chunk is placed after the refined last pose
         self.ctx.upload(self.d_base.data_ptr(), self.records[last].T_wc)
