@@ -74,6 +74,7 @@ def main():
         t0 = time.perf_counter()
         for c in range(n // chunk):
             fe.process_chunk(d[2 * c * chunk:2 * (c + 1) * chunk], sec)
+        fe.flush(sec)
         torch.cuda.synchronize()
         return fe, time.perf_counter() - t0, sec
 

@@ -118,6 +118,7 @@ GEOM_SIGNATURES = {
     "yv_ba_set_problem": (_I, [_P, _I, _I, _I, _P, _P, _P, _I, _P]),
     "yv_ba_solve": (_I, [_P, _P, _P, _I, _P, ctypes.POINTER(_I)]),
     "yv_ba_debug_read": (_I, [_P, _I, _P, ctypes.c_int64]),
+    "yv_ba_set_stream": (_I, [_P, _P]),
     "yv_lm_sum_mode": (_I, []),
 }
 
@@ -594,6 +595,11 @@ class BundleAdjuster:
             self.close()
         except Exception:
             pass
+
+    def set_stream(self, stream: int = 0) -> None:
+        """Run on a caller stream (yv_ba_set_stream; 0 = the context's stream)."""
+        _check(self.lib.yv_ba_set_stream(self.handle, ctypes.c_void_p(stream) if stream else None),
+               "yv_ba_set_stream")
 
     def set_problem(self, n_poses: int, n_fixed: int, n_landmarks: int, edge_pose, edge_landmark, meas, K) -> None:
         self._ep = np.ascontiguousarray(edge_pose, np.int32).reshape(-1)

@@ -882,6 +882,7 @@ struct yv_ba {
     yv_ctx* ctx = nullptr;
     int dev = 0;
     hipStream_t st = nullptr;
+    hipStream_t ctx_st = nullptr;  // the context's stream (yv_ba_set_stream(b, NULL) returns to it)
     int max_poses = 0, max_landmarks = 0, max_edges = 0;
     int64_t cv_cap = 0;
     yavo::BaParams P;
@@ -934,6 +935,7 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
     b->ctx = ctx;
     b->dev = yavo::ctx_device(ctx);
     b->st = yavo::ctx_stream(ctx);
+    b->ctx_st = b->st;
     b->max_poses = max_poses;
     b->max_landmarks = max_landmarks;
     b->max_edges = max_edges;
@@ -991,6 +993,13 @@ extern "C" void yv_ba_destroy(yv_ba* b) {
     for (void* p : b->owned) (void)hipFree(p);
     if (b->h_scal) (void)hipHostFree(b->h_scal);
     delete b;
+}
+
+extern "C" int yv_ba_set_stream(yv_ba* b, void* stream) {
+    if (!b) return YV_ERR_INVALID;
+    if (hipSetDevice(b->dev) != hipSuccess || hipStreamSynchronize(b->st) != hipSuccess) return YV_ERR_HIP;
+    b->st = stream ? reinterpret_cast<hipStream_t>(stream) : b->ctx_st;
+    return YV_OK;
 }
 
 extern "C" int yv_ba_set_problem(yv_ba* b, int n_poses, int n_fixed, int n_landmarks, const int32_t* edge_pose,

@@ -131,16 +131,24 @@ class SequenceFrontend:
         self.d_prior = torch.from_numpy(np.tile(IDENTITY, (chunk, 1))).to(dev)
         self.d_poses = torch.zeros((chunk, 7), dtype=torch.float64, device=dev)
         self.ba = BundleAdjuster(ctx, window, window * max_kp, 2 * window * max_kp)
+        self.ba_stream = torch.cuda.Stream(device=dev)  # the BA beside the next chunk's kernels
+        self.ba.set_stream(self.ba_stream.cuda_stream)
+        self._ba_pending = False
         self.records: Dict[int, FrameRecord] = {}
         self.next_frame = 0
         self.ba_log: List[Tuple[int, int, float, float]] = []  # (last frame, iterations, chi2 first, chi2 last)
 
     def close(self) -> None:
+        self.ba.set_stream(0)
         self.ba.close()
         self.batch.close()
 
     def process_chunk(self, d_images, seconds: Dict[str, float] = None) -> None:
-        """d_images: device uint8 [2 * chunk, H, W] (L_k, R_k interleaved) of frames next_frame ..."""
+        """d_images: device uint8 [2 * chunk, H, W] (L_k, R_k interleaved) of frames next_frame ...
+
+        Pipelined: this chunk's detect .. pose LM is issued on the context stream first, then the previous chunk's
+        BA window runs (its own stream, host-driven LM) while the GPU works on this chunk; the refined last pose
+        then anchors this chunk's placement. The data flow is the sequential loop's, so results are identical."""
         import time
         ctx, n, kp = self.ctx, self.chunk, self.max_kp
         t0 = time.perf_counter()
@@ -148,29 +156,45 @@ class SequenceFrontend:
         self.batch.run(d_images.data_ptr(), 2 * n, self.W, self.H * self.W, self.match_thr,
                        carry_from=2 * (n - 1))
         self.batch.track_map(self.d_prior.data_ptr(), self.d_poses.data_ptr(), first, 1, self.d_block.data_ptr(), n)
+        t1 = time.perf_counter()
+        ba_sec = {}
+        if self._ba_pending:
+            self._local_ba(ba_sec)  # the previous chunk's window, beside this chunk's kernels
+        t2 = time.perf_counter()
         ctx.map_place(self.d_block.data_ptr(), 1, self.bb, self.d_base.data_ptr(), self.d_anchors.data_ptr())
         ctx.sync()
-        t1 = time.perf_counter()
+        t3 = time.perf_counter()
         v = self.batch.view()
         block = ctx.download(self.d_block.data_ptr(), np.uint8, self.bb)
         uv = ctx.download(v.edge_uv, np.float64, n * kp * 2).reshape(n, kp, 2)
         q = ctx.download(v.edge_query, np.int32, n * kp).reshape(n, kp)
         m = ctx.download(v.matches, np.uint8, 2 * n * kp * 100).reshape(2 * n, kp, 100)[0::2]
         own = m[:, :, 48:56].copy().view(np.int32).reshape(n, kp, 2)  # Matches::pt2.{x, y}
-        t2 = time.perf_counter()
         self.records.update(frame_records_from_block(block, uv, q, own))
         self.next_frame = first + n
-        ba_sec = {}
-        self._local_ba(ba_sec)
-        t3 = time.perf_counter()
+        self._ba_pending = True
+        t4 = time.perf_counter()
         if seconds is not None:
-            for key, dt in (("device", t1 - t0), ("download", t2 - t1), ("ba", t3 - t2)):
+            for key, dt in (("issue", t1 - t0), ("ba", t2 - t1), ("device_wait", t3 - t2), ("download", t4 - t3)):
                 seconds[key] = seconds.get(key, 0.0) + dt
             for key, dt in ba_sec.items():
                 seconds[key] = seconds.get(key, 0.0) + dt
 
+    def flush(self, seconds: Dict[str, float] = None) -> None:
+        """The last chunk's BA window (process_chunk runs each window one chunk late)."""
+        import time
+        if self._ba_pending:
+            t0 = time.perf_counter()
+            ba_sec = {}
+            self._local_ba(ba_sec)
+            if seconds is not None:
+                seconds["ba"] = seconds.get("ba", 0.0) + time.perf_counter() - t0
+                for key, dt in ba_sec.items():
+                    seconds[key] = seconds.get(key, 0.0) + dt
+
     def _local_ba(self, sec) -> None:
         import time
+        self._ba_pending = False
         last = self.next_frame - 1
         frames = list(range(max(0, last - self.window + 1), last + 1))
         if len(frames) <= self.n_fixed:
@@ -193,5 +217,6 @@ class SequenceFrontend:
         self.ctx.upload(self.d_base.data_ptr(), self.records[last].T_wc)
 
     def trajectory(self) -> np.ndarray:
-        """[n_frames, 7] T_wc in frame order."""
+        """[n_frames, 7] T_wc in frame order (after the last BA window)."""
+        self.flush()
         return np.stack([self.records[g].T_wc for g in sorted(self.records)])
