@@ -340,9 +340,15 @@ class Context(_GeomMixin):
     def sync(self) -> None:
         _check(self.lib.yv_sync(self.handle), "yv_sync")
 
-    def download(self, dev_ptr: int, dtype, count: int) -> np.ndarray:
-        """Copy `count` elements of `dtype` from device memory to a new host array."""
-        out = np.zeros(max(count, 1), dtype=dtype)
+    def download(self, dev_ptr: int, dtype, count: int, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """Copy `count` elements of `dtype` from device memory to a new host array, or into `out` (contiguous,
+        e.g. a pinned buffer: a DMA instead of the pageable staging copy)."""
+        if out is None:
+            out = np.zeros(max(count, 1), dtype=dtype)
+        else:
+            out = out.reshape(-1).view(dtype)
+            if not out.flags["C_CONTIGUOUS"] or out.size < count:
+                raise ValueError("download: `out` must be contiguous and hold `count` elements")
         nbytes = out.dtype.itemsize * count
         _check(self.lib.yv_download(self.handle, _ptr(out), ctypes.c_void_p(dev_ptr), nbytes), "yv_download")
         return out[:count]

@@ -130,6 +130,13 @@ class SequenceFrontend:
         self.d_anchors = torch.zeros((1, 7), dtype=torch.float64, device=dev)
         self.d_prior = torch.from_numpy(np.tile(IDENTITY, (chunk, 1))).to(dev)
         self.d_poses = torch.zeros((chunk, 7), dtype=torch.float64, device=dev)
+        # pinned read-back buffers (block, edge uv / query, the temporal pairs' match records): DMA, not staging
+        def pinned(nbytes):
+            return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True).numpy()
+        self._h_block = pinned(self.bb)
+        self._h_uv = pinned(chunk * max_kp * 16)
+        self._h_q = pinned(chunk * max_kp * 4)
+        self._h_m = pinned(2 * chunk * max_kp * 100)
         self.ba = BundleAdjuster(ctx, window, window * max_kp, 2 * window * max_kp)
         self.ba_stream = torch.cuda.Stream(device=dev)  # the BA beside the next chunk's kernels
         self.ba.set_stream(self.ba_stream.cuda_stream)
@@ -165,10 +172,10 @@ class SequenceFrontend:
         ctx.sync()
         t3 = time.perf_counter()
         v = self.batch.view()
-        block = ctx.download(self.d_block.data_ptr(), np.uint8, self.bb)
-        uv = ctx.download(v.edge_uv, np.float64, n * kp * 2).reshape(n, kp, 2)
-        q = ctx.download(v.edge_query, np.int32, n * kp).reshape(n, kp)
-        m = ctx.download(v.matches, np.uint8, 2 * n * kp * 100).reshape(2 * n, kp, 100)[0::2]
+        block = ctx.download(self.d_block.data_ptr(), np.uint8, self.bb, out=self._h_block)
+        uv = ctx.download(v.edge_uv, np.float64, n * kp * 2, out=self._h_uv).reshape(n, kp, 2)
+        q = ctx.download(v.edge_query, np.int32, n * kp, out=self._h_q).reshape(n, kp)
+        m = ctx.download(v.matches, np.uint8, 2 * n * kp * 100, out=self._h_m).reshape(2 * n, kp, 100)[0::2]
         own = m[:, :, 48:56].copy().view(np.int32).reshape(n, kp, 2)  # Matches::pt2.{x, y}
         self.records.update(frame_records_from_block(block, uv, q, own))
         self.next_frame = first + n
