@@ -40,7 +40,7 @@ def load(out_dir, counter):
 
 def main():
     out_dir = sys.argv[1]
-    frames = 256  # bench.py's default
+    frames = 512  # bench.py's default (--frames)
     args = sys.argv[2:]
     if "--frames" in args:
         frames = int(args[args.index("--frames") + 1])
