@@ -29,6 +29,6 @@ run bench 900 python bench.py "$@"; st=$?; ok $st || exit $st
 [ "${PROFILE:-1}" = "1" ] || exit 0
 export TMPDIR=/tmp
 run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
-    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --cpu-baseline none "$@"; st=$?; ok $st || exit $st
+    python3 "$ROOT/bench.py" --cpu-baseline none "$@"; st=$?; ok $st || exit $st
 find "$OUT/prof" -name "*stats*" | head
 exit 0
