@@ -48,7 +48,10 @@ def max_keyframes(n_frames: int, first_frame: int, kf_every: int) -> int:
 
 def parse_block(buf) -> Tuple[np.ndarray, np.ndarray, List[np.ndarray]]:
     """(header, written keyframes, per-keyframe written landmarks) of one block (bytes / uint8 array)."""
-    raw = np.frombuffer(bytes(buf) if not isinstance(buf, np.ndarray) else buf.tobytes(), np.uint8)
+    if isinstance(buf, np.ndarray) and buf.dtype == np.uint8 and buf.flags["C_CONTIGUOUS"]:
+        raw = buf.reshape(-1)  # views into the caller's buffer (no 1+ MB copy); callers copy what they keep
+    else:
+        raw = np.frombuffer(bytes(buf) if not isinstance(buf, np.ndarray) else buf.tobytes(), np.uint8)
     h = raw[:HEADER_DTYPE.itemsize].view(HEADER_DTYPE)[0]
     max_kf, stride, n_kf = int(h["max_kf"]), int(h["lm_stride"]), int(h["n_kf"])
     if not 0 <= n_kf <= max_kf:
