@@ -137,7 +137,8 @@ int yv_batch_set_track_lk(yv_batch* b, int image_step, int win, int max_level, i
  * on the run stream around every stage).  Stages: 0 detect (FAST + Harris + blur, one fused kernel),
  * 1 top-K + checkBoundry, 2 BRIEF, 3 match, 4 Matches records + removeOutliers (+ carry copies),
  * 5 track edges (stereo triangulation), 6 track poses (LM).  ms[i] = summed milliseconds, *n_runs = runs
- * accumulated (stages 5-6 summed over the runs followed by yv_batch_track). */
+ * accumulated (stages 5-6 summed over the runs followed by yv_batch_track).  on = 2: events around the
+ * detect kernel only (ms[0]; the other stages read 0) -- two events per run instead of nine. */
 int yv_batch_enable_timing(yv_batch* b, int on);
 int yv_batch_stage_times(yv_batch* b, float* ms /* [8] */, int* n_runs);
 #define YV_NUM_STAGES 7

@@ -227,6 +227,12 @@ def test_batch_is_deterministic_and_timed(ctx):
     np.testing.assert_array_equal(outs[0], outs[2])
     ms, n = b.stage_times()
     assert n == 3 and np.all(ms[:5] > 0) and np.all(ms[5:] == 0)  # no tracks set: stages 5-6 idle
+    b.enable_timing(2)  # detect-only events (bench.py's timed region): same results, only ms[0]
+    b.run(d.data_ptr(), 4, W, H * W, 20)
+    ctx.sync()
+    np.testing.assert_array_equal(ctx.download(b.view().matches, yv.MATCH_DTYPE, 3 * 2000), outs[0])
+    ms, n = b.stage_times()
+    assert n == 1 and ms[0] > 0 and np.all(ms[1:] == 0)
     b.close()
 
 

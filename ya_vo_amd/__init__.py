@@ -490,8 +490,10 @@ class Batch:
     def track_sync(self) -> None:
         _check(self.lib.yv_batch_track_sync(self.handle), "yv_batch_track_sync")
 
-    def enable_timing(self, on: bool = True) -> None:
-        _check(self.lib.yv_batch_enable_timing(self.handle, 1 if on else 0), "yv_batch_enable_timing")
+    def enable_timing(self, on=True) -> None:
+        """on: False/0 off, True/1 every stage, 2 the detect kernel only (yavo.h)."""
+        mode = 2 if (not isinstance(on, bool) and on == 2) else (1 if on else 0)
+        _check(self.lib.yv_batch_enable_timing(self.handle, mode), "yv_batch_enable_timing")
 
     def stage_times(self) -> Tuple[np.ndarray, int]:
         ms = np.zeros(8, np.float32)

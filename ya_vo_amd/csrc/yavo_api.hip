@@ -114,7 +114,7 @@ struct yv_batch {
     hipEvent_t ev_map_release = nullptr;  // the block's readers (yv_batch_map_release): the next block write waits
     bool map_release_pending = false;
     // stage timing: events 0..5 bracket the run's stages, 6..8 the track's
-    bool timing = false;
+    int timing = 0;  // 0 off, 1 every stage, 2 detect only
     std::vector<hipEvent_t> events;  // kEvPerRun per recorded run
     std::vector<uint8_t> tracked;    // run r was followed by a timed yv_batch_track
     int runs_recorded = 0;
@@ -218,6 +218,7 @@ int ensure_single(yv_ctx* ctx, int H, int W) {
 
 int record_stage(yv_batch* b, hipStream_t s, int run, int stage) {
     if (!b->timing || run < 0) return YV_OK;
+    if (b->timing == 2 && stage > 1) return YV_OK;  // detect-only: the two events around the detect kernel
     YV_HIP(hipEventRecord(b->events[(size_t)run * kEvPerRun + stage], s));
     return YV_OK;
 }
@@ -432,7 +433,7 @@ int yv_batch_enable_timing(yv_batch* b, int on) {
         for (auto& e : b->events) YV_HIP(hipEventCreate(&e));
         b->tracked.assign(kMaxTimedRuns, 0);
     }
-    b->timing = on != 0;
+    b->timing = on == 2 ? 2 : (on != 0 ? 1 : 0);
     b->runs_recorded = 0;
     b->last_run = -1;
     std::fill(b->tracked.begin(), b->tracked.end(), 0);
@@ -447,6 +448,13 @@ int yv_batch_stage_times(yv_batch* b, float* ms, int* n_runs) {
     if (runs == 0) return YV_OK;
     for (int r = 0; r < runs; ++r) {
         const hipEvent_t* ev = &b->events[(size_t)r * kEvPerRun];
+        if (b->timing == 2) {
+            float t = 0.f;
+            YV_HIP(hipEventSynchronize(ev[1]));
+            YV_HIP(hipEventElapsedTime(&t, ev[0], ev[1]));
+            ms[0] += t;
+            continue;
+        }
         YV_HIP(hipEventSynchronize(ev[b->tracked[r] ? 8 : 5]));
         for (int st = 0; st < 5; ++st) {
             float t = 0.f;
@@ -757,7 +765,7 @@ int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stre
     int32_t* eq = b->edge_query + k * nt * nk;
     int32_t* ec = b->edge_count + k * nt;
     const int run = b->last_run;
-    const bool timed = b->timing && run >= 0 && !b->tracked[run];
+    const bool timed = b->timing == 1 && run >= 0 && !b->tracked[run];
     hipEvent_t* ev = timed ? &b->events[(size_t)run * kEvPerRun] : nullptr;
     // buffer k was last read by the LM two tracks ago (side stream): the build must not overwrite it early
     if (b->lm_pending[k]) YV_HIP(hipStreamWaitEvent(s, b->ev_lm[k], 0));
