@@ -8,7 +8,9 @@ matching L_{k-1} -> L_k (the reference's temporal matchFeatures, src/LoopHandler
 (LoopHandler::triangulation) and the pose-only LM (LoopHandler::optimizePoseOnly) solves every frame's pose
 from the kept temporal matches, and the chunk's shared-map block (keyframe poses + LM-inlier landmarks,
 include/yavo/yavo_map.h) is written after the LM.  `value` = stereo frames per second over all GPUs
-(max-over-ranks wall time).  One process per GPU; frames shard across ranks (weak scaling).  The only
+(max-over-ranks wall time).  One process per GPU; ONE sequence shards across ranks (weak scaling): rank r owns
+frames [1 + rB, 1 + (r+1)B) and detects / describes its predecessor frame rB in the same run (the 1-frame halo,
+ya_vo_amd.sharding.FrameShard), so no image stage communicates.  The only
 collective is the shared map's: every step the ranks all-gather their map blocks (RCCL over xGMI) on a
 communication stream and place them in world coordinates, overlapped with the next step's image kernels.
 
@@ -43,7 +45,9 @@ def parse():
     ap.add_argument("--frames", type=int, default=512,
                     help="stereo frames per step per GPU (512: two pose-LM problems per CU, 137.7k vs 130.0k frames/s at 256)")
     ap.add_argument("--cpu-baseline", choices=["both", "literal", "efficient", "none"], default="both")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads of the CPU baseline (0: the usable cores, affinity capped by OMP_NUM_THREADS)")
+    ap.add_argument("--literal-frames", type=int, default=20, help="frames of the ref-literal CPU sample")
     ap.add_argument("--no-timing", action="store_true", help="do not record per-stage HIP events")
     ap.add_argument("--stage-steps", type=int, default=5,
                     help="steps of the separate per-stage pass after the timed region (events around every stage)")
@@ -59,10 +63,9 @@ def parse():
     return ap.parse_args()
 
 
-def stage_bytes(counts, B):
-    """Algorithmic HBM bytes per launch of each stage (DESIGN.md 'Algorithmic bytes')."""
+def stage_bytes(counts, n_img):
+    """Algorithmic HBM bytes per launch of each stage over n_img images (DESIGN.md 'Algorithmic bytes')."""
     img = H * W
-    n_img = 2 * B
     cand = float(np.sum(counts["cand"][:n_img]))
     det = float(np.sum(counts["det"][:n_img]))
     kp = float(np.sum(counts["kp"][:n_img]))
@@ -86,9 +89,8 @@ def stage_bytes(counts, B):
     }
 
 
-def stage_valu_ops(counts, B):
+def stage_valu_ops(counts, n_img):
     """Algorithmic lane-operations of the VALU-bound stages, SURVEY.md 8(d)'s per-unit figures."""
-    n_img = 2 * B
     kq = counts["match"].astype(np.float64)
     kt = counts["train"].astype(np.float64)
     # detect: FAST P * (16 abs-diff-compare + run scan) = 36 M lane-ops per image (SURVEY 8d) + the 9x9
@@ -97,57 +99,122 @@ def stage_valu_ops(counts, B):
     return {"detect": n_img * (36.0e6 + 18.0 * H * W), "match": float(np.sum(kq * kt)) * 18.0}
 
 
-def cpu_baseline(kind, threads, offsets, frames, gpu_poses):
-    """Oracle (CPU restatement of the reference) on the GPU box's host cores, bounded sample of the SAME
-    frames the GPU processed; the CPU poses are compared with the GPU's (pose RMSE vs the CPU path)."""
+def cpu_threads_available() -> int:
+    """Host cores this process may use: its affinity mask, capped by OMP_NUM_THREADS (the GPU box sets it to the
+    CPU share of one GPU, 16; os.cpu_count() there reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(omp))) if omp.isdigit() and int(omp) > 0 else n
+
+
+def cpu_baseline(kind, threads, offsets, images, B, gpu_poses, edges, literal_frames=20):
+    """Oracle (CPU restatement of the reference) on the GPU box's host cores, on bounded samples of the SAME frames
+    the GPU processed.  images: the shard layout (L_k, R_k interleaved, then the halo frame's left image at 2B).
+
+    literal:   the reference's costs (per-pixel ring rebuild, three whole-image products per corner, bit-loop
+               popcount), one thread per frame; `literal_frames` frames run concurrently on `threads` cores and the
+               median frame time is reported (value = 1 / median).
+    efficient: the same outputs (local Harris sums, precomputed ring), `threads` threads over frames.
+    Both report per-stage milliseconds per frame (FAST+Harris, blur+BRIEF, match+removeOutliers, triangulation,
+    pose LM; the timers of src/FastDetector.cc:289,336-349 and src/LoopHandler.cc:471-482 split the same way).
+    pose_check: the GPU's relative poses against the CPU chain (bit-identity in the kernel's edge-sum order on the
+    sample frames) and, over EVERY frame of the step, the pose LM on the GPU's edges in the reference's sequential
+    sum order (sum_mode 0): the metric's "RMSE vs CPU ref"."""
+    from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bind
     from track_chain import track_pose
+    import ya_vo_amd as yv
     from ya_vo_amd import scene
     orc = oracle_bind.Oracle()
 
-    def one_frame(k, prev_left_kp, mode):
-        kps = []
-        for img in frames[2 * k:2 * k + 2]:
-            rc, _, _ = orc.fast(img, MAX_KP, mode=mode)
-            kps.append(orc.brief(img, rc, offsets))
-        # temporal + stereo Matches, removeOutliers, triangulation, pose LM (tests/track_chain.py)
-        return kps[0], track_pose(orc, prev_left_kp, kps[0], kps[1], scene.K_KITTI, T_RIGHT)[3]
+    def prev_image(k):
+        return images[2 * B] if k == 0 else images[2 * (k - 1)]
 
-    def left_kp(k):
-        return orc.brief(frames[2 * k], orc.fast(frames[2 * k], MAX_KP)[0], offsets)
+    def left_kp(img):
+        return orc.brief(img, orc.fast(img, MAX_KP)[0], offsets)
+
+    def one_frame(k, prev_left_kp, mode):
+        """Frame k (track k): detect+describe L_k, R_k; temporal + stereo matches; triangulation; pose LM."""
+        timers = {}
+        t_start = time.perf_counter()
+        kps = []
+        for img in images[2 * k:2 * k + 2]:
+            t0 = time.perf_counter()
+            rc, _, _ = orc.fast(img, MAX_KP, mode=mode)
+            t1 = time.perf_counter()
+            kps.append(orc.brief(img, rc, offsets))
+            t2 = time.perf_counter()
+            timers["fast_harris"] = timers.get("fast_harris", 0.0) + t1 - t0
+            timers["blur_brief"] = timers.get("blur_brief", 0.0) + t2 - t1
+        T = track_pose(orc, prev_left_kp, kps[0], kps[1], scene.K_KITTI, T_RIGHT, timers=timers)[3]
+        return T, time.perf_counter() - t_start, timers
+
+    def stage_table(results):
+        keys = ("fast_harris", "blur_brief", "match", "triangulate", "pose_lm")
+        return {key: round(1e3 * float(np.mean([r[2].get(key, 0.0) for r in results])), 3) for key in keys}
 
     res, cpu_poses = {}, {}
     if kind in ("both", "literal"):
-        prev = left_kp(0)
+        n = min(literal_frames, B)
+        prevs = [left_kp(prev_image(k)) for k in range(n)]  # frame k-1's keypoints, as the reference carries them
         t0 = time.perf_counter()
-        _, cpu_poses[1] = one_frame(1, prev, 0)
-        dt = time.perf_counter() - t0
-        res["literal"] = {"value": 1.0 / dt, "unit": "frames/s", "cores": 1, "kind": "port",
-                          "sample": "frame 1 of the benchmarked batch (detect+describe L,R; match L0->L1, "
-                                    "L1->R1; removeOutliers; triangulation; pose LM), ref-literal costs: "
-                                    "per-pixel ring rebuild, three whole-image products per corner "
-                                    "(src/FastDetector.cc:249-251), bit-loop popcount; single thread",
-                          "seconds": dt}
+        with ThreadPoolExecutor(min(threads, n)) as ex:  # ctypes releases the GIL inside the oracle
+            out = list(ex.map(lambda k: one_frame(k, prevs[k], 0), range(n)))
+        wall = time.perf_counter() - t0
+        per = np.array([r[1] for r in out])
+        for k, r in enumerate(out):
+            cpu_poses[k] = r[0]
+        res["literal"] = {"value": 1.0 / float(np.median(per)), "unit": "frames/s", "cores": 1, "kind": "port",
+                          "sample": f"frames 0..{n - 1} of the benchmarked shard (detect+describe L,R; match "
+                                    "L_{k-1}->L_k, L_k->R_k; removeOutliers; triangulation; pose LM) with the "
+                                    "reference's costs: per-pixel ring rebuild, three whole-image products per corner "
+                                    "(src/FastDetector.cc:249-251), bit-loop popcount; one thread per frame, "
+                                    f"{n} frames run concurrently on {min(threads, n)} cores, value = 1 / median "
+                                    "frame time",
+                          "median_frame_s": round(float(np.median(per)), 4),
+                          "min_frame_s": round(float(per.min()), 4), "max_frame_s": round(float(per.max()), 4),
+                          "frames": n, "wall_s": round(wall, 3), "stages_ms_per_frame": stage_table(out)}
     if kind in ("both", "efficient"):
-        from concurrent.futures import ThreadPoolExecutor
-        nfr = min(2 * threads, len(frames) // 2 - 1)
-        lefts = [left_kp(k) for k in range(nfr)]
+        n = min(2 * threads, B)
+        prevs = [left_kp(prev_image(k)) for k in range(n)]
         t0 = time.perf_counter()
-        with ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL inside the oracle
-            out = list(ex.map(lambda k: one_frame(k + 1, lefts[k], 1), range(nfr)))
+        with ThreadPoolExecutor(threads) as ex:
+            out = list(ex.map(lambda k: one_frame(k, prevs[k], 1), range(n)))
         dt = time.perf_counter() - t0
-        for k, (_, T) in enumerate(out):
-            cpu_poses[k + 1] = T
-        res["efficient"] = {"value": nfr / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-                            "sample": f"frames 1..{nfr} of the benchmarked batch, same outputs with local Harris "
-                                      f"sums and a precomputed ring, {threads} threads over frames", "seconds": dt}
+        for k, r in enumerate(out):
+            cpu_poses[k] = r[0]
+        res["efficient"] = {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+                            "sample": f"frames 0..{n - 1} of the benchmarked shard, same outputs with local Harris "
+                                      f"sums and a precomputed ring, {threads} threads over frames",
+                            "seconds": round(dt, 3), "stages_ms_per_frame": stage_table(out)}
     ks = sorted(cpu_poses)
-    d = np.array([gpu_poses[k] - cpu_poses[k] for k in ks])
-    res["pose_check"] = {"frames": len(ks), "pose_rmse_vs_cpu_ref": float(np.sqrt(np.mean(d[:, 4:] ** 2))),
-                         "max_abs_diff": float(np.abs(d).max()),
-                         "bit_identical": bool(np.array_equal(np.array([gpu_poses[k] for k in ks]),
-                                                              np.array([cpu_poses[k] for k in ks])))}
+    same = bool(np.array_equal(np.array([gpu_poses[k] for k in ks]), np.array([cpu_poses[k] for k in ks])))
+    # every frame of the step: the oracle's pose LM on the GPU's own edges, in the kernel's order (must reproduce the
+    # GPU pose bit for bit) and in the reference's sequential order (the metric's RMSE)
+    ec, eX, euv = edges
+    prior = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
+
+    def both_orders(k):
+        X, uv = eX[k, :ec[k]], euv[k, :ec[k]]
+        return (orc.pose_lm(X, uv, scene.K_KITTI, prior, yv.lm_sum_mode())[0],
+                orc.pose_lm(X, uv, scene.K_KITTI, prior, 0)[0])
+
+    with ThreadPoolExecutor(threads) as ex:
+        lm = list(ex.map(both_orders, range(len(ec))))
+    gpu_order = np.array([x[0] for x in lm])
+    seq_order = np.array([x[1] for x in lm])
+    d = gpu_poses - seq_order
+    res["pose_check"] = {
+        "frames": len(ec),
+        "pose_rmse_vs_cpu_ref": float(np.sqrt(np.mean(np.sum(d[:, 4:] ** 2, axis=1)))),
+        "max_abs_diff_vs_cpu_ref": float(np.abs(d).max()),
+        "cpu_ref": "oracle pose LM (optimizePoseOnly) in the reference's sequential edge order (sum_mode 0) on the "
+                   "GPU's edges, every frame of the step",
+        "bit_identical_gpu_order_all_frames": bool(np.array_equal(gpu_poses, gpu_order)),
+        "chain_frames": len(ks),
+        "chain_bit_identical": same,
+        "chain": "full CPU chain (detect .. pose LM) of the cpu_baseline sample frames vs the GPU, kernel sum order"}
     return res
 
 
@@ -156,6 +223,9 @@ def main():
     import torch
     import torch.distributed as dist
     import ya_vo_amd as yv
+    from ya_vo_amd import map as ymap
+    from ya_vo_amd import scene
+    from ya_vo_amd.sharding import FrameShard, shard_images
     from ya_vo_amd.synth import synth_stereo_batch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -175,88 +245,30 @@ def main():
     ctx = yv.Context(dev_index)
     ctx.set_brief_offsets(offsets)
     B = args.frames
-    n_img = 2 * B
-    # each rank owns a contiguous chunk of the sequence (frame sharding)
-    frames = synth_stereo_batch(1234 + rank, B, start=rank * B)
-    d_frames = torch.from_numpy(frames).to(dev)
-    batch = yv.Batch(ctx, n_img, H, W, MAX_KP, n_img)
-    carry = n_img
-    pairs, tracks = [], []
-    for k in range(B):
-        pairs.append((carry if k == 0 else 2 * (k - 1), 2 * k))  # temporal L_{k-1} -> L_k
-        pairs.append((2 * k, 2 * k + 1))                          # stereo L_k -> R_k
-        if args.tracker == "match":
-            tracks.append((2 * k + 1, 2 * k))                     # PnP of frame k-1 against frame k's map
-        elif k > 0:
-            tracks.append((2 * (k - 1) + 1, 2 * k))               # LK: frame k-1's stereo map -> L_k
-    batch.set_pairs(pairs)
-    from ya_vo_amd import scene
-    if args.tracker == "lk":
-        batch.set_track_lk(2)  # LK images = the left images 0, 2, 4, ...
-    batch.set_tracks(tracks, scene.K_KITTI, T_RIGHT)
-    NT = len(tracks)
-    identity = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
-    d_prior = torch.from_numpy(np.tile(identity, (NT, 1))).to(dev)
-    # the pose LM of step i runs on the batch's side stream beside step i + 1's image kernels; its output
-    # buffer alternates so step i + 1 never writes poses step i's LM is still producing
-    batch.set_track_overlap(0 if args.no_overlap else args.overlap_mode)
-    d_poses = [torch.zeros((NT, 7), dtype=torch.float64, device=dev) for _ in range(2)]
-    calls = [0]
-
-    # shared map (include/yavo/yavo_map.h): this rank's chunk block after the LM, all-gathered over RCCL and
-    # placed in world coordinates on a communication stream; the next block write waits for the gather only
-    from ya_vo_amd import map as ymap
+    # one sequence (one synthetic field) sharded over the ranks: rank r owns frames
+    # [1 + r B, 1 + (r + 1) B) and recomputes its predecessor frame r B (the 1-frame halo) in the same run, so its
+    # first temporal pair is the sequence's own L_{rB} -> L_{rB+1}; frame 0 is the sequence's first (no predecessor)
+    first = 1 + rank * B
+    fr = synth_stereo_batch(1234, B + 1, start=first - 1)  # [2(B+1), H, W]: the halo frame, then the shard
+    images = shard_images(fr[2:], fr[0])
+    del fr
+    n_img = images.shape[0]
+    d_frames = torch.from_numpy(images).to(dev)
     use_map = args.kf_every > 0 and args.tracker == "match"
-    first_frame = rank * B  # track k relates frame rank * B + k to its predecessor (the carry slot for k = 0)
-    if use_map:
-        max_kf = max(ymap.max_keyframes(NT, r * B, args.kf_every) for r in range(world))
-        max_kf = max(max_kf, 1)
-        bb = ymap.block_bytes(max_kf, MAX_KP)
-        d_block = torch.zeros(bb, dtype=torch.uint8, device=dev)
-        d_gathered = torch.zeros((world, bb), dtype=torch.uint8, device=dev) if world > 1 else d_block
-        d_base = torch.from_numpy(identity.copy()).to(dev)
-        d_anchors = torch.zeros((world, 7), dtype=torch.float64, device=dev)
-        comm = torch.cuda.Stream(device=dev)
-
-    pending = [False]
-
-    def exchange():
-        # the last track_map's block: all-gathered and placed on the communication stream once it is written
-        batch.map_wait(comm.cuda_stream)
-        with torch.cuda.stream(comm):
-            if world > 1 and backend == "nccl":
-                dist.all_gather_into_tensor(d_gathered, d_block)
-            elif world > 1:  # gloo rehearsal (YAVO_BENCH_BACKEND=gloo): list form
-                dist.all_gather(list(d_gathered.unbind(0)), d_block)
-            ctx.map_place(d_gathered.data_ptr(), world, bb, d_base.data_ptr(), d_anchors.data_ptr(),
-                          stream=comm.cuda_stream)
-        batch.map_release(comm.cuda_stream)
-        pending[0] = False
+    max_kf = max(ymap.max_keyframes(B, 1 + r * B, args.kf_every) for r in range(world)) if use_map else 0
+    shard = FrameShard(ctx, B, first, scene.K_KITTI, T_RIGHT, halo=True, world=world, rank=rank, backend=backend,
+                       kf_every=args.kf_every if use_map else 0, max_kf=max_kf,
+                       overlap_mode=0 if args.no_overlap else args.overlap_mode, tracker=args.tracker)
+    batch = shard.batch
+    NT = shard.n_tracks
+    pairs, tracks = shard.pairs, shard.tracks
 
     def step():
-        # overlap modes 2 / 3 launch the previous step's pose LM (and its map block) inside this run, so the
-        # previous block is exchanged after it (one step behind: map_wait before the launch would force it early)
-        batch.run(d_frames.data_ptr(), n_img, W, H * W, 20, carry_from=2 * (B - 1))
-        if pending[0]:
-            exchange()
-        if not use_map:
-            batch.track(d_prior.data_ptr(), d_poses[calls[0] & 1].data_ptr())
-        else:
-            batch.track_map(d_prior.data_ptr(), d_poses[calls[0] & 1].data_ptr(), first_frame, args.kf_every,
-                            d_block.data_ptr(), max_kf)
-            pending[0] = True
-        calls[0] += 1
-
-    def drain():
-        if pending[0]:
-            exchange()
+        shard.step(d_frames.data_ptr())
 
     for _ in range(args.warmup):
         step()
-    drain()
-    ctx.sync()
-    batch.track_sync()
-    torch.cuda.synchronize()
+    shard.drain()
     if not args.no_timing:
         # inside the timed region only the dominant kernel (detect) is bracketed by events; the per-stage table
         # comes from a separate pass after it (--stage-steps), so nine events per step do not tax `value`
@@ -268,9 +280,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    drain()
-    ctx.sync()
-    batch.track_sync()
+    shard.drain()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -279,9 +289,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # PCIe-inclusive rate (DESIGN.md 6): the same step's frames uploaded from pinned host memory, timed alone;
+    # PCIe-inclusive rate (DESIGN.md 7): the same step's frames uploaded from pinned host memory, timed alone;
     # reported beside `value` (which has the inputs resident in HBM), never as it
-    h_frames = torch.from_numpy(frames).pin_memory()
+    h_frames = torch.from_numpy(images).pin_memory()
     d_up = torch.empty_like(d_frames)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -300,10 +310,16 @@ def main():
         "filt": ctx.download(v.filt_count, np.int32, len(pairs)).astype(np.int64),
     }
     counts["train"] = np.array([counts["kp"][t] for _, t in pairs], np.int64)
-    counts["edges"] = float(np.sum(ctx.download(v.edge_count, np.int32, NT)))
+    ec = ctx.download(v.edge_count, np.int32, NT)
+    counts["edges"] = float(np.sum(ec))
     counts["tq"] = float(np.sum([counts["match"][tp] for _, tp in tracks])) if args.tracker == "match" else 0.0
     inliers = ctx.download(v.track_inliers, np.int32, NT)
-    gpu_poses = d_poses[(calls[0] - 1) & 1].cpu().numpy()
+    gpu_poses = shard.poses()
+    edges = None
+    if rank == 0 and world == 1 and args.cpu_baseline != "none" and args.tracker == "match":
+        eX = ctx.download(v.edge_X, np.float64, NT * MAX_KP * 3).reshape(NT, MAX_KP, 3)
+        euv = ctx.download(v.edge_uv, np.float64, NT * MAX_KP * 2).reshape(NT, MAX_KP, 2)
+        edges = (ec, eX, euv)
 
     stages = {}
     roofline = None
@@ -314,15 +330,12 @@ def main():
         batch.enable_timing(True)
         for _ in range(args.stage_steps):
             step()
-        drain()
-        ctx.sync()
-        batch.track_sync()
-        torch.cuda.synchronize()
+        shard.drain()
         ms, nruns = batch.stage_times()
         per_launch_ms = {name: float(ms[i]) / max(nruns, 1) for i, name in enumerate(yv.STAGE_NAMES)}
         per_launch_ms["detect"] = detect_timed_ms
         stages = {k: round(x, 4) for k, x in per_launch_ms.items()}
-        nbytes = stage_bytes(counts, B)
+        nbytes = stage_bytes(counts, n_img)
         # the dominant kernel is the longest on the critical path: with overlap the pose LM runs beside the
         # next batch on the side stream and is not on it
         crit = {k: t for k, t in per_launch_ms.items() if args.no_overlap or k != "track_pose"}
@@ -343,7 +356,7 @@ def main():
                     "algorithmic_bytes_per_launch": int(nbytes[dom]), "launch_ms": round(per_launch_ms[dom], 4)}
         # every stage against the bound that limits it: VALU lane-ops for detect, int8 MFMA ops
         # for the matcher (2 * Kq * Kt * 256 per pair), HBM bytes for the rest
-        ops = stage_valu_ops(counts, B)
+        ops = stage_valu_ops(counts, n_img)
         per_stage = {}
         for st, t_ms in per_launch_ms.items():
             if t_ms <= 0:
@@ -388,6 +401,10 @@ def main():
                                "kp/image, stereo triangulation + pose-only LM per frame",
                    "H": H, "W": W, "max_kp": MAX_KP, "frames_per_step_per_gpu": B, "images_per_frame": 2,
                    "match_pairs_per_frame": 2,
+                   "frames": f"one synthetic sequence (field seed 1234); rank r owns frames [1 + r*B, 1 + (r+1)*B) "
+                             f"and detects / describes its predecessor frame r*B in the same run (1-frame halo, "
+                             f"image {n_img - 1}), so every temporal pair L_(k-1) -> L_k is the sequence's own",
+                   "halo_images_per_step_per_gpu": 1,
                    "parallelism": f"frame-sharded x{world}" + (f", {'RCCL' if backend == 'nccl' else backend} "
                                                                  "all-gather of shared-map blocks"
                                                                  if use_map and world > 1 else ""),
@@ -409,7 +426,8 @@ def main():
     }
     if use_map:
         # the last placed map (rank 0's copy of every rank's block): its keyframes and landmarks per step
-        raw = d_gathered.cpu().numpy().reshape(world, bb)
+        raw = shard.placed_map()
+        bb = shard.bb
         n_kf = n_lm = 0
         for r in range(world):
             h, kfs, lms = ymap.parse_block(raw[r])
@@ -421,16 +439,19 @@ def main():
                                             "all_gather_into_tensor (RCCL)" if backend == "nccl" else
                                             f"all_gather ({backend} rehearsal)")}
     if rank == 0 and world == 1 and args.cpu_baseline != "none" and args.tracker == "match":
-        cb = cpu_baseline(args.cpu_baseline, args.cpu_threads, offsets.reshape(256, 4), frames, gpu_poses)
+        threads = args.cpu_threads or cpu_threads_available()
+        cb = cpu_baseline(args.cpu_baseline, threads, offsets.reshape(256, 4), images, B, gpu_poses, edges,
+                          args.literal_frames)
         main_cb = cb.get("literal") or cb.get("efficient")
         out["cpu_baseline"] = main_cb
         if "efficient" in cb and main_cb is not cb["efficient"]:
             out["cpu_baseline_efficient"] = cb["efficient"]
         out["cpu_baseline_host_cpus"] = os.cpu_count()
+        out["cpu_baseline_usable_cpus"] = cpu_threads_available()
         out["pose_check"] = cb["pose_check"]
     if rank == 0:
         print(json.dumps(out), flush=True)
-    batch.close()
+    shard.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -1,0 +1,82 @@
+"""The multi-rank product path shards ONE sequence (BASELINE configs[3] in miniature): two ranks, each
+a fresh child process running ya_vo_amd.sharding.FrameShard on its chunk with the 1-frame halo, all-gather their
+shared-map blocks (gloo here: both ranks share the test box's one GPU; the bench uses RCCL) and place them with the
+serial anchor chain.  The result must be the 1-rank run of the same frames: every relative pose bit for bit (the
+halo gives rank 1's first temporal pair the same keypoints the 1-rank run's carry slot does) and the placed map
+(keyframe poses, landmark ids and world points) within 1e-12 -- the chunked anchor chain A_1 * L_k re-associates the
+1-rank left fold rel_0 * ... * rel_k.  Reference: the serial chaining of
+src/LoopHandler.cc:139,156."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from ya_vo_amd import map as ymap
+from ya_vo_amd import scene
+from ya_vo_amd.sharding import FrameShard, shard_images
+from ya_vo_amd.synth import synth_stereo_batch
+
+pytestmark = pytest.mark.gpu
+
+TESTS = os.path.dirname(os.path.abspath(__file__))
+T_RIGHT = np.array([0, 0, 0, 1, 0, -0.54, 0], np.float64)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _one_rank(ctx, n, kf_every, seed):
+    import torch
+    fr = synth_stereo_batch(seed, n + 1, start=0)
+    d = torch.from_numpy(shard_images(fr[2:], fr[0])).to("cuda:0")
+    shard = FrameShard(ctx, n, 1, scene.K_KITTI, T_RIGHT, halo=True, kf_every=kf_every,
+                       max_kf=ymap.max_keyframes(n, 1, kf_every))
+    for _ in range(2):  # as the workers: the placement base advances by the sequence's span every step
+        shard.step(d.data_ptr())
+    shard.drain()
+    out = shard.poses(), shard.placed_map()
+    shard.close()
+    return out
+
+
+def _map(placed):
+    m = ymap.Map()
+    m.insert_blocks(placed, placed.shape[0], placed.shape[1])
+    return m
+
+
+@pytest.mark.parametrize("B,kf_every", [(4, 1), (6, 2)])
+def test_two_rank_shards_equal_one_rank(ctx, tmp_path, B, kf_every):
+    world, seed = 2, 91
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = [subprocess.Popen([sys.executable, os.path.join(TESTS, "shard_worker.py"), str(r), str(world), str(port),
+                               str(B), str(kf_every), str(seed), str(tmp_path / f"rank{r}.npz")], env=env)
+             for r in range(world)]
+    for p in procs:
+        assert p.wait(timeout=110) == 0
+    res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    ref_poses, ref_placed = _one_rank(ctx, world * B, kf_every, seed)
+
+    # relative poses: bit for bit, including rank 1's first frame (its predecessor comes from the halo)
+    np.testing.assert_array_equal(np.concatenate([r["poses"] for r in res]), ref_poses)
+    assert all(int(r["edge_count"][0]) > 1000 for r in res), "the halo pair must produce PnP edges"
+    # every rank holds the same placed map
+    np.testing.assert_array_equal(res[0]["placed"], res[1]["placed"])
+    got, ref = _map(res[0]["placed"]), _map(ref_placed)
+    assert sorted(got.frames) == sorted(ref.frames) == list(range(kf_every, world * B + 1, kf_every))
+    assert sorted(got.landmarks) == sorted(ref.landmarks)
+    for g in ref.frames:
+        np.testing.assert_allclose(got.frames[g], ref.frames[g], rtol=0, atol=1e-12)
+    gl = np.array([got.landmarks[i] for i in sorted(ref.landmarks)])
+    rl = np.array([ref.landmarks[i] for i in sorted(ref.landmarks)])
+    np.testing.assert_allclose(gl, rl, rtol=0, atol=1e-12)
+    # the rank boundary carries the sequence's real motion (the synthetic camera moves 0.21 m per frame), not the
+    # identity an empty or stale predecessor would give
+    assert np.linalg.norm(res[1]["poses"][0][4:]) > 0.1

@@ -7,6 +7,8 @@ removeOutliers, src/BriefDescriptor.cc:163-231), stereo triangulation with the l
 LoopHandler::optimizePoseOnly (src/LoopHandler.cc:730-861) of frame k-1's pose in frame k's camera from
 the frame-(k-1) measurements.
 """
+import time
+
 import numpy as np
 
 from ya_vo_amd import MATCH_DTYPE, lm_sum_mode
@@ -24,13 +26,24 @@ def kept_flags(orc, m, thr=20):
     return np.array([i in kept_ids for i in m["pt1"]["id"].tolist()], bool)
 
 
-def track_edges(orc, kq, kl, kr, K, T_right, thr=20):
-    """Edges of one track -> (X [n,3], uv [n,2], query index [n])."""
+def _tick(timers, key, t0):
+    """Accumulate seconds since t0 under `key` (timers None: no timing); returns the new start."""
+    t = time.perf_counter()
+    if timers is not None:
+        timers[key] = timers.get(key, 0.0) + t - t0
+    return t
+
+
+def track_edges(orc, kq, kl, kr, K, T_right, thr=20, timers=None):
+    """Edges of one track -> (X [n,3], uv [n,2], query index [n]).  timers: optional dict of per-stage seconds
+    ("match": matchFeatures + removeOutliers of both pairs, "triangulate": the stereo triangulation)."""
     if len(kq) == 0:
         return np.zeros((0, 3)), np.zeros((0, 2)), np.zeros(0, np.int32)
+    t0 = time.perf_counter()
     mt = orc.match(kq, kl)
     ms = orc.match(kl, kr) if len(kl) else np.zeros(0, MATCH_DTYPE)
     kt, ks = kept_flags(orc, mt, thr), kept_flags(orc, ms, thr)
+    t0 = _tick(timers, "match", t0)
     l_index = {int(i): j for j, i in enumerate(kl["id"].tolist())}
     cand, recs = [], []
     for i in range(len(kq)):
@@ -44,16 +57,21 @@ def track_edges(orc, kq, kl, kr, K, T_right, thr=20):
     if not cand:
         return np.zeros((0, 3)), np.zeros((0, 2)), np.zeros(0, np.int32)
     _, X, ok = orc.triangulate_matches(IDENTITY, T_right, K, np.array(recs, MATCH_DTYPE))
+    _tick(timers, "triangulate", t0)
     q = np.array(cand, np.int32)[ok]
     uv = np.stack([kq["x"][q], kq["y"][q]], 1).astype(np.float64)
     return X[ok], uv, q
 
 
-def track_pose(orc, kq, kl, kr, K, T_right, prior=IDENTITY, thr=20, sum_mode=None):
+def track_pose(orc, kq, kl, kr, K, T_right, prior=IDENTITY, thr=20, sum_mode=None, timers=None):
+    """track_edges + optimizePoseOnly in `sum_mode` (None: the GPU kernel's order; 0: the reference's sequential
+    order).  timers: as track_edges, plus "pose_lm"."""
     if sum_mode is None:
         sum_mode = lm_sum_mode()
-    X, uv, q = track_edges(orc, kq, kl, kr, K, T_right, thr)
+    X, uv, q = track_edges(orc, kq, kl, kr, K, T_right, thr, timers)
+    t0 = time.perf_counter()
     T, out, inl = orc.pose_lm(X, uv, K, prior, sum_mode)
+    _tick(timers, "pose_lm", t0)
     return X, uv, q, T, out, inl
 
 

@@ -62,3 +62,134 @@ def gather_frame_records(local, n_frames: int, world: int, rank: int):
     outs = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(outs, pad)
     return torch.cat([o[: len(s.frames)] for o, s in zip(outs, shards)], dim=0)
+
+
+def shard_images(stereo, halo_left=None):
+    """Device image layout of one rank's shard: [L_0, R_0, ..., L_{B-1}, R_{B-1}] then, when the shard has a
+    predecessor, the halo frame's left image (index 2B).  `stereo` [B, 2, H, W] or [2B, H, W] uint8."""
+    import numpy as np
+    s = np.asarray(stereo, np.uint8)
+    s = s.reshape(-1, s.shape[-2], s.shape[-1])
+    if halo_left is None:
+        return np.ascontiguousarray(s)
+    return np.ascontiguousarray(np.concatenate([s, np.asarray(halo_left, np.uint8)[None]]))
+
+
+class FrameShard:
+    """One rank's share of a frame-sharded stereo sequence on its GPU: frames
+    [first_frame, first_frame + n_frames) and, with `halo`, the predecessor frame first_frame - 1 whose left image is
+    detected and described in the same run (image index 2 * n_frames), so the shard's first temporal pair
+    L_{first-1} -> L_first needs no communication and gives the same matches a 1-rank run over the whole sequence
+    gets from its carry slot.  Without `halo` the first pair reads the batch's carry slot (empty on the first run:
+    the sequence's frame 0 has no predecessor, as in the reference's first takeVOStep).
+
+    Per step (one pass over the shard's resident images, `step`): yv_batch_run (detect / describe L and R, match
+    L_{k-1} -> L_k and L_k -> R_k, removeOutliers), then yv_batch_track_map (stereo triangulation + pose-only LM per
+    frame, the shard's shared-map block).  With a map, every rank's block is all-gathered (RCCL over xGMI on "nccl",
+    list all_gather on gloo) on a communication stream one step behind and placed in world coordinates by the serial
+    anchor chain A_{r+1} = A_r * C_r (yavo_map.hip), the reference's pose chaining (src/LoopHandler.cc:139,156)."""
+
+    def __init__(self, ctx, n_frames: int, first_frame: int, K, T_right, *, halo: bool = True, world: int = 1,
+                 rank: int = 0, backend: str = "nccl", kf_every: int = 0, max_kf: int = 0, overlap_mode: int = 1,
+                 tracker: str = "match", H: int = 376, W: int = 1241, max_kp: int = 2000, match_thr: int = 20):
+        import numpy as np
+        import torch
+        from . import Batch
+        from . import map as ymap
+        if n_frames < 1 or first_frame < 0 or (halo and first_frame < 1):
+            raise ValueError("bad shard: n_frames >= 1 and a halo needs first_frame >= 1")
+        if tracker not in ("match", "lk"):
+            raise ValueError("tracker must be 'match' or 'lk'")
+        self.ctx, self.B, self.first, self.halo = ctx, n_frames, first_frame, halo
+        self.world, self.rank, self.backend = world, rank, backend
+        self.H, self.W, self.max_kp, self.match_thr = H, W, max_kp, match_thr
+        B = n_frames
+        self.n_images = 2 * B + (1 if halo else 0)
+        self.batch = Batch(ctx, self.n_images, H, W, max_kp, 2 * B)
+        prev0 = 2 * B if halo else self.n_images  # the halo image, or the carry slot (index max_images)
+        pairs, tracks = [], []
+        for k in range(B):
+            pairs.append((prev0 if k == 0 else 2 * (k - 1), 2 * k))  # temporal L_{k-1} -> L_k
+            pairs.append((2 * k, 2 * k + 1))                          # stereo L_k -> R_k
+            if tracker == "match":
+                tracks.append((2 * k + 1, 2 * k))                     # PnP of frame k-1 against frame k's map
+            elif k > 0:
+                tracks.append((2 * (k - 1) + 1, 2 * k))               # LK: frame k-1's stereo map -> L_k
+        self.pairs, self.tracks = pairs, tracks
+        self.batch.set_pairs(pairs)
+        if tracker == "lk":
+            self.batch.set_track_lk(2)  # LK images = the left images 0, 2, 4, ...
+        self.batch.set_tracks(tracks, K, T_right)
+        self.n_tracks = len(tracks)
+        dev = torch.device("cuda", ctx.device)
+        identity = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
+        self.d_prior = torch.from_numpy(np.tile(identity, (self.n_tracks, 1))).to(dev)
+        # the pose LM of step i runs on the batch's side stream beside step i + 1's image kernels; its output buffer
+        # alternates so step i + 1 never writes poses step i's LM is still producing
+        self.batch.set_track_overlap(overlap_mode)
+        self.d_poses = [torch.zeros((self.n_tracks, 7), dtype=torch.float64, device=dev) for _ in range(2)]
+        self.calls = 0
+        self.use_map = kf_every > 0 and tracker == "match"
+        self.kf_every = kf_every
+        self._pending = False
+        if self.use_map:
+            self.max_kf = max(max_kf, ymap.max_keyframes(self.n_tracks, first_frame, kf_every), 1)
+            self.bb = ymap.block_bytes(self.max_kf, max_kp)
+            self.d_block = torch.zeros(self.bb, dtype=torch.uint8, device=dev)
+            self.d_gathered = torch.zeros((world, self.bb), dtype=torch.uint8, device=dev) if world > 1 \
+                else self.d_block
+            self.d_base = torch.from_numpy(identity.copy()).to(dev)
+            self.d_anchors = torch.zeros((world, 7), dtype=torch.float64, device=dev)
+            self.comm = torch.cuda.Stream(device=dev)
+
+    def _exchange(self) -> None:
+        import torch
+        import torch.distributed as dist
+        # the last track_map's block: all-gathered and placed on the communication stream once it is written
+        self.batch.map_wait(self.comm.cuda_stream)
+        with torch.cuda.stream(self.comm):
+            if self.world > 1 and self.backend == "nccl":
+                dist.all_gather_into_tensor(self.d_gathered, self.d_block)
+            elif self.world > 1:  # gloo: list form
+                dist.all_gather(list(self.d_gathered.unbind(0)), self.d_block)
+            self.ctx.map_place(self.d_gathered.data_ptr(), self.world, self.bb, self.d_base.data_ptr(),
+                               self.d_anchors.data_ptr(), stream=self.comm.cuda_stream)
+        self.batch.map_release(self.comm.cuda_stream)
+        self._pending = False
+
+    def step(self, d_images: int) -> None:
+        """One pass over the shard's resident images (device pointer, layout of shard_images)."""
+        # overlap modes 2 / 3 launch the previous step's pose LM (and its map block) inside this run, so the previous
+        # block is exchanged after it (one step behind: map_wait before the launch would force it early)
+        self.batch.run(d_images, self.n_images, self.W, self.H * self.W, self.match_thr, carry_from=-1)
+        if self._pending:
+            self._exchange()
+        d_out = self.d_poses[self.calls & 1]
+        if not self.use_map:
+            self.batch.track(self.d_prior.data_ptr(), d_out.data_ptr())
+        else:
+            self.batch.track_map(self.d_prior.data_ptr(), d_out.data_ptr(), self.first, self.kf_every,
+                                 self.d_block.data_ptr(), self.max_kf)
+            self._pending = True
+        self.calls += 1
+
+    def drain(self) -> None:
+        """Exchange the last block, then wait for every stream of the shard."""
+        import torch
+        if self._pending:
+            self._exchange()
+        self.ctx.sync()
+        self.batch.track_sync()
+        torch.cuda.synchronize(self.d_prior.device)
+
+    def poses(self):
+        """[n_tracks, 7] relative poses of the last step: track k = frame first + k - 1 in frame first + k's
+        camera (SE3d::data())."""
+        return self.d_poses[(self.calls - 1) & 1].cpu().numpy()
+
+    def placed_map(self):
+        """The last placed shared map: [world, block_bytes] uint8 (rank order; every rank holds the same)."""
+        return self.d_gathered.cpu().numpy().reshape(self.world, self.bb)
+
+    def close(self) -> None:
+        self.batch.close()
