@@ -78,6 +78,22 @@ def test_pose_lm_matches_oracle(ctx, oracle, n, noise, outl, seed):
     np.testing.assert_allclose(T, rT, rtol=0, atol=POSE_TOL)
 
 
+@pytest.mark.parametrize("noise,outl,perturb", [(0.0, 0.0, False), (0.2, 0.0, False), (0.2, 0.0, True),
+                                                (0.5, 0.05, False), (2.2, 0.0, True)])
+def test_pose_lm_round_replay_matches_oracle(ctx, oracle, noise, outl, perturb):
+    """The kernel skips a round that replays the last executed one (same active set and, across the Huber drop, no
+    Huber weight applied); the oracle runs all four rounds.  Cases: exact prior (no Huber, no outliers: rounds 1-3
+    replayed), perturbed prior (Huber active early: round 3 runs), noise near the chi2 threshold (levels flip between
+    rounds: no replay)."""
+    X, uv, T_true, _ = scene.random_scene(1200, seed=31, noise_px=noise, outlier_frac=outl)
+    prior = scene.perturb(T_true, np.random.default_rng(31)) if perturb else T_true
+    T, out, inl = ctx.pose_lm(X, uv, scene.K_KITTI, prior)
+    oT, oout, oinl = oracle.pose_lm(X, uv, scene.K_KITTI, prior, LM_ORDER)
+    assert inl == oinl
+    np.testing.assert_array_equal(out, oout)
+    np.testing.assert_array_equal(T, oT)
+
+
 @pytest.mark.parametrize("n,seed", [(100, 12), (2000, 14)])
 def test_pose_gn_matches_oracle(ctx, oracle, n, seed):
     X, uv, T_true, _ = scene.random_scene(n, seed=seed, noise_px=0.3)

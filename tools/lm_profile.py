@@ -62,6 +62,8 @@ def main():
     print(f"track_pose {ms[6]:.4f} ms, frames {B}; mean cycles per workgroup: total {tot.mean():.0f}")
     for i in range(9):
         print(f"  {PHASES[i]:32s} {p[:, i].mean():12.0f}  ({100 * p[:, i].mean() / tot.mean():5.1f}%)")
+    print(f"  passes per problem: mean {p[:, 9].mean():.1f}, max {p[:, 9].max():.0f}; "
+          f"cycles per pass {tot.mean() / max(p[:, 9].mean(), 1):.0f}")
     b.close()
     ctx.close()
 

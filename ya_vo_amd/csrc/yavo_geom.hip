@@ -963,6 +963,7 @@ struct LMShared {
     double Hf[36];                     // the same H, full symmetric (the LDLT's gather source)
     double lambda, ni, currentChi, tempChi, rho;
     int flag;  // control broadcast from lane 0
+    int hub;   // a Huber weight (c2 > delta^2 on a robust edge) was applied in some pass of the current round
 };
 
 constexpr int kLMVals = 28;  // 21 lower-triangle H entries + 6 b + 1 chi2
@@ -1038,6 +1039,7 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
         // into an unconditional sqrt + division)
         const bool hub = rob && c2 > 1.0;
         if (__any(hub)) {
+            if ((tid & 63) == 0) S.hub = 1;
             if (rob) chi = huber_rho(c2, &w);
         }
         part[27] = part[27] + chi;
@@ -1080,6 +1082,7 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
         lmp[0] += p1 - p0;
         lmp[1] += p2 - ps;  // the reduction proper
         lmp[8] += ps - p1;  // waiting at the first barrier for the other waves' edges
+        lmp[9] += 1;        // passes (error + system evaluations)
     }
 #else
     lm_reduce<kLMVals, NT>(part, s_red, S.vals);
@@ -1128,161 +1131,176 @@ __global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t*
     const double chi2th = 5.991;
     const double tau = 1e-5, goodLower = 1.0 / 3.0, goodUpper = 2.0 / 3.0;
     int outlierCount = 0;
+    // Round memoization (exact): every round restarts from the same prior with a fresh LM (src/LoopHandler.cc:817-
+    // 819: setEstimate(currentFrame->pose), initializeOptimization(), optimize(10)), so a round whose active edge set
+    // and robust kernels equal those of the last executed round replays it operation for operation: its estimate,
+    // its edges' errors and hence its classification are the last round's, and it is skipped.  The active set is
+    // unchanged iff the last classification moved no edge between levels.  Dropping the Huber kernel after round 2
+    // changes nothing either when no pass of the replayed round applied a Huber weight: below delta^2 the kernel's
+    // rho = e2 and rho' = 1.0, and every product with 1.0 is exact.
+    bool replay = false;
 
     for (int round = 0; round < 4; ++round) {
-        if (tid < 7) S.T[tid] = prior[tid];
-        // initializeOptimization(): active = level-0 edges in insertion order (block compaction)
-        int na = 0;
-        for (int base = 0; base < n; base += NT) {
-            const int i = base + tid;
-            const int f = (i < n && s_level[i] == 0) ? 1 : 0;
-            int tot = 0;
-            const int off = block_excl_scan_geom<NT>(f, s_tmp, &tot);
-            if (f) s_active[na + off] = (int16_t)i;
-            na += tot;
-        }
-        __syncthreads();
-        if (na > 0) {
-            double lambda = 0, ni = 2;
-            // S.vals holds {H, b, chi2} at S.T when `have` (the last trial was accepted: g2o's next
-            // computeActiveErrors + buildSystem happen at exactly that estimate, so the trial pass builds the
-            // system along with its chi2 and the rebuild is skipped)
-            bool have = false;
-            for (int it = 0; it < 10; ++it) {
-#ifdef YAVO_LM_PROFILE
-                LMP_MARK(5);
-                if (!have) lm_pass<NT>(S, s_active, na, s_robust, X, uv, s_red, lmp_acc);
-                lmp_t = __builtin_readcyclecounter();
-#else
-                if (!have) lm_pass<NT>(S, s_active, na, s_robust, X, uv, s_red);
-#endif
-                if (tid == 0) {
-                    double sys[28];
-#pragma unroll
-                    for (int v = 0; v < 28; ++v) sys[v] = S.vals[v];
-#pragma unroll
-                    for (int v = 0; v < 28; ++v) S.sys[v] = sys[v];
-#pragma unroll
-                    for (int r = 0; r < 6; ++r)
-#pragma unroll
-                        for (int c = 0; c <= r; ++c) {
-                            S.Hf[r * 6 + c] = sys[r * (r + 1) / 2 + c];
-                            S.Hf[c * 6 + r] = sys[r * (r + 1) / 2 + c];
-                        }
-                    S.currentChi = sys[27];
-                    if (it == 0) {
-                        double maxDiag = 0;
-#pragma unroll
-                        for (int j = 0; j < 6; ++j) {
-                            const double d = fabs(sys[j * (j + 1) / 2 + j]);
-                            maxDiag = d > maxDiag ? d : maxDiag;
-                        }
-                        lambda = tau * maxDiag;
-                        ni = 2;
-                    }
-                }
-                LMP_MARK(7);
-                // trial loop (do ... while (rho < 0 && qmax < 10))
-                int qmax = 0;
-                int f = 0;
-                while (true) {
-                    if (tid == 0) {
-                        double Tc[7], xs[6];
-#pragma unroll
-                        for (int q = 0; q < 7; ++q) Tc[q] = S.T[q];
-#pragma unroll
-                        for (int q = 0; q < 7; ++q) S.Tbak[q] = Tc[q];
-                        const int ok2 = ldlt6_solve_lds<0>(S.Hf, lambda, S.sys + 21, S.x) ? 1 : 0;
-#pragma unroll
-                        for (int q = 0; q < 6; ++q) xs[q] = S.x[q];
-                        LMP_MARK(6);
-                        double Tn[7], Tnew[7];
-                        se3_exp(xs, Tn);
-                        se3_mul(Tn, Tc, Tnew);
-#pragma unroll
-                        for (int q = 0; q < 7; ++q) S.T[q] = Tnew[q];
-                        S.flag = ok2;
-                    }
-                    LMP_MARK(2);
-#ifdef YAVO_LM_PROFILE
-                    lm_pass<NT>(S, s_active, na, s_robust, X, uv, s_red, lmp_acc);
+        int changed = 0;
+        if (!replay) {
+            if (tid == 0) S.hub = 0;  // the first pass starts with a barrier: no wave writes S.hub before this store
+            if (tid < 7) S.T[tid] = prior[tid];
+            // initializeOptimization(): active = level-0 edges in insertion order (block compaction)
+            int na = 0;
+            for (int base = 0; base < n; base += NT) {
+                const int i = base + tid;
+                const int f = (i < n && s_level[i] == 0) ? 1 : 0;
+                int tot = 0;
+                const int off = block_excl_scan_geom<NT>(f, s_tmp, &tot);
+                if (f) s_active[na + off] = (int16_t)i;
+                na += tot;
+            }
+            __syncthreads();
+            if (na > 0) {
+                double lambda = 0, ni = 2;
+                // S.vals holds {H, b, chi2} at S.T when `have` (the last trial was accepted: g2o's next
+                // computeActiveErrors + buildSystem happen at exactly that estimate, so the trial pass builds the
+                // system along with its chi2 and the rebuild is skipped)
+                bool have = false;
+                for (int it = 0; it < 10; ++it) {
+    #ifdef YAVO_LM_PROFILE
+                    LMP_MARK(5);
+                    if (!have) lm_pass<NT>(S, s_active, na, s_robust, X, uv, s_red, lmp_acc);
                     lmp_t = __builtin_readcyclecounter();
-#else
-                    lm_pass<NT>(S, s_active, na, s_robust, X, uv, s_red);  // errors + system at the trial estimate
-#endif
+    #else
+                    if (!have) lm_pass<NT>(S, s_active, na, s_robust, X, uv, s_red);
+    #endif
                     if (tid == 0) {
-                        const int ok2 = S.flag;
-                        double tempChi = S.vals[27];
-                        if (!ok2) tempChi = DBL_MAX;
-                        double rho = S.currentChi - tempChi;
-                        double scale = 1;
-                        if (ok2) {
-                            double sc = 0;
-                            for (int j = 0; j < 6; ++j) sc += S.x[j] * (lambda * S.x[j] + S.sys[21 + j]);
-                            scale = sc + 1e-3;
-                        }
-                        rho /= scale;
-                        int brk = 0, accepted = 0;
-                        if (rho > 0 && isfinite(tempChi) && ok2) {
-                            double t = 2 * rho - 1;
-                            double alpha = 1. - t * t * t;
-                            alpha = alpha < goodUpper ? alpha : goodUpper;
-                            double sf = goodLower > alpha ? goodLower : alpha;
-                            lambda *= sf;
+                        double sys[28];
+    #pragma unroll
+                        for (int v = 0; v < 28; ++v) sys[v] = S.vals[v];
+    #pragma unroll
+                        for (int v = 0; v < 28; ++v) S.sys[v] = sys[v];
+    #pragma unroll
+                        for (int r = 0; r < 6; ++r)
+    #pragma unroll
+                            for (int c = 0; c <= r; ++c) {
+                                S.Hf[r * 6 + c] = sys[r * (r + 1) / 2 + c];
+                                S.Hf[c * 6 + r] = sys[r * (r + 1) / 2 + c];
+                            }
+                        S.currentChi = sys[27];
+                        if (it == 0) {
+                            double maxDiag = 0;
+    #pragma unroll
+                            for (int j = 0; j < 6; ++j) {
+                                const double d = fabs(sys[j * (j + 1) / 2 + j]);
+                                maxDiag = d > maxDiag ? d : maxDiag;
+                            }
+                            lambda = tau * maxDiag;
                             ni = 2;
-                            S.currentChi = tempChi;
-                            accepted = 1;
-                        } else {
-                            lambda *= ni;
-                            ni *= 2;
-                            for (int q = 0; q < 7; ++q) S.T[q] = S.Tbak[q];
-                            if (!isfinite(lambda)) brk = 1;
                         }
-                        qmax++;
-                        const bool again = !brk && rho < 0 && qmax < 10;
-                        int fl = again ? 1 : 0;
-                        if (!again) fl = (qmax == 10 || rho == 0 || !isfinite(lambda)) ? 2 : 0;
-                        S.flag = fl | (accepted << 2);
                     }
-                    __syncthreads();
-                    f = S.flag;
-                    __syncthreads();
-                    LMP_MARK(3);
-                    if ((f & 3) == 1) continue;
-                    break;
+                    LMP_MARK(7);
+                    // trial loop (do ... while (rho < 0 && qmax < 10))
+                    int qmax = 0;
+                    int f = 0;
+                    while (true) {
+                        if (tid == 0) {
+                            double Tc[7], xs[6];
+    #pragma unroll
+                            for (int q = 0; q < 7; ++q) Tc[q] = S.T[q];
+    #pragma unroll
+                            for (int q = 0; q < 7; ++q) S.Tbak[q] = Tc[q];
+                            const int ok2 = ldlt6_solve_lds<0>(S.Hf, lambda, S.sys + 21, S.x) ? 1 : 0;
+    #pragma unroll
+                            for (int q = 0; q < 6; ++q) xs[q] = S.x[q];
+                            LMP_MARK(6);
+                            double Tn[7], Tnew[7];
+                            se3_exp(xs, Tn);
+                            se3_mul(Tn, Tc, Tnew);
+    #pragma unroll
+                            for (int q = 0; q < 7; ++q) S.T[q] = Tnew[q];
+                            S.flag = ok2;
+                        }
+                        LMP_MARK(2);
+    #ifdef YAVO_LM_PROFILE
+                        lm_pass<NT>(S, s_active, na, s_robust, X, uv, s_red, lmp_acc);
+                        lmp_t = __builtin_readcyclecounter();
+    #else
+                        lm_pass<NT>(S, s_active, na, s_robust, X, uv, s_red);  // errors + system at the trial estimate
+    #endif
+                        if (tid == 0) {
+                            const int ok2 = S.flag;
+                            double tempChi = S.vals[27];
+                            if (!ok2) tempChi = DBL_MAX;
+                            double rho = S.currentChi - tempChi;
+                            double scale = 1;
+                            if (ok2) {
+                                double sc = 0;
+                                for (int j = 0; j < 6; ++j) sc += S.x[j] * (lambda * S.x[j] + S.sys[21 + j]);
+                                scale = sc + 1e-3;
+                            }
+                            rho /= scale;
+                            int brk = 0, accepted = 0;
+                            if (rho > 0 && isfinite(tempChi) && ok2) {
+                                double t = 2 * rho - 1;
+                                double alpha = 1. - t * t * t;
+                                alpha = alpha < goodUpper ? alpha : goodUpper;
+                                double sf = goodLower > alpha ? goodLower : alpha;
+                                lambda *= sf;
+                                ni = 2;
+                                S.currentChi = tempChi;
+                                accepted = 1;
+                            } else {
+                                lambda *= ni;
+                                ni *= 2;
+                                for (int q = 0; q < 7; ++q) S.T[q] = S.Tbak[q];
+                                if (!isfinite(lambda)) brk = 1;
+                            }
+                            qmax++;
+                            const bool again = !brk && rho < 0 && qmax < 10;
+                            int fl = again ? 1 : 0;
+                            if (!again) fl = (qmax == 10 || rho == 0 || !isfinite(lambda)) ? 2 : 0;
+                            S.flag = fl | (accepted << 2);
+                        }
+                        __syncthreads();
+                        f = S.flag;
+                        __syncthreads();
+                        LMP_MARK(3);
+                        if ((f & 3) == 1) continue;
+                        break;
+                    }
+                    if ((f & 3) == 2) break;
+                    have = (f & 4) != 0;
                 }
-                if ((f & 3) == 2) break;
-                have = (f & 4) != 0;
             }
-        }
-        __syncthreads();
-        // classify: previous outliers are recomputed at the final estimate (e->computeError()); the
-        // active edges keep the error of the last computeActiveErrors, i.e. at the last TRIAL estimate
-        // Tlast (possibly a rejected one) -- recomputed here from Tlast, bit-identical to the stored value
-        double T[7], Tl[7], K[9];
-        for (int q = 0; q < 7; ++q) T[q] = S.T[q];
-        for (int q = 0; q < 7; ++q) Tl[q] = S.Tlast[q];
-        for (int q = 0; q < 9; ++q) K[q] = S.K[q];
-        int cnt = 0;
-        for (int i = tid; i < n; i += NT) {
-            double ee[2];
-            edge_error(s_out[i] ? T : Tl, K, X + 3 * i, uv + 2 * i, ee);
-            const double c2 = ee[0] * ee[0] + ee[1] * ee[1];
-            if (c2 > chi2th) {
-                s_out[i] = 1;
-                s_level[i] = 1;
-                cnt++;
-            } else {
-                s_out[i] = 0;
-                s_level[i] = 0;
+            __syncthreads();
+            // classify: previous outliers are recomputed at the final estimate (e->computeError()); the
+            // active edges keep the error of the last computeActiveErrors, i.e. at the last TRIAL estimate
+            // Tlast (possibly a rejected one) -- recomputed here from Tlast, bit-identical to the stored value
+            double T[7], Tl[7], K[9];
+            for (int q = 0; q < 7; ++q) T[q] = S.T[q];
+            for (int q = 0; q < 7; ++q) Tl[q] = S.Tlast[q];
+            for (int q = 0; q < 9; ++q) K[q] = S.K[q];
+            int cnt = 0, chg = 0;
+            for (int i = tid; i < n; i += NT) {
+                double ee[2];
+                edge_error(s_out[i] ? T : Tl, K, X + 3 * i, uv + 2 * i, ee);
+                const double c2 = ee[0] * ee[0] + ee[1] * ee[1];
+                const uint8_t lev = c2 > chi2th ? 1 : 0;
+                chg |= lev != s_level[i];
+                s_out[i] = lev;
+                s_level[i] = lev;
+                cnt += lev;
+                if (round == 2) s_robust[i] = 0;
             }
-            if (round == 2) s_robust[i] = 0;
+            int tot = 0;
+            block_excl_scan_geom<NT>(cnt, s_tmp, &tot);
+            outlierCount = tot;
+            changed = __syncthreads_or(chg);
+            LMP_MARK(4);
+        } else if (round == 2) {  // a replayed round 2 still drops the Huber kernels
+            for (int i = tid; i < n; i += NT) s_robust[i] = 0;
+            __syncthreads();
         }
-        int tot = 0;
-        block_excl_scan_geom<NT>(cnt, s_tmp, &tot);
-        outlierCount = tot;
-        __syncthreads();
-        LMP_MARK(4);
+        // round + 1 replays the last executed round iff no edge changed level and, across the Huber drop after round 2,
+        // no pass of that round applied a Huber weight (S.hub is that round's: replayed rounds run no pass)
+        replay = !changed && (round != 2 || S.hub == 0);
     }
     LMP_STORE();
     if (tid < 7) poses[7 * prob + tid] = S.T[tid];
