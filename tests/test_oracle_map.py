@@ -189,3 +189,19 @@ def test_gather_and_place_gloo_world2(oracle):
     for g, T in mref.get_frames().items():
         np.testing.assert_allclose(frames[g], T, atol=1e-12)
     np.testing.assert_allclose(end, ref_end, atol=1e-12)
+
+
+def test_parse_block_views_are_read_only(oracle):
+    """parse_block parses a uint8 buffer in place: its views alias the buffer, so writes through them are refused and
+    a later reuse of the buffer shows through (ya_vo_amd/map.py docstring)."""
+    rel, ec, eX, eo = _sequence(oracle, 3, 6)
+    blk = oracle.map_chunk(rel, 0, 1, ec, eX, eo, MAX_KP, 3)
+    h, kfs, lms = ymap.parse_block(blk)
+    with pytest.raises(ValueError):
+        lms[0]["X"][0] = 1.0
+    with pytest.raises(ValueError):
+        kfs["T"][0] = 0.0
+    before = kfs["frame_id"].copy()
+    blk[128:136] = 0xFF  # the caller reuses its buffer: the view follows it
+    assert kfs["frame_id"][0] != before[0]
+    assert blk.flags.writeable  # the caller's own array stays writable

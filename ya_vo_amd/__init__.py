@@ -1,8 +1,9 @@
-"""ya_vo_amd -- MI355X-native YA_VO visual-odometry front end (detect / describe / match hot path).
+"""ya_vo_amd -- MI355X-native YA_VO visual-odometry front end (detect / describe / match / PnP hot path).
 
-The product is libyavo.so (gfx950 HIP kernels behind the C ABI in include/yavo/yavo.h).  This module is
-a thin ctypes binding plus a Python mirror of the reference's operator classes (FastDetector, Brief; see
-ya_vo_amd/frontend.py).  There is no CPU fallback: if the library or a GPU is missing, the calls raise.
+The product is libyavo.so (gfx950 HIP kernels behind the C ABI in include/yavo/yavo.h).  This module is the ctypes
+binding of that ABI (Context, Batch, Lk, Essential, BundleAdjuster); the reference-shaped C++ host classes
+(FastDetector, Brief, LoopHandler) live in ya_vo_amd/frontend/.  There is no CPU fallback: if the library or a GPU is
+missing, the calls raise.
 """
 from __future__ import annotations
 

@@ -47,9 +47,14 @@ def max_keyframes(n_frames: int, first_frame: int, kf_every: int) -> int:
 
 
 def parse_block(buf) -> Tuple[np.ndarray, np.ndarray, List[np.ndarray]]:
-    """(header, written keyframes, per-keyframe written landmarks) of one block (bytes / uint8 array)."""
+    """(header, written keyframes, per-keyframe written landmarks) of one block (bytes / uint8 array).
+
+    A C-contiguous uint8 array is parsed in place: the results are READ-ONLY views that alias `buf` (no 1+ MB
+    copy), so they change when the caller reuses the buffer (ya_vo_amd.sequence reuses one pinned block); copy what
+    you keep.  Any other input is copied first."""
     if isinstance(buf, np.ndarray) and buf.dtype == np.uint8 and buf.flags["C_CONTIGUOUS"]:
-        raw = buf.reshape(-1)  # views into the caller's buffer (no 1+ MB copy); callers copy what they keep
+        raw = buf.reshape(-1).view()
+        raw.flags.writeable = False  # the views alias the caller's buffer: writes through them are refused
     else:
         raw = np.frombuffer(bytes(buf) if not isinstance(buf, np.ndarray) else buf.tobytes(), np.uint8)
     h = raw[:HEADER_DTYPE.itemsize].view(HEADER_DTYPE)[0]
