@@ -139,6 +139,49 @@ def test_pose_lm_batch(ctx, oracle):
         np.testing.assert_array_equal(out[offs[i]:offs[i + 1]], oout)
 
 
+def test_pose_lm_batch_many_repeatable(ctx, oracle):
+    """512 bench-sized problems (the batch's 512 frames per step), launched three times: every launch bit-identical
+    to the oracle.  Many concurrent 4-wave workgroups expose cross-wave races in the kernel's round control (the
+    Huber-flag read of the replay decision raced with the next round's reset before it was read ahead of the
+    barrier: 3 of 512 bench poses moved by up to 2.6e-4 between steps)."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    rng = np.random.default_rng(77)
+    probs, priors = [], []
+    for i in range(512):
+        n = int(rng.integers(1700, 2000))
+        noise = float(rng.choice([0.2, 0.5, 0.9, 1.3]))
+        p = scene.random_scene(n, seed=1000 + i, noise_px=noise, outlier_frac=float(rng.choice([0.0, 0.02, 0.1])))
+        probs.append(p)
+        priors.append(p[2] if i % 3 == 0 else scene.perturb(p[2], np.random.default_rng(i)))
+    offs = np.cumsum([0] + [len(p[0]) for p in probs]).astype(np.int32)
+    Xall = np.ascontiguousarray(np.concatenate([p[0] for p in probs]))
+    uvall = np.ascontiguousarray(np.concatenate([p[1] for p in probs]))
+    dev = "cuda:0"
+    d_off = torch.from_numpy(offs).to(dev)
+    d_X = torch.from_numpy(Xall).to(dev)
+    d_uv = torch.from_numpy(uvall).to(dev)
+    d_K = torch.from_numpy(np.tile(scene.K_KITTI.reshape(1, 9), (len(probs), 1))).to(dev)
+    with ThreadPoolExecutor(8) as ex:
+        ref = list(ex.map(lambda i: oracle.pose_lm(probs[i][0], probs[i][1], scene.K_KITTI, priors[i], LM_ORDER),
+                          range(len(probs))))
+    oP = np.stack([r[0] for r in ref])
+    oinl = np.array([r[2] for r in ref])
+    for _ in range(3):
+        d_P = torch.from_numpy(np.stack(priors)).to(dev)
+        d_out = torch.zeros(len(Xall), dtype=torch.uint8, device=dev)
+        d_inl = torch.zeros(len(probs), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        assert ctx.lib.yv_pose_lm_batch(ctx.handle, len(probs), d_off.data_ptr(), d_X.data_ptr(), d_uv.data_ptr(),
+                                        d_K.data_ptr(), d_P.data_ptr(), d_out.data_ptr(), d_inl.data_ptr(),
+                                        None) == 0
+        ctx.sync()
+        P = d_P.cpu().numpy()
+        bad = np.nonzero(np.any(P != oP, axis=1))[0]
+        assert len(bad) == 0, f"problems {bad[:10].tolist()} differ from the oracle"
+        np.testing.assert_array_equal(d_inl.cpu().numpy(), oinl)
+
+
 def test_pose_gn_batch(ctx, oracle):
     import torch
     probs = [scene.random_scene(n, seed=30 + i, noise_px=0.3) for i, n in enumerate((40, 700, 2000, 0))]

@@ -1139,6 +1139,7 @@ __global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t*
     // changes nothing either when no pass of the replayed round applied a Huber weight: below delta^2 the kernel's
     // rho = e2 and rho' = 1.0, and every product with 1.0 is exact.
     bool replay = false;
+    int hub = 0;
 
     for (int round = 0; round < 4; ++round) {
         int changed = 0;
@@ -1292,6 +1293,7 @@ __global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t*
             int tot = 0;
             block_excl_scan_geom<NT>(cnt, s_tmp, &tot);
             outlierCount = tot;
+            hub = S.hub;  // read before the barrier: the next executed round's lane 0 clears S.hub right after it
             changed = __syncthreads_or(chg);
             LMP_MARK(4);
         } else if (round == 2) {  // a replayed round 2 still drops the Huber kernels
@@ -1299,8 +1301,10 @@ __global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t*
             __syncthreads();
         }
         // round + 1 replays the last executed round iff no edge changed level and, across the Huber drop after round 2,
-        // no pass of that round applied a Huber weight (S.hub is that round's: replayed rounds run no pass)
-        replay = !changed && (round != 2 || S.hub == 0);
+        // no pass of that round applied a Huber weight (`hub` is that round's: replayed rounds run no pass).  Every
+        // wave takes the same decision: `changed` comes from the barrier vote and `hub` from a read every wave made
+        // before that barrier.
+        replay = !changed && (round != 2 || hub == 0);
     }
     LMP_STORE();
     if (tid < 7) poses[7 * prob + tid] = S.T[tid];
