@@ -154,7 +154,7 @@ typedef struct yv_batch_view {
     const float* det_resp;            /* [max_images+1][max_kp] */
     const int32_t* kp_count;          /* [max_images+1]: keypoints that passed checkBoundry */
     const yv_keypoint* keypoints;     /* [max_images+1][max_kp] */
-    const uint8_t* blurred;           /* [max_images][H*W] */
+    const uint8_t* blurred;           /* [max_images][H][blur_pitch] (row pitch: the last field) */
     const int32_t* match_count;       /* [max_pairs]: = kp_count of the query image */
     const yv_match* matches;          /* [max_pairs][max_kp] */
     const int32_t* filt_count;        /* [max_pairs] */
@@ -171,6 +171,7 @@ typedef struct yv_batch_view {
     const int32_t* edge_query;        /* [n_tracks][max_kp]: temporal query keypoint index */
     const uint8_t* edge_outlier;      /* [n_tracks][max_kp] */
     const int32_t* track_inliers;     /* [n_tracks] */
+    int blur_pitch;                   /* row pitch of `blurred` in bytes (128-B aligned, >= W + 1) */
 } yv_batch_view;
 int yv_batch_view_get(yv_batch* b, yv_batch_view* view);
 

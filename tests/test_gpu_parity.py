@@ -186,7 +186,9 @@ def test_batch_pipeline_matches_oracle(ctx, oracle, offsets):
             kps = ctx.download(v.keypoints + i * 2000 * 48, yv.KEYPOINT_DTYPE, kpc[i])
             ok = oracle.brief(img, orc, offsets)
             np.testing.assert_array_equal(kps, ok)
-            blur = ctx.download(v.blurred + i * H * W, np.uint8, H * W).reshape(H, W)
+            bp = v.blur_pitch  # 128-B aligned row pitch >= W + 1 (the padding columns are not part of the image)
+            assert bp % 128 == 0 and bp > W
+            blur = ctx.download(v.blurred + i * H * bp, np.uint8, H * bp).reshape(H, bp)[:, :W]
             np.testing.assert_array_equal(blur, oracle.blur(img))
             ref_kp[(run, i)] = ok
         mc = ctx.download(v.match_count, np.int32, len(pairs))

@@ -52,7 +52,7 @@ class _BatchView(ctypes.Structure):
                 ("match_dj", ctypes.c_void_p), ("match_lim", ctypes.c_void_p), ("n_tracks", ctypes.c_int),
                 ("edge_count", ctypes.c_void_p), ("edge_X", ctypes.c_void_p), ("edge_uv", ctypes.c_void_p),
                 ("edge_query", ctypes.c_void_p), ("edge_outlier", ctypes.c_void_p),
-                ("track_inliers", ctypes.c_void_p)]
+                ("track_inliers", ctypes.c_void_p), ("blur_pitch", ctypes.c_int)]
 
 
 _lib: Optional[ctypes.CDLL] = None

@@ -369,7 +369,7 @@ int yv_batch_create(yv_ctx* ctx, int max_images, int H, int W, int max_kp, int m
     rc |= dalloc(&b->kp_count, ns);
     rc |= dalloc(&b->keypoints, ns * nk);
     rc |= dalloc(&b->desc, ns * nk);
-    rc |= dalloc(&b->blur, (size_t)max_images * (size_t)H * W);
+    rc |= dalloc(&b->blur, (size_t)max_images * (size_t)yavo::blur_image_bytes(H, W));
     rc |= dalloc(&b->pairs, np * 2);
     rc |= dalloc(&b->match_key, np * nk);
     rc |= dalloc(&b->matches, np * nk);
@@ -545,6 +545,7 @@ int yv_batch_view_get(yv_batch* b, yv_batch_view* v) {
     v->kp_count = b->kp_count;
     v->keypoints = b->keypoints;
     v->blurred = b->blur;
+    v->blur_pitch = yavo::blur_pitch(b->W);
     v->match_count = b->match_count;
     v->matches = b->matches;
     v->filt_count = b->filt_count;

@@ -14,6 +14,22 @@ constexpr int kMaxKp = 4096;
 constexpr int kMaxWidth = 2048;  // image width limit (BRIEF keeps 49 rows of the blurred image in LDS)       // per-image keypoint capacity supported by the top-K / scan kernels
 constexpr int kFastTileW = 64;     // FAST / blur output tile: one wave per tile row
 constexpr int kFastTileH = 56;
+// The blurred image (detect's second output, BRIEF's input) is stored with a 128-B aligned row pitch, so the
+// detect tiles write whole 64-B row segments with dword stores (a row stride of W = 1241 put every segment across
+// two cache lines, stored byte by byte).  Columns [W, pitch) are padding no reader uses; pitch >= W + 1
+// (brief_lds_stride(W) <= pitch: BRIEF stages whole 16-B words of a row).
+__host__ __device__ constexpr int blur_pitch(int W) { return (W + 1 + 127) & ~127; }
+// BRIEF's LDS band row stride: >= W + 1 (column W holds the next row's first pixel, see brief_kernel), 16-B rows
+__host__ __device__ constexpr int brief_lds_stride(int W) { return (W + 1 + 15) & ~15; }
+// Blurred images are laid out [image][H][blur_pitch(W)].
+__host__ __device__ constexpr int64_t blur_image_bytes(int H, int W) { return (int64_t)H * blur_pitch(W); }
+// XCD-aware block order (MI355X: 8 XCDs, each with its own L2; blocks are observed to round-robin over them by
+// linear id): the bijective remap turns linear block b into a logical index so that every XCD runs one contiguous
+// range of logical blocks -- neighbouring tiles (and their shared halo rows) stay in one L2.  Pure speed.
+__device__ __forceinline__ int xcd_swizzle(int b, int nblocks) {
+    const int q = nblocks >> 3, r = nblocks & 7, xcd = b & 7, slot = b >> 3;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+}
 
 struct Desc {                      // 256-bit BRIEF descriptor, test j -> bit j (LSB-first bytes)
     uint32_t w[8];
@@ -27,7 +43,7 @@ void launch_fast_harris(const uint8_t* imgs, int n_images, int H, int W, int str
 void launch_detect_blur(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch, int thr,
                         uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, const uint16_t* k9_host,
                         uint8_t* blur, hipStream_t s);
-// 9-tap separable fixed-point Gaussian, BORDER_REFLECT_101; output H x W contiguous per image.
+// 9-tap separable fixed-point Gaussian, BORDER_REFLECT_101; output [image][H][blur_pitch(W)].
 void launch_blur9(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,
                   const uint16_t* k9_host, uint8_t* blur, hipStream_t s);
 // Per-image top-K (response desc, index asc) + checkBoundry compaction.

@@ -157,7 +157,7 @@ __device__ unsigned long long g_det_prof[kDetProfSlots][6];
 #define DP_DECL unsigned long long dp_acc[6] = {0, 0, 0, 0, 0, 0}; unsigned long long dp_t = __builtin_readcyclecounter();
 #define DP_MARK(k) do { const unsigned long long t_ = __builtin_readcyclecounter(); dp_acc[k] += t_ - dp_t; dp_t = t_; } while (0)
 #define DP_STORE() do { \
-        const unsigned slot_ = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; \
+        const unsigned slot_ = blockIdx.x; \
         if (threadIdx.x == 0 && slot_ < kDetProfSlots) for (int q_ = 0; q_ < 6; ++q_) g_det_prof[slot_][q_] = dp_acc[q_]; \
     } while (0)
 #else
@@ -185,8 +185,11 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
     __shared__ uint16_t s_pos[FT_W * FT_H];
     __shared__ uint32_t s_n, s_npre, s_base;
     DP_DECL
-    const int img = blockIdx.z;
-    const int r0 = blockIdx.y * FT_H, c0 = blockIdx.x * FT_W;
+    // 1-D grid, XCD-aware: an image's tiles (and the halo rows neighbouring tiles share) stay in one XCD's L2
+    const int ntx = (W + FT_W - 1) / FT_W, nty = (H + FT_H - 1) / FT_H;
+    const int lb = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
+    const int img = lb / (ntx * nty), tyx = lb - img * (ntx * nty);
+    const int r0 = (tyx / ntx) * FT_H, c0 = (tyx % ntx) * FT_W;
     const uint8_t* src = imgs + (int64_t)img * pitch;
     const int tid = threadIdx.x;
     const int lane = lane_id();
@@ -264,15 +267,21 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
     uint32_t row_ok = 0;
 #pragma unroll
     for (int u = 0; u < kRowIters; ++u) row_ok |= (uint32_t)((unsigned)(r0 + ty + 4 * u - 4) < (unsigned)(H - 8)) << u;
-    // "similar" is the sign bit of sad(c, p) - thr: pre <=> !(s0 | s7) && !(s4 & s12) <=> sign bit clear in
-    // (d0 | d7) | (d4 & d12); the sign bits are shifted into nmask (bit u = not pre) with v_alignbit
+    // The reference's corner test is pre && run12 with pre = diff0 && diff7 && (diff4 || diff12)
+    // (src/FastDetector.cc:304-317) and run12 = 12 consecutive "different" ring pixels without wrap
+    // (checkContiguousPixels).  Any such run covers ring indices 4..11, so run12 implies diff7 and diff4, and
+    // pre && run12 == diff0 && run12.  Phase 1 therefore filters on diff0 && diff4 && diff8 && diff11 (left, bottom,
+    // right and top of the ring: a necessary condition, ~7% survivors against the pretest's ~18%) and phase 2
+    // evaluates run12 exactly; the corner set is the reference's.
+    // "similar" is the sign bit of sad(c, p) - thr, so the filter holds iff the sign bit of d0 | d4 | d8 | d11 is
+    // clear; the sign bits are shifted into nmask (bit u = filtered out) with v_alignbit
     uint32_t nmask = 0;
 #pragma unroll
     for (int u = kRowIters - 1; u >= 0; --u) {
         const uint8_t* t0 = &tile[(ty + 4 * u + FT_R) * FT_LW + tx + FT_R];
         const uint32_t cent = t0[0];
         auto d = [&](int k) { return __builtin_amdgcn_sad_u8(cent, (uint32_t)t0[ring_dr[k] * FT_LW + ring_dc[k]], neg_thr); };
-        const uint32_t v = (d(0) | d(7)) | (d(4) & d(12));
+        const uint32_t v = (d(0) | d(4)) | (d(8) | d(11));
         nmask = __builtin_amdgcn_alignbit(nmask, v, 31);  // (nmask << 1) | (v >> 31)
     }
     const uint32_t pmask = (unsigned)(c - 4) < (unsigned)(W - 8) ? (~nmask & row_ok) : 0u;
@@ -390,27 +399,35 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
     }
     DP_MARK(4);
     if (kBlur) {
-        // vertical pass, exact u32: rows 2m and 2m+1 of column x from the row-pair dwords P_m .. P_{m+4}
+        // vertical pass, exact u32: rows 2m and 2m+1 of columns xq..xq+3 from the row-pair dwords P_m .. P_{m+4}
+        // (one 16-B LDS read per row pair); each row's 4 bytes go out as one dword store, so 16 lanes write a
+        // tile row's 64-B segment of the 128-B aligned pitched image (columns past W land in the row padding)
         typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-        uint8_t* dst = blur + (int64_t)img * H * W;
-        for (int i = tid; i < (FT_H / 2) * FT_W; i += 256) {
-            const int m = i >> 6, x = i & 63;
-            uint32_t P[5];
+        const int bp = blur_pitch(W);
+        uint8_t* dst = blur + (int64_t)img * H * bp;
+        for (int i = tid; i < (FT_H / 2) * (FT_W / 4); i += 256) {
+            const int m = i >> 4, xq = (i & 15) * 4;
+            uint4 P[5];
 #pragma unroll
-            for (int t = 0; t < 5; ++t) P[t] = hbuf[(m + t) * FT_W + x];
-            uint32_t ev = 0, od = kw.k[0] * (P[0] >> 16);
+            for (int t = 0; t < 5; ++t) P[t] = *reinterpret_cast<const uint4*>(&hbuf[(m + t) * FT_W + xq]);
+            uint32_t w0 = 0, w1 = 0;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                ev = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, P[t]), __builtin_bit_cast(us2, kw.k2e[t]), ev, false);
-                od = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, P[t + 1]), __builtin_bit_cast(us2, kw.k2o[t]), od, false);
+            for (int j = 0; j < 4; ++j) {
+                auto col = [&](const uint4& q) { return j == 0 ? q.x : j == 1 ? q.y : j == 2 ? q.z : q.w; };
+                uint32_t ev = 0, od = kw.k[0] * (col(P[0]) >> 16);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    ev = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, col(P[t])), __builtin_bit_cast(us2, kw.k2e[t]), ev, false);
+                    od = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, col(P[t + 1])), __builtin_bit_cast(us2, kw.k2o[t]), od, false);
+                }
+                ev += kw.k[8] * (col(P[4]) & 0xFFFFu);
+                const uint32_t v0 = min((ev + (1u << 15)) >> 16, 255u), v1 = min((od + (1u << 15)) >> 16, 255u);
+                w0 |= v0 << (8 * j);
+                w1 |= v1 << (8 * j);
             }
-            ev += kw.k[8] * (P[4] & 0xFFFFu);
-            const int r = r0 + 2 * m, c = c0 + x;
-            if (c < W) {
-                const uint32_t v0 = (ev + (1u << 15)) >> 16, v1 = (od + (1u << 15)) >> 16;
-                if (r < H) dst[(int64_t)r * W + c] = (uint8_t)(v0 > 255u ? 255u : v0);
-                if (r + 1 < H) dst[(int64_t)(r + 1) * W + c] = (uint8_t)(v1 > 255u ? 255u : v1);
-            }
+            const int r = r0 + 2 * m, c = c0 + xq;
+            if (r < H) *reinterpret_cast<uint32_t*>(&dst[(int64_t)r * bp + c]) = w0;
+            if (r + 1 < H) *reinterpret_cast<uint32_t*>(&dst[(int64_t)(r + 1) * bp + c]) = w1;
         }
     }
     DP_MARK(5);
@@ -419,7 +436,7 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
 
 void launch_fast_harris(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,
                         int thr, uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, hipStream_t s) {
-    dim3 grid((W + FT_W - 1) / FT_W, (H + FT_H - 1) / FT_H, n_images);
+    dim3 grid(((W + FT_W - 1) / FT_W) * ((H + FT_H - 1) / FT_H) * n_images);
     K9 kw = {};
     hipLaunchKernelGGL(detect_kernel<false>, grid, dim3(256), 0, s, imgs, H, W, stride, pitch, thr, cand_keys,
                        cap, cand_count, kw, (uint8_t*)nullptr);
@@ -428,7 +445,7 @@ void launch_fast_harris(const uint8_t* imgs, int n_images, int H, int W, int str
 void launch_detect_blur(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch, int thr,
                         uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, const uint16_t* k9_host,
                         uint8_t* blur, hipStream_t s) {
-    dim3 grid((W + FT_W - 1) / FT_W, (H + FT_H - 1) / FT_H, n_images);
+    dim3 grid(((W + FT_W - 1) / FT_W) * ((H + FT_H - 1) / FT_H) * n_images);
     const K9 kw = make_k9(k9_host);
     hipLaunchKernelGGL(detect_kernel<true>, grid, dim3(256), 0, s, imgs, H, W, stride, pitch, thr, cand_keys, cap,
                        cand_count, kw, blur);
@@ -474,7 +491,7 @@ __global__ __launch_bounds__(256) void blur9_kernel(const uint8_t* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 9; ++i) acc += kw.k[i] * th[(rr + i) * BL_W + tx];
         uint32_t v = (acc + (1u << 15)) >> 16;
-        if (r < H && c < W) blur[(int64_t)img * H * W + (int64_t)r * W + c] = (uint8_t)(v > 255u ? 255u : v);
+        if (r < H && c < W) blur[(int64_t)img * blur_image_bytes(H, W) + (int64_t)r * blur_pitch(W) + c] = (uint8_t)(v > 255u ? 255u : v);
     }
 }
 
@@ -683,10 +700,15 @@ __device__ __forceinline__ uint32_t reg_select(const uint32_t (&v)[N], int idx) 
 }
 
 // One workgroup per (32-row band, image): the band's keypoints (rows [r0, r0 + 32)) read their 17 x 17
-// patches from an LDS copy of the blurred rows [r0 - 8, r0 + 41) -- stored with row stride W, so the
-// reference's linear index (row + dr) * W + (col + dc) (which wraps into the neighbouring row at the
-// image's left/right edge, src/BriefDescriptor.cc getPixelVal) addresses it unchanged.  One wave per
-// keypoint: lane l evaluates tests l, l + 64, l + 128, l + 192 -> 4 ballots = 256 bits.
+// patches from an LDS copy of the blurred rows [r0 - 8, r0 + 41) with row stride LS = brief_lds_stride(W) >= W + 1.
+// The reference samples getPixelVal at the linear index (row + dr) * W + (col + dc) (src/BriefDescriptor.cc:
+// 100-118, src/Image.cc:15-17).  checkBoundry keeps 8 <= row <= H - 8 and 8 <= col <= W - 8, and |dr|, |dc| <= 8
+// (yv_set_brief_offsets), so a sample is pixel (row + dr, col + dc) except (a) col + dc == W, which wraps to the
+// first pixel of the next row, and (b) any index past the image end (row + dr == H, or row + dr == H - 1 at
+// col + dc == W), which the reference reads out of bounds (UB; both paths read 0).  The band therefore holds in
+// LDS column W of each row the next row's first pixel, and zero rows past the image: every sample is then
+// s_band[(row + dr - (r0 - 8)) * LS + col + dc] with no test.  One wave per keypoint: lane l evaluates tests l,
+// l + 64, l + 128, l + 192 -> 4 ballots = 256 bits.
 constexpr int BR_BAND = 32;
 constexpr int BR_ROWS = BR_BAND + 17;  // rows r0-8 .. r0+40 (the last one for the wrap of col + 8 == W)
 // 16 waves share one staged band: the ~61 KB band limits a CU to 2 workgroups, so the workgroup is as wide as
@@ -699,11 +721,14 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
                                                     const int32_t* __restrict__ kp_src,
                                                     const int32_t* __restrict__ kp_count, int max_kp,
                                                     yv_keypoint* __restrict__ keypoints, Desc* __restrict__ desc) {
-    extern __shared__ uint8_t s_band[];  // BR_ROWS * W + 32 bytes
+    extern __shared__ uint8_t s_band[];  // BR_ROWS * brief_lds_stride(W) bytes
     __shared__ int16_t s_list[kMaxKp];
     __shared__ int s_n;
-    const int img = blockIdx.y;
-    const int r0 = blockIdx.x * BR_BAND;
+    // 1-D grid, XCD-aware: neighbouring bands of an image (17 shared rows) stay in one XCD's L2
+    const int nbands = (H + BR_BAND - 1) / BR_BAND;
+    const int lb = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
+    const int img = lb / nbands;
+    const int r0 = (lb - img * nbands) * BR_BAND;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int n = kp_count[img];
     const int4* src = reinterpret_cast<const int4*>(kp_src) + (int64_t)img * max_kp;
@@ -728,46 +753,53 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
     __syncthreads();
     const int nb = s_n;
     if (nb == 0) return;
-    // 2. stage the band: linear bytes [L0, L1) of the image, from a 16-B aligned global address; each
-    // thread's loads are all in flight before the LDS writes (H * W < 2^31: 32-bit indices)
-    const uint8_t* b = blur + (int64_t)img * H * W;
-    const int npix = H * W;
-    const int L0 = max(0, r0 - 8) * W;
-    const int L1 = min(npix, (r0 + BR_BAND + 9) * W);
-    const uintptr_t g0 = reinterpret_cast<uintptr_t>(b + L0);
-    const int sh = (int)(g0 & 15);
-    const uint4* gal = reinterpret_cast<const uint4*>(g0 - sh);
-    const int nbytes = (L1 - L0) + sh;  // bytes from gal to the end of the range
-    const int nfull = nbytes >> 4;
+    // 2. stage the band: rows rb .. rb + BR_ROWS - 1 (rb = r0 - 8) of the pitched blurred image as 16-B words,
+    // LS bytes per row (LS <= the pitch: inside the row); column W of row r is patched with pixel (r + 1, 0) (0 past
+    // the image), rows outside [0, H) are zero.  Each thread's loads are all in flight before the LDS writes.
+    const int bp = blur_pitch(W), LS = brief_lds_stride(W);
+    const uint8_t* b = blur + (int64_t)img * H * bp;
+    const int rb = r0 - 8;
+    const int wpr = LS >> 4;              // 16-B words per LDS row
+    const int nw = BR_ROWS * wpr;
+    const int kw_fix = W >> 4, sh_fix = 8 * (W & 3), dw_fix = (W >> 2) & 3;
     uint4* s4 = reinterpret_cast<uint4*>(s_band);
-    // 4 16-B words in flight per thread (written out: an array here is not kept in registers); indices are
-    // clamped so every load is a valid word inside [gal, b + L1)
-    for (int k0 = tid; k0 < nfull; k0 += 4 * BR_NT) {
-        const int last = nfull - 1;
-        const uint4 v0 = gal[min(k0, last)], v1 = gal[min(k0 + BR_NT, last)], v2 = gal[min(k0 + 2 * BR_NT, last)],
-                    v3 = gal[min(k0 + 3 * BR_NT, last)];
-        s4[k0] = v0;
-        if (k0 + BR_NT < nfull) s4[k0 + BR_NT] = v1;
-        if (k0 + 2 * BR_NT < nfull) s4[k0 + 2 * BR_NT] = v2;
-        if (k0 + 3 * BR_NT < nfull) s4[k0 + 3 * BR_NT] = v3;
+    for (int k0 = tid; k0 < nw; k0 += 4 * BR_NT) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + u * BR_NT;
+            const int j = k / wpr, q = k - j * wpr;
+            const int r = rb + j;
+            v[u] = make_uint4(0, 0, 0, 0);
+            if (k < nw && r >= 0 && r < H) {
+                v[u] = reinterpret_cast<const uint4*>(b + (int64_t)r * bp)[q];
+                if (q == kw_fix) {  // the word holding column W: the next row's first pixel (0 past the image)
+                    const uint32_t nx = r + 1 < H ? (uint32_t)b[(int64_t)(r + 1) * bp] : 0u;
+                    const uint32_t m = ~(0xFFu << sh_fix);
+                    if (dw_fix == 0) v[u].x = (v[u].x & m) | (nx << sh_fix);
+                    else if (dw_fix == 1) v[u].y = (v[u].y & m) | (nx << sh_fix);
+                    else if (dw_fix == 2) v[u].z = (v[u].z & m) | (nx << sh_fix);
+                    else v[u].w = (v[u].w & m) | (nx << sh_fix);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (k0 + u * BR_NT < nw) s4[k0 + u * BR_NT] = v[u];
     }
-    for (int k = nfull * 16 + tid; k < nbytes; k += BR_NT)  // tail bytes
-        s_band[k] = reinterpret_cast<const uint8_t*>(gal)[k];
     __syncthreads();
-    // 3. descriptors.  Each lane's 8 sample offsets as linear offsets dr * W + dc (the reference's index is
-    // (row + dr) * W + (col + dc) = row * W + col + (dr * W + dc)).
+    // 3. descriptors.  Each lane's 8 sample offsets as LDS offsets dr * LS + dc.
     int ol[4][2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const uint32_t packed = reinterpret_cast<const uint32_t*>(offsets)[lane + 64 * t];
         const int o0 = (int)(int8_t)(packed & 0xFFu), o1 = (int)(int8_t)((packed >> 8) & 0xFFu);
         const int o2 = (int)(int8_t)((packed >> 16) & 0xFFu), o3 = (int)(int8_t)((packed >> 24) & 0xFFu);
-        ol[t][0] = o0 * W + o1;
-        ol[t][1] = o2 * W + o3;
+        ol[t][0] = o0 * LS + o1;
+        ol[t][1] = o2 * LS + o3;
     }
     uint32_t* rec_base = reinterpret_cast<uint32_t*>(keypoints + (int64_t)img * max_kp);
     Desc* d_base = desc + (int64_t)img * max_kp;
-    const int lds_off = sh - L0;  // LDS index of linear pixel L = L + lds_off
     auto emit = [&](int i, const int4 kp, const uint64_t (&w)[4]) {
         // descriptor (32 B) and the 48-B KeyPoint record {x, y, id, matched=0, featVec[32], pad 0}
         uint32_t bd[9];
@@ -794,16 +826,12 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
         const bool two = k + BR_NW < nb;
         const int ia = s_list[k], ib = two ? s_list[k + BR_NW] : ia;
         const int4 kpa = src[ia], kpb = src[ib];
-        const int la = kpa.x * W + kpa.y, lb = kpb.x * W + kpb.y;
+        const int la = (kpa.x - rb) * LS + kpa.y, lbb = (kpb.x - rb) * LS + kpb.y;
         uint64_t wa[4], wb[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            // getPixelVal's linear index; past the image end the reference reads out of bounds -> 0
-            const int a1 = la + ol[t][0], a2 = la + ol[t][1], b1 = lb + ol[t][0], b2 = lb + ol[t][1];
-            const int pa1 = a1 < npix ? (int)s_band[a1 + lds_off] : 0;
-            const int pa2 = a2 < npix ? (int)s_band[a2 + lds_off] : 0;
-            const int pb1 = b1 < npix ? (int)s_band[b1 + lds_off] : 0;
-            const int pb2 = b2 < npix ? (int)s_band[b2 + lds_off] : 0;
+            const int pa1 = s_band[la + ol[t][0]], pa2 = s_band[la + ol[t][1]];
+            const int pb1 = s_band[lbb + ol[t][0]], pb2 = s_band[lbb + ol[t][1]];
             wa[t] = __ballot(pa1 > pa2);
             wb[t] = __ballot(pb1 > pb2);
         }
@@ -814,8 +842,8 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
 
 void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t* offsets, const int32_t* kp_src,
                   const int32_t* kp_count, int max_kp, yv_keypoint* keypoints, Desc* desc, hipStream_t s) {
-    dim3 grid((H + BR_BAND - 1) / BR_BAND, n_images);
-    const size_t lds = (size_t)BR_ROWS * W + 32;
+    dim3 grid(((H + BR_BAND - 1) / BR_BAND) * n_images);
+    const size_t lds = (size_t)BR_ROWS * brief_lds_stride(W);
     hipLaunchKernelGGL(brief_kernel, grid, dim3(BR_NT), lds, s, blur, H, W, offsets, kp_src, kp_count, max_kp,
                        keypoints, desc);
 }
