@@ -19,4 +19,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
     echo "[$(date +%T)] pmc pass $C exit=$st"
     [ $st -eq 0 ] || exit $st
 done
-python3 "$ROOT/tools/pmc_traffic.py" "$OUT" "$@"
+python3 "$ROOT/tools/pmc_traffic.py" "$OUT" "$@" && cp "$ROOT/profiles/pmc_traffic.json" "$OUT/pmc_traffic.json"
