@@ -99,6 +99,8 @@ int or_triangulate_matches(const double* Ta, const double* Tb, const double* K, 
 void or_se3_exp(const double* a, double* out);
 void or_se3_mul(const double* A, const double* B, double* out);
 void or_se3_act(const double* T, const double* p, double* out);
+void or_se3_inverse(const double* T, double* out);
+void or_se3_from_Rt(const double* R, const double* t, double* out);
 void or_quat_to_R(const double* q, double* R);
 double or_ksin(double x);
 double or_kcos(double x);

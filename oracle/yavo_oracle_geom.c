@@ -513,6 +513,51 @@ void or_se3_mul(const double* A, const double* B, double* out) {
     out[4] = t0; out[5] = t1; out[6] = t2;
 }
 
+/* Sophus SE3::inverse (LoopHandler: lastFrame->pose.inverse(), SE3(R, t).inverse(), src/LoopHandler.cc:160,285,
+ * 644-648): invR = SO3(q.conjugate()) -- the SO3 quaternion constructor normalises: q / |q| with Eigen's SSE2
+ * packet redux of the Vector4d squared norm, (x^2 + z^2) + (y^2 + w^2) -- and t' = invR * (t * -1). */
+void or_se3_inverse(const double* T, double* out) {
+    double q[4] = {-T[0], -T[1], -T[2], T[3]};
+    const double len = sqrt((q[0] * q[0] + q[2] * q[2]) + (q[1] * q[1] + q[3] * q[3]));
+    for (int i = 0; i < 4; ++i) q[i] = q[i] / len;
+    const double mt[3] = {T[4] * -1.0, T[5] * -1.0, T[6] * -1.0};
+    double r[3];
+    quat_rotate(q, mt, r);
+    out[0] = q[0]; out[1] = q[1]; out[2] = q[2]; out[3] = q[3];
+    out[4] = r[0]; out[5] = r[1]; out[6] = r[2];
+}
+
+/* Sophus SE3d(Matrix3d R, Vector3d t) (src/LoopHandler.cc:283, 643): SO3(R) = Eigen's Quaternion from a rotation
+ * matrix (quaternion_assign_impl<3,3>: the trace branch, else the largest-diagonal branch; no normalisation).
+ * R row-major. */
+void or_se3_from_Rt(const double* R, const double* t, double* out) {
+#define M(i, j) R[3 * (i) + (j)]
+    double q[4];  /* x, y, z, w */
+    double tr = (M(0, 0) + M(1, 1)) + M(2, 2);
+    if (tr > 0.0) {
+        tr = sqrt(tr + 1.0);
+        q[3] = 0.5 * tr;
+        tr = 0.5 / tr;
+        q[0] = (M(2, 1) - M(1, 2)) * tr;
+        q[1] = (M(0, 2) - M(2, 0)) * tr;
+        q[2] = (M(1, 0) - M(0, 1)) * tr;
+    } else {
+        int i = 0;
+        if (M(1, 1) > M(0, 0)) i = 1;
+        if (M(2, 2) > M(i, i)) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        tr = sqrt(M(i, i) - M(j, j) - M(k, k) + 1.0);
+        q[i] = 0.5 * tr;
+        tr = 0.5 / tr;
+        q[3] = (M(k, j) - M(j, k)) * tr;
+        q[j] = (M(j, i) + M(i, j)) * tr;
+        q[k] = (M(k, i) + M(i, k)) * tr;
+    }
+#undef M
+    for (int i = 0; i < 4; ++i) out[i] = q[i];
+    out[4] = t[0]; out[5] = t[1]; out[6] = t[2];
+}
+
 /* SE3::exp(a), a = (upsilon, omega) */
 void or_se3_exp(const double* a, double* out) {
     const double* om = a + 3;

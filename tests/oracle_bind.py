@@ -47,6 +47,8 @@ class Oracle:
             "or_triangulate_matches": (_I, [_P, _P, _P, _P, _I, _P, _P]),
             "or_se3_exp": (None, [_P, _P]),
             "or_se3_mul": (None, [_P, _P, _P]),
+            "or_se3_inverse": (None, [_P, _P]),
+            "or_se3_from_Rt": (None, [_P, _P, _P]),
             "or_se3_act": (None, [_P, _P, _P]),
             "or_quat_to_R": (None, [_P, _P]),
             "or_ksin": (ctypes.c_double, [ctypes.c_double]),
@@ -224,6 +226,19 @@ class Oracle:
         B = np.ascontiguousarray(B, np.float64)
         out = np.zeros(7)
         self.lib.or_se3_mul(_p(A), _p(B), _p(out))
+        return out
+
+    def se3_inverse(self, T):
+        T = np.ascontiguousarray(T, np.float64)
+        out = np.zeros(7)
+        self.lib.or_se3_inverse(_p(T), _p(out))
+        return out
+
+    def se3_from_Rt(self, R, t):
+        R = np.ascontiguousarray(R, np.float64).reshape(9)
+        t = np.ascontiguousarray(t, np.float64).reshape(3)
+        out = np.zeros(7)
+        self.lib.or_se3_from_Rt(_p(R), _p(t), _p(out))
         return out
 
     def se3_act(self, T, p):

@@ -1,0 +1,429 @@
+// loop_handler.cpp -- LoopHandler over the C ABI (see loop_handler.hpp).  Line references are to
+// /root/reference/src/LoopHandler.cc unless noted.
+#include "loop_handler.hpp"
+
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <fstream>
+#include <iostream>
+#include <iterator>
+
+#include "../../include/yavo/yavo_geom.h"
+#include "json_config.hpp"
+
+namespace yavo_fe {
+
+namespace {
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// int(v) for the reference's cv::Point2i(double, double) / Point2i(float, float): truncation toward zero; a value
+// outside int (or NaN) gives INT_MIN, what x86-64's cvttsd2si returns (the reference's conversion is UB there)
+int trunc_int(double v) {
+    if (!(v > -2147483649.0 && v < 2147483648.0)) return INT_MIN;
+    return (int)v;
+}
+
+}  // namespace
+
+MapPoint::ptr MapPoint::createMapPoint() {
+    static unsigned long _ptID = 0;
+    auto mp = std::make_shared<MapPoint>();
+    mp->ptID = ++_ptID;
+    return mp;
+}
+
+unsigned long Frame::createFrameID() {
+    static unsigned long frameID_ = 0;
+    frameID_++;
+    return frameID_;
+}
+
+// :7-33.  cameraType "mono" -> image_0 only; anything else -> stereo with image_1.  Calibration from
+// basePath + sequence + "/calib.txt" (handler3D.setCalibParams -> Camera::K of P0).
+LoopHandler::LoopHandler(const std::string& config, Device* dev) : dev_(dev) {
+    JsonConfig value;
+    if (!value.parse_file(config)) {
+        error_ = "cannot parse config " + config;
+        return;
+    }
+    basePath_ = value.asString("basePath");
+    seqNo_ = value.asString("sequence");
+    const std::string camType = value.asString("cameraType");
+    if (camType == "mono") {
+        isStereo_ = false;
+        leftImagesPath_ = basePath_ + seqNo_ + "/image_0/";
+        rightImagesPath_ = "";
+    } else {
+        isStereo_ = true;
+        leftImagesPath_ = basePath_ + seqNo_ + "/image_0/";
+        rightImagesPath_ = basePath_ + seqNo_ + "/image_1/";
+    }
+    // generatePathTrain (:37-57): the sorted listings of getFilesInFolder
+    yv_seq* seq = nullptr;
+    int st = yv_seq_open((basePath_ + seqNo_).c_str(), isStereo_ ? 1 : 0, &seq);
+    if (st != YV_OK) {
+        error_ = "no image_0 listing under " + basePath_ + seqNo_;
+        return;
+    }
+    const int n = yv_seq_frames(seq);
+    char buf[4096];
+    for (int i = 0; i < n; ++i) {
+        if (yv_seq_path(seq, i, 0, buf, sizeof buf) > 0) leftPathTrain.emplace_back(buf);
+        if (isStereo_ && yv_seq_path(seq, i, 1, buf, sizeof buf) > 0) rightPathTrain.emplace_back(buf);
+    }
+    double P0[16], P1[16], K1[9];
+    st = yv_seq_calib(seq, P0, P1, K_, K1);
+    yv_seq_close(seq);
+    if (st != YV_OK) {
+        error_ = "no calib.txt under " + basePath_ + seqNo_;
+        return;
+    }
+    map = std::make_shared<Map>();
+    if (dev_ && dev_->ok()) {
+        fd_ = std::make_unique<FastDetector>(*dev_, 12, 50);  // fd(12, 50), brief(256) (:7)
+        brief_ = std::make_unique<Brief>(*dev_, 256);
+    }
+    ok_ = true;
+}
+
+bool LoopHandler::gpu(int st, const char* what) {
+    if (st == YV_OK) return true;
+    gpu_status_ = st;
+    std::cerr << "yavo: " << what << " failed: " << yv_status_string(st) << std::endl;
+    return false;
+}
+
+// :918-930
+Frame::ptr LoopHandler::getNextFrame() {
+    if (train_it_ >= leftPathTrain.size()) return nullptr;
+    const std::string& path = leftPathTrain[train_it_];
+    // cv::imread(path, IMREAD_GRAYSCALE) (:919) = the PNG file decoded to 8-bit grey
+    std::ifstream fin(path, std::ios::binary);
+    std::vector<uint8_t> file((std::istreambuf_iterator<char>(fin)), std::istreambuf_iterator<char>());
+    int H = 0, W = 0;
+    if (file.empty() || yv_png_info(file.data(), file.size(), &H, &W) != YV_OK) {
+        std::cerr << "yavo: cannot read " << path << std::endl;
+        return nullptr;
+    }
+    auto frame = std::make_shared<Frame>();
+    frame->rows = H;
+    frame->cols = W;
+    frame->data.resize((size_t)H * W);
+    const int st = yv_png_decode_gray(file.data(), file.size(), frame->data.data(), W, H, W);
+    if (st != YV_OK) {
+        std::cerr << "yavo: cannot decode " << path << " (" << yv_status_string(st) << ")" << std::endl;
+        return nullptr;
+    }
+    currentFrameId_ = (int)train_it_;
+    train_it_++;
+    frame->frameID = Frame::createFrameID();
+    return frame;
+}
+
+// :457-466
+bool LoopHandler::takeVOStep() {
+    Frame::ptr frame = getNextFrame();
+    if (!frame) return false;
+    insertFrameFeatures(frame);
+    addFrame(frame);
+    return gpu_status_ == YV_OK;
+}
+
+// :468-485: getFastFeatures + computeBrief (the keypoints go to the frame's Image)
+void LoopHandler::insertFrameFeatures(const Frame::ptr& frame) {
+    const double t0 = now_s();
+    if (!fd_ || !brief_) {
+        gpu(YV_ERR_NODEVICE, "insertFrameFeatures");
+        return;
+    }
+    auto features = fd_->getFastFeatures(*frame);
+    if (!gpu(fd_->status(), "getFastFeatures")) return;
+    brief_->computeBrief(features, *frame);
+    gpu(brief_->status(), "computeBrief");
+    t_features += now_s() - t0;
+}
+
+// :80-124
+void LoopHandler::addFrame(const Frame::ptr& frame) {
+    currentFrame_ = frame;
+    ev_ = FrameEvent();
+    ev_.frame = currentFrameId_;
+    ev_.keypoints = (int)frame->keypoints.size();
+    if (status_ == INIT) {
+        if (lastFrame_) {
+            const double t0 = now_s();
+            if (buildInitMap()) status_ = TRACKING;
+            ev_.kind = FrameEvent::INIT_MAP;
+            t_init += now_s() - t0;
+        }
+    } else if (status_ == TRACKING) {
+        const double t0 = now_s();
+        const bool trackSuccess = track();
+        t_track += now_s() - t0;
+        ev_.kind = FrameEvent::TRACKED;
+        if (!trackSuccess) {
+            const double t1 = now_s();
+            reinitialize();
+            map->insertKeyFrame(currentFrame_);
+            ev_.kind = FrameEvent::REINIT;
+            t_reinit += now_s() - t1;
+        }
+    } else if (status_ == RESET) {
+        if (reinitialize()) status_ = TRACKING;
+        ev_.kind = FrameEvent::REINIT;
+    }
+    // the previous frame's pixels and descriptors are not read again (the map keeps the frame for its pose)
+    if (lastFrame_) {
+        lastFrame_->data.clear();
+        lastFrame_->data.shrink_to_fit();
+        lastFrame_->keypoints.clear();
+        lastFrame_->keypoints.shrink_to_fit();
+    }
+    lastFrame_ = currentFrame_;
+    trajectory_.push_back(currentFrame_->pose);
+    events_.push_back(ev_);
+}
+
+// _3DHandler::getFRANSAC(filterMatches, F, 400, 0.1) (src/3DHandler.cc:145-195): 400 hypotheses of 8 indices drawn
+// uniformly from [0, n) with replacement.  The reference's F is never used after the call (:222, :562).
+int LoopHandler::getFRANSAC(const std::vector<Matches>& m, double F[9]) {
+    const int n = (int)m.size();
+    for (int i = 0; i < 9; ++i) F[i] = 0;
+    if (n < 8) return 0;
+    const int iters = 400;
+    std::vector<int32_t> samples(8 * iters);
+    std::uniform_int_distribution<int> dist(0, n - 1);
+    for (auto& s : samples) s = dist(ransac_rng_);
+    int max_inl = 0, found = 0;
+    if (!gpu(yv_f_ransac(dev_->ctx(), m.data(), n, samples.data(), iters, 0.1, F, &max_inl, &found), "getFRANSAC"))
+        return 0;
+    return found ? max_inl : 0;
+}
+
+// :575-648 / :228-290: E = findEssentialMat(curr, prev, 718.8560, (607.1928, 185.2157), RANSAC, 0.999, 1.0);
+// recoverPose(E, curr, last, K, R, t); currPose = SE3(R, t)
+bool LoopHandler::essentialPose(const std::vector<Matches>& filt, SE3& currPose) {
+    const int n = (int)filt.size();
+    std::vector<float> curr(2 * n), prev(2 * n);
+    for (int i = 0; i < n; ++i) {
+        prev[2 * i] = (float)filt[i].pt1.x;
+        prev[2 * i + 1] = (float)filt[i].pt1.y;
+        curr[2 * i] = (float)filt[i].pt2.x;
+        curr[2 * i + 1] = (float)filt[i].pt2.y;
+    }
+    double E[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    std::vector<uint8_t> mask(n > 0 ? n : 1);
+    int found = 0;
+    if (!gpu(yv_find_essential(dev_->ctx(), curr.data(), prev.data(), n, 718.8560, 607.1928, 185.2157, 0.999, 1.0,
+                               E, mask.data(), &found),
+             "findEssentialMat"))
+        return false;
+    ev_.essential_found = found;
+    double R[9], t[3];
+    int good = 0;
+    if (!gpu(yv_recover_pose(dev_->ctx(), E, curr.data(), prev.data(), n, K_, R, t, &good), "recoverPose"))
+        return false;
+    currPose = se3::from_Rt(R, t);
+    return true;
+}
+
+// :532-652
+bool LoopHandler::buildInitMap() {
+    std::vector<Matches> matches = brief_->matchFeatures(*lastFrame_, *currentFrame_);
+    std::vector<Matches> filterMatches;
+    brief_->removeOutliers(matches, filterMatches, 20);
+    if (!gpu(brief_->status(), "matchFeatures / removeOutliers")) return false;
+    ev_.matches_kept = (int)filterMatches.size();
+    // only the matched-and-kept points become features (:555-561)
+    for (const auto& m : filterMatches) {
+        Feature f1, f2;
+        f1.kp = Point{m.pt1.x, m.pt1.y};
+        f2.kp = Point{m.pt2.x, m.pt2.y};
+        lastFrame_->features.push_back(f1);
+        currentFrame_->features.push_back(f2);
+    }
+    double F[9];
+    ev_.f_inliers = getFRANSAC(filterMatches, F);
+    SE3 currPose;
+    if (!essentialPose(filterMatches, currPose)) return false;
+    currentFrame_->pose = se3::inverse(currPose);  // :621-622
+    map->insertKeyFrame(lastFrame_);
+    map->insertKeyFrame(currentFrame_);
+    ev_.new_landmarks = triangulate2View(lastFrame_, currentFrame_, filterMatches, true);
+    relativeMotion = se3::mul(currentFrame_->pose, se3::inverse(lastFrame_->pose));  // :649
+    return true;
+}
+
+// :658-726: each kept match triangulated from the two poses (pixel2camera of pt1 / pt2, DLT + SVD); accepted
+// points (triangulation ok and Z > 0) become map points.  firstView: linked to the existing features i of both
+// frames; otherwise a new current-frame feature at pt2 carries the point.
+int LoopHandler::triangulate2View(const Frame::ptr& last, const Frame::ptr& curr,
+                                  const std::vector<Matches>& filtMatches, bool firstView) {
+    const int n = (int)filtMatches.size();
+    if (n == 0) return 0;
+    std::vector<double> X(3 * (size_t)n);
+    std::vector<uint8_t> ok(n);
+    int n_ok = 0;
+    if (!gpu(yv_triangulate(dev_->ctx(), last->pose.d, curr->pose.d, K_, filtMatches.data(), n, X.data(), ok.data(),
+                            &n_ok),
+             "triangulation"))
+        return 0;
+    int landMarks = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!ok[i]) continue;
+        auto mp = MapPoint::createMapPoint();
+        mp->position[0] = X[3 * i];
+        mp->position[1] = X[3 * i + 1];
+        mp->position[2] = X[3 * i + 2];
+        if (firstView) {
+            mp->observations += 2;
+            currentFrame_->features[i].mapPoint = mp;
+            last->features[i].mapPoint = mp;
+        } else {
+            Feature f;
+            f.kp = Point{filtMatches[i].pt2.x, filtMatches[i].pt2.y};
+            f.mapPoint = mp;
+            currentFrame_->features.push_back(f);
+            mp->observations += 1;
+        }
+        map->insertMapPoint(mp);
+        landMarks++;
+    }
+    return landMarks;
+}
+
+// :132-165
+bool LoopHandler::track() {
+    if (lastFrame_) currentFrame_->pose = se3::mul(relativeMotion, lastFrame_->pose);
+    const int goodInliers = trackLastFrame();
+    ev_.tracked = goodInliers;
+    if (goodInliers < 2) return false;
+    const int optimizedInliers = optimizePoseOnly();
+    ev_.inliers = optimizedInliers;
+    if (optimizedInliers < 100) return false;
+    relativeMotion = se3::mul(currentFrame_->pose, se3::inverse(lastFrame_->pose));
+    return true;
+}
+
+// :306-449: the last frame's features with a map point, projected with the current pose guess (world2Camera;
+// kept when neither truncated coordinate is negative), tracked by pyramidal LK (11x11, 3 levels, 30 its / 0.01,
+// flags 0: the projection is not an initial guess), status-1 points become current features at
+// Point2i(next.y, next.x) carrying the same map point.
+int LoopHandler::trackLastFrame() {
+    std::vector<int> idx;
+    std::vector<double> Xs;
+    std::vector<MapPoint::ptr> mps;
+    for (int i = 0; i < (int)lastFrame_->features.size(); ++i) {
+        if (auto mp = lastFrame_->features[i].mapPoint.lock()) {
+            idx.push_back(i);
+            mps.push_back(mp);
+            Xs.insert(Xs.end(), mp->position, mp->position + 3);
+        }
+    }
+    const int nc = (int)idx.size();
+    std::vector<double> proj(3 * (size_t)std::max(nc, 1));
+    if (nc > 0 &&
+        !gpu(yv_world2camera(dev_->ctx(), Xs.data(), nc, currentFrame_->pose.d, K_, proj.data()), "world2Camera"))
+        return 0;
+    std::vector<float> lastKpt, currKpt;
+    std::vector<int> lastIndex;
+    std::vector<MapPoint::ptr> lastMps;
+    for (int k = 0; k < nc; ++k) {
+        const int nx = trunc_int(proj[3 * k + 1] / proj[3 * k + 2]);  // Point2i(coeff(1)/coeff(2), coeff(0)/coeff(2))
+        const int ny = trunc_int(proj[3 * k] / proj[3 * k + 2]);
+        if (!(nx < 0 || ny < 0)) {
+            currKpt.push_back((float)nx);
+            currKpt.push_back((float)ny);
+            const Point kp = lastFrame_->features[idx[k]].kp;
+            lastKpt.push_back((float)kp.y);  // Point2i(kp.y, kp.x)
+            lastKpt.push_back((float)kp.x);
+            lastIndex.push_back(idx[k]);
+            lastMps.push_back(mps[k]);
+        }
+    }
+    const int n = (int)lastIndex.size();
+    if (n == 0) return 0;  // an empty point set: calcOpticalFlowPyrLK returns empty status
+    std::vector<float> next(2 * (size_t)n), err(n);
+    std::vector<uint8_t> flowStatus(n);
+    if (!gpu(yv_calc_optical_flow_pyr_lk(dev_->ctx(), lastFrame_->data.data(), currentFrame_->data.data(),
+                                         currentFrame_->rows, currentFrame_->cols, currentFrame_->cols, lastKpt.data(),
+                                         n, 11, 3, 30, 0.01, 0.001, next.data(), flowStatus.data(), err.data()),
+             "calcOpticalFlowPyrLK"))
+        return 0;
+    int goodFeatures = 0;
+    for (int i = 0; i < n; ++i) {
+        if (flowStatus[i] != 1) continue;
+        if (auto mp = lastFrame_->features[lastIndex[i]].mapPoint.lock()) {
+            Feature f;
+            f.kp = Point{trunc_int(next[2 * i + 1]), trunc_int(next[2 * i])};  // Point2i(currFrameKpt.y, .x)
+            f.mapPoint = mp;
+            currentFrame_->features.push_back(f);
+            goodFeatures++;
+        }
+    }
+    return goodFeatures;
+}
+
+// :730-861: one pose vertex at the current pose, one projection edge per feature with a map point (measurement
+// (kp.x, kp.y), Huber), 4 rounds of optimize(10) with chi2 > 5.991 outliers; outliers lose their map point
+int LoopHandler::optimizePoseOnly() {
+    std::vector<int> fi;
+    std::vector<double> X, uv;
+    for (int i = 0; i < (int)currentFrame_->features.size(); ++i) {
+        const Feature& f = currentFrame_->features[i];
+        if (auto mp = f.mapPoint.lock()) {
+            fi.push_back(i);
+            X.insert(X.end(), mp->position, mp->position + 3);
+            uv.push_back((double)f.kp.x);
+            uv.push_back((double)f.kp.y);
+        }
+    }
+    const int n = (int)fi.size();
+    std::vector<uint8_t> outlier(n > 0 ? n : 1);
+    int inliers = 0;
+    SE3 pose = currentFrame_->pose;
+    if (!gpu(yv_pose_lm(dev_->ctx(), X.data(), uv.data(), n, K_, pose.d, outlier.data(), &inliers),
+             "optimizePoseOnly"))
+        return 0;
+    currentFrame_->pose = pose;
+    for (int k = 0; k < n; ++k) {
+        Feature& f = currentFrame_->features[fi[k]];
+        if (outlier[k]) f.mapPoint.reset();
+        f.isOutlier = false;
+    }
+    return inliers;
+}
+
+// :168-296
+bool LoopHandler::reinitialize() {
+    currentFrame_->features.clear();
+    std::vector<Matches> matches = brief_->matchFeatures(*lastFrame_, *currentFrame_);
+    std::vector<Matches> filterMatches;
+    brief_->removeOutliers(matches, filterMatches, 20);
+    if (!gpu(brief_->status(), "matchFeatures / removeOutliers")) return false;
+    ev_.matches_kept = (int)filterMatches.size();
+    double F[9];
+    ev_.f_inliers = getFRANSAC(filterMatches, F);
+    SE3 currPose;
+    if (!essentialPose(filterMatches, currPose)) return false;
+    currPose = se3::inverse(currPose);
+    currentFrame_->pose = se3::mul(currPose, lastFrame_->pose);  // :283-285
+    ev_.new_landmarks = triangulate2View(lastFrame_, currentFrame_, filterMatches, false);
+    relativeMotion = se3::mul(currentFrame_->pose, se3::inverse(lastFrame_->pose));
+    return true;
+}
+
+// :501-512
+void LoopHandler::runVO(int max_frames) {
+    int k = 0;
+    while (max_frames < 0 || k < max_frames) {
+        if (!takeVOStep()) break;
+        ++k;
+    }
+}
+
+}  // namespace yavo_fe
