@@ -60,6 +60,13 @@ int yv_upload(yv_ctx* ctx, void* dev_dst, const void* host_src, size_t bytes);
 /* FastDetector constructor constants (include/FastDetector.hpp:32-38): intensityThreshold (40) and
  * fastCornerNumThreshold (2000). */
 int yv_set_fast_params(yv_ctx* ctx, int intensity_threshold, int max_corners);
+/* Which cv::eigen the Harris response (src/FastDetector.cc:265) restates -- the reference's OpenCV build decides:
+ * 0 (default) = OpenCV's JacobiImpl_<float> (built without Eigen), 1 = HAVE_EIGEN's
+ * Eigen::SelfAdjointEigenSolver<MatrixXf> (Eigen 3.4).  Both are bit-exact against the oracle's restatements; they
+ * differ from each other in the last bits of most responses. */
+#define YV_HARRIS_EIGEN_JACOBI 0
+#define YV_HARRIS_EIGEN_EIGEN3 1
+int yv_set_harris_eigen(yv_ctx* ctx, int flavour);
 /* Brief offsets table (src/BriefDescriptor.cc:4-20): 256 rows of {drow1, dcol1, drow2, dcol2},
  * each in [-8, 8]. */
 int yv_set_brief_offsets(yv_ctx* ctx, const int8_t* offsets /* [256*4] */);

@@ -193,13 +193,114 @@ void or_eigen_jacobi_f32(const float* Ain, int n, float* W) {
     }
 }
 
+/* cv::eigen(M, evals) for CV_32F in an OpenCV built WITH_EIGEN (HAVE_EIGEN, modules/core/src/lapack.cpp):
+ * Eigen::SelfAdjointEigenSolver<MatrixXf>::compute(M, EigenvaluesOnly), eigenvalues reversed to descending.
+ * Restated from Eigen 3.4.0 (Eigenvalues/SelfAdjointEigenSolver.h, Tridiagonalization.h, Jacobi/Jacobi.h), the
+ * release the reference's macOS / Ubuntu setup installs (macInstalltion.txt; parity with a running build unpinned):
+ *   - the lower triangle scaled by s = max |m_ij| (1 if 0); for n = 2 the tridiagonalisation is the identity
+ *     (a one-element Householder vector: tau = 0, beta = m10; the rank update adds -0 terms only), so
+ *     diag = (m00 / s, m11 / s), subdiag = m10 / s;
+ *   - computeFromTridiagonal_impl: deflate when |e| < FLT_MIN or (e / FLT_EPSILON)^2 <= |d0| + |d1|, otherwise one
+ *     implicit Wilkinson-shift QR step (tridiagonal_qr_step with numext::hypot and JacobiRotation::makeGivens), at
+ *     most 30 n iterations; the eigenvalues are sorted ascending and multiplied back by s. */
+static inline float eig_hypotf(float x, float y) {
+    /* numext::hypot -> positive_real_hypot(|x|, |y|) */
+    x = fabsf(x);
+    y = fabsf(y);
+    if (isinf(x) || isinf(y)) return INFINITY;
+    if (isnan(x) || isnan(y)) return NAN;
+    const float p = x > y ? x : y;  /* numext::maxi(x, y) = std::max */
+    if (p == 0.0f) return 0.0f;
+    const float qp = (y < x ? y : x) / p;  /* numext::mini(y, x) = std::min */
+    return p * sqrtf(1.0f + qp * qp);
+}
+
+static inline void eig_make_givens(float p, float q, float* c, float* s) {
+    if (q == 0.0f) {
+        *c = p < 0.0f ? -1.0f : 1.0f;
+        *s = 0.0f;
+    } else if (p == 0.0f) {
+        *c = 0.0f;
+        *s = q < 0.0f ? 1.0f : -1.0f;
+    } else if (fabsf(p) > fabsf(q)) {
+        const float t = q / p;
+        float u = sqrtf(1.0f + t * t);
+        if (p < 0.0f) u = -u;
+        *c = 1.0f / u;
+        *s = -t * *c;
+    } else {
+        const float t = p / q;
+        float u = sqrtf(1.0f + t * t);
+        if (q < 0.0f) u = -u;
+        *s = -1.0f / u;
+        *c = -t * *s;
+    }
+}
+
+void or_eigen_selfadjoint2_f32(float m00, float m01, float m11, float* W) {
+    float scale = fabsf(m00);
+    if (fabsf(m01) > scale) scale = fabsf(m01);
+    if (fabsf(m11) > scale) scale = fabsf(m11);
+    if (scale == 0.0f) scale = 1.0f;
+    float d0 = m00 / scale, d1 = m11 / scale, e = m01 / scale;
+    const float considerAsZero = FLT_MIN, precision_inv = 1.0f / FLT_EPSILON;
+    int iter = 0, ok = 1;
+    while (1) {
+        if (fabsf(e) < considerAsZero) {
+            e = 0.0f;
+        } else {
+            const float se = precision_inv * e;
+            if (se * se <= (fabsf(d0) + fabsf(d1))) e = 0.0f;
+        }
+        if (e == 0.0f) break;
+        iter++;
+        if (iter > 30 * 2) { ok = 0; break; }
+        /* tridiagonal_qr_step(start 0, end 1): Wilkinson shift, one Givens rotation */
+        const float td = (d0 - d1) * 0.5f;
+        float mu = d1;
+        if (td == 0.0f) {
+            mu -= fabsf(e);
+        } else if (e != 0.0f) {
+            const float e2 = e * e;
+            const float h = eig_hypotf(td, e);
+            if (e2 == 0.0f) mu -= e / ((td + (td > 0.0f ? h : -h)) / e);
+            else mu -= e2 / (td + (td > 0.0f ? h : -h));
+        }
+        const float x = d0 - mu, z = e;
+        if (z != 0.0f) {
+            float c, sn;
+            eig_make_givens(x, z, &c, &sn);
+            const float sdk = sn * d0 + c * e;
+            const float dkp1 = sn * e + c * d1;
+            const float nd0 = c * (c * d0 - sn * e) - sn * (c * e - sn * d1);
+            const float nd1 = sn * sdk + c * dkp1;
+            const float ne = c * sdk - sn * dkp1;
+            d0 = nd0;
+            d1 = nd1;
+            e = ne;
+        }
+    }
+    /* ascending sort (only on success; NoConvergence leaves them, and cv::eigen then returns false with the output
+     * array unwritten -- not reachable for 2 x 2 in practice), scale back, reverse to descending */
+    if (ok && d1 < d0) { const float t = d0; d0 = d1; d1 = t; }
+    d0 *= scale;
+    d1 *= scale;
+    W[0] = d1;
+    W[1] = d0;
+}
+
+/* which cv::eigen the Harris response uses: 0 = JacobiImpl_ (OpenCV without Eigen), 1 = HAVE_EIGEN */
+static int g_harris_eigen = 0;
+void or_set_harris_eigen(int flavour) { g_harris_eigen = flavour; }
+
 /* src/FastDetector.cc:264-272: eigenValues(0) is the larger.  The expression is
  *   (float)( (double)(float)(e0*e1) - 0.04 * std::pow((double)(float)(e1+e0), 2) )
  * std::pow(float,int) promotes to double; the square of a float is exact in double. */
 float or_harris_response(float m00, float m01, float m11) {
     float M[4] = {m00, m01, m01, m11};
     float ev[2];
-    or_eigen_jacobi_f32(M, 2, ev);
+    if (g_harris_eigen == 1) or_eigen_selfadjoint2_f32(m00, m01, m11, ev);
+    else or_eigen_jacobi_f32(M, 2, ev);
     float prod = ev[0] * ev[1];
     float sum = ev[1] + ev[0];
     double sq = (double)sum * (double)sum;

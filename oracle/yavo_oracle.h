@@ -44,6 +44,10 @@ int or_fast_detect(const uint8_t* img, int H, int W, int stride, int thr, int ma
 float or_harris_response(float m00, float m01, float m11);
 /* OpenCV JacobiImpl_<float> eigenvalues (descending), the cv::eigen path without HAVE_EIGEN. */
 void or_eigen_jacobi_f32(const float* A, int n, float* w);
+/* cv::eigen with HAVE_EIGEN: Eigen 3.4 SelfAdjointEigenSolver<MatrixXf> on [m00 m01; m01 m11], descending. */
+void or_eigen_selfadjoint2_f32(float m00, float m01, float m11, float* w);
+/* the cv::eigen flavour of or_harris_response: 0 = JacobiImpl_ (default), 1 = HAVE_EIGEN */
+void or_set_harris_eigen(int flavour);
 
 /* ---- Gaussian blur (cv::GaussianBlur(img, out, Size(9,9), 2.5, 2.5): src/BriefDescriptor.cc:90) ---- */
 /* Bit-exact 8U fixed-point kernel: error-diffusion rounding (ed=1, OpenCV >= 3.4 bit-exact path) or

@@ -30,6 +30,9 @@ class Oracle:
                                     _P, _P, _I]),
             "or_harris_response": (ctypes.c_float, [ctypes.c_float, ctypes.c_float, ctypes.c_float]),
             "or_eigen_jacobi_f32": (None, [_P, _I, _P]),
+            "or_eigen_selfadjoint2_f32": (None, [ctypes.c_float, ctypes.c_float, ctypes.c_float, _P]),
+            "or_set_harris_eigen": (None, [_I]),
+            "or_std_sort_cut": (_I, [_P, _P, _I, _I, _I, _P]),
             "or_gauss_kernel_fixed": (None, [_I, ctypes.c_double, _I, _P]),
             "or_gaussian_blur_u8": (None, [_P, _I, _I, _I, _P, _I, _P]),
             "or_compute_brief_blurred": (_I, [_P, _I, _I, _P, _P, _I, _P, ctypes.POINTER(_I)]),
@@ -113,6 +116,23 @@ class Oracle:
 
     def harris_response(self, m00, m01, m11):
         return self.lib.or_harris_response(m00, m01, m11)
+
+    def set_harris_eigen(self, flavour):
+        """cv::eigen flavour of the Harris response: 0 = JacobiImpl_ (default), 1 = HAVE_EIGEN (Eigen 3.4)."""
+        self.lib.or_set_harris_eigen(int(flavour))
+
+    def eigen_selfadjoint2(self, m00, m01, m11):
+        w = np.zeros(2, np.float32)
+        self.lib.or_eigen_selfadjoint2_f32(m00, m01, m11, _p(w))
+        return w
+
+    def std_sort_cut(self, idx, resp, W, K=2000):
+        """The reference's std::sort(corners, response >) + first K (libstdc++), on scan-ordered candidates."""
+        idx = np.ascontiguousarray(idx, np.int32)
+        resp = np.ascontiguousarray(resp, np.float32)
+        out = np.zeros(max(min(len(idx), K), 1), np.int32)
+        m = self.lib.or_std_sort_cut(_p(idx), _p(resp), len(idx), W, K, _p(out))
+        return out[:m]
 
     def eigen_jacobi(self, A):
         A = np.ascontiguousarray(A, np.float32)

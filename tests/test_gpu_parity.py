@@ -46,6 +46,50 @@ def test_detect_matches_oracle(ctx, oracle, name):
     np.testing.assert_array_equal(resp.view(np.uint32), oresp.view(np.uint32))
 
 
+@pytest.mark.parametrize("name", ["synth_kitti_1234", "crop_epilines", "crop_epilinesOpencv", "uniform_noise",
+                                  "odd_shape", "checker"])
+def test_detect_eigen_flavour_matches_oracle(ctx, oracle, name):
+    """HAVE_EIGEN's cv::eigen (Eigen 3.4 SelfAdjointEigenSolver<MatrixXf>, yv_set_harris_eigen(1)): candidate set,
+    responses and the top-2000 order bit-identical to the oracle's restatement."""
+    img = _images()[name]
+    ctx.set_harris_eigen(1)
+    oracle.set_harris_eigen(1)
+    try:
+        rc, resp, nc = ctx.detect(img, 2000)
+        orc, oresp, onc = oracle.fast(img, 2000)
+    finally:
+        ctx.set_harris_eigen(0)
+        oracle.set_harris_eigen(0)
+    assert nc == onc
+    np.testing.assert_array_equal(rc, orc)
+    np.testing.assert_array_equal(resp.view(np.uint32), oresp.view(np.uint32))
+
+
+def test_batch_eigen_flavour_matches_oracle(ctx, oracle):
+    """The fused batch detect kernel with the HAVE_EIGEN flavour: keypoints of every image equal the oracle's."""
+    import torch
+    frames = [synth_frame(9, 2 * k, 5 * k) for k in range(3)]
+    offsets = np.fromfile(os.path.join(GOLDEN, "brief_offsets_mt19937_42.bin"), np.int8).reshape(256, 4)
+    H, W = frames[0].shape
+    d = torch.from_numpy(np.stack(frames)).to("cuda:0")
+    b = yv.Batch(ctx, 3, H, W, 2000, 0)
+    ctx.set_harris_eigen(1)
+    oracle.set_harris_eigen(1)
+    try:
+        b.run(d.data_ptr(), 3, W, H * W, 20)
+        ctx.sync()
+        v = b.view()
+        kpc = ctx.download(v.kp_count, np.int32, 3)
+        for i, img in enumerate(frames):
+            orc, _, _ = oracle.fast(img, 2000)
+            kps = ctx.download(v.keypoints + i * 2000 * 48, yv.KEYPOINT_DTYPE, kpc[i])
+            np.testing.assert_array_equal(kps, oracle.brief(img, orc, offsets))
+    finally:
+        ctx.set_harris_eigen(0)
+        oracle.set_harris_eigen(0)
+        b.close()
+
+
 @pytest.mark.parametrize("max_kp", [0, 1, 7, 100, 1999, 2000])
 def test_detect_cut_sizes(ctx, oracle, max_kp):
     img = synth_frame(1234, 0, 0)

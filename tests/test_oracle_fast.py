@@ -233,3 +233,44 @@ def test_calib_kitti00_fixture(oracle):
     assert nv == 12  # KITTI rows hold 12 values; the reference reads 16 (out of bounds), 0 here
     assert abs(left[0, 0] - 718.856) < 1 and abs(right[0, 0] - 718.856) < 1
     assert abs(left[1, 2] - 185.216) < 1 and abs(right[1, 2] - 185.216) < 1
+
+
+def test_eigen_selfadjoint_flavour(oracle):
+    """HAVE_EIGEN's cv::eigen restatement (Eigen 3.4 SelfAdjointEigenSolver<MatrixXf>): eigenvalues of integer
+    structure tensors within float rounding of the exact ones, descending; diagonal and zero tensors exact."""
+    rng = np.random.default_rng(11)
+    for _ in range(2000):
+        a, d = float(rng.integers(0, 2 ** 22)), float(rng.integers(0, 2 ** 22))
+        b = float(rng.integers(-2 ** 21, 2 ** 21)) if rng.random() > 0.1 else 0.0
+        w = oracle.eigen_selfadjoint2(a, b, d)
+        ref = np.linalg.eigvalsh(np.array([[a, b], [b, d]]))[::-1]
+        assert w[0] >= w[1]
+        np.testing.assert_allclose(w, ref, rtol=0, atol=4e-7 * max(abs(ref).max(), 1.0))
+    np.testing.assert_array_equal(oracle.eigen_selfadjoint2(5.0, 0.0, 9.0), [9.0, 5.0])
+    np.testing.assert_array_equal(oracle.eigen_selfadjoint2(0.0, 0.0, 0.0), [0.0, 0.0])
+
+
+def test_eigen_flavours_keep_the_candidate_set(oracle):
+    """The flavour moves response bits, never the FAST candidate set (an integer test)."""
+    from ya_vo_amd.synth import synth_frame
+    img = synth_frame(3, 0, 0, 160, 400)
+    out = []
+    for fl in (0, 1):
+        oracle.set_harris_eigen(fl)
+        out.append(oracle.fast(img, 100000, with_candidates=True))
+    oracle.set_harris_eigen(0)
+    np.testing.assert_array_equal(np.sort(out[0][3]), np.sort(out[1][3]))
+    assert out[0][2] == out[1][2]
+
+
+def test_std_sort_diagnostic_matches_canonical_without_ties(oracle):
+    """libstdc++ std::sort of the reference's comparator agrees with the canonical order when responses are
+    distinct, and keeps a tie group's members (in some order) when they are not."""
+    rng = np.random.default_rng(5)
+    idx = np.arange(3000, dtype=np.int32)
+    resp = rng.permutation(3000).astype(np.float32)
+    cut = oracle.std_sort_cut(idx, resp, 100, 2000)
+    np.testing.assert_array_equal(cut, np.argsort(-resp, kind="stable")[:2000])
+    resp[:50] = 7.0e6  # a tie group above every other response
+    cut = oracle.std_sort_cut(idx, resp, 100, 2000)
+    assert set(cut[:50].tolist()) == set(range(50))

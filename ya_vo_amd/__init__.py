@@ -71,6 +71,7 @@ SIGNATURES = {
     "yv_download": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "yv_upload": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "yv_set_fast_params": (_I, [_P, _I, _I]),
+    "yv_set_harris_eigen": (_I, [_P, _I]),
     "yv_set_brief_offsets": (_I, [_P, _P]),
     "yv_set_blur_kernel": (_I, [_P, _P]),
     "yv_detect": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
@@ -360,6 +361,10 @@ class Context(_GeomMixin):
 
     def set_fast_params(self, intensity_threshold: int = 40, max_corners: int = 2000) -> None:
         _check(self.lib.yv_set_fast_params(self.handle, intensity_threshold, max_corners), "yv_set_fast_params")
+
+    def set_harris_eigen(self, flavour: int = 0) -> None:
+        """cv::eigen flavour of the Harris response: 0 = OpenCV JacobiImpl_ (default), 1 = HAVE_EIGEN (Eigen 3.4)."""
+        _check(self.lib.yv_set_harris_eigen(self.handle, int(flavour)), "yv_set_harris_eigen")
 
     def set_brief_offsets(self, offsets: np.ndarray) -> None:
         o = np.ascontiguousarray(offsets, dtype=np.int8).reshape(256, 4)

@@ -20,6 +20,7 @@ struct yv_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     int fast_thr = 40;         // include/FastDetector.hpp:35
+    int harris_eigen = 0;      // cv::eigen flavour of the Harris response (yv_set_harris_eigen)
     int max_corners = 2000;    // include/FastDetector.hpp:36
     uint16_t k9[9] = {12, 22, 31, 41, 44, 41, 31, 22, 12};  // cv::GaussianBlur 9x9, sigma 2.5, 8U
     int8_t* d_offsets = nullptr;                              // [256*4]
@@ -315,6 +316,12 @@ int yv_set_fast_params(yv_ctx* ctx, int intensity_threshold, int max_corners) {
     return YV_OK;
 }
 
+int yv_set_harris_eigen(yv_ctx* ctx, int flavour) {
+    if (!ctx || flavour < 0 || flavour > 1) return YV_ERR_INVALID;
+    ctx->harris_eigen = flavour;
+    return YV_OK;
+}
+
 int yv_set_brief_offsets(yv_ctx* ctx, const int8_t* offsets) {
     if (!ctx || !offsets) return YV_ERR_INVALID;
     for (int i = 0; i < 1024; ++i)
@@ -499,7 +506,7 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
     b->last_run = run;
     int rc = YV_OK;
     rc |= record_stage(b, s, run, 0);
-    yavo::launch_detect_blur(d_images, n_images, H, W, stride, image_pitch, ctx->fast_thr, b->cand_keys, b->cap,
+    yavo::launch_detect_blur(d_images, n_images, H, W, stride, image_pitch, ctx->fast_thr, ctx->harris_eigen, b->cand_keys, b->cap,
                              b->cand_count, ctx->k9, b->blur, s);
     rc |= record_stage(b, s, run, 1);
     if (b->overlap_mode == 2) rc |= launch_deferred_after(b, s);
@@ -890,7 +897,7 @@ int yv_detect(yv_ctx* ctx, const uint8_t* img, int H, int W, int stride, int max
     hipStream_t s = ctx->stream;
     const int keep = std::min(std::min(ctx->max_corners, max_kp), b->max_kp);
     if (upload_image(b, img, stride, s) != YV_OK) return YV_ERR_HIP;
-    yavo::launch_fast_harris(b->staging, 1, H, W, W, (int64_t)H * W, ctx->fast_thr, b->cand_keys, b->cap,
+    yavo::launch_fast_harris(b->staging, 1, H, W, W, (int64_t)H * W, ctx->fast_thr, ctx->harris_eigen, b->cand_keys, b->cap,
                              b->cand_count, s);
     yavo::launch_topk(b->cand_keys, b->cap, b->cand_count, b->cand_seen, 1, H, W, b->max_kp, keep, b->det_rc, b->det_resp,
                       b->det_count, b->kp_src, b->kp_count, s);

@@ -35,13 +35,14 @@ struct Desc {                      // 256-bit BRIEF descriptor, test j -> bit j 
     uint32_t w[8];
 };
 
-// FAST-12 candidate test + Harris response, appends (response, index) keys per image.
+// FAST-12 candidate test + Harris response, appends (response, index) keys per image.  eig: the cv::eigen
+// flavour (0 = JacobiImpl_, 1 = HAVE_EIGEN's SelfAdjointEigenSolver).
 void launch_fast_harris(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,
-                        int thr, uint64_t* cand_keys, int64_t cap, uint32_t* cand_count,
+                        int thr, int eig, uint64_t* cand_keys, int64_t cap, uint32_t* cand_count,
                         hipStream_t s);
 // Fused FAST + Harris + 9x9 blur over the same LDS tile (the image is read once).
 void launch_detect_blur(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch, int thr,
-                        uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, const uint16_t* k9_host,
+                        int eig, uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, const uint16_t* k9_host,
                         uint8_t* blur, hipStream_t s);
 // 9-tap separable fixed-point Gaussian, BORDER_REFLECT_101; output [image][H][blur_pitch(W)].
 void launch_blur9(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,

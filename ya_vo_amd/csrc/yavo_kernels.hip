@@ -81,12 +81,89 @@ __device__ __forceinline__ float cv_hypotf(float a, float b) {
     return 0.0f;
 }
 
-// cv::eigen on the 2x2 float structure tensor = JacobiImpl_<float>(n=2): one rotation unless
-// |m01| <= FLT_EPSILON, then a descending sort; followed by the response expression of
-// src/FastDetector.cc:270 evaluated in double and rounded to float.
-__device__ __forceinline__ float harris_response(float a, float b, float d) {
+// cv::eigen in an OpenCV built with HAVE_EIGEN: Eigen 3.4 SelfAdjointEigenSolver<MatrixXf> on the 2x2 (oracle
+// or_eigen_selfadjoint2_f32 states the derivation): scale by the largest |entry|, implicit Wilkinson-shift QR steps
+// until (e / FLT_EPSILON)^2 <= |d0| + |d1| (or |e| < FLT_MIN), at most 60; ascending sort, scale back.  Returns
+// (w0 >= w1).  Every float operation in the oracle's order (-ffp-contract=off, IEEE div / sqrt).
+__device__ __forceinline__ float eig_hypotf(float x, float y) {
+    x = fabsf(x);
+    y = fabsf(y);
+    if (isinf(x) || isinf(y)) return __builtin_inff();
+    if (isnan(x) || isnan(y)) return __builtin_nanf("");
+    const float p = x > y ? x : y;
+    if (p == 0.0f) return 0.0f;
+    const float qp = (y < x ? y : x) / p;
+    return p * sqrtf(1.0f + qp * qp);
+}
+
+__device__ void eig_selfadjoint2(float m00, float m01, float m11, float& w0, float& w1) {
+    float scale = fabsf(m00);
+    if (fabsf(m01) > scale) scale = fabsf(m01);
+    if (fabsf(m11) > scale) scale = fabsf(m11);
+    if (scale == 0.0f) scale = 1.0f;
+    float d0 = m00 / scale, d1 = m11 / scale, e = m01 / scale;
+    int iter = 0, ok = 1;
+    while (true) {
+        if (fabsf(e) < 1.17549435082228750797e-38f) {
+            e = 0.0f;
+        } else {
+            const float se = 8388608.0f * e;
+            if (se * se <= (fabsf(d0) + fabsf(d1))) e = 0.0f;
+        }
+        if (e == 0.0f) break;
+        if (++iter > 60) { ok = 0; break; }
+        const float td = (d0 - d1) * 0.5f;
+        float mu = d1;
+        if (td == 0.0f) {
+            mu -= fabsf(e);
+        } else {
+            const float e2 = e * e;
+            const float h = eig_hypotf(td, e);
+            if (e2 == 0.0f) mu -= e / ((td + (td > 0.0f ? h : -h)) / e);
+            else mu -= e2 / (td + (td > 0.0f ? h : -h));
+        }
+        const float x = d0 - mu, z = e;
+        float c, sn;
+        if (x == 0.0f) {  // makeGivens(x, z) with z != 0
+            c = 0.0f;
+            sn = z < 0.0f ? 1.0f : -1.0f;
+        } else if (fabsf(x) > fabsf(z)) {
+            const float t = z / x;
+            float u = sqrtf(1.0f + t * t);
+            if (x < 0.0f) u = -u;
+            c = 1.0f / u;
+            sn = -t * c;
+        } else {
+            const float t = x / z;
+            float u = sqrtf(1.0f + t * t);
+            if (z < 0.0f) u = -u;
+            sn = -1.0f / u;
+            c = -t * sn;
+        }
+        const float sdk = sn * d0 + c * e;
+        const float dkp1 = sn * e + c * d1;
+        const float nd0 = c * (c * d0 - sn * e) - sn * (c * e - sn * d1);
+        const float nd1 = sn * sdk + c * dkp1;
+        const float ne = c * sdk - sn * dkp1;
+        d0 = nd0;
+        d1 = nd1;
+        e = ne;
+    }
+    if (ok && d1 < d0) { const float t = d0; d0 = d1; d1 = t; }
+    d0 *= scale;
+    d1 *= scale;
+    w0 = d1;
+    w1 = d0;
+}
+
+// cv::eigen on the 2x2 float structure tensor (eig = 0: JacobiImpl_<float>(n=2): one rotation unless
+// |m01| <= FLT_EPSILON, then a descending sort; eig = 1: the HAVE_EIGEN solver above), followed by the response
+// expression of src/FastDetector.cc:270 evaluated in double and rounded to float.
+__device__ __forceinline__ float harris_response(float a, float b, float d, int eig) {
     float w0 = a, w1 = d;
-    if (!(fabsf(b) <= 1.1920928955078125e-07f)) {
+    if (eig == 1) {
+        eig_selfadjoint2(a, b, d, w0, w1);
+    } else if (!(fabsf(b) <= 1.1920928955078125e-07f)) {
         const float p = b;
         const float y = (float)((double)(w1 - w0) * 0.5);
         float t = fabsf(y) + cv_hypotf(p, y);
@@ -98,7 +175,7 @@ __device__ __forceinline__ float harris_response(float a, float b, float d) {
         w0 -= t;
         w1 += t;
     }
-    if (w0 < w1) { float tmp = w0; w0 = w1; w1 = tmp; }
+    if (eig != 1 && w0 < w1) { float tmp = w0; w0 = w1; w1 = tmp; }
     const float prod = w0 * w1;
     const float sum = w1 + w0;
     const double sq = (double)sum * (double)sum;
@@ -173,7 +250,7 @@ constexpr int FT_LH = FT_H + 2 * FT_R;  // 64 LDS rows
 
 template <bool kBlur>
 __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__ imgs, int H, int W, int stride,
-                                                     int64_t pitch, int thr, uint64_t* __restrict__ cand_keys,
+                                                     int64_t pitch, int thr, int eig, uint64_t* __restrict__ cand_keys,
                                                      int64_t cap, uint32_t* __restrict__ cand_count, K9 kw,
                                                      uint8_t* __restrict__ blur) {
     __shared__ __align__(16) uint8_t tile[FT_LH * FT_LW];
@@ -393,7 +470,7 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
                 }
             }
             // all partial sums are integers < 2^24: exact in float, as in the reference
-            const float resp = harris_response((float)sxx, (float)sxy, (float)syy);
+            const float resp = harris_response((float)sxx, (float)sxy, (float)syy, eig);
             out[i] = make_key(resp, (uint32_t)((r0 + prr) * W + (c0 + ptx)));  // cap >= every pixel: in range
         }
     }
@@ -435,19 +512,19 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
 }
 
 void launch_fast_harris(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch,
-                        int thr, uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, hipStream_t s) {
+                        int thr, int eig, uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, hipStream_t s) {
     dim3 grid(((W + FT_W - 1) / FT_W) * ((H + FT_H - 1) / FT_H) * n_images);
     K9 kw = {};
-    hipLaunchKernelGGL(detect_kernel<false>, grid, dim3(256), 0, s, imgs, H, W, stride, pitch, thr, cand_keys,
+    hipLaunchKernelGGL(detect_kernel<false>, grid, dim3(256), 0, s, imgs, H, W, stride, pitch, thr, eig, cand_keys,
                        cap, cand_count, kw, (uint8_t*)nullptr);
 }
 
 void launch_detect_blur(const uint8_t* imgs, int n_images, int H, int W, int stride, int64_t pitch, int thr,
-                        uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, const uint16_t* k9_host,
+                        int eig, uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, const uint16_t* k9_host,
                         uint8_t* blur, hipStream_t s) {
     dim3 grid(((W + FT_W - 1) / FT_W) * ((H + FT_H - 1) / FT_H) * n_images);
     const K9 kw = make_k9(k9_host);
-    hipLaunchKernelGGL(detect_kernel<true>, grid, dim3(256), 0, s, imgs, H, W, stride, pitch, thr, cand_keys, cap,
+    hipLaunchKernelGGL(detect_kernel<true>, grid, dim3(256), 0, s, imgs, H, W, stride, pitch, thr, eig, cand_keys, cap,
                        cand_count, kw, blur);
 }
 
