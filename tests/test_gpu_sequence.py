@@ -2,6 +2,8 @@
 match / PnP / shared map / local BA through libyavo (ya_vo_amd.sequence.SequenceFrontend) against the same loop
 over the CPU oracle (tests/sequence_chain.py): trajectories and refined landmarks bit for bit (the metric's "RMSE
 vs CPU ref" is 0), and the trajectory follows the synthetic ground truth."""
+import os
+
 import numpy as np
 import pytest
 
@@ -40,3 +42,32 @@ def test_sequence_matches_oracle(ctx, oracle, offsets, n, chunk, tmp_path):
     back = yio.read_kitti_poses(path)
     np.testing.assert_allclose(back[:, :, 3], traj[:, 4:], atol=1e-9)
     fe.close()
+
+
+def _threads():
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(omp))) if omp.isdigit() and int(omp) > 0 else min(n, 16)
+
+
+@pytest.mark.timeout(900)
+def test_sequence_200_frames_matches_oracle(ctx, oracle, offsets):
+    """BASELINE configs[2] at its stated size: the first 200 frames of a sequence in chunks of 20 (10 BA windows of
+    22 poses), trajectory and BA logs bit-identical to the oracle loop (RMSE vs CPU ref = 0), and within 2 cm of the
+    synthetic ground truth."""
+    import torch
+    n, chunk = 200, 20
+    frames = synth_sequence(71, n, stereo=True)
+    fe = SequenceFrontend(ctx, chunk, scene.K_KITTI, T_RIGHT)
+    d = torch.from_numpy(frames.reshape(2 * n, *frames.shape[2:])).to("cuda:0")
+    for c in range(n // chunk):
+        fe.process_chunk(d[2 * c * chunk:2 * (c + 1) * chunk])
+    traj = fe.trajectory()
+    ba_log = list(fe.ba_log)
+    fe.close()
+    del d
+    ref, _, log = oracle_sequence(oracle, frames, chunk, scene.K_KITTI, T_RIGHT, offsets, threads=_threads())
+    assert [x[:2] for x in ba_log] == [x[:2] for x in log]
+    np.testing.assert_array_equal(np.array([x[2:] for x in ba_log]), np.array([x[2:] for x in log]))
+    np.testing.assert_array_equal(traj, ref)
+    assert rmse_translation(traj, ground_truth(n, scene.K_KITTI)) < 0.02
