@@ -590,38 +590,48 @@ __device__ __forceinline__ bool brief_boundary(int row, int col, int H, int W) {
 }
 
 // Compacts points 0..K-1 (rc_at(i) -> int2 {row, col}) to those inside checkBoundry, keeping order;
-// kp_src[slot] = {row, col, id = input index, 0}.  Handles K <= 4 * TK_NT.
-template <class RcAt>
+// kp_src[slot] = {row, col, id = input index, 0}.  Chunks of 4 * NT points, 4 consecutive per thread.
+template <int NT, class RcAt>
 __device__ void boundary_compact(RcAt rc_at, int K, int H, int W, int32_t* kp_src, int32_t* kp_count, int* s_tmp) {
     const int tid = threadIdx.x;
-    int flags[4];
-    int2 rcs[4];
-    int cnt = 0;
+    int base = 0;
+    for (int c0 = 0; c0 < K; c0 += 4 * NT) {
+        int flags[4];
+        int2 rcs[4];
+        int cnt = 0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int i = tid * 4 + u;
-        flags[u] = 0;
-        rcs[u] = make_int2(0, 0);
-        if (i < K) {
-            rcs[u] = rc_at(i);
-            flags[u] = brief_boundary(rcs[u].x, rcs[u].y, H, W) ? 1 : 0;
+        for (int u = 0; u < 4; ++u) {
+            const int i = c0 + tid * 4 + u;
+            flags[u] = 0;
+            rcs[u] = make_int2(0, 0);
+            if (i < K) {
+                rcs[u] = rc_at(i);
+                flags[u] = brief_boundary(rcs[u].x, rcs[u].y, H, W) ? 1 : 0;
+            }
+            cnt += flags[u];
         }
-        cnt += flags[u];
-    }
-    int total = 0;
-    int off = block_excl_scan<TK_NT>(cnt, s_tmp, &total);
+        int total = 0;
+        int off = base + block_excl_scan<NT>(cnt, s_tmp, &total);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int i = tid * 4 + u;
-        if (flags[u]) {
-            reinterpret_cast<int4*>(kp_src)[off] = make_int4(rcs[u].x, rcs[u].y, i, 0);
-            off++;
+        for (int u = 0; u < 4; ++u) {
+            const int i = c0 + tid * 4 + u;
+            if (flags[u]) {
+                reinterpret_cast<int4*>(kp_src)[off] = make_int4(rcs[u].x, rcs[u].y, i, 0);
+                off++;
+            }
         }
+        base += total;
     }
-    if (tid == 0) *kp_count = total;
+    if (tid == 0) *kp_count = base;
 }
 
-__global__ __launch_bounds__(TK_NT) void topk_kernel(const uint64_t* __restrict__ cand_keys, int64_t cap,
+// top-K per image: one workgroup of NT threads per image.  (256-thread workgroups, meant to fit beside the side-stream
+// pose LM, measured the same 0.44-0.48 ms in the step: the LM's two workgroups per CU hold the whole register file,
+// so nothing dispatches there until they retire.)
+constexpr int TK_SEL_NT = 1024;
+static_assert(TK_SEL_NT >= 256 && TK_SEL_NT % 64 == 0, "the radix-select histogram scan uses the first 256 threads");
+template <int NT>
+__global__ __launch_bounds__(NT) void topk_kernel(const uint64_t* __restrict__ cand_keys, int64_t cap,
                                                      uint32_t* __restrict__ cand_count, uint32_t* __restrict__ cand_seen,
                                                      int H, int W, int max_kp, int keep, int32_t* __restrict__ det_rc,
                                                      float* __restrict__ det_resp, int32_t* __restrict__ det_count,
@@ -661,7 +671,7 @@ __global__ __launch_bounds__(TK_NT) void topk_kernel(const uint64_t* __restrict_
             const int krem = s_krem;
             if (tid < 256) s_hist[tid] = 0;
             __syncthreads();
-            for (int i = tid; i < C; i += TK_NT) {
+            for (int i = tid; i < C; i += NT) {
                 const uint64_t k = keys[i];
                 if ((k & pm) == pp) atomicAdd(&s_hist[(k >> shift) & 255u], 1u);
             }
@@ -695,7 +705,7 @@ __global__ __launch_bounds__(TK_NT) void topk_kernel(const uint64_t* __restrict_
     // collect the K selected keys into LDS (any order), pad to a power of two, bitonic sort
     if (tid == 0) s_n = 0;
     __syncthreads();
-    for (int i = tid; i < C; i += TK_NT) {
+    for (int i = tid; i < C; i += NT) {
         const uint64_t k = keys[i];
         if ((k & sel_mask) <= sel_prefix) {
             const int p = atomicAdd(&s_n, 1);
@@ -705,11 +715,11 @@ __global__ __launch_bounds__(TK_NT) void topk_kernel(const uint64_t* __restrict_
     __syncthreads();
     int P2 = 1;
     while (P2 < K) P2 <<= 1;
-    for (int i = K + tid; i < P2; i += TK_NT) s_keys[i] = ~0ull;
+    for (int i = K + tid; i < P2; i += NT) s_keys[i] = ~0ull;
     __syncthreads();
     for (int size = 2; size <= P2; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = tid; t < (P2 >> 1); t += TK_NT) {
+            for (int t = tid; t < (P2 >> 1); t += NT) {
                 const int i = 2 * t - (t & (stride - 1));
                 const int j = i + stride;
                 const bool up = ((i & size) == 0);
@@ -719,7 +729,7 @@ __global__ __launch_bounds__(TK_NT) void topk_kernel(const uint64_t* __restrict_
             __syncthreads();
         }
     }
-    for (int i = tid; i < K; i += TK_NT) {
+    for (int i = tid; i < K; i += NT) {
         const uint64_t k = s_keys[i];
         const uint32_t idx = (uint32_t)k;
         const int row = (int)(idx / (uint32_t)W), col = (int)(idx - (uint32_t)row * (uint32_t)W);
@@ -734,7 +744,7 @@ __global__ __launch_bounds__(TK_NT) void topk_kernel(const uint64_t* __restrict_
         const uint32_t row = idx / Wu;
         return make_int2((int)row, (int)(idx - row * Wu));
     };
-    boundary_compact(rc_from_lds, K, H, W, kp_src + (int64_t)img * max_kp * 4, kp_count + img, s_tmp);
+    boundary_compact<NT>(rc_from_lds, K, H, W, kp_src + (int64_t)img * max_kp * 4, kp_count + img, s_tmp);
 }
 
 __global__ __launch_bounds__(TK_NT) void kp_boundary_kernel(const int32_t* __restrict__ det_rc,
@@ -747,14 +757,14 @@ __global__ __launch_bounds__(TK_NT) void kp_boundary_kernel(const int32_t* __res
     if (K > max_kp) K = max_kp;
     const int32_t* rc = det_rc + (int64_t)img * max_kp * 2;
     auto rc_from_global = [&](int i) -> int2 { return make_int2(rc[2 * i], rc[2 * i + 1]); };
-    boundary_compact(rc_from_global, K, H, W, kp_src + (int64_t)img * max_kp * 4, kp_count + img, s_tmp);
+    boundary_compact<TK_NT>(rc_from_global, K, H, W, kp_src + (int64_t)img * max_kp * 4, kp_count + img, s_tmp);
 }
 
 void launch_topk(const uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, uint32_t* cand_seen, int n_images,
                  int H, int W, int max_kp, int keep, int32_t* det_rc, float* det_resp, int32_t* det_count, int32_t* kp_src,
                  int32_t* kp_count, hipStream_t s) {
-    hipLaunchKernelGGL(topk_kernel, dim3(n_images), dim3(TK_NT), 0, s, cand_keys, cap, cand_count, cand_seen, H, W,
-                       max_kp, keep, det_rc, det_resp, det_count, kp_src, kp_count);
+    hipLaunchKernelGGL(topk_kernel<TK_SEL_NT>, dim3(n_images), dim3(TK_SEL_NT), 0, s, cand_keys, cap, cand_count,
+                       cand_seen, H, W, max_kp, keep, det_rc, det_resp, det_count, kp_src, kp_count);
 }
 
 void launch_kp_boundary(const int32_t* det_rc, const int32_t* det_count, int n_images, int H, int W, int max_kp,
