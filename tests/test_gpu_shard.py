@@ -3,8 +3,9 @@ a fresh child process running ya_vo_amd.sharding.FrameShard on its chunk with th
 shared-map blocks (gloo here: both ranks share the test box's one GPU; the bench uses RCCL) and place them with the
 serial anchor chain.  The result must be the 1-rank run of the same frames: every relative pose bit for bit (the
 halo gives rank 1's first temporal pair the same keypoints the 1-rank run's carry slot does) and the placed map
-(keyframe poses, landmark ids and world points) within 1e-12 -- the chunked anchor chain A_1 * L_k re-associates the
-1-rank left fold rel_0 * ... * rel_k.  Reference: the serial chaining of
+(keyframe poses, landmark ids and world points) within 1e-12 absolute + 1e-13 relative -- the chunked anchor chain
+A_1 * L_k re-associates the 1-rank left fold rel_0 * ... * rel_k.  The last case is BASELINE
+configs[3]'s length (KITTI sequence 00: 4541 frames) on two ranks.  Reference: the serial chaining of
 src/LoopHandler.cc:139,156."""
 import os
 import socket
@@ -51,7 +52,9 @@ def _map(placed):
     return m
 
 
-@pytest.mark.parametrize("B,kf_every", [(4, 1), (6, 2)])
+# (2270, 4): BASELINE configs[3]'s length -- KITTI sequence 00 has 4541 frames = the halo frame 0 + 2 x 2270
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("B,kf_every", [(4, 1), (6, 2), (2270, 4)])
 def test_two_rank_shards_equal_one_rank(ctx, tmp_path, B, kf_every):
     world, seed = 2, 91
     port = _free_port()
@@ -60,7 +63,7 @@ def test_two_rank_shards_equal_one_rank(ctx, tmp_path, B, kf_every):
                                str(B), str(kf_every), str(seed), str(tmp_path / f"rank{r}.npz")], env=env)
              for r in range(world)]
     for p in procs:
-        assert p.wait(timeout=110) == 0
+        assert p.wait(timeout=110 if B < 100 else 600) == 0
     res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     ref_poses, ref_placed = _one_rank(ctx, world * B, kf_every, seed)
 
@@ -72,11 +75,13 @@ def test_two_rank_shards_equal_one_rank(ctx, tmp_path, B, kf_every):
     got, ref = _map(res[0]["placed"]), _map(ref_placed)
     assert sorted(got.frames) == sorted(ref.frames) == list(range(kf_every, world * B + 1, kf_every))
     assert sorted(got.landmarks) == sorted(ref.landmarks)
+    # the re-association error grows with the chain: 1e-12 absolute on short sequences, plus 1e-13 relative at the
+    # full sequence length (4540 chained frames, ~920 m of synthetic trajectory)
     for g in ref.frames:
-        np.testing.assert_allclose(got.frames[g], ref.frames[g], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(got.frames[g], ref.frames[g], rtol=1e-13, atol=1e-12)
     gl = np.array([got.landmarks[i] for i in sorted(ref.landmarks)])
     rl = np.array([ref.landmarks[i] for i in sorted(ref.landmarks)])
-    np.testing.assert_allclose(gl, rl, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(gl, rl, rtol=1e-13, atol=1e-12)
     # the rank boundary carries the sequence's real motion (the synthetic camera moves 0.21 m per frame), not the
     # identity an empty or stale predecessor would give
     assert np.linalg.norm(res[1]["poses"][0][4:]) > 0.1
