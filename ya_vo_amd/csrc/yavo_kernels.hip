@@ -242,6 +242,26 @@ __device__ unsigned long long g_det_prof[kDetProfSlots][6];
 #define DP_MARK(k) do {} while (0)
 #define DP_STORE() do {} while (0)
 #endif
+#ifdef YAVO_LM_PROFILE
+constexpr int kBriefProfSlots = 16384;
+__device__ unsigned long long g_brief_prof[kBriefProfSlots][6];
+#define BP_DECL unsigned long long bp_acc[4] = {0, 0, 0, 0}; unsigned long long bp_t = __builtin_readcyclecounter(); \
+    const unsigned long long bp_rt0 = __builtin_amdgcn_s_memrealtime();
+#define BP_MARK(k) do { const unsigned long long t_ = __builtin_readcyclecounter(); bp_acc[k] += t_ - bp_t; bp_t = t_; } while (0)
+#define BP_STORE() do { \
+        if (threadIdx.x == 0 && blockIdx.x < kBriefProfSlots) { \
+            g_brief_prof[blockIdx.x][0] = bp_acc[0] + bp_acc[1]; g_brief_prof[blockIdx.x][1] = bp_acc[2]; \
+            g_brief_prof[blockIdx.x][2] = bp_rt0; \
+            g_brief_prof[blockIdx.x][3] = __builtin_amdgcn_s_memrealtime(); \
+            g_brief_prof[blockIdx.x][4] = (unsigned long long)__builtin_amdgcn_s_getreg(0xF804); \
+            g_brief_prof[blockIdx.x][5] = (unsigned long long)__builtin_amdgcn_s_getreg(0xF814); \
+        } \
+    } while (0)
+#else
+#define BP_DECL
+#define BP_MARK(k) do {} while (0)
+#define BP_STORE() do {} while (0)
+#endif
 constexpr int FT_W = kFastTileW;        // 64 output columns per tile (one wave-row)
 constexpr int FT_H = kFastTileH;        // 56 output rows per tile
 constexpr int FT_R = 4;                 // halo: blur radius 4 (ring radius 3, Sobel + 3x3 window radius 2)
@@ -777,6 +797,13 @@ void launch_kp_boundary(const int32_t* det_rc, const int32_t* det_count, int n_i
 // BRIEF
 // ------------------------------------------------------------------------------------------------
 
+// v_writelane_b32: lane LANE of `dst` takes the wave-uniform `val` (no clang builtin for it in this toolchain)
+template <int LANE>
+__device__ __forceinline__ uint32_t writelane(uint32_t dst, uint32_t val) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(val), "i"(LANE));
+    return dst;
+}
+
 // v[idx] for a small register array without dynamic indexing (keeps it out of scratch).
 template <int N>
 __device__ __forceinline__ uint32_t reg_select(const uint32_t (&v)[N], int idx) {
@@ -800,7 +827,10 @@ constexpr int BR_BAND = 32;
 constexpr int BR_ROWS = BR_BAND + 17;  // rows r0-8 .. r0+40 (the last one for the wrap of col + 8 == W)
 // 16 waves share one staged band: the ~61 KB band limits a CU to 2 workgroups, so the workgroup is as wide as
 // the 64-VGPR budget of 8 waves per SIMD allows
-constexpr int BR_NT = 1024;
+#ifndef YAVO_BR_NT
+#define YAVO_BR_NT 1024
+#endif
+constexpr int BR_NT = YAVO_BR_NT;
 constexpr int BR_NW = BR_NT / 64;
 
 __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict__ blur, int H, int W,
@@ -809,8 +839,10 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
                                                     const int32_t* __restrict__ kp_count, int max_kp,
                                                     yv_keypoint* __restrict__ keypoints, Desc* __restrict__ desc) {
     extern __shared__ uint8_t s_band[];  // BR_ROWS * brief_lds_stride(W) bytes
-    __shared__ int16_t s_list[kMaxKp];
+    // this band's keypoints, packed (index << 16) | (col << 5) | (row - r0): index < 4096, col < 2048, 32-row band
+    __shared__ uint32_t s_list[kMaxKp];
     __shared__ int s_n;
+    BP_DECL
     // 1-D grid, XCD-aware: neighbouring bands of an image (17 shared rows) stay in one XCD's L2
     const int nbands = (H + BR_BAND - 1) / BR_BAND;
     const int lb = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
@@ -820,61 +852,99 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
     const int n = kp_count[img];
     const int4* src = reinterpret_cast<const int4*>(kp_src) + (int64_t)img * max_kp;
     if (tid == 0) s_n = 0;
-    __syncthreads();
-    // 1. this band's keypoints (any order: each keypoint's outputs go to its own index); all row loads are
-    // issued before the first use
-    const int nscan = (n + BR_NT - 1) / BR_NT;
-    int next_row = tid < n ? src[tid].x : -1;  // software-pipelined: the next row load is in flight
-    for (int u = 0; u < nscan; ++u) {
+    // Every global load of the workgroup is issued up front, in this order: the keypoint list (n <= 4096 = 4 per
+    // thread), then the band (<= 4 16-B words per thread).  vmcnt retires loads in order, so the list scan below waits
+    // only for the list while the band's loads stay in flight behind it; the band goes to LDS after the scan.
+    int2 kq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
         const int i = u * BR_NT + tid;
-        const int row = next_row;
-        const int inext = i + BR_NT;
-        next_row = inext < n ? src[inext].x : -1;
-        const bool mine = i < n && row >= r0 && row < r0 + BR_BAND;
-        const uint64_t bal = __ballot(mine);
-        int wbase = 0;
-        if (lane == 0 && bal) wbase = atomicAdd(&s_n, (int)__popcll(bal));
-        wbase = __shfl(wbase, 0, 64);
-        if (mine) s_list[wbase + (int)__popcll(bal & ((1ull << lane) - 1))] = (int16_t)i;
+        kq[u] = make_int2(-1, 0);
+        if (i < n) {
+            const int4 k4 = src[i];
+            kq[u] = make_int2(k4.x, k4.y);
+        }
     }
-    __syncthreads();
-    const int nb = s_n;
-    if (nb == 0) return;
-    // 2. stage the band: rows rb .. rb + BR_ROWS - 1 (rb = r0 - 8) of the pitched blurred image as 16-B words,
-    // LS bytes per row (LS <= the pitch: inside the row); column W of row r is patched with pixel (r + 1, 0) (0 past
-    // the image), rows outside [0, H) are zero.  Each thread's loads are all in flight before the LDS writes.
+    // band: rows rb .. rb + BR_ROWS - 1 (rb = r0 - 8) of the pitched blurred image as 16-B words, LS bytes per row
+    // (LS <= the pitch: inside the row); column W of row r is patched with pixel (r + 1, 0) (0 past the image), rows
+    // outside [0, H) are zero
     const int bp = blur_pitch(W), LS = brief_lds_stride(W);
     const uint8_t* b = blur + (int64_t)img * H * bp;
     const int rb = r0 - 8;
     const int wpr = LS >> 4;              // 16-B words per LDS row
     const int nw = BR_ROWS * wpr;
     const int kw_fix = W >> 4, sh_fix = 8 * (W & 3), dw_fix = (W >> 2) & 3;
-    uint4* s4 = reinterpret_cast<uint4*>(s_band);
-    for (int k0 = tid; k0 < nw; k0 += 4 * BR_NT) {
-        uint4 v[4];
+    uint4 v[4];
+    uint32_t nx[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int k = k0 + u * BR_NT;
-            const int j = k / wpr, q = k - j * wpr;
-            const int r = rb + j;
-            v[u] = make_uint4(0, 0, 0, 0);
-            if (k < nw && r >= 0 && r < H) {
-                v[u] = reinterpret_cast<const uint4*>(b + (int64_t)r * bp)[q];
-                if (q == kw_fix) {  // the word holding column W: the next row's first pixel (0 past the image)
-                    const uint32_t nx = r + 1 < H ? (uint32_t)b[(int64_t)(r + 1) * bp] : 0u;
-                    const uint32_t m = ~(0xFFu << sh_fix);
-                    if (dw_fix == 0) v[u].x = (v[u].x & m) | (nx << sh_fix);
-                    else if (dw_fix == 1) v[u].y = (v[u].y & m) | (nx << sh_fix);
-                    else if (dw_fix == 2) v[u].z = (v[u].z & m) | (nx << sh_fix);
-                    else v[u].w = (v[u].w & m) | (nx << sh_fix);
-                }
+    for (int u = 0; u < 4; ++u) {
+        const int k = tid + u * BR_NT;
+        const int j = k / wpr, q = k - j * wpr;
+        const int r = rb + j;
+        v[u] = make_uint4(0, 0, 0, 0);
+        nx[u] = 0u;
+        if (k < nw && r >= 0 && r < H) {
+            v[u] = reinterpret_cast<const uint4*>(b + (int64_t)r * bp)[q];
+            if (q == kw_fix && r + 1 < H) nx[u] = (uint32_t)b[(int64_t)(r + 1) * bp];
+        }
+    }
+    __syncthreads();  // s_n = 0
+    // 1. this band's keypoints (any order: each keypoint's outputs go to its own index)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = u * BR_NT + tid;
+        const int row = kq[u].x;
+        const bool mine = i < n && row >= r0 && row < r0 + BR_BAND;
+        const uint64_t bal = __ballot(mine);
+        int wbase = 0;
+        if (lane == 0 && bal) wbase = atomicAdd(&s_n, (int)__popcll(bal));
+        wbase = __shfl(wbase, 0, 64);
+        if (mine)
+            s_list[wbase + (int)__popcll(bal & ((1ull << lane) - 1))] =
+                ((uint32_t)i << 16) | ((uint32_t)kq[u].y << 5) | (uint32_t)(row - r0);
+    }
+    // 2. the band to LDS (the word holding column W takes the next row's first pixel)
+    uint4* s4 = reinterpret_cast<uint4*>(s_band);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int k = tid + u * BR_NT;
+        if (k < nw) {
+            uint4 w = v[u];
+            if (k - (k / wpr) * wpr == kw_fix) {
+                const uint32_t m = ~(0xFFu << sh_fix);
+                if (dw_fix == 0) w.x = (w.x & m) | (nx[u] << sh_fix);
+                else if (dw_fix == 1) w.y = (w.y & m) | (nx[u] << sh_fix);
+                else if (dw_fix == 2) w.z = (w.z & m) | (nx[u] << sh_fix);
+                else w.w = (w.w & m) | (nx[u] << sh_fix);
+            }
+            s4[k] = w;
+        }
+    }
+    // wide images (W > 1320): the rest of the band, word by word
+    for (int k = tid + 4 * BR_NT; k < nw; k += BR_NT) {
+        const int j = k / wpr, q = k - j * wpr;
+        const int r = rb + j;
+        uint4 w = make_uint4(0, 0, 0, 0);
+        if (r >= 0 && r < H) {
+            w = reinterpret_cast<const uint4*>(b + (int64_t)r * bp)[q];
+            if (q == kw_fix) {
+                const uint32_t nxx = r + 1 < H ? (uint32_t)b[(int64_t)(r + 1) * bp] : 0u;
+                const uint32_t m = ~(0xFFu << sh_fix);
+                if (dw_fix == 0) w.x = (w.x & m) | (nxx << sh_fix);
+                else if (dw_fix == 1) w.y = (w.y & m) | (nxx << sh_fix);
+                else if (dw_fix == 2) w.z = (w.z & m) | (nxx << sh_fix);
+                else w.w = (w.w & m) | (nxx << sh_fix);
             }
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (k0 + u * BR_NT < nw) s4[k0 + u * BR_NT] = v[u];
+        s4[k] = w;
     }
     __syncthreads();
+    const int nb = s_n;
+    BP_MARK(1);
+    if (nb == 0) {
+        BP_STORE();
+        return;
+    }
     // 3. descriptors.  Each lane's 8 sample offsets as LDS offsets dr * LS + dc.
     int ol[4][2];
 #pragma unroll
@@ -887,33 +957,51 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
     }
     uint32_t* rec_base = reinterpret_cast<uint32_t*>(keypoints + (int64_t)img * max_kp);
     Desc* d_base = desc + (int64_t)img * max_kp;
-    auto emit = [&](int i, const int4 kp, const uint64_t (&w)[4]) {
-        // descriptor (32 B) and the 48-B KeyPoint record {x, y, id, matched=0, featVec[32], pad 0}
-        uint32_t bd[9];
+    // The outputs of one keypoint: its descriptor (8 dwords, lanes 0-7) and its 48-B KeyPoint record {x, y, id,
+    // matched = 0, featVec[32], 3 pad bytes = 0} (12 dwords, lanes 0-11).  Every value is wave-uniform (ballot
+    // results, the keypoint's fields), so the dwords are formed by the scalar unit and placed into the storing lanes
+    // with v_writelane -- one VALU op per stored dword (a per-lane select over the 9 candidates costs ~18).
+    auto emit = [&](int i, int row, int col, int id, const uint64_t (&w)[4]) {
+        uint32_t bd[8];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) { bd[2 * t] = (uint32_t)w[t]; bd[2 * t + 1] = (uint32_t)(w[t] >> 32); }
-        bd[8] = 0;
-        if (lane < 8) d_base[i].w[lane] = reg_select(bd, lane);
-        if (lane < 12) {
-            uint32_t v;
-            if (lane == 0) v = (uint32_t)kp.x;
-            else if (lane == 1) v = (uint32_t)kp.y;
-            else if (lane == 2) v = (uint32_t)kp.z;
-            else {
-                const int m = lane - 3;  // record dword 3+m = featVec bytes shifted by one (matched byte first)
-                const uint32_t hi = reg_select(bd, m);
-                const uint32_t lo = m > 0 ? reg_select(bd, m - 1) : 0u;
-                v = (hi << 8) | (lo >> 24);
-            }
-            rec_base[(int64_t)i * 12 + lane] = v;
+        for (int t = 0; t < 4; ++t) {
+            bd[2 * t] = __builtin_amdgcn_readfirstlane((uint32_t)w[t]);
+            bd[2 * t + 1] = __builtin_amdgcn_readfirstlane((uint32_t)(w[t] >> 32));
         }
+        uint32_t dv = 0u, rv = 0u;
+        dv = writelane<0>(dv, bd[0]); dv = writelane<1>(dv, bd[1]); dv = writelane<2>(dv, bd[2]);
+        dv = writelane<3>(dv, bd[3]); dv = writelane<4>(dv, bd[4]); dv = writelane<5>(dv, bd[5]);
+        dv = writelane<6>(dv, bd[6]); dv = writelane<7>(dv, bd[7]);
+        // record dword 3+m = featVec bytes shifted by one (the matched byte first)
+        auto rec = [&](int m) -> uint32_t {
+            const uint32_t hi = m < 8 ? bd[m] : 0u, lo = m > 0 ? bd[m - 1] : 0u;
+            return __builtin_amdgcn_readfirstlane((hi << 8) | (lo >> 24));
+        };
+        rv = writelane<0>(rv, (uint32_t)row); rv = writelane<1>(rv, (uint32_t)col); rv = writelane<2>(rv, (uint32_t)id);
+        rv = writelane<3>(rv, rec(0)); rv = writelane<4>(rv, rec(1)); rv = writelane<5>(rv, rec(2));
+        rv = writelane<6>(rv, rec(3)); rv = writelane<7>(rv, rec(4)); rv = writelane<8>(rv, rec(5));
+        rv = writelane<9>(rv, rec(6)); rv = writelane<10>(rv, rec(7)); rv = writelane<11>(rv, rec(8));
+        if (lane < 8) d_base[i].w[lane] = dv;
+        if (lane < 12) rec_base[(int64_t)i * 12 + lane] = rv;
     };
-    // two keypoints per iteration: 16 LDS reads per lane in flight
+    // two keypoints per iteration: 16 LDS reads per lane in flight.  The record's id (the keypoint's index before
+    // checkBoundry, kp_src[i].z) is the only field not in the packed list: lane 2, which stores it, loads it one
+    // iteration ahead
+    auto id_of = [&](int k) -> int {
+        if (lane != 2 || k >= nb) return 0;
+        return src[s_list[k] >> 16].z;
+    };
+    int ida_next = id_of(wave), idb_next = id_of(wave + BR_NW);
     for (int k = wave; k < nb; k += 2 * BR_NW) {
         const bool two = k + BR_NW < nb;
-        const int ia = s_list[k], ib = two ? s_list[k + BR_NW] : ia;
-        const int4 kpa = src[ia], kpb = src[ib];
-        const int la = (kpa.x - rb) * LS + kpa.y, lbb = (kpb.x - rb) * LS + kpb.y;
+        const uint32_t ea = s_list[k], eb = two ? s_list[k + BR_NW] : ea;
+        const int ida = __builtin_amdgcn_readlane(ida_next, 2), idb = __builtin_amdgcn_readlane(idb_next, 2);
+        ida_next = id_of(k + 2 * BR_NW);
+        idb_next = id_of(k + 3 * BR_NW);
+        const int ia = (int)(ea >> 16), ib = (int)(eb >> 16);
+        const int rowa = r0 + (int)(ea & 31u), cola = (int)((ea >> 5) & 2047u);
+        const int rowb = r0 + (int)(eb & 31u), colb = (int)((eb >> 5) & 2047u);
+        const int la = (rowa - rb) * LS + cola, lbb = (rowb - rb) * LS + colb;
         uint64_t wa[4], wb[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -922,9 +1010,11 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
             wa[t] = __ballot(pa1 > pa2);
             wb[t] = __ballot(pb1 > pb2);
         }
-        emit(ia, kpa, wa);
-        if (two) emit(ib, kpb, wb);
+        emit(ia, __builtin_amdgcn_readfirstlane(rowa), __builtin_amdgcn_readfirstlane(cola), ida, wa);
+        if (two) emit(ib, __builtin_amdgcn_readfirstlane(rowb), __builtin_amdgcn_readfirstlane(colb), idb, wb);
     }
+    BP_MARK(2);
+    BP_STORE();
 }
 
 void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t* offsets, const int32_t* kp_src,
@@ -1349,6 +1439,10 @@ void launch_filter_records(const yv_match* in, int n, int thr, yv_match* out, in
 }  // namespace yavo
 
 #ifdef YAVO_LM_PROFILE
+extern "C" int yv_debug_brief_prof(unsigned long long* out /* [16384][6] */) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(yavo::g_brief_prof), sizeof(unsigned long long) * 16384 * 6) ==
+                   hipSuccess ? 0 : -2;
+}
 extern "C" int yv_debug_det_prof(unsigned long long* out /* [131072][6] */) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(yavo::g_det_prof), sizeof(unsigned long long) * 131072 * 6) ==
                    hipSuccess ? 0 : -2;
