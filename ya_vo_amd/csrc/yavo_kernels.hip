@@ -356,11 +356,12 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
     // phase 1: the reference's pretest on ring pixels 0, 7 and (4 | 12) (src/FastDetector.cc:304-317) for
     // every pixel; each lane keeps a mask of its passing rows and the survivors are compacted into s_pre
     // once per wave (one scan, one LDS atomic)
-    const int tx = lane, ty = wave;
+    const int tx = lane;
+    const int ty = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the row bookkeeping below stays scalar
     const int c = c0 + tx;
     constexpr int kRowIters = FT_H / 4;
     // pixel (r, c) is tested iff 4 <= r < H - 4 and 4 <= c < W - 4: rows are wave-uniform, so the row test is one
-    // mask over the row iterations and the column test one compare
+    // scalar mask over the row iterations and the column test one compare
     uint32_t row_ok = 0;
 #pragma unroll
     for (int u = 0; u < kRowIters; ++u) row_ok |= (uint32_t)((unsigned)(r0 + ty + 4 * u - 4) < (unsigned)(H - 8)) << u;
@@ -371,18 +372,24 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
     // right and top of the ring: a necessary condition, ~7% survivors against the pretest's ~18%) and phase 2
     // evaluates run12 exactly; the corner set is the reference's.
     // "similar" is the sign bit of sad(c, p) - thr, so the filter holds iff the sign bit of d0 | d4 | d8 | d11 is
-    // clear; the sign bits are shifted into nmask (bit u = filtered out) with v_alignbit
+    // clear; the sign bits are shifted into nmask (bit u = filtered out) with v_alignbit.  Every LDS read is one base
+    // register (the 7 x 7 window's top-left of row iteration 0) plus a constant non-negative offset, so the
+    // addresses cost no VALU.
     uint32_t nmask = 0;
+    const uint8_t* wbase = &tile[(ty + FT_R - 3) * FT_LW + tx + FT_R - 3];
 #pragma unroll
     for (int u = kRowIters - 1; u >= 0; --u) {
-        const uint8_t* t0 = &tile[(ty + 4 * u + FT_R) * FT_LW + tx + FT_R];
-        const uint32_t cent = t0[0];
-        auto d = [&](int k) { return __builtin_amdgcn_sad_u8(cent, (uint32_t)t0[ring_dr[k] * FT_LW + ring_dc[k]], neg_thr); };
+        const uint8_t* t0 = wbase + 4 * u * FT_LW;
+        const uint32_t cent = t0[3 * FT_LW + 3];
+        auto d = [&](int k) {
+            return __builtin_amdgcn_sad_u8(cent, (uint32_t)t0[(ring_dr[k] + 3) * FT_LW + ring_dc[k] + 3], neg_thr);
+        };
         const uint32_t v = (d(0) | d(4)) | (d(8) | d(11));
         nmask = __builtin_amdgcn_alignbit(nmask, v, 31);  // (nmask << 1) | (v >> 31)
     }
-    const uint32_t pmask = (unsigned)(c - 4) < (unsigned)(W - 8) ? (~nmask & row_ok) : 0u;
+    uint32_t pmask = (unsigned)(c - 4) < (unsigned)(W - 8) ? (~nmask & row_ok) : 0u;
     {
+        // survivors (~1 per lane) compacted into s_pre: a loop over the set bits, not one masked store per row
         const int cnt = __popc(pmask);
         const int incl = wave_incl_scan(cnt);
         const int total = __shfl(incl, 63, 64);
@@ -390,9 +397,11 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         if (lane == 0 && total > 0) base = atomicAdd(&s_npre, (uint32_t)total);
         base = __shfl(base, 0, 64);
         uint32_t off = base + (uint32_t)(incl - cnt);
-#pragma unroll
-        for (int u = 0; u < kRowIters; ++u)
-            if (pmask & (1u << u)) s_pre[off++] = (uint16_t)((ty + 4 * u) * FT_W + tx);
+        while (pmask) {
+            const int u = __builtin_ctz(pmask);
+            s_pre[off++] = (uint16_t)((ty + 4 * u) * FT_W + tx);
+            pmask &= pmask - 1;
+        }
     }
     __syncthreads();
     DP_MARK(1);
@@ -405,14 +414,17 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         int pos = 0;
         if (i < npre) {
             pos = s_pre[i];
-            const uint8_t* t0 = &tile[((pos >> 6) + FT_R) * FT_LW + (pos & 63) + FT_R];
-            const uint32_t cent = t0[0];
+            // the 7 x 7 window's top-left: every ring read is this base plus a constant non-negative offset
+            const uint8_t* t0 = &tile[((pos >> 6) + FT_R - 3) * FT_LW + (pos & 63) + FT_R - 3];
+            const uint32_t cent = t0[3 * FT_LW + 3];
             // similar bits in reverse ring order (bit 15 - k for ring pixel k), one v_alignbit each; a run of
             // 12 consecutive bits without wrap is the same test in either order
             uint32_t sim = 0;
 #pragma unroll
             for (int k = 0; k < 16; ++k)
-                sim = __builtin_amdgcn_alignbit(sim, __builtin_amdgcn_sad_u8(cent, (uint32_t)t0[ring_dr[k] * FT_LW + ring_dc[k]], neg_thr), 31);
+                sim = __builtin_amdgcn_alignbit(
+                    sim, __builtin_amdgcn_sad_u8(cent, (uint32_t)t0[(ring_dr[k] + 3) * FT_LW + ring_dc[k] + 3], neg_thr),
+                    31);
             const uint32_t mask = ~sim & 0xFFFFu;  // "different" ring pixels
             const uint32_t a2 = mask & (mask >> 1);
             const uint32_t a4 = a2 & (a2 >> 2);
@@ -471,14 +483,15 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         for (uint32_t i = tid; i < n; i += 256) {
             const int pos = s_pos[i];
             const int prr = pos >> 6, ptx = pos & 63;
-            const uint8_t* t0 = &tile[(prr + FT_R) * FT_LW + ptx + FT_R];
+            // the 5 x 5 patch's top-left: every read is this base plus a constant non-negative offset
+            const uint8_t* t0 = &tile[(prr + FT_R - 2) * FT_LW + ptx + FT_R - 2];
             // Sobel Ix / Iy (3x3 correlation) at the 3x3 window around the corner, from the 5x5 patch.
             int sxx = 0, sxy = 0, syy = 0;
 #pragma unroll
             for (int ii = -1; ii <= 1; ++ii) {
 #pragma unroll
                 for (int j = -1; j <= 1; ++j) {
-                    const uint8_t* q = t0 + ii * FT_LW + j;
+                    const uint8_t* q = t0 + (ii + 2) * FT_LW + j + 2;
                     const int pmm = q[-FT_LW - 1], pm0 = q[-FT_LW], pmp = q[-FT_LW + 1];
                     const int p0m = q[-1], p0p = q[1];
                     const int ppm = q[FT_LW - 1], pp0 = q[FT_LW], ppp = q[FT_LW + 1];
