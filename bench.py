@@ -33,7 +33,8 @@ MAX_KP = 2000
 T_RIGHT = np.array([0, 0, 0, 1, 0, -0.54, 0], np.float64)  # stereo right camera, KITTI baseline 0.54 m
 METRIC = "frames/sec (detect+describe+match+PnP) on 1241×376 KITTI stereo; RMSE vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-INT8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA peak (MI355X_MICROARCH.md; no sparsity)
+FP4_MFMA_PEAK_TOPS = 10000.0  # dense FP4 MFMA peak (MI355X_MICROARCH.md; no sparsity): the matcher runs on
+# v_mfma_scale_f32_16x16x128_f8f6f4 with FP4 operands (max_kp <= 2048)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-op/s
 
 
@@ -406,8 +407,8 @@ def main():
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                     "algorithmic_bytes_per_launch": int(nbytes[dom]), "launch_ms": round(per_launch_ms[dom], 4)}
-        # every stage against the bound that limits it: VALU lane-ops for detect, int8 MFMA ops
-        # for the matcher (2 * Kq * Kt * 256 per pair), HBM bytes for the rest
+        # every stage against the bound that limits it: VALU lane-ops for detect, FP4 MFMA ops
+        # for the matcher (2 * Kq * Kt * 256 per pair, FP4 MFMA), HBM bytes for the rest
         ops = stage_valu_ops(counts, n_img)
         per_stage = {}
         for st, t_ms in per_launch_ms.items():
@@ -420,8 +421,8 @@ def main():
             elif st == "match":
                 mops = float(np.sum(counts["match"].astype(np.float64) * counts["train"])) * 256 * 2
                 a = mops / (t_ms / 1e3) / 1e12
-                per_stage[st] = {"bound": "mfma_i8", "achieved": round(a, 1), "peak": INT8_MFMA_PEAK_TOPS,
-                                 "unit": "T op/s", "frac": round(a / INT8_MFMA_PEAK_TOPS, 4)}
+                per_stage[st] = {"bound": "mfma_fp4", "achieved": round(a, 1), "peak": FP4_MFMA_PEAK_TOPS,
+                                 "unit": "T op/s", "frac": round(a / FP4_MFMA_PEAK_TOPS, 4)}
             elif st == "track_pose":
                 per_stage[st] = {"bound": "latency", "note": "serial LM per problem (DESIGN.md 4.2)",
                                  "ms": round(t_ms, 4)}

@@ -517,7 +517,7 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
     rc |= record_stage(b, s, run, 3);
     if (b->overlap_mode == 3) rc |= launch_deferred_after(b, s);
     if (b->n_pairs > 0) {
-        yavo::launch_match(b->desc, b->kp_count, b->pairs, b->n_pairs, K, b->match_key, s);
+        yavo::launch_match(b->desc, b->kp_count, b->pairs, b->n_pairs, K, K, b->match_key, s);
         rc |= record_stage(b, s, run, 4);
         yavo::launch_match_finalize(b->match_key, b->keypoints, b->kp_count, b->pairs, b->n_pairs, K, match_thr,
                                     b->matches, b->match_count, b->filtered, b->filt_count, b->match_dj,
@@ -961,7 +961,7 @@ int yv_match_features(yv_ctx* ctx, const yv_keypoint* q, int nq, const yv_keypoi
     ctx->h_pinned[1] = nt;
     YV_HIP(hipMemcpyAsync(b->kp_count, ctx->h_pinned, 2 * sizeof(int32_t), hipMemcpyHostToDevice, s));
     yavo::launch_pack_desc(b->keypoints, b->kp_count, 2, b->max_kp, b->desc, s);
-    yavo::launch_match(b->desc, b->kp_count, b->pairs, 1, b->max_kp, b->match_key, s);
+    yavo::launch_match(b->desc, b->kp_count, b->pairs, 1, b->max_kp, nt, b->match_key, s);
     yavo::launch_match_finalize(b->match_key, b->keypoints, b->kp_count, b->pairs, 1, b->max_kp, 0, b->matches,
                                 b->match_count, b->filtered, b->filt_count, b->match_dj, b->match_lim, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;

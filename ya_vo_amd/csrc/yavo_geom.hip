@@ -1104,14 +1104,17 @@ __global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t*
                                                       int stride, const double* __restrict__ Xall,
                                                       const double* __restrict__ uvall, const double* __restrict__ Kall,
                                                       const double* priors, double* poses,
-                                                      uint8_t* __restrict__ outlier_all, int32_t* __restrict__ inliers) {
+                                                      uint8_t* __restrict__ outlier_all, int32_t* __restrict__ inliers,
+                                                      int n_prob) {
     __shared__ uint8_t s_level[kMaxEdges], s_out[kMaxEdges], s_robust[kMaxEdges];
     __shared__ int16_t s_active[kMaxEdges];
     __shared__ double s_red[NT > 64 ? kLMVals * (NT / 64) : 1];
     __shared__ LMShared S;
     __shared__ int s_tmp[40];
     LMP_DECL
-    const int prob = blockIdx.x;
+    // problems blockIdx.x, blockIdx.x + gridDim.x, ...: a grid smaller than the problem count keeps the LM on fewer
+    // CUs (launch_lm), every problem is solved exactly as with one workgroup each
+    for (int prob = blockIdx.x; prob < n_prob; prob += gridDim.x) {
     const int tid = threadIdx.x;
     const int64_t e0 = counts ? (int64_t)prob * stride : (int64_t)offsets[prob];
     int n = counts ? counts[prob] : (int)(offsets[prob + 1] - e0);
@@ -1306,10 +1309,12 @@ __global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t*
         // before that barrier.
         replay = !changed && (round != 2 || hub == 0);
     }
-    LMP_STORE();
     if (tid < 7) poses[7 * prob + tid] = S.T[tid];
     for (int i = tid; i < n; i += NT) outlier_all[e0 + i] = s_out[i];
     if (tid == 0) inliers[prob] = n - outlierCount;
+    __syncthreads();  // the next problem reinitialises the shared state
+    }
+    LMP_STORE();
 }
 
 // Track edges of the batched frontend: track t = {stereo pair sp, temporal pair tp} with
@@ -1561,12 +1566,23 @@ inline int lm_threads() {
     return nt;
 }
 
+// Workgroups of one LM launch (YAVO_LM_GRID, 0 = one per problem): fewer workgroups loop over the problems, so the
+// LM holds fewer CUs' registers while it runs beside the image kernels.
+inline int lm_grid() {
+    static const int g = [] {
+        const char* e = getenv("YAVO_LM_GRID");
+        return e ? atoi(e) : 0;
+    }();
+    return g;
+}
+
 template <typename... A>
 void launch_lm(int n, hipStream_t s, A... args) {
+    const int g = lm_grid() > 0 && lm_grid() < n ? lm_grid() : n;
     switch (lm_threads()) {
-        case 256: hipLaunchKernelGGL(pose_lm_kernel<256>, dim3(n), dim3(256), 0, s, args...); break;
-        case 128: hipLaunchKernelGGL(pose_lm_kernel<128>, dim3(n), dim3(128), 0, s, args...); break;
-        default: hipLaunchKernelGGL(pose_lm_kernel<64>, dim3(n), dim3(64), 0, s, args...); break;
+        case 256: hipLaunchKernelGGL(pose_lm_kernel<256>, dim3(g), dim3(256), 0, s, args..., n); break;
+        case 128: hipLaunchKernelGGL(pose_lm_kernel<128>, dim3(g), dim3(128), 0, s, args..., n); break;
+        default: hipLaunchKernelGGL(pose_lm_kernel<64>, dim3(g), dim3(64), 0, s, args..., n); break;
     }
 }
 

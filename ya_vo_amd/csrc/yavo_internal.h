@@ -62,9 +62,10 @@ void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t*
 // Pack KeyPoint records -> descriptors (host-supplied keypoints).
 void launch_pack_desc(const yv_keypoint* keypoints, const int32_t* kp_count, int n_slots, int max_kp,
                       Desc* desc, hipStream_t s);
-// Brute-force Hamming NN: match_key[pair][q] = min over t of (dist << 16 | t).
+// Brute-force Hamming NN: match_key[pair][q] = min over t of (dist << 16 | t).  max_train bounds every train
+// list's length (<= 2048: the FP4 matcher, otherwise the int8 +-1 form); max_kp is the slot stride.
 void launch_match(const Desc* desc, const int32_t* kp_count, const int32_t* pairs, int n_pairs,
-                  int max_kp, uint32_t* match_key, hipStream_t s);
+                  int max_kp, int max_train, uint32_t* match_key, hipStream_t s);
 // Matches records (matchFeatures) + removeOutliers per pair.  match_key entries are reset to
 // 0xFFFFFFFF after they are read (ready for the next match).
 void launch_match_finalize(uint32_t* match_key, const yv_keypoint* keypoints,

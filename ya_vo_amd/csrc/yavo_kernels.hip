@@ -15,6 +15,8 @@
 //   match_finalize      Matches records + removeOutliers        src/BriefDescriptor.cc:163-231
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "yavo_internal.h"
 
@@ -1087,7 +1089,7 @@ __device__ __forceinline__ uint4 expand16_pm1(uint32_t bits) {
                       expand_pm1((bits >> 12) & 0xF));
 }
 
-// 4 descriptor bits -> 4 bytes of 64 (bit set) / 0 (bit clear): the 0/64 encoding of the max_kp <= 2048 matcher
+// 4 descriptor bits -> 4 bytes of 64 (bit set) / 0 (bit clear): the 0/64 encoding of the matcher for train lists <= 2048
 __device__ __forceinline__ uint32_t expand_01x64(uint32_t nib) {
     // v_mul_u32_u24 (full rate; nib <= 15) kept as written: LLVM would otherwise fold the shift into one
     // quarter-rate v_mul_lo_u32 by 0x08102040
@@ -1108,7 +1110,7 @@ __device__ __forceinline__ int desc_popcount(const Desc& d) {
     return c;
 }
 
-// kFast (max_kp <= 2048): bytes 0 / 64, so the MFMA's dot is 4096 * popcount(a & b) and, started from the
+// kFast (train lists <= 2048): bytes 0 / 64, so the MFMA's dot is 4096 * popcount(a & b) and, started from the
 // accumulator c_j = (2047 - j) - 2048 * popcount(b_j), a 4-step chain ends at the key itself:
 //   key = 2048 * (2 popcount(a & b_j) - popcount(b_j)) + (2047 - j) = 2048 * (pa - Hamming) + (2047 - j)
 // (pa - Hamming orders like -Hamming for one query; 2047 - j >= 0 breaks ties toward the first j). The epilogue is
@@ -1284,13 +1286,223 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// The same matcher on the FP4 matrix cores (train lists <= 2048)
+// ------------------------------------------------------------------------------------------------
+// v_mfma_scale_f32_16x16x128_f8f6f4 with both operands FP4 (e2m1) runs a 16 x 16 x 128 tile in the cycles the
+// int8 form needs for 16 x 16 x 64, so a 256-bit descriptor is two K-steps instead of four and an expanded
+// descriptor is 128 B instead of 256 B (half the LDS staging and fragment reads per distance).  Every bit b
+// becomes the FP4 value b (nibble 0b0010 = 1.0, 0b0000 = 0), and both E8M0 block scales are 2^6, so every
+// product is 4096 * a_k * b_k: exact.  The accumulator is f32 and every partial sum an integer of magnitude
+// < 2^22 (the chain starts from c_j = (2047 - j) - 2048 * popcount(b_j), adds 4096 * popcount(a & b) <= 2^20),
+// so every sum is exact in any order and the chain ends at the int8 kernel's key exactly:
+//   key = 2048 * (pa - Hamming) + (2047 - j).
+// v_max3_f32 on integer-valued floats orders them as the integers.  Descriptor dword w (32 bits) of lane group g
+// is K-block g of K-step w >> 2 for both operands alike; inside a dword the nibble order is a fixed permutation
+// of the bits (the same for A and B), so the products pair matching bits.
+constexpr int MF_TC = 128;               // train descriptors per LDS chunk
+constexpr int MF_ROW = 9;                // uint4 per expanded train row (8 + 1 pad)
+
+// 8 descriptor bits -> 8 FP4 nibbles (1.0 / 0): bit i (i < 4) in nibble 2i, bit i + 4 in nibble 2i + 1
+__device__ __forceinline__ uint32_t expand8_fp4(uint32_t byte) {
+    uint32_t lo, hi;
+    asm("v_mul_u32_u24 %0, 0x204081, %1" : "=v"(lo) : "v"(byte & 0xFu));
+    asm("v_mul_u32_u24 %0, 0x204081, %1" : "=v"(hi) : "v"(byte >> 4));
+    return ((lo & 0x01010101u) << 1) | ((hi & 0x01010101u) << 5);
+}
+
+__device__ __forceinline__ uint4 expand32_fp4(uint32_t w) {
+    return make_uint4(expand8_fp4(w & 0xFFu), expand8_fp4((w >> 8) & 0xFFu), expand8_fp4((w >> 16) & 0xFFu),
+                      expand8_fp4(w >> 24));
+}
+
+typedef int mf_v8i __attribute__((ext_vector_type(8)));
+typedef float mf_v4f __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ mf_v4f mfma_fp4(const mm_v4i& a, const mm_v4i& b, const mf_v4f& c) {
+    // FP4 operands use 4 of the 8 operand registers (the backend narrows them); scales 133 = 2^(133-127) = 64
+    const mf_v8i a8 = __builtin_shufflevector(a, a, 0, 1, 2, 3, -1, -1, -1, -1);
+    const mf_v8i b8 = __builtin_shufflevector(b, b, 0, 1, 2, 3, -1, -1, -1, -1);
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, c, 4, 4, 0, 133, 0, 133);
+}
+
+template <int QT, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void match_fp4_kernel(const Desc* __restrict__ desc,
+                                                        const int32_t* __restrict__ kp_count,
+                                                        const int32_t* __restrict__ pairs, int max_kp,
+                                                        uint32_t* __restrict__ match_key) {
+    constexpr int QB = 4 * QT * 16;  // queries per workgroup
+    __shared__ uint4 s_t[2][MF_TC * MF_ROW];
+    __shared__ float s_c[2][MF_TC];  // c_j = (2047 - j) - 2048 popcount(b_j), -2^30 past the list
+    const int pair = blockIdx.y;
+    const int qi = pairs[2 * pair], ti = pairs[2 * pair + 1];
+    const int nq = kp_count[qi], nt = kp_count[ti];
+    const int q0 = blockIdx.x * QB;
+    if (q0 >= nq) return;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int col = lane & 15, g = lane >> 4;
+    const Desc* qd = desc + (int64_t)qi * max_kp;
+    const uint32_t* tw = reinterpret_cast<const uint32_t*>(desc + (int64_t)ti * max_kp);
+    const Desc* td = desc + (int64_t)ti * max_kp;
+
+    // query fragments: tile qt row (lane & 15) = query q0 + 16 QT wave + 16 qt + (lane & 15); K-step s, lane
+    // group g holds descriptor dword 4 s + g
+    mm_v4i A[QT][2];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const int q = q0 + 16 * QT * wave + 16 * qt + col;
+        const Desc d = qd[q < nq ? q : 0];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            // blend, not an index: keeps d in registers
+            const uint32_t w01 = (g & 1) ? d.w[4 * s + 1] : d.w[4 * s];
+            const uint32_t w23 = (g & 1) ? d.w[4 * s + 3] : d.w[4 * s + 2];
+            const uint4 e = expand32_fp4((g & 2) ? w23 : w01);
+            A[qt][s] = mm_v4i{(int)e.x, (int)e.y, (int)e.z, (int)e.w};
+        }
+    }
+    float best[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) best[qt][r] = -__builtin_inff();
+
+    // staging: thread -> (train tt = idx >> 3, descriptor dword u = idx & 7), kF dwords per thread per chunk; the
+    // first MF_TC threads also form train tt = tid's chain start
+    constexpr int kF = MF_TC * 8 / 256;
+    uint32_t pre[kF];
+    float pre_c = 0.f;
+    auto fetch = [&](int t0) {
+#pragma unroll
+        for (int k = 0; k < kF; ++k) {
+            const int idx = tid + 256 * k, tt = idx >> 3, u = idx & 7;
+            const int t = t0 + tt;
+            pre[k] = t < nt ? tw[(int64_t)t * 8 + u] : 0u;
+        }
+        if (tid < MF_TC) {
+            const int t = t0 + tid;
+            pre_c = t < nt ? (float)((2047 - t) - 2048 * desc_popcount(td[t])) : -1073741824.f;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int k = 0; k < kF; ++k) {
+            const int idx = tid + 256 * k, tt = idx >> 3, u = idx & 7;
+            s_t[buf][tt * MF_ROW + u] = expand32_fp4(pre[k]);
+        }
+        if (tid < MF_TC) s_c[buf][tid] = pre_c;
+    };
+    if (nt > 0) {
+        fetch(0);
+        store(0);
+    }
+    int buf = 0;
+    for (int t0 = 0; t0 < nt; t0 += MF_TC) {
+        const bool more = t0 + MF_TC < nt;
+        if (more) fetch(t0 + MF_TC);
+        __syncthreads();
+        // two 16-column train tiles per pass: four independent MFMA chains, one v_max3 folds both tiles' keys into
+        // the running maximum; a column past nt starts at -2^30 (below every real key), so no select is needed
+#pragma unroll
+        for (int tt0 = 0; tt0 < MF_TC; tt0 += 32) {
+            if (t0 + tt0 >= nt) break;
+            mm_v4i Ba[2], Bb[2];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const uint4 va = s_t[buf][(tt0 + col) * MF_ROW + 4 * s + g];
+                const uint4 vb = s_t[buf][(tt0 + 16 + col) * MF_ROW + 4 * s + g];
+                Ba[s] = mm_v4i{(int)va.x, (int)va.y, (int)va.z, (int)va.w};
+                Bb[s] = mm_v4i{(int)vb.x, (int)vb.y, (int)vb.z, (int)vb.w};
+            }
+            const float ca = s_c[buf][tt0 + col], cb = s_c[buf][tt0 + 16 + col];
+            const mf_v4f Ca = {ca, ca, ca, ca}, Cb = {cb, cb, cb, cb};
+#pragma unroll
+            for (int qt = 0; qt < QT; qt += 2) {
+                mf_v4f a0 = mfma_fp4(A[qt][0], Ba[0], Ca);
+                mf_v4f b0 = mfma_fp4(A[qt][0], Bb[0], Cb);
+                mf_v4f a1 = mfma_fp4(A[qt + 1][0], Ba[0], Ca);
+                mf_v4f b1 = mfma_fp4(A[qt + 1][0], Bb[0], Cb);
+                a0 = mfma_fp4(A[qt][1], Ba[1], a0);
+                b0 = mfma_fp4(A[qt][1], Bb[1], b0);
+                a1 = mfma_fp4(A[qt + 1][1], Ba[1], a1);
+                b1 = mfma_fp4(A[qt + 1][1], Bb[1], b1);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    best[qt][r] = fmaxf(best[qt][r], fmaxf(a0[r], b0[r]));
+                    best[qt + 1][r] = fmaxf(best[qt + 1][r], fmaxf(a1[r], b1[r]));
+                }
+            }
+        }
+        if (more) {
+            store(buf ^ 1);  // the other buffer: last read before the barrier at the top of this chunk
+            buf ^= 1;
+        }
+    }
+    // per query row: max over the 16 lanes (train columns) of its lane group
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v = best[qt][r];
+#pragma unroll
+            for (int m = 8; m > 0; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 16));
+            const int q = q0 + 16 * QT * wave + 16 * qt + 4 * g + r;
+            if (col == r && q < nq) {
+                uint32_t key = 0xFFFFFFFFu;  // empty train set (nt >= 1 always leaves a real key in the row max)
+                if (nt > 0) {
+                    const int iv = (int)v;
+                    const int pa = desc_popcount(qd[q]);
+                    const uint32_t d = (uint32_t)(pa - (iv >> 11));
+                    const uint32_t jj = 2047u - ((uint32_t)iv & 2047u);
+                    key = (d << 16) | jj;
+                }
+                match_key[(int64_t)pair * max_kp + q] = key;
+            }
+        }
+    }
+}
+
+namespace {
+// YAVO_MATCH_FORM selects the matcher's form for measurements: "i8" (int8 MFMA, 0/64 bytes), "fp4" (default;
+// FP4 MFMA, 8 query tiles per wave, 3 waves per SIMD), "fp4w2" (8 tiles, 2 waves), "fp4q4" (4 tiles, 4 waves) or
+// "fp4q16" (16 tiles, 1 wave).  Every form gives the same keys.  At 512 stereo frames per step (1024 pairs, 1941
+// keypoints) the matcher runs i8 0.77 ms, fp4w2 0.51, fp4 0.46, fp4q4 0.52, fp4q16 0.73 (alone, HIP events).
+int match_form() {
+    static int form = -1;
+    if (form < 0) {
+        const char* e = getenv("YAVO_MATCH_FORM");
+        form = !e ? 1 : !strcmp(e, "i8") ? 0 : !strcmp(e, "fp4q16") ? 2 : !strcmp(e, "fp4w2") ? 3 : !strcmp(e, "fp4q4") ? 4 : 1;
+    }
+    return form;
+}
+
+template <int QT, int WPE>
+void launch_fp4(const Desc* desc, const int32_t* kp_count, const int32_t* pairs, int n_pairs, int max_kp,
+                uint32_t* match_key, hipStream_t s) {
+    constexpr int QB = 4 * QT * 16;
+    dim3 grid((max_kp + QB - 1) / QB, n_pairs);
+    hipLaunchKernelGGL((match_fp4_kernel<QT, WPE>), grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
+}
+}  // namespace
+
 void launch_match(const Desc* desc, const int32_t* kp_count, const int32_t* pairs, int n_pairs, int max_kp,
-                  uint32_t* match_key, hipStream_t s) {
-    dim3 grid((max_kp + MM_QB - 1) / MM_QB, n_pairs);
-    if (max_kp <= 2048)
-        hipLaunchKernelGGL(match_kernel<true>, grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
-    else
+                  int max_train, uint32_t* match_key, hipStream_t s) {
+    if (max_train > 2048) {
+        dim3 grid((max_kp + MM_QB - 1) / MM_QB, n_pairs);
         hipLaunchKernelGGL(match_kernel<false>, grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
+        return;
+    }
+    switch (match_form()) {
+        case 0: {
+            dim3 grid((max_kp + MM_QB - 1) / MM_QB, n_pairs);
+            hipLaunchKernelGGL(match_kernel<true>, grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
+            break;
+        }
+        case 2: launch_fp4<16, 1>(desc, kp_count, pairs, n_pairs, max_kp, match_key, s); break;
+        case 3: launch_fp4<8, 2>(desc, kp_count, pairs, n_pairs, max_kp, match_key, s); break;
+        case 4: launch_fp4<4, 4>(desc, kp_count, pairs, n_pairs, max_kp, match_key, s); break;
+        default: launch_fp4<8, 3>(desc, kp_count, pairs, n_pairs, max_kp, match_key, s); break;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
