@@ -160,7 +160,10 @@ def _rand_kp(n, rng, pool=None):
     return k
 
 
-@pytest.mark.parametrize("nq,nt", [(1970, 1970), (1, 1), (7, 4096), (4096, 33), (513, 511), (5, 0)])
+# train lists <= 2048 run the FP4 MFMA matcher (the key's 11-bit train index: 2048 is its last size), longer ones the
+# int8 +-1 form; the pool of 37 descriptors makes most minima ties
+@pytest.mark.parametrize("nq,nt", [(1970, 1970), (1, 1), (7, 4096), (4096, 33), (513, 511), (5, 0), (2048, 2048),
+                                   (65, 2049)])
 def test_match_matches_oracle(ctx, oracle, nq, nt):
     rng = np.random.default_rng(nq * 131 + nt)
     pool = rng.integers(0, 256, (37, 32)).astype(np.uint8)  # few distinct descriptors: many exact ties
