@@ -1295,9 +1295,11 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
 // becomes the FP4 value b (nibble 0b0010 = 1.0, 0b0000 = 0), and both E8M0 block scales are 2^6, so every
 // product is 4096 * a_k * b_k: exact.  The accumulator is f32 and every partial sum an integer of magnitude
 // < 2^22 (the chain starts from c_j = (2047 - j) - 2048 * popcount(b_j), adds 4096 * popcount(a & b) <= 2^20),
-// so every sum is exact in any order and the chain ends at the int8 kernel's key exactly:
-//   key = 2048 * (pa - Hamming) + (2047 - j).
-// v_max3_f32 on integer-valued floats orders them as the integers.  Descriptor dword w (32 bits) of lane group g
+// so every sum is exact in any order and the chain ends at the int8 kernel's key plus 2^21 exactly:
+//   key' = 2048 * (pa - Hamming) + (2047 - j) + 2^21 >= 2^21 - 2^19.
+// Every key' is a positive float (a column past the list starts at 0 and, its staged descriptor being zero, stays
+// 0), and positive floats order as their bit patterns, so the running maximum is v_max3_u32 on the raw bits (a float
+// max would first canonicalise both MFMA results: three VALU ops per pair of distances instead of one).  Descriptor dword w (32 bits) of lane group g
 // is K-block g of K-step w >> 2 for both operands alike; inside a dword the nibble order is a fixed permutation
 // of the bits (the same for A and B), so the products pair matching bits.
 constexpr int MF_TC = 128;               // train descriptors per LDS chunk
@@ -1333,7 +1335,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                                                         uint32_t* __restrict__ match_key) {
     constexpr int QB = 4 * QT * 16;  // queries per workgroup
     __shared__ uint4 s_t[2][MF_TC * MF_ROW];
-    __shared__ float s_c[2][MF_TC];  // c_j = (2047 - j) - 2048 popcount(b_j), -2^30 past the list
+    __shared__ float s_c[2][MF_TC];  // c_j = (2047 - j) - 2048 popcount(b_j) + 2^21, 0 past the list
     const int pair = blockIdx.y;
     const int qi = pairs[2 * pair], ti = pairs[2 * pair + 1];
     const int nq = kp_count[qi], nt = kp_count[ti];
@@ -1361,11 +1363,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
             A[qt][s] = mm_v4i{(int)e.x, (int)e.y, (int)e.z, (int)e.w};
         }
     }
-    float best[QT][4];
+    uint32_t best[QT][4];  // bits of the largest key' so far (0 = +0.0: at most every key')
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) best[qt][r] = -__builtin_inff();
+        for (int r = 0; r < 4; ++r) best[qt][r] = 0u;
 
     // staging: thread -> (train tt = idx >> 3, descriptor dword u = idx & 7), kF dwords per thread per chunk; the
     // first MF_TC threads also form train tt = tid's chain start
@@ -1381,7 +1383,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         }
         if (tid < MF_TC) {
             const int t = t0 + tid;
-            pre_c = t < nt ? (float)((2047 - t) - 2048 * desc_popcount(td[t])) : -1073741824.f;
+            pre_c = t < nt ? (float)((2047 - t) - 2048 * desc_popcount(td[t]) + (1 << 21)) : 0.f;
         }
     };
     auto store = [&](int buf) {
@@ -1402,7 +1404,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         if (more) fetch(t0 + MF_TC);
         __syncthreads();
         // two 16-column train tiles per pass: four independent MFMA chains, one v_max3 folds both tiles' keys into
-        // the running maximum; a column past nt starts at -2^30 (below every real key), so no select is needed
+        // the running maximum; a column past nt starts at 0 (below every real key'), so no select is needed
 #pragma unroll
         for (int tt0 = 0; tt0 < MF_TC; tt0 += 32) {
             if (t0 + tt0 >= nt) break;
@@ -1428,8 +1430,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 b1 = mfma_fp4(A[qt + 1][1], Bb[1], b1);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    best[qt][r] = fmaxf(best[qt][r], fmaxf(a0[r], b0[r]));
-                    best[qt + 1][r] = fmaxf(best[qt + 1][r], fmaxf(a1[r], b1[r]));
+                    best[qt][r] = max(best[qt][r], max(__float_as_uint(a0[r]), __float_as_uint(b0[r])));
+                    best[qt + 1][r] = max(best[qt + 1][r], max(__float_as_uint(a1[r]), __float_as_uint(b1[r])));
                 }
             }
         }
@@ -1443,14 +1445,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     for (int qt = 0; qt < QT; ++qt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            float v = best[qt][r];
+            uint32_t v = best[qt][r];
 #pragma unroll
-            for (int m = 8; m > 0; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 16));
+            for (int m = 8; m > 0; m >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m, 16));
             const int q = q0 + 16 * QT * wave + 16 * qt + 4 * g + r;
             if (col == r && q < nq) {
                 uint32_t key = 0xFFFFFFFFu;  // empty train set (nt >= 1 always leaves a real key in the row max)
                 if (nt > 0) {
-                    const int iv = (int)v;
+                    const int iv = (int)__uint_as_float(v) - (1 << 21);
                     const int pa = desc_popcount(qd[q]);
                     const uint32_t d = (uint32_t)(pa - (iv >> 11));
                     const uint32_t jj = 2047u - ((uint32_t)iv & 2047u);
