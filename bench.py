@@ -36,6 +36,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP4_MFMA_PEAK_TOPS = 10000.0  # dense FP4 MFMA peak (MI355X_MICROARCH.md; no sparsity): the matcher runs on
 # v_mfma_scale_f32_16x16x128_f8f6f4 with FP4 operands (max_kp <= 2048)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-op/s
+# FP64 vector peak (AMD MI355X spec, 78.6 TFLOP/s: 16 FP64 FMA lanes per SIMD per clock, so one wave64 FP64
+# instruction issues in 4 cycles); the MI355X guide does not list FP64
+FP64_PEAK_TFLOPS = 256 * 4 * 16 * 2 * 2.4e9 / 1e12
+SIMD_CYCLES_PER_S = 256 * 4 * 2.4e9
 
 
 def parse():
@@ -396,12 +400,14 @@ def main():
         dur_s = per_launch_ms[dom] / 1e3
         achieved = nbytes[dom] / dur_s / 1e9
         traffic = None
+        fp64 = {}
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc_path):
             try:
                 pmc = json.load(open(pmc_path))
                 if pmc.get("frames_per_step") == B:
                     traffic = pmc.get("per_launch_bytes", {}).get(dom)
+                    fp64 = pmc.get("fp64_per_launch", {})
             except (OSError, ValueError):
                 traffic = None
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -424,8 +430,23 @@ def main():
                 per_stage[st] = {"bound": "mfma_fp4", "achieved": round(a, 1), "peak": FP4_MFMA_PEAK_TOPS,
                                  "unit": "T op/s", "frac": round(a / FP4_MFMA_PEAK_TOPS, 4)}
             elif st == "track_pose":
-                per_stage[st] = {"bound": "latency", "note": "serial LM per problem (DESIGN.md 4.2)",
-                                 "ms": round(t_ms, 4)}
+                # FP64 VALU: the launch's FP64 wave-instructions from the PMC pass (tools/pmc_traffic.sh,
+                # profiles/pmc_traffic.json) over this run's per-launch time.  SQ_INSTS_VALU_FLOPS_FP64 counts per
+                # wave-instruction (ADD + MUL + 2 FMA), so lane-FLOPs = 64 x it, an upper bound (the LM's lane-0 LDLT
+                # runs one lane); issue_frac = FP64 wave-instructions x 4 cycles / SIMD-cycles of the launch
+                f = fp64.get(st)
+                if f:
+                    a = 64.0 * f["flops"] / (t_ms / 1e3) / 1e12
+                    per_stage[st] = {"bound": "fp64_valu", "achieved": round(a, 3), "peak": round(FP64_PEAK_TFLOPS, 1),
+                                     "unit": "TFLOP/s", "frac": round(a / FP64_PEAK_TFLOPS, 4),
+                                     "issue_frac": round(4 * f["wave_instructions"] / (SIMD_CYCLES_PER_S * t_ms / 1e3), 4),
+                                     "fp64_wave_flops_per_launch": f["flops"],
+                                     "fp64_wave_instructions_per_launch": f["wave_instructions"],
+                                     "note": "serial LM per problem, beside the next step's image kernels (DESIGN.md "
+                                             "4.2, 4.4); achieved = 64 lanes x PMC FP64 wave-FLOPs / launch time"}
+                else:
+                    per_stage[st] = {"bound": "latency", "note": "serial LM per problem (DESIGN.md 4.2)",
+                                     "ms": round(t_ms, 4)}
             else:
                 a = nbytes[st] / (t_ms / 1e3) / 1e9
                 per_stage[st] = {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -3,7 +3,11 @@
 gfx950 correction (MI355X_MICROARCH.md 'HBM'; cdna_hip_programming.md section 7): FETCH_SIZE and WRITE_SIZE
 are in KiB; FETCH_SIZE reports exactly half the bytes of a wide coalesced streaming read, so
     traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
-The raw counters are kept next to the corrected figure (other access widths are uncalibrated)."""
+The raw counters are kept next to the corrected figure (other access widths are uncalibrated).
+
+The third pass (FP64) holds the FP64 VALU counters: SQ_INSTS_VALU_FLOPS_FP64 (+ _TRANS) is the FP64 FLOP count of
+the launch (per active lane, FMA = 2), SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 the FP64 wave-instructions issued; bench.py
+reads both for the pose LM's FP64 roofline."""
 import csv
 import glob
 import json
@@ -11,7 +15,8 @@ import os
 import sys
 
 STAGE_OF = {"detect_kernel": "detect", "topk_kernel": "topk", "brief_kernel": "brief",
-            "match_finalize_kernel": "finalize", "match_kernel": "match", "track_build_kernel": "track_edges",
+            "match_finalize_kernel": "finalize", "match_kernel": "match", "match_fp4_kernel": "match",
+            "track_build_kernel": "track_edges",
             "pose_lm_kernel": "track_pose"}
 
 
@@ -22,8 +27,9 @@ def stage(kernel_name):
     return STAGE_OF.get(base)
 
 
-def load(out_dir, counter):
-    files = glob.glob(os.path.join(out_dir, f"pmc_{counter}", "**", "*counter_collection*.csv"), recursive=True)
+def load(out_dir, counter, pass_dir=None):
+    files = glob.glob(os.path.join(out_dir, f"pmc_{pass_dir or counter}", "**", "*counter_collection*.csv"),
+                      recursive=True)
     per = {}
     for f in files:
         with open(f) as fh:
@@ -58,6 +64,25 @@ def main():
         wm = sum(w) / len(w) if w else 0.0
         res["raw_kib"][st] = {"FETCH_SIZE": fm, "WRITE_SIZE": wm, "dispatches": [len(f), len(w)]}
         res["per_launch_bytes"][st] = int((2 * fm + wm) * 1024)
+    fp64 = {c: load(out_dir, c, "FP64") for c in ("SQ_INSTS_VALU_FLOPS_FP64", "SQ_INSTS_VALU_FLOPS_FP64_TRANS",
+                                                   "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                                   "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")}
+    stages = sorted(set().union(*[set(v) for v in fp64.values()]))
+    if stages:
+        res["fp64_per_launch"] = {}
+        for st in stages:
+            vals = {}
+            for c, per in fp64.items():
+                x = per.get(st, [])
+                x = x[-3:] if len(x) > 3 else x
+                vals[c] = sum(x) / len(x) if x else 0.0
+            if not any(vals.values()):
+                continue
+            res["fp64_per_launch"][st] = {
+                "flops": vals["SQ_INSTS_VALU_FLOPS_FP64"] + vals["SQ_INSTS_VALU_FLOPS_FP64_TRANS"],
+                "wave_instructions": sum(vals[c] for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                                           "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")),
+                "raw": vals}
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     path = os.path.join(root, "profiles", "pmc_traffic.json")
     os.makedirs(os.path.dirname(path), exist_ok=True)

@@ -10,9 +10,13 @@ cd "$ROOT"
 OUT="$ROOT/gpurun_out"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-for C in FETCH_SIZE WRITE_SIZE; do
+# third pass: the FP64 VALU counters (6 SQ slots of 8) -- FLOPs and instructions of the pose LM
+FP64="SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64"
+for C in FETCH_SIZE WRITE_SIZE FP64; do
     echo "[$(date +%T)] pmc pass $C"
-    timeout -k 10 600 rocprofv3 --pmc "$C" --output-format csv -d "$OUT/pmc_$C" -o pmc -- \
+    CTRS="$C"
+    [ "$C" = "FP64" ] && CTRS="$FP64"
+    timeout -k 10 600 rocprofv3 --pmc $CTRS --output-format csv -d "$OUT/pmc_$C" -o pmc -- \
         python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-baseline none --no-timing "$@" \
         > "$OUT/pmc_$C.log" 2>&1
     st=$?
