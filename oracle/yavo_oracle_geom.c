@@ -957,7 +957,7 @@ static int lm_optimize(lm_problem* P, double* T, int iterations) {
             if (rho > 0 && isfinite(tempChi) && ok2) {
                 g_lm_stats[2]++;
                 double t = 2 * rho - 1;
-                double alpha = 1. - t * t * t;
+                double alpha = 1. - or_cube(t);
                 alpha = alpha < goodUpper ? alpha : goodUpper;
                 double sf = goodLower > alpha ? goodLower : alpha;
                 lambda *= sf;

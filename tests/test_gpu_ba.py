@@ -46,6 +46,22 @@ def test_ba_config5_matches_oracle(ctx, oracle):
     assert log[-1] < 0.05 * log[0]
 
 
+@pytest.mark.parametrize("on_device", [True, False])
+def test_ba_control_modes_match_oracle(ctx, oracle, on_device):
+    """The LM control on the device (default: the host enqueues every iteration, one read-back per solve; iterations
+    whose first damping trial is rejected suspend and resume) and on the host (one read-back per trial): both bit for
+    bit the oracle's, with a poor start (rejected trials) and an exact one (rho = 0 ends the run)."""
+    for kw, nf, iters in [(dict(noise_px=2.0, init_rot=0.05, init_trans=0.5, init_point=1.0, seed=21), 1, 12),
+                          (dict(noise_px=0.0, seed=22), 2, 25)]:
+        w = scene.ba_window(n_poses=7, n_landmarks=300, obs=4, **kw)
+        if kw["noise_px"] == 0.0:
+            w["poses0"][:nf] = w["poses_true"][:nf]
+        ba = yv.BundleAdjuster(ctx, 7, 300, 1200)
+        ba.set_control(on_device)
+        _both(ctx, oracle, w, nf, iters, ba)
+        ba.close()
+
+
 def test_ba_reuse_and_shrink(ctx, oracle):
     """One workspace, several graphs of different sizes (the structure rebuilt per set_problem)."""
     ba = yv.BundleAdjuster(ctx, 20, 3000, 15000)

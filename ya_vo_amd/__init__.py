@@ -121,6 +121,7 @@ GEOM_SIGNATURES = {
     "yv_ba_solve": (_I, [_P, _P, _P, _I, _P, ctypes.POINTER(_I)]),
     "yv_ba_debug_read": (_I, [_P, _I, _P, ctypes.c_int64]),
     "yv_ba_set_stream": (_I, [_P, _P]),
+    "yv_ba_set_control": (_I, [_P, _I]),
     "yv_lm_sum_mode": (_I, []),
 }
 
@@ -614,6 +615,10 @@ class BundleAdjuster:
         """Run on a caller stream (yv_ba_set_stream; 0 = the context's stream)."""
         _check(self.lib.yv_ba_set_stream(self.handle, ctypes.c_void_p(stream) if stream else None),
                "yv_ba_set_stream")
+
+    def set_control(self, on_device: bool = True) -> None:
+        """LM control on the device (default: no read-back per trial) or on the host (yv_ba_set_control)."""
+        _check(self.lib.yv_ba_set_control(self.handle, 1 if on_device else 0), "yv_ba_set_control")
 
     def set_problem(self, n_poses: int, n_fixed: int, n_landmarks: int, edge_pose, edge_landmark, meas, K) -> None:
         self._ep = np.ascontiguousarray(edge_pose, np.int32).reshape(-1)

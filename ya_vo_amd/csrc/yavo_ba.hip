@@ -70,6 +70,7 @@ __device__ __forceinline__ double tree256(double v, double* red) {
 }
 
 __global__ __launch_bounds__(256) void ba_linearize_kernel(BaParams P, BaMat3 K) {
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= P.E) return;
     const double* T = P.poses + 7 * P.ep[e];
@@ -107,6 +108,7 @@ __global__ __launch_bounds__(256) void ba_linearize_kernel(BaParams P, BaMat3 K)
 // one workgroup per free pose (blockIdx.x + nf): 21 upper H entries + 6 b entries in tree256 order
 __global__ __launch_bounds__(256) void ba_pose_reduce_kernel(BaParams P) {
     __shared__ double red[27 * kNT];
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     const int p = P.nf + blockIdx.x;
     const int k0 = P.pe_off[p], k1 = P.pe_off[p + 1];
     const int t = threadIdx.x;
@@ -160,6 +162,7 @@ __global__ __launch_bounds__(256) void ba_pose_reduce_kernel(BaParams P) {
 
 // H_ll / b_l per landmark; maxdiag (|H| diagonal of free poses and landmarks) as uint64 bits of a non-negative double
 __global__ __launch_bounds__(256) void ba_landmark_reduce_kernel(BaParams P, unsigned long long* maxdiag) {
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     const int l = blockIdx.x * blockDim.x + threadIdx.x;
     double m = 0.0;
     if (l < P.L) {
@@ -206,6 +209,8 @@ __device__ __forceinline__ void inv3(const double* a, double* o) {
 // lanes [0, L): D^-1 of landmark l (H_ll + lambda I)^-1; lanes [0, E): W_e = H_pl(e) D^-1 of its landmark, with that
 // inverse recomputed in the lane (the same expressions, so the same bits as the landmark lane's)
 __global__ __launch_bounds__(256) void ba_landmark_trial_kernel(BaParams P, double lambda) {
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
+    if (P.lam) lambda = *P.lam;
     const int id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id < P.L) {
         double d[9], Di[9];
@@ -280,6 +285,8 @@ __device__ __forceinline__ double schur_chain(double v, const double* sd, int n,
 // value in both mirrored entries). b_schur: lane a < 6 runs v = b_p[a] - sum_e W_e[a] . b_l(e) over the pose's edges.
 __global__ __launch_bounds__(kSchurChunk) void ba_schur_kernel(BaParams P, double lambda) {
     __shared__ double sd[kSchurChunk * kSchurStride];
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
+    if (P.lam) lambda = *P.lam;
     const int np = P.np, nb = np * (np + 1) / 2;
     const int lane = threadIdx.x;
     const int a = lane / 6, b = lane - 6 * (lane / 6);
@@ -395,6 +402,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 __global__ __launch_bounds__(kLdltThreads) void ba_ldlt_lds_kernel(BaParams P) {
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     __shared__ double Ls[kLdltMaxN * (kLdltMaxN + 1) / 2];  // the factor, for the solves
     __shared__ double colk[kLdltMaxN];  // L(i, k) of the current step
     __shared__ __attribute__((aligned(16))) double tc[kLdltMaxN];  // t_i = D(k) L(i, k)
@@ -605,6 +613,7 @@ __global__ __launch_bounds__(kLdltThreads) void ba_ldlt_lds_kernel(BaParams P) {
 
 // larger systems: the same steps on S in global memory
 __global__ __launch_bounds__(256) void ba_ldlt_kernel(BaParams P) {
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     extern __shared__ double s_dyn[];  // v [n], temp [n]
     __shared__ double s_pv[kNT];
     __shared__ int s_pi[kNT];
@@ -746,6 +755,7 @@ __global__ __launch_bounds__(256) void ba_ldlt_kernel(BaParams P) {
 }
 
 __global__ __launch_bounds__(256) void ba_backsub_kernel(BaParams P) {
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     const int l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= P.L) return;
     double tv[3] = {P.bl[3 * l], P.bl[3 * l + 1], P.bl[3 * l + 2]};
@@ -769,6 +779,7 @@ __global__ __launch_bounds__(256) void ba_backsub_kernel(BaParams P) {
 
 // lanes [0, np): free poses; [np, np + 3 L): landmark coordinates
 __global__ __launch_bounds__(256) void ba_update_kernel(BaParams P) {
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     const int id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id < P.np) {
         const int p = P.nf + id;
@@ -785,6 +796,7 @@ __global__ __launch_bounds__(256) void ba_update_kernel(BaParams P) {
 
 // one lane per edge: its squared error at the current estimate (summed by ba_chi2_kernel)
 __global__ __launch_bounds__(256) void ba_edge_chi2_kernel(BaParams P, BaMat3 K) {
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= P.E) return;
     double r[2];
@@ -796,6 +808,8 @@ __global__ __launch_bounds__(256) void ba_edge_chi2_kernel(BaParams P, BaMat3 K)
 // x.(lambda x + b) over the variables (free poses, then landmarks) -> scal[1]
 __global__ __launch_bounds__(256) void ba_chi2_kernel(BaParams P, BaMat3 K, double lambda, int with_scale) {
     __shared__ double red[kNT];
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
+    if (P.lam) lambda = *P.lam;
     const int t = threadIdx.x;
     double acc = 0.0;
     if (blockIdx.x == 0) {
@@ -841,7 +855,131 @@ __global__ __launch_bounds__(256) void ba_chi2_kernel(BaParams P, BaMat3 K, doub
     }
 }
 
+// ---- device-driven LM control (one lane each; the host loop of yv_ba_solve's host form, operation for operation) ----
+__global__ void ba_ctl_init_kernel(BaCtl* c, const double* scal, double* log) {
+    c->currentChi = scal[0];
+    log[0] = scal[0];
+    c->lambda = 0;
+    c->ni = 2;
+    c->rho = 0;
+    c->q = 0;
+    c->it = 0;
+    c->stop = 0;
+    c->iters = 0;
+    c->skip_iter = 0;
+    c->skip_trial = 1;
+    c->skip_restore = 1;
+    c->suspended = 0;
+    c->iter_done = 0;
+}
+
+// an iteration's trial loop starts (after its linearisation); the first one sets lambda = tau max|H_ii|
+__global__ void ba_ctl_iter_begin_kernel(BaCtl* c, const unsigned long long* maxdiag) {
+    if (c->skip_iter) return;
+    if (maxdiag) {
+        const double maxd = __longlong_as_double((long long)*maxdiag);
+        c->lambda = 1e-5 * maxd;
+        c->ni = 2;
+    }
+    c->q = 0;
+    c->iter_done = 0;
+    c->skip_trial = 0;
+}
+
+// after a trial: rho, accept (lambda *= max(1/3, min(2/3, 1 - (2 rho - 1)^3))) or reject (lambda *= ni, ni *= 2,
+// restore); the trial loop ends when !(rho < 0 && q < 10)
+__global__ void ba_ctl_decide_kernel(BaCtl* c, const double* scal, int has_ns) {
+    if (c->skip_trial) {
+        c->skip_restore = 1;
+        return;
+    }
+    double tempChi = scal[0];
+    const bool ok2 = has_ns ? scal[2] != 0.0 : true;
+    if (!ok2) tempChi = DBL_MAX;
+    double rho = c->currentChi - tempChi;
+    double scale = scal[1];
+    scale += 1e-3;
+    rho /= scale;
+    if (rho > 0 && isfinite(tempChi)) {
+        double alpha = 1. - cube_cr(2 * rho - 1);  // pow(2 rho - 1, 3), correctly rounded
+        alpha = fmin(alpha, 2. / 3.);
+        const double sf = fmax(1. / 3., alpha);
+        c->lambda *= sf;
+        c->ni = 2;
+        c->currentChi = tempChi;
+        c->skip_restore = 1;
+    } else {
+        c->lambda *= c->ni;
+        c->ni *= 2;
+        c->skip_restore = 0;
+    }
+    c->rho = rho;
+    c->q += 1;
+    if (!(rho < 0 && c->q < 10)) {
+        c->iter_done = 1;
+        c->skip_trial = 1;
+    }
+}
+
+// an iteration ends: its chi2 is logged; stop on q == 10 / rho == 0 / non-finite lambda.  A trial loop still running
+// after the trial slots the host enqueued suspends the solve (every later kernel skips) until the host resumes it.
+__global__ void ba_ctl_iter_end_kernel(BaCtl* c, double* log) {
+    if (c->skip_iter) return;
+    if (!c->iter_done) {
+        c->suspended = 1;
+        c->skip_iter = 1;
+        c->skip_trial = 1;
+        return;
+    }
+    log[c->it + 1] = c->currentChi;
+    if (c->q == 10 || c->rho == 0 || !isfinite(c->lambda)) {
+        c->stop = 1;
+        c->iters = c->it + 1;
+        c->skip_iter = 1;
+        c->skip_trial = 1;
+    } else {
+        c->it += 1;
+        c->iters = c->it;
+    }
+}
+
+__global__ void ba_ctl_resume_kernel(BaCtl* c) {
+    c->suspended = 0;
+    c->skip_iter = 0;
+    c->skip_trial = 0;
+}
+
+__global__ __launch_bounds__(256) void ba_copy2_kernel(const int* gate, double* d1, const double* s1, int n1, double* d2,
+                                                       const double* s2, int n2) {
+    if (*gate) return;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n1) d1[i] = s1[i];
+    else if (i - n1 < n2) d2[i - n1] = s2[i - n1];
+}
+
 }  // namespace ba
+
+void launch_ba_ctl_init(BaCtl* c, const double* scal, double* log, hipStream_t s) {
+    hipLaunchKernelGGL(ba::ba_ctl_init_kernel, dim3(1), dim3(1), 0, s, c, scal, log);
+}
+void launch_ba_ctl_iter_begin(BaCtl* c, const unsigned long long* maxdiag, hipStream_t s) {
+    hipLaunchKernelGGL(ba::ba_ctl_iter_begin_kernel, dim3(1), dim3(1), 0, s, c, maxdiag);
+}
+void launch_ba_ctl_decide(BaCtl* c, const double* scal, int has_ns, hipStream_t s) {
+    hipLaunchKernelGGL(ba::ba_ctl_decide_kernel, dim3(1), dim3(1), 0, s, c, scal, has_ns);
+}
+void launch_ba_ctl_iter_end(BaCtl* c, double* log, hipStream_t s) {
+    hipLaunchKernelGGL(ba::ba_ctl_iter_end_kernel, dim3(1), dim3(1), 0, s, c, log);
+}
+void launch_ba_ctl_resume(BaCtl* c, hipStream_t s) {
+    hipLaunchKernelGGL(ba::ba_ctl_resume_kernel, dim3(1), dim3(1), 0, s, c);
+}
+void launch_ba_copy2(const int* gate, double* d1, const double* s1, int n1, double* d2, const double* s2, int n2,
+                     hipStream_t s) {
+    if (n1 + n2 > 0)
+        hipLaunchKernelGGL(ba::ba_copy2_kernel, dim3((n1 + n2 + 255) / 256), dim3(256), 0, s, gate, d1, s1, n1, d2, s2,
+                           n2);
+}
 
 void launch_ba_linearize(const BaParams& P, const BaMat3& K, hipStream_t s) {
     if (P.E > 0) hipLaunchKernelGGL(ba::ba_linearize_kernel, dim3((P.E + 255) / 256), dim3(256), 0, s, P, K);
@@ -894,6 +1032,11 @@ struct yv_ba {
     double *bak_poses = nullptr, *bak_X = nullptr;
     unsigned long long* d_maxdiag = nullptr;
     double* h_scal = nullptr;  // pinned [4]
+    yavo::BaCtl* d_ctl = nullptr;  // the device-driven LM's control block
+    yavo::BaCtl* h_ctl = nullptr;  // pinned copy
+    double* d_log = nullptr;       // [log_cap] chi2 per iteration
+    int log_cap = 0;
+    int device_control = 1;        // yv_ba_set_control
     bool ready = false;
 };
 
@@ -976,7 +1119,10 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
     rc |= ba_alloc(b, &Q.scal, 16);
     rc |= ba_alloc(b, &Q.e2, E);
     rc |= ba_alloc(b, &b->d_maxdiag, 1);
+    rc |= ba_alloc(b, &b->d_ctl, 1);
     if (rc == YV_OK && hipHostMalloc(reinterpret_cast<void**>(&b->h_scal), 4 * sizeof(double)) != hipSuccess)
+        rc = YV_ERR_HIP;
+    if (rc == YV_OK && hipHostMalloc(reinterpret_cast<void**>(&b->h_ctl), sizeof(yavo::BaCtl)) != hipSuccess)
         rc = YV_ERR_HIP;
     if (rc != YV_OK) {
         yv_ba_destroy(b);
@@ -992,6 +1138,7 @@ extern "C" void yv_ba_destroy(yv_ba* b) {
     (void)hipStreamSynchronize(b->st);
     for (void* p : b->owned) (void)hipFree(p);
     if (b->h_scal) (void)hipHostFree(b->h_scal);
+    if (b->h_ctl) (void)hipHostFree(b->h_ctl);
     delete b;
 }
 
@@ -1100,9 +1247,99 @@ extern "C" int yv_ba_set_problem(yv_ba* b, int n_poses, int n_fixed, int n_landm
 
 // g2o OptimizationAlgorithmLevenberg::solve, as or_ba_lm: the host runs the damping control on the device's chi2
 // and scale (bit-identical double arithmetic), the device everything per edge / landmark / pose
+namespace {
+
+// Trial slots the device-driven solve enqueues per iteration (YAVO_BA_TRIALS, default 1): g2o's trial loop usually
+// accepts its first trial; an iteration that needs more suspends the solve and the host enqueues the rest.
+int ba_trial_slots() {
+    static const int n = [] {
+        const char* e = getenv("YAVO_BA_TRIALS");
+        const int v = e ? atoi(e) : 1;
+        return v >= 1 && v <= 10 ? v : 1;
+    }();
+    return n;
+}
+
+// The LM of yv_ba_solve with its control on the device (default): the host enqueues every iteration's kernels
+// without waiting -- linearise, (iteration begin), per trial slot {backup, trial, decide, restore}, (iteration end)
+// -- and the one-lane ba_ctl_* kernels carry lambda, ni, currentChi and the stop / accept decisions in a device
+// control block that gates the other kernels.  One read-back per solve, plus one per suspended trial loop.
+int ba_solve_device(yv_ba* b, double* poses, double* landmarks, int max_iters, double* chi2_log, int* iters) {
+    yavo::BaParams& Q = b->P;
+    const size_t pb = sizeof(double) * 7 * Q.P, xb = sizeof(double) * 3 * Q.L;
+    hipStream_t st = b->st;
+    if (max_iters + 1 > b->log_cap) {
+        if (hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
+        ba_free_one(b, b->d_log);
+        b->d_log = nullptr;
+        b->log_cap = 0;
+        if (ba_alloc(b, &b->d_log, (size_t)max_iters + 1) != YV_OK) return YV_ERR_HIP;
+        b->log_cap = max_iters + 1;
+    }
+    yavo::BaCtl* c = b->d_ctl;
+    yavo::BaParams Pit = Q, Ptr = Q;
+    Pit.gate = &c->skip_iter;
+    Ptr.gate = &c->skip_trial;
+    Ptr.lam = &c->lambda;
+    if (hipMemcpyAsync(Q.poses, poses, pb, hipMemcpyHostToDevice, st) != hipSuccess ||
+        (xb && hipMemcpyAsync(Q.X, landmarks, xb, hipMemcpyHostToDevice, st) != hipSuccess))
+        return YV_ERR_HIP;
+    yavo::launch_ba_chi2(Q, b->K, st);
+    yavo::launch_ba_ctl_init(c, Q.scal, b->d_log, st);
+    const int slots = ba_trial_slots();
+    int first = 0;
+    bool resume = false;
+    for (;;) {
+        for (int it = first; it < max_iters; ++it) {
+            if (!(resume && it == first)) {
+                yavo::launch_ba_linearize(Pit, b->K, st);
+                if (it == 0) {
+                    if (hipMemsetAsync(b->d_maxdiag, 0, sizeof(unsigned long long), st) != hipSuccess) return YV_ERR_HIP;
+                    yavo::launch_ba_landmark_reduce(Pit, b->d_maxdiag, st);
+                } else {
+                    yavo::launch_ba_landmark_reduce(Pit, nullptr, st);
+                }
+                yavo::launch_ba_ctl_iter_begin(c, it == 0 ? b->d_maxdiag : nullptr, st);
+            }
+            for (int q = 0; q < slots; ++q) {
+                yavo::launch_ba_copy2(&c->skip_trial, b->bak_poses, Q.poses, 7 * Q.P, b->bak_X, Q.X, 3 * Q.L, st);
+                yavo::launch_ba_trial(Ptr, b->K, 0.0, st);
+                yavo::launch_ba_ctl_decide(c, Q.scal, Q.ns > 0 ? 1 : 0, st);
+                yavo::launch_ba_copy2(&c->skip_restore, Q.poses, b->bak_poses, 7 * Q.P, Q.X, b->bak_X, 3 * Q.L, st);
+            }
+            yavo::launch_ba_ctl_iter_end(c, b->d_log, st);
+        }
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(b->h_ctl, c, sizeof(yavo::BaCtl), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return YV_ERR_HIP;
+        if (!b->h_ctl->suspended) break;
+        yavo::launch_ba_ctl_resume(c, st);  // the suspended iteration's trial loop continues at its trial q
+        first = b->h_ctl->it;
+        resume = true;
+    }
+    const int n_it = max_iters > 0 ? b->h_ctl->iters : 0;
+    if (hipMemcpyAsync(poses, Q.poses, pb, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        (xb && hipMemcpyAsync(landmarks, Q.X, xb, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        (chi2_log && hipMemcpyAsync(chi2_log, b->d_log, sizeof(double) * (n_it + 1), hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return YV_ERR_HIP;
+    if (iters) *iters = n_it;
+    return YV_OK;
+}
+
+}  // namespace
+
+extern "C" int yv_ba_set_control(yv_ba* b, int on_device) {
+    if (!b || on_device < 0 || on_device > 1) return YV_ERR_INVALID;
+    b->device_control = on_device;
+    return YV_OK;
+}
+
 extern "C" int yv_ba_solve(yv_ba* b, double* poses, double* landmarks, int max_iters, double* chi2_log, int* iters) {
     if (!b || !b->ready || !poses || (b->P.L > 0 && !landmarks) || max_iters < 0) return YV_ERR_INVALID;
     if (hipSetDevice(b->dev) != hipSuccess) return YV_ERR_HIP;
+    if (b->device_control) return ba_solve_device(b, poses, landmarks, max_iters, chi2_log, iters);
     yavo::BaParams& Q = b->P;
     const size_t pb = sizeof(double) * 7 * Q.P, xb = sizeof(double) * 3 * Q.L;
     hipStream_t st = b->st;
@@ -1147,7 +1384,7 @@ extern "C" int yv_ba_solve(yv_ba* b, double* poses, double* landmarks, int max_i
             scale += 1e-3;
             rho /= scale;
             if (rho > 0 && std::isfinite(tempChi)) {
-                double alpha = 1. - pow((2 * rho - 1), 3);
+                double alpha = 1. - yavo::cube_cr(2 * rho - 1);  // pow(2 rho - 1, 3), correctly rounded
                 alpha = fmin(alpha, 2. / 3.);
                 const double sf = fmax(1. / 3., alpha);
                 lambda *= sf;

@@ -1243,7 +1243,7 @@ __global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t*
                             int brk = 0, accepted = 0;
                             if (rho > 0 && isfinite(tempChi) && ok2) {
                                 double t = 2 * rho - 1;
-                                double alpha = 1. - t * t * t;
+                                double alpha = 1. - cube_cr(t);  // pow(t, 3), correctly rounded
                                 alpha = alpha < goodUpper ? alpha : goodUpper;
                                 double sf = goodLower > alpha ? goodLower : alpha;
                                 lambda *= sf;

@@ -10,6 +10,14 @@ struct yv_ctx;
 
 namespace yavo {
 
+// pow(t, 3) of g2o's LM step scaling (alpha = 1 - pow(2 rho - 1, 3)), correctly rounded: t^2 = p + e1 and p t = q + e2
+// exactly (fma), t^3 = q + (e2 + e1 t) rounded once (oracle/yavo_oracle.h or_cube, the same operations).
+__host__ __device__ inline double cube_cr(double t) {
+    const double p = t * t, e1 = fma(t, t, -p);
+    const double q = p * t, e2 = fma(p, t, -q);
+    return q + (e2 + e1 * t);
+}
+
 constexpr int kMaxKp = 4096;
 constexpr int kMaxWidth = 2048;  // image width limit (BRIEF keeps 49 rows of the blurred image in LDS)       // per-image keypoint capacity supported by the top-K / scan kernels
 constexpr int kFastTileW = 64;     // FAST / blur output tile: one wave per tile row
@@ -182,6 +190,17 @@ struct BaParams {
     int32_t* tr = nullptr;            // [ns] LDLT transpositions
     double* scal = nullptr;           // [4]: chi2, scale, LDLT ok
     double* e2 = nullptr;             // [E] squared error per edge
+    // device-driven LM (yv_ba_solve): a kernel returns at once when *gate != 0 (its phase is skipped), and the trial
+    // kernels read lambda from *lam; both nullptr under host control
+    const int* gate = nullptr;
+    const double* lam = nullptr;
+};
+// The device-side Levenberg-Marquardt control of one solve (g2o OptimizationAlgorithmLevenberg::solve, the
+// host loop's arithmetic): written by the one-lane ba_ctl_* kernels, read by the gates of the others.
+struct BaCtl {
+    double currentChi, lambda, ni, rho;
+    int q, it, stop, iters;
+    int skip_iter, skip_trial, skip_restore, suspended, iter_done, pad[3];
 };
 struct BaMat3 {
     double v[9];
@@ -190,6 +209,14 @@ void launch_ba_linearize(const BaParams& P, const BaMat3& K, hipStream_t s);
 void launch_ba_landmark_reduce(const BaParams& P, unsigned long long* maxdiag, hipStream_t s);
 void launch_ba_trial(const BaParams& P, const BaMat3& K, double lambda, hipStream_t s);
 void launch_ba_chi2(const BaParams& P, const BaMat3& K, hipStream_t s);
+// device control: init after the first chi2, per iteration begin / end, per trial decide, backup / restore copies
+void launch_ba_ctl_init(BaCtl* c, const double* scal, double* log, hipStream_t s);
+void launch_ba_ctl_iter_begin(BaCtl* c, const unsigned long long* maxdiag, hipStream_t s);
+void launch_ba_ctl_decide(BaCtl* c, const double* scal, int has_ns, hipStream_t s);
+void launch_ba_ctl_iter_end(BaCtl* c, double* log, hipStream_t s);
+void launch_ba_ctl_resume(BaCtl* c, hipStream_t s);
+void launch_ba_copy2(const int* gate, double* d1, const double* s1, int n1, double* d2, const double* s2, int n2,
+                     hipStream_t s);
 
 // the shared map (yavo_map.hip): one chunk's block after its pose LM
 void launch_map_chunk(const double* rel, int n, int64_t first_frame, int kf_every, const int32_t* edge_count,
