@@ -374,18 +374,31 @@ __global__ __launch_bounds__(kSchurChunk) void ba_schur_kernel(BaParams P, doubl
 //  2. Pivoting commutes with the left-looking factorisation: the oracle swaps untouched original entries in the
 //     trailing part and the finished rows of L, so its result equals the unpivoted factorisation of P S P^T (S is
 //     bitwise symmetric: each Schur entry is stored to both halves from one value).
-//  3. The unpivoted factorisation runs right-looking with the matrix in registers: the oracle forms column k as
-//     acc = L(i, k) - L(i, 0) t_0 - L(i, 1) t_1 - ... (t_j = D(j) L(k, j)) and D(k) = L(k, k) - (L(k, 0) t_0 + ...);
-//     step j here applies term j of every such chain at once (L(i, c) -= L(i, j) (D(j) L(c, j)), i > c > j;
-//     dot_c += L(c, j) (D(j) L(c, j))), the same operations in the same order per entry. Thread = one 16-column
-//     segment of one row of the lower triangle (504 segments at n = 120); per step the owners of column k divide
-//     and publish L(i, k) and t_i through LDS, then every segment updates its entries in registers.
+//  3. The unpivoted factorisation runs right-looking on the packed lower triangle in LDS: the oracle forms column k
+//     as acc = L(i, k) - L(i, 0) t_0 - L(i, 1) t_1 - ... (t_j = D(j) L(k, j)) and D(k) = L(k, k) - (L(k, 0) t_0 +
+//     ...); step j here applies term j of every such chain at once (L(i, c) -= L(i, j) (D(j) L(c, j)), i > c > j;
+//     dot_c += L(c, j) (D(j) L(c, j))), the same operations in the same order per entry.  Per step only the live
+//     trailing triangle is touched (its entries dealt to the threads by row group and column lane), and the entries
+//     of the next column are updated, divided and published in the same step, so one barrier separates the steps.
+//     (The round-1 form kept 16-column row segments in registers with two barriers per step: every segment paid its
+//     predicated FP64 updates each step, 188 us at n = 114 against this form's 130 us.)
 // The triangular solves then run on wave 0 alone, the vector in registers, broadcasts by v_readlane.
 constexpr int kLdltMaxN = 120;
-constexpr int kLdltThreads = 512;
-constexpr int kLdltSeg = 16;
+
+#ifndef YAVO_LDLT_THREADS
+#define YAVO_LDLT_THREADS 1024  // 256 / 512 / 1024 threads: 184 / 138 / 123 us per factorisation at n = 114
+#endif
+constexpr int kLdltThreads = YAVO_LDLT_THREADS;
 
 __device__ __forceinline__ int tri(int i, int j) { return (i * (i + 1) >> 1) + j; }
+
+// the row of packed lower-triangle index e: the largest q with q (q + 1) / 2 <= e (e < 2^20)
+__device__ __forceinline__ int tri_row(int e) {
+    int q = (int)((sqrtf(8.f * (float)e + 1.f) - 1.f) * 0.5f);
+    if (((q + 1) * (q + 2) >> 1) <= e) ++q;
+    if ((q * (q + 1) >> 1) > e) --q;
+    return q;
+}
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
     const long long b = __double_as_longlong(v);
@@ -401,16 +414,28 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#ifdef YAVO_LM_PROFILE
+// profiling builds: cycles of lane 0 of every wave in the LDLT's phases, summed over the launches
+__device__ unsigned long long g_ldlt_prof[kLdltThreads / 64][8];
+#define LDP_DECL unsigned long long ldp_t = __builtin_readcyclecounter(), ldp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define LDP_MARK(k) do { const unsigned long long t_ = __builtin_readcyclecounter(); ldp_acc[k] += t_ - ldp_t; ldp_t = t_; } while (0)
+#define LDP_STORE() do { if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 8; ++q_) atomicAdd(&g_ldlt_prof[threadIdx.x >> 6][q_], ldp_acc[q_]); } while (0)
+#else
+#define LDP_DECL
+#define LDP_MARK(k) do {} while (0)
+#define LDP_STORE() do {} while (0)
+#endif
 __global__ __launch_bounds__(kLdltThreads) void ba_ldlt_lds_kernel(BaParams P) {
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     __shared__ double Ls[kLdltMaxN * (kLdltMaxN + 1) / 2];  // the factor, for the solves
-    __shared__ double colk[kLdltMaxN];  // L(i, k) of the current step
-    __shared__ __attribute__((aligned(16))) double tc[kLdltMaxN];  // t_i = D(k) L(i, k)
+    __shared__ double tv[2][kLdltMaxN];  // t_i = D(k) L(i, k) of step k in tv[k & 1]
+    __shared__ double dor[kLdltMaxN];    // the diagonal of P S P^T
+    __shared__ double dotp[kLdltMaxN];   // row i's diagonal chain L(i, 0) t_i(0) + ... through the last step
     __shared__ double dg[kLdltMaxN];    // |diagonal|, permuted as the pivots are taken
     __shared__ int perm[kLdltMaxN];     // position -> original index: (P S P^T)(i, j) = S(perm[i], perm[j])
-    __shared__ double s_akk;
     __shared__ int s_slow;
     const int n = P.ns, t = threadIdx.x;
+    LDP_DECL
     if (t == 0) s_slow = 0;
     for (int i = t; i < n; i += kLdltThreads) dg[i] = fabs(P.S[(int64_t)i * n + i]);
     __syncthreads();
@@ -477,104 +502,88 @@ __global__ __launch_bounds__(kLdltThreads) void ba_ldlt_lds_kernel(BaParams P) {
         for (int i = t; i < n; i += kLdltThreads) perm[i] = i == 0 ? big0 : (i == big0 ? 0 : i);
         __syncthreads();
     }
-    // 2. this thread's segment of P S P^T: row my_i, columns [cb, cb + 16) below the diagonal
-    int my_i = -1, cb = 0;
-    {
-        int r = t;
-        for (int i = 1; i < n; ++i) {
-            const int nsg = (i + kLdltSeg - 1) / kLdltSeg;
-            if (r < nsg) {
-                my_i = i;
-                cb = r * kLdltSeg;
-                break;
-            }
-            r -= nsg;
-        }
+    // 2. P S P^T (lower triangle and diagonal) into LDS, packed by rows: Ls[tri(i, j)] = S(perm[i], perm[j])
+    const int ntri = n * (n + 1) / 2;
+    for (int e = t; e < ntri; e += kLdltThreads) {
+        const int i = tri_row(e);
+        Ls[e] = P.S[(int64_t)perm[i] * n + perm[e - tri(i, 0)]];
     }
-    const bool owner = my_i >= 0;
-    const bool diag_owner = owner && (my_i - 1) / kLdltSeg == cb / kLdltSeg;  // holds the row's diagonal chain
-    double L[kLdltSeg];
-    double dorig = 0.0, dotv = 0.0;
-    if (owner) {
-        const int64_t pr = (int64_t)perm[my_i] * n;
-#pragma unroll
-        for (int u = 0; u < kLdltSeg; ++u) {
-            const int c = cb + u;
-            L[u] = c < my_i ? P.S[pr + perm[c < my_i ? c : 0]] : 0.0;
-        }
-        if (diag_owner) dorig = P.S[pr + perm[my_i]];
-    }
-    if (t == 0) {
-        s_akk = a00;
-        Ls[0] = a00;  // D(0) when the factorisation runs (with brk the solve reads the untouched diagonal)
-    }
-    // the row-0 diagonal is not in any segment: with brk the solves read the original entries
     __syncthreads();
-    // 3. right-looking, unpivoted
+    for (int i = t; i < n; i += kLdltThreads) dor[i] = Ls[tri(i, i)];
+    // column 0: L(i, 0) = S(i, 0) / D(0), t_i = D(0) L(i, 0), the diagonal chains' first terms
+    if (!brk) {
+        for (int i = t + 1; i < n; i += kLdltThreads) {
+            const double l = Ls[tri(i, 0)] / a00;
+            Ls[tri(i, 0)] = l;
+            const double tt = a00 * l;
+            tv[0][i] = tt;
+            dotp[i] = l * tt;
+        }
+    }
+    __syncthreads();
+    LDP_MARK(0);
+    // 3. right-looking, unpivoted, one barrier per step.  At step k column k is final (L(i, k), t_i = D(k) L(i, k)
+    // in tv[k & 1]) and dotp[i] holds row i's diagonal chain through term k.  Every thread forms D(k + 1) = S(k+1,
+    // k+1) - dotp[k + 1]; the rows of column k + 1 apply term k to that entry, divide by D(k + 1) and publish it (the
+    // next step's input, and term k + 1 of their diagonal chain); the rest of the trailing triangle (k + 2 <= c < i)
+    // applies term k, its entries dealt to the threads in row-major order.
     int sign = 0;
+    double akk = a00;
     for (int k = 0; k < n && !brk; ++k) {
-        const double akk = s_akk;
-        const bool valid = fabs(akk) > 0;
+        const int buf = k & 1;
+        const double* tk = tv[buf];
         if (t == 0) {
             Ls[tri(k, k)] = akk;
             if (sign == 1) { if (akk < 0) sign = 3; }
             else if (sign == 2) { if (akk > 0) sign = 3; }
             else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
         }
-        // column k: divide, publish L(i, k) and t_i
-        if (owner && my_i > k && cb <= k && k < cb + kLdltSeg) {
-            const int uk = k - cb;
-            double lv = 0.0;
-#pragma unroll
-            for (int u = 0; u < kLdltSeg; ++u)
-                if (u == uk) lv = L[u];
-            const double l = valid ? lv / akk : lv;
-#pragma unroll
-            for (int u = 0; u < kLdltSeg; ++u)
-                if (u == uk) L[u] = l;
-            colk[my_i] = l;
-            tc[my_i] = akk * l;
-        }
-        __syncthreads();
-        // term k of every chain in this segment, and of the row's diagonal chain
-        if (owner && my_i > k) {
-            const double lik = colk[my_i];
-            if (cb > k && cb + kLdltSeg <= my_i) {  // the whole segment is trailing: no per-column predicate
-                double tv[kLdltSeg];
-#pragma unroll
-                for (int u = 0; u < kLdltSeg; u += 2) {
-                    const double2 q = *reinterpret_cast<const double2*>(tc + cb + u);
-                    tv[u] = q.x;
-                    tv[u + 1] = q.y;
-                }
-#pragma unroll
-                for (int u = 0; u < kLdltSeg; ++u) L[u] = L[u] - lik * tv[u];
-            } else if (cb + kLdltSeg - 1 > k) {
-#pragma unroll
-                for (int u = 0; u < kLdltSeg; ++u) {
-                    const int c = cb + u;
-                    const double tq = tc[c < kLdltMaxN ? c : 0];
-                    const double nv = L[u] - lik * tq;
-                    L[u] = (c > k && c < my_i) ? nv : L[u];
+        if (k + 1 < n) {
+            // column k + 1: row k + 2 + j on thread t with j = (t % NW) 64 + t / NW (NW waves), so the rows, and the
+            // latency of their divisions, are spread over every wave; the row's loads are issued before D(k + 1)
+            constexpr int NW = kLdltThreads / 64;
+            const int i1 = k + 2 + (t % NW) * 64 + t / NW;
+            double cx = 0.0, lk = 0.0, dp = 0.0;
+            if (i1 < n) {
+                cx = Ls[tri(i1, k + 1)];
+                lk = Ls[tri(i1, k)];
+                dp = dotp[i1];
+            }
+            const double akk1 = dor[k + 1] - dotp[k + 1];
+            const bool v1 = fabs(akk1) > 0;
+            const double t1 = tk[k + 1];
+            LDP_MARK(1);
+            if (i1 < n) {
+                const double acc = cx - lk * t1;
+                const double l = v1 ? acc / akk1 : acc;
+                Ls[tri(i1, k + 1)] = l;
+                const double tt = akk1 * l;
+                tv[buf ^ 1][i1] = tt;
+                dotp[i1] = dp + l * tt;
+            }
+            LDP_MARK(2);
+            // the rest of the trailing triangle, k + 2 <= c < i: thread (row group t >> 4, column lane t & 15) takes
+            // rows k + 3 + (t >> 4) + (kLdltThreads / 16) m and, in each, columns k + 2 + (t & 15) + 16 j (no index
+            // decode; a wave's 16 column lanes read consecutive entries)
+            {
+                const int rg = t >> 4, cl = t & 15;
+                for (int i = k + 3 + rg; i < n; i += kLdltThreads / 16) {
+                    const int rb = tri(i, 0);
+                    const double li = Ls[rb + k];
+                    for (int c = k + 2 + cl; c < i; c += 16) Ls[rb + c] = Ls[rb + c] - li * tk[c];
                 }
             }
-            if (diag_owner) {
-                dotv = k > 0 ? dotv + lik * tc[my_i] : lik * tc[my_i];
-                if (my_i == k + 1) s_akk = dorig - dotv;
-            }
+            akk = akk1;
+            LDP_MARK(3);
         }
         __syncthreads();
+        LDP_MARK(4);
     }
-    if (brk) sign = 0;
-    // the factor into LDS for the solves (with brk: the untouched P S P^T)
-    if (owner) {
-#pragma unroll
-        for (int u = 0; u < kLdltSeg; ++u)
-            if (cb + u < my_i) Ls[tri(my_i, cb + u)] = L[u];
-        if (brk && diag_owner) Ls[tri(my_i, my_i)] = dorig;
+    if (brk) sign = 0;  // the solves read the untouched P S P^T
+    if (t >= 64) {
+        LDP_STORE();
+        return;  // no barrier below
     }
-    __syncthreads();
-    if (t >= 64) return;  // no barrier below
     // the solves on wave 0: lane l holds positions l and l + 64
     const int q0 = t, q1 = t + 64;
     double v0 = 0.0, v1 = 0.0;
@@ -609,6 +618,8 @@ __global__ __launch_bounds__(kLdltThreads) void ba_ldlt_lds_kernel(BaParams P) {
     if (q0 < n) P.xp[brk ? q0 : perm[q0]] = v0;
     if (q1 < n) P.xp[brk ? q1 : perm[q1]] = v1;
     if (t == 0) P.scal[2] = (sign == 1 || sign == 0) ? 1.0 : 0.0;
+    LDP_MARK(5);
+    LDP_STORE();
 }
 
 // larger systems: the same steps on S in global memory
@@ -1428,3 +1439,15 @@ extern "C" int yv_ba_debug_read(yv_ba* b, int which, double* dst, int64_t count)
         return YV_ERR_HIP;
     return YV_OK;
 }
+
+#ifdef YAVO_LM_PROFILE
+// profiling builds only (lib/libyavo_prof.so): LDLT phase cycles per wave [8][8], summed since the last call (reset)
+extern "C" int yv_debug_ldlt_prof(unsigned long long* out) {
+    unsigned long long z[yavo::ba::kLdltThreads / 64 * 8] = {};
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpyFromSymbol(out, HIP_SYMBOL(yavo::ba::g_ldlt_prof), sizeof z) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(yavo::ba::g_ldlt_prof), z, sizeof z) != hipSuccess)
+        return -2;
+    return 0;
+}
+#endif
