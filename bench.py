@@ -47,8 +47,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=512,
-                    help="stereo frames per step per GPU (512: two pose-LM problems per CU, 137.7k vs 130.0k frames/s at 256)")
+    ap.add_argument("--frames", type=int, default=1024,
+                    help="stereo frames per step per GPU (1024: four pose-LM problems per CU, two rounds; r02 measured "
+                         "188k / 195k / 198k / 200k frames/s at 512 / 768 / 1024 / 1536)")
     ap.add_argument("--cpu-baseline", choices=["both", "literal", "efficient", "none"], default="both")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads of the CPU baseline (0: the usable cores, affinity capped by OMP_NUM_THREADS)")

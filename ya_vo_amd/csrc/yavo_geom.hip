@@ -814,10 +814,8 @@ __device__ bool ldlt6_solve_lds(const double* Hf, double lambda, const double* b
 // ------------------------------------------------------------------------------------------------
 // pose-only LM (g2o semantics) and GN, one workgroup per problem
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void edge_error(const double* T, const double* K, const double* X, const double* meas,
-                                           double* e) {
-    double pc[3];
-    se3_act(T, X, pc);
+// the edge's error from its camera-frame point pc = T X (computeError: K pc, projected)
+__device__ __forceinline__ void edge_error_pc(const double* pc, const double* K, const double* meas, double* e) {
     double u0 = K[0] * pc[0] + K[1] * pc[1] + K[2] * pc[2];
     double u1 = K[3] * pc[0] + K[4] * pc[1] + K[5] * pc[2];
     double u2 = K[6] * pc[0] + K[7] * pc[1] + K[8] * pc[2];
@@ -825,9 +823,16 @@ __device__ __forceinline__ void edge_error(const double* T, const double* K, con
     e[1] = meas[1] - u1 / u2;
 }
 
-__device__ __forceinline__ void edge_jacobian(const double* T, const double* K, const double* X, double* J) {
+__device__ __forceinline__ void edge_error(const double* T, const double* K, const double* X, const double* meas,
+                                           double* e) {
     double pc[3];
     se3_act(T, X, pc);
+    edge_error_pc(pc, K, meas, e);
+}
+
+// linearizeOplus's 2 x 6 Jacobian from the same pc (computeError and linearizeOplus both form T X at one estimate:
+// one evaluation serves both, the same operations)
+__device__ __forceinline__ void edge_jacobian_pc(const double* pc, const double* K, double* J) {
     double fx = K[0], fy = K[4];
     double x = pc[0], y = pc[1], z = pc[2];
     double zinv = 1.0 / (z + 1e-18);
@@ -1030,8 +1035,9 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
             nx[0] = X[3 * i]; nx[1] = X[3 * i + 1]; nx[2] = X[3 * i + 2]; nx[3] = uv[2 * i]; nx[4] = uv[2 * i + 1];
             nrob = s_robust[i];
         }
-        double e[2];
-        edge_error(T, K, xi, mi, e);
+        double e[2], pc[3];
+        se3_act(T, xi, pc);
+        edge_error_pc(pc, K, mi, e);
         const double c2 = e[0] * e[0] + e[1] * e[1];
         double w = 1.0;
         double chi = c2;
@@ -1044,7 +1050,7 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
         }
         part[27] = part[27] + chi;
         double J[12];
-        edge_jacobian(T, K, xi, J);
+        edge_jacobian_pc(pc, K, J);
         // g2o forms J^T (rho' Omega) J and -J^T (rho' Omega) e with Omega = I, i.e. products with the literal
         // 0.0 / 1.0 of Omega, and J[1] = J[6] = 0 structurally.  With finite operands those products only
         // contribute signed zeros, which cannot change a partial sum (a partial that starts at +0.0 never
@@ -1576,13 +1582,24 @@ inline int lm_grid() {
     return g;
 }
 
+// Dynamic LDS of one LM launch (YAVO_LM_LDS_PAD bytes, default 0): unused padding that caps the LM at one workgroup
+// per CU, so a CU running it keeps half of every SIMD's registers for the image kernels beside it.
+inline size_t lm_lds_pad() {
+    static const size_t p = [] {
+        const char* e = getenv("YAVO_LM_LDS_PAD");
+        return e ? (size_t)atol(e) : (size_t)0;
+    }();
+    return p;
+}
+
 template <typename... A>
 void launch_lm(int n, hipStream_t s, A... args) {
     const int g = lm_grid() > 0 && lm_grid() < n ? lm_grid() : n;
+    const size_t pad = lm_lds_pad();
     switch (lm_threads()) {
-        case 256: hipLaunchKernelGGL(pose_lm_kernel<256>, dim3(g), dim3(256), 0, s, args..., n); break;
-        case 128: hipLaunchKernelGGL(pose_lm_kernel<128>, dim3(g), dim3(128), 0, s, args..., n); break;
-        default: hipLaunchKernelGGL(pose_lm_kernel<64>, dim3(g), dim3(64), 0, s, args..., n); break;
+        case 256: hipLaunchKernelGGL(pose_lm_kernel<256>, dim3(g), dim3(256), pad, s, args..., n); break;
+        case 128: hipLaunchKernelGGL(pose_lm_kernel<128>, dim3(g), dim3(128), pad, s, args..., n); break;
+        default: hipLaunchKernelGGL(pose_lm_kernel<64>, dim3(g), dim3(64), pad, s, args..., n); break;
     }
 }
 
