@@ -48,6 +48,8 @@ struct yv_batch {
     int32_t* det_count = nullptr;
     int32_t* kp_src = nullptr;
     int32_t* kp_count = nullptr;
+    int32_t* kp_band = nullptr;     // [slot][max_kp] int4 {row, col, id, slot}: the kept keypoints by BRIEF band
+    int32_t* band_off = nullptr;    // [slot][kMaxBands + 1]
     yv_keypoint* keypoints = nullptr;
     Desc* desc = nullptr;
     uint8_t* blur = nullptr;
@@ -167,7 +169,7 @@ int dalloc(T** p, size_t count) {
 
 void batch_free(yv_batch* b) {
     if (!b) return;
-    void* ptrs[] = {b->cand_keys, b->cand_count, b->cand_seen, b->det_rc,   b->det_resp,    b->det_count, b->kp_src,
+    void* ptrs[] = {b->cand_keys, b->cand_count, b->cand_seen, b->det_rc,   b->det_resp,    b->det_count, b->kp_src, b->kp_band, b->band_off,
                     b->kp_count,  b->keypoints,  b->desc,     b->blur,        b->pairs,     b->match_key,
                     b->matches,   b->match_count, b->filtered, b->filt_count, b->staging,  b->match_dj,
                     b->match_lim, b->tracks,     b->track_K,  b->T_right,    b->edge_X,    b->edge_uv,
@@ -352,6 +354,7 @@ int yv_batch_create(yv_ctx* ctx, int max_images, int H, int W, int max_kp, int m
         max_pairs < 0 || (int64_t)H * W >= (1ll << 31))
         return YV_ERR_INVALID;
     if (W > yavo::kMaxWidth) return YV_ERR_CAPACITY;  // BRIEF stages 49 image rows in LDS
+    if (H > yavo::kBandRows * yavo::kMaxBands) return YV_ERR_CAPACITY;  // top-K's band lists
     *out = nullptr;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
     yv_batch* b = new (std::nothrow) yv_batch();
@@ -374,6 +377,8 @@ int yv_batch_create(yv_ctx* ctx, int max_images, int H, int W, int max_kp, int m
     rc |= dalloc(&b->det_count, ns);
     rc |= dalloc(&b->kp_src, ns * nk * 4);
     rc |= dalloc(&b->kp_count, ns);
+    rc |= dalloc(&b->kp_band, ns * nk * 4);
+    rc |= dalloc(&b->band_off, ns * (size_t)(yavo::kMaxBands + 1));
     rc |= dalloc(&b->keypoints, ns * nk);
     rc |= dalloc(&b->desc, ns * nk);
     rc |= dalloc(&b->blur, (size_t)max_images * (size_t)yavo::blur_image_bytes(H, W));
@@ -511,9 +516,10 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
     rc |= record_stage(b, s, run, 1);
     if (b->overlap_mode == 2) rc |= launch_deferred_after(b, s);
     yavo::launch_topk(b->cand_keys, b->cap, b->cand_count, b->cand_seen, n_images, H, W, K, keep, b->det_rc,
-                      b->det_resp, b->det_count, b->kp_src, b->kp_count, s);
+                      b->det_resp, b->det_count, b->kp_src, b->kp_count, b->kp_band, b->band_off, s);
     rc |= record_stage(b, s, run, 2);
-    yavo::launch_brief(b->blur, n_images, H, W, ctx->d_offsets, b->kp_src, b->kp_count, K, b->keypoints, b->desc, s);
+    yavo::launch_brief(b->blur, n_images, H, W, ctx->d_offsets, b->kp_src, b->kp_band, b->band_off, K, b->keypoints,
+                       b->desc, s);
     rc |= record_stage(b, s, run, 3);
     if (b->overlap_mode == 3) rc |= launch_deferred_after(b, s);
     if (b->n_pairs > 0) {
@@ -900,7 +906,7 @@ int yv_detect(yv_ctx* ctx, const uint8_t* img, int H, int W, int stride, int max
     yavo::launch_fast_harris(b->staging, 1, H, W, W, (int64_t)H * W, ctx->fast_thr, ctx->harris_eigen, b->cand_keys, b->cap,
                              b->cand_count, s);
     yavo::launch_topk(b->cand_keys, b->cap, b->cand_count, b->cand_seen, 1, H, W, b->max_kp, keep, b->det_rc, b->det_resp,
-                      b->det_count, b->kp_src, b->kp_count, s);
+                      b->det_count, b->kp_src, b->kp_count, b->kp_band, b->band_off, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
     YV_HIP(hipMemcpyAsync(ctx->h_pinned, b->det_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     YV_HIP(hipMemcpyAsync(ctx->h_pinned + 1, b->cand_seen, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -930,8 +936,10 @@ int yv_describe(yv_ctx* ctx, const uint8_t* img, int H, int W, int stride, const
     if (n > 0) YV_HIP(hipMemcpyAsync(b->det_rc, rc, sizeof(int32_t) * 2 * (size_t)n, hipMemcpyHostToDevice, s));
     YV_HIP(hipMemcpyAsync(b->det_count, ctx->h_pinned, sizeof(int32_t), hipMemcpyHostToDevice, s));
     yavo::launch_blur9(b->staging, 1, H, W, W, (int64_t)H * W, ctx->k9, b->blur, s);
-    yavo::launch_kp_boundary(b->det_rc, b->det_count, 1, H, W, b->max_kp, b->kp_src, b->kp_count, s);
-    yavo::launch_brief(b->blur, 1, H, W, ctx->d_offsets, b->kp_src, b->kp_count, b->max_kp, b->keypoints, b->desc, s);
+    yavo::launch_kp_boundary(b->det_rc, b->det_count, 1, H, W, b->max_kp, b->kp_src, b->kp_count, b->kp_band,
+                             b->band_off, s);
+    yavo::launch_brief(b->blur, 1, H, W, ctx->d_offsets, b->kp_src, b->kp_band, b->band_off, b->max_kp, b->keypoints,
+                       b->desc, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
     YV_HIP(hipMemcpyAsync(ctx->h_pinned + 2, b->kp_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     YV_HIP(hipStreamSynchronize(s));

@@ -20,6 +20,11 @@ __host__ __device__ inline double cube_cr(double t) {
 
 constexpr int kMaxKp = 4096;
 constexpr int kMaxWidth = 2048;  // image width limit (BRIEF keeps 49 rows of the blurred image in LDS)       // per-image keypoint capacity supported by the top-K / scan kernels
+// BRIEF's row bands: 32 image rows per workgroup.  top-K buckets each image's kept keypoints by band
+// (kp_band[image][max_kp] int4 {row, col, id, slot}, band b at [band_off[image][b], band_off[image][b + 1])), so a
+// BRIEF workgroup reads its band's keypoints only; H <= kBandRows * kMaxBands.
+constexpr int kBandRows = 32;
+constexpr int kMaxBands = 256;
 constexpr int kFastTileW = 64;     // FAST / blur output tile: one wave per tile row
 constexpr int kFastTileH = 56;
 // The blurred image (detect's second output, BRIEF's input) is stored with a 128-B aligned row pitch, so the
@@ -59,14 +64,15 @@ void launch_blur9(const uint8_t* imgs, int n_images, int H, int W, int stride, i
 // cand_count is copied to cand_seen and reset to 0 after it is read (ready for the next detection).
 void launch_topk(const uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, uint32_t* cand_seen, int n_images,
                  int H, int W, int max_kp, int keep, int32_t* det_rc, float* det_resp, int32_t* det_count,
-                 int32_t* kp_src, int32_t* kp_count, hipStream_t s);
+                 int32_t* kp_src, int32_t* kp_count, int32_t* kp_band, int32_t* band_off, hipStream_t s);
 // checkBoundry compaction of externally supplied points (det_rc / det_count already on the device).
 void launch_kp_boundary(const int32_t* det_rc, const int32_t* det_count, int n_images, int H, int W,
-                        int max_kp, int32_t* kp_src, int32_t* kp_count, hipStream_t s);
+                        int max_kp, int32_t* kp_src, int32_t* kp_count, int32_t* kp_band, int32_t* band_off,
+                        hipStream_t s);
 // BRIEF: one wave per keypoint, 256 tests -> 4 ballots; writes KeyPoint records + packed descriptors.
 void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t* offsets,
-                  const int32_t* kp_src, const int32_t* kp_count, int max_kp, yv_keypoint* keypoints,
-                  Desc* desc, hipStream_t s);
+                  const int32_t* kp_src, const int32_t* kp_band, const int32_t* band_off, int max_kp,
+                  yv_keypoint* keypoints, Desc* desc, hipStream_t s);
 // Pack KeyPoint records -> descriptors (host-supplied keypoints).
 void launch_pack_desc(const yv_keypoint* keypoints, const int32_t* kp_count, int n_slots, int max_kp,
                       Desc* desc, hipStream_t s);

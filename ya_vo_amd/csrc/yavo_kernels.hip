@@ -625,37 +625,67 @@ __device__ __forceinline__ bool brief_boundary(int row, int col, int H, int W) {
 }
 
 // Compacts points 0..K-1 (rc_at(i) -> int2 {row, col}) to those inside checkBoundry, keeping order;
-// kp_src[slot] = {row, col, id = input index, 0}.  Chunks of 4 * NT points, 4 consecutive per thread.
+// kp_src[slot] = {row, col, id = input index, 0}.  Chunks of 4 * NT points, 4 consecutive per thread.  The kept
+// points are also bucketed by BRIEF band (row / kBandRows): kp_band = {row, col, id, slot} grouped by band (any order
+// inside a band), band_off[b] = the first entry of band b, band_off[nb] = the count (nb = bands of H rows).  A second
+// pass recomputes the same flags and slots and places each point after its band's counter.
 template <int NT, class RcAt>
-__device__ void boundary_compact(RcAt rc_at, int K, int H, int W, int32_t* kp_src, int32_t* kp_count, int* s_tmp) {
+__device__ void boundary_compact(RcAt rc_at, int K, int H, int W, int32_t* kp_src, int32_t* kp_count,
+                                 int32_t* kp_band, int32_t* band_off, int* s_tmp, int* s_band) {
     const int tid = threadIdx.x;
+    const int nb = (H + kBandRows - 1) / kBandRows;
+    for (int b = tid; b < nb; b += NT) s_band[b] = 0;
+    __syncthreads();
     int base = 0;
-    for (int c0 = 0; c0 < K; c0 += 4 * NT) {
-        int flags[4];
-        int2 rcs[4];
-        int cnt = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        base = 0;
+        for (int c0 = 0; c0 < K; c0 += 4 * NT) {
+            int flags[4];
+            int2 rcs[4];
+            int cnt = 0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = c0 + tid * 4 + u;
-            flags[u] = 0;
-            rcs[u] = make_int2(0, 0);
-            if (i < K) {
-                rcs[u] = rc_at(i);
-                flags[u] = brief_boundary(rcs[u].x, rcs[u].y, H, W) ? 1 : 0;
+            for (int u = 0; u < 4; ++u) {
+                const int i = c0 + tid * 4 + u;
+                flags[u] = 0;
+                rcs[u] = make_int2(0, 0);
+                if (i < K) {
+                    rcs[u] = rc_at(i);
+                    flags[u] = brief_boundary(rcs[u].x, rcs[u].y, H, W) ? 1 : 0;
+                }
+                cnt += flags[u];
             }
-            cnt += flags[u];
-        }
-        int total = 0;
-        int off = base + block_excl_scan<NT>(cnt, s_tmp, &total);
+            int total = 0;
+            int off = base + block_excl_scan<NT>(cnt, s_tmp, &total);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = c0 + tid * 4 + u;
-            if (flags[u]) {
-                reinterpret_cast<int4*>(kp_src)[off] = make_int4(rcs[u].x, rcs[u].y, i, 0);
-                off++;
+            for (int u = 0; u < 4; ++u) {
+                const int i = c0 + tid * 4 + u;
+                if (flags[u]) {
+                    const int band = rcs[u].x / kBandRows;
+                    if (pass == 0) {
+                        reinterpret_cast<int4*>(kp_src)[off] = make_int4(rcs[u].x, rcs[u].y, i, 0);
+                        atomicAdd(&s_band[band], 1);
+                    } else {
+                        const int pos = atomicAdd(&s_band[band], 1);
+                        reinterpret_cast<int4*>(kp_band)[pos] = make_int4(rcs[u].x, rcs[u].y, i, off);
+                    }
+                    off++;
+                }
             }
+            base += total;
         }
-        base += total;
+        __syncthreads();
+        if (pass == 0 && tid == 0) {
+            // band counts -> first entries (the second pass's cursors) and the offsets table
+            int acc = 0;
+            for (int b = 0; b < nb; ++b) {
+                const int c = s_band[b];
+                s_band[b] = acc;
+                band_off[b] = acc;
+                acc += c;
+            }
+            band_off[nb] = acc;
+        }
+        __syncthreads();
     }
     if (tid == 0) *kp_count = base;
 }
@@ -670,10 +700,12 @@ __global__ __launch_bounds__(NT) void topk_kernel(const uint64_t* __restrict__ c
                                                      uint32_t* __restrict__ cand_count, uint32_t* __restrict__ cand_seen,
                                                      int H, int W, int max_kp, int keep, int32_t* __restrict__ det_rc,
                                                      float* __restrict__ det_resp, int32_t* __restrict__ det_count,
-                                                     int32_t* __restrict__ kp_src, int32_t* __restrict__ kp_count) {
+                                                     int32_t* __restrict__ kp_src, int32_t* __restrict__ kp_count,
+                                                     int32_t* __restrict__ kp_band, int32_t* __restrict__ band_off) {
     __shared__ uint64_t s_keys[kMaxKp];
     __shared__ uint32_t s_hist[256];
     __shared__ int s_tmp[40];
+    __shared__ int s_band[kMaxBands];
     __shared__ uint64_t s_prefix, s_mask;
     __shared__ int s_krem, s_done, s_n;
 
@@ -693,6 +725,8 @@ __global__ __launch_bounds__(NT) void topk_kernel(const uint64_t* __restrict__ c
     float* resp_out = det_resp + (int64_t)img * max_kp;
 
     if (K == 0) {  // no corners (or max_kp == 0): nothing to select
+        const int nb = (H + kBandRows - 1) / kBandRows;
+        for (int b = tid; b <= nb; b += NT) band_off[(int64_t)img * (kMaxBands + 1) + b] = 0;
         if (tid == 0) { det_count[img] = 0; kp_count[img] = 0; }
         return;
     }
@@ -779,33 +813,38 @@ __global__ __launch_bounds__(NT) void topk_kernel(const uint64_t* __restrict__ c
         const uint32_t row = idx / Wu;
         return make_int2((int)row, (int)(idx - row * Wu));
     };
-    boundary_compact<NT>(rc_from_lds, K, H, W, kp_src + (int64_t)img * max_kp * 4, kp_count + img, s_tmp);
+    boundary_compact<NT>(rc_from_lds, K, H, W, kp_src + (int64_t)img * max_kp * 4, kp_count + img,
+                         kp_band + (int64_t)img * max_kp * 4, band_off + (int64_t)img * (kMaxBands + 1), s_tmp, s_band);
 }
 
 __global__ __launch_bounds__(TK_NT) void kp_boundary_kernel(const int32_t* __restrict__ det_rc,
                                                             const int32_t* __restrict__ det_count, int H, int W,
                                                             int max_kp, int32_t* __restrict__ kp_src,
-                                                            int32_t* __restrict__ kp_count) {
+                                                            int32_t* __restrict__ kp_count, int32_t* __restrict__ kp_band,
+                                                            int32_t* __restrict__ band_off) {
     __shared__ int s_tmp[40];
+    __shared__ int s_band[kMaxBands];
     const int img = blockIdx.x;
     int K = det_count[img];
     if (K > max_kp) K = max_kp;
     const int32_t* rc = det_rc + (int64_t)img * max_kp * 2;
     auto rc_from_global = [&](int i) -> int2 { return make_int2(rc[2 * i], rc[2 * i + 1]); };
-    boundary_compact<TK_NT>(rc_from_global, K, H, W, kp_src + (int64_t)img * max_kp * 4, kp_count + img, s_tmp);
+    boundary_compact<TK_NT>(rc_from_global, K, H, W, kp_src + (int64_t)img * max_kp * 4, kp_count + img,
+                            kp_band + (int64_t)img * max_kp * 4, band_off + (int64_t)img * (kMaxBands + 1), s_tmp,
+                            s_band);
 }
 
 void launch_topk(const uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, uint32_t* cand_seen, int n_images,
                  int H, int W, int max_kp, int keep, int32_t* det_rc, float* det_resp, int32_t* det_count, int32_t* kp_src,
-                 int32_t* kp_count, hipStream_t s) {
+                 int32_t* kp_count, int32_t* kp_band, int32_t* band_off, hipStream_t s) {
     hipLaunchKernelGGL(topk_kernel<TK_SEL_NT>, dim3(n_images), dim3(TK_SEL_NT), 0, s, cand_keys, cap, cand_count,
-                       cand_seen, H, W, max_kp, keep, det_rc, det_resp, det_count, kp_src, kp_count);
+                       cand_seen, H, W, max_kp, keep, det_rc, det_resp, det_count, kp_src, kp_count, kp_band, band_off);
 }
 
 void launch_kp_boundary(const int32_t* det_rc, const int32_t* det_count, int n_images, int H, int W, int max_kp,
-                        int32_t* kp_src, int32_t* kp_count, hipStream_t s) {
+                        int32_t* kp_src, int32_t* kp_count, int32_t* kp_band, int32_t* band_off, hipStream_t s) {
     hipLaunchKernelGGL(kp_boundary_kernel, dim3(n_images), dim3(TK_NT), 0, s, det_rc, det_count, H, W, max_kp,
-                       kp_src, kp_count);
+                       kp_src, kp_count, kp_band, band_off);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -838,7 +877,7 @@ __device__ __forceinline__ uint32_t reg_select(const uint32_t (&v)[N], int idx) 
 // LDS column W of each row the next row's first pixel, and zero rows past the image: every sample is then
 // s_band[(row + dr - (r0 - 8)) * LS + col + dc] with no test.  One wave per keypoint: lane l evaluates tests l,
 // l + 64, l + 128, l + 192 -> 4 ballots = 256 bits.
-constexpr int BR_BAND = 32;
+constexpr int BR_BAND = kBandRows;
 constexpr int BR_ROWS = BR_BAND + 17;  // rows r0-8 .. r0+40 (the last one for the wrap of col + 8 == W)
 // 16 waves share one staged band: the ~61 KB band limits a CU to 2 workgroups, so the workgroup is as wide as
 // the 64-VGPR budget of 8 waves per SIMD allows
@@ -851,7 +890,8 @@ constexpr int BR_NW = BR_NT / 64;
 __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict__ blur, int H, int W,
                                                     const int8_t* __restrict__ offsets,
                                                     const int32_t* __restrict__ kp_src,
-                                                    const int32_t* __restrict__ kp_count, int max_kp,
+                                                    const int32_t* __restrict__ kp_band,
+                                                    const int32_t* __restrict__ band_off, int max_kp,
                                                     yv_keypoint* __restrict__ keypoints, Desc* __restrict__ desc) {
     extern __shared__ uint8_t s_band[];  // BR_ROWS * brief_lds_stride(W) bytes
     // this band's keypoints, packed (index << 16) | (col << 5) | (row - r0): index < 4096, col < 2048, 32-row band
@@ -862,23 +902,24 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
     const int nbands = (H + BR_BAND - 1) / BR_BAND;
     const int lb = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
     const int img = lb / nbands;
-    const int r0 = (lb - img * nbands) * BR_BAND;
+    const int band = lb - img * nbands;
+    const int r0 = band * BR_BAND;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int n = kp_count[img];
     const int4* src = reinterpret_cast<const int4*>(kp_src) + (int64_t)img * max_kp;
-    if (tid == 0) s_n = 0;
-    // Every global load of the workgroup is issued up front, in this order: the keypoint list (n <= 4096 = 4 per
-    // thread), then the band (<= 4 16-B words per thread).  vmcnt retires loads in order, so the list scan below waits
-    // only for the list while the band's loads stay in flight behind it; the band goes to LDS after the scan.
-    int2 kq[4];
+    // this band's keypoints, bucketed by top-K (kp_band {row, col, id, slot}, band_off): the workgroup reads its own
+    // ~K / bands records, not the image's whole list
+    const int32_t* bo = band_off + (int64_t)img * (kMaxBands + 1);
+    const int lo = bo[band], nbk = bo[band + 1] - lo;
+    const int4* kb = reinterpret_cast<const int4*>(kp_band) + (int64_t)img * max_kp + lo;
+    // Every global load of the workgroup is issued up front, in this order: the band's keypoint records (<= 4096 = 4
+    // per thread), then the band (<= 4 16-B words per thread).  vmcnt retires loads in order, so the list packing
+    // below waits only for the records while the band's loads stay in flight behind it.
+    int4 kq[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int i = u * BR_NT + tid;
-        kq[u] = make_int2(-1, 0);
-        if (i < n) {
-            const int4 k4 = src[i];
-            kq[u] = make_int2(k4.x, k4.y);
-        }
+        const int j = u * BR_NT + tid;
+        kq[u] = make_int4(0, 0, 0, 0);
+        if (j < nbk) kq[u] = kb[j];
     }
     // band: rows rb .. rb + BR_ROWS - 1 (rb = r0 - 8) of the pitched blurred image as 16-B words, LS bytes per row
     // (LS <= the pitch: inside the row); column W of row r is patched with pixel (r + 1, 0) (0 past the image), rows
@@ -903,20 +944,13 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
             if (q == kw_fix && r + 1 < H) nx[u] = (uint32_t)b[(int64_t)(r + 1) * bp];
         }
     }
-    __syncthreads();  // s_n = 0
-    // 1. this band's keypoints (any order: each keypoint's outputs go to its own index)
+    // 1. this band's keypoints (any order: each keypoint's outputs go to its own slot)
+    if (tid == 0) s_n = nbk;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int i = u * BR_NT + tid;
-        const int row = kq[u].x;
-        const bool mine = i < n && row >= r0 && row < r0 + BR_BAND;
-        const uint64_t bal = __ballot(mine);
-        int wbase = 0;
-        if (lane == 0 && bal) wbase = atomicAdd(&s_n, (int)__popcll(bal));
-        wbase = __shfl(wbase, 0, 64);
-        if (mine)
-            s_list[wbase + (int)__popcll(bal & ((1ull << lane) - 1))] =
-                ((uint32_t)i << 16) | ((uint32_t)kq[u].y << 5) | (uint32_t)(row - r0);
+        const int j = u * BR_NT + tid;
+        if (j < nbk)
+            s_list[j] = ((uint32_t)kq[u].w << 16) | ((uint32_t)kq[u].y << 5) | (uint32_t)(kq[u].x - r0);
     }
     // 2. the band to LDS (the word holding column W takes the next row's first pixel)
     uint4* s4 = reinterpret_cast<uint4*>(s_band);
@@ -1033,10 +1067,11 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
 }
 
 void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t* offsets, const int32_t* kp_src,
-                  const int32_t* kp_count, int max_kp, yv_keypoint* keypoints, Desc* desc, hipStream_t s) {
+                  const int32_t* kp_band, const int32_t* band_off, int max_kp, yv_keypoint* keypoints, Desc* desc,
+                  hipStream_t s) {
     dim3 grid(((H + BR_BAND - 1) / BR_BAND) * n_images);
     const size_t lds = (size_t)BR_ROWS * brief_lds_stride(W);
-    hipLaunchKernelGGL(brief_kernel, grid, dim3(BR_NT), lds, s, blur, H, W, offsets, kp_src, kp_count, max_kp,
+    hipLaunchKernelGGL(brief_kernel, grid, dim3(BR_NT), lds, s, blur, H, W, offsets, kp_src, kp_band, band_off, max_kp,
                        keypoints, desc);
 }
 
