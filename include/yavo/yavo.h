@@ -95,7 +95,8 @@ int yv_filter_matches(yv_ctx* ctx, const yv_match* in, int n, int thr, yv_match*
 /* ---- batched device pipeline (inputs resident in HBM) ---------------------------------------------- */
 /* A batch owns device workspace for up to max_images images of H x W and max_pairs match pairs.  Slot
  * index max_images is the "carry" slot: it holds the keypoints / descriptors of one image of the
- * previous run (see yv_batch_run's carry_from), so consecutive runs chain frame k-1 -> k. */
+ * previous run (see yv_batch_run's carry_from), so consecutive runs chain frame k-1 -> k.  YV_ERR_CAPACITY for
+ * W > 2048 (BRIEF stages 49 image rows in LDS) or H > 8192 (top-K's per-band keypoint lists). */
 int yv_batch_create(yv_ctx* ctx, int max_images, int H, int W, int max_kp, int max_pairs,
                     yv_batch** out);
 void yv_batch_destroy(yv_batch* b);
