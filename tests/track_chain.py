@@ -34,9 +34,23 @@ def _tick(timers, key, t0):
     return t
 
 
-def track_edges(orc, kq, kl, kr, K, T_right, thr=20, timers=None):
+def f_ransac_seconds(orc, matches, iters=400, thr=0.1, seed=0):
+    """Seconds of the oracle's getFRANSAC (src/3DHandler.cc:145-195: `iters` hypotheses of 8 draws with replacement,
+    |p2^T F p1| < thr) on a kept match list: the reference runs it at (re)initialisation (buildInitMap /
+    reinitialize, src/LoopHandler.cc:225,567), not per tracked frame."""
+    if len(matches) < 8:
+        return 0.0
+    samples = np.random.default_rng(seed).integers(0, len(matches), (iters, 8)).astype(np.int32)
+    t0 = time.perf_counter()
+    orc.f_ransac(matches, samples, thr)
+    return time.perf_counter() - t0
+
+
+def track_edges(orc, kq, kl, kr, K, T_right, thr=20, timers=None, init_timers=None):
     """Edges of one track -> (X [n,3], uv [n,2], query index [n]).  timers: optional dict of per-stage seconds
-    ("match": matchFeatures + removeOutliers of both pairs, "triangulate": the stereo triangulation)."""
+    ("match": matchFeatures + removeOutliers of both pairs, "triangulate": the stereo triangulation).  init_timers:
+    optional dict that gets "f_ransac", the (re)initialisation stage timed on this track's kept temporal matches
+    (outside `timers`)."""
     if len(kq) == 0:
         return np.zeros((0, 3)), np.zeros((0, 2)), np.zeros(0, np.int32)
     t0 = time.perf_counter()
@@ -44,6 +58,9 @@ def track_edges(orc, kq, kl, kr, K, T_right, thr=20, timers=None):
     ms = orc.match(kl, kr) if len(kl) else np.zeros(0, MATCH_DTYPE)
     kt, ks = kept_flags(orc, mt, thr), kept_flags(orc, ms, thr)
     t0 = _tick(timers, "match", t0)
+    if init_timers is not None:
+        init_timers["f_ransac"] = init_timers.get("f_ransac", 0.0) + f_ransac_seconds(orc, mt[kt])
+        t0 = time.perf_counter()
     l_index = {int(i): j for j, i in enumerate(kl["id"].tolist())}
     cand, recs = [], []
     for i in range(len(kq)):
@@ -63,12 +80,12 @@ def track_edges(orc, kq, kl, kr, K, T_right, thr=20, timers=None):
     return X[ok], uv, q
 
 
-def track_pose(orc, kq, kl, kr, K, T_right, prior=IDENTITY, thr=20, sum_mode=None, timers=None):
+def track_pose(orc, kq, kl, kr, K, T_right, prior=IDENTITY, thr=20, sum_mode=None, timers=None, init_timers=None):
     """track_edges + optimizePoseOnly in `sum_mode` (None: the GPU kernel's order; 0: the reference's sequential
-    order).  timers: as track_edges, plus "pose_lm"."""
+    order).  timers: as track_edges, plus "pose_lm"; init_timers: as track_edges."""
     if sum_mode is None:
         sum_mode = lm_sum_mode()
-    X, uv, q = track_edges(orc, kq, kl, kr, K, T_right, thr, timers)
+    X, uv, q = track_edges(orc, kq, kl, kr, K, T_right, thr, timers, init_timers)
     t0 = time.perf_counter()
     T, out, inl = orc.pose_lm(X, uv, K, prior, sum_mode)
     _tick(timers, "pose_lm", t0)
