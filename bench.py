@@ -58,8 +58,9 @@ def parse():
     ap.add_argument("--stage-steps", type=int, default=5,
                     help="steps of the separate per-stage pass after the timed region (events around every stage)")
     ap.add_argument("--no-overlap", action="store_true", help="run the pose LM in order on the main stream")
-    ap.add_argument("--overlap-mode", type=int, default=1, choices=[1, 2, 3],
-                    help="pose LM beside the next step: 1 after the edge build, 2 / 3 after the next detect / describe")
+    ap.add_argument("--overlap-mode", type=int, default=1, choices=[1, 2, 3, 4],
+                    help="pose LM beside the next step: 1 after the edge build, 2 / 3 / 4 after the next detect / "
+                         "describe / top-K")
     ap.add_argument("--tracker", choices=["match", "lk"], default="match",
                     help="PnP correspondences: BRIEF temporal matches (default) or calcOpticalFlowPyrLK of frame "
                          "k-1's stereo map points (the reference's trackLastFrame)")

@@ -483,8 +483,8 @@ class Batch:
 
     def set_track_overlap(self, on=True) -> None:
         """Run each track's pose LM on the batch's own stream beside the next run (yv_batch_set_track_overlap):
-        True / 1 after the edge build, 2 / 3 deferred until the next run's detect / describe stage, False / 0 in
-        order."""
+        True / 1 after the edge build, 2 / 3 / 4 deferred until the next run's detect / describe / top-K stage,
+        False / 0 in order."""
         mode = int(on) if not isinstance(on, bool) else (1 if on else 0)
         _check(self.lib.yv_batch_set_track_overlap(self.handle, mode), "yv_batch_set_track_overlap")
 

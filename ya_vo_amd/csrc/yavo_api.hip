@@ -35,6 +35,10 @@ int ctx_device(yv_ctx* ctx) { return ctx->device; }
 hipStream_t ctx_stream(yv_ctx* ctx) { return ctx->stream; }
 }  // namespace yavo
 
+// Track edge buffers in flight: the build of track i + kEdgeBufs waits for the pose LM of track i (side stream), so
+// an LM deferred into the next run (overlap modes 2-4) does not hold up the next build.
+constexpr int kEdgeBufs = 3;
+
 struct yv_batch {
     yv_ctx* ctx = nullptr;
     int max_images = 0, H = 0, W = 0, max_kp = 0, max_pairs = 0, n_pairs = 0;
@@ -96,7 +100,7 @@ struct yv_batch {
     int tbuf = 0;                   // buffer of the last yv_batch_track
     int track_calls = 0;
     bool overlap = false;           // LM on the side stream
-    int overlap_mode = 0;           // 1: LM after the edge build; 2 / 3: after the next run's detect / describe
+    int overlap_mode = 0;           // 1: LM after the edge build; 2 / 3 / 4: after the next run's detect / describe / top-K
     struct DeferredLM {              // overlap modes 2 / 3: an LM launch waiting for the next yv_batch_run
         bool active = false;
         int k = 0, run = -1;
@@ -110,8 +114,8 @@ struct yv_batch {
     } deferred;
     hipEvent_t ev_defer = nullptr;
     hipStream_t side = nullptr;
-    hipEvent_t ev_edges[2] = {nullptr, nullptr}, ev_lm[2] = {nullptr, nullptr};
-    bool lm_pending[2] = {false, false};
+    hipEvent_t ev_edges[kEdgeBufs] = {}, ev_lm[kEdgeBufs] = {};
+    bool lm_pending[kEdgeBufs] = {};
     hipEvent_t ev_map = nullptr;    // after the last yv_batch_track_map's block (yv_batch_map_wait)
     bool map_written = false;
     hipEvent_t ev_map_release = nullptr;  // the block's readers (yv_batch_map_release): the next block write waits
@@ -183,7 +187,7 @@ void batch_free(yv_batch* b) {
         if (p) (void)hipFree(p);
     if (b->lk) yv_lk_destroy(b->lk);
     for (hipEvent_t e : b->events) (void)hipEventDestroy(e);
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < kEdgeBufs; ++k) {
         if (b->ev_edges[k]) (void)hipEventDestroy(b->ev_edges[k]);
         if (b->ev_lm[k]) (void)hipEventDestroy(b->ev_lm[k]);
     }
@@ -518,10 +522,11 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
     yavo::launch_topk(b->cand_keys, b->cap, b->cand_count, b->cand_seen, n_images, H, W, K, keep, b->det_rc,
                       b->det_resp, b->det_count, b->kp_src, b->kp_count, b->kp_band, b->band_off, s);
     rc |= record_stage(b, s, run, 2);
+    if (b->overlap_mode == 4) rc |= launch_deferred_after(b, s);  // after top-K
     yavo::launch_brief(b->blur, n_images, H, W, ctx->d_offsets, b->kp_src, b->kp_band, b->band_off, K, b->keypoints,
                        b->desc, s);
     rc |= record_stage(b, s, run, 3);
-    if (b->overlap_mode == 3) rc |= launch_deferred_after(b, s);
+    if (b->overlap_mode == 3) rc |= launch_deferred_after(b, s);  // after describe
     if (b->n_pairs > 0) {
         yavo::launch_match(b->desc, b->kp_count, b->pairs, b->n_pairs, K, K, b->match_key, s);
         rc |= record_stage(b, s, run, 4);
@@ -613,12 +618,12 @@ int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks, int n_tracks, const 
         rc |= dalloc(&b->tracks, 2 * nt);
         rc |= dalloc(&b->track_K, 9 * nt);
         rc |= dalloc(&b->T_right, 7);
-        rc |= dalloc(&b->edge_X, 2 * 3 * nt * nk);
-        rc |= dalloc(&b->edge_uv, 2 * 2 * nt * nk);
-        rc |= dalloc(&b->edge_query, 2 * nt * nk);
-        rc |= dalloc(&b->edge_count, 2 * nt);
-        rc |= dalloc(&b->edge_outlier, 2 * nt * nk);
-        rc |= dalloc(&b->track_inliers, 2 * nt);
+        rc |= dalloc(&b->edge_X, kEdgeBufs * 3 * nt * nk);
+        rc |= dalloc(&b->edge_uv, kEdgeBufs * 2 * nt * nk);
+        rc |= dalloc(&b->edge_query, kEdgeBufs * nt * nk);
+        rc |= dalloc(&b->edge_count, kEdgeBufs * nt);
+        rc |= dalloc(&b->edge_outlier, kEdgeBufs * nt * nk);
+        rc |= dalloc(&b->track_inliers, kEdgeBufs * nt);
         void* lk_old[] = {b->lk_sp, b->lk_pairs, b->lk_X, b->lk_pts, b->lk_next, b->lk_err, b->lk_status, b->lk_q,
                           b->lk_count};
         for (void* p : lk_old)
@@ -645,7 +650,7 @@ int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks, int n_tracks, const 
         YV_HIP(hipMemcpyAsync(b->tracks, tracks, 2 * sizeof(int32_t) * (size_t)n_tracks, hipMemcpyHostToDevice, s));
         YV_HIP(hipMemcpyAsync(b->track_K, Ks.data(), Ks.size() * sizeof(double), hipMemcpyHostToDevice, s));
         YV_HIP(hipMemcpyAsync(b->T_right, T_right, 7 * sizeof(double), hipMemcpyHostToDevice, s));
-        YV_HIP(hipMemsetAsync(b->edge_count, 0, 2 * sizeof(int32_t) * (size_t)b->max_tracks, s));
+        YV_HIP(hipMemsetAsync(b->edge_count, 0, kEdgeBufs * sizeof(int32_t) * (size_t)b->max_tracks, s));
         if (b->lk_step > 0) {
             std::vector<int32_t> sp(n_tracks), lp(2 * (size_t)n_tracks);
             for (int t = 0; t < n_tracks; ++t) {
@@ -772,7 +777,7 @@ int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stre
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->ctx->stream;
     if (flush_deferred(b) != YV_OK) return YV_ERR_HIP;  // two tracks without a run between them
-    const int k = b->track_calls++ & 1;
+    const int k = b->track_calls++ % kEdgeBufs;
     const size_t nt = (size_t)b->max_tracks, nk = (size_t)b->max_kp;
     double* eX = b->edge_X + k * nt * nk * 3;
     double* euv = b->edge_uv + k * nt * nk * 2;
@@ -831,7 +836,7 @@ int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stre
 }  // namespace
 
 int yv_batch_set_track_overlap(yv_batch* b, int on) {
-    if (!b || on < 0 || on > 3) return YV_ERR_INVALID;
+    if (!b || on < 0 || on > 4) return YV_ERR_INVALID;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
     if (flush_deferred(b) != YV_OK) return YV_ERR_HIP;
     if (on && !b->side) {
@@ -839,7 +844,7 @@ int yv_batch_set_track_overlap(yv_batch* b, int on) {
         int least = 0, greatest = 0;
         YV_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
         YV_HIP(hipStreamCreateWithPriority(&b->side, hipStreamNonBlocking, least));
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kEdgeBufs; ++k) {
             YV_HIP(hipEventCreateWithFlags(&b->ev_edges[k], hipEventDisableTiming));
             YV_HIP(hipEventCreateWithFlags(&b->ev_lm[k], hipEventDisableTiming));
         }
