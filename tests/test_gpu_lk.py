@@ -12,6 +12,16 @@ pytestmark = pytest.mark.gpu
 LK_TOL = 1e-2  # px, GPU vs OpenCV's scalar summation order
 
 
+def _d2h(ptr, shape, dtype):
+    """Copy device memory at a raw pointer (already complete) into a new host array (hipMemcpy D2H)."""
+    import ctypes
+    out = np.empty(shape, dtype)
+    hip = ctypes.CDLL("libamdhip64.so")
+    rc = hip.hipMemcpy(ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(ptr), ctypes.c_size_t(out.nbytes), 2)
+    assert rc == 0, f"hipMemcpy {rc}"
+    return out
+
+
 def _pts(rng, n, H, W, margin=-20):
     return np.stack([rng.uniform(margin, W - 1 - margin, n), rng.uniform(margin, H - 1 - margin, n)], 1).astype(np.float32)
 
@@ -74,4 +84,33 @@ def test_lk_batch_pairs(ctx, oracle):
         np.testing.assert_array_equal(gs[p, :n], os_)
         np.testing.assert_array_equal(g[p, :n], o)
         np.testing.assert_array_equal(ge[p, :n], oe)
+    lk.close()
+
+
+@pytest.mark.parametrize("H,W,stride,n_img,win", [(376, 1241, 1241, 2, 11), (376, 1241, 1299, 1, 11),
+                                                   (121, 203, 205, 3, 3), (37, 61, 61, 2, 3), (9, 13, 14, 2, 3),
+                                                   (64, 1, 1, 1, 3), (1, 40, 40, 1, 3)])
+def test_lk_pyramid_and_derivatives_match_oracle(ctx, oracle, H, W, stride, n_img, win):
+    """Every level's pyrDown image and Scharr derivatives (yv_lk_level) byte for byte against the oracle, on noise
+    images with odd sizes and strides (the border columns and rows take the reflected path)."""
+    import torch
+    rng = np.random.default_rng(H * 7 + W)
+    pitch = stride * H + 3
+    flat = rng.integers(0, 256, pitch * n_img, dtype=np.uint8)
+    d_flat = torch.from_numpy(flat).to("cuda:0")
+    lk = yv.Lk(ctx, n_img, H, W, win=win)
+    lk.build(d_flat.data_ptr(), n_img, stride, pitch)
+    ctx.sync()
+    torch.cuda.synchronize()
+    for i in range(n_img):
+        ref = np.lib.stride_tricks.as_strided(flat[i * pitch:], (H, W), (stride, 1)).copy()
+        for lvl in range(lk.levels + 1):
+            d_img, st, d_der, dst, h, w = lk.level(i, lvl)
+            assert (h, w) == ref.shape
+            if lvl > 0:
+                got = _d2h(d_img, (h, st), np.uint8)[:, :w]
+                np.testing.assert_array_equal(got, ref, err_msg=f"level {lvl} image {i}")
+            np.testing.assert_array_equal(_d2h(d_der, (h, dst, 2), np.int16)[:, :w], oracle.scharr(ref),
+                                          err_msg=f"derivatives level {lvl} image {i}")
+            ref = oracle.pyr_down(ref)
     lk.close()

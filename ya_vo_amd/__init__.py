@@ -106,6 +106,8 @@ GEOM_SIGNATURES = {
     "yv_lk_create": (_I, [_P, _I, _I, _I, _I, _I, ctypes.POINTER(_P)]),
     "yv_lk_destroy": (None, [_P]),
     "yv_lk_levels": (_I, [_P]),
+    "yv_lk_level": (_I, [_P, _I, _I, ctypes.POINTER(_P), ctypes.POINTER(_I), ctypes.POINTER(_P), ctypes.POINTER(_I),
+                         ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "yv_lk_build": (_I, [_P, _P, _I, _I, ctypes.c_int64, _P]),
     "yv_lk_track_batch": (_I, [_P, _P, _I, _P, _P, _I, _I, _D, _D, _P, _P, _P, _P]),
     "yv_calc_optical_flow_pyr_lk": (_I, [_P, _P, _P, _I, _I, _I, _P, _I, _I, _I, _I, _D, _D, _P, _P, _P]),
@@ -538,6 +540,14 @@ class Lk:
     def build(self, d_images: int, n_images: int, stride: int, pitch: int, stream: int = 0) -> None:
         _check(self.lib.yv_lk_build(self.handle, ctypes.c_void_p(d_images), n_images, stride, pitch,
                                     ctypes.c_void_p(stream) if stream else None), "yv_lk_build")
+
+    def level(self, image: int, level: int):
+        """(d_img, img_stride, d_deriv, deriv_stride, H, W) of one pyramid level of the last build (yv_lk_level)."""
+        img, st, der, dst = ctypes.c_void_p(), ctypes.c_int(), ctypes.c_void_p(), ctypes.c_int()
+        H, W = ctypes.c_int(), ctypes.c_int()
+        _check(self.lib.yv_lk_level(self.handle, image, level, ctypes.byref(img), ctypes.byref(st), ctypes.byref(der),
+                                    ctypes.byref(dst), ctypes.byref(H), ctypes.byref(W)), "yv_lk_level")
+        return img.value, st.value, der.value, dst.value, H.value, W.value
 
     def track(self, d_pairs: int, n_pairs: int, d_pts: int, d_counts: int, pts_stride: int, d_next: int,
               d_status: int, d_err: int, max_count: int = 30, eps: float = 0.01, min_eig: float = 0.001,

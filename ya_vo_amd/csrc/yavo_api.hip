@@ -1239,6 +1239,7 @@ int yv_f_ransac_batch(yv_ctx* ctx, const yv_match* d_matches, int64_t list_strid
 struct yv_lk {
     yv_ctx* ctx = nullptr;
     int max_images = 0, H = 0, W = 0;
+    int built_images = 0;  // n_images of the last yv_lk_build
     yavo::LkParams P;
 };
 
@@ -1272,12 +1273,14 @@ int yv_lk_create(yv_ctx* ctx, int max_images, int H, int W, int win, int max_lev
     P.levels = levels;
     int64_t off = 0, doff = 0;
     for (int l = 0; l <= levels; ++l) {
+        P.ps[l] = (P.w[l] + 63) & ~63;
+        P.ds[l] = (P.w[l] + 15) & ~15;
         if (l >= 1) {
             P.off[l] = off;
-            off += ((int64_t)P.h[l] * P.w[l] + 255) & ~(int64_t)255;
+            off += ((int64_t)P.h[l] * P.ps[l] + 255) & ~(int64_t)255;
         }
         P.der_off[l] = doff;
-        doff += ((int64_t)P.h[l] * P.w[l] * 2 + 127) & ~(int64_t)127;
+        doff += ((int64_t)P.h[l] * P.ds[l] * 2 + 127) & ~(int64_t)127;
     }
     P.pyr_pitch = std::max<int64_t>(off, 256);
     P.der_pitch = doff;
@@ -1303,6 +1306,26 @@ void yv_lk_destroy(yv_lk* lk) {
 
 int yv_lk_levels(const yv_lk* lk) { return lk ? lk->P.levels : YV_ERR_INVALID; }
 
+int yv_lk_level(const yv_lk* lk, int image, int level, const uint8_t** d_img, int* img_stride,
+                const int16_t** d_deriv, int* deriv_stride, int* H, int* W) {
+    if (!lk || !lk->P.img0 || image < 0 || image >= lk->built_images || level < 0 || level > lk->P.levels ||
+        !d_img || !img_stride || !d_deriv || !deriv_stride || !H || !W)
+        return YV_ERR_INVALID;
+    const yavo::LkParams& P = lk->P;
+    if (level == 0) {
+        *d_img = P.img0 + image * P.pitch0;
+        *img_stride = P.stride0;
+    } else {
+        *d_img = P.pyr + image * P.pyr_pitch + P.off[level];
+        *img_stride = P.ps[level];
+    }
+    *d_deriv = P.der + image * P.der_pitch + P.der_off[level];  // int16 units
+    *deriv_stride = P.ds[level];
+    *H = P.h[level];
+    *W = P.w[level];
+    return YV_OK;
+}
+
 int yv_lk_build(yv_lk* lk, const uint8_t* d_images, int n_images, int stride, int64_t image_pitch, void* stream) {
     if (!lk || !d_images || n_images <= 0 || n_images > lk->max_images || stride < lk->W ||
         image_pitch < (int64_t)stride * (lk->H - 1) + lk->W)
@@ -1312,6 +1335,7 @@ int yv_lk_build(yv_lk* lk, const uint8_t* d_images, int n_images, int stride, in
     lk->P.img0 = d_images;
     lk->P.stride0 = stride;
     lk->P.pitch0 = image_pitch;
+    lk->built_images = n_images;
     yavo::launch_lk_pyramid(lk->P, n_images, s);
     return check_launch();
 }

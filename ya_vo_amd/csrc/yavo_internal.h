@@ -102,13 +102,16 @@ void launch_pose_lm(const int32_t* offsets, int n_problems, const double* X, con
 void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
                     double* poses, int32_t* iters, hipStream_t s);
 // cv::calcOpticalFlowPyrLK workspace view (yavo_lk.hip).  Level 0 is the caller's image; levels >= 1 live in
-// `pyr` ([image][pyr_pitch], level l at off[l], row stride w[l]); derivatives of every level in `der`
-// ([image][der_pitch] int16, level l at der_off[l], (dx, dy) interleaved, row stride 2 w[l]).
+// `pyr` ([image][pyr_pitch], level l at off[l], row stride ps[l] = w[l] rounded up to 64 bytes); derivatives of
+// every level in `der` ([image][der_pitch] int16, level l at der_off[l], (dx, dy) interleaved, ds[l] pixels per
+// row = w[l] rounded up to 16, i.e. 64-byte rows).  The padded rows make every store of the pyramid kernels a
+// whole aligned dword / dwordx4 of full cache lines.
 constexpr int kLkMaxLevels = 8;
 struct LkParams {
     int levels = 0, win = 11, max_count = 30;
     double eps2 = 1e-4, min_eig = 1e-3;
     int h[kLkMaxLevels] = {}, w[kLkMaxLevels] = {};
+    int ps[kLkMaxLevels] = {}, ds[kLkMaxLevels] = {};
     int64_t off[kLkMaxLevels] = {}, der_off[kLkMaxLevels] = {};
     const uint8_t* img0 = nullptr;
     int stride0 = 0;

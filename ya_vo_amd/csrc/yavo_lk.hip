@@ -2,9 +2,10 @@
 // src/LoopHandler.cc:372-375: winSize 11x11, maxLevel 3, TermCriteria(COUNT+EPS, 30, 0.01), flags 0,
 // minEigThreshold 0.001).  Restates OpenCV's lkpyramid.cpp (scalar path) like oracle/yavo_oracle_lk.c:
 //
-//   pyr_down_kernel   cv::pyrDown CV_8U, 5x5 [1 4 6 4 1]^2 / 256, BORDER_REFLECT_101 (exact integers); a
-//                     16 x 64 output tile per workgroup, its 35 x 131 source patch staged in LDS
-//   scharr_kernel     calcSharrDeriv: int16 (dx, dy), REFLECT_101 rows / columns
+//   pyr_down_kernel   cv::pyrDown CV_8U, 5x5 [1 4 6 4 1]^2 / 256, BORDER_REFLECT_101 (exact integers); 4
+//                     output pixels x 4 rows per lane, packed-u16 sums over aligned 16-byte source-row loads
+//   scharr_kernel     calcSharrDeriv: int16 (dx, dy), REFLECT_101 rows / columns; 4 pixels x 4 rows per lane,
+//                     one aligned 16-byte store per output row
 //   lk_kernel         LKTrackerInvoker for every level of one point per 16-lane DPP row (4 points per wave):
 //                     each lane owns an S x S task of the window (S = ceil(win / 4)); bilinear samples (14-bit
 //                     weights, CV_DESCALE) straight from the level images (REFLECT_101 image border, zero
@@ -30,65 +31,243 @@ __device__ __forceinline__ int refl(int p, int len) {
     return p;
 }
 
-// ------------------------------------------------------------------------------------------------
-// pyrDown
-// ------------------------------------------------------------------------------------------------
-constexpr int PD_TH = 16, PD_TW = 64;                  // output tile
-constexpr int PD_SH = 2 * PD_TH + 3, PD_SW = 2 * PD_TW + 3;  // source patch 35 x 131
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Both kernels split a level into interior lanes, which read their source columns straight from the row, and border
+// lanes (x0 = 0 and x0 >= x1), whose columns reflect.  The interior covers output columns [4, x1) in workgroups of
+// 4 waves x 256 columns; one extra workgroup column packs the border lanes 8 groups x 8 row bands per wave, so
+// the reflection's byte loads never run in an interior wave (a border lane there would make the whole wave run
+// both forms).  Inside a wave the source rows are uniform (the wave index comes through readfirstlane, so the row
+// arithmetic is scalar), and so is each row's dword misalignment: x0 is a multiple of 4.
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ u16x2 pair(uint16_t lo, uint16_t hi) {
+    u16x2 v = {lo, hi};
+    return v;
+}
+
+constexpr int kBorderGroups = 8;  // border lanes per row band: x0 = 0 and up to 7 groups at the right
+
+// ------------------------------------------------------------------------------------------------
+// pyrDown: a lane makes output pixels x0 .. x0 + 3 of PD_R output rows from source columns 2 x0 - 2 .. 2 x0 + 8 of
+// rows 2 oy - 2 .. 2 oy + 2.  Interior lanes: one aligned dwordx4 per source row, the bytes split into even / odd
+// columns as packed u16 pairs (w & 0x00FF00FF, (w >> 8) & 0x00FF00FF), the vertical [1 4 6 4 1] as packed
+// multiply-adds, the horizontal one on pairs of outputs (a sum of 16 bytes <= 65280 fits a u16 lane), rounding
+// and the byte pack in three ops.  The 5x5 sum is exact in integers, so any order gives cv::pyrDown's bytes.
+// ------------------------------------------------------------------------------------------------
+constexpr int PD_TW = 256;
+
+// interior x0 < pd_x1(W): 2 x0 + 13 < W, so the aligned 16 bytes of every source row stay inside it
+__host__ __device__ __forceinline__ int pd_x1(int W) {
+    const int xm = W >= 22 ? ((W - 14) / 2) & ~3 : 0;  // last interior x0
+    return xm >= 4 ? xm + 4 : 4;
+}
+
+template <int PD_R>
 __global__ __launch_bounds__(256) void pyr_down_kernel(const uint8_t* __restrict__ src, int H, int W, int sstride,
-                                                       int64_t spitch, uint8_t* __restrict__ dst, int64_t dpitch) {
-    __shared__ uint8_t s_src[PD_SH * PD_SW];
-    __shared__ int s_h[PD_SH * PD_TW];
+                                                       int64_t spitch, uint8_t* __restrict__ dst, int dstride,
+                                                       int64_t dpitch) {
+    constexpr int PD_SR = 2 * PD_R + 3;  // source rows per lane
     const int img = blockIdx.z;
     const int Hd = (H + 1) / 2, Wd = (W + 1) / 2;
-    const int oy0 = blockIdx.y * PD_TH, ox0 = blockIdx.x * PD_TW;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int x1 = pd_x1(W);
     const uint8_t* s = src + (int64_t)img * spitch;
-    const int sy0 = 2 * oy0 - 2, sx0 = 2 * ox0 - 2;
-    for (int i = threadIdx.x; i < PD_SH * PD_SW; i += 256) {
-        const int r = i / PD_SW, c = i - r * PD_SW;
-        const int y = refl(min(sy0 + r, 2 * H - 2), H), x = refl(min(sx0 + c, 2 * W - 2), W);
-        s_src[i] = s[(int64_t)y * sstride + x];
-    }
-    __syncthreads();
-    // horizontal: h(r, x) = src(r, 2x-2) + 4 src(r, 2x-1) + 6 src(r, 2x) + 4 src(r, 2x+1) + src(r, 2x+2)
-    for (int i = threadIdx.x; i < PD_SH * PD_TW; i += 256) {
-        const int r = i / PD_TW, x = i - r * PD_TW;
-        const uint8_t* p = s_src + r * PD_SW + 2 * x;
-        s_h[i] = p[0] + 4 * p[1] + 6 * p[2] + 4 * p[3] + p[4];
-    }
-    __syncthreads();
     uint8_t* d = dst + (int64_t)img * dpitch;
-    for (int i = threadIdx.x; i < PD_TH * PD_TW; i += 256) {
-        const int y = i / PD_TW, x = i - y * PD_TW;
-        const int oy = oy0 + y, ox = ox0 + x;
-        if (oy >= Hd || ox >= Wd) continue;
-        const int* q = s_h + (2 * y) * PD_TW + x;
-        const int acc = q[0] + 4 * q[PD_TW] + 6 * q[2 * PD_TW] + 4 * q[3 * PD_TW] + q[4 * PD_TW];
-        d[(int64_t)oy * Wd + ox] = (uint8_t)((acc + 128) >> 8);
+    if (blockIdx.x != gridDim.x - 1) {
+        const int x0 = 4 + blockIdx.x * PD_TW + lane * 4;
+        const int oy0 = (blockIdx.y * 4 + wave) * PD_R;
+        if (x0 >= x1 || oy0 >= Hd) return;
+        const int c0 = 2 * x0 - 2;
+        uint32_t raw[PD_SR][4];
+        uint32_t mis[PD_SR];
+#pragma unroll
+        for (int r = 0; r < PD_SR; ++r) {
+            const uint8_t* row = s + (int64_t)refl(min(2 * oy0 - 2 + r, 2 * H - 2), H) * sstride;
+            mis[r] = ((uint32_t)(uintptr_t)row + 2u) & 3u;  // (row + c0) & 3, c0 = 6 mod 8
+            __builtin_memcpy(raw[r], __builtin_assume_aligned(row + c0 - mis[r], 4), 16);
+        }
+        // vertical sums of even (e) / odd (o) columns: e[m] = column c0 + 4m, c0 + 4m + 2; o[m] = the next ones
+        u16x2 ve[PD_R][3], vo[PD_R][3];
+#pragma unroll
+        for (int i = 0; i < PD_R; ++i)
+#pragma unroll
+            for (int m = 0; m < 3; ++m) ve[i][m] = vo[i][m] = pair(0, 0);
+#pragma unroll
+        for (int r = 0; r < PD_SR; ++r) {
+            u16x2 e[3], o[3];
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                const uint32_t w = __builtin_amdgcn_alignbyte(raw[r][m + 1], raw[r][m], mis[r]);
+                e[m] = as_u16x2(w & 0x00FF00FFu);
+                o[m] = as_u16x2((w >> 8) & 0x00FF00FFu);
+            }
+#pragma unroll
+            for (int i = 0; i < PD_R; ++i) {
+                const int t = r - 2 * i;  // tap of source row r for output row i
+                if (t < 0 || t > 4) continue;
+                const uint16_t c = (t == 0 || t == 4) ? 1 : (t == 2 ? 6 : 4);
+#pragma unroll
+                for (int m = 0; m < 3; ++m) {
+                    ve[i][m] += e[m] * pair(c, c);
+                    vo[i][m] += o[m] * pair(c, c);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < PD_R; ++i) {
+            const int oy = oy0 + i;
+            if (oy >= Hd) break;
+            // outputs (2p, 2p + 1): e[p] + 4 o[p] + 6 e'[p] + 4 o'[p] + e[p + 1], e' = (e[p].hi, e[p + 1].lo)
+            uint32_t q[2];
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const u16x2 es = as_u16x2(__builtin_amdgcn_alignbit(as_u32(ve[i][p + 1]), as_u32(ve[i][p]), 16));
+                const u16x2 os = as_u16x2(__builtin_amdgcn_alignbit(as_u32(vo[i][p + 1]), as_u32(vo[i][p]), 16));
+                const u16x2 acc = ve[i][p] + vo[i][p] * pair(4, 4) + es * pair(6, 6) + os * pair(4, 4) +
+                                  ve[i][p + 1] + pair(128, 128);
+                q[p] = as_u32(acc) >> 8;  // bytes 0 and 2: the two outputs
+            }
+            const uint32_t packed = __builtin_amdgcn_perm(q[1], q[0], 0x06040200u);
+            // the row padding (stride >= Wd rounded up to 64) takes the bytes past Wd
+            __builtin_memcpy(__builtin_assume_aligned(d + (int64_t)oy * dstride + x0, 4), &packed, 4);
+        }
+        return;
+    }
+    // border workgroup: lane = (row band, group)
+    const int g = lane % kBorderGroups;
+    const int x0 = g == 0 ? 0 : x1 + 4 * (g - 1);
+    const int oy0 = ((blockIdx.y * 4 + wave) * (64 / kBorderGroups) + lane / kBorderGroups) * PD_R;
+    if (x0 >= Wd || oy0 >= Hd) return;
+    const int c0 = 2 * x0 - 2;
+    int v[PD_R][11];
+#pragma unroll
+    for (int i = 0; i < PD_R; ++i)
+#pragma unroll
+        for (int k = 0; k < 11; ++k) v[i][k] = 0;
+    int cols[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) cols[k] = refl(min(c0 + k, 2 * W - 2), W);
+#pragma unroll
+    for (int r = 0; r < PD_SR; ++r) {
+        const uint8_t* row = s + (int64_t)refl(min(2 * oy0 - 2 + r, 2 * H - 2), H) * sstride;
+        int b[11];
+#pragma unroll
+        for (int k = 0; k < 11; ++k) b[k] = row[cols[k]];
+#pragma unroll
+        for (int i = 0; i < PD_R; ++i) {
+            const int t = r - 2 * i;
+            if (t < 0 || t > 4) continue;
+            const int c = (t == 0 || t == 4) ? 1 : (t == 2 ? 6 : 4);
+#pragma unroll
+            for (int k = 0; k < 11; ++k) v[i][k] += c * b[k];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < PD_R; ++i) {
+        const int oy = oy0 + i;
+        if (oy >= Hd) break;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int acc = v[i][2 * j] + 4 * v[i][2 * j + 1] + 6 * v[i][2 * j + 2] + 4 * v[i][2 * j + 3] + v[i][2 * j + 4];
+            packed |= (uint32_t)((acc + 128) >> 8) << (8 * j);
+        }
+        __builtin_memcpy(__builtin_assume_aligned(d + (int64_t)oy * dstride + x0, 4), &packed, 4);
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// calcSharrDeriv
+// calcSharrDeriv: a lane makes pixels x0 .. x0 + 3 of SC_R rows from source columns x0 - 1 .. x0 + 4 of rows
+// y0 - 1 .. y0 + SC_R (interior: one aligned dwordx3 per row); the 4 (dx, dy) int16 pairs of a row leave as one
+// aligned 16-byte store (derivative rows are padded to 16 pixels).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void scharr_kernel(const uint8_t* __restrict__ src, int H, int W, int sstride,
-                                                     int64_t spitch, int16_t* __restrict__ der, int64_t dpitch) {
-    const int img = blockIdx.z;
-    const int y = blockIdx.y;
-    const uint8_t* s = src + (int64_t)img * spitch;
-    const uint8_t* s0 = s + (int64_t)refl(y - 1, H) * sstride;
-    const uint8_t* s1 = s + (int64_t)y * sstride;
-    const uint8_t* s2 = s + (int64_t)refl(y + 1, H) * sstride;
-    int16_t* d = der + (int64_t)img * dpitch + (int64_t)y * W * 2;
-    for (int x = blockIdx.x * 256 + threadIdx.x; x < W; x += gridDim.x * 256) {
-        const int xl = refl(x - 1, W), xr = refl(x + 1, W);
-        const int t0l = (s0[xl] + s2[xl]) * 3 + s1[xl] * 10, t0r = (s0[xr] + s2[xr]) * 3 + s1[xr] * 10;
-        const int t1l = s2[xl] - s0[xl], t1r = s2[xr] - s0[xr], t1c = s2[x] - s0[x];
-        const int dx = t0r - t0l, dy = (t1r + t1l) * 3 + t1c * 10;
-        d[2 * x] = (int16_t)dx;
-        d[2 * x + 1] = (int16_t)dy;
+constexpr int SC_TW = 256;
+
+// interior x0 < sc_x1(W): x0 + 10 < W, so the aligned 12 bytes of every source row stay inside it
+__host__ __device__ __forceinline__ int sc_x1(int W) {
+    const int xm = W >= 18 ? (W - 11) & ~3 : 0;
+    return xm >= 4 ? xm + 4 : 4;
+}
+
+template <int SC_R>
+__device__ __forceinline__ void scharr_rows(const int (&a)[SC_R + 2][6], int y0, int H, int x0, int dstride,
+                                            int16_t* __restrict__ d) {
+#pragma unroll
+    for (int i = 0; i < SC_R; ++i) {
+        const int y = y0 + i;
+        if (y >= H) break;
+        int t0[6], t1[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            t0[k] = (a[i][k] + a[i + 2][k]) * 3 + a[i + 1][k] * 10;
+            t1[k] = a[i + 2][k] - a[i][k];
+        }
+        uint32_t out[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int dx = t0[j + 2] - t0[j], dy = (t1[j] + t1[j + 2]) * 3 + t1[j + 1] * 10;
+            out[j] = (uint32_t)(uint16_t)dx | ((uint32_t)(uint16_t)dy << 16);
+        }
+        // pixels past W land in the row padding
+        __builtin_memcpy(__builtin_assume_aligned(d + 2 * ((int64_t)y * dstride + x0), 16), out, 16);
     }
+}
+
+template <int SC_R>
+__global__ __launch_bounds__(256) void scharr_kernel(const uint8_t* __restrict__ src, int H, int W, int sstride,
+                                                     int64_t spitch, int16_t* __restrict__ der, int dstride,
+                                                     int64_t dpitch) {
+    const int img = blockIdx.z;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int x1 = sc_x1(W);
+    const uint8_t* s = src + (int64_t)img * spitch;
+    int16_t* d = der + (int64_t)img * dpitch;
+    int a[SC_R + 2][6];  // source (y0 - 1 + r, x0 - 1 + k)
+    if (blockIdx.x != gridDim.x - 1) {
+        const int x0 = 4 + blockIdx.x * SC_TW + lane * 4;
+        const int y0 = (blockIdx.y * 4 + wave) * SC_R;
+        if (x0 >= x1 || y0 >= H) return;
+        uint32_t raw[SC_R + 2][3];
+        uint32_t mis[SC_R + 2];
+#pragma unroll
+        for (int r = 0; r < SC_R + 2; ++r) {
+            const uint8_t* row = s + (int64_t)refl(min(y0 - 1 + r, H), H) * sstride;
+            mis[r] = ((uint32_t)(uintptr_t)row + 3u) & 3u;  // (row + x0 - 1) & 3
+            __builtin_memcpy(raw[r], __builtin_assume_aligned(row + x0 - 1 - mis[r], 4), 12);
+        }
+#pragma unroll
+        for (int r = 0; r < SC_R + 2; ++r) {
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(raw[r][1], raw[r][0], mis[r]);
+            const uint32_t w1 = __builtin_amdgcn_alignbyte(raw[r][2], raw[r][1], mis[r]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) a[r][k] = (w0 >> (8 * k)) & 0xFF;
+            a[r][4] = w1 & 0xFF;
+            a[r][5] = (w1 >> 8) & 0xFF;
+        }
+        scharr_rows<SC_R>(a, y0, H, x0, dstride, d);
+        return;
+    }
+    // border workgroup: lane = (row band, group)
+    const int g = lane % kBorderGroups;
+    const int x0 = g == 0 ? 0 : x1 + 4 * (g - 1);
+    const int y0 = ((blockIdx.y * 4 + wave) * (64 / kBorderGroups) + lane / kBorderGroups) * SC_R;
+    if (x0 >= W || y0 >= H) return;
+    int cols[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) cols[k] = refl(min(x0 - 1 + k, W), W);
+#pragma unroll
+    for (int r = 0; r < SC_R + 2; ++r) {
+        const uint8_t* row = s + (int64_t)refl(min(y0 - 1 + r, H), H) * sstride;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) a[r][k] = row[cols[k]];
+    }
+    scharr_rows<SC_R>(a, y0, H, x0, dstride, d);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -106,9 +285,6 @@ __device__ __forceinline__ void weights(float a, float b, int* iw) {
     iw[2] = (int)__builtin_rintf((1.f - a) * b * (float)(1 << kWBits));
     iw[3] = (1 << kWBits) - iw[0] - iw[1] - iw[2];
 }
-
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // a * b + c with |a|, |b| < 2^23 (v_mad_i32_i24): samples are u8 / int16, weights <= 2^14
 __device__ __forceinline__ int mad24(int a, int b, int c) { return __mul24(a, b) + c; }
@@ -200,7 +376,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
         const int Wl = P.w[level], Hl = P.h[level];
         const uint8_t* I = level == 0 ? P.img0 + (int64_t)ia * P.pitch0 : P.pyr + (int64_t)ia * P.pyr_pitch + P.off[level];
         const uint8_t* J = level == 0 ? P.img0 + (int64_t)ib * P.pitch0 : P.pyr + (int64_t)ib * P.pyr_pitch + P.off[level];
-        const int sI = level == 0 ? P.stride0 : Wl;
+        const int sI = level == 0 ? P.stride0 : P.ps[level];
+        const int sD = P.ds[level];
         const uint32_t* D = reinterpret_cast<const uint32_t*>(P.der + (int64_t)ia * P.der_pitch + P.der_off[level]);
         const float scale = (float)(1. / (1 << level));
         float px = px0 * scale, py = py0 * scale;
@@ -235,7 +412,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
 #pragma unroll
             for (int i = 0; i <= S; ++i) {
                 u32x4 d;
-                __builtin_memcpy(&d, __builtin_assume_aligned(D + (uint32_t)((ipy + r0 + i) * Wl + ipx + c0), 4), 16);
+                __builtin_memcpy(&d, __builtin_assume_aligned(D + (uint32_t)((ipy + r0 + i) * sD + ipx + c0), 4), 16);
 #pragma unroll
                 for (int j = 0; j <= S; ++j) dv[i][j] = (int)d[j & 3];
             }
@@ -247,7 +424,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
                 const int y = ipy + r0 + i, x = ipx + c0 + i;
                 rin[i] = y >= 0 && y < Hl;
                 cin[i] = x >= 0 && x < Wl;
-                r[i] = min(max(y, 0), Hl - 1) * Wl;
+                r[i] = min(max(y, 0), Hl - 1) * sD;
                 c[i] = min(max(x, 0), Wl - 1);
             }
 #pragma unroll
@@ -368,23 +545,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
 }  // namespace lk
 
 void launch_lk_pyramid(const LkParams& P, int n_images, hipStream_t s) {
-    // level l (>= 1) from level l-1, then the derivatives of every level
+    constexpr int kPdR = 4, kScR = 4;  // output rows per lane
+    // level l (>= 1) from level l-1, then the derivatives of every level; each grid = the interior workgroup
+    // columns + one border column (whose workgroups cover 8x the rows: row tiles past the image return at once)
     for (int l = 1; l <= P.levels; ++l) {
         const int Hs = P.h[l - 1], Ws = P.w[l - 1];
         const uint8_t* src = l == 1 ? P.img0 : P.pyr + P.off[l - 1];
-        const int sstride = l == 1 ? P.stride0 : Ws;
+        const int sstride = l == 1 ? P.stride0 : P.ps[l - 1];
         const int64_t spitch = l == 1 ? P.pitch0 : P.pyr_pitch;
-        dim3 grid((P.w[l] + lk::PD_TW - 1) / lk::PD_TW, (P.h[l] + lk::PD_TH - 1) / lk::PD_TH, n_images);
-        hipLaunchKernelGGL(lk::pyr_down_kernel, grid, dim3(256), 0, s, src, Hs, Ws, sstride, spitch,
-                           P.pyr + P.off[l], P.pyr_pitch);
+        dim3 grid((lk::pd_x1(Ws) - 4 + lk::PD_TW - 1) / lk::PD_TW + 1, (P.h[l] + 4 * kPdR - 1) / (4 * kPdR), n_images);
+        hipLaunchKernelGGL(lk::pyr_down_kernel<kPdR>, grid, dim3(256), 0, s, src, Hs, Ws, sstride, spitch,
+                           P.pyr + P.off[l], P.ps[l], P.pyr_pitch);
     }
     for (int l = 0; l <= P.levels; ++l) {
         const uint8_t* src = l == 0 ? P.img0 : P.pyr + P.off[l];
-        const int sstride = l == 0 ? P.stride0 : P.w[l];
+        const int sstride = l == 0 ? P.stride0 : P.ps[l];
         const int64_t spitch = l == 0 ? P.pitch0 : P.pyr_pitch;
-        dim3 grid((P.w[l] + 255) / 256, P.h[l], n_images);
-        hipLaunchKernelGGL(lk::scharr_kernel, grid, dim3(256), 0, s, src, P.h[l], P.w[l], sstride, spitch,
-                           P.der + P.der_off[l], P.der_pitch);
+        dim3 grid((lk::sc_x1(P.w[l]) - 4 + lk::SC_TW - 1) / lk::SC_TW + 1, (P.h[l] + 4 * kScR - 1) / (4 * kScR),
+                  n_images);
+        hipLaunchKernelGGL(lk::scharr_kernel<kScR>, grid, dim3(256), 0, s, src, P.h[l], P.w[l], sstride, spitch,
+                           P.der + P.der_off[l], P.ds[l], P.der_pitch);
     }
 }
 
