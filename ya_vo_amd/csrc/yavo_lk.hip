@@ -289,9 +289,10 @@ __device__ __forceinline__ void weights(float a, float b, int* iw) {
 // a * b + c with |a|, |b| < 2^23 (v_mad_i32_i24): samples are u8 / int16, weights <= 2^14
 __device__ __forceinline__ int mad24(int a, int b, int c) { return __mul24(a, b) + c; }
 
+// row rotations read a lane of the same row for every lane, so no old value is needed (mov_dpp, bound_ctrl)
 template <int kCtrl>
 __device__ __forceinline__ float row_dpp(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kCtrl, 0xF, 0xF, true));
 }
 
 // Sum over a point's 16 lanes (one DPP row) in the oracle's sum_mode 1 order: the butterfly q[l] + q[l ^ off],
@@ -346,6 +347,44 @@ __device__ __forceinline__ void load_footprint(const uint8_t* __restrict__ J, in
 #pragma unroll
             for (int j = 0; j <= S; ++j) v[i][j] = J[(uint32_t)(r[i] + c[j])];
     }
+}
+
+// The footprint as horizontal pairs p[i][j] = (v[i][j], v[i][j + 1]) packed u16x2 (v_perm from the row's dword
+// inside the image), the operand form of v_dot2_u32_u16: the bilinear sum w0 J00 + w1 J01 + w2 J10 + w3 J11 + c is
+// two dot2 on the pairs (w0, w1) / (w2, w3), exact integers mod 2^32 like the mad24 chain.
+template <int S>
+__device__ __forceinline__ void load_footprint_pairs(const uint8_t* __restrict__ J, int sJ, int Hl, int Wl, int x0,
+                                                     int y0, uint32_t (&p)[S + 1][S]) {
+    if (S <= 3 && x0 >= 0 && y0 >= 0 && x0 + 7 < Wl && y0 + S < Hl) {
+        const uint32_t off = (uint32_t)(y0 * sJ + x0);
+#pragma unroll
+        for (int i = 0; i <= S; ++i) {
+            const uint32_t o = off + (uint32_t)(i * sJ);
+            const uint32_t mis = (uint32_t)((uintptr_t)J + o) & 3u;
+            u32x2 a;
+            __builtin_memcpy(&a, __builtin_assume_aligned(J + (o - mis), 4), 8);
+            const uint32_t w = __builtin_amdgcn_alignbyte(a.y, a.x, mis);
+#pragma unroll
+            for (int j = 0; j < S; ++j)  // bytes j, j + 1 into the low bytes of the two halves (0x0C selects 0)
+                p[i][j] = __builtin_amdgcn_perm(0u, w, 0x0C000C00u | ((uint32_t)(j + 1) << 16) | (uint32_t)j);
+        }
+    } else {
+        int v[S + 1][S + 1];
+        load_footprint<S>(J, sJ, Hl, Wl, x0, y0, v);
+#pragma unroll
+        for (int i = 0; i <= S; ++i)
+#pragma unroll
+            for (int j = 0; j < S; ++j) p[i][j] = (uint32_t)v[i][j] | ((uint32_t)v[i][j + 1] << 16);
+    }
+}
+
+typedef uint16_t lk_us2 __attribute__((ext_vector_type(2)));
+typedef float lk_f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int bilinear_dot2(uint32_t top, uint32_t bot, uint32_t w01, uint32_t w23, int c) {
+    const uint32_t t = __builtin_amdgcn_udot2(__builtin_bit_cast(lk_us2, bot), __builtin_bit_cast(lk_us2, w23),
+                                              (uint32_t)c, false);
+    return (int)__builtin_amdgcn_udot2(__builtin_bit_cast(lk_us2, top), __builtin_bit_cast(lk_us2, w01), t, false);
 }
 
 // One point per 16-lane row, 4 per wave.  Lane g of the row owns the S x S task at window rows S (g >> 2) ..,
@@ -480,22 +519,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
                 break;
             }
             weights(nx - (float)inx, ny - (float)iny, iw);
-            int jv[S + 1][S + 1];
-            load_footprint<S>(J, sI, Hl, Wl, inx + c0, iny + r0, jv);
-            float b1 = 0.0f, b2 = 0.0f;
+            const uint32_t w01 = (uint32_t)iw[0] | ((uint32_t)iw[1] << 16), w23 = (uint32_t)iw[2] | ((uint32_t)iw[3] << 16);
+            uint32_t jp[S + 1][S];
+            load_footprint_pairs<S>(J, sI, Hl, Wl, inx + c0, iny + r0, jp);
+            // (b1, b2) as one packed pair: v_pk_mul_f32 / v_pk_add_f32 round each half like the scalar ops
+            lk_f2 bb = {0.0f, 0.0f};
 #pragma unroll
             for (int i = 0; i < S; ++i)
 #pragma unroll
                 for (int j = 0; j < S; ++j) {
-                    const int acc = mad24(jv[i][j], iw[0], mad24(jv[i][j + 1], iw[1],
-                                    mad24(jv[i + 1][j], iw[2], mad24(jv[i + 1][j + 1], iw[3], ck[i][j]))));
+                    const int acc = bilinear_dot2(jp[i][j], jp[i + 1][j], w01, w23, ck[i][j]);
                     // (float)(diff * ixv): |diff * ixv| < 2^27, one rounding either way
                     const float d = (float)(acc >> (kWBits - 5));
-                    b1 = b1 + d * fx[i][j];
-                    b2 = b2 + d * fy[i][j];
+                    const lk_f2 dd = {d, d}, f = {fx[i][j], fy[i][j]};
+                    bb = bb + dd * f;
                 }
-            const float B1 = row_sum(b1) * FLT_SCALE;
-            const float B2 = row_sum(b2) * FLT_SCALE;
+            const float B1 = row_sum(bb.x) * FLT_SCALE;
+            const float B2 = row_sum(bb.y) * FLT_SCALE;
             const float dx = (float)((A12 * B2 - A22 * B1) * Dd);
             const float dy = (float)((A12 * B1 - A11 * B2) * Dd);
             nx += dx;
