@@ -43,6 +43,23 @@ def test_lk_matches_oracle(ctx, oracle, H, W, win, seed):
     np.testing.assert_allclose(g[both], r[both], atol=LK_TOL)
 
 
+def test_lk_negative_fourth_weight(ctx, oracle):
+    """Identical frames (zero flow, J sampled at I's positions) with level-0 fractions whose three rounded bilinear
+    weights sum past 2^14, so the fourth is -1 (a = 0.49951171875, b = 2^-14 and a = 0.332763671875, b = 3 2^-16):
+    the J interpolation must treat it as signed."""
+    H, W = 376, 1241
+    img = synth_frame(77, 0, 0, H, W)
+    xs = np.arange(60, 1180, 37, dtype=np.float64)
+    pts = np.concatenate([
+        np.stack([xs + 5 + 0.49951171875, np.full_like(xs, 55 + 2.0 ** -14)], 1),
+        np.stack([xs + 5 + 0.332763671875, np.full_like(xs, 201 + 3 * 2.0 ** -16)], 1)]).astype(np.float32)
+    g, gs, ge = ctx.calc_optical_flow_pyr_lk(img, img, pts)
+    o, os_, oe, _ = oracle.lk(img, img, pts, sum_mode=1)
+    np.testing.assert_array_equal(gs, os_)
+    np.testing.assert_array_equal(g, o)
+    np.testing.assert_array_equal(ge, oe)
+
+
 def test_lk_flat_image_fails_min_eig(ctx, oracle):
     flat = np.full((64, 80), 128, np.uint8)
     pts = np.array([[40.0, 30.0], [10.5, 12.25]], np.float32)

@@ -349,9 +349,10 @@ __device__ __forceinline__ void load_footprint(const uint8_t* __restrict__ J, in
     }
 }
 
-// The footprint as horizontal pairs p[i][j] = (v[i][j], v[i][j + 1]) packed u16x2 (v_perm from the row's dword
-// inside the image), the operand form of v_dot2_u32_u16: the bilinear sum w0 J00 + w1 J01 + w2 J10 + w3 J11 + c is
-// two dot2 on the pairs (w0, w1) / (w2, w3), exact integers mod 2^32 like the mad24 chain.
+// The footprint as horizontal pairs p[i][j] = (v[i][j], v[i][j + 1]) packed 16-bit (v_perm from the row's dword
+// inside the image), the operand form of v_dot2_i32_i16: the bilinear sum w0 J00 + w1 J01 + w2 J10 + w3 J11 + c is
+// two signed dot2 on the pairs (w0, w1) / (w2, w3), exact integers like the mad24 chain.  Signed: w3 = 2^14 - w0 -
+// w1 - w2 is -1 when all three round up (a b 2^14 < 1.5, e.g. a = 0.4995, b = 2^-14).
 template <int S>
 __device__ __forceinline__ void load_footprint_pairs(const uint8_t* __restrict__ J, int sJ, int Hl, int Wl, int x0,
                                                      int y0, uint32_t (&p)[S + 1][S]) {
@@ -378,13 +379,12 @@ __device__ __forceinline__ void load_footprint_pairs(const uint8_t* __restrict__
     }
 }
 
-typedef uint16_t lk_us2 __attribute__((ext_vector_type(2)));
+typedef int16_t lk_s2 __attribute__((ext_vector_type(2)));
 typedef float lk_f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int bilinear_dot2(uint32_t top, uint32_t bot, uint32_t w01, uint32_t w23, int c) {
-    const uint32_t t = __builtin_amdgcn_udot2(__builtin_bit_cast(lk_us2, bot), __builtin_bit_cast(lk_us2, w23),
-                                              (uint32_t)c, false);
-    return (int)__builtin_amdgcn_udot2(__builtin_bit_cast(lk_us2, top), __builtin_bit_cast(lk_us2, w01), t, false);
+    const int t = __builtin_amdgcn_sdot2(__builtin_bit_cast(lk_s2, bot), __builtin_bit_cast(lk_s2, w23), c, false);
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(lk_s2, top), __builtin_bit_cast(lk_s2, w01), t, false);
 }
 
 // One point per 16-lane row, 4 per wave.  Lane g of the row owns the S x S task at window rows S (g >> 2) ..,
@@ -519,7 +519,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
                 break;
             }
             weights(nx - (float)inx, ny - (float)iny, iw);
-            const uint32_t w01 = (uint32_t)iw[0] | ((uint32_t)iw[1] << 16), w23 = (uint32_t)iw[2] | ((uint32_t)iw[3] << 16);
+            const uint32_t w01 = ((uint32_t)iw[0] & 0xFFFFu) | ((uint32_t)iw[1] << 16);
+            const uint32_t w23 = ((uint32_t)iw[2] & 0xFFFFu) | ((uint32_t)iw[3] << 16);
             uint32_t jp[S + 1][S];
             load_footprint_pairs<S>(J, sI, Hl, Wl, inx + c0, iny + r0, jp);
             // (b1, b2) as one packed pair: v_pk_mul_f32 / v_pk_add_f32 round each half like the scalar ops
