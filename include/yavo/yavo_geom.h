@@ -83,11 +83,12 @@ int yv_lk_levels(const yv_lk* lk);
 int yv_lk_build(yv_lk* lk, const uint8_t* d_images, int n_images, int stride, int64_t image_pitch, void* stream);
 /* Level `level` (0 .. yv_lk_levels) of image `image` of the last yv_lk_build, as cv::buildOpticalFlowPyramid
  * would hand it over without derivatives interleaved: the level image (*d_img, rows *img_stride bytes apart;
- * level 0 is the caller's image) and its Scharr derivatives (*d_deriv, (dx, dy) int16 pairs, rows *deriv_stride
- * pairs apart), size *H x *W.  Device pointers, valid until the next yv_lk_build / yv_lk_destroy; read them after
- * the build's stream work has completed. */
-int yv_lk_level(const yv_lk* lk, int image, int level, const uint8_t** d_img, int* img_stride,
-                const int16_t** d_deriv, int* deriv_stride, int* H, int* W);
+ * level 0 is the caller's image; valid until the next yv_lk_build / yv_lk_destroy, after the build's stream work)
+ * and its Scharr derivatives (*d_deriv, (dx, dy) int16 pairs, rows *deriv_stride pairs apart; computed on the
+ * context stream and complete on return, valid until the next yv_lk_level), size *H x *W.  The tracker itself
+ * computes derivatives inside its windows and keeps no derivative pyramid. */
+int yv_lk_level(yv_lk* lk, int image, int level, const uint8_t** d_img, int* img_stride, const int16_t** d_deriv,
+                int* deriv_stride, int* H, int* W);
 /* Track d_counts[p] points of pair p (prev image d_pairs[2p], next image d_pairs[2p+1], indices into the
  * last yv_lk_build): points d_pts + 2*(p*pts_stride + i); results at the same positions of d_next / d_status /
  * d_err.  max_count, eps, min_eig: TermCriteria(COUNT+EPS, max_count, eps) and minEigThreshold. */

@@ -1279,13 +1279,12 @@ int yv_lk_create(yv_ctx* ctx, int max_images, int H, int W, int win, int max_lev
             P.off[l] = off;
             off += ((int64_t)P.h[l] * P.ps[l] + 255) & ~(int64_t)255;
         }
-        P.der_off[l] = doff;
-        doff += ((int64_t)P.h[l] * P.ds[l] * 2 + 127) & ~(int64_t)127;
     }
+    doff = (int64_t)P.h[0] * P.ds[0] * 2;  // yv_lk_level's one-level derivative image (level 0 is the largest)
     P.pyr_pitch = std::max<int64_t>(off, 256);
     P.der_pitch = doff;
     if (dalloc(&P.pyr, (size_t)P.pyr_pitch * max_images) != YV_OK ||
-        dalloc(&P.der, (size_t)P.der_pitch * max_images) != YV_OK) {
+        dalloc(&P.der, (size_t)P.der_pitch * sizeof(int16_t)) != YV_OK) {
         if (P.pyr) (void)hipFree(P.pyr);
         if (P.der) (void)hipFree(P.der);
         delete lk;
@@ -1306,12 +1305,16 @@ void yv_lk_destroy(yv_lk* lk) {
 
 int yv_lk_levels(const yv_lk* lk) { return lk ? lk->P.levels : YV_ERR_INVALID; }
 
-int yv_lk_level(const yv_lk* lk, int image, int level, const uint8_t** d_img, int* img_stride,
-                const int16_t** d_deriv, int* deriv_stride, int* H, int* W) {
+int yv_lk_level(yv_lk* lk, int image, int level, const uint8_t** d_img, int* img_stride, const int16_t** d_deriv,
+                int* deriv_stride, int* H, int* W) {
     if (!lk || !lk->P.img0 || image < 0 || image >= lk->built_images || level < 0 || level > lk->P.levels ||
         !d_img || !img_stride || !d_deriv || !deriv_stride || !H || !W)
         return YV_ERR_INVALID;
+    if (set_device(lk->ctx) != YV_OK) return YV_ERR_HIP;
     const yavo::LkParams& P = lk->P;
+    // the level's derivatives into the workspace's one-level image, complete on return
+    yavo::launch_lk_derivs(P, image, level, P.der, lk->ctx->stream);
+    if (check_launch() != YV_OK || hipStreamSynchronize(lk->ctx->stream) != hipSuccess) return YV_ERR_HIP;
     if (level == 0) {
         *d_img = P.img0 + image * P.pitch0;
         *img_stride = P.stride0;
@@ -1319,7 +1322,7 @@ int yv_lk_level(const yv_lk* lk, int image, int level, const uint8_t** d_img, in
         *d_img = P.pyr + image * P.pyr_pitch + P.off[level];
         *img_stride = P.ps[level];
     }
-    *d_deriv = P.der + image * P.der_pitch + P.der_off[level];  // int16 units
+    *d_deriv = P.der;
     *deriv_stride = P.ds[level];
     *H = P.h[level];
     *W = P.w[level];

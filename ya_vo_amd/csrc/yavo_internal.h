@@ -102,26 +102,26 @@ void launch_pose_lm(const int32_t* offsets, int n_problems, const double* X, con
 void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
                     double* poses, int32_t* iters, hipStream_t s);
 // cv::calcOpticalFlowPyrLK workspace view (yavo_lk.hip).  Level 0 is the caller's image; levels >= 1 live in
-// `pyr` ([image][pyr_pitch], level l at off[l], row stride ps[l] = w[l] rounded up to 64 bytes); derivatives of
-// every level in `der` ([image][der_pitch] int16, level l at der_off[l], (dx, dy) interleaved, ds[l] pixels per
-// row = w[l] rounded up to 16, i.e. 64-byte rows).  The padded rows make every store of the pyramid kernels a
-// whole aligned dword / dwordx4 of full cache lines.
+// `pyr` ([image][pyr_pitch], level l at off[l], row stride ps[l] = w[l] rounded up to 64 bytes: every pyrDown store
+// is a whole aligned dword of full cache lines).  The tracker computes Scharr derivatives inside its windows; `der`
+// is one level's (dx, dy) int16 image for yv_lk_level only (ds[l] pixels per row = w[l] rounded up to 16).
 constexpr int kLkMaxLevels = 8;
 struct LkParams {
     int levels = 0, win = 11, max_count = 30;
     double eps2 = 1e-4, min_eig = 1e-3;
     int h[kLkMaxLevels] = {}, w[kLkMaxLevels] = {};
     int ps[kLkMaxLevels] = {}, ds[kLkMaxLevels] = {};
-    int64_t off[kLkMaxLevels] = {}, der_off[kLkMaxLevels] = {};
+    int64_t off[kLkMaxLevels] = {};
     const uint8_t* img0 = nullptr;
     int stride0 = 0;
     int64_t pitch0 = 0;
     uint8_t* pyr = nullptr;
     int64_t pyr_pitch = 0;
     int16_t* der = nullptr;
-    int64_t der_pitch = 0;
+    int64_t der_pitch = 0;  // int16 elements of `der`
 };
 void launch_lk_pyramid(const LkParams& P, int n_images, hipStream_t s);
+void launch_lk_derivs(const LkParams& P, int image, int level, int16_t* der, hipStream_t s);
 void launch_lk_track(const LkParams& P, const int32_t* pairs, int n_pairs, const float* pts, const int32_t* counts,
                      int pts_stride, int max_pts, float* next_pts, uint8_t* status, float* err, hipStream_t s);
 void launch_track_build(const int32_t* tracks, int n_tracks, const int32_t* pairs, const yv_keypoint* keypoints,

@@ -349,6 +349,69 @@ __device__ __forceinline__ void load_footprint(const uint8_t* __restrict__ J, in
     }
 }
 
+// calcSharrDeriv of the level image I at the (S + 1) x (S + 1) footprint positions (y0 + i, x0 + j), computed in
+// place from I's (S + 3) x (S + 3) neighbourhood instead of read from a derivative pyramid: the same exact integers
+// as scharr_kernel (REFLECT_101 on I), packed (dx, dy) as scharr_kernel stores them, and 0 at positions outside the
+// image (the derivative border LK reads); the window's inside is also the I footprint of the level.  Inside the
+// image one dword-aligned dwordx3 + two v_alignbyte per window row; near a border, reflected byte loads.
+template <int S>
+__device__ __forceinline__ void scharr_footprint(const uint8_t* __restrict__ I, int sI, int Hl, int Wl, int x0,
+                                                 int y0, int (&dv)[S + 1][S + 1], int (&iv)[S + 1][S + 1]) {
+    constexpr int N = S + 3, NW = (N + 3) / 4;
+    uint32_t w[N][NW];  // bytes of I(y0 - 1 + r, x0 - 1 .. x0 + S + 1), packed 4 per dword
+    if (S <= 3 && x0 >= 1 && y0 >= 1 && x0 + 8 <= Wl && y0 + S + 1 < Hl) {
+        uint32_t raw[N][3];
+        uint32_t mis[N];
+#pragma unroll
+        for (int r = 0; r < N; ++r) {
+            const uint32_t o = (uint32_t)((y0 - 1 + r) * sI + x0 - 1);
+            mis[r] = (uint32_t)((uintptr_t)I + o) & 3u;
+            __builtin_memcpy(raw[r], __builtin_assume_aligned(I + (o - mis[r]), 4), 12);
+        }
+#pragma unroll
+        for (int r = 0; r < N; ++r) {
+#pragma unroll
+            for (int q = 0; q < NW; ++q) w[r][q] = __builtin_amdgcn_alignbyte(raw[r][q + 1], raw[r][q], mis[r]);
+        }
+    } else {
+        int cc[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) cc[k] = refl_c(x0 - 1 + k, Wl);
+#pragma unroll
+        for (int r = 0; r < N; ++r) {
+            const uint32_t rr = (uint32_t)(refl_c(y0 - 1 + r, Hl) * sI);
+#pragma unroll
+            for (int q = 0; q < NW; ++q) w[r][q] = 0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) w[r][k >> 2] |= (uint32_t)I[rr + (uint32_t)cc[k]] << (8 * (k & 3));
+        }
+    }
+    // the window's inner (S + 1) x (S + 1) is the I footprint: refl_c at the borders, as load_footprint reads it
+#pragma unroll
+    for (int i = 0; i <= S; ++i)
+#pragma unroll
+        for (int j = 0; j <= S; ++j) iv[i][j] = (w[i + 1][(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 0xFF;
+#pragma unroll
+    for (int i = 0; i <= S; ++i) {
+        int t0[N], t1[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const int sh = 8 * (k & 3);
+            const int a0 = (w[i][k >> 2] >> sh) & 0xFF, a1 = (w[i + 1][k >> 2] >> sh) & 0xFF;
+            const int a2 = (w[i + 2][k >> 2] >> sh) & 0xFF;
+            t0[k] = (a0 + a2) * 3 + a1 * 10;
+            t1[k] = a2 - a0;
+        }
+        const bool rin = y0 + i >= 0 && y0 + i < Hl;
+#pragma unroll
+        for (int j = 0; j <= S; ++j) {
+            const bool in = rin && x0 + j >= 0 && x0 + j < Wl;
+            const int dx = t0[j + 2] - t0[j], dy = (t1[j] + t1[j + 2]) * 3 + t1[j + 1] * 10;
+            dv[i][j] = in ? (int)((uint32_t)(uint16_t)dx | ((uint32_t)dy << 16)) : 0;  // as scharr_kernel packs
+        }
+    }
+}
+
 // The footprint as horizontal pairs p[i][j] = (v[i][j], v[i][j + 1]) packed 16-bit (v_perm from the row's dword
 // inside the image), the operand form of v_dot2_i32_i16: the bilinear sum w0 J00 + w1 J01 + w2 J10 + w3 J11 + c is
 // two signed dot2 on the pairs (w0, w1) / (w2, w3), exact integers like the mad24 chain.  Signed: w3 = 2^14 - w0 -
@@ -416,8 +479,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
         const uint8_t* I = level == 0 ? P.img0 + (int64_t)ia * P.pitch0 : P.pyr + (int64_t)ia * P.pyr_pitch + P.off[level];
         const uint8_t* J = level == 0 ? P.img0 + (int64_t)ib * P.pitch0 : P.pyr + (int64_t)ib * P.pyr_pitch + P.off[level];
         const int sI = level == 0 ? P.stride0 : P.ps[level];
-        const int sD = P.ds[level];
-        const uint32_t* D = reinterpret_cast<const uint32_t*>(P.der + (int64_t)ia * P.der_pitch + P.der_off[level]);
         const float scale = (float)(1. / (1 << level));
         float px = px0 * scale, py = py0 * scale;
         float nx, ny;
@@ -443,37 +504,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
         int iw[4];
         weights(px - (float)ipx, py - (float)ipy, iw);
         // I and (dx, dy) over the task footprint; the derivative image is zero outside [0, Hl) x [0, Wl)
-        int iv8[S + 1][S + 1];
-        load_footprint<S>(I, sI, Hl, Wl, ipx + c0, ipy + r0, iv8);
-        int dv[S + 1][S + 1];
-        if (S == 3 && ipx + c0 >= 0 && ipy + r0 >= 0 && ipx + c0 + S < Wl && ipy + r0 + S < Hl) {
-            // all inside: one dwordx4 per footprint row
-#pragma unroll
-            for (int i = 0; i <= S; ++i) {
-                u32x4 d;
-                __builtin_memcpy(&d, __builtin_assume_aligned(D + (uint32_t)((ipy + r0 + i) * sD + ipx + c0), 4), 16);
-#pragma unroll
-                for (int j = 0; j <= S; ++j) dv[i][j] = (int)d[j & 3];
-            }
-        } else {
-            int r[S + 1], c[S + 1];
-            bool rin[S + 1], cin[S + 1];
-#pragma unroll
-            for (int i = 0; i <= S; ++i) {
-                const int y = ipy + r0 + i, x = ipx + c0 + i;
-                rin[i] = y >= 0 && y < Hl;
-                cin[i] = x >= 0 && x < Wl;
-                r[i] = min(max(y, 0), Hl - 1) * sD;
-                c[i] = min(max(x, 0), Wl - 1);
-            }
-#pragma unroll
-            for (int i = 0; i <= S; ++i)
-#pragma unroll
-                for (int j = 0; j <= S; ++j) {
-                    const uint32_t d = D[(uint32_t)(r[i] + c[j])];
-                    dv[i][j] = rin[i] && cin[j] ? (int)d : 0;
-                }
-        }
+        int iv8[S + 1][S + 1], dv[S + 1][S + 1];
+        scharr_footprint<S>(I, sI, Hl, Wl, ipx + c0, ipy + r0, dv, iv8);
         int ck[S][S];
         float fx[S][S], fy[S][S];
         float a11 = 0.0f, a12 = 0.0f, a22 = 0.0f;
@@ -483,7 +515,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
             for (int j = 0; j < S; ++j) {
                 const int ival = descale(mad24(iv8[i][j], iw[0], mad24(iv8[i][j + 1], iw[1],
                                          mad24(iv8[i + 1][j], iw[2], iv8[i + 1][j + 1] * iw[3]))), kWBits - 5);
-                // (int16) low / high halves of the interleaved (dx, dy) derivative
+                // (int16) low / high halves of the packed (dx, dy) derivative
                 const int x00 = (int16_t)dv[i][j], x01 = (int16_t)dv[i][j + 1];
                 const int x10 = (int16_t)dv[i + 1][j], x11 = (int16_t)dv[i + 1][j + 1];
                 const int y00 = dv[i][j] >> 16, y01 = dv[i][j + 1] >> 16;
@@ -586,9 +618,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
 }  // namespace lk
 
 void launch_lk_pyramid(const LkParams& P, int n_images, hipStream_t s) {
-    constexpr int kPdR = 4, kScR = 4;  // output rows per lane
-    // level l (>= 1) from level l-1, then the derivatives of every level; each grid = the interior workgroup
-    // columns + one border column (whose workgroups cover 8x the rows: row tiles past the image return at once)
+    constexpr int kPdR = 4;  // output rows per lane
+    // level l (>= 1) from level l-1 (the tracker computes the Scharr derivatives inside its windows); the grid is the
+    // interior workgroup columns + one border column (whose workgroups cover 8x the rows: row tiles past the image
+    // return at once)
     for (int l = 1; l <= P.levels; ++l) {
         const int Hs = P.h[l - 1], Ws = P.w[l - 1];
         const uint8_t* src = l == 1 ? P.img0 : P.pyr + P.off[l - 1];
@@ -598,15 +631,16 @@ void launch_lk_pyramid(const LkParams& P, int n_images, hipStream_t s) {
         hipLaunchKernelGGL(lk::pyr_down_kernel<kPdR>, grid, dim3(256), 0, s, src, Hs, Ws, sstride, spitch,
                            P.pyr + P.off[l], P.ps[l], P.pyr_pitch);
     }
-    for (int l = 0; l <= P.levels; ++l) {
-        const uint8_t* src = l == 0 ? P.img0 : P.pyr + P.off[l];
-        const int sstride = l == 0 ? P.stride0 : P.ps[l];
-        const int64_t spitch = l == 0 ? P.pitch0 : P.pyr_pitch;
-        dim3 grid((lk::sc_x1(P.w[l]) - 4 + lk::SC_TW - 1) / lk::SC_TW + 1, (P.h[l] + 4 * kScR - 1) / (4 * kScR),
-                  n_images);
-        hipLaunchKernelGGL(lk::scharr_kernel<kScR>, grid, dim3(256), 0, s, src, P.h[l], P.w[l], sstride, spitch,
-                           P.der + P.der_off[l], P.ds[l], P.der_pitch);
-    }
+}
+
+void launch_lk_derivs(const LkParams& P, int image, int level, int16_t* der, hipStream_t s) {
+    // one level of one image into der (rows ds[level] pixels apart): the inspection path of yv_lk_level
+    constexpr int kScR = 4;
+    const uint8_t* src = level == 0 ? P.img0 + (int64_t)image * P.pitch0 : P.pyr + (int64_t)image * P.pyr_pitch + P.off[level];
+    const int sstride = level == 0 ? P.stride0 : P.ps[level];
+    dim3 grid((lk::sc_x1(P.w[level]) - 4 + lk::SC_TW - 1) / lk::SC_TW + 1, (P.h[level] + 4 * kScR - 1) / (4 * kScR), 1);
+    hipLaunchKernelGGL(lk::scharr_kernel<kScR>, grid, dim3(256), 0, s, src, P.h[level], P.w[level], sstride, (int64_t)0,
+                       der, P.ds[level], (int64_t)0);
 }
 
 void launch_lk_track(const LkParams& P, const int32_t* pairs, int n_pairs, const float* pts, const int32_t* counts,
