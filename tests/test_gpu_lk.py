@@ -60,6 +60,22 @@ def test_lk_negative_fourth_weight(ctx, oracle):
     np.testing.assert_array_equal(ge, oe)
 
 
+def test_lk_empty_and_tiny(ctx, oracle):
+    """No points (nothing launched, empty outputs), and a 12 x 15 image with win 3 (one pyramid level) whose points
+    sit on the corners and just outside: the border paths of the pyramid, the in-window derivatives and the footprints."""
+    img = synth_frame(5, 0, 0, 12, 15)
+    g, gs, ge = ctx.calc_optical_flow_pyr_lk(img, img, np.zeros((0, 2), np.float32))
+    assert g.shape == (0, 2) and gs.shape == (0,) and ge.shape == (0,)
+    nxt = synth_frame(5, 1, 1, 12, 15)
+    pts = np.array([[0, 0], [14, 0], [0, 11], [14, 11], [7.25, 5.5], [-1.5, 3], [15.5, 6], [3, -0.75]], np.float32)
+    for win in (3, 5):
+        g, gs, ge = ctx.calc_optical_flow_pyr_lk(img, nxt, pts, win=win, max_level=2)
+        o, os_, oe, _ = oracle.lk(img, nxt, pts, win=win, max_level=2, sum_mode=1)
+        np.testing.assert_array_equal(gs, os_)
+        np.testing.assert_array_equal(g, o)
+        np.testing.assert_array_equal(ge, oe)
+
+
 def test_lk_flat_image_fails_min_eig(ctx, oracle):
     flat = np.full((64, 80), 128, np.uint8)
     pts = np.array([[40.0, 30.0], [10.5, 12.25]], np.float32)
