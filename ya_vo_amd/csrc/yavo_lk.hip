@@ -576,7 +576,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
             nxo = nx + halfw;
             nyo = ny + halfw;
             if ((double)dx * dx + (double)dy * dy <= P.eps2) break;
-            if (it > 0 && fabsf(dx + pdx) < 0.01 && fabsf(dy + pdy) < 0.01) {
+            // |v| < 0.01 (double) <=> |v| <= 0.01f: the float nearest 0.01 lies below it and the next one above
+            if (it > 0 && fabsf(dx + pdx) <= 0.01f && fabsf(dy + pdy) <= 0.01f) {
                 nxo -= dx * 0.5f;
                 nyo -= dy * 0.5f;
                 break;
