@@ -299,6 +299,23 @@ __device__ __forceinline__ float row_dpp(float v) {
 // off = 8, 4, 2, 1, as row rotations (after the step with off the values have period off, so rotating by off / 2
 // brings lane l ^ (off / 2)).  Lane 0 follows the tree p[l] += p[l + off]; every lane ends with the same bits
 // (IEEE addition commutes), so the Newton step needs no broadcast.
+// One butterfly step as a single v_add_f32 with the DPP row rotation on its first operand (an opaque register
+// copy keeps the two sums of a pair from being packed into v_pk_add_f32, which takes no DPP operand).
+template <int kCtrl>
+__device__ __forceinline__ float row_add_dpp(float q) {
+    float r = q + row_dpp<kCtrl>(q);
+    __asm__ volatile("" : "+v"(r));
+    return r;
+}
+
+__device__ __forceinline__ float row_sum_dpp(float q) {
+    q = row_add_dpp<0x128>(q);  // row_ror:8
+    q = row_add_dpp<0x124>(q);  // row_ror:4
+    q = row_add_dpp<0x122>(q);  // row_ror:2
+    q = row_add_dpp<0x121>(q);  // row_ror:1
+    return q;
+}
+
 __device__ __forceinline__ float row_sum(float q) {
     q = q + row_dpp<0x128>(q);  // row_ror:8
     q = q + row_dpp<0x124>(q);  // row_ror:4
@@ -567,8 +584,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
                     const lk_f2 dd = {d, d}, f = {fx[i][j], fy[i][j]};
                     bb = bb + dd * f;
                 }
-            const float B1 = row_sum(bb.x) * FLT_SCALE;
-            const float B2 = row_sum(bb.y) * FLT_SCALE;
+            const float B1 = row_sum_dpp(bb.x) * FLT_SCALE;
+            const float B2 = row_sum_dpp(bb.y) * FLT_SCALE;
             const float dx = (float)((A12 * B2 - A22 * B1) * Dd);
             const float dy = (float)((A12 * B1 - A11 * B2) * Dd);
             nx += dx;
