@@ -299,21 +299,22 @@ __device__ __forceinline__ float row_dpp(float v) {
 // off = 8, 4, 2, 1, as row rotations (after the step with off the values have period off, so rotating by off / 2
 // brings lane l ^ (off / 2)).  Lane 0 follows the tree p[l] += p[l + off]; every lane ends with the same bits
 // (IEEE addition commutes), so the Newton step needs no broadcast.
-// One butterfly step as a single v_add_f32 with the DPP row rotation on its first operand (an opaque register
-// copy keeps the two sums of a pair from being packed into v_pk_add_f32, which takes no DPP operand).
+// Butterfly steps as single v_add_f32 with the DPP row rotation on an operand (an opaque register copy keeps the
+// two sums of a pair from being packed into v_pk_add_f32, which takes no DPP operand).
+// two independent sums, their steps alternated so each DPP read finds its operand's write two instructions back
+// (no s_nop for the VALU-write -> DPP-read hazard)
 template <int kCtrl>
-__device__ __forceinline__ float row_add_dpp(float q) {
-    float r = q + row_dpp<kCtrl>(q);
-    __asm__ volatile("" : "+v"(r));
-    return r;
+__device__ __forceinline__ void row_add_dpp2(float& p, float& q) {
+    p = p + row_dpp<kCtrl>(p);
+    q = q + row_dpp<kCtrl>(q);
+    __asm__ volatile("" : "+v"(p), "+v"(q));
 }
 
-__device__ __forceinline__ float row_sum_dpp(float q) {
-    q = row_add_dpp<0x128>(q);  // row_ror:8
-    q = row_add_dpp<0x124>(q);  // row_ror:4
-    q = row_add_dpp<0x122>(q);  // row_ror:2
-    q = row_add_dpp<0x121>(q);  // row_ror:1
-    return q;
+__device__ __forceinline__ void row_sum_dpp2(float& p, float& q) {
+    row_add_dpp2<0x128>(p, q);  // row_ror:8
+    row_add_dpp2<0x124>(p, q);  // row_ror:4
+    row_add_dpp2<0x122>(p, q);  // row_ror:2
+    row_add_dpp2<0x121>(p, q);  // row_ror:1
 }
 
 __device__ __forceinline__ float row_sum(float q) {
@@ -463,7 +464,9 @@ typedef int16_t lk_s2 __attribute__((ext_vector_type(2)));
 typedef float lk_f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int bilinear_dot2(uint32_t top, uint32_t bot, uint32_t w01, uint32_t w23, int c) {
-    const int t = __builtin_amdgcn_sdot2(__builtin_bit_cast(lk_s2, bot), __builtin_bit_cast(lk_s2, w23), c, false);
+    // clamp on the first dot2 (its sums stay far inside int32, so it never saturates) selects the three-operand
+    // VOP3P form: the accumulate-in-place v_dot2c would need a copy of the loop-invariant c every time
+    const int t = __builtin_amdgcn_sdot2(__builtin_bit_cast(lk_s2, bot), __builtin_bit_cast(lk_s2, w23), c, true);
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(lk_s2, top), __builtin_bit_cast(lk_s2, w01), t, false);
 }
 
@@ -584,8 +587,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
                     const lk_f2 dd = {d, d}, f = {fx[i][j], fy[i][j]};
                     bb = bb + dd * f;
                 }
-            const float B1 = row_sum_dpp(bb.x) * FLT_SCALE;
-            const float B2 = row_sum_dpp(bb.y) * FLT_SCALE;
+            float s1 = bb.x, s2 = bb.y;
+            row_sum_dpp2(s1, s2);
+            const float B1 = s1 * FLT_SCALE;
+            const float B2 = s2 * FLT_SCALE;
             const float dx = (float)((A12 * B2 - A22 * B1) * Dd);
             const float dy = (float)((A12 * B1 - A11 * B2) * Dd);
             nx += dx;
