@@ -499,7 +499,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
         const uint8_t* I = level == 0 ? P.img0 + (int64_t)ia * P.pitch0 : P.pyr + (int64_t)ia * P.pyr_pitch + P.off[level];
         const uint8_t* J = level == 0 ? P.img0 + (int64_t)ib * P.pitch0 : P.pyr + (int64_t)ib * P.pyr_pitch + P.off[level];
         const int sI = level == 0 ? P.stride0 : P.ps[level];
-        const float scale = (float)(1. / (1 << level));
+        const float scale = __builtin_ldexpf(1.f, -level);  // (float)(1. / (1 << level)), exact
         float px = px0 * scale, py = py0 * scale;
         float nx, ny;
         if (level == P.levels) {
@@ -551,8 +551,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
                 a12 = a12 + fx[i][j] * fy[i][j];
                 a22 = a22 + fy[i][j] * fy[i][j];
             }
-        const float A11 = row_sum(a11) * FLT_SCALE;
-        const float A12 = row_sum(a12) * FLT_SCALE;
+        row_sum_dpp2(a11, a12);
+        const float A11 = a11 * FLT_SCALE;
+        const float A12 = a12 * FLT_SCALE;
         const float A22 = row_sum(a22) * FLT_SCALE;
         float Dd = A11 * A22 - A12 * A12;
         const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * win * win);
