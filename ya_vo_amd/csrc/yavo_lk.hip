@@ -374,7 +374,7 @@ __device__ __forceinline__ void load_footprint(const uint8_t* __restrict__ J, in
 // image one dword-aligned dwordx3 + two v_alignbyte per window row; near a border, reflected byte loads.
 template <int S>
 __device__ __forceinline__ void scharr_footprint(const uint8_t* __restrict__ I, int sI, int Hl, int Wl, int x0,
-                                                 int y0, int (&dv)[S + 1][S + 1], int (&iv)[S + 1][S + 1]) {
+                                                 int y0, int (&dv)[S + 1][S + 1], uint32_t (&ip)[S + 1][S]) {
     constexpr int N = S + 3, NW = (N + 3) / 4;
     uint32_t w[N][NW];  // bytes of I(y0 - 1 + r, x0 - 1 .. x0 + S + 1), packed 4 per dword
     if (S <= 3 && x0 >= 1 && y0 >= 1 && x0 + 8 <= Wl && y0 + S + 1 < Hl) {
@@ -404,11 +404,17 @@ __device__ __forceinline__ void scharr_footprint(const uint8_t* __restrict__ I, 
             for (int k = 0; k < N; ++k) w[r][k >> 2] |= (uint32_t)I[rr + (uint32_t)cc[k]] << (8 * (k & 3));
         }
     }
-    // the window's inner (S + 1) x (S + 1) is the I footprint: refl_c at the borders, as load_footprint reads it
+    // the window's inner (S + 1) x (S + 1) is the I footprint (refl_c at the borders, as load_footprint reads it),
+    // as the horizontal pairs (I(i, j), I(i, j + 1)) of bilinear_dot2: bytes j + 1, j + 2 of window row i + 1
 #pragma unroll
     for (int i = 0; i <= S; ++i)
 #pragma unroll
-        for (int j = 0; j <= S; ++j) iv[i][j] = (w[i + 1][(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 0xFF;
+        for (int j = 0; j < S; ++j) {
+            constexpr int kLastW = NW - 1;
+            const int q = (j + 1) >> 2, o = (j + 1) & 3;
+            ip[i][j] = __builtin_amdgcn_perm(w[i + 1][q + 1 <= kLastW ? q + 1 : kLastW], w[i + 1][q],
+                                             0x0C000C00u | ((uint32_t)(o + 1) << 16) | (uint32_t)o);
+        }
 #pragma unroll
     for (int i = 0; i <= S; ++i) {
         int t0[N], t1[N];
@@ -524,8 +530,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
         int iw[4];
         weights(px - (float)ipx, py - (float)ipy, iw);
         // I and (dx, dy) over the task footprint; the derivative image is zero outside [0, Hl) x [0, Wl)
-        int iv8[S + 1][S + 1], dv[S + 1][S + 1];
-        scharr_footprint<S>(I, sI, Hl, Wl, ipx + c0, ipy + r0, dv, iv8);
+        int dv[S + 1][S + 1];
+        uint32_t ip[S + 1][S];
+        scharr_footprint<S>(I, sI, Hl, Wl, ipx + c0, ipy + r0, dv, ip);
+        const uint32_t iw01 = ((uint32_t)iw[0] & 0xFFFFu) | ((uint32_t)iw[1] << 16);
+        const uint32_t iw23 = ((uint32_t)iw[2] & 0xFFFFu) | ((uint32_t)iw[3] << 16);
         int ck[S][S];
         float fx[S][S], fy[S][S];
         float a11 = 0.0f, a12 = 0.0f, a22 = 0.0f;
@@ -533,15 +542,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
         for (int i = 0; i < S; ++i)
 #pragma unroll
             for (int j = 0; j < S; ++j) {
-                const int ival = descale(mad24(iv8[i][j], iw[0], mad24(iv8[i][j + 1], iw[1],
-                                         mad24(iv8[i + 1][j], iw[2], iv8[i + 1][j + 1] * iw[3]))), kWBits - 5);
-                // (int16) low / high halves of the packed (dx, dy) derivative
-                const int x00 = (int16_t)dv[i][j], x01 = (int16_t)dv[i][j + 1];
-                const int x10 = (int16_t)dv[i + 1][j], x11 = (int16_t)dv[i + 1][j + 1];
-                const int y00 = dv[i][j] >> 16, y01 = dv[i][j + 1] >> 16;
-                const int y10 = dv[i + 1][j] >> 16, y11 = dv[i + 1][j + 1] >> 16;
-                const int ixv = descale(mad24(x00, iw[0], mad24(x01, iw[1], mad24(x10, iw[2], __mul24(x11, iw[3])))), kWBits);
-                const int iyv = descale(mad24(y00, iw[0], mad24(y01, iw[1], mad24(y10, iw[2], __mul24(y11, iw[3])))), kWBits);
+                const int ival = descale(bilinear_dot2(ip[i][j], ip[i + 1][j], iw01, iw23, 0), kWBits - 5);
+                // the dx (low) / dy (high) halves of the packed derivatives as horizontal pairs, one v_perm each
+                const uint32_t xt = __builtin_amdgcn_perm((uint32_t)dv[i][j + 1], (uint32_t)dv[i][j], 0x05040100u);
+                const uint32_t xb = __builtin_amdgcn_perm((uint32_t)dv[i + 1][j + 1], (uint32_t)dv[i + 1][j], 0x05040100u);
+                const uint32_t yt = __builtin_amdgcn_perm((uint32_t)dv[i][j + 1], (uint32_t)dv[i][j], 0x07060302u);
+                const uint32_t yb = __builtin_amdgcn_perm((uint32_t)dv[i + 1][j + 1], (uint32_t)dv[i + 1][j], 0x07060302u);
+                const int ixv = descale(bilinear_dot2(xt, xb, iw01, iw23, 0), kWBits);
+                const int iyv = descale(bilinear_dot2(yt, yb, iw01, iw23, 0), kWBits);
                 const bool in = r0 + i < win && c0 + j < win;
                 ck[i][j] = (1 << (kWBits - 6)) - (ival << (kWBits - 5));
                 fx[i][j] = in ? (float)ixv : 0.f;
