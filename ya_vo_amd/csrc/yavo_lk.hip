@@ -286,8 +286,6 @@ __device__ __forceinline__ void weights(float a, float b, int* iw) {
     iw[3] = (1 << kWBits) - iw[0] - iw[1] - iw[2];
 }
 
-// a * b + c with |a|, |b| < 2^23 (v_mad_i32_i24): samples are u8 / int16, weights <= 2^14
-__device__ __forceinline__ int mad24(int a, int b, int c) { return __mul24(a, b) + c; }
 
 // row rotations read a lane of the same row for every lane, so no old value is needed (mov_dpp, bound_ctrl)
 template <int kCtrl>
@@ -623,15 +621,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S <= 2 ? 8 
                 status = 0;
             } else {
                 weights(ex - (float)inx, ey - (float)iny, iw);
-                int jv[S + 1][S + 1];
-                load_footprint<S>(J, sI, Hl, Wl, inx + c0, iny + r0, jv);
+                const uint32_t w01 = ((uint32_t)iw[0] & 0xFFFFu) | ((uint32_t)iw[1] << 16);
+                const uint32_t w23 = ((uint32_t)iw[2] & 0xFFFFu) | ((uint32_t)iw[3] << 16);
+                uint32_t jp[S + 1][S];
+                load_footprint_pairs<S>(J, sI, Hl, Wl, inx + c0, iny + r0, jp);
                 float e = 0.0f;
 #pragma unroll
                 for (int i = 0; i < S; ++i)
 #pragma unroll
                     for (int j = 0; j < S; ++j) {
-                        const int acc = mad24(jv[i][j], iw[0], mad24(jv[i][j + 1], iw[1],
-                                        mad24(jv[i + 1][j], iw[2], mad24(jv[i + 1][j + 1], iw[3], ck[i][j]))));
+                        const int acc = bilinear_dot2(jp[i][j], jp[i + 1][j], w01, w23, ck[i][j]);
                         const bool in = r0 + i < win && c0 + j < win;
                         e = e + (in ? fabsf((float)(acc >> (kWBits - 5))) : 0.f);
                     }
