@@ -298,31 +298,28 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         s_npre = 0;
     }
 
-    // stage (FT_H + 8) x (FT_W + 8) = 64 x 72 bytes.  Interior tiles (every source byte inside the image, and the
-    // last staged row not the image's last, so the alignment slack past a row end stays inside the image): each
-    // LDS dword is one dword-aligned dwordx2 load funnel-shifted by the row's misalignment (v_alignbyte), 5 per
-    // thread, all in flight before the LDS writes.  Border tiles take the REFLECT_101 byte path.
+    // stage (FT_H + 8) x (FT_W + 8) = 64 x 72 bytes.  Interior tiles (every source byte inside the image): each LDS
+    // dword is one unaligned dword load, 5 per thread, all in flight before the LDS writes.  Border tiles take the
+    // REFLECT_101 byte path.
     const bool interior = (c0 >= FT_R) && (c0 + FT_W + FT_R <= W) && (r0 >= FT_R) && (r0 + FT_H + FT_R < H);
     if (interior) {
-        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
         constexpr int kDw = FT_LW / 4;               // 18 LDS dwords per row
         constexpr int kSlots = FT_LH * kDw;          // 1152
         constexpr int kPer = (kSlots + 255) / 256;   // 5
-        u32x2 v[kPer];
-        uint32_t sh[kPer];
+        // one unaligned dword load per LDS dword (the hardware's unaligned mode splits it): no alignment
+        // arithmetic in VALU
+        uint32_t v[kPer];
 #pragma unroll
         for (int u = 0; u < kPer; ++u) {
             const int t = min(tid + 256 * u, kSlots - 1);
             const int lr = t / kDw, j = t - lr * kDw;
-            const uint8_t* a = src + (int64_t)(r0 - FT_R + lr) * stride + (c0 - FT_R) + 4 * j;
-            sh[u] = (uint32_t)reinterpret_cast<uintptr_t>(a) & 3u;
-            __builtin_memcpy(&v[u], __builtin_assume_aligned(a - sh[u], 4), 8);
+            __builtin_memcpy(&v[u], src + (int64_t)(r0 - FT_R + lr) * stride + (c0 - FT_R) + 4 * j, 4);
         }
         uint32_t* tile32 = reinterpret_cast<uint32_t*>(tile);
 #pragma unroll
         for (int u = 0; u < kPer; ++u) {
             const int t = tid + 256 * u;
-            if (t < kSlots) tile32[t] = __builtin_amdgcn_alignbyte(v[u].y, v[u].x, sh[u]);
+            if (t < kSlots) tile32[t] = v[u];
         }
     } else {
         // wave w loads rows w, w+4, ...; lanes 0..63 (+ 0..7) cover 72 columns; all of this wave's row loads

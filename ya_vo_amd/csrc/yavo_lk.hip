@@ -369,25 +369,18 @@ __device__ __forceinline__ void load_footprint(const uint8_t* __restrict__ J, in
 // place from I's (S + 3) x (S + 3) neighbourhood instead of read from a derivative pyramid: the same exact integers
 // as scharr_kernel (REFLECT_101 on I), packed (dx, dy) as scharr_kernel stores them, and 0 at positions outside the
 // image (the derivative border LK reads); the window's inside is also the I footprint of the level.  Inside the
-// image one dword-aligned dwordx3 + two v_alignbyte per window row; near a border, reflected byte loads.
+// image one unaligned 8-byte load per window row; near a border, reflected byte loads.
 template <int S>
 __device__ __forceinline__ void scharr_footprint(const uint8_t* __restrict__ I, int sI, int Hl, int Wl, int x0,
                                                  int y0, int (&dv)[S + 1][S + 1], uint32_t (&ip)[S + 1][S]) {
     constexpr int N = S + 3, NW = (N + 3) / 4;
     uint32_t w[N][NW];  // bytes of I(y0 - 1 + r, x0 - 1 .. x0 + S + 1), packed 4 per dword
     if (S <= 3 && x0 >= 1 && y0 >= 1 && x0 + 8 <= Wl && y0 + S + 1 < Hl) {
-        uint32_t raw[N][3];
-        uint32_t mis[N];
+        // one unaligned 4 NW-byte load per window row (x0 - 1 + 4 NW <= x0 + 7 < Wl: inside the row)
 #pragma unroll
         for (int r = 0; r < N; ++r) {
             const uint32_t o = (uint32_t)((y0 - 1 + r) * sI + x0 - 1);
-            mis[r] = (uint32_t)((uintptr_t)I + o) & 3u;
-            __builtin_memcpy(raw[r], __builtin_assume_aligned(I + (o - mis[r]), 4), 12);
-        }
-#pragma unroll
-        for (int r = 0; r < N; ++r) {
-#pragma unroll
-            for (int q = 0; q < NW; ++q) w[r][q] = __builtin_amdgcn_alignbyte(raw[r][q + 1], raw[r][q], mis[r]);
+            __builtin_memcpy(w[r], I + o, 4 * NW);
         }
     } else {
         int cc[N];
