@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -114,6 +115,12 @@ struct yv_batch {
     } deferred;
     hipEvent_t ev_defer = nullptr;
     hipStream_t side = nullptr;
+    // edge build beside the next run (YAVO_BUILD_ASYNC, default on with the overlap, match tracker only): the
+    // build runs on `bstream` after the run's finalize (ev_fin); the next run's top-K, which rewrites the keypoint
+    // counts the build reads, waits for ev_built
+    hipStream_t bstream = nullptr;
+    bool build_async = false, build_pending = false;
+    hipEvent_t ev_fin = nullptr, ev_built = nullptr;
     hipEvent_t ev_edges[kEdgeBufs] = {}, ev_lm[kEdgeBufs] = {};
     bool lm_pending[kEdgeBufs] = {};
     hipEvent_t ev_map = nullptr;    // after the last yv_batch_track_map's block (yv_batch_map_wait)
@@ -153,6 +160,15 @@ int check_launch() {
     return YV_OK;
 }
 
+// the next writer of what an asynchronous edge build reads (keypoint counts, keypoints, match lists, pairs,
+// tracks) is ordered after it on stream s
+int join_build(yv_batch* b, hipStream_t s) {
+    if (!b->build_pending) return YV_OK;
+    YV_HIP(hipStreamWaitEvent(s, b->ev_built, 0));
+    b->build_pending = false;
+    return YV_OK;
+}
+
 bool finite_pose(const double* p) {
     for (int i = 0; i < 7; ++i)
         if (!(p[i] == p[i])) return false;
@@ -178,6 +194,7 @@ void batch_free(yv_batch* b) {
                     b->matches,   b->match_count, b->filtered, b->filt_count, b->staging,  b->match_dj,
                     b->match_lim, b->tracks,     b->track_K,  b->T_right,    b->edge_X,    b->edge_uv,
                     b->edge_query, b->edge_count, b->edge_outlier, b->track_inliers};
+    if (b->bstream) (void)hipStreamSynchronize(b->bstream);
     if (b->side) (void)hipStreamSynchronize(b->side);
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -194,6 +211,9 @@ void batch_free(yv_batch* b) {
     if (b->ev_map) (void)hipEventDestroy(b->ev_map);
     if (b->ev_defer) (void)hipEventDestroy(b->ev_defer);
     if (b->ev_map_release) (void)hipEventDestroy(b->ev_map_release);
+    if (b->ev_fin) (void)hipEventDestroy(b->ev_fin);
+    if (b->ev_built) (void)hipEventDestroy(b->ev_built);
+    if (b->bstream) (void)hipStreamDestroy(b->bstream);
     if (b->side) (void)hipStreamDestroy(b->side);
     delete b;
 }
@@ -430,6 +450,8 @@ int yv_batch_set_pairs(yv_batch* b, const int32_t* pairs, int n_pairs) {
     for (int i = 0; i < 2 * n_pairs; ++i)
         if (pairs[i] < 0 || pairs[i] > b->max_images) return YV_ERR_INVALID;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
+    if (b->bstream) YV_HIP(hipStreamSynchronize(b->bstream));  // an edge build in flight reads pairs
+    b->build_pending = false;
     if (n_pairs > 0) {
         YV_HIP(hipMemcpyAsync(b->pairs, pairs, sizeof(int32_t) * 2 * (size_t)n_pairs, hipMemcpyHostToDevice,
                               b->ctx->stream));
@@ -502,6 +524,7 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
     const int H = b->H, W = b->W, K = b->max_kp;
     const int keep = std::min(ctx->max_corners, K);
+    if (b->pending_carry >= 0 && join_build(b, s) != YV_OK) return YV_ERR_HIP;
     if (b->pending_carry >= 0) {
         const size_t c = (size_t)b->pending_carry, dst = (size_t)b->max_images, nk = (size_t)K;
         YV_HIP(hipMemcpyAsync(b->keypoints + dst * nk, b->keypoints + c * nk, nk * sizeof(yv_keypoint),
@@ -519,6 +542,7 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
                              b->cand_count, ctx->k9, b->blur, s);
     rc |= record_stage(b, s, run, 1);
     if (b->overlap_mode == 2) rc |= launch_deferred_after(b, s);
+    rc |= join_build(b, s);  // the previous track's build (beside detect) reads kp_count / keypoints / matches
     yavo::launch_topk(b->cand_keys, b->cap, b->cand_count, b->cand_seen, n_images, H, W, K, keep, b->det_rc,
                       b->det_resp, b->det_count, b->kp_src, b->kp_count, b->kp_band, b->band_off, s);
     rc |= record_stage(b, s, run, 2);
@@ -601,6 +625,8 @@ int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks, int n_tracks, const 
     if (n_tracks > 0 && !finite_pose(T_right)) return YV_ERR_INVALID;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
     hipStream_t s = b->ctx->stream;
+    if (b->bstream) YV_HIP(hipStreamSynchronize(b->bstream));  // a build in flight reads tracks / K
+    b->build_pending = false;
     if (b->side) YV_HIP(hipStreamSynchronize(b->side));  // an LM in flight reads tracks / K
     if (n_tracks > b->max_tracks) {
         void* old[] = {b->tracks, b->track_K, b->T_right, b->edge_X, b->edge_uv, b->edge_query, b->edge_count,
@@ -786,7 +812,14 @@ int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stre
     const int run = b->last_run;
     const bool timed = b->timing == 1 && run >= 0 && !b->tracked[run];
     hipEvent_t* ev = timed ? &b->events[(size_t)run * kEvPerRun] : nullptr;
-    // buffer k was last read by the LM two tracks ago (side stream): the build must not overwrite it early
+    const hipStream_t s_run = s;
+    if (b->overlap && b->build_async && b->lk_step == 0) {
+        // the build waits for the run's matches on s and leaves s free for the next run's detect
+        YV_HIP(hipEventRecord(b->ev_fin, s_run));
+        YV_HIP(hipStreamWaitEvent(b->bstream, b->ev_fin, 0));
+        s = b->bstream;
+    }
+    // buffer k was last read by the LM kEdgeBufs tracks ago (side stream): the build must not overwrite it early
     if (b->lm_pending[k]) YV_HIP(hipStreamWaitEvent(s, b->ev_lm[k], 0));
     if (timed) YV_HIP(hipEventRecord(ev[6], s));
     if (b->lk_step > 0) {
@@ -808,6 +841,10 @@ int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stre
                                  b->match_lim, b->max_kp, b->track_K, b->T_right, eX, euv, eq, ec, s);
     }
     if (b->overlap) YV_HIP(hipEventRecord(b->ev_edges[k], s));
+    if (s != s_run) {
+        YV_HIP(hipEventRecord(b->ev_built, s));
+        b->build_pending = true;
+    }
     yv_batch::DeferredLM L;
     L.active = true;
     L.k = k;
@@ -848,6 +885,20 @@ int yv_batch_set_track_overlap(yv_batch* b, int on) {
             YV_HIP(hipEventCreateWithFlags(&b->ev_edges[k], hipEventDisableTiming));
             YV_HIP(hipEventCreateWithFlags(&b->ev_lm[k], hipEventDisableTiming));
         }
+        {
+            // YAVO_BUILD_PRIO=1: the build stream at the highest priority (measured)
+            const char* e = std::getenv("YAVO_BUILD_PRIO");
+            YV_HIP(hipStreamCreateWithPriority(&b->bstream, hipStreamNonBlocking,
+                                               (e && e[0] == '1') ? greatest : 0));
+        }
+        YV_HIP(hipEventCreateWithFlags(&b->ev_fin, hipEventDisableTiming));
+        YV_HIP(hipEventCreateWithFlags(&b->ev_built, hipEventDisableTiming));
+    }
+    if (!on && b->bstream) YV_HIP(hipStreamSynchronize(b->bstream));
+    if (!on) b->build_pending = false;
+    {
+        const char* e = std::getenv("YAVO_BUILD_ASYNC");
+        b->build_async = on != 0 && !(e && e[0] == '0');
     }
     if (!on && b->side) YV_HIP(hipStreamSynchronize(b->side));
     b->overlap = on != 0;
@@ -859,6 +910,7 @@ int yv_batch_track_sync(yv_batch* b) {
     if (!b) return YV_ERR_INVALID;
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
     if (flush_deferred(b) != YV_OK) return YV_ERR_HIP;
+    if (b->bstream) YV_HIP(hipStreamSynchronize(b->bstream));
     if (b->side) YV_HIP(hipStreamSynchronize(b->side));
     return YV_OK;
 }
