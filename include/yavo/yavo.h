@@ -124,10 +124,12 @@ int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks /* [2*n_tracks] */, i
  * context stream).  d_priors [n_tracks][7] in, d_poses [n_tracks][7] out (may alias d_priors). */
 int yv_batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stream);
 /* Overlap mode: the pose LM of each yv_batch_track runs on a stream of the batch, ordered after that call's
- * edge build only, so it executes beside the next yv_batch_run's kernels (edge buffers alternate between
- * two copies; the build of track i + 2 waits for the LM of track i).  d_priors / d_poses / the track views
- * are then complete only after yv_batch_track_sync (or a device-wide synchronization).  on = 2 / 3 defer each
- * LM further: it is launched by the next yv_batch_run once that run's detect (2) / describe (3) stage is issued
+ * edge build only, so it executes beside the next yv_batch_run's kernels (edge buffers rotate over three
+ * copies; the build of track i + 3 waits for the LM of track i).  With the match tracker the edge build itself
+ * also runs on a stream of the batch, after the run's matches, beside the next run's detect; the next run's
+ * top-K waits for it (environment YAVO_BUILD_ASYNC=0 keeps it on the call's stream).  d_priors / d_poses / the
+ * track views are then complete only after yv_batch_track_sync (or a device-wide synchronization).  on = 2 / 3 / 4 defer each
+ * LM further: it is launched by the next yv_batch_run once that run's detect (2) / describe (3) / top-K (4) stage is issued
  * (so it runs beside the later, less occupancy-sensitive stages), or by yv_batch_track_sync /
  * yv_batch_map_wait / the next yv_batch_track, whichever comes first. */
 int yv_batch_set_track_overlap(yv_batch* b, int on);

@@ -1,6 +1,6 @@
+# same-box A/B of one bench knob: default vs the environment assignment given as $1 (e.g. YAVO_BUILD_ASYNC=0)
 mkdir -p gpurun_out && cd $GRAFT_REPO_ROOT && \
-timeout -k 10 300 python bench.py --cpu-baseline none > gpurun_out/b_async.log 2>&1 && \
-YAVO_BUILD_PRIO=1 timeout -k 10 300 python bench.py --cpu-baseline none > gpurun_out/b_prio.log 2>&1 && \
-YAVO_BUILD_ASYNC=0 timeout -k 10 300 python bench.py --cpu-baseline none > gpurun_out/b_sync.log 2>&1 && \
-YAVO_BUILD_PRIO=1 timeout -k 10 300 python bench.py --cpu-baseline none > gpurun_out/b_prio2.log 2>&1 && \
-timeout -k 10 300 python bench.py --cpu-baseline none > gpurun_out/b_async2.log 2>&1
+timeout -k 10 300 python bench.py > gpurun_out/ab_a1.log 2>&1 && \
+env $1 timeout -k 10 300 python bench.py > gpurun_out/ab_b1.log 2>&1 && \
+timeout -k 10 300 python bench.py > gpurun_out/ab_a2.log 2>&1 && \
+env $1 timeout -k 10 300 python bench.py > gpurun_out/ab_b2.log 2>&1
