@@ -16,6 +16,7 @@
 // with -ffp-contract=off, so each kernel matches oracle/yavo_oracle_geom.c bit for bit (sums over edges
 // in the oracle's sum_mode 1 = this file's tree order).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <float.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -1637,9 +1638,22 @@ void launch_track_build(const int32_t* tracks, int n_tracks, const int32_t* pair
                         const double* K, const double* T_right, double* edge_X, double* edge_uv, int32_t* edge_query,
                         int32_t* edge_count, hipStream_t s) {
     if (n_tracks <= 0) return;
-    // 1024 threads: about one query keypoint per thread (the FP64 triangulations are latency-bound)
-    hipLaunchKernelGGL(geom::track_build_kernel<1024>, dim3(n_tracks), dim3(1024), 0, s, tracks, pairs, keypoints,
-                       kp_count, match_dj, match_lim, max_kp, K, T_right, edge_X, edge_uv, edge_query, edge_count);
+    // 1024 threads: about one query keypoint per thread (the FP64 triangulations are latency-bound).
+    // YAVO_BUILD_NT=256 / 512 select narrower workgroups (measured).
+    static const int nt = [] {
+        const char* e = std::getenv("YAVO_BUILD_NT");
+        const int v = e ? std::atoi(e) : 1024;
+        return (v == 256 || v == 512) ? v : 1024;
+    }();
+    if (nt == 256)
+        hipLaunchKernelGGL(geom::track_build_kernel<256>, dim3(n_tracks), dim3(256), 0, s, tracks, pairs, keypoints,
+                           kp_count, match_dj, match_lim, max_kp, K, T_right, edge_X, edge_uv, edge_query, edge_count);
+    else if (nt == 512)
+        hipLaunchKernelGGL(geom::track_build_kernel<512>, dim3(n_tracks), dim3(512), 0, s, tracks, pairs, keypoints,
+                           kp_count, match_dj, match_lim, max_kp, K, T_right, edge_X, edge_uv, edge_query, edge_count);
+    else
+        hipLaunchKernelGGL(geom::track_build_kernel<1024>, dim3(n_tracks), dim3(1024), 0, s, tracks, pairs, keypoints,
+                           kp_count, match_dj, match_lim, max_kp, K, T_right, edge_X, edge_uv, edge_query, edge_count);
 }
 
 void launch_stereo_points(const int32_t* stereo_pairs, int n_tracks, const int32_t* pairs,
