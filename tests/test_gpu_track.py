@@ -93,12 +93,15 @@ def test_track_rejects_inconsistent_pairs(ctx):
     b.close()
 
 
-def test_track_overlap_pipelined(ctx, oracle, offsets):
-    """Overlap mode without any host synchronization between steps: three run + track steps back to back
-    (the LM of step i beside the kernels of step i + 1, edge buffers alternating); every step's poses, read
-    after one final sync, equal the oracle chain's."""
+@pytest.mark.parametrize("build_async", ["1", "0"])
+def test_track_overlap_pipelined(ctx, oracle, offsets, monkeypatch, build_async):
+    """Overlap mode without any host synchronization between steps: four run + track steps back to back
+    (the LM of step i beside the kernels of step i + 1, the three edge buffers wrapping; with build_async the
+    edge build of step i also runs beside step i + 1's detect and the carry-slot copy waits for it); every
+    step's poses, read after one final sync, equal the oracle chain's."""
     import torch
-    n_frames, steps = 2, 3
+    monkeypatch.setenv("YAVO_BUILD_ASYNC", build_async)  # read by yv_batch_set_track_overlap
+    n_frames, steps = 2, 4
     b, carry = _setup(ctx, n_frames)
     b.set_track_overlap(True)
     seq = [(synth_frame(61, k, 3 * k), synth_frame(61, k, 3 * k + 8)) for k in range(n_frames * steps)]
