@@ -886,10 +886,10 @@ int yv_batch_set_track_overlap(yv_batch* b, int on) {
             YV_HIP(hipEventCreateWithFlags(&b->ev_lm[k], hipEventDisableTiming));
         }
         {
-            // YAVO_BUILD_PRIO=1: the build stream at the highest priority (measured)
+            // YAVO_BUILD_PRIO=1 / 2: the build stream at the highest / lowest priority (measured)
             const char* e = std::getenv("YAVO_BUILD_PRIO");
             YV_HIP(hipStreamCreateWithPriority(&b->bstream, hipStreamNonBlocking,
-                                               (e && e[0] == '1') ? greatest : 0));
+                                               (e && e[0] == '1') ? greatest : (e && e[0] == '2') ? least : 0));
         }
         YV_HIP(hipEventCreateWithFlags(&b->ev_fin, hipEventDisableTiming));
         YV_HIP(hipEventCreateWithFlags(&b->ev_built, hipEventDisableTiming));
