@@ -265,7 +265,7 @@ def main():
     # first temporal pair is the sequence's own L_{rB} -> L_{rB+1}; frame 0 is the sequence's first (no predecessor)
     first = 1 + rank * B
     fr = synth_stereo_batch(1234, B + 1, start=first - 1)  # [2(B+1), H, W]: the halo frame, then the shard
-    images = shard_images(fr[2:], fr[0])
+    images = shard_images(fr[2:], fr[0], fr[1] if args.tracker == "lk" else None)
     del fr
     n_img = images.shape[0]
     d_frames = torch.from_numpy(images).to(dev)
@@ -485,7 +485,7 @@ def main():
                    "frames": f"one synthetic sequence (field seed 1234); rank r owns frames [1 + r*B, 1 + (r+1)*B) "
                              f"and detects / describes its predecessor frame r*B in the same run (1-frame halo, "
                              f"image {n_img - 1}), so every temporal pair L_(k-1) -> L_k is the sequence's own",
-                   "halo_images_per_step_per_gpu": 1,
+                   "halo_images_per_step_per_gpu": n_img - 2 * B,
                    "parallelism": f"frame-sharded x{world}" + (f", {'RCCL' if backend == 'nccl' else backend} "
                                                                  "all-gather of shared-map blocks"
                                                                  if use_map and world > 1 else ""),

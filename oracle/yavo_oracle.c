@@ -403,7 +403,8 @@ int or_fast_detect(const uint8_t* img, int H, int W, int stride, int thr, int ma
             uint8_t cent = img[(size_t)i * stride + j];
             int ring[16][2];
             if (mode == 0) {
-                or_bresenham_ring(i, j, ring); /* rebuilt per pixel, as the reference does */
+                /* rebuilt per pixel with the reference's std::vector / std::set containers, as it does */
+                or_bresenham_ring_stl(i, j, ring);
             } else {
                 for (int k = 0; k < 16; ++k) { ring[k][0] = i + ring0[k][0]; ring[k][1] = j + ring0[k][1]; }
             }

@@ -39,6 +39,9 @@ extern "C" {
 /* Literal Bresenham ring with the reference's two std::set orderings (src/FastDetector.cc:50-112).
  * out[k][0] = row, out[k][1] = col (absolute), k = 0..15. */
 void or_bresenham_ring(int xc, int yc, int out[16][2]);
+/* The same ring built with the reference's std::vector / std::set containers (yavo_oracle_sort.cc): the literal
+ * CPU baseline's per-pixel cost. */
+void or_bresenham_ring_stl(int xc, int yc, int out[16][2]);
 /* checkContiguousPixels (src/FastDetector.cc:135-153) with checkInBetween (:155-161). */
 int or_check_contiguous(uint8_t cent, const int ring[16][2], const uint8_t* img, int stride, int thr);
 

@@ -6,6 +6,7 @@
 // then row-major index ascending (= a stable sort of the scan order).  This entry point runs the reference's
 // actual call on the same list so the tools can count where the two orders (and the 2000-corner cuts) differ.
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <vector>
 
@@ -26,4 +27,57 @@ extern "C" int or_std_sort_cut(const int32_t* idx, const float* resp, int n, int
     const int m = n < K ? n : K;
     for (int i = 0; i < m; ++i) out_idx[i] = v[(size_t)i].x * W + v[(size_t)i].y;
     return m;
+}
+
+// The literal mode's ring (CPU baseline only): FastDetector::getBresenhamCirclePoints (src/FastDetector.cc:50-112)
+// with the reference's containers, so the per-pixel cost includes what the reference pays for them: a returned
+// std::vector of points (no reserve, push_back growth), a fresh std::vector from getAllSymPoints on every loop
+// iteration (src/FastDetector.cc:114-116), and two std::set whose comparators order by .second only
+// (src/FastDetector.cc:19-45: pairs with equal .second are equivalent, so their second insert is dropped).  The output
+// is the same ring as or_bresenham_ring's (tests/test_oracle_fast.py checks it).
+#include <set>
+#include <utility>
+namespace {
+struct RingPoint {
+    int x, y;
+};
+bool ring_comp_first(std::pair<int, int> a, std::pair<int, int> b) { return a.second < b.second; }
+bool ring_comp_sec(std::pair<int, int> a, std::pair<int, int> b) { return a.second > b.second; }
+std::vector<RingPoint> ring_sym_points(int x, int y) {
+    return {{x, y}, {y, x}, {y, -x}, {x, -y}, {-x, -y}, {-y, -x}, {-y, x}, {-x, y}};
+}
+}  // namespace
+
+extern "C" void or_bresenham_ring_stl(int xc, int yc, int out[16][2]) {
+    const int bresRadius = 3;  // include/FastDetector.hpp:34
+    int xLoop = 0, yLoop = bresRadius, d = 3 - 2 * bresRadius;
+    std::vector<RingPoint> circlePoints;
+    std::set<std::pair<int, int>, decltype(&ring_comp_first)> ordFirstHalf(&ring_comp_first);
+    std::set<std::pair<int, int>, decltype(&ring_comp_sec)> ordSecHalf(&ring_comp_sec);
+    while (yLoop >= xLoop) {
+        xLoop++;
+        if (d <= 0) {
+            d = d + 4 * xLoop + 6;
+        } else {
+            yLoop--;
+            d = d + 4 * (xLoop - yLoop) + 10;
+        }
+        const std::vector<RingPoint> sym = ring_sym_points(xLoop, yLoop);
+        for (size_t i = 0; i < sym.size(); i++) {
+            const int xAct = sym[i].x >= 0 ? xc + std::abs(sym[i].x) : xc - std::abs(sym[i].x);
+            const int yAct = sym[i].y >= 0 ? yc - std::abs(sym[i].y) : yc + std::abs(sym[i].y);
+            if (sym[i].x >= 0) ordFirstHalf.insert(std::make_pair(xAct, yAct));
+            else ordSecHalf.insert(std::make_pair(xAct, yAct));
+        }
+    }
+    ordFirstHalf.insert(std::make_pair(xc + bresRadius, yc));
+    ordSecHalf.insert(std::make_pair(xc - bresRadius, yc));
+    circlePoints.push_back({xc, yc - bresRadius});
+    for (const auto& v : ordFirstHalf) circlePoints.push_back({v.first, v.second});
+    circlePoints.push_back({xc, yc + bresRadius});
+    for (const auto& v : ordSecHalf) circlePoints.push_back({v.first, v.second});
+    for (size_t k = 0; k < 16 && k < circlePoints.size(); ++k) {
+        out[k][0] = circlePoints[k].x;
+        out[k][1] = circlePoints[k].y;
+    }
 }

@@ -25,6 +25,7 @@ class Oracle:
         lib = ctypes.CDLL(path)
         sig = {
             "or_bresenham_ring": (None, [_I, _I, _P]),
+            "or_bresenham_ring_stl": (None, [_I, _I, _P]),
             "or_check_contiguous": (_I, [ctypes.c_uint8, _P, _P, _I, _I]),
             "or_fast_detect": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, ctypes.POINTER(_I), ctypes.POINTER(_I),
                                     _P, _P, _I]),
@@ -87,9 +88,9 @@ class Oracle:
             f.argtypes = args
         self.lib = lib
 
-    def ring(self, xc=0, yc=0):
+    def ring(self, xc=0, yc=0, stl=False):
         out = np.zeros((16, 2), np.int32)
-        self.lib.or_bresenham_ring(xc, yc, _p(out))
+        (self.lib.or_bresenham_ring_stl if stl else self.lib.or_bresenham_ring)(xc, yc, _p(out))
         return out
 
     def check_contiguous(self, cent, ring, img, thr=40):

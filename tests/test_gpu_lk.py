@@ -147,3 +147,26 @@ def test_lk_pyramid_and_derivatives_match_oracle(ctx, oracle, H, W, stride, n_im
                                           err_msg=f"derivatives level {lvl} image {i}")
             ref = oracle.pyr_down(ref)
     lk.close()
+
+
+def test_lk_level_waits_for_a_build_on_another_stream(ctx, oracle):
+    """yv_lk_build on a caller stream (as the batch's LK mode does), then yv_lk_level with no synchronisation in
+    between: the level's derivatives must see the finished pyramid (it waits for the build's event)."""
+    import torch
+    H, W, n_img = 376, 1241, 6
+    rng = np.random.default_rng(11)
+    flat = rng.integers(0, 256, H * W * n_img, dtype=np.uint8)
+    d_flat = torch.from_numpy(flat).to("cuda:0")
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    lk = yv.Lk(ctx, n_img, H, W, win=11)
+    lk.build(d_flat.data_ptr(), n_img, W, H * W, stream=side.cuda_stream)
+    i = n_img - 1  # the last image's levels are written last
+    ref = flat[i * H * W:(i + 1) * H * W].reshape(H, W)
+    for lvl in range(lk.levels + 1):
+        if lvl > 0:
+            ref = oracle.pyr_down(ref)
+    d_img, st, d_der, dst, h, w = lk.level(i, lk.levels)
+    got = _d2h(d_der, (h, dst, 2), np.int16)[:, :w]
+    np.testing.assert_array_equal(got, oracle.scharr(ref))
+    lk.close()

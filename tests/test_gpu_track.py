@@ -172,3 +172,27 @@ def test_track_lk_mode_matches_oracle(ctx, oracle, offsets):
         # truncation biases the measurements by up to 1 px = 0.07 m at this depth
         np.testing.assert_allclose(T[4:], [-0.0675, -0.2025, 0.0], atol=0.07)
     b.close()
+
+
+def test_frame_shard_lk_halo_tracks_the_boundary_pair(ctx, oracle, offsets):
+    """FrameShard in LK mode with a halo: the halo frame's stereo pair seeds track 0 (halo frame -> first frame), so
+    a multi-rank LK trajectory loses no pose at a rank boundary; every track bit for bit against lk_track_pose."""
+    import torch
+    from track_chain import lk_track_pose
+    from ya_vo_amd.sharding import FrameShard, shard_images
+    B, first = 3, 5
+    seq = [(synth_frame(81, k, 3 * k), synth_frame(81, k, 3 * k + 8)) for k in range(first - 1, first + B)]
+    images = shard_images(np.stack([im for fr in seq[1:] for im in fr]), seq[0][0], seq[0][1])
+    shard = FrameShard(ctx, B, first, scene.K_KITTI, T_RIGHT, halo=True, tracker="lk", overlap_mode=0)
+    assert shard.n_tracks == B and shard.n_images == 2 * B + 2
+    d = torch.from_numpy(images).to("cuda:0")
+    torch.cuda.synchronize()
+    shard.step(d.data_ptr())
+    shard.drain()
+    P = shard.poses()
+    kps = [(oracle.brief(L, oracle.fast(L, 2000)[0], offsets), oracle.brief(R, oracle.fast(R, 2000)[0], offsets))
+           for L, R in seq]
+    for k in range(B):  # track k: frame first + k - 1 (seq[k]) -> frame first + k (seq[k + 1])
+        T = lk_track_pose(oracle, seq[k][0], seq[k + 1][0], kps[k][0], kps[k][1], scene.K_KITTI, T_RIGHT)[3]
+        np.testing.assert_array_equal(P[k], T, err_msg=f"track {k}")
+    shard.close()

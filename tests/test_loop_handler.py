@@ -137,3 +137,30 @@ def test_loop_handler_matches_oracle_loop(tmp_path, oracle):
     # the KITTI-format trajectory (T_wc rows) is the same poses
     rows = np.loadtxt(pt).reshape(n, 3, 4)
     np.testing.assert_allclose(rows[:, :, 3], [oracle.se3_inverse(p)[4:] for p in P], rtol=0, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_loop_handler_pipelined_matches_oracle_loop(tmp_path, oracle):
+    """The pipelined C++ LoopHandler (--pipeline 2: frame k + 1's read + detect + describe on a worker thread with its
+    own GPU context while frame k is tracked) over 60 synthetic mono frames with a reinitialisation at frame 40: the
+    trajectory and per-frame events equal the oracle loop's bit for bit."""
+    from loop_chain import EVENT_FIELDS, LoopChain
+    from ya_vo_amd import scene
+    n = 60
+    frames = [synth_frame(4321, *offset(k, 40), 376, 1241) for k in range(n)]
+    cfg, _ = make_sequence(tmp_path, frames)
+    pb, eb = tmp_path / "poses.bin", tmp_path / "events.bin"
+    r = subprocess.run([BIN, cfg, "--poses-bin", str(pb), "--events", str(eb), "--pipeline", "2"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    stats = json.loads(r.stdout.strip().splitlines()[-1])
+    assert stats["frames"] == n and stats["pipeline"] == 2
+    gpu_poses = np.fromfile(pb, np.float64).reshape(-1, 7)
+    gpu_events = np.fromfile(eb, np.int32).reshape(-1, len(EVENT_FIELDS))
+    offsets = np.fromfile(OFFSETS, np.int8).reshape(256, 4)
+    P, ev = LoopChain(oracle, scene.K_KITTI, offsets).run(frames)
+    ref_events = np.array([[e[f] for f in EVENT_FIELDS] for e in ev], np.int32)
+    cols = [i for i, f in enumerate(EVENT_FIELDS) if f != "f_inliers"]
+    np.testing.assert_array_equal(gpu_events[:, cols], ref_events[:, cols])
+    np.testing.assert_array_equal(gpu_poses, P)
+    assert stats["init"] == 1 and stats["reinit"] >= 1 and stats["tracked"] >= 40

@@ -43,6 +43,13 @@ def test_ring_order_literal(oracle):
     assert [tuple(map(int, ring[i])) for i in (0, 7, 4, 12)] == [(0, -3), (1, 3), (3, 0), (-3, 0)]
 
 
+def test_ring_stl_containers_build_the_same_ring(oracle):
+    """The literal CPU baseline rebuilds the ring per pixel with the reference's std::vector / std::set containers
+    (or_bresenham_ring_stl): the same 16 points in the same order, at any centre."""
+    for xc, yc in [(0, 0), (25, 25), (4, 1236), (371, 4), (187, 600)]:
+        np.testing.assert_array_equal(oracle.ring(xc, yc, stl=True), oracle.ring(xc, yc))
+
+
 def test_ring_table_in_kernel_matches_oracle(oracle):
     src = open(os.path.join(ROOT, "ya_vo_amd", "csrc", "yavo_kernels.hip")).read()
     dr = [int(v) for v in re.search(r"#define YV_RING_DR \{([^}]*)\}", src).group(1).split(",")]

@@ -1,0 +1,101 @@
+"""Throughput of the drop-in C++ caller: yavo_loop_handler (ya_vo_amd/frontend/loop_handler.cpp, the reference's
+LoopHandler over the C ABI) on a synthetic KITTI-shaped mono sequence written as PNG files, serial and pipelined.
+
+The timed region is the binary's own runVO (src/main.cc's loop): per frame cv::imread (PNG read + decode),
+getFastFeatures + computeBrief, and addFrame (INIT / trackLastFrame + optimizePoseOnly / reinitialize), every
+primitive a host-pointer C-ABI call that synchronises its stream.  Pipelined (--pipeline 2), frame k + 1's read +
+detect + describe run on a worker thread with its own GPU context while frame k is tracked; the two trajectories
+must be identical (the pipelined run computes the same things, only earlier).
+
+    python tools/bench_loop_handler.py [--frames 200] [--out profiles/r03/loop_handler.json]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "ya_vo_amd", "bin", "yavo_loop_handler")
+CALIB = ("P0: 7.188560000000e+02 0.000000000000e+00 6.071928000000e+02 0.000000000000e+00 0.000000000000e+00 "
+         "7.188560000000e+02 1.852157000000e+02 0.000000000000e+00 0.000000000000e+00 0.000000000000e+00 "
+         "1.000000000000e+00 0.000000000000e+00\n"
+         "P1: 7.188560000000e+02 0.000000000000e+00 6.071928000000e+02 -3.861448000000e+02 0.000000000000e+00 "
+         "7.188560000000e+02 1.852157000000e+02 0.000000000000e+00 0.000000000000e+00 0.000000000000e+00 "
+         "1.000000000000e+00 0.000000000000e+00\n")
+
+
+def write_sequence(base, n_frames, H=376, W=1241, seed=2024):
+    """KITTI layout under base: sequences/00/image_0/%06d.png + calib.txt, and the JSON config the binary reads."""
+    sys.path.insert(0, ROOT)
+    from PIL import Image
+    from ya_vo_amd.synth import synth_frame
+    seq = os.path.join(base, "sequences") + "/"
+    d = os.path.join(seq, "00", "image_0")
+    os.makedirs(d, exist_ok=True)
+    for k in range(n_frames):
+        Image.fromarray(synth_frame(seed, k, 3 * k, H, W)).save(os.path.join(d, f"{k:06d}.png"))
+    with open(os.path.join(seq, "00", "calib.txt"), "w") as f:
+        f.write(CALIB)
+    cfg = os.path.join(base, "config.json")
+    with open(cfg, "w") as f:
+        f.write('{\n  "basePath" : "%s",\n  "sequence" : "00",\n  "cameraType" : "mono"\n}\n' % seq)
+    return cfg
+
+
+def run_binary(cfg, out_dir, pipeline, timeout=600):
+    pb = os.path.join(out_dir, f"poses_p{pipeline}.bin")
+    t0 = time.perf_counter()
+    r = subprocess.run([BIN, cfg, "--poses-bin", pb, "--pipeline", str(pipeline)], capture_output=True, text=True,
+                       timeout=timeout)
+    wall = time.perf_counter() - t0
+    if r.returncode != 0:
+        raise RuntimeError(f"yavo_loop_handler rc={r.returncode}: {r.stderr[-1500:]}")
+    stats = json.loads(r.stdout.strip().splitlines()[-1])
+    stats["process_wall_s"] = round(wall, 4)
+    return stats, np.fromfile(pb, np.float64).reshape(-1, 7)
+
+
+def measure(n_frames=200, depth=2):
+    with tempfile.TemporaryDirectory(prefix="yavo_lh_") as tmp:
+        t0 = time.perf_counter()
+        cfg = write_sequence(tmp, n_frames)
+        write_s = time.perf_counter() - t0
+        serial, P0 = run_binary(cfg, tmp, 0)
+        piped, P1 = run_binary(cfg, tmp, depth)
+    keep = ("frames", "seconds", "frames_per_s", "init", "tracked", "reinit", "seconds_read", "seconds_features",
+            "seconds_init", "seconds_track", "seconds_reinit", "seconds_wait", "process_wall_s")
+    return {
+        "what": "ya_vo_amd/bin/yavo_loop_handler (C++ LoopHandler over the C ABI, src/LoopHandler.cc restated) on "
+                f"{n_frames} synthetic 1241x376 mono PNG frames; timed region = runVO: PNG read+decode, "
+                "detect+describe, track (world2Camera + LK + pose LM) per frame, host-pointer ABI calls",
+        "serial": {k: serial[k] for k in keep if k in serial},
+        "pipelined": {k: piped[k] for k in keep if k in piped},
+        "pipeline_depth": depth,
+        "speedup": round(piped["frames_per_s"] / serial["frames_per_s"], 3) if serial["frames_per_s"] else None,
+        "trajectories_identical": bool(P0.shape == P1.shape and np.array_equal(P0, P1)),
+        "png_write_s": round(write_s, 2),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=200)
+    ap.add_argument("--depth", type=int, default=2)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    res = measure(a.frames, a.depth)
+    s = json.dumps(res, indent=1)
+    print(s)
+    if a.out:
+        os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+        with open(a.out, "w") as f:
+            f.write(s + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -921,6 +921,8 @@ int yv_batch_set_track_lk(yv_batch* b, int image_step, int win, int max_level, i
     if (set_device(b->ctx) != YV_OK) return YV_ERR_HIP;
     if (flush_deferred(b) != YV_OK) return YV_ERR_HIP;
     if (b->side) YV_HIP(hipStreamSynchronize(b->side));
+    if (b->bstream) YV_HIP(hipStreamSynchronize(b->bstream));  // an edge build in flight (as its siblings drain)
+    b->build_pending = false;
     YV_HIP(hipStreamSynchronize(b->ctx->stream));
     if (b->lk) {
         yv_lk_destroy(b->lk);
@@ -1292,6 +1294,7 @@ struct yv_lk {
     yv_ctx* ctx = nullptr;
     int max_images = 0, H = 0, W = 0;
     int built_images = 0;  // n_images of the last yv_lk_build
+    hipEvent_t built = nullptr;  // recorded after the last yv_lk_build's pyramid, on the stream it ran on
     yavo::LkParams P;
 };
 
@@ -1336,9 +1339,11 @@ int yv_lk_create(yv_ctx* ctx, int max_images, int H, int W, int win, int max_lev
     P.pyr_pitch = std::max<int64_t>(off, 256);
     P.der_pitch = doff;
     if (dalloc(&P.pyr, (size_t)P.pyr_pitch * max_images) != YV_OK ||
-        dalloc(&P.der, (size_t)P.der_pitch * sizeof(int16_t)) != YV_OK) {
+        dalloc(&P.der, (size_t)P.der_pitch * sizeof(int16_t)) != YV_OK ||
+        hipEventCreateWithFlags(&lk->built, hipEventDisableTiming) != hipSuccess) {
         if (P.pyr) (void)hipFree(P.pyr);
         if (P.der) (void)hipFree(P.der);
+        lk->built = nullptr;
         delete lk;
         return YV_ERR_HIP;
     }
@@ -1352,6 +1357,7 @@ void yv_lk_destroy(yv_lk* lk) {
     (void)hipDeviceSynchronize();
     if (lk->P.pyr) (void)hipFree(lk->P.pyr);
     if (lk->P.der) (void)hipFree(lk->P.der);
+    if (lk->built) (void)hipEventDestroy(lk->built);
     delete lk;
 }
 
@@ -1364,7 +1370,9 @@ int yv_lk_level(yv_lk* lk, int image, int level, const uint8_t** d_img, int* img
         return YV_ERR_INVALID;
     if (set_device(lk->ctx) != YV_OK) return YV_ERR_HIP;
     const yavo::LkParams& P = lk->P;
-    // the level's derivatives into the workspace's one-level image, complete on return
+    // the level's derivatives into the workspace's one-level image, complete on return.  The pyramid may have been
+    // built on a caller stream (the batch's LK mode passes its track stream): wait for that build first
+    if (hipStreamWaitEvent(lk->ctx->stream, lk->built, 0) != hipSuccess) return YV_ERR_HIP;
     yavo::launch_lk_derivs(P, image, level, P.der, lk->ctx->stream);
     if (check_launch() != YV_OK || hipStreamSynchronize(lk->ctx->stream) != hipSuccess) return YV_ERR_HIP;
     if (level == 0) {
@@ -1392,7 +1400,8 @@ int yv_lk_build(yv_lk* lk, const uint8_t* d_images, int n_images, int stride, in
     lk->P.pitch0 = image_pitch;
     lk->built_images = n_images;
     yavo::launch_lk_pyramid(lk->P, n_images, s);
-    return check_launch();
+    if (check_launch() != YV_OK || hipEventRecord(lk->built, s) != hipSuccess) return YV_ERR_HIP;
+    return YV_OK;
 }
 
 int yv_lk_track_batch(yv_lk* lk, const int32_t* d_pairs, int n_pairs, const float* d_pts, const int32_t* d_counts,

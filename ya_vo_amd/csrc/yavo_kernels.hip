@@ -200,20 +200,35 @@ __device__ __forceinline__ float key_resp(uint64_t key) {
 
 struct K9 {
     uint32_t k[9];
-    uint32_t k4[2];   // taps 0..3 and 4..7 as packed u8 (v_dot4_u32_u8)
-    uint32_t k2e[4];  // (k0,k1) (k2,k3) (k4,k5) (k6,k7) as packed u16 (v_dot2_u32_u16), even output rows
-    uint32_t k2o[4];  // (k1,k2) (k3,k4) (k5,k6) (k7,k8), odd output rows
+    // horizontal pass: output column j (0..3) of a 4-column item is dot4(d0, kh[j][0]) + dot4(d1, kh[j][1]) +
+    // dot4(d2, kh[j][2]) over the row's 3 aligned LDS dwords d0..d2 (bytes 0..11): byte i of kh[j][m] is tap
+    // 4m + i - j (0 outside 0..8), so no byte of the row is shifted or extracted in VALU
+    uint32_t kh[4][3];
+    // vertical pass over row-pair dwords P_t = {h[2m + 2t] (lo16), h[2m + 2t + 1] (hi16)}, t = 0..4:
+    // even output row 2m = sum_t dot2(P_t, kve[t]), odd row 2m + 1 = sum_t dot2(P_t, kvo[t])
+    uint32_t kve[5];  // (k0,k1) (k2,k3) (k4,k5) (k6,k7) (k8,0)
+    uint32_t kvo[5];  // (0,k0) (k1,k2) (k3,k4) (k5,k6) (k7,k8)
+    // sum of the taps <= 256: every rounded output (acc + 2^15) >> 16 is <= 255 and acc < 2^24, so the output byte
+    // is byte 2 of the accumulator and needs no clamp (OpenCV's bit-exact kernels sum to exactly 256)
+    int byte2;
 };
 
 static K9 make_k9(const uint16_t* k9) {
-    K9 kw;
-    for (int i = 0; i < 9; ++i) kw.k[i] = k9[i];
-    for (int h = 0; h < 2; ++h)
-        kw.k4[h] = k9[4 * h] | (k9[4 * h + 1] << 8) | (k9[4 * h + 2] << 16) | ((uint32_t)k9[4 * h + 3] << 24);
-    for (int t = 0; t < 4; ++t) {
-        kw.k2e[t] = k9[2 * t] | ((uint32_t)k9[2 * t + 1] << 16);
-        kw.k2o[t] = k9[2 * t + 1] | ((uint32_t)k9[2 * t + 2] << 16);
+    K9 kw = {};
+    uint32_t sum = 0;
+    for (int i = 0; i < 9; ++i) {
+        kw.k[i] = k9[i];
+        sum += k9[i];
     }
+    auto tap = [&](int t) -> uint32_t { return (t >= 0 && t <= 8) ? (uint32_t)k9[t] : 0u; };
+    for (int j = 0; j < 4; ++j)
+        for (int m = 0; m < 3; ++m)
+            for (int i = 0; i < 4; ++i) kw.kh[j][m] |= tap(4 * m + i - j) << (8 * i);
+    for (int t = 0; t < 5; ++t) {
+        kw.kve[t] = tap(2 * t) | (tap(2 * t + 1) << 16);
+        kw.kvo[t] = tap(2 * t - 1) | (tap(2 * t) << 16);
+    }
+    kw.byte2 = sum <= 256 ? 1 : 0;
     return kw;
 }
 
@@ -460,12 +475,9 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
                 const uint32_t d0 = wr[0], d1 = wr[1], d2 = wr[2];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const uint32_t b0 = j ? __builtin_amdgcn_alignbyte(d1, d0, j) : d0;
-                    const uint32_t b1 = j ? __builtin_amdgcn_alignbyte(d2, d1, j) : d1;
-                    const uint32_t b8 = (d2 >> (8 * j)) & 0xFFu;
-                    uint32_t acc = __builtin_amdgcn_udot4(b0, kw.k4[0], 0u, false);
-                    acc = __builtin_amdgcn_udot4(b1, kw.k4[1], acc, false);
-                    hv[h][j] = acc + kw.k[8] * b8;
+                    uint32_t acc = __builtin_amdgcn_udot4(d0, kw.kh[j][0], 0u, false);
+                    acc = __builtin_amdgcn_udot4(d1, kw.kh[j][1], acc, false);
+                    hv[h][j] = __builtin_amdgcn_udot4(d2, kw.kh[j][2], acc, false);
                 }
             }
             *reinterpret_cast<uint4*>(&hbuf[q * FT_W + xq]) =
@@ -519,20 +531,34 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
             uint4 P[5];
 #pragma unroll
             for (int t = 0; t < 5; ++t) P[t] = *reinterpret_cast<const uint4*>(&hbuf[(m + t) * FT_W + xq]);
-            uint32_t w0 = 0, w1 = 0;
+            // accumulators start at 2^15 (the rounding term of (acc + 2^15) >> 16)
+            uint32_t ev[4], od[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 auto col = [&](const uint4& q) { return j == 0 ? q.x : j == 1 ? q.y : j == 2 ? q.z : q.w; };
-                uint32_t ev = 0, od = kw.k[0] * (col(P[0]) >> 16);
+                uint32_t e = 1u << 15, o = 1u << 15;
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    ev = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, col(P[t])), __builtin_bit_cast(us2, kw.k2e[t]), ev, false);
-                    od = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, col(P[t + 1])), __builtin_bit_cast(us2, kw.k2o[t]), od, false);
+                for (int t = 0; t < 5; ++t) {
+                    e = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, col(P[t])), __builtin_bit_cast(us2, kw.kve[t]), e, false);
+                    o = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, col(P[t])), __builtin_bit_cast(us2, kw.kvo[t]), o, false);
                 }
-                ev += kw.k[8] * (col(P[4]) & 0xFFFFu);
-                const uint32_t v0 = min((ev + (1u << 15)) >> 16, 255u), v1 = min((od + (1u << 15)) >> 16, 255u);
-                w0 |= v0 << (8 * j);
-                w1 |= v1 << (8 * j);
+                ev[j] = e;
+                od[j] = o;
+            }
+            uint32_t w0, w1;
+            if (kw.byte2) {
+                // output byte = byte 2 of each accumulator: two v_perm pick them pairwise, one v_perm joins the pairs
+                w0 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(ev[3], ev[2], 0x0c0c0602u),
+                                           __builtin_amdgcn_perm(ev[1], ev[0], 0x0c0c0602u), 0x05040100u);
+                w1 = __builtin_amdgcn_perm(__builtin_amdgcn_perm(od[3], od[2], 0x0c0c0602u),
+                                           __builtin_amdgcn_perm(od[1], od[0], 0x0c0c0602u), 0x05040100u);
+            } else {
+                w0 = w1 = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    w0 |= min(ev[j] >> 16, 255u) << (8 * j);
+                    w1 |= min(od[j] >> 16, 255u) << (8 * j);
+                }
             }
             const int r = r0 + 2 * m, c = c0 + xq;
             if (r < H) *reinterpret_cast<uint32_t*>(&dst[(int64_t)r * bp + c]) = w0;
@@ -883,6 +909,8 @@ constexpr int BR_ROWS = BR_BAND + 17;  // rows r0-8 .. r0+40 (the last one for t
 #endif
 constexpr int BR_NT = YAVO_BR_NT;
 constexpr int BR_NW = BR_NT / 64;
+// the band's keypoint records are loaded as 4 per thread (kq below): a band may hold every keypoint of the image
+static_assert(4 * BR_NT >= kMaxKp, "brief_kernel loads at most 4 * BR_NT band records");
 
 __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict__ blur, int H, int W,
                                                     const int8_t* __restrict__ offsets,

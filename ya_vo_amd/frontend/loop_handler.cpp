@@ -5,9 +5,13 @@
 #include <chrono>
 #include <climits>
 #include <cmath>
+#include <condition_variable>
+#include <deque>
 #include <fstream>
 #include <iostream>
 #include <iterator>
+#include <mutex>
+#include <thread>
 
 #include "../../include/yavo/yavo_geom.h"
 #include "json_config.hpp"
@@ -100,6 +104,7 @@ bool LoopHandler::gpu(int st, const char* what) {
 // :918-930
 Frame::ptr LoopHandler::getNextFrame() {
     if (train_it_ >= leftPathTrain.size()) return nullptr;
+    const double t0 = now_s();
     const std::string& path = leftPathTrain[train_it_];
     // cv::imread(path, IMREAD_GRAYSCALE) (:919) = the PNG file decoded to 8-bit grey
     std::ifstream fin(path, std::ios::binary);
@@ -121,6 +126,7 @@ Frame::ptr LoopHandler::getNextFrame() {
     currentFrameId_ = (int)train_it_;
     train_it_++;
     frame->frameID = Frame::createFrameID();
+    t_read += now_s() - t0;
     return frame;
 }
 
@@ -419,11 +425,106 @@ bool LoopHandler::reinitialize() {
 
 // :501-512
 void LoopHandler::runVO(int max_frames) {
+    if (pipeline_depth_ > 0) {
+        runVOPipelined(max_frames);
+        return;
+    }
     int k = 0;
     while (max_frames < 0 || k < max_frames) {
         if (!takeVOStep()) break;
         ++k;
     }
+}
+
+void LoopHandler::setPipeline(int depth, int device, const std::vector<int8_t>& briefOffsets) {
+    pipeline_depth_ = depth > 0 ? depth : 0;
+    pipeline_device_ = device;
+    pipeline_offsets_ = briefOffsets;
+}
+
+// takeVOStep split over two threads: the worker runs getNextFrame + insertFrameFeatures on its own context for
+// frame k + 1 while this thread runs addFrame(frame k).  Frames leave the worker in path-train order, so ids,
+// keypoints and every later result are the serial loop's.
+void LoopHandler::runVOPipelined(int max_frames) {
+    struct Item {
+        Frame::ptr frame;  // nullptr: the end of the train (or a failure, with status != YV_OK)
+        int index = -1;
+        int status = YV_OK;
+    };
+    std::mutex mu;
+    std::condition_variable cv_put, cv_get;
+    std::deque<Item> q;
+    bool stop = false;
+    double worker_features = 0;
+    const size_t depth = (size_t)pipeline_depth_;
+    std::thread worker([&]() {
+        Device wdev(pipeline_device_);
+        int st = wdev.ok() ? YV_OK : wdev.status();
+        std::unique_ptr<FastDetector> wfd;
+        std::unique_ptr<Brief> wbrief;
+        if (st == YV_OK) {
+            wfd = std::make_unique<FastDetector>(wdev, 12, 50);
+            wbrief = std::make_unique<Brief>(wdev, 256);
+            if (!wbrief->setOffsets(pipeline_offsets_)) st = wbrief->status() != YV_OK ? wbrief->status() : YV_ERR_INVALID;
+            if (st == YV_OK) st = wfd->status();
+        }
+        int produced = 0;
+        while (true) {
+            Item it;
+            it.status = st;
+            if (st == YV_OK && (max_frames < 0 || produced < max_frames)) {
+                it.frame = getNextFrame();  // only this thread reads the path train
+                it.index = currentFrameId_;
+                if (it.frame) {
+                    const double t0 = now_s();
+                    auto features = wfd->getFastFeatures(*it.frame);
+                    it.status = wfd->status();
+                    if (it.status == YV_OK) {
+                        wbrief->computeBrief(features, *it.frame);
+                        it.status = wbrief->status();
+                    }
+                    worker_features += now_s() - t0;
+                    if (it.status != YV_OK) it.frame = nullptr;
+                }
+            }
+            const bool last = !it.frame;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv_put.wait(lk, [&]() { return stop || q.size() < depth; });
+                if (stop) return;
+                q.push_back(std::move(it));
+            }
+            cv_get.notify_one();
+            if (last) return;
+            ++produced;
+        }
+    });
+    while (true) {
+        Item it;
+        {
+            const double t0 = now_s();
+            std::unique_lock<std::mutex> lk(mu);
+            cv_get.wait(lk, [&]() { return !q.empty(); });
+            it = std::move(q.front());
+            q.pop_front();
+            t_wait += now_s() - t0;
+        }
+        cv_put.notify_one();
+        if (!it.frame) {
+            if (it.status != YV_OK) gpu(it.status, "insertFrameFeatures (pipeline worker)");
+            break;
+        }
+        currentFrameId_ = it.index;
+        addFrame(it.frame);
+        if (gpu_status_ != YV_OK) break;
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        stop = true;
+    }
+    cv_put.notify_all();
+    worker.join();
+    t_features += worker_features;
 }
 
 }  // namespace yavo_fe

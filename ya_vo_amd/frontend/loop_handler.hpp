@@ -111,6 +111,13 @@ public:
                          bool firstView);
     void runVO(int max_frames = -1);
 
+    // Pipelined loop (the reference runs takeVOStep strictly in series, src/LoopHandler.cc:453-530): frame k + 1's
+    // getNextFrame + insertFrameFeatures (PNG decode, detect, describe) do not depend on frame k's addFrame, so a
+    // worker thread with its own GPU context (its own stream) computes them while this thread tracks frame k.  The
+    // queue between the two holds at most `depth` frames.  Every result is the serial loop's: same frames, same
+    // ids, same kernels, only earlier.  BRIEF's offsets must be given here (they are per context).
+    void setPipeline(int depth, int device, const std::vector<int8_t>& briefOffsets);
+
     // every added frame's pose (T_cw, SE3d::data()) in order, and what happened to it
     const std::vector<SE3>& trajectory() const { return trajectory_; }
     const std::vector<FrameEvent>& events() const { return events_; }
@@ -122,6 +129,8 @@ public:
     Map::ptr map;
     SE3 relativeMotion;
     double t_features = 0, t_init = 0, t_track = 0, t_reinit = 0;  // seconds, summed
+    double t_read = 0;  // getNextFrame (file read + PNG decode), summed
+    double t_wait = 0;  // pipelined: the tracking thread waiting for the worker's next frame
 
 private:
     std::string seqNo_, leftImagesPath_, rightImagesPath_, basePath_;
@@ -142,7 +151,11 @@ private:
     std::mt19937 ransac_rng_{0};  // getFRANSAC's sample draws (the reference seeds from std::random_device)
     int gpu_status_ = YV_OK;
 
+    int pipeline_depth_ = 0, pipeline_device_ = 0;
+    std::vector<int8_t> pipeline_offsets_;
+
     bool gpu(int st, const char* what);
+    void runVOPipelined(int max_frames);
     int getFRANSAC(const std::vector<Matches>& m, double F[9]);
     bool essentialPose(const std::vector<Matches>& filt, SE3& currPose);
 };

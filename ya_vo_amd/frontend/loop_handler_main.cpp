@@ -3,12 +3,15 @@
 //
 // usage: yavo_loop_handler CONFIG.json [--frames N] [--poses KITTI.txt] [--poses-bin POSES.bin]
 //                                      [--events EVENTS.bin] [--offsets-seed S] [--device D] [--check-config]
+//                                      [--pipeline DEPTH]
 //   --check-config   no GPU: print the parsed configuration, the path train and the first frames as JSON (the
 //                    reference's LoopHandlerTest cases: stereoStatus, getSeqNo, getLeftImagesPath,
 //                    getLeftTrainLength, getNextFrame dimensions, frame ids)
 //   --poses-bin      n x 7 doubles (SE3d::data() of T_cw per frame), exact
 //   --events         n x 9 int32 (FrameEvent fields)
 //   --offsets-seed   BRIEF's preComputeOffsets seed (the reference uses std::random_device; default 42)
+//   --pipeline       DEPTH > 0: frame k + 1's read + detect + describe on a worker thread (own GPU context) while
+//                    frame k is tracked (LoopHandler::setPipeline); the results are the serial loop's
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -37,7 +40,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     const std::string config = argv[1];
-    int frames = -1, device = 0;
+    int frames = -1, device = 0, pipeline = 0;
     uint32_t seed = 42;
     bool check = false;
     std::string poses_txt, poses_bin, events_bin;
@@ -50,6 +53,7 @@ int main(int argc, char** argv) {
         else if (a == "--events") events_bin = next();
         else if (a == "--offsets-seed") seed = (uint32_t)std::strtoul(next().c_str(), nullptr, 10);
         else if (a == "--device") device = std::atoi(next().c_str());
+        else if (a == "--pipeline") pipeline = std::atoi(next().c_str());
         else if (a == "--check-config") check = true;
         else {
             std::cerr << "unknown option " << a << std::endl;
@@ -88,7 +92,9 @@ int main(int argc, char** argv) {
         return 1;
     }
     Brief offsets_setter(dev, 256);
-    if (!offsets_setter.setOffsets(Brief::preComputeOffsets(seed))) return 3;
+    const std::vector<int8_t> offsets = Brief::preComputeOffsets(seed);
+    if (!offsets_setter.setOffsets(offsets)) return 3;
+    if (pipeline > 0) lh.setPipeline(pipeline, device, offsets);
 
     const auto t0 = std::chrono::steady_clock::now();
     lh.runVO(frames);
@@ -124,6 +130,8 @@ int main(int argc, char** argv) {
               << ", \"init\": " << n_init << ", \"tracked\": " << n_track << ", \"reinit\": " << n_reinit
               << ", \"keyframes\": " << lh.map->getFrames().size() << ", \"map_points\": " << lh.map->getMps().size()
               << ", \"seconds_features\": " << lh.t_features << ", \"seconds_init\": " << lh.t_init
-              << ", \"seconds_track\": " << lh.t_track << ", \"seconds_reinit\": " << lh.t_reinit << "}" << std::endl;
+              << ", \"seconds_track\": " << lh.t_track << ", \"seconds_reinit\": " << lh.t_reinit
+              << ", \"seconds_read\": " << lh.t_read << ", \"seconds_wait\": " << lh.t_wait
+              << ", \"pipeline\": " << pipeline << "}" << std::endl;
     return 0;
 }

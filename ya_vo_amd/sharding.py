@@ -64,15 +64,19 @@ def gather_frame_records(local, n_frames: int, world: int, rank: int):
     return torch.cat([o[: len(s.frames)] for o, s in zip(outs, shards)], dim=0)
 
 
-def shard_images(stereo, halo_left=None):
+def shard_images(stereo, halo_left=None, halo_right=None):
     """Device image layout of one rank's shard: [L_0, R_0, ..., L_{B-1}, R_{B-1}] then, when the shard has a
-    predecessor, the halo frame's left image (index 2B).  `stereo` [B, 2, H, W] or [2B, H, W] uint8."""
+    predecessor, the halo frame's left image (index 2B) and, for the LK tracker, its right image (index 2B + 1: the
+    halo frame's stereo map points seed the shard's first LK track).  `stereo` [B, 2, H, W] or [2B, H, W] uint8."""
     import numpy as np
     s = np.asarray(stereo, np.uint8)
     s = s.reshape(-1, s.shape[-2], s.shape[-1])
     if halo_left is None:
         return np.ascontiguousarray(s)
-    return np.ascontiguousarray(np.concatenate([s, np.asarray(halo_left, np.uint8)[None]]))
+    extra = [np.asarray(halo_left, np.uint8)[None]]
+    if halo_right is not None:
+        extra.append(np.asarray(halo_right, np.uint8)[None])
+    return np.ascontiguousarray(np.concatenate([s] + extra))
 
 
 class FrameShard:
@@ -81,7 +85,10 @@ class FrameShard:
     detected and described in the same run (image index 2 * n_frames), so the shard's first temporal pair
     L_{first-1} -> L_first needs no communication and gives the same matches a 1-rank run over the whole sequence
     gets from its carry slot.  Without `halo` the first pair reads the batch's carry slot (empty on the first run:
-    the sequence's frame 0 has no predecessor, as in the reference's first takeVOStep).
+    the sequence's frame 0 has no predecessor, as in the reference's first takeVOStep).  The LK tracker
+    (trackLastFrame, src/LoopHandler.cc:327-413) tracks frame k-1's stereo map points into L_k, so with a halo it also
+    takes the halo frame's right image (index 2B + 1, `shard_images(..., halo_right)`) and its stereo pair: track 0 is
+    then the halo frame -> first_frame, as in match mode, and no pose is lost at a rank boundary.
 
     Per step (one pass over the shard's resident images, `step`): yv_batch_run (detect / describe L and R, match
     L_{k-1} -> L_k and L_k -> R_k, removeOutliers), then yv_batch_track_map (stereo triangulation + pose-only LM per
@@ -104,8 +111,9 @@ class FrameShard:
         self.world, self.rank, self.backend = world, rank, backend
         self.H, self.W, self.max_kp, self.match_thr = H, W, max_kp, match_thr
         B = n_frames
-        self.n_images = 2 * B + (1 if halo else 0)
-        self.batch = Batch(ctx, self.n_images, H, W, max_kp, 2 * B)
+        lk_halo = halo and tracker == "lk"
+        self.n_images = 2 * B + (2 if lk_halo else 1 if halo else 0)
+        self.batch = Batch(ctx, self.n_images, H, W, max_kp, 2 * B + (1 if lk_halo else 0))
         prev0 = 2 * B if halo else self.n_images  # the halo image, or the carry slot (index max_images)
         pairs, tracks = [], []
         for k in range(B):
@@ -115,6 +123,9 @@ class FrameShard:
                 tracks.append((2 * k + 1, 2 * k))                     # PnP of frame k-1 against frame k's map
             elif k > 0:
                 tracks.append((2 * (k - 1) + 1, 2 * k))               # LK: frame k-1's stereo map -> L_k
+        if lk_halo:
+            pairs.append((2 * B, 2 * B + 1))                          # the halo frame's stereo pair (index 2B)
+            tracks.insert(0, (2 * B, 0))                              # LK: halo frame's stereo map -> L_0
         self.pairs, self.tracks = pairs, tracks
         self.batch.set_pairs(pairs)
         if tracker == "lk":
@@ -183,8 +194,11 @@ class FrameShard:
         torch.cuda.synchronize(self.d_prior.device)
 
     def poses(self):
-        """[n_tracks, 7] relative poses of the last step: track k = frame first + k - 1 in frame first + k's
-        camera (SE3d::data())."""
+        """[n_tracks, 7] relative poses of the last step (SE3d::data()), track k for the frame pair
+        (first + k - 1, first + k).  Match tracker: the edges hold frame first + k's stereo points and frame
+        first + k - 1's keypoints, so the pose maps frame first + k's camera coordinates into frame first + k - 1's.
+        LK tracker (trackLastFrame): frame first + k - 1's stereo points tracked into frame first + k, so the pose maps
+        the other way.  Without a halo the LK tracks start at the pair (first, first + 1)."""
         return self.d_poses[(self.calls - 1) & 1].cpu().numpy()
 
     def placed_map(self):
