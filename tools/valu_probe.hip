@@ -31,7 +31,7 @@ static const char* kOpName[OP_N] = {
 #define R8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 
 template <int OP>
-__global__ __launch_bounds__(256) void probe(int rounds, uint32_t seed, unsigned long long* stamps, uint32_t* sink) {
+__global__ __launch_bounds__(1024) void probe(int rounds, uint32_t seed, unsigned long long* stamps, uint32_t* sink) {
     extern __shared__ uint32_t lds[];
     const uint32_t t = threadIdx.x;
     uint32_t a0 = seed ^ t, a1 = a0 * 3u, a2 = a0 * 5u, a3 = a0 * 7u, a4 = a0 * 11u, a5 = a0 * 13u, a6 = a0 * 17u,
@@ -41,12 +41,12 @@ __global__ __launch_bounds__(256) void probe(int rounds, uint32_t seed, unsigned
     const float fb = 1.0000001f;
     double d0 = a0, d1 = d0 + 1, d2 = d0 + 2, d3 = d0 + 3, d4 = d0 + 4, d5 = d0 + 5, d6 = d0 + 6, d7 = d0 + 7;
     const double db = 1.0000000001;
-    if (OP == OP_DS_READ_U8 || OP == OP_DS_READ_B32) {
-        for (int i = t; i < 4096; i += 256) lds[i] = i * 2654435761u;
-        __syncthreads();
-    }
     // lane l reads byte / dword l (+ a per-chain row): conflict-free
     const uint32_t lbase = (OP == OP_DS_READ_U8 ? (t & 63) : 4 * (t & 63));
+    if (OP == OP_DS_READ_U8 || OP == OP_DS_READ_B32) {
+        for (int i = t; i < 4096; i += blockDim.x) lds[i] = i * 2654435761u;
+        __syncthreads();
+    }
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
     for (int r = 0; r < rounds; ++r) {
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(256) void probe(int rounds, uint32_t seed, unsigned
                          (uint32_t)(d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7);
     if (acc == 0x12345678u) sink[0] = acc;  // keeps every chain live
     if ((t & 63) == 0) {
-        const uint32_t w = blockIdx.x * 4 + (t >> 6);
+        const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (t >> 6);
         stamps[4 * w + 0] = t0;
         stamps[4 * w + 1] = t1;
         stamps[4 * w + 2] = rt0;
@@ -154,12 +154,12 @@ int main(int argc, char** argv) {
     unsigned long long* stamps;
     uint32_t* sink;
     const int max_blocks = ncu * 8;
-    CK(hipMalloc(&stamps, (size_t)max_blocks * 4 * 4 * sizeof(unsigned long long)));
+    CK(hipMalloc(&stamps, (size_t)max_blocks * 16 * 4 * sizeof(unsigned long long)));
     CK(hipMalloc(&sink, 4));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    std::vector<unsigned long long> h((size_t)max_blocks * 16);
+    std::vector<unsigned long long> h((size_t)max_blocks * 64);
     printf("%-20s %3s %12s %12s %10s %8s\n", "op", "W", "cyc/inst/SIMD", "wall cyc/in", "clock GHz", "ms");
     for (int op = 0; op < OP_N; ++op) {
         const bool f64 = (op == OP_FMA_F64 || op == OP_ADD_F64);
@@ -194,6 +194,47 @@ int main(int argc, char** argv) {
             const double per_simd = med / (W * inst);
             const double wall = ms * 1e-3 * ghz * 1e9 / (W * inst);
             printf("%-20s %3d %12.2f %12.2f %10.3f %8.3f\n", kOpName[op], W, per_simd, wall, ghz, ms);
+        }
+    }
+    // Mode 2: ONE workgroup of 256 W threads per CU (W waves on each SIMD, dispatched together), long runs; per CU the
+    // window max(end) - min(start) over its waves: cycles per instruction per SIMD = window / (W * inst)
+    printf("\nmode 2: one %s per CU\n", "256 W-thread workgroup");
+    printf("%-20s %3s %14s %10s %8s\n", "op", "W", "cyc/inst/SIMD", "clock GHz", "ms");
+    for (int op = 0; op < OP_N; ++op) {
+        const bool f64 = (op == OP_FMA_F64 || op == OP_ADD_F64);
+        const bool lds = (op == OP_DS_READ_U8 || op == OP_DS_READ_B32);
+        for (int W : {1, 2, 4}) {
+            const int rounds = (f64 || lds ? 8000 : 16000) / W;
+            const int nt = 256 * W;
+            const size_t dyn = 100 * 1024;  // one workgroup per CU
+            CK(hipFuncSetAttribute((const void*)kFn[op], hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+            hipLaunchKernelGGL(kFn[op], dim3(ncu), dim3(nt), dyn, 0, rounds, 7u, stamps, sink);
+            CK(hipGetLastError());
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0, 0));
+            hipLaunchKernelGGL(kFn[op], dim3(ncu), dim3(nt), dyn, 0, rounds, 7u, stamps, sink);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            const int nw = ncu * 4 * W;
+            CK(hipMemcpy(h.data(), stamps, (size_t)nw * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+            std::vector<double> win, clk;
+            for (int b = 0; b < ncu; ++b) {
+                unsigned long long lo = ~0ull, hi = 0, rlo = ~0ull, rhi = 0;
+                for (int w = 0; w < 4 * W; ++w) {
+                    const unsigned long long* q = &h[4 * (size_t)(b * 4 * W + w)];
+                    lo = std::min(lo, q[0]); hi = std::max(hi, q[1]);
+                    rlo = std::min(rlo, q[2]); rhi = std::max(rhi, q[3]);
+                }
+                win.push_back((double)(hi - lo));
+                if (rhi > rlo) clk.push_back((double)(hi - lo) / (double)(rhi - rlo) * 0.1);
+            }
+            std::sort(win.begin(), win.end());
+            std::sort(clk.begin(), clk.end());
+            const double inst = 8.0 * rounds;
+            printf("%-20s %3d %14.2f %10.3f %8.3f\n", kOpName[op], W, win[win.size() / 2] / (W * inst),
+                   clk.empty() ? 0 : clk[clk.size() / 2], ms);
         }
     }
     return 0;

@@ -29,6 +29,22 @@ struct yv_ctx {
     int32_t* h_pinned = nullptr;                              // small pinned scratch for counts
     void* scratch = nullptr;                                  // device arena of the geometry host calls
     size_t scratch_cap = 0;
+    // yv_calc_optical_flow_pyr_lk's pyramid workspace, kept between calls (creating and destroying it per call
+    // costs two hipMalloc / hipFree pairs and a device-wide synchronisation per tracked frame)
+    yv_lk* lk_cache = nullptr;
+    int lk_key[4] = {0, 0, 0, 0};  // H, W, win, max_level
+    // Pinned staging of the host-pointer entry points.  The caller's buffers are pageable: a hipMemcpyAsync from or to
+    // pageable memory is synchronous and goes through the runtime's own staging (~250 us per call, even for a
+    // 4-byte count, and serialised across threads).  Uploads are copied into this buffer and DMA'd from it;
+    // downloads land in it and are copied out after the call's stream synchronisation (stage_sync).
+    uint8_t* h_stage = nullptr;
+    size_t h_stage_cap = 0, h_stage_off = 0;
+    struct PendingD2H {
+        void* dst;
+        const void* src;
+        size_t bytes;
+    };
+    std::vector<PendingD2H> pending;
 };
 
 namespace yavo {
@@ -223,6 +239,91 @@ int set_device(yv_ctx* ctx) {
     return YV_OK;
 }
 
+// ---- pinned staging of the host-pointer entry points (yv_ctx::h_stage) ----
+bool in_pinned_scratch(const yv_ctx* ctx, const void* p) {
+    const char* c = static_cast<const char*>(p);
+    const char* b = reinterpret_cast<const char*>(ctx->h_pinned);
+    return ctx->h_pinned && c >= b && c < b + 64 * sizeof(int32_t);
+}
+
+// the downloads of the call land in the caller's buffers once the stream has drained
+hipError_t stage_sync(yv_ctx* ctx, hipStream_t s) {
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        ctx->pending.clear();
+        return e;
+    }
+    for (const auto& d : ctx->pending) std::memcpy(d.dst, d.src, d.bytes);
+    ctx->pending.clear();
+    ctx->h_stage_off = 0;
+    return hipSuccess;
+}
+
+// `bytes` of the staging buffer for this call (64-B aligned); grows it after draining the stream when full
+uint8_t* stage_alloc(yv_ctx* ctx, size_t bytes, hipStream_t s) {
+    const size_t need = (bytes + 63) & ~(size_t)63;
+    if (ctx->h_stage_off + need > ctx->h_stage_cap) {
+        if (ctx->h_stage_off > 0 && stage_sync(ctx, s) != hipSuccess) return nullptr;
+        if (need > ctx->h_stage_cap) {
+            if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+            ctx->h_stage = nullptr;
+            ctx->h_stage_cap = 0;
+            const size_t cap = std::max(need, (size_t)4 << 20);
+            if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_stage), cap) != hipSuccess) {
+                ctx->h_stage = nullptr;
+                return nullptr;
+            }
+            ctx->h_stage_cap = cap;
+        }
+    }
+    uint8_t* p = ctx->h_stage + ctx->h_stage_off;
+    ctx->h_stage_off += need;
+    return p;
+}
+
+hipError_t stage_h2d(yv_ctx* ctx, void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    if (in_pinned_scratch(ctx, src)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+    uint8_t* p = stage_alloc(ctx, bytes, s);
+    if (!p) return hipErrorOutOfMemory;
+    std::memcpy(p, src, bytes);
+    return hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, s);
+}
+
+// a pitched host image (rows of `width` bytes, `spitch` apart) into a pitched device image
+hipError_t stage_h2d_2d(yv_ctx* ctx, void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
+                        size_t height, hipStream_t s) {
+    if (width == 0 || height == 0) return hipSuccess;
+    uint8_t* p = stage_alloc(ctx, width * height, s);
+    if (!p) return hipErrorOutOfMemory;
+    const uint8_t* q = static_cast<const uint8_t*>(src);
+    if (spitch == width) std::memcpy(p, q, width * height);
+    else
+        for (size_t r = 0; r < height; ++r) std::memcpy(p + r * width, q + r * spitch, width);
+    // a packed destination takes one linear DMA: hipMemcpy2DAsync moves a 376-row image as row-sized transfers at
+    // ~0.2 GB/s (2.6 ms per KITTI frame in the r03 LoopHandler trace)
+    if (dpitch == width) return hipMemcpyAsync(dst, p, width * height, hipMemcpyHostToDevice, s);
+    return hipMemcpy2DAsync(dst, dpitch, p, width, width, height, hipMemcpyHostToDevice, s);
+}
+
+hipError_t stage_d2h(yv_ctx* ctx, void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    if (in_pinned_scratch(ctx, dst)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
+    uint8_t* p = stage_alloc(ctx, bytes, s);
+    if (!p) return hipErrorOutOfMemory;
+    ctx->pending.push_back({dst, p, bytes});
+    return hipMemcpyAsync(p, src, bytes, hipMemcpyDeviceToHost, s);
+}
+
+// Drops the downloads of a call that returns before its stage_sync (an error path): they must not be copied into
+// buffers the caller no longer expects to be written.  The staging offset is kept, so nothing still in flight is
+// overwritten before the next stage_sync.
+struct StageScope {
+    yv_ctx* ctx;
+    explicit StageScope(yv_ctx* c) : ctx(c) {}
+    ~StageScope() { ctx->pending.clear(); }
+};
+
 // The host-pointer entry points share one single-image workspace per context.
 int ensure_single(yv_ctx* ctx, int H, int W) {
     if (ctx->single && ctx->single->H == H && ctx->single->W == W) return YV_OK;
@@ -299,10 +400,12 @@ void yv_destroy(yv_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->lk_cache) yv_lk_destroy(ctx->lk_cache);
     batch_free(ctx->single);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->d_offsets) (void)hipFree(ctx->d_offsets);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -947,8 +1050,7 @@ int yv_batch_set_track_lk(yv_batch* b, int image_step, int win, int max_level, i
 // host-pointer drop-in entry points
 // ------------------------------------------------------------------------------------------------
 static int upload_image(yv_batch* b, const uint8_t* img, int stride, hipStream_t s) {
-    YV_HIP(hipMemcpy2DAsync(b->staging, (size_t)b->W, img, (size_t)stride, (size_t)b->W, (size_t)b->H,
-                            hipMemcpyHostToDevice, s));
+    YV_HIP(stage_h2d_2d(b->ctx, b->staging, (size_t)b->W, img, (size_t)stride, (size_t)b->W, (size_t)b->H, s));
     return YV_OK;
 }
 
@@ -956,6 +1058,7 @@ int yv_detect(yv_ctx* ctx, const uint8_t* img, int H, int W, int stride, int max
               int* n, int* n_candidates) {
     if (!ctx || !img || !rc || !n || H < 9 || W < 9 || stride < W || max_kp < 0) return YV_ERR_INVALID;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     int st = ensure_single(ctx, H, W);
     if (st != YV_OK) return st;
     yv_batch* b = ctx->single;
@@ -967,14 +1070,14 @@ int yv_detect(yv_ctx* ctx, const uint8_t* img, int H, int W, int stride, int max
     yavo::launch_topk(b->cand_keys, b->cap, b->cand_count, b->cand_seen, 1, H, W, b->max_kp, keep, b->det_rc, b->det_resp,
                       b->det_count, b->kp_src, b->kp_count, b->kp_band, b->band_off, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(hipMemcpyAsync(ctx->h_pinned, b->det_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    YV_HIP(hipMemcpyAsync(ctx->h_pinned + 1, b->cand_seen, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    YV_HIP(hipStreamSynchronize(s));
+    YV_HIP(stage_d2h(ctx, ctx->h_pinned, b->det_count, sizeof(int32_t), s));
+    YV_HIP(stage_d2h(ctx, ctx->h_pinned + 1, b->cand_seen, sizeof(uint32_t), s));
+    YV_HIP(stage_sync(ctx, s));
     const int k = ctx->h_pinned[0];
     if (k > 0) {
-        YV_HIP(hipMemcpyAsync(rc, b->det_rc, sizeof(int32_t) * 2 * (size_t)k, hipMemcpyDeviceToHost, s));
-        if (resp) YV_HIP(hipMemcpyAsync(resp, b->det_resp, sizeof(float) * (size_t)k, hipMemcpyDeviceToHost, s));
-        YV_HIP(hipStreamSynchronize(s));
+        YV_HIP(stage_d2h(ctx, rc, b->det_rc, sizeof(int32_t) * 2 * (size_t)k, s));
+        if (resp) YV_HIP(stage_d2h(ctx, resp, b->det_resp, sizeof(float) * (size_t)k, s));
+        YV_HIP(stage_sync(ctx, s));
     }
     *n = k;
     if (n_candidates) *n_candidates = ctx->h_pinned[1];
@@ -986,26 +1089,27 @@ int yv_describe(yv_ctx* ctx, const uint8_t* img, int H, int W, int stride, const
     if (!ctx || !img || !out || !n_out || H < 9 || W < 9 || stride < W || n < 0 || (n > 0 && !rc)) return YV_ERR_INVALID;
     if (n > yavo::kMaxKp) return YV_ERR_CAPACITY;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     int st = ensure_single(ctx, H, W);
     if (st != YV_OK) return st;
     yv_batch* b = ctx->single;
     hipStream_t s = ctx->stream;
     if (upload_image(b, img, stride, s) != YV_OK) return YV_ERR_HIP;
     ctx->h_pinned[0] = n;
-    if (n > 0) YV_HIP(hipMemcpyAsync(b->det_rc, rc, sizeof(int32_t) * 2 * (size_t)n, hipMemcpyHostToDevice, s));
-    YV_HIP(hipMemcpyAsync(b->det_count, ctx->h_pinned, sizeof(int32_t), hipMemcpyHostToDevice, s));
+    if (n > 0) YV_HIP(stage_h2d(ctx, b->det_rc, rc, sizeof(int32_t) * 2 * (size_t)n, s));
+    YV_HIP(stage_h2d(ctx, b->det_count, ctx->h_pinned, sizeof(int32_t), s));
     yavo::launch_blur9(b->staging, 1, H, W, W, (int64_t)H * W, ctx->k9, b->blur, s);
     yavo::launch_kp_boundary(b->det_rc, b->det_count, 1, H, W, b->max_kp, b->kp_src, b->kp_count, b->kp_band,
                              b->band_off, s);
     yavo::launch_brief(b->blur, 1, H, W, ctx->d_offsets, b->kp_src, b->kp_band, b->band_off, b->max_kp, b->keypoints,
                        b->desc, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(hipMemcpyAsync(ctx->h_pinned + 2, b->kp_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    YV_HIP(hipStreamSynchronize(s));
+    YV_HIP(stage_d2h(ctx, ctx->h_pinned + 2, b->kp_count, sizeof(int32_t), s));
+    YV_HIP(stage_sync(ctx, s));
     const int m = ctx->h_pinned[2];
     if (m > 0) {
-        YV_HIP(hipMemcpyAsync(out, b->keypoints, sizeof(yv_keypoint) * (size_t)m, hipMemcpyDeviceToHost, s));
-        YV_HIP(hipStreamSynchronize(s));
+        YV_HIP(stage_d2h(ctx, out, b->keypoints, sizeof(yv_keypoint) * (size_t)m, s));
+        YV_HIP(stage_sync(ctx, s));
     }
     *n_out = m;
     return YV_OK;
@@ -1016,24 +1120,25 @@ int yv_match_features(yv_ctx* ctx, const yv_keypoint* q, int nq, const yv_keypoi
     if (nq > yavo::kMaxKp || nt > yavo::kMaxKp) return YV_ERR_CAPACITY;
     if (nq == 0) return YV_OK;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     // the matcher does not look at the image size: reuse whatever workspace exists (or a minimal one)
     int st = ctx->single ? YV_OK : ensure_single(ctx, 16, 16);
     if (st != YV_OK) return st;
     yv_batch* b = ctx->single;
     hipStream_t s = ctx->stream;
     const size_t nk = (size_t)b->max_kp;
-    YV_HIP(hipMemcpyAsync(b->keypoints, q, sizeof(yv_keypoint) * (size_t)nq, hipMemcpyHostToDevice, s));
-    if (nt > 0) YV_HIP(hipMemcpyAsync(b->keypoints + nk, t, sizeof(yv_keypoint) * (size_t)nt, hipMemcpyHostToDevice, s));
+    YV_HIP(stage_h2d(ctx, b->keypoints, q, sizeof(yv_keypoint) * (size_t)nq, s));
+    if (nt > 0) YV_HIP(stage_h2d(ctx, b->keypoints + nk, t, sizeof(yv_keypoint) * (size_t)nt, s));
     ctx->h_pinned[0] = nq;
     ctx->h_pinned[1] = nt;
-    YV_HIP(hipMemcpyAsync(b->kp_count, ctx->h_pinned, 2 * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    YV_HIP(stage_h2d(ctx, b->kp_count, ctx->h_pinned, 2 * sizeof(int32_t), s));
     yavo::launch_pack_desc(b->keypoints, b->kp_count, 2, b->max_kp, b->desc, s);
     yavo::launch_match(b->desc, b->kp_count, b->pairs, 1, b->max_kp, nt, b->match_key, s);
     yavo::launch_match_finalize(b->match_key, b->keypoints, b->kp_count, b->pairs, 1, b->max_kp, 0, b->matches,
                                 b->match_count, b->filtered, b->filt_count, b->match_dj, b->match_lim, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(hipMemcpyAsync(out, b->matches, sizeof(yv_match) * (size_t)nq, hipMemcpyDeviceToHost, s));
-    YV_HIP(hipStreamSynchronize(s));
+    YV_HIP(stage_d2h(ctx, out, b->matches, sizeof(yv_match) * (size_t)nq, s));
+    YV_HIP(stage_sync(ctx, s));
     return YV_OK;
 }
 
@@ -1043,19 +1148,20 @@ int yv_filter_matches(yv_ctx* ctx, const yv_match* in, int n, int thr, yv_match*
     *n_out = 0;
     if (n == 0) return YV_OK;  // reference: minmax_element on an empty list is dereferenced (UB)
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     int st = ctx->single ? YV_OK : ensure_single(ctx, 16, 16);
     if (st != YV_OK) return st;
     yv_batch* b = ctx->single;
     hipStream_t s = ctx->stream;
-    YV_HIP(hipMemcpyAsync(b->matches, in, sizeof(yv_match) * (size_t)n, hipMemcpyHostToDevice, s));
+    YV_HIP(stage_h2d(ctx, b->matches, in, sizeof(yv_match) * (size_t)n, s));
     yavo::launch_filter_records(b->matches, n, thr, b->filtered, b->filt_count, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(hipMemcpyAsync(ctx->h_pinned, b->filt_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    YV_HIP(hipStreamSynchronize(s));
+    YV_HIP(stage_d2h(ctx, ctx->h_pinned, b->filt_count, sizeof(int32_t), s));
+    YV_HIP(stage_sync(ctx, s));
     const int m = ctx->h_pinned[0];
     if (m > 0) {
-        YV_HIP(hipMemcpyAsync(out, b->filtered, sizeof(yv_match) * (size_t)m, hipMemcpyDeviceToHost, s));
-        YV_HIP(hipStreamSynchronize(s));
+        YV_HIP(stage_d2h(ctx, out, b->filtered, sizeof(yv_match) * (size_t)m, s));
+        YV_HIP(stage_sync(ctx, s));
     }
     *n_out = m;
     return YV_OK;
@@ -1113,6 +1219,7 @@ int yv_f_ransac(yv_ctx* ctx, const yv_match* m, int n, const int32_t* samples, i
     for (int i = 0; i < 8 * iters; ++i)
         if (samples[i] < 0 || samples[i] >= n) return YV_ERR_INVALID;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     hipStream_t s = ctx->stream;
     Arena a{ctx};
     yv_match* dm;
@@ -1126,16 +1233,16 @@ int yv_f_ransac(yv_ctx* ctx, const yv_match* m, int n, const int32_t* samples, i
     a.add(&dfound, 1);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
     ctx->h_pinned[0] = n;
-    YV_HIP(hipMemcpyAsync(dm, m, sizeof(yv_match) * (size_t)n, hipMemcpyHostToDevice, s));
-    YV_HIP(hipMemcpyAsync(dcnt, ctx->h_pinned, sizeof(int32_t), hipMemcpyHostToDevice, s));
-    if (iters > 0) YV_HIP(hipMemcpyAsync(dsmp, samples, sizeof(int32_t) * 8 * (size_t)iters, hipMemcpyHostToDevice, s));
-    YV_HIP(hipMemcpyAsync(dF, F, sizeof(double) * 9, hipMemcpyHostToDevice, s));  // untouched if iters == 0
+    YV_HIP(stage_h2d(ctx, dm, m, sizeof(yv_match) * (size_t)n, s));
+    YV_HIP(stage_h2d(ctx, dcnt, ctx->h_pinned, sizeof(int32_t), s));
+    if (iters > 0) YV_HIP(stage_h2d(ctx, dsmp, samples, sizeof(int32_t) * 8 * (size_t)iters, s));
+    YV_HIP(stage_h2d(ctx, dF, F, sizeof(double) * 9, s));  // untouched if iters == 0
     yavo::launch_f_ransac(dm, n, dcnt, 1, dsmp, 8 * (int64_t)iters, iters, thr, dF, dmax, dfound, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(hipMemcpyAsync(F, dF, sizeof(double) * 9, hipMemcpyDeviceToHost, s));
-    YV_HIP(hipMemcpyAsync(ctx->h_pinned + 1, dmax, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    YV_HIP(hipMemcpyAsync(ctx->h_pinned + 2, dfound, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    YV_HIP(hipStreamSynchronize(s));
+    YV_HIP(stage_d2h(ctx, F, dF, sizeof(double) * 9, s));
+    YV_HIP(stage_d2h(ctx, ctx->h_pinned + 1, dmax, sizeof(int32_t), s));
+    YV_HIP(stage_d2h(ctx, ctx->h_pinned + 2, dfound, sizeof(int32_t), s));
+    YV_HIP(stage_sync(ctx, s));
     *max_inliers = ctx->h_pinned[1];
     *found = ctx->h_pinned[2];
     return YV_OK;
@@ -1147,6 +1254,7 @@ int yv_triangulate(yv_ctx* ctx, const double pose_a[7], const double pose_b[7], 
     *n_ok = 0;
     if (n == 0) return YV_OK;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     hipStream_t s = ctx->stream;
     Arena a{ctx};
     yv_match* dm;
@@ -1160,17 +1268,17 @@ int yv_triangulate(yv_ctx* ctx, const double pose_a[7], const double pose_b[7], 
     a.add(&dok, (size_t)n);
     a.add(&dn, 1);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(hipMemcpyAsync(dm, m, sizeof(yv_match) * (size_t)n, hipMemcpyHostToDevice, s));
-    YV_HIP(hipMemcpyAsync(dposes, pose_a, sizeof(double) * 7, hipMemcpyHostToDevice, s));
-    YV_HIP(hipMemcpyAsync(dposes + 7, pose_b, sizeof(double) * 7, hipMemcpyHostToDevice, s));
-    YV_HIP(hipMemcpyAsync(dK, K, sizeof(double) * 9, hipMemcpyHostToDevice, s));
+    YV_HIP(stage_h2d(ctx, dm, m, sizeof(yv_match) * (size_t)n, s));
+    YV_HIP(stage_h2d(ctx, dposes, pose_a, sizeof(double) * 7, s));
+    YV_HIP(stage_h2d(ctx, dposes + 7, pose_b, sizeof(double) * 7, s));
+    YV_HIP(stage_h2d(ctx, dK, K, sizeof(double) * 9, s));
     YV_HIP(hipMemsetAsync(dn, 0, sizeof(int32_t), s));
     yavo::launch_triangulate(dm, n, dposes, dK, dX, dok, dn, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(hipMemcpyAsync(Xw, dX, sizeof(double) * 3 * (size_t)n, hipMemcpyDeviceToHost, s));
-    YV_HIP(hipMemcpyAsync(ok, dok, (size_t)n, hipMemcpyDeviceToHost, s));
-    YV_HIP(hipMemcpyAsync(ctx->h_pinned, dn, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    YV_HIP(hipStreamSynchronize(s));
+    YV_HIP(stage_d2h(ctx, Xw, dX, sizeof(double) * 3 * (size_t)n, s));
+    YV_HIP(stage_d2h(ctx, ok, dok, (size_t)n, s));
+    YV_HIP(stage_d2h(ctx, ctx->h_pinned, dn, sizeof(int32_t), s));
+    YV_HIP(stage_sync(ctx, s));
     *n_ok = ctx->h_pinned[0];
     return YV_OK;
 }
@@ -1179,6 +1287,7 @@ int yv_world2camera(yv_ctx* ctx, const double* X, int n, const double pose[7], c
     if (!ctx || !pose || !K || n < 0 || (n > 0 && (!X || !out))) return YV_ERR_INVALID;
     if (n == 0) return YV_OK;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     hipStream_t s = ctx->stream;
     Arena a{ctx};
     double *dX, *dT, *dK, *dO;
@@ -1187,13 +1296,13 @@ int yv_world2camera(yv_ctx* ctx, const double* X, int n, const double pose[7], c
     a.add(&dK, 9);
     a.add(&dO, 3 * (size_t)n);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(hipMemcpyAsync(dX, X, sizeof(double) * 3 * (size_t)n, hipMemcpyHostToDevice, s));
-    YV_HIP(hipMemcpyAsync(dT, pose, sizeof(double) * 7, hipMemcpyHostToDevice, s));
-    YV_HIP(hipMemcpyAsync(dK, K, sizeof(double) * 9, hipMemcpyHostToDevice, s));
+    YV_HIP(stage_h2d(ctx, dX, X, sizeof(double) * 3 * (size_t)n, s));
+    YV_HIP(stage_h2d(ctx, dT, pose, sizeof(double) * 7, s));
+    YV_HIP(stage_h2d(ctx, dK, K, sizeof(double) * 9, s));
     yavo::launch_world2camera(dX, n, dT, dK, dO, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(hipMemcpyAsync(out, dO, sizeof(double) * 3 * (size_t)n, hipMemcpyDeviceToHost, s));
-    YV_HIP(hipStreamSynchronize(s));
+    YV_HIP(stage_d2h(ctx, out, dO, sizeof(double) * 3 * (size_t)n, s));
+    YV_HIP(stage_sync(ctx, s));
     return YV_OK;
 }
 
@@ -1204,6 +1313,7 @@ static int pose_single(yv_ctx* ctx, const double* X, const double* uv, int n, co
     if (n > 4096) return YV_ERR_CAPACITY;
     if (!finite_pose(pose)) return YV_ERR_INVALID;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     hipStream_t s = ctx->stream;
     Arena a{ctx};
     int32_t *doff, *dres;
@@ -1219,20 +1329,20 @@ static int pose_single(yv_ctx* ctx, const double* X, const double* uv, int n, co
     if (a.commit() != YV_OK) return YV_ERR_HIP;
     ctx->h_pinned[0] = 0;
     ctx->h_pinned[1] = n;
-    YV_HIP(hipMemcpyAsync(doff, ctx->h_pinned, 2 * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    YV_HIP(stage_h2d(ctx, doff, ctx->h_pinned, 2 * sizeof(int32_t), s));
     if (n > 0) {
-        YV_HIP(hipMemcpyAsync(dX, X, sizeof(double) * 3 * (size_t)n, hipMemcpyHostToDevice, s));
-        YV_HIP(hipMemcpyAsync(duv, uv, sizeof(double) * 2 * (size_t)n, hipMemcpyHostToDevice, s));
+        YV_HIP(stage_h2d(ctx, dX, X, sizeof(double) * 3 * (size_t)n, s));
+        YV_HIP(stage_h2d(ctx, duv, uv, sizeof(double) * 2 * (size_t)n, s));
     }
-    YV_HIP(hipMemcpyAsync(dK, K, sizeof(double) * 9, hipMemcpyHostToDevice, s));
-    YV_HIP(hipMemcpyAsync(dP, pose, sizeof(double) * 7, hipMemcpyHostToDevice, s));
+    YV_HIP(stage_h2d(ctx, dK, K, sizeof(double) * 9, s));
+    YV_HIP(stage_h2d(ctx, dP, pose, sizeof(double) * 7, s));
     if (lm) yavo::launch_pose_lm(doff, 1, dX, duv, dK, dP, dout, dres, s);
     else yavo::launch_pose_gn(doff, 1, dX, duv, dK, dP, dres, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(hipMemcpyAsync(pose, dP, sizeof(double) * 7, hipMemcpyDeviceToHost, s));
-    if (lm && n > 0) YV_HIP(hipMemcpyAsync(outlier, dout, (size_t)n, hipMemcpyDeviceToHost, s));
-    YV_HIP(hipMemcpyAsync(ctx->h_pinned + 2, dres, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    YV_HIP(hipStreamSynchronize(s));
+    YV_HIP(stage_d2h(ctx, pose, dP, sizeof(double) * 7, s));
+    if (lm && n > 0) YV_HIP(stage_d2h(ctx, outlier, dout, (size_t)n, s));
+    YV_HIP(stage_d2h(ctx, ctx->h_pinned + 2, dres, sizeof(int32_t), s));
+    YV_HIP(stage_sync(ctx, s));
     *result = ctx->h_pinned[2];
     return YV_OK;
 }
@@ -1254,6 +1364,7 @@ int yv_pose_lm_batch(yv_ctx* ctx, int n_problems, const int32_t* d_offsets, cons
         return YV_ERR_INVALID;
     if (n_problems == 0) return YV_OK;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
     yavo::launch_pose_lm(d_offsets, n_problems, d_X, d_uv, d_K, d_poses, d_outlier, d_inliers, s);
     return check_launch();
@@ -1266,6 +1377,7 @@ int yv_pose_gn_batch(yv_ctx* ctx, int n_problems, const int32_t* d_offsets, cons
         return YV_ERR_INVALID;
     if (n_problems == 0) return YV_OK;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
     yavo::launch_pose_gn(d_offsets, n_problems, d_X, d_uv, d_K, d_poses, d_iterations, s);
     return check_launch();
@@ -1279,6 +1391,7 @@ int yv_f_ransac_batch(yv_ctx* ctx, const yv_match* d_matches, int64_t list_strid
         return YV_ERR_INVALID;
     if (n_lists == 0) return YV_OK;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
     yavo::launch_f_ransac(d_matches, list_stride, d_counts, n_lists, d_samples, sample_stride, iters, thr, d_F,
                           d_max_inliers, d_found, s);
@@ -1306,6 +1419,7 @@ int yv_lk_create(yv_ctx* ctx, int max_images, int H, int W, int win, int max_lev
         return YV_ERR_INVALID;
     *out = nullptr;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     yv_lk* lk = new (std::nothrow) yv_lk();
     if (!lk) return YV_ERR_INVALID;
     lk->ctx = ctx;
@@ -1431,9 +1545,19 @@ int yv_calc_optical_flow_pyr_lk(yv_ctx* ctx, const uint8_t* prev, const uint8_t*
     if (n > 65536) return YV_ERR_CAPACITY;
     if (n == 0) return YV_OK;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
-    yv_lk* lk = nullptr;
-    int rc = yv_lk_create(ctx, 2, H, W, win, max_level, &lk);
-    if (rc != YV_OK) return rc;
+    StageScope stage_scope(ctx);
+    const int key[4] = {H, W, win, max_level};
+    if (!ctx->lk_cache || !std::equal(key, key + 4, ctx->lk_key)) {
+        if (ctx->lk_cache) yv_lk_destroy(ctx->lk_cache);
+        ctx->lk_cache = nullptr;
+        int rc = yv_lk_create(ctx, 2, H, W, win, max_level, &ctx->lk_cache);
+        if (rc != YV_OK) {
+            ctx->lk_cache = nullptr;
+            return rc;
+        }
+        std::copy(key, key + 4, ctx->lk_key);
+    }
+    yv_lk* lk = ctx->lk_cache;
     hipStream_t s = ctx->stream;
     Arena a{ctx};
     uint8_t* dimg;
@@ -1448,23 +1572,20 @@ int yv_calc_optical_flow_pyr_lk(yv_ctx* ctx, const uint8_t* prev, const uint8_t*
     a.add(&dpair, 2);
     a.add(&dcnt, 1);
     a.add(&dst, (size_t)n);
-    if (a.commit() != YV_OK) {
-        yv_lk_destroy(lk);
-        return YV_ERR_HIP;
-    }
+    if (a.commit() != YV_OK) return YV_ERR_HIP;
     int status_rc = YV_OK;
     do {
-        if (hipMemcpy2DAsync(dimg, W, prev, stride, W, H, hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpy2DAsync(dimg + pitch, W, next, stride, W, H, hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(dpts, prev_pts, sizeof(float) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess) {
+        if (stage_h2d_2d(ctx, dimg, W, prev, stride, W, H, s) != hipSuccess ||
+            stage_h2d_2d(ctx, dimg + pitch, W, next, stride, W, H, s) != hipSuccess ||
+            stage_h2d(ctx, dpts, prev_pts, sizeof(float) * 2 * n, s) != hipSuccess) {
             status_rc = YV_ERR_HIP;
             break;
         }
         ctx->h_pinned[0] = 0;
         ctx->h_pinned[1] = 1;
         ctx->h_pinned[2] = n;
-        if (hipMemcpyAsync(dpair, ctx->h_pinned, 2 * sizeof(int32_t), hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(dcnt, ctx->h_pinned + 2, sizeof(int32_t), hipMemcpyHostToDevice, s) != hipSuccess) {
+        if (stage_h2d(ctx, dpair, ctx->h_pinned, 2 * sizeof(int32_t), s) != hipSuccess ||
+            stage_h2d(ctx, dcnt, ctx->h_pinned + 2, sizeof(int32_t), s) != hipSuccess) {
             status_rc = YV_ERR_HIP;
             break;
         }
@@ -1472,13 +1593,12 @@ int yv_calc_optical_flow_pyr_lk(yv_ctx* ctx, const uint8_t* prev, const uint8_t*
         if (status_rc != YV_OK) break;
         status_rc = yv_lk_track_batch(lk, dpair, 1, dpts, dcnt, n, max_count, eps, min_eig, dnext, dst, derr, nullptr);
         if (status_rc != YV_OK) break;
-        if (hipMemcpyAsync(next_pts, dnext, sizeof(float) * 2 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipMemcpyAsync(status, dst, (size_t)n, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipMemcpyAsync(err, derr, sizeof(float) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
+        if (stage_d2h(ctx, next_pts, dnext, sizeof(float) * 2 * n, s) != hipSuccess ||
+            stage_d2h(ctx, status, dst, (size_t)n, s) != hipSuccess ||
+            stage_d2h(ctx, err, derr, sizeof(float) * n, s) != hipSuccess ||
+            stage_sync(ctx, s) != hipSuccess)
             status_rc = YV_ERR_HIP;
     } while (0);
-    yv_lk_destroy(lk);
     return status_rc;
 }
 
@@ -1511,6 +1631,7 @@ int yv_essential_create(yv_ctx* ctx, int max_pairs, int max_points, int max_iter
         return YV_ERR_INVALID;
     *out = nullptr;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     yv_essential* es = new (std::nothrow) yv_essential();
     if (!es) return YV_ERR_INVALID;
     es->ctx = ctx;
@@ -1584,6 +1705,7 @@ int yv_find_essential(yv_ctx* ctx, const float* pts1, const float* pts2, int n, 
         return YV_OK;
     }
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     yv_essential* es = nullptr;
     int rc = yv_essential_create(ctx, 1, n, 1000, &es);
     if (rc != YV_OK) return rc;
@@ -1606,19 +1728,19 @@ int yv_find_essential(yv_ctx* ctx, const float* pts1, const float* pts2, int n, 
     int st = YV_OK;
     do {
         ctx->h_pinned[0] = n;
-        if (hipMemcpyAsync(d1, pts1, sizeof(float) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(d2, pts2, sizeof(float) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(dcnt, ctx->h_pinned, sizeof(int32_t), hipMemcpyHostToDevice, s) != hipSuccess) {
+        if (stage_h2d(ctx, d1, pts1, sizeof(float) * 2 * n, s) != hipSuccess ||
+            stage_h2d(ctx, d2, pts2, sizeof(float) * 2 * n, s) != hipSuccess ||
+            stage_h2d(ctx, dcnt, ctx->h_pinned, sizeof(int32_t), s) != hipSuccess) {
             st = YV_ERR_HIP;
             break;
         }
         st = yv_find_essential_batch(es, d1, d2, dcnt, 1, n, focal, ppx, ppy, prob, threshold, dE, dm, dfound,
                                      nullptr, nullptr);
         if (st != YV_OK) break;
-        if (hipMemcpyAsync(E, dE, sizeof(double) * 9, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipMemcpyAsync(ctx->h_pinned + 1, dfound, sizeof(int32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
-            (mask && hipMemcpyAsync(mask, dm, (size_t)n, hipMemcpyDeviceToHost, s) != hipSuccess) ||
-            hipStreamSynchronize(s) != hipSuccess) {
+        if (stage_d2h(ctx, E, dE, sizeof(double) * 9, s) != hipSuccess ||
+            stage_d2h(ctx, ctx->h_pinned + 1, dfound, sizeof(int32_t), s) != hipSuccess ||
+            (mask && stage_d2h(ctx, mask, dm, (size_t)n, s) != hipSuccess) ||
+            stage_sync(ctx, s) != hipSuccess) {
             st = YV_ERR_HIP;
             break;
         }
@@ -1633,6 +1755,7 @@ int yv_recover_pose(yv_ctx* ctx, const double E[9], const float* pts1, const flo
     if (!ctx || !E || !K || !R || !t || !good || n < 0 || (n > 0 && (!pts1 || !pts2))) return YV_ERR_INVALID;
     if (n > 65536) return YV_ERR_CAPACITY;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    StageScope stage_scope(ctx);
     yv_essential* es = nullptr;
     int rc = yv_essential_create(ctx, 1, std::max(n, 5), 1, &es);
     if (rc != YV_OK) return rc;
@@ -1655,19 +1778,19 @@ int yv_recover_pose(yv_ctx* ctx, const double E[9], const float* pts1, const flo
     int st = YV_OK;
     do {
         ctx->h_pinned[0] = n;
-        if ((n > 0 && (hipMemcpyAsync(d1, pts1, sizeof(float) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess ||
-                       hipMemcpyAsync(d2, pts2, sizeof(float) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess)) ||
-            hipMemcpyAsync(dE, E, sizeof(double) * 9, hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(dcnt, ctx->h_pinned, sizeof(int32_t), hipMemcpyHostToDevice, s) != hipSuccess) {
+        if ((n > 0 && (stage_h2d(ctx, d1, pts1, sizeof(float) * 2 * n, s) != hipSuccess ||
+                       stage_h2d(ctx, d2, pts2, sizeof(float) * 2 * n, s) != hipSuccess)) ||
+            stage_h2d(ctx, dE, E, sizeof(double) * 9, s) != hipSuccess ||
+            stage_h2d(ctx, dcnt, ctx->h_pinned, sizeof(int32_t), s) != hipSuccess) {
             st = YV_ERR_HIP;
             break;
         }
         st = yv_recover_pose_batch(es, dE, d1, d2, dcnt, 1, std::max(n, 5), K, dR, dt, dgood, nullptr);
         if (st != YV_OK) break;
-        if (hipMemcpyAsync(R, dR, sizeof(double) * 9, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipMemcpyAsync(t, dt, sizeof(double) * 3, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipMemcpyAsync(ctx->h_pinned + 1, dgood, sizeof(int32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess) {
+        if (stage_d2h(ctx, R, dR, sizeof(double) * 9, s) != hipSuccess ||
+            stage_d2h(ctx, t, dt, sizeof(double) * 3, s) != hipSuccess ||
+            stage_d2h(ctx, ctx->h_pinned + 1, dgood, sizeof(int32_t), s) != hipSuccess ||
+            stage_sync(ctx, s) != hipSuccess) {
             st = YV_ERR_HIP;
             break;
         }

@@ -27,14 +27,16 @@ namespace yavo {
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
-// Inclusive scan across one 64-lane wave.
+// Inclusive scan across one 64-lane wave, all in DPP (no LDS permutes): Hillis-Steele inside each 16-lane row
+// (row_shr 1, 2, 4, 8; lanes without a source add the `old` 0), then row_bcast:15 adds row 0's total to row 1 and
+// row 2's to row 3, and row_bcast:31 adds rows 0-1's total to rows 2 and 3 (GFX9 DPP).
 __device__ __forceinline__ int wave_incl_scan(int v) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        int t = __shfl_up(v, off, 64);
-        if (lane >= off) v += t;
-    }
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
     return v;
 }
 
@@ -313,50 +315,49 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         s_npre = 0;
     }
 
-    // stage (FT_H + 8) x (FT_W + 8) = 64 x 72 bytes.  Interior tiles (every source byte inside the image): each LDS
-    // dword is one unaligned dword load, 5 per thread, all in flight before the LDS writes.  Border tiles take the
-    // REFLECT_101 byte path.
-    const bool interior = (c0 >= FT_R) && (c0 + FT_W + FT_R <= W) && (r0 >= FT_R) && (r0 + FT_H + FT_R < H);
-    if (interior) {
+    // stage (FT_H + 8) x (FT_W + 8) = 64 x 72 bytes, one LDS dword per load: 5 per thread, all in flight before the
+    // LDS writes.  Interior tiles (every source byte inside the image): each LDS dword is one unaligned dword load
+    // (the hardware's unaligned mode splits it), no alignment arithmetic in VALU.  Border tiles (36% of a KITTI
+    // image's 140 tiles): REFLECT_101 rows are whole source rows, so a dword whose 4 columns are inside the image is
+    // still one dword load from the reflected row; only the dwords that cross the left / right edge gather their
+    // 4 reflected columns byte by byte.
+    {
         constexpr int kDw = FT_LW / 4;               // 18 LDS dwords per row
         constexpr int kSlots = FT_LH * kDw;          // 1152
         constexpr int kPer = (kSlots + 255) / 256;   // 5
-        // one unaligned dword load per LDS dword (the hardware's unaligned mode splits it): no alignment
-        // arithmetic in VALU
+        const bool interior = (c0 >= FT_R) && (c0 + FT_W + FT_R <= W) && (r0 >= FT_R) && (r0 + FT_H + FT_R < H);
         uint32_t v[kPer];
+        if (interior) {
 #pragma unroll
-        for (int u = 0; u < kPer; ++u) {
-            const int t = min(tid + 256 * u, kSlots - 1);
-            const int lr = t / kDw, j = t - lr * kDw;
-            __builtin_memcpy(&v[u], src + (int64_t)(r0 - FT_R + lr) * stride + (c0 - FT_R) + 4 * j, 4);
+            for (int u = 0; u < kPer; ++u) {
+                const int t = min(tid + 256 * u, kSlots - 1);
+                const int lr = t / kDw, j = t - lr * kDw;
+                __builtin_memcpy(&v[u], src + (int64_t)(r0 - FT_R + lr) * stride + (c0 - FT_R) + 4 * j, 4);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int t = min(tid + 256 * u, kSlots - 1);
+                const int lr = t / kDw, j = t - lr * kDw;
+                const int r = reflect101(min(max(r0 - FT_R + lr, -(H - 1)), 2 * H - 2), H);
+                const uint8_t* row = src + (int64_t)r * stride;
+                const int cc = c0 - FT_R + 4 * j;
+                if (cc >= 0 && cc + 4 <= W) {
+                    __builtin_memcpy(&v[u], row + cc, 4);
+                } else {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        w |= (uint32_t)row[reflect101(min(max(cc + b, -(W - 1)), 2 * W - 2), W)] << (8 * b);
+                    v[u] = w;
+                }
+            }
         }
         uint32_t* tile32 = reinterpret_cast<uint32_t*>(tile);
 #pragma unroll
         for (int u = 0; u < kPer; ++u) {
             const int t = tid + 256 * u;
             if (t < kSlots) tile32[t] = v[u];
-        }
-    } else {
-        // wave w loads rows w, w+4, ...; lanes 0..63 (+ 0..7) cover 72 columns; all of this wave's row loads
-        // are issued before the first LDS write
-        const int cA = reflect101(min(max(c0 - FT_R + lane, -(W - 1)), 2 * W - 2), W);
-        const int cB = reflect101(min(max(c0 - FT_R + 64 + (lane & 7), -(W - 1)), 2 * W - 2), W);
-        constexpr int kRowsPerWave = FT_LH / 4;
-        static_assert(FT_LH % 4 == 0, "rows split evenly over the 4 waves");
-        uint8_t va[kRowsPerWave], vb[kRowsPerWave];
-#pragma unroll
-        for (int u = 0; u < kRowsPerWave; ++u) {
-            const int lr = wave + 4 * u;
-            const int r = reflect101(min(max(r0 - FT_R + lr, -(H - 1)), 2 * H - 2), H);
-            const uint8_t* row = src + (int64_t)r * stride;
-            va[u] = row[cA];
-            vb[u] = row[cB];
-        }
-#pragma unroll
-        for (int u = 0; u < kRowsPerWave; ++u) {
-            const int lr = wave + 4 * u;
-            tile[lr * FT_LW + lane] = va[u];
-            if (lane < FT_LW - 64) tile[lr * FT_LW + 64 + lane] = vb[u];
         }
     }
     __syncthreads();
@@ -530,7 +531,15 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
             const int m = i >> 4, xq = (i & 15) * 4;
             uint4 P[5];
 #pragma unroll
-            for (int t = 0; t < 5; ++t) P[t] = *reinterpret_cast<const uint4*>(&hbuf[(m + t) * FT_W + xq]);
+            for (int t = 0; t < 5; ++t) {
+                // one ds_read_b128 per row pair: 16 lanes cover a row pair's 64 dwords (every bank once).  The
+                // volatile access keeps it whole: otherwise the compiler splits it into ds_read2_b32 pairs at a
+                // 4-dword lane stride, 4-way bank conflicts (SQ_LDS_BANK_CONFLICT ~240 cycles per wave, r03 counters)
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                typedef const volatile __attribute__((address_space(3))) u32x4 lds_u32x4;
+                const u32x4 q = *(lds_u32x4*)(&s_share[(m + t) * FT_W + xq]);
+                P[t] = make_uint4(q.x, q.y, q.z, q.w);
+            }
             // accumulators start at 2^15 (the rounding term of (acc + 2^15) >> 16)
             uint32_t ev[4], od[4];
 #pragma unroll
