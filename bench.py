@@ -67,6 +67,15 @@ def parse():
     ap.add_argument("--e2e-steps", type=int, default=20,
                     help="steps of the end-to-end leg (every step's frames uploaded from pinned host memory, "
                          "overlapped with the previous step's kernels); 0 skips it")
+    ap.add_argument("--png-steps", type=int, default=3,
+                    help="steps of the PNG-input end-to-end leg (rank 0, N=1): the step's frames written once as a "
+                         "KITTI stereo sequence of PNG files, every step decoded on the host threads (cv::imread's "
+                         "part, yv_seq_upload) into pinned staging and copied to HBM, overlapped with the previous "
+                         "step's kernels; 0 skips it")
+    ap.add_argument("--png-threads", type=int, default=0, help="decode threads of the PNG leg (0: the usable cores)")
+    ap.add_argument("--loop-handler-frames", type=int, default=200,
+                    help="frames of the drop-in C++ LoopHandler leg (rank 0, N=1; tools/bench_loop_handler.py); 0 "
+                         "skips it")
     ap.add_argument("--kf-every", type=int, default=4,
                     help="shared map: frames with global index %% kf_every == 0 are keyframes (their LM inliers "
                          "become landmarks); 0 disables the map and its all-gather")
@@ -107,6 +116,89 @@ def stage_valu_ops(counts, n_img):
     # separable blur, 9 + 9 MACs per pixel
     # matcher (VALU formulation): Kq * Kt * (8 xor + 8 bcnt-accumulate + 2 min) = 18 per pair
     return {"detect": n_img * (36.0e6 + 18.0 * H * W), "match": float(np.sum(kq * kt)) * 18.0}
+
+
+def write_png_sequence(base, left, right, threads):
+    """KITTI layout: base/image_0/%06d.png (left), image_1 (right) and a calib.txt."""
+    from concurrent.futures import ThreadPoolExecutor
+    for side in ("image_0", "image_1"):
+        os.makedirs(os.path.join(base, side), exist_ok=True)
+    jobs = [(os.path.join(base, side, f"{k:06d}.png"), imgs[k]) for side, imgs in (("image_0", left), ("image_1", right))
+            for k in range(len(imgs))]
+
+    from ya_vo_amd.io import png_write_gray
+
+    def write(j):
+        png_write_gray(j[0], j[1])  # Paeth rows, zlib level 1 (cv::imwrite's default); ctypes releases the GIL
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(write, jobs))
+    with open(os.path.join(base, "calib.txt"), "w") as f:
+        for i in range(2):
+            f.write(f"P{i}: 7.188560e+02 0 6.071928e+02 {-386.1448 * i:.6e} 0 7.188560e+02 1.852157e+02 0 0 0 1 0\n")
+
+
+def png_end_to_end(ctx, shard, images, halo_right, B, steps, threads):
+    """PNG-input end-to-end rate: the shard's frames as a KITTI stereo PNG sequence (sequence frame 0 =
+    the halo frame, 1..B = the shard), every step decoded on `threads` host threads into pinned staging and copied to
+    one of two device buffers on the context stream (yv_seq_upload), then the step's kernels; the host decodes step
+    i + 1 while the GPU runs step i.  Timed: every decode, copy and step."""
+    import shutil
+    import tempfile
+    import torch
+    from ya_vo_amd.io import Sequence
+    tmp = tempfile.mkdtemp(prefix="yavo_png_")
+    try:
+        t0 = time.perf_counter()
+        left = [images[2 * B]] + [images[2 * k] for k in range(B)]
+        right = [halo_right] + [images[2 * k + 1] for k in range(B)]
+        write_png_sequence(tmp, left, right, threads)
+        write_s = time.perf_counter() - t0
+        png_bytes = sum(os.path.getsize(os.path.join(tmp, d, f)) for d in ("image_0", "image_1")
+                        for f in os.listdir(os.path.join(tmp, d)))
+        seq = Sequence(tmp, stereo=True)
+        dev = torch.device("cuda", ctx.device)
+        img = H * W
+        bufs = [torch.empty((2 * B + 2) * img, dtype=torch.uint8, device=dev) for _ in range(2)]
+
+        def upload(k):
+            seq.upload(ctx, 1, B, bufs[k].data_ptr(), img, threads)              # frames -> images 0 .. 2B-1
+            seq.upload(ctx, 0, 1, bufs[k].data_ptr() + 2 * B * img, img, threads)  # halo frame -> 2B (+ its right)
+
+        upload(0)
+        shard.step(bufs[0].data_ptr())
+        shard.drain()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(steps):
+            upload(i % 2)  # the context stream orders it after step i - 2's kernels, the last readers of the buffer
+            shard.step(bufs[i % 2].data_ptr())
+        shard.drain()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t1
+        # the decode alone on the same threads (no GPU), for the bound
+        t2 = time.perf_counter()
+        seq.read(1, B, threads)
+        dec_s = time.perf_counter() - t2
+        seq.close()
+        return {"frames_per_s": round(B * steps / el, 2), "ms_per_step": round(1e3 * el / steps, 3), "steps": steps,
+                "decode_threads": threads, "decode_only_frames_per_s": round(B / dec_s, 2),
+                "png_bytes_per_stereo_frame": round(png_bytes / (B + 1)), "png_write_s": round(write_s, 2),
+                "how": "KITTI stereo PNG sequence (Paeth rows, zlib 1) -> yv_seq_upload (host decode threads -> pinned "
+                       "staging -> async HBM copy on the context stream) -> the step's kernels; the decode of step i+1 "
+                       "overlaps step i on the GPU; timed region = every decode + copy + step"}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def loop_handler_leg(frames):
+    """The drop-in C++ LoopHandler (ya_vo_amd/bin/yavo_loop_handler) on a synthetic mono PNG sequence, serial and
+    pipelined (tools/bench_loop_handler.py)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_loop_handler
+    r = bench_loop_handler.measure(frames)
+    return {"serial_frames_per_s": r["serial"]["frames_per_s"], "pipelined_frames_per_s": r["pipelined"]["frames_per_s"],
+            "trajectories_identical": r["trajectories_identical"], "serial": r["serial"], "pipelined": r["pipelined"],
+            "what": r["what"]}
 
 
 def cpu_threads_available() -> int:
@@ -266,6 +358,7 @@ def main():
     first = 1 + rank * B
     fr = synth_stereo_batch(1234, B + 1, start=first - 1)  # [2(B+1), H, W]: the halo frame, then the shard
     images = shard_images(fr[2:], fr[0], fr[1] if args.tracker == "lk" else None)
+    halo_right = fr[1].copy()
     del fr
     n_img = images.shape[0]
     d_frames = torch.from_numpy(images).to(dev)
@@ -364,6 +457,20 @@ def main():
                "how": "pinned host frames -> two device buffers on a copy stream, step i+1's upload overlapped with "
                       "step i's kernels; timed region = all uploads + all steps"}
         del h_frames, bufs
+
+    png_e2e = None
+    if args.png_steps > 0 and world == 1 and args.tracker == "match":
+        try:
+            png_e2e = png_end_to_end(ctx, shard, images, halo_right, B, args.png_steps,
+                                     args.png_threads or cpu_threads_available())
+        except Exception as e:  # reported, never fatal to the headline
+            png_e2e = {"error": repr(e)[:300]}
+    lh = None
+    if args.loop_handler_frames > 0 and world == 1 and rank == 0:
+        try:
+            lh = loop_handler_leg(args.loop_handler_frames)
+        except Exception as e:
+            lh = {"error": repr(e)[:300]}
 
     v = batch.view()
     counts = {
@@ -503,6 +610,8 @@ def main():
         "h2d_upload_ms_per_step": round(h2d_ms, 4),
         "pcie_inclusive_frames_per_s": round(frames_total / (elapsed + args.steps * h2d_ms / 1e3), 2),
         "end_to_end": e2e,
+        "png_end_to_end": png_e2e,
+        "loop_handler": lh,
         "roofline": roofline,
         "cpu_baseline": None,
     }

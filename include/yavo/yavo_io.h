@@ -53,6 +53,10 @@ int yv_seq_read(yv_seq* seq, int first, int n, uint8_t* dst, int64_t pitch, int 
 int yv_seq_upload(yv_seq* seq, struct yv_ctx* ctx, int first, int n, uint8_t* d_dst, int64_t pitch, int threads,
                   void* stream);
 
+/* The writer side, for test sequences (the reference only reads PNGs): an 8-bit grey image to a PNG file, every row
+ * Paeth-filtered, zlib level 1 (cv::imwrite's default IMWRITE_PNG_COMPRESSION); rows of W bytes, stride bytes apart. */
+int yv_png_write_gray(const char* path, const uint8_t* img, int H, int W, int stride);
+
 /* KITTI odometry poses: one line per frame, the 12 row-major numbers of the 3x4 [R | t] of T_wc = T_cw^-1, for
  * poses given as Sophus SE3d::data() of T_cw ({qx, qy, qz, qw, tx, ty, tz}, yavo_geom.h). */
 int yv_write_kitti_poses(const char* path, const double* poses, int n);

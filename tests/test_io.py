@@ -202,3 +202,17 @@ def test_kitti_poses_roundtrip(tmp_path):
                       [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
         np.testing.assert_allclose(M[k, :, :3], R.T, atol=1e-12)
         np.testing.assert_allclose(M[k, :, 3], -R.T @ t[k], atol=1e-10)
+
+
+def test_png_writer_round_trip(tmp_path):
+    """yv_png_write_gray (the bench's and tools' sequence writer: Paeth rows, zlib level 1) round-trips through the
+    decoder, PIL agrees, and odd sizes / strides take the same path."""
+    from PIL import Image
+    from ya_vo_amd.io import png_decode_gray, png_write_gray
+    rng = np.random.default_rng(3)
+    for H, W in [(376, 1241), (1, 1), (7, 13), (64, 3)]:
+        img = rng.integers(0, 256, (H, W), dtype=np.uint8)
+        p = str(tmp_path / f"w{H}x{W}.png")
+        png_write_gray(p, img)
+        np.testing.assert_array_equal(np.array(Image.open(p)), img)
+        np.testing.assert_array_equal(png_decode_gray(open(p, "rb").read()), img)

@@ -143,6 +143,20 @@ int png_decode(const uint8_t* data, size_t len, uint8_t* dst, int stride, int H,
                 }
                 break;
             case 4:
+                if (fbpp == 1 && prev) {
+                    // 8-bit grey rows below the first: a (left) and c (upper left) carried in registers and the
+                    // predictor picked without branches, p - a = b - c, p - b = a - c, p - c = a + b - 2c
+                    int a = 0, c = 0;
+                    for (size_t i = 0; i < rowb; ++i) {
+                        const int b = prev[i];
+                        const int pa = std::abs(b - c), pb = std::abs(a - c), pc = std::abs(a + b - 2 * c);
+                        const int pred = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
+                        a = (uint8_t)(cur[i] + pred);
+                        cur[i] = (uint8_t)a;
+                        c = b;
+                    }
+                    break;
+                }
                 for (size_t i = 0; i < rowb; ++i) {
                     const int a = i >= fbpp ? cur[i - fbpp] : 0, b = prev ? prev[i] : 0;
                     const int c = (prev && i >= fbpp) ? prev[i - fbpp] : 0;
@@ -443,6 +457,59 @@ int yv_seq_upload(yv_seq* s, yv_ctx* ctx, int first, int n, uint8_t* d_dst, int6
         return YV_ERR_HIP;
     s->pending[k] = true;
     return YV_OK;
+}
+
+int yv_png_write_gray(const char* path, const uint8_t* img, int H, int W, int stride) {
+    if (!path || !img || H < 1 || W < 1 || stride < W) return YV_ERR_INVALID;
+    // filtered scanlines: filter byte 4 (Paeth) + W bytes each
+    std::vector<uint8_t> raw((size_t)H * (W + 1));
+    for (int r = 0; r < H; ++r) {
+        const uint8_t* cur = img + (size_t)r * stride;
+        const uint8_t* up = r ? img + (size_t)(r - 1) * stride : nullptr;
+        uint8_t* o = &raw[(size_t)r * (W + 1)];
+        o[0] = 4;
+        for (int c = 0; c < W; ++c) {
+            const int a = c ? cur[c - 1] : 0, b = up ? up[c] : 0, d = (c && up) ? up[c - 1] : 0;
+            const int p = a + b - d, pa = std::abs(p - a), pb = std::abs(p - b), pc = std::abs(p - d);
+            const int pred = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : d);
+            o[1 + c] = (uint8_t)(cur[c] - pred);
+        }
+    }
+    uLongf zlen = compressBound((uLong)raw.size());
+    std::vector<uint8_t> z(zlen);
+    if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), 1) != Z_OK) return YV_ERR_INVALID;
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return YV_ERR_INVALID;
+    auto be32 = [](uint32_t v, uint8_t* b) {
+        b[0] = (uint8_t)(v >> 24); b[1] = (uint8_t)(v >> 16); b[2] = (uint8_t)(v >> 8); b[3] = (uint8_t)v;
+    };
+    auto chunk = [&](const char* type, const uint8_t* data, uint32_t len) {
+        uint8_t hdr[8];
+        be32(len, hdr);
+        std::memcpy(hdr + 4, type, 4);
+        uLong crc = crc32(0L, hdr + 4, 4);
+        if (len) crc = crc32(crc, data, len);
+        uint8_t tail[4];
+        be32((uint32_t)crc, tail);
+        std::fwrite(hdr, 1, 8, f);
+        if (len) std::fwrite(data, 1, len, f);
+        std::fwrite(tail, 1, 4, f);
+    };
+    static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    std::fwrite(sig, 1, 8, f);
+    uint8_t ihdr[13];
+    be32((uint32_t)W, ihdr);
+    be32((uint32_t)H, ihdr + 4);
+    ihdr[8] = 8;   // bit depth
+    ihdr[9] = 0;   // grey
+    ihdr[10] = 0;  // deflate
+    ihdr[11] = 0;  // adaptive filtering
+    ihdr[12] = 0;  // no interlace
+    chunk("IHDR", ihdr, 13);
+    chunk("IDAT", z.data(), (uint32_t)zlen);
+    chunk("IEND", nullptr, 0);
+    const bool ok = !std::ferror(f);
+    return (std::fclose(f) == 0 && ok) ? YV_OK : YV_ERR_INVALID;
 }
 
 int yv_write_kitti_poses(const char* path, const double* poses, int n) {

@@ -8,6 +8,7 @@
 #include <condition_variable>
 #include <deque>
 #include <fstream>
+#include <future>
 #include <iostream>
 #include <iterator>
 #include <mutex>
@@ -101,12 +102,9 @@ bool LoopHandler::gpu(int st, const char* what) {
     return false;
 }
 
-// :918-930
-Frame::ptr LoopHandler::getNextFrame() {
-    if (train_it_ >= leftPathTrain.size()) return nullptr;
-    const double t0 = now_s();
-    const std::string& path = leftPathTrain[train_it_];
-    // cv::imread(path, IMREAD_GRAYSCALE) (:919) = the PNG file decoded to 8-bit grey
+// cv::imread(path, IMREAD_GRAYSCALE) (:919) = the PNG file decoded to 8-bit grey; nullptr (with a message) when
+// the file cannot be read.  Thread-safe: the pipelined loop decodes several frames at once.
+Frame::ptr LoopHandler::readFrame(const std::string& path) {
     std::ifstream fin(path, std::ios::binary);
     std::vector<uint8_t> file((std::istreambuf_iterator<char>(fin)), std::istreambuf_iterator<char>());
     int H = 0, W = 0;
@@ -123,6 +121,15 @@ Frame::ptr LoopHandler::getNextFrame() {
         std::cerr << "yavo: cannot decode " << path << " (" << yv_status_string(st) << ")" << std::endl;
         return nullptr;
     }
+    return frame;
+}
+
+// :918-930
+Frame::ptr LoopHandler::getNextFrame() {
+    if (train_it_ >= leftPathTrain.size()) return nullptr;
+    const double t0 = now_s();
+    Frame::ptr frame = readFrame(leftPathTrain[train_it_]);
+    if (!frame) return nullptr;
     currentFrameId_ = (int)train_it_;
     train_it_++;
     frame->frameID = Frame::createFrameID();
@@ -436,7 +443,8 @@ void LoopHandler::runVO(int max_frames) {
     }
 }
 
-void LoopHandler::setPipeline(int depth, int device, const std::vector<int8_t>& briefOffsets) {
+void LoopHandler::setPipeline(int depth, int device, const std::vector<int8_t>& briefOffsets, int readers) {
+    pipeline_readers_ = readers;
     pipeline_depth_ = depth > 0 ? depth : 0;
     pipeline_device_ = device;
     pipeline_offsets_ = briefOffsets;
@@ -455,8 +463,11 @@ void LoopHandler::runVOPipelined(int max_frames) {
     std::condition_variable cv_put, cv_get;
     std::deque<Item> q;
     bool stop = false;
-    double worker_features = 0;
+    double worker_features = 0, worker_read = 0;
     const size_t depth = (size_t)pipeline_depth_;
+    // PNG decoding (the reference's cv::imread) is the longest per-frame step on the host: the worker keeps the next
+    // `readers` frames decoding on their own threads and consumes them in path-train order, so ids stay sequential
+    const int readers = std::max(1, pipeline_readers_);
     std::thread worker([&]() {
         Device wdev(pipeline_device_);
         int st = wdev.ok() ? YV_OK : wdev.status();
@@ -469,11 +480,34 @@ void LoopHandler::runVOPipelined(int max_frames) {
             if (st == YV_OK) st = wfd->status();
         }
         int produced = 0;
+        const size_t n_train = leftPathTrain.size();
+        const size_t limit = max_frames < 0 ? n_train : std::min(n_train, train_it_ + (size_t)max_frames);
+        std::deque<std::future<Frame::ptr>> ahead;  // decodes of frames next_read - ahead.size() .. next_read - 1
+        size_t next_read = train_it_;
+        auto refill = [&]() {
+            while (ahead.size() < (size_t)readers && next_read < limit) {
+                const std::string path = leftPathTrain[next_read++];
+                ahead.push_back(std::async(std::launch::async, [path]() { return readFrame(path); }));
+            }
+        };
         while (true) {
             Item it;
             it.status = st;
             if (st == YV_OK && (max_frames < 0 || produced < max_frames)) {
-                it.frame = getNextFrame();  // only this thread reads the path train
+                // getNextFrame, its decode done ahead (only this thread advances the path train)
+                refill();
+                if (!ahead.empty()) {
+                    const double t0 = now_s();
+                    it.frame = ahead.front().get();
+                    ahead.pop_front();
+                    refill();
+                    worker_read += now_s() - t0;
+                    if (it.frame) {
+                        currentFrameId_ = (int)train_it_;
+                        train_it_++;
+                        it.frame->frameID = Frame::createFrameID();
+                    }
+                }
                 it.index = currentFrameId_;
                 if (it.frame) {
                     const double t0 = now_s();
@@ -491,13 +525,14 @@ void LoopHandler::runVOPipelined(int max_frames) {
             {
                 std::unique_lock<std::mutex> lk(mu);
                 cv_put.wait(lk, [&]() { return stop || q.size() < depth; });
-                if (stop) return;
+                if (stop) break;
                 q.push_back(std::move(it));
             }
             cv_get.notify_one();
-            if (last) return;
+            if (last) break;
             ++produced;
         }
+        for (auto& f : ahead) f.wait();  // no decode outlives the loop
     });
     while (true) {
         Item it;
@@ -525,6 +560,7 @@ void LoopHandler::runVOPipelined(int max_frames) {
     cv_put.notify_all();
     worker.join();
     t_features += worker_features;
+    t_read += worker_read;  // in the pipelined loop: the worker waiting for the next decoded frame
 }
 
 }  // namespace yavo_fe

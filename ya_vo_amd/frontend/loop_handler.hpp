@@ -115,8 +115,10 @@ public:
     // getNextFrame + insertFrameFeatures (PNG decode, detect, describe) do not depend on frame k's addFrame, so a
     // worker thread with its own GPU context (its own stream) computes them while this thread tracks frame k.  The
     // queue between the two holds at most `depth` frames.  Every result is the serial loop's: same frames, same
-    // ids, same kernels, only earlier.  BRIEF's offsets must be given here (they are per context).
-    void setPipeline(int depth, int device, const std::vector<int8_t>& briefOffsets);
+    // ids, same kernels, only earlier.  BRIEF's offsets must be given here (they are per context).  `readers` frames
+    // are read and PNG-decoded ahead on threads of their own.
+    void setPipeline(int depth, int device, const std::vector<int8_t>& briefOffsets, int readers = 4);
+    static Frame::ptr readFrame(const std::string& path);  // cv::imread(path, IMREAD_GRAYSCALE)
 
     // every added frame's pose (T_cw, SE3d::data()) in order, and what happened to it
     const std::vector<SE3>& trajectory() const { return trajectory_; }
@@ -129,7 +131,7 @@ public:
     Map::ptr map;
     SE3 relativeMotion;
     double t_features = 0, t_init = 0, t_track = 0, t_reinit = 0;  // seconds, summed
-    double t_read = 0;  // getNextFrame (file read + PNG decode), summed
+    double t_read = 0;  // getNextFrame (file read + PNG decode), summed; pipelined: waiting for the decode pool
     double t_wait = 0;  // pipelined: the tracking thread waiting for the worker's next frame
 
 private:
@@ -151,7 +153,7 @@ private:
     std::mt19937 ransac_rng_{0};  // getFRANSAC's sample draws (the reference seeds from std::random_device)
     int gpu_status_ = YV_OK;
 
-    int pipeline_depth_ = 0, pipeline_device_ = 0;
+    int pipeline_depth_ = 0, pipeline_device_ = 0, pipeline_readers_ = 4;
     std::vector<int8_t> pipeline_offsets_;
 
     bool gpu(int st, const char* what);

@@ -3,7 +3,7 @@
 //
 // usage: yavo_loop_handler CONFIG.json [--frames N] [--poses KITTI.txt] [--poses-bin POSES.bin]
 //                                      [--events EVENTS.bin] [--offsets-seed S] [--device D] [--check-config]
-//                                      [--pipeline DEPTH]
+//                                      [--pipeline DEPTH] [--readers N]
 //   --check-config   no GPU: print the parsed configuration, the path train and the first frames as JSON (the
 //                    reference's LoopHandlerTest cases: stereoStatus, getSeqNo, getLeftImagesPath,
 //                    getLeftTrainLength, getNextFrame dimensions, frame ids)
@@ -12,6 +12,7 @@
 //   --offsets-seed   BRIEF's preComputeOffsets seed (the reference uses std::random_device; default 42)
 //   --pipeline       DEPTH > 0: frame k + 1's read + detect + describe on a worker thread (own GPU context) while
 //                    frame k is tracked (LoopHandler::setPipeline); the results are the serial loop's
+//   --readers        pipelined: frames read + PNG-decoded ahead on their own threads (default 4)
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -40,7 +41,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     const std::string config = argv[1];
-    int frames = -1, device = 0, pipeline = 0;
+    int frames = -1, device = 0, pipeline = 0, readers = 4;
     uint32_t seed = 42;
     bool check = false;
     std::string poses_txt, poses_bin, events_bin;
@@ -54,6 +55,7 @@ int main(int argc, char** argv) {
         else if (a == "--offsets-seed") seed = (uint32_t)std::strtoul(next().c_str(), nullptr, 10);
         else if (a == "--device") device = std::atoi(next().c_str());
         else if (a == "--pipeline") pipeline = std::atoi(next().c_str());
+        else if (a == "--readers") readers = std::atoi(next().c_str());
         else if (a == "--check-config") check = true;
         else {
             std::cerr << "unknown option " << a << std::endl;
@@ -94,7 +96,7 @@ int main(int argc, char** argv) {
     Brief offsets_setter(dev, 256);
     const std::vector<int8_t> offsets = Brief::preComputeOffsets(seed);
     if (!offsets_setter.setOffsets(offsets)) return 3;
-    if (pipeline > 0) lh.setPipeline(pipeline, device, offsets);
+    if (pipeline > 0) lh.setPipeline(pipeline, device, offsets, readers);
 
     const auto t0 = std::chrono::steady_clock::now();
     lh.runVO(frames);
@@ -132,6 +134,7 @@ int main(int argc, char** argv) {
               << ", \"seconds_features\": " << lh.t_features << ", \"seconds_init\": " << lh.t_init
               << ", \"seconds_track\": " << lh.t_track << ", \"seconds_reinit\": " << lh.t_reinit
               << ", \"seconds_read\": " << lh.t_read << ", \"seconds_wait\": " << lh.t_wait
-              << ", \"pipeline\": " << pipeline << "}" << std::endl;
+              << ", \"pipeline\": " << pipeline << ", \"readers\": " << (pipeline > 0 ? readers : 0) << "}"
+              << std::endl;
     return 0;
 }

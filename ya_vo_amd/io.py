@@ -29,6 +29,13 @@ def imread_gray(path: str) -> np.ndarray:
         return png_decode_gray(f.read())
 
 
+def png_write_gray(path: str, img) -> None:
+    """8-bit grey image -> PNG file (Paeth rows, zlib level 1 as cv::imwrite; yv_png_write_gray).  Releases the GIL (ctypes)."""
+    a = np.ascontiguousarray(img, np.uint8)
+    _check(_lib().yv_png_write_gray(path.encode(), a.ctypes.data, a.shape[0], a.shape[1], a.shape[1]),
+           "yv_png_write_gray")
+
+
 def parse_calib_string(line: str) -> np.ndarray:
     """parseCalibString (src/Utils.cc:4-28) -> 4x4 float64 (missing values 0)."""
     out = np.zeros(16, np.float64)
