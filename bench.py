@@ -129,7 +129,7 @@ def write_png_sequence(base, left, right, threads):
     from ya_vo_amd.io import png_write_gray
 
     def write(j):
-        png_write_gray(j[0], j[1])  # Paeth rows, zlib level 1 (cv::imwrite's default); ctypes releases the GIL
+        png_write_gray(j[0], j[1])  # Sub rows, deflate level 1 + Z_RLE as cv::imwrite; ctypes releases the GIL
     with ThreadPoolExecutor(max_workers=threads) as ex:
         list(ex.map(write, jobs))
     with open(os.path.join(base, "calib.txt"), "w") as f:
@@ -137,15 +137,16 @@ def write_png_sequence(base, left, right, threads):
             f.write(f"P{i}: 7.188560e+02 0 6.071928e+02 {-386.1448 * i:.6e} 0 7.188560e+02 1.852157e+02 0 0 0 1 0\n")
 
 
-def png_end_to_end(ctx, shard, images, halo_right, B, steps, threads):
+def png_end_to_end(ctx, shard, images, halo_right, B, steps, threads, gpu_decode=True):
     """PNG-input end-to-end rate: the shard's frames as a KITTI stereo PNG sequence (sequence frame 0 =
-    the halo frame, 1..B = the shard), every step decoded on `threads` host threads into pinned staging and copied to
-    one of two device buffers on the context stream (yv_seq_upload), then the step's kernels; the host decodes step
-    i + 1 while the GPU runs step i.  Timed: every decode, copy and step."""
+    the halo frame, 1..B = the shard).  gpu_decode: every step the files are read by `threads` host threads straight
+    into pinned staging, copied up compressed and decoded by the inflate / unfilter kernels on the context stream
+    (yv_seq_upload_gpu); otherwise decoded on the host threads into pinned staging and copied up (yv_seq_upload).
+    Either way the host prepares step i + 1 while the GPU runs step i.  Timed: every read, decode, copy and step."""
     import shutil
     import tempfile
     import torch
-    from ya_vo_amd.io import Sequence
+    from ya_vo_amd.io import PngDecoder, Sequence
     tmp = tempfile.mkdtemp(prefix="yavo_png_")
     try:
         t0 = time.perf_counter()
@@ -159,8 +160,13 @@ def png_end_to_end(ctx, shard, images, halo_right, B, steps, threads):
         dev = torch.device("cuda", ctx.device)
         img = H * W
         bufs = [torch.empty((2 * B + 2) * img, dtype=torch.uint8, device=dev) for _ in range(2)]
+        dec = PngDecoder(ctx, 2 * B, H, W) if gpu_decode else None
 
         def upload(k):
+            if dec is not None:
+                dec.upload_sequence(seq, 1, B, bufs[k].data_ptr(), img, threads)
+                dec.upload_sequence(seq, 0, 1, bufs[k].data_ptr() + 2 * B * img, img, threads)
+                return
             seq.upload(ctx, 1, B, bufs[k].data_ptr(), img, threads)              # frames -> images 0 .. 2B-1
             seq.upload(ctx, 0, 1, bufs[k].data_ptr() + 2 * B * img, img, threads)  # halo frame -> 2B (+ its right)
 
@@ -175,17 +181,35 @@ def png_end_to_end(ctx, shard, images, halo_right, B, steps, threads):
         shard.drain()
         torch.cuda.synchronize()
         el = time.perf_counter() - t1
-        # the decode alone on the same threads (no GPU), for the bound
-        t2 = time.perf_counter()
-        seq.read(1, B, threads)
-        dec_s = time.perf_counter() - t2
+        res = {"frames_per_s": round(B * steps / el, 2), "ms_per_step": round(1e3 * el / steps, 3), "steps": steps,
+               "host_threads": threads, "png_bytes_per_stereo_frame": round(png_bytes / (B + 1)),
+               "png_write_s": round(write_s, 2)}
+        if dec is not None:
+            codes, bad = dec.status()
+            # the decoded images are the step's frames: the pipeline's inputs came through the PNG files intact
+            res["decode_errors"] = int(bad)
+            res["images_bit_identical"] = bool(np.array_equal(
+                bufs[(steps - 1) % 2][:2 * B * img].cpu().numpy(), images[:2 * B].reshape(-1)))
+            # the decode alone (read + inflate + unfilter), GPU idle otherwise
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            dec.upload_sequence(seq, 1, B, bufs[0].data_ptr(), img, threads)
+            dec.status()
+            res["decode_only_frames_per_s"] = round(B / (time.perf_counter() - t2), 2)
+            res["how"] = ("KITTI stereo PNG sequence written as cv::imwrite does (Sub rows, deflate level 1, Z_RLE) -> "
+                          "yv_seq_upload_gpu (host threads read the files into pinned staging, the IDAT streams go up "
+                          "compressed, inflate + unfilter kernels on the context stream) -> the step's kernels; the "
+                          "host reads step i+1 while the GPU runs step i; timed region = every read + copy + decode + "
+                          "step")
+            dec.close()
+        else:
+            t2 = time.perf_counter()
+            seq.read(1, B, threads)
+            res["decode_only_frames_per_s"] = round(B / (time.perf_counter() - t2), 2)
+            res["how"] = ("the same files -> yv_seq_upload (host decode threads -> pinned staging -> async HBM copy on "
+                          "the context stream) -> the step's kernels")
         seq.close()
-        return {"frames_per_s": round(B * steps / el, 2), "ms_per_step": round(1e3 * el / steps, 3), "steps": steps,
-                "decode_threads": threads, "decode_only_frames_per_s": round(B / dec_s, 2),
-                "png_bytes_per_stereo_frame": round(png_bytes / (B + 1)), "png_write_s": round(write_s, 2),
-                "how": "KITTI stereo PNG sequence (Paeth rows, zlib 1) -> yv_seq_upload (host decode threads -> pinned "
-                       "staging -> async HBM copy on the context stream) -> the step's kernels; the decode of step i+1 "
-                       "overlaps step i on the GPU; timed region = every decode + copy + step"}
+        return res
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
@@ -460,11 +484,16 @@ def main():
 
     png_e2e = None
     if args.png_steps > 0 and world == 1 and args.tracker == "match":
+        thr = args.png_threads or cpu_threads_available()
         try:
-            png_e2e = png_end_to_end(ctx, shard, images, halo_right, B, args.png_steps,
-                                     args.png_threads or cpu_threads_available())
+            png_e2e = png_end_to_end(ctx, shard, images, halo_right, B, args.png_steps, thr, gpu_decode=True)
         except Exception as e:  # reported, never fatal to the headline
             png_e2e = {"error": repr(e)[:300]}
+        try:
+            png_e2e["host_decode"] = png_end_to_end(ctx, shard, images, halo_right, B, args.png_steps, thr,
+                                                    gpu_decode=False)
+        except Exception as e:
+            png_e2e["host_decode"] = {"error": repr(e)[:300]}
     lh = None
     if args.loop_handler_frames > 0 and world == 1 and rank == 0:
         try:

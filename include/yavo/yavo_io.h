@@ -53,8 +53,30 @@ int yv_seq_read(yv_seq* seq, int first, int n, uint8_t* dst, int64_t pitch, int 
 int yv_seq_upload(yv_seq* seq, struct yv_ctx* ctx, int first, int n, uint8_t* d_dst, int64_t pitch, int threads,
                   void* stream);
 
+/* PNG decoding on the GPU (yavo_inflate.hip): the inflate (RFC 1950/1951) and the scanline filters run as kernels,
+ * one wave per image; the host only reads the files and gathers each image's IDAT stream into pinned staging.
+ * Formats: 8-bit grey, non-interlaced, H x W (every KITTI frame); anything else is YV_ERR_INVALID with nothing
+ * enqueued (yv_png_decode_gray / yv_seq_upload decode every format on the host).  Calls of one decoder are ordered on
+ * the stream they are given (use one stream per decoder); the staging of a call is reused two calls later, after its
+ * copy completed. */
+typedef struct yv_pngdec yv_pngdec;
+int yv_pngdec_create(struct yv_ctx* ctx, int max_images, int H, int W, yv_pngdec** out);
+void yv_pngdec_destroy(yv_pngdec* d);
+/* n PNG files in host memory (files[i], sizes[i] bytes) -> device images at d_dst + i * pitch, rows of W bytes;
+ * asynchronous on stream (NULL: the context stream) */
+int yv_pngdec_decode(yv_pngdec* d, const uint8_t* const* files, const size_t* sizes, int n, uint8_t* d_dst,
+                     int64_t pitch, void* stream);
+/* the frames [first, first + n) of a sequence (left, right per frame for stereo), read by `threads` host threads
+ * straight into the pinned staging, then decoded as yv_pngdec_decode does */
+int yv_seq_upload_gpu(yv_seq* seq, yv_pngdec* d, int first, int n, uint8_t* d_dst, int64_t pitch, int threads,
+                      void* stream);
+/* waits for the last decode; codes[i] (optional, host, n of the last call) = 0 or the image's decode error;
+ * *n_bad = images that failed */
+int yv_pngdec_status(yv_pngdec* d, int32_t* codes, int* n_bad);
+
 /* The writer side, for test sequences (the reference only reads PNGs): an 8-bit grey image to a PNG file, every row
- * Paeth-filtered, zlib level 1 (cv::imwrite's default IMWRITE_PNG_COMPRESSION); rows of W bytes, stride bytes apart. */
+ * Sub-filtered and deflated at level 1 with Z_RLE, as cv::imwrite writes PNGs (the reference's tests/epilines.png:
+ * filter 1 on every row, zlib header 0x7801); rows of W bytes, stride bytes apart. */
 int yv_png_write_gray(const char* path, const uint8_t* img, int H, int W, int stride);
 
 /* KITTI odometry poses: one line per frame, the 12 row-major numbers of the 3x4 [R | t] of T_wc = T_cw^-1, for

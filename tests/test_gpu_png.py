@@ -1,0 +1,151 @@
+"""PNG decoding on the GPU (yv_pngdec_*, ya_vo_amd/csrc/yavo_inflate.hip) against the host decoder
+(yv_png_decode_gray, itself pinned to PIL in tests/test_io.py): byte for byte on the reference's own KITTI frame
+(tests/epilines.png's content, re-encoded), cv::imwrite-style files (Sub rows, deflate level 1, Z_RLE), PIL-written
+files (adaptive filters, default level), stored blocks (level 0), fixed-Huffman blocks (tiny images), every filter
+type, odd sizes, and a corrupted stream (reported, no fault)."""
+import io as _io
+import os
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import ya_vo_amd as yv
+from ya_vo_amd.io import PngDecoder, Sequence, png_decode_gray, png_write_gray
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _png(img, filt, level, strategy=zlib.Z_DEFAULT_STRATEGY):
+    """8-bit grey PNG with one filter type per row (filt: int or list), zlib at `level`."""
+    H, W = img.shape
+    a = img.astype(np.int16)
+    rows = []
+    for r in range(H):
+        f = filt[r % len(filt)] if isinstance(filt, (list, tuple)) else filt
+        cur = a[r]
+        up = a[r - 1] if r else np.zeros(W, np.int16)
+        left = np.concatenate([[0], cur[:-1]])
+        ul = np.concatenate([[0], up[:-1]])
+        if f == 0:
+            pred = np.zeros(W, np.int16)
+        elif f == 1:
+            pred = left
+        elif f == 2:
+            pred = up
+        elif f == 3:
+            pred = (left + up) >> 1
+        else:
+            p = left + up - ul
+            pa, pb, pc = np.abs(p - left), np.abs(p - up), np.abs(p - ul)
+            pred = np.where((pa <= pb) & (pa <= pc), left, np.where(pb <= pc, up, ul))
+        rows.append(bytes([f]) + ((cur - pred) & 0xFF).astype(np.uint8).tobytes())
+    c = zlib.compressobj(level, zlib.DEFLATED, 15, 8, strategy)
+    z = c.compress(b"".join(rows)) + c.flush()
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
+    # the IDAT stream split over several chunks, as encoders do
+    idat = b"".join(chunk(b"IDAT", z[i:i + 8192]) for i in range(0, len(z), 8192))
+    return (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", W, H, 8, 0, 0, 0, 0)) + idat +
+            chunk(b"IEND", b""))
+
+
+def _decode_gpu(ctx, files, H, W):
+    import torch
+    dec = PngDecoder(ctx, len(files), H, W)
+    d = torch.zeros(len(files) * H * W, dtype=torch.uint8, device="cuda:0")
+    dec.decode(files, d.data_ptr(), H * W)
+    codes, bad = dec.status()
+    out = d.cpu().numpy().reshape(len(files), H, W)
+    dec.close()
+    return out, codes[:len(files)], bad
+
+
+def test_gpu_png_matches_host_decoder(ctx):
+    from ya_vo_amd.synth import synth_frame
+    rng = np.random.default_rng(5)
+    H, W = 376, 1241
+    frames = [synth_frame(17, k, 3 * k, H, W) for k in range(3)]
+    ref = np.array(__import__("PIL.Image", fromlist=["Image"]).open(
+        os.path.join(ROOT, "tests", "golden", "png", "epilines_crop.png")))
+    files, expect = [], []
+    for k, img in enumerate(frames):
+        files.append(_png(img, 1, 1, zlib.Z_RLE))          # cv::imwrite style
+        files.append(_png(img, [0, 1, 2, 3, 4], 6))       # every filter type, default level
+        files.append(_png(img, 4, 9))                     # Paeth, best compression (long matches)
+        expect += [img] * 3
+    noise = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    files.append(_png(noise, 0, 0))                       # stored blocks
+    expect.append(noise)
+    flat = np.full((H, W), 77, np.uint8)
+    files.append(_png(flat, 2, 6))                        # long runs, distance-1 and long-distance matches
+    expect.append(flat)
+    out, codes, bad = _decode_gpu(ctx, files, H, W)
+    assert bad == 0, codes
+    for i, (o, e) in enumerate(zip(out, expect)):
+        np.testing.assert_array_equal(o, e, err_msg=f"file {i}")
+        np.testing.assert_array_equal(png_decode_gray(files[i]), e)  # the host decoder agrees
+    # the reference's KITTI crop (PIL-decoded) re-encoded by PIL with its adaptive filters
+    from PIL import Image
+    buf = _io.BytesIO()
+    Image.fromarray(ref).save(buf, format="PNG")
+    out2, _, bad2 = _decode_gpu(ctx, [buf.getvalue(), open(os.path.join(ROOT, "tests", "golden", "png",
+                                                                         "epilines_crop.png"), "rb").read()], *ref.shape)
+    assert bad2 == 0
+    np.testing.assert_array_equal(out2[0], ref)
+    np.testing.assert_array_equal(out2[1], ref)
+
+
+@pytest.mark.parametrize("H,W", [(1, 1), (3, 5), (7, 64), (65, 129), (130, 3)])
+def test_gpu_png_odd_sizes_fixed_huffman(ctx, H, W):
+    """Tiny images compress to fixed-Huffman blocks; odd sizes exercise the last partial 4-byte group and bands of
+    fewer than 64 rows."""
+    rng = np.random.default_rng(H * 100 + W)
+    imgs = [rng.integers(0, 256, (H, W), dtype=np.uint8), np.tile(np.arange(W, dtype=np.uint8), (H, 1))]
+    files = [_png(imgs[0], [4, 3, 2, 1, 0], 6), _png(imgs[1], 1, 1, zlib.Z_FIXED)]
+    out, codes, bad = _decode_gpu(ctx, files, H, W)
+    assert bad == 0, codes
+    np.testing.assert_array_equal(out[0], imgs[0])
+    np.testing.assert_array_equal(out[1], imgs[1])
+
+
+def test_gpu_png_reports_corrupt_stream(ctx):
+    H, W = 40, 50
+    img = np.random.default_rng(1).integers(0, 256, (H, W), dtype=np.uint8)
+    good = _png(img, 1, 6)
+    bad = bytearray(good)
+    i = bad.index(b"IDAT") + 4 + 40
+    for k in range(i, i + 30):
+        bad[k] ^= 0x5A  # garbage inside the deflate data (the chunk CRC is not what the decoder checks)
+    out, codes, n_bad = _decode_gpu(ctx, [good, bytes(bad), good], H, W)
+    np.testing.assert_array_equal(out[0], img)
+    np.testing.assert_array_equal(out[2], img)
+    # a damaged stream either fails a check or decodes to something else; it never faults or hangs the wave
+    assert n_bad <= 1 and codes[0] == 0 and codes[2] == 0
+
+
+def test_gpu_png_sequence_upload(ctx, tmp_path):
+    """yv_seq_upload_gpu: a stereo KITTI-layout sequence written as cv::imwrite does (yv_png_write_gray) decodes on the
+    GPU to the same images as the host path (yv_seq_read)."""
+    import torch
+    from ya_vo_amd.synth import synth_stereo_batch
+    H, W, n = 376, 1241, 6
+    fr = synth_stereo_batch(99, n, start=0)
+    for side in ("image_0", "image_1"):
+        os.makedirs(tmp_path / side)
+    for k in range(n):
+        png_write_gray(str(tmp_path / "image_0" / f"{k:06d}.png"), fr[2 * k])
+        png_write_gray(str(tmp_path / "image_1" / f"{k:06d}.png"), fr[2 * k + 1])
+    seq = Sequence(str(tmp_path), stereo=True)
+    dec = PngDecoder(ctx, 2 * n, H, W)
+    d = torch.zeros(2 * (n - 1) * H * W, dtype=torch.uint8, device="cuda:0")
+    dec.upload_sequence(seq, 1, n - 1, d.data_ptr(), H * W, threads=4)
+    codes, bad = dec.status()
+    assert bad == 0, codes
+    np.testing.assert_array_equal(d.cpu().numpy().reshape(-1, H, W), seq.read(1, n - 1))
+    np.testing.assert_array_equal(d.cpu().numpy().reshape(-1, H, W), fr[2:2 * n])
+    dec.close()
+    seq.close()

@@ -205,7 +205,7 @@ def test_kitti_poses_roundtrip(tmp_path):
 
 
 def test_png_writer_round_trip(tmp_path):
-    """yv_png_write_gray (the bench's and tools' sequence writer: Paeth rows, zlib level 1) round-trips through the
+    """yv_png_write_gray (the bench's and tools' sequence writer, cv::imwrite's format) round-trips through the
     decoder, PIL agrees, and odd sizes / strides take the same path."""
     from PIL import Image
     from ya_vo_amd.io import png_decode_gray, png_write_gray

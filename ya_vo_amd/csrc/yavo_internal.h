@@ -232,6 +232,16 @@ void launch_map_chunk(const double* rel, int n, int64_t first_frame, int kf_ever
                       const double* edge_X, const uint8_t* edge_outlier, int max_kp, int max_kf, void* block,
                       hipStream_t s);
 
+// PNG decoding on the GPU (yavo_inflate.hip): per-image status codes and the two kernels
+enum : int32_t {
+    kPngOk = 0, kPngErrHeader = 1, kPngErrBlock = 2, kPngErrCode = 3, kPngErrOverrun = 4, kPngErrShort = 5,
+    kPngErrFilter = 6
+};
+void launch_png_inflate(const uint8_t* src, const int64_t* off, const int32_t* len, int n, uint8_t* out,
+                        int64_t out_pitch, uint32_t out_len, int32_t* status, hipStream_t s);
+void launch_png_unfilter(const uint8_t* raw, int64_t raw_pitch, int n, int H, int W, uint8_t* dst, int64_t dst_pitch,
+                         int dst_stride, int32_t* status, hipStream_t s);
+
 void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, const double* edge_X,
                        const double* edge_uv, const double* K, const double* priors, double* poses,
                        uint8_t* edge_outlier, int32_t* inliers, hipStream_t s);

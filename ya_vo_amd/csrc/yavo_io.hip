@@ -459,25 +459,275 @@ int yv_seq_upload(yv_seq* s, yv_ctx* ctx, int first, int n, uint8_t* d_dst, int6
     return YV_OK;
 }
 
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// PNG decoding on the GPU: host side (chunk walk, staging, copies, launches)
+// ------------------------------------------------------------------------------------------------
+struct yv_pngdec {
+    yv_ctx* ctx = nullptr;
+    int max_images = 0, H = 0, W = 0;
+    int64_t raw_pitch = 0;        // inflated image: H rows of 1 + W bytes (+ 64 B of over-read slack), 256-B aligned
+    uint8_t* d_raw = nullptr;     // [max_images][raw_pitch]
+    int32_t* d_status = nullptr;  // [max_images]
+    int n_last = 0;
+    hipStream_t last_stream = nullptr;
+    // two slots of staging: pinned host {streams | offsets | lengths} and the device copy of the streams
+    struct Slot {
+        uint8_t* h = nullptr;   // pinned: compressed streams (64-B aligned each)
+        size_t cap = 0;
+        int64_t* h_off = nullptr;
+        int32_t* h_len = nullptr;
+        uint8_t* d = nullptr;   // device copy of the streams
+        size_t dcap = 0;
+        int64_t* d_off = nullptr;
+        int32_t* d_len = nullptr;
+        hipEvent_t done = nullptr;  // the slot's copy and inflate completed
+        bool pending = false;
+    } slot[2];
+    int next = 0;
+};
+
+namespace {
+
+// IDAT payloads of one 8-bit grey non-interlaced H x W PNG moved to the front of buf, in place (memmove);
+// returns their length or -1
+int64_t png_gather_idat(uint8_t* buf, size_t len, int H, int W) {
+    PngHeader h;
+    if (png_parse(buf, len, h, nullptr, nullptr) != YV_OK) return -1;
+    if (h.ctype != 0 || h.depth != 8 || h.interlace != 0 || h.H != H || h.W != W) return -1;
+    size_t off = 8, out = 0;
+    while (off + 12 <= len) {
+        const uint32_t n = be32(buf + off);
+        if (n > len - off - 12) return -1;
+        const uint8_t* type = buf + off + 4;
+        if (!std::memcmp(type, "IDAT", 4)) {
+            std::memmove(buf + out, buf + off + 8, n);  // out <= off + 8: the move never overruns unread chunks
+            out += n;
+        } else if (!std::memcmp(type, "IEND", 4)) {
+            break;
+        }
+        off += 12 + n;
+    }
+    return out ? (int64_t)out : -1;
+}
+
+int slot_reserve(yv_pngdec::Slot& sl, size_t bytes, int n) {
+    if (bytes > sl.cap) {
+        if (sl.h) (void)hipHostFree(sl.h);
+        sl.h = nullptr;
+        sl.cap = 0;
+        const size_t cap = std::max(bytes + bytes / 4, (size_t)16 << 20);
+        if (hipHostMalloc(reinterpret_cast<void**>(&sl.h), cap) != hipSuccess) return YV_ERR_HIP;
+        sl.cap = cap;
+    }
+    if (bytes > sl.dcap) {
+        if (sl.d) (void)hipFree(sl.d);
+        sl.d = nullptr;
+        sl.dcap = 0;
+        const size_t cap = std::max(bytes + bytes / 4, (size_t)16 << 20);
+        if (hipMalloc(reinterpret_cast<void**>(&sl.d), cap) != hipSuccess) return YV_ERR_HIP;
+        sl.dcap = cap;
+    }
+    (void)n;
+    return YV_OK;
+}
+
+// the slot's streams are gathered: copy them (and the job table) up, inflate, unfilter
+int pngdec_launch(yv_pngdec* d, yv_pngdec::Slot& sl, size_t bytes, int n, uint8_t* d_dst, int64_t pitch,
+                  hipStream_t st) {
+    if (hipMemcpyAsync(sl.d, sl.h, bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(sl.d_off, sl.h_off, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(sl.d_len, sl.h_len, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, st) != hipSuccess)
+        return YV_ERR_HIP;
+    yavo::launch_png_inflate(sl.d, sl.d_off, sl.d_len, n, d->d_raw, d->raw_pitch, (uint32_t)d->H * (d->W + 1),
+                             d->d_status, st);
+    yavo::launch_png_unfilter(d->d_raw, d->raw_pitch, n, d->H, d->W, d_dst, pitch, d->W, d->d_status, st);
+    if (hipGetLastError() != hipSuccess || hipEventRecord(sl.done, st) != hipSuccess) return YV_ERR_HIP;
+    sl.pending = true;
+    d->n_last = n;
+    d->last_stream = st;
+    return YV_OK;
+}
+
+yv_pngdec::Slot* pngdec_next_slot(yv_pngdec* d) {
+    yv_pngdec::Slot& sl = d->slot[d->next];
+    d->next ^= 1;
+    if (sl.pending && hipEventSynchronize(sl.done) != hipSuccess) return nullptr;
+    sl.pending = false;
+    return &sl;
+}
+
+}  // namespace
+
+extern "C" {
+
+int yv_pngdec_create(yv_ctx* ctx, int max_images, int H, int W, yv_pngdec** out) {
+    if (!ctx || !out || max_images <= 0 || H < 1 || W < 1 || (int64_t)H * (W + 1) >= (1ll << 31)) return YV_ERR_INVALID;
+    *out = nullptr;
+    if (hipSetDevice(yavo::ctx_device(ctx)) != hipSuccess) return YV_ERR_HIP;
+    yv_pngdec* d = new (std::nothrow) yv_pngdec();
+    if (!d) return YV_ERR_INVALID;
+    d->ctx = ctx;
+    d->max_images = max_images;
+    d->H = H;
+    d->W = W;
+    d->raw_pitch = (((int64_t)H * (W + 1) + 64) + 255) & ~(int64_t)255;
+    bool ok = hipMalloc(reinterpret_cast<void**>(&d->d_raw), (size_t)d->raw_pitch * max_images) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&d->d_status), sizeof(int32_t) * (size_t)max_images) == hipSuccess;
+    for (auto& sl : d->slot) {
+        ok = ok && hipHostMalloc(reinterpret_cast<void**>(&sl.h_off), sizeof(int64_t) * (size_t)max_images) == hipSuccess &&
+             hipHostMalloc(reinterpret_cast<void**>(&sl.h_len), sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
+             hipMalloc(reinterpret_cast<void**>(&sl.d_off), sizeof(int64_t) * (size_t)max_images) == hipSuccess &&
+             hipMalloc(reinterpret_cast<void**>(&sl.d_len), sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
+             hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
+    }
+    if (!ok) {
+        yv_pngdec_destroy(d);
+        return YV_ERR_HIP;
+    }
+    *out = d;
+    return YV_OK;
+}
+
+void yv_pngdec_destroy(yv_pngdec* d) {
+    if (!d) return;
+    (void)hipSetDevice(yavo::ctx_device(d->ctx));
+    for (auto& sl : d->slot) {
+        if (sl.done) {
+            (void)hipEventSynchronize(sl.done);
+            (void)hipEventDestroy(sl.done);
+        }
+        if (sl.h) (void)hipHostFree(sl.h);
+        if (sl.h_off) (void)hipHostFree(sl.h_off);
+        if (sl.h_len) (void)hipHostFree(sl.h_len);
+        if (sl.d) (void)hipFree(sl.d);
+        if (sl.d_off) (void)hipFree(sl.d_off);
+        if (sl.d_len) (void)hipFree(sl.d_len);
+    }
+    if (d->d_raw) (void)hipFree(d->d_raw);
+    if (d->d_status) (void)hipFree(d->d_status);
+    delete d;
+}
+
+int yv_pngdec_decode(yv_pngdec* d, const uint8_t* const* files, const size_t* sizes, int n, uint8_t* d_dst,
+                     int64_t pitch, void* stream) {
+    if (!d || n < 0 || n > d->max_images || (n > 0 && (!files || !sizes || !d_dst)) || pitch < (int64_t)d->H * d->W)
+        return YV_ERR_INVALID;
+    if (n == 0) return YV_OK;
+    for (int i = 0; i < n; ++i)
+        if (!files[i]) return YV_ERR_INVALID;
+    if (hipSetDevice(yavo::ctx_device(d->ctx)) != hipSuccess) return YV_ERR_HIP;
+    yv_pngdec::Slot* sl = pngdec_next_slot(d);
+    if (!sl) return YV_ERR_HIP;
+    size_t bytes = 0;
+    for (int i = 0; i < n; ++i) bytes += (sizes[i] + 63) & ~(size_t)63;
+    if (slot_reserve(*sl, bytes, n) != YV_OK) return YV_ERR_HIP;
+    size_t off = 0;
+    for (int i = 0; i < n; ++i) {
+        std::memcpy(sl->h + off, files[i], sizes[i]);
+        const int64_t len = png_gather_idat(sl->h + off, sizes[i], d->H, d->W);
+        if (len < 0) return YV_ERR_INVALID;
+        sl->h_off[i] = (int64_t)off;
+        sl->h_len[i] = (int32_t)len;
+        off += (sizes[i] + 63) & ~(size_t)63;
+    }
+    hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : yavo::ctx_stream(d->ctx);
+    return pngdec_launch(d, *sl, off, n, d_dst, pitch, st);
+}
+
+int yv_pngdec_status(yv_pngdec* d, int32_t* codes, int* n_bad) {
+    if (!d || !n_bad) return YV_ERR_INVALID;
+    *n_bad = 0;
+    if (d->n_last == 0) return YV_OK;
+    if (hipSetDevice(yavo::ctx_device(d->ctx)) != hipSuccess) return YV_ERR_HIP;
+    std::vector<int32_t> h((size_t)d->n_last);
+    if (hipStreamSynchronize(d->last_stream) != hipSuccess ||
+        hipMemcpy(h.data(), d->d_status, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        return YV_ERR_HIP;
+    for (int32_t c : h) *n_bad += c != 0;
+    if (codes) std::memcpy(codes, h.data(), sizeof(int32_t) * h.size());
+    return YV_OK;
+}
+
+int yv_seq_upload_gpu(yv_seq* s, yv_pngdec* d, int first, int n, uint8_t* d_dst, int64_t pitch, int threads,
+                      void* stream) {
+    if (!s || !d || !d_dst || first < 0 || n < 0 || first + n > (int)s->left.size() || s->H != d->H || s->W != d->W)
+        return YV_ERR_INVALID;
+    const int per = s->stereo ? 2 : 1;
+    const int total = n * per;
+    if (total > d->max_images || pitch < (int64_t)d->H * d->W) return YV_ERR_INVALID;
+    if (n == 0) return YV_OK;
+    if (hipSetDevice(yavo::ctx_device(d->ctx)) != hipSuccess) return YV_ERR_HIP;
+    yv_pngdec::Slot* sl = pngdec_next_slot(d);
+    if (!sl) return YV_ERR_HIP;
+    // file sizes -> 64-B aligned regions of the pinned slot; the threads read each file into its region and gather
+    // its IDAT stream to the region's front
+    std::vector<size_t> size((size_t)total), off((size_t)total);
+    size_t bytes = 0;
+    for (int k = 0; k < total; ++k) {
+        const std::string& path = (k % per) ? s->right[first + k / per] : s->left[first + k / per];
+        FILE* f = std::fopen(path.c_str(), "rb");
+        if (!f) return YV_ERR_INVALID;
+        std::fseek(f, 0, SEEK_END);
+        const long z = std::ftell(f);
+        std::fclose(f);
+        if (z <= 0) return YV_ERR_INVALID;
+        size[k] = (size_t)z;
+        off[k] = bytes;
+        bytes += ((size_t)z + 63) & ~(size_t)63;
+    }
+    if (slot_reserve(*sl, bytes, total) != YV_OK) return YV_ERR_HIP;
+    if (threads <= 0) threads = (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 64u);
+    threads = std::max(1, std::min(threads, total));
+    std::atomic<int> next{0}, status{YV_OK};
+    auto work = [&]() {
+        for (int k; (k = next.fetch_add(1)) < total;) {
+            const std::string& path = (k % per) ? s->right[first + k / per] : s->left[first + k / per];
+            FILE* f = std::fopen(path.c_str(), "rb");
+            const size_t got = f ? std::fread(sl->h + off[k], 1, size[k], f) : 0;
+            if (f) std::fclose(f);
+            const int64_t len = got == size[k] ? png_gather_idat(sl->h + off[k], size[k], d->H, d->W) : -1;
+            if (len < 0) {
+                status = YV_ERR_INVALID;
+                continue;
+            }
+            sl->h_off[k] = (int64_t)off[k];
+            sl->h_len[k] = (int32_t)len;
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    if (status.load() != YV_OK) return status.load();
+    hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : yavo::ctx_stream(d->ctx);
+    return pngdec_launch(d, *sl, bytes, total, d_dst, pitch, st);
+}
+
 int yv_png_write_gray(const char* path, const uint8_t* img, int H, int W, int stride) {
     if (!path || !img || H < 1 || W < 1 || stride < W) return YV_ERR_INVALID;
-    // filtered scanlines: filter byte 4 (Paeth) + W bytes each
+    // filtered scanlines as cv::imwrite writes them (the reference's tests/epilines.png: every row filter 1 = Sub,
+    // zlib header 0x7801): filter byte + W bytes each, then deflate at level 1 with the Z_RLE strategy
     std::vector<uint8_t> raw((size_t)H * (W + 1));
     for (int r = 0; r < H; ++r) {
         const uint8_t* cur = img + (size_t)r * stride;
-        const uint8_t* up = r ? img + (size_t)(r - 1) * stride : nullptr;
         uint8_t* o = &raw[(size_t)r * (W + 1)];
-        o[0] = 4;
-        for (int c = 0; c < W; ++c) {
-            const int a = c ? cur[c - 1] : 0, b = up ? up[c] : 0, d = (c && up) ? up[c - 1] : 0;
-            const int p = a + b - d, pa = std::abs(p - a), pb = std::abs(p - b), pc = std::abs(p - d);
-            const int pred = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : d);
-            o[1 + c] = (uint8_t)(cur[c] - pred);
-        }
+        o[0] = 1;
+        for (int c = 0; c < W; ++c) o[1 + c] = (uint8_t)(cur[c] - (c ? cur[c - 1] : 0));
     }
-    uLongf zlen = compressBound((uLong)raw.size());
-    std::vector<uint8_t> z(zlen);
-    if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), 1) != Z_OK) return YV_ERR_INVALID;
+    z_stream zs;
+    std::memset(&zs, 0, sizeof zs);
+    if (deflateInit2(&zs, 1, Z_DEFLATED, 15, 8, Z_RLE) != Z_OK) return YV_ERR_INVALID;
+    std::vector<uint8_t> z(deflateBound(&zs, (uLong)raw.size()));
+    zs.next_in = raw.data();
+    zs.avail_in = (uInt)raw.size();
+    zs.next_out = z.data();
+    zs.avail_out = (uInt)z.size();
+    const int zr = deflate(&zs, Z_FINISH);
+    const uLongf zlen = (uLongf)(z.size() - zs.avail_out);
+    deflateEnd(&zs);
+    if (zr != Z_STREAM_END) return YV_ERR_INVALID;
     FILE* f = std::fopen(path, "wb");
     if (!f) return YV_ERR_INVALID;
     auto be32 = [](uint32_t v, uint8_t* b) {

@@ -30,7 +30,7 @@ def imread_gray(path: str) -> np.ndarray:
 
 
 def png_write_gray(path: str, img) -> None:
-    """8-bit grey image -> PNG file (Paeth rows, zlib level 1 as cv::imwrite; yv_png_write_gray).  Releases the GIL (ctypes)."""
+    """8-bit grey image -> PNG file (Sub rows, deflate level 1 + Z_RLE as cv::imwrite writes; yv_png_write_gray).  Releases the GIL (ctypes)."""
     a = np.ascontiguousarray(img, np.uint8)
     _check(_lib().yv_png_write_gray(path.encode(), a.ctypes.data, a.shape[0], a.shape[1], a.shape[1]),
            "yv_png_write_gray")
@@ -116,3 +116,43 @@ def read_kitti_poses(path: str, cap: int = 1 << 20) -> np.ndarray:
     _check(_lib().yv_read_kitti_poses(path.encode(), out.ctypes.data, len(out), ctypes.byref(n)),
            "yv_read_kitti_poses")
     return out[:n.value].reshape(-1, 3, 4)
+
+
+class PngDecoder:
+    """PNG decoding on the GPU (yv_pngdec_*): inflate + scanline filters as kernels, one wave per image, for 8-bit
+    grey non-interlaced H x W files (KITTI frames).  Calls are asynchronous on `stream` (0: the context stream)."""
+
+    def __init__(self, ctx, max_images: int, H: int, W: int):
+        self.lib = _lib()
+        h = ctypes.c_void_p()
+        _check(self.lib.yv_pngdec_create(ctx.handle, max_images, H, W, ctypes.byref(h)), "yv_pngdec_create")
+        self.handle, self.H, self.W = h, H, W
+
+    def decode(self, files, d_dst: int, pitch: int = 0, stream: int = 0) -> None:
+        """files: list of PNG bytes objects -> device images at d_dst + i * pitch"""
+        n = len(files)
+        bufs = [np.frombuffer(f, np.uint8) for f in files]
+        ptrs = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+        sizes = (ctypes.c_size_t * n)(*[len(b) for b in bufs])
+        _check(self.lib.yv_pngdec_decode(self.handle, ptrs, sizes, n, ctypes.c_void_p(d_dst), pitch or self.H * self.W,
+                                         ctypes.c_void_p(stream) if stream else None), "yv_pngdec_decode")
+        self._n = n
+
+    def upload_sequence(self, seq, first: int, n: int, d_dst: int, pitch: int = 0, threads: int = 0,
+                        stream: int = 0) -> None:
+        _check(self.lib.yv_seq_upload_gpu(seq.handle, self.handle, first, n, ctypes.c_void_p(d_dst),
+                                          pitch or self.H * self.W, threads, ctypes.c_void_p(stream) if stream else None),
+               "yv_seq_upload_gpu")
+        self._n = n * (2 if seq.stereo else 1)
+
+    def status(self):
+        """(codes of the last call's images, number failed); waits for the last call"""
+        bad = ctypes.c_int()
+        codes = np.zeros(max(getattr(self, "_n", 0), 1), np.int32)
+        _check(self.lib.yv_pngdec_status(self.handle, codes.ctypes.data, ctypes.byref(bad)), "yv_pngdec_status")
+        return codes, bad.value
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.yv_pngdec_destroy(self.handle)
+            self.handle = None
