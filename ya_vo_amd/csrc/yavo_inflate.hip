@@ -3,13 +3,19 @@
 // tests/epilines.png).  The host only reads the files and gathers each image's IDAT payload (its zlib stream); the
 // GPU inflates it (RFC 1950 / 1951) and undoes the scanline filters (PNG filter method 0).
 //
-// inflate: one 64-lane wave per image.  Huffman decoding is sequential, so the decoder state (bit buffer, stream
-// position, output position) is wave-uniform and lives in SGPRs; lookups go to tables in the wave's LDS (a fast table
-// per code indexed by the next 10 / 8 stream bits, canonical decoding for longer codes).  Output bytes go to a 32 KB
-// LDS ring (the deflate window, which back-references read) and every completed 4 KB of it is streamed to HBM by all
-// 64 lanes.  Length / distance copies use the lanes: byte j of a match of length L at distance D is the window byte
-// op - D + (j mod D), so each LDS read + write moves up to 64 bytes whatever D is.  The images of a batch decode
-// concurrently; the per-symbol latency of each wave sets the rate.  The Adler-32 trailer is not checked.
+// inflate: one 64-lane wave per image, and the 64 lanes decode ONE deflate block together.  Huffman codes
+// self-synchronise: a decoder started at an arbitrary bit falls onto the true token boundaries within a few tokens
+// (measured on cv::imwrite KITTI-size frames: 34 bits on average, 99% within 167).  So a chunk of the block's bits is
+// cut into 64 segments of `seg` bits; lane k decodes segment k, starting kLead bits early to synchronise, and records
+// where its last token ends.  A lane whose start differs from where its left neighbour ended re-decodes from there
+// (rarely needed twice); lane 0 starts at the true position, so the fixed point is the true token sequence.  Then a
+// prefix sum over the lanes' output counts places every lane's output, a second decode of the segment writes the
+// literals into the wave's LDS output ring and lists the (length, distance) matches, and the wave copies the matches
+// in stream order, 64 bytes per pass (byte j of a match = output byte op - D + (j mod D)).  The block's end-of-block
+// token ends the chunk early.  Block headers are parsed wave-uniformly; the dynamic code lengths use the same
+// lane-parallel decoder (repeat code 16 is a distance-1 match).  Completed 16-byte groups of the ring are streamed to
+// HBM after every chunk; matches reaching further back than the 16 KB ring read the already-written output.  The
+// Adler-32 trailer is not checked.
 //
 // unfilter: one wave per image, lane l owning row 64 b + l of band b.  Row r needs row r - 1 (Up / Average / Paeth),
 // so lane l runs one step behind lane l - 1: at step t it undoes the 4-byte group t - l of its row, and the same
@@ -22,10 +28,14 @@
 namespace yavo {
 namespace png {
 
-constexpr int kRing = 32768;  // deflate window
-constexpr int kRingMask = kRing - 1;
-constexpr int kFlush = 4096;  // ring bytes streamed to HBM at once
-constexpr int kLitBits = 10, kDistBits = 8;
+constexpr int kRing = 16384;  // LDS output ring
+constexpr uint32_t kRingMask = kRing - 1;
+constexpr int kLitBits = 12, kDistBits = 9, kClBits = 7;  // fast-table index widths
+constexpr uint32_t kSegMax = 1024, kSegMin = 64;         // bits per lane per chunk
+constexpr uint32_t kLead = 256;                          // synchronisation lead-in, bits
+constexpr int kStageWords = 2 * kSegMax + 8;             // the chunk's stream words (+ look-ahead)
+constexpr int kMaxMatch = 512;                           // matches listed per chunk
+constexpr uint32_t kCap = kRing - 64;                    // output bytes per chunk (the ring keeps the unflushed tail)
 
 struct Table {
     uint16_t cnt[16];   // codes per length
@@ -35,55 +45,53 @@ struct Table {
 };
 
 struct Lds {
-    uint8_t ring[kRing];
-    uint16_t lit_fast[1 << kLitBits];  // (symbol << 4) | length; 0: the code is longer than kLitBits
-    uint16_t dist_fast[1 << kDistBits];
+    alignas(16) uint8_t ring[kRing];
+    alignas(16) uint32_t stage[kStageWords];
+    alignas(16) uint16_t lit_fast[1 << kLitBits];   // (symbol << 4) | length; 0: longer than kLitBits (or no code)
+    alignas(16) uint16_t dist_fast[1 << kDistBits];  // distance codes; the code-length code while lengths are read
+    uint32_t mdst[kMaxMatch];                        // the chunk's matches: output position,
+    uint32_t mld[kMaxMatch];                         // (length << 16) | distance
     Table lit, dist;
-    uint8_t lens[320];  // code lengths: litlen [0, 288), distance [288, 320); the code-length code in [0, 19)
+    uint8_t lens[320];  // code lengths: litlen [0, 288), distance [288, 320)
     uint8_t cl[20];
 };
+static_assert(sizeof(Lds) <= 40 * 1024, "four waves per CU");
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t lane_of(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
-// bit reader over a 4-B aligned stream, LSB first (RFC 1951 3.1.1)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+
+// wave-uniform bit reader over a 4-B aligned stream, LSB first (RFC 1951 3.1.1); block headers only
 struct Bits {
     const uint32_t* src;
-    uint32_t nwords, wp;  // words in the stream, next word to load
-    uint64_t bb;          // bit buffer
-    uint32_t nb;          // valid bits in bb
-    uint32_t over;        // words read past the end (zeros)
-    __device__ __forceinline__ void refill() {
-        if (nb <= 32) {
-            uint32_t w = 0;
-            if (wp < nwords) w = src[wp];
-            else ++over;
-            ++wp;
-            bb |= (uint64_t)w << nb;
-            nb += 32;
-        }
-    }
-    __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)bb & ((1u << n) - 1u); }
-    __device__ __forceinline__ void drop(uint32_t n) {
-        bb >>= n;
-        nb -= n;
-    }
+    uint32_t nwords;
+    uint32_t pos;  // absolute bit position
+    __device__ __forceinline__ uint32_t word(uint32_t w) const { return w < nwords ? src[w] : 0u; }
     __device__ __forceinline__ uint32_t get(uint32_t n) {  // n <= 16
-        refill();
-        const uint32_t v = peek(n);
-        drop(n);
-        return v;
+        const uint32_t w = pos >> 5, sh = pos & 31u;
+        const uint64_t x = (((uint64_t)word(w + 1) << 32) | word(w)) >> sh;
+        pos += n;
+        return (uint32_t)x & ((1u << n) - 1u);
     }
 };
 
-// Canonical Huffman tables from the code lengths lens[0, n) in LDS (RFC 1951 3.2.2): counts, the symbols sorted by
-// (length, symbol), and the fast table: entry (reversed code + k 2^len) = (symbol << 4) | len for len <= fast_bits.
-// Lane-parallel over the symbols: counts and per-length ranks from ballots (wave-uniform running totals in SGPRs),
-// fast-table replicas written by the lanes.  Returns false on an over-subscribed code (incomplete codes are
-// accepted, as zlib's inflate does).
-__device__ bool build_table(const uint8_t* lens, int n, Table& T, uint16_t* fast, int fast_bits) {
+// Canonical Huffman tables from the code lengths lens[0, n) (RFC 1951 3.2.2): counts, first codes, the symbols sorted
+// by (length, symbol) for codes longer than the fast table, and the fast table of 2^F entries (entry i: the code whose
+// bits, first bit lowest, are a prefix of i).  Ranks come from ballots; the fast table is built by doubling: the table
+// for codes of <= l - 1 bits is copied once to fill 2^l entries, then the l-bit codes are placed.  Returns false on
+// an over-subscribed code (incomplete codes are accepted, as zlib's inflate does).
+__device__ bool build_table(const uint8_t* lens, int n, Table& T, uint16_t* fast, int F) {
     const int lane = threadIdx.x & 63;
     const uint64_t below = (1ull << lane) - 1ull;
-    for (int i = lane; i < (1 << fast_bits); i += 64) fast[i] = 0;
     uint32_t c[16];
 #pragma unroll
     for (int l = 0; l < 16; ++l) c[l] = 0;
@@ -103,20 +111,29 @@ __device__ bool build_table(const uint8_t* lens, int n, Table& T, uint16_t* fast
         off[l] = l == 1 ? 0 : off[l - 1] + c[l - 1];
     }
     if (left < 0) return false;
+    if (lane < 16) {
+        T.cnt[lane] = 0;
+        T.offs[lane] = 0;
+        T.next[lane] = 0;
+    }
+    __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
 #pragma unroll
-        for (int l = 0; l < 16; ++l) {
+        for (int l = 1; l < 16; ++l) {
             T.cnt[l] = (uint16_t)c[l];
             T.offs[l] = (uint16_t)off[l];
             T.next[l] = (uint16_t)nxt[l];
         }
     }
     __builtin_amdgcn_wave_barrier();
+    constexpr int G = 5;  // n <= 320
+    uint32_t gl[G], gr[G], ge[G];
     uint32_t run[16];
 #pragma unroll
     for (int l = 0; l < 16; ++l) run[l] = 0;
-    for (int s0 = 0; s0 < n; s0 += 64) {
-        const int s = s0 + lane;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int s = 64 * g + lane;
         const int l = s < n ? (int)lens[s] : 0;
         uint32_t idx = 0;
 #pragma unroll
@@ -125,40 +142,153 @@ __device__ bool build_table(const uint8_t* lens, int n, Table& T, uint16_t* fast
             if (l == len) idx = run[len] + (uint32_t)__popcll(m & below);
             run[len] += (uint32_t)__popcll(m);
         }
-        if (l) {
+        gl[g] = (uint32_t)l;
+        gr[g] = 0;
+        ge[g] = ((uint32_t)s << 4) | (uint32_t)l;
+        if (l) {  // per-lane length: the LDS copies of off / nxt
             T.sym[T.offs[l] + idx] = (uint16_t)s;
-            if (l <= fast_bits) {
-                const uint32_t cd = (uint32_t)T.next[l] + idx;
-                const uint32_t rev = __builtin_bitreverse32(cd) >> (32 - l);
-                const uint16_t e = (uint16_t)((s << 4) | l);
-                for (uint32_t k = 0; k < (1u << (fast_bits - l)); ++k) fast[rev + (k << l)] = e;
-            }
+            gr[g] = __builtin_bitreverse32((uint32_t)T.next[l] + idx) >> (32 - l);
         }
     }
+    if (lane < 2) fast[lane] = 0;
     __builtin_amdgcn_wave_barrier();
+    for (int l = 1; l <= F; ++l) {
+        if (l > 1) {  // entries [h, 2h) = entries [0, h)
+            const int h = 1 << (l - 1);
+            if (h < 8) {
+                if (lane < h) fast[h + lane] = fast[lane];
+            } else {
+                uint4* f4 = reinterpret_cast<uint4*>(fast);
+                for (int i = lane; i < h / 8; i += 64) f4[h / 8 + i] = f4[i];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+            if (gl[g] == (uint32_t)l) fast[gr[g]] = (uint16_t)ge[g];
+        __builtin_amdgcn_wave_barrier();
+    }
     return true;
 }
 
-// one symbol: the fast table, else canonical decoding bit by bit (RFC 1951 3.2.2; zlib's puff.c decode())
-__device__ __forceinline__ int decode_sym(Bits& br, const uint16_t* fast, int fast_bits, const Table& T) {
-    br.refill();
-    const uint32_t e = uni(fast[br.peek(fast_bits)]);
+// a code longer than the fast table: canonical decoding of lengths F+1..15 from the next 15 bits
+__device__ __forceinline__ bool slow_code(const Table& T, uint32_t bits, int F, uint32_t& len, uint32_t& sym) {
+    const uint32_t rev = __builtin_bitreverse32(bits) >> 17;  // first stream bit as the MSB of 15
+    for (int l = F + 1; l < 16; ++l) {
+        const uint32_t cd = rev >> (15 - l);
+        const uint32_t i = cd - (uint32_t)T.next[l];
+        if (i < (uint32_t)T.cnt[l]) {
+            len = (uint32_t)l;
+            sym = T.sym[T.offs[l] + i];
+            return true;
+        }
+    }
+    return false;
+}
+
+__constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+enum : uint32_t { kLit = 0, kMatch = 1, kFill = 2, kEob = 3, kErr = 4 };
+
+// One token at bit p of the staged chunk (stage[0] = stream word w0): a literal (a = byte), a match (a = length,
+// b = distance), a fill of a zero code lengths (code-length codes 17 / 18) or end of block; nbits = its size.
+// CL: the code-length alphabet (RFC 1951 3.2.7), code 16 = distance-1 match of 3..6.
+template <bool CL>
+__device__ __forceinline__ uint32_t decode_tok(const Lds& S, uint32_t w0, uint32_t p, uint32_t& nbits, uint32_t& a,
+                                               uint32_t& b) {
+    const uint32_t i = (p >> 5) - w0, sh = p & 31u;
+    const uint32_t x0 = S.stage[i], x1 = S.stage[i + 1], x2 = S.stage[i + 2];
+    const uint32_t lo = __builtin_amdgcn_alignbit(x1, x0, sh);
+    const uint32_t hi = __builtin_amdgcn_alignbit(x2, x1, sh);
+    if (CL) {
+        const uint32_t e = S.dist_fast[lo & ((1u << kClBits) - 1u)];
+        if (!e) return kErr;
+        const uint32_t len = e & 15u, sym = e >> 4;
+        if (sym < 16) {
+            a = sym;
+            nbits = len;
+            return kLit;
+        }
+        if (sym == 16) {
+            a = 3 + ((lo >> len) & 3u);
+            b = 1;
+            nbits = len + 2;
+            return kMatch;
+        }
+        const uint32_t xb = sym == 17 ? 3u : 7u;
+        a = (sym == 17 ? 3u : 11u) + ((lo >> len) & ((1u << xb) - 1u));
+        nbits = len + xb;
+        return kFill;
+    }
+    uint32_t e = S.lit_fast[lo & ((1u << kLitBits) - 1u)], len, sym;
     if (e) {
-        br.drop(e & 15u);
-        return (int)(e >> 4);
+        len = e & 15u;
+        sym = e >> 4;
+    } else if (!slow_code(S.lit, lo, kLitBits, len, sym)) {
+        return kErr;
     }
-    int code = 0, first = 0, index = 0;
-    for (int len = 1; len < 16; ++len) {
-        code |= (int)(br.bb & 1u);
-        br.drop(1);
-        const int count = (int)uni(T.cnt[len]);
-        if (code - count < first) return (int)uni(T.sym[index + (code - first)]);
-        index += count;
-        first += count;
-        first <<= 1;
-        code <<= 1;
+    if (sym < 256) {
+        a = sym;
+        nbits = len;
+        return kLit;
     }
-    return -1;
+    if (sym == 256) {
+        nbits = len;
+        return kEob;
+    }
+    const uint32_t li = sym - 257;
+    if (li >= 29) return kErr;
+    // length base / extra bits (RFC 1951 3.2.5) from the symbol: 3..10 plain, then 4 per extra-bit count, 258
+    uint32_t le = 0, lb = li + 3;
+    if (li == 28) {
+        lb = 258;
+    } else if (li >= 8) {
+        le = (li >> 2) - 1;
+        lb = ((4u | (li & 3u)) << le) + 3;
+    }
+    a = lb + ((lo >> len) & ((1u << le) - 1u));
+    const uint32_t q = len + le;  // <= 20
+    const uint32_t dv = (uint32_t)((((uint64_t)hi << 32) | lo) >> q);
+    uint32_t e2 = S.dist_fast[dv & ((1u << kDistBits) - 1u)], dl, ds;
+    if (e2) {
+        dl = e2 & 15u;
+        ds = e2 >> 4;
+    } else if (!slow_code(S.dist, dv, kDistBits, dl, ds)) {
+        return kErr;
+    }
+    if (ds >= 30) return kErr;
+    uint32_t de = 0, db = ds + 1;
+    if (ds >= 4) {
+        de = (ds >> 1) - 1;
+        db = ((2u | (ds & 1u)) << de) + 1;
+    }
+    b = db + ((dv >> dl) & ((1u << de) - 1u));  // dl + de <= 28
+    nbits = q + dl + de;                        // <= 48
+    return kMatch;
+}
+
+// tokens from p while p < to: output bytes, matches, stop (1 end of block, 2 invalid code)
+template <bool CL>
+__device__ __forceinline__ void count_pass(const Lds& S, uint32_t w0, uint32_t& p, uint32_t to, uint32_t& cnt,
+                                           uint32_t& nmt, uint32_t& stop) {
+    cnt = 0;
+    nmt = 0;
+    stop = 0;
+    while (p < to) {
+        uint32_t nb = 0, a = 0, b = 0;
+        const uint32_t k = decode_tok<CL>(S, w0, p, nb, a, b);
+        if (k == kErr) {
+            stop = 2;
+            break;
+        }
+        p += nb;
+        if (k == kEob) {
+            stop = 1;
+            break;
+        }
+        cnt += k == kLit ? 1u : a;
+        nmt += k == kMatch ? 1u : 0u;
+    }
 }
 
 // ring bytes [from, to) of the output to HBM (from a multiple of 16)
@@ -174,16 +304,161 @@ __device__ void flush(const Lds& S, uint8_t* out, uint32_t from, uint32_t to) {
     }
 }
 
-__constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                      31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
-                                      2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t kDistBase[30] = {1,    2,    3,    4,    5,    7,     9,     13,    17,  25,
-                                       33,   49,   65,   97,   129,  193,   257,   385,   513, 769,
-                                       1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
-                                       6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
-__constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+__device__ __forceinline__ uint32_t lens_slot(uint32_t k, uint32_t hlit) { return k < hlit ? k : 288 + (k - hlit); }
+
+// One chunk of the lane-parallel decoder from the true token boundary P0 (see the file comment).
+// DATA (CL false): output position op, the ring, matches against the window; `done` at the end-of-block token.
+// CL: code lengths k = op of need in total into S.lens; `done` when all are read.
+// Advances P0 / op, adapts seg; returns kPngOk or an error.
+template <bool CL>
+__device__ int run_chunk(Lds& S, const uint32_t* __restrict__ src, uint32_t nwords, uint32_t& P0, uint32_t& op,
+                         uint32_t& seg, uint32_t need, uint32_t hlit, uint8_t* __restrict__ dst, uint32_t& flushed,
+                         uint32_t out_len, bool& done) {
+    const int lane = threadIdx.x & 63;
+    done = false;
+    if (P0 > nwords * 32u + 64u) return kPngErrShort;
+    // stage the chunk's words
+    const uint32_t w0 = P0 >> 5;
+    const uint32_t nst = 2 * seg + 4;
+    for (uint32_t i = lane; i < nst; i += 64) S.stage[i] = w0 + i < nwords ? src[w0 + i] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t Sk = P0 + (uint32_t)lane * seg, Sn = Sk + seg;
+    // lead-in: synchronise before the segment (lane 0 starts on the true boundary)
+    uint32_t p = Sk >= P0 + kLead ? Sk - kLead : P0;
+    if (lane == 0) p = P0;
+    while (p < Sk) {
+        uint32_t nb = 0, a = 0, b = 0;
+        const uint32_t k = decode_tok<CL>(S, w0, p, nb, a, b);
+        p += k == kErr ? 1u : nb;
+    }
+    uint32_t start = p, cnt, nmt, stop;
+    count_pass<CL>(S, w0, p, Sn, cnt, nmt, stop);
+    uint32_t E = p;
+    const uint32_t cap = CL ? 0xFFFFFFFFu : kCap;
+    int m = 0;
+    uint32_t incl_c = 0, incl_m = 0;
+    bool capped = false;
+    for (int round = 0;; ++round) {
+        incl_c = wave_incl_scan(cnt);
+        incl_m = wave_incl_scan(nmt);
+        uint64_t endm = __ballot(stop != 0);
+        if (CL) endm |= __ballot(incl_c >= need);
+        m = endm ? (int)__builtin_ctzll(endm) : 63;
+        const uint64_t capm = __ballot(incl_c > cap || incl_m > (uint32_t)kMaxMatch);
+        capped = false;
+        if (capm) {
+            const int mc = (int)__builtin_ctzll(capm) - 1;
+            if (mc < m) {
+                m = mc;
+                capped = true;
+            }
+        }
+        const uint32_t prevE = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)E, 0x138, 0xf, 0xf, false);  // wave_shr:1
+        const bool bad = lane >= 1 && lane <= m && start != prevE;
+        if (!__ballot(bad)) break;
+        if (round >= 64) return kPngErrCode;  // cannot happen: every round fixes at least one more lane
+        if (bad) {
+            start = prevE;
+            p = start;
+            count_pass<CL>(S, w0, p, Sn, cnt, nmt, stop);
+            E = p;
+        }
+    }
+    if (m < 0) {  // lane 0's segment alone overflows the ring: smaller segments (at kSegMin it cannot)
+        seg = seg > 4 * kSegMin ? seg >> 2 : kSegMin;
+        return kPngOk;
+    }
+    const uint32_t stop_m = lane_of(stop, m);
+    if (!CL && stop_m == 2) return kPngErrCode;
+    if (CL && stop_m != 0 && lane_of(incl_c, m) < need) return kPngErrCode;
+    if (!CL && op + lane_of(incl_c, m) > out_len) return kPngErrOverrun;
+    // write pass: literals into place, matches listed in stream order
+    uint32_t o = 0, mi = incl_m - nmt, werr = 0;
+    const uint32_t o_end = op + need;  // CL only
+    if (lane <= m) {
+        o = op + (incl_c - cnt);
+        p = start;
+        while (p < Sn) {
+            if (CL && o >= o_end) break;
+            uint32_t nb = 0, a = 0, b = 0;
+            const uint32_t k = decode_tok<CL>(S, w0, p, nb, a, b);
+            if (k == kErr) break;
+            p += nb;
+            if (k == kEob) break;
+            if (k == kLit) {
+                if (CL) S.lens[lens_slot(o, hlit)] = (uint8_t)a;
+                else S.ring[o & kRingMask] = (uint8_t)a;
+                ++o;
+            } else if (k == kMatch) {
+                S.mdst[mi] = o;
+                S.mld[mi] = (a << 16) | b;
+                ++mi;
+                o += a;
+            } else {
+                for (uint32_t j = 0; j < a; ++j)
+                    if (o + j < o_end) S.lens[lens_slot(o + j, hlit)] = 0;
+                o += a;
+            }
+        }
+        if (CL && o > o_end) werr = 1;
+    }
+    if (__ballot(werr != 0)) return kPngErrCode;
+    const uint32_t P1 = lane_of(p, m), op1 = lane_of(o, m), nm = lane_of(mi, m);
+    __builtin_amdgcn_wave_barrier();
+    // matches, in stream order
+    const uint32_t ring_lo = op1 > (uint32_t)kRing ? op1 - kRing : 0u;  // older output is in HBM only
+    bool fenced = false;
+    for (uint32_t i = 0; i < nm; ++i) {
+        const uint32_t d = uni(S.mdst[i]), ld = uni(S.mld[i]);
+        const uint32_t L = ld >> 16, D = ld & 0xFFFFu;
+        if (D > d) return kPngErrCode;
+        if (CL) {
+            const uint32_t v = S.lens[lens_slot(d - 1, hlit)];
+            for (uint32_t j = lane; j < L; j += 64) S.lens[lens_slot(d + j, hlit)] = (uint8_t)v;
+            __builtin_amdgcn_wave_barrier();
+            continue;
+        }
+        const bool far = d - D < ring_lo;
+        if (far && !fenced) {  // the output flushed so far must be visible to the loads below
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            fenced = true;
+        }
+        for (uint32_t j0 = 0; j0 < L; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            uint32_t v = 0;
+            if (j < L) {
+                const uint32_t s = d - D + (D == 1 ? 0u : j % D);
+                if (s >= ring_lo) {
+                    v = S.ring[s & kRingMask];
+                } else {
+                    uint32_t* wp = reinterpret_cast<uint32_t*>(dst + (s & ~3u));
+                    v = (__hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (8 * (s & 3u))) & 0xFFu;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (j < L) S.ring[(d + j) & kRingMask] = (uint8_t)v;
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    const uint32_t op0 = op;
+    P0 = P1;
+    if (CL) {
+        op = op1;
+        done = op1 >= o_end;
+        return kPngOk;
+    }
+    // stream the completed 16-byte groups
+    const uint32_t to = op1 & ~15u;
+    __builtin_amdgcn_wave_barrier();
+    flush(S, dst, flushed, to);
+    flushed = to;
+    __builtin_amdgcn_wave_barrier();
+    op = op1;
+    done = stop_m == 1;
+    if (capped) seg = seg > 2 * kSegMin ? seg >> 1 : kSegMin;
+    else if (m == 63 && op1 - op0 < kCap / 4 && seg < kSegMax) seg <<= 1;
+    return kPngOk;
+}
 
 // image i: zlib stream at src + off[i] (4-B aligned), len[i] bytes -> out_len bytes at out + i * out_pitch
 __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__ src, const int64_t* __restrict__ off,
@@ -197,12 +472,10 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__
     Bits br;
     br.src = reinterpret_cast<const uint32_t*>(src + off[img]);
     br.nwords = (uint32_t)(len[img] + 3) / 4;
-    br.wp = 0;
-    br.bb = 0;
-    br.nb = 0;
-    br.over = 0;
+    br.pos = 0;
+    const uint32_t nbytes = (uint32_t)len[img];
     int32_t st = kPngOk;
-    uint32_t op = 0, flushed = 0;
+    uint32_t op = 0, flushed = 0, seg = kSegMax;
     // zlib header (RFC 1950): CM 8, CINFO <= 7, no preset dictionary, FCHECK
     {
         const uint32_t cmf = br.get(8), flg = br.get(8);
@@ -210,35 +483,36 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__
     }
     bool last = false;
     while (st == kPngOk && !last) {
-        if (br.over > 2) {  // a damaged stream decoding zeros past its end: every block then fails or ends, but stop
+        if (br.pos > br.nwords * 32u) {
             st = kPngErrShort;
             break;
         }
         last = br.get(1) != 0;
         const uint32_t type = br.get(2);
         if (type == 0) {
-            // stored block: byte-align, LEN, NLEN, LEN raw bytes
-            br.drop(br.nb & 7u);
+            // stored block: byte-align, LEN, NLEN, LEN raw bytes (copied by the lanes through the ring)
+            br.pos = (br.pos + 7u) & ~7u;
             const uint32_t n = br.get(16), nn = br.get(16);
             if ((n ^ 0xFFFFu) != nn) {
                 st = kPngErrBlock;
                 break;
             }
-            if (op + n > out_len) {
-                st = kPngErrOverrun;
+            if (op + n > out_len || (br.pos >> 3) + n > nbytes) {
+                st = op + n > out_len ? kPngErrOverrun : kPngErrShort;
                 break;
             }
-            for (uint32_t k = 0; k < n; ++k) {
-                const uint32_t v = br.get(8);
-                if (lane == 0) S.ring[(op + k) & kRingMask] = (uint8_t)v;
+            const uint8_t* sb = src + off[img] + (br.pos >> 3);
+            for (uint32_t k0 = 0; k0 < n; k0 += 4096) {
+                const uint32_t piece = min(4096u, n - k0);
+                for (uint32_t k = lane; k < piece; k += 64) S.ring[(op + k) & kRingMask] = sb[k0 + k];
+                op += piece;
+                const uint32_t to = op & ~15u;
                 __builtin_amdgcn_wave_barrier();
-                if (((op + k + 1) & (kFlush - 1)) == 0) {
-                    flush(S, dst, flushed, op + k + 1);
-                    flushed = op + k + 1;
-                    __builtin_amdgcn_wave_barrier();
-                }
+                flush(S, dst, flushed, to);
+                flushed = to;
+                __builtin_amdgcn_wave_barrier();
             }
-            op += n;
+            br.pos += 8u * n;
             continue;
         }
         if (type == 3) {
@@ -257,54 +531,34 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__
             }
             if (lane < 20) S.cl[lane] = 0;
             __builtin_amdgcn_wave_barrier();
-            for (uint32_t k = 0; k < hclen; ++k) {
-                const uint32_t v = br.get(3);
-                if (lane == 0) S.cl[kClOrder[k]] = (uint8_t)v;
+            {
+                // hclen 3-bit lengths in the order 16 17 18 0 8 7 9 6 10 5 11 4 12 3 13 2 14 1 15: lane k takes the k-th
+                const uint32_t pos0 = br.pos;
+                if ((uint32_t)lane < hclen) {
+                    const uint32_t q = pos0 + 3u * lane, w = q >> 5, sh = q & 31u;
+                    const uint64_t x = (((uint64_t)br.word(w + 1) << 32) | br.word(w)) >> sh;
+                    S.cl[kClOrder[lane]] = (uint8_t)(x & 7u);
+                }
+                br.pos = pos0 + 3u * hclen;
             }
             __builtin_amdgcn_wave_barrier();
             // the code-length code: its table in dist_fast / dist (7-bit codes)
-            if (!build_table(S.cl, 19, S.dist, S.dist_fast, kDistBits)) {
+            if (!build_table(S.cl, 19, S.dist, S.dist_fast, kClBits)) {
                 st = kPngErrCode;
                 break;
             }
             // hlit + hdist code lengths, litlen into lens[0, hlit), distance into lens[288, 288 + hdist)
             for (int s = lane; s < 320; s += 64) S.lens[s] = 0;
             __builtin_amdgcn_wave_barrier();
-            uint32_t k = 0, prevlen = 0;
+            uint32_t k = 0, P = br.pos, cseg = kSegMin;
             const uint32_t total = hlit + hdist;
-            while (k < total) {
-                const int sym = decode_sym(br, S.dist_fast, kDistBits, S.dist);
-                uint32_t rep = 1, val = (uint32_t)sym;
-                if (sym < 0 || sym > 18) {
-                    st = kPngErrCode;
-                    break;
-                }
-                if (sym == 16) {
-                    if (k == 0) {
-                        st = kPngErrCode;
-                        break;
-                    }
-                    val = prevlen;
-                    rep = 3 + br.get(2);
-                } else if (sym == 17) {
-                    val = 0;
-                    rep = 3 + br.get(3);
-                } else if (sym == 18) {
-                    val = 0;
-                    rep = 11 + br.get(7);
-                }
-                if (k + rep > total) {
-                    st = kPngErrCode;
-                    break;
-                }
-                for (uint32_t q = lane; q < rep; q += 64) {
-                    const uint32_t idx = k + q;
-                    S.lens[idx < hlit ? idx : 288 + (idx - hlit)] = (uint8_t)val;
-                }
-                prevlen = val;
-                k += rep;
+            bool done = false;
+            while (!done) {
+                st = run_chunk<true>(S, br.src, br.nwords, P, k, cseg, total - k, hlit, dst, flushed, out_len, done);
+                if (st != kPngOk) break;
             }
             if (st != kPngOk) break;
+            br.pos = P;
             __builtin_amdgcn_wave_barrier();
             if (uni(S.lens[256]) == 0) {  // no end-of-block code
                 st = kPngErrCode;
@@ -316,57 +570,17 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__
             st = kPngErrCode;
             break;
         }
-        // the block's symbols
-        while (true) {
-            const int sym = decode_sym(br, S.lit_fast, kLitBits, S.lit);
-            if (sym < 256) {
-                if (sym < 0 || op >= out_len) {
-                    st = sym < 0 ? kPngErrCode : kPngErrOverrun;
-                    break;
-                }
-                if (lane == 0) S.ring[op & kRingMask] = (uint8_t)sym;
-                ++op;
-            } else if (sym == 256) {
-                break;
-            } else {
-                const int li = sym - 257;
-                if (li >= 29) {
-                    st = kPngErrCode;
-                    break;
-                }
-                const uint32_t L = kLenBase[li] + br.get(kLenExtra[li]);
-                const int ds = decode_sym(br, S.dist_fast, kDistBits, S.dist);
-                if (ds < 0 || ds >= 30) {
-                    st = kPngErrCode;
-                    break;
-                }
-                const uint32_t D = kDistBase[ds] + br.get(kDistExtra[ds]);
-                if (D > op || op + L > out_len) {
-                    st = D > op ? kPngErrCode : kPngErrOverrun;
-                    break;
-                }
-                // byte j of the match = window byte op - D + (j mod D); 64 bytes per pass, every read before the writes
-                __builtin_amdgcn_wave_barrier();
-                for (uint32_t j0 = 0; j0 < L; j0 += 64) {
-                    const uint32_t j = j0 + lane;
-                    uint32_t v = 0;
-                    if (j < L) v = S.ring[(op - D + (j % D)) & kRingMask];
-                    __builtin_amdgcn_wave_barrier();
-                    if (j < L) S.ring[(op + j) & kRingMask] = (uint8_t)v;
-                    __builtin_amdgcn_wave_barrier();
-                }
-                op += L;
-            }
-            if ((op & ~(uint32_t)(kFlush - 1)) != flushed) {
-                const uint32_t to = op & ~(uint32_t)(kFlush - 1);
-                __builtin_amdgcn_wave_barrier();
-                flush(S, dst, flushed, to);
-                flushed = to;
-                __builtin_amdgcn_wave_barrier();
-            }
+        // the block's tokens
+        uint32_t P = br.pos;
+        bool done = false;
+        while (!done) {
+            st = run_chunk<false>(S, br.src, br.nwords, P, op, seg, 0xFFFFFFFFu, 0, dst, flushed, out_len, done);
+            if (st != kPngOk) break;
         }
+        if (st != kPngOk) break;
+        br.pos = P;
     }
-    if (st == kPngOk && br.over > 1) st = kPngErrShort;  // decoding ran past the stream (beyond the look-ahead word)
+    if (st == kPngOk && br.pos > br.nwords * 32u) st = kPngErrShort;  // decoding ran past the stream
     if (st == kPngOk && op != out_len) st = kPngErrShort;
     __builtin_amdgcn_wave_barrier();
     if (st == kPngOk) flush(S, dst, flushed, op);
