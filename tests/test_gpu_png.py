@@ -112,6 +112,20 @@ def test_gpu_png_odd_sizes_fixed_huffman(ctx, H, W):
     np.testing.assert_array_equal(out[1], imgs[1])
 
 
+@pytest.mark.parametrize("H,W", [(9, 1241), (5, 3000), (4, 4100)])
+def test_gpu_png_rowwise_and_wavefront_unfilter(ctx, H, W):
+    """None / Sub / Up rows take the row-wise unfilter (64 lanes per row, up to W = 4096); any Average or Paeth row sends
+    the image to the wavefront; wider images always take the wavefront."""
+    rng = np.random.default_rng(W)
+    img = rng.integers(0, 256, (H, W), dtype=np.uint8)
+    img[:, W // 3:] = np.cumsum(img[:, W // 3:] & 3, axis=1, dtype=np.uint8)  # some compressible runs
+    files = [_png(img, 1, 1, zlib.Z_RLE), _png(img, [2, 1, 0], 6), _png(img, [1, 2, 3], 6), _png(img, [2, 4], 6)]
+    out, codes, bad = _decode_gpu(ctx, files, H, W)
+    assert bad == 0, codes
+    for o in out:
+        np.testing.assert_array_equal(o, img)
+
+
 def test_gpu_png_reports_corrupt_stream(ctx):
     H, W = 40, 50
     img = np.random.default_rng(1).integers(0, 256, (H, W), dtype=np.uint8)

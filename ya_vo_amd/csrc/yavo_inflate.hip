@@ -28,20 +28,24 @@
 namespace yavo {
 namespace png {
 
-constexpr int kRing = 16384;  // LDS output ring
+// LDS per wave <= 20 KB: eight waves (two per SIMD) hide each other's LDS latency
+constexpr int kRing = 8192;  // LDS output ring
 constexpr uint32_t kRingMask = kRing - 1;
-constexpr int kLitBits = 12, kDistBits = 9, kClBits = 7;  // fast-table index widths
-constexpr uint32_t kSegMax = 1024, kSegMin = 64;         // bits per lane per chunk
+constexpr int kLitBits = 11, kDistBits = 8, kClBits = 7;  // fast-table index widths
+constexpr uint32_t kSegMax = 512, kSegMin = 32;          // bits per lane per chunk
 constexpr uint32_t kLead = 256;                          // synchronisation lead-in, bits
 constexpr int kStageWords = 2 * kSegMax + 8;             // the chunk's stream words (+ look-ahead)
-constexpr int kMaxMatch = 512;                           // matches listed per chunk
+constexpr int kMaxMatch = 256;                           // matches listed per chunk
 constexpr uint32_t kCap = kRing - 64;                    // output bytes per chunk (the ring keeps the unflushed tail)
+// kSegMin: lane 0's segment alone always fits (<= 16 tokens start in 32 bits, <= 258 bytes each)
+static_assert(16 * 258 <= (int)kCap && 16 <= kMaxMatch, "minimum segment");
 
+template <int NS>
 struct Table {
-    uint16_t cnt[16];   // codes per length
+    uint16_t cnt[16];  // codes per length
     uint16_t offs[16];  // first index of each length in sym
     uint16_t next[16];  // first canonical code of each length
-    uint16_t sym[288];  // symbols ordered by (length, symbol)
+    uint16_t sym[NS];   // symbols ordered by (length, symbol)
 };
 
 struct Lds {
@@ -51,11 +55,12 @@ struct Lds {
     alignas(16) uint16_t dist_fast[1 << kDistBits];  // distance codes; the code-length code while lengths are read
     uint32_t mdst[kMaxMatch];                        // the chunk's matches: output position,
     uint32_t mld[kMaxMatch];                         // (length << 16) | distance
-    Table lit, dist;
+    Table<288> lit;
+    Table<32> dist;  // distance codes (30) or the code-length code (19)
     uint8_t lens[320];  // code lengths: litlen [0, 288), distance [288, 320)
     uint8_t cl[20];
 };
-static_assert(sizeof(Lds) <= 40 * 1024, "four waves per CU");
+static_assert(sizeof(Lds) <= 20 * 1024, "eight waves per CU");
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint32_t lane_of(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -89,7 +94,8 @@ struct Bits {
 // bits, first bit lowest, are a prefix of i).  Ranks come from ballots; the fast table is built by doubling: the table
 // for codes of <= l - 1 bits is copied once to fill 2^l entries, then the l-bit codes are placed.  Returns false on
 // an over-subscribed code (incomplete codes are accepted, as zlib's inflate does).
-__device__ bool build_table(const uint8_t* lens, int n, Table& T, uint16_t* fast, int F) {
+template <int NS>
+__device__ bool build_table(const uint8_t* lens, int n, Table<NS>& T, uint16_t* fast, int F) {
     const int lane = threadIdx.x & 63;
     const uint64_t below = (1ull << lane) - 1ull;
     uint32_t c[16];
@@ -172,7 +178,8 @@ __device__ bool build_table(const uint8_t* lens, int n, Table& T, uint16_t* fast
 }
 
 // a code longer than the fast table: canonical decoding of lengths F+1..15 from the next 15 bits
-__device__ __forceinline__ bool slow_code(const Table& T, uint32_t bits, int F, uint32_t& len, uint32_t& sym) {
+template <int NS>
+__device__ __forceinline__ bool slow_code(const Table<NS>& T, uint32_t bits, int F, uint32_t& len, uint32_t& sym) {
     const uint32_t rev = __builtin_bitreverse32(bits) >> 17;  // first stream bit as the MSB of 15
     for (int l = F + 1; l < 16; ++l) {
         const uint32_t cd = rev >> (15 - l);
@@ -291,6 +298,79 @@ __device__ __forceinline__ void count_pass(const Lds& S, uint32_t w0, uint32_t& 
     }
 }
 
+// DATA tokens through a per-lane 64-bit bit buffer over the staged words: a literal with a fast code costs one LDS
+// lookup (the next stream word is read ahead every step); anything else (matches, long codes, end of block) goes
+// through decode_tok at the buffer's position and re-seeks.
+struct Dec {
+    uint32_t p;      // stream bit of bb's bit 0
+    uint64_t bb;     // stream bits [p, p + avail)
+    uint32_t avail;  // > 32 after the refill at the top of a step
+    uint32_t wi;     // stage index of wn
+    uint32_t wn;     // stage[wi]
+};
+
+__device__ __forceinline__ void dec_seek(const Lds& S, uint32_t w0, Dec& d, uint32_t p) {
+    const uint32_t i = (p >> 5) - w0, sh = p & 31u;
+    const uint32_t x0 = S.stage[i], x1 = S.stage[i + 1];
+    d.p = p;
+    d.bb = (((uint64_t)x1 << 32) | x0) >> sh;
+    d.avail = 64u - sh;
+    d.wi = i + 2;
+    d.wn = S.stage[i + 2];
+}
+
+__device__ __forceinline__ uint32_t data_step(const Lds& S, uint32_t w0, Dec& d, uint32_t& a, uint32_t& b) {
+    const bool need = d.avail <= 32u;
+    d.bb |= need ? ((uint64_t)d.wn << d.avail) : 0ull;
+    d.avail += need ? 32u : 0u;
+    d.wi += need ? 1u : 0u;
+    d.wn = S.stage[d.wi];
+    const uint32_t e = S.lit_fast[(uint32_t)d.bb & ((1u << kLitBits) - 1u)];
+    if (e - 1u < (256u << 4) - 1u) {  // 0 < e < 256 << 4: a literal with a fast code
+        const uint32_t n = e & 15u;
+        a = e >> 4;
+        d.bb >>= n;
+        d.avail -= n;
+        d.p += n;
+        return kLit;
+    }
+    uint32_t nb = 0;
+    const uint32_t k = decode_tok<false>(S, w0, d.p, nb, a, b);
+    if (k != kErr) dec_seek(S, w0, d, d.p + nb);
+    return k;
+}
+
+__device__ __forceinline__ void count_pass_data(const Lds& S, uint32_t w0, uint32_t& p, uint32_t to, uint32_t& cnt,
+                                                uint32_t& nmt, uint32_t& stop) {
+    cnt = 0;
+    nmt = 0;
+    stop = 0;
+    Dec d;
+    dec_seek(S, w0, d, p);
+    while (d.p < to) {
+        uint32_t a = 0, b = 0;
+        const uint32_t k = data_step(S, w0, d, a, b);
+        if (k == kErr) {
+            stop = 2;
+            break;
+        }
+        if (k == kEob) {
+            stop = 1;
+            break;
+        }
+        cnt += k == kLit ? 1u : a;
+        nmt += k == kMatch ? 1u : 0u;
+    }
+    p = d.p;
+}
+
+template <bool CL>
+__device__ __forceinline__ void count_any(const Lds& S, uint32_t w0, uint32_t& p, uint32_t to, uint32_t& cnt,
+                                         uint32_t& nmt, uint32_t& stop) {
+    if (CL) count_pass<true>(S, w0, p, to, cnt, nmt, stop);
+    else count_pass_data(S, w0, p, to, cnt, nmt, stop);
+}
+
 // ring bytes [from, to) of the output to HBM (from a multiple of 16)
 __device__ void flush(const Lds& S, uint8_t* out, uint32_t from, uint32_t to) {
     const int lane = threadIdx.x & 63;
@@ -319,20 +399,30 @@ __device__ int run_chunk(Lds& S, const uint32_t* __restrict__ src, uint32_t nwor
     if (P0 > nwords * 32u + 64u) return kPngErrShort;
     // stage the chunk's words
     const uint32_t w0 = P0 >> 5;
-    const uint32_t nst = 2 * seg + 4;
+    const uint32_t nst = 2 * seg + 6;
     for (uint32_t i = lane; i < nst; i += 64) S.stage[i] = w0 + i < nwords ? src[w0 + i] : 0u;
     __builtin_amdgcn_wave_barrier();
     const uint32_t Sk = P0 + (uint32_t)lane * seg, Sn = Sk + seg;
     // lead-in: synchronise before the segment (lane 0 starts on the true boundary)
     uint32_t p = Sk >= P0 + kLead ? Sk - kLead : P0;
     if (lane == 0) p = P0;
-    while (p < Sk) {
-        uint32_t nb = 0, a = 0, b = 0;
-        const uint32_t k = decode_tok<CL>(S, w0, p, nb, a, b);
-        p += k == kErr ? 1u : nb;
+    if (CL) {
+        while (p < Sk) {
+            uint32_t nb = 0, a = 0, b = 0;
+            const uint32_t k = decode_tok<true>(S, w0, p, nb, a, b);
+            p += k == kErr ? 1u : nb;
+        }
+    } else if (p < Sk) {
+        Dec d;
+        dec_seek(S, w0, d, p);
+        while (d.p < Sk) {
+            uint32_t a = 0, b = 0;
+            if (data_step(S, w0, d, a, b) == kErr) dec_seek(S, w0, d, d.p + 1);
+        }
+        p = d.p;
     }
     uint32_t start = p, cnt, nmt, stop;
-    count_pass<CL>(S, w0, p, Sn, cnt, nmt, stop);
+    count_any<CL>(S, w0, p, Sn, cnt, nmt, stop);
     uint32_t E = p;
     const uint32_t cap = CL ? 0xFFFFFFFFu : kCap;
     int m = 0;
@@ -360,12 +450,12 @@ __device__ int run_chunk(Lds& S, const uint32_t* __restrict__ src, uint32_t nwor
         if (bad) {
             start = prevE;
             p = start;
-            count_pass<CL>(S, w0, p, Sn, cnt, nmt, stop);
+            count_any<CL>(S, w0, p, Sn, cnt, nmt, stop);
             E = p;
         }
     }
     if (m < 0) {  // lane 0's segment alone overflows the ring: smaller segments (at kSegMin it cannot)
-        seg = seg > 4 * kSegMin ? seg >> 2 : kSegMin;
+        seg = seg >= 4 * kSegMin ? seg >> 2 : kSegMin;
         return kPngOk;
     }
     const uint32_t stop_m = lane_of(stop, m);
@@ -378,29 +468,47 @@ __device__ int run_chunk(Lds& S, const uint32_t* __restrict__ src, uint32_t nwor
     if (lane <= m) {
         o = op + (incl_c - cnt);
         p = start;
-        while (p < Sn) {
-            if (CL && o >= o_end) break;
-            uint32_t nb = 0, a = 0, b = 0;
-            const uint32_t k = decode_tok<CL>(S, w0, p, nb, a, b);
-            if (k == kErr) break;
-            p += nb;
-            if (k == kEob) break;
-            if (k == kLit) {
-                if (CL) S.lens[lens_slot(o, hlit)] = (uint8_t)a;
-                else S.ring[o & kRingMask] = (uint8_t)a;
-                ++o;
-            } else if (k == kMatch) {
-                S.mdst[mi] = o;
-                S.mld[mi] = (a << 16) | b;
-                ++mi;
-                o += a;
-            } else {
-                for (uint32_t j = 0; j < a; ++j)
-                    if (o + j < o_end) S.lens[lens_slot(o + j, hlit)] = 0;
-                o += a;
+        if (CL) {
+            while (p < Sn) {
+                if (o >= o_end) break;
+                uint32_t nb = 0, a = 0, b = 0;
+                const uint32_t k = decode_tok<true>(S, w0, p, nb, a, b);
+                if (k == kErr) break;
+                p += nb;
+                if (k == kLit) {
+                    S.lens[lens_slot(o, hlit)] = (uint8_t)a;
+                    ++o;
+                } else if (k == kMatch) {
+                    S.mdst[mi] = o;
+                    S.mld[mi] = (a << 16) | b;
+                    ++mi;
+                    o += a;
+                } else {
+                    for (uint32_t j = 0; j < a; ++j)
+                        if (o + j < o_end) S.lens[lens_slot(o + j, hlit)] = 0;
+                    o += a;
+                }
             }
+            if (o > o_end) werr = 1;
+        } else {
+            Dec d;
+            dec_seek(S, w0, d, p);
+            while (d.p < Sn) {
+                uint32_t a = 0, b = 0;
+                const uint32_t k = data_step(S, w0, d, a, b);
+                if (k == kErr || k == kEob) break;
+                if (k == kLit) {
+                    S.ring[o & kRingMask] = (uint8_t)a;
+                    ++o;
+                } else {
+                    S.mdst[mi] = o;
+                    S.mld[mi] = (a << 16) | b;
+                    ++mi;
+                    o += a;
+                }
+            }
+            p = d.p;
         }
-        if (CL && o > o_end) werr = 1;
     }
     if (__ballot(werr != 0)) return kPngErrCode;
     const uint32_t P1 = lane_of(p, m), op1 = lane_of(o, m), nm = lane_of(mi, m);
@@ -455,7 +563,7 @@ __device__ int run_chunk(Lds& S, const uint32_t* __restrict__ src, uint32_t nwor
     __builtin_amdgcn_wave_barrier();
     op = op1;
     done = stop_m == 1;
-    if (capped) seg = seg > 2 * kSegMin ? seg >> 1 : kSegMin;
+    if (capped) seg = seg >= 2 * kSegMin ? seg >> 1 : kSegMin;
     else if (m == 63 && op1 - op0 < kCap / 4 && seg < kSegMax) seg <<= 1;
     return kPngOk;
 }
@@ -589,16 +697,10 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__
 
 __device__ __forceinline__ uint32_t byte_of(uint32_t v, int k) { return (v >> (8 * k)) & 0xFFu; }
 
-// PNG scanline filters (filter method 0) of 8-bit grey rows: raw rows of 1 + W bytes (filter type first) -> rows of W
-// bytes at dst + i * dst_pitch with row stride dst_stride.  Wavefront over rows (see the file comment).
-__global__ __launch_bounds__(64) void unfilter_kernel(const uint8_t* __restrict__ raw, int64_t raw_pitch, int H, int W,
-                                                      uint8_t* __restrict__ dst, int64_t dst_pitch, int dst_stride,
-                                                      int32_t* __restrict__ status) {
-    const int img = blockIdx.x;
+// Any filter types: a wavefront over rows (see the file comment), one 4-byte group per lane per step.
+__device__ void unfilter_wavefront(const uint8_t* __restrict__ rimg, int H, int W, uint8_t* __restrict__ dimg,
+                                   int dst_stride, int32_t* __restrict__ st) {
     const int lane = threadIdx.x & 63;
-    if (status[img] != kPngOk) return;  // wave-uniform
-    const uint8_t* rimg = raw + (int64_t)img * raw_pitch;
-    uint8_t* dimg = dst + (int64_t)img * dst_pitch;
     const int G = (W + 3) >> 2;  // 4-byte groups per row
     int bad = 0;
     for (int r0 = 0; r0 < H; r0 += 64) {
@@ -653,9 +755,111 @@ __global__ __launch_bounds__(64) void unfilter_kernel(const uint8_t* __restrict_
         }
     }
     const uint64_t any_bad = __ballot(bad != 0);
-    if (lane == 0 && any_bad) status[img] = kPngErrFilter;
+    if (lane == 0 && any_bad) *st = kPngErrFilter;
 }
 
+
+// bytewise a + b mod 256 in each of the four bytes
+__device__ __forceinline__ uint32_t add8(uint32_t a, uint32_t b) {
+    return ((a & 0x7F7F7F7Fu) + (b & 0x7F7F7F7Fu)) ^ ((a ^ b) & 0x80808080u);
+}
+
+// Rows filtered None / Sub / Up only (cv::imwrite writes Sub rows): no dependency between bytes beyond a running sum, so
+// the 64 lanes share each row, lane l owning its bytes [4 NW l, 4 NW (l + 1)).  Sub = a prefix sum mod 256 along the
+// row: within the lane's dwords by shifted bytewise adds, across lanes by a wave scan of the lanes' sums.  Up adds the
+// row above, which the same lane made one row earlier.  Rows stream through registers PF rows ahead of their use.
+template <int NW>
+__device__ void unfilter_rowwise(const uint8_t* __restrict__ rimg, int H, int W, uint8_t* __restrict__ dimg,
+                                 int dst_stride) {
+    constexpr int PF = 4;
+    const int lane = threadIdx.x & 63;
+    const int b0 = 4 * NW * lane;
+    const int nb = min(max(W - b0, 0), 4 * NW);
+    uint32_t buf[PF][NW], fb[PF], prev[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) prev[i] = 0;
+    auto load = [&](int r, uint32_t* x, uint32_t& f) {
+        if (r < H) {
+            const uint8_t* rr = rimg + (int64_t)r * (W + 1);
+            f = rr[0];
+            if (nb > 0) __builtin_memcpy(x, rr + 1 + b0, 4 * NW);  // the last lane may over-read: the buffer is padded
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < PF; ++k) load(k, buf[k], fb[k]);
+    for (int r0 = 0; r0 < H; r0 += PF) {
+#pragma unroll
+        for (int k = 0; k < PF; ++k) {
+            const int r = r0 + k;
+            if (r >= H) break;
+            uint32_t x[NW];
+#pragma unroll
+            for (int i = 0; i < NW; ++i) x[i] = buf[k][i];
+            const uint32_t f = uni(fb[k]);
+            load(r + PF, buf[k], fb[k]);
+            if (f == 1) {
+                uint32_t carry = 0;
+#pragma unroll
+                for (int i = 0; i < NW; ++i) {
+                    uint32_t y = add8(x[i], x[i] << 8);
+                    y = add8(y, y << 16);
+                    y = add8(y, carry * 0x01010101u);
+                    carry = y >> 24;
+                    x[i] = y;
+                }
+                const uint32_t c = (wave_incl_scan(carry) - carry) & 0xFFu;
+#pragma unroll
+                for (int i = 0; i < NW; ++i) x[i] = add8(x[i], c * 0x01010101u);
+            } else if (f == 2) {
+#pragma unroll
+                for (int i = 0; i < NW; ++i) x[i] = add8(x[i], prev[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < NW; ++i) prev[i] = x[i];
+            uint8_t* po = dimg + (int64_t)r * dst_stride + b0;
+            if (nb == 4 * NW) {
+                __builtin_memcpy(po, x, 4 * NW);
+            } else {
+#pragma unroll
+                for (int i = 0; i < NW; ++i)
+#pragma unroll
+                    for (int k2 = 0; k2 < 4; ++k2)
+                        if (4 * i + k2 < nb) po[4 * i + k2] = (uint8_t)(x[i] >> (8 * k2));
+            }
+        }
+    }
+}
+
+// PNG scanline filters (filter method 0) of 8-bit grey rows: raw rows of 1 + W bytes (filter type first) -> rows of W
+// bytes at dst + i * dst_pitch with row stride dst_stride.  NW = ceil(W / 256) (0: W > 4096): images whose rows are all
+// None / Sub / Up take the row-wise path, others the wavefront.
+template <int NW>
+__global__ __launch_bounds__(64) void unfilter_kernel(const uint8_t* __restrict__ raw, int64_t raw_pitch, int H, int W,
+                                                      uint8_t* __restrict__ dst, int64_t dst_pitch, int dst_stride,
+                                                      int32_t* __restrict__ status) {
+    const int img = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    if (status[img] != kPngOk) return;  // wave-uniform
+    const uint8_t* rimg = raw + (int64_t)img * raw_pitch;
+    uint8_t* dimg = dst + (int64_t)img * dst_pitch;
+    if (NW > 0) {
+        bool rowwise = true, bad = false;
+        for (int r = lane; r < H; r += 64) {
+            const uint32_t f = rimg[(int64_t)r * (W + 1)];
+            rowwise = rowwise && f <= 2;
+            bad = bad || f > 4;
+        }
+        if (__ballot(bad)) {
+            if (lane == 0) status[img] = kPngErrFilter;
+            return;
+        }
+        if (!__ballot(!rowwise)) {
+            unfilter_rowwise<(NW > 0 ? NW : 1)>(rimg, H, W, dimg, dst_stride);
+            return;
+        }
+    }
+    unfilter_wavefront(rimg, H, W, dimg, dst_stride, status + img);
+}
 }  // namespace png
 
 void launch_png_inflate(const uint8_t* src, const int64_t* off, const int32_t* len, int n, uint8_t* out,
@@ -666,8 +870,25 @@ void launch_png_inflate(const uint8_t* src, const int64_t* off, const int32_t* l
 
 void launch_png_unfilter(const uint8_t* raw, int64_t raw_pitch, int n, int H, int W, uint8_t* dst, int64_t dst_pitch,
                          int dst_stride, int32_t* status, hipStream_t s) {
-    hipLaunchKernelGGL(png::unfilter_kernel, dim3(n), dim3(64), 0, s, raw, raw_pitch, H, W, dst, dst_pitch, dst_stride,
-                       status);
+    const int nw = (W + 255) / 256;
+#define YV_UNFILTER(NW)                                                                                              \
+    hipLaunchKernelGGL(png::unfilter_kernel<NW>, dim3(n), dim3(64), 0, s, raw, raw_pitch, H, W, dst, dst_pitch,     \
+                       dst_stride, status)
+    switch (nw) {
+    case 1: YV_UNFILTER(1); break;
+    case 2: YV_UNFILTER(2); break;
+    case 3: YV_UNFILTER(3); break;
+    case 4: YV_UNFILTER(4); break;
+    case 5: YV_UNFILTER(5); break;
+    case 6: YV_UNFILTER(6); break;
+    case 7: YV_UNFILTER(7); break;
+    case 8: YV_UNFILTER(8); break;
+    case 9: case 10: YV_UNFILTER(10); break;
+    case 11: case 12: YV_UNFILTER(12); break;
+    case 13: case 14: case 15: case 16: YV_UNFILTER(16); break;
+    default: YV_UNFILTER(0); break;
+    }
+#undef YV_UNFILTER
 }
 
 }  // namespace yavo

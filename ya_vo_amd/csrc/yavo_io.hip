@@ -3,6 +3,9 @@
 // whose copies to HBM run asynchronously on the caller's stream.  Host code only (no kernels).
 #include <hip/hip_runtime.h>
 #include <dirent.h>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -472,7 +475,8 @@ struct yv_pngdec {
     int32_t* d_status = nullptr;  // [max_images]
     int n_last = 0;
     hipStream_t last_stream = nullptr;
-    // two slots of staging: pinned host {streams | offsets | lengths} and the device copy of the streams
+    // slots of staging: pinned host {streams | offsets | lengths} and the device copy of the streams; four, so that a
+    // caller issuing two decodes per step (frames + halo) copies step i + 1's streams while step i's are inflated
     struct Slot {
         uint8_t* h = nullptr;   // pinned: compressed streams (64-B aligned each)
         size_t cap = 0;
@@ -482,10 +486,13 @@ struct yv_pngdec {
         size_t dcap = 0;
         int64_t* d_off = nullptr;
         int32_t* d_len = nullptr;
-        hipEvent_t done = nullptr;  // the slot's copy and inflate completed
+        hipEvent_t copied = nullptr;  // the pinned streams are on the device: the host may refill the slot
+        hipEvent_t done = nullptr;    // the slot's inflate completed: the device copy may be overwritten
         bool pending = false;
-    } slot[2];
+    } slot[4];
     int next = 0;
+    hipStream_t copy = nullptr;      // the H2D copies of the streams, beside the kernels
+    hipEvent_t last_done = nullptr;  // the last launch's unfilter completed (d_raw / d_status are free)
 };
 
 namespace {
@@ -522,6 +529,7 @@ int slot_reserve(yv_pngdec::Slot& sl, size_t bytes, int n) {
         sl.cap = cap;
     }
     if (bytes > sl.dcap) {
+        if (sl.pending && hipEventSynchronize(sl.done) != hipSuccess) return YV_ERR_HIP;  // a kernel may still read it
         if (sl.d) (void)hipFree(sl.d);
         sl.d = nullptr;
         sl.dcap = 0;
@@ -534,16 +542,25 @@ int slot_reserve(yv_pngdec::Slot& sl, size_t bytes, int n) {
 }
 
 // the slot's streams are gathered: copy them (and the job table) up, inflate, unfilter
+// The copies run on the decoder's copy stream once the slot's last inflate is done with its device buffer; the kernels
+// run on st after the copies and after the last launch's kernels (d_raw and d_status are shared).  The host waits only
+// for a slot's copies before refilling it (pngdec_next_slot).
 int pngdec_launch(yv_pngdec* d, yv_pngdec::Slot& sl, size_t bytes, int n, uint8_t* d_dst, int64_t pitch,
                   hipStream_t st) {
-    if (hipMemcpyAsync(sl.d, sl.h, bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(sl.d_off, sl.h_off, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(sl.d_len, sl.h_len, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, st) != hipSuccess)
+    hipStream_t cs = d->copy;
+    if (sl.pending && hipStreamWaitEvent(cs, sl.done, 0) != hipSuccess) return YV_ERR_HIP;
+    if (hipMemcpyAsync(sl.d, sl.h, bytes, hipMemcpyHostToDevice, cs) != hipSuccess ||
+        hipMemcpyAsync(sl.d_off, sl.h_off, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, cs) != hipSuccess ||
+        hipMemcpyAsync(sl.d_len, sl.h_len, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, cs) != hipSuccess ||
+        hipEventRecord(sl.copied, cs) != hipSuccess || hipStreamWaitEvent(st, sl.copied, 0) != hipSuccess ||
+        (d->n_last && hipStreamWaitEvent(st, d->last_done, 0) != hipSuccess))
         return YV_ERR_HIP;
     yavo::launch_png_inflate(sl.d, sl.d_off, sl.d_len, n, d->d_raw, d->raw_pitch, (uint32_t)d->H * (d->W + 1),
                              d->d_status, st);
     yavo::launch_png_unfilter(d->d_raw, d->raw_pitch, n, d->H, d->W, d_dst, pitch, d->W, d->d_status, st);
-    if (hipGetLastError() != hipSuccess || hipEventRecord(sl.done, st) != hipSuccess) return YV_ERR_HIP;
+    if (hipGetLastError() != hipSuccess || hipEventRecord(sl.done, st) != hipSuccess ||
+        hipEventRecord(d->last_done, st) != hipSuccess)
+        return YV_ERR_HIP;
     sl.pending = true;
     d->n_last = n;
     d->last_stream = st;
@@ -552,9 +569,8 @@ int pngdec_launch(yv_pngdec* d, yv_pngdec::Slot& sl, size_t bytes, int n, uint8_
 
 yv_pngdec::Slot* pngdec_next_slot(yv_pngdec* d) {
     yv_pngdec::Slot& sl = d->slot[d->next];
-    d->next ^= 1;
-    if (sl.pending && hipEventSynchronize(sl.done) != hipSuccess) return nullptr;
-    sl.pending = false;
+    d->next = (d->next + 1) % 4;
+    if (sl.pending && hipEventSynchronize(sl.copied) != hipSuccess) return nullptr;
     return &sl;
 }
 
@@ -580,8 +596,11 @@ int yv_pngdec_create(yv_ctx* ctx, int max_images, int H, int W, yv_pngdec** out)
              hipHostMalloc(reinterpret_cast<void**>(&sl.h_len), sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
              hipMalloc(reinterpret_cast<void**>(&sl.d_off), sizeof(int64_t) * (size_t)max_images) == hipSuccess &&
              hipMalloc(reinterpret_cast<void**>(&sl.d_len), sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
+             hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
     }
+    ok = ok && hipEventCreateWithFlags(&d->last_done, hipEventDisableTiming) == hipSuccess &&
+         hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking) == hipSuccess;
     if (!ok) {
         yv_pngdec_destroy(d);
         return YV_ERR_HIP;
@@ -593,11 +612,13 @@ int yv_pngdec_create(yv_ctx* ctx, int max_images, int H, int W, yv_pngdec** out)
 void yv_pngdec_destroy(yv_pngdec* d) {
     if (!d) return;
     (void)hipSetDevice(yavo::ctx_device(d->ctx));
+    if (d->copy) (void)hipStreamSynchronize(d->copy);
     for (auto& sl : d->slot) {
         if (sl.done) {
             (void)hipEventSynchronize(sl.done);
             (void)hipEventDestroy(sl.done);
         }
+        if (sl.copied) (void)hipEventDestroy(sl.copied);
         if (sl.h) (void)hipHostFree(sl.h);
         if (sl.h_off) (void)hipHostFree(sl.h_off);
         if (sl.h_len) (void)hipHostFree(sl.h_len);
@@ -605,6 +626,8 @@ void yv_pngdec_destroy(yv_pngdec* d) {
         if (sl.d_off) (void)hipFree(sl.d_off);
         if (sl.d_len) (void)hipFree(sl.d_len);
     }
+    if (d->last_done) (void)hipEventDestroy(d->last_done);
+    if (d->copy) (void)hipStreamDestroy(d->copy);
     if (d->d_raw) (void)hipFree(d->d_raw);
     if (d->d_status) (void)hipFree(d->d_status);
     delete d;
@@ -661,45 +684,60 @@ int yv_seq_upload_gpu(yv_seq* s, yv_pngdec* d, int first, int n, uint8_t* d_dst,
     if (hipSetDevice(yavo::ctx_device(d->ctx)) != hipSuccess) return YV_ERR_HIP;
     yv_pngdec::Slot* sl = pngdec_next_slot(d);
     if (!sl) return YV_ERR_HIP;
-    // file sizes -> 64-B aligned regions of the pinned slot; the threads read each file into its region and gather
-    // its IDAT stream to the region's front
-    std::vector<size_t> size((size_t)total), off((size_t)total);
-    size_t bytes = 0;
-    for (int k = 0; k < total; ++k) {
-        const std::string& path = (k % per) ? s->right[first + k / per] : s->left[first + k / per];
-        FILE* f = std::fopen(path.c_str(), "rb");
-        if (!f) return YV_ERR_INVALID;
-        std::fseek(f, 0, SEEK_END);
-        const long z = std::ftell(f);
-        std::fclose(f);
-        if (z <= 0) return YV_ERR_INVALID;
-        size[k] = (size_t)z;
-        off[k] = bytes;
-        bytes += ((size_t)z + 63) & ~(size_t)63;
-    }
-    if (slot_reserve(*sl, bytes, total) != YV_OK) return YV_ERR_HIP;
+    // the threads stat the files, their sizes place them in 64-B aligned regions of the pinned slot, then the threads
+    // read each file into its region and gather its IDAT stream to the region's front
     if (threads <= 0) threads = (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 64u);
     threads = std::max(1, std::min(threads, total));
-    std::atomic<int> next{0}, status{YV_OK};
-    auto work = [&]() {
-        for (int k; (k = next.fetch_add(1)) < total;) {
-            const std::string& path = (k % per) ? s->right[first + k / per] : s->left[first + k / per];
-            FILE* f = std::fopen(path.c_str(), "rb");
-            const size_t got = f ? std::fread(sl->h + off[k], 1, size[k], f) : 0;
-            if (f) std::fclose(f);
-            const int64_t len = got == size[k] ? png_gather_idat(sl->h + off[k], size[k], d->H, d->W) : -1;
-            if (len < 0) {
-                status = YV_ERR_INVALID;
-                continue;
-            }
-            sl->h_off[k] = (int64_t)off[k];
-            sl->h_len[k] = (int32_t)len;
-        }
+    auto path_of = [&](int k) -> const std::string& {
+        return (k % per) ? s->right[first + k / per] : s->left[first + k / per];
     };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < threads; ++t) pool.emplace_back(work);
-    work();
-    for (auto& t : pool) t.join();
+    std::vector<size_t> size((size_t)total), off((size_t)total);
+    std::atomic<int> next{0}, status{YV_OK};
+    auto run = [&](auto&& job) {
+        next = 0;
+        auto work = [&]() {
+            for (int k; (k = next.fetch_add(1)) < total;) job(k);
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < threads; ++t) pool.emplace_back(work);
+        work();
+        for (auto& t : pool) t.join();
+    };
+    run([&](int k) {
+        struct stat sb;
+        if (::stat(path_of(k).c_str(), &sb) != 0 || sb.st_size <= 0) {
+            status = YV_ERR_INVALID;
+            size[k] = 0;
+            return;
+        }
+        size[k] = (size_t)sb.st_size;
+    });
+    if (status.load() != YV_OK) return status.load();
+    size_t bytes = 0;
+    for (int k = 0; k < total; ++k) {
+        off[k] = bytes;
+        bytes += (size[k] + 63) & ~(size_t)63;
+    }
+    if (slot_reserve(*sl, bytes, total) != YV_OK) return YV_ERR_HIP;
+    run([&](int k) {
+        const int fd = ::open(path_of(k).c_str(), O_RDONLY);
+        size_t got = 0;
+        if (fd >= 0) {
+            while (got < size[k]) {
+                const ssize_t r = ::read(fd, sl->h + off[k] + got, size[k] - got);
+                if (r <= 0) break;
+                got += (size_t)r;
+            }
+            ::close(fd);
+        }
+        const int64_t len = got == size[k] ? png_gather_idat(sl->h + off[k], size[k], d->H, d->W) : -1;
+        if (len < 0) {
+            status = YV_ERR_INVALID;
+            return;
+        }
+        sl->h_off[k] = (int64_t)off[k];
+        sl->h_len[k] = (int32_t)len;
+    });
     if (status.load() != YV_OK) return status.load();
     hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : yavo::ctx_stream(d->ctx);
     return pngdec_launch(d, *sl, bytes, total, d_dst, pitch, st);
