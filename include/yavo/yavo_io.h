@@ -70,6 +70,10 @@ int yv_pngdec_decode(yv_pngdec* d, const uint8_t* const* files, const size_t* si
  * straight into the pinned staging, then decoded as yv_pngdec_decode does */
 int yv_seq_upload_gpu(yv_seq* seq, yv_pngdec* d, int first, int n, uint8_t* d_dst, int64_t pitch, int threads,
                       void* stream);
+/* the same for the listed frames: frame frames[i] -> images per * i (+ 1 for its right image) at d_dst, in one decode
+ * (e.g. a shard's frames then its halo frame) */
+int yv_seq_upload_gpu_frames(yv_seq* seq, yv_pngdec* d, const int* frames, int n, uint8_t* d_dst, int64_t pitch,
+                             int threads, void* stream);
 /* waits for the last decode; codes[i] (optional, host, n of the last call) = 0 or the image's decode error;
  * *n_bad = images that failed */
 int yv_pngdec_status(yv_pngdec* d, int32_t* codes, int* n_bad);

@@ -161,5 +161,12 @@ def test_gpu_png_sequence_upload(ctx, tmp_path):
     assert bad == 0, codes
     np.testing.assert_array_equal(d.cpu().numpy().reshape(-1, H, W), seq.read(1, n - 1))
     np.testing.assert_array_equal(d.cpu().numpy().reshape(-1, H, W), fr[2:2 * n])
+    # a frame list in one decode (a shard's frames, then its halo frame)
+    d.zero_()
+    dec.upload_frames(seq, [2, 3, 4, 0], d.data_ptr(), H * W, threads=3)
+    codes, bad = dec.status()
+    assert bad == 0, codes
+    np.testing.assert_array_equal(d.cpu().numpy().reshape(-1, H, W)[:8],
+                                  np.concatenate([fr[4:10], fr[0:2]]))
     dec.close()
     seq.close()

@@ -28,39 +28,52 @@
 namespace yavo {
 namespace png {
 
-// LDS per wave <= 20 KB: eight waves (two per SIMD) hide each other's LDS latency
+// LDS per wave <= 17.5 KB: nine waves per CU, so a step's 2 x 1024 + 2 images are resident at once
 constexpr int kRing = 8192;  // LDS output ring
 constexpr uint32_t kRingMask = kRing - 1;
-constexpr int kLitBits = 11, kDistBits = 8, kClBits = 7;  // fast-table index widths
+constexpr int kLitBits = 10, kDistBits = 8, kClBits = 7;  // fast-table index widths
 constexpr uint32_t kSegMax = 512, kSegMin = 32;          // bits per lane per chunk
 constexpr uint32_t kLead = 256;                          // synchronisation lead-in, bits
-constexpr int kStageWords = 2 * kSegMax + 8;             // the chunk's stream words (+ look-ahead)
+constexpr int kStageWords = (2 * kSegMax + 8 + 31) / 32 * 32;  // the chunk's stream words (+ look-ahead), whole rows
 constexpr int kMaxMatch = 256;                           // matches listed per chunk
 constexpr uint32_t kCap = kRing - 64;                    // output bytes per chunk (the ring keeps the unflushed tail)
 // kSegMin: lane 0's segment alone always fits (<= 16 tokens start in 32 bits, <= 258 bytes each)
 static_assert(16 * 258 <= (int)kCap && 16 <= kMaxMatch, "minimum segment");
 
+struct LenInfo {
+    uint16_t next;  // first canonical code of the length
+    uint16_t cnt;   // codes of the length
+    uint16_t offs;  // index of its first symbol in sym
+    uint16_t pad;
+};
+
 template <int NS>
 struct Table {
-    uint16_t cnt[16];  // codes per length
-    uint16_t offs[16];  // first index of each length in sym
-    uint16_t next[16];  // first canonical code of each length
-    uint16_t sym[NS];   // symbols ordered by (length, symbol)
+    LenInfo len[16];
+    uint16_t sym[NS];  // symbols ordered by (length, symbol)
 };
 
 struct Lds {
     alignas(16) uint8_t ring[kRing];
     alignas(16) uint32_t stage[kStageWords];
-    alignas(16) uint16_t lit_fast[1 << kLitBits];   // (symbol << 4) | length; 0: longer than kLitBits (or no code)
+    alignas(16) union {
+        uint16_t lit_fast[1 << kLitBits];  // (symbol << 4) | length; 0: longer than kLitBits (or no code)
+        struct {
+            uint8_t lens[320];  // code lengths while a block header is read: litlen [0, 288), distance [288, 320)
+            uint8_t cl[20];     // the code-length code's lengths
+        } h;                    // (the litlen table is built last, after every read of lens)
+    } u;
     alignas(16) uint16_t dist_fast[1 << kDistBits];  // distance codes; the code-length code while lengths are read
     uint32_t mdst[kMaxMatch];                        // the chunk's matches: output position,
     uint32_t mld[kMaxMatch];                         // (length << 16) | distance
     Table<288> lit;
     Table<32> dist;  // distance codes (30) or the code-length code (19)
-    uint8_t lens[320];  // code lengths: litlen [0, 288), distance [288, 320)
-    uint8_t cl[20];
 };
-static_assert(sizeof(Lds) <= 20 * 1024, "eight waves per CU");
+static_assert(sizeof(Lds) <= 17920, "nine waves per CU (2304 resident images on 256 CUs)");
+
+// stage word i's slot: XOR-swizzled within each 32-word row, so that the lanes' segments (seg / 32 words apart) fall
+// on different LDS banks (ds_read_b32 banks = dword index mod 32; unswizzled, 512-bit segments were 16-way conflicts)
+__device__ __forceinline__ uint32_t sw(uint32_t i) { return i ^ ((i >> 5) & 31u); }
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint32_t lane_of(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -117,19 +130,10 @@ __device__ bool build_table(const uint8_t* lens, int n, Table<NS>& T, uint16_t* 
         off[l] = l == 1 ? 0 : off[l - 1] + c[l - 1];
     }
     if (left < 0) return false;
-    if (lane < 16) {
-        T.cnt[lane] = 0;
-        T.offs[lane] = 0;
-        T.next[lane] = 0;
-    }
-    __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
+        T.len[0] = LenInfo{0, 0, 0, 0};
 #pragma unroll
-        for (int l = 1; l < 16; ++l) {
-            T.cnt[l] = (uint16_t)c[l];
-            T.offs[l] = (uint16_t)off[l];
-            T.next[l] = (uint16_t)nxt[l];
-        }
+        for (int l = 1; l < 16; ++l) T.len[l] = LenInfo{(uint16_t)nxt[l], (uint16_t)c[l], (uint16_t)off[l], 0};
     }
     __builtin_amdgcn_wave_barrier();
     constexpr int G = 5;  // n <= 320
@@ -152,8 +156,9 @@ __device__ bool build_table(const uint8_t* lens, int n, Table<NS>& T, uint16_t* 
         gr[g] = 0;
         ge[g] = ((uint32_t)s << 4) | (uint32_t)l;
         if (l) {  // per-lane length: the LDS copies of off / nxt
-            T.sym[T.offs[l] + idx] = (uint16_t)s;
-            gr[g] = __builtin_bitreverse32((uint32_t)T.next[l] + idx) >> (32 - l);
+            const LenInfo li = T.len[l];
+            T.sym[li.offs + idx] = (uint16_t)s;
+            gr[g] = __builtin_bitreverse32((uint32_t)li.next + idx) >> (32 - l);
         }
     }
     if (lane < 2) fast[lane] = 0;
@@ -177,20 +182,27 @@ __device__ bool build_table(const uint8_t* lens, int n, Table<NS>& T, uint16_t* 
     return true;
 }
 
-// a code longer than the fast table: canonical decoding of lengths F+1..15 from the next 15 bits
+// a code longer than the fast table: canonical decoding from the first 15 stream bits (bit 0 first).  Every candidate
+// length F+1..15 is tested at once (one LDS round trip for the length table, one for the symbol); the code is prefix
+// free, so at most one length matches.
 template <int NS>
 __device__ __forceinline__ bool slow_code(const Table<NS>& T, uint32_t bits, int F, uint32_t& len, uint32_t& sym) {
-    const uint32_t rev = __builtin_bitreverse32(bits) >> 17;  // first stream bit as the MSB of 15
-    for (int l = F + 1; l < 16; ++l) {
-        const uint32_t cd = rev >> (15 - l);
-        const uint32_t i = cd - (uint32_t)T.next[l];
-        if (i < (uint32_t)T.cnt[l]) {
-            len = (uint32_t)l;
-            sym = T.sym[T.offs[l] + i];
-            return true;
+    const uint32_t rev = __builtin_bitreverse32(bits) >> 17;
+    uint32_t found = 0, idx = 0;
+#pragma unroll
+    for (int l = 15; l >= 8; --l) {
+        if (l <= F) break;
+        const LenInfo li = T.len[l];
+        const uint32_t i = (rev >> (15 - l)) - (uint32_t)li.next;
+        if (i < (uint32_t)li.cnt) {
+            found = (uint32_t)l;
+            idx = (uint32_t)li.offs + i;
         }
     }
-    return false;
+    if (!found) return false;
+    len = found;
+    sym = T.sym[idx];
+    return true;
 }
 
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
@@ -204,7 +216,7 @@ template <bool CL>
 __device__ __forceinline__ uint32_t decode_tok(const Lds& S, uint32_t w0, uint32_t p, uint32_t& nbits, uint32_t& a,
                                                uint32_t& b) {
     const uint32_t i = (p >> 5) - w0, sh = p & 31u;
-    const uint32_t x0 = S.stage[i], x1 = S.stage[i + 1], x2 = S.stage[i + 2];
+    const uint32_t x0 = S.stage[sw(i)], x1 = S.stage[sw(i + 1)], x2 = S.stage[sw(i + 2)];
     const uint32_t lo = __builtin_amdgcn_alignbit(x1, x0, sh);
     const uint32_t hi = __builtin_amdgcn_alignbit(x2, x1, sh);
     if (CL) {
@@ -227,7 +239,7 @@ __device__ __forceinline__ uint32_t decode_tok(const Lds& S, uint32_t w0, uint32
         nbits = len + xb;
         return kFill;
     }
-    uint32_t e = S.lit_fast[lo & ((1u << kLitBits) - 1u)], len, sym;
+    uint32_t e = S.u.lit_fast[lo & ((1u << kLitBits) - 1u)], len, sym;
     if (e) {
         len = e & 15u;
         sym = e >> 4;
@@ -311,33 +323,84 @@ struct Dec {
 
 __device__ __forceinline__ void dec_seek(const Lds& S, uint32_t w0, Dec& d, uint32_t p) {
     const uint32_t i = (p >> 5) - w0, sh = p & 31u;
-    const uint32_t x0 = S.stage[i], x1 = S.stage[i + 1];
+    const uint32_t x0 = S.stage[sw(i)], x1 = S.stage[sw(i + 1)];
     d.p = p;
     d.bb = (((uint64_t)x1 << 32) | x0) >> sh;
     d.avail = 64u - sh;
     d.wi = i + 2;
-    d.wn = S.stage[i + 2];
+    d.wn = S.stage[sw(i + 2)];
 }
 
-__device__ __forceinline__ uint32_t data_step(const Lds& S, uint32_t w0, Dec& d, uint32_t& a, uint32_t& b) {
+__device__ __forceinline__ void dec_refill(const Lds& S, Dec& d) {
     const bool need = d.avail <= 32u;
     d.bb |= need ? ((uint64_t)d.wn << d.avail) : 0ull;
     d.avail += need ? 32u : 0u;
     d.wi += need ? 1u : 0u;
-    d.wn = S.stage[d.wi];
-    const uint32_t e = S.lit_fast[(uint32_t)d.bb & ((1u << kLitBits) - 1u)];
+    d.wn = S.stage[sw(d.wi)];
+}
+
+__device__ __forceinline__ void dec_drop(Dec& d, uint32_t n) {
+    d.bb >>= n;
+    d.avail -= n;
+    d.p += n;
+}
+
+// one token from the bit buffer.  Literal / length codes <= 15 bits + 5 extra fit the > 32 refilled bits; the buffer is
+// refilled again before the distance code (<= 15 bits + 13 extra).
+__device__ __forceinline__ uint32_t data_step(const Lds& S, Dec& d, uint32_t& a, uint32_t& b) {
+    dec_refill(S, d);
+    const uint32_t e = S.u.lit_fast[(uint32_t)d.bb & ((1u << kLitBits) - 1u)];
     if (e - 1u < (256u << 4) - 1u) {  // 0 < e < 256 << 4: a literal with a fast code
-        const uint32_t n = e & 15u;
         a = e >> 4;
-        d.bb >>= n;
-        d.avail -= n;
-        d.p += n;
+        dec_drop(d, e & 15u);
         return kLit;
     }
-    uint32_t nb = 0;
-    const uint32_t k = decode_tok<false>(S, w0, d.p, nb, a, b);
-    if (k != kErr) dec_seek(S, w0, d, d.p + nb);
-    return k;
+    uint32_t len, sym;
+    if (e) {
+        len = e & 15u;
+        sym = e >> 4;
+    } else if (!slow_code(S.lit, (uint32_t)d.bb, kLitBits, len, sym)) {
+        return kErr;
+    }
+    if (sym < 256) {
+        a = sym;
+        dec_drop(d, len);
+        return kLit;
+    }
+    if (sym == 256) {
+        dec_drop(d, len);
+        return kEob;
+    }
+    const uint32_t li = sym - 257;
+    if (li >= 29) return kErr;
+    uint32_t le = 0, lb = li + 3;  // RFC 1951 3.2.5: 3..10 plain, then 4 per extra-bit count, 258
+    if (li == 28) {
+        lb = 258;
+    } else if (li >= 8) {
+        le = (li >> 2) - 1;
+        lb = ((4u | (li & 3u)) << le) + 3;
+    }
+    a = lb + (((uint32_t)d.bb >> len) & ((1u << le) - 1u));
+    dec_drop(d, len + le);
+    dec_refill(S, d);
+    const uint32_t lo = (uint32_t)d.bb;
+    const uint32_t e2 = S.dist_fast[lo & ((1u << kDistBits) - 1u)];
+    uint32_t dl, ds;
+    if (e2) {
+        dl = e2 & 15u;
+        ds = e2 >> 4;
+    } else if (!slow_code(S.dist, lo, kDistBits, dl, ds)) {
+        return kErr;
+    }
+    if (ds >= 30) return kErr;
+    uint32_t de = 0, db = ds + 1;
+    if (ds >= 4) {
+        de = (ds >> 1) - 1;
+        db = ((2u | (ds & 1u)) << de) + 1;
+    }
+    b = db + ((lo >> dl) & ((1u << de) - 1u));
+    dec_drop(d, dl + de);
+    return kMatch;
 }
 
 __device__ __forceinline__ void count_pass_data(const Lds& S, uint32_t w0, uint32_t& p, uint32_t to, uint32_t& cnt,
@@ -349,7 +412,7 @@ __device__ __forceinline__ void count_pass_data(const Lds& S, uint32_t w0, uint3
     dec_seek(S, w0, d, p);
     while (d.p < to) {
         uint32_t a = 0, b = 0;
-        const uint32_t k = data_step(S, w0, d, a, b);
+        const uint32_t k = data_step(S, d, a, b);
         if (k == kErr) {
             stop = 2;
             break;
@@ -388,7 +451,7 @@ __device__ __forceinline__ uint32_t lens_slot(uint32_t k, uint32_t hlit) { retur
 
 // One chunk of the lane-parallel decoder from the true token boundary P0 (see the file comment).
 // DATA (CL false): output position op, the ring, matches against the window; `done` at the end-of-block token.
-// CL: code lengths k = op of need in total into S.lens; `done` when all are read.
+// CL: code lengths k = op of need in total into S.u.h.lens; `done` when all are read.
 // Advances P0 / op, adapts seg; returns kPngOk or an error.
 template <bool CL>
 __device__ int run_chunk(Lds& S, const uint32_t* __restrict__ src, uint32_t nwords, uint32_t& P0, uint32_t& op,
@@ -400,7 +463,7 @@ __device__ int run_chunk(Lds& S, const uint32_t* __restrict__ src, uint32_t nwor
     // stage the chunk's words
     const uint32_t w0 = P0 >> 5;
     const uint32_t nst = 2 * seg + 6;
-    for (uint32_t i = lane; i < nst; i += 64) S.stage[i] = w0 + i < nwords ? src[w0 + i] : 0u;
+    for (uint32_t i = lane; i < nst; i += 64) S.stage[sw(i)] = w0 + i < nwords ? src[w0 + i] : 0u;
     __builtin_amdgcn_wave_barrier();
     const uint32_t Sk = P0 + (uint32_t)lane * seg, Sn = Sk + seg;
     // lead-in: synchronise before the segment (lane 0 starts on the true boundary)
@@ -417,7 +480,7 @@ __device__ int run_chunk(Lds& S, const uint32_t* __restrict__ src, uint32_t nwor
         dec_seek(S, w0, d, p);
         while (d.p < Sk) {
             uint32_t a = 0, b = 0;
-            if (data_step(S, w0, d, a, b) == kErr) dec_seek(S, w0, d, d.p + 1);
+            if (data_step(S, d, a, b) == kErr) dec_seek(S, w0, d, d.p + 1);
         }
         p = d.p;
     }
@@ -476,7 +539,7 @@ __device__ int run_chunk(Lds& S, const uint32_t* __restrict__ src, uint32_t nwor
                 if (k == kErr) break;
                 p += nb;
                 if (k == kLit) {
-                    S.lens[lens_slot(o, hlit)] = (uint8_t)a;
+                    S.u.h.lens[lens_slot(o, hlit)] = (uint8_t)a;
                     ++o;
                 } else if (k == kMatch) {
                     S.mdst[mi] = o;
@@ -485,7 +548,7 @@ __device__ int run_chunk(Lds& S, const uint32_t* __restrict__ src, uint32_t nwor
                     o += a;
                 } else {
                     for (uint32_t j = 0; j < a; ++j)
-                        if (o + j < o_end) S.lens[lens_slot(o + j, hlit)] = 0;
+                        if (o + j < o_end) S.u.h.lens[lens_slot(o + j, hlit)] = 0;
                     o += a;
                 }
             }
@@ -495,7 +558,7 @@ __device__ int run_chunk(Lds& S, const uint32_t* __restrict__ src, uint32_t nwor
             dec_seek(S, w0, d, p);
             while (d.p < Sn) {
                 uint32_t a = 0, b = 0;
-                const uint32_t k = data_step(S, w0, d, a, b);
+                const uint32_t k = data_step(S, d, a, b);
                 if (k == kErr || k == kEob) break;
                 if (k == kLit) {
                     S.ring[o & kRingMask] = (uint8_t)a;
@@ -521,8 +584,8 @@ __device__ int run_chunk(Lds& S, const uint32_t* __restrict__ src, uint32_t nwor
         const uint32_t L = ld >> 16, D = ld & 0xFFFFu;
         if (D > d) return kPngErrCode;
         if (CL) {
-            const uint32_t v = S.lens[lens_slot(d - 1, hlit)];
-            for (uint32_t j = lane; j < L; j += 64) S.lens[lens_slot(d + j, hlit)] = (uint8_t)v;
+            const uint32_t v = S.u.h.lens[lens_slot(d - 1, hlit)];
+            for (uint32_t j = lane; j < L; j += 64) S.u.h.lens[lens_slot(d + j, hlit)] = (uint8_t)v;
             __builtin_amdgcn_wave_barrier();
             continue;
         }
@@ -629,7 +692,7 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__
         }
         if (type == 1) {
             // fixed codes (RFC 1951 3.2.6)
-            for (int s = lane; s < 320; s += 64) S.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
+            for (int s = lane; s < 320; s += 64) S.u.h.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
             __builtin_amdgcn_wave_barrier();
         } else {
             const uint32_t hlit = br.get(5) + 257, hdist = br.get(5) + 1, hclen = br.get(4) + 4;
@@ -637,7 +700,7 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__
                 st = kPngErrBlock;
                 break;
             }
-            if (lane < 20) S.cl[lane] = 0;
+            if (lane < 20) S.u.h.cl[lane] = 0;
             __builtin_amdgcn_wave_barrier();
             {
                 // hclen 3-bit lengths in the order 16 17 18 0 8 7 9 6 10 5 11 4 12 3 13 2 14 1 15: lane k takes the k-th
@@ -645,18 +708,18 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__
                 if ((uint32_t)lane < hclen) {
                     const uint32_t q = pos0 + 3u * lane, w = q >> 5, sh = q & 31u;
                     const uint64_t x = (((uint64_t)br.word(w + 1) << 32) | br.word(w)) >> sh;
-                    S.cl[kClOrder[lane]] = (uint8_t)(x & 7u);
+                    S.u.h.cl[kClOrder[lane]] = (uint8_t)(x & 7u);
                 }
                 br.pos = pos0 + 3u * hclen;
             }
             __builtin_amdgcn_wave_barrier();
             // the code-length code: its table in dist_fast / dist (7-bit codes)
-            if (!build_table(S.cl, 19, S.dist, S.dist_fast, kClBits)) {
+            if (!build_table(S.u.h.cl, 19, S.dist, S.dist_fast, kClBits)) {
                 st = kPngErrCode;
                 break;
             }
             // hlit + hdist code lengths, litlen into lens[0, hlit), distance into lens[288, 288 + hdist)
-            for (int s = lane; s < 320; s += 64) S.lens[s] = 0;
+            for (int s = lane; s < 320; s += 64) S.u.h.lens[s] = 0;
             __builtin_amdgcn_wave_barrier();
             uint32_t k = 0, P = br.pos, cseg = kSegMin;
             const uint32_t total = hlit + hdist;
@@ -668,13 +731,13 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__
             if (st != kPngOk) break;
             br.pos = P;
             __builtin_amdgcn_wave_barrier();
-            if (uni(S.lens[256]) == 0) {  // no end-of-block code
+            if (uni(S.u.h.lens[256]) == 0) {  // no end-of-block code
                 st = kPngErrCode;
                 break;
             }
         }
-        if (!build_table(S.lens, 288, S.lit, S.lit_fast, kLitBits) ||
-            !build_table(S.lens + 288, 30, S.dist, S.dist_fast, kDistBits)) {
+        if (!build_table(S.u.h.lens + 288, 30, S.dist, S.dist_fast, kDistBits) ||
+            !build_table(S.u.h.lens, 288, S.lit, S.u.lit_fast, kLitBits)) {  // last: lit_fast overlays lens
             st = kPngErrCode;
             break;
         }
@@ -860,7 +923,29 @@ __global__ __launch_bounds__(64) void unfilter_kernel(const uint8_t* __restrict_
     }
     unfilter_wavefront(rimg, H, W, dimg, dst_stride, status + img);
 }
+// IDAT payloads of the staged files -> contiguous zlib streams: one wave per payload, 16 bytes per lane per pass
+__global__ __launch_bounds__(64) void gather_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                   const PngPiece* __restrict__ pieces) {
+    const int lane = threadIdx.x & 63;
+    const PngPiece pc = pieces[blockIdx.x];
+    const uint8_t* s = src + pc.src;
+    uint8_t* d = dst + pc.dst;
+    for (int64_t i = 16 * lane; i < pc.len; i += 1024) {
+        if (i + 16 <= pc.len) {
+            uint4 v;
+            __builtin_memcpy(&v, s + i, 16);
+            __builtin_memcpy(d + i, &v, 16);
+        } else {
+            for (int64_t k = i; k < pc.len; ++k) d[k] = s[k];
+        }
+    }
+}
+
 }  // namespace png
+
+void launch_png_gather(const uint8_t* src, uint8_t* dst, const PngPiece* pieces, int n, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(png::gather_kernel, dim3(n), dim3(64), 0, s, src, dst, pieces);
+}
 
 void launch_png_inflate(const uint8_t* src, const int64_t* off, const int32_t* len, int n, uint8_t* out,
                         int64_t out_pitch, uint32_t out_len, int32_t* status, hipStream_t s) {

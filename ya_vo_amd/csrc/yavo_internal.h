@@ -237,6 +237,12 @@ enum : int32_t {
     kPngOk = 0, kPngErrHeader = 1, kPngErrBlock = 2, kPngErrCode = 3, kPngErrOverrun = 4, kPngErrShort = 5,
     kPngErrFilter = 6
 };
+// one IDAT payload of a PNG file staged on the device: len bytes from src to dst (byte offsets in the staging buffers)
+struct PngPiece {
+    int64_t src, dst;
+    int32_t len, pad;
+};
+void launch_png_gather(const uint8_t* src, uint8_t* dst, const PngPiece* pieces, int n, hipStream_t s);
 void launch_png_inflate(const uint8_t* src, const int64_t* off, const int32_t* len, int n, uint8_t* out,
                         int64_t out_pitch, uint32_t out_len, int32_t* status, hipStream_t s);
 void launch_png_unfilter(const uint8_t* raw, int64_t raw_pitch, int n, int H, int W, uint8_t* dst, int64_t dst_pitch,

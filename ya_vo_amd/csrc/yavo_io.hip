@@ -482,8 +482,13 @@ struct yv_pngdec {
         size_t cap = 0;
         int64_t* h_off = nullptr;
         int32_t* h_len = nullptr;
-        uint8_t* d = nullptr;   // device copy of the streams
+        uint8_t* d = nullptr;   // device copy of the files
+        uint8_t* dg = nullptr;  // their zlib streams, gathered on the device (same offsets)
         size_t dcap = 0;
+        yavo::PngPiece* h_pc = nullptr;  // pinned: the IDAT payloads
+        yavo::PngPiece* d_pc = nullptr;
+        size_t pc_cap = 0;
+        hipEvent_t gathered = nullptr;
         int64_t* d_off = nullptr;
         int32_t* d_len = nullptr;
         hipEvent_t copied = nullptr;  // the pinned streams are on the device: the host may refill the slot
@@ -497,26 +502,27 @@ struct yv_pngdec {
 
 namespace {
 
-// IDAT payloads of one 8-bit grey non-interlaced H x W PNG moved to the front of buf, in place (memmove);
-// returns their length or -1
-int64_t png_gather_idat(uint8_t* buf, size_t len, int H, int W) {
+// IDAT payloads of one 8-bit grey non-interlaced H x W PNG staged at `base` of the slot: appended to pcs as pieces
+// (src = base + payload offset, dst = base + position in the zlib stream); returns the stream's length or -1
+int64_t png_idat_pieces(const uint8_t* buf, size_t len, int H, int W, int64_t base, std::vector<yavo::PngPiece>& pcs) {
     PngHeader h;
     if (png_parse(buf, len, h, nullptr, nullptr) != YV_OK) return -1;
     if (h.ctype != 0 || h.depth != 8 || h.interlace != 0 || h.H != H || h.W != W) return -1;
-    size_t off = 8, out = 0;
+    size_t off = 8;
+    int64_t out = 0;
     while (off + 12 <= len) {
         const uint32_t n = be32(buf + off);
         if (n > len - off - 12) return -1;
         const uint8_t* type = buf + off + 4;
         if (!std::memcmp(type, "IDAT", 4)) {
-            std::memmove(buf + out, buf + off + 8, n);  // out <= off + 8: the move never overruns unread chunks
+            if (n) pcs.push_back({base + (int64_t)off + 8, base + out, (int32_t)n, 0});
             out += n;
         } else if (!std::memcmp(type, "IEND", 4)) {
             break;
         }
         off += 12 + n;
     }
-    return out ? (int64_t)out : -1;
+    return out ? out : -1;
 }
 
 int slot_reserve(yv_pngdec::Slot& sl, size_t bytes, int n) {
@@ -531,13 +537,49 @@ int slot_reserve(yv_pngdec::Slot& sl, size_t bytes, int n) {
     if (bytes > sl.dcap) {
         if (sl.pending && hipEventSynchronize(sl.done) != hipSuccess) return YV_ERR_HIP;  // a kernel may still read it
         if (sl.d) (void)hipFree(sl.d);
-        sl.d = nullptr;
+        if (sl.dg) (void)hipFree(sl.dg);
+        sl.d = sl.dg = nullptr;
         sl.dcap = 0;
         const size_t cap = std::max(bytes + bytes / 4, (size_t)16 << 20);
-        if (hipMalloc(reinterpret_cast<void**>(&sl.d), cap) != hipSuccess) return YV_ERR_HIP;
+        if (hipMalloc(reinterpret_cast<void**>(&sl.d), cap) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&sl.dg), cap) != hipSuccess)
+            return YV_ERR_HIP;
         sl.dcap = cap;
     }
     (void)n;
+    return YV_OK;
+}
+
+// the slot's piece table holds at least n entries (host: the copies of its last use are done; device: its last
+// gather is done)
+int slot_reserve_pieces(yv_pngdec::Slot& sl, size_t n) {
+    if (n <= sl.pc_cap) return YV_OK;
+    if (sl.pending && hipEventSynchronize(sl.done) != hipSuccess) return YV_ERR_HIP;
+    if (sl.h_pc) (void)hipHostFree(sl.h_pc);
+    if (sl.d_pc) (void)hipFree(sl.d_pc);
+    sl.h_pc = nullptr;
+    sl.d_pc = nullptr;
+    sl.pc_cap = 0;
+    const size_t cap = std::max(n + n / 4, (size_t)4096);
+    if (hipHostMalloc(reinterpret_cast<void**>(&sl.h_pc), cap * sizeof(yavo::PngPiece)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&sl.d_pc), cap * sizeof(yavo::PngPiece)) != hipSuccess)
+        return YV_ERR_HIP;
+    sl.pc_cap = cap;
+    return YV_OK;
+}
+
+// per-image piece lists -> the slot's pinned table
+int slot_set_pieces(yv_pngdec::Slot& sl, const std::vector<std::vector<yavo::PngPiece>>& pcs, int& npc) {
+    size_t n = 0;
+    for (const auto& v : pcs) n += v.size();
+    if (n > (size_t)INT32_MAX) return YV_ERR_INVALID;
+    if (slot_reserve_pieces(sl, n) != YV_OK) return YV_ERR_HIP;
+    size_t k = 0;
+    for (const auto& v : pcs) {
+        std::memcpy(sl.h_pc + k, v.data(), v.size() * sizeof(yavo::PngPiece));
+        k += v.size();
+    }
+    npc = (int)n;
     return YV_OK;
 }
 
@@ -545,17 +587,23 @@ int slot_reserve(yv_pngdec::Slot& sl, size_t bytes, int n) {
 // The copies run on the decoder's copy stream once the slot's last inflate is done with its device buffer; the kernels
 // run on st after the copies and after the last launch's kernels (d_raw and d_status are shared).  The host waits only
 // for a slot's copies before refilling it (pngdec_next_slot).
-int pngdec_launch(yv_pngdec* d, yv_pngdec::Slot& sl, size_t bytes, int n, uint8_t* d_dst, int64_t pitch,
+int pngdec_launch(yv_pngdec* d, yv_pngdec::Slot& sl, size_t bytes, int n, int npc, uint8_t* d_dst, int64_t pitch,
                   hipStream_t st) {
     hipStream_t cs = d->copy;
     if (sl.pending && hipStreamWaitEvent(cs, sl.done, 0) != hipSuccess) return YV_ERR_HIP;
     if (hipMemcpyAsync(sl.d, sl.h, bytes, hipMemcpyHostToDevice, cs) != hipSuccess ||
         hipMemcpyAsync(sl.d_off, sl.h_off, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, cs) != hipSuccess ||
         hipMemcpyAsync(sl.d_len, sl.h_len, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, cs) != hipSuccess ||
-        hipEventRecord(sl.copied, cs) != hipSuccess || hipStreamWaitEvent(st, sl.copied, 0) != hipSuccess ||
+        hipMemcpyAsync(sl.d_pc, sl.h_pc, sizeof(yavo::PngPiece) * (size_t)npc, hipMemcpyHostToDevice, cs) !=
+            hipSuccess ||
+        hipEventRecord(sl.copied, cs) != hipSuccess)
+        return YV_ERR_HIP;
+    yavo::launch_png_gather(sl.d, sl.dg, sl.d_pc, npc, cs);
+    if (hipGetLastError() != hipSuccess || hipEventRecord(sl.gathered, cs) != hipSuccess ||
+        hipStreamWaitEvent(st, sl.gathered, 0) != hipSuccess ||
         (d->n_last && hipStreamWaitEvent(st, d->last_done, 0) != hipSuccess))
         return YV_ERR_HIP;
-    yavo::launch_png_inflate(sl.d, sl.d_off, sl.d_len, n, d->d_raw, d->raw_pitch, (uint32_t)d->H * (d->W + 1),
+    yavo::launch_png_inflate(sl.dg, sl.d_off, sl.d_len, n, d->d_raw, d->raw_pitch, (uint32_t)d->H * (d->W + 1),
                              d->d_status, st);
     yavo::launch_png_unfilter(d->d_raw, d->raw_pitch, n, d->H, d->W, d_dst, pitch, d->W, d->d_status, st);
     if (hipGetLastError() != hipSuccess || hipEventRecord(sl.done, st) != hipSuccess ||
@@ -597,6 +645,7 @@ int yv_pngdec_create(yv_ctx* ctx, int max_images, int H, int W, yv_pngdec** out)
              hipMalloc(reinterpret_cast<void**>(&sl.d_off), sizeof(int64_t) * (size_t)max_images) == hipSuccess &&
              hipMalloc(reinterpret_cast<void**>(&sl.d_len), sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
              hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&sl.gathered, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
     }
     ok = ok && hipEventCreateWithFlags(&d->last_done, hipEventDisableTiming) == hipSuccess &&
@@ -619,6 +668,10 @@ void yv_pngdec_destroy(yv_pngdec* d) {
             (void)hipEventDestroy(sl.done);
         }
         if (sl.copied) (void)hipEventDestroy(sl.copied);
+        if (sl.gathered) (void)hipEventDestroy(sl.gathered);
+        if (sl.h_pc) (void)hipHostFree(sl.h_pc);
+        if (sl.d_pc) (void)hipFree(sl.d_pc);
+        if (sl.dg) (void)hipFree(sl.dg);
         if (sl.h) (void)hipHostFree(sl.h);
         if (sl.h_off) (void)hipHostFree(sl.h_off);
         if (sl.h_len) (void)hipHostFree(sl.h_len);
@@ -647,16 +700,19 @@ int yv_pngdec_decode(yv_pngdec* d, const uint8_t* const* files, const size_t* si
     for (int i = 0; i < n; ++i) bytes += (sizes[i] + 63) & ~(size_t)63;
     if (slot_reserve(*sl, bytes, n) != YV_OK) return YV_ERR_HIP;
     size_t off = 0;
+    std::vector<std::vector<yavo::PngPiece>> pcs((size_t)n);
     for (int i = 0; i < n; ++i) {
         std::memcpy(sl->h + off, files[i], sizes[i]);
-        const int64_t len = png_gather_idat(sl->h + off, sizes[i], d->H, d->W);
-        if (len < 0) return YV_ERR_INVALID;
+        const int64_t len = png_idat_pieces(sl->h + off, sizes[i], d->H, d->W, (int64_t)off, pcs[(size_t)i]);
+        if (len < 0 || len > INT32_MAX) return YV_ERR_INVALID;
         sl->h_off[i] = (int64_t)off;
         sl->h_len[i] = (int32_t)len;
         off += (sizes[i] + 63) & ~(size_t)63;
     }
+    int npc = 0;
+    if (slot_set_pieces(*sl, pcs, npc) != YV_OK) return YV_ERR_HIP;
     hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : yavo::ctx_stream(d->ctx);
-    return pngdec_launch(d, *sl, off, n, d_dst, pitch, st);
+    return pngdec_launch(d, *sl, off, n, npc, d_dst, pitch, st);
 }
 
 int yv_pngdec_status(yv_pngdec* d, int32_t* codes, int* n_bad) {
@@ -675,8 +731,17 @@ int yv_pngdec_status(yv_pngdec* d, int32_t* codes, int* n_bad) {
 
 int yv_seq_upload_gpu(yv_seq* s, yv_pngdec* d, int first, int n, uint8_t* d_dst, int64_t pitch, int threads,
                       void* stream) {
-    if (!s || !d || !d_dst || first < 0 || n < 0 || first + n > (int)s->left.size() || s->H != d->H || s->W != d->W)
-        return YV_ERR_INVALID;
+    if (!s || first < 0 || n < 0 || first + n > (int)s->left.size()) return YV_ERR_INVALID;
+    std::vector<int> frames((size_t)n);
+    for (int i = 0; i < n; ++i) frames[(size_t)i] = first + i;
+    return yv_seq_upload_gpu_frames(s, d, frames.data(), n, d_dst, pitch, threads, stream);
+}
+
+int yv_seq_upload_gpu_frames(yv_seq* s, yv_pngdec* d, const int* frames, int n, uint8_t* d_dst, int64_t pitch,
+                             int threads, void* stream) {
+    if (!s || !d || !d_dst || n < 0 || (n > 0 && !frames) || s->H != d->H || s->W != d->W) return YV_ERR_INVALID;
+    for (int i = 0; i < n; ++i)
+        if (frames[i] < 0 || frames[i] >= (int)s->left.size()) return YV_ERR_INVALID;
     const int per = s->stereo ? 2 : 1;
     const int total = n * per;
     if (total > d->max_images || pitch < (int64_t)d->H * d->W) return YV_ERR_INVALID;
@@ -689,7 +754,7 @@ int yv_seq_upload_gpu(yv_seq* s, yv_pngdec* d, int first, int n, uint8_t* d_dst,
     if (threads <= 0) threads = (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 64u);
     threads = std::max(1, std::min(threads, total));
     auto path_of = [&](int k) -> const std::string& {
-        return (k % per) ? s->right[first + k / per] : s->left[first + k / per];
+        return (k % per) ? s->right[frames[k / per]] : s->left[frames[k / per]];
     };
     std::vector<size_t> size((size_t)total), off((size_t)total);
     std::atomic<int> next{0}, status{YV_OK};
@@ -719,6 +784,7 @@ int yv_seq_upload_gpu(yv_seq* s, yv_pngdec* d, int first, int n, uint8_t* d_dst,
         bytes += (size[k] + 63) & ~(size_t)63;
     }
     if (slot_reserve(*sl, bytes, total) != YV_OK) return YV_ERR_HIP;
+    std::vector<std::vector<yavo::PngPiece>> pcs((size_t)total);
     run([&](int k) {
         const int fd = ::open(path_of(k).c_str(), O_RDONLY);
         size_t got = 0;
@@ -730,8 +796,9 @@ int yv_seq_upload_gpu(yv_seq* s, yv_pngdec* d, int first, int n, uint8_t* d_dst,
             }
             ::close(fd);
         }
-        const int64_t len = got == size[k] ? png_gather_idat(sl->h + off[k], size[k], d->H, d->W) : -1;
-        if (len < 0) {
+        const int64_t len =
+            got == size[k] ? png_idat_pieces(sl->h + off[k], size[k], d->H, d->W, (int64_t)off[k], pcs[(size_t)k]) : -1;
+        if (len < 0 || len > INT32_MAX) {
             status = YV_ERR_INVALID;
             return;
         }
@@ -739,8 +806,10 @@ int yv_seq_upload_gpu(yv_seq* s, yv_pngdec* d, int first, int n, uint8_t* d_dst,
         sl->h_len[k] = (int32_t)len;
     });
     if (status.load() != YV_OK) return status.load();
+    int npc = 0;
+    if (slot_set_pieces(*sl, pcs, npc) != YV_OK) return YV_ERR_HIP;
     hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : yavo::ctx_stream(d->ctx);
-    return pngdec_launch(d, *sl, bytes, total, d_dst, pitch, st);
+    return pngdec_launch(d, *sl, bytes, total, npc, d_dst, pitch, st);
 }
 
 int yv_png_write_gray(const char* path, const uint8_t* img, int H, int W, int stride) {

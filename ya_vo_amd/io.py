@@ -145,6 +145,15 @@ class PngDecoder:
                "yv_seq_upload_gpu")
         self._n = n * (2 if seq.stereo else 1)
 
+    def upload_frames(self, seq, frames, d_dst: int, pitch: int = 0, threads: int = 0, stream: int = 0) -> None:
+        """the listed frames in one decode: frame frames[i] -> images (2 i, 2 i + 1) (stereo) or i at d_dst"""
+        fr = np.ascontiguousarray(frames, dtype=np.int32)
+        _check(self.lib.yv_seq_upload_gpu_frames(seq.handle, self.handle, fr.ctypes.data, len(fr), ctypes.c_void_p(d_dst),
+                                                 pitch or self.H * self.W, threads,
+                                                 ctypes.c_void_p(stream) if stream else None),
+               "yv_seq_upload_gpu_frames")
+        self._n = len(fr) * (2 if seq.stereo else 1)
+
     def status(self):
         """(codes of the last call's images, number failed); waits for the last call"""
         bad = ctypes.c_int()
