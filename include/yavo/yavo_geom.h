@@ -162,6 +162,36 @@ int yv_ba_set_control(yv_ba* ba, int on_device);
  * as the last yv_ba_solve left it. */
 int yv_ba_debug_read(yv_ba* ba, int which, double* dst, int64_t count);
 
+/* ---- the sliding BA window of the chained stereo front end, on the device (BASELINE configs[2]) ----
+ * The window LoopHandler's loop would hand Optimizer (src/LoopHandler.cc:60-165, src/Optimizer.cc:17-70), as
+ * ya_vo_amd/sequence.py assembles it: frame records (T_wc, landmarks X_w, and each landmark's two observations --
+ * its own frame's keypoint of the temporal match and the PnP measurement in the frame before) kept in HBM, the graph
+ * built from per-frame counts, solved by the yv_ba it is tied to, written back; nothing crosses to the host but the
+ * counts and the chi2 log.  Results are bit-identical to the host assembly + yv_ba_set_problem / yv_ba_solve. */
+typedef struct yv_ba_window yv_ba_window;
+/* max_lm: landmark slots per frame (the batch's max_kp); max_kf: keyframes per added block */
+int yv_ba_window_create(yv_ba* ba, int max_lm, int max_kf, yv_ba_window** out);
+void yv_ba_window_destroy(yv_ba_window* w);
+/* record the frames [first_frame, first_frame + n_frames) of a placed map block (yv_map_place; every frame a
+ * keyframe) on `stream` (NULL: the context's): T_wc, landmarks, uv_prev = edge_uv[k][e], uv_own =
+ * matches[2 k][edge_query[k][e]].pt2 with e = landmark id & 0xFFFF and k the frame's track (device pointers of
+ * the batch: edge_uv [n][max_kp][2] f64, edge_query [n][max_kp] i32, matches [2 n][max_kp] yv_match, temporal
+ * pairs at even indices) */
+int yv_ba_window_add_block(yv_ba_window* w, const void* d_block, int64_t first_frame, int n_frames,
+                           const double* d_edge_uv, const int32_t* d_edge_query, const void* d_matches, int max_kp,
+                           void* stream);
+/* BA over the recorded frames [first, first + n) (n <= 128), the first n_fixed held fixed, on the yv_ba's stream;
+ * refined T_wc / X written back to the records, d_anchor (7 doubles, device, may be NULL) = the last frame's T_wc.
+ * *solved = 0 when there is nothing to solve (n <= n_fixed or no landmark): the records stay, the anchor is set. */
+int yv_ba_window_solve(yv_ba_window* w, int64_t first, int n, int n_fixed, const double K[9], int max_iters,
+                       double* d_anchor, double* chi2_log, int* iters, int* solved);
+/* one frame's record (host, blocking): T_wc[7], *n landmarks, up to cap of edge ids / X [3] / uv_own [2] /
+ * uv_prev [2] (any may be NULL) */
+int yv_ba_window_read(yv_ba_window* w, int64_t frame, double* T_wc, int* n, int32_t* edge, double* X, double* uv_own,
+                      double* uv_prev, int cap);
+/* T_wc [n][7] of the recorded frames [first, first + n) (host, blocking) */
+int yv_ba_window_trajectory(yv_ba_window* w, int64_t first, int n, double* T_wc);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,3 +71,29 @@ def test_sequence_200_frames_matches_oracle(ctx, oracle, offsets):
     np.testing.assert_array_equal(np.array([x[2:] for x in ba_log]), np.array([x[2:] for x in log]))
     np.testing.assert_array_equal(traj, ref)
     assert rmse_translation(traj, ground_truth(n, scene.K_KITTI)) < 0.02
+
+
+def test_sequence_device_window_equals_host_assembly(ctx):
+    """The BA window recorded, assembled and written back on the device (yv_ba_window_*) gives the host assembly's
+    (window_problem / yv_ba_set_problem / apply_window) trajectory, BA logs and frame records bit for bit."""
+    import torch
+    n, chunk = 60, 20
+    frames = synth_sequence(71, n, stereo=True)
+    d = torch.from_numpy(frames.reshape(2 * n, *frames.shape[2:])).to("cuda:0")
+    out = []
+    for device_window in (True, False):
+        fe = SequenceFrontend(ctx, chunk, scene.K_KITTI, T_RIGHT, device_window=device_window)
+        for c in range(n // chunk):
+            fe.process_chunk(d[2 * c * chunk:2 * (c + 1) * chunk])
+        out.append((fe.trajectory(), fe.records, list(fe.ba_log)))
+        fe.close()
+    (t_dev, r_dev, l_dev), (t_host, r_host, l_host) = out
+    assert len(l_dev) == n // chunk - 1 + 1 and l_dev == l_host
+    np.testing.assert_array_equal(t_dev, t_host)
+    assert sorted(r_dev) == sorted(r_host)
+    for g in r_host:
+        np.testing.assert_array_equal(r_dev[g].T_wc, r_host[g].T_wc)
+        np.testing.assert_array_equal(r_dev[g].edge, r_host[g].edge)
+        np.testing.assert_array_equal(r_dev[g].X, r_host[g].X)
+        np.testing.assert_array_equal(r_dev[g].uv_own, r_host[g].uv_own)
+        np.testing.assert_array_equal(r_dev[g].uv_prev, r_host[g].uv_prev)

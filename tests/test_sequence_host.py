@@ -18,6 +18,11 @@ def test_se3_inverse(oracle):
         T = oracle.se3_exp(rng.normal(0, 0.5, 6))
         np.testing.assert_allclose(oracle.se3_mul(T, se3_inverse(T)), [0, 0, 0, 1, 0, 0, 0], atol=1e-12)
         np.testing.assert_allclose(se3_inverse(se3_inverse(T)), T, atol=1e-12)
+        # the window assembly's inverse is the oracle's (Sophus SE3d::inverse) bit for bit
+        np.testing.assert_array_equal(se3_inverse(T), oracle.se3_inverse(T))
+        Tn = T.copy()
+        Tn[:4] *= 1.0 + 1e-9  # an SE3 built from a not-quite-unit quaternion: the SO3 constructor renormalises
+        np.testing.assert_array_equal(se3_inverse(Tn), oracle.se3_inverse(Tn))
 
 
 def _records(oracle, n_frames, n_pts, noise, seed):

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kitti", default="")
     ap.add_argument("--out", default="")
+    ap.add_argument("--host-window", action="store_true",
+                    help="assemble the BA window on the host (the round-2 path) instead of on the device")
     args = ap.parse_args()
 
     import torch
@@ -68,7 +70,8 @@ def main():
     torch.cuda.synchronize()
 
     def run():
-        fe = SequenceFrontend(ctx, chunk, K, t_right, n_fixed=args.n_fixed, ba_iters=args.ba_iters, H=H, W=W)
+        fe = SequenceFrontend(ctx, chunk, K, t_right, n_fixed=args.n_fixed, ba_iters=args.ba_iters, H=H, W=W,
+                              device_window=not args.host_window)
         sec = {}
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -94,6 +97,8 @@ def main():
                     f"first {n} frames, 1 x MI355X",
         "data": data, "frames": n, "chunk_frames": chunk, "ba_window": chunk + args.n_fixed,
         "ba_fixed": args.n_fixed, "ba_iters": args.ba_iters,
+        "ba_window_assembly": "host (window_problem / apply_window, per-chunk read-back)" if args.host_window else
+        "device (yv_ba_window_*: records in HBM, graph built on the device, no per-chunk read-back)",
         "frames_per_s": round(n / times[best], 2), "seconds": round(times[best], 4),
         "seconds_all_repeats": [round(t, 4) for t in times],
         "phase_seconds": {k: round(v, 4) for k, v in secs[best].items()},

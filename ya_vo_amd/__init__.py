@@ -124,6 +124,12 @@ GEOM_SIGNATURES = {
     "yv_ba_debug_read": (_I, [_P, _I, _P, ctypes.c_int64]),
     "yv_ba_set_stream": (_I, [_P, _P]),
     "yv_ba_set_control": (_I, [_P, _I]),
+    "yv_ba_window_create": (_I, [_P, _I, _I, ctypes.POINTER(_P)]),
+    "yv_ba_window_destroy": (None, [_P]),
+    "yv_ba_window_add_block": (_I, [_P, _P, ctypes.c_int64, _I, _P, _P, _P, _I, _P]),
+    "yv_ba_window_solve": (_I, [_P, ctypes.c_int64, _I, _I, _P, _I, _P, _P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "yv_ba_window_read": (_I, [_P, ctypes.c_int64, _P, ctypes.POINTER(_I), _P, _P, _P, _P, _I]),
+    "yv_ba_window_trajectory": (_I, [_P, ctypes.c_int64, _I, _P]),
     "yv_lm_sum_mode": (_I, []),
 }
 
@@ -659,3 +665,60 @@ class BundleAdjuster:
         _check(self.lib.yv_ba_solve(self.handle, _ptr(poses), _ptr(X), max_iters, _ptr(log), ctypes.byref(it)),
                "yv_ba_solve")
         return poses, X, log[: it.value + 1], it.value
+
+
+class BaWindow:
+    """The chained front end's sliding BA window on the device (yv_ba_window_*; include/yavo/yavo_geom.h): frame
+    records from placed map blocks, the window graph built and solved by `ba` and written back in HBM."""
+
+    def __init__(self, ba: "BundleAdjuster", max_lm: int, max_kf: int):
+        self.ba, self.lib = ba, ba.lib
+        h = ctypes.c_void_p()
+        _check(self.lib.yv_ba_window_create(ba.handle, max_lm, max_kf, ctypes.byref(h)), "yv_ba_window_create")
+        self.handle, self.max_lm = h, max_lm
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.yv_ba_window_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_block(self, d_block: int, first_frame: int, n_frames: int, d_edge_uv: int, d_edge_query: int,
+                  d_matches: int, max_kp: int, stream: int = 0) -> None:
+        _check(self.lib.yv_ba_window_add_block(self.handle, ctypes.c_void_p(d_block), first_frame, n_frames,
+                                               ctypes.c_void_p(d_edge_uv), ctypes.c_void_p(d_edge_query),
+                                               ctypes.c_void_p(d_matches), max_kp,
+                                               ctypes.c_void_p(stream) if stream else None), "yv_ba_window_add_block")
+
+    def solve(self, first: int, n: int, n_fixed: int, K, max_iters: int, d_anchor: int = 0):
+        """-> (solved, chi2 log [iters + 1], iterations run)"""
+        K = _f64(K, (9,))
+        log = np.zeros(max_iters + 1)
+        it, ok = ctypes.c_int(0), ctypes.c_int(0)
+        _check(self.lib.yv_ba_window_solve(self.handle, first, n, n_fixed, _ptr(K), max_iters,
+                                           ctypes.c_void_p(d_anchor) if d_anchor else None, _ptr(log),
+                                           ctypes.byref(it), ctypes.byref(ok)), "yv_ba_window_solve")
+        return bool(ok.value), log[: it.value + 1], it.value
+
+    def read(self, frame: int):
+        """-> (T_wc [7], edge ids [n], X [n, 3], uv_own [n, 2], uv_prev [n, 2])"""
+        T = np.zeros(7)
+        e = np.zeros(self.max_lm, np.int32)
+        X = np.zeros((self.max_lm, 3))
+        uo = np.zeros((self.max_lm, 2))
+        up = np.zeros((self.max_lm, 2))
+        n = ctypes.c_int(0)
+        _check(self.lib.yv_ba_window_read(self.handle, frame, _ptr(T), ctypes.byref(n), _ptr(e), _ptr(X), _ptr(uo),
+                                          _ptr(up), self.max_lm), "yv_ba_window_read")
+        k = n.value
+        return T, e[:k].copy(), X[:k].copy(), uo[:k].copy(), up[:k].copy()
+
+    def trajectory(self, first: int, n: int) -> np.ndarray:
+        T = np.zeros((n, 7))
+        _check(self.lib.yv_ba_window_trajectory(self.handle, first, n, _ptr(T)), "yv_ba_window_trajectory")
+        return T

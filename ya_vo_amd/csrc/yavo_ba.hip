@@ -31,6 +31,7 @@
 
 #include "../../include/yavo/yavo.h"
 #include "../../include/yavo/yavo_geom.h"
+#include "../../include/yavo/yavo_map.h"
 #include "yavo_internal.h"
 #include "yavo_se3.h"
 
@@ -1275,7 +1276,10 @@ int ba_trial_slots() {
 // without waiting -- linearise, (iteration begin), per trial slot {backup, trial, decide, restore}, (iteration end)
 // -- and the one-lane ba_ctl_* kernels carry lambda, ni, currentChi and the stop / accept decisions in a device
 // control block that gates the other kernels.  One read-back per solve, plus one per suspended trial loop.
+// poses / landmarks: host in / out; both nullptr: the problem's poses and landmarks are already in Q.poses / Q.X on
+// the device (yv_ba_window_solve) and stay there.
 int ba_solve_device(yv_ba* b, double* poses, double* landmarks, int max_iters, double* chi2_log, int* iters) {
+    const bool host_io = poses != nullptr;
     yavo::BaParams& Q = b->P;
     const size_t pb = sizeof(double) * 7 * Q.P, xb = sizeof(double) * 3 * Q.L;
     hipStream_t st = b->st;
@@ -1292,8 +1296,8 @@ int ba_solve_device(yv_ba* b, double* poses, double* landmarks, int max_iters, d
     Pit.gate = &c->skip_iter;
     Ptr.gate = &c->skip_trial;
     Ptr.lam = &c->lambda;
-    if (hipMemcpyAsync(Q.poses, poses, pb, hipMemcpyHostToDevice, st) != hipSuccess ||
-        (xb && hipMemcpyAsync(Q.X, landmarks, xb, hipMemcpyHostToDevice, st) != hipSuccess))
+    if (host_io && (hipMemcpyAsync(Q.poses, poses, pb, hipMemcpyHostToDevice, st) != hipSuccess ||
+                    (xb && hipMemcpyAsync(Q.X, landmarks, xb, hipMemcpyHostToDevice, st) != hipSuccess)))
         return YV_ERR_HIP;
     yavo::launch_ba_chi2(Q, b->K, st);
     yavo::launch_ba_ctl_init(c, Q.scal, b->d_log, st);
@@ -1330,8 +1334,8 @@ int ba_solve_device(yv_ba* b, double* poses, double* landmarks, int max_iters, d
         resume = true;
     }
     const int n_it = max_iters > 0 ? b->h_ctl->iters : 0;
-    if (hipMemcpyAsync(poses, Q.poses, pb, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        (xb && hipMemcpyAsync(landmarks, Q.X, xb, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+    if ((host_io && (hipMemcpyAsync(poses, Q.poses, pb, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                     (xb && hipMemcpyAsync(landmarks, Q.X, xb, hipMemcpyDeviceToHost, st) != hipSuccess))) ||
         (chi2_log && hipMemcpyAsync(chi2_log, b->d_log, sizeof(double) * (n_it + 1), hipMemcpyDeviceToHost, st) != hipSuccess) ||
         hipStreamSynchronize(st) != hipSuccess)
         return YV_ERR_HIP;
@@ -1451,3 +1455,456 @@ extern "C" int yv_debug_ldlt_prof(unsigned long long* out) {
     return 0;
 }
 #endif
+
+// ------------------------------------------------------------------------------------------------
+// The sliding BA window of the chained stereo front end, assembled on the device (ya_vo_amd/sequence.py
+// window_problem / apply_window / frame_records_from_block, restated): frame records in HBM, the graph's index
+// arrays from per-frame counts (every landmark is seen by its own frame and the one before), no host round trip.
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+// Sophus SE3d::inverse on data() = {qx, qy, qz, qw, tx, ty, tz}: SO3(q*) renormalised, -t rotated as Eigen's
+// Quaternion * Vector3 (uv = 2 (q.vec x v); v + w uv + q.vec x uv): or_se3_inverse / ya_vo_amd/sequence.py
+// se3_inverse, operation for operation (no contraction: -ffp-contract=off; sqrt and / correctly rounded)
+__device__ void se3_inverse_dev(const double* T, double* o) {
+    double x = -T[0], y = -T[1], z = -T[2], w = T[3];
+    const double len = sqrt((x * x + z * z) + (y * y + w * w));  // the SO3 constructor's normalisation
+    x = x / len;
+    y = y / len;
+    z = z / len;
+    w = w / len;
+    const double vx = T[4] * -1.0, vy = T[5] * -1.0, vz = T[6] * -1.0;
+    double ux = y * vz - z * vy, uy = z * vx - x * vz, uz = x * vy - y * vx;
+    ux += ux;
+    uy += uy;
+    uz += uz;
+    const double cx = y * uz - z * uy, cy = z * ux - x * uz, cz = x * uy - y * ux;
+    o[0] = x;
+    o[1] = y;
+    o[2] = z;
+    o[3] = w;
+    o[4] = vx + w * ux + cx;
+    o[5] = vy + w * uy + cy;
+    o[6] = vz + w * uz + cz;
+}
+
+constexpr int kWinMaxPoses = 128;
+
+// one workgroup per keyframe of a placed block: its T_wc, landmarks and their two observations into the records
+__global__ __launch_bounds__(256) void win_add_kernel(const uint8_t* __restrict__ block, const double* __restrict__ edge_uv,
+                                                      const int32_t* __restrict__ edge_query,
+                                                      const uint8_t* __restrict__ matches, int max_kp, int64_t g0,
+                                                      int64_t cap, int max_lm, double* __restrict__ T, int32_t* __restrict__ cnt,
+                                                      int32_t* __restrict__ edge, double* __restrict__ X,
+                                                      double* __restrict__ uvo, double* __restrict__ uvp,
+                                                      int64_t* __restrict__ info) {
+    const yv_map_header* h = reinterpret_cast<const yv_map_header*>(block);
+    const int j = blockIdx.x;
+    if (j == 0 && threadIdx.x == 0) info[0] = h->n_kf;
+    if (j >= h->n_kf) return;
+    const yv_keyframe* kf = reinterpret_cast<const yv_keyframe*>(block + sizeof(yv_map_header)) + j;
+    const int64_t lmo = ((int64_t)sizeof(yv_map_header) + (int64_t)h->max_kf * (int64_t)sizeof(yv_keyframe) + 255) & ~255ll;
+    const yv_landmark* lm = reinterpret_cast<const yv_landmark*>(block + lmo) + (int64_t)j * h->lm_stride;
+    const int64_t g = kf->frame_id, s = g - g0;
+    const int64_t k64 = g - h->first_frame;
+    if (s < 0 || s >= cap || k64 < 0 || k64 >= h->n_frames) return;  // not a frame of the reserved range
+    const int k = (int)k64;
+    const int n = min(kf->n_landmarks, max_lm);
+    if (threadIdx.x < 7) T[s * 7 + threadIdx.x] = kf->T[threadIdx.x];
+    if (threadIdx.x == 0) {
+        cnt[s] = n;
+        info[1 + 2 * j] = g;
+        info[2 + 2 * j] = n;
+    }
+    for (int l = threadIdx.x; l < n; l += 256) {
+        const int e = (int)(lm[l].id & 0xFFFF);
+        const int64_t o = s * max_lm + l;
+        edge[o] = e;
+        X[3 * o] = lm[l].X[0];
+        X[3 * o + 1] = lm[l].X[1];
+        X[3 * o + 2] = lm[l].X[2];
+        const int64_t ke = (int64_t)k * max_kp + e;
+        uvp[2 * o] = edge_uv[2 * ke];
+        uvp[2 * o + 1] = edge_uv[2 * ke + 1];
+        const int q = edge_query[ke];
+        const uint8_t* rec = matches + ((int64_t)(2 * k) * max_kp + q) * 100;  // the temporal pair's Matches
+        int32_t px[2];
+        __builtin_memcpy(px, rec + 48, 8);  // Matches::pt2 {x, y}
+        uvo[2 * o] = (double)px[0];
+        uvo[2 * o + 1] = (double)px[1];
+    }
+}
+
+struct WinFrames {
+    int P;
+    int64_t s0;                   // store index of the window's first frame
+    int32_t c[kWinMaxPoses];      // landmarks owned by pose i (0 for the first pose)
+    int32_t base[kWinMaxPoses];   // their first landmark index
+    int32_t pe0[kWinMaxPoses];    // pe_off of pose i
+    int32_t row[kWinMaxPoses];    // first co-visibility entry of row p1 = i
+};
+
+// the graph of window_problem: poses (T_cw = inverse T_wc), landmarks, edges (own frame, then the frame before),
+// edges per pose / landmark and the co-visibility lists, each entry written by its landmark's thread
+__global__ __launch_bounds__(256) void win_build_kernel(WinFrames F, int L, int max_lm, const double* __restrict__ T,
+                                                        const double* __restrict__ Xs, const double* __restrict__ uvo,
+                                                        const double* __restrict__ uvp, double* __restrict__ poses,
+                                                        double* __restrict__ X, int32_t* __restrict__ ep,
+                                                        int32_t* __restrict__ el, double* __restrict__ meas,
+                                                        int32_t* __restrict__ le_off, int32_t* __restrict__ le,
+                                                        int32_t* __restrict__ pe, int32_t* __restrict__ cv1,
+                                                        int32_t* __restrict__ cv2) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t < F.P) se3_inverse_dev(T + (F.s0 + t) * 7, poses + 7 * t);
+    if (t == 0) le_off[L] = 2 * L;
+    if (t >= L) return;
+    int i = 1;  // the owning pose: base[i] <= t < base[i] + c[i]
+    while (i + 1 < F.P && t >= F.base[i + 1]) ++i;
+    while (F.c[i] == 0 || t >= F.base[i] + F.c[i]) ++i;
+    const int j = t - F.base[i];
+    const int64_t o = (F.s0 + i) * max_lm + j;
+    X[3 * t] = Xs[3 * o];
+    X[3 * t + 1] = Xs[3 * o + 1];
+    X[3 * t + 2] = Xs[3 * o + 2];
+    const int own = 2 * F.base[i] + j, prev = 2 * F.base[i] + F.c[i] + j;
+    ep[own] = i;
+    ep[prev] = i - 1;
+    el[own] = t;
+    el[prev] = t;
+    meas[2 * own] = uvo[2 * o];
+    meas[2 * own + 1] = uvo[2 * o + 1];
+    meas[2 * prev] = uvp[2 * o];
+    meas[2 * prev + 1] = uvp[2 * o + 1];
+    le_off[t] = 2 * t;
+    le[2 * t] = own;
+    le[2 * t + 1] = prev;
+    // pose i: its own edges first; pose i - 1: its own edges, then frame i's prev edges
+    pe[F.pe0[i] + j] = own;
+    pe[F.pe0[i - 1] + F.c[i - 1] + j] = prev;
+    // (i, i): frame i's (own, own) first, frame i + 1's (prev, prev) after; (i - 1, i - 1) likewise;
+    // (i - 1, i): frame i's (prev, own)
+    cv1[F.row[i] + j] = own;
+    cv2[F.row[i] + j] = own;
+    const int r = F.row[i - 1] + F.c[i - 1];
+    cv1[r + j] = prev;
+    cv2[r + j] = prev;
+    cv1[r + F.c[i] + j] = prev;
+    cv2[r + F.c[i] + j] = own;
+}
+
+// apply_window: T_wc = inverse(T_cw) for every window frame, refined landmarks back to their frames, the anchor
+__global__ __launch_bounds__(256) void win_scatter_kernel(WinFrames F, int L, int max_lm, const double* __restrict__ poses,
+                                                          const double* __restrict__ X, double* __restrict__ T,
+                                                          double* __restrict__ Xs, double* __restrict__ anchor) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t < F.P) {
+        double o[7];
+        se3_inverse_dev(poses + 7 * t, o);
+        for (int k = 0; k < 7; ++k) T[(F.s0 + t) * 7 + k] = o[k];
+        if (anchor && t == F.P - 1)
+            for (int k = 0; k < 7; ++k) anchor[k] = o[k];
+    }
+    if (t >= L) return;
+    int i = 1;
+    while (i + 1 < F.P && t >= F.base[i + 1]) ++i;
+    while (F.c[i] == 0 || t >= F.base[i] + F.c[i]) ++i;
+    const int64_t o = (F.s0 + i) * max_lm + (t - F.base[i]);
+    Xs[3 * o] = X[3 * t];
+    Xs[3 * o + 1] = X[3 * t + 1];
+    Xs[3 * o + 2] = X[3 * t + 2];
+}
+
+__global__ void win_anchor_kernel(const double* __restrict__ T, double* __restrict__ anchor) {
+    if (threadIdx.x < 7) anchor[threadIdx.x] = T[threadIdx.x];
+}
+
+}  // namespace
+
+struct yv_ba_window {
+    yv_ba* ba = nullptr;
+    int max_lm = 0, max_kf = 0;
+    int64_t g0 = -1, cap = 0;  // store index 0 = frame g0; frames [g0, g0 + cap) fit
+    double *d_T = nullptr, *d_X = nullptr, *d_uvo = nullptr, *d_uvp = nullptr;
+    int32_t *d_cnt = nullptr, *d_edge = nullptr;
+    int64_t* d_info = nullptr;  // [1 + 2 max_kf]: n_kf, (frame, count) per keyframe of the last block
+    int64_t* h_info = nullptr;  // pinned copy
+    hipEvent_t added = nullptr;
+    bool add_pending = false;
+    std::vector<int32_t> h_cnt;  // per store index, -1 = not recorded
+    int32_t* h_struct = nullptr;  // pinned: pe_off [P + 1], cv_off [P P + 1]
+    size_t h_struct_cap = 0;
+};
+
+namespace {
+
+void win_free_store(yv_ba_window* w) {
+    for (void* p : {(void*)w->d_T, (void*)w->d_X, (void*)w->d_uvo, (void*)w->d_uvp, (void*)w->d_cnt, (void*)w->d_edge})
+        if (p) (void)hipFree(p);
+    w->d_T = w->d_X = w->d_uvo = w->d_uvp = nullptr;
+    w->d_cnt = w->d_edge = nullptr;
+}
+
+// the store covers frames [g0, end): grown by doubling, the recorded frames copied over (stream-ordered)
+int win_reserve(yv_ba_window* w, int64_t first, int64_t end, hipStream_t st) {
+    if (w->g0 < 0) w->g0 = first;
+    if (first < w->g0) return YV_ERR_INVALID;
+    if (end - w->g0 <= w->cap) return YV_OK;
+    int64_t cap = std::max<int64_t>(64, w->cap);
+    while (cap < end - w->g0) cap *= 2;
+    const int64_t M = w->max_lm;
+    double *T = nullptr, *X = nullptr, *uvo = nullptr, *uvp = nullptr;
+    int32_t *cnt = nullptr, *edge = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&T), sizeof(double) * 7 * cap) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&X), sizeof(double) * 3 * M * cap) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&uvo), sizeof(double) * 2 * M * cap) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&uvp), sizeof(double) * 2 * M * cap) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&cnt), sizeof(int32_t) * cap) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&edge), sizeof(int32_t) * M * cap) != hipSuccess) {
+        for (void* p : {(void*)T, (void*)X, (void*)uvo, (void*)uvp, (void*)cnt, (void*)edge})
+            if (p) (void)hipFree(p);
+        return YV_ERR_HIP;
+    }
+    const int64_t c0 = w->cap;
+    bool ok = true;
+    if (c0 > 0) {
+        ok = hipMemcpyAsync(T, w->d_T, sizeof(double) * 7 * c0, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+             hipMemcpyAsync(X, w->d_X, sizeof(double) * 3 * M * c0, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+             hipMemcpyAsync(uvo, w->d_uvo, sizeof(double) * 2 * M * c0, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+             hipMemcpyAsync(uvp, w->d_uvp, sizeof(double) * 2 * M * c0, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+             hipMemcpyAsync(cnt, w->d_cnt, sizeof(int32_t) * c0, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+             hipMemcpyAsync(edge, w->d_edge, sizeof(int32_t) * M * c0, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+             hipStreamSynchronize(st) == hipSuccess;
+    }
+    win_free_store(w);
+    w->d_T = T;
+    w->d_X = X;
+    w->d_uvo = uvo;
+    w->d_uvp = uvp;
+    w->d_cnt = cnt;
+    w->d_edge = edge;
+    w->cap = cap;
+    w->h_cnt.resize((size_t)cap, -1);
+    return ok ? YV_OK : YV_ERR_HIP;
+}
+
+// the last add's keyframe counts are on the host
+int win_collect(yv_ba_window* w) {
+    if (!w->add_pending) return YV_OK;
+    if (hipEventSynchronize(w->added) != hipSuccess) return YV_ERR_HIP;
+    w->add_pending = false;
+    const int64_t n = std::min<int64_t>(w->h_info[0], w->max_kf);
+    for (int64_t j = 0; j < n; ++j) {
+        const int64_t s = w->h_info[1 + 2 * j] - w->g0;
+        if (s >= 0 && s < w->cap) w->h_cnt[(size_t)s] = (int32_t)w->h_info[2 + 2 * j];
+    }
+    return YV_OK;
+}
+
+}  // namespace
+
+extern "C" int yv_ba_window_create(yv_ba* ba, int max_lm, int max_kf, yv_ba_window** out) {
+    if (!out) return YV_ERR_INVALID;
+    *out = nullptr;
+    if (!ba || max_lm < 1 || max_lm > 65536 || max_kf < 1) return YV_ERR_INVALID;
+    if (hipSetDevice(ba->dev) != hipSuccess) return YV_ERR_HIP;
+    yv_ba_window* w = new yv_ba_window();
+    w->ba = ba;
+    w->max_lm = max_lm;
+    w->max_kf = max_kf;
+    if (hipMalloc(reinterpret_cast<void**>(&w->d_info), sizeof(int64_t) * (1 + 2 * (size_t)max_kf)) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&w->h_info), sizeof(int64_t) * (1 + 2 * (size_t)max_kf)) != hipSuccess ||
+        hipEventCreateWithFlags(&w->added, hipEventDisableTiming) != hipSuccess) {
+        yv_ba_window_destroy(w);
+        return YV_ERR_HIP;
+    }
+    *out = w;
+    return YV_OK;
+}
+
+extern "C" void yv_ba_window_destroy(yv_ba_window* w) {
+    if (!w) return;
+    (void)hipSetDevice(w->ba->dev);
+    if (w->added) {
+        (void)hipEventSynchronize(w->added);
+        (void)hipEventDestroy(w->added);
+    }
+    (void)hipStreamSynchronize(w->ba->st);
+    win_free_store(w);
+    if (w->d_info) (void)hipFree(w->d_info);
+    if (w->h_info) (void)hipHostFree(w->h_info);
+    if (w->h_struct) (void)hipHostFree(w->h_struct);
+    delete w;
+}
+
+extern "C" int yv_ba_window_add_block(yv_ba_window* w, const void* d_block, int64_t first_frame, int n_frames,
+                                      const double* d_edge_uv, const int32_t* d_edge_query, const void* d_matches,
+                                      int max_kp, void* stream) {
+    if (!w || !d_block || !d_edge_uv || !d_edge_query || !d_matches || n_frames < 1 || first_frame < 0 ||
+        max_kp < 1 || max_kp > 65536)
+        return YV_ERR_INVALID;
+    if (hipSetDevice(w->ba->dev) != hipSuccess) return YV_ERR_HIP;
+    hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : yavo::ctx_stream(w->ba->ctx);
+    if (win_collect(w) != YV_OK) return YV_ERR_HIP;  // one block in flight: its info buffer is reused
+    const int rc = win_reserve(w, first_frame, first_frame + n_frames, st);
+    if (rc != YV_OK) return rc;
+    hipLaunchKernelGGL(win_add_kernel, dim3(w->max_kf), dim3(256), 0, st, reinterpret_cast<const uint8_t*>(d_block),
+                       d_edge_uv, d_edge_query, reinterpret_cast<const uint8_t*>(d_matches), max_kp, w->g0, w->cap,
+                       w->max_lm,
+                       w->d_T, w->d_cnt, w->d_edge, w->d_X, w->d_uvo, w->d_uvp, w->d_info);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(w->h_info, w->d_info, sizeof(int64_t) * (1 + 2 * (size_t)w->max_kf), hipMemcpyDeviceToHost,
+                       st) != hipSuccess ||
+        hipEventRecord(w->added, st) != hipSuccess)
+        return YV_ERR_HIP;
+    w->add_pending = true;
+    return YV_OK;
+}
+
+extern "C" int yv_ba_window_solve(yv_ba_window* w, int64_t first, int n, int n_fixed, const double K[9], int max_iters,
+                                  double* d_anchor, double* chi2_log, int* iters, int* solved) {
+    if (!w || !K || n < 1 || n > kWinMaxPoses || n_fixed < 0 || max_iters < 0) return YV_ERR_INVALID;
+    for (int i = 0; i < 9; ++i)
+        if (!std::isfinite(K[i])) return YV_ERR_INVALID;
+    yv_ba* b = w->ba;
+    if (hipSetDevice(b->dev) != hipSuccess || win_collect(w) != YV_OK) return YV_ERR_HIP;
+    if (first < w->g0 || first + n > w->g0 + w->cap) return YV_ERR_INVALID;
+    WinFrames F{};
+    F.P = n;
+    F.s0 = first - w->g0;
+    int L = 0;
+    for (int i = 0; i < n; ++i) {
+        const int32_t c = w->h_cnt[(size_t)(F.s0 + i)];
+        if (c < 0) return YV_ERR_INVALID;  // frame not recorded
+        F.c[i] = i == 0 ? 0 : c;           // the first frame's predecessor is outside the window
+        F.base[i] = L;
+        L += F.c[i];
+    }
+    if (iters) *iters = 0;
+    if (solved) *solved = 0;
+    hipStream_t st = b->st;
+    if (n <= n_fixed || L == 0) {  // nothing to solve: the anchor is the last frame's pose as recorded
+        if (d_anchor) {
+            hipLaunchKernelGGL(win_anchor_kernel, dim3(1), dim3(64), 0, st, w->d_T + (F.s0 + n - 1) * 7, d_anchor);
+            if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
+        }
+        return YV_OK;
+    }
+    const int E = 2 * L;
+    const int64_t nc = 3 * (int64_t)L;
+    if (n > b->max_poses || L > b->max_landmarks || E > b->max_edges) return YV_ERR_CAPACITY;
+    // per pose: pe_off (own edges of frame p, then the prev edges of frame p + 1); per row p1 of the co-visibility
+    // buckets: (p1, p1) = c[p1] + c[p1 + 1] entries, (p1, p1 + 1) = c[p1 + 1]
+    const size_t need = (size_t)(n + 1) + (size_t)n * n + 1;
+    if (need > w->h_struct_cap) {
+        if (hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
+        if (w->h_struct) (void)hipHostFree(w->h_struct);
+        w->h_struct = nullptr;
+        w->h_struct_cap = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&w->h_struct), sizeof(int32_t) * need) != hipSuccess)
+            return YV_ERR_HIP;
+        w->h_struct_cap = need;
+    }
+    int32_t* pe_off = w->h_struct;
+    int32_t* cv_off = w->h_struct + n + 1;
+    int32_t acc = 0, racc = 0;
+    for (int p = 0; p < n; ++p) {
+        const int32_t cn = p + 1 < n ? F.c[p + 1] : 0;
+        pe_off[p] = acc;
+        F.pe0[p] = acc;
+        acc += F.c[p] + cn;
+        F.row[p] = racc;
+        racc += F.c[p] + 2 * cn;
+    }
+    pe_off[n] = acc;
+    cv_off[0] = 0;
+    for (int p1 = 0; p1 < n; ++p1) {
+        const int32_t cn = p1 + 1 < n ? F.c[p1 + 1] : 0;
+        int32_t r = F.row[p1];
+        for (int p2 = 0; p2 < n; ++p2) {
+            if (p2 == p1) r += F.c[p1] + cn;
+            else if (p2 == p1 + 1) r += cn;
+            cv_off[(int64_t)p1 * n + p2 + 1] = r;
+        }
+    }
+    if (nc > b->cv_cap) {
+        if (hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
+        ba_free_one(b, b->d_cv_e1);
+        ba_free_one(b, b->d_cv_e2);
+        b->d_cv_e1 = b->d_cv_e2 = nullptr;
+        b->cv_cap = 0;
+        if (ba_alloc(b, &b->d_cv_e1, nc) != YV_OK || ba_alloc(b, &b->d_cv_e2, nc) != YV_OK) return YV_ERR_HIP;
+        b->cv_cap = nc;
+    }
+    b->ready = false;
+    yavo::BaParams& Q = b->P;
+    if (hipMemcpyAsync(b->d_pe_off, pe_off, sizeof(int32_t) * (n + 1), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(b->d_cv_off, cv_off, sizeof(int32_t) * ((size_t)n * n + 1), hipMemcpyHostToDevice, st) !=
+            hipSuccess)
+        return YV_ERR_HIP;
+    const int nb = (std::max(L, n) + 255) / 256;
+    hipLaunchKernelGGL(win_build_kernel, dim3(nb), dim3(256), 0, st, F, L, w->max_lm, w->d_T, w->d_X, w->d_uvo,
+                       w->d_uvp, Q.poses, Q.X, b->d_ep, b->d_el, b->d_meas, b->d_le_off, b->d_le, b->d_pe, b->d_cv_e1,
+                       b->d_cv_e2);
+    if (hipGetLastError() != hipSuccess) return YV_ERR_HIP;
+    Q.P = n;
+    Q.nf = n_fixed;
+    Q.np = n - n_fixed;
+    Q.ns = 6 * Q.np;
+    Q.L = L;
+    Q.E = E;
+    Q.ep = b->d_ep;
+    Q.el = b->d_el;
+    Q.meas = b->d_meas;
+    Q.pe_off = b->d_pe_off;
+    Q.pe = b->d_pe;
+    Q.le_off = b->d_le_off;
+    Q.le = b->d_le;
+    Q.cv_off = b->d_cv_off;
+    Q.cv_e1 = b->d_cv_e1;
+    Q.cv_e2 = b->d_cv_e2;
+    std::memcpy(b->K.v, K, sizeof b->K.v);
+    b->ready = true;
+    int it = 0;
+    const int rc = ba_solve_device(b, nullptr, nullptr, max_iters, chi2_log, &it);
+    if (rc != YV_OK) return rc;
+    hipLaunchKernelGGL(win_scatter_kernel, dim3(nb), dim3(256), 0, st, F, L, w->max_lm, Q.poses, Q.X, w->d_T, w->d_X,
+                       d_anchor);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
+    if (iters) *iters = it;
+    if (solved) *solved = 1;
+    return YV_OK;
+}
+
+extern "C" int yv_ba_window_read(yv_ba_window* w, int64_t frame, double* T_wc, int* n, int32_t* edge, double* X,
+                                 double* uv_own, double* uv_prev, int cap) {
+    if (!w || !n) return YV_ERR_INVALID;
+    if (hipSetDevice(w->ba->dev) != hipSuccess || win_collect(w) != YV_OK) return YV_ERR_HIP;
+    const int64_t s = frame - w->g0;
+    if (w->g0 < 0 || s < 0 || s >= w->cap || w->h_cnt[(size_t)s] < 0) return YV_ERR_INVALID;
+    hipStream_t st = w->ba->st;
+    const int m = w->h_cnt[(size_t)s];
+    *n = m;
+    if (hipStreamSynchronize(yavo::ctx_stream(w->ba->ctx)) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+        return YV_ERR_HIP;
+    const int k = std::min(m, cap);
+    const int64_t o = s * w->max_lm;
+    if ((T_wc && hipMemcpy(T_wc, w->d_T + 7 * s, sizeof(double) * 7, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (edge && k && hipMemcpy(edge, w->d_edge + o, sizeof(int32_t) * k, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (X && k && hipMemcpy(X, w->d_X + 3 * o, sizeof(double) * 3 * k, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (uv_own && k && hipMemcpy(uv_own, w->d_uvo + 2 * o, sizeof(double) * 2 * k, hipMemcpyDeviceToHost) != hipSuccess) ||
+        (uv_prev && k && hipMemcpy(uv_prev, w->d_uvp + 2 * o, sizeof(double) * 2 * k, hipMemcpyDeviceToHost) != hipSuccess))
+        return YV_ERR_HIP;
+    return YV_OK;
+}
+
+extern "C" int yv_ba_window_trajectory(yv_ba_window* w, int64_t first, int n, double* T_wc) {
+    if (!w || !T_wc || n < 0) return YV_ERR_INVALID;
+    if (hipSetDevice(w->ba->dev) != hipSuccess || win_collect(w) != YV_OK) return YV_ERR_HIP;
+    if (n == 0) return YV_OK;
+    if (first < w->g0 || first + n > w->g0 + w->cap) return YV_ERR_INVALID;
+    if (hipStreamSynchronize(yavo::ctx_stream(w->ba->ctx)) != hipSuccess ||
+        hipStreamSynchronize(w->ba->st) != hipSuccess ||
+        hipMemcpy(T_wc, w->d_T + 7 * (first - w->g0), sizeof(double) * 7 * n, hipMemcpyDeviceToHost) != hipSuccess)
+        return YV_ERR_HIP;
+    return YV_OK;
+}

@@ -16,23 +16,30 @@ tests/sequence_chain.py restates the same loop over the CPU oracle for the traje
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Tuple
 
 import numpy as np
 
 from . import map as ymap
-from .scene import quat_to_R
 
 IDENTITY = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
 
 
 def se3_inverse(T) -> np.ndarray:
-    """Sophus SE3d::inverse on data() = {qx, qy, qz, qw, tx, ty, tz}: q* and -R^T t."""
-    T = np.asarray(T, np.float64)
-    q = np.array([-T[0], -T[1], -T[2], T[3]])
-    t = -(quat_to_R(T[:4]).T @ T[4:])
-    return np.concatenate([q, t])
+    """Sophus SE3d::inverse on data() = {qx, qy, qz, qw, tx, ty, tz}: SO3(q*) (renormalised by the SO3 constructor,
+    |q| summed as Eigen's squaredNorm pairs it) and that rotation applied to -t as Eigen's Quaternion * Vector3 does
+    (uv = 2 (q.vec x v); v + w uv + q.vec x uv) -- oracle/yavo_oracle_geom.c or_se3_inverse's arithmetic, in scalar
+    IEEE doubles, which the device restatement (yavo_ba.hip se3_inverse_dev, no contraction) repeats bit for bit."""
+    x, y, z, w = -float(T[0]), -float(T[1]), -float(T[2]), float(T[3])
+    n = math.sqrt((x * x + z * z) + (y * y + w * w))
+    x, y, z, w = x / n, y / n, z / n, w / n
+    vx, vy, vz = float(T[4]) * -1.0, float(T[5]) * -1.0, float(T[6]) * -1.0
+    ux, uy, uz = y * vz - z * vy, z * vx - x * vz, x * vy - y * vx
+    ux, uy, uz = ux + ux, uy + uy, uz + uz
+    cx, cy, cz = y * uz - z * uy, z * ux - x * uz, x * uy - y * ux
+    return np.array([x, y, z, w, vx + w * ux + cx, vy + w * uy + cy, vz + w * uz + cz])
 
 
 @dataclass
@@ -105,9 +112,12 @@ class SequenceFrontend:
     """The device front end over a stereo sequence in chunks of `chunk` frames (module docstring)."""
 
     def __init__(self, ctx, chunk: int, K, T_right, n_fixed: int = 2, ba_iters: int = 10,
-                 H: int = 376, W: int = 1241, max_kp: int = 2000, match_thr: int = 20):
+                 H: int = 376, W: int = 1241, max_kp: int = 2000, match_thr: int = 20, device_window: bool = True):
+        """device_window: the BA window is recorded, assembled and written back on the device (yv_ba_window_*,
+        no per-chunk read-back); False: the host assembly below (window_problem / apply_window), kept as the
+        restatement the device path is checked against."""
         import torch
-        from . import Batch, BundleAdjuster
+        from . import Batch, BaWindow, BundleAdjuster
         if chunk < 2 or n_fixed < 1:
             raise ValueError("bad chunk / n_fixed")
         window = chunk + n_fixed
@@ -141,14 +151,29 @@ class SequenceFrontend:
         self.ba_stream = torch.cuda.Stream(device=dev)  # the BA beside the next chunk's kernels
         self.ba.set_stream(self.ba_stream.cuda_stream)
         self._ba_pending = False
-        self.records: Dict[int, FrameRecord] = {}
+        self.device_window = device_window
+        self.win = BaWindow(self.ba, max_kp, chunk) if device_window else None
+        self._records: Dict[int, FrameRecord] = {}
         self.next_frame = 0
         self.ba_log: List[Tuple[int, int, float, float]] = []  # (last frame, iterations, chi2 first, chi2 last)
 
     def close(self) -> None:
+        if self.win is not None:
+            self.win.close()
         self.ba.set_stream(0)
         self.ba.close()
         self.batch.close()
+
+    @property
+    def records(self) -> Dict[int, FrameRecord]:
+        """frame -> FrameRecord (device window: read back from the records in HBM, as they stand)."""
+        if self.win is None:
+            return self._records
+        out = {}
+        for g in range(self.next_frame):
+            T, e, X, uo, up = self.win.read(g)
+            out[g] = FrameRecord(T, e.astype(np.int64), X, up, uo)
+        return out
 
     def process_chunk(self, d_images, seconds: Dict[str, float] = None) -> None:
         """d_images: device uint8 [2 * chunk, H, W] (L_k, R_k interleaved) of frames next_frame ...
@@ -163,6 +188,8 @@ class SequenceFrontend:
         self.batch.run(d_images.data_ptr(), 2 * n, self.W, self.H * self.W, self.match_thr,
                        carry_from=2 * (n - 1))
         self.batch.track_map(self.d_prior.data_ptr(), self.d_poses.data_ptr(), first, 1, self.d_block.data_ptr(), n)
+        if self.win is not None:
+            return self._process_chunk_device(first, t0, seconds)
         t1 = time.perf_counter()
         ba_sec = {}
         if self._ba_pending:
@@ -177,7 +204,7 @@ class SequenceFrontend:
         q = ctx.download(v.edge_query, np.int32, n * kp, out=self._h_q).reshape(n, kp)
         m = ctx.download(v.matches, np.uint8, 2 * n * kp * 100, out=self._h_m).reshape(2 * n, kp, 100)[0::2]
         own = m[:, :, 48:56].copy().view(np.int32).reshape(n, kp, 2)  # Matches::pt2.{x, y}
-        self.records.update(frame_records_from_block(block, uv, q, own))
+        self._records.update(frame_records_from_block(block, uv, q, own))
         self.next_frame = first + n
         self._ba_pending = True
         t4 = time.perf_counter()
@@ -187,10 +214,44 @@ class SequenceFrontend:
             for key, dt in ba_sec.items():
                 seconds[key] = seconds.get(key, 0.0) + dt
 
+    def _process_chunk_device(self, first: int, t0: float, seconds) -> None:
+        """process_chunk with the device window: the previous window's BA (its stream; the host waits for its result,
+        the anchor lands in d_base), this chunk's placement after it, then the chunk's frames recorded from the placed
+        block -- no read-back."""
+        import time
+        ctx, n = self.ctx, self.chunk
+        t1 = time.perf_counter()
+        if self._ba_pending:
+            self._local_ba_device()
+        t2 = time.perf_counter()
+        ctx.map_place(self.d_block.data_ptr(), 1, self.bb, self.d_base.data_ptr(), self.d_anchors.data_ptr())
+        v = self.batch.view()
+        self.win.add_block(self.d_block.data_ptr(), first, n, v.edge_uv, v.edge_query, v.matches, self.max_kp)
+        self.next_frame = first + n
+        self._ba_pending = True
+        t3 = time.perf_counter()
+        if seconds is not None:
+            for key, dt in (("issue", t1 - t0), ("ba", t2 - t1), ("place_record", t3 - t2)):
+                seconds[key] = seconds.get(key, 0.0) + dt
+
+    def _local_ba_device(self) -> None:
+        self._ba_pending = False
+        last = self.next_frame - 1
+        lo = max(0, last - self.window + 1)
+        solved, log, it = self.win.solve(lo, last + 1 - lo, self.n_fixed, self.K, self.ba_iters,
+                                         self.d_base.data_ptr())
+        if solved:
+            self.ba_log.append((last, it, float(log[0]), float(log[-1])))
+
     def flush(self, seconds: Dict[str, float] = None) -> None:
         """The last chunk's BA window (process_chunk runs each window one chunk late)."""
         import time
-        if self._ba_pending:
+        if self._ba_pending and self.win is not None:
+            t0 = time.perf_counter()
+            self._local_ba_device()
+            if seconds is not None:
+                seconds["ba"] = seconds.get("ba", 0.0) + time.perf_counter() - t0
+        elif self._ba_pending:
             t0 = time.perf_counter()
             ba_sec = {}
             self._local_ba(ba_sec)
@@ -207,7 +268,7 @@ class SequenceFrontend:
         if len(frames) <= self.n_fixed:
             return
         t0 = time.perf_counter()
-        poses, X, ep, el, meas, owners = window_problem(self.records, frames, self.n_fixed)
+        poses, X, ep, el, meas, owners = window_problem(self._records, frames, self.n_fixed)
         if len(ep) == 0:
             return
         t1 = time.perf_counter()
@@ -215,15 +276,17 @@ class SequenceFrontend:
         t2 = time.perf_counter()
         poses, X, log, it = self.ba.solve(poses, X, self.ba_iters)
         t3 = time.perf_counter()
-        apply_window(self.records, frames, poses, X, owners)
+        apply_window(self._records, frames, poses, X, owners)
         sec["ba_assemble"] = t1 - t0 + time.perf_counter() - t3
         sec["ba_set_problem"] = t2 - t1
         sec["ba_solve"] = t3 - t2
         self.ba_log.append((last, it, float(log[0]), float(log[-1])))
         # the next chunk is placed after the refined last pose
-        self.ctx.upload(self.d_base.data_ptr(), self.records[last].T_wc)
+        self.ctx.upload(self.d_base.data_ptr(), self._records[last].T_wc)
 
     def trajectory(self) -> np.ndarray:
         """[n_frames, 7] T_wc in frame order (after the last BA window)."""
         self.flush()
-        return np.stack([self.records[g].T_wc for g in sorted(self.records)])
+        if self.win is not None:
+            return self.win.trajectory(0, self.next_frame)
+        return np.stack([self._records[g].T_wc for g in sorted(self._records)])
