@@ -196,3 +196,40 @@ def test_frame_shard_lk_halo_tracks_the_boundary_pair(ctx, oracle, offsets):
         T = lk_track_pose(oracle, seq[k][0], seq[k + 1][0], kps[k][0], kps[k][1], scene.K_KITTI, T_RIGHT)[3]
         np.testing.assert_array_equal(P[k], T, err_msg=f"track {k}")
     shard.close()
+
+
+def test_lk_overlap_pipelined_matches_serial(ctx):
+    """LK mode with the asynchronous build (overlap on): the LK stage of step i runs beside step i + 1's run, its
+    stereo points in the other of two point sets; every step's poses equal the serial mode's bit for bit."""
+    import torch
+    n_frames, steps = 3, 4
+    frames = [np.stack([im for k in range(n_frames) for im in (synth_frame(91 + s, k, 3 * k), synth_frame(91 + s, k, 3 * k + 8))])
+              for s in range(steps)]
+    d = [torch.from_numpy(f).to("cuda:0") for f in frames]
+    tracks = [(2 * (k - 1) + 1, 2 * k) for k in range(1, n_frames)]
+    nt = len(tracks)
+    out = []
+    for overlap in (0, 1):
+        b = yv.Batch(ctx, 2 * n_frames, H, W, 2000, 2 * n_frames)
+        carry = 2 * n_frames
+        pairs = []
+        for k in range(n_frames):
+            pairs.append((carry if k == 0 else 2 * (k - 1), 2 * k))
+            pairs.append((2 * k, 2 * k + 1))
+        b.set_pairs(pairs)
+        b.set_track_lk(2)
+        b.set_tracks(tracks, scene.K_KITTI, T_RIGHT)
+        b.set_track_overlap(overlap)
+        d_prior = torch.from_numpy(np.tile(IDENTITY, (nt, 1))).to("cuda:0")
+        poses = [torch.zeros((nt, 7), dtype=torch.float64, device="cuda:0") for _ in range(steps)]
+        torch.cuda.synchronize()
+        for s in range(steps):
+            b.run(d[s].data_ptr(), 2 * n_frames, W, H * W, 20)
+            b.track(d_prior.data_ptr(), poses[s].data_ptr())
+        b.track_sync()
+        ctx.sync()
+        torch.cuda.synchronize()
+        out.append(np.stack([p.cpu().numpy() for p in poses]))
+        b.close()
+    assert np.all(np.isfinite(out[0])) and np.abs(out[0][:, :, 4]).max() > 0.01
+    np.testing.assert_array_equal(out[1], out[0])

@@ -111,6 +111,11 @@ struct yv_batch {
     uint8_t* lk_status = nullptr;
     int32_t* lk_q = nullptr;
     int32_t* lk_count = nullptr;
+    // lk_X / lk_pts / lk_q / lk_count come in two sets: with the asynchronous build (overlap mode) the LK stage of
+    // track i reads set i & 1 on bstream while track i + 1's stereo points fill the other one on the run's stream
+    int lk_set = 0;
+    hipEvent_t ev_lk[2] = {};
+    bool lk_ev_pending[2] = {false, false};
     const uint8_t* run_images = nullptr;  // the last yv_batch_run's images (LK reads them)
     int run_n = 0, run_stride = 0;
     int64_t run_pitch = 0;
@@ -229,6 +234,8 @@ void batch_free(yv_batch* b) {
     if (b->ev_map_release) (void)hipEventDestroy(b->ev_map_release);
     if (b->ev_fin) (void)hipEventDestroy(b->ev_fin);
     if (b->ev_built) (void)hipEventDestroy(b->ev_built);
+    for (hipEvent_t e : b->ev_lk)
+        if (e) (void)hipEventDestroy(e);
     if (b->bstream) (void)hipStreamDestroy(b->bstream);
     if (b->side) (void)hipStreamDestroy(b->side);
     delete b;
@@ -763,13 +770,14 @@ int yv_batch_set_tracks(yv_batch* b, const int32_t* tracks, int n_tracks, const 
         b->lk_status = nullptr;
         rc |= dalloc(&b->lk_sp, nt);
         rc |= dalloc(&b->lk_pairs, 2 * nt);
-        rc |= dalloc(&b->lk_X, 3 * nt * nk);
-        rc |= dalloc(&b->lk_pts, 2 * nt * nk);
+        rc |= dalloc(&b->lk_X, 2 * 3 * nt * nk);
+        rc |= dalloc(&b->lk_pts, 2 * 2 * nt * nk);
         rc |= dalloc(&b->lk_next, 2 * nt * nk);
         rc |= dalloc(&b->lk_err, nt * nk);
         rc |= dalloc(&b->lk_status, nt * nk);
-        rc |= dalloc(&b->lk_q, nt * nk);
-        rc |= dalloc(&b->lk_count, nt);
+        rc |= dalloc(&b->lk_q, 2 * nt * nk);
+        rc |= dalloc(&b->lk_count, 2 * nt);
+        b->lk_ev_pending[0] = b->lk_ev_pending[1] = false;
         if (rc != YV_OK) return YV_ERR_HIP;
         b->max_tracks = n_tracks;
     }
@@ -916,8 +924,28 @@ int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stre
     const bool timed = b->timing == 1 && run >= 0 && !b->tracked[run];
     hipEvent_t* ev = timed ? &b->events[(size_t)run * kEvPerRun] : nullptr;
     const hipStream_t s_run = s;
-    if (b->overlap && b->build_async && b->lk_step == 0) {
-        // the build waits for the run's matches on s and leaves s free for the next run's detect
+    double* lkX = nullptr;
+    float* lkP = nullptr;
+    int32_t *lkQ = nullptr, *lkC = nullptr;
+    int lk_j = 0;
+    if (b->lk_step > 0) {
+        // LK: frame k-1's stereo map points from this run's keypoints / matches, on the run's stream (the next run
+        // rewrites them), into the point set the LK stage two tracks ago has finished reading
+        if (!b->run_images || b->run_n < b->lk_step) return YV_ERR_INVALID;
+        lk_j = b->lk_set;
+        b->lk_set ^= 1;
+        lkX = b->lk_X + (size_t)lk_j * nt * nk * 3;
+        lkP = b->lk_pts + (size_t)lk_j * nt * nk * 2;
+        lkQ = b->lk_q + (size_t)lk_j * nt * nk;
+        lkC = b->lk_count + (size_t)lk_j * nt;
+        if (b->lk_ev_pending[lk_j]) YV_HIP(hipStreamWaitEvent(s_run, b->ev_lk[lk_j], 0));
+        b->lk_ev_pending[lk_j] = false;
+        yavo::launch_stereo_points(b->lk_sp, b->n_tracks, b->pairs, b->keypoints, b->kp_count, b->match_dj,
+                                   b->match_lim, b->max_kp, b->track_K, b->T_right, lkX, lkP, lkQ, lkC, s_run);
+    }
+    if (b->overlap && b->build_async) {
+        // the build (match: edges from the run's matches; LK: pyramids, flow, edges) waits for the run on s and
+        // leaves s free for the next run's detect
         YV_HIP(hipEventRecord(b->ev_fin, s_run));
         YV_HIP(hipStreamWaitEvent(b->bstream, b->ev_fin, 0));
         s = b->bstream;
@@ -927,24 +955,24 @@ int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stre
     if (timed) YV_HIP(hipEventRecord(ev[6], s));
     if (b->lk_step > 0) {
         // trackLastFrame: frame k-1's stereo map points -> calcOpticalFlowPyrLK into frame k -> edges
-        if (!b->run_images || b->run_n < b->lk_step) return YV_ERR_INVALID;
-        yavo::launch_stereo_points(b->lk_sp, b->n_tracks, b->pairs, b->keypoints, b->kp_count, b->match_dj,
-                                   b->match_lim, b->max_kp, b->track_K, b->T_right, b->lk_X, b->lk_pts, b->lk_q,
-                                   b->lk_count, s);
         const int n_lk = (b->run_n + b->lk_step - 1) / b->lk_step;
         int rc = yv_lk_build(b->lk, b->run_images, n_lk, b->run_stride, b->run_pitch * b->lk_step, s);
         if (rc != YV_OK) return rc;
-        rc = yv_lk_track_batch(b->lk, b->lk_pairs, b->n_tracks, b->lk_pts, b->lk_count, b->max_kp, b->lk_max_count,
-                               b->lk_eps, b->lk_min_eig, b->lk_next, b->lk_status, b->lk_err, s);
+        rc = yv_lk_track_batch(b->lk, b->lk_pairs, b->n_tracks, lkP, lkC, b->max_kp, b->lk_max_count, b->lk_eps,
+                               b->lk_min_eig, b->lk_next, b->lk_status, b->lk_err, s);
         if (rc != YV_OK) return rc;
-        yavo::launch_lk_edges(b->n_tracks, b->lk_X, b->lk_next, b->lk_status, b->lk_q, b->lk_count, b->max_kp, eX,
-                              euv, eq, ec, s);
+        yavo::launch_lk_edges(b->n_tracks, lkX, b->lk_next, b->lk_status, lkQ, lkC, b->max_kp, eX, euv, eq, ec, s);
+        if (s != s_run) {
+            if (!b->ev_lk[lk_j]) YV_HIP(hipEventCreateWithFlags(&b->ev_lk[lk_j], hipEventDisableTiming));
+            YV_HIP(hipEventRecord(b->ev_lk[lk_j], s));
+            b->lk_ev_pending[lk_j] = true;
+        }
     } else {
         yavo::launch_track_build(b->tracks, b->n_tracks, b->pairs, b->keypoints, b->kp_count, b->match_dj,
                                  b->match_lim, b->max_kp, b->track_K, b->T_right, eX, euv, eq, ec, s);
     }
     if (b->overlap) YV_HIP(hipEventRecord(b->ev_edges[k], s));
-    if (s != s_run) {
+    if (s != s_run && b->lk_step == 0) {  // (the LK stage reads nothing the next run writes: no join)
         YV_HIP(hipEventRecord(b->ev_built, s));
         b->build_pending = true;
     }
