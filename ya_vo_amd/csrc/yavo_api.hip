@@ -69,6 +69,7 @@ struct yv_batch {
     int32_t* det_count = nullptr;
     int32_t* kp_src = nullptr;
     int32_t* kp_count = nullptr;
+    int32_t* kp_count_build = nullptr;  // the asynchronous edge build's copy of the run's counts (top-K rewrites them)
     int32_t* kp_band = nullptr;     // [slot][max_kp] int4 {row, col, id, slot}: the kept keypoints by BRIEF band
     int32_t* band_off = nullptr;    // [slot][kMaxBands + 1]
     yv_keypoint* keypoints = nullptr;
@@ -211,7 +212,7 @@ int dalloc(T** p, size_t count) {
 void batch_free(yv_batch* b) {
     if (!b) return;
     void* ptrs[] = {b->cand_keys, b->cand_count, b->cand_seen, b->det_rc,   b->det_resp,    b->det_count, b->kp_src, b->kp_band, b->band_off,
-                    b->kp_count,  b->keypoints,  b->desc,     b->blur,        b->pairs,     b->match_key,
+                    b->kp_count,  b->kp_count_build, b->keypoints,  b->desc, b->blur,   b->pairs,     b->match_key,
                     b->matches,   b->match_count, b->filtered, b->filt_count, b->staging,  b->match_dj,
                     b->match_lim, b->tracks,     b->track_K,  b->T_right,    b->edge_X,    b->edge_uv,
                     b->edge_query, b->edge_count, b->edge_outlier, b->track_inliers};
@@ -511,6 +512,7 @@ int yv_batch_create(yv_ctx* ctx, int max_images, int H, int W, int max_kp, int m
     rc |= dalloc(&b->det_count, ns);
     rc |= dalloc(&b->kp_src, ns * nk * 4);
     rc |= dalloc(&b->kp_count, ns);
+    rc |= dalloc(&b->kp_count_build, ns);
     rc |= dalloc(&b->kp_band, ns * nk * 4);
     rc |= dalloc(&b->band_off, ns * (size_t)(yavo::kMaxBands + 1));
     rc |= dalloc(&b->keypoints, ns * nk);
@@ -652,11 +654,13 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
                              b->cand_count, ctx->k9, b->blur, s);
     rc |= record_stage(b, s, run, 1);
     if (b->overlap_mode == 2) rc |= launch_deferred_after(b, s);
-    rc |= join_build(b, s);  // the previous track's build (beside detect) reads kp_count / keypoints / matches
     yavo::launch_topk(b->cand_keys, b->cap, b->cand_count, b->cand_seen, n_images, H, W, K, keep, b->det_rc,
                       b->det_resp, b->det_count, b->kp_src, b->kp_count, b->kp_band, b->band_off, s);
     rc |= record_stage(b, s, run, 2);
     if (b->overlap_mode == 4) rc |= launch_deferred_after(b, s);  // after top-K
+    // the previous track's build (beside detect and top-K) reads keypoints / matches: BRIEF and finalize rewrite them
+    // (its keypoint counts are a copy, kp_count_build, so top-K need not wait)
+    rc |= join_build(b, s);
     yavo::launch_brief(b->blur, n_images, H, W, ctx->d_offsets, b->kp_src, b->kp_band, b->band_off, K, b->keypoints,
                        b->desc, s);
     rc |= record_stage(b, s, run, 3);
@@ -943,9 +947,15 @@ int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stre
         yavo::launch_stereo_points(b->lk_sp, b->n_tracks, b->pairs, b->keypoints, b->kp_count, b->match_dj,
                                    b->match_lim, b->max_kp, b->track_K, b->T_right, lkX, lkP, lkQ, lkC, s_run);
     }
+    const int32_t* build_counts = b->kp_count;
     if (b->overlap && b->build_async) {
         // the build (match: edges from the run's matches; LK: pyramids, flow, edges) waits for the run on s and
-        // leaves s free for the next run's detect
+        // leaves s free for the next run's detect; the match build reads a copy of the keypoint counts
+        if (b->lk_step == 0) {
+            YV_HIP(hipMemcpyAsync(b->kp_count_build, b->kp_count, sizeof(int32_t) * (size_t)b->nslots,
+                                  hipMemcpyDeviceToDevice, s_run));
+            build_counts = b->kp_count_build;
+        }
         YV_HIP(hipEventRecord(b->ev_fin, s_run));
         YV_HIP(hipStreamWaitEvent(b->bstream, b->ev_fin, 0));
         s = b->bstream;
@@ -968,7 +978,7 @@ int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stre
             b->lk_ev_pending[lk_j] = true;
         }
     } else {
-        yavo::launch_track_build(b->tracks, b->n_tracks, b->pairs, b->keypoints, b->kp_count, b->match_dj,
+        yavo::launch_track_build(b->tracks, b->n_tracks, b->pairs, b->keypoints, build_counts, b->match_dj,
                                  b->match_lim, b->max_kp, b->track_K, b->T_right, eX, euv, eq, ec, s);
     }
     if (b->overlap) YV_HIP(hipEventRecord(b->ev_edges[k], s));

@@ -20,6 +20,17 @@
 
 #include "yavo_internal.h"
 
+// Issue priority of the critical-path image kernels over the pose LM that runs beside them on the side stream
+// (s_setprio: the SIMD's arbiter issues the higher-priority wave first).  YAVO_CRIT_PRIO: 0 off, 1 top-K only,
+// 2 every stage of yv_batch_run.
+#ifndef YAVO_CRIT_PRIO
+#define YAVO_CRIT_PRIO 0
+#endif
+#define YV_PRIO_TOPK() \
+    if (YAVO_CRIT_PRIO >= 1) __builtin_amdgcn_s_setprio(3)
+#define YV_PRIO_RUN() \
+    if (YAVO_CRIT_PRIO >= 2) __builtin_amdgcn_s_setprio(3)
+
 namespace yavo {
 
 // ------------------------------------------------------------------------------------------------
@@ -292,6 +303,7 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
                                                      int64_t pitch, int thr, int eig, uint64_t* __restrict__ cand_keys,
                                                      int64_t cap, uint32_t* __restrict__ cand_count, K9 kw,
                                                      uint8_t* __restrict__ blur) {
+    YV_PRIO_RUN();
     __shared__ __align__(16) uint8_t tile[FT_LH * FT_LW];
     // the pretest survivors (phases 1-2) and the horizontal blur (from the barrier after phase 2) share LDS
     constexpr int kPreDw = FT_W * FT_H / 2, kHbufDw = kBlur ? (FT_LH / 2) * FT_W : 0;
@@ -734,6 +746,7 @@ __global__ __launch_bounds__(NT) void topk_kernel(const uint64_t* __restrict__ c
                                                      float* __restrict__ det_resp, int32_t* __restrict__ det_count,
                                                      int32_t* __restrict__ kp_src, int32_t* __restrict__ kp_count,
                                                      int32_t* __restrict__ kp_band, int32_t* __restrict__ band_off) {
+    YV_PRIO_TOPK();
     __shared__ uint64_t s_keys[kMaxKp];
     __shared__ uint32_t s_hist[256];
     __shared__ int s_tmp[40];
@@ -927,6 +940,7 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
                                                     const int32_t* __restrict__ kp_band,
                                                     const int32_t* __restrict__ band_off, int max_kp,
                                                     yv_keypoint* __restrict__ keypoints, Desc* __restrict__ desc) {
+    YV_PRIO_RUN();
     extern __shared__ uint8_t s_band[];  // BR_ROWS * brief_lds_stride(W) bytes
     // this band's keypoints, packed (index << 16) | (col << 5) | (row - r0): index < 4096, col < 2048, 32-row band
     __shared__ uint32_t s_list[kMaxKp];
@@ -1402,6 +1416,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                                                         const int32_t* __restrict__ kp_count,
                                                         const int32_t* __restrict__ pairs, int max_kp,
                                                         uint32_t* __restrict__ match_key) {
+    YV_PRIO_RUN();
     constexpr int QB = 4 * QT * 16;  // queries per workgroup
     __shared__ uint4 s_t[2][MF_TC * MF_ROW];
     __shared__ float s_c[2][MF_TC];  // c_j = (2047 - j) - 2048 popcount(b_j) + 2^21, 0 past the list
@@ -1604,6 +1619,7 @@ __global__ __launch_bounds__(FZ_NT) void match_finalize_kernel(
     const int32_t* __restrict__ kp_count, const int32_t* __restrict__ pairs, int max_kp, int thr,
     yv_match* __restrict__ matches, int32_t* __restrict__ match_count, yv_match* __restrict__ filtered,
     int32_t* __restrict__ filt_count, int2* __restrict__ match_dj, int32_t* __restrict__ match_lim) {
+    YV_PRIO_RUN();
     __shared__ int s_dist[kMaxKp];
     __shared__ int s_j[kMaxKp];
     __shared__ int s_pos[kMaxKp];
