@@ -40,7 +40,7 @@ constexpr uint32_t kCap = kRing - 64;                    // output bytes per chu
 // kSegMin: lane 0's segment alone always fits (<= 16 tokens start in 32 bits, <= 258 bytes each)
 static_assert(16 * 258 <= (int)kCap && 16 <= kMaxMatch, "minimum segment");
 
-struct LenInfo {
+struct alignas(8) LenInfo {  // one ds_read_b64
     uint16_t next;  // first canonical code of the length
     uint16_t cnt;   // codes of the length
     uint16_t offs;  // index of its first symbol in sym
@@ -182,22 +182,23 @@ __device__ bool build_table(const uint8_t* lens, int n, Table<NS>& T, uint16_t* 
     return true;
 }
 
-// a code longer than the fast table: canonical decoding from the first 15 stream bits (bit 0 first).  Every candidate
-// length F+1..15 is tested at once (one LDS round trip for the length table, one for the symbol); the code is prefix
-// free, so at most one length matches.
-template <int NS>
-__device__ __forceinline__ bool slow_code(const Table<NS>& T, uint32_t bits, int F, uint32_t& len, uint32_t& sym) {
+// a code longer than the fast table (F bits): canonical decoding from the first 15 stream bits (bit 0 first).  The
+// length table entries F+1..15 are all read first (one LDS round trip), every candidate length is tested without a
+// branch (the code is prefix free: at most one matches), then the symbol is read (a second round trip).
+template <int F, int NS>
+__device__ __forceinline__ bool slow_code(const Table<NS>& T, uint32_t bits, uint32_t& len, uint32_t& sym) {
     const uint32_t rev = __builtin_bitreverse32(bits) >> 17;
+    uint2 li[15 - F];
+#pragma unroll
+    for (int l = F + 1; l < 16; ++l) li[l - F - 1] = *reinterpret_cast<const uint2*>(&T.len[l]);
     uint32_t found = 0, idx = 0;
 #pragma unroll
-    for (int l = 15; l >= 8; --l) {
-        if (l <= F) break;
-        const LenInfo li = T.len[l];
-        const uint32_t i = (rev >> (15 - l)) - (uint32_t)li.next;
-        if (i < (uint32_t)li.cnt) {
-            found = (uint32_t)l;
-            idx = (uint32_t)li.offs + i;
-        }
+    for (int l = F + 1; l < 16; ++l) {
+        const uint2 v = li[l - F - 1];
+        const uint32_t i = (rev >> (15 - l)) - (v.x & 0xFFFFu);
+        const bool hit = i < (v.x >> 16);
+        found = hit ? (uint32_t)l : found;
+        idx = hit ? (v.y & 0xFFFFu) + i : idx;
     }
     if (!found) return false;
     len = found;
@@ -243,7 +244,7 @@ __device__ __forceinline__ uint32_t decode_tok(const Lds& S, uint32_t w0, uint32
     if (e) {
         len = e & 15u;
         sym = e >> 4;
-    } else if (!slow_code(S.lit, lo, kLitBits, len, sym)) {
+    } else if (!slow_code<kLitBits>(S.lit, lo, len, sym)) {
         return kErr;
     }
     if (sym < 256) {
@@ -272,7 +273,7 @@ __device__ __forceinline__ uint32_t decode_tok(const Lds& S, uint32_t w0, uint32
     if (e2) {
         dl = e2 & 15u;
         ds = e2 >> 4;
-    } else if (!slow_code(S.dist, dv, kDistBits, dl, ds)) {
+    } else if (!slow_code<kDistBits>(S.dist, dv, dl, ds)) {
         return kErr;
     }
     if (ds >= 30) return kErr;
@@ -359,7 +360,7 @@ __device__ __forceinline__ uint32_t data_step(const Lds& S, Dec& d, uint32_t& a,
     if (e) {
         len = e & 15u;
         sym = e >> 4;
-    } else if (!slow_code(S.lit, (uint32_t)d.bb, kLitBits, len, sym)) {
+    } else if (!slow_code<kLitBits>(S.lit, (uint32_t)d.bb, len, sym)) {
         return kErr;
     }
     if (sym < 256) {
@@ -389,7 +390,7 @@ __device__ __forceinline__ uint32_t data_step(const Lds& S, Dec& d, uint32_t& a,
     if (e2) {
         dl = e2 & 15u;
         ds = e2 >> 4;
-    } else if (!slow_code(S.dist, lo, kDistBits, dl, ds)) {
+    } else if (!slow_code<kDistBits>(S.dist, lo, dl, ds)) {
         return kErr;
     }
     if (ds >= 30) return kErr;
