@@ -19,10 +19,15 @@ __device__ __forceinline__ void mm3(const double* A, const double* B, double* C)
     for (int i = 0; i < 9; ++i) C[i] = R[i];
 }
 
+// the library's full-range sin / cos (Payne-Hanek reduction and all): rare (|x| > pi/4), and register-hungry, so kept
+// out of line -- inlined into the pose LM's lane-0 step they set the whole kernel's register peak
+__device__ __noinline__ double k_sin_full(double x) { return sin(x); }
+__device__ __noinline__ double k_cos_full(double x) { return cos(x); }
+
 __device__ __forceinline__ double k_sin(double x) {
     const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03, S3 = -1.98412698298579493134e-04,
                  S4 = 2.75573137070700676789e-06, S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
-    if (!(fabs(x) <= 0.78539816339744827900)) return sin(x);
+    if (!(fabs(x) <= 0.78539816339744827900)) return k_sin_full(x);
     double z = x * x, v = z * x;
     double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
     return x + v * (S1 + z * r);
@@ -31,7 +36,7 @@ __device__ __forceinline__ double k_sin(double x) {
 __device__ __forceinline__ double k_cos(double x) {
     const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03, C3 = 2.48015872894767294178e-05,
                  C4 = -2.75573143513906633035e-07, C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
-    if (!(fabs(x) <= 0.78539816339744827900)) return cos(x);
+    if (!(fabs(x) <= 0.78539816339744827900)) return k_cos_full(x);
     double z = x * x;
     double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
     double hz = 0.5 * z, w = 1.0 - hz;
