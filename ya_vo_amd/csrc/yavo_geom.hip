@@ -1001,6 +1001,12 @@ __device__ __forceinline__ void lm_accumulate_short(double (&part)[28], const do
 // One pass over the active edges at S.T: computeActiveErrors + activeRobustChi2 + buildSystem of g2o's
 // BlockSolver (Huber-weighted J^T J lower triangle, -J^T W e, robust chi2), summed in the oracle's tree
 // order into S.vals[0..28).  Also records S.Tlast (the estimate the active edges' errors refer to).
+__device__ __forceinline__ double uni_f64(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 template <int NT>
 __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, int na, const uint8_t* s_robust,
                                         const double* X, const double* uv, double* s_red,
@@ -1010,12 +1016,13 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
 #ifdef YAVO_LM_PROFILE
     const unsigned long long p0 = __builtin_readcyclecounter();
 #endif
+    // the estimate and K are wave-uniform: held in SGPRs (16 doubles = 32 VGPRs fewer through the edge loop)
     double T[7], K[9];
 #pragma unroll
-    for (int q = 0; q < 7; ++q) T[q] = S.T[q];
+    for (int q = 0; q < 7; ++q) T[q] = uni_f64(S.T[q]);
 #pragma unroll
-    for (int q = 0; q < 9; ++q) K[q] = S.K[q];
-    if (tid < 7) S.Tlast[tid] = T[tid];
+    for (int q = 0; q < 9; ++q) K[q] = uni_f64(S.K[q]);
+    if (tid < 7) S.Tlast[tid] = S.T[tid];
     double part[kLMVals];
 #pragma unroll
     for (int v = 0; v < kLMVals; ++v) part[v] = 0.0;
@@ -1285,9 +1292,9 @@ __global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t*
             // active edges keep the error of the last computeActiveErrors, i.e. at the last TRIAL estimate
             // Tlast (possibly a rejected one) -- recomputed here from Tlast, bit-identical to the stored value
             double T[7], Tl[7], K[9];
-            for (int q = 0; q < 7; ++q) T[q] = S.T[q];
-            for (int q = 0; q < 7; ++q) Tl[q] = S.Tlast[q];
-            for (int q = 0; q < 9; ++q) K[q] = S.K[q];
+            for (int q = 0; q < 7; ++q) T[q] = uni_f64(S.T[q]);
+            for (int q = 0; q < 7; ++q) Tl[q] = uni_f64(S.Tlast[q]);
+            for (int q = 0; q < 9; ++q) K[q] = uni_f64(S.K[q]);
             int cnt = 0, chg = 0;
             for (int i = tid; i < n; i += NT) {
                 double ee[2];
