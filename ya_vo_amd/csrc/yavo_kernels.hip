@@ -734,10 +734,13 @@ __device__ void boundary_compact(RcAt rc_at, int K, int H, int W, int32_t* kp_sr
     if (tid == 0) *kp_count = base;
 }
 
-// top-K per image: one workgroup of NT threads per image.  (256-thread workgroups, meant to fit beside the side-stream
-// pose LM, measured the same 0.44-0.48 ms in the step: the LM's two workgroups per CU hold the whole register file,
-// so nothing dispatches there until they retire.)
-constexpr int TK_SEL_NT = 1024;
+// top-K per image: one workgroup of NT threads per image.  512 threads: same-box A/B in the headline step (r03 c32,
+// two runs each) 1024 -> 206.0k fps, 512 -> 209.7k, 256 -> 207.3k; in-step top-K 757 -> 488 us per dispatch (half
+// the waves at each of its ~80 workgroup barriers, twice the per-thread work in the sort stages).
+#ifndef YAVO_TOPK_NT
+#define YAVO_TOPK_NT 512
+#endif
+constexpr int TK_SEL_NT = YAVO_TOPK_NT;
 static_assert(TK_SEL_NT >= 256 && TK_SEL_NT % 64 == 0, "the radix-select histogram scan uses the first 256 threads");
 template <int NT>
 __global__ __launch_bounds__(NT) void topk_kernel(const uint64_t* __restrict__ cand_keys, int64_t cap,
