@@ -27,8 +27,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=64)
     ap.add_argument("--plain", action="store_true", help="use the product library (for PMC runs), no phase timers")
+    ap.add_argument("--lib", default="", help="with --plain: this library instead of lib/libyavo.so")
     args = ap.parse_args()
-    lib = yv.load_library(os.path.join(ROOT, "ya_vo_amd", "lib", "libyavo.so" if args.plain else "libyavo_prof.so"))
+    lib = yv.load_library(args.lib if (args.plain and args.lib) else
+                          os.path.join(ROOT, "ya_vo_amd", "lib", "libyavo.so" if args.plain else "libyavo_prof.so"))
     if not args.plain:
         lib.yv_debug_lm_prof.argtypes = [ctypes.c_void_p]
     H, W, B = 376, 1241, args.frames

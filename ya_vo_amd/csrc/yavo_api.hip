@@ -72,6 +72,7 @@ struct yv_batch {
     int32_t* kp_count_build = nullptr;  // the asynchronous edge build's copy of the run's counts (top-K rewrites them)
     int32_t* kp_band = nullptr;     // [slot][max_kp] int4 {row, col, id, slot}: the kept keypoints by BRIEF band
     int32_t* band_off = nullptr;    // [slot][kMaxBands + 1]
+    int32_t* brief_loff = nullptr;  // [256][2] BRIEF test offsets in the band's LDS layout (launch_brief)
     yv_keypoint* keypoints = nullptr;
     Desc* desc = nullptr;
     uint8_t* blur = nullptr;
@@ -212,7 +213,7 @@ int dalloc(T** p, size_t count) {
 void batch_free(yv_batch* b) {
     if (!b) return;
     void* ptrs[] = {b->cand_keys, b->cand_count, b->cand_seen, b->det_rc,   b->det_resp,    b->det_count, b->kp_src, b->kp_band, b->band_off,
-                    b->kp_count,  b->kp_count_build, b->keypoints,  b->desc, b->blur,   b->pairs,     b->match_key,
+                    b->brief_loff, b->kp_count,  b->kp_count_build, b->keypoints,  b->desc, b->blur,   b->pairs,     b->match_key,
                     b->matches,   b->match_count, b->filtered, b->filt_count, b->staging,  b->match_dj,
                     b->match_lim, b->tracks,     b->track_K,  b->T_right,    b->edge_X,    b->edge_uv,
                     b->edge_query, b->edge_count, b->edge_outlier, b->track_inliers};
@@ -515,6 +516,7 @@ int yv_batch_create(yv_ctx* ctx, int max_images, int H, int W, int max_kp, int m
     rc |= dalloc(&b->kp_count_build, ns);
     rc |= dalloc(&b->kp_band, ns * nk * 4);
     rc |= dalloc(&b->band_off, ns * (size_t)(yavo::kMaxBands + 1));
+    rc |= dalloc(&b->brief_loff, 512);
     rc |= dalloc(&b->keypoints, ns * nk);
     rc |= dalloc(&b->desc, ns * nk);
     rc |= dalloc(&b->blur, (size_t)max_images * (size_t)yavo::blur_image_bytes(H, W));
@@ -662,7 +664,7 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
     // (its keypoint counts are a copy, kp_count_build, so top-K need not wait)
     rc |= join_build(b, s);
     yavo::launch_brief(b->blur, n_images, H, W, ctx->d_offsets, b->kp_src, b->kp_band, b->band_off, K, b->keypoints,
-                       b->desc, s);
+                       b->desc, b->brief_loff, s);
     rc |= record_stage(b, s, run, 3);
     if (b->overlap_mode == 3) rc |= launch_deferred_after(b, s);  // after describe
     if (b->n_pairs > 0) {
@@ -1140,7 +1142,7 @@ int yv_describe(yv_ctx* ctx, const uint8_t* img, int H, int W, int stride, const
     yavo::launch_kp_boundary(b->det_rc, b->det_count, 1, H, W, b->max_kp, b->kp_src, b->kp_count, b->kp_band,
                              b->band_off, s);
     yavo::launch_brief(b->blur, 1, H, W, ctx->d_offsets, b->kp_src, b->kp_band, b->band_off, b->max_kp, b->keypoints,
-                       b->desc, s);
+                       b->desc, b->brief_loff, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
     YV_HIP(stage_d2h(ctx, ctx->h_pinned + 2, b->kp_count, sizeof(int32_t), s));
     YV_HIP(stage_sync(ctx, s));

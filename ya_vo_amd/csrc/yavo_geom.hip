@@ -24,6 +24,7 @@
 #include "yavo_internal.h"
 #include "yavo_cvsvd.h"
 #include "yavo_se3.h"
+#include "yavo_xlane.h"
 
 namespace yavo {
 namespace geom {
@@ -915,16 +916,22 @@ __device__ void tree_reduce(double (&part)[NV], double* red, double* out, unsign
 // IEEE addition commutes, so the lane with bit off set computes the lower lane's bits). After the six levels the
 // lane pair (l, l ^ 1) holds value v(l) = 14 b5 + 7 b4 + 4 b3 + 2 b2 + b1 (28 values: v < 28 is real, the rest
 // are padding slots).
+// The exchanges run on the VALU side (yavo_xlane.h): permlane swaps at offsets 32 / 16, DPP below.
 template <int N, int OFF>
 __device__ __forceinline__ void rs_level(const double* in, double* out, int lane, int& v) {
     constexpr int h = (N + 1) / 2;
     const bool up = (lane & OFF) != 0;
 #pragma unroll
     for (int j = 0; j < h; ++j) {
-        const double lo = in[j];
-        const double hi = (h + j < N) ? in[h + j] : 0.0;
-        const double keep = up ? hi : lo;
-        out[j] = keep + __shfl_xor(up ? lo : hi, OFF, 64);
+        double lo = in[j];
+        double hi = (h + j < N) ? in[h + j] : 0.0;
+        if constexpr (OFF >= 16) {
+            xl::swap_halves_f64<OFF>(lo, hi);  // {own kept, partner's} in some order: the sum commutes
+            out[j] = lo + hi;
+        } else {
+            const double keep = up ? hi : lo;
+            out[j] = keep + xl::xor_row_f64<OFF>(up ? lo : hi);
+        }
     }
     if (up) v += h;
 }
@@ -945,7 +952,7 @@ __device__ void lm_reduce(double (&part)[NV], double* red /* >= NV * NT / 64 */,
     rs_level<7, 8>(a7, a4, lane, v);
     rs_level<4, 4>(a4, a2, lane, v);
     rs_level<2, 2>(a2, a1, lane, v);
-    const double tot = a1[0] + __shfl_xor(a1[0], 1, 64);
+    const double tot = a1[0] + xl::xor_row_f64<1>(a1[0]);
     const bool owner = v < NV && (lane & 1) == 0;
     if (W == 1) {
         if (owner) out[v] = tot;

@@ -69,10 +69,11 @@ void launch_topk(const uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, u
 void launch_kp_boundary(const int32_t* det_rc, const int32_t* det_count, int n_images, int H, int W,
                         int max_kp, int32_t* kp_src, int32_t* kp_count, int32_t* kp_band, int32_t* band_off,
                         hipStream_t s);
-// BRIEF: one wave per keypoint, 256 tests -> 4 ballots; writes KeyPoint records + packed descriptors.
+// BRIEF: writes KeyPoint records + packed descriptors.  loff: a 2 KB device scratch of the caller (the tests' LDS
+// offsets for this W, rewritten by every launch on stream s).
 void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t* offsets,
                   const int32_t* kp_src, const int32_t* kp_band, const int32_t* band_off, int max_kp,
-                  yv_keypoint* keypoints, Desc* desc, hipStream_t s);
+                  yv_keypoint* keypoints, Desc* desc, int32_t* loff, hipStream_t s);
 // Pack KeyPoint records -> descriptors (host-supplied keypoints).
 void launch_pack_desc(const yv_keypoint* keypoints, const int32_t* kp_count, int n_slots, int max_kp,
                       Desc* desc, hipStream_t s);

@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "yavo_xlane.h"
 #include "yavo_internal.h"
 
 // Issue priority of the critical-path image kernels over the pose LM that runs beside them on the side stream
@@ -899,22 +900,6 @@ void launch_kp_boundary(const int32_t* det_rc, const int32_t* det_count, int n_i
 // BRIEF
 // ------------------------------------------------------------------------------------------------
 
-// v_writelane_b32: lane LANE of `dst` takes the wave-uniform `val` (no clang builtin for it in this toolchain)
-template <int LANE>
-__device__ __forceinline__ uint32_t writelane(uint32_t dst, uint32_t val) {
-    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(val), "i"(LANE));
-    return dst;
-}
-
-// v[idx] for a small register array without dynamic indexing (keeps it out of scratch).
-template <int N>
-__device__ __forceinline__ uint32_t reg_select(const uint32_t (&v)[N], int idx) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int q = 0; q < N; ++q) r = (q == idx) ? v[q] : r;
-    return r;
-}
-
 // One workgroup per (32-row band, image): the band's keypoints (rows [r0, r0 + 32)) read their 17 x 17
 // patches from an LDS copy of the blurred rows [r0 - 8, r0 + 41) with row stride LS = brief_lds_stride(W) >= W + 1.
 // The reference samples getPixelVal at the linear index (row + dr) * W + (col + dc) (src/BriefDescriptor.cc:
@@ -923,8 +908,8 @@ __device__ __forceinline__ uint32_t reg_select(const uint32_t (&v)[N], int idx) 
 // first pixel of the next row, and (b) any index past the image end (row + dr == H, or row + dr == H - 1 at
 // col + dc == W), which the reference reads out of bounds (UB; both paths read 0).  The band therefore holds in
 // LDS column W of each row the next row's first pixel, and zero rows past the image: every sample is then
-// s_band[(row + dr - (r0 - 8)) * LS + col + dc] with no test.  One wave per keypoint: lane l evaluates tests l,
-// l + 64, l + 128, l + 192 -> 4 ballots = 256 bits.
+// s_band[(row + dr - (r0 - 8)) * LS + col + dc] with no test.  Lanes = keypoints: a wave takes 64 keypoints and
+// one quarter (64) of the tests, whose sample offsets are wave-uniform scalars (loff).
 constexpr int BR_BAND = kBandRows;
 constexpr int BR_ROWS = BR_BAND + 17;  // rows r0-8 .. r0+40 (the last one for the wrap of col + 8 == W)
 // 16 waves share one staged band: the ~61 KB band limits a CU to 2 workgroups, so the workgroup is as wide as
@@ -938,11 +923,11 @@ constexpr int BR_NW = BR_NT / 64;
 static_assert(4 * BR_NT >= kMaxKp, "brief_kernel loads at most 4 * BR_NT band records");
 
 __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict__ blur, int H, int W,
-                                                    const int8_t* __restrict__ offsets,
                                                     const int32_t* __restrict__ kp_src,
                                                     const int32_t* __restrict__ kp_band,
                                                     const int32_t* __restrict__ band_off, int max_kp,
-                                                    yv_keypoint* __restrict__ keypoints, Desc* __restrict__ desc) {
+                                                    yv_keypoint* __restrict__ keypoints, Desc* __restrict__ desc,
+                                                    const int2* __restrict__ loff) {
     YV_PRIO_RUN();
     extern __shared__ uint8_t s_band[];  // BR_ROWS * brief_lds_stride(W) bytes
     // this band's keypoints, packed (index << 16) | (col << 5) | (row - r0): index < 4096, col < 2048, 32-row band
@@ -1045,85 +1030,79 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
         BP_STORE();
         return;
     }
-    // 3. descriptors.  Each lane's 8 sample offsets as LDS offsets dr * LS + dc.
-    int ol[4][2];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const uint32_t packed = reinterpret_cast<const uint32_t*>(offsets)[lane + 64 * t];
-        const int o0 = (int)(int8_t)(packed & 0xFFu), o1 = (int)(int8_t)((packed >> 8) & 0xFFu);
-        const int o2 = (int)(int8_t)((packed >> 16) & 0xFFu), o3 = (int)(int8_t)((packed >> 24) & 0xFFu);
-        ol[t][0] = o0 * LS + o1;
-        ol[t][1] = o2 * LS + o3;
-    }
-    uint32_t* rec_base = reinterpret_cast<uint32_t*>(keypoints + (int64_t)img * max_kp);
+    // 3. descriptors, lanes = keypoints: wave item = (block of 64 keypoints, group g of 64 tests).  The tests'
+    // offsets are wave-uniform (loff, scalar loads), so a test costs each lane two LDS byte reads, two address adds,
+    // a subtraction and one v_alignbit that shifts the result bit in: 4 VALU per test and keypoint, against ~110
+    // VALU of per-keypoint ballot / emit work per wave in the lanes = tests form.
+    uint8_t* rec_b = reinterpret_cast<uint8_t*>(keypoints + (int64_t)img * max_kp);
     Desc* d_base = desc + (int64_t)img * max_kp;
-    // The outputs of one keypoint: its descriptor (8 dwords, lanes 0-7) and its 48-B KeyPoint record {x, y, id,
-    // matched = 0, featVec[32], 3 pad bytes = 0} (12 dwords, lanes 0-11).  Every value is wave-uniform (ballot
-    // results, the keypoint's fields), so the dwords are formed by the scalar unit and placed into the storing lanes
-    // with v_writelane -- one VALU op per stored dword (a per-lane select over the 9 candidates costs ~18).
-    auto emit = [&](int i, int row, int col, int id, const uint64_t (&w)[4]) {
-        uint32_t bd[8];
+    const int nitems = ((nb + 63) >> 6) * 4;
+    // the item index in an SGPR (tid >> 6 is not known to be wave-uniform): loff then comes by scalar loads
+    for (int item = __builtin_amdgcn_readfirstlane(wave); item < nitems; item += BR_NW) {
+        const int g = item & 3, k = (item >> 2) * 64 + lane;
+        const bool act = k < nb;
+        const uint32_t e = s_list[act ? k : nb - 1];
+        const int i = (int)(e >> 16), row = r0 + (int)(e & 31u), col = (int)((e >> 5) & 2047u);
+        const int id = (act && g == 0) ? src[i].z : 0;
+        const int la = (row - rb) * LS + col;
+        const int2* lo = loff + 64 * g;
+        uint32_t w[2] = {0u, 0u};
+        // tests 64g + 63 down to 64g: w[h] = (w[h] << 1) | (p1 > p2), so bit j of w[h] is test 64g + 32h + j; eight
+        // tests (16 LDS reads in flight) per iteration keep the lane within the 64 VGPRs of 8 waves per SIMD
+#pragma unroll 1
+        for (int c = 7; c >= 0; --c) {
+            const int2* oc = lo + 8 * c;
+            uint32_t acc = w[c >> 2];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            bd[2 * t] = __builtin_amdgcn_readfirstlane((uint32_t)w[t]);
-            bd[2 * t + 1] = __builtin_amdgcn_readfirstlane((uint32_t)(w[t] >> 32));
+            for (int j = 7; j >= 0; --j) {
+                const int2 o = oc[j];
+                const uint32_t p1 = s_band[la + o.x], p2 = s_band[la + o.y];
+                acc = __builtin_amdgcn_alignbit(acc, p2 - p1, 31);  // p2 - p1 < 0 iff p1 > p2
+            }
+            if (c >= 4) w[1] = acc;
+            else w[0] = acc;
         }
-        uint32_t dv = 0u, rv = 0u;
-        dv = writelane<0>(dv, bd[0]); dv = writelane<1>(dv, bd[1]); dv = writelane<2>(dv, bd[2]);
-        dv = writelane<3>(dv, bd[3]); dv = writelane<4>(dv, bd[4]); dv = writelane<5>(dv, bd[5]);
-        dv = writelane<6>(dv, bd[6]); dv = writelane<7>(dv, bd[7]);
-        // record dword 3+m = featVec bytes shifted by one (the matched byte first)
-        auto rec = [&](int m) -> uint32_t {
-            const uint32_t hi = m < 8 ? bd[m] : 0u, lo = m > 0 ? bd[m - 1] : 0u;
-            return __builtin_amdgcn_readfirstlane((hi << 8) | (lo >> 24));
-        };
-        rv = writelane<0>(rv, (uint32_t)row); rv = writelane<1>(rv, (uint32_t)col); rv = writelane<2>(rv, (uint32_t)id);
-        rv = writelane<3>(rv, rec(0)); rv = writelane<4>(rv, rec(1)); rv = writelane<5>(rv, rec(2));
-        rv = writelane<6>(rv, rec(3)); rv = writelane<7>(rv, rec(4)); rv = writelane<8>(rv, rec(5));
-        rv = writelane<9>(rv, rec(6)); rv = writelane<10>(rv, rec(7)); rv = writelane<11>(rv, rec(8));
-        if (lane < 8) d_base[i].w[lane] = dv;
-        if (lane < 12) rec_base[(int64_t)i * 12 + lane] = rv;
-    };
-    // two keypoints per iteration: 16 LDS reads per lane in flight.  The record's id (the keypoint's index before
-    // checkBoundry, kp_src[i].z) is the only field not in the packed list: lane 2, which stores it, loads it one
-    // iteration ahead
-    auto id_of = [&](int k) -> int {
-        if (lane != 2 || k >= nb) return 0;
-        return src[s_list[k] >> 16].z;
-    };
-    int ida_next = id_of(wave), idb_next = id_of(wave + BR_NW);
-    for (int k = wave; k < nb; k += 2 * BR_NW) {
-        const bool two = k + BR_NW < nb;
-        const uint32_t ea = s_list[k], eb = two ? s_list[k + BR_NW] : ea;
-        const int ida = __builtin_amdgcn_readlane(ida_next, 2), idb = __builtin_amdgcn_readlane(idb_next, 2);
-        ida_next = id_of(k + 2 * BR_NW);
-        idb_next = id_of(k + 3 * BR_NW);
-        const int ia = (int)(ea >> 16), ib = (int)(eb >> 16);
-        const int rowa = r0 + (int)(ea & 31u), cola = (int)((ea >> 5) & 2047u);
-        const int rowb = r0 + (int)(eb & 31u), colb = (int)((eb >> 5) & 2047u);
-        const int la = (rowa - rb) * LS + cola, lbb = (rowb - rb) * LS + colb;
-        uint64_t wa[4], wb[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int pa1 = s_band[la + ol[t][0]], pa2 = s_band[la + ol[t][1]];
-            const int pb1 = s_band[lbb + ol[t][0]], pb2 = s_band[lbb + ol[t][1]];
-            wa[t] = __ballot(pa1 > pa2);
-            wb[t] = __ballot(pb1 > pb2);
+        if (act) {
+            reinterpret_cast<uint2*>(d_base + i)[g] = make_uint2(w[0], w[1]);
+            // the 48-B record {row, col, id, matched = 0, featVec[32], 3 pad bytes}: featVec bytes 8g .. 8g + 7 at
+            // record byte 13 + 8g (byte, short, dword, byte: the natural alignments of 13 + 8g ...)
+            uint8_t* r = rec_b + (int64_t)i * 48;
+            if (g == 0) {
+                reinterpret_cast<int32_t*>(r)[0] = row;
+                reinterpret_cast<int32_t*>(r)[1] = col;
+                reinterpret_cast<int32_t*>(r)[2] = id;
+                r[12] = 0;
+            }
+            r[13 + 8 * g] = (uint8_t)w[0];
+            *reinterpret_cast<uint16_t*>(r + 14 + 8 * g) = (uint16_t)(w[0] >> 8);
+            *reinterpret_cast<uint32_t*>(r + 16 + 8 * g) = (w[0] >> 24) | (w[1] << 8);
+            r[20 + 8 * g] = (uint8_t)(w[1] >> 24);
+            if (g == 3) {
+                r[45] = 0;
+                *reinterpret_cast<uint16_t*>(r + 46) = 0;
+            }
         }
-        emit(ia, __builtin_amdgcn_readfirstlane(rowa), __builtin_amdgcn_readfirstlane(cola), ida, wa);
-        if (two) emit(ib, __builtin_amdgcn_readfirstlane(rowb), __builtin_amdgcn_readfirstlane(colb), idb, wb);
     }
     BP_MARK(2);
     BP_STORE();
 }
 
+// the 256 tests' sample offsets in the band's LDS layout: loff[t] = {dr1 * LS + dc1, dr2 * LS + dc2}
+__global__ void brief_loff_kernel(const int8_t* __restrict__ offsets, int LS, int2* __restrict__ loff) {
+    const int t = threadIdx.x;
+    const int8_t* o = offsets + 4 * t;
+    loff[t] = make_int2((int)o[0] * LS + (int)o[1], (int)o[2] * LS + (int)o[3]);
+}
+
 void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t* offsets, const int32_t* kp_src,
                   const int32_t* kp_band, const int32_t* band_off, int max_kp, yv_keypoint* keypoints, Desc* desc,
-                  hipStream_t s) {
+                  int32_t* loff, hipStream_t s) {
     dim3 grid(((H + BR_BAND - 1) / BR_BAND) * n_images);
     const size_t lds = (size_t)BR_ROWS * brief_lds_stride(W);
-    hipLaunchKernelGGL(brief_kernel, grid, dim3(BR_NT), lds, s, blur, H, W, offsets, kp_src, kp_band, band_off, max_kp,
-                       keypoints, desc);
+    int2* lo = reinterpret_cast<int2*>(loff);
+    hipLaunchKernelGGL(brief_loff_kernel, dim3(1), dim3(256), 0, s, offsets, brief_lds_stride(W), lo);
+    hipLaunchKernelGGL(brief_kernel, grid, dim3(BR_NT), lds, s, blur, H, W, kp_src, kp_band, band_off, max_kp,
+                       keypoints, desc, lo);
 }
 
 __global__ void pack_desc_kernel(const yv_keypoint* __restrict__ keypoints, const int32_t* __restrict__ kp_count,
@@ -1348,8 +1327,10 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             int v = best[qt][r];
-#pragma unroll
-            for (int m = 8; m > 0; m >>= 1) v = max(v, __shfl_xor(v, m, 16));
+            v = max(v, xl::xor_row_i32<8>(v));  // DPP butterflies inside the 16-lane group (yavo_xlane.h)
+            v = max(v, xl::xor_row_i32<4>(v));
+            v = max(v, xl::xor_row_i32<2>(v));
+            v = max(v, xl::xor_row_i32<1>(v));
             const int q = q0 + 16 * MM_QT * wave + 16 * qt + 4 * g + r;
             if (col == r && q < nq) {
                 uint32_t key = 0xFFFFFFFFu;  // empty train set (nt >= 1 always leaves a real key in the row max)
@@ -1533,8 +1514,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             uint32_t v = best[qt][r];
-#pragma unroll
-            for (int m = 8; m > 0; m >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m, 16));
+            v = max(v, (uint32_t)xl::xor_row_i32<8>((int)v));
+            v = max(v, (uint32_t)xl::xor_row_i32<4>((int)v));
+            v = max(v, (uint32_t)xl::xor_row_i32<2>((int)v));
+            v = max(v, (uint32_t)xl::xor_row_i32<1>((int)v));
             const int q = q0 + 16 * QT * wave + 16 * qt + 4 * g + r;
             if (col == r && q < nq) {
                 uint32_t key = 0xFFFFFFFFu;  // empty train set (nt >= 1 always leaves a real key in the row max)
@@ -1763,3 +1746,30 @@ extern "C" int yv_debug_det_prof(unsigned long long* out /* [131072][6] */) {
                    hipSuccess ? 0 : -2;
 }
 #endif
+
+// yavo_xlane.h self-check (tests/test_gpu_xlane.py): rows 0-3 = lane ^ {1, 2, 4, 8} through the DPP butterflies;
+// rows 4-5 / 6-7 = the permlane16 / permlane32 half exchange of (lo = lane, hi = 100 + lane).
+namespace yavo {
+__global__ void xlane_check_kernel(int32_t* out) {
+    const int l = threadIdx.x;
+    out[0 * 64 + l] = xl::xor_row_i32<1>(l);
+    out[1 * 64 + l] = xl::xor_row_i32<2>(l);
+    out[2 * 64 + l] = xl::xor_row_i32<4>(l);
+    out[3 * 64 + l] = xl::xor_row_i32<8>(l);
+    uint32_t a = (uint32_t)l, b = 100u + (uint32_t)l;
+    xl::swap_halves<16>(a, b);
+    out[4 * 64 + l] = (int32_t)a;
+    out[5 * 64 + l] = (int32_t)b;
+    a = (uint32_t)l;
+    b = 100u + (uint32_t)l;
+    xl::swap_halves<32>(a, b);
+    out[6 * 64 + l] = (int32_t)a;
+    out[7 * 64 + l] = (int32_t)b;
+}
+}  // namespace yavo
+
+extern "C" int yv_debug_xlane(int32_t* d_out /* [8][64] */, void* stream) {
+    if (!d_out) return -1;
+    hipLaunchKernelGGL(yavo::xlane_check_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -127,29 +127,32 @@ __global__ void map_anchor_kernel(const uint8_t* blocks, int world, int64_t bb, 
     for (int i = 0; i < 7; ++i) base[i] = A[i];
 }
 
+// keyframes j = blockIdx.x, blockIdx.x + gridDim.x, ... of block blockIdx.y (n_kf is a device value; the grid is
+// sized by the host to cover the usual count without launching a workgroup per possible keyframe)
 __global__ __launch_bounds__(kNT) void map_place_kernel(uint8_t* blocks, int64_t bb, const double* anchors) {
-    const int r = blockIdx.y, j = blockIdx.x;
+    const int r = blockIdx.y;
     uint8_t* block = blocks + r * bb;
     yv_map_header* h = reinterpret_cast<yv_map_header*>(block);
     const int n_kf = h->n_kf;
-    if (j >= n_kf) return;
-    yv_keyframe* kf = reinterpret_cast<yv_keyframe*>(block + kf_offset()) + j;
-    yv_landmark* lm = reinterpret_cast<yv_landmark*>(block + lm_offset(h->max_kf)) + (int64_t)j * h->lm_stride;
-    double Lk[7], T[7];
-    for (int i = 0; i < 7; ++i) Lk[i] = kf->T[i];
-    se3_mul(anchors + 7 * r, Lk, T);
-    const int n = kf->n_landmarks;
-    __syncthreads();  // every lane has read L_k
-    if (threadIdx.x == 0) {
-        for (int i = 0; i < 7; ++i) kf->T[i] = T[i];
-        if (j == 0) h->placed = 1;
-    }
-    for (int q = threadIdx.x; q < n; q += kNT) {
-        double Xc[3] = {lm[q].X[0], lm[q].X[1], lm[q].X[2]}, Xw[3];
-        se3_act(T, Xc, Xw);
-        lm[q].X[0] = Xw[0];
-        lm[q].X[1] = Xw[1];
-        lm[q].X[2] = Xw[2];
+    for (int j = blockIdx.x; j < n_kf; j += gridDim.x) {
+        yv_keyframe* kf = reinterpret_cast<yv_keyframe*>(block + kf_offset()) + j;
+        yv_landmark* lm = reinterpret_cast<yv_landmark*>(block + lm_offset(h->max_kf)) + (int64_t)j * h->lm_stride;
+        double Lk[7], T[7];
+        for (int i = 0; i < 7; ++i) Lk[i] = kf->T[i];
+        se3_mul(anchors + 7 * r, Lk, T);
+        const int n = kf->n_landmarks;
+        __syncthreads();  // every lane has read L_k
+        if (threadIdx.x == 0) {
+            for (int i = 0; i < 7; ++i) kf->T[i] = T[i];
+            if (j == 0) h->placed = 1;
+        }
+        for (int q = threadIdx.x; q < n; q += kNT) {
+            double Xc[3] = {lm[q].X[0], lm[q].X[1], lm[q].X[2]}, Xw[3];
+            se3_act(T, Xc, Xw);
+            lm[q].X[0] = Xw[0];
+            lm[q].X[1] = Xw[1];
+            lm[q].X[2] = Xw[2];
+        }
     }
 }
 
@@ -179,7 +182,9 @@ extern "C" int yv_map_place(yv_ctx* ctx, void* d_blocks, int world, int64_t bloc
     if (hipSetDevice(yavo::ctx_device(ctx)) != hipSuccess) return YV_ERR_HIP;
     // the header's max_kf (a device value) bounds the grid: the block size bounds it from above
     const int64_t per_kf = (int64_t)sizeof(yv_keyframe) + sizeof(yv_landmark);
-    const int grid_kf = (int)std::min<int64_t>(block_bytes / per_kf, 65535);
+    // (one workgroup per possible keyframe was up to 65535 mostly empty workgroups per block: 0.14 ms of dispatch for
+    // a 1024-frame chunk's 256 keyframes; 512 covers that count in one pass and loops beyond it)
+    const int grid_kf = (int)std::min<int64_t>(block_bytes / per_kf, 512);
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : yavo::ctx_stream(ctx);
     uint8_t* blk = static_cast<uint8_t*>(d_blocks);
     hipLaunchKernelGGL(yavo::map::map_anchor_kernel, dim3(1), dim3(64), 0, s, blk, world, block_bytes, d_base,
