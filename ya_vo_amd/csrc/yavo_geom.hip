@@ -57,6 +57,9 @@ __device__ unsigned long long g_lm_prof[1024][10];
 #define LMP_STORE() do {} while (0)
 #endif
 constexpr int kMaxEdges = 4096;   // edges per pose problem held in LDS
+// edge capacity of the LDS-resident pose LM (X 24 B + uv 8 B + 5 B of flags / index per edge: 76 KB, two workgroups
+// per CU)
+constexpr int kLMResCap = 2048;
 
 // exclusive scan over an NT-thread block; s_tmp >= NT/64 ints
 template <int NT = kNT>
@@ -1014,9 +1017,9 @@ __device__ __forceinline__ double uni_f64(double v) {
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-template <int NT>
+template <int NT, typename UV>
 __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, int na, const uint8_t* s_robust,
-                                        const double* X, const double* uv, double* s_red,
+                                        const double* X, const UV* uv, double* s_red,
                                         unsigned long long* lmp = nullptr) {
     const int tid = threadIdx.x;
     __syncthreads();  // S.T written by lane 0
@@ -1039,7 +1042,7 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
     int nrob = 0;
     if (tid < na) {
         const int i = s_active[tid];
-        nx[0] = X[3 * i]; nx[1] = X[3 * i + 1]; nx[2] = X[3 * i + 2]; nx[3] = uv[2 * i]; nx[4] = uv[2 * i + 1];
+        nx[0] = X[3 * i]; nx[1] = X[3 * i + 1]; nx[2] = X[3 * i + 2]; nx[3] = (double)uv[2 * i]; nx[4] = (double)uv[2 * i + 1];
         nrob = s_robust[i];
     }
     for (int a = tid; a < na; a += NT) {
@@ -1047,7 +1050,7 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
         const int rob = nrob;
         if (a + NT < na) {
             const int i = s_active[a + NT];
-            nx[0] = X[3 * i]; nx[1] = X[3 * i + 1]; nx[2] = X[3 * i + 2]; nx[3] = uv[2 * i]; nx[4] = uv[2 * i + 1];
+            nx[0] = X[3 * i]; nx[1] = X[3 * i + 1]; nx[2] = X[3 * i + 2]; nx[3] = (double)uv[2 * i]; nx[4] = (double)uv[2 * i + 1];
             nrob = s_robust[i];
         }
         double e[2], pc[3];
@@ -1120,15 +1123,21 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
 #define YAVO_LM_WAVES_PER_EU 2
 #endif
 #define YAVO_LM_ATTR __attribute__((amdgpu_waves_per_eu(YAVO_LM_WAVES_PER_EU)))
-template <int NT>
-__global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
+// CAP < kMaxEdges: the problem's edges (at most CAP) are held in LDS for all its passes -- X as doubles, uv as floats.
+// That form is exact only for measurements representable in float: the batch's track edges, whose uv are keypoint
+// or LK pixel positions (track_build_kernel, lk_edges_kernel); launch_track_pose selects it for them alone.
+template <int NT, int CAP>
+__device__ __forceinline__ void pose_lm_body(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
                                                       int stride, const double* __restrict__ Xall,
                                                       const double* __restrict__ uvall, const double* __restrict__ Kall,
                                                       const double* priors, double* poses,
                                                       uint8_t* __restrict__ outlier_all, int32_t* __restrict__ inliers,
                                                       int n_prob) {
-    __shared__ uint8_t s_level[kMaxEdges], s_out[kMaxEdges], s_robust[kMaxEdges];
-    __shared__ int16_t s_active[kMaxEdges];
+    constexpr bool kRes = CAP < kMaxEdges;
+    __shared__ uint8_t s_level[CAP], s_out[CAP], s_robust[CAP];
+    __shared__ int16_t s_active[CAP];
+    __shared__ double s_X[kRes ? 3 * CAP : 1];
+    __shared__ float s_uv[kRes ? 2 * CAP : 1];
     __shared__ double s_red[NT > 64 ? kLMVals * (NT / 64) : 1];
     __shared__ LMShared S;
     __shared__ int s_tmp[40];
@@ -1139,9 +1148,18 @@ __global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t*
     const int tid = threadIdx.x;
     const int64_t e0 = counts ? (int64_t)prob * stride : (int64_t)offsets[prob];
     int n = counts ? counts[prob] : (int)(offsets[prob + 1] - e0);
-    if (n > kMaxEdges) n = kMaxEdges;
-    const double* X = Xall + 3 * e0;
-    const double* uv = uvall + 2 * e0;
+    if (n > CAP) n = CAP;
+    const double* Xg = Xall + 3 * e0;
+    const double* uvg = uvall + 2 * e0;
+    if constexpr (kRes) {
+        for (int i = tid; i < 3 * n; i += NT) s_X[i] = Xg[i];
+        for (int i = tid; i < 2 * n; i += NT) s_uv[i] = (float)uvg[i];
+    }
+    const double* X = kRes ? s_X : Xg;
+    const auto* uv = [&] {
+        if constexpr (kRes) return static_cast<const float*>(s_uv);
+        else return uvg;
+    }();
     if (tid < 9) S.K[tid] = Kall[9 * prob + tid];
     if (tid < 7) S.T[tid] = priors[7 * prob + tid];
     for (int i = tid; i < n; i += NT) {
@@ -1305,7 +1323,8 @@ __global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t*
             int cnt = 0, chg = 0;
             for (int i = tid; i < n; i += NT) {
                 double ee[2];
-                edge_error(s_out[i] ? T : Tl, K, X + 3 * i, uv + 2 * i, ee);
+                const double mi[2] = {(double)uv[2 * i], (double)uv[2 * i + 1]};
+                edge_error(s_out[i] ? T : Tl, K, X + 3 * i, mi, ee);
                 const double c2 = ee[0] * ee[0] + ee[1] * ee[1];
                 const uint8_t lev = c2 > chi2th ? 1 : 0;
                 chg |= lev != s_level[i];
@@ -1336,6 +1355,26 @@ __global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t*
     __syncthreads();  // the next problem reinitialises the shared state
     }
     LMP_STORE();
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
+                                                      int stride, const double* __restrict__ Xall,
+                                                      const double* __restrict__ uvall, const double* __restrict__ Kall,
+                                                      const double* priors, double* poses,
+                                                      uint8_t* __restrict__ outlier_all, int32_t* __restrict__ inliers,
+                                                      int n_prob) {
+    pose_lm_body<NT, kMaxEdges>(offsets, counts, stride, Xall, uvall, Kall, priors, poses, outlier_all, inliers, n_prob);
+}
+// The LDS-resident form (CAP = kLMResCap)
+template <int NT>
+__global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_res_kernel(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
+                                                      int stride, const double* __restrict__ Xall,
+                                                      const double* __restrict__ uvall, const double* __restrict__ Kall,
+                                                      const double* priors, double* poses,
+                                                      uint8_t* __restrict__ outlier_all, int32_t* __restrict__ inliers,
+                                                      int n_prob) {
+    pose_lm_body<NT, kLMResCap>(offsets, counts, stride, Xall, uvall, Kall, priors, poses, outlier_all, inliers, n_prob);
 }
 
 // Track edges of the batched frontend: track t = {stereo pair sp, temporal pair tp} with
@@ -1607,14 +1646,35 @@ inline size_t lm_lds_pad() {
     return p;
 }
 
-template <typename... A>
+// YAVO_LM_RESIDENT=1 puts the track path on the LDS-resident form: its HBM/L2 traffic is the edges once (1.04x the
+// algorithmic bytes, against ~16x when every pass re-streams them), but it takes 256 VGPRs and 78 KB of LDS per
+// workgroup, so two of them fill a CU's register file and half its LDS; measured 1.10 vs 1.06 ms alone and 210.6k vs
+// 214.8k frames/s in the step (profiles/r03/c43).  Off by default.
+inline int& lm_resident_flag() {
+    static int r = [] {
+        const char* e = getenv("YAVO_LM_RESIDENT");
+        return e ? (atoi(e) != 0 ? 1 : 0) : 0;
+    }();
+    return r;
+}
+inline bool lm_resident() { return lm_resident_flag() != 0; }
+
+template <int CAP, typename... A>
 void launch_lm(int n, hipStream_t s, A... args) {
     const int g = lm_grid() > 0 && lm_grid() < n ? lm_grid() : n;
     const size_t pad = lm_lds_pad();
-    switch (lm_threads()) {
-        case 256: hipLaunchKernelGGL(pose_lm_kernel<256>, dim3(g), dim3(256), pad, s, args..., n); break;
-        case 128: hipLaunchKernelGGL(pose_lm_kernel<128>, dim3(g), dim3(128), pad, s, args..., n); break;
-        default: hipLaunchKernelGGL(pose_lm_kernel<64>, dim3(g), dim3(64), pad, s, args..., n); break;
+    if constexpr (CAP == kLMResCap) {
+        switch (lm_threads()) {
+            case 256: hipLaunchKernelGGL(pose_lm_res_kernel<256>, dim3(g), dim3(256), pad, s, args..., n); break;
+            case 128: hipLaunchKernelGGL(pose_lm_res_kernel<128>, dim3(g), dim3(128), pad, s, args..., n); break;
+            default: hipLaunchKernelGGL(pose_lm_res_kernel<64>, dim3(g), dim3(64), pad, s, args..., n); break;
+        }
+    } else {
+        switch (lm_threads()) {
+            case 256: hipLaunchKernelGGL(pose_lm_kernel<256>, dim3(g), dim3(256), pad, s, args..., n); break;
+            case 128: hipLaunchKernelGGL(pose_lm_kernel<128>, dim3(g), dim3(128), pad, s, args..., n); break;
+            default: hipLaunchKernelGGL(pose_lm_kernel<64>, dim3(g), dim3(64), pad, s, args..., n); break;
+        }
     }
 }
 
@@ -1643,8 +1703,8 @@ void launch_world2camera(const double* X, int n, const double* T, const double* 
 
 void launch_pose_lm(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
                     double* poses, uint8_t* outlier, int32_t* inliers, hipStream_t s) {
-    geom::launch_lm(n_problems, s, offsets, static_cast<const int32_t*>(nullptr), 0, X, uv, K,
-                    static_cast<const double*>(poses), poses, outlier, inliers);
+    geom::launch_lm<geom::kMaxEdges>(n_problems, s, offsets, static_cast<const int32_t*>(nullptr), 0, X, uv, K,
+                               static_cast<const double*>(poses), poses, outlier, inliers);
 }
 
 void launch_track_build(const int32_t* tracks, int n_tracks, const int32_t* pairs, const yv_keypoint* keypoints,
@@ -1692,8 +1752,13 @@ void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, cons
                        const double* edge_uv, const double* K, const double* priors, double* poses,
                        uint8_t* edge_outlier, int32_t* inliers, hipStream_t s) {
     if (n_tracks <= 0) return;
-    geom::launch_lm(n_tracks, s, static_cast<const int32_t*>(nullptr), edge_count, stride, edge_X, edge_uv, K,
-                    priors, poses, edge_outlier, inliers);
+    // track edges: uv are keypoint / LK pixel positions (float-exact), at most stride per frame
+    if (stride <= geom::kLMResCap && geom::lm_resident())
+        geom::launch_lm<geom::kLMResCap>(n_tracks, s, static_cast<const int32_t*>(nullptr), edge_count, stride, edge_X,
+                                         edge_uv, K, priors, poses, edge_outlier, inliers);
+    else
+        geom::launch_lm<geom::kMaxEdges>(n_tracks, s, static_cast<const int32_t*>(nullptr), edge_count, stride, edge_X,
+                                   edge_uv, K, priors, poses, edge_outlier, inliers);
 }
 
 void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
@@ -1715,3 +1780,10 @@ extern "C" int yv_debug_lm_prof(unsigned long long* out) {
                    hipSuccess ? 0 : -2;
 }
 #endif
+
+// tests: select the pose LM form of the track path (1 = LDS-resident); returns the previous setting
+extern "C" int yv_debug_lm_resident(int on) {
+    const int prev = yavo::geom::lm_resident_flag();
+    yavo::geom::lm_resident_flag() = on ? 1 : 0;
+    return prev;
+}
