@@ -919,7 +919,9 @@ constexpr int BR_ROWS = BR_BAND + 17;  // rows r0-8 .. r0+40 (the last one for t
 #endif
 constexpr int BR_NT = YAVO_BR_NT;
 constexpr int BR_NW = BR_NT / 64;
-// the band's keypoint records are loaded as 4 per thread (kq below): a band may hold every keypoint of the image
+// the band's keypoint records are loaded as 4 per thread (kq below): a band may hold every keypoint of the image.
+// (A loop over any further records would lift this bound but takes the kernel from 46 to 64 VGPRs, and at <= 48 one
+// BRIEF wave per SIMD still fits beside the side stream's two pose-LM waves: 2 x 232 of 512.)
 static_assert(4 * BR_NT >= kMaxKp, "brief_kernel loads at most 4 * BR_NT band records");
 
 __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict__ blur, int H, int W,
