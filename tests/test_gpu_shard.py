@@ -5,7 +5,8 @@ serial anchor chain.  The result must be the 1-rank run of the same frames: ever
 halo gives rank 1's first temporal pair the same keypoints the 1-rank run's carry slot does) and the placed map
 (keyframe poses, landmark ids and world points) within 1e-12 absolute + 1e-13 relative -- the chunked anchor chain
 A_1 * L_k re-associates the 1-rank left fold rel_0 * ... * rel_k.  The last case is BASELINE
-configs[3]'s length (KITTI sequence 00: 4541 frames) on two ranks.  Reference: the serial chaining of
+configs[3]'s length (KITTI sequence 00: 4541 frames) on two ranks.  RCCL itself needs a GPU per rank, so its leg
+runs at world 1 here (test_rccl_exchange_world1_equals_local).  Reference: the serial chaining of
 src/LoopHandler.cc:139,156."""
 import os
 import socket
@@ -85,3 +86,22 @@ def test_two_rank_shards_equal_one_rank(ctx, tmp_path, B, kf_every):
     # the rank boundary carries the sequence's real motion (the synthetic camera moves 0.21 m per frame), not the
     # identity an empty or stale predecessor would give
     assert np.linalg.norm(res[1]["poses"][0][4:]) > 0.1
+
+
+@pytest.mark.timeout(300)
+def test_rccl_exchange_world1_equals_local(ctx, tmp_path):
+    """The RCCL leg of the shared-map exchange (all_gather_into_tensor on the communication stream, sharding.py) on
+    the box's one GPU: a 1-rank "nccl" process group gathers the block into its own buffer and places it from there.
+    Poses and the placed map must be the no-collective run's, bit for bit."""
+    B, kf_every, seed = 6, 2, 91
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    out = tmp_path / "rank0.npz"
+    p = subprocess.Popen([sys.executable, os.path.join(TESTS, "shard_worker.py"), "0", "1", str(port), str(B),
+                          str(kf_every), str(seed), str(out), "nccl"], env=env)
+    assert p.wait(timeout=240) == 0
+    res = np.load(out)
+    ref_poses, ref_placed = _one_rank(ctx, B, kf_every, seed)
+    np.testing.assert_array_equal(res["poses"], ref_poses)
+    np.testing.assert_array_equal(res["placed"], ref_placed)
+    assert sorted(_map(res["placed"]).frames) == list(range(kf_every, B + 1, kf_every))

@@ -247,7 +247,9 @@ __device__ __forceinline__ JRot make_jacobi(double x, double y, double z) {
     double t = tau > 0 ? 1 / (tau + w) : 1 / (tau - w);
     double sign_t = t > 0 ? 1 : -1;
     double nn = 1 / sqrt(t * t + 1);
-    r.s = -sign_t * (y / fabs(y)) * fabs(t) * nn;
+    // Eigen's y / |y|: exactly +-1 here (2|y| >= DBL_MIN, and the inputs are finite and scaled to <= 1), so the
+    // sign is taken instead of an FP64 division (one of the seven per rotation); the products are unchanged
+    r.s = -sign_t * copysign(1.0, y) * fabs(t) * nn;
     r.c = nn;
     return r;
 }

@@ -147,8 +147,14 @@ class FrameShard:
             self.max_kf = max(max_kf, ymap.max_keyframes(self.n_tracks, first_frame, kf_every), 1)
             self.bb = ymap.block_bytes(self.max_kf, max_kp)
             self.d_block = torch.zeros(self.bb, dtype=torch.uint8, device=dev)
-            self.d_gathered = torch.zeros((world, self.bb), dtype=torch.uint8, device=dev) if world > 1 \
-                else self.d_block
+            # the collective runs whenever a process group is up, so RCCL also carries a 1-rank run's block (the
+            # same stream / event hand-off as at N > 1); without one the block is placed where it was written
+            import torch.distributed as dist
+            self.collective = dist.is_available() and dist.is_initialized()
+            if (self.collective and dist.get_world_size() != world) or (world > 1 and not self.collective):
+                raise ValueError("world must match the process group (and N > 1 needs one)")
+            self.d_gathered = torch.zeros((world, self.bb), dtype=torch.uint8, device=dev) if self.collective \
+                else self.d_block.view(1, self.bb)
             self.d_base = torch.from_numpy(identity.copy()).to(dev)
             self.d_anchors = torch.zeros((world, 7), dtype=torch.float64, device=dev)
             self.comm = torch.cuda.Stream(device=dev)
@@ -159,9 +165,9 @@ class FrameShard:
         # the last track_map's block: all-gathered and placed on the communication stream once it is written
         self.batch.map_wait(self.comm.cuda_stream)
         with torch.cuda.stream(self.comm):
-            if self.world > 1 and self.backend == "nccl":
+            if self.collective and self.backend == "nccl":
                 dist.all_gather_into_tensor(self.d_gathered, self.d_block)
-            elif self.world > 1:  # gloo: list form
+            elif self.collective:  # gloo: list form
                 dist.all_gather(list(self.d_gathered.unbind(0)), self.d_block)
             self.ctx.map_place(self.d_gathered.data_ptr(), self.world, self.bb, self.d_base.data_ptr(),
                                self.d_anchors.data_ptr(), stream=self.comm.cuda_stream)
