@@ -47,9 +47,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=1024,
-                    help="stereo frames per step per GPU (1024: four pose-LM problems per CU, two rounds; r02 measured "
-                         "188k / 195k / 198k / 200k frames/s at 512 / 768 / 1024 / 1536)")
+    ap.add_argument("--frames", type=int, default=2048,
+                    help="stereo frames per step per GPU (2048: eight pose-LM problems per CU, four rounds; r03 measured "
+                         "214k / 219k / 221k frames/s at 1024 / 1536 / 2048 on one box, profiles/r03/c51)")
     ap.add_argument("--cpu-baseline", choices=["both", "literal", "efficient", "none"], default="both")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads of the CPU baseline (0: the usable cores, affinity capped by OMP_NUM_THREADS)")
@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--loop-handler-frames", type=int, default=200,
                     help="frames of the drop-in C++ LoopHandler leg (rank 0, N=1; tools/bench_loop_handler.py); 0 "
                          "skips it")
+    ap.add_argument("--collective-world1", action="store_true",
+                    help="at N=1, still run the shared-map exchange through a 1-rank process group (RCCL)")
     ap.add_argument("--kf-every", type=int, default=4,
                     help="shared map: frames with global index %% kf_every == 0 are keyframes (their LM inliers "
                          "become landmarks); 0 disables the map and its all-gather")
@@ -369,6 +371,16 @@ def main():
     if world > 1:
         torch.cuda.set_device(dev_index)
         dist.init_process_group(backend)
+    elif args.collective_world1:
+        # a 1-rank group: the shared-map exchange then runs the N > 1 path (the RCCL all-gather on its stream)
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(port))
+        torch.cuda.set_device(dev_index)
+        dist.init_process_group(backend, rank=0, world_size=1)
     dev = torch.device("cuda", dev_index)
     torch.cuda.set_device(dev)
 
@@ -656,7 +668,8 @@ def main():
             n_lm += sum(len(x) for x in lms)
         out["shared_map"] = {"kf_every": args.kf_every, "block_bytes": bb, "keyframes_per_step": n_kf,
                              "landmarks_per_step": n_lm, "allgather_bytes_per_rank_per_step": bb * world,
-                             "collective": ("none (1 rank)" if world == 1 else
+                             "collective": ("none (1 rank)" if world == 1 and not shard.collective else
+                                            "all_gather_into_tensor (RCCL, 1-rank group)" if world == 1 else
                                             "all_gather_into_tensor (RCCL)" if backend == "nccl" else
                                             f"all_gather ({backend} rehearsal)")}
     if rank == 0 and world == 1 and args.cpu_baseline != "none" and args.tracker == "match":
@@ -674,7 +687,7 @@ def main():
         print(json.dumps(out), flush=True)
     shard.close()
     ctx.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

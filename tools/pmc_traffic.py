@@ -46,7 +46,7 @@ def load(out_dir, counter, pass_dir=None):
 
 def main():
     out_dir = sys.argv[1]
-    frames = 1024  # bench.py's default (--frames)
+    frames = 2048  # bench.py's default (--frames)
     args = sys.argv[2:]
     if "--frames" in args:
         frames = int(args[args.index("--frames") + 1])
