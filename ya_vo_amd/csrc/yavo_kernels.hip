@@ -1651,29 +1651,43 @@ __global__ __launch_bounds__(FZ_NT) void match_finalize_kernel(
     uint32_t* out_all = reinterpret_cast<uint32_t*>(matches + (int64_t)pair * max_kp);
     uint32_t* out_f = reinterpret_cast<uint32_t*>(filtered + (int64_t)pair * max_kp);
     const int ndw = nq * REC_DW;
-    for (int dw = tid; dw < ndw; dw += FZ_NT) {
-        const int i = dw / REC_DW;
-        const int f = dw - i * REC_DW;
-        uint32_t v;
-        bool is_matched_dw = false;
-        if (f < 12) {
-            v = qrec[(int64_t)i * 12 + f];
-            if (f == 11) v &= 0xFFu;  // featVec[31]; the 3 pad bytes are always written as 0
-            is_matched_dw = (f == 3);
-        } else if (f < 24) {
-            const int g = f - 12;
+    // Branch-free record assembly: every lane issues one load per record dword from an address that is always
+    // valid (query record dword f < 12; train record dword min(f - 12, 2) of train j, or of train 0 when j < 0; the
+    // value is then selected), FZ_U dwords per thread with every load in flight before the stores.  A wave's 64
+    // consecutive dwords span ~2.5 records, so per-field branches ran all three paths with a load wait in each
+    // (0.83 -> 0.67 ms per 2048-frame step, profiles/r03/c54).
+#ifndef YAVO_FZ_U
+#define YAVO_FZ_U 4
+#endif
+    constexpr int FZ_U = YAVO_FZ_U;
+    for (int dw0 = tid; dw0 < ndw; dw0 += FZ_U * FZ_NT) {
+        uint32_t v[FZ_U];
+        int ii[FZ_U], ff[FZ_U];
+#pragma unroll
+        for (int u = 0; u < FZ_U; ++u) {
+            const int dw = min(dw0 + u * FZ_NT, ndw - 1);
+            const int i = dw / REC_DW, f = dw - i * REC_DW;
             const int j = s_j[i];
-            v = 0;
-            if (g < 3 && j >= 0) v = trec[(int64_t)j * 12 + g];
-            is_matched_dw = (g == 3);
-        } else {
-            v = (uint32_t)s_dist[i];
+            const uint32_t* src = f < 12 ? qrec + (int64_t)i * 12 + f : trec + (int64_t)max(j, 0) * 12 + min(f - 12, 2);
+            v[u] = *src;
+            ii[u] = i;
+            ff[u] = f;
         }
-        out_all[dw] = v;
-        const int p = s_pos[i];
-        if (p >= 0) {
-            if (is_matched_dw) v = (v & ~0xFFu) | 1u;  // matched = true on both copies
-            out_f[(int64_t)p * REC_DW + f] = v;
+#pragma unroll
+        for (int u = 0; u < FZ_U; ++u) {
+            const int dw = dw0 + u * FZ_NT;
+            if (dw >= ndw) break;
+            const int i = ii[u], f = ff[u];
+            uint32_t x = v[u];
+            if (f == 11) x &= 0xFFu;                         // featVec[31]; the 3 pad bytes are always written as 0
+            else if (f >= 12 && (f >= 15 || s_j[i] < 0)) x = 0;  // pt2: x, y, id of the train keypoint only
+            if (f == 24) x = (uint32_t)s_dist[i];
+            out_all[dw] = x;
+            const int p = s_pos[i];
+            if (p >= 0) {
+                if (f == 3 || f == 15) x = (x & ~0xFFu) | 1u;  // matched = true on both copies
+                out_f[(int64_t)p * REC_DW + f] = x;
+            }
         }
     }
     if (tid == 0) {
