@@ -143,6 +143,7 @@ class FrameShard:
         self.use_map = kf_every > 0 and tracker == "match"
         self.kf_every = kf_every
         self._pending = False
+        self.collective = False
         if self.use_map:
             self.max_kf = max(max_kf, ymap.max_keyframes(self.n_tracks, first_frame, kf_every), 1)
             self.bb = ymap.block_bytes(self.max_kf, max_kp)
