@@ -341,12 +341,33 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         const bool interior = (c0 >= FT_R) && (c0 + FT_W + FT_R <= W) && (r0 >= FT_R) && (r0 + FT_H + FT_R < H);
         uint32_t v[kPer];
         if (interior) {
+#ifndef YAVO_DET_STAGE_OLD
+            // one wave-uniform base (SGPRs) and a 32-bit lane offset: slot t + 256 is 14 rows and 4 dwords on, or 15
+            // rows and 14 dwords back when the dword index wraps past 18 (256 = 14 * 18 + 4), so one division for
+            // the first slot and a compare + select + add for each further one (the same slots as the division form)
+            const uint8_t* base = src + (int64_t)(r0 - FT_R) * stride + (c0 - FT_R);
+            const int lr0 = tid / kDw, j0 = tid - lr0 * kDw;
+            uint32_t off = (uint32_t)(lr0 * stride + 4 * j0);
+            int j = j0;
+            const uint32_t step = (uint32_t)(14 * stride + 16), wrap = (uint32_t)(15 * stride - 56);
+            const uint32_t last = (uint32_t)((kSlots - 1) / kDw * stride + 4 * ((kSlots - 1) % kDw));
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                // slots past the tile (t >= kSlots, last pass only) read the last slot again; their store is skipped
+                const uint32_t o = (256 * u + 255 >= kSlots && tid + 256 * u >= kSlots) ? last : off;
+                __builtin_memcpy(&v[u], base + o, 4);
+                const bool c = j + 4 >= kDw;
+                off += c ? wrap : step;
+                j += c ? 4 - kDw : 4;
+            }
+#else
 #pragma unroll
             for (int u = 0; u < kPer; ++u) {
                 const int t = min(tid + 256 * u, kSlots - 1);
                 const int lr = t / kDw, j = t - lr * kDw;
                 __builtin_memcpy(&v[u], src + (int64_t)(r0 - FT_R + lr) * stride + (c0 - FT_R) + 4 * j, 4);
             }
+#endif
         } else {
 #pragma unroll
             for (int u = 0; u < kPer; ++u) {
@@ -1451,6 +1472,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
             const int t = t0 + tt;
             pre[k] = t < nt ? tw[(int64_t)t * 8 + u] : 0u;
         }
+        // (c_j from the staged dwords by DPP popcount sums over each descriptor's 8 lanes, instead of waves 0-1
+        // re-reading 128 descriptors here, measured slower: match 1.64 -> 1.70 ms per 2048-frame step, r03/c56)
         if (tid < MF_TC) {
             const int t = t0 + tid;
             pre_c = t < nt ? (float)((2047 - t) - 2048 * desc_popcount(td[t]) + (1 << 21)) : 0.f;
@@ -1510,6 +1533,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
             buf ^= 1;
         }
     }
+    // the popcount of the query each lane writes (row 4g + (col & 3) of every tile; lanes col >= 4 repeat one of
+    // those), its descriptor loads all issued here at once: read inside the 32 writer branches below, each load was
+    // waited for before its branch joined (match 1.74 -> 1.64 ms per 2048-frame step, profiles/r03/c56)
+    int pa_q[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+        pa_q[qt] = desc_popcount(qd[min(q0 + 16 * QT * wave + 16 * qt + 4 * g + (col & 3), nq - 1)]);
     // per query row: max over the 16 lanes (train columns) of its lane group
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
@@ -1525,7 +1555,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 uint32_t key = 0xFFFFFFFFu;  // empty train set (nt >= 1 always leaves a real key in the row max)
                 if (nt > 0) {
                     const int iv = (int)__uint_as_float(v) - (1 << 21);
-                    const int pa = desc_popcount(qd[q]);
+                    const int pa = pa_q[qt];
                     const uint32_t d = (uint32_t)(pa - (iv >> 11));
                     const uint32_t jj = 2047u - ((uint32_t)iv & 2047u);
                     key = (d << 16) | jj;
