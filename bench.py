@@ -351,8 +351,84 @@ def cpu_baseline(kind, threads, offsets, images, B, gpu_poses, edges, literal_fr
     return res
 
 
+def launch_plan(n_gpus, environ, device_count, backend):
+    """Rank environments for `bench.py --gpus N` started without a launcher (no WORLD_SIZE in the environment): one
+    fresh child process per GPU, each told its RANK / LOCAL_RANK / WORLD_SIZE and the rendezvous on 127.0.0.1.
+    Returns None when this process is itself the only rank (N = 1 or a launcher already set WORLD_SIZE).  Raises
+    ValueError when the request cannot be honoured: RCCL ("nccl") needs one visible device per rank; the gloo rehearsal
+    may place several ranks on one device (device = local rank modulo the visible devices)."""
+    if n_gpus < 1:
+        raise ValueError(f"--gpus must be >= 1 (got {n_gpus})")
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != n_gpus and n_gpus != 1:
+            raise ValueError(f"--gpus {n_gpus} but the launcher set WORLD_SIZE={ws}")
+        return None
+    if n_gpus == 1:
+        return None
+    if backend == "nccl" and device_count < n_gpus:
+        raise ValueError(f"--gpus {n_gpus} needs {n_gpus} visible GPUs for RCCL, {device_count} visible")
+    if device_count < 1:
+        raise ValueError("no visible GPU")
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    plans = []
+    for r in range(n_gpus):
+        env = dict(environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n_gpus), "LOCAL_WORLD_SIZE": str(n_gpus),
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between processes on this host)
+        plans.append(env)
+    return plans
+
+
+def spawn_ranks(plans, argv, script=None):
+    """Run one child per rank environment (this script again, same arguments), rank 0's stdout passed through (it prints
+    the JSON line), the other ranks' stdout sent to stderr.  Waits for all; if any rank fails the others are stopped
+    (by their own PIDs) and its exit code is returned."""
+    import subprocess
+    procs = []
+    for env in plans:
+        out = None if env["RANK"] == "0" else sys.stderr
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env, stdout=out))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     args = parse()
+    backend = os.environ.get("YAVO_BENCH_BACKEND", "nccl")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` without torchrun: one fresh process per GPU, started before this process touches the GPU
+        # (counting devices does not initialise the runtime on this image)
+        import torch
+        try:
+            plans = launch_plan(args.gpus, os.environ, torch.cuda.device_count(), backend)
+        except ValueError as e:
+            print(f"bench.py: {e}", file=sys.stderr)
+            sys.exit(2)
+        sys.exit(spawn_ranks(plans, sys.argv[1:]))
+    elif "WORLD_SIZE" in os.environ:
+        try:
+            launch_plan(args.gpus, os.environ, 0, backend)
+        except ValueError as e:
+            print(f"bench.py: {e}", file=sys.stderr)
+            sys.exit(2)
     import torch
     import torch.distributed as dist
     import ya_vo_amd as yv
@@ -366,7 +442,6 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU over RCCL ("nccl"); YAVO_BENCH_BACKEND=gloo rehearses the multi-rank logic with
     # several ranks sharing fewer GPUs (device = local rank modulo the visible devices)
-    backend = os.environ.get("YAVO_BENCH_BACKEND", "nccl")
     dev_index = local_rank % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(dev_index)
@@ -635,6 +710,7 @@ def main():
                              f"and detects / describes its predecessor frame r*B in the same run (1-frame halo, "
                              f"image {n_img - 1}), so every temporal pair L_(k-1) -> L_k is the sequence's own",
                    "halo_images_per_step_per_gpu": n_img - 2 * B,
+                   "devices_used": min(world, max(torch.cuda.device_count(), 1)),
                    "parallelism": f"frame-sharded x{world}" + (f", {'RCCL' if backend == 'nccl' else backend} "
                                                                  "all-gather of shared-map blocks"
                                                                  if use_map and world > 1 else ""),

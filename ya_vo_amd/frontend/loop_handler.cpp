@@ -502,13 +502,14 @@ void LoopHandler::runVOPipelined(int max_frames) {
                     ahead.pop_front();
                     refill();
                     worker_read += now_s() - t0;
+                    // the index travels with the item: only the tracking thread sets currentFrameId_, and
+                    // train_it_ is advanced by this thread alone while the pipeline runs
                     if (it.frame) {
-                        currentFrameId_ = (int)train_it_;
+                        it.index = (int)train_it_;
                         train_it_++;
                         it.frame->frameID = Frame::createFrameID();
                     }
                 }
-                it.index = currentFrameId_;
                 if (it.frame) {
                     const double t0 = now_s();
                     auto features = wfd->getFastFeatures(*it.frame);
