@@ -321,8 +321,24 @@ def cpu_baseline(kind, threads, offsets, images, B, gpu_poses, edges, literal_fr
                             "sample": f"frames 0..{n - 1} of the benchmarked shard, same outputs with local Harris "
                                       f"sums and a precomputed ring, {threads} threads over frames",
                             "seconds": round(dt, 3), "stages_ms_per_frame": stage_table(out)}
+    # the full chain also on a block in the middle of the step and on its last 16 frames (images up to 4096: the
+    # device buffers' offsets there are far past 2^31 bytes), efficient mode (same outputs)
+    extra = sorted((set(range(max(B // 2 - 8, 0), min(B // 2 + 8, B))) | set(range(max(B - 16, 0), B))) - set(cpu_poses))
+    if extra:
+        prevs_x = {k: left_kp(prev_image(k)) for k in extra}
+        with ThreadPoolExecutor(threads) as ex:
+            out_x = list(ex.map(lambda k: one_frame(k, prevs_x[k], 1), extra))
+        for k, r in zip(extra, out_x):
+            cpu_poses[k] = r[0]
     ks = sorted(cpu_poses)
     same = bool(np.array_equal(np.array([gpu_poses[k] for k in ks]), np.array([cpu_poses[k] for k in ks])))
+    runs, start = [], None
+    for i, k in enumerate(ks):
+        if start is None:
+            start = k
+        if i + 1 == len(ks) or ks[i + 1] != k + 1:
+            runs.append(f"{start}..{k}")
+            start = None
     # every frame of the step: the oracle's pose LM on the GPU's own edges, in the kernel's order (must reproduce the
     # GPU pose bit for bit) and in the reference's sequential order (the metric's RMSE)
     ec, eX, euv = edges
@@ -338,6 +354,17 @@ def cpu_baseline(kind, threads, offsets, images, B, gpu_poses, edges, literal_fr
     gpu_order = np.array([x[0] for x in lm])
     seq_order = np.array([x[1] for x in lm])
     d = gpu_poses - seq_order
+    # the same LMs with the host C library's pow / sin / cos (as g2o / Sophus call them) instead of the restated
+    # functions the kernels share: how many of the step's poses the substitution moves, and by how much
+    orc.set_libm_flavour(1)
+    try:
+        with ThreadPoolExecutor(threads) as ex:
+            libm = np.array(list(ex.map(
+                lambda k: orc.pose_lm(eX[k, :ec[k]], euv[k, :ec[k]], scene.K_KITTI, prior, yv.lm_sum_mode())[0],
+                range(len(ec)))))
+    finally:
+        orc.set_libm_flavour(0)
+    dl = gpu_poses - libm
     res["pose_check"] = {
         "frames": len(ec),
         "pose_rmse_vs_cpu_ref": float(np.sqrt(np.mean(np.sum(d[:, 4:] ** 2, axis=1)))),
@@ -345,9 +372,15 @@ def cpu_baseline(kind, threads, offsets, images, B, gpu_poses, edges, literal_fr
         "cpu_ref": "oracle pose LM (optimizePoseOnly) in the reference's sequential edge order (sum_mode 0) on the "
                    "GPU's edges, every frame of the step",
         "bit_identical_gpu_order_all_frames": bool(np.array_equal(gpu_poses, gpu_order)),
+        "host_libm_flavour": {"poses_differing": int(np.sum(~np.all(dl == 0, axis=1))),
+                              "max_abs_diff": float(np.abs(dl).max()),
+                              "what": "oracle pose LM on the GPU's edges, kernel sum order, with glibc's pow / sin / "
+                                      "cos (the reference's g2o / Sophus calls) instead of the restated ones"},
         "chain_frames": len(ks),
+        "chain_frame_ranges": runs,
         "chain_bit_identical": same,
-        "chain": "full CPU chain (detect .. pose LM) of the cpu_baseline sample frames vs the GPU, kernel sum order"}
+        "chain": "full CPU chain (detect .. pose LM) vs the GPU, kernel sum order: the cpu_baseline sample frames, a "
+                 "16-frame block in the middle of the step and its last 16 frames"}
     return res
 
 

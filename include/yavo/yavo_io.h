@@ -74,9 +74,14 @@ int yv_seq_upload_gpu(yv_seq* seq, yv_pngdec* d, int first, int n, uint8_t* d_ds
  * (e.g. a shard's frames then its halo frame) */
 int yv_seq_upload_gpu_frames(yv_seq* seq, yv_pngdec* d, const int* frames, int n, uint8_t* d_dst, int64_t pitch,
                              int threads, void* stream);
-/* waits for the last decode; codes[i] (optional, host, n of the last call) = 0 or the image's decode error;
- * *n_bad = images that failed */
+/* waits for the last decode; codes[i] (optional, host, n of the last call) = 0 or the image's decode error
+ * (1 zlib header, 2 block, 3 Huffman code, 4 output overrun, 5 stream short, 6 filter type, 7 an IDAT chunk's CRC-32,
+ * 8 the zlib Adler-32 trailer: missing or wrong); *n_bad = images that failed in EVERY decode since the previous
+ * yv_pngdec_status call.  A failed image's device output is zero-filled (cv::imread returns an empty Mat). */
 int yv_pngdec_status(yv_pngdec* d, int32_t* codes, int* n_bad);
+/* the integrity checks of the following decodes (default both on, as libpng / zlib do): crc = every IDAT chunk's
+ * CRC-32 (libpng png_set_crc_action), adler = the zlib Adler-32 trailer (libpng PNG_IGNORE_ADLER32 turns it off) */
+int yv_pngdec_set_checks(yv_pngdec* d, int crc, int adler);
 
 /* The writer side, for test sequences (the reference only reads PNGs): an 8-bit grey image to a PNG file, every row
  * Sub-filtered and deflated at level 1 with Z_RLE, as cv::imwrite writes PNGs (the reference's tests/epilines.png:

@@ -626,6 +626,21 @@ void or_brief_offsets_mt19937(uint32_t seed, int8_t* out) {
         for (int j = 0; j < 4; j++) out[4 * i + j] = (int8_t)mt_uniform_int(&g, -8, 8);
 }
 
+/* A persistent std::mt19937 drawing uniform_int_distribution<int>(a, b) values, as the C++ LoopHandler's getFRANSAC
+ * draws its 400 x 8 sample indices (ya_vo_amd/frontend/loop_handler.cpp: one engine seeded once, a fresh
+ * distribution of range [0, n - 1] per call; the reference seeds from std::random_device, src/3DHandler.cc:157-159). */
+void* or_mt19937_new(uint32_t seed) {
+    or_mt19937* g = (or_mt19937*)malloc(sizeof(or_mt19937));
+    if (g) mt_seed(g, seed);
+    return g;
+}
+
+void or_mt19937_uniform_ints(void* g, int a, int b, int count, int32_t* out) {
+    for (int i = 0; i < count; ++i) out[i] = mt_uniform_int((or_mt19937*)g, a, b);
+}
+
+void or_mt19937_free(void* g) { free(g); }
+
 /* Brief::popCount, src/BriefDescriptor.cc:151-160 (bit loop kept literally). */
 static int or_popcount_literal(uint8_t v) {
     int count = 0;

@@ -31,6 +31,15 @@ static inline double or_cube(double t) {
     return q + (e2 + e1 * t);
 }
 
+/* libm flavour of the oracle's geometry (or_set_libm_flavour): 0 (default) = the restated functions the GPU kernels
+ * share (or_cube above for g2o's pow(2 rho - 1, 3); fdlibm's __kernel_sin / __kernel_cos in Sophus' SO3::exp);
+ * 1 = the host C library's pow / sin / cos, as g2o (OptimizationAlgorithmLevenberg::solve) and Sophus (std::sin /
+ * std::cos) call them in the reference's build.  Flavour 1 measures what the substitution moves. */
+extern int or_libm_flavour;
+void or_set_libm_flavour(int flavour);
+void or_cube_batch(const double* t, int n, int flavour, double* out);
+static inline double or_lm_cube(double t) { return or_libm_flavour ? pow(t, 3) : or_cube(t); }
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -82,6 +91,10 @@ int or_compute_brief(const uint8_t* img, int H, int W, int stride, const uint16_
 /* Brief::preComputeOffsets (:4-20) with an explicit seed instead of std::random_device:
  * std::mt19937(seed) + uniform_int_distribution<int>(-8, 8) (libstdc++ algorithm). */
 void or_brief_offsets_mt19937(uint32_t seed, int8_t* out /* 1024 */);
+/* a persistent std::mt19937(seed); or_mt19937_uniform_ints draws `count` uniform_int_distribution<int>(a, b) values */
+void* or_mt19937_new(uint32_t seed);
+void or_mt19937_uniform_ints(void* g, int a, int b, int count, int32_t* out);
+void or_mt19937_free(void* g);
 
 /* Brief::popCount (:151-160) / hammingDistance (:139-146). */
 int or_hamming(const uint8_t* a, const uint8_t* b);

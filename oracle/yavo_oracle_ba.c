@@ -418,7 +418,7 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
             scale += 1e-3;
             rho /= scale;
             if (rho > 0 && isfinite(tempChi)) {
-                double alpha = 1. - or_cube(2 * rho - 1);  /* pow(2 rho - 1, 3), correctly rounded */
+                double alpha = 1. - or_lm_cube(2 * rho - 1);  /* pow(2 rho - 1, 3): correctly rounded, or libm */
                 alpha = fmin(alpha, 2. / 3.);
                 const double sf = fmax(1. / 3., alpha);
                 lambda *= sf;

@@ -432,11 +432,19 @@ int or_eigen_jacobi_svd(const double* A, int n, double* sv, double* V) {
 /* Sophus SE3 (pose = {qx, qy, qz, qw, tx, ty, tz}, SE3d::data() layout)                        */
 /* ========================================================================================== */
 
-/* fdlibm __kernel_sin / __kernel_cos (|x| <= pi/4); larger |x| falls back to the C library. */
+int or_libm_flavour = 0;
+void or_set_libm_flavour(int flavour) { or_libm_flavour = flavour ? 1 : 0; }
+
+/* or_cube (flavour 0) or the C library's pow(t, 3) (flavour 1) over n arguments */
+void or_cube_batch(const double* t, int n, int flavour, double* out) {
+    for (int i = 0; i < n; ++i) out[i] = flavour ? pow(t[i], 3) : or_cube(t[i]);
+}
+
+/* fdlibm __kernel_sin / __kernel_cos (|x| <= pi/4); larger |x|, or the libm flavour, call the C library. */
 static double k_sin(double x) {
     const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03, S3 = -1.98412698298579493134e-04,
                  S4 = 2.75573137070700676789e-06, S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
-    if (!(fabs(x) <= 0.78539816339744827900)) return sin(x);
+    if (or_libm_flavour || !(fabs(x) <= 0.78539816339744827900)) return sin(x);
     double z = x * x, v = z * x;
     double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
     return x + v * (S1 + z * r);
@@ -445,7 +453,7 @@ static double k_sin(double x) {
 static double k_cos(double x) {
     const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03, C3 = 2.48015872894767294178e-05,
                  C4 = -2.75573143513906633035e-07, C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
-    if (!(fabs(x) <= 0.78539816339744827900)) return cos(x);
+    if (or_libm_flavour || !(fabs(x) <= 0.78539816339744827900)) return cos(x);
     double z = x * x;
     double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
     double hz = 0.5 * z, w = 1.0 - hz;
@@ -957,7 +965,7 @@ static int lm_optimize(lm_problem* P, double* T, int iterations) {
             if (rho > 0 && isfinite(tempChi) && ok2) {
                 g_lm_stats[2]++;
                 double t = 2 * rho - 1;
-                double alpha = 1. - or_cube(t);
+                double alpha = 1. - or_lm_cube(t);
                 alpha = alpha < goodUpper ? alpha : goodUpper;
                 double sf = goodLower > alpha ? goodLower : alpha;
                 lambda *= sf;

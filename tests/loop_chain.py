@@ -48,6 +48,7 @@ class LoopChain:
         self.keyframes = set()
         self.poses, self.events = [], []
         self._ev = None
+        self.rng = orc.mt19937(0)  # getFRANSAC's engine (loop_handler.hpp ransac_rng_{0})
 
     # ---- primitives ----
     def features(self, img):
@@ -57,6 +58,16 @@ class LoopChain:
     def matches(self):
         m = self.orc.match(self.last.kps, self.curr.kps)
         return self.orc.remove_outliers(m, 20) if len(m) else np.zeros(0, MATCH_DTYPE)
+
+    def f_ransac(self, filt):
+        """getFRANSAC(filterMatches, F, 400, 0.1) (src/3DHandler.cc:145-195; F unused, :222, :562): the inlier count
+        of the best of 400 eight-point hypotheses, or 0 when fewer than 8 matches (no draws then)."""
+        n = len(filt)
+        if n < 8:
+            return 0
+        smp = self.rng.uniform_ints(0, n - 1, 8 * 400)
+        ok, _, mi = self.orc.f_ransac(filt, smp, 0.1)
+        return mi if ok else 0
 
     def essential_pose(self, filt):
         prev = np.stack([filt["pt1"]["x"], filt["pt1"]["y"]], 1).astype(np.float32).astype(np.float64)
@@ -91,6 +102,7 @@ class LoopChain:
         for m in filt:
             self.last.features.append([int(m["pt1"]["x"]), int(m["pt1"]["y"]), None])
             self.curr.features.append([int(m["pt2"]["x"]), int(m["pt2"]["y"]), None])
+        self._ev["f_inliers"] = self.f_ransac(filt)
         curr_pose = self.essential_pose(filt)
         self.curr.pose = self.orc.se3_inverse(curr_pose)
         self.keyframes.update((self.last.id, self.curr.id))
@@ -151,6 +163,7 @@ class LoopChain:
         self.curr.features = []
         filt = self.matches()
         self._ev["matches_kept"] = len(filt)
+        self._ev["f_inliers"] = self.f_ransac(filt)
         curr_pose = self.orc.se3_inverse(self.essential_pose(filt))
         self.curr.pose = self.orc.se3_mul(curr_pose, self.last.pose)
         self._ev["new_landmarks"] = self.triangulate2view(filt, False)

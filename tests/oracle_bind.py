@@ -33,12 +33,17 @@ class Oracle:
             "or_eigen_jacobi_f32": (None, [_P, _I, _P]),
             "or_eigen_selfadjoint2_f32": (None, [ctypes.c_float, ctypes.c_float, ctypes.c_float, _P]),
             "or_set_harris_eigen": (None, [_I]),
+            "or_set_libm_flavour": (None, [_I]),
+            "or_cube_batch": (None, [_P, _I, _I, _P]),
             "or_std_sort_cut": (_I, [_P, _P, _I, _I, _I, _P]),
             "or_gauss_kernel_fixed": (None, [_I, ctypes.c_double, _I, _P]),
             "or_gaussian_blur_u8": (None, [_P, _I, _I, _I, _P, _I, _P]),
             "or_compute_brief_blurred": (_I, [_P, _I, _I, _P, _P, _I, _P, ctypes.POINTER(_I)]),
             "or_compute_brief": (_I, [_P, _I, _I, _I, _P, _P, _P, _I, _P, ctypes.POINTER(_I)]),
             "or_brief_offsets_mt19937": (None, [ctypes.c_uint32, _P]),
+            "or_mt19937_new": (ctypes.c_void_p, [ctypes.c_uint32]),
+            "or_mt19937_uniform_ints": (None, [ctypes.c_void_p, _I, _I, _I, _P]),
+            "or_mt19937_free": (None, [ctypes.c_void_p]),
             "or_hamming": (_I, [_P, _P]),
             "or_match": (_I, [_P, _I, _P, _I, _P]),
             "or_remove_outliers": (_I, [_P, _I, _I, _P, ctypes.POINTER(_I)]),
@@ -117,6 +122,18 @@ class Oracle:
 
     def harris_response(self, m00, m01, m11):
         return self.lib.or_harris_response(m00, m01, m11)
+
+    def set_libm_flavour(self, flavour):
+        """0: the restated pow / sin / cos the GPU kernels share (default); 1: the host C library's, as g2o / Sophus
+        call them (process-wide switch of the oracle library)."""
+        self.lib.or_set_libm_flavour(int(flavour))
+
+    def cube(self, t, flavour=0):
+        """g2o's pow(t, 3) as the oracle evaluates it: correctly rounded (0) or the host C library's pow (1)."""
+        t = np.ascontiguousarray(t, np.float64)
+        out = np.empty_like(t)
+        self.lib.or_cube_batch(_p(t), len(t), int(flavour), _p(out))
+        return out
 
     def set_harris_eigen(self, flavour):
         """cv::eigen flavour of the Harris response: 0 = JacobiImpl_ (default), 1 = HAVE_EIGEN (Eigen 3.4)."""
@@ -209,6 +226,25 @@ class Oracle:
         F = np.zeros(9)
         ok = self.lib.or_fundamental_8pt(_p(pts), len(pts), _p(F))
         return bool(ok), F.reshape(3, 3)
+
+    def mt19937(self, seed):
+        """A persistent std::mt19937(seed): .uniform_ints(a, b, count) draws uniform_int_distribution<int>(a, b)."""
+        lib = self.lib
+
+        class _MT:
+            def __init__(self):
+                self.h = lib.or_mt19937_new(seed)
+
+            def uniform_ints(self, a, b, count):
+                out = np.zeros(count, np.int32)
+                lib.or_mt19937_uniform_ints(self.h, a, b, count, _p(out))
+                return out
+
+            def __del__(self):
+                if self.h:
+                    lib.or_mt19937_free(self.h)
+                    self.h = None
+        return _MT()
 
     def f_ransac(self, matches, samples, thr=0.1):
         m = np.ascontiguousarray(matches, MATCH_DTYPE)

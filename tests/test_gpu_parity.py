@@ -259,6 +259,62 @@ def test_batch_pipeline_matches_oracle(ctx, oracle, offsets):
     b.close()
 
 
+def test_large_batch_tail_matches_oracle(ctx, oracle, offsets):
+    """A 642-image batch (321 stereo frames, the bench's layout and pairs): the candidate-key buffer offsets pass
+    2^31 bytes at image 592 (453,744 keys x 8 B per image), so the images on both sides of that boundary and the last
+    ones are compared with the oracle: candidate counts, FAST + Harris + top-2000 rows / columns, the blurred image,
+    BRIEF keypoints, and the temporal + stereo Matches / removeOutliers of the pairs between them
+    (src/FastDetector.cc:277-369, src/BriefDescriptor.cc:86-231)."""
+    from ya_vo_amd.synth import synth_stereo_batch
+    H, W, n_frames, thr = 376, 1241, 321, 20
+    frames = synth_stereo_batch(4242, n_frames)
+    n_img = len(frames)
+    assert (n_img - 1) * (H - 8) * (W - 8) * 8 > 2 ** 31
+    pairs = []
+    for k in range(n_frames):
+        if k > 0:
+            pairs.append((2 * (k - 1), 2 * k))  # temporal L_{k-1} -> L_k
+        pairs.append((2 * k, 2 * k + 1))        # stereo L_k -> R_k
+    b = yv.Batch(ctx, n_img, H, W, 2000, len(pairs))
+    b.set_pairs(pairs)
+    d = _device_frames(ctx, frames)
+    b.run(d.data_ptr(), n_img, W, H * W, thr, carry_from=-1)
+    ctx.sync()
+    v = b.view()
+    kpc = ctx.download(v.kp_count, np.int32, b.max_images + 1)
+    detc = ctx.download(v.det_count, np.int32, b.max_images + 1)
+    candc = ctx.download(v.cand_count, np.uint32, b.max_images + 1)
+    check = [0, 1, 590, 591, 592, 593, 594, 595, n_img - 4, n_img - 3, n_img - 2, n_img - 1]
+    ref = {}
+    bp = v.blur_pitch
+    for i in check:
+        img = frames[i]
+        orc, _, onc = oracle.fast(img, 2000)
+        assert candc[i] == onc and detc[i] == len(orc), i
+        rc = ctx.download(v.det_rc + i * 2000 * 8, np.int32, 2 * detc[i]).reshape(-1, 2)
+        np.testing.assert_array_equal(rc, orc)
+        blur = ctx.download(v.blurred + i * H * bp, np.uint8, H * bp).reshape(H, bp)[:, :W]
+        np.testing.assert_array_equal(blur, oracle.blur(img))
+        kps = ctx.download(v.keypoints + i * 2000 * 48, yv.KEYPOINT_DTYPE, kpc[i])
+        ref[i] = oracle.brief(img, orc, offsets)
+        np.testing.assert_array_equal(kps, ref[i])
+    mc = ctx.download(v.match_count, np.int32, len(pairs))
+    fc = ctx.download(v.filt_count, np.int32, len(pairs))
+    compared = 0
+    for p, (qi, ti) in enumerate(pairs):
+        if qi not in ref or ti not in ref:
+            continue
+        om = oracle.match(ref[qi], ref[ti])
+        of = oracle.remove_outliers(om, thr)
+        assert mc[p] == len(om) and fc[p] == len(of)
+        np.testing.assert_array_equal(ctx.download(v.matches + p * 2000 * 100, yv.MATCH_DTYPE, mc[p]), om)
+        np.testing.assert_array_equal(ctx.download(v.filtered + p * 2000 * 100, yv.MATCH_DTYPE, fc[p]), of)
+        compared += 1
+    assert compared >= 8
+    b.close()
+    del d
+
+
 def test_batch_is_deterministic_and_timed(ctx):
     H, W = 376, 1241
     frames = np.stack([synth_frame(2, k, 3 * k) for k in range(4)])

@@ -44,18 +44,35 @@ def _png(img, filt, level, strategy=zlib.Z_DEFAULT_STRATEGY):
         rows.append(bytes([f]) + ((cur - pred) & 0xFF).astype(np.uint8).tobytes())
     c = zlib.compressobj(level, zlib.DEFLATED, 15, 8, strategy)
     z = c.compress(b"".join(rows)) + c.flush()
-
-    def chunk(t, d):
-        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
-    # the IDAT stream split over several chunks, as encoders do
-    idat = b"".join(chunk(b"IDAT", z[i:i + 8192]) for i in range(0, len(z), 8192))
-    return (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", W, H, 8, 0, 0, 0, 0)) + idat +
-            chunk(b"IEND", b""))
+    return _png_from_z(z, H, W)
 
 
-def _decode_gpu(ctx, files, H, W):
+def _chunk(t, d):
+    return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
+
+
+def _png_from_z(z, H, W):
+    """A PNG around the zlib stream z, IDAT split over 8 KB chunks as encoders do, every chunk CRC correct."""
+    idat = b"".join(_chunk(b"IDAT", z[i:i + 8192]) for i in range(0, len(z), 8192))
+    return (b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", struct.pack(">IIBBBBB", W, H, 8, 0, 0, 0, 0)) + idat +
+            _chunk(b"IEND", b""))
+
+
+def _zstream(f):
+    """The zlib stream of a PNG file (its IDAT payloads concatenated)."""
+    p, z = 8, b""
+    while p < len(f):
+        n = struct.unpack(">I", f[p:p + 4])[0]
+        if f[p + 4:p + 8] == b"IDAT":
+            z += bytes(f[p + 8:p + 8 + n])
+        p += 12 + n
+    return z
+
+
+def _decode_gpu(ctx, files, H, W, checks=(1, 1)):
     import torch
     dec = PngDecoder(ctx, len(files), H, W)
+    dec.set_checks(*checks)
     d = torch.zeros(len(files) * H * W, dtype=torch.uint8, device="cuda:0")
     dec.decode(files, d.data_ptr(), H * W)
     codes, bad = dec.status()
@@ -126,19 +143,60 @@ def test_gpu_png_rowwise_and_wavefront_unfilter(ctx, H, W):
         np.testing.assert_array_equal(o, img)
 
 
+PNG_ERR_CRC, PNG_ERR_ADLER = 7, 8
+
+
 def test_gpu_png_reports_corrupt_stream(ctx):
+    """cv::imread's integrity checks (libpng: a critical chunk's CRC-32; zlib: the Adler-32 trailer): a damaged IDAT
+    chunk is reported by its CRC, a stream whose CRCs were recomputed by its Adler-32 (or a decode error), a wrong or
+    missing trailer by its Adler-32; failed images come back zero-filled, the good ones intact."""
     H, W = 40, 50
     img = np.random.default_rng(1).integers(0, 256, (H, W), dtype=np.uint8)
     good = _png(img, 1, 6)
+    z = _zstream(good)
     bad = bytearray(good)
     i = bad.index(b"IDAT") + 4 + 40
     for k in range(i, i + 30):
-        bad[k] ^= 0x5A  # garbage inside the deflate data (the chunk CRC is not what the decoder checks)
-    out, codes, n_bad = _decode_gpu(ctx, [good, bytes(bad), good], H, W)
+        bad[k] ^= 0x5A  # garbage inside the deflate data, the chunk CRC left as it was
+    zb = bytearray(z)
+    for k in range(40, 70):
+        zb[k] ^= 0x5A   # the same garbage with valid chunk CRCs: zlib's own checks must catch it
+    wrong_adler = z[:-4] + bytes([z[-4] ^ 1]) + z[-3:]
+    no_trailer = z[:-4]
+    files = [good, bytes(bad), good, _png_from_z(bytes(zb), H, W), _png_from_z(wrong_adler, H, W),
+             _png_from_z(no_trailer, H, W)]
+    out, codes, n_bad = _decode_gpu(ctx, files, H, W)
     np.testing.assert_array_equal(out[0], img)
     np.testing.assert_array_equal(out[2], img)
-    # a damaged stream either fails a check or decodes to something else; it never faults or hangs the wave
-    assert n_bad <= 1 and codes[0] == 0 and codes[2] == 0
+    assert codes[0] == 0 and codes[2] == 0
+    assert codes[1] == PNG_ERR_CRC
+    assert codes[3] != 0
+    assert codes[4] == PNG_ERR_ADLER and codes[5] == PNG_ERR_ADLER
+    assert n_bad == 4
+    for k in (1, 3, 4, 5):
+        assert not out[k].any(), k  # zero-filled
+
+
+def test_gpu_png_status_counts_every_decode(ctx):
+    """yv_pngdec_status's n_bad covers every decode since the previous query (a bench step decodes twice per status)."""
+    import torch
+    H, W = 16, 24
+    img = np.random.default_rng(3).integers(0, 256, (H, W), dtype=np.uint8)
+    good = _png(img, 2, 6)
+    bad = bytearray(good)
+    bad[bad.index(b"IDAT") + 10] ^= 0xFF
+    dec = PngDecoder(ctx, 3, H, W)
+    d = torch.zeros(3 * H * W, dtype=torch.uint8, device="cuda:0")
+    dec.decode([good, bytes(bad), good], d.data_ptr(), H * W)
+    dec.decode([bytes(bad), good, bytes(bad)], d.data_ptr(), H * W)
+    codes, n_bad = dec.status()
+    assert n_bad == 3
+    assert list(codes[:3]) == [PNG_ERR_CRC, 0, PNG_ERR_CRC]  # the codes are the last decode's
+    dec.decode([good, good, good], d.data_ptr(), H * W)
+    codes, n_bad = dec.status()
+    assert n_bad == 0 and not any(codes[:3])
+    np.testing.assert_array_equal(d.cpu().numpy().reshape(3, H, W), np.stack([img] * 3))
+    dec.close()
 
 
 def test_gpu_png_sequence_upload(ctx, tmp_path):
@@ -175,8 +233,10 @@ def test_gpu_png_sequence_upload(ctx, tmp_path):
 def test_gpu_png_randomized_streams_match_zlib(ctx):
     """Differential fuzz of the lane-parallel inflate: random sizes, row filters, zlib levels and strategies (every
     block type, short and long matches, far distances, chunks capped by highly compressible rows); then the same
-    streams with random bytes flipped inside the deflate data: whenever zlib's raw inflate (no Adler-32 check) yields
-    an image's worth of valid rows, the GPU yields the same image; otherwise it reports an error (never a fault)."""
+    streams with random bytes flipped inside the deflate data: with the chunk CRCs left as they were every damaged file
+    is reported by its CRC; with the CRCs recomputed every damaged file that zlib rejects (decode error or Adler-32) is
+    reported too, and whenever zlib's raw inflate (no Adler-32 check) yields an image's worth of valid rows, the GPU's
+    inflate produced the same bytes, which the Adler-32 then rejects (never a fault)."""
     rng = np.random.default_rng(20261017)
     strategies = [zlib.Z_DEFAULT_STRATEGY, zlib.Z_FILTERED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE, zlib.Z_FIXED]
     H, W = 61, 203
@@ -223,7 +283,22 @@ def test_gpu_png_randomized_streams_match_zlib(ctx):
         except zlib.error:
             ref = None
         expect.append(ref)
-    out, codes, _ = _decode_gpu(ctx, bad_files, H, W)
+    out, codes, n_bad = _decode_gpu(ctx, bad_files, H, W)
+    assert n_bad == len(bad_files) and all(c == PNG_ERR_CRC for c in codes), codes
+    # the damaged streams again, in files whose chunk CRCs were recomputed: zlib's decode or its Adler-32 rejects every
+    # one of them (checked here), and so does the GPU
+    refiled = [_png_from_z(_zstream(b), H, W) for b in bad_files]
+    for b in refiled:
+        with pytest.raises(zlib.error):
+            zlib.decompress(_zstream(b))
+    out, codes, n_bad = _decode_gpu(ctx, refiled, H, W)
+    assert n_bad == len(refiled) and all(c != 0 for c in codes), codes
+    assert not out.any()
+    for i, ref in enumerate(expect):
+        if ref is not None:  # zlib's raw inflate yields valid rows: the GPU got past inflate and unfilter too
+            assert codes[i] == PNG_ERR_ADLER, (i, codes[i])
+    # with the checks off (libpng's PNG_CRC_QUIET_USE / PNG_IGNORE_ADLER32), the damaged streams' bytes themselves
+    out, codes, _ = _decode_gpu(ctx, bad_files, H, W, checks=(0, 0))
     n_ok = 0
     for i, ref in enumerate(expect):
         if ref is None:

@@ -141,8 +141,9 @@ def main():
     # ---- pyramidal LK: L frame pairs (synthetic 1241x376, frame k+1 = frame k shifted), 2000 points each --
     from ya_vo_amd.synth import synth_stereo_batch
     H, W = 376, 1241
-    imgs = synth_stereo_batch(77, L // 2 + 1)[::2]  # left images of consecutive frames
-    imgs = np.ascontiguousarray(imgs[: L // 2 + 1])
+    LP = max(L // 2, 1)
+    imgs = synth_stereo_batch(77, LP + 1)[::2]  # left images of consecutive frames
+    imgs = np.ascontiguousarray(imgs[: LP + 1])
     n_img = len(imgs)
     n_pairs = n_img - 1
     npts = 2000

@@ -163,6 +163,7 @@ IO_SIGNATURES = {
     "yv_seq_upload_gpu": (_I, [_P, _P, _I, _I, _P, ctypes.c_int64, _I, _P]),
     "yv_seq_upload_gpu_frames": (_I, [_P, _P, _P, _I, _P, ctypes.c_int64, _I, _P]),
     "yv_pngdec_status": (_I, [_P, _P, ctypes.POINTER(_I)]),
+    "yv_pngdec_set_checks": (_I, [_P, _I, _I]),
     "yv_write_kitti_poses": (_I, [ctypes.c_char_p, _P, _I]),
     "yv_read_kitti_poses": (_I, [ctypes.c_char_p, _P, _I, ctypes.POINTER(_I)]),
 }

@@ -29,9 +29,14 @@ struct yv_ctx {
     int32_t* h_pinned = nullptr;                              // small pinned scratch for counts
     void* scratch = nullptr;                                  // device arena of the geometry host calls
     size_t scratch_cap = 0;
+    void* fr_ws = nullptr;                                    // yv_f_ransac_batch's hypothesis workspace
+    size_t fr_ws_cap = 0;
     // yv_calc_optical_flow_pyr_lk's pyramid workspace, kept between calls (creating and destroying it per call
     // costs two hipMalloc / hipFree pairs and a device-wide synchronisation per tracked frame)
     yv_lk* lk_cache = nullptr;
+    // the host findEssentialMat / recoverPose calls' workspace (yv_essential_create is ~10 hipMallocs, its destroy a
+    // device synchronisation: per call they cost more than the solve), grown on demand
+    yv_essential* ess_cache = nullptr;
     int lk_key[4] = {0, 0, 0, 0};  // H, W, win, max_level
     // Pinned staging of the host-pointer entry points.  The caller's buffers are pageable: a hipMemcpyAsync from or to
     // pageable memory is synchronous and goes through the runtime's own staging (~250 us per call, even for a
@@ -410,8 +415,10 @@ void yv_destroy(yv_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->lk_cache) yv_lk_destroy(ctx->lk_cache);
+    if (ctx->ess_cache) yv_essential_destroy(ctx->ess_cache);
     batch_free(ctx->single);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->fr_ws) (void)hipFree(ctx->fr_ws);
     if (ctx->d_offsets) (void)hipFree(ctx->d_offsets);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
@@ -1265,7 +1272,9 @@ int yv_f_ransac(yv_ctx* ctx, const yv_match* m, int n, const int32_t* samples, i
     yv_match* dm;
     int32_t *dcnt, *dsmp, *dmax, *dfound;
     double* dF;
+    uint8_t* dws;
     a.add(&dm, (size_t)n);
+    a.add(&dws, yavo::f_ransac_ws_bytes(1, iters));
     a.add(&dcnt, 1);
     a.add(&dsmp, (size_t)std::max(8 * iters, 1));
     a.add(&dF, 9);
@@ -1277,7 +1286,7 @@ int yv_f_ransac(yv_ctx* ctx, const yv_match* m, int n, const int32_t* samples, i
     YV_HIP(stage_h2d(ctx, dcnt, ctx->h_pinned, sizeof(int32_t), s));
     if (iters > 0) YV_HIP(stage_h2d(ctx, dsmp, samples, sizeof(int32_t) * 8 * (size_t)iters, s));
     YV_HIP(stage_h2d(ctx, dF, F, sizeof(double) * 9, s));  // untouched if iters == 0
-    yavo::launch_f_ransac(dm, n, dcnt, 1, dsmp, 8 * (int64_t)iters, iters, thr, dF, dmax, dfound, s);
+    yavo::launch_f_ransac(dm, n, dcnt, 1, dsmp, 8 * (int64_t)iters, iters, thr, dF, dmax, dfound, dws, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
     YV_HIP(stage_d2h(ctx, F, dF, sizeof(double) * 9, s));
     YV_HIP(stage_d2h(ctx, ctx->h_pinned + 1, dmax, sizeof(int32_t), s));
@@ -1433,8 +1442,17 @@ int yv_f_ransac_batch(yv_ctx* ctx, const yv_match* d_matches, int64_t list_strid
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
     StageScope stage_scope(ctx);
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+    const size_t need = yavo::f_ransac_ws_bytes(n_lists, iters);
+    if (need > ctx->fr_ws_cap) {  // grown outside any timed loop; earlier launches that use it have finished
+        YV_HIP(hipDeviceSynchronize());
+        if (ctx->fr_ws) (void)hipFree(ctx->fr_ws);
+        ctx->fr_ws = nullptr;
+        ctx->fr_ws_cap = 0;
+        YV_HIP(hipMalloc(&ctx->fr_ws, need));
+        ctx->fr_ws_cap = need;
+    }
     yavo::launch_f_ransac(d_matches, list_stride, d_counts, n_lists, d_samples, sample_stride, iters, thr, d_F,
-                          d_max_inliers, d_found, s);
+                          d_max_inliers, d_found, ctx->fr_ws, s);
     return check_launch();
 }
 
@@ -1679,10 +1697,11 @@ int yv_essential_create(yv_ctx* ctx, int max_pairs, int max_points, int max_iter
     P.max_pairs = max_pairs;
     P.max_points = max_points;
     P.max_iters = max_iters;
+    P.chunk = yavo::ess_chunk_for(max_pairs);
     const size_t np = (size_t)max_pairs;
     if (dalloc(&P.m1, np * max_points * 2) != YV_OK || dalloc(&P.m2, np * max_points * 2) != YV_OK ||
-        dalloc(&P.idx, np * max_iters * 5) != YV_OK || dalloc(&P.models, np * yavo::kEssChunk * 90) != YV_OK ||
-        dalloc(&P.nmod, np * yavo::kEssChunk) != YV_OK || dalloc(&P.good, np * yavo::kEssChunk * 10) != YV_OK ||
+        dalloc(&P.idx, np * max_iters * 5) != YV_OK || dalloc(&P.models, np * P.chunk * 90) != YV_OK ||
+        dalloc(&P.nmod, np * P.chunk) != YV_OK || dalloc(&P.good, np * P.chunk * 10) != YV_OK ||
         dalloc(&P.state, np * 8) != YV_OK || dalloc(&P.best, np * 9) != YV_OK || dalloc(&P.cand, np * 48) != YV_OK ||
         dalloc(&P.cgood, np * 4) != YV_OK) {
         essential_free(es);
@@ -1733,6 +1752,22 @@ int yv_recover_pose_batch(yv_essential* es, const double* d_E, const float* d_pt
     return check_launch();
 }
 
+// the context's cached one-list essential workspace with room for `points` points and `iters` RANSAC iterations
+static int ctx_essential(yv_ctx* ctx, int points, int iters, yv_essential** out) {
+    yv_essential* es = ctx->ess_cache;
+    if (!es || es->P.max_points < points || es->P.max_iters < iters) {
+        if (es) yv_essential_destroy(es);
+        ctx->ess_cache = nullptr;
+        const int rc = yv_essential_create(ctx, 1, std::max(points, 2048), std::max(iters, 1000), &ctx->ess_cache);
+        if (rc != YV_OK) {
+            ctx->ess_cache = nullptr;
+            return rc;
+        }
+    }
+    *out = ctx->ess_cache;
+    return YV_OK;
+}
+
 int yv_find_essential(yv_ctx* ctx, const float* pts1, const float* pts2, int n, double focal, double ppx, double ppy,
                       double prob, double threshold, double E[9], uint8_t* mask, int* found) {
     if (!ctx || !E || !found || n < 0 || (n > 0 && (!pts1 || !pts2))) return YV_ERR_INVALID;
@@ -1747,7 +1782,7 @@ int yv_find_essential(yv_ctx* ctx, const float* pts1, const float* pts2, int n, 
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
     StageScope stage_scope(ctx);
     yv_essential* es = nullptr;
-    int rc = yv_essential_create(ctx, 1, n, 1000, &es);
+    int rc = ctx_essential(ctx, n, 1000, &es);
     if (rc != YV_OK) return rc;
     hipStream_t s = ctx->stream;
     Arena a{ctx};
@@ -1761,10 +1796,7 @@ int yv_find_essential(yv_ctx* ctx, const float* pts1, const float* pts2, int n, 
     a.add(&dm, (size_t)n);
     a.add(&dcnt, 1);
     a.add(&dfound, 1);
-    if (a.commit() != YV_OK) {
-        yv_essential_destroy(es);
-        return YV_ERR_HIP;
-    }
+    if (a.commit() != YV_OK) return YV_ERR_HIP;
     int st = YV_OK;
     do {
         ctx->h_pinned[0] = n;
@@ -1786,7 +1818,6 @@ int yv_find_essential(yv_ctx* ctx, const float* pts1, const float* pts2, int n, 
         }
         *found = ctx->h_pinned[1];
     } while (0);
-    yv_essential_destroy(es);
     return st;
 }
 
@@ -1797,7 +1828,7 @@ int yv_recover_pose(yv_ctx* ctx, const double E[9], const float* pts1, const flo
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
     StageScope stage_scope(ctx);
     yv_essential* es = nullptr;
-    int rc = yv_essential_create(ctx, 1, std::max(n, 5), 1, &es);
+    int rc = ctx_essential(ctx, std::max(n, 5), 1, &es);
     if (rc != YV_OK) return rc;
     hipStream_t s = ctx->stream;
     Arena a{ctx};
@@ -1811,10 +1842,7 @@ int yv_recover_pose(yv_ctx* ctx, const double E[9], const float* pts1, const flo
     a.add(&dt, 3);
     a.add(&dcnt, 1);
     a.add(&dgood, 1);
-    if (a.commit() != YV_OK) {
-        yv_essential_destroy(es);
-        return YV_ERR_HIP;
-    }
+    if (a.commit() != YV_OK) return YV_ERR_HIP;
     int st = YV_OK;
     do {
         ctx->h_pinned[0] = n;
@@ -1836,7 +1864,6 @@ int yv_recover_pose(yv_ctx* ctx, const double E[9], const float* pts1, const flo
         }
         *good = ctx->h_pinned[1];
     } while (0);
-    yv_essential_destroy(es);
     return st;
 }
 

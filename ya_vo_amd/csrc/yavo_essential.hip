@@ -3,7 +3,7 @@
 // 4.x path like oracle/yavo_oracle_essential.c, expression for expression (built with -ffp-contract=off):
 //
 //   ess_prepare_kernel   (p - c) / f per point as OpenCV's MatExpr evaluates it, float -> double
-//   ess_subsets_kernel   getSubset's cv::RNG((uint64)-1) draws of a 64-iteration round (one lane per list; the draws
+//   ess_subsets_kernel   getSubset's cv::RNG((uint64)-1) draws of a round (64 iterations; 256 for <= 8 lists) (one lane per list; the draws
 //                        never depend on the models, so a round's subsets are drawn before its models)
 //   ess_models_kernel    EMEstimatorCallback::runKernel, one lane per RANSAC iteration of a 64-iteration round
 //                        (16-lane workgroups):
@@ -454,7 +454,7 @@ __global__ __launch_bounds__(256) void ess_prepare_kernel(const float* __restric
     m2[1] = (double)b[1] * ay + sy;
 }
 
-// the draws of iterations [chunk0, chunk0 + kEssChunk) of a still-running list; the RNG state carries over in
+// the draws of iterations [chunk0, chunk0 + P.chunk) of a still-running list; the RNG state carries over in
 // state[6..7] (cv::RNG((uint64)-1) at chunk 0)
 __global__ void ess_subsets_kernel(int n_pairs, EssParams P, int chunk0, int iters) {
     const int pair = blockIdx.x * blockDim.x + threadIdx.x;
@@ -464,7 +464,7 @@ __global__ void ess_subsets_kernel(int n_pairs, EssParams P, int chunk0, int ite
     if (count <= 5 || chunk0 >= st[0]) return;
     int32_t* idx = P.idx + (int64_t)pair * P.max_iters * 5;
     uint64_t rng = chunk0 == 0 ? (uint64_t)-1 : ((uint64_t)(uint32_t)st[7] << 32) | (uint32_t)st[6];
-    const int end = min(chunk0 + kEssChunk, iters);
+    const int end = min(chunk0 + P.chunk, iters);
     for (int it = chunk0; it < end; ++it) {
         int d[5];
 #pragma unroll
@@ -496,7 +496,7 @@ __global__ __launch_bounds__(kModelLanes) void ess_models_kernel(EssParams P, in
     const int it = chunk0 + k;
     const int32_t* st = P.state + 8 * pair;
     const int n = st[5];
-    int32_t* nmod = P.nmod + pair * kEssChunk + k;
+    int32_t* nmod = P.nmod + pair * P.chunk + k;
     const bool single = n == 5;
     if (n < 5 || it >= st[0] || (single && it > 0)) {
         *nmod = 0;
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(kModelLanes) void ess_models_kernel(EssParams P, in
         q2[2 * i] = m2[2 * j];
         q2[2 * i + 1] = m2[2 * j + 1];
     }
-    double* out = P.models + ((int64_t)pair * kEssChunk + k) * 90;
+    double* out = P.models + ((int64_t)pair * P.chunk + k) * 90;
     *nmod = em_models(q1, q2, out);
 }
 
@@ -525,9 +525,9 @@ __global__ __launch_bounds__(256) void ess_score_kernel(EssParams P, int chunk0,
     const int k = blockIdx.x;
     const int32_t* st = P.state + 8 * pair;
     const int n = st[5];
-    const int nm = P.nmod[pair * kEssChunk + k];
+    const int nm = P.nmod[pair * P.chunk + k];
     if (n <= 5 || chunk0 + k >= st[0] || nm == 0) return;
-    const double* src = P.models + ((int64_t)pair * kEssChunk + k) * 90;
+    const double* src = P.models + ((int64_t)pair * P.chunk + k) * 90;
     for (int i = threadIdx.x; i < nm * 9; i += 256) s_E[i] = src[i];
     if (threadIdx.x < 10) s_cnt[threadIdx.x] = 0;
     __syncthreads();
@@ -548,7 +548,7 @@ __global__ __launch_bounds__(256) void ess_score_kernel(EssParams P, int chunk0,
         if (m < nm && (threadIdx.x & 63) == 0 && v) atomicAdd(&s_cnt[m], v);
     }
     __syncthreads();
-    if (threadIdx.x < nm) P.good[(pair * kEssChunk + k) * 10 + threadIdx.x] = s_cnt[threadIdx.x];
+    if (threadIdx.x < nm) P.good[(pair * P.chunk + k) * 10 + threadIdx.x] = s_cnt[threadIdx.x];
 }
 
 __global__ void ess_select_kernel(EssParams P, int n_pairs, int chunk0, double prob) {
@@ -557,8 +557,8 @@ __global__ void ess_select_kernel(EssParams P, int n_pairs, int chunk0, double p
     int32_t* st = P.state + 8 * pair;
     const int n = st[5];
     if (n < 5) return;
-    const int32_t* nmod = P.nmod + pair * kEssChunk;
-    const double* models = P.models + (int64_t)pair * kEssChunk * 90;
+    const int32_t* nmod = P.nmod + pair * P.chunk;
+    const double* models = P.models + (int64_t)pair * P.chunk * 90;
     double* best = P.best + 9 * pair;
     if (n == 5) {
         if (chunk0 == 0) {
@@ -573,8 +573,8 @@ __global__ void ess_select_kernel(EssParams P, int n_pairs, int chunk0, double p
         return;
     }
     int niters = st[0], max_good = st[1], run = st[2], total = st[3];
-    const int32_t* good = P.good + pair * kEssChunk * 10;
-    for (int k = 0; k < kEssChunk; ++k) {
+    const int32_t* good = P.good + pair * P.chunk * 10;
+    for (int k = 0; k < P.chunk; ++k) {
         const int it = chunk0 + k;
         if (it >= niters) break;
         const int nm = nmod[k];
@@ -776,11 +776,11 @@ void launch_find_essential(const EssParams& P, const EssRun& r, const float* pts
     double thr = r.threshold;
     thr /= (r.focal + r.focal) / 2;
     const float t = (float)(thr * thr);
-    for (int c0 = 0; c0 < iters; c0 += kEssChunk) {
+    for (int c0 = 0; c0 < iters; c0 += P.chunk) {
         hipLaunchKernelGGL(ess::ess_subsets_kernel, dim3((n_pairs + 63) / 64), dim3(64), 0, s, n_pairs, P, c0, iters);
-        hipLaunchKernelGGL(ess::ess_models_kernel, dim3(kEssChunk / ess::kModelLanes, n_pairs), dim3(ess::kModelLanes),
+        hipLaunchKernelGGL(ess::ess_models_kernel, dim3(P.chunk / ess::kModelLanes, n_pairs), dim3(ess::kModelLanes),
                            0, s, P, c0);
-        hipLaunchKernelGGL(ess::ess_score_kernel, dim3(kEssChunk, n_pairs), dim3(256), 0, s, P, c0, t);
+        hipLaunchKernelGGL(ess::ess_score_kernel, dim3(P.chunk, n_pairs), dim3(256), 0, s, P, c0, t);
         hipLaunchKernelGGL(ess::ess_select_kernel, dim3((n_pairs + 63) / 64), dim3(64), 0, s, P, n_pairs, c0, r.prob);
     }
     hipLaunchKernelGGL(ess::ess_output_kernel, gpts, dim3(256), 0, s, P, pts_stride, t, E, mask, found, stats);

@@ -85,14 +85,147 @@ __device__ int block_excl_scan_geom(int v, int* s_tmp, int* total) {
 
 // OpenCV JacobiSVDImpl_<double>, cv::RNG, hypot: yavo_cvsvd.h
 
+// a wave-uniform double (the value of lane 0) in SGPRs
+__device__ __forceinline__ double uni_f64(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
 
-// getFundamentalMatrix (src/3DHandler.cc:50-142) on 8 correspondences pts[8][4] = (x1, y1, x2, y2)
-__device__ void fundamental_8pt(const double* pts, double* F) {
+
+// OpenCV JacobiSVDImpl_<double>(At 9x9, W, Vt) (yavo_cvsvd.h cv_jacobi_svd_mn<9, 9, 9>, operation for operation) as
+// getFundamentalMatrix uses it: only the row of Vt that OpenCV's descending sort of W leaves last is read
+// (src/3DHandler.cc:104-106, F0 = V row 8), so U's normalisation, its FULL_UV completion (both write At only) and the
+// sorted W itself are not formed.  The sort's swap sequence is replayed on the row indices, ties and NaNs included,
+// so the row picked is the one OpenCV's swaps leave at position 8.  At, Vt and W are lane-private rows in LDS laid out
+// [element][lane] (s[e * 64 + lane]): every access of a wave is one conflict-free ds_*_b64, and the rotation loops
+// stay rolled (a 9 x 9 SVD unrolled into registers is ~10k instructions, more than the instruction cache).
+__device__ void cv_svd9_last_v(double* sA, double* sV, double* sW, double out[9]) {
+    constexpr int L = 64;  // lane stride of one element
+    const double eps = DBL_EPSILON * 10;
+    for (int i = 0; i < 9; i++) {
+        double sd = 0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            const double t = sA[(i * 9 + k) * L];
+            sd += t * t;
+        }
+        sW[i * L] = sd;
+#pragma unroll
+        for (int k = 0; k < 9; k++) sV[(i * 9 + k) * L] = i == k ? 1.0 : 0.0;
+    }
+    for (int iter = 0; iter < 30; iter++) {  // max_iter = max(m, 30)
+        bool changed = false;
+        for (int i = 0; i < 8; i++) {
+            double* Ai = sA + i * 9 * L;
+            double* Vi = sV + i * 9 * L;
+            for (int j = i + 1; j < 9; j++) {
+                double* Aj = sA + j * 9 * L;
+                double ai[9], aj[9];
+#pragma unroll
+                for (int k = 0; k < 9; k++) {
+                    ai[k] = Ai[k * L];
+                    aj[k] = Aj[k * L];
+                }
+                double a = sW[i * L], p = 0, b = sW[j * L];
+#pragma unroll
+                for (int k = 0; k < 9; k++) p += ai[k] * aj[k];
+                if (fabs(p) <= eps * sqrt(a * b)) continue;
+                p *= 2;
+                double c, s;
+                const double beta = a - b, gamma = cv_hypot(p, beta);
+                if (beta < 0) {
+                    const double delta = (gamma - beta) * 0.5;
+                    s = sqrt(delta / gamma);
+                    c = p / (gamma * s * 2);
+                } else {
+                    c = sqrt((gamma + beta) / (gamma * 2));
+                    s = p / (gamma * c * 2);
+                }
+                a = b = 0;
+#pragma unroll
+                for (int k = 0; k < 9; k++) {
+                    const double t0 = c * ai[k] + s * aj[k];
+                    const double t1 = -s * ai[k] + c * aj[k];
+                    Ai[k * L] = t0;
+                    Aj[k * L] = t1;
+                    a += t0 * t0;
+                    b += t1 * t1;
+                }
+                sW[i * L] = a;
+                sW[j * L] = b;
+                changed = true;
+                double* Vj = sV + j * 9 * L;
+                double vi[9], vj[9];
+#pragma unroll
+                for (int k = 0; k < 9; k++) {
+                    vi[k] = Vi[k * L];
+                    vj[k] = Vj[k * L];
+                }
+#pragma unroll
+                for (int k = 0; k < 9; k++) {
+                    Vi[k * L] = c * vi[k] + s * vj[k];
+                    Vj[k * L] = -s * vi[k] + c * vj[k];
+                }
+            }
+        }
+        if (!changed) break;
+    }
+    // W[i] = |row i of At|, then OpenCV's selection sort (descending, first maximum) on (W, row index)
+    double w[9];
+    int idx[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        double sd = 0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            const double t = sA[(i * 9 + k) * L];
+            sd += t * t;
+        }
+        w[i] = sqrt(sd);
+        idx[i] = i;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        int j = i;
+        double wj = w[i];
+        int xj = idx[i];
+#pragma unroll
+        for (int k = i + 1; k < 9; k++)
+            if (wj < w[k]) {
+                j = k;
+                wj = w[k];
+                xj = idx[k];
+            }
+        // swap positions i and j (a no-op when j == i)
+        const double wi = w[i];
+        const int xi = idx[i];
+#pragma unroll
+        for (int k = i + 1; k < 9; k++)
+            if (k == j) {
+                w[k] = wi;
+                idx[k] = xi;
+            }
+        w[i] = wj;
+        idx[i] = xj;
+    }
+    const double* Vr = sV + idx[8] * 9 * L;
+#pragma unroll
+    for (int k = 0; k < 9; k++) out[k] = Vr[k * L];
+}
+
+// getFundamentalMatrix (src/3DHandler.cc:50-142) on 8 correspondences pts[8][4] = (x1, y1, x2, y2); sA / sV / sW:
+// this lane's LDS rows of cv_svd9_last_v
+__device__ void fundamental_8pt(const double* pts, double* F, double* sA, double* sV, double* sW) {
+    constexpr int L = 64;
     const int n = 8;
     double xs[4][8];
+#pragma unroll
     for (int i = 0; i < n; ++i)
+#pragma unroll
         for (int q = 0; q < 4; ++q) xs[q][i] = pts[4 * i + q];
     double N[2][9];
+#pragma unroll
     for (int v = 0; v < 2; ++v) {
         const double* x = xs[2 * v];
         const double* y = xs[2 * v + 1];
@@ -113,6 +246,7 @@ __device__ void fundamental_8pt(const double* pts, double* F) {
         M[6] = 0; M[7] = 0; M[8] = 1;
     }
     double A[8][9];
+#pragma unroll
     for (int i = 0; i < n; i++) {
         const double* N1 = N[0];
         const double* N2 = N[1];
@@ -124,22 +258,27 @@ __device__ void fundamental_8pt(const double* pts, double* F) {
         A[i][3] = ny1 * nx2; A[i][4] = ny1 * ny2; A[i][5] = ny1;
         A[i][6] = nx2; A[i][7] = ny2; A[i][8] = 1;
     }
-    double At[81], V[81], w9[9];
     // AtA = A^T A (symmetric); _SVDcompute transposes it into temp_a
+#pragma unroll
     for (int i = 0; i < 9; ++i)
+#pragma unroll
         for (int j = 0; j < 9; ++j) {
             double s = 0;
+#pragma unroll
             for (int k = 0; k < n; ++k) s += A[k][i] * A[k][j];
-            At[j * 9 + i] = s;
+            sA[(j * 9 + i) * L] = s;
         }
-    cv_jacobi_svd<9>(At, w9, V);
     double F0[9], A3[9], V3[9], w3[3];
-    for (int i = 0; i < 9; ++i) F0[i] = V[8 * 9 + i];
+    cv_svd9_last_v(sA, sV, sW, F0);
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
         for (int j = 0; j < 3; ++j) A3[i * 3 + j] = F0[j * 3 + i];
     cv_jacobi_svd<3>(A3, w3, V3);
     double U[9];
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
         for (int j = 0; j < 3; ++j) U[i * 3 + j] = A3[j * 3 + i];
     w3[2] = 0;
     double D[9] = {w3[0], 0, 0, 0, w3[1], 0, 0, 0, w3[2]};
@@ -152,6 +291,7 @@ __device__ void fundamental_8pt(const double* pts, double* F) {
     mm3(N2t, F0, T);
     mm3(T, N1, F0);
     double inv = 1. / F0[8];
+#pragma unroll
     for (int i = 0; i < 9; ++i) F[i] = F0[i] * inv + 0.0;
 }
 
@@ -162,68 +302,102 @@ __device__ __forceinline__ double epipolar_error(const double* F, double x1, dou
     return r0 * x1 + r1 * y1 + r2 * 1.0;
 }
 
-// One workgroup per match list; hypotheses h = tid, tid + 256, ... ; strict '>' keeps the first best.
-__global__ __launch_bounds__(kNT) void f_ransac_kernel(const yv_match* __restrict__ matches, int64_t list_stride,
-                                                       const int32_t* __restrict__ counts,
-                                                       const int32_t* __restrict__ samples, int64_t sample_stride,
-                                                       int iters, double thr, double* __restrict__ F_out,
-                                                       int32_t* __restrict__ max_inliers, int32_t* __restrict__ found) {
-    __shared__ int s_best_cnt[kNT];
-    __shared__ int s_best_h[kNT];
-    const int list = blockIdx.x;
-    const int tid = threadIdx.x;
+// getFRANSAC (src/3DHandler.cc:145-195) in three launches, so a list's 400 hypotheses spread over the chip instead of
+// one workgroup (round 3: 5.1 ms per 1,935-match list, the 9 x 9 SVDs in scratch):
+//   f_hyp_kernel    one lane per hypothesis, 64 per workgroup: its 8 sampled matches -> F (getFundamentalMatrix)
+//   f_count_kernel  one wave per hypothesis, lanes over the matches: inliers |p2^T F p1| < thr (exact integer counts,
+//                   so the order of the partial counts does not matter)
+//   f_select_kernel one wave per list: the most inliers, then the first hypothesis (the reference's strict '>' in
+//                   hypothesis order), its F, the count and `found`
+constexpr int kFHypWG = 64;
+constexpr int kFCountWaves = 4;
+
+__global__ __launch_bounds__(kFHypWG) void f_hyp_kernel(const yv_match* __restrict__ matches, int64_t list_stride,
+                                                        const int32_t* __restrict__ counts,
+                                                        const int32_t* __restrict__ samples, int64_t sample_stride,
+                                                        int iters, double* __restrict__ ws_F) {
+    __shared__ double s_A[81 * kFHypWG], s_V[81 * kFHypWG], s_W[9 * kFHypWG];
+    const int list = blockIdx.y, lane = threadIdx.x;
+    const int h = blockIdx.x * kFHypWG + lane;
+    int n = counts[list];
+    if (n > kMaxKp) n = kMaxKp;
+    if (n < 8 || h >= iters) return;  // no barriers below: lanes leave independently
+    const yv_match* m = matches + (int64_t)list * list_stride;
+    const int32_t* smp = samples + (int64_t)list * sample_stride + 8 * (int64_t)h;
+    double pts8[32];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        int idx = smp[j];
+        idx = idx < 0 ? 0 : (idx >= n ? n - 1 : idx);
+        pts8[4 * j + 0] = (double)m[idx].pt1.x;
+        pts8[4 * j + 1] = (double)m[idx].pt1.y;
+        pts8[4 * j + 2] = (double)m[idx].pt2.x;
+        pts8[4 * j + 3] = (double)m[idx].pt2.y;
+    }
+    double Fh[9];
+    fundamental_8pt(pts8, Fh, s_A + lane, s_V + lane, s_W + lane);
+    double* o = ws_F + ((int64_t)list * iters + h) * 9;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) o[q] = Fh[q];
+}
+
+__global__ __launch_bounds__(64 * kFCountWaves) void f_count_kernel(const yv_match* __restrict__ matches,
+                                                                    int64_t list_stride,
+                                                                    const int32_t* __restrict__ counts, int iters,
+                                                                    double thr, const double* __restrict__ ws_F,
+                                                                    int32_t* __restrict__ ws_cnt) {
+    const int list = blockIdx.y, lane = threadIdx.x & 63;
+    const int h = blockIdx.x * kFCountWaves + (threadIdx.x >> 6);
+    int n = counts[list];
+    if (n > kMaxKp) n = kMaxKp;
+    if (n < 8 || h >= iters) return;
+    const double* Fp = ws_F + ((int64_t)list * iters + h) * 9;
+    double F[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) F[q] = uni_f64(Fp[q]);  // wave-uniform: the hypothesis' F in SGPRs
+    const yv_match* m = matches + (int64_t)list * list_stride;
+    int cnt = 0;
+    for (int k = lane; k < n; k += 64) {
+        const yv_match& mk = m[k];
+        const double e = epipolar_error(F, (double)mk.pt1.x, (double)mk.pt1.y, (double)mk.pt2.x, (double)mk.pt2.y);
+        cnt += __popcll(__ballot(fabs(e) < thr));
+    }
+    if (lane == 0) ws_cnt[(int64_t)list * iters + h] = cnt;
+}
+
+__global__ __launch_bounds__(64) void f_select_kernel(const int32_t* __restrict__ counts, int iters,
+                                                      const double* __restrict__ ws_F,
+                                                      const int32_t* __restrict__ ws_cnt, double* __restrict__ F_out,
+                                                      int32_t* __restrict__ max_inliers, int32_t* __restrict__ found) {
+    const int list = blockIdx.x, lane = threadIdx.x;
     int n = counts[list];
     if (n > kMaxKp) n = kMaxKp;
     if (n < 8) {  // "Not enough matches": return false, F untouched
-        if (tid == 0) found[list] = 0;
+        if (lane == 0) found[list] = 0;
         return;
     }
-    const yv_match* m = matches + (int64_t)list * list_stride;
-    // all lanes read the same match at the same time: one broadcast load per field
-    auto px = [&](int i, int q) -> int {
-        return q == 0 ? m[i].pt1.x : q == 1 ? m[i].pt1.y : q == 2 ? m[i].pt2.x : m[i].pt2.y;
-    };
-    const int32_t* smp = samples + (int64_t)list * sample_stride;
-    int best_cnt = INT32_MIN, best_h = 0x7fffffff;
-    double best_F[9];
-    for (int q = 0; q < 9; ++q) best_F[q] = 0;
-    for (int h = tid; h < iters; h += kNT) {
-        double pts8[32];
-        for (int j = 0; j < 8; ++j) {
-            int idx = smp[8 * h + j];
-            idx = idx < 0 ? 0 : (idx >= n ? n - 1 : idx);
-            for (int q = 0; q < 4; ++q) pts8[4 * j + q] = (double)px(idx, q);
-        }
-        double Fh[9];
-        fundamental_8pt(pts8, Fh);
-        int cnt = 0;
-        for (int k = 0; k < n; ++k) {
-            const double e = epipolar_error(Fh, (double)m[k].pt1.x, (double)m[k].pt1.y, (double)m[k].pt2.x,
-                                            (double)m[k].pt2.y);
-            if (fabs(e) < thr) cnt++;
-        }
-        if (cnt > best_cnt) {  // h increases within a lane: the first best of this lane wins
-            best_cnt = cnt;
-            best_h = h;
-            for (int q = 0; q < 9; ++q) best_F[q] = Fh[q];
+    // (count, -h) lexicographic maximum: hypotheses in order, strict '>' keeps the first best
+    int bc = INT32_MIN, bh = 0x7fffffff;
+    for (int h = lane; h < iters; h += 64) {
+        const int c = ws_cnt[(int64_t)list * iters + h];
+        if (c > bc) {  // h increases within a lane
+            bc = c;
+            bh = h;
         }
     }
-    s_best_cnt[tid] = best_cnt;
-    s_best_h[tid] = best_h;
-    __syncthreads();
-    if (tid == 0) {
-        int bc = INT32_MIN, bh = 0x7fffffff, bt = -1;
-        for (int t = 0; t < kNT; ++t) {
-            const int c = s_best_cnt[t], hh = s_best_h[t];
-            if (c > bc || (c == bc && hh < bh)) { bc = c; bh = hh; bt = t; }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const int oc = __shfl_xor(bc, off, 64), oh = __shfl_xor(bh, off, 64);
+        if (oc > bc || (oc == bc && oh < bh)) {
+            bc = oc;
+            bh = oh;
         }
-        s_best_h[0] = bt;
+    }
+    if (lane == 0) {
         max_inliers[list] = bc;
         found[list] = 1;
     }
-    __syncthreads();
-    if (tid == s_best_h[0] && iters > 0)
-        for (int q = 0; q < 9; ++q) F_out[(int64_t)list * 9 + q] = best_F[q];
+    if (iters > 0 && lane < 9) F_out[(int64_t)list * 9 + lane] = ws_F[((int64_t)list * iters + bh) * 9 + lane];
 }
 
 // Sophus SE3 (pose = {qx, qy, qz, qw, tx, ty, tz}): yavo_se3.h
@@ -1013,11 +1187,6 @@ __device__ __forceinline__ void lm_accumulate_short(double (&part)[28], const do
 // One pass over the active edges at S.T: computeActiveErrors + activeRobustChi2 + buildSystem of g2o's
 // BlockSolver (Huber-weighted J^T J lower triangle, -J^T W e, robust chi2), summed in the oracle's tree
 // order into S.vals[0..28).  Also records S.Tlast (the estimate the active edges' errors refer to).
-__device__ __forceinline__ double uni_f64(double v) {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
 
 template <int NT, typename UV>
 __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, int na, const uint8_t* s_robust,
@@ -1685,11 +1854,26 @@ void launch_lm(int n, hipStream_t s, A... args) {
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
+size_t f_ransac_ws_bytes(int n_lists, int iters) {
+    const size_t h = (size_t)std::max(n_lists, 1) * (size_t)std::max(iters, 1);
+    return ((h * 9 * sizeof(double) + 255) & ~(size_t)255) + h * sizeof(int32_t);
+}
+
 void launch_f_ransac(const yv_match* matches, int64_t list_stride, const int32_t* counts, int n_lists,
                      const int32_t* samples, int64_t sample_stride, int iters, double thr, double* F_out,
-                     int32_t* max_inliers, int32_t* found, hipStream_t s) {
-    hipLaunchKernelGGL(geom::f_ransac_kernel, dim3(n_lists), dim3(geom::kNT), 0, s, matches, list_stride, counts,
-                       samples, sample_stride, iters, thr, F_out, max_inliers, found);
+                     int32_t* max_inliers, int32_t* found, void* ws, hipStream_t s) {
+    if (n_lists <= 0) return;
+    const size_t h = (size_t)n_lists * (size_t)std::max(iters, 1);
+    double* ws_F = static_cast<double*>(ws);
+    int32_t* ws_cnt = reinterpret_cast<int32_t*>(static_cast<char*>(ws) + ((h * 9 * sizeof(double) + 255) & ~(size_t)255));
+    if (iters > 0) {
+        hipLaunchKernelGGL(geom::f_hyp_kernel, dim3((iters + geom::kFHypWG - 1) / geom::kFHypWG, n_lists),
+                           dim3(geom::kFHypWG), 0, s, matches, list_stride, counts, samples, sample_stride, iters, ws_F);
+        hipLaunchKernelGGL(geom::f_count_kernel, dim3((iters + geom::kFCountWaves - 1) / geom::kFCountWaves, n_lists),
+                           dim3(64 * geom::kFCountWaves), 0, s, matches, list_stride, counts, iters, thr, ws_F, ws_cnt);
+    }
+    hipLaunchKernelGGL(geom::f_select_kernel, dim3(n_lists), dim3(64), 0, s, counts, iters, ws_F, ws_cnt, F_out,
+                       max_inliers, found);
 }
 
 void launch_triangulate(const yv_match* m, int n, const double* poses2, const double* K, double* Xw, uint8_t* ok,

@@ -14,8 +14,13 @@
 // in stream order, 64 bytes per pass (byte j of a match = output byte op - D + (j mod D)).  The block's end-of-block
 // token ends the chunk early.  Block headers are parsed wave-uniformly; the dynamic code lengths use the same
 // lane-parallel decoder (repeat code 16 is a distance-1 match).  Completed 16-byte groups of the ring are streamed to
-// HBM after every chunk; matches reaching further back than the 16 KB ring read the already-written output.  The
-// Adler-32 trailer is not checked.
+// HBM after every chunk; matches reaching further back than the 8 KB ring read the already-written output.
+//
+// integrity, as libpng / zlib check it for cv::imread: every IDAT chunk's CRC-32 (over its type and data) is computed
+// by the gather kernel (a wave per chunk, slice-by-8 tables in LDS per lane segment, the lanes' CRCs joined by the
+// GF(2) combination rule), and the Adler-32 of the inflated bytes by the unfilter kernel (per lane sum d and sum i d
+// by v_dot4, one 64-bit reduction), checked against the zlib trailer the inflate kernel reads after the final
+// block.  A failing image gets its own status code and a zero-filled output.
 //
 // unfilter: one wave per image, lane l owning row 64 b + l of band b.  Row r needs row r - 1 (Up / Average / Paeth),
 // so lane l runs one step behind lane l - 1: at step t it undoes the 4-byte group t - l of its row, and the same
@@ -86,6 +91,50 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return v;
+}
+
+// ---- CRC-32 (ISO-HDLC: reflected polynomial 0xEDB88320, init and final XOR ~0; the PNG chunk CRC) ----
+constexpr uint32_t kCrcPoly = 0xEDB88320u;
+struct CrcTables {
+    uint32_t t[8][256];  // slice-by-8: t[k][b] = the CRC contribution of byte b followed by k zero bytes
+};
+constexpr CrcTables make_crc_tables() {
+    CrcTables r{};
+    for (uint32_t b = 0; b < 256; ++b) {
+        uint32_t c = b;
+        for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ kCrcPoly : c >> 1;
+        r.t[0][b] = c;
+    }
+    for (int k = 1; k < 8; ++k)
+        for (uint32_t b = 0; b < 256; ++b) r.t[k][b] = (r.t[k - 1][b] >> 8) ^ r.t[0][r.t[k - 1][b] & 0xFFu];
+    return r;
+}
+__constant__ CrcTables kCrcTab = make_crc_tables();
+
+// a(x) b(x) mod P(x) in the reflected representation (bit 31 = x^0)
+__device__ __forceinline__ uint32_t crc_multmodp(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int k = 31; k >= 0; --k) {
+        p ^= (a >> k) & 1u ? b : 0u;
+        b = (b & 1u) ? (b >> 1) ^ kCrcPoly : b >> 1;
+    }
+    return p;
+}
+// x^(8 n) mod P: square-and-multiply over the bits of n, from x^8
+__device__ uint32_t crc_x8n(uint32_t n) {
+    uint32_t p = 1u << 31;     // x^0
+    uint32_t sq = 1u << 23;    // x^8
+    while (n) {
+        if (n & 1u) p = crc_multmodp(sq, p);
+        sq = crc_multmodp(sq, sq);
+        n >>= 1;
+    }
+    return p;
+}
+// CRC of A followed by B (len_b bytes) from CRC(A) and CRC(B) (the zlib crc32_combine rule)
+__device__ __forceinline__ uint32_t crc_combine(uint32_t ca, uint32_t cb, uint32_t len_b) {
+    return crc_multmodp(crc_x8n(len_b), ca) ^ cb;
 }
 
 // wave-uniform bit reader over a 4-B aligned stream, LSB first (RFC 1951 3.1.1); block headers only
@@ -635,7 +684,8 @@ __device__ int run_chunk(Lds& S, const uint32_t* __restrict__ src, uint32_t nwor
 // image i: zlib stream at src + off[i] (4-B aligned), len[i] bytes -> out_len bytes at out + i * out_pitch
 __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__ src, const int64_t* __restrict__ off,
                                                      const int32_t* __restrict__ len, uint8_t* __restrict__ out,
-                                                     int64_t out_pitch, uint32_t out_len, int32_t* __restrict__ status) {
+                                                     int64_t out_pitch, uint32_t out_len, int32_t* __restrict__ status,
+                                                     int32_t* __restrict__ crc_bad, uint32_t* __restrict__ adler) {
     extern __shared__ __align__(16) uint8_t lds_raw[];
     Lds& S = *reinterpret_cast<Lds*>(lds_raw);
     const int img = blockIdx.x;
@@ -648,6 +698,14 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__
     const uint32_t nbytes = (uint32_t)len[img];
     int32_t st = kPngOk;
     uint32_t op = 0, flushed = 0, seg = kSegMax;
+    // an IDAT chunk whose CRC failed (gather_kernel): libpng stops at it (a critical chunk's CRC error is fatal)
+    if (uni((uint32_t)crc_bad[img]) != 0u) {
+        if (lane == 0) {
+            crc_bad[img] = 0;  // the flag is read (readfirstlane waited for it) before it is cleared for the slot's reuse
+            status[img] = kPngErrCrc;
+        }
+        return;
+    }
     // zlib header (RFC 1950): CM 8, CINFO <= 7, no preset dictionary, FCHECK
     {
         const uint32_t cmf = br.get(8), flg = br.get(8);
@@ -754,6 +812,16 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__
     }
     if (st == kPngOk && br.pos > br.nwords * 32u) st = kPngErrShort;  // decoding ran past the stream
     if (st == kPngOk && op != out_len) st = kPngErrShort;
+    // the zlib trailer: Adler-32 of the inflated bytes, big-endian, at the next byte boundary (RFC 1950 2.2)
+    if (st == kPngOk && adler) {  // (null: the Adler-32 check is off, yv_pngdec_set_checks)
+        br.pos = (br.pos + 7u) & ~7u;
+        if ((br.pos >> 3) + 4u > nbytes) {
+            st = kPngErrAdler;  // no trailer: zlib never reports the stream's end
+        } else {
+            const uint32_t b0 = br.get(8), b1 = br.get(8), b2 = br.get(8), b3 = br.get(8);
+            if (lane == 0) adler[img] = (b0 << 24) | (b1 << 16) | (b2 << 8) | b3;
+        }
+    }
     __builtin_amdgcn_wave_barrier();
     if (st == kPngOk) flush(S, dst, flushed, op);
     if (lane == 0) status[img] = st;
@@ -761,9 +829,40 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__
 
 __device__ __forceinline__ uint32_t byte_of(uint32_t v, int k) { return (v >> (8 * k)) & 0xFFu; }
 
+// Adler-32 sums of the inflated stream, per lane: s1 = sum d_i, s2 = sum i d_i over the bytes the lane read (i = the
+// byte's position in the stream).  A dword x of nb valid bytes at position pos: v_dot4 gives sum d and sum k d_k.
+struct AdlerAcc {
+    uint64_t s1 = 0, s2 = 0;
+    __device__ __forceinline__ void add_dword(uint32_t x, int nb, uint64_t pos) {
+        if (nb < 4) x &= nb <= 0 ? 0u : (0xFFFFFFFFu >> (8 * (4 - nb)));
+        const uint32_t t = __builtin_amdgcn_udot4(x, 0x01010101u, 0u, false);
+        const uint32_t u = __builtin_amdgcn_udot4(x, 0x03020100u, 0u, false);
+        s1 += t;
+        s2 += pos * t + u;
+    }
+    __device__ __forceinline__ void add_byte(uint32_t d, uint64_t pos) {
+        s1 += d;
+        s2 += pos * d;
+    }
+};
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// adler32 of n bytes from the sums: a = 1 + s1, b = n + sum (n - i) d_i = n + n s1 - s2 (mod 65521)
+__device__ __forceinline__ uint32_t adler_of(uint64_t s1, uint64_t s2, uint64_t n) {
+    const uint64_t a = (1u + s1) % 65521u;
+    const uint64_t b = (n + n * s1 - s2) % 65521u;
+    return (uint32_t)((b << 16) | a);
+}
+
 // Any filter types: a wavefront over rows (see the file comment), one 4-byte group per lane per step.
-__device__ void unfilter_wavefront(const uint8_t* __restrict__ rimg, int H, int W, uint8_t* __restrict__ dimg,
-                                   int dst_stride, int32_t* __restrict__ st) {
+// returns true (wave-uniform) when a row has a filter type > 4
+__device__ bool unfilter_wavefront(const uint8_t* __restrict__ rimg, int H, int W, uint8_t* __restrict__ dimg,
+                                   int dst_stride, AdlerAcc& acc) {
     const int lane = threadIdx.x & 63;
     const int G = (W + 3) >> 2;  // 4-byte groups per row
     int bad = 0;
@@ -773,6 +872,7 @@ __device__ void unfilter_wavefront(const uint8_t* __restrict__ rimg, int H, int 
         const uint8_t* rr = rimg + (int64_t)(row_ok ? r : 0) * (W + 1);
         const int f = row_ok ? rr[0] : 0;
         bad |= f > 4 ? 1 : 0;
+        if (row_ok) acc.add_byte((uint32_t)f, (uint64_t)r * (W + 1));
         uint32_t out = 0;       // this lane's group of the last step (DPP source)
         uint32_t left = 0;      // this row's byte before the current group ("a" of its first byte)
         uint32_t upleft = 0;    // the row above's byte before the current group ("c" of its first byte)
@@ -794,6 +894,7 @@ __device__ void unfilter_wavefront(const uint8_t* __restrict__ rimg, int H, int 
                 const int nb = min(4, W - 4 * g);
                 uint32_t x;
                 __builtin_memcpy(&x, rr + 1 + 4 * g, 4);  // the raw buffer is padded: the last group may over-read
+                acc.add_dword(x, nb, (uint64_t)r * (W + 1) + 1 + 4 * g);
                 uint32_t a = left, c = upleft, o = 0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -818,8 +919,7 @@ __device__ void unfilter_wavefront(const uint8_t* __restrict__ rimg, int H, int 
             }
         }
     }
-    const uint64_t any_bad = __ballot(bad != 0);
-    if (lane == 0 && any_bad) *st = kPngErrFilter;
+    return __ballot(bad != 0) != 0;
 }
 
 
@@ -834,7 +934,7 @@ __device__ __forceinline__ uint32_t add8(uint32_t a, uint32_t b) {
 // row above, which the same lane made one row earlier.  Rows stream through registers PF rows ahead of their use.
 template <int NW>
 __device__ void unfilter_rowwise(const uint8_t* __restrict__ rimg, int H, int W, uint8_t* __restrict__ dimg,
-                                 int dst_stride) {
+                                 int dst_stride, AdlerAcc& acc) {
     constexpr int PF = 4;
     const int lane = threadIdx.x & 63;
     const int b0 = 4 * NW * lane;
@@ -861,6 +961,22 @@ __device__ void unfilter_rowwise(const uint8_t* __restrict__ rimg, int H, int W,
             for (int i = 0; i < NW; ++i) x[i] = buf[k][i];
             const uint32_t f = uni(fb[k]);
             load(r + PF, buf[k], fb[k]);
+            {  // the row's raw bytes into the Adler sums: this lane's dwords, the filter byte on lane 0
+                const uint64_t rpos = (uint64_t)r * (W + 1);
+                uint32_t T = 0, Q = 0;
+#pragma unroll
+                for (int i = 0; i < NW; ++i) {
+                    const int vb = nb - 4 * i;
+                    uint32_t xi = x[i];
+                    if (vb < 4) xi &= vb <= 0 ? 0u : (0xFFFFFFFFu >> (8 * (4 - vb)));
+                    const uint32_t t = __builtin_amdgcn_udot4(xi, 0x01010101u, 0u, false);
+                    T += t;
+                    Q += (uint32_t)(4 * i) * t + __builtin_amdgcn_udot4(xi, 0x03020100u, 0u, false);
+                }
+                acc.s1 += T;
+                acc.s2 += (rpos + 1 + b0) * T + Q;
+                if (lane == 0) acc.add_byte(f, rpos);
+            }
             if (f == 1) {
                 uint32_t carry = 0;
 #pragma unroll
@@ -897,15 +1013,18 @@ __device__ void unfilter_rowwise(const uint8_t* __restrict__ rimg, int H, int W,
 // PNG scanline filters (filter method 0) of 8-bit grey rows: raw rows of 1 + W bytes (filter type first) -> rows of W
 // bytes at dst + i * dst_pitch with row stride dst_stride.  NW = ceil(W / 256) (0: W > 4096): images whose rows are all
 // None / Sub / Up take the row-wise path, others the wavefront.
-template <int NW>
-__global__ __launch_bounds__(64) void unfilter_kernel(const uint8_t* __restrict__ raw, int64_t raw_pitch, int H, int W,
-                                                      uint8_t* __restrict__ dst, int64_t dst_pitch, int dst_stride,
-                                                      int32_t* __restrict__ status) {
-    const int img = blockIdx.x;
+// a failed image: zeros (cv::imread's empty Mat has no pixels; the caller sees the status)
+__device__ void zero_image(uint8_t* __restrict__ dimg, int H, int W, int dst_stride) {
     const int lane = threadIdx.x & 63;
-    if (status[img] != kPngOk) return;  // wave-uniform
-    const uint8_t* rimg = raw + (int64_t)img * raw_pitch;
-    uint8_t* dimg = dst + (int64_t)img * dst_pitch;
+    for (int r = 0; r < H; ++r)
+        for (int c = lane; c < W; c += 64) dimg[(int64_t)r * dst_stride + c] = 0;
+}
+
+// the image's status after its filters (wave-uniform): kPngOk or kPngErrFilter
+template <int NW>
+__device__ int32_t unfilter_body(const uint8_t* __restrict__ rimg, int H, int W, uint8_t* __restrict__ dimg,
+                                 int dst_stride, AdlerAcc& acc) {
+    const int lane = threadIdx.x & 63;
     if (NW > 0) {
         bool rowwise = true, bad = false;
         for (int r = lane; r < H; r += 64) {
@@ -913,21 +1032,48 @@ __global__ __launch_bounds__(64) void unfilter_kernel(const uint8_t* __restrict_
             rowwise = rowwise && f <= 2;
             bad = bad || f > 4;
         }
-        if (__ballot(bad)) {
-            if (lane == 0) status[img] = kPngErrFilter;
-            return;
-        }
+        if (__ballot(bad)) return kPngErrFilter;
         if (!__ballot(!rowwise)) {
-            unfilter_rowwise<(NW > 0 ? NW : 1)>(rimg, H, W, dimg, dst_stride);
-            return;
+            unfilter_rowwise<(NW > 0 ? NW : 1)>(rimg, H, W, dimg, dst_stride, acc);
+            return kPngOk;
         }
     }
-    unfilter_wavefront(rimg, H, W, dimg, dst_stride, status + img);
+    return unfilter_wavefront(rimg, H, W, dimg, dst_stride, acc) ? kPngErrFilter : kPngOk;
 }
-// IDAT payloads of the staged files -> contiguous zlib streams: one wave per payload, 16 bytes per lane per pass
-__global__ __launch_bounds__(64) void gather_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                   const PngPiece* __restrict__ pieces) {
+
+template <int NW>
+__global__ __launch_bounds__(64) void unfilter_kernel(const uint8_t* __restrict__ raw, int64_t raw_pitch, int H, int W,
+                                                      uint8_t* __restrict__ dst, int64_t dst_pitch, int dst_stride,
+                                                      int32_t* __restrict__ status, const uint32_t* __restrict__ adler,
+                                                      uint32_t* __restrict__ bad_total) {
+    const int img = blockIdx.x;
     const int lane = threadIdx.x & 63;
+    const uint8_t* rimg = raw + (int64_t)img * raw_pitch;
+    uint8_t* dimg = dst + (int64_t)img * dst_pitch;
+    int32_t st = (int32_t)uni((uint32_t)status[img]);
+    if (st == kPngOk) {
+        AdlerAcc acc;
+        st = unfilter_body<NW>(rimg, H, W, dimg, dst_stride, acc);
+        if (st == kPngOk && adler) {
+            const uint64_t s1 = wave_sum_u64(acc.s1), s2 = wave_sum_u64(acc.s2);
+            if (adler_of(s1, s2, (uint64_t)H * (W + 1)) != uni(adler[img])) st = kPngErrAdler;
+        }
+        if (st != kPngOk && lane == 0) status[img] = st;
+    }
+    if (st != kPngOk) {
+        zero_image(dimg, H, W, dst_stride);
+        if (lane == 0) atomicAdd(bad_total, 1u);
+    }
+}
+// IDAT payloads of the staged files -> contiguous zlib streams: one wave per payload, 16 bytes per lane per pass; then
+// the chunk's CRC-32 over its type and data (each lane one contiguous segment, slice-by-8 from LDS tables, the 64
+// segment CRCs joined pairwise up a tree), against the stored big-endian CRC after the data
+__global__ __launch_bounds__(64) void gather_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                   const PngPiece* __restrict__ pieces, int32_t* __restrict__ crc_bad) {
+    __shared__ uint32_t s_tab[8][256];
+    const int lane = threadIdx.x & 63;
+    if (crc_bad)
+        for (int i = lane; i < 8 * 256; i += 64) s_tab[i >> 8][i & 255] = kCrcTab.t[i >> 8][i & 255];
     const PngPiece pc = pieces[blockIdx.x];
     const uint8_t* s = src + pc.src;
     uint8_t* d = dst + pc.dst;
@@ -940,26 +1086,61 @@ __global__ __launch_bounds__(64) void gather_kernel(const uint8_t* __restrict__ 
             for (int64_t k = i; k < pc.len; ++k) d[k] = s[k];
         }
     }
+    if (!crc_bad) return;  // checks off (yv_pngdec_set_checks)
+    __syncthreads();  // the tables
+    const uint8_t* c0 = s - 4;  // chunk type, then the data
+    const uint32_t total = (uint32_t)pc.len + 4u;
+    const uint32_t seg = (((total + 63u) / 64u) + 7u) & ~7u;
+    const uint32_t lo = min((uint32_t)lane * seg, total), hi = min(lo + seg, total);
+    uint32_t c = 0xFFFFFFFFu;
+    uint32_t p = lo;
+    for (; p + 8u <= hi; p += 8u) {
+        uint32_t w0, w1;
+        __builtin_memcpy(&w0, c0 + p, 4);
+        __builtin_memcpy(&w1, c0 + p + 4, 4);
+        w0 ^= c;
+        c = s_tab[7][w0 & 255u] ^ s_tab[6][(w0 >> 8) & 255u] ^ s_tab[5][(w0 >> 16) & 255u] ^ s_tab[4][w0 >> 24] ^
+            s_tab[3][w1 & 255u] ^ s_tab[2][(w1 >> 8) & 255u] ^ s_tab[1][(w1 >> 16) & 255u] ^ s_tab[0][w1 >> 24];
+    }
+    for (; p < hi; ++p) c = s_tab[0][(c ^ c0[p]) & 255u] ^ (c >> 8);
+    c ^= 0xFFFFFFFFu;
+    uint32_t n = hi - lo;
+    // lanes l and l + off (off = 1, 2, 4, ...): lane l's span is followed by lane l + off's
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t cb = (uint32_t)__shfl_down((int)c, off, 64), nb = (uint32_t)__shfl_down((int)n, off, 64);
+        if ((lane & (2 * off - 1)) == 0) {
+            c = crc_combine(c, cb, nb);
+            n += nb;
+        }
+    }
+    if (lane == 0) {
+        const uint8_t* t = s + pc.len;
+        const uint32_t stored = ((uint32_t)t[0] << 24) | ((uint32_t)t[1] << 16) | ((uint32_t)t[2] << 8) | t[3];
+        if (stored != c) crc_bad[pc.img] = 1;
+    }
 }
 
 }  // namespace png
 
-void launch_png_gather(const uint8_t* src, uint8_t* dst, const PngPiece* pieces, int n, hipStream_t s) {
-    if (n > 0) hipLaunchKernelGGL(png::gather_kernel, dim3(n), dim3(64), 0, s, src, dst, pieces);
+void launch_png_gather(const uint8_t* src, uint8_t* dst, const PngPiece* pieces, int n, int32_t* crc_bad,
+                       hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(png::gather_kernel, dim3(n), dim3(64), 0, s, src, dst, pieces, crc_bad);
 }
 
 void launch_png_inflate(const uint8_t* src, const int64_t* off, const int32_t* len, int n, uint8_t* out,
-                        int64_t out_pitch, uint32_t out_len, int32_t* status, hipStream_t s) {
+                        int64_t out_pitch, uint32_t out_len, int32_t* status, int32_t* crc_bad, uint32_t* adler,
+                        hipStream_t s) {
     hipLaunchKernelGGL(png::inflate_kernel, dim3(n), dim3(64), sizeof(png::Lds), s, src, off, len, out, out_pitch,
-                       out_len, status);
+                       out_len, status, crc_bad, adler);
 }
 
 void launch_png_unfilter(const uint8_t* raw, int64_t raw_pitch, int n, int H, int W, uint8_t* dst, int64_t dst_pitch,
-                         int dst_stride, int32_t* status, hipStream_t s) {
+                         int dst_stride, int32_t* status, const uint32_t* adler, uint32_t* bad_total, hipStream_t s) {
     const int nw = (W + 255) / 256;
 #define YV_UNFILTER(NW)                                                                                              \
     hipLaunchKernelGGL(png::unfilter_kernel<NW>, dim3(n), dim3(64), 0, s, raw, raw_pitch, H, W, dst, dst_pitch,     \
-                       dst_stride, status)
+                       dst_stride, status, adler, bad_total)
     switch (nw) {
     case 1: YV_UNFILTER(1); break;
     case 2: YV_UNFILTER(2); break;

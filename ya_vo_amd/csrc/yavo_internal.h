@@ -92,9 +92,11 @@ void launch_filter_records(const yv_match* in, int n, int thr, yv_match* out, in
                            hipStream_t s);
 
 // ---- geometry (yavo_geom.hip) ----
+// device workspace of launch_f_ransac: [n_lists][iters] hypotheses' F and inlier counts
+size_t f_ransac_ws_bytes(int n_lists, int iters);
 void launch_f_ransac(const yv_match* matches, int64_t list_stride, const int32_t* counts, int n_lists,
                      const int32_t* samples, int64_t sample_stride, int iters, double thr, double* F_out,
-                     int32_t* max_inliers, int32_t* found, hipStream_t s);
+                     int32_t* max_inliers, int32_t* found, void* ws, hipStream_t s);
 void launch_triangulate(const yv_match* m, int n, const double* poses2, const double* K, double* Xw, uint8_t* ok,
                         int32_t* n_ok, hipStream_t s);
 void launch_world2camera(const double* X, int n, const double* T, const double* K, double* out, hipStream_t s);
@@ -138,15 +140,22 @@ void launch_lk_edges(int n_tracks, const double* pX, const float* next, const ui
                      int32_t* edge_count, hipStream_t s);
 
 // cv::findEssentialMat (RANSAC) + cv::recoverPose (yavo_essential.hip).  Workspace of a yv_essential.
-constexpr int kEssChunk = 64;  // RANSAC iterations evaluated per round (one lane each)
+// RANSAC iterations evaluated per round (one lane each): 64, or 256 for workspaces of at most kEssWidePairs lists, where
+// the chip is otherwise idle and a wider speculative round saves the dependent rounds' latency (the sequential
+// selection ignores the iterations past niters, so the result is the same)
+constexpr int kEssChunk = 64;
+constexpr int kEssChunkWide = 256;
+constexpr int kEssWidePairs = 8;
+inline int ess_chunk_for(int max_pairs) { return max_pairs <= kEssWidePairs ? kEssChunkWide : kEssChunk; }
 struct EssParams {
     int max_pairs = 0, max_points = 0, max_iters = 0;
+    int chunk = kEssChunk;     // iterations per round (ess_chunk_for)
     double* m1 = nullptr;      // [max_pairs][max_points][2] normalised points1
     double* m2 = nullptr;      // [max_pairs][max_points][2] normalised points2
     int32_t* idx = nullptr;    // [max_pairs][max_iters][5] getSubset draws
-    double* models = nullptr;  // [max_pairs][kEssChunk][10][9]
-    int32_t* nmod = nullptr;   // [max_pairs][kEssChunk]
-    int32_t* good = nullptr;   // [max_pairs][kEssChunk][10]
+    double* models = nullptr;  // [max_pairs][chunk][10][9]
+    int32_t* nmod = nullptr;   // [max_pairs][chunk]
+    int32_t* good = nullptr;   // [max_pairs][chunk][10]
     int32_t* state = nullptr;  // [max_pairs][8]: niters, max_good, iterations run, models, found, n, -, -
     double* best = nullptr;    // [max_pairs][9]
     double* cand = nullptr;    // [max_pairs][4][12] recoverPose candidates P1..P4
@@ -236,18 +245,24 @@ void launch_map_chunk(const double* rel, int n, int64_t first_frame, int kf_ever
 // PNG decoding on the GPU (yavo_inflate.hip): per-image status codes and the two kernels
 enum : int32_t {
     kPngOk = 0, kPngErrHeader = 1, kPngErrBlock = 2, kPngErrCode = 3, kPngErrOverrun = 4, kPngErrShort = 5,
-    kPngErrFilter = 6
+    kPngErrFilter = 6, kPngErrCrc = 7, kPngErrAdler = 8
 };
-// one IDAT payload of a PNG file staged on the device: len bytes from src to dst (byte offsets in the staging buffers)
+// one IDAT payload of a PNG file staged on the device: len bytes from src to dst (byte offsets in the staging buffers);
+// the chunk's type is the 4 bytes before src, its CRC the 4 after src + len; img = the payload's image in the call
 struct PngPiece {
     int64_t src, dst;
-    int32_t len, pad;
+    int32_t len, img;
 };
-void launch_png_gather(const uint8_t* src, uint8_t* dst, const PngPiece* pieces, int n, hipStream_t s);
+// gather + chunk CRCs: crc_bad[img] = 1 when a payload's CRC-32 (type + data) differs from the stored one
+void launch_png_gather(const uint8_t* src, uint8_t* dst, const PngPiece* pieces, int n, int32_t* crc_bad, hipStream_t s);
+// inflate: reads and clears crc_bad; adler[i] = the zlib trailer of image i
 void launch_png_inflate(const uint8_t* src, const int64_t* off, const int32_t* len, int n, uint8_t* out,
-                        int64_t out_pitch, uint32_t out_len, int32_t* status, hipStream_t s);
+                        int64_t out_pitch, uint32_t out_len, int32_t* status, int32_t* crc_bad, uint32_t* adler,
+                        hipStream_t s);
+// unfilter + the Adler-32 of the inflated bytes against adler[i]; failed images are zero-filled and counted in
+// *bad_total
 void launch_png_unfilter(const uint8_t* raw, int64_t raw_pitch, int n, int H, int W, uint8_t* dst, int64_t dst_pitch,
-                         int dst_stride, int32_t* status, hipStream_t s);
+                         int dst_stride, int32_t* status, const uint32_t* adler, uint32_t* bad_total, hipStream_t s);
 
 void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, const double* edge_X,
                        const double* edge_uv, const double* K, const double* priors, double* poses,

@@ -473,6 +473,9 @@ struct yv_pngdec {
     int64_t raw_pitch = 0;        // inflated image: H rows of 1 + W bytes (+ 64 B of over-read slack), 256-B aligned
     uint8_t* d_raw = nullptr;     // [max_images][raw_pitch]
     int32_t* d_status = nullptr;  // [max_images]
+    uint32_t* d_adler = nullptr;  // [max_images] the zlib trailers of the last decode
+    uint32_t* d_bad = nullptr;    // images failed since the last yv_pngdec_status
+    int check_crc = 1, check_adler = 1;  // yv_pngdec_set_checks
     int n_last = 0;
     hipStream_t last_stream = nullptr;
     // slots of staging: pinned host {streams | offsets | lengths} and the device copy of the streams; four, so that a
@@ -491,6 +494,7 @@ struct yv_pngdec {
         hipEvent_t gathered = nullptr;
         int64_t* d_off = nullptr;
         int32_t* d_len = nullptr;
+        int32_t* d_crc = nullptr;     // [max_images] a payload CRC failed (gather -> inflate, cleared by the inflate)
         hipEvent_t copied = nullptr;  // the pinned streams are on the device: the host may refill the slot
         hipEvent_t done = nullptr;    // the slot's inflate completed: the device copy may be overwritten
         bool pending = false;
@@ -504,7 +508,8 @@ namespace {
 
 // IDAT payloads of one 8-bit grey non-interlaced H x W PNG staged at `base` of the slot: appended to pcs as pieces
 // (src = base + payload offset, dst = base + position in the zlib stream); returns the stream's length or -1
-int64_t png_idat_pieces(const uint8_t* buf, size_t len, int H, int W, int64_t base, std::vector<yavo::PngPiece>& pcs) {
+int64_t png_idat_pieces(const uint8_t* buf, size_t len, int H, int W, int64_t base, int img,
+                        std::vector<yavo::PngPiece>& pcs) {
     PngHeader h;
     if (png_parse(buf, len, h, nullptr, nullptr) != YV_OK) return -1;
     if (h.ctype != 0 || h.depth != 8 || h.interlace != 0 || h.H != H || h.W != W) return -1;
@@ -515,7 +520,7 @@ int64_t png_idat_pieces(const uint8_t* buf, size_t len, int H, int W, int64_t ba
         if (n > len - off - 12) return -1;
         const uint8_t* type = buf + off + 4;
         if (!std::memcmp(type, "IDAT", 4)) {
-            if (n) pcs.push_back({base + (int64_t)off + 8, base + out, (int32_t)n, 0});
+            if (n) pcs.push_back({base + (int64_t)off + 8, base + out, (int32_t)n, (int32_t)img});
             out += n;
         } else if (!std::memcmp(type, "IEND", 4)) {
             break;
@@ -598,14 +603,15 @@ int pngdec_launch(yv_pngdec* d, yv_pngdec::Slot& sl, size_t bytes, int n, int np
             hipSuccess ||
         hipEventRecord(sl.copied, cs) != hipSuccess)
         return YV_ERR_HIP;
-    yavo::launch_png_gather(sl.d, sl.dg, sl.d_pc, npc, cs);
+    yavo::launch_png_gather(sl.d, sl.dg, sl.d_pc, npc, d->check_crc ? sl.d_crc : nullptr, cs);
     if (hipGetLastError() != hipSuccess || hipEventRecord(sl.gathered, cs) != hipSuccess ||
         hipStreamWaitEvent(st, sl.gathered, 0) != hipSuccess ||
         (d->n_last && hipStreamWaitEvent(st, d->last_done, 0) != hipSuccess))
         return YV_ERR_HIP;
     yavo::launch_png_inflate(sl.dg, sl.d_off, sl.d_len, n, d->d_raw, d->raw_pitch, (uint32_t)d->H * (d->W + 1),
-                             d->d_status, st);
-    yavo::launch_png_unfilter(d->d_raw, d->raw_pitch, n, d->H, d->W, d_dst, pitch, d->W, d->d_status, st);
+                             d->d_status, sl.d_crc, d->check_adler ? d->d_adler : nullptr, st);
+    yavo::launch_png_unfilter(d->d_raw, d->raw_pitch, n, d->H, d->W, d_dst, pitch, d->W, d->d_status,
+                              d->check_adler ? d->d_adler : nullptr, d->d_bad, st);
     if (hipGetLastError() != hipSuccess || hipEventRecord(sl.done, st) != hipSuccess ||
         hipEventRecord(d->last_done, st) != hipSuccess)
         return YV_ERR_HIP;
@@ -638,12 +644,17 @@ int yv_pngdec_create(yv_ctx* ctx, int max_images, int H, int W, yv_pngdec** out)
     d->W = W;
     d->raw_pitch = (((int64_t)H * (W + 1) + 64) + 255) & ~(int64_t)255;
     bool ok = hipMalloc(reinterpret_cast<void**>(&d->d_raw), (size_t)d->raw_pitch * max_images) == hipSuccess &&
-              hipMalloc(reinterpret_cast<void**>(&d->d_status), sizeof(int32_t) * (size_t)max_images) == hipSuccess;
+              hipMalloc(reinterpret_cast<void**>(&d->d_status), sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&d->d_adler), sizeof(uint32_t) * (size_t)max_images) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&d->d_bad), sizeof(uint32_t)) == hipSuccess &&
+              hipMemset(d->d_bad, 0, sizeof(uint32_t)) == hipSuccess;
     for (auto& sl : d->slot) {
         ok = ok && hipHostMalloc(reinterpret_cast<void**>(&sl.h_off), sizeof(int64_t) * (size_t)max_images) == hipSuccess &&
              hipHostMalloc(reinterpret_cast<void**>(&sl.h_len), sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
              hipMalloc(reinterpret_cast<void**>(&sl.d_off), sizeof(int64_t) * (size_t)max_images) == hipSuccess &&
              hipMalloc(reinterpret_cast<void**>(&sl.d_len), sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
+             hipMalloc(reinterpret_cast<void**>(&sl.d_crc), sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
+             hipMemset(sl.d_crc, 0, sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
              hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&sl.gathered, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
@@ -678,11 +689,14 @@ void yv_pngdec_destroy(yv_pngdec* d) {
         if (sl.d) (void)hipFree(sl.d);
         if (sl.d_off) (void)hipFree(sl.d_off);
         if (sl.d_len) (void)hipFree(sl.d_len);
+        if (sl.d_crc) (void)hipFree(sl.d_crc);
     }
     if (d->last_done) (void)hipEventDestroy(d->last_done);
     if (d->copy) (void)hipStreamDestroy(d->copy);
     if (d->d_raw) (void)hipFree(d->d_raw);
     if (d->d_status) (void)hipFree(d->d_status);
+    if (d->d_adler) (void)hipFree(d->d_adler);
+    if (d->d_bad) (void)hipFree(d->d_bad);
     delete d;
 }
 
@@ -703,7 +717,7 @@ int yv_pngdec_decode(yv_pngdec* d, const uint8_t* const* files, const size_t* si
     std::vector<std::vector<yavo::PngPiece>> pcs((size_t)n);
     for (int i = 0; i < n; ++i) {
         std::memcpy(sl->h + off, files[i], sizes[i]);
-        const int64_t len = png_idat_pieces(sl->h + off, sizes[i], d->H, d->W, (int64_t)off, pcs[(size_t)i]);
+        const int64_t len = png_idat_pieces(sl->h + off, sizes[i], d->H, d->W, (int64_t)off, i, pcs[(size_t)i]);
         if (len < 0 || len > INT32_MAX) return YV_ERR_INVALID;
         sl->h_off[i] = (int64_t)off;
         sl->h_len[i] = (int32_t)len;
@@ -715,16 +729,26 @@ int yv_pngdec_decode(yv_pngdec* d, const uint8_t* const* files, const size_t* si
     return pngdec_launch(d, *sl, off, n, npc, d_dst, pitch, st);
 }
 
+int yv_pngdec_set_checks(yv_pngdec* d, int crc, int adler) {
+    if (!d) return YV_ERR_INVALID;
+    d->check_crc = crc ? 1 : 0;
+    d->check_adler = adler ? 1 : 0;
+    return YV_OK;
+}
+
 int yv_pngdec_status(yv_pngdec* d, int32_t* codes, int* n_bad) {
     if (!d || !n_bad) return YV_ERR_INVALID;
     *n_bad = 0;
     if (d->n_last == 0) return YV_OK;
     if (hipSetDevice(yavo::ctx_device(d->ctx)) != hipSuccess) return YV_ERR_HIP;
     std::vector<int32_t> h((size_t)d->n_last);
+    uint32_t bad = 0;
     if (hipStreamSynchronize(d->last_stream) != hipSuccess ||
-        hipMemcpy(h.data(), d->d_status, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(h.data(), d->d_status, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&bad, d->d_bad, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemset(d->d_bad, 0, sizeof(uint32_t)) != hipSuccess)
         return YV_ERR_HIP;
-    for (int32_t c : h) *n_bad += c != 0;
+    *n_bad = (int)bad;  // every decode since the last status query, not only the last one
     if (codes) std::memcpy(codes, h.data(), sizeof(int32_t) * h.size());
     return YV_OK;
 }
@@ -797,7 +821,8 @@ int yv_seq_upload_gpu_frames(yv_seq* s, yv_pngdec* d, const int* frames, int n, 
             ::close(fd);
         }
         const int64_t len =
-            got == size[k] ? png_idat_pieces(sl->h + off[k], size[k], d->H, d->W, (int64_t)off[k], pcs[(size_t)k]) : -1;
+            got == size[k] ? png_idat_pieces(sl->h + off[k], size[k], d->H, d->W, (int64_t)off[k], k, pcs[(size_t)k])
+                           : -1;
         if (len < 0 || len > INT32_MAX) {
             status = YV_ERR_INVALID;
             return;

@@ -154,8 +154,14 @@ class PngDecoder:
                "yv_seq_upload_gpu_frames")
         self._n = len(fr) * (2 if seq.stereo else 1)
 
+    def set_checks(self, crc: int = 1, adler: int = 1) -> None:
+        """integrity checks of the following decodes: IDAT chunk CRC-32, zlib Adler-32 (both on by default)"""
+        _check(self.lib.yv_pngdec_set_checks(self.handle, int(crc), int(adler)), "yv_pngdec_set_checks")
+
     def status(self):
-        """(codes of the last call's images, number failed); waits for the last call"""
+        """(codes of the last call's images, images failed in every call since the previous status); waits for the
+        last call.  Codes: 7 = an IDAT chunk's CRC-32, 8 = the zlib Adler-32 trailer (yavo_io.h); failed images are
+        zero-filled on the device."""
         bad = ctypes.c_int()
         codes = np.zeros(max(getattr(self, "_n", 0), 1), np.int32)
         _check(self.lib.yv_pngdec_status(self.handle, codes.ctypes.data, ctypes.byref(bad)), "yv_pngdec_status")
