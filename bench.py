@@ -221,10 +221,10 @@ def loop_handler_leg(frames):
     pipelined (tools/bench_loop_handler.py)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_loop_handler
-    r = bench_loop_handler.measure(frames)
+    r = bench_loop_handler.measure(frames, readers=min(16, cpu_threads_available()))
     return {"serial_frames_per_s": r["serial"]["frames_per_s"], "pipelined_frames_per_s": r["pipelined"]["frames_per_s"],
             "trajectories_identical": r["trajectories_identical"], "serial": r["serial"], "pipelined": r["pipelined"],
-            "what": r["what"]}
+            "pipelined_modes": r["pipelined_modes"], "what": r["what"]}
 
 
 def cpu_threads_available() -> int:

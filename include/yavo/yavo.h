@@ -56,6 +56,12 @@ int yv_sync(yv_ctx* ctx);
  * context stream. */
 int yv_download(yv_ctx* ctx, void* host_dst, const void* dev_src, size_t bytes);
 int yv_upload(yv_ctx* ctx, void* dev_dst, const void* host_src, size_t bytes);
+/* Device memory on the context's GPU and pinned host memory, for callers without a HIP toolchain of their own (the C++
+ * LoopHandler's GPU-decode look-ahead): the batch / decoder entry points take device pointers. */
+int yv_device_alloc(yv_ctx* ctx, size_t bytes, void** out);
+void yv_device_free(yv_ctx* ctx, void* p);
+int yv_host_alloc(yv_ctx* ctx, size_t bytes, void** out);
+void yv_host_free(yv_ctx* ctx, void* p);
 
 /* FastDetector constructor constants (include/FastDetector.hpp:32-38): intensityThreshold (40) and
  * fastCornerNumThreshold (2000). */

@@ -56,7 +56,7 @@ int yv_pose_lm_batch(struct yv_ctx* ctx, int n_problems, const int32_t* d_offset
                      const double* d_uv, const double* d_K, double* d_poses, uint8_t* d_outlier,
                      int32_t* d_inliers, void* stream);
 /* The order in which the pose-LM kernel sums over edges, as the oracle's sum_mode (oracle/yavo_oracle.h:
- * 4 / 5 / 6 = 64- / 128- / 256-thread workgroups; YAVO_LM_THREADS selects, default 256). Results are bit-identical
+ * 4 / 5 / 6 = 64- / 128- / 256-thread workgroups; the library runs 256). Results are bit-identical
  * to the oracle in that order and within 1e-9 of the reference's sequential order. */
 int yv_lm_sum_mode(void);
 int yv_pose_gn_batch(struct yv_ctx* ctx, int n_problems, const int32_t* d_offsets, const double* d_X,

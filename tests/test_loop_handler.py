@@ -163,3 +163,30 @@ def test_loop_handler_pipelined_matches_oracle_loop(tmp_path, oracle):
     np.testing.assert_array_equal(gpu_events, ref_events)
     np.testing.assert_array_equal(gpu_poses, P)
     assert stats["init"] == 1 and stats["reinit"] >= 1 and stats["tracked"] >= 40
+
+
+@pytest.mark.gpu
+def test_loop_handler_gpu_decode_matches_oracle_loop(tmp_path, oracle):
+    """The pipelined C++ LoopHandler with the look-ahead decoded on the GPU (--gpu-decode 16: PNG inflate + unfilter,
+    detect and describe of 16 frames per batch on the device, the next batch enqueued while this one is handed over)
+    over 45 frames (three batches, the last one partial) with a reinitialisation: the trajectory and per-frame events
+    equal the oracle loop's bit for bit."""
+    from loop_chain import EVENT_FIELDS, LoopChain
+    from ya_vo_amd import scene
+    n = 45
+    frames = [synth_frame(777, *offset(k, 30), 376, 1241) for k in range(n)]
+    cfg, _ = make_sequence(tmp_path, frames)
+    pb, eb = tmp_path / "poses.bin", tmp_path / "events.bin"
+    r = subprocess.run([BIN, cfg, "--poses-bin", str(pb), "--events", str(eb), "--pipeline", "2", "--gpu-decode", "16",
+                        "--readers", "4"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    stats = json.loads(r.stdout.strip().splitlines()[-1])
+    assert stats["frames"] == n and stats["gpu_decode_batch"] == 16
+    gpu_poses = np.fromfile(pb, np.float64).reshape(-1, 7)
+    gpu_events = np.fromfile(eb, np.int32).reshape(-1, len(EVENT_FIELDS))
+    offsets = np.fromfile(OFFSETS, np.int8).reshape(256, 4)
+    P, ev = LoopChain(oracle, scene.K_KITTI, offsets).run(frames)
+    ref_events = np.array([[e[f] for f in EVENT_FIELDS] for e in ev], np.int32)
+    np.testing.assert_array_equal(gpu_events, ref_events)
+    np.testing.assert_array_equal(gpu_poses, P)
+    assert stats["reinit"] >= 1 and stats["tracked"] >= 20

@@ -70,6 +70,10 @@ SIGNATURES = {
     "yv_sync": (_I, [_P]),
     "yv_download": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "yv_upload": (_I, [_P, _P, _P, ctypes.c_size_t]),
+    "yv_device_alloc": (_I, [_P, ctypes.c_size_t, ctypes.POINTER(_P)]),
+    "yv_device_free": (None, [_P, _P]),
+    "yv_host_alloc": (_I, [_P, ctypes.c_size_t, ctypes.POINTER(_P)]),
+    "yv_host_free": (None, [_P, _P]),
     "yv_set_fast_params": (_I, [_P, _I, _I]),
     "yv_set_harris_eigen": (_I, [_P, _I]),
     "yv_set_brief_offsets": (_I, [_P, _P]),

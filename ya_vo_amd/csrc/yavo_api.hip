@@ -452,6 +452,36 @@ int yv_upload(yv_ctx* ctx, void* dev_dst, const void* host_src, size_t bytes) {
     return YV_OK;
 }
 
+int yv_device_alloc(yv_ctx* ctx, size_t bytes, void** out) {
+    if (!ctx || !out) return YV_ERR_INVALID;
+    *out = nullptr;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipMalloc(out, bytes ? bytes : 1));
+    return YV_OK;
+}
+
+void yv_device_free(yv_ctx* ctx, void* p) {
+    if (!ctx || !p) return;
+    (void)set_device(ctx);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(p);
+}
+
+int yv_host_alloc(yv_ctx* ctx, size_t bytes, void** out) {
+    if (!ctx || !out) return YV_ERR_INVALID;
+    *out = nullptr;
+    if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
+    YV_HIP(hipHostMalloc(out, bytes ? bytes : 1));
+    return YV_OK;
+}
+
+void yv_host_free(yv_ctx* ctx, void* p) {
+    if (!ctx || !p) return;
+    (void)set_device(ctx);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipHostFree(p);
+}
+
 int yv_set_fast_params(yv_ctx* ctx, int intensity_threshold, int max_corners) {
     if (!ctx || intensity_threshold < 0 || intensity_threshold > 255 || max_corners < 0 ||
         max_corners > yavo::kMaxKp)
@@ -1035,12 +1065,8 @@ int yv_batch_set_track_overlap(yv_batch* b, int on) {
             YV_HIP(hipEventCreateWithFlags(&b->ev_edges[k], hipEventDisableTiming));
             YV_HIP(hipEventCreateWithFlags(&b->ev_lm[k], hipEventDisableTiming));
         }
-        {
-            // YAVO_BUILD_PRIO=1 / 2: the build stream at the highest / lowest priority (measured)
-            const char* e = std::getenv("YAVO_BUILD_PRIO");
-            YV_HIP(hipStreamCreateWithPriority(&b->bstream, hipStreamNonBlocking,
-                                               (e && e[0] == '1') ? greatest : (e && e[0] == '2') ? least : 0));
-        }
+        // the build stream at the default priority (the highest and the lowest measured the same)
+        YV_HIP(hipStreamCreateWithFlags(&b->bstream, hipStreamNonBlocking));
         YV_HIP(hipEventCreateWithFlags(&b->ev_fin, hipEventDisableTiming));
         YV_HIP(hipEventCreateWithFlags(&b->ev_built, hipEventDisableTiming));
     }

@@ -386,10 +386,7 @@ __global__ __launch_bounds__(kSchurChunk) void ba_schur_kernel(BaParams P, doubl
 // The triangular solves then run on wave 0 alone, the vector in registers, broadcasts by v_readlane.
 constexpr int kLdltMaxN = 120;
 
-#ifndef YAVO_LDLT_THREADS
-#define YAVO_LDLT_THREADS 1024  // 256 / 512 / 1024 threads: 184 / 138 / 123 us per factorisation at n = 114
-#endif
-constexpr int kLdltThreads = YAVO_LDLT_THREADS;
+constexpr int kLdltThreads = 1024;  // 256 / 512 / 1024 threads: 184 / 138 / 123 us per factorisation at n = 114
 
 __device__ __forceinline__ int tri(int i, int j) { return (i * (i + 1) >> 1) + j; }
 
@@ -1261,16 +1258,9 @@ extern "C" int yv_ba_set_problem(yv_ba* b, int n_poses, int n_fixed, int n_landm
 // and scale (bit-identical double arithmetic), the device everything per edge / landmark / pose
 namespace {
 
-// Trial slots the device-driven solve enqueues per iteration (YAVO_BA_TRIALS, default 1): g2o's trial loop usually
-// accepts its first trial; an iteration that needs more suspends the solve and the host enqueues the rest.
-int ba_trial_slots() {
-    static const int n = [] {
-        const char* e = getenv("YAVO_BA_TRIALS");
-        const int v = e ? atoi(e) : 1;
-        return v >= 1 && v <= 10 ? v : 1;
-    }();
-    return n;
-}
+// Trial slots the device-driven solve enqueues per iteration: g2o's trial loop usually accepts its first trial; an
+// iteration that needs more suspends the solve and the host enqueues the rest.
+int ba_trial_slots() { return 1; }
 
 // The LM of yv_ba_solve with its control on the device (default): the host enqueues every iteration's kernels
 // without waiting -- linearise, (iteration begin), per trial slot {backup, trial, decide, restore}, (iteration end)

@@ -29,9 +29,19 @@ __device__ __forceinline__ uint32_t cv_rng_next(uint64_t* state) {
     return (uint32_t)*state;
 }
 
-// At: N1 rows of M (the first N are the input vectors), Vt: N x N; n1 = N1 rows normalised / completed.
-template <int M, int N, int N1>
-__device__ void cv_jacobi_svd_mn(double* At, double* Wout, double* Vt) {
+// Lane-private arrays in LDS laid out [element][lane] (element e of lane l at p[e * L]): a wave's access to one element
+// is one conflict-free ds_*_b64, and dynamic indices cost no scratch.  Indexing and pointer arithmetic as on a double*.
+template <int L>
+struct LdsArr {
+    double* p;
+    __device__ __forceinline__ double& operator[](int i) const { return p[i * L]; }
+    __device__ __forceinline__ LdsArr operator+(int o) const { return LdsArr{p + o * L}; }
+};
+
+// At: N1 rows of M (the first N are the input vectors), Vt: N x N; n1 = N1 rows normalised / completed.  PA / PV:
+// double* (private arrays) or LdsArr<L>.
+template <int M, int N, int N1, class PA = double*, class PV = double*>
+__device__ void cv_jacobi_svd_mn(PA At, double* Wout, PV Vt) {
     const double minval = DBL_MIN, eps = DBL_EPSILON * 10;
     double W[N];
     const int m = M, n = N, max_iter = m > 30 ? m : 30;
@@ -50,7 +60,8 @@ __device__ void cv_jacobi_svd_mn(double* At, double* Wout, double* Vt) {
         bool changed = false;
         for (int i = 0; i < n - 1; i++)
             for (int j = i + 1; j < n; j++) {
-                double *Ai = At + i * M, *Aj = At + j * M;
+                auto Ai = At + i * M;
+                auto Aj = At + j * M;
                 double a = W[i], p = 0, b = W[j];
                 for (int k = 0; k < m; k++) p += Ai[k] * Aj[k];
                 if (fabs(p) <= eps * sqrt(a * b)) continue;
@@ -76,7 +87,8 @@ __device__ void cv_jacobi_svd_mn(double* At, double* Wout, double* Vt) {
                 W[i] = a;
                 W[j] = b;
                 changed = true;
-                double *Vi = Vt + i * N, *Vj = Vt + j * N;
+                auto Vi = Vt + i * N;
+                auto Vj = Vt + j * N;
                 for (int k = 0; k < n; k++) {
                     double t0 = c * Vi[k] + s * Vj[k];
                     double t1 = -s * Vi[k] + c * Vj[k];

@@ -25,6 +25,22 @@
 namespace yavo {
 namespace ess {
 
+// YAVO_LM_PROFILE builds (tools/ess_profile.py): the five-point solver's phase cycles per lane of the first 256
+// iterations of list 0 (SVD, coefficient matrix, LU inverse + product, det B(z), Durand-Kerner, solveZ), and the
+// Durand-Kerner sweep count
+#ifdef YAVO_LM_PROFILE
+__device__ unsigned long long g_ess_prof[256][8];
+#define EP_DECL unsigned long long ep_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long ep_t = __builtin_readcyclecounter();
+#define EP_MARK(slot) do { const unsigned long long t_ = __builtin_readcyclecounter(); ep_acc[slot] += t_ - ep_t; ep_t = t_; } while (0)
+#define EP_SET(slot, v) (ep_acc[slot] = (v))
+#define EP_STORE(k) do { if ((k) < 256) for (int q_ = 0; q_ < 8; ++q_) g_ess_prof[(k)][q_] = ep_acc[q_]; } while (0)
+#else
+#define EP_DECL
+#define EP_MARK(slot) do {} while (0)
+#define EP_SET(slot, v) do {} while (0)
+#define EP_STORE(k) do {} while (0)
+#endif
+
 using cv::cv_jacobi_svd;
 using cv::cv_jacobi_svd_mn;
 using cv::cv_rng_next;
@@ -238,7 +254,7 @@ __device__ void em_det_poly(const double* B, double* c) {
 
 // cv::solvePoly (Durand-Kerner) of degree NN (the coefficients above NN were trimmed); rre / rim [10]
 template <int NN>
-__device__ void dk_solve(const double* c, double* rre, double* rim) {
+__device__ int dk_solve(const double* c, double* rre, double* rim) {
     double cr[NN + 1], xr[NN], xi[NN];
 #pragma unroll
     for (int i = 0; i <= NN; ++i) cr[i] = c[i];
@@ -254,8 +270,14 @@ __device__ void dk_solve(const double* c, double* rre, double* rim) {
             pi = ti;
         }
     }
+    // A sweep that leaves every root bit-identical is a fixed point: the next sweep computes exactly the same values
+    // from the same state (maxDiff is recomputed from zero each sweep and nothing else carries over), so every sweep
+    // up to OpenCV's 300 would too.  Stopping there gives the 300-sweep result bit for bit.
+    int sweeps = 0;
     for (int iter = 0; iter < 300; iter++) {
+        ++sweeps;
         double maxDiff = 0;
+        bool moved = false;
 #pragma unroll
         for (int i = 0; i < NN; i++) {
             const double pr = xr[i], pi = xi[i];
@@ -276,10 +298,12 @@ __device__ void dk_solve(const double* c, double* rre, double* rim) {
             const double qr = (nr * dr + ni * di) * t, qi = (-nr * di + ni * dr) * t;
             xr[i] = pr - qr;
             xi[i] = pi - qi;
+            moved |= __double_as_longlong(xr[i]) != __double_as_longlong(pr) ||
+                     __double_as_longlong(xi[i]) != __double_as_longlong(pi);
             const double an = sqrt(qr * qr + qi * qi);
             maxDiff = maxDiff < an ? an : maxDiff;
         }
-        if (maxDiff <= 0) break;
+        if (maxDiff <= 0 || !moved) break;
     }
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
@@ -291,28 +315,30 @@ __device__ void dk_solve(const double* c, double* rre, double* rim) {
             rim[i] = 0.0;
         }
     }
+    return sweeps;
 }
 
-__device__ void solve_poly10(const double* c, double* rre, double* rim) {
+__device__ int solve_poly10(const double* c, double* rre, double* rim) {
     int n = 10;
     for (; n > 1; n--)
         if (fabs(c[n]) + fabs(0.0) > DBL_EPSILON) break;
     switch (n) {
-        case 10: dk_solve<10>(c, rre, rim); break;
-        case 9: dk_solve<9>(c, rre, rim); break;
-        case 8: dk_solve<8>(c, rre, rim); break;
-        case 7: dk_solve<7>(c, rre, rim); break;
-        case 6: dk_solve<6>(c, rre, rim); break;
-        case 5: dk_solve<5>(c, rre, rim); break;
-        case 4: dk_solve<4>(c, rre, rim); break;
-        case 3: dk_solve<3>(c, rre, rim); break;
-        case 2: dk_solve<2>(c, rre, rim); break;
-        default: dk_solve<1>(c, rre, rim); break;
+        case 10: return dk_solve<10>(c, rre, rim);
+        case 9: return dk_solve<9>(c, rre, rim);
+        case 8: return dk_solve<8>(c, rre, rim);
+        case 7: return dk_solve<7>(c, rre, rim);
+        case 6: return dk_solve<6>(c, rre, rim);
+        case 5: return dk_solve<5>(c, rre, rim);
+        case 4: return dk_solve<4>(c, rre, rim);
+        case 3: return dk_solve<3>(c, rre, rim);
+        case 2: return dk_solve<2>(c, rre, rim);
+        default: return dk_solve<1>(c, rre, rim);
     }
 }
 
 // EMEstimatorCallback::runKernel (oracle or_em_kernel); models [10][9]; returns the count
-__device__ int em_models(const double* q1, const double* q2, double* models) {
+__device__ int em_models(const double* q1, const double* q2, double* models, int prof_k = 1 << 30) {
+    EP_DECL
     double At[81], Vt5[25], W[5];
 #pragma unroll
     for (int i = 0; i < 81; ++i) At[i] = 0.0;
@@ -325,9 +351,11 @@ __device__ int em_models(const double* q1, const double* q2, double* models) {
         r[6] = x1 * 1.0; r[7] = y1 * 1.0; r[8] = 1.0;
     }
     cv_jacobi_svd_mn<9, 5, 9>(At, W, Vt5);
+    EP_MARK(0);
     const double* EE = At + 5 * 9;
     double A[200];
     em_coeff_mat(EE, A);
+    EP_MARK(1);
     double inv[100], M[100];
     lu_inverse10(A, inv);
     for (int i = 0; i < 10; ++i)
@@ -355,9 +383,13 @@ __device__ int em_models(const double* q1, const double* q2, double* models) {
 #pragma unroll
         for (int k = 0; k < 13; ++k) B[i * 13 + k] = r1[k] - r2[k];
     }
+    EP_MARK(2);
     double c[11], rre[10], rim[10];
     em_det_poly(B, c);
-    solve_poly10(c, rre, rim);
+    EP_MARK(3);
+    const int sweeps = solve_poly10(c, rre, rim);
+    EP_MARK(4);
+    EP_SET(7, sweeps);
     int count = 0;
     for (int i = 0; i < 10; i++) {
         if (fabs(rim[i]) > 1e-10) continue;
@@ -392,6 +424,9 @@ __device__ int em_models(const double* q1, const double* q2, double* models) {
         for (int k = 0; k < 9; ++k) models[count * 9 + k] = ev[k] * sc;
         count++;
     }
+    EP_MARK(5);
+    EP_STORE(prof_k);
+    (void)prof_k;
     return count;
 }
 
@@ -515,7 +550,7 @@ __global__ __launch_bounds__(kModelLanes) void ess_models_kernel(EssParams P, in
         q2[2 * i + 1] = m2[2 * j + 1];
     }
     double* out = P.models + ((int64_t)pair * P.chunk + k) * 90;
-    *nmod = em_models(q1, q2, out);
+    *nmod = em_models(q1, q2, out, pair == 0 ? it : 1 << 30);
 }
 
 __global__ __launch_bounds__(256) void ess_score_kernel(EssParams P, int chunk0, float t) {
@@ -764,6 +799,13 @@ __global__ void rp_select_kernel(int n_pairs, EssParams P, double* __restrict__ 
 }
 
 }  // namespace ess
+
+#ifdef YAVO_LM_PROFILE
+extern "C" int yv_debug_ess_prof(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(ess::g_ess_prof), sizeof(unsigned long long) * 256 * 8) == hipSuccess
+               ? 0 : -2;
+}
+#endif
 
 void launch_find_essential(const EssParams& P, const EssRun& r, const float* pts1, const float* pts2,
                            const int32_t* counts, int n_pairs, int pts_stride, double* E, uint8_t* mask,

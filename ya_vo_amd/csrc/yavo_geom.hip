@@ -57,9 +57,6 @@ __device__ unsigned long long g_lm_prof[1024][10];
 #define LMP_STORE() do {} while (0)
 #endif
 constexpr int kMaxEdges = 4096;   // edges per pose problem held in LDS
-// edge capacity of the LDS-resident pose LM (X 24 B + uv 8 B + 5 B of flags / index per edge: 76 KB, two workgroups
-// per CU)
-constexpr int kLMResCap = 2048;
 
 // exclusive scan over an NT-thread block; s_tmp >= NT/64 ints
 template <int NT = kNT>
@@ -1290,25 +1287,17 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
 // Register budget of the LM: 2 waves per SIMD = 256 VGPRs and no AGPRs (36 B of scratch), so a SIMD running an LM
 // wave keeps 256 registers for the image kernels beside it (4 detect waves instead of 3): 125k -> 131k frames/s.
 // 3 / 4 (168 / 128 VGPRs) spill 400-600 B per lane in the lane-0 LDLT and triple the LM's latency.
-#ifndef YAVO_LM_WAVES_PER_EU
-#define YAVO_LM_WAVES_PER_EU 2
-#endif
-#define YAVO_LM_ATTR __attribute__((amdgpu_waves_per_eu(YAVO_LM_WAVES_PER_EU)))
-// CAP < kMaxEdges: the problem's edges (at most CAP) are held in LDS for all its passes -- X as doubles, uv as floats.
-// That form is exact only for measurements representable in float: the batch's track edges, whose uv are keypoint
-// or LK pixel positions (track_build_kernel, lk_edges_kernel); launch_track_pose selects it for them alone.
-template <int NT, int CAP>
+#define YAVO_LM_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+template <int NT>
 __device__ __forceinline__ void pose_lm_body(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
                                                       int stride, const double* __restrict__ Xall,
                                                       const double* __restrict__ uvall, const double* __restrict__ Kall,
                                                       const double* priors, double* poses,
                                                       uint8_t* __restrict__ outlier_all, int32_t* __restrict__ inliers,
                                                       int n_prob) {
-    constexpr bool kRes = CAP < kMaxEdges;
+    constexpr int CAP = kMaxEdges;
     __shared__ uint8_t s_level[CAP], s_out[CAP], s_robust[CAP];
     __shared__ int16_t s_active[CAP];
-    __shared__ double s_X[kRes ? 3 * CAP : 1];
-    __shared__ float s_uv[kRes ? 2 * CAP : 1];
     __shared__ double s_red[NT > 64 ? kLMVals * (NT / 64) : 1];
     __shared__ LMShared S;
     __shared__ int s_tmp[40];
@@ -1320,17 +1309,8 @@ __device__ __forceinline__ void pose_lm_body(const int32_t* __restrict__ offsets
     const int64_t e0 = counts ? (int64_t)prob * stride : (int64_t)offsets[prob];
     int n = counts ? counts[prob] : (int)(offsets[prob + 1] - e0);
     if (n > CAP) n = CAP;
-    const double* Xg = Xall + 3 * e0;
-    const double* uvg = uvall + 2 * e0;
-    if constexpr (kRes) {
-        for (int i = tid; i < 3 * n; i += NT) s_X[i] = Xg[i];
-        for (int i = tid; i < 2 * n; i += NT) s_uv[i] = (float)uvg[i];
-    }
-    const double* X = kRes ? s_X : Xg;
-    const auto* uv = [&] {
-        if constexpr (kRes) return static_cast<const float*>(s_uv);
-        else return uvg;
-    }();
+    const double* X = Xall + 3 * e0;
+    const double* uv = uvall + 2 * e0;
     if (tid < 9) S.K[tid] = Kall[9 * prob + tid];
     if (tid < 7) S.T[tid] = priors[7 * prob + tid];
     for (int i = tid; i < n; i += NT) {
@@ -1535,17 +1515,7 @@ __global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_kernel(const int32_t*
                                                       const double* priors, double* poses,
                                                       uint8_t* __restrict__ outlier_all, int32_t* __restrict__ inliers,
                                                       int n_prob) {
-    pose_lm_body<NT, kMaxEdges>(offsets, counts, stride, Xall, uvall, Kall, priors, poses, outlier_all, inliers, n_prob);
-}
-// The LDS-resident form (CAP = kLMResCap)
-template <int NT>
-__global__ __launch_bounds__(NT) YAVO_LM_ATTR void pose_lm_res_kernel(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
-                                                      int stride, const double* __restrict__ Xall,
-                                                      const double* __restrict__ uvall, const double* __restrict__ Kall,
-                                                      const double* priors, double* poses,
-                                                      uint8_t* __restrict__ outlier_all, int32_t* __restrict__ inliers,
-                                                      int n_prob) {
-    pose_lm_body<NT, kLMResCap>(offsets, counts, stride, Xall, uvall, Kall, priors, poses, outlier_all, inliers, n_prob);
+    pose_lm_body<NT>(offsets, counts, stride, Xall, uvall, Kall, priors, poses, outlier_all, inliers, n_prob);
 }
 
 // Track edges of the batched frontend: track t = {stereo pair sp, temporal pair tp} with
@@ -1785,68 +1755,15 @@ __global__ __launch_bounds__(kNT) void pose_gn_kernel(const int32_t* __restrict_
     if (tid == 0) iters_out[prob] = acc;
 }
 
-// Threads per pose-LM workgroup: 256 by default (one wave per SIMD: the LM is latency-bound, and 64 / 128 threads
-// measured 2.1 / 1.5 ms against 1.0 ms per 256-frame batch); YAVO_LM_THREADS = 64 / 128 for experiments. The
-// summation order follows (yv_lm_sum_mode).
-inline int lm_threads() {
-    static const int nt = [] {
-        const char* e = getenv("YAVO_LM_THREADS");
-        const int v = e ? atoi(e) : 256;
-        return (v == 64 || v == 128) ? v : 256;
-    }();
-    return nt;
-}
+// Threads per pose-LM workgroup: 256, one wave per SIMD (the LM is latency-bound: 64 / 128 threads measured 2.1 /
+// 1.5 ms against 1.0 ms per 256-frame batch).  The summation order follows (yv_lm_sum_mode 6).  Measured and not kept
+// (DESIGN.md 4.3, 10): fewer workgroups looping over the problems, LDS padding to one workgroup per CU, and a form
+// holding each problem's edges in LDS.
+constexpr int kLMThreads = 256;
 
-// Workgroups of one LM launch (YAVO_LM_GRID, 0 = one per problem): fewer workgroups loop over the problems, so the
-// LM holds fewer CUs' registers while it runs beside the image kernels.
-inline int lm_grid() {
-    static const int g = [] {
-        const char* e = getenv("YAVO_LM_GRID");
-        return e ? atoi(e) : 0;
-    }();
-    return g;
-}
-
-// Dynamic LDS of one LM launch (YAVO_LM_LDS_PAD bytes, default 0): unused padding that caps the LM at one workgroup
-// per CU, so a CU running it keeps half of every SIMD's registers for the image kernels beside it.
-inline size_t lm_lds_pad() {
-    static const size_t p = [] {
-        const char* e = getenv("YAVO_LM_LDS_PAD");
-        return e ? (size_t)atol(e) : (size_t)0;
-    }();
-    return p;
-}
-
-// YAVO_LM_RESIDENT=1 puts the track path on the LDS-resident form: its HBM/L2 traffic is the edges once (1.04x the
-// algorithmic bytes, against ~16x when every pass re-streams them), but it takes 256 VGPRs and 78 KB of LDS per
-// workgroup, so two of them fill a CU's register file and half its LDS; measured 1.10 vs 1.06 ms alone and 210.6k vs
-// 214.8k frames/s in the step (profiles/r03/c43).  Off by default.
-inline int& lm_resident_flag() {
-    static int r = [] {
-        const char* e = getenv("YAVO_LM_RESIDENT");
-        return e ? (atoi(e) != 0 ? 1 : 0) : 0;
-    }();
-    return r;
-}
-inline bool lm_resident() { return lm_resident_flag() != 0; }
-
-template <int CAP, typename... A>
+template <typename... A>
 void launch_lm(int n, hipStream_t s, A... args) {
-    const int g = lm_grid() > 0 && lm_grid() < n ? lm_grid() : n;
-    const size_t pad = lm_lds_pad();
-    if constexpr (CAP == kLMResCap) {
-        switch (lm_threads()) {
-            case 256: hipLaunchKernelGGL(pose_lm_res_kernel<256>, dim3(g), dim3(256), pad, s, args..., n); break;
-            case 128: hipLaunchKernelGGL(pose_lm_res_kernel<128>, dim3(g), dim3(128), pad, s, args..., n); break;
-            default: hipLaunchKernelGGL(pose_lm_res_kernel<64>, dim3(g), dim3(64), pad, s, args..., n); break;
-        }
-    } else {
-        switch (lm_threads()) {
-            case 256: hipLaunchKernelGGL(pose_lm_kernel<256>, dim3(g), dim3(256), pad, s, args..., n); break;
-            case 128: hipLaunchKernelGGL(pose_lm_kernel<128>, dim3(g), dim3(128), pad, s, args..., n); break;
-            default: hipLaunchKernelGGL(pose_lm_kernel<64>, dim3(g), dim3(64), pad, s, args..., n); break;
-        }
-    }
+    hipLaunchKernelGGL(pose_lm_kernel<kLMThreads>, dim3(n), dim3(kLMThreads), 0, s, args..., n);
 }
 
 }  // namespace geom
@@ -1889,7 +1806,7 @@ void launch_world2camera(const double* X, int n, const double* T, const double* 
 
 void launch_pose_lm(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
                     double* poses, uint8_t* outlier, int32_t* inliers, hipStream_t s) {
-    geom::launch_lm<geom::kMaxEdges>(n_problems, s, offsets, static_cast<const int32_t*>(nullptr), 0, X, uv, K,
+    geom::launch_lm(n_problems, s, offsets, static_cast<const int32_t*>(nullptr), 0, X, uv, K,
                                static_cast<const double*>(poses), poses, outlier, inliers);
 }
 
@@ -1898,22 +1815,10 @@ void launch_track_build(const int32_t* tracks, int n_tracks, const int32_t* pair
                         const double* K, const double* T_right, double* edge_X, double* edge_uv, int32_t* edge_query,
                         int32_t* edge_count, hipStream_t s) {
     if (n_tracks <= 0) return;
-    // 1024 threads: about one query keypoint per thread (the FP64 triangulations are latency-bound).
-    // YAVO_BUILD_NT=256 / 512 select narrower workgroups (measured).
-    static const int nt = [] {
-        const char* e = std::getenv("YAVO_BUILD_NT");
-        const int v = e ? std::atoi(e) : 1024;
-        return (v == 256 || v == 512) ? v : 1024;
-    }();
-    if (nt == 256)
-        hipLaunchKernelGGL(geom::track_build_kernel<256>, dim3(n_tracks), dim3(256), 0, s, tracks, pairs, keypoints,
-                           kp_count, match_dj, match_lim, max_kp, K, T_right, edge_X, edge_uv, edge_query, edge_count);
-    else if (nt == 512)
-        hipLaunchKernelGGL(geom::track_build_kernel<512>, dim3(n_tracks), dim3(512), 0, s, tracks, pairs, keypoints,
-                           kp_count, match_dj, match_lim, max_kp, K, T_right, edge_X, edge_uv, edge_query, edge_count);
-    else
-        hipLaunchKernelGGL(geom::track_build_kernel<1024>, dim3(n_tracks), dim3(1024), 0, s, tracks, pairs, keypoints,
-                           kp_count, match_dj, match_lim, max_kp, K, T_right, edge_X, edge_uv, edge_query, edge_count);
+    // 1024 threads: about one query keypoint per thread (the FP64 triangulations are latency-bound; 256 / 512 were
+    // measured)
+    hipLaunchKernelGGL(geom::track_build_kernel<1024>, dim3(n_tracks), dim3(1024), 0, s, tracks, pairs, keypoints,
+                       kp_count, match_dj, match_lim, max_kp, K, T_right, edge_X, edge_uv, edge_query, edge_count);
 }
 
 void launch_stereo_points(const int32_t* stereo_pairs, int n_tracks, const int32_t* pairs,
@@ -1938,13 +1843,8 @@ void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, cons
                        const double* edge_uv, const double* K, const double* priors, double* poses,
                        uint8_t* edge_outlier, int32_t* inliers, hipStream_t s) {
     if (n_tracks <= 0) return;
-    // track edges: uv are keypoint / LK pixel positions (float-exact), at most stride per frame
-    if (stride <= geom::kLMResCap && geom::lm_resident())
-        geom::launch_lm<geom::kLMResCap>(n_tracks, s, static_cast<const int32_t*>(nullptr), edge_count, stride, edge_X,
-                                         edge_uv, K, priors, poses, edge_outlier, inliers);
-    else
-        geom::launch_lm<geom::kMaxEdges>(n_tracks, s, static_cast<const int32_t*>(nullptr), edge_count, stride, edge_X,
-                                   edge_uv, K, priors, poses, edge_outlier, inliers);
+    geom::launch_lm(n_tracks, s, static_cast<const int32_t*>(nullptr), edge_count, stride, edge_X, edge_uv, K, priors,
+                    poses, edge_outlier, inliers);
 }
 
 void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
@@ -1955,7 +1855,7 @@ void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, con
 }  // namespace yavo
 
 extern "C" int yv_lm_sum_mode(void) {
-    const int nt = yavo::geom::lm_threads();
+    constexpr int nt = yavo::geom::kLMThreads;
     return nt == 256 ? 6 : nt == 128 ? 5 : 4;
 }
 
@@ -1967,9 +1867,3 @@ extern "C" int yv_debug_lm_prof(unsigned long long* out) {
 }
 #endif
 
-// tests: select the pose LM form of the track path (1 = LDS-resident); returns the previous setting
-extern "C" int yv_debug_lm_resident(int on) {
-    const int prev = yavo::geom::lm_resident_flag();
-    yavo::geom::lm_resident_flag() = on ? 1 : 0;
-    return prev;
-}

@@ -21,16 +21,6 @@
 #include "yavo_xlane.h"
 #include "yavo_internal.h"
 
-// Issue priority of the critical-path image kernels over the pose LM that runs beside them on the side stream
-// (s_setprio: the SIMD's arbiter issues the higher-priority wave first).  YAVO_CRIT_PRIO: 0 off, 1 top-K only,
-// 2 every stage of yv_batch_run.
-#ifndef YAVO_CRIT_PRIO
-#define YAVO_CRIT_PRIO 0
-#endif
-#define YV_PRIO_TOPK() \
-    if (YAVO_CRIT_PRIO >= 1) __builtin_amdgcn_s_setprio(3)
-#define YV_PRIO_RUN() \
-    if (YAVO_CRIT_PRIO >= 2) __builtin_amdgcn_s_setprio(3)
 
 namespace yavo {
 
@@ -304,7 +294,6 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
                                                      int64_t pitch, int thr, int eig, uint64_t* __restrict__ cand_keys,
                                                      int64_t cap, uint32_t* __restrict__ cand_count, K9 kw,
                                                      uint8_t* __restrict__ blur) {
-    YV_PRIO_RUN();
     __shared__ __align__(16) uint8_t tile[FT_LH * FT_LW];
     // the pretest survivors (phases 1-2) and the horizontal blur (from the barrier after phase 2) share LDS
     constexpr int kPreDw = FT_W * FT_H / 2, kHbufDw = kBlur ? (FT_LH / 2) * FT_W : 0;
@@ -341,7 +330,6 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
         const bool interior = (c0 >= FT_R) && (c0 + FT_W + FT_R <= W) && (r0 >= FT_R) && (r0 + FT_H + FT_R < H);
         uint32_t v[kPer];
         if (interior) {
-#ifndef YAVO_DET_STAGE_OLD
             // one wave-uniform base (SGPRs) and a 32-bit lane offset: slot t + 256 is 14 rows and 4 dwords on, or 15
             // rows and 14 dwords back when the dword index wraps past 18 (256 = 14 * 18 + 4), so one division for
             // the first slot and a compare + select + add for each further one (the same slots as the division form)
@@ -360,14 +348,6 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
                 off += c ? wrap : step;
                 j += c ? 4 - kDw : 4;
             }
-#else
-#pragma unroll
-            for (int u = 0; u < kPer; ++u) {
-                const int t = min(tid + 256 * u, kSlots - 1);
-                const int lr = t / kDw, j = t - lr * kDw;
-                __builtin_memcpy(&v[u], src + (int64_t)(r0 - FT_R + lr) * stride + (c0 - FT_R) + 4 * j, 4);
-            }
-#endif
         } else {
 #pragma unroll
             for (int u = 0; u < kPer; ++u) {
@@ -759,10 +739,7 @@ __device__ void boundary_compact(RcAt rc_at, int K, int H, int W, int32_t* kp_sr
 // top-K per image: one workgroup of NT threads per image.  512 threads: same-box A/B in the headline step (r03 c32,
 // two runs each) 1024 -> 206.0k fps, 512 -> 209.7k, 256 -> 207.3k; in-step top-K 757 -> 488 us per dispatch (half
 // the waves at each of its ~80 workgroup barriers, twice the per-thread work in the sort stages).
-#ifndef YAVO_TOPK_NT
-#define YAVO_TOPK_NT 512
-#endif
-constexpr int TK_SEL_NT = YAVO_TOPK_NT;
+constexpr int TK_SEL_NT = 512;
 static_assert(TK_SEL_NT >= 256 && TK_SEL_NT % 64 == 0, "the radix-select histogram scan uses the first 256 threads");
 template <int NT>
 __global__ __launch_bounds__(NT) void topk_kernel(const uint64_t* __restrict__ cand_keys, int64_t cap,
@@ -771,7 +748,6 @@ __global__ __launch_bounds__(NT) void topk_kernel(const uint64_t* __restrict__ c
                                                      float* __restrict__ det_resp, int32_t* __restrict__ det_count,
                                                      int32_t* __restrict__ kp_src, int32_t* __restrict__ kp_count,
                                                      int32_t* __restrict__ kp_band, int32_t* __restrict__ band_off) {
-    YV_PRIO_TOPK();
     __shared__ uint64_t s_keys[kMaxKp];
     __shared__ uint32_t s_hist[256];
     __shared__ int s_tmp[40];
@@ -935,10 +911,7 @@ constexpr int BR_BAND = kBandRows;
 constexpr int BR_ROWS = BR_BAND + 17;  // rows r0-8 .. r0+40 (the last one for the wrap of col + 8 == W)
 // 16 waves share one staged band: the ~61 KB band limits a CU to 2 workgroups, so the workgroup is as wide as
 // the 64-VGPR budget of 8 waves per SIMD allows
-#ifndef YAVO_BR_NT
-#define YAVO_BR_NT 1024
-#endif
-constexpr int BR_NT = YAVO_BR_NT;
+constexpr int BR_NT = 1024;
 constexpr int BR_NW = BR_NT / 64;
 // the band's keypoint records are loaded as 4 per thread (kq below): a band may hold every keypoint of the image.
 // (A loop over any further records would lift this bound but takes the kernel from 46 to 64 VGPRs, and at <= 48 one
@@ -951,7 +924,6 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
                                                     const int32_t* __restrict__ band_off, int max_kp,
                                                     yv_keypoint* __restrict__ keypoints, Desc* __restrict__ desc,
                                                     const int2* __restrict__ loff) {
-    YV_PRIO_RUN();
     extern __shared__ uint8_t s_band[];  // BR_ROWS * brief_lds_stride(W) bytes
     // this band's keypoints, packed (index << 16) | (col << 5) | (row - r0): index < 4096, col < 2048, 32-row band
     __shared__ uint32_t s_list[kMaxKp];
@@ -1177,20 +1149,6 @@ __device__ __forceinline__ uint4 expand16_pm1(uint32_t bits) {
                       expand_pm1((bits >> 12) & 0xF));
 }
 
-// 4 descriptor bits -> 4 bytes of 64 (bit set) / 0 (bit clear): the 0/64 encoding of the matcher for train lists <= 2048
-__device__ __forceinline__ uint32_t expand_01x64(uint32_t nib) {
-    // v_mul_u32_u24 (full rate; nib <= 15) kept as written: LLVM would otherwise fold the shift into one
-    // quarter-rate v_mul_lo_u32 by 0x08102040
-    uint32_t spread;
-    asm("v_mul_u32_u24 %0, 0x204081, %1" : "=v"(spread) : "v"(nib));
-    return (spread & 0x01010101u) << 6;
-}
-
-__device__ __forceinline__ uint4 expand16_01x64(uint32_t bits) {
-    return make_uint4(expand_01x64(bits & 0xF), expand_01x64((bits >> 4) & 0xF), expand_01x64((bits >> 8) & 0xF),
-                      expand_01x64((bits >> 12) & 0xF));
-}
-
 __device__ __forceinline__ int desc_popcount(const Desc& d) {
     int c = 0;
 #pragma unroll
@@ -1198,19 +1156,12 @@ __device__ __forceinline__ int desc_popcount(const Desc& d) {
     return c;
 }
 
-// kFast (train lists <= 2048): bytes 0 / 64, so the MFMA's dot is 4096 * popcount(a & b) and, started from the
-// accumulator c_j = (2047 - j) - 2048 * popcount(b_j), a 4-step chain ends at the key itself:
-//   key = 2048 * (2 popcount(a & b_j) - popcount(b_j)) + (2047 - j) = 2048 * (pa - Hamming) + (2047 - j)
-// (pa - Hamming orders like -Hamming for one query; 2047 - j >= 0 breaks ties toward the first j). The epilogue is
-// one v_max3 per two distances, the train staging four full-rate ops per nibble, and the decode Hamming =
-// pa - (key >> 11), j = 2047 - (key & 2047). Otherwise (max_kp up to 4096): the +-1 encoding, dot = 256 - 2 Hamming,
-// key = (dot << 16) + 0xFFFF - j formed per element.
-template <bool kFast>
+// Train lists above 2048 (up to kMaxKp; lists <= 2048 take the FP4 kernel below): the +-1 encoding, dot = 256 -
+// 2 Hamming, key = (dot << 16) + 0xFFFF - j formed per element.
 __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ desc, const int32_t* __restrict__ kp_count,
                                                     const int32_t* __restrict__ pairs, int max_kp,
                                                     uint32_t* __restrict__ match_key) {
     __shared__ uint4 s_t[2][MM_TC * MM_ROW];
-    __shared__ int s_pb[2][MM_TC];
     const int pair = blockIdx.y;
     const int qi = pairs[2 * pair], ti = pairs[2 * pair + 1];
     const int nq = kp_count[qi], nt = kp_count[ti];
@@ -1220,7 +1171,6 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
     const int col = lane & 15, g = lane >> 4;
     const Desc* qd = desc + (int64_t)qi * max_kp;
     const uint32_t* tw = reinterpret_cast<const uint32_t*>(desc + (int64_t)ti * max_kp);
-    const Desc* td = desc + (int64_t)ti * max_kp;
 
     // query fragments: tile qt row (lane & 15) = query q0 + 16 MM_QT wave + 16 qt + (lane & 15)
     mm_v4i A[MM_QT][4];
@@ -1233,7 +1183,7 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
             const uint32_t hi_mask = 0u - (uint32_t)(g >> 1);  // blend, not an index: keeps d in registers
             const uint32_t w = d.w[2 * s] ^ ((d.w[2 * s] ^ d.w[2 * s + 1]) & hi_mask);
             const uint32_t bits = (w >> (16 * (g & 1))) & 0xFFFFu;
-            const uint4 e = kFast ? expand16_01x64(bits) : expand16_pm1(bits);
+            const uint4 e = expand16_pm1(bits);
             A[qt][s] = mm_v4i{(int)e.x, (int)e.y, (int)e.z, (int)e.w};
         }
     }
@@ -1243,11 +1193,9 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
 #pragma unroll
         for (int r = 0; r < 4; ++r) best[qt][r] = INT_MIN;
 
-    // staging: thread -> (train tt = idx >> 4, 16-bit field u = idx & 15), kF fields per thread per chunk; in kFast
-    // the first MM_TC threads also count the set bits of train tt = tid
+    // staging: thread -> (train tt = idx >> 4, 16-bit field u = idx & 15), kF fields per thread per chunk
     constexpr int kF = MM_TC * 16 / 256;  // 16-bit fields per thread per chunk
     uint32_t pre[kF];
-    int pre_pb = 0;
     auto fetch = [&](int t0) {
 #pragma unroll
         for (int k = 0; k < kF; ++k) {
@@ -1255,16 +1203,14 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
             const int t = t0 + tt;
             pre[k] = t < nt ? tw[(int64_t)t * 8 + (u >> 1)] : 0u;
         }
-        if (kFast && tid < MM_TC) pre_pb = t0 + tid < nt ? desc_popcount(td[t0 + tid]) : 0;
     };
     auto store = [&](int buf) {
 #pragma unroll
         for (int k = 0; k < kF; ++k) {
             const int idx = tid + 256 * k, tt = idx >> 4, u = idx & 15;
             const uint32_t bits = (pre[k] >> (16 * (u & 1))) & 0xFFFFu;
-            s_t[buf][tt * MM_ROW + u] = kFast ? expand16_01x64(bits) : expand16_pm1(bits);
+            s_t[buf][tt * MM_ROW + u] = expand16_pm1(bits);
         }
-        if (kFast && tid < MM_TC) s_pb[buf][tid] = pre_pb;
     };
     if (nt > 0) {
         fetch(0);
@@ -1291,30 +1237,7 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
             // a column past nt (including the whole second tile at the end of the list) gets -2^30, below every
             // real key and above INT_MIN, so no per-element select and no branch are needed
             const int ja = t0 + tt0 + col, jb = ja + 16;
-            if (kFast) {
-                const int ca = ja < nt ? (2047 - ja) - 2048 * s_pb[buf][tt0 + col] : -(1 << 30);
-                const int cb = jb < nt ? (2047 - jb) - 2048 * s_pb[buf][tt0 + 16 + col] : -(1 << 30);
-                const mm_v4i Ca = {ca, ca, ca, ca}, Cb = {cb, cb, cb, cb};
-#pragma unroll
-                for (int qt = 0; qt < MM_QT; qt += 2) {
-                    mm_v4i a0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][0], Ba[0], Ca, 0, 0, 0);
-                    mm_v4i b0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][0], Bb[0], Cb, 0, 0, 0);
-                    mm_v4i a1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][0], Ba[0], Ca, 0, 0, 0);
-                    mm_v4i b1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][0], Bb[0], Cb, 0, 0, 0);
-#pragma unroll
-                    for (int s = 1; s < 4; ++s) {
-                        a0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], Ba[s], a0, 0, 0, 0);
-                        b0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt][s], Bb[s], b0, 0, 0, 0);
-                        a1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][s], Ba[s], a1, 0, 0, 0);
-                        b1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[qt + 1][s], Bb[s], b1, 0, 0, 0);
-                    }
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        best[qt][r] = max(best[qt][r], max(a0[r], b0[r]));
-                        best[qt + 1][r] = max(best[qt + 1][r], max(a1[r], b1[r]));
-                    }
-                }
-            } else {
+            {
                 // key = (dot << 16) + bias: bias = 0xFFFF - j for a real train column
                 const int bias_a = ja < nt ? 0xFFFF - ja : -(1 << 30);
                 const int bias_b = jb < nt ? 0xFFFF - jb : -(1 << 30);
@@ -1358,17 +1281,10 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
             if (col == r && q < nq) {
                 uint32_t key = 0xFFFFFFFFu;  // empty train set (nt >= 1 always leaves a real key in the row max)
                 if (v != INT_MIN) {
-                    if (kFast) {
-                        const int pa = desc_popcount(qd[q]);
-                        const uint32_t d = (uint32_t)(pa - (v >> 11));
-                        const uint32_t jj = 2047u - ((uint32_t)v & 2047u);
-                        key = (d << 16) | jj;
-                    } else {
-                        const int dot = v >> 16;
-                        const uint32_t d = (uint32_t)((256 - dot) >> 1);
-                        const uint32_t jj = 0xFFFFu - ((uint32_t)v & 0xFFFFu);
-                        key = (d << 16) | jj;
-                    }
+                    const int dot = v >> 16;
+                    const uint32_t d = (uint32_t)((256 - dot) >> 1);
+                    const uint32_t jj = 0xFFFFu - ((uint32_t)v & 0xFFFFu);
+                    key = (d << 16) | jj;
                 }
                 match_key[(int64_t)pair * max_kp + q] = key;
             }
@@ -1423,7 +1339,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                                                         const int32_t* __restrict__ kp_count,
                                                         const int32_t* __restrict__ pairs, int max_kp,
                                                         uint32_t* __restrict__ match_key) {
-    YV_PRIO_RUN();
     constexpr int QB = 4 * QT * 16;  // queries per workgroup
     __shared__ uint4 s_t[2][MF_TC * MF_ROW];
     __shared__ float s_c[2][MF_TC];  // c_j = (2047 - j) - 2048 popcount(b_j) + 2^21, 0 past the list
@@ -1567,19 +1482,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
 }
 
 namespace {
-// YAVO_MATCH_FORM selects the matcher's form for measurements: "i8" (int8 MFMA, 0/64 bytes), "fp4" (default;
-// FP4 MFMA, 8 query tiles per wave, 3 waves per SIMD), "fp4w2" (8 tiles, 2 waves), "fp4q4" (4 tiles, 4 waves) or
-// "fp4q16" (16 tiles, 1 wave).  Every form gives the same keys.  At 512 stereo frames per step (1024 pairs, 1941
-// keypoints) the matcher runs i8 0.77 ms, fp4w2 0.51, fp4 0.46, fp4q4 0.52, fp4q16 0.73 (alone, HIP events).
-int match_form() {
-    static int form = -1;
-    if (form < 0) {
-        const char* e = getenv("YAVO_MATCH_FORM");
-        form = !e ? 1 : !strcmp(e, "i8") ? 0 : !strcmp(e, "fp4q16") ? 2 : !strcmp(e, "fp4w2") ? 3 : !strcmp(e, "fp4q4") ? 4 : 1;
-    }
-    return form;
-}
-
 template <int QT, int WPE>
 void launch_fp4(const Desc* desc, const int32_t* kp_count, const int32_t* pairs, int n_pairs, int max_kp,
                 uint32_t* match_key, hipStream_t s) {
@@ -1593,20 +1495,11 @@ void launch_match(const Desc* desc, const int32_t* kp_count, const int32_t* pair
                   int max_train, uint32_t* match_key, hipStream_t s) {
     if (max_train > 2048) {
         dim3 grid((max_kp + MM_QB - 1) / MM_QB, n_pairs);
-        hipLaunchKernelGGL(match_kernel<false>, grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
+        hipLaunchKernelGGL(match_kernel, grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
         return;
     }
-    switch (match_form()) {
-        case 0: {
-            dim3 grid((max_kp + MM_QB - 1) / MM_QB, n_pairs);
-            hipLaunchKernelGGL(match_kernel<true>, grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
-            break;
-        }
-        case 2: launch_fp4<16, 1>(desc, kp_count, pairs, n_pairs, max_kp, match_key, s); break;
-        case 3: launch_fp4<8, 2>(desc, kp_count, pairs, n_pairs, max_kp, match_key, s); break;
-        case 4: launch_fp4<4, 4>(desc, kp_count, pairs, n_pairs, max_kp, match_key, s); break;
-        default: launch_fp4<8, 3>(desc, kp_count, pairs, n_pairs, max_kp, match_key, s); break;
-    }
+    // FP4: 8 query tiles per wave, 3 waves per SIMD (measured against 2 / 4 waves and 4 / 16 tiles)
+    launch_fp4<8, 3>(desc, kp_count, pairs, n_pairs, max_kp, match_key, s);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1637,7 +1530,6 @@ __global__ __launch_bounds__(FZ_NT) void match_finalize_kernel(
     const int32_t* __restrict__ kp_count, const int32_t* __restrict__ pairs, int max_kp, int thr,
     yv_match* __restrict__ matches, int32_t* __restrict__ match_count, yv_match* __restrict__ filtered,
     int32_t* __restrict__ filt_count, int2* __restrict__ match_dj, int32_t* __restrict__ match_lim) {
-    YV_PRIO_RUN();
     __shared__ int s_dist[kMaxKp];
     __shared__ int s_j[kMaxKp];
     __shared__ int s_pos[kMaxKp];
@@ -1686,10 +1578,7 @@ __global__ __launch_bounds__(FZ_NT) void match_finalize_kernel(
     // value is then selected), FZ_U dwords per thread with every load in flight before the stores.  A wave's 64
     // consecutive dwords span ~2.5 records, so per-field branches ran all three paths with a load wait in each
     // (0.83 -> 0.67 ms per 2048-frame step, profiles/r03/c54).
-#ifndef YAVO_FZ_U
-#define YAVO_FZ_U 4
-#endif
-    constexpr int FZ_U = YAVO_FZ_U;
+    constexpr int FZ_U = 4;
     for (int dw0 = tid; dw0 < ndw; dw0 += FZ_U * FZ_NT) {
         uint32_t v[FZ_U];
         int ii[FZ_U], ff[FZ_U];

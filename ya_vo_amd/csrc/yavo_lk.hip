@@ -434,24 +434,14 @@ __device__ __forceinline__ void scharr_footprint(const uint8_t* __restrict__ I, 
 template <int S>
 __device__ __forceinline__ void load_footprint_pairs(const uint8_t* __restrict__ J, int sJ, int Hl, int Wl, int x0,
                                                      int y0, uint32_t (&p)[S + 1][S]) {
-#ifndef YAVO_LK_UNALIGNED
-#define YAVO_LK_UNALIGNED 1
-#endif
-    if (S <= 3 && x0 >= 0 && y0 >= 0 && x0 + (YAVO_LK_UNALIGNED ? 3 : 7) < Wl && y0 + S < Hl) {
+    if (S <= 3 && x0 >= 0 && y0 >= 0 && x0 + 3 < Wl && y0 + S < Hl) {
         const uint32_t off = (uint32_t)(y0 * sJ + x0);
 #pragma unroll
         for (int i = 0; i <= S; ++i) {
             const uint32_t o = off + (uint32_t)(i * sJ);
-#if YAVO_LK_UNALIGNED
             // one byte-aligned dword load (the hardware's unaligned mode splits it), no alignment arithmetic in VALU
             uint32_t w;
             __builtin_memcpy(&w, J + o, 4);
-#else
-            const uint32_t mis = (uint32_t)((uintptr_t)J + o) & 3u;
-            u32x2 a;
-            __builtin_memcpy(&a, __builtin_assume_aligned(J + (o - mis), 4), 8);
-            const uint32_t w = __builtin_amdgcn_alignbyte(a.y, a.x, mis);
-#endif
 #pragma unroll
             for (int j = 0; j < S; ++j)  // bytes j, j + 1 into the low bytes of the two halves (0x0C selects 0)
                 p[i][j] = __builtin_amdgcn_perm(0u, w, 0x0C000C00u | ((uint32_t)(j + 1) << 16) | (uint32_t)j);

@@ -212,6 +212,12 @@ int LoopHandler::getFRANSAC(const std::vector<Matches>& m, double F[9]) {
     std::uniform_int_distribution<int> dist(0, n - 1);
     for (auto& s : samples) s = dist(ransac_rng_);
     int max_inl = 0, found = 0;
+    const double t0 = now_s();
+    struct Acc {
+        double& v;
+        double t;
+        ~Acc() { v += now_s() - t; }
+    } acc{prim_.f_ransac, t0};
     if (!gpu(yv_f_ransac(dev_->ctx(), m.data(), n, samples.data(), iters, 0.1, F, &max_inl, &found), "getFRANSAC"))
         return 0;
     return found ? max_inl : 0;
@@ -231,15 +237,19 @@ bool LoopHandler::essentialPose(const std::vector<Matches>& filt, SE3& currPose)
     double E[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     std::vector<uint8_t> mask(n > 0 ? n : 1);
     int found = 0;
+    const double t0 = now_s();
     if (!gpu(yv_find_essential(dev_->ctx(), curr.data(), prev.data(), n, 718.8560, 607.1928, 185.2157, 0.999, 1.0,
                                E, mask.data(), &found),
              "findEssentialMat"))
         return false;
     ev_.essential_found = found;
+    const double t1 = now_s();
+    prim_.find_essential += t1 - t0;
     double R[9], t[3];
     int good = 0;
     if (!gpu(yv_recover_pose(dev_->ctx(), E, curr.data(), prev.data(), n, K_, R, t, &good), "recoverPose"))
         return false;
+    prim_.recover_pose += now_s() - t1;
     currPose = se3::from_Rt(R, t);
     return true;
 }
@@ -339,9 +349,11 @@ int LoopHandler::trackLastFrame() {
     }
     const int nc = (int)idx.size();
     std::vector<double> proj(3 * (size_t)std::max(nc, 1));
+    const double tw = now_s();
     if (nc > 0 &&
         !gpu(yv_world2camera(dev_->ctx(), Xs.data(), nc, currentFrame_->pose.d, K_, proj.data()), "world2Camera"))
         return 0;
+    prim_.world2camera += now_s() - tw;
     std::vector<float> lastKpt, currKpt;
     std::vector<int> lastIndex;
     std::vector<MapPoint::ptr> lastMps;
@@ -362,11 +374,13 @@ int LoopHandler::trackLastFrame() {
     if (n == 0) return 0;  // an empty point set: calcOpticalFlowPyrLK returns empty status
     std::vector<float> next(2 * (size_t)n), err(n);
     std::vector<uint8_t> flowStatus(n);
+    const double tl = now_s();
     if (!gpu(yv_calc_optical_flow_pyr_lk(dev_->ctx(), lastFrame_->data.data(), currentFrame_->data.data(),
                                          currentFrame_->rows, currentFrame_->cols, currentFrame_->cols, lastKpt.data(),
                                          n, 11, 3, 30, 0.01, 0.001, next.data(), flowStatus.data(), err.data()),
              "calcOpticalFlowPyrLK"))
         return 0;
+    prim_.lk += now_s() - tl;
     int goodFeatures = 0;
     for (int i = 0; i < n; ++i) {
         if (flowStatus[i] != 1) continue;
@@ -399,9 +413,11 @@ int LoopHandler::optimizePoseOnly() {
     std::vector<uint8_t> outlier(n > 0 ? n : 1);
     int inliers = 0;
     SE3 pose = currentFrame_->pose;
+    const double t0 = now_s();
     if (!gpu(yv_pose_lm(dev_->ctx(), X.data(), uv.data(), n, K_, pose.d, outlier.data(), &inliers),
              "optimizePoseOnly"))
         return 0;
+    prim_.pose_lm += now_s() - t0;
     currentFrame_->pose = pose;
     for (int k = 0; k < n; ++k) {
         Feature& f = currentFrame_->features[fi[k]];
@@ -414,9 +430,11 @@ int LoopHandler::optimizePoseOnly() {
 // :168-296
 bool LoopHandler::reinitialize() {
     currentFrame_->features.clear();
+    const double t0 = now_s();
     std::vector<Matches> matches = brief_->matchFeatures(*lastFrame_, *currentFrame_);
     std::vector<Matches> filterMatches;
     brief_->removeOutliers(matches, filterMatches, 20);
+    prim_.match += now_s() - t0;
     if (!gpu(brief_->status(), "matchFeatures / removeOutliers")) return false;
     ev_.matches_kept = (int)filterMatches.size();
     double F[9];
@@ -443,12 +461,103 @@ void LoopHandler::runVO(int max_frames) {
     }
 }
 
-void LoopHandler::setPipeline(int depth, int device, const std::vector<int8_t>& briefOffsets, int readers) {
+void LoopHandler::setPipeline(int depth, int device, const std::vector<int8_t>& briefOffsets, int readers,
+                              int gpu_batch) {
     pipeline_readers_ = readers;
+    pipeline_gpu_batch_ = gpu_batch > 0 ? gpu_batch : 0;
     pipeline_depth_ = depth > 0 ? depth : 0;
     pipeline_device_ = device;
     pipeline_offsets_ = briefOffsets;
 }
+
+namespace {
+
+// The pipelined worker's GPU look-ahead: frames [first, first + n) of the left train read by host threads, inflated +
+// unfiltered on the GPU (yv_seq_upload_gpu, the device half of cv::imread), detected and described by one yv_batch run
+// over the decoded device images (no match pairs), then the images and keypoint records copied back for the frames.
+class GpuLookahead {
+public:
+    GpuLookahead(yv_ctx* ctx, const std::string& seq_dir, int batch) : ctx_(ctx), B_(batch) {
+        st_ = yv_seq_open(seq_dir.c_str(), 0, &seq_);
+        if (st_ == YV_OK) st_ = yv_seq_size(seq_, &H_, &W_);
+        const size_t img = (size_t)H_ * W_;
+        if (st_ == YV_OK) st_ = yv_pngdec_create(ctx_, B_, H_, W_, &dec_);
+        if (st_ == YV_OK) st_ = yv_batch_create(ctx_, B_, H_, W_, kMaxKp, 1, &batch_);
+        if (st_ == YV_OK) st_ = yv_batch_view_get(batch_, &view_);
+        if (st_ == YV_OK) st_ = yv_device_alloc(ctx_, B_ * img, &d_img_);
+        if (st_ == YV_OK) st_ = yv_host_alloc(ctx_, B_ * img, reinterpret_cast<void**>(&h_img_));
+        if (st_ == YV_OK) st_ = yv_host_alloc(ctx_, (size_t)B_ * kMaxKp * sizeof(KeyPoint), reinterpret_cast<void**>(&h_kp_));
+        if (st_ == YV_OK) st_ = yv_host_alloc(ctx_, sizeof(int32_t) * (B_ + 1), reinterpret_cast<void**>(&h_cnt_));
+    }
+    ~GpuLookahead() {
+        if (dec_) yv_pngdec_destroy(dec_);
+        if (batch_) yv_batch_destroy(batch_);
+        if (seq_) yv_seq_close(seq_);
+        yv_device_free(ctx_, d_img_);
+        yv_host_free(ctx_, h_img_);
+        yv_host_free(ctx_, h_kp_);
+        yv_host_free(ctx_, h_cnt_);
+    }
+    int status() const { return st_; }
+    int H() const { return H_; }
+    int W() const { return W_; }
+
+    // enqueue frames [first, first + n): the file reads on `readers` threads now, decode + detect + describe on the
+    // context stream (returns before the kernels finish)
+    int launch(int first, int n, int readers) {
+        first_ = first;
+        n_ = n;
+        if (n <= 0) return YV_OK;
+        int st = yv_seq_upload_gpu(seq_, dec_, first, n, static_cast<uint8_t*>(d_img_), (int64_t)H_ * W_, readers,
+                                   nullptr);
+        if (st == YV_OK)
+            st = yv_batch_run(batch_, static_cast<const uint8_t*>(d_img_), n, W_, (int64_t)H_ * W_, 20, -1, nullptr);
+        return st;
+    }
+    // waits for the launched frames; frames[i] = frame first + i, or nullptr when its PNG failed a check (the reference's
+    // cv::imread returns an empty Mat: the loop ends there)
+    int collect(std::vector<Frame::ptr>& frames) {
+        frames.assign((size_t)n_, nullptr);
+        const int n = n_;
+        n_ = 0;  // collected once: a further collect without a launch returns no frames (the end of the train)
+        if (n <= 0) return YV_OK;
+        std::vector<int32_t> codes((size_t)B_);
+        int bad = 0;
+        int st = yv_pngdec_status(dec_, codes.data(), &bad);
+        const size_t img = (size_t)H_ * W_;
+        if (st == YV_OK) st = yv_download(ctx_, h_cnt_, view_.kp_count, sizeof(int32_t) * n);
+        if (st == YV_OK) st = yv_download(ctx_, h_kp_, view_.keypoints, sizeof(KeyPoint) * (size_t)n * kMaxKp);
+        if (st == YV_OK) st = yv_download(ctx_, h_img_, d_img_, img * n);
+        if (st != YV_OK) return st;
+        for (int i = 0; i < n; ++i) {
+            if (codes[(size_t)i] != 0) break;
+            auto f = std::make_shared<Frame>();
+            f->rows = H_;
+            f->cols = W_;
+            f->data.assign(h_img_ + img * i, h_img_ + img * (i + 1));
+            const int nk = h_cnt_[i];
+            if (nk == 0) std::cout << "No corners found" << std::endl;  // src/FastDetector.cc:364-366
+            f->keypoints.assign(h_kp_ + (size_t)i * kMaxKp, h_kp_ + (size_t)i * kMaxKp + nk);
+            frames[(size_t)i] = f;
+        }
+        return YV_OK;
+    }
+
+private:
+    static constexpr int kMaxKp = 2000;  // FastDetector's top-2000 (include/FastDetector.hpp:36)
+    yv_ctx* ctx_;
+    int B_, H_ = 0, W_ = 0, st_ = YV_OK, first_ = 0, n_ = 0;
+    yv_seq* seq_ = nullptr;
+    yv_pngdec* dec_ = nullptr;
+    yv_batch* batch_ = nullptr;
+    yv_batch_view view_{};
+    void* d_img_ = nullptr;
+    uint8_t* h_img_ = nullptr;
+    KeyPoint* h_kp_ = nullptr;
+    int32_t* h_cnt_ = nullptr;
+};
+
+}  // namespace
 
 // takeVOStep split over two threads: the worker runs getNextFrame + insertFrameFeatures on its own context for
 // frame k + 1 while this thread runs addFrame(frame k).  Frames leave the worker in path-train order, so ids,
@@ -482,6 +591,70 @@ void LoopHandler::runVOPipelined(int max_frames) {
         int produced = 0;
         const size_t n_train = leftPathTrain.size();
         const size_t limit = max_frames < 0 ? n_train : std::min(n_train, train_it_ + (size_t)max_frames);
+        auto push = [&](Item&& it) -> bool {  // false: the tracking thread stopped the pipeline
+            std::unique_lock<std::mutex> lk(mu);
+            cv_put.wait(lk, [&]() { return stop || q.size() < depth; });
+            if (stop) return false;
+            q.push_back(std::move(it));
+            lk.unlock();
+            cv_get.notify_one();
+            return true;
+        };
+        if (pipeline_gpu_batch_ > 0) {
+            // GPU look-ahead: batch j + 1 is read and enqueued on the GPU before batch j's frames are handed over
+            std::unique_ptr<GpuLookahead> la;
+            if (st == YV_OK) {
+                la = std::make_unique<GpuLookahead>(wdev.ctx(), basePath_ + seqNo_, pipeline_gpu_batch_);
+                st = la->status();  // (the worker context's BRIEF offsets were set above)
+            }
+            size_t next = train_it_;
+            auto launch_next = [&]() -> int {
+                const int n = (int)std::min((size_t)pipeline_gpu_batch_, limit - next);
+                const double t0 = now_s();
+                const int s = la->launch((int)next, n, readers);
+                worker_read += now_s() - t0;
+                next += (size_t)n;
+                return s;
+            };
+            if (st == YV_OK) st = launch_next();
+            bool done = false;
+            while (!done) {
+                std::vector<Frame::ptr> frames;
+                if (st == YV_OK) {
+                    const double t0 = now_s();
+                    st = la->collect(frames);
+                    worker_features += now_s() - t0;
+                }
+                if (st == YV_OK && next < limit) st = launch_next();
+                bool ended = st != YV_OK || frames.empty();
+                for (auto& f : frames) {
+                    Item it;
+                    it.status = st;
+                    if (f) {
+                        it.index = (int)train_it_;
+                        train_it_++;
+                        f->frameID = Frame::createFrameID();
+                        it.frame = f;
+                    }
+                    const bool last = !it.frame;
+                    if (!push(std::move(it))) {
+                        done = true;
+                        break;
+                    }
+                    if (last) {
+                        done = true;
+                        break;
+                    }
+                }
+                if (!done && ended) {
+                    Item it;
+                    it.status = st;
+                    push(std::move(it));
+                    done = true;
+                }
+            }
+            return;
+        }
         std::deque<std::future<Frame::ptr>> ahead;  // decodes of frames next_read - ahead.size() .. next_read - 1
         size_t next_read = train_it_;
         auto refill = [&]() {

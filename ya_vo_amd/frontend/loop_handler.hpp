@@ -117,7 +117,12 @@ public:
     // queue between the two holds at most `depth` frames.  Every result is the serial loop's: same frames, same
     // ids, same kernels, only earlier.  BRIEF's offsets must be given here (they are per context).  `readers` frames
     // are read and PNG-decoded ahead on threads of their own.
-    void setPipeline(int depth, int device, const std::vector<int8_t>& briefOffsets, int readers = 4);
+    // gpu_batch > 0: the worker decodes the look-ahead frames on the GPU instead (yv_pngdec: the files are read by
+    // `readers` host threads, inflated and unfiltered by kernels), gpu_batch frames per decode, and detects / describes
+    // them in one yv_batch run on the decoded device images (the same kernels as yv_detect / yv_describe); the next
+    // batch is decoded while this one's frames are handed over.
+    void setPipeline(int depth, int device, const std::vector<int8_t>& briefOffsets, int readers = 4,
+                     int gpu_batch = 0);
     static Frame::ptr readFrame(const std::string& path);  // cv::imread(path, IMREAD_GRAYSCALE)
 
     // every added frame's pose (T_cw, SE3d::data()) in order, and what happened to it
@@ -133,6 +138,10 @@ public:
     double t_features = 0, t_init = 0, t_track = 0, t_reinit = 0;  // seconds, summed
     double t_read = 0;  // getNextFrame (file read + PNG decode), summed; pipelined: waiting for the decode pool
     double t_wait = 0;  // pipelined: the tracking thread waiting for the worker's next frame
+    struct PrimitiveTimes {  // seconds per host-pointer primitive of the tracking thread, summed
+        double world2camera = 0, lk = 0, pose_lm = 0, match = 0, f_ransac = 0, find_essential = 0, recover_pose = 0;
+    };
+    const PrimitiveTimes& primitiveTimes() const { return prim_; }
 
 private:
     std::string seqNo_, leftImagesPath_, rightImagesPath_, basePath_;
@@ -152,8 +161,9 @@ private:
     FrameEvent ev_;
     std::mt19937 ransac_rng_{0};  // getFRANSAC's sample draws (the reference seeds from std::random_device)
     int gpu_status_ = YV_OK;
+    PrimitiveTimes prim_;
 
-    int pipeline_depth_ = 0, pipeline_device_ = 0, pipeline_readers_ = 4;
+    int pipeline_depth_ = 0, pipeline_device_ = 0, pipeline_readers_ = 4, pipeline_gpu_batch_ = 0;
     std::vector<int8_t> pipeline_offsets_;
 
     bool gpu(int st, const char* what);

@@ -3,7 +3,7 @@
 //
 // usage: yavo_loop_handler CONFIG.json [--frames N] [--poses KITTI.txt] [--poses-bin POSES.bin]
 //                                      [--events EVENTS.bin] [--offsets-seed S] [--device D] [--check-config]
-//                                      [--pipeline DEPTH] [--readers N]
+//                                      [--pipeline DEPTH] [--readers N] [--gpu-decode B]
 //   --check-config   no GPU: print the parsed configuration, the path train and the first frames as JSON (the
 //                    reference's LoopHandlerTest cases: stereoStatus, getSeqNo, getLeftImagesPath,
 //                    getLeftTrainLength, getNextFrame dimensions, frame ids)
@@ -41,7 +41,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     const std::string config = argv[1];
-    int frames = -1, device = 0, pipeline = 0, readers = 4;
+    int frames = -1, device = 0, pipeline = 0, readers = 4, gpu_decode = 0;
     uint32_t seed = 42;
     bool check = false;
     std::string poses_txt, poses_bin, events_bin;
@@ -56,6 +56,7 @@ int main(int argc, char** argv) {
         else if (a == "--device") device = std::atoi(next().c_str());
         else if (a == "--pipeline") pipeline = std::atoi(next().c_str());
         else if (a == "--readers") readers = std::atoi(next().c_str());
+        else if (a == "--gpu-decode") gpu_decode = std::atoi(next().c_str());
         else if (a == "--check-config") check = true;
         else {
             std::cerr << "unknown option " << a << std::endl;
@@ -96,7 +97,7 @@ int main(int argc, char** argv) {
     Brief offsets_setter(dev, 256);
     const std::vector<int8_t> offsets = Brief::preComputeOffsets(seed);
     if (!offsets_setter.setOffsets(offsets)) return 3;
-    if (pipeline > 0) lh.setPipeline(pipeline, device, offsets, readers);
+    if (pipeline > 0) lh.setPipeline(pipeline, device, offsets, readers, gpu_decode);
 
     const auto t0 = std::chrono::steady_clock::now();
     lh.runVO(frames);
@@ -134,7 +135,13 @@ int main(int argc, char** argv) {
               << ", \"seconds_features\": " << lh.t_features << ", \"seconds_init\": " << lh.t_init
               << ", \"seconds_track\": " << lh.t_track << ", \"seconds_reinit\": " << lh.t_reinit
               << ", \"seconds_read\": " << lh.t_read << ", \"seconds_wait\": " << lh.t_wait
-              << ", \"pipeline\": " << pipeline << ", \"readers\": " << (pipeline > 0 ? readers : 0) << "}"
+              << ", \"pipeline\": " << pipeline << ", \"readers\": " << (pipeline > 0 ? readers : 0)
+              << ", \"gpu_decode_batch\": " << (pipeline > 0 ? gpu_decode : 0) << ", \"primitives_s\": {"
+              << "\"world2camera\": " << lh.primitiveTimes().world2camera << ", \"lk\": " << lh.primitiveTimes().lk
+              << ", \"pose_lm\": " << lh.primitiveTimes().pose_lm << ", \"match_reinit\": " << lh.primitiveTimes().match
+              << ", \"f_ransac\": " << lh.primitiveTimes().f_ransac
+              << ", \"find_essential\": " << lh.primitiveTimes().find_essential
+              << ", \"recover_pose\": " << lh.primitiveTimes().recover_pose << "}}"
               << std::endl;
     return 0;
 }
