@@ -74,3 +74,12 @@ def test_oracle_sequence_follows_ground_truth(oracle, offsets):
     gt = ground_truth(n, scene.K_KITTI)
     assert rmse_translation(traj, gt) < 0.02
     assert sum(len(r.edge) for r in records.values()) > 1000
+
+
+def test_device_window_cap_is_checked_up_front():
+    """chunk + n_fixed above the device window's pose capacity fails in the constructor with a clear message, before
+    any device work (it used to fail at the first BA with YV_ERR_INVALID)."""
+    import pytest
+    from ya_vo_amd import sequence
+    with pytest.raises(ValueError, match="at most 128 poses"):
+        sequence.SequenceFrontend(None, 127, np.eye(3), np.array([0, 0, 0, 1, 0, -0.54, 0.0]), n_fixed=2)

@@ -252,92 +252,101 @@ __device__ void em_det_poly(const double* B, double* c) {
     for (int k = 0; k < 11; ++k) c[k] = t0[k] - t1[k] + t2[k];
 }
 
-// cv::solvePoly (Durand-Kerner) of degree NN (the coefficients above NN were trimmed); rre / rim [10]
+// cv::solvePoly's Durand-Kerner sweep with one root per lane of a 10-lane group (lane r owns root r; group lanes
+// base .. base + 9, all active whenever this runs).  The same operations in the same order as solvePoly: OpenCV's
+// sweep is Gauss-Seidel -- root i's denominator prod_{j != i} (x_i - x_j) takes the roots j < i already updated in
+// this sweep and j > i as they were -- so per sweep every lane first gathers the group's old roots and evaluates its
+// Horner value (independent of the other roots), then for k = 0 .. NN-1: lane k multiplies its denominator by its
+// suffix terms j > k (old values, in order), divides and updates; its new root is broadcast and every lane r > k
+// multiplies its running denominator by (x_r - x_k^new): solvePoly's left-to-right product, factor by factor.
+// A wave issues ~650 instead of ~1750 FP64 instructions per sweep (the ten roots' Horner chains and the tail of the
+// products run side by side), and six hypotheses share a wave.  rre / rim: this lane's root (0 past NN).  Returns
+// the sweeps run.
 template <int NN>
-__device__ int dk_solve(const double* c, double* rre, double* rim) {
-    double cr[NN + 1], xr[NN], xi[NN];
+__device__ int dk_group(const double* c, int r, int base, uint64_t gmask, double& rre, double& rim) {
+    double cr[NN + 1];
 #pragma unroll
     for (int i = 0; i <= NN; ++i) cr[i] = c[i];
+    // initial roots (1 + i)^r, the same products as solvePoly's sequence
+    double xr = 1, xi = 0;
     {
         double pr = 1, pi = 0;
         const double qr = 1, qi = 1;
 #pragma unroll
         for (int i = 0; i < NN; i++) {
-            xr[i] = pr;
-            xi[i] = pi;
+            if (i == r) {
+                xr = pr;
+                xi = pi;
+            }
             const double tr = pr * qr - pi * qi, ti = pr * qi + pi * qr;
             pr = tr;
             pi = ti;
         }
     }
-    // A sweep that leaves every root bit-identical is a fixed point: the next sweep computes exactly the same values
-    // from the same state (maxDiff is recomputed from zero each sweep and nothing else carries over), so every sweep
-    // up to OpenCV's 300 would too.  Stopping there gives the 300-sweep result bit for bit.
+    const bool own = r < NN;
     int sweeps = 0;
     for (int iter = 0; iter < 300; iter++) {
         ++sweeps;
-        double maxDiff = 0;
+        double ox[NN], oy[NN];
+#pragma unroll
+        for (int j = 0; j < NN; ++j) {
+            ox[j] = __shfl(xr, base + j, 64);
+            oy[j] = __shfl(xi, base + j, 64);
+        }
+        const double pr = xr, pi = xi;
+        double nr = cr[NN], ni = 0.0, dr = cr[NN], di = 0.0;
+#pragma unroll
+        for (int j = 0; j < NN; j++) {
+            const double tr = nr * pr - ni * pi, ti = nr * pi + ni * pr;
+            nr = tr + cr[NN - j - 1];
+            ni = ti + 0.0;
+        }
         bool moved = false;
+        double an2 = 0;
 #pragma unroll
-        for (int i = 0; i < NN; i++) {
-            const double pr = xr[i], pi = xi[i];
-            double nr = cr[NN], ni = 0.0, dr = cr[NN], di = 0.0;
+        for (int k = 0; k < NN; ++k) {
+            if (r == k) {
 #pragma unroll
-            for (int j = 0; j < NN; j++) {
-                const double tr = nr * pr - ni * pi, ti = nr * pi + ni * pr;
-                nr = tr + cr[NN - j - 1];
-                ni = ti + 0.0;
-                if (j != i && (pr != xr[j] || pi != xi[j])) {
-                    const double sr = pr - xr[j], si = pi - xi[j];
+                for (int j = k + 1; j < NN; ++j) {
+                    const bool same = pr == ox[j] && pi == oy[j];
+                    const double sr = pr - ox[j], si = pi - oy[j];
                     const double ur = dr * sr - di * si, ui = dr * si + di * sr;
-                    dr = ur;
-                    di = ui;
+                    dr = same ? dr : ur;
+                    di = same ? di : ui;
                 }
+                const double t = 1. / (dr * dr + di * di);
+                const double qr = (nr * dr + ni * di) * t, qi = (-nr * di + ni * dr) * t;
+                xr = pr - qr;
+                xi = pi - qi;
+                moved = __double_as_longlong(xr) != __double_as_longlong(pr) ||
+                        __double_as_longlong(xi) != __double_as_longlong(pi);
+                an2 = qr * qr + qi * qi;
             }
-            const double t = 1. / (dr * dr + di * di);
-            const double qr = (nr * dr + ni * di) * t, qi = (-nr * di + ni * dr) * t;
-            xr[i] = pr - qr;
-            xi[i] = pi - qi;
-            moved |= __double_as_longlong(xr[i]) != __double_as_longlong(pr) ||
-                     __double_as_longlong(xi[i]) != __double_as_longlong(pi);
-            const double an = sqrt(qr * qr + qi * qi);
-            maxDiff = maxDiff < an ? an : maxDiff;
+            const double kr = __shfl(xr, base + k, 64), ki = __shfl(xi, base + k, 64);
+            if (r > k && own) {
+                const bool same = pr == kr && pi == ki;
+                const double sr = pr - kr, si = pi - ki;
+                const double ur = dr * sr - di * si, ui = dr * si + di * sr;
+                dr = same ? dr : ur;
+                di = same ? di : ui;
+            }
         }
-        if (maxDiff <= 0 || !moved) break;
+        // OpenCV stops when the largest |update| is 0 (an2 > 0 iff |q| > 0; NaN compares false); a sweep that moved no
+        // root is a fixed point (every later sweep repeats it), so stopping there gives the 300-sweep roots too
+        const uint64_t any_moved = __ballot(own && moved) & gmask, any_pos = __ballot(own && an2 > 0) & gmask;
+        if (!any_moved || !any_pos) break;
     }
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-        if (i < NN) {
-            rre[i] = xr[i];
-            rim[i] = fabs(xi[i]) < 1e-100 ? 0.0 : xi[i];
-        } else {
-            rre[i] = 0.0;
-            rim[i] = 0.0;
-        }
-    }
+    rre = own ? xr : 0.0;
+    rim = own ? (fabs(xi) < 1e-100 ? 0.0 : xi) : 0.0;
     return sweeps;
 }
 
-__device__ int solve_poly10(const double* c, double* rre, double* rim) {
-    int n = 10;
-    for (; n > 1; n--)
-        if (fabs(c[n]) + fabs(0.0) > DBL_EPSILON) break;
-    switch (n) {
-        case 10: return dk_solve<10>(c, rre, rim);
-        case 9: return dk_solve<9>(c, rre, rim);
-        case 8: return dk_solve<8>(c, rre, rim);
-        case 7: return dk_solve<7>(c, rre, rim);
-        case 6: return dk_solve<6>(c, rre, rim);
-        case 5: return dk_solve<5>(c, rre, rim);
-        case 4: return dk_solve<4>(c, rre, rim);
-        case 3: return dk_solve<3>(c, rre, rim);
-        case 2: return dk_solve<2>(c, rre, rim);
-        default: return dk_solve<1>(c, rre, rim);
-    }
-}
-
-// EMEstimatorCallback::runKernel (oracle or_em_kernel); models [10][9]; returns the count
-__device__ int em_models(const double* q1, const double* q2, double* models, int prof_k = 1 << 30) {
+// EMEstimatorCallback::runKernel (oracle or_em_kernel) on a 10-lane group (lane r of the group at base, mask gmask):
+// every lane forms the null space, the constraint matrix, its LU inverse and det B(z) redundantly, the
+// Durand-Kerner roots are one per lane (dk_group), and lane r then runs the reference loop's iteration i = r (solveZ
+// and the model) -- the models land in root order by a ballot prefix.  models [10][9]; returns the count (every lane).
+__device__ int em_models(const double* q1, const double* q2, double* models, int r, int base, uint64_t gmask,
+                         int prof_k = 1 << 30) {
     EP_DECL
     double At[81], Vt5[25], W[5];
 #pragma unroll
@@ -384,16 +393,35 @@ __device__ int em_models(const double* q1, const double* q2, double* models, int
         for (int k = 0; k < 13; ++k) B[i * 13 + k] = r1[k] - r2[k];
     }
     EP_MARK(2);
-    double c[11], rre[10], rim[10];
+    double c[11];
     em_det_poly(B, c);
     EP_MARK(3);
-    const int sweeps = solve_poly10(c, rre, rim);
+    int nn = 10;
+    for (; nn > 1; nn--)
+        if (fabs(c[nn]) + fabs(0.0) > DBL_EPSILON) break;  // solvePoly trims the vanishing leading coefficients
+    double rre = 0, rim = 0;
+    int sweeps = 0;
+    switch (nn) {  // group-uniform
+        case 10: sweeps = dk_group<10>(c, r, base, gmask, rre, rim); break;
+        case 9: sweeps = dk_group<9>(c, r, base, gmask, rre, rim); break;
+        case 8: sweeps = dk_group<8>(c, r, base, gmask, rre, rim); break;
+        case 7: sweeps = dk_group<7>(c, r, base, gmask, rre, rim); break;
+        case 6: sweeps = dk_group<6>(c, r, base, gmask, rre, rim); break;
+        case 5: sweeps = dk_group<5>(c, r, base, gmask, rre, rim); break;
+        case 4: sweeps = dk_group<4>(c, r, base, gmask, rre, rim); break;
+        case 3: sweeps = dk_group<3>(c, r, base, gmask, rre, rim); break;
+        case 2: sweeps = dk_group<2>(c, r, base, gmask, rre, rim); break;
+        default: sweeps = dk_group<1>(c, r, base, gmask, rre, rim); break;
+    }
     EP_MARK(4);
     EP_SET(7, sweeps);
-    int count = 0;
-    for (int i = 0; i < 10; i++) {
-        if (fabs(rim[i]) > 1e-10) continue;
-        const double z1 = rre[i], z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
+    (void)sweeps;
+    // the reference loop's iteration i = r: a real root (|Im| <= 1e-10) and a non-degenerate solveZ give a model
+    bool valid = false;
+    double ev[9];
+    do {
+        if (fabs(rim) > 1e-10) break;
+        const double z1 = rre, z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
         double bz[9];
 #pragma unroll
         for (int j = 0; j < 3; j++) {
@@ -410,9 +438,8 @@ __device__ int em_models(const double* q1, const double* q2, double* models, int
             for (int b = 0; b < 3; ++b) A3[a * 3 + b] = bz[b * 3 + a];
         cv_jacobi_svd<3>(A3, w3, V3);
         const double* xy1 = V3 + 6;
-        if (fabs(xy1[2]) < 1e-10) continue;
+        if (fabs(xy1[2]) < 1e-10) break;
         const double xs = xy1[0] / xy1[2], ys = xy1[1] / xy1[2], zs = z1;
-        double ev[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) ev[k] = ((EE[0 * 9 + k] * xs + EE[1 * 9 + k] * ys) + EE[2 * 9 + k] * zs) + EE[3 * 9 + k];
         double s2 = 0;
@@ -421,13 +448,20 @@ __device__ int em_models(const double* q1, const double* q2, double* models, int
         s2 += ev[8] * ev[8];
         const double sc = 1. / sqrt(s2);
 #pragma unroll
-        for (int k = 0; k < 9; ++k) models[count * 9 + k] = ev[k] * sc;
-        count++;
+        for (int k = 0; k < 9; ++k) ev[k] = ev[k] * sc;
+        valid = true;
+    } while (false);
+    const uint64_t vb = __ballot(valid) & gmask;
+    const int lane = (int)(threadIdx.x & 63);
+    const int pos = __popcll(vb & ((1ull << lane) - 1ull));
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) models[pos * 9 + k] = ev[k];
     }
     EP_MARK(5);
-    EP_STORE(prof_k);
+    if (r == 0) EP_STORE(prof_k);
     (void)prof_k;
-    return count;
+    return __popcll(vb);
 }
 
 // Sampson error (EMEstimatorCallback::computeError) <= t
@@ -521,20 +555,25 @@ __global__ void ess_subsets_kernel(int n_pairs, EssParams P, int chunk0, int ite
     st[7] = (int32_t)(uint32_t)(rng >> 32);
 }
 
-// 16 lanes per workgroup: the solver is a latency-bound dependent chain (Durand-Kerner), so a round spreads over 4x
-// the waves (SIMDs) at the same instruction count per wave
-constexpr int kModelLanes = 16;
+// A 64-lane workgroup holds six RANSAC iterations, one per 10-lane group (lanes 60..63 idle): the per-hypothesis
+// solver runs redundantly on its group's lanes except the Durand-Kerner sweep and solveZ, which run one root per lane
+constexpr int kModelGroup = 10;
+constexpr int kModelIters = 6;  // iterations per workgroup
 
-__global__ __launch_bounds__(kModelLanes) void ess_models_kernel(EssParams P, int chunk0) {
+__global__ __launch_bounds__(64) void ess_models_kernel(EssParams P, int chunk0) {
     const int pair = blockIdx.y;
-    const int k = blockIdx.x * kModelLanes + threadIdx.x;
+    const int lane = threadIdx.x;
+    const int g = lane / kModelGroup, r = lane - g * kModelGroup, base = g * kModelGroup;
+    const int k = blockIdx.x * kModelIters + g;
+    if (g >= kModelIters || k >= P.chunk) return;  // whole groups leave together
+    const uint64_t gmask = ((1ull << kModelGroup) - 1ull) << base;
     const int it = chunk0 + k;
     const int32_t* st = P.state + 8 * pair;
     const int n = st[5];
     int32_t* nmod = P.nmod + pair * P.chunk + k;
     const bool single = n == 5;
     if (n < 5 || it >= st[0] || (single && it > 0)) {
-        *nmod = 0;
+        if (r == 0) *nmod = 0;
         return;
     }
     const double* m1 = P.m1 + 2 * (int64_t)pair * P.max_points;
@@ -550,7 +589,8 @@ __global__ __launch_bounds__(kModelLanes) void ess_models_kernel(EssParams P, in
         q2[2 * i + 1] = m2[2 * j + 1];
     }
     double* out = P.models + ((int64_t)pair * P.chunk + k) * 90;
-    *nmod = em_models(q1, q2, out, pair == 0 ? it : 1 << 30);
+    const int cnt = em_models(q1, q2, out, r, base, gmask, pair == 0 ? it : 1 << 30);
+    if (r == 0) *nmod = cnt;
 }
 
 __global__ __launch_bounds__(256) void ess_score_kernel(EssParams P, int chunk0, float t) {
@@ -820,7 +860,7 @@ void launch_find_essential(const EssParams& P, const EssRun& r, const float* pts
     const float t = (float)(thr * thr);
     for (int c0 = 0; c0 < iters; c0 += P.chunk) {
         hipLaunchKernelGGL(ess::ess_subsets_kernel, dim3((n_pairs + 63) / 64), dim3(64), 0, s, n_pairs, P, c0, iters);
-        hipLaunchKernelGGL(ess::ess_models_kernel, dim3(P.chunk / ess::kModelLanes, n_pairs), dim3(ess::kModelLanes),
+        hipLaunchKernelGGL(ess::ess_models_kernel, dim3((P.chunk + ess::kModelIters - 1) / ess::kModelIters, n_pairs), dim3(64),
                            0, s, P, c0);
         hipLaunchKernelGGL(ess::ess_score_kernel, dim3(P.chunk, n_pairs), dim3(256), 0, s, P, c0, t);
         hipLaunchKernelGGL(ess::ess_select_kernel, dim3((n_pairs + 63) / 64), dim3(64), 0, s, P, n_pairs, c0, r.prob);

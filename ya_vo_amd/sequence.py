@@ -108,6 +108,10 @@ def apply_window(records: Dict[int, FrameRecord], frames: List[int], poses: np.n
             base += n
 
 
+# poses of one device BA window (yv_ba_window_solve, yavo_ba.hip kWinMaxPoses)
+WINDOW_MAX_POSES = 128
+
+
 class SequenceFrontend:
     """The device front end over a stereo sequence in chunks of `chunk` frames (module docstring)."""
 
@@ -121,6 +125,9 @@ class SequenceFrontend:
         if chunk < 2 or n_fixed < 1:
             raise ValueError("bad chunk / n_fixed")
         window = chunk + n_fixed
+        if device_window and window > WINDOW_MAX_POSES:
+            raise ValueError(f"the device BA window holds at most {WINDOW_MAX_POSES} poses (chunk + n_fixed = {window}); "
+                             "use a smaller chunk or device_window=False")
         self.ctx, self.chunk, self.H, self.W, self.max_kp = ctx, chunk, H, W, max_kp
         self.K = np.asarray(K, np.float64)
         self.window, self.n_fixed, self.ba_iters, self.match_thr = window, n_fixed, ba_iters, match_thr
