@@ -56,9 +56,12 @@ int yv_pose_lm_batch(struct yv_ctx* ctx, int n_problems, const int32_t* d_offset
                      const double* d_uv, const double* d_K, double* d_poses, uint8_t* d_outlier,
                      int32_t* d_inliers, void* stream);
 /* The order in which the pose-LM kernel sums over edges, as the oracle's sum_mode (oracle/yavo_oracle.h:
- * 4 / 5 / 6 = 64- / 128- / 256-thread workgroups; the library runs 256). Results are bit-identical
- * to the oracle in that order and within 1e-9 of the reference's sequential order. */
+ * 4 / 5 / 6 / 7 = 64- / 128- / 256- / 512-thread workgroups). yv_lm_sum_mode: the batch's track LM (256 threads).
+ * yv_pose_lm_sum_mode(n): yv_pose_lm (n = 1) and yv_pose_lm_batch with n problems (512 threads up to 256 problems,
+ * where the call's latency is set by one problem per CU; 256 above). Results are bit-identical to the oracle in
+ * that order and within 1e-9 of the reference's sequential order. */
 int yv_lm_sum_mode(void);
+int yv_pose_lm_sum_mode(int n_problems);
 int yv_pose_gn_batch(struct yv_ctx* ctx, int n_problems, const int32_t* d_offsets, const double* d_X,
                      const double* d_uv, const double* d_K, double* d_poses, int32_t* d_iterations, void* stream);
 /* F-RANSAC over n_lists match lists: list l = d_matches + l*list_stride, d_counts[l] entries, samples

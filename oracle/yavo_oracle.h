@@ -141,7 +141,8 @@ void or_world2camera(const double* X, int n, const double* T, const double* K, d
 int or_ldlt6_solve(const double* H, const double* b, double* x, int variant);
 /* LoopHandler::optimizePoseOnly (src/LoopHandler.cc:730-861); returns inliers.  sum_mode 0 = sequential
  * edge sums (reference), 1 = 256-thread tree (GN kernel), 2 / 3 = 512- / 256-thread segmented (earlier LM
- * kernels), 4 / 5 / 6 = 64- / 128- / 256-thread wave trees (the LM kernel: yv_lm_sum_mode()). */
+ * kernels), 4 / 5 / 6 / 7 = 64- / 128- / 256- / 512-thread wave trees (the LM kernel: yv_lm_sum_mode(),
+ * yv_pose_lm_sum_mode(n)). */
 int or_pose_lm(const double* X, const double* uv, int n, const double* K, double* pose, uint8_t* outlier,
                int sum_mode);
 /* bundleAdjustmentGaussNewton (src/test.cc:172-244); returns accepted iterations (GPU order: sum_mode 1). */

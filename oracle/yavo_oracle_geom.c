@@ -782,7 +782,7 @@ static void edge_jacobian(const double* T, const double* K, const double* X, dou
  * partial.  Mode 1 then sums the pairwise tree p[t] += p[t + off] for off = NT/2 .. 1.  Mode 2 (512 threads)
  * and mode 3 (256 threads, the pose-LM kernel) halve once (p[t] += p[t + NT/2]), sum each of 16 runs of
  * NT/32 partials left to right (q[s] = p[Rs] + p[Rs+1] + ... , R = NT/32) and finish with the tree
- * q[s] += q[s + off], off = 8, 4, 2, 1.  Modes 4, 5, 6 (the pose-LM kernel at 64, 128, 256 threads): the halving
+ * q[s] += q[s + off], off = 8, 4, 2, 1.  Modes 4, 5, 6, 7 (the pose-LM kernel at 64, 128, 256, 512 threads): the halving
  * tree p[l] += p[l + off], off = 32 .. 1, inside each 64-thread wave, then the wave totals left to right. */
 #define OR_NT_MAX 1024
 typedef struct { int mode, nt; double part[OR_NT_MAX]; } or_sum;

@@ -139,7 +139,7 @@ class LoopChain:
         fi = [i for i, f in enumerate(self.curr.features) if f[2] is not None]
         X = np.array([self.mps[self.curr.features[i][2]] for i in fi]).reshape(-1, 3)
         uv = np.array([(self.curr.features[i][0], self.curr.features[i][1]) for i in fi], np.float64).reshape(-1, 2)
-        T, out, inl = self.orc.pose_lm(X, uv, self.K, self.curr.pose, lm_sum_mode())
+        T, out, inl = self.orc.pose_lm(X, uv, self.K, self.curr.pose, lm_sum_mode(1))
         self.curr.pose = T
         for k, i in enumerate(fi):
             if out[k]:

@@ -33,8 +33,11 @@ def test_find_essential_host_small(ctx):
     assert not ok and not E.any() and not mask.any()
 
 
-def test_essential_batch_matches_oracle(ctx, oracle):
-    """Lists of different lengths (incl. n < 5, n == 5 and pure noise) in one batched call."""
+@pytest.mark.parametrize("capacity", [8, 9])
+def test_essential_batch_matches_oracle(ctx, oracle, capacity):
+    """Lists of different lengths (incl. n < 5, n == 5 and pure noise) in one batched call.  A workspace of <= 8 lists
+    runs the five-point solver's latency form (10-lane groups, 256-iteration rounds), a larger one the throughput form
+    (one iteration per lane, 64-iteration rounds): both give the oracle's results."""
     import torch
     cases = [(2000, 0.2, 10), (0, 0.0, 11), (4, 0.0, 12), (5, 0.0, 13), (300, 0.5, 14), (150, 1.0, 15), (64, 0.1, 16),
              (1000, 0.0, 17)]
@@ -57,7 +60,7 @@ def test_essential_batch_matches_oracle(ctx, oracle):
     dR = torch.zeros((P, 9), dtype=torch.float64, device=dev)
     dt = torch.zeros((P, 3), dtype=torch.float64, device=dev)
     dgood = torch.zeros(P, dtype=torch.int32, device=dev)
-    es = yv.Essential(ctx, P, stride)
+    es = yv.Essential(ctx, max(P, capacity), stride)
     stream = torch.cuda.Stream()
     with torch.cuda.stream(stream):
         es.find(d1.data_ptr(), d2.data_ptr(), dc.data_ptr(), P, stride, dE.data_ptr(), dfound.data_ptr(),

@@ -11,7 +11,7 @@ from ya_vo_amd import MATCH_DTYPE, scene
 pytestmark = pytest.mark.gpu
 
 POSE_TOL = 1e-9  # |pose_gpu - pose_reference_order| (quaternion + translation), stated in DESIGN.md
-LM_ORDER = yv.lm_sum_mode()  # the pose-LM kernel's edge-sum order (oracle sum_mode 4 / 5 / 6, yv_lm_sum_mode)
+LM_ORDER = yv.lm_sum_mode(1)  # yv_pose_lm's edge-sum order (oracle sum_mode 4 / 5 / 6 / 7, yv_pose_lm_sum_mode)
 GN_ORDER = 1     # the GN kernel's: 256-thread tree
 
 
@@ -133,22 +133,24 @@ def test_pose_lm_batch(ctx, oracle):
     out = d_out.cpu().numpy().astype(bool)
     inl = d_inl.cpu().numpy()
     for i, p in enumerate(probs):
-        oT, oout, oinl = oracle.pose_lm(p[0], p[1], scene.K_KITTI, priors[i], LM_ORDER)
+        oT, oout, oinl = oracle.pose_lm(p[0], p[1], scene.K_KITTI, priors[i], yv.lm_sum_mode(len(probs)))
         assert inl[i] == oinl
         np.testing.assert_array_equal(P[i], oT)
         np.testing.assert_array_equal(out[offs[i]:offs[i + 1]], oout)
 
 
-def test_pose_lm_batch_many_repeatable(ctx, oracle):
-    """512 bench-sized problems (the batch's 512 frames per step), launched three times: every launch bit-identical
-    to the oracle.  Many concurrent 4-wave workgroups expose cross-wave races in the kernel's round control (the
+@pytest.mark.parametrize("count", [256, 512])
+def test_pose_lm_batch_many_repeatable(ctx, oracle, count):
+    """256 / 512 bench-sized problems (the 512- and the 256-thread kernel), launched three times: every launch
+    bit-identical to the oracle.  Many concurrent 4-wave workgroups expose cross-wave races in the kernel's round control (the
     Huber-flag read of the replay decision raced with the next round's reset before it was read ahead of the
     barrier: 3 of 512 bench poses moved by up to 2.6e-4 between steps)."""
     import torch
     from concurrent.futures import ThreadPoolExecutor
     rng = np.random.default_rng(77)
     probs, priors = [], []
-    for i in range(512):
+    mode = yv.lm_sum_mode(count)
+    for i in range(count):
         n = int(rng.integers(1700, 2000))
         noise = float(rng.choice([0.2, 0.5, 0.9, 1.3]))
         p = scene.random_scene(n, seed=1000 + i, noise_px=noise, outlier_frac=float(rng.choice([0.0, 0.02, 0.1])))
@@ -163,7 +165,7 @@ def test_pose_lm_batch_many_repeatable(ctx, oracle):
     d_uv = torch.from_numpy(uvall).to(dev)
     d_K = torch.from_numpy(np.tile(scene.K_KITTI.reshape(1, 9), (len(probs), 1))).to(dev)
     with ThreadPoolExecutor(8) as ex:
-        ref = list(ex.map(lambda i: oracle.pose_lm(probs[i][0], probs[i][1], scene.K_KITTI, priors[i], LM_ORDER),
+        ref = list(ex.map(lambda i: oracle.pose_lm(probs[i][0], probs[i][1], scene.K_KITTI, priors[i], mode),
                           range(len(probs))))
     oP = np.stack([r[0] for r in ref])
     oinl = np.array([r[2] for r in ref])

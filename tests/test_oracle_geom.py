@@ -171,7 +171,7 @@ def test_ldlt6(oracle):
         assert not pos
 
 
-@pytest.mark.parametrize("sum_mode", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("sum_mode", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_pose_lm_noise_free(oracle, sum_mode):
     X, uv, T_true, _ = scene.random_scene(300, seed=9)
     prior = scene.perturb(T_true, np.random.default_rng(1))
@@ -180,7 +180,7 @@ def test_pose_lm_noise_free(oracle, sum_mode):
     np.testing.assert_allclose(scene.project(T, X), uv, atol=1e-6)
 
 
-@pytest.mark.parametrize("order", [3, 4, 5, 6])
+@pytest.mark.parametrize("order", [3, 4, 5, 6, 7])
 def test_pose_lm_outliers_and_sum_orders(oracle, order):
     X, uv, T_true, gross = scene.random_scene(800, seed=10, noise_px=0.5, outlier_frac=0.1)
     prior = scene.perturb(T_true, np.random.default_rng(2))

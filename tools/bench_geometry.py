@@ -112,7 +112,7 @@ def main():
         assert ctx.lib.yv_pose_gn_batch(ctx.handle, L, d_off.data_ptr(), d_X.data_ptr(), d_uv.data_ptr(),
                                         d_K.data_ptr(), d_P.data_ptr(), d_res.data_ptr(), stream) == 0
 
-    for name, fn, cpu_fn in (("pose_lm", lm, lambda: orc.pose_lm(probs[0][0], probs[0][1], scene.K_KITTI, priors[0], yv.lm_sum_mode())),
+    for name, fn, cpu_fn in (("pose_lm", lm, lambda: orc.pose_lm(probs[0][0], probs[0][1], scene.K_KITTI, priors[0], yv.lm_sum_mode(1))),
                              ("pose_gn", gn, lambda: orc.pose_gn(probs[0][0], probs[0][1], scene.K_KITTI, priors[0], 1))):
         ms = timed(fn)
         torch.cuda.synchronize()

@@ -8,6 +8,7 @@ detect + describe run on a worker thread with its own GPU context while frame k 
 must be identical (the pipelined run computes the same things, only earlier).
 
     python tools/bench_loop_handler.py [--frames 200] [--out profiles/r03/loop_handler.json]
+    python tools/bench_loop_handler.py --frames 400 --write-only /tmp/seq   # then: rocprofv3 ... -- BIN /tmp/seq/config.json
 """
 import argparse
 import json
@@ -103,7 +104,12 @@ def main():
     ap.add_argument("--readers", type=int, default=16)
     ap.add_argument("--gpu-batch", type=int, default=32)
     ap.add_argument("--out", default="")
+    ap.add_argument("--write-only", default="", metavar="DIR",
+                    help="write the sequence and its config under DIR and exit (for profiling the binary directly)")
     a = ap.parse_args()
+    if a.write_only:
+        print(write_sequence(a.write_only, a.frames))
+        return
     res = measure(a.frames, a.depth, a.readers, a.gpu_batch)
     s = json.dumps(res, indent=1)
     print(s)

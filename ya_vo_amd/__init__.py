@@ -135,6 +135,7 @@ GEOM_SIGNATURES = {
     "yv_ba_window_read": (_I, [_P, ctypes.c_int64, _P, ctypes.POINTER(_I), _P, _P, _P, _P, _I]),
     "yv_ba_window_trajectory": (_I, [_P, ctypes.c_int64, _I, _P]),
     "yv_lm_sum_mode": (_I, []),
+    "yv_pose_lm_sum_mode": (_I, [_I]),
 }
 
 # include/yavo/yavo_map.h (the shared map; ya_vo_amd/map.py wraps the block layout)
@@ -199,9 +200,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     return lib
 
 
-def lm_sum_mode() -> int:
-    """The pose-LM kernel's edge-sum order as the oracle's sum_mode (yv_lm_sum_mode; parity tests use it)."""
-    return int(load_library().yv_lm_sum_mode())
+def lm_sum_mode(n_problems=None) -> int:
+    """The pose-LM kernel's edge-sum order as the oracle's sum_mode (parity tests use it): the batch's track LM
+    (yv_lm_sum_mode) when n_problems is None, else yv_pose_lm / yv_pose_lm_batch over n_problems problems
+    (yv_pose_lm_sum_mode)."""
+    lib = load_library()
+    return int(lib.yv_lm_sum_mode() if n_problems is None else lib.yv_pose_lm_sum_mode(int(n_problems)))
 
 
 def _check(status: int, what: str) -> None:

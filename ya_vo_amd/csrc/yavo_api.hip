@@ -29,6 +29,7 @@ struct yv_ctx {
     int32_t* h_pinned = nullptr;                              // small pinned scratch for counts
     void* scratch = nullptr;                                  // device arena of the geometry host calls
     size_t scratch_cap = 0;
+    uint8_t* scratch_h = nullptr;                             // its pinned host mirror (same offsets)
     void* fr_ws = nullptr;                                    // yv_f_ransac_batch's hypothesis workspace
     size_t fr_ws_cap = 0;
     // yv_calc_optical_flow_pyr_lk's pyramid workspace, kept between calls (creating and destroying it per call
@@ -418,6 +419,7 @@ void yv_destroy(yv_ctx* ctx) {
     if (ctx->ess_cache) yv_essential_destroy(ctx->ess_cache);
     batch_free(ctx->single);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->scratch_h) (void)hipHostFree(ctx->scratch_h);
     if (ctx->fr_ws) (void)hipFree(ctx->fr_ws);
     if (ctx->d_offsets) (void)hipFree(ctx->d_offsets);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
@@ -1248,11 +1250,21 @@ int yv_filter_matches(yv_ctx* ctx, const yv_match* in, int n, int thr, yv_match*
 namespace {
 
 // Carves 256-B aligned sub-buffers out of the context's device arena (grown on demand, outside any
-// timed loop: the host-pointer calls are synchronous anyway).
+// timed loop: the host-pointer calls are synchronous anyway).  The arena has a pinned host mirror with the same
+// offsets: a call's inputs are copied into the mirror (`in`), one DMA moves the range they span (`upload`), and its
+// outputs come back in one DMA of the range they span (`download`, then `finish` after the stream drained).  A
+// host-pointer call is then two copies however many buffers it has (round 3: one staged copy per buffer, ~10 per
+// LoopHandler frame).
 struct Arena {
     yv_ctx* ctx;
     size_t need = 0;
     std::vector<std::pair<void**, size_t>> reqs;
+    size_t in_lo = SIZE_MAX, in_hi = 0, out_lo = SIZE_MAX, out_hi = 0;
+    struct Out {
+        void* dst;
+        size_t off, bytes;
+    };
+    std::vector<Out> outs;
     template <class T>
     void add(T** p, size_t count) {
         reqs.push_back({reinterpret_cast<void**>(p), count * sizeof(T)});
@@ -1261,10 +1273,16 @@ struct Arena {
     int commit() {
         if (need > ctx->scratch_cap) {
             if (ctx->scratch) (void)hipFree(ctx->scratch);
+            if (ctx->scratch_h) (void)hipHostFree(ctx->scratch_h);
             ctx->scratch = nullptr;
+            ctx->scratch_h = nullptr;
             ctx->scratch_cap = 0;
             size_t cap = std::max(need, (size_t)1 << 20);
             if (hipMalloc(&ctx->scratch, cap) != hipSuccess) return YV_ERR_HIP;
+            if (hipHostMalloc(reinterpret_cast<void**>(&ctx->scratch_h), cap) != hipSuccess) {
+                ctx->scratch_h = nullptr;
+                return YV_ERR_HIP;
+            }
             ctx->scratch_cap = cap;
         }
         char* base = reinterpret_cast<char*>(ctx->scratch);
@@ -1274,6 +1292,55 @@ struct Arena {
             off += (r.second + 255) & ~(size_t)255;
         }
         return YV_OK;
+    }
+    size_t off_of(const void* dev) const {
+        return (size_t)(static_cast<const char*>(dev) - static_cast<const char*>(ctx->scratch));
+    }
+    void in(const void* dev, const void* src, size_t bytes) {
+        if (!bytes) return;
+        const size_t o = off_of(dev);
+        std::memcpy(ctx->scratch_h + o, src, bytes);
+        in_lo = std::min(in_lo, o);
+        in_hi = std::max(in_hi, o + bytes);
+    }
+    // a pitched host image into a packed device image
+    void in_2d(const void* dev, const uint8_t* src, size_t spitch, size_t width, size_t height) {
+        if (!width || !height) return;
+        const size_t o = off_of(dev);
+        uint8_t* p = ctx->scratch_h + o;
+        if (spitch == width) std::memcpy(p, src, width * height);
+        else
+            for (size_t r = 0; r < height; ++r) std::memcpy(p + r * width, src + r * spitch, width);
+        in_lo = std::min(in_lo, o);
+        in_hi = std::max(in_hi, o + width * height);
+    }
+    void out(void* dst, const void* dev, size_t bytes) {
+        if (!bytes) return;
+        const size_t o = off_of(dev);
+        outs.push_back({dst, o, bytes});
+        out_lo = std::min(out_lo, o);
+        out_hi = std::max(out_hi, o + bytes);
+    }
+    hipError_t upload(hipStream_t s) {
+        if (in_hi <= in_lo) return hipSuccess;
+        return hipMemcpyAsync(static_cast<char*>(ctx->scratch) + in_lo, ctx->scratch_h + in_lo, in_hi - in_lo,
+                              hipMemcpyHostToDevice, s);
+    }
+    hipError_t download(hipStream_t s) {
+        if (out_hi <= out_lo) return hipSuccess;
+        return hipMemcpyAsync(ctx->scratch_h + out_lo, static_cast<char*>(ctx->scratch) + out_lo, out_hi - out_lo,
+                              hipMemcpyDeviceToHost, s);
+    }
+    // after the stream drained: the outputs into the caller's buffers
+    void finish() {
+        for (const auto& o : outs) std::memcpy(o.dst, ctx->scratch_h + o.off, o.bytes);
+    }
+    // download, wait, finish
+    hipError_t fetch(hipStream_t s) {
+        hipError_t e = download(s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess) finish();
+        return e;
     }
 };
 
@@ -1307,19 +1374,17 @@ int yv_f_ransac(yv_ctx* ctx, const yv_match* m, int n, const int32_t* samples, i
     a.add(&dmax, 1);
     a.add(&dfound, 1);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
-    ctx->h_pinned[0] = n;
-    YV_HIP(stage_h2d(ctx, dm, m, sizeof(yv_match) * (size_t)n, s));
-    YV_HIP(stage_h2d(ctx, dcnt, ctx->h_pinned, sizeof(int32_t), s));
-    if (iters > 0) YV_HIP(stage_h2d(ctx, dsmp, samples, sizeof(int32_t) * 8 * (size_t)iters, s));
-    YV_HIP(stage_h2d(ctx, dF, F, sizeof(double) * 9, s));  // untouched if iters == 0
+    a.in(dm, m, sizeof(yv_match) * (size_t)n);
+    a.in(dcnt, &n, sizeof(int32_t));
+    if (iters > 0) a.in(dsmp, samples, sizeof(int32_t) * 8 * (size_t)iters);
+    a.in(dF, F, sizeof(double) * 9);  // untouched if iters == 0
+    YV_HIP(a.upload(s));
     yavo::launch_f_ransac(dm, n, dcnt, 1, dsmp, 8 * (int64_t)iters, iters, thr, dF, dmax, dfound, dws, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(stage_d2h(ctx, F, dF, sizeof(double) * 9, s));
-    YV_HIP(stage_d2h(ctx, ctx->h_pinned + 1, dmax, sizeof(int32_t), s));
-    YV_HIP(stage_d2h(ctx, ctx->h_pinned + 2, dfound, sizeof(int32_t), s));
-    YV_HIP(stage_sync(ctx, s));
-    *max_inliers = ctx->h_pinned[1];
-    *found = ctx->h_pinned[2];
+    a.out(F, dF, sizeof(double) * 9);
+    a.out(max_inliers, dmax, sizeof(int32_t));
+    a.out(found, dfound, sizeof(int32_t));
+    YV_HIP(a.fetch(s));
     return YV_OK;
 }
 
@@ -1343,18 +1408,19 @@ int yv_triangulate(yv_ctx* ctx, const double pose_a[7], const double pose_b[7], 
     a.add(&dok, (size_t)n);
     a.add(&dn, 1);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(stage_h2d(ctx, dm, m, sizeof(yv_match) * (size_t)n, s));
-    YV_HIP(stage_h2d(ctx, dposes, pose_a, sizeof(double) * 7, s));
-    YV_HIP(stage_h2d(ctx, dposes + 7, pose_b, sizeof(double) * 7, s));
-    YV_HIP(stage_h2d(ctx, dK, K, sizeof(double) * 9, s));
-    YV_HIP(hipMemsetAsync(dn, 0, sizeof(int32_t), s));
+    const int32_t zero = 0;
+    a.in(dm, m, sizeof(yv_match) * (size_t)n);
+    a.in(dposes, pose_a, sizeof(double) * 7);
+    a.in(dposes + 7, pose_b, sizeof(double) * 7);
+    a.in(dK, K, sizeof(double) * 9);
+    a.in(dn, &zero, sizeof(int32_t));
+    YV_HIP(a.upload(s));
     yavo::launch_triangulate(dm, n, dposes, dK, dX, dok, dn, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(stage_d2h(ctx, Xw, dX, sizeof(double) * 3 * (size_t)n, s));
-    YV_HIP(stage_d2h(ctx, ok, dok, (size_t)n, s));
-    YV_HIP(stage_d2h(ctx, ctx->h_pinned, dn, sizeof(int32_t), s));
-    YV_HIP(stage_sync(ctx, s));
-    *n_ok = ctx->h_pinned[0];
+    a.out(Xw, dX, sizeof(double) * 3 * (size_t)n);
+    a.out(ok, dok, (size_t)n);
+    a.out(n_ok, dn, sizeof(int32_t));
+    YV_HIP(a.fetch(s));
     return YV_OK;
 }
 
@@ -1371,13 +1437,14 @@ int yv_world2camera(yv_ctx* ctx, const double* X, int n, const double pose[7], c
     a.add(&dK, 9);
     a.add(&dO, 3 * (size_t)n);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(stage_h2d(ctx, dX, X, sizeof(double) * 3 * (size_t)n, s));
-    YV_HIP(stage_h2d(ctx, dT, pose, sizeof(double) * 7, s));
-    YV_HIP(stage_h2d(ctx, dK, K, sizeof(double) * 9, s));
+    a.in(dX, X, sizeof(double) * 3 * (size_t)n);
+    a.in(dT, pose, sizeof(double) * 7);
+    a.in(dK, K, sizeof(double) * 9);
+    YV_HIP(a.upload(s));
     yavo::launch_world2camera(dX, n, dT, dK, dO, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(stage_d2h(ctx, out, dO, sizeof(double) * 3 * (size_t)n, s));
-    YV_HIP(stage_sync(ctx, s));
+    a.out(out, dO, sizeof(double) * 3 * (size_t)n);
+    YV_HIP(a.fetch(s));
     return YV_OK;
 }
 
@@ -1402,23 +1469,22 @@ static int pose_single(yv_ctx* ctx, const double* X, const double* uv, int n, co
     a.add(&dout, (size_t)std::max(n, 1));
     a.add(&dres, 1);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
-    ctx->h_pinned[0] = 0;
-    ctx->h_pinned[1] = n;
-    YV_HIP(stage_h2d(ctx, doff, ctx->h_pinned, 2 * sizeof(int32_t), s));
+    const int32_t off2[2] = {0, n};
+    a.in(doff, off2, 2 * sizeof(int32_t));
     if (n > 0) {
-        YV_HIP(stage_h2d(ctx, dX, X, sizeof(double) * 3 * (size_t)n, s));
-        YV_HIP(stage_h2d(ctx, duv, uv, sizeof(double) * 2 * (size_t)n, s));
+        a.in(dX, X, sizeof(double) * 3 * (size_t)n);
+        a.in(duv, uv, sizeof(double) * 2 * (size_t)n);
     }
-    YV_HIP(stage_h2d(ctx, dK, K, sizeof(double) * 9, s));
-    YV_HIP(stage_h2d(ctx, dP, pose, sizeof(double) * 7, s));
+    a.in(dK, K, sizeof(double) * 9);
+    a.in(dP, pose, sizeof(double) * 7);
+    YV_HIP(a.upload(s));
     if (lm) yavo::launch_pose_lm(doff, 1, dX, duv, dK, dP, dout, dres, s);
     else yavo::launch_pose_gn(doff, 1, dX, duv, dK, dP, dres, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
-    YV_HIP(stage_d2h(ctx, pose, dP, sizeof(double) * 7, s));
-    if (lm && n > 0) YV_HIP(stage_d2h(ctx, outlier, dout, (size_t)n, s));
-    YV_HIP(stage_d2h(ctx, ctx->h_pinned + 2, dres, sizeof(int32_t), s));
-    YV_HIP(stage_sync(ctx, s));
-    *result = ctx->h_pinned[2];
+    a.out(pose, dP, sizeof(double) * 7);
+    if (lm && n > 0) a.out(outlier, dout, (size_t)n);
+    a.out(result, dres, sizeof(int32_t));
+    YV_HIP(a.fetch(s));
     return YV_OK;
 }
 
@@ -1659,17 +1725,13 @@ int yv_calc_optical_flow_pyr_lk(yv_ctx* ctx, const uint8_t* prev, const uint8_t*
     if (a.commit() != YV_OK) return YV_ERR_HIP;
     int status_rc = YV_OK;
     do {
-        if (stage_h2d_2d(ctx, dimg, W, prev, stride, W, H, s) != hipSuccess ||
-            stage_h2d_2d(ctx, dimg + pitch, W, next, stride, W, H, s) != hipSuccess ||
-            stage_h2d(ctx, dpts, prev_pts, sizeof(float) * 2 * n, s) != hipSuccess) {
-            status_rc = YV_ERR_HIP;
-            break;
-        }
-        ctx->h_pinned[0] = 0;
-        ctx->h_pinned[1] = 1;
-        ctx->h_pinned[2] = n;
-        if (stage_h2d(ctx, dpair, ctx->h_pinned, 2 * sizeof(int32_t), s) != hipSuccess ||
-            stage_h2d(ctx, dcnt, ctx->h_pinned + 2, sizeof(int32_t), s) != hipSuccess) {
+        const int32_t pair[3] = {0, 1, n};
+        a.in_2d(dimg, prev, (size_t)stride, (size_t)W, (size_t)H);
+        a.in_2d(dimg + pitch, next, (size_t)stride, (size_t)W, (size_t)H);
+        a.in(dpts, prev_pts, sizeof(float) * 2 * n);
+        a.in(dpair, pair, 2 * sizeof(int32_t));
+        a.in(dcnt, pair + 2, sizeof(int32_t));
+        if (a.upload(s) != hipSuccess) {
             status_rc = YV_ERR_HIP;
             break;
         }
@@ -1677,11 +1739,10 @@ int yv_calc_optical_flow_pyr_lk(yv_ctx* ctx, const uint8_t* prev, const uint8_t*
         if (status_rc != YV_OK) break;
         status_rc = yv_lk_track_batch(lk, dpair, 1, dpts, dcnt, n, max_count, eps, min_eig, dnext, dst, derr, nullptr);
         if (status_rc != YV_OK) break;
-        if (stage_d2h(ctx, next_pts, dnext, sizeof(float) * 2 * n, s) != hipSuccess ||
-            stage_d2h(ctx, status, dst, (size_t)n, s) != hipSuccess ||
-            stage_d2h(ctx, err, derr, sizeof(float) * n, s) != hipSuccess ||
-            stage_sync(ctx, s) != hipSuccess)
-            status_rc = YV_ERR_HIP;
+        a.out(next_pts, dnext, sizeof(float) * 2 * n);
+        a.out(status, dst, (size_t)n);
+        a.out(err, derr, sizeof(float) * n);
+        if (a.fetch(s) != hipSuccess) status_rc = YV_ERR_HIP;
     } while (0);
     return status_rc;
 }
@@ -1825,24 +1886,20 @@ int yv_find_essential(yv_ctx* ctx, const float* pts1, const float* pts2, int n, 
     if (a.commit() != YV_OK) return YV_ERR_HIP;
     int st = YV_OK;
     do {
-        ctx->h_pinned[0] = n;
-        if (stage_h2d(ctx, d1, pts1, sizeof(float) * 2 * n, s) != hipSuccess ||
-            stage_h2d(ctx, d2, pts2, sizeof(float) * 2 * n, s) != hipSuccess ||
-            stage_h2d(ctx, dcnt, ctx->h_pinned, sizeof(int32_t), s) != hipSuccess) {
+        a.in(d1, pts1, sizeof(float) * 2 * n);
+        a.in(d2, pts2, sizeof(float) * 2 * n);
+        a.in(dcnt, &n, sizeof(int32_t));
+        if (a.upload(s) != hipSuccess) {
             st = YV_ERR_HIP;
             break;
         }
         st = yv_find_essential_batch(es, d1, d2, dcnt, 1, n, focal, ppx, ppy, prob, threshold, dE, dm, dfound,
                                      nullptr, nullptr);
         if (st != YV_OK) break;
-        if (stage_d2h(ctx, E, dE, sizeof(double) * 9, s) != hipSuccess ||
-            stage_d2h(ctx, ctx->h_pinned + 1, dfound, sizeof(int32_t), s) != hipSuccess ||
-            (mask && stage_d2h(ctx, mask, dm, (size_t)n, s) != hipSuccess) ||
-            stage_sync(ctx, s) != hipSuccess) {
-            st = YV_ERR_HIP;
-            break;
-        }
-        *found = ctx->h_pinned[1];
+        a.out(E, dE, sizeof(double) * 9);
+        a.out(found, dfound, sizeof(int32_t));
+        if (mask) a.out(mask, dm, (size_t)n);
+        if (a.fetch(s) != hipSuccess) st = YV_ERR_HIP;
     } while (0);
     return st;
 }
@@ -1871,24 +1928,22 @@ int yv_recover_pose(yv_ctx* ctx, const double E[9], const float* pts1, const flo
     if (a.commit() != YV_OK) return YV_ERR_HIP;
     int st = YV_OK;
     do {
-        ctx->h_pinned[0] = n;
-        if ((n > 0 && (stage_h2d(ctx, d1, pts1, sizeof(float) * 2 * n, s) != hipSuccess ||
-                       stage_h2d(ctx, d2, pts2, sizeof(float) * 2 * n, s) != hipSuccess)) ||
-            stage_h2d(ctx, dE, E, sizeof(double) * 9, s) != hipSuccess ||
-            stage_h2d(ctx, dcnt, ctx->h_pinned, sizeof(int32_t), s) != hipSuccess) {
+        if (n > 0) {
+            a.in(d1, pts1, sizeof(float) * 2 * n);
+            a.in(d2, pts2, sizeof(float) * 2 * n);
+        }
+        a.in(dE, E, sizeof(double) * 9);
+        a.in(dcnt, &n, sizeof(int32_t));
+        if (a.upload(s) != hipSuccess) {
             st = YV_ERR_HIP;
             break;
         }
         st = yv_recover_pose_batch(es, dE, d1, d2, dcnt, 1, std::max(n, 5), K, dR, dt, dgood, nullptr);
         if (st != YV_OK) break;
-        if (stage_d2h(ctx, R, dR, sizeof(double) * 9, s) != hipSuccess ||
-            stage_d2h(ctx, t, dt, sizeof(double) * 3, s) != hipSuccess ||
-            stage_d2h(ctx, ctx->h_pinned + 1, dgood, sizeof(int32_t), s) != hipSuccess ||
-            stage_sync(ctx, s) != hipSuccess) {
-            st = YV_ERR_HIP;
-            break;
-        }
-        *good = ctx->h_pinned[1];
+        a.out(R, dR, sizeof(double) * 9);
+        a.out(t, dt, sizeof(double) * 3);
+        a.out(good, dgood, sizeof(int32_t));
+        if (a.fetch(s) != hipSuccess) st = YV_ERR_HIP;
     } while (0);
     return st;
 }

@@ -252,6 +252,74 @@ __device__ void em_det_poly(const double* B, double* c) {
     for (int k = 0; k < 11; ++k) c[k] = t0[k] - t1[k] + t2[k];
 }
 
+// cv::solvePoly (Durand-Kerner) of degree NN (the coefficients above NN were trimmed) on one lane; rre / rim [10].
+// Every loop is unrolled (NN is a template constant), so j != i is resolved at compile time and a coincident root
+// (OpenCV skips its factor) is a select, not a branch.  OpenCV stops when the largest |update| is 0; |q| > 0 exactly
+// when qr^2 + qi^2 > 0 (NaN compares false either way), so the squared magnitude decides without the square root; a
+// sweep that moved no root is a fixed point (every later sweep repeats it).  Returns the sweeps run.
+template <int NN>
+__device__ int dk_solve(const double* c, double* rre, double* rim) {
+    double cr[NN + 1], xr[NN], xi[NN];
+#pragma unroll
+    for (int i = 0; i <= NN; ++i) cr[i] = c[i];
+    {
+        double pr = 1, pi = 0;
+        const double qr = 1, qi = 1;
+#pragma unroll
+        for (int i = 0; i < NN; i++) {
+            xr[i] = pr;
+            xi[i] = pi;
+            const double tr = pr * qr - pi * qi, ti = pr * qi + pi * qr;
+            pr = tr;
+            pi = ti;
+        }
+    }
+    int sweeps = 0;
+    for (int iter = 0; iter < 300; iter++) {
+        ++sweeps;
+        double maxDiff2 = 0;
+        bool moved = false;
+#pragma unroll
+        for (int i = 0; i < NN; i++) {
+            const double pr = xr[i], pi = xi[i];
+            double nr = cr[NN], ni = 0.0, dr = cr[NN], di = 0.0;
+#pragma unroll
+            for (int j = 0; j < NN; j++) {
+                const double tr = nr * pr - ni * pi, ti = nr * pi + ni * pr;
+                nr = tr + cr[NN - j - 1];
+                ni = ti + 0.0;
+                if (j != i) {
+                    const bool same = pr == xr[j] && pi == xi[j];
+                    const double sr = pr - xr[j], si = pi - xi[j];
+                    const double ur = dr * sr - di * si, ui = dr * si + di * sr;
+                    dr = same ? dr : ur;
+                    di = same ? di : ui;
+                }
+            }
+            const double t = 1. / (dr * dr + di * di);
+            const double qr = (nr * dr + ni * di) * t, qi = (-nr * di + ni * dr) * t;
+            xr[i] = pr - qr;
+            xi[i] = pi - qi;
+            moved |= __double_as_longlong(xr[i]) != __double_as_longlong(pr) ||
+                     __double_as_longlong(xi[i]) != __double_as_longlong(pi);
+            const double an2 = qr * qr + qi * qi;
+            maxDiff2 = maxDiff2 < an2 ? an2 : maxDiff2;
+        }
+        if (maxDiff2 <= 0 || !moved) break;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        if (i < NN) {
+            rre[i] = xr[i];
+            rim[i] = fabs(xi[i]) < 1e-100 ? 0.0 : xi[i];
+        } else {
+            rre[i] = 0.0;
+            rim[i] = 0.0;
+        }
+    }
+    return sweeps;
+}
+
 // cv::solvePoly's Durand-Kerner sweep with one root per lane of a 10-lane group (lane r owns root r; group lanes
 // base .. base + 9, all active whenever this runs).  The same operations in the same order as solvePoly: OpenCV's
 // sweep is Gauss-Seidel -- root i's denominator prod_{j != i} (x_i - x_j) takes the roots j < i already updated in
@@ -341,10 +409,48 @@ __device__ int dk_group(const double* c, int r, int base, uint64_t gmask, double
     return sweeps;
 }
 
-// EMEstimatorCallback::runKernel (oracle or_em_kernel) on a 10-lane group (lane r of the group at base, mask gmask):
-// every lane forms the null space, the constraint matrix, its LU inverse and det B(z) redundantly, the
-// Durand-Kerner roots are one per lane (dk_group), and lane r then runs the reference loop's iteration i = r (solveZ
-// and the model) -- the models land in root order by a ballot prefix.  models [10][9]; returns the count (every lane).
+// solveZ of root (re, im) and its model: the body of runKernel's loop over the roots; false when the root is complex
+// (|Im| > 1e-10) or solveZ degenerate
+__device__ __forceinline__ bool em_root_model(const double* B, const double* EE, double re, double im, double* ev) {
+    if (fabs(im) > 1e-10) return false;
+    const double z1 = re, z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
+    double bz[9];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const double* br = B + j * 13;
+        bz[j * 3 + 0] = br[0] * z3 + br[1] * z2 + br[2] * z1 + br[3];
+        bz[j * 3 + 1] = br[4] * z3 + br[5] * z2 + br[6] * z1 + br[7];
+        bz[j * 3 + 2] = br[8] * z4 + br[9] * z3 + br[10] * z2 + br[11] * z1 + br[12];
+    }
+    // SVD::solveZ: the square SVD transposes into At; the answer is the last row of Vt
+    double A3[9], V3[9], w3[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) A3[a * 3 + b] = bz[b * 3 + a];
+    cv_jacobi_svd<3>(A3, w3, V3);
+    const double* xy1 = V3 + 6;
+    if (fabs(xy1[2]) < 1e-10) return false;
+    const double xs = xy1[0] / xy1[2], ys = xy1[1] / xy1[2], zs = z1;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) ev[k] = ((EE[0 * 9 + k] * xs + EE[1 * 9 + k] * ys) + EE[2 * 9 + k] * zs) + EE[3 * 9 + k];
+    double s2 = 0;
+    s2 += ev[0] * ev[0] + ev[1] * ev[1] + ev[2] * ev[2] + ev[3] * ev[3];
+    s2 += ev[4] * ev[4] + ev[5] * ev[5] + ev[6] * ev[6] + ev[7] * ev[7];
+    s2 += ev[8] * ev[8];
+    const double sc = 1. / sqrt(s2);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) ev[k] = ev[k] * sc;
+    return true;
+}
+
+// EMEstimatorCallback::runKernel (oracle or_em_kernel); models [10][9]; returns the count.  kGroup: on a 10-lane
+// group (lane r of the group at base, mask gmask) every lane forms the null space, the constraint matrix, its LU
+// inverse and det B(z) redundantly, the Durand-Kerner roots are one per lane (dk_group) and lane r runs the loop's
+// iteration i = r (solveZ and the model), the models landing in root order by a ballot prefix -- the latency form
+// (1.5 vs 2.5 ms for one list).  Otherwise one lane per iteration (dk_solve and the loop over the ten roots) -- the
+// throughput form (a whole 64-lane wave of iterations).
+template <bool kGroup>
 __device__ int em_models(const double* q1, const double* q2, double* models, int r, int base, uint64_t gmask,
                          int prof_k = 1 << 30) {
     EP_DECL
@@ -399,69 +505,61 @@ __device__ int em_models(const double* q1, const double* q2, double* models, int
     int nn = 10;
     for (; nn > 1; nn--)
         if (fabs(c[nn]) + fabs(0.0) > DBL_EPSILON) break;  // solvePoly trims the vanishing leading coefficients
-    double rre = 0, rim = 0;
-    int sweeps = 0;
-    switch (nn) {  // group-uniform
-        case 10: sweeps = dk_group<10>(c, r, base, gmask, rre, rim); break;
-        case 9: sweeps = dk_group<9>(c, r, base, gmask, rre, rim); break;
-        case 8: sweeps = dk_group<8>(c, r, base, gmask, rre, rim); break;
-        case 7: sweeps = dk_group<7>(c, r, base, gmask, rre, rim); break;
-        case 6: sweeps = dk_group<6>(c, r, base, gmask, rre, rim); break;
-        case 5: sweeps = dk_group<5>(c, r, base, gmask, rre, rim); break;
-        case 4: sweeps = dk_group<4>(c, r, base, gmask, rre, rim); break;
-        case 3: sweeps = dk_group<3>(c, r, base, gmask, rre, rim); break;
-        case 2: sweeps = dk_group<2>(c, r, base, gmask, rre, rim); break;
-        default: sweeps = dk_group<1>(c, r, base, gmask, rre, rim); break;
+    int sweeps = 0, count = 0;
+    if constexpr (kGroup) {
+        double rre = 0, rim = 0;
+        switch (nn) {  // group-uniform
+            case 10: sweeps = dk_group<10>(c, r, base, gmask, rre, rim); break;
+            case 9: sweeps = dk_group<9>(c, r, base, gmask, rre, rim); break;
+            case 8: sweeps = dk_group<8>(c, r, base, gmask, rre, rim); break;
+            case 7: sweeps = dk_group<7>(c, r, base, gmask, rre, rim); break;
+            case 6: sweeps = dk_group<6>(c, r, base, gmask, rre, rim); break;
+            case 5: sweeps = dk_group<5>(c, r, base, gmask, rre, rim); break;
+            case 4: sweeps = dk_group<4>(c, r, base, gmask, rre, rim); break;
+            case 3: sweeps = dk_group<3>(c, r, base, gmask, rre, rim); break;
+            case 2: sweeps = dk_group<2>(c, r, base, gmask, rre, rim); break;
+            default: sweeps = dk_group<1>(c, r, base, gmask, rre, rim); break;
+        }
+        EP_MARK(4);
+        double ev[9];
+        const bool valid = em_root_model(B, EE, rre, rim, ev);
+        const uint64_t vb = __ballot(valid) & gmask;
+        const int lane = (int)(threadIdx.x & 63);
+        const int pos = __popcll(vb & ((1ull << lane) - 1ull));
+        if (valid) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) models[pos * 9 + k] = ev[k];
+        }
+        count = __popcll(vb);
+    } else {
+        double rre[10], rim[10];
+        switch (nn) {
+            case 10: sweeps = dk_solve<10>(c, rre, rim); break;
+            case 9: sweeps = dk_solve<9>(c, rre, rim); break;
+            case 8: sweeps = dk_solve<8>(c, rre, rim); break;
+            case 7: sweeps = dk_solve<7>(c, rre, rim); break;
+            case 6: sweeps = dk_solve<6>(c, rre, rim); break;
+            case 5: sweeps = dk_solve<5>(c, rre, rim); break;
+            case 4: sweeps = dk_solve<4>(c, rre, rim); break;
+            case 3: sweeps = dk_solve<3>(c, rre, rim); break;
+            case 2: sweeps = dk_solve<2>(c, rre, rim); break;
+            default: sweeps = dk_solve<1>(c, rre, rim); break;
+        }
+        EP_MARK(4);
+        for (int i = 0; i < 10; i++) {
+            double ev[9];
+            if (!em_root_model(B, EE, rre[i], rim[i], ev)) continue;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) models[count * 9 + k] = ev[k];
+            count++;
+        }
     }
-    EP_MARK(4);
     EP_SET(7, sweeps);
     (void)sweeps;
-    // the reference loop's iteration i = r: a real root (|Im| <= 1e-10) and a non-degenerate solveZ give a model
-    bool valid = false;
-    double ev[9];
-    do {
-        if (fabs(rim) > 1e-10) break;
-        const double z1 = rre, z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
-        double bz[9];
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-            const double* br = B + j * 13;
-            bz[j * 3 + 0] = br[0] * z3 + br[1] * z2 + br[2] * z1 + br[3];
-            bz[j * 3 + 1] = br[4] * z3 + br[5] * z2 + br[6] * z1 + br[7];
-            bz[j * 3 + 2] = br[8] * z4 + br[9] * z3 + br[10] * z2 + br[11] * z1 + br[12];
-        }
-        // SVD::solveZ: the square SVD transposes into At; the answer is the last row of Vt
-        double A3[9], V3[9], w3[3];
-#pragma unroll
-        for (int a = 0; a < 3; ++a)
-#pragma unroll
-            for (int b = 0; b < 3; ++b) A3[a * 3 + b] = bz[b * 3 + a];
-        cv_jacobi_svd<3>(A3, w3, V3);
-        const double* xy1 = V3 + 6;
-        if (fabs(xy1[2]) < 1e-10) break;
-        const double xs = xy1[0] / xy1[2], ys = xy1[1] / xy1[2], zs = z1;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) ev[k] = ((EE[0 * 9 + k] * xs + EE[1 * 9 + k] * ys) + EE[2 * 9 + k] * zs) + EE[3 * 9 + k];
-        double s2 = 0;
-        s2 += ev[0] * ev[0] + ev[1] * ev[1] + ev[2] * ev[2] + ev[3] * ev[3];
-        s2 += ev[4] * ev[4] + ev[5] * ev[5] + ev[6] * ev[6] + ev[7] * ev[7];
-        s2 += ev[8] * ev[8];
-        const double sc = 1. / sqrt(s2);
-#pragma unroll
-        for (int k = 0; k < 9; ++k) ev[k] = ev[k] * sc;
-        valid = true;
-    } while (false);
-    const uint64_t vb = __ballot(valid) & gmask;
-    const int lane = (int)(threadIdx.x & 63);
-    const int pos = __popcll(vb & ((1ull << lane) - 1ull));
-    if (valid) {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) models[pos * 9 + k] = ev[k];
-    }
     EP_MARK(5);
     if (r == 0) EP_STORE(prof_k);
     (void)prof_k;
-    return __popcll(vb);
+    return count;
 }
 
 // Sampson error (EMEstimatorCallback::computeError) <= t
@@ -555,18 +653,22 @@ __global__ void ess_subsets_kernel(int n_pairs, EssParams P, int chunk0, int ite
     st[7] = (int32_t)(uint32_t)(rng >> 32);
 }
 
-// A 64-lane workgroup holds six RANSAC iterations, one per 10-lane group (lanes 60..63 idle): the per-hypothesis
-// solver runs redundantly on its group's lanes except the Durand-Kerner sweep and solveZ, which run one root per lane
+// The five-point models of a round.  kGroup (workspaces of <= kEssWidePairs lists, latency): a 64-lane workgroup
+// holds six RANSAC iterations, one per 10-lane group (lanes 60..63 idle).  Otherwise (throughput) one iteration per
+// lane, 64 per workgroup.
 constexpr int kModelGroup = 10;
-constexpr int kModelIters = 6;  // iterations per workgroup
+constexpr int kModelIters = 6;  // iterations per workgroup in the group form
 
+template <bool kGroup>
 __global__ __launch_bounds__(64) void ess_models_kernel(EssParams P, int chunk0) {
     const int pair = blockIdx.y;
     const int lane = threadIdx.x;
-    const int g = lane / kModelGroup, r = lane - g * kModelGroup, base = g * kModelGroup;
-    const int k = blockIdx.x * kModelIters + g;
-    if (g >= kModelIters || k >= P.chunk) return;  // whole groups leave together
-    const uint64_t gmask = ((1ull << kModelGroup) - 1ull) << base;
+    const int g = kGroup ? lane / kModelGroup : lane;
+    const int r = kGroup ? lane - g * kModelGroup : 0;
+    const int base = kGroup ? g * kModelGroup : lane;
+    const int k = blockIdx.x * (kGroup ? kModelIters : 64) + g;
+    if ((kGroup && g >= kModelIters) || k >= P.chunk) return;  // whole groups leave together
+    const uint64_t gmask = kGroup ? ((1ull << kModelGroup) - 1ull) << base : 1ull << lane;
     const int it = chunk0 + k;
     const int32_t* st = P.state + 8 * pair;
     const int n = st[5];
@@ -589,7 +691,7 @@ __global__ __launch_bounds__(64) void ess_models_kernel(EssParams P, int chunk0)
         q2[2 * i + 1] = m2[2 * j + 1];
     }
     double* out = P.models + ((int64_t)pair * P.chunk + k) * 90;
-    const int cnt = em_models(q1, q2, out, r, base, gmask, pair == 0 ? it : 1 << 30);
+    const int cnt = em_models<kGroup>(q1, q2, out, r, base, gmask, pair == 0 ? it : 1 << 30);
     if (r == 0) *nmod = cnt;
 }
 
@@ -860,8 +962,11 @@ void launch_find_essential(const EssParams& P, const EssRun& r, const float* pts
     const float t = (float)(thr * thr);
     for (int c0 = 0; c0 < iters; c0 += P.chunk) {
         hipLaunchKernelGGL(ess::ess_subsets_kernel, dim3((n_pairs + 63) / 64), dim3(64), 0, s, n_pairs, P, c0, iters);
-        hipLaunchKernelGGL(ess::ess_models_kernel, dim3((P.chunk + ess::kModelIters - 1) / ess::kModelIters, n_pairs), dim3(64),
-                           0, s, P, c0);
+        if (P.chunk == kEssChunkWide)  // few lists: the latency form
+            hipLaunchKernelGGL(ess::ess_models_kernel<true>,
+                               dim3((P.chunk + ess::kModelIters - 1) / ess::kModelIters, n_pairs), dim3(64), 0, s, P, c0);
+        else
+            hipLaunchKernelGGL(ess::ess_models_kernel<false>, dim3((P.chunk + 63) / 64, n_pairs), dim3(64), 0, s, P, c0);
         hipLaunchKernelGGL(ess::ess_score_kernel, dim3(P.chunk, n_pairs), dim3(256), 0, s, P, c0, t);
         hipLaunchKernelGGL(ess::ess_select_kernel, dim3((n_pairs + 63) / 64), dim3(64), 0, s, P, n_pairs, c0, r.prob);
     }

@@ -1760,11 +1760,18 @@ __global__ __launch_bounds__(kNT) void pose_gn_kernel(const int32_t* __restrict_
 // (DESIGN.md 4.3, 10): fewer workgroups looping over the problems, LDS padding to one workgroup per CU, and a form
 // holding each problem's edges in LDS.
 constexpr int kLMThreads = 256;
+// A few problems (the host-pointer yv_pose_lm of the LoopHandler, small yv_pose_lm_batch calls) leave most CUs idle,
+// so their latency is what counts: 512 threads, two waves per SIMD of the problem's own CU, halve each thread's edge
+// share (sum order 7, yv_pose_lm_sum_mode).  The batch's tracks keep 256 (two problems per CU interleave there).
+constexpr int kLMThreadsWide = 512;
+constexpr int kLMWideMaxProblems = 256;
 
-template <typename... A>
+template <int NT = kLMThreads, typename... A>
 void launch_lm(int n, hipStream_t s, A... args) {
-    hipLaunchKernelGGL(pose_lm_kernel<kLMThreads>, dim3(n), dim3(kLMThreads), 0, s, args..., n);
+    hipLaunchKernelGGL(pose_lm_kernel<NT>, dim3(n), dim3(NT), 0, s, args..., n);
 }
+
+constexpr int lm_mode_of(int nt) { return nt == 512 ? 7 : nt == 256 ? 6 : nt == 128 ? 5 : 4; }
 
 }  // namespace geom
 
@@ -1806,8 +1813,12 @@ void launch_world2camera(const double* X, int n, const double* T, const double* 
 
 void launch_pose_lm(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
                     double* poses, uint8_t* outlier, int32_t* inliers, hipStream_t s) {
-    geom::launch_lm(n_problems, s, offsets, static_cast<const int32_t*>(nullptr), 0, X, uv, K,
-                               static_cast<const double*>(poses), poses, outlier, inliers);
+    if (n_problems <= geom::kLMWideMaxProblems)
+        geom::launch_lm<geom::kLMThreadsWide>(n_problems, s, offsets, static_cast<const int32_t*>(nullptr), 0, X, uv, K,
+                                              static_cast<const double*>(poses), poses, outlier, inliers);
+    else
+        geom::launch_lm(n_problems, s, offsets, static_cast<const int32_t*>(nullptr), 0, X, uv, K,
+                        static_cast<const double*>(poses), poses, outlier, inliers);
 }
 
 void launch_track_build(const int32_t* tracks, int n_tracks, const int32_t* pairs, const yv_keypoint* keypoints,
@@ -1854,9 +1865,11 @@ void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, con
 
 }  // namespace yavo
 
-extern "C" int yv_lm_sum_mode(void) {
-    constexpr int nt = yavo::geom::kLMThreads;
-    return nt == 256 ? 6 : nt == 128 ? 5 : 4;
+extern "C" int yv_lm_sum_mode(void) { return yavo::geom::lm_mode_of(yavo::geom::kLMThreads); }
+
+extern "C" int yv_pose_lm_sum_mode(int n_problems) {
+    return yavo::geom::lm_mode_of(n_problems <= yavo::geom::kLMWideMaxProblems ? yavo::geom::kLMThreadsWide
+                                                                               : yavo::geom::kLMThreads);
 }
 
 #ifdef YAVO_LM_PROFILE
