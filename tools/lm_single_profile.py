@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--prof", action="store_true", help="phase cycles from lib/libyavo_prof.so instead of wall times")
     a = ap.parse_args()
     probs = problems(a.edges)
+    if a.prof:  # before anything loads the product library
+        lib = yv.load_library(os.path.join(ROOT, "ya_vo_amd", "lib", "libyavo_prof.so"))
+        lib.yv_debug_lm_prof.argtypes = [ctypes.c_void_p]
     res = {"sum_mode": yv.lm_sum_mode(1)}
     if not a.prof:
         ctx = yv.Context(0)
@@ -56,8 +59,6 @@ def main():
                            "call_ms_min": round(1e3 * float(np.min(ts)), 4)}
         ctx.close()
     else:
-        lib = yv.load_library(os.path.join(ROOT, "ya_vo_amd", "lib", "libyavo_prof.so"))
-        lib.yv_debug_lm_prof.argtypes = [ctypes.c_void_p]
         ctx = yv.Context(0)
         for n, (X, uv, prior) in zip(a.edges, probs):
             ctx.pose_lm(X, uv, scene.K_KITTI, prior)

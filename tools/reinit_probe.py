@@ -46,23 +46,30 @@ def probe_list(ctx, m, reps, rng):
             "essential_inliers": int(mask.sum()), "same_shift_frac": float(np.mean(np.all(d == np.median(d, 0), 1)))}
 
 
+def loop_handler_lists(ctx, pairs, H=376, W=1241):
+    """matchFeatures + removeOutliers(20) of `pairs` consecutive-frame pairs of bench_loop_handler.py's sequence (crops
+    one (1, 3) px step apart), as the LoopHandler's re-initialisation sees them.  ctx needs the BRIEF offsets."""
+    out = []
+    for j in range(pairs):
+        kps = []
+        for k in (37 * j, 37 * j + 1):
+            img = synth_frame(2024, k, 3 * k, H, W)
+            rc, _, _ = ctx.detect(img)
+            kps.append(ctx.describe(img, rc))
+        out.append(ctx.filter_matches(ctx.match_features(kps[0], kps[1]), 20))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pairs", type=int, default=4)
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
-    H, W = 376, 1241
     ctx = yv.Context(0)
     ctx.set_brief_offsets(np.fromfile(os.path.join(ROOT, "tests", "golden", "brief_offsets_mt19937_42.bin"), np.int8))
     rng = np.random.default_rng(0)
     out = {"loop_handler_lists": [], "two_view_scene": None}
-    for j in range(a.pairs):
-        kps = []
-        for k in (37 * j, 37 * j + 1):  # consecutive frames of the sequence: crops one (1, 3) px step apart
-            img = synth_frame(2024, k, 3 * k, H, W)
-            rc, _, _ = ctx.detect(img)
-            kps.append(ctx.describe(img, rc))
-        m = ctx.filter_matches(ctx.match_features(kps[0], kps[1]), 20)
+    for m in loop_handler_lists(ctx, a.pairs):
         out["loop_handler_lists"].append(probe_list(ctx, m, a.reps, rng))
     # bench_geometry's list: a two-view scene with 20% gross outliers as match records
     from epipolar_scene import two_view_scene

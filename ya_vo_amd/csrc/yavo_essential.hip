@@ -3,10 +3,10 @@
 // 4.x path like oracle/yavo_oracle_essential.c, expression for expression (built with -ffp-contract=off):
 //
 //   ess_prepare_kernel   (p - c) / f per point as OpenCV's MatExpr evaluates it, float -> double
-//   ess_subsets_kernel   getSubset's cv::RNG((uint64)-1) draws of a round (64 iterations; 256 for <= 8 lists) (one lane per list; the draws
-//                        never depend on the models, so a round's subsets are drawn before its models)
-//   ess_models_kernel    EMEstimatorCallback::runKernel, one lane per RANSAC iteration of a 64-iteration round
-//                        (16-lane workgroups):
+//   ess_subsets_kernel   getSubset's cv::RNG((uint64)-1) draws of a round (64 iterations; 1024 for <= 8 lists) (one lane
+//                        per list; the draws never depend on the models, so a round's subsets are drawn before its models)
+//   ess_models_kernel    EMEstimatorCallback::runKernel, one RANSAC iteration per lane (64-lane workgroups) or, for
+//                        <= 8 lists, per 10-lane group (six per workgroup):
 //                        JacobiSVD null space, the cubic-constraint matrix, LU inverse, det B(z), Durand-Kerner,
 //                        solveZ, up to 10 models
 //   ess_score_kernel     one workgroup per iteration: float Sampson errors of its models over the whole list
@@ -21,6 +21,7 @@
 
 #include "yavo_internal.h"
 #include "yavo_cvsvd.h"
+#include "yavo_xlane.h"
 
 namespace yavo {
 namespace ess {
@@ -191,19 +192,21 @@ __device__ void lu_inverse10(const double* A, double* inv) {
             for (int j = i; j < n; j++) { const double t = a[i * n + j]; a[i * n + j] = a[k * n + j]; a[k * n + j] = t; }
             for (int j = 0; j < n; j++) { const double t = b[i * n + j]; b[i * n + j] = b[k * n + j]; b[k * n + j] = t; }
         }
-        const double d = -1 / a[i * n + i];
+        const double d = fp64::div(-1.0, a[i * n + i]);  // yavo_fp64.h: the operators' results
         for (int j = i + 1; j < n; j++) {
             const double alpha = a[j * n + i] * d;
             for (int q = i + 1; q < n; q++) a[j * n + q] += alpha * a[i * n + q];
             for (int q = 0; q < n; q++) b[j * n + q] += alpha * b[i * n + q];
         }
     }
-    for (int i = n - 1; i >= 0; i--)
+    for (int i = n - 1; i >= 0; i--) {
+        const fp64::Rcp64 ri(a[i * n + i]);  // the row's ten divisions share one refined reciprocal
         for (int j = 0; j < n; j++) {
             double s = b[i * n + j];
             for (int q = i + 1; q < n; q++) s -= a[i * n + q] * b[q * n + j];
-            b[i * n + j] = s / a[i * n + i];
+            b[i * n + j] = ri.div(s);
         }
+    }
     for (int q = 0; q < n * n; ++q) inv[q] = b[q];
 }
 
@@ -296,7 +299,7 @@ __device__ int dk_solve(const double* c, double* rre, double* rim) {
                     di = same ? di : ui;
                 }
             }
-            const double t = 1. / (dr * dr + di * di);
+            const double t = fp64::rcp(dr * dr + di * di);
             const double qr = (nr * dr + ni * di) * t, qi = (-nr * di + ni * dr) * t;
             xr[i] = pr - qr;
             xi[i] = pi - qi;
@@ -320,8 +323,8 @@ __device__ int dk_solve(const double* c, double* rre, double* rim) {
     return sweeps;
 }
 
-// cv::solvePoly's Durand-Kerner sweep with one root per lane of a 10-lane group (lane r owns root r; group lanes
-// base .. base + 9, all active whenever this runs).  The same operations in the same order as solvePoly: OpenCV's
+// cv::solvePoly's Durand-Kerner sweep with one root per lane of a group: lanes 0 .. 9 of a 16-lane row (lane r owns
+// root r; all ten active whenever this runs), the roots exchanged by DPP row broadcasts.  The same operations in the same order as solvePoly: OpenCV's
 // sweep is Gauss-Seidel -- root i's denominator prod_{j != i} (x_i - x_j) takes the roots j < i already updated in
 // this sweep and j > i as they were -- so per sweep every lane first gathers the group's old roots and evaluates its
 // Horner value (independent of the other roots), then for k = 0 .. NN-1: lane k multiplies its denominator by its
@@ -330,6 +333,27 @@ __device__ int dk_solve(const double* c, double* rre, double* rim) {
 // A wave issues ~650 instead of ~1750 FP64 instructions per sweep (the ten roots' Horner chains and the tail of the
 // products run side by side), and six hypotheses share a wave.  rre / rim: this lane's root (0 past NN).  Returns
 // the sweeps run.
+// the row's roots 0 .. N-1 into ox / oy, and root k (a loop counter the compiler unrolls) into kr / ki
+template <int N, int J = 0>
+__device__ __forceinline__ void bcast_all(double xr, double xi, double* ox, double* oy) {
+    if constexpr (J < N) {
+        ox[J] = xl::row_bcast_f64<J>(xr);
+        oy[J] = xl::row_bcast_f64<J>(xi);
+        bcast_all<N, J + 1>(xr, xi, ox, oy);
+    }
+}
+template <int N, int J = 0>
+__device__ __forceinline__ void bcast_one(int k, double xr, double xi, double& kr, double& ki) {
+    if constexpr (J < N) {
+        if (k == J) {
+            kr = xl::row_bcast_f64<J>(xr);
+            ki = xl::row_bcast_f64<J>(xi);
+        } else {
+            bcast_one<N, J + 1>(k, xr, xi, kr, ki);
+        }
+    }
+}
+
 template <int NN>
 __device__ int dk_group(const double* c, int r, int base, uint64_t gmask, double& rre, double& rim) {
     double cr[NN + 1];
@@ -356,11 +380,7 @@ __device__ int dk_group(const double* c, int r, int base, uint64_t gmask, double
     for (int iter = 0; iter < 300; iter++) {
         ++sweeps;
         double ox[NN], oy[NN];
-#pragma unroll
-        for (int j = 0; j < NN; ++j) {
-            ox[j] = __shfl(xr, base + j, 64);
-            oy[j] = __shfl(xi, base + j, 64);
-        }
+        bcast_all<NN>(xr, xi, ox, oy);
         const double pr = xr, pi = xi;
         double nr = cr[NN], ni = 0.0, dr = cr[NN], di = 0.0;
 #pragma unroll
@@ -382,7 +402,7 @@ __device__ int dk_group(const double* c, int r, int base, uint64_t gmask, double
                     dr = same ? dr : ur;
                     di = same ? di : ui;
                 }
-                const double t = 1. / (dr * dr + di * di);
+                const double t = fp64::rcp(dr * dr + di * di);
                 const double qr = (nr * dr + ni * di) * t, qi = (-nr * di + ni * dr) * t;
                 xr = pr - qr;
                 xi = pi - qi;
@@ -390,7 +410,8 @@ __device__ int dk_group(const double* c, int r, int base, uint64_t gmask, double
                         __double_as_longlong(xi) != __double_as_longlong(pi);
                 an2 = qr * qr + qi * qi;
             }
-            const double kr = __shfl(xr, base + k, 64), ki = __shfl(xi, base + k, 64);
+            double kr, ki;
+            bcast_one<NN>(k, xr, xi, kr, ki);
             if (r > k && own) {
                 const bool same = pr == kr && pi == ki;
                 const double sr = pr - kr, si = pi - ki;
@@ -431,14 +452,15 @@ __device__ __forceinline__ bool em_root_model(const double* B, const double* EE,
     cv_jacobi_svd<3>(A3, w3, V3);
     const double* xy1 = V3 + 6;
     if (fabs(xy1[2]) < 1e-10) return false;
-    const double xs = xy1[0] / xy1[2], ys = xy1[1] / xy1[2], zs = z1;
+    const fp64::Rcp64 rz(xy1[2]);
+    const double xs = rz.div(xy1[0]), ys = rz.div(xy1[1]), zs = z1;
 #pragma unroll
     for (int k = 0; k < 9; ++k) ev[k] = ((EE[0 * 9 + k] * xs + EE[1 * 9 + k] * ys) + EE[2 * 9 + k] * zs) + EE[3 * 9 + k];
     double s2 = 0;
     s2 += ev[0] * ev[0] + ev[1] * ev[1] + ev[2] * ev[2] + ev[3] * ev[3];
     s2 += ev[4] * ev[4] + ev[5] * ev[5] + ev[6] * ev[6] + ev[7] * ev[7];
     s2 += ev[8] * ev[8];
-    const double sc = 1. / sqrt(s2);
+    const double sc = fp64::rcp(fp64::sqrt(s2));
 #pragma unroll
     for (int k = 0; k < 9; ++k) ev[k] = ev[k] * sc;
     return true;
@@ -654,20 +676,22 @@ __global__ void ess_subsets_kernel(int n_pairs, EssParams P, int chunk0, int ite
 }
 
 // The five-point models of a round.  kGroup (workspaces of <= kEssWidePairs lists, latency): a 64-lane workgroup
-// holds six RANSAC iterations, one per 10-lane group (lanes 60..63 idle).  Otherwise (throughput) one iteration per
-// lane, 64 per workgroup.
+// holds four RANSAC iterations, one per 16-lane row, whose lanes 0 .. 9 are the group (10 .. 15 idle: the row
+// broadcasts of dk_group need the group inside one DPP row).  Otherwise (throughput) one iteration per lane, 64 per
+// workgroup.
 constexpr int kModelGroup = 10;
-constexpr int kModelIters = 6;  // iterations per workgroup in the group form
+constexpr int kModelRow = 16;
+constexpr int kModelIters = 4;  // iterations per workgroup in the group form
 
 template <bool kGroup>
 __global__ __launch_bounds__(64) void ess_models_kernel(EssParams P, int chunk0) {
     const int pair = blockIdx.y;
     const int lane = threadIdx.x;
-    const int g = kGroup ? lane / kModelGroup : lane;
-    const int r = kGroup ? lane - g * kModelGroup : 0;
-    const int base = kGroup ? g * kModelGroup : lane;
+    const int g = kGroup ? lane / kModelRow : lane;
+    const int r = kGroup ? lane - g * kModelRow : 0;
+    const int base = kGroup ? g * kModelRow : lane;
     const int k = blockIdx.x * (kGroup ? kModelIters : 64) + g;
-    if ((kGroup && g >= kModelIters) || k >= P.chunk) return;  // whole groups leave together
+    if ((kGroup && r >= kModelGroup) || k >= P.chunk) return;  // whole groups leave together
     const uint64_t gmask = kGroup ? ((1ull << kModelGroup) - 1ull) << base : 1ull << lane;
     const int it = chunk0 + k;
     const int32_t* st = P.state + 8 * pair;
@@ -910,7 +934,8 @@ __global__ __launch_bounds__(64) void rp_count_kernel(const float* __restrict__ 
     cv_jacobi_svd<4>(At, w, V);
     const double Q0 = V[12], Q1 = V[13], Q2 = V[14], Q3 = V[15];
     bool ok = Q2 * Q3 > 0;
-    const double X[4] = {Q0 / Q3, Q1 / Q3, Q2 / Q3, Q3 / Q3};
+    const fp64::Rcp64 rq(Q3);
+    const double X[4] = {rq.div(Q0), rq.div(Q1), rq.div(Q2), rq.div(Q3)};
     ok = (X[2] < dist) && ok;
     double z = 0;
 #pragma unroll

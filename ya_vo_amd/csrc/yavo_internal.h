@@ -140,11 +140,13 @@ void launch_lk_edges(int n_tracks, const double* pX, const float* next, const ui
                      int32_t* edge_count, hipStream_t s);
 
 // cv::findEssentialMat (RANSAC) + cv::recoverPose (yavo_essential.hip).  Workspace of a yv_essential.
-// RANSAC iterations evaluated per round (one lane each): 64, or 256 for workspaces of at most kEssWidePairs lists, where
-// the chip is otherwise idle and a wider speculative round saves the dependent rounds' latency (the sequential
-// selection ignores the iterations past niters, so the result is the same)
+// RANSAC iterations evaluated per round: 64, or 1024 (>= findEssentialMat's 1000) for workspaces of at most kEssWidePairs
+// lists, where the chip is otherwise idle: a list that needs all its iterations (the LoopHandler's re-initialisation
+// lists, one image translation apart, never reach the 0.999 confidence early) then takes one round instead of four
+// dependent ones, and a list that converges early costs the same one round (the sequential selection ignores the
+// iterations past niters, so the result is the same)
 constexpr int kEssChunk = 64;
-constexpr int kEssChunkWide = 256;
+constexpr int kEssChunkWide = 1024;
 constexpr int kEssWidePairs = 8;
 inline int ess_chunk_for(int max_pairs) { return max_pairs <= kEssWidePairs ? kEssChunkWide : kEssChunk; }
 struct EssParams {

@@ -38,6 +38,15 @@ __device__ __forceinline__ double xor_row_f64(double v) {
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
+// v of lane L of this lane's 16-lane row (DPP row_newbcast, gfx90a+): a row-wide broadcast without the LDS unit
+template <int L>
+__device__ __forceinline__ double row_bcast_f64(double v) {
+    static_assert(L >= 0 && L < 16, "a lane of the row");
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = dpp<0x150 + L>((uint32_t)b), hi = dpp<0x150 + L>((uint32_t)(b >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 template <int OFF>
 __device__ __forceinline__ int xor_row_i32(int v) {
     return (int)xor_row<OFF>((uint32_t)v);

@@ -8,6 +8,7 @@
 #include <condition_variable>
 #include <deque>
 #include <fstream>
+#include <functional>
 #include <future>
 #include <iostream>
 #include <iterator>
@@ -201,8 +202,55 @@ void LoopHandler::addFrame(const Frame::ptr& frame) {
     events_.push_back(ev_);
 }
 
+// A helper thread with a GPU context of its own, running the calls it is handed in order (SideLane::submit); the
+// destructor runs what is queued and joins.
+class SideLane {
+public:
+    explicit SideLane(int device) : th_([this, device]() { run(device); }) {}
+    ~SideLane() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    SideLane(const SideLane&) = delete;
+    SideLane& operator=(const SideLane&) = delete;
+    void submit(std::function<void(Device&)> f) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            q_.push_back(std::move(f));
+        }
+        cv_.notify_one();
+    }
+
+private:
+    void run(int device) {
+        Device dev(device);
+        while (true) {
+            std::function<void(Device&)> f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&]() { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;  // stop_ and nothing left
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            f(dev);
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void(Device&)>> q_;
+    bool stop_ = false;
+    std::thread th_;  // last: starts after the members it uses exist
+};
+
 // _3DHandler::getFRANSAC(filterMatches, F, 400, 0.1) (src/3DHandler.cc:145-195): 400 hypotheses of 8 indices drawn
-// uniformly from [0, n) with replacement.  The reference's F is never used after the call (:222, :562).
+// uniformly from [0, n) with replacement.  The reference's F is never used after the call (:222, :562), and neither is
+// the count: with a side lane (the pipelined loop) the call is handed to it with its samples (drawn here, in loop
+// order) and its count lands in the frame's event later (resolvePendingF); F stays zero.
 int LoopHandler::getFRANSAC(const std::vector<Matches>& m, double F[9]) {
     const int n = (int)m.size();
     for (int i = 0; i < 9; ++i) F[i] = 0;
@@ -211,6 +259,23 @@ int LoopHandler::getFRANSAC(const std::vector<Matches>& m, double F[9]) {
     std::vector<int32_t> samples(8 * iters);
     std::uniform_int_distribution<int> dist(0, n - 1);
     for (auto& s : samples) s = dist(ransac_rng_);
+    if (side_) {
+        auto task = std::make_shared<std::packaged_task<FResult(Device&)>>(
+            [m, samples = std::move(samples), n, iters](Device& d) {
+                FResult r;
+                const double t0 = now_s();
+                double Fs[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+                int max_inl = 0, found = 0;
+                r.status = d.ok() ? yv_f_ransac(d.ctx(), m.data(), n, samples.data(), iters, 0.1, Fs, &max_inl, &found)
+                                  : d.status();
+                r.inliers = r.status == YV_OK && found ? max_inl : 0;
+                r.seconds = now_s() - t0;
+                return r;
+            });
+        pending_f_.emplace_back(events_.size(), task->get_future());  // this frame's event is pushed at that index
+        side_->submit([task](Device& d) { (*task)(d); });
+        return 0;
+    }
     int max_inl = 0, found = 0;
     const double t0 = now_s();
     struct Acc {
@@ -577,6 +642,8 @@ void LoopHandler::runVOPipelined(int max_frames) {
     // PNG decoding (the reference's cv::imread) is the longest per-frame step on the host: the worker keeps the next
     // `readers` frames decoding on their own threads and consumes them in path-train order, so ids stay sequential
     const int readers = std::max(1, pipeline_readers_);
+    auto side = std::make_unique<SideLane>(pipeline_device_);
+    side_ = side.get();
     std::thread worker([&]() {
         Device wdev(pipeline_device_);
         int st = wdev.ok() ? YV_OK : wdev.status();
@@ -733,8 +800,21 @@ void LoopHandler::runVOPipelined(int max_frames) {
     }
     cv_put.notify_all();
     worker.join();
+    side_ = nullptr;
+    side.reset();  // runs what is still queued
+    resolvePendingF();
     t_features += worker_features;
     t_read += worker_read;  // in the pipelined loop: the worker waiting for the next decoded frame
+}
+
+void LoopHandler::resolvePendingF() {
+    for (auto& p : pending_f_) {
+        const FResult r = p.second.get();
+        prim_.f_ransac += r.seconds;  // on the side lane, beside the tracking thread
+        if (!gpu(r.status, "getFRANSAC (side lane)")) continue;
+        if (p.first < events_.size()) events_[p.first].f_inliers = r.inliers;
+    }
+    pending_f_.clear();
 }
 
 }  // namespace yavo_fe

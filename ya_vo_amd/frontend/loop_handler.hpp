@@ -21,6 +21,7 @@
 #pragma once
 
 #include <cstdint>
+#include <future>
 #include <map>
 #include <memory>
 #include <random>
@@ -33,6 +34,8 @@
 #include "se3_host.hpp"
 
 namespace yavo_fe {
+
+class SideLane;
 
 enum voStatus { INIT, TRACKING, ERROR, RESET };  // include/LoopHandler.hpp:26
 
@@ -165,6 +168,16 @@ private:
 
     int pipeline_depth_ = 0, pipeline_device_ = 0, pipeline_readers_ = 4, pipeline_gpu_batch_ = 0;
     std::vector<int8_t> pipeline_offsets_;
+    // pipelined loop: getFRANSAC runs on a helper thread with its own GPU context (nothing downstream reads its
+    // result: the reference discards F and the count, src/LoopHandler.cc:225, 567); each pending call's count is
+    // written into its frame's event when the loop ends
+    struct FResult {
+        int status = YV_OK, inliers = 0;
+        double seconds = 0;
+    };
+    SideLane* side_ = nullptr;
+    std::vector<std::pair<size_t, std::future<FResult>>> pending_f_;
+    void resolvePendingF();
 
     bool gpu(int st, const char* what);
     void runVOPipelined(int max_frames);
