@@ -170,3 +170,35 @@ def test_lk_level_waits_for_a_build_on_another_stream(ctx, oracle):
     got = _d2h(d_der, (h, dst, 2), np.int16)[:, :w]
     np.testing.assert_array_equal(got, oracle.scharr(ref))
     lk.close()
+
+
+def test_lk_host_calls_reuse_the_previous_next_image(ctx, oracle):
+    """A tracking loop's consecutive calls (f0, f1), (f1, f2), ...: the host call finds f1 (and its pyramid) in the
+    slot its previous call left it in and uploads only the new image.  Every call equals the oracle, also when the
+    reused buffer's bytes change in place, when prev is not the previous next, and after a size change."""
+    H, W = 120, 200
+    frames = [synth_frame(31, k, 3 * k, H, W) for k in range(5)]
+    rng = np.random.default_rng(4)
+    pts = _pts(rng, 300, H, W)
+
+    def check(a, b):
+        g, gs, ge = ctx.calc_optical_flow_pyr_lk(a, b, pts)
+        o, os_, oe, _ = oracle.lk(a, b, pts, sum_mode=1)
+        np.testing.assert_array_equal(gs, os_)
+        np.testing.assert_array_equal(g, o)
+        np.testing.assert_array_equal(ge, oe)
+
+    buf = frames[0].copy()
+    check(buf, frames[1])
+    check(frames[1], frames[2])          # prev == the previous next: reused
+    check(frames[2].copy(), frames[3])   # equal bytes in another buffer: reused
+    mod = frames[3].copy()
+    mod[60, 100] ^= 0x55                 # one byte differs from the previous next: uploaded again
+    check(mod, frames[4])
+    check(frames[0], frames[1])          # not the previous next
+    small = [synth_frame(32, k, k, 60, 90) for k in range(2)]
+    g, gs, ge = ctx.calc_optical_flow_pyr_lk(small[0], small[1], pts[:50] * 0.4)
+    o, os_, oe, _ = oracle.lk(small[0], small[1], pts[:50] * 0.4, sum_mode=1)
+    np.testing.assert_array_equal(g, o)
+    check(frames[1], frames[2])          # after a size change: nothing to reuse
+    check(frames[2], frames[3])

@@ -35,6 +35,11 @@ struct yv_ctx {
     // yv_calc_optical_flow_pyr_lk's pyramid workspace, kept between calls (creating and destroying it per call
     // costs two hipMalloc / hipFree pairs and a device-wide synchronisation per tracked frame)
     yv_lk* lk_cache = nullptr;
+    // its two image slots (device, with a pinned host copy of what each holds): a call whose prev image is the previous
+    // call's next image (the tracking loop's consecutive frames) finds it and its pyramid already there
+    uint8_t* lk_img_d = nullptr;
+    uint8_t* lk_img_h = nullptr;
+    int lk_last = -1;  // the slot holding the previous call's next image (-1: none)
     // the host findEssentialMat / recoverPose calls' workspace (yv_essential_create is ~10 hipMallocs, its destroy a
     // device synchronisation: per call they cost more than the solve), grown on demand
     yv_essential* ess_cache = nullptr;
@@ -416,6 +421,8 @@ void yv_destroy(yv_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->lk_cache) yv_lk_destroy(ctx->lk_cache);
+    if (ctx->lk_img_d) (void)hipFree(ctx->lk_img_d);
+    if (ctx->lk_img_h) (void)hipHostFree(ctx->lk_img_h);
     if (ctx->ess_cache) yv_essential_destroy(ctx->ess_cache);
     batch_free(ctx->single);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
@@ -1696,26 +1703,54 @@ int yv_calc_optical_flow_pyr_lk(yv_ctx* ctx, const uint8_t* prev, const uint8_t*
     if (n == 0) return YV_OK;
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
     StageScope stage_scope(ctx);
+    const int64_t pitch = (int64_t)H * W;
     const int key[4] = {H, W, win, max_level};
     if (!ctx->lk_cache || !std::equal(key, key + 4, ctx->lk_key)) {
         if (ctx->lk_cache) yv_lk_destroy(ctx->lk_cache);
         ctx->lk_cache = nullptr;
+        if (ctx->lk_img_d) (void)hipFree(ctx->lk_img_d);
+        if (ctx->lk_img_h) (void)hipHostFree(ctx->lk_img_h);
+        ctx->lk_img_d = ctx->lk_img_h = nullptr;
+        ctx->lk_last = -1;
         int rc = yv_lk_create(ctx, 2, H, W, win, max_level, &ctx->lk_cache);
         if (rc != YV_OK) {
             ctx->lk_cache = nullptr;
             return rc;
         }
+        if (hipMalloc(reinterpret_cast<void**>(&ctx->lk_img_d), (size_t)(2 * pitch + 64)) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&ctx->lk_img_h), (size_t)(2 * pitch)) != hipSuccess) {
+            yv_lk_destroy(ctx->lk_cache);
+            ctx->lk_cache = nullptr;
+            if (ctx->lk_img_d) (void)hipFree(ctx->lk_img_d);
+            ctx->lk_img_d = ctx->lk_img_h = nullptr;
+            return YV_ERR_HIP;
+        }
         std::copy(key, key + 4, ctx->lk_key);
     }
     yv_lk* lk = ctx->lk_cache;
     hipStream_t s = ctx->stream;
+    // the image slots: prev is found in the slot the previous call left its next image in when the bytes are equal
+    // (its pyramid is still in that slot too); otherwise both images go up and both pyramids are built
+    auto same_image = [&](const uint8_t* img, const uint8_t* slot) {
+        if (stride == W) return std::memcmp(img, slot, (size_t)pitch) == 0;
+        for (int r = 0; r < H; ++r)
+            if (std::memcmp(img + (size_t)r * stride, slot + (size_t)r * W, (size_t)W) != 0) return false;
+        return true;
+    };
+    auto put_image = [&](const uint8_t* img, int slot) -> hipError_t {
+        uint8_t* h = ctx->lk_img_h + slot * pitch;
+        if (stride == W) std::memcpy(h, img, (size_t)pitch);
+        else
+            for (int r = 0; r < H; ++r) std::memcpy(h + (size_t)r * W, img + (size_t)r * stride, (size_t)W);
+        return hipMemcpyAsync(ctx->lk_img_d + slot * pitch, h, (size_t)pitch, hipMemcpyHostToDevice, s);
+    };
+    const bool reuse = ctx->lk_last >= 0 && same_image(prev, ctx->lk_img_h + ctx->lk_last * pitch);
+    const int ps = reuse ? ctx->lk_last : 0, ns = 1 - ps;
+    ctx->lk_last = -1;  // until this call has completed
     Arena a{ctx};
-    uint8_t* dimg;
     float *dpts, *dnext, *derr;
     int32_t *dpair, *dcnt;
     uint8_t* dst;
-    const int64_t pitch = (int64_t)H * W;
-    a.add(&dimg, (size_t)(2 * pitch + 64));
     a.add(&dpts, 2 * (size_t)n);
     a.add(&dnext, 2 * (size_t)n);
     a.add(&derr, (size_t)n);
@@ -1723,28 +1758,34 @@ int yv_calc_optical_flow_pyr_lk(yv_ctx* ctx, const uint8_t* prev, const uint8_t*
     a.add(&dcnt, 1);
     a.add(&dst, (size_t)n);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
-    int status_rc = YV_OK;
-    do {
-        const int32_t pair[3] = {0, 1, n};
-        a.in_2d(dimg, prev, (size_t)stride, (size_t)W, (size_t)H);
-        a.in_2d(dimg + pitch, next, (size_t)stride, (size_t)W, (size_t)H);
-        a.in(dpts, prev_pts, sizeof(float) * 2 * n);
-        a.in(dpair, pair, 2 * sizeof(int32_t));
-        a.in(dcnt, pair + 2, sizeof(int32_t));
-        if (a.upload(s) != hipSuccess) {
-            status_rc = YV_ERR_HIP;
-            break;
-        }
-        status_rc = yv_lk_build(lk, dimg, 2, W, pitch, nullptr);
-        if (status_rc != YV_OK) break;
-        status_rc = yv_lk_track_batch(lk, dpair, 1, dpts, dcnt, n, max_count, eps, min_eig, dnext, dst, derr, nullptr);
-        if (status_rc != YV_OK) break;
-        a.out(next_pts, dnext, sizeof(float) * 2 * n);
-        a.out(status, dst, (size_t)n);
-        a.out(err, derr, sizeof(float) * n);
-        if (a.fetch(s) != hipSuccess) status_rc = YV_ERR_HIP;
-    } while (0);
-    return status_rc;
+    const int32_t pair[3] = {ps, ns, n};
+    a.in(dpts, prev_pts, sizeof(float) * 2 * n);
+    a.in(dpair, pair, 2 * sizeof(int32_t));
+    a.in(dcnt, pair + 2, sizeof(int32_t));
+    if ((!reuse && put_image(prev, ps) != hipSuccess) || put_image(next, ns) != hipSuccess || a.upload(s) != hipSuccess)
+        return YV_ERR_HIP;
+    yavo::LkParams& P = lk->P;
+    P.img0 = ctx->lk_img_d;
+    P.stride0 = W;
+    P.pitch0 = pitch;
+    lk->built_images = 2;
+    if (reuse) {  // only the new image's pyramid (slot ns)
+        yavo::LkParams P1 = P;
+        P1.img0 = ctx->lk_img_d + ns * pitch;
+        P1.pyr = P.pyr + ns * P.pyr_pitch;
+        yavo::launch_lk_pyramid(P1, 1, s);
+    } else {
+        yavo::launch_lk_pyramid(P, 2, s);
+    }
+    if (check_launch() != YV_OK || hipEventRecord(lk->built, s) != hipSuccess) return YV_ERR_HIP;
+    int status_rc = yv_lk_track_batch(lk, dpair, 1, dpts, dcnt, n, max_count, eps, min_eig, dnext, dst, derr, nullptr);
+    if (status_rc != YV_OK) return status_rc;
+    a.out(next_pts, dnext, sizeof(float) * 2 * n);
+    a.out(status, dst, (size_t)n);
+    a.out(err, derr, sizeof(float) * n);
+    if (a.fetch(s) != hipSuccess) return YV_ERR_HIP;
+    ctx->lk_last = ns;
+    return YV_OK;
 }
 
 }  // extern "C"
