@@ -36,8 +36,10 @@ def test_find_essential_host_small(ctx):
 @pytest.mark.parametrize("capacity", [8, 9])
 def test_essential_batch_matches_oracle(ctx, oracle, capacity):
     """Lists of different lengths (incl. n < 5, n == 5 and pure noise) in one batched call.  A workspace of <= 8 lists
-    runs the five-point solver's latency form (10-lane groups, 256-iteration rounds), a larger one the throughput form
-    (one iteration per lane, 64-iteration rounds): both give the oracle's results."""
+    runs the five-point solver's latency form (one iteration per 16-lane row, 1024-iteration rounds, subsets drawn in
+    parallel from the RNG table: the 64-point list re-draws often, the noise list needs all 1000 iterations), a larger
+    one the throughput form (one iteration per lane, 64-iteration rounds, sequential draws): both give the oracle's
+    results."""
     import torch
     cases = [(2000, 0.2, 10), (0, 0.0, 11), (4, 0.0, 12), (5, 0.0, 13), (300, 0.5, 14), (150, 1.0, 15), (64, 0.1, 16),
              (1000, 0.0, 17)]

@@ -30,6 +30,7 @@ struct yv_ctx {
     void* scratch = nullptr;                                  // device arena of the geometry host calls
     size_t scratch_cap = 0;
     uint8_t* scratch_h = nullptr;                             // its pinned host mirror (same offsets)
+    uint8_t* scratch_hd = nullptr;                            // the mirror's address for kernels (zero-copy regions)
     void* fr_ws = nullptr;                                    // yv_f_ransac_batch's hypothesis workspace
     size_t fr_ws_cap = 0;
     // yv_calc_optical_flow_pyr_lk's pyramid workspace, kept between calls (creating and destroying it per call
@@ -1262,10 +1263,20 @@ namespace {
 // outputs come back in one DMA of the range they span (`download`, then `finish` after the stream drained).  A
 // host-pointer call is then two copies however many buffers it has (round 3: one staged copy per buffer, ~10 per
 // LoopHandler frame).
+//
+// Regions added with add_host live in the pinned mirror itself and kernels address them there (zero-copy over PCIe):
+// read-once inputs and the small outputs, which then need no DMA at all (a host call's outputs are a few hundred
+// bytes to a few tens of KB; a DMA costs a copy-engine round trip each way).  Inputs the kernels read many times stay
+// device regions.
 struct Arena {
     yv_ctx* ctx;
     size_t need = 0;
-    std::vector<std::pair<void**, size_t>> reqs;
+    struct Req {
+        void** p;
+        size_t bytes;
+        bool host;
+    };
+    std::vector<Req> reqs;
     size_t in_lo = SIZE_MAX, in_hi = 0, out_lo = SIZE_MAX, out_hi = 0;
     struct Out {
         void* dst;
@@ -1274,7 +1285,12 @@ struct Arena {
     std::vector<Out> outs;
     template <class T>
     void add(T** p, size_t count) {
-        reqs.push_back({reinterpret_cast<void**>(p), count * sizeof(T)});
+        reqs.push_back({reinterpret_cast<void**>(p), count * sizeof(T), false});
+        need += (count * sizeof(T) + 255) & ~(size_t)255;
+    }
+    template <class T>
+    void add_host(T** p, size_t count) {
+        reqs.push_back({reinterpret_cast<void**>(p), count * sizeof(T), true});
         need += (count * sizeof(T) + 255) & ~(size_t)255;
     }
     int commit() {
@@ -1286,27 +1302,40 @@ struct Arena {
             ctx->scratch_cap = 0;
             size_t cap = std::max(need, (size_t)1 << 20);
             if (hipMalloc(&ctx->scratch, cap) != hipSuccess) return YV_ERR_HIP;
-            if (hipHostMalloc(reinterpret_cast<void**>(&ctx->scratch_h), cap) != hipSuccess) {
+            void* hd = nullptr;
+            // coherent (fine-grained) host memory: kernels read and write the host regions uncached, so nothing of a
+            // previous call can be stale in the GPU's caches
+            if (hipHostMalloc(reinterpret_cast<void**>(&ctx->scratch_h), cap,
+                              hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+                hipHostGetDevicePointer(&hd, ctx->scratch_h, 0) != hipSuccess) {
+                if (ctx->scratch_h) (void)hipHostFree(ctx->scratch_h);
                 ctx->scratch_h = nullptr;
                 return YV_ERR_HIP;
             }
+            ctx->scratch_hd = static_cast<uint8_t*>(hd);
             ctx->scratch_cap = cap;
         }
         char* base = reinterpret_cast<char*>(ctx->scratch);
         size_t off = 0;
         for (auto& r : reqs) {
-            *r.first = base + off;
-            off += (r.second + 255) & ~(size_t)255;
+            *r.p = r.host ? static_cast<void*>(ctx->scratch_hd + off) : static_cast<void*>(base + off);
+            off += (r.bytes + 255) & ~(size_t)255;
         }
         return YV_OK;
     }
-    size_t off_of(const void* dev) const {
-        return (size_t)(static_cast<const char*>(dev) - static_cast<const char*>(ctx->scratch));
+    bool is_host(const void* p) const {
+        const uint8_t* q = static_cast<const uint8_t*>(p);
+        return q >= ctx->scratch_hd && q < ctx->scratch_hd + ctx->scratch_cap;
+    }
+    size_t off_of(const void* p) const {
+        return is_host(p) ? (size_t)(static_cast<const uint8_t*>(p) - ctx->scratch_hd)
+                          : (size_t)(static_cast<const char*>(p) - static_cast<const char*>(ctx->scratch));
     }
     void in(const void* dev, const void* src, size_t bytes) {
         if (!bytes) return;
         const size_t o = off_of(dev);
         std::memcpy(ctx->scratch_h + o, src, bytes);
+        if (is_host(dev)) return;  // read by the kernel where it is
         in_lo = std::min(in_lo, o);
         in_hi = std::max(in_hi, o + bytes);
     }
@@ -1325,6 +1354,7 @@ struct Arena {
         if (!bytes) return;
         const size_t o = off_of(dev);
         outs.push_back({dst, o, bytes});
+        if (is_host(dev)) return;  // written by the kernel where it is
         out_lo = std::min(out_lo, o);
         out_hi = std::max(out_hi, o + bytes);
     }
@@ -1373,13 +1403,13 @@ int yv_f_ransac(yv_ctx* ctx, const yv_match* m, int n, const int32_t* samples, i
     int32_t *dcnt, *dsmp, *dmax, *dfound;
     double* dF;
     uint8_t* dws;
-    a.add(&dm, (size_t)n);
+    a.add(&dm, (size_t)n);  // every hypothesis' count reads the whole list: on the device
     a.add(&dws, yavo::f_ransac_ws_bytes(1, iters));
-    a.add(&dcnt, 1);
-    a.add(&dsmp, (size_t)std::max(8 * iters, 1));
-    a.add(&dF, 9);
-    a.add(&dmax, 1);
-    a.add(&dfound, 1);
+    a.add_host(&dcnt, 1);
+    a.add_host(&dsmp, (size_t)std::max(8 * iters, 1));
+    a.add_host(&dF, 9);
+    a.add_host(&dmax, 1);
+    a.add_host(&dfound, 1);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
     a.in(dm, m, sizeof(yv_match) * (size_t)n);
     a.in(dcnt, &n, sizeof(int32_t));
@@ -1407,27 +1437,25 @@ int yv_triangulate(yv_ctx* ctx, const double pose_a[7], const double pose_b[7], 
     yv_match* dm;
     double *dposes, *dK, *dX;
     uint8_t* dok;
-    int32_t* dn;
-    a.add(&dm, (size_t)n);
-    a.add(&dposes, 14);
-    a.add(&dK, 9);
-    a.add(&dX, 3 * (size_t)n);
-    a.add(&dok, (size_t)n);
-    a.add(&dn, 1);
+    // every record, pose and output is read or written once: all in the pinned mirror, no DMA
+    a.add_host(&dm, (size_t)n);
+    a.add_host(&dposes, 14);
+    a.add_host(&dK, 9);
+    a.add_host(&dX, 3 * (size_t)n);
+    a.add_host(&dok, (size_t)n);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
-    const int32_t zero = 0;
     a.in(dm, m, sizeof(yv_match) * (size_t)n);
     a.in(dposes, pose_a, sizeof(double) * 7);
     a.in(dposes + 7, pose_b, sizeof(double) * 7);
     a.in(dK, K, sizeof(double) * 9);
-    a.in(dn, &zero, sizeof(int32_t));
-    YV_HIP(a.upload(s));
-    yavo::launch_triangulate(dm, n, dposes, dK, dX, dok, dn, s);
+    yavo::launch_triangulate(dm, n, dposes, dK, dX, dok, nullptr, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
     a.out(Xw, dX, sizeof(double) * 3 * (size_t)n);
     a.out(ok, dok, (size_t)n);
-    a.out(n_ok, dn, sizeof(int32_t));
     YV_HIP(a.fetch(s));
+    int cnt = 0;
+    for (int i = 0; i < n; ++i) cnt += ok[i] ? 1 : 0;
+    *n_ok = cnt;
     return YV_OK;
 }
 
@@ -1439,15 +1467,15 @@ int yv_world2camera(yv_ctx* ctx, const double* X, int n, const double pose[7], c
     hipStream_t s = ctx->stream;
     Arena a{ctx};
     double *dX, *dT, *dK, *dO;
-    a.add(&dX, 3 * (size_t)n);
-    a.add(&dT, 7);
-    a.add(&dK, 9);
-    a.add(&dO, 3 * (size_t)n);
+    // one read and one write per point: all in the pinned mirror, no DMA
+    a.add_host(&dX, 3 * (size_t)n);
+    a.add_host(&dT, 7);
+    a.add_host(&dK, 9);
+    a.add_host(&dO, 3 * (size_t)n);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
     a.in(dX, X, sizeof(double) * 3 * (size_t)n);
     a.in(dT, pose, sizeof(double) * 7);
     a.in(dK, K, sizeof(double) * 9);
-    YV_HIP(a.upload(s));
     yavo::launch_world2camera(dX, n, dT, dK, dO, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
     a.out(out, dO, sizeof(double) * 3 * (size_t)n);
@@ -1468,13 +1496,13 @@ static int pose_single(yv_ctx* ctx, const double* X, const double* uv, int n, co
     int32_t *doff, *dres;
     double *dX, *duv, *dK, *dP;
     uint8_t* dout;
-    a.add(&doff, 2);
-    a.add(&dX, 3 * (size_t)std::max(n, 1));
+    a.add(&dX, 3 * (size_t)std::max(n, 1));  // read by every pass: on the device
     a.add(&duv, 2 * (size_t)std::max(n, 1));
-    a.add(&dK, 9);
-    a.add(&dP, 7);
-    a.add(&dout, (size_t)std::max(n, 1));
-    a.add(&dres, 1);
+    a.add_host(&doff, 2);                      // read once, or written once: in the pinned mirror
+    a.add_host(&dK, 9);
+    a.add_host(&dP, 7);
+    a.add_host(&dout, (size_t)std::max(n, 1));
+    a.add_host(&dres, 1);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
     const int32_t off2[2] = {0, n};
     a.in(doff, off2, 2 * sizeof(int32_t));
@@ -1751,12 +1779,13 @@ int yv_calc_optical_flow_pyr_lk(yv_ctx* ctx, const uint8_t* prev, const uint8_t*
     float *dpts, *dnext, *derr;
     int32_t *dpair, *dcnt;
     uint8_t* dst;
-    a.add(&dpts, 2 * (size_t)n);
-    a.add(&dnext, 2 * (size_t)n);
-    a.add(&derr, (size_t)n);
-    a.add(&dpair, 2);
-    a.add(&dcnt, 1);
-    a.add(&dst, (size_t)n);
+    // points read once, outputs written once: in the pinned mirror (the images have their own slots)
+    a.add_host(&dpts, 2 * (size_t)n);
+    a.add_host(&dnext, 2 * (size_t)n);
+    a.add_host(&derr, (size_t)n);
+    a.add_host(&dpair, 2);
+    a.add_host(&dcnt, 1);
+    a.add_host(&dst, (size_t)n);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
     const int32_t pair[3] = {ps, ns, n};
     a.in(dpts, prev_pts, sizeof(float) * 2 * n);
@@ -1802,7 +1831,7 @@ namespace {
 void essential_free(yv_essential* es) {
     if (!es) return;
     yavo::EssParams& P = es->P;
-    void* ptrs[] = {P.m1, P.m2, P.idx, P.models, P.nmod, P.good, P.state, P.best, P.cand, P.cgood};
+    void* ptrs[] = {P.m1, P.m2, P.idx, P.models, P.nmod, P.good, P.state, P.best, P.cand, P.cgood, P.rng_tab};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete es;
@@ -1834,6 +1863,22 @@ int yv_essential_create(yv_ctx* ctx, int max_pairs, int max_points, int max_iter
         dalloc(&P.cgood, np * 4) != YV_OK) {
         essential_free(es);
         return YV_ERR_HIP;
+    }
+    if (P.chunk == yavo::kEssChunkWide) {
+        // cv::RNG((uint64)-1) states after 1 .. len draws: five per iteration plus room for the duplicate re-draws
+        const int len = 5 * max_iters + 2048;
+        std::vector<uint64_t> tab((size_t)len);
+        uint64_t st = ~0ull;
+        for (int k = 0; k < len; ++k) {
+            st = (uint64_t)(uint32_t)st * 4164903690ull + (st >> 32);  // cv::RNG::next (CV_RNG_COEFF)
+            tab[(size_t)k] = st;
+        }
+        if (dalloc(&P.rng_tab, (size_t)len) != YV_OK ||
+            hipMemcpy(P.rng_tab, tab.data(), sizeof(uint64_t) * (size_t)len, hipMemcpyHostToDevice) != hipSuccess) {
+            essential_free(es);
+            return YV_ERR_HIP;
+        }
+        P.rng_len = len;
     }
     *out = es;
     return YV_OK;
@@ -1918,12 +1963,14 @@ int yv_find_essential(yv_ctx* ctx, const float* pts1, const float* pts2, int n, 
     double* dE;
     uint8_t* dm;
     int32_t *dcnt, *dfound;
-    a.add(&d1, 2 * (size_t)n);
-    a.add(&d2, 2 * (size_t)n);
-    a.add(&dE, 9);
-    a.add(&dm, (size_t)n);
-    a.add(&dcnt, 1);
-    a.add(&dfound, 1);
+    // the points are read once (ess_prepare_kernel normalises them into the workspace), the outputs written once: all
+    // in the pinned mirror, no DMA
+    a.add_host(&d1, 2 * (size_t)n);
+    a.add_host(&d2, 2 * (size_t)n);
+    a.add_host(&dE, 9);
+    a.add_host(&dm, (size_t)n);
+    a.add_host(&dcnt, 1);
+    a.add_host(&dfound, 1);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
     int st = YV_OK;
     do {
@@ -1959,13 +2006,14 @@ int yv_recover_pose(yv_ctx* ctx, const double E[9], const float* pts1, const flo
     float *d1, *d2;
     double *dE, *dR, *dt;
     int32_t *dcnt, *dgood;
-    a.add(&d1, 2 * (size_t)std::max(n, 1));
-    a.add(&d2, 2 * (size_t)std::max(n, 1));
-    a.add(&dE, 9);
-    a.add(&dR, 9);
-    a.add(&dt, 3);
-    a.add(&dcnt, 1);
-    a.add(&dgood, 1);
+    // each point is read by its four candidate lanes once: all in the pinned mirror, no DMA
+    a.add_host(&d1, 2 * (size_t)std::max(n, 1));
+    a.add_host(&d2, 2 * (size_t)std::max(n, 1));
+    a.add_host(&dE, 9);
+    a.add_host(&dR, 9);
+    a.add_host(&dt, 3);
+    a.add_host(&dcnt, 1);
+    a.add_host(&dgood, 1);
     if (a.commit() != YV_OK) return YV_ERR_HIP;
     int st = YV_OK;
     do {

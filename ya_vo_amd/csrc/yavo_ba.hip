@@ -52,9 +52,8 @@ __device__ __forceinline__ void ba_error(const double* T, const double* K, const
     const double u0 = K[0] * pc[0] + K[1] * pc[1] + K[2] * pc[2];
     const double u1 = K[3] * pc[0] + K[4] * pc[1] + K[5] * pc[2];
     const double u2 = K[6] * pc[0] + K[7] * pc[1] + K[8] * pc[2];
-    const fp64::Rcp64 ru(u2);  // yavo_fp64.h: the operators' results
-    e[0] = meas[0] - ru.div(u0);
-    e[1] = meas[1] - ru.div(u1);
+    e[0] = meas[0] - u0 / u2;
+    e[1] = meas[1] - u1 / u2;
 }
 
 // the 256-lane halving tree over one value per thread (LDS), result valid in thread 0
@@ -84,7 +83,7 @@ __global__ __launch_bounds__(256) void ba_linearize_kernel(BaParams P, BaMat3 K)
     quat_to_R(T, R);
     const double fx = K.v[0], fy = K.v[4];
     const double x = pc[0], y = pc[1], z = pc[2];
-    const double zinv = fp64::rcp(z + 1e-18);
+    const double zinv = 1.0 / (z + 1e-18);
     const double zinv2 = zinv * zinv;
     Jp[0] = -fx * zinv; Jp[1] = 0; Jp[2] = fx * x * zinv2; Jp[3] = fx * x * y * zinv2;
     Jp[4] = -fx - fx * x * x * zinv2; Jp[5] = fx * y * zinv;
@@ -202,7 +201,7 @@ __global__ __launch_bounds__(256) void ba_landmark_reduce_kernel(BaParams P, uns
 __device__ __forceinline__ void inv3(const double* a, double* o) {
     const double c00 = a[4] * a[8] - a[5] * a[7], c01 = a[5] * a[6] - a[3] * a[8], c02 = a[3] * a[7] - a[4] * a[6];
     const double det = a[0] * c00 + a[1] * c01 + a[2] * c02;
-    const double id = fp64::rcp(det);
+    const double id = 1.0 / det;
     o[0] = c00 * id; o[1] = (a[2] * a[7] - a[1] * a[8]) * id; o[2] = (a[1] * a[5] - a[2] * a[4]) * id;
     o[3] = c01 * id; o[4] = (a[0] * a[8] - a[2] * a[6]) * id; o[5] = (a[2] * a[3] - a[0] * a[5]) * id;
     o[6] = c02 * id; o[7] = (a[1] * a[6] - a[0] * a[7]) * id; o[8] = (a[0] * a[4] - a[1] * a[3]) * id;
@@ -512,7 +511,7 @@ __global__ __launch_bounds__(kLdltThreads) void ba_ldlt_lds_kernel(BaParams P) {
     // column 0: L(i, 0) = S(i, 0) / D(0), t_i = D(0) L(i, 0), the diagonal chains' first terms
     if (!brk) {
         for (int i = t + 1; i < n; i += kLdltThreads) {
-            const double l = fp64::div(Ls[tri(i, 0)], a00);
+            const double l = Ls[tri(i, 0)] / a00;
             Ls[tri(i, 0)] = l;
             const double tt = a00 * l;
             tv[0][i] = tt;
@@ -554,7 +553,7 @@ __global__ __launch_bounds__(kLdltThreads) void ba_ldlt_lds_kernel(BaParams P) {
             LDP_MARK(1);
             if (i1 < n) {
                 const double acc = cx - lk * t1;
-                const double l = v1 ? fp64::div(acc, akk1) : acc;
+                const double l = v1 ? acc / akk1 : acc;
                 Ls[tri(i1, k + 1)] = l;
                 const double tt = akk1 * l;
                 tv[buf ^ 1][i1] = tt;

@@ -1,14 +1,11 @@
 // yavo_cvsvd.h -- device restatements of OpenCV's small dense linear algebra shared by the geometry kernels:
 // JacobiSVDImpl_<double> (lapack.cpp; with the FULL_UV completion by cv::RNG(0x12345678)), its hypot, and cv::RNG's
 // multiply-with-carry step.  Per lane, private arrays; every expression in OpenCV's order (files are built with
-// -ffp-contract=off), matching oracle/yavo_oracle_geom.c or_cv_jacobi_svd.  The sweep's divisions and square roots
-// use yavo_fp64.h's forms (the operators' results, shorter for mid-range operands).
+// -ffp-contract=off), matching oracle/yavo_oracle_geom.c or_cv_jacobi_svd.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
-
-#include "yavo_fp64.h"
 
 namespace yavo {
 namespace cv {
@@ -17,12 +14,12 @@ __device__ __forceinline__ double cv_hypot(double a, double b) {
     a = fabs(a);
     b = fabs(b);
     if (a > b) {
-        b = fp64::div(b, a);
-        return a * fp64::sqrt(1 + b * b);
+        b /= a;
+        return a * sqrt(1 + b * b);
     }
     if (b > 0) {
-        a = fp64::div(a, b);
-        return b * fp64::sqrt(1 + a * a);
+        a /= b;
+        return b * sqrt(1 + a * a);
     }
     return 0;
 }
@@ -67,16 +64,16 @@ __device__ void cv_jacobi_svd_mn(PA At, double* Wout, PV Vt) {
                 auto Aj = At + j * M;
                 double a = W[i], p = 0, b = W[j];
                 for (int k = 0; k < m; k++) p += Ai[k] * Aj[k];
-                if (fabs(p) <= eps * fp64::sqrt(a * b)) continue;
+                if (fabs(p) <= eps * sqrt(a * b)) continue;
                 p *= 2;
                 double beta = a - b, gamma = cv_hypot(p, beta);
                 if (beta < 0) {
                     double delta = (gamma - beta) * 0.5;
-                    s = fp64::sqrt(fp64::div(delta, gamma));
-                    c = fp64::div(p, gamma * s * 2);
+                    s = sqrt(delta / gamma);
+                    c = p / (gamma * s * 2);
                 } else {
-                    c = fp64::sqrt(fp64::div(gamma + beta, gamma * 2));
-                    s = fp64::div(p, gamma * c * 2);
+                    c = sqrt((gamma + beta) / (gamma * 2));
+                    s = p / (gamma * c * 2);
                 }
                 a = b = 0;
                 for (int k = 0; k < m; k++) {
@@ -107,7 +104,7 @@ __device__ void cv_jacobi_svd_mn(PA At, double* Wout, PV Vt) {
             double t = At[i * M + k];
             sd += t * t;
         }
-        W[i] = fp64::sqrt(sd);
+        W[i] = sqrt(sd);
     }
     for (int i = 0; i < n - 1; i++) {
         int j = i;

@@ -192,21 +192,19 @@ __device__ void lu_inverse10(const double* A, double* inv) {
             for (int j = i; j < n; j++) { const double t = a[i * n + j]; a[i * n + j] = a[k * n + j]; a[k * n + j] = t; }
             for (int j = 0; j < n; j++) { const double t = b[i * n + j]; b[i * n + j] = b[k * n + j]; b[k * n + j] = t; }
         }
-        const double d = fp64::div(-1.0, a[i * n + i]);  // yavo_fp64.h: the operators' results
+        const double d = -1 / a[i * n + i];
         for (int j = i + 1; j < n; j++) {
             const double alpha = a[j * n + i] * d;
             for (int q = i + 1; q < n; q++) a[j * n + q] += alpha * a[i * n + q];
             for (int q = 0; q < n; q++) b[j * n + q] += alpha * b[i * n + q];
         }
     }
-    for (int i = n - 1; i >= 0; i--) {
-        const fp64::Rcp64 ri(a[i * n + i]);  // the row's ten divisions share one refined reciprocal
+    for (int i = n - 1; i >= 0; i--)
         for (int j = 0; j < n; j++) {
             double s = b[i * n + j];
             for (int q = i + 1; q < n; q++) s -= a[i * n + q] * b[q * n + j];
-            b[i * n + j] = ri.div(s);
+            b[i * n + j] = s / a[i * n + i];
         }
-    }
     for (int q = 0; q < n * n; ++q) inv[q] = b[q];
 }
 
@@ -299,7 +297,7 @@ __device__ int dk_solve(const double* c, double* rre, double* rim) {
                     di = same ? di : ui;
                 }
             }
-            const double t = fp64::rcp(dr * dr + di * di);
+            const double t = 1. / (dr * dr + di * di);
             const double qr = (nr * dr + ni * di) * t, qi = (-nr * di + ni * dr) * t;
             xr[i] = pr - qr;
             xi[i] = pi - qi;
@@ -402,7 +400,7 @@ __device__ int dk_group(const double* c, int r, int base, uint64_t gmask, double
                     dr = same ? dr : ur;
                     di = same ? di : ui;
                 }
-                const double t = fp64::rcp(dr * dr + di * di);
+                const double t = 1. / (dr * dr + di * di);
                 const double qr = (nr * dr + ni * di) * t, qi = (-nr * di + ni * dr) * t;
                 xr = pr - qr;
                 xi = pi - qi;
@@ -452,15 +450,14 @@ __device__ __forceinline__ bool em_root_model(const double* B, const double* EE,
     cv_jacobi_svd<3>(A3, w3, V3);
     const double* xy1 = V3 + 6;
     if (fabs(xy1[2]) < 1e-10) return false;
-    const fp64::Rcp64 rz(xy1[2]);
-    const double xs = rz.div(xy1[0]), ys = rz.div(xy1[1]), zs = z1;
+    const double xs = xy1[0] / xy1[2], ys = xy1[1] / xy1[2], zs = z1;
 #pragma unroll
     for (int k = 0; k < 9; ++k) ev[k] = ((EE[0 * 9 + k] * xs + EE[1 * 9 + k] * ys) + EE[2 * 9 + k] * zs) + EE[3 * 9 + k];
     double s2 = 0;
     s2 += ev[0] * ev[0] + ev[1] * ev[1] + ev[2] * ev[2] + ev[3] * ev[3];
     s2 += ev[4] * ev[4] + ev[5] * ev[5] + ev[6] * ev[6] + ev[7] * ev[7];
     s2 += ev[8] * ev[8];
-    const double sc = fp64::rcp(fp64::sqrt(s2));
+    const double sc = 1. / sqrt(s2);
 #pragma unroll
     for (int k = 0; k < 9; ++k) ev[k] = ev[k] * sc;
     return true;
@@ -673,6 +670,132 @@ __global__ void ess_subsets_kernel(int n_pairs, EssParams P, int chunk0, int ite
     }
     st[6] = (int32_t)(uint32_t)rng;
     st[7] = (int32_t)(uint32_t)(rng >> 32);
+}
+
+// Round 0 of a wide round (<= 8 lists, the whole iteration budget in one round) drawn in parallel.  The sequential
+// draw stream is list-independent (cv::RNG((uint64)-1), P.rng_tab holds its states), and an iteration without a
+// duplicate consumes exactly five draws, so iteration it's draws are the five from offset 5 it as long as no earlier
+// iteration re-drew.  One workgroup per list: every thread takes iterations at those offsets, the first iteration f
+// with a duplicate is found by a block minimum, thread 0 replays f with getSubset's re-draws, every later offset
+// shifts by its extra draws, and the pass repeats from f + 1 (one pass per re-drawing iteration: ~0.5% of the
+// iterations for a 2000-point list).  Lists under 64 points (frequent re-draws) and draw counts past the table run
+// the sequential loop.  The RNG state after the round goes to state[6..7] as in ess_subsets_kernel.
+__device__ void subsets_sequential(EssParams& P, int32_t* st, int32_t* idx, int count, uint64_t rng, int it0, int end) {
+    for (int it = it0; it < end; ++it) {
+        int d[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            int v;
+            bool dup;
+            do {
+                v = (int)(cv_rng_next(&rng) % (uint32_t)count + 0u);
+                dup = false;
+#pragma unroll
+                for (int j = 0; j < i; ++j) dup |= d[j] == v;
+            } while (dup);
+            d[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) idx[5 * it + i] = d[i];
+    }
+    st[6] = (int32_t)(uint32_t)rng;
+    st[7] = (int32_t)(uint32_t)(rng >> 32);
+}
+
+__global__ __launch_bounds__(256) void ess_subsets_par_kernel(EssParams P, int iters) {
+    __shared__ int s_red[4];
+    __shared__ int s_base_it, s_base_off, s_bad;
+    const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int32_t* st = P.state + 8 * pair;
+    const int count = st[5];
+    if (count <= 5 || 0 >= st[0]) return;
+    int32_t* idx = P.idx + (int64_t)pair * P.max_iters * 5;
+    const int end = min(P.chunk, iters);
+    const uint64_t* tab = P.rng_tab;
+    const int len = P.rng_len;
+    if (count < 64) {
+        if (tid == 0) subsets_sequential(P, st, idx, count, ~0ull, 0, end);
+        return;
+    }
+    int base_it = 0, base_off = 0;  // iterations < base_it are final; base_it's draws start at table offset base_off
+    while (true) {
+        int first = end;  // this thread's first iteration with a duplicate
+        bool over = false;
+        for (int it = base_it + tid; it < end; it += 256) {
+            const int off = base_off + 5 * (it - base_it);
+            if (off + 5 > len) {
+                over = true;
+                break;
+            }
+            int d[5];
+            bool dup = false;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                d[i] = (int)((uint32_t)tab[off + i] % (uint32_t)count);
+#pragma unroll
+                for (int j = 0; j < i; ++j) dup |= d[j] == d[i];
+            }
+            if (dup) {
+                first = it;
+                break;  // later iterations of this thread are past it
+            }
+#pragma unroll
+            for (int i = 0; i < 5; ++i) idx[5 * it + i] = d[i];
+        }
+        // block minimum of the first duplicate, and any table overflow
+        int m = first;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o, 64));
+        const bool any_over = __syncthreads_or(over);
+        if (lane == 0) s_red[wave] = m;
+        __syncthreads();
+        const int f = min(min(s_red[0], s_red[1]), min(s_red[2], s_red[3]));
+        if (any_over) {  // a pathological re-draw count: the sequential stream from the start
+            if (tid == 0) subsets_sequential(P, st, idx, count, ~0ull, 0, end);
+            return;
+        }
+        if (f >= end) {  // every iteration from base_it on is final
+            if (tid == 0) {
+                const int off_end = base_off + 5 * (end - base_it);
+                const uint64_t rng = off_end > 0 ? tab[off_end - 1] : ~0ull;
+                st[6] = (int32_t)(uint32_t)rng;
+                st[7] = (int32_t)(uint32_t)(rng >> 32);
+            }
+            return;
+        }
+        if (tid == 0) {  // iteration f with getSubset's re-draws
+            int off = base_off + 5 * (f - base_it);
+            int d[5];
+            bool bad = false;
+            for (int i = 0; i < 5 && !bad; ++i) {
+                int v;
+                bool dup;
+                do {
+                    if (off >= len) {
+                        bad = true;
+                        break;
+                    }
+                    v = (int)((uint32_t)tab[off++] % (uint32_t)count);
+                    dup = false;
+                    for (int j = 0; j < i; ++j) dup |= d[j] == v;
+                } while (dup);
+                d[i] = v;
+            }
+            if (!bad)
+                for (int i = 0; i < 5; ++i) idx[5 * f + i] = d[i];
+            s_bad = bad ? 1 : 0;
+            s_base_it = f + 1;
+            s_base_off = off;
+        }
+        __syncthreads();
+        if (s_bad) {
+            if (tid == 0) subsets_sequential(P, st, idx, count, ~0ull, 0, end);
+            return;
+        }
+        base_it = s_base_it;
+        base_off = s_base_off;
+        __syncthreads();  // s_red / s_base_* are rewritten by the next pass
+    }
 }
 
 // The five-point models of a round.  kGroup (workspaces of <= kEssWidePairs lists, latency): a 64-lane workgroup
@@ -934,8 +1057,7 @@ __global__ __launch_bounds__(64) void rp_count_kernel(const float* __restrict__ 
     cv_jacobi_svd<4>(At, w, V);
     const double Q0 = V[12], Q1 = V[13], Q2 = V[14], Q3 = V[15];
     bool ok = Q2 * Q3 > 0;
-    const fp64::Rcp64 rq(Q3);
-    const double X[4] = {rq.div(Q0), rq.div(Q1), rq.div(Q2), rq.div(Q3)};
+    const double X[4] = {Q0 / Q3, Q1 / Q3, Q2 / Q3, Q3 / Q3};
     ok = (X[2] < dist) && ok;
     double z = 0;
 #pragma unroll
@@ -986,7 +1108,10 @@ void launch_find_essential(const EssParams& P, const EssRun& r, const float* pts
     thr /= (r.focal + r.focal) / 2;
     const float t = (float)(thr * thr);
     for (int c0 = 0; c0 < iters; c0 += P.chunk) {
-        hipLaunchKernelGGL(ess::ess_subsets_kernel, dim3((n_pairs + 63) / 64), dim3(64), 0, s, n_pairs, P, c0, iters);
+        if (c0 == 0 && P.rng_tab && P.chunk >= iters)  // the whole budget in one wide round: parallel draws
+            hipLaunchKernelGGL(ess::ess_subsets_par_kernel, dim3(n_pairs), dim3(256), 0, s, P, iters);
+        else
+            hipLaunchKernelGGL(ess::ess_subsets_kernel, dim3((n_pairs + 63) / 64), dim3(64), 0, s, n_pairs, P, c0, iters);
         if (P.chunk == kEssChunkWide)  // few lists: the latency form
             hipLaunchKernelGGL(ess::ess_models_kernel<true>,
                                dim3((P.chunk + ess::kModelIters - 1) / ess::kModelIters, n_pairs), dim3(64), 0, s, P, c0);

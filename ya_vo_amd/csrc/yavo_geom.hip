@@ -23,7 +23,6 @@
 
 #include "yavo_internal.h"
 #include "yavo_cvsvd.h"
-#include "yavo_fp64.h"
 #include "yavo_se3.h"
 #include "yavo_xlane.h"
 
@@ -414,12 +413,11 @@ __device__ __forceinline__ JRot make_jacobi(double x, double y, double z) {
         r.c = 1; r.s = 0;
         return r;
     }
-    // divisions and square roots in yavo_fp64.h's forms (the operators' results, shorter for mid-range operands)
-    double tau = fp64::div(x - z, deno);
-    double w = fp64::sqrt(tau * tau + 1);
-    double t = fp64::rcp(tau > 0 ? tau + w : tau - w);
+    double tau = (x - z) / deno;
+    double w = sqrt(tau * tau + 1);
+    double t = tau > 0 ? 1 / (tau + w) : 1 / (tau - w);
     double sign_t = t > 0 ? 1 : -1;
-    double nn = fp64::rcp(fp64::sqrt(t * t + 1));
+    double nn = 1 / sqrt(t * t + 1);
     // Eigen's y / |y|: exactly +-1 here (2|y| >= DBL_MIN, and the inputs are finite and scaled to <= 1), so the
     // sign is taken instead of an FP64 division (one of the seven per rotation); the products are unchanged
     r.s = -sign_t * copysign(1.0, y) * fabs(t) * nn;
@@ -440,11 +438,8 @@ __device__ bool eigen_jacobi_svd4(const double (&Ain)[16], double (&sv)[4], doub
     }
     if (!isfinite(scale)) return false;
     if (scale == 0) scale = 1;
-    {
-        const fp64::Rcp64 rs(scale);  // one refined reciprocal for the 16 divisions
 #pragma unroll
-        for (int i = 0; i < 16; ++i) Wk[i] = rs.div(Ain[i]);
-    }
+    for (int i = 0; i < 16; ++i) Wk[i] = Ain[i] / scale;
 #pragma unroll
     for (int i = 0; i < 16; ++i) V[i] = (i % 5 == 0) ? 1.0 : 0.0;
     const double considerAsZero = DBL_MIN, precision = 2 * DBL_EPSILON;
@@ -474,11 +469,10 @@ __device__ bool eigen_jacobi_svd4(const double (&Ain)[16], double (&sv)[4], doub
                     if (fabs(d) < DBL_MIN) {
                         rot1.s = 0; rot1.c = 1;
                     } else {
-                        double u = fp64::div(t, d);
-                        double tmp = fp64::sqrt(1 + u * u);
-                        const fp64::Rcp64 rt(tmp);
-                        rot1.s = rt.div(1.0);
-                        rot1.c = rt.div(u);
+                        double u = t / d;
+                        double tmp = sqrt(1 + u * u);
+                        rot1.s = 1 / tmp;
+                        rot1.c = u / tmp;
                     }
                     if (!(rot1.c == 1 && rot1.s == 0)) {
                         double a0 = m00, b0 = m10, a1 = m01, b1 = m11;
@@ -554,9 +548,8 @@ __device__ bool eigen_jacobi_svd4(const double (&Ain)[16], double (&sv)[4], doub
 __device__ bool triangulate_px(int x1, int y1, int x2, int y2, const double* Ta, const double* Tb,
                                const double* K, double* Xo) {
     const double K0 = K[0], K2 = K[2], K4 = K[4], K5 = K[5];
-    const fp64::Rcp64 r0(K0), r4(K4);
-    const double pa[2] = {r0.div(((double)x1 - K2) * 1.0), r4.div(((double)y1 - K5) * 1.0)};
-    const double pb[2] = {r0.div(((double)x2 - K2) * 1.0), r4.div(((double)y2 - K5) * 1.0)};
+    const double pa[2] = {((double)x1 - K2) * 1.0 / K0, ((double)y1 - K5) * 1.0 / K4};
+    const double pb[2] = {((double)x2 - K2) * 1.0 / K0, ((double)y2 - K5) * 1.0 / K4};
     double A[16];
 #pragma unroll
     for (int v = 0; v < 2; ++v) {
@@ -579,11 +572,10 @@ __device__ bool triangulate_px(int x1, int y1, int x2, int y2, const double* Ta,
     double X0 = NAN, X1 = NAN, X2 = NAN;
     bool s = false;
     if (eigen_jacobi_svd4(A, sv, V)) {
-        const fp64::Rcp64 rw(V[3 + 12]);
-        X0 = rw.div(V[0 + 12]);
-        X1 = rw.div(V[1 + 12]);
-        X2 = rw.div(V[2 + 12]);
-        s = fp64::div(sv[3], sv[2]) < 1e-2;
+        X0 = V[0 + 12] / V[3 + 12];
+        X1 = V[1 + 12] / V[3 + 12];
+        X2 = V[2 + 12] / V[3 + 12];
+        s = sv[3] / sv[2] < 1e-2;
     }
     Xo[0] = X0;
     Xo[1] = X1;
@@ -600,6 +592,7 @@ __global__ __launch_bounds__(256) void triangulate_kernel(const yv_match* __rest
         good = triangulate_px(m[i].pt1.x, m[i].pt1.y, m[i].pt2.x, m[i].pt2.y, poses, poses + 7, K, Xw + 3 * i);
         ok[i] = good ? 1 : 0;
     }
+    if (!n_ok) return;  // the host counts ok[] (yv_triangulate)
     const uint64_t bal = __ballot(good);
     if ((threadIdx.x & 63) == 0 && bal) atomicAdd(n_ok, (int32_t)__popcll(bal));
 }
@@ -756,8 +749,7 @@ __device__ bool ldlt6_solve(const double* Hin, const double* b, double* x) {
 // of unpivoted LDLT on P H P^T: the permutation is resolved first, P H P^T's lower triangle is gathered
 // from LDS, and the factorization runs straight-line in registers.
 // Hf the full symmetric 6x6 (row-major), bs the right-hand side, xs the solution (all LDS); P b and P^T v are indexed
-// LDS accesses.  Divisions by D(k) (the column's five and the solve's one) share one refined reciprocal
-// (yavo_fp64.h: the operator's results).
+// LDS accesses.
 template <int variant>
 __device__ bool ldlt6_solve_lds(const double* Hf, double lambda, const double* bs, double* xs) {
     constexpr int n = 6;
@@ -807,7 +799,6 @@ __device__ bool ldlt6_solve_lds(const double* Hf, double lambda, const double* b
     }
     int sign = 0;
     int found_zero_pivot = 0;
-    fp64::Rcp64 rk[6];  // D(k)'s refined reciprocal (set by the factorization)
     if (!zero0) {
 #pragma unroll
         for (int k = 0; k < n; ++k) {
@@ -836,10 +827,9 @@ __device__ bool ldlt6_solve_lds(const double* Hf, double lambda, const double* b
             }
             const double akk = m[k * 7];
             const int valid = fabs(akk) > 0;
-            rk[k] = fp64::Rcp64(akk);
             if (k + 1 < n && valid) {
 #pragma unroll
-                for (int i = k + 1; i < n; ++i) m[i * 6 + k] = rk[k].div(m[i * 6 + k]);
+                for (int i = k + 1; i < n; ++i) m[i * 6 + k] /= akk;
             }
             if (!(found_zero_pivot && valid) && !valid) found_zero_pivot = 1;
             if (sign == 1) { if (akk < 0) sign = 3; }
@@ -857,7 +847,7 @@ __device__ bool ldlt6_solve_lds(const double* Hf, double lambda, const double* b
         for (int i = j + 1; i < n; ++i) v[i] = v[i] - m[i * 6 + j] * v[j];
 #pragma unroll
     for (int i = 0; i < n; ++i) {
-        if (fabs(m[i * 7]) > DBL_MIN) v[i] = zero0 ? v[i] / m[i * 7] : rk[i].div(v[i]);
+        if (fabs(m[i * 7]) > DBL_MIN) v[i] /= m[i * 7];
         else v[i] = 0;
     }
 #pragma unroll
@@ -877,9 +867,8 @@ __device__ __forceinline__ void edge_error_pc(const double* pc, const double* K,
     double u0 = K[0] * pc[0] + K[1] * pc[1] + K[2] * pc[2];
     double u1 = K[3] * pc[0] + K[4] * pc[1] + K[5] * pc[2];
     double u2 = K[6] * pc[0] + K[7] * pc[1] + K[8] * pc[2];
-    const fp64::Rcp64 ru(u2);  // yavo_fp64.h: u0 / u2 and u1 / u2 exactly, one refined reciprocal
-    e[0] = meas[0] - ru.div(u0);
-    e[1] = meas[1] - ru.div(u1);
+    e[0] = meas[0] - u0 / u2;
+    e[1] = meas[1] - u1 / u2;
 }
 
 __device__ __forceinline__ void edge_error(const double* T, const double* K, const double* X, const double* meas,
@@ -894,7 +883,7 @@ __device__ __forceinline__ void edge_error(const double* T, const double* K, con
 __device__ __forceinline__ void edge_jacobian_pc(const double* pc, const double* K, double* J) {
     double fx = K[0], fy = K[4];
     double x = pc[0], y = pc[1], z = pc[2];
-    double zinv = fp64::rcp(z + 1e-18);
+    double zinv = 1.0 / (z + 1e-18);
     double zinv2 = zinv * zinv;
     J[0] = -fx * zinv; J[1] = 0; J[2] = fx * x * zinv2; J[3] = fx * x * y * zinv2;
     J[4] = -fx - fx * x * x * zinv2; J[5] = fx * y * zinv;
@@ -1745,35 +1734,6 @@ void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, con
 }
 
 }  // namespace yavo
-
-namespace yavo {
-namespace geom {
-// yavo_fp64.h against the compiler's operators, element by element (tests/test_gpu_fp64.py)
-__global__ void fp64_check_kernel(const double* __restrict__ a, const double* __restrict__ b, int n,
-                                  double* __restrict__ out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const double x = a[i], y = b[i];
-    double* o = out + 8 * (int64_t)i;
-    o[0] = fp64::div(x, y);
-    o[1] = x / y;
-    o[2] = fp64::rcp(y);
-    o[3] = 1.0 / y;
-    o[4] = fp64::sqrt(x);
-    o[5] = ::sqrt(x);
-    o[6] = fp64::Rcp64(y).div(x);
-    o[7] = (double)(fp64::mid(x) && fp64::mid(y)) + 2.0 * (double)fp64::sqrt_ok(x);  // which path ran
-}
-}  // namespace geom
-}  // namespace yavo
-
-extern "C" int yv_debug_fp64(const double* d_a, const double* d_b, int n, double* d_out /* [n][8] */, void* stream) {
-    if (!d_a || !d_b || !d_out || n < 0) return -1;
-    if (n == 0) return 0;
-    hipLaunchKernelGGL(yavo::geom::fp64_check_kernel, dim3((n + 255) / 256), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), d_a, d_b, n, d_out);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-}
 
 extern "C" int yv_lm_sum_mode(void) { return yavo::geom::lm_mode_of(yavo::geom::kLMThreads); }
 

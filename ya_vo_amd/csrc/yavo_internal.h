@@ -162,6 +162,10 @@ struct EssParams {
     double* best = nullptr;    // [max_pairs][9]
     double* cand = nullptr;    // [max_pairs][4][12] recoverPose candidates P1..P4
     int32_t* cgood = nullptr;  // [max_pairs][4]
+    // cv::RNG((uint64)-1)'s states after 1 .. rng_len draws (list-independent: every list's round 0 starts there), for
+    // the parallel subset draws of wide rounds (ess_subsets_par_kernel); null for narrow rounds
+    uint64_t* rng_tab = nullptr;
+    int rng_len = 0;
 };
 struct EssRun {
     double focal, ppx, ppy, prob, threshold;

@@ -5,8 +5,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include "yavo_fp64.h"
-
 namespace yavo {
 namespace se3 {
 
@@ -92,7 +90,7 @@ __device__ __forceinline__ void se3_mul(const double* A, const double* B, double
     quat_mul(A, B, q);
     double sn = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
     if (sn != 1.0) {
-        double sc = fp64::div(2.0, 1.0 + sn);
+        double sc = 2.0 / (1.0 + sn);
         for (int i = 0; i < 4; ++i) q[i] *= sc;
     }
     out[0] = q[0]; out[1] = q[1]; out[2] = q[2]; out[3] = q[3];
@@ -110,9 +108,9 @@ __device__ void se3_exp(const double* a, double* out) {
         imag = 0.5 - (1.0 / 48.0) * theta_sq + (1.0 / 3840.0) * theta_po4;
         real = 1 - (1.0 / 8.0) * theta_sq + (1.0 / 384.0) * theta_po4;
     } else {
-        theta = fp64::sqrt(theta_sq);  // yavo_fp64.h: the operators' results
+        theta = sqrt(theta_sq);
         double half = 0.5 * theta;
-        imag = fp64::div(k_sin(half), theta);
+        imag = k_sin(half) / theta;
         real = k_cos(half);
     }
     double q[4] = {imag * om[0], imag * om[1], imag * om[2], real};
@@ -124,8 +122,8 @@ __device__ void se3_exp(const double* a, double* out) {
         quat_to_R(q, V);
     } else {
         double theta_sq2 = theta * theta;
-        double a1 = fp64::div(1 - k_cos(theta), theta_sq2);
-        double a2 = fp64::div(theta - k_sin(theta), theta_sq2 * theta);
+        double a1 = (1 - k_cos(theta)) / theta_sq2;
+        double a2 = (theta - k_sin(theta)) / (theta_sq2 * theta);
         for (int i = 0; i < 9; ++i) V[i] = ((i % 4 == 0) ? 1.0 : 0.0) + a1 * O[i] + a2 * O2[i];
     }
     out[0] = q[0]; out[1] = q[1]; out[2] = q[2]; out[3] = q[3];
