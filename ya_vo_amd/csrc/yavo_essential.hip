@@ -352,6 +352,56 @@ __device__ __forceinline__ void bcast_one(int k, double xr, double xi, double& k
     }
 }
 
+// One Gauss-Seidel sweep of the group (see dk_group).  kSel: solvePoly's skip of a factor whose roots coincide, as a
+// select; otherwise every factor is multiplied and `hit` reports whether a coincidence occurred in this lane.
+template <int NN, bool kSel>
+__device__ __forceinline__ void dk_sweep(const double* cr, int r, bool own, double& xr, double& xi, bool& moved,
+                                         double& an2, bool& hit) {
+    double ox[NN], oy[NN];
+    bcast_all<NN>(xr, xi, ox, oy);
+    const double pr = xr, pi = xi;
+    double nr = cr[NN], ni = 0.0, dr = cr[NN], di = 0.0;
+#pragma unroll
+    for (int j = 0; j < NN; j++) {
+        const double tr = nr * pr - ni * pi, ti = nr * pi + ni * pr;
+        nr = tr + cr[NN - j - 1];
+        ni = ti + 0.0;
+    }
+    moved = false;
+    an2 = 0;
+    hit = false;
+    auto factor = [&](double xj, double yj) {
+        const bool same = pr == xj && pi == yj;
+        const double sr = pr - xj, si = pi - yj;
+        const double ur = dr * sr - di * si, ui = dr * si + di * sr;
+        if (kSel) {
+            dr = same ? dr : ur;
+            di = same ? di : ui;
+        } else {
+            hit |= same;
+            dr = ur;
+            di = ui;
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < NN; ++k) {
+        if (r == k) {
+#pragma unroll
+            for (int j = k + 1; j < NN; ++j) factor(ox[j], oy[j]);
+            const double t = 1. / (dr * dr + di * di);
+            const double qr = (nr * dr + ni * di) * t, qi = (-nr * di + ni * dr) * t;
+            xr = pr - qr;
+            xi = pi - qi;
+            moved = __double_as_longlong(xr) != __double_as_longlong(pr) ||
+                    __double_as_longlong(xi) != __double_as_longlong(pi);
+            an2 = qr * qr + qi * qi;
+        }
+        double kr, ki;
+        bcast_one<NN>(k, xr, xi, kr, ki);
+        if (r > k && own) factor(kr, ki);
+    }
+}
+
 template <int NN>
 __device__ int dk_group(const double* c, int r, int base, uint64_t gmask, double& rre, double& rim) {
     double cr[NN + 1];
@@ -377,46 +427,17 @@ __device__ int dk_group(const double* c, int r, int base, uint64_t gmask, double
     int sweeps = 0;
     for (int iter = 0; iter < 300; iter++) {
         ++sweeps;
-        double ox[NN], oy[NN];
-        bcast_all<NN>(xr, xi, ox, oy);
-        const double pr = xr, pi = xi;
-        double nr = cr[NN], ni = 0.0, dr = cr[NN], di = 0.0;
-#pragma unroll
-        for (int j = 0; j < NN; j++) {
-            const double tr = nr * pr - ni * pi, ti = nr * pi + ni * pr;
-            nr = tr + cr[NN - j - 1];
-            ni = ti + 0.0;
-        }
-        bool moved = false;
+        // the sweep without solvePoly's coincident-root skip (a select per factor); a coincidence anywhere in the group
+        // is seen by its first occurrence, before which both forms computed the same values, and the sweep then runs
+        // again from the same roots with the skip
+        const double xr0 = xr, xi0 = xi;
+        bool moved = false, hit = false;
         double an2 = 0;
-#pragma unroll
-        for (int k = 0; k < NN; ++k) {
-            if (r == k) {
-#pragma unroll
-                for (int j = k + 1; j < NN; ++j) {
-                    const bool same = pr == ox[j] && pi == oy[j];
-                    const double sr = pr - ox[j], si = pi - oy[j];
-                    const double ur = dr * sr - di * si, ui = dr * si + di * sr;
-                    dr = same ? dr : ur;
-                    di = same ? di : ui;
-                }
-                const double t = 1. / (dr * dr + di * di);
-                const double qr = (nr * dr + ni * di) * t, qi = (-nr * di + ni * dr) * t;
-                xr = pr - qr;
-                xi = pi - qi;
-                moved = __double_as_longlong(xr) != __double_as_longlong(pr) ||
-                        __double_as_longlong(xi) != __double_as_longlong(pi);
-                an2 = qr * qr + qi * qi;
-            }
-            double kr, ki;
-            bcast_one<NN>(k, xr, xi, kr, ki);
-            if (r > k && own) {
-                const bool same = pr == kr && pi == ki;
-                const double sr = pr - kr, si = pi - ki;
-                const double ur = dr * sr - di * si, ui = dr * si + di * sr;
-                dr = same ? dr : ur;
-                di = same ? di : ui;
-            }
+        dk_sweep<NN, false>(cr, r, own, xr, xi, moved, an2, hit);
+        if (__ballot(own && hit) & gmask) {
+            xr = xr0;
+            xi = xi0;
+            dk_sweep<NN, true>(cr, r, own, xr, xi, moved, an2, hit);
         }
         // OpenCV stops when the largest |update| is 0 (an2 > 0 iff |q| > 0; NaN compares false); a sweep that moved no
         // root is a fixed point (every later sweep repeats it), so stopping there gives the 300-sweep roots too
