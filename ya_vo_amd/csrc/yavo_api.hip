@@ -1772,9 +1772,12 @@ int yv_calc_optical_flow_pyr_lk(yv_ctx* ctx, const uint8_t* prev, const uint8_t*
             for (int r = 0; r < H; ++r) std::memcpy(h + (size_t)r * W, img + (size_t)r * stride, (size_t)W);
         return hipMemcpyAsync(ctx->lk_img_d + slot * pitch, h, (size_t)pitch, hipMemcpyHostToDevice, s);
     };
-    const bool reuse = ctx->lk_last >= 0 && same_image(prev, ctx->lk_img_h + ctx->lk_last * pitch);
-    const int ps = reuse ? ctx->lk_last : 0, ns = 1 - ps;
+    // next goes to the slot the previous call's next is not in; its upload runs while prev is compared with that one
+    const int ns = ctx->lk_last >= 0 ? 1 - ctx->lk_last : 1, ps = 1 - ns;
+    const bool had = ctx->lk_last >= 0;
     ctx->lk_last = -1;  // until this call has completed
+    if (put_image(next, ns) != hipSuccess) return YV_ERR_HIP;
+    const bool reuse = had && same_image(prev, ctx->lk_img_h + ps * pitch);
     Arena a{ctx};
     float *dpts, *dnext, *derr;
     int32_t *dpair, *dcnt;
@@ -1791,8 +1794,7 @@ int yv_calc_optical_flow_pyr_lk(yv_ctx* ctx, const uint8_t* prev, const uint8_t*
     a.in(dpts, prev_pts, sizeof(float) * 2 * n);
     a.in(dpair, pair, 2 * sizeof(int32_t));
     a.in(dcnt, pair + 2, sizeof(int32_t));
-    if ((!reuse && put_image(prev, ps) != hipSuccess) || put_image(next, ns) != hipSuccess || a.upload(s) != hipSuccess)
-        return YV_ERR_HIP;
+    if ((!reuse && put_image(prev, ps) != hipSuccess) || a.upload(s) != hipSuccess) return YV_ERR_HIP;
     yavo::LkParams& P = lk->P;
     P.img0 = ctx->lk_img_d;
     P.stride0 = W;

@@ -258,6 +258,55 @@ __device__ void em_det_poly(const double* B, double* c) {
 // (OpenCV skips its factor) is a select, not a branch.  OpenCV stops when the largest |update| is 0; |q| > 0 exactly
 // when qr^2 + qi^2 > 0 (NaN compares false either way), so the squared magnitude decides without the square root; a
 // sweep that moved no root is a fixed point (every later sweep repeats it).  Returns the sweeps run.
+// One sweep of dk_solve.  kSel: solvePoly's skip of a coincident root's factor, as a select; otherwise every factor is
+// multiplied and `hit` reports a coincidence (the sweep is then run again from the same roots with the skip).
+template <int NN, bool kSel>
+__device__ __forceinline__ void dk_solve_sweep(const double* cr, double* xr, double* xi, bool& moved, double& maxDiff2,
+                                               bool& hit) {
+    maxDiff2 = 0;
+    moved = false;
+    hit = false;
+#pragma unroll
+    for (int i = 0; i < NN; i++) {
+        const double pr = xr[i], pi = xi[i];
+        double nr = cr[NN], ni = 0.0, dr = cr[NN], di = 0.0;
+#pragma unroll
+        for (int j = 0; j < NN; j++) {
+            const double tr = nr * pr - ni * pi, ti = nr * pi + ni * pr;
+            nr = tr + cr[NN - j - 1];
+            ni = ti + 0.0;
+            if (j != i) {
+                const bool same = pr == xr[j] && pi == xi[j];
+                const double sr = pr - xr[j], si = pi - xi[j];
+                const double ur = dr * sr - di * si, ui = dr * si + di * sr;
+                if (kSel) {
+                    dr = same ? dr : ur;
+                    di = same ? di : ui;
+                } else {
+                    hit |= same;
+                    dr = ur;
+                    di = ui;
+                }
+            }
+        }
+        const double t = 1. / (dr * dr + di * di);
+        const double qr = (nr * dr + ni * di) * t, qi = (-nr * di + ni * dr) * t;
+        xr[i] = pr - qr;
+        xi[i] = pi - qi;
+        moved |= __double_as_longlong(xr[i]) != __double_as_longlong(pr) ||
+                 __double_as_longlong(xi[i]) != __double_as_longlong(pi);
+        const double an2 = qr * qr + qi * qi;
+        maxDiff2 = maxDiff2 < an2 ? an2 : maxDiff2;
+    }
+}
+
+// cv::solvePoly (Durand-Kerner) of degree NN (the coefficients above NN were trimmed) on one lane; rre / rim [10].
+// Every loop is unrolled (NN is a template constant), so j != i is resolved at compile time and a coincident root
+// (OpenCV skips its factor) is a select, not a branch.  (The group form's replay-on-coincidence does not pay here:
+// with 64 independent lanes a wave replays whenever any lane meets a coincidence -- 256 lists 2.75 -> 3.03 ms.)
+// OpenCV stops when the largest |update| is 0; |q| > 0 exactly when qr^2 + qi^2 > 0 (NaN compares false either way),
+// so the squared magnitude decides without the square root; a sweep that moved no root is a fixed point (every later
+// sweep repeats it).  Returns the sweeps run.
 template <int NN>
 __device__ int dk_solve(const double* c, double* rre, double* rim) {
     double cr[NN + 1], xr[NN], xi[NN];
@@ -278,34 +327,9 @@ __device__ int dk_solve(const double* c, double* rre, double* rim) {
     int sweeps = 0;
     for (int iter = 0; iter < 300; iter++) {
         ++sweeps;
-        double maxDiff2 = 0;
-        bool moved = false;
-#pragma unroll
-        for (int i = 0; i < NN; i++) {
-            const double pr = xr[i], pi = xi[i];
-            double nr = cr[NN], ni = 0.0, dr = cr[NN], di = 0.0;
-#pragma unroll
-            for (int j = 0; j < NN; j++) {
-                const double tr = nr * pr - ni * pi, ti = nr * pi + ni * pr;
-                nr = tr + cr[NN - j - 1];
-                ni = ti + 0.0;
-                if (j != i) {
-                    const bool same = pr == xr[j] && pi == xi[j];
-                    const double sr = pr - xr[j], si = pi - xi[j];
-                    const double ur = dr * sr - di * si, ui = dr * si + di * sr;
-                    dr = same ? dr : ur;
-                    di = same ? di : ui;
-                }
-            }
-            const double t = 1. / (dr * dr + di * di);
-            const double qr = (nr * dr + ni * di) * t, qi = (-nr * di + ni * dr) * t;
-            xr[i] = pr - qr;
-            xi[i] = pi - qi;
-            moved |= __double_as_longlong(xr[i]) != __double_as_longlong(pr) ||
-                     __double_as_longlong(xi[i]) != __double_as_longlong(pi);
-            const double an2 = qr * qr + qi * qi;
-            maxDiff2 = maxDiff2 < an2 ? an2 : maxDiff2;
-        }
+        bool moved, hit;
+        double maxDiff2;
+        dk_solve_sweep<NN, true>(cr, xr, xi, moved, maxDiff2, hit);
         if (maxDiff2 <= 0 || !moved) break;
     }
 #pragma unroll
