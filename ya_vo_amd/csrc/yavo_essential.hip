@@ -169,9 +169,31 @@ __device__ void em_coeff_mat(const double* EE, double* A) {
     for (int q = 0; q < 20; ++q) row[q] = c0[q] - c1[q] + c2[q];
 }
 
+// every lane gets lane j's v in out[j] (j < N) of its 16-lane row
+template <int N, int J = 0>
+__device__ __forceinline__ void bcast_col(double v, double* out) {
+    if constexpr (J < N) {
+        out[J] = xl::row_bcast_f64<J>(v);
+        bcast_col<N, J + 1>(v, out);
+    }
+}
+// every lane gets lane `from`'s row[0 .. N) (from: a loop counter the compiler unrolls)
+template <int N, int J = 0>
+__device__ __forceinline__ void bcast_row_from(int from, const double* row, double* out) {
+    if constexpr (J < N) {
+        if (from == J) {
+#pragma unroll
+            for (int q = 0; q < N; ++q) out[q] = xl::row_bcast_f64<J>(row[q]);
+        } else {
+            bcast_row_from<N, J + 1>(from, row, out);
+        }
+    }
+}
+
 // cv::invert(DECOMP_LU), n = 10: LUImpl<double> with b = I, eps = 100 DBL_EPSILON, zeros when singular.
-// A: 10 rows of stride 20 (the first 10 columns are inverted).
-__device__ void lu_inverse10(const double* A, double* inv) {
+// A: 10 rows of stride 20 (the first 10 columns are inverted).  Only rows first .. 9 of the inverse are formed (the
+// back substitution of row i reads rows > i alone; runKernel uses rows 4 .. 9); the others are left as they are.
+__device__ void lu_inverse10(const double* A, double* inv, int first = 0) {
     constexpr int n = 10;
     double a[100], b[100];
     for (int i = 0; i < n; ++i)
@@ -199,13 +221,105 @@ __device__ void lu_inverse10(const double* A, double* inv) {
             for (int q = 0; q < n; q++) b[j * n + q] += alpha * b[i * n + q];
         }
     }
-    for (int i = n - 1; i >= 0; i--)
+    for (int i = n - 1; i >= first; i--)
         for (int j = 0; j < n; j++) {
             double s = b[i * n + j];
             for (int q = i + 1; q < n; q++) s -= a[i * n + q] * b[q * n + j];
             b[i * n + j] = s / a[i * n + i];
         }
-    for (int q = 0; q < n * n; ++q) inv[q] = b[q];
+    for (int q = first * n; q < n * n; ++q) inv[q] = b[q];
+}
+
+// The same LU inverse on a 10-lane group, lane r holding row r of a and b in registers: the pivot search is the
+// sequential scan over the column broadcast to every lane, row swaps exchange two lanes' rows, the pivot row is
+// broadcast (DPP) and every lower lane eliminates its own row -- each row's operations are the sequential code's, in
+// its order.  The back substitution forms rows 9 .. 4 (lane i, rows q > i broadcast as they become final).  Then lane
+// r's M row (r >= 4) = inv row r x A's right block; M4 gets rows 4 .. 9 in every lane.
+__device__ void lu_m_group(const double* A, int r, int base, double* M4 /* [6][10] */) {
+    constexpr int n = 10;
+    const int rr = r < n ? r : 0;
+    double a[n], b[n];
+#pragma unroll
+    for (int q = 0; q < n; ++q) {
+        a[q] = A[rr * 20 + q];
+        b[q] = q == r ? 1.0 : 0.0;
+    }
+    const double eps = DBL_EPSILON * 100;
+    bool singular = false;
+#pragma unroll
+    for (int i = 0; i < n; i++) {
+        if (singular) break;  // group-uniform
+        double col[n];
+        bcast_col<n>(a[i], col);
+        int k = i;
+        double vk = fabs(col[i]);
+#pragma unroll
+        for (int j = i + 1; j < n; j++)
+            if (fabs(col[j]) > vk) {
+                k = j;
+                vk = fabs(col[j]);
+            }
+        if (vk < eps) {
+            singular = true;
+            break;
+        }
+        if (k != i) {  // group-uniform: rows i and k trade lanes (columns i .. 9 of a, all of b)
+            const int src = base + (r == i ? k : (r == k ? i : r));
+#pragma unroll
+            for (int q = i; q < n; ++q) a[q] = __shfl(a[q], src, 64);
+#pragma unroll
+            for (int q = 0; q < n; ++q) b[q] = __shfl(b[q], src, 64);
+        }
+        double pa[n], pb[n];
+        bcast_row_from<n>(i, a, pa);
+        bcast_row_from<n>(i, b, pb);
+        const double d = -1 / pa[i];
+        if (r > i) {
+            const double alpha = a[i] * d;
+#pragma unroll
+            for (int q = i + 1; q < n; q++) a[q] += alpha * pa[q];
+#pragma unroll
+            for (int q = 0; q < n; q++) b[q] += alpha * pb[q];
+        }
+    }
+    if (singular) {
+#pragma unroll
+        for (int q = 0; q < n; ++q) b[q] = 0.0;
+    } else {
+#pragma unroll
+        for (int i = n - 1; i >= 4; i--) {
+            double sv[n];
+#pragma unroll
+            for (int j = 0; j < n; j++) sv[j] = b[j];
+#pragma unroll
+            for (int q = i + 1; q < n; q++) {
+                double bq[n];
+                bcast_row_from<n>(q, b, bq);
+#pragma unroll
+                for (int j = 0; j < n; j++) sv[j] -= a[q] * bq[j];
+            }
+            if (r == i) {
+#pragma unroll
+                for (int j = 0; j < n; j++) b[j] = sv[j] / a[i];
+            }
+        }
+    }
+    // M row r (r >= 4): sum over k of inv[r][k] * A[k][10 + j], k in order
+    double m[n];
+#pragma unroll
+    for (int j = 0; j < n; ++j) {
+        double s = 0;
+#pragma unroll
+        for (int k = 0; k < n; ++k) s += b[k] * A[k * 20 + 10 + j];
+        m[j] = s;
+    }
+#pragma unroll
+    for (int q = 4; q < n; ++q) {
+        double mq[n];
+        bcast_row_from<n>(q, m, mq);
+#pragma unroll
+        for (int j = 0; j < n; ++j) M4[(q - 4) * n + j] = mq[j];
+    }
 }
 
 template <int NP, int NQ>
@@ -535,19 +649,25 @@ __device__ int em_models(const double* q1, const double* q2, double* models, int
     double A[200];
     em_coeff_mat(EE, A);
     EP_MARK(1);
-    double inv[100], M[100];
-    lu_inverse10(A, inv);
-    for (int i = 0; i < 10; ++i)
-        for (int j = 0; j < 10; ++j) {
-            double s = 0;
-            for (int k = 0; k < 10; ++k) s += inv[i * 10 + k] * A[k * 20 + 10 + j];
-            M[i * 10 + j] = s;
-        }
+    // runKernel reads rows 4 .. 9 of M = inv(A[:, :10]) A[:, 10:] only (B below)
+    double M4[60];
+    if constexpr (kGroup) {
+        lu_m_group(A, r, base, M4);
+    } else {
+        double inv[100];
+        lu_inverse10(A, inv, 4);
+        for (int i = 4; i < 10; ++i)
+            for (int j = 0; j < 10; ++j) {
+                double s = 0;
+                for (int k = 0; k < 10; ++k) s += inv[i * 10 + k] * A[k * 20 + 10 + j];
+                M4[(i - 4) * 10 + j] = s;
+            }
+    }
     double B[39];
 #pragma unroll
     for (int i = 0; i < 3; i++) {
-        const double* a1 = M + (i * 2 + 4) * 10;
-        const double* a2 = M + (i * 2 + 5) * 10;
+        const double* a1 = M4 + (i * 2) * 10;
+        const double* a2 = M4 + (i * 2 + 1) * 10;
         double r1[13], r2[13];
 #pragma unroll
         for (int k = 0; k < 13; ++k) r1[k] = r2[k] = 0.0;

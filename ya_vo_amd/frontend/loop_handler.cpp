@@ -533,7 +533,13 @@ void LoopHandler::setPipeline(int depth, int device, const std::vector<int8_t>& 
     pipeline_depth_ = depth > 0 ? depth : 0;
     pipeline_device_ = device;
     pipeline_offsets_ = briefOffsets;
+    if (pipeline_depth_ > 0) {
+        worker_dev_ = std::make_unique<Device>(device);
+        side_lane_ = std::make_unique<SideLane>(device);  // its thread makes its own context meanwhile
+    }
 }
+
+LoopHandler::~LoopHandler() = default;
 
 namespace {
 
@@ -642,10 +648,11 @@ void LoopHandler::runVOPipelined(int max_frames) {
     // PNG decoding (the reference's cv::imread) is the longest per-frame step on the host: the worker keeps the next
     // `readers` frames decoding on their own threads and consumes them in path-train order, so ids stay sequential
     const int readers = std::max(1, pipeline_readers_);
-    auto side = std::make_unique<SideLane>(pipeline_device_);
-    side_ = side.get();
+    if (!worker_dev_) worker_dev_ = std::make_unique<Device>(pipeline_device_);  // a second run: made again here
+    if (!side_lane_) side_lane_ = std::make_unique<SideLane>(pipeline_device_);
+    side_ = side_lane_.get();
     std::thread worker([&]() {
-        Device wdev(pipeline_device_);
+        Device& wdev = *worker_dev_;
         int st = wdev.ok() ? YV_OK : wdev.status();
         std::unique_ptr<FastDetector> wfd;
         std::unique_ptr<Brief> wbrief;
@@ -801,7 +808,7 @@ void LoopHandler::runVOPipelined(int max_frames) {
     cv_put.notify_all();
     worker.join();
     side_ = nullptr;
-    side.reset();  // runs what is still queued
+    side_lane_.reset();  // runs what is still queued
     resolvePendingF();
     t_features += worker_features;
     t_read += worker_read;  // in the pipelined loop: the worker waiting for the next decoded frame

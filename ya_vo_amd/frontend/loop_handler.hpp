@@ -93,6 +93,7 @@ public:
     // The reference's constructor (src/LoopHandler.cc:7-33).  `dev` may be null or without a GPU: config parsing,
     // the path train and frame reading still work (the accessors below), the VO steps fail.
     LoopHandler(const std::string& config, Device* dev);
+    ~LoopHandler();
     bool ok() const { return ok_; }
     const std::string& error() const { return error_; }
 
@@ -176,6 +177,10 @@ private:
         double seconds = 0;
     };
     SideLane* side_ = nullptr;
+    // the pipelined loop's worker context and side lane, made by setPipeline (like the tracking thread's context,
+    // before the loop: a context costs a few ms of allocations and stream set-up)
+    std::unique_ptr<Device> worker_dev_;
+    std::unique_ptr<SideLane> side_lane_;
     std::vector<std::pair<size_t, std::future<FResult>>> pending_f_;
     void resolvePendingF();
 
