@@ -142,8 +142,9 @@ def test_loop_handler_matches_oracle_loop(tmp_path, oracle):
 @pytest.mark.gpu
 def test_loop_handler_pipelined_matches_oracle_loop(tmp_path, oracle):
     """The pipelined C++ LoopHandler (--pipeline 2: frame k + 1's read + detect + describe on a worker thread with its
-    own GPU context while frame k is tracked) over 60 synthetic mono frames with a reinitialisation at frame 40: the
-    trajectory and per-frame events equal the oracle loop's bit for bit."""
+    own GPU context while frame k is tracked; frame k + 1's LK on the side lane during frame k's pose LM) over 60
+    synthetic mono frames with a reinitialisation at frame 40: the trajectory and per-frame events equal the oracle
+    loop's bit for bit."""
     from loop_chain import EVENT_FIELDS, LoopChain
     from ya_vo_amd import scene
     n = 60
@@ -163,6 +164,7 @@ def test_loop_handler_pipelined_matches_oracle_loop(tmp_path, oracle):
     np.testing.assert_array_equal(gpu_events, ref_events)
     np.testing.assert_array_equal(gpu_poses, P)
     assert stats["init"] == 1 and stats["reinit"] >= 1 and stats["tracked"] >= 40
+    assert stats["lk_ahead_frames"] >= 1  # the look-ahead LK's rows were used (and matched the oracle above)
 
 
 @pytest.mark.gpu

@@ -79,7 +79,7 @@ def measure(n_frames=200, depth=2, readers=16, gpu_batch=32):
         }
     keep = ("frames", "seconds", "frames_per_s", "init", "tracked", "reinit", "seconds_read", "seconds_features",
             "seconds_init", "seconds_track", "seconds_reinit", "seconds_wait", "process_wall_s", "readers",
-            "gpu_decode_batch", "primitives_s")
+            "gpu_decode_batch", "primitives_s", "lk_ahead_frames", "lk_ahead_s")
     identical = {k: bool(P.shape == P0.shape and np.array_equal(P, P0)) for k, (_, P) in modes.items()}
     best = max(modes, key=lambda k: modes[k][0]["frames_per_s"])
     return {

@@ -164,6 +164,7 @@ void LoopHandler::insertFrameFeatures(const Frame::ptr& frame) {
 // :80-124
 void LoopHandler::addFrame(const Frame::ptr& frame) {
     currentFrame_ = frame;
+    lk_cur_ = std::move(lk_ahead_);
     ev_ = FrameEvent();
     ev_.frame = currentFrameId_;
     ev_.keypoints = (int)frame->keypoints.size();
@@ -180,6 +181,7 @@ void LoopHandler::addFrame(const Frame::ptr& frame) {
         t_track += now_s() - t0;
         ev_.kind = FrameEvent::TRACKED;
         if (!trackSuccess) {
+            dropLKAhead(lk_ahead_);  // its rows index the features reinitialize() replaces
             const double t1 = now_s();
             reinitialize();
             map->insertKeyFrame(currentFrame_);
@@ -190,6 +192,7 @@ void LoopHandler::addFrame(const Frame::ptr& frame) {
         if (reinitialize()) status_ = TRACKING;
         ev_.kind = FrameEvent::REINIT;
     }
+    dropLKAhead(lk_cur_);  // reads lastFrame_'s pixels
     // the previous frame's pixels and descriptors are not read again (the map keeps the frame for its pose)
     if (lastFrame_) {
         lastFrame_->data.clear();
@@ -390,6 +393,7 @@ bool LoopHandler::track() {
     const int goodInliers = trackLastFrame();
     ev_.tracked = goodInliers;
     if (goodInliers < 2) return false;
+    if (side_ && peek_next_) launchLKAhead();
     const int optimizedInliers = optimizePoseOnly();
     ev_.inliers = optimizedInliers;
     if (optimizedInliers < 100) return false;
@@ -440,10 +444,32 @@ int LoopHandler::trackLastFrame() {
     std::vector<float> next(2 * (size_t)n), err(n);
     std::vector<uint8_t> flowStatus(n);
     const double tl = now_s();
-    if (!gpu(yv_calc_optical_flow_pyr_lk(dev_->ctx(), lastFrame_->data.data(), currentFrame_->data.data(),
-                                         currentFrame_->rows, currentFrame_->cols, currentFrame_->cols, lastKpt.data(),
-                                         n, 11, 3, 30, 0.01, 0.001, next.data(), flowStatus.data(), err.data()),
-             "calcOpticalFlowPyrLK"))
+    bool have = false;
+    if (lk_cur_ && lk_cur_->last == lastFrame_ && lk_cur_->next == currentFrame_) {
+        LKAhead& a = *lk_cur_;
+        have = a.done.get() == YV_OK;
+        if (have) {
+            lk_ahead_seconds += a.seconds;
+            for (int i = 0; i < n && have; ++i) {
+                const int r = lastIndex[i] < (int)a.row_of.size() ? a.row_of[lastIndex[i]] : -1;
+                if (r < 0 || a.pts[2 * r] != lastKpt[2 * i] || a.pts[2 * r + 1] != lastKpt[2 * i + 1]) {
+                    have = false;  // not in the superset: the call below tracks the list itself
+                    break;
+                }
+                next[2 * i] = a.nxt[2 * r];
+                next[2 * i + 1] = a.nxt[2 * r + 1];
+                flowStatus[i] = a.status[r];
+                err[i] = a.err[r];
+            }
+        }
+        lk_cur_.reset();
+        if (have) ++lk_ahead_frames;
+    }
+    if (!have && !gpu(yv_calc_optical_flow_pyr_lk(dev_->ctx(), lastFrame_->data.data(), currentFrame_->data.data(),
+                                                  currentFrame_->rows, currentFrame_->cols, currentFrame_->cols,
+                                                  lastKpt.data(), n, 11, 3, 30, 0.01, 0.001, next.data(),
+                                                  flowStatus.data(), err.data()),
+                      "calcOpticalFlowPyrLK"))
         return 0;
     prim_.lk += now_s() - tl;
     int goodFeatures = 0;
@@ -458,6 +484,47 @@ int LoopHandler::trackLastFrame() {
         }
     }
     return goodFeatures;
+}
+
+void LoopHandler::launchLKAhead() {
+    const Frame::ptr nf = peek_next_();
+    if (!nf || nf->rows != currentFrame_->rows || nf->cols != currentFrame_->cols || nf->data.empty()) return;
+    auto a = std::make_shared<LKAhead>();
+    a->last = currentFrame_;
+    a->next = nf;
+    a->row_of.assign(currentFrame_->features.size(), -1);
+    int n = 0;
+    for (size_t i = 0; i < currentFrame_->features.size(); ++i) {
+        const Feature& f = currentFrame_->features[i];
+        if (!f.mapPoint.lock()) continue;
+        a->row_of[i] = n++;
+        a->pts.push_back((float)f.kp.y);  // trackLastFrame's Point2i(kp.y, kp.x)
+        a->pts.push_back((float)f.kp.x);
+    }
+    if (n == 0) return;
+    a->nxt.resize(2 * (size_t)n);
+    a->err.resize((size_t)n);
+    a->status.resize((size_t)n);
+    auto task = std::make_shared<std::packaged_task<int(Device&)>>([a, n](Device& d) {
+        const double t0 = now_s();
+        const int st = d.ok() ? yv_calc_optical_flow_pyr_lk(d.ctx(), a->last->data.data(), a->next->data.data(),
+                                                           a->last->rows, a->last->cols, a->last->cols, a->pts.data(),
+                                                           n, 11, 3, 30, 0.01, 0.001, a->nxt.data(), a->status.data(),
+                                                           a->err.data())
+                              : d.status();
+        a->seconds = now_s() - t0;
+        return st;
+    });
+    a->done = task->get_future();
+    side_->submit([task](Device& d) { (*task)(d); });
+    lk_ahead_ = std::move(a);
+}
+
+// a look-ahead no one will read: its call may still be reading the frames' pixels, so wait for it
+void LoopHandler::dropLKAhead(std::shared_ptr<LKAhead>& a) {
+    if (!a) return;
+    if (a->done.valid()) a->done.wait();
+    a.reset();
 }
 
 // :730-861: one pose vertex at the current pose, one projection edge per feature with a map point (measurement
@@ -651,6 +718,10 @@ void LoopHandler::runVOPipelined(int max_frames) {
     if (!worker_dev_) worker_dev_ = std::make_unique<Device>(pipeline_device_);  // a second run: made again here
     if (!side_lane_) side_lane_ = std::make_unique<SideLane>(pipeline_device_);
     side_ = side_lane_.get();
+    peek_next_ = [&]() -> Frame::ptr {
+        std::lock_guard<std::mutex> lk(mu);
+        return q.empty() ? nullptr : q.front().frame;
+    };
     std::thread worker([&]() {
         Device& wdev = *worker_dev_;
         int st = wdev.ok() ? YV_OK : wdev.status();
@@ -807,6 +878,9 @@ void LoopHandler::runVOPipelined(int max_frames) {
     }
     cv_put.notify_all();
     worker.join();
+    peek_next_ = nullptr;
+    dropLKAhead(lk_ahead_);
+    dropLKAhead(lk_cur_);
     side_ = nullptr;
     side_lane_.reset();  // runs what is still queued
     resolvePendingF();

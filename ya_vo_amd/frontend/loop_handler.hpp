@@ -21,6 +21,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <future>
 #include <map>
 #include <memory>
@@ -183,6 +184,29 @@ private:
     std::unique_ptr<SideLane> side_lane_;
     std::vector<std::pair<size_t, std::future<FResult>>> pending_f_;
     void resolvePendingF();
+    // pipelined loop: frame k + 1's pyramidal LK runs on the side lane during frame k's pose LM, over every frame-k
+    // feature holding a map point at that moment (a superset of what trackLastFrame(k + 1) tracks: the LM only drops
+    // map points, world2Camera only drops points).  LK tracks each point on its own, so the rows trackLastFrame(k + 1)
+    // takes are the values its own call would return.  Dropped when frame k reinitialises.
+    struct LKAhead {
+        Frame::ptr last, next;
+        std::vector<int> row_of;  // row per feature index of `last`, -1 without a map point
+        std::vector<float> pts, nxt, err;
+        std::vector<uint8_t> status;
+        std::future<int> done;
+        double seconds = 0;
+    };
+    std::function<Frame::ptr()> peek_next_;  // the pipelined loop's next queued frame, or nullptr
+    std::shared_ptr<LKAhead> lk_ahead_;      // launched during the current frame's LM, for the next frame
+    std::shared_ptr<LKAhead> lk_cur_;        // launched during the last frame's LM, for the current frame
+    void launchLKAhead();
+    void dropLKAhead(std::shared_ptr<LKAhead>& a);
+
+public:
+    int lk_ahead_frames = 0;  // tracked frames whose LK came from the side lane
+    double lk_ahead_seconds = 0;  // side-lane LK time, summed (beside the tracking thread)
+
+private:
 
     bool gpu(int st, const char* what);
     void runVOPipelined(int max_frames);

@@ -141,7 +141,8 @@ int main(int argc, char** argv) {
               << ", \"pose_lm\": " << lh.primitiveTimes().pose_lm << ", \"match_reinit\": " << lh.primitiveTimes().match
               << ", \"f_ransac\": " << lh.primitiveTimes().f_ransac
               << ", \"find_essential\": " << lh.primitiveTimes().find_essential
-              << ", \"recover_pose\": " << lh.primitiveTimes().recover_pose << "}}"
+              << ", \"recover_pose\": " << lh.primitiveTimes().recover_pose << "}"
+              << ", \"lk_ahead_frames\": " << lh.lk_ahead_frames << ", \"lk_ahead_s\": " << lh.lk_ahead_seconds << "}"
               << std::endl;
     return 0;
 }
