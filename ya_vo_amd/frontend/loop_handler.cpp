@@ -393,8 +393,7 @@ bool LoopHandler::track() {
     const int goodInliers = trackLastFrame();
     ev_.tracked = goodInliers;
     if (goodInliers < 2) return false;
-    if (side_ && peek_next_) launchLKAhead();
-    const int optimizedInliers = optimizePoseOnly();
+    const int optimizedInliers = optimizePoseOnly(side_ && peek_next_);
     ev_.inliers = optimizedInliers;
     if (optimizedInliers < 100) return false;
     relativeMotion = se3::mul(currentFrame_->pose, se3::inverse(lastFrame_->pose));
@@ -475,7 +474,7 @@ int LoopHandler::trackLastFrame() {
     int goodFeatures = 0;
     for (int i = 0; i < n; ++i) {
         if (flowStatus[i] != 1) continue;
-        if (auto mp = lastFrame_->features[lastIndex[i]].mapPoint.lock()) {
+        if (const MapPoint::ptr& mp = lastMps[i]) {  // locked above; nothing has released it since
             Feature f;
             f.kp = Point{trunc_int(next[2 * i + 1]), trunc_int(next[2 * i])};  // Point2i(currFrameKpt.y, .x)
             f.mapPoint = mp;
@@ -486,22 +485,22 @@ int LoopHandler::trackLastFrame() {
     return goodFeatures;
 }
 
-void LoopHandler::launchLKAhead() {
+void LoopHandler::launchLKAhead(const std::vector<int>& fi) {
     const Frame::ptr nf = peek_next_();
     if (!nf || nf->rows != currentFrame_->rows || nf->cols != currentFrame_->cols || nf->data.empty()) return;
+    const int n = (int)fi.size();
+    if (n == 0) return;
     auto a = std::make_shared<LKAhead>();
     a->last = currentFrame_;
     a->next = nf;
     a->row_of.assign(currentFrame_->features.size(), -1);
-    int n = 0;
-    for (size_t i = 0; i < currentFrame_->features.size(); ++i) {
-        const Feature& f = currentFrame_->features[i];
-        if (!f.mapPoint.lock()) continue;
-        a->row_of[i] = n++;
-        a->pts.push_back((float)f.kp.y);  // trackLastFrame's Point2i(kp.y, kp.x)
-        a->pts.push_back((float)f.kp.x);
+    a->pts.resize(2 * (size_t)n);
+    for (int r = 0; r < n; ++r) {
+        const Feature& f = currentFrame_->features[fi[r]];
+        a->row_of[fi[r]] = r;
+        a->pts[2 * r] = (float)f.kp.y;  // trackLastFrame's Point2i(kp.y, kp.x)
+        a->pts[2 * r + 1] = (float)f.kp.x;
     }
-    if (n == 0) return;
     a->nxt.resize(2 * (size_t)n);
     a->err.resize((size_t)n);
     a->status.resize((size_t)n);
@@ -529,7 +528,7 @@ void LoopHandler::dropLKAhead(std::shared_ptr<LKAhead>& a) {
 
 // :730-861: one pose vertex at the current pose, one projection edge per feature with a map point (measurement
 // (kp.x, kp.y), Huber), 4 rounds of optimize(10) with chi2 > 5.991 outliers; outliers lose their map point
-int LoopHandler::optimizePoseOnly() {
+int LoopHandler::optimizePoseOnly(bool lk_ahead) {
     std::vector<int> fi;
     std::vector<double> X, uv;
     for (int i = 0; i < (int)currentFrame_->features.size(); ++i) {
@@ -542,6 +541,7 @@ int LoopHandler::optimizePoseOnly() {
         }
     }
     const int n = (int)fi.size();
+    if (lk_ahead) launchLKAhead(fi);  // fi: the features holding a map point now
     std::vector<uint8_t> outlier(n > 0 ? n : 1);
     int inliers = 0;
     SE3 pose = currentFrame_->pose;

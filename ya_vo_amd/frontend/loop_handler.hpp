@@ -110,7 +110,7 @@ public:
     bool buildInitMap();
     bool track();
     int trackLastFrame();
-    int optimizePoseOnly();
+    int optimizePoseOnly(bool lk_ahead = false);  // lk_ahead: hand the next frame's LK to the side lane first
     bool reinitialize();
     int triangulate2View(const Frame::ptr& last, const Frame::ptr& curr, const std::vector<Matches>& filtMatches,
                          bool firstView);
@@ -199,7 +199,7 @@ private:
     std::function<Frame::ptr()> peek_next_;  // the pipelined loop's next queued frame, or nullptr
     std::shared_ptr<LKAhead> lk_ahead_;      // launched during the current frame's LM, for the next frame
     std::shared_ptr<LKAhead> lk_cur_;        // launched during the last frame's LM, for the current frame
-    void launchLKAhead();
+    void launchLKAhead(const std::vector<int>& fi);
     void dropLKAhead(std::shared_ptr<LKAhead>& a);
 
 public:
