@@ -42,6 +42,21 @@ FP64_PEAK_TFLOPS = 256 * 4 * 16 * 2 * 2.4e9 / 1e12
 SIMD_CYCLES_PER_S = 256 * 4 * 2.4e9
 
 
+def kernel_source_digest() -> str:
+    """sha256 over the product's kernel and ABI sources (ya_vo_amd/csrc, include/yavo): the stamp tying
+    profiles/pmc_traffic.json's counters to the code they were measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    files = []
+    for d, exts in ((os.path.join(ROOT, "ya_vo_amd", "csrc"), (".hip", ".h")), (os.path.join(ROOT, "include", "yavo"), (".h",))):
+        files += sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(exts))
+    for f in files:
+        h.update(os.path.relpath(f, ROOT).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,6 +93,13 @@ def parse():
                          "skips it")
     ap.add_argument("--collective-world1", action="store_true",
                     help="at N=1, still run the shared-map exchange through a 1-rank process group (RCCL)")
+    ap.add_argument("--sequence-frames", type=int, default=200,
+                    help="frames of the configs[2] leg (rank 0, N=1): the full front end with the local BA window "
+                         "(tools/bench_sequence.py), its trajectory compared with the CPU oracle loop after the timed "
+                         "runs; 0 skips it")
+    ap.add_argument("--sequence-cpu", type=int, default=1,
+                    help="1: run tests/sequence_chain.py (the same loop over the CPU oracle) for the sequence leg's "
+                         "trajectory check; 0: skip it")
     ap.add_argument("--kf-every", type=int, default=4,
                     help="shared map: frames with global index %% kf_every == 0 are keyframes (their LM inliers "
                          "become landmarks); 0 disables the map and its all-gather")
@@ -620,6 +642,18 @@ def main():
                                                     gpu_decode=False)
         except Exception as e:
             png_e2e["host_decode"] = {"error": repr(e)[:300]}
+    seq = None
+    if args.sequence_frames > 0 and world == 1 and rank == 0 and args.tracker == "match":
+        # BASELINE configs[2]: the full front end + local BA over the first 200 frames (tools/bench_sequence.py)
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import bench_sequence
+            seq = bench_sequence.measure(args.sequence_frames, 20, repeats=3, cpu=bool(args.sequence_cpu),
+                                         cpu_threads=min(16, cpu_threads_available()), ctx=ctx)
+            seq.pop("_trajectory", None)
+        except Exception as e:  # reported, never fatal to the headline
+            seq = {"error": repr(e)[:300]}
     lh = None
     if args.loop_handler_frames > 0 and world == 1 and rank == 0:
         try:
@@ -650,13 +684,17 @@ def main():
     stages = {}
     roofline = None
     per_stage = None
+    coll_stats = None
     if not args.no_timing:
         ms_t, nruns_t = batch.stage_times()
         detect_timed_ms = float(ms_t[0]) / max(nruns_t, 1)
         batch.enable_timing(True)
+        shard.set_collective_timing(True)
         for _ in range(args.stage_steps):
             step()
         shard.drain()
+        coll_stats = shard.collective_stats()
+        shard.set_collective_timing(False)
         ms, nruns = batch.stage_times()
         per_launch_ms = {name: float(ms[i]) / max(nruns, 1) for i, name in enumerate(yv.STAGE_NAMES)}
         per_launch_ms["detect"] = detect_timed_ms
@@ -672,16 +710,21 @@ def main():
         traffic = None
         fp64 = {}
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        traffic_stamp = None
         if os.path.exists(pmc_path):
             try:
                 pmc = json.load(open(pmc_path))
-                if pmc.get("frames_per_step") == B:
+                # counters taken on this step size AND on this code (the kernel sources' digest), else null
+                traffic_stamp = {"commit": pmc.get("commit"), "source_sha256": pmc.get("source_sha256"),
+                                 "matches_code": pmc.get("source_sha256") == kernel_source_digest()}
+                if pmc.get("frames_per_step") == B and traffic_stamp["matches_code"]:
                     traffic = pmc.get("per_launch_bytes", {}).get(dom)
                     fp64 = pmc.get("fp64_per_launch", {})
             except (OSError, ValueError):
                 traffic = None
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "traffic_stamp": traffic_stamp,
                     "algorithmic_bytes_per_launch": int(nbytes[dom]), "launch_ms": round(per_launch_ms[dom], 4)}
         # every stage against the bound that limits it: VALU lane-ops for detect, FP4 MFMA ops
         # for the matcher (2 * Kq * Kt * 256 per pair, FP4 MFMA), HBM bytes for the rest
@@ -769,6 +812,7 @@ def main():
         "end_to_end": e2e,
         "png_end_to_end": png_e2e,
         "loop_handler": lh,
+        "sequence": seq,
         "roofline": roofline,
         "cpu_baseline": None,
     }
@@ -783,6 +827,8 @@ def main():
             n_lm += sum(len(x) for x in lms)
         out["shared_map"] = {"kf_every": args.kf_every, "block_bytes": bb, "keyframes_per_step": n_kf,
                              "landmarks_per_step": n_lm, "allgather_bytes_per_rank_per_step": bb * world,
+                             "world_size_seen": dist.get_world_size() if dist.is_initialized() else 1,
+                             "collective_timing": coll_stats,
                              "collective": ("none (1 rank)" if world == 1 and not shard.collective else
                                             "all_gather_into_tensor (RCCL, 1-rank group)" if world == 1 else
                                             "all_gather_into_tensor (RCCL)" if backend == "nccl" else

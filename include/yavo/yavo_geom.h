@@ -164,6 +164,11 @@ int yv_ba_set_control(yv_ba* ba, int on_device);
  * 6 b_p, 7 H_ll, 8 b_l, 9 D^-1, 10 S (as assembled for n <= 120; LDLT-factorised in place above), 11 b_schur, 12 x_p, 13 x_l, 14 poses, 15 landmarks)
  * as the last yv_ba_solve left it. */
 int yv_ba_debug_read(yv_ba* ba, int which, double* dst, int64_t count);
+/* Diagnostics: the reduced-system solver of yv_ba_solve on its own -- Eigen LDLT with diagonal pivoting of the
+ * symmetric n x n S (row-major, bitwise symmetric as the Schur kernel writes it), then x = S^-1 b as
+ * or_ldlt_solve computes it; *ok = its isPositive flag.  The same kernels the solve launches (n <= 128: the
+ * register form, above: the global-memory form). */
+int yv_ba_debug_ldlt(yv_ctx* ctx, const double* S, int n, const double* b, double* x, int* ok);
 
 /* ---- the sliding BA window of the chained stereo front end, on the device (BASELINE configs[2]) ----
  * The window LoopHandler's loop would hand Optimizer (src/LoopHandler.cc:60-165, src/Optimizer.cc:17-70), as

@@ -55,8 +55,9 @@ int yv_seq_upload(yv_seq* seq, struct yv_ctx* ctx, int first, int n, uint8_t* d_
 
 /* PNG decoding on the GPU (yavo_inflate.hip): the inflate (RFC 1950/1951) and the scanline filters run as kernels,
  * one wave per image; the host only reads the files and gathers each image's IDAT stream into pinned staging.
- * Formats: 8-bit grey, non-interlaced, H x W (every KITTI frame); anything else is YV_ERR_INVALID with nothing
- * enqueued (yv_png_decode_gray / yv_seq_upload decode every format on the host).  Calls of one decoder are ordered on
+ * Formats: 8-bit grey, non-interlaced, H x W (every KITTI frame). A file in any other format (yv_png_decode_gray /
+ * yv_seq_upload decode every format on the host), or missing, unreadable or truncated, fails alone with code 9: its
+ * output is zero-filled and the call's other images decode, as cv::imread fails per file.  Calls of one decoder are ordered on
  * the stream they are given (use one stream per decoder); the staging of a call is reused two calls later, after its
  * copy completed. */
 typedef struct yv_pngdec yv_pngdec;
@@ -76,7 +77,8 @@ int yv_seq_upload_gpu_frames(yv_seq* seq, yv_pngdec* d, const int* frames, int n
                              int threads, void* stream);
 /* waits for the last decode; codes[i] (optional, host, n of the last call) = 0 or the image's decode error
  * (1 zlib header, 2 block, 3 Huffman code, 4 output overrun, 5 stream short, 6 filter type, 7 an IDAT chunk's CRC-32,
- * 8 the zlib Adler-32 trailer: missing or wrong); *n_bad = images that failed in EVERY decode since the previous
+ * 8 the zlib Adler-32 trailer: missing or wrong, 9 the file: missing, unreadable, truncated or not an 8-bit grey
+ * non-interlaced H x W PNG); *n_bad = images that failed in EVERY decode since the previous
  * yv_pngdec_status call.  A failed image's device output is zero-filled (cv::imread returns an empty Mat). */
 int yv_pngdec_status(yv_pngdec* d, int32_t* codes, int* n_bad);
 /* the integrity checks of the following decodes (default both on, as libpng / zlib do): crc = every IDAT chunk's

@@ -87,3 +87,29 @@ def test_bench_cli_refuses_too_few_devices():
     assert r.returncode == 2
     assert "visible GPUs" in r.stderr
     assert r.stdout == ""
+
+
+def test_exchange_summary_reports_hidden_and_exposed_gathers():
+    """The bench's shared_map.collective_timing block (FrameShard.collective_stats over HIP events): mean / max gather
+    time, placement time, and the fraction of exchanges whose gather ended before the run it overlapped."""
+    from ya_vo_amd.sharding import exchange_summary
+    assert exchange_summary([], [], []) is None
+    s = exchange_summary([0.2, 0.4, 0.3, 0.1], [0.01, 0.02, 0.01, 0.01], [1.5, -0.2, 0.0, 2.0])
+    assert s["exchanges"] == 4
+    assert s["allgather_ms_mean"] == 0.25 and s["allgather_ms_max"] == 0.4
+    assert s["hidden_fraction"] == 0.75 and s["min_slack_ms"] == -0.2
+
+
+def test_bench_reports_world_size_and_collective_timing():
+    """The bench line carries world_size_seen and the collective timing beside the shared map,
+    and the configs[2] sequence leg is on by default."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert '"world_size_seen": dist.get_world_size() if dist.is_initialized() else 1' in src
+    assert '"collective_timing": coll_stats' in src
+    sys_argv = sys.argv
+    try:
+        sys.argv = ["bench.py"]
+        a = bench.parse()
+    finally:
+        sys.argv = sys_argv
+    assert a.sequence_frames == 200 and a.sequence_cpu == 1

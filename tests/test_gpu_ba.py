@@ -88,3 +88,62 @@ def test_ba_rejects_bad_graph(ctx):
         ba.set_problem(5, 1, 10, ep, el, np.zeros((2, 2)), scene.K_KITTI)  # more poses than the workspace
     with pytest.raises(yv.YavoError):
         ba.set_problem(4, 5, 10, np.array([0, 1], np.int32), el, np.zeros((2, 2)), scene.K_KITTI)
+
+
+def _spd(n, seed, cond=1e3):
+    rng = np.random.default_rng(seed)
+    Q, _ = np.linalg.qr(rng.normal(size=(n, n)))
+    H = (Q * np.geomspace(1.0, cond, n)) @ Q.T
+    return np.tril(H) + np.tril(H, -1).T  # bitwise symmetric, as the Schur kernel writes S
+
+
+def _block_tridiagonal(nb, seed):
+    """The configs[2] window's reduced system: 6 x 6 pose blocks coupled to their neighbours only."""
+    rng = np.random.default_rng(seed)
+    n = 6 * nb
+    J = np.zeros((3 * n, n))
+    for p in range(nb):
+        J[18 * p:18 * p + 18, 6 * p:6 * p + 6] = rng.normal(size=(18, 6))
+        if p + 1 < nb:
+            J[18 * p:18 * p + 18, 6 * p + 6:6 * p + 12] = 0.3 * rng.normal(size=(18, 6))
+    H = J.T @ J + 1e-3 * np.eye(n)
+    return np.tril(H) + np.tril(H, -1).T
+
+
+def _ldlt_cases():
+    cases = [(f"spd{n}", _spd(n, n)) for n in (1, 2, 5, 6, 60, 63, 64, 65, 114, 120, 127, 128, 129, 200)]
+    cases.append(("window120", _block_tridiagonal(20, 7)))
+    cases.append(("window126", _block_tridiagonal(21, 8)))
+    tie = _spd(24, 9)
+    np.fill_diagonal(tie, 5.0)  # every pivot tied: the scan-and-swap replay
+    cases.append(("ties", tie))
+    part = _spd(40, 10)
+    part[3, 3] = part[17, 17] = part[30, 30]  # a few tied diagonals among distinct ones
+    cases.append(("some_ties", part))
+    z = np.zeros((12, 12))
+    z[1, 0] = z[0, 1] = 1.0  # zero diagonal: the first pivot is zero (factorisation stops)
+    cases.append(("zero_first_pivot", z))
+    cases.append(("zero_matrix", np.zeros((7, 7))))
+    later = np.array([[4.0, 2.0, 1.0], [2.0, 1.0, 3.0], [1.0, 3.0, 2.5]])  # D(1) = 0 after the first step
+    cases.append(("zero_later_pivot", later))
+    ind = _spd(30, 11)
+    ind[np.arange(0, 30, 4), np.arange(0, 30, 4)] *= -1.0  # indefinite: isPositive false
+    cases.append(("indefinite", ind))
+    nan_off = _spd(16, 12)
+    nan_off[9, 2] = nan_off[2, 9] = np.nan
+    cases.append(("nan_offdiag", nan_off))
+    nan_diag = _spd(16, 13)
+    nan_diag[5, 5] = np.nan
+    cases.append(("nan_diag", nan_diag))
+    return cases
+
+
+@pytest.mark.parametrize("name,S", _ldlt_cases(), ids=[c[0] for c in _ldlt_cases()])
+def test_ba_ldlt_matches_oracle(ctx, oracle, name, S):
+    """The reduced-system solver alone (n <= 128: registers + LDS column hand-offs; above: global memory) against the
+    oracle's or_ldlt_solve, bit for bit, including the pivot replay on ties, zero and NaN pivots and the flag."""
+    b = np.random.default_rng(len(S)).normal(size=len(S))
+    x, ok = ctx.ba_ldlt(S, b)
+    ox, ook = oracle.ldlt_solve(S, b)
+    assert ok == ook
+    np.testing.assert_array_equal(x, ox)

@@ -230,6 +230,36 @@ def test_gpu_png_sequence_upload(ctx, tmp_path):
     seq.close()
 
 
+def test_gpu_png_bad_files_fail_alone(ctx, tmp_path):
+    """A missing, truncated, RGB or wrong-size file in a GPU-decoded batch fails alone with code 9 (its image zero-filled,
+    counted), as cv::imread fails per file; the batch's other images decode as the host decoder does (ADVICE r04)."""
+    import torch
+    from PIL import Image
+    from ya_vo_amd.synth import synth_stereo_batch
+    H, W, n = 376, 1241, 8
+    fr = synth_stereo_batch(5, n // 2, start=0).reshape(n, H, W)
+    os.makedirs(tmp_path / "image_0")
+    for k in range(n):
+        png_write_gray(str(tmp_path / "image_0" / f"{k:06d}.png"), fr[k])
+    seq = Sequence(str(tmp_path), stereo=False)
+    p = lambda k: str(tmp_path / "image_0" / f"{k:06d}.png")  # noqa: E731
+    data = open(p(2), "rb").read()
+    open(p(2), "wb").write(data[:len(data) // 2])                                         # truncated
+    Image.fromarray(np.stack([fr[4]] * 3, -1)).save(p(4))                                  # RGB
+    png_write_gray(p(5), fr[5][:, :W - 1].copy())                                          # wrong size
+    os.remove(p(6))                                                                        # missing (listed already)
+    dec = PngDecoder(ctx, n, H, W)
+    d = torch.full((n * H * W,), 7, dtype=torch.uint8, device="cuda:0")
+    dec.upload_sequence(seq, 0, n, d.data_ptr(), H * W, threads=3)
+    codes, bad = dec.status()
+    assert list(codes) == [0, 0, 9, 0, 9, 9, 9, 0] and bad == 4
+    out = d.cpu().numpy().reshape(n, H, W)
+    for k in range(n):
+        np.testing.assert_array_equal(out[k], fr[k] if codes[k] == 0 else np.zeros((H, W), np.uint8))
+    dec.close()
+    seq.close()
+
+
 def test_gpu_png_randomized_streams_match_zlib(ctx):
     """Differential fuzz of the lane-parallel inflate: random sizes, row filters, zlib levels and strategies (every
     block type, short and long matches, far distances, chunks capped by highly compressible rows); then the same

@@ -192,3 +192,31 @@ def test_loop_handler_gpu_decode_matches_oracle_loop(tmp_path, oracle):
     np.testing.assert_array_equal(gpu_events, ref_events)
     np.testing.assert_array_equal(gpu_poses, P)
     assert stats["reinit"] >= 1 and stats["tracked"] >= 20
+
+
+@pytest.mark.gpu
+def test_loop_handler_gpu_decode_truncated_png_ends_the_train(tmp_path, oracle):
+    """A truncated PNG in the middle of a GPU-decoded batch (frame 20 of the 16-frame batch 16..31) fails alone, as
+    cv::imread does per file: the frames before it are tracked, the loop ends cleanly (exit 0) at exactly that frame,
+    and the trajectory is the oracle loop's over frames 0..19 -- the same end as the host-decoding pipeline."""
+    from loop_chain import EVENT_FIELDS, LoopChain
+    from ya_vo_amd import scene
+    n, bad = 40, 20
+    frames = [synth_frame(777, *offset(k, 30), 376, 1241) for k in range(n)]
+    cfg, base = make_sequence(tmp_path, frames)
+    path = os.path.join(base, "00", "image_0", f"{bad:06d}.png")
+    data = open(path, "rb").read()
+    with open(path, "wb") as f:
+        f.write(data[:len(data) // 2])
+    offsets = np.fromfile(OFFSETS, np.int8).reshape(256, 4)
+    P, ev = LoopChain(oracle, scene.K_KITTI, offsets).run(frames[:bad])
+    ref_events = np.array([[e[f] for f in EVENT_FIELDS] for e in ev], np.int32)
+    for mode in (["--gpu-decode", "16"], []):
+        pb, eb = tmp_path / "poses.bin", tmp_path / "events.bin"
+        r = subprocess.run([BIN, cfg, "--poses-bin", str(pb), "--events", str(eb), "--pipeline", "2", "--readers", "4"]
+                           + mode, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, (mode, r.stderr[-2000:])
+        stats = json.loads(r.stdout.strip().splitlines()[-1])
+        assert stats["frames"] == bad, mode
+        np.testing.assert_array_equal(np.fromfile(eb, np.int32).reshape(-1, len(EVENT_FIELDS)), ref_events)
+        np.testing.assert_array_equal(np.fromfile(pb, np.float64).reshape(-1, 7), P)

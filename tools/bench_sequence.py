@@ -24,6 +24,107 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 T_RIGHT = np.array([0, 0, 0, 1, 0, -0.54, 0], np.float64)
 
 
+def measure(frames=200, chunk=20, n_fixed=2, ba_iters=10, repeats=3, cpu_threads=16, cpu=True, kitti="",
+            host_window=False, ctx=None):
+    """Run the configs[2] front end `repeats` times on frames resident in HBM (after one warm-up run) and return the
+    result dict of the best run; cpu: also run tests/sequence_chain.py (the same loop over the CPU oracle) on the same
+    frames and compare the trajectories (after the timed runs)."""
+    import torch
+    import ya_vo_amd as yv
+    from ya_vo_amd import io as yio
+    from ya_vo_amd import scene
+    from ya_vo_amd.sequence import SequenceFrontend
+    from ya_vo_amd.synth import synth_sequence
+
+    n = frames
+    if n % chunk:
+        raise ValueError("frames must be a multiple of chunk")
+    K = scene.K_KITTI
+    if kitti and os.path.isdir(kitti):
+        seq = yio.Sequence(kitti, stereo=True)
+        _, P1, K0, _ = seq.calib()
+        K = K0
+        t_right = np.array([0, 0, 0, 1, 0, P1[0, 3] / P1[0, 0], 0])  # baseline from P1 (reference col axis)
+        fr = seq.read(0, n, threads=16).reshape(n, 2, seq.H, seq.W)
+        data = f"KITTI {kitti}"
+    else:
+        t_right = T_RIGHT
+        fr = synth_sequence(1234, n, stereo=True)
+        data = "synthetic (ya_vo_amd/synth.py crops of one textured plane; known trajectory)"
+    H, W = fr.shape[2:]
+
+    offsets = np.fromfile(os.path.join(ROOT, "tests", "golden", "brief_offsets_mt19937_42.bin"), np.int8)
+    own_ctx = ctx is None
+    if own_ctx:
+        ctx = yv.Context(0)
+    ctx.set_brief_offsets(offsets)
+    d = torch.from_numpy(fr.reshape(2 * n, H, W)).to(torch.device("cuda", ctx.device))
+    torch.cuda.synchronize()
+
+    def run():
+        fe = SequenceFrontend(ctx, chunk, K, t_right, n_fixed=n_fixed, ba_iters=ba_iters, H=H, W=W,
+                              device_window=not host_window)
+        sec = {}
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for c in range(n // chunk):
+            fe.process_chunk(d[2 * c * chunk:2 * (c + 1) * chunk], sec)
+        fe.flush(sec)
+        torch.cuda.synchronize()
+        return fe, time.perf_counter() - t0, sec
+
+    fe, _, _ = run()  # warm-up (first launches, allocations)
+    fe.close()
+    times, secs = [], []
+    traj = ba_log = records = None
+    for _ in range(repeats):
+        fe, dt, sec = run()
+        times.append(dt)
+        secs.append(sec)
+        traj, ba_log = fe.trajectory(), fe.ba_log
+        records = fe.records
+        fe.close()
+    best = int(np.argmin(times))
+    out = {
+        "workload": "BASELINE configs[2]: full front end (detect+describe+match+PnP + shared map + local BA), "
+                    f"first {n} frames, 1 x MI355X",
+        "data": data, "frames": n, "chunk_frames": chunk, "ba_window": chunk + n_fixed,
+        "ba_fixed": n_fixed, "ba_iters": ba_iters,
+        "ba_window_assembly": "host (window_problem / apply_window, per-chunk read-back)" if host_window else
+        "device (yv_ba_window_*: records in HBM, graph built on the device, no per-chunk read-back)",
+        "frames_per_s": round(n / times[best], 2), "seconds": round(times[best], 4),
+        "seconds_all_repeats": [round(t, 4) for t in times],
+        "phase_seconds": {k: round(v, 4) for k, v in secs[best].items()},
+        "ba_solves": len(ba_log),
+        "ba_ms_per_solve": round(1e3 * secs[best].get("ba", 0.0) / max(len(ba_log), 1), 4),
+        "ba_chi2_first_last": [[round(a, 3), round(b, 3)] for _, _, a, b in ba_log],
+        "landmarks": int(sum(len(r.edge) for r in records.values())),
+        "inputs": "frames resident in HBM before the timed region (PCIe excluded)",
+    }
+    from sequence_chain import ground_truth, oracle_sequence, rmse_translation
+    if not kitti:
+        out["rmse_vs_ground_truth_m"] = rmse_translation(traj, ground_truth(n, K))
+    if cpu:
+        import oracle_bind
+        orc = oracle_bind.Oracle()
+        t0 = time.perf_counter()
+        ref, _, ref_log = oracle_sequence(orc, fr, chunk, K, t_right, offsets.reshape(256, 4),
+                                          n_fixed=n_fixed, ba_iters=ba_iters, threads=cpu_threads)
+        cpu_s = time.perf_counter() - t0
+        out["cpu_reference"] = {"frames_per_s": round(n / cpu_s, 3), "seconds": round(cpu_s, 2),
+                                "cores": cpu_threads, "kind": "port",
+                                "sample": f"the same {n} frames through tests/sequence_chain.py (oracle FAST/BRIEF/"
+                                          "match/triangulation/pose LM/map/BA), ref-efficient costs, threads over "
+                                          "frames for the per-frame stages"}
+        out["trajectory_rmse_vs_cpu_ref_m"] = rmse_translation(traj, ref)
+        out["trajectory_bit_identical"] = bool(np.array_equal(traj, ref))
+        out["ba_log_identical"] = ref_log == ba_log
+    out["_trajectory"] = traj
+    if own_ctx:
+        ctx.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=200)
@@ -38,93 +139,11 @@ def main():
     ap.add_argument("--host-window", action="store_true",
                     help="assemble the BA window on the host (the round-2 path) instead of on the device")
     args = ap.parse_args()
-
-    import torch
-    import ya_vo_amd as yv
     from ya_vo_amd import io as yio
-    from ya_vo_amd import scene
-    from ya_vo_amd.sequence import SequenceFrontend, se3_inverse
-    from ya_vo_amd.synth import synth_sequence
-
-    n, chunk = args.frames, args.chunk
-    if n % chunk:
-        raise SystemExit("--frames must be a multiple of --chunk")
-    K = scene.K_KITTI
-    if args.kitti and os.path.isdir(args.kitti):
-        seq = yio.Sequence(args.kitti, stereo=True)
-        _, P1, K0, _ = seq.calib()
-        K = K0
-        t_right = np.array([0, 0, 0, 1, 0, P1[0, 3] / P1[0, 0], 0])  # baseline from P1 (reference col axis)
-        frames = seq.read(0, n, threads=16).reshape(n, 2, seq.H, seq.W)
-        data = f"KITTI {args.kitti}"
-    else:
-        t_right = T_RIGHT
-        frames = synth_sequence(1234, n, stereo=True)
-        data = "synthetic (ya_vo_amd/synth.py crops of one textured plane; known trajectory)"
-    H, W = frames.shape[2:]
-
-    offsets = np.fromfile(os.path.join(ROOT, "tests", "golden", "brief_offsets_mt19937_42.bin"), np.int8)
-    ctx = yv.Context(0)
-    ctx.set_brief_offsets(offsets)
-    d = torch.from_numpy(frames.reshape(2 * n, H, W)).to("cuda:0")
-    torch.cuda.synchronize()
-
-    def run():
-        fe = SequenceFrontend(ctx, chunk, K, t_right, n_fixed=args.n_fixed, ba_iters=args.ba_iters, H=H, W=W,
-                              device_window=not args.host_window)
-        sec = {}
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for c in range(n // chunk):
-            fe.process_chunk(d[2 * c * chunk:2 * (c + 1) * chunk], sec)
-        fe.flush(sec)
-        torch.cuda.synchronize()
-        return fe, time.perf_counter() - t0, sec
-
-    fe, _, _ = run()  # warm-up (first launches, allocations)
-    fe.close()
-    times, secs = [], []
-    for _ in range(args.repeats):
-        fe, dt, sec = run()
-        times.append(dt)
-        secs.append(sec)
-        traj, ba_log = fe.trajectory(), fe.ba_log
-        records = fe.records
-        fe.close()
-    best = int(np.argmin(times))
-    out = {
-        "workload": "BASELINE configs[2]: full front end (detect+describe+match+PnP + shared map + local BA), "
-                    f"first {n} frames, 1 x MI355X",
-        "data": data, "frames": n, "chunk_frames": chunk, "ba_window": chunk + args.n_fixed,
-        "ba_fixed": args.n_fixed, "ba_iters": args.ba_iters,
-        "ba_window_assembly": "host (window_problem / apply_window, per-chunk read-back)" if args.host_window else
-        "device (yv_ba_window_*: records in HBM, graph built on the device, no per-chunk read-back)",
-        "frames_per_s": round(n / times[best], 2), "seconds": round(times[best], 4),
-        "seconds_all_repeats": [round(t, 4) for t in times],
-        "phase_seconds": {k: round(v, 4) for k, v in secs[best].items()},
-        "ba_solves": len(ba_log),
-        "ba_chi2_first_last": [[round(a, 3), round(b, 3)] for _, _, a, b in ba_log],
-        "landmarks": int(sum(len(r.edge) for r in records.values())),
-        "inputs": "frames resident in HBM before the timed region (PCIe excluded)",
-    }
-    from sequence_chain import ground_truth, oracle_sequence, rmse_translation
-    if not args.kitti:
-        out["rmse_vs_ground_truth_m"] = rmse_translation(traj, ground_truth(n, K))
-    if not args.no_cpu:
-        import oracle_bind
-        orc = oracle_bind.Oracle()
-        t0 = time.perf_counter()
-        ref, _, ref_log = oracle_sequence(orc, frames, chunk, K, t_right, offsets.reshape(256, 4),
-                                          n_fixed=args.n_fixed, ba_iters=args.ba_iters, threads=args.cpu_threads)
-        cpu_s = time.perf_counter() - t0
-        out["cpu_reference"] = {"frames_per_s": round(n / cpu_s, 3), "seconds": round(cpu_s, 2),
-                                "cores": args.cpu_threads, "kind": "port",
-                                "sample": f"the same {n} frames through tests/sequence_chain.py (oracle FAST/BRIEF/"
-                                          "match/triangulation/pose LM/map/BA), ref-efficient costs, threads over "
-                                          "frames for the per-frame stages"}
-        out["trajectory_rmse_vs_cpu_ref_m"] = rmse_translation(traj, ref)
-        out["trajectory_bit_identical"] = bool(np.array_equal(traj, ref))
-        out["ba_log_identical"] = ref_log == ba_log
+    from ya_vo_amd.sequence import se3_inverse
+    out = measure(args.frames, args.chunk, args.n_fixed, args.ba_iters, args.repeats, args.cpu_threads,
+                  not args.no_cpu, args.kitti, args.host_window)
+    traj = out.pop("_trajectory")
     if args.out:
         yio.write_kitti_poses(os.path.splitext(args.out)[0] + "_poses.txt", np.stack([se3_inverse(T) for T in traj]))
     line = json.dumps(out)
@@ -132,7 +151,6 @@ def main():
     if args.out:
         with open(args.out, "w") as f:
             f.write(line + "\n")
-    ctx.close()
 
 
 if __name__ == "__main__":

@@ -84,6 +84,11 @@ def main():
                                                            "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")),
                 "raw": vals}
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    # the code the counters were taken on: bench.py uses `traffic` only while its kernel sources hash the same
+    sys.path.insert(0, root)
+    import bench
+    res["source_sha256"] = bench.kernel_source_digest()
+    res["commit"] = os.environ.get("YAVO_COMMIT", "")
     path = os.path.join(root, "profiles", "pmc_traffic.json")
     os.makedirs(os.path.dirname(path), exist_ok=True)
     json.dump(res, open(path, "w"), indent=1)

@@ -126,6 +126,7 @@ GEOM_SIGNATURES = {
     "yv_ba_set_problem": (_I, [_P, _I, _I, _I, _P, _P, _P, _I, _P]),
     "yv_ba_solve": (_I, [_P, _P, _P, _I, _P, ctypes.POINTER(_I)]),
     "yv_ba_debug_read": (_I, [_P, _I, _P, ctypes.c_int64]),
+    "yv_ba_debug_ldlt": (_I, [_P, _P, _I, _P, _P, ctypes.POINTER(_I)]),
     "yv_ba_set_stream": (_I, [_P, _P]),
     "yv_ba_set_control": (_I, [_P, _I]),
     "yv_ba_window_create": (_I, [_P, _I, _I, ctypes.POINTER(_P)]),
@@ -300,6 +301,18 @@ class _GeomMixin:
         _check(self.lib.yv_world2camera(self.handle, _ptr(X), len(X), _ptr(_f64(pose, 7)), _ptr(_f64(K, 9)),
                                         _ptr(out)), "yv_world2camera")
         return out
+
+    def ba_ldlt(self, S, b):
+        """The BA's reduced-system solver alone (yv_ba_debug_ldlt): Eigen LDLT with diagonal pivoting of the symmetric S,
+        x = S^-1 b. -> (x, isPositive)."""
+        S = np.ascontiguousarray(S, np.float64)
+        b = np.ascontiguousarray(b, np.float64)
+        n = len(b)
+        x = np.zeros(n)
+        ok = ctypes.c_int()
+        _check(self.lib.yv_ba_debug_ldlt(self.handle, S.ctypes.data, n, b.ctypes.data, x.ctypes.data, ctypes.byref(ok)),
+               "yv_ba_debug_ldlt")
+        return x, bool(ok.value)
 
     def pose_lm(self, X, uv, K, pose):
         """LoopHandler::optimizePoseOnly -> (pose [7], outlier [n] bool, inliers)."""
@@ -634,7 +647,8 @@ class BundleAdjuster:
 
     def close(self) -> None:
         if self.handle:
-            self.lib.yv_ba_destroy(self.handle)
+            if getattr(self.ctx, "handle", None):  # a closed context took its stream (and the device state) with it
+                self.lib.yv_ba_destroy(self.handle)
             self.handle = None
 
     def __del__(self):

@@ -11,8 +11,9 @@
 //                         inverse per landmark and W = H_pl Dinv per edge
 //   ba_schur_kernel       one 64-lane workgroup per upper Schur block (p1 <= p2), a lane per entry, and one per pose
 //                         for b_schur: sequential over the landmarks the two poses share, pairs staged in LDS
-//   ba_ldlt_lds_kernel    one workgroup: Eigen's LDLT (diagonal pivoting) on the reduced pose system with its lower
-//                         triangle in LDS (n <= 120; ba_ldlt_kernel on global memory above), then the solve
+//   ba_ldlt_reg_kernel    one workgroup: Eigen's LDLT (diagonal pivoting) on the reduced pose system, the matrix in
+//                         registers, columns handed between waves through LDS (n <= 128; ba_ldlt_kernel on global
+//                         memory above), then the solve
 //   ba_backsub_kernel     one lane per landmark: x_l = Dinv (b_l - sum_e H_pl^T x_p)
 //   ba_update_kernel      T <- exp(x_p) T per free pose, X <- X + x_l per landmark
 //   ba_edge_chi2_kernel   one lane per edge: |e|^2 at the current estimate
@@ -70,12 +71,16 @@ __device__ __forceinline__ double tree256(double v, double* red) {
     return r;
 }
 
+// the state (poses, landmarks) the current estimate is in: 0 = P.poses / P.X, 1 = P.poses2 / P.X2
+__device__ __forceinline__ int ba_cur(const BaParams& P) { return P.cur ? *P.cur : 0; }
+
 __global__ __launch_bounds__(256) void ba_linearize_kernel(BaParams P, BaMat3 K) {
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= P.E) return;
-    const double* T = P.poses + 7 * P.ep[e];
-    const double* X = P.X + 3 * P.el[e];
+    const int cur = ba_cur(P);
+    const double* T = (cur ? P.poses2 : P.poses) + 7 * P.ep[e];
+    const double* X = (cur ? P.X2 : P.X) + 3 * P.el[e];
     double err[2];
     ba_error(T, K.v, X, P.meas + 2 * e, err);
     double pc[3], R[9], Jp[12], Jl[6];
@@ -94,108 +99,175 @@ __global__ __launch_bounds__(256) void ba_linearize_kernel(BaParams P, BaMat3 K)
 #pragma unroll
         for (int c = 0; c < 3; ++c)
             Jl[r * 3 + c] = Jp[r * 6 + 0] * R[0 * 3 + c] + Jp[r * 6 + 1] * R[1 * 3 + c] + Jp[r * 6 + 2] * R[2 * 3 + c];
-    P.err[2 * e] = err[0];
-    P.err[2 * e + 1] = err[1];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) P.Jp[12 * (int64_t)e + i] = Jp[i];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) P.Jl[6 * (int64_t)e + i] = Jl[i];
+    double H[18];
 #pragma unroll
     for (int a = 0; a < 6; ++a)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) P.Hpl[18 * (int64_t)e + 3 * a + c] = Jp[a] * Jl[c] + Jp[6 + a] * Jl[3 + c];
+        for (int c = 0; c < 3; ++c) H[3 * a + c] = Jp[a] * Jl[c] + Jp[6 + a] * Jl[3 + c];
+    // 16-B stores (every per-edge block is 16-B aligned)
+    reinterpret_cast<double2*>(P.err)[e] = make_double2(err[0], err[1]);
+    double2* jp2 = reinterpret_cast<double2*>(P.Jp + 12 * (int64_t)e);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) jp2[i] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
+    double2* jl2 = reinterpret_cast<double2*>(P.Jl + 6 * (int64_t)e);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) jl2[i] = make_double2(Jl[2 * i], Jl[2 * i + 1]);
+    double2* h2 = reinterpret_cast<double2*>(P.Hpl + 18 * (int64_t)e);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) h2[i] = make_double2(H[2 * i], H[2 * i + 1]);
 }
 
-// one workgroup per free pose (blockIdx.x + nf): 21 upper H entries + 6 b entries in tree256 order
-__global__ __launch_bounds__(256) void ba_pose_reduce_kernel(BaParams P) {
+// last-block-done: every workgroup of the launch arrives once, after its global stores; true in the workgroup that
+// arrived last, after an agent-scope acquire, so it reads what every other workgroup stored (release: each
+// arriving workgroup's fence before its ticket; per-XCD L2s are not coherent, the agent-scope fences write back and
+// invalidate). The counter is left at 0 for the next launch. Every thread of the workgroup must call it.
+__device__ bool ba_last_block(unsigned* ticket) {
+    __shared__ unsigned s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const unsigned tk = atomicAdd(ticket, 1u);
+        const bool last = tk == gridDim.x - 1;
+        if (last) {
+            __threadfence();
+            atomicExch(ticket, 0u);
+        }
+        s_last = last ? 1u : 0u;
+    }
+    __syncthreads();
+    return s_last != 0;
+}
+
+// an iteration's trial loop starts (after its linearisation); the first one sets lambda = tau max|H_ii|
+__device__ void ba_ctl_iter_begin(BaCtl* c, const unsigned long long* maxdiag) {
+    if (maxdiag) {
+        const double maxd = __longlong_as_double((long long)*maxdiag);
+        c->lambda = 1e-5 * maxd;
+        c->ni = 2;
+    }
+    c->q = 0;
+    c->iter_done = 0;
+    c->skip_trial = 0;
+}
+
+__device__ __forceinline__ void atomic_max_abs(unsigned long long* m, double v) {
+    if (v > 0.0) atomicMax(m, (unsigned long long)__double_as_longlong(v));  // NaN never, as fmax ignores it
+}
+
+// One launch for the iteration's blocks of H and b:
+//  blocks [0, np)      one per free pose: 21 upper H_pp entries + 6 b_p entries in tree256 order over the pose's
+//                      edges (each thread's strided chain, two edges' loads in flight, then the 27 halving trees)
+//  blocks [np, ...)    one lane per landmark: H_ll, b_l sequential over its edges
+// first: the largest |diagonal| (free poses and landmarks) into *P.maxdiag (uint64 bits of a non-negative double).
+// Device control: the last workgroup starts the iteration's trial loop (lambda on the first iteration).
+__global__ __launch_bounds__(256) void ba_reduce_kernel(BaParams P, int first) {
     __shared__ double red[27 * kNT];
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    const int p = P.nf + blockIdx.x;
-    const int k0 = P.pe_off[p], k1 = P.pe_off[p + 1];
     const int t = threadIdx.x;
-    double h[21], g[6];
+    if ((int)blockIdx.x < P.np) {
+        const int p = P.nf + blockIdx.x;
+        const int k0 = P.pe_off[p], k1 = P.pe_off[p + 1];
+        double h[21], g[6];
 #pragma unroll
-    for (int i = 0; i < 21; ++i) h[i] = 0.0;
+        for (int i = 0; i < 21; ++i) h[i] = 0.0;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) g[i] = 0.0;
-    for (int k = k0 + t; k < k1; k += kNT) {
-        const int e = P.pe[k];
-        const double* jp = P.Jp + 12 * (int64_t)e;
-        double J[12];
+        for (int i = 0; i < 6; ++i) g[i] = 0.0;
+        // this thread's edges k0 + t, k0 + t + 256, ...: the next edge's J and e are loaded (and the one after's index)
+        // while this edge's terms are added
+        auto load_edge = [&](int e, double (&J)[12], double (&er)[2]) {
+            const double2* jp = reinterpret_cast<const double2*>(P.Jp + 12 * (int64_t)e);
 #pragma unroll
-        for (int i = 0; i < 12; ++i) J[i] = jp[i];
-        const double e0 = P.err[2 * e], e1 = P.err[2 * e + 1];
-        int q = 0;
+            for (int i = 0; i < 6; ++i) {
+                const double2 v = jp[i];
+                J[2 * i] = v.x;
+                J[2 * i + 1] = v.y;
+            }
+            const double2 ev = reinterpret_cast<const double2*>(P.err)[e];
+            er[0] = ev.x;
+            er[1] = ev.y;
+        };
+        int k = k0 + t;
+        double Jc[12], ec[2];
+        if (k < k1) load_edge(P.pe[k], Jc, ec);
+        int e_next = k + kNT < k1 ? P.pe[k + kNT] : 0;
+        while (k < k1) {
+            double Jn[12], en[2];
+            const bool more = k + kNT < k1;
+            if (more) load_edge(e_next, Jn, en);
+            if (k + 2 * kNT < k1) e_next = P.pe[k + 2 * kNT];
+            int q = 0;
 #pragma unroll
-        for (int a = 0; a < 6; ++a)
+            for (int a = 0; a < 6; ++a)
 #pragma unroll
-            for (int b = a; b < 6; ++b, ++q) h[q] = h[q] + (J[a] * J[b] + J[6 + a] * J[6 + b]);
+                for (int b = a; b < 6; ++b, ++q) h[q] = h[q] + (Jc[a] * Jc[b] + Jc[6 + a] * Jc[6 + b]);
 #pragma unroll
-        for (int a = 0; a < 6; ++a) g[a] = g[a] + (J[a] * e0 + J[6 + a] * e1);
-    }
-    // the 27 halving trees at once: level `off` has 27 * off independent additions p[t] = p[t] + p[t + off],
-    // spread over all 256 threads (each tree's order is the one tree256 uses)
+            for (int a = 0; a < 6; ++a) g[a] = g[a] + (Jc[a] * ec[0] + Jc[6 + a] * ec[1]);
+            k += kNT;
+            if (more) {
 #pragma unroll
-    for (int i = 0; i < 21; ++i) red[i * kNT + t] = h[i];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) red[(21 + i) * kNT + t] = g[i];
-    __syncthreads();
-    for (int off = kNT / 2; off > 0; off >>= 1) {
-        for (int idx = t; idx < 27 * off; idx += kNT) {
-            const int q = idx / off, u = idx - q * off;
-            red[q * kNT + u] = red[q * kNT + u] + red[q * kNT + u + off];
+                for (int i = 0; i < 12; ++i) Jc[i] = Jn[i];
+                ec[0] = en[0];
+                ec[1] = en[1];
+            }
         }
+        // the 27 halving trees at once: level `off` has 27 * off independent additions p[t] = p[t] + p[t + off],
+        // spread over all 256 threads (each tree's order is the one tree256 uses)
+#pragma unroll
+        for (int i = 0; i < 21; ++i) red[i * kNT + t] = h[i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) red[(21 + i) * kNT + t] = g[i];
         __syncthreads();
-    }
-    double* H = P.Hpp + 36 * p;
-    if (t < 21) {
-        int a = 0, q = t;
-        while (q >= 6 - a) {
-            q -= 6 - a;
-            ++a;
+        for (int off = kNT / 2; off > 0; off >>= 1) {
+            for (int idx = t; idx < 27 * off; idx += kNT) {
+                const int q = idx / off, u = idx - q * off;
+                red[q * kNT + u] = red[q * kNT + u] + red[q * kNT + u + off];
+            }
+            __syncthreads();
         }
-        const int b = a + q;
-        H[6 * a + b] = H[6 * b + a] = red[t * kNT];
-    } else if (t < 27) {
-        P.bp[6 * p + t - 21] = -red[t * kNT];
-    }
-}
-
-// H_ll / b_l per landmark; maxdiag (|H| diagonal of free poses and landmarks) as uint64 bits of a non-negative double
-__global__ __launch_bounds__(256) void ba_landmark_reduce_kernel(BaParams P, unsigned long long* maxdiag) {
-    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    const int l = blockIdx.x * blockDim.x + threadIdx.x;
-    double m = 0.0;
-    if (l < P.L) {
-        double h[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-        for (int k = P.le_off[l]; k < P.le_off[l + 1]; ++k) {
-            const int e = P.le[k];
-            const double* jl = P.Jl + 6 * (int64_t)e;
-            const double e0 = P.err[2 * e], e1 = P.err[2 * e + 1];
+        double* H = P.Hpp + 36 * p;
+        if (t < 21) {
+            int a = 0, q = t;
+            while (q >= 6 - a) {
+                q -= 6 - a;
+                ++a;
+            }
+            const int b = a + q;
+            const double v = red[t * kNT];
+            H[6 * a + b] = H[6 * b + a] = v;
+            if (first && a == b) atomic_max_abs(P.maxdiag, fabs(v));
+        } else if (t < 27) {
+            P.bp[6 * p + t - 21] = -red[t * kNT];
+        }
+    } else {
+        const int l = (blockIdx.x - P.np) * kNT + t;
+        if (l < P.L) {
+            double h[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+            for (int k = P.le_off[l]; k < P.le_off[l + 1]; ++k) {
+                const int e = P.le[k];
+                const double* jl = P.Jl + 6 * (int64_t)e;
+                const double e0 = P.err[2 * e], e1 = P.err[2 * e + 1];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+#pragma unroll
+                    for (int b = a; b < 3; ++b) h[3 * a + b] = h[3 * a + b] + (jl[a] * jl[b] + jl[3 + a] * jl[3 + b]);
+                    g[a] = g[a] + (jl[a] * e0 + jl[3 + a] * e1);
+                }
+            }
+            double m = 0.0;
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
 #pragma unroll
-                for (int b = a; b < 3; ++b) h[3 * a + b] = h[3 * a + b] + (jl[a] * jl[b] + jl[3 + a] * jl[3 + b]);
-                g[a] = g[a] + (jl[a] * e0 + jl[3 + a] * e1);
+                for (int b = a; b < 3; ++b) {
+                    P.Hll[9 * l + 3 * a + b] = h[3 * a + b];
+                    P.Hll[9 * l + 3 * b + a] = h[3 * a + b];
+                }
+                P.bl[3 * l + a] = -g[a];
+                m = fmax(m, fabs(h[4 * a]));
             }
-        }
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-#pragma unroll
-            for (int b = a; b < 3; ++b) {
-                P.Hll[9 * l + 3 * a + b] = h[3 * a + b];
-                P.Hll[9 * l + 3 * b + a] = h[3 * a + b];
-            }
-            P.bl[3 * l + a] = -g[a];
-            m = fmax(m, fabs(h[4 * a]));
+            if (first) atomic_max_abs(P.maxdiag, m);
         }
     }
-    if (l < P.np) {  // the free poses' diagonals, lane l -> pose nf + l
-        const double* H = P.Hpp + 36 * (P.nf + l);
-#pragma unroll
-        for (int a = 0; a < 6; ++a) m = fmax(m, fabs(H[7 * a]));
-    }
-    if (maxdiag && m > 0.0) atomicMax(maxdiag, (unsigned long long)__double_as_longlong(m));
+    if (P.ctl && ba_last_block(P.ticket + 0) && t == 0) ba_ctl_iter_begin(P.ctl, first ? P.maxdiag : nullptr);
 }
 
 __device__ __forceinline__ void inv3(const double* a, double* o) {
@@ -250,8 +322,9 @@ __global__ __launch_bounds__(256) void ba_landmark_trial_kernel(BaParams P, doub
     }
 }
 
-constexpr int kSchurChunk = 128;  // pairs per pass = threads per workgroup
+constexpr int kSchurPass = 128;   // pairs per pass
 constexpr int kSchurStride = 37;  // doubles per staged pair: 36 products + 1 (2-way instead of 8-way bank conflicts)
+constexpr int kSchurThreads = 256;
 
 // 18 doubles (one 6 x 3 block, 144 B, 16-B aligned) into registers
 __device__ __forceinline__ void load18(const double* src, double* r) {
@@ -264,33 +337,48 @@ __device__ __forceinline__ void load18(const double* src, double* r) {
     }
 }
 
-// the sequential chain v = v - d_0 - d_1 - ... over n staged products (LDS loads 8 ahead of the chain)
+// the sequential chain v = v - d_0 - d_1 - ... over n staged products: the LDS loads of the next eight are issued
+// before this eight's subtractions (double-buffered), so the chain waits on FP64 latency, not on LDS
 __device__ __forceinline__ double schur_chain(double v, const double* sd, int n, int col) {
     int j = 0;
-    for (; j + 8 <= n; j += 8) {
+    if (n >= 8) {
         double d[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) d[u] = sd[(j + u) * kSchurStride + col];
+        for (int u = 0; u < 8; ++u) d[u] = sd[u * kSchurStride + col];
+        for (; j + 16 <= n; j += 8) {
+            double e[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) e[u] = sd[(j + 8 + u) * kSchurStride + col];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v = v - d[u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) d[u] = e[u];
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u) v = v - d[u];
+        j += 8;
     }
     for (; j < n; ++j) v = v - sd[j * kSchurStride + col];
     return v;
 }
 
-// One 128-lane workgroup per upper Schur block (p1 <= p2) of the free poses, then one per free pose for b_schur.
+// One 256-thread workgroup per upper Schur block (p1 <= p2) of the free poses, then one per free pose for b_schur.
 // Block: entry (a, b) is the oracle's sequential chain over the landmarks the two poses share,
-// v = v - (W_e1[a] . H_pl(e2)[b]). Per pass of 128 pairs every lane forms one pair's 36 products from its registers
-// into LDS (the next pass's blocks already loading), then lane a * 6 + b (< 36) runs its chain over them: one LDS
-// load and one subtraction per pair. On a diagonal block only a >= b writes (the oracle's loop leaves the (max, min)
-// value in both mirrored entries). b_schur: lane a < 6 runs v = b_p[a] - sum_e W_e[a] . b_l(e) over the pose's edges.
-__global__ __launch_bounds__(kSchurChunk) void ba_schur_kernel(BaParams P, double lambda) {
-    __shared__ double sd[kSchurChunk * kSchurStride];
+// v = v - (W_e1[a] . H_pl(e2)[b]). The waves are specialised: waves 1-3 produce, wave 0 consumes. In pass q the
+// producers form pass q's 128 pairs' 36 products from their registers into one half of a double-buffered LDS stage
+// (and start loading pass q + 2's blocks), while lanes a * 6 + b (< 36) of wave 0 run their chains over pass q - 1's
+// products in the other half (one LDS load and one subtraction per pair); one barrier per pass. On a diagonal block
+// only a >= b writes (the oracle's loop leaves the (max, min) value in both mirrored entries). b_schur: lanes a < 6
+// run v = b_p[a] - sum_e W_e[a] . b_l(e) over the pose's edges, the products formed the same way.
+__global__ __launch_bounds__(kSchurThreads) void ba_schur_kernel(BaParams P, double lambda) {
+    __shared__ double sd[2][kSchurPass * kSchurStride];
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     if (P.lam) lambda = *P.lam;
     const int np = P.np, nb = np * (np + 1) / 2;
-    const int lane = threadIdx.x;
-    const int a = lane / 6, b = lane - 6 * (lane / 6);
+    const int t = threadIdx.x;
+    const int pi = t - 64;  // producer index (waves 1-3), < kSchurPass for the producing lanes
+    const bool prod = pi >= 0 && pi < kSchurPass;
+    const int a = t / 6, b = t - 6 * (t / 6);
     if ((int)blockIdx.x < nb) {
         int blk = blockIdx.x, i1 = 0;
         while (blk >= np - i1) {
@@ -299,33 +387,43 @@ __global__ __launch_bounds__(kSchurChunk) void ba_schur_kernel(BaParams P, doubl
         }
         const int i2 = i1 + blk;
         const int p1 = P.nf + i1, p2 = P.nf + i2;
-        const bool active = lane < 36 && !(i1 == i2 && a < b);
+        const bool active = t < 36 && !(i1 == i2 && a < b);
         double v = 0.0;
         if (active) v = p1 == p2 ? P.Hpp[36 * p1 + 6 * a + b] + (a == b ? lambda : 0.0) : 0.0;
         const int c0 = P.cv_off[p1 * P.P + p2], c1 = P.cv_off[p1 * P.P + p2 + 1];
-        double rw[18], rh[18];
-        if (c0 + lane < c1) {
-            load18(P.W + 18 * (int64_t)P.cv_e1[c0 + lane], rw);
-            load18(P.Hpl + 18 * (int64_t)P.cv_e2[c0 + lane], rh);
+        const int npass = (c1 - c0 + kSchurPass - 1) / kSchurPass;
+        double rw[2][18], rh[2][18];  // the blocks of passes q (slot q & 1) and q + 1
+        if (prod) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                if (c0 + u * kSchurPass + pi < c1) {
+                    load18(P.W + 18 * (int64_t)P.cv_e1[c0 + u * kSchurPass + pi], rw[u]);
+                    load18(P.Hpl + 18 * (int64_t)P.cv_e2[c0 + u * kSchurPass + pi], rh[u]);
+                }
         }
-        for (int base = c0; base < c1; base += kSchurChunk) {
-            const int n = min(kSchurChunk, c1 - base);
-            if (lane < n) {
+        // passes in pairs so the register slot (q & 1) is a compile-time index
+        auto pass = [&](const int q, double (&w_)[18], double (&h_)[18], double* buf, const double* prev) {
+            if (prod && q < npass) {
+                if (c0 + q * kSchurPass + pi < c1) {
+                    double* dst = &buf[pi * kSchurStride];
 #pragma unroll
-                for (int x = 0; x < 6; ++x)
+                    for (int x = 0; x < 6; ++x)
 #pragma unroll
-                    for (int y = 0; y < 6; ++y)
-                        sd[lane * kSchurStride + 6 * x + y] =
-                            rw[3 * x] * rh[3 * y] + rw[3 * x + 1] * rh[3 * y + 1] + rw[3 * x + 2] * rh[3 * y + 2];
+                        for (int y = 0; y < 6; ++y)
+                            dst[6 * x + y] = w_[3 * x] * h_[3 * y] + w_[3 * x + 1] * h_[3 * y + 1] + w_[3 * x + 2] * h_[3 * y + 2];
+                }
+                const int nx = c0 + (q + 2) * kSchurPass + pi;
+                if (nx < c1) {
+                    load18(P.W + 18 * (int64_t)P.cv_e1[nx], w_);
+                    load18(P.Hpl + 18 * (int64_t)P.cv_e2[nx], h_);
+                }
             }
-            const int nxt = base + kSchurChunk + lane;
-            if (nxt < c1) {
-                load18(P.W + 18 * (int64_t)P.cv_e1[nxt], rw);
-                load18(P.Hpl + 18 * (int64_t)P.cv_e2[nxt], rh);
-            }
+            if (active && q > 0) v = schur_chain(v, prev, min(kSchurPass, c1 - c0 - (q - 1) * kSchurPass), t);
             __syncthreads();
-            if (active) v = schur_chain(v, sd, n, lane);
-            __syncthreads();
+        };
+        for (int q = 0; q <= npass; q += 2) {
+            pass(q, rw[0], rh[0], sd[0], sd[1]);
+            if (q + 1 <= npass) pass(q + 1, rw[1], rh[1], sd[1], sd[0]);
         }
         if (active) {
             const int r = 6 * i1 + a, c = 6 * i2 + b, ns = P.ns;
@@ -334,40 +432,53 @@ __global__ __launch_bounds__(kSchurChunk) void ba_schur_kernel(BaParams P, doubl
         }
     } else {
         const int j = blockIdx.x - nb, p = P.nf + j;
-        const bool active = lane < 6;
-        double v = active ? P.bp[6 * p + lane] : 0.0;
+        const bool active = t < 6;
+        double v = active ? P.bp[6 * p + t] : 0.0;
         const int k0 = P.pe_off[p], k1 = P.pe_off[p + 1];
-        double rw[18], rg[3];
-        if (k0 + lane < k1) {
-            const int e = P.pe[k0 + lane];
-            load18(P.W + 18 * (int64_t)e, rw);
-            const double* g = P.bl + 3 * P.el[e];
-            rg[0] = g[0]; rg[1] = g[1]; rg[2] = g[2];
-        }
-        for (int base = k0; base < k1; base += kSchurChunk) {
-            const int n = min(kSchurChunk, k1 - base);
-            if (lane < n) {
+        const int npass = (k1 - k0 + kSchurPass - 1) / kSchurPass;
+        double rw[2][18], rg[2][3];
+        if (prod) {
 #pragma unroll
-                for (int x = 0; x < 6; ++x)
-                    sd[lane * kSchurStride + x] = rw[3 * x] * rg[0] + rw[3 * x + 1] * rg[1] + rw[3 * x + 2] * rg[2];
-            }
-            const int nxt = base + kSchurChunk + lane;
-            if (nxt < k1) {
-                const int e = P.pe[nxt];
-                load18(P.W + 18 * (int64_t)e, rw);
-                const double* g = P.bl + 3 * P.el[e];
-                rg[0] = g[0]; rg[1] = g[1]; rg[2] = g[2];
-            }
-            __syncthreads();
-            if (active) v = schur_chain(v, sd, n, lane);
-            __syncthreads();
+            for (int u = 0; u < 2; ++u)
+                if (k0 + u * kSchurPass + pi < k1) {
+                    const int e = P.pe[k0 + u * kSchurPass + pi];
+                    load18(P.W + 18 * (int64_t)e, rw[u]);
+                    const double* g = P.bl + 3 * P.el[e];
+                    rg[u][0] = g[0];
+                    rg[u][1] = g[1];
+                    rg[u][2] = g[2];
+                }
         }
-        if (active) P.bs[6 * j + lane] = v;
+        auto pass = [&](const int q, double (&w_)[18], double (&g_)[3], double* buf, const double* prev) {
+            if (prod && q < npass) {
+                if (k0 + q * kSchurPass + pi < k1) {
+                    double* dst = &buf[pi * kSchurStride];
+#pragma unroll
+                    for (int x = 0; x < 6; ++x) dst[x] = w_[3 * x] * g_[0] + w_[3 * x + 1] * g_[1] + w_[3 * x + 2] * g_[2];
+                }
+                const int nx = k0 + (q + 2) * kSchurPass + pi;
+                if (nx < k1) {
+                    const int e = P.pe[nx];
+                    load18(P.W + 18 * (int64_t)e, w_);
+                    const double* g = P.bl + 3 * P.el[e];
+                    g_[0] = g[0];
+                    g_[1] = g[1];
+                    g_[2] = g[2];
+                }
+            }
+            if (active && q > 0) v = schur_chain(v, prev, min(kSchurPass, k1 - k0 - (q - 1) * kSchurPass), t);
+            __syncthreads();
+        };
+        for (int q = 0; q <= npass; q += 2) {
+            pass(q, rw[0], rg[0], sd[0], sd[1]);
+            if (q + 1 <= npass) pass(q + 1, rw[1], rg[1], sd[1], sd[0]);
+        }
+        if (active) P.bs[6 * j + t] = v;
     }
 }
 
-// Eigen LDLT on the reduced system (n <= kLdltMaxN), bit-identical to the oracle's left-looking or_ldlt_solve
-// (diagonal pivoting), in three steps:
+// Eigen LDLT on the reduced system (n <= kLdltRegN = 128), bit-identical to the oracle's left-looking
+// or_ldlt_solve (diagonal pivoting), in one 256-thread workgroup with no workgroup barrier inside the factorisation:
 //  1. The pivot sequence. At step k the oracle takes the first position of the largest |L(i, i)|, i >= k, and L(i, i)
 //     for i >= k still holds an original diagonal entry (it is only updated at its own step), so the sequence follows
 //     from the diagonal alone. Distinct values (the usual case): it is the descending order, by ranks. Any tie or NaN:
@@ -375,28 +486,28 @@ __global__ __launch_bounds__(kSchurChunk) void ba_schur_kernel(BaParams P, doubl
 //  2. Pivoting commutes with the left-looking factorisation: the oracle swaps untouched original entries in the
 //     trailing part and the finished rows of L, so its result equals the unpivoted factorisation of P S P^T (S is
 //     bitwise symmetric: each Schur entry is stored to both halves from one value).
-//  3. The unpivoted factorisation runs right-looking on the packed lower triangle in LDS: the oracle forms column k
-//     as acc = L(i, k) - L(i, 0) t_0 - L(i, 1) t_1 - ... (t_j = D(j) L(k, j)) and D(k) = L(k, k) - (L(k, 0) t_0 +
-//     ...); step j here applies term j of every such chain at once (L(i, c) -= L(i, j) (D(j) L(c, j)), i > c > j;
-//     dot_c += L(c, j) (D(j) L(c, j))), the same operations in the same order per entry.  Per step only the live
-//     trailing triangle is touched (its entries dealt to the threads by row group and column lane), and the entries
-//     of the next column are updated, divided and published in the same step, so one barrier separates the steps.
-//     (The round-1 form kept 16-column row segments in registers with two barriers per step: every segment paid its
-//     predicated FP64 updates each step, 188 us at n = 114 against this form's 130 us.)
-// The triangular solves then run on wave 0 alone, the vector in registers, broadcasts by v_readlane.
-constexpr int kLdltMaxN = 120;
-
-constexpr int kLdltThreads = 1024;  // 256 / 512 / 1024 threads: 184 / 138 / 123 us per factorisation at n = 114
-
-__device__ __forceinline__ int tri(int i, int j) { return (i * (i + 1) >> 1) + j; }
-
-// the row of packed lower-triangle index e: the largest q with q (q + 1) / 2 <= e (e < 2^20)
-__device__ __forceinline__ int tri_row(int e) {
-    int q = (int)((sqrtf(8.f * (float)e + 1.f) - 1.f) * 0.5f);
-    if (((q + 1) * (q + 2) >> 1) <= e) ++q;
-    if ((q * (q + 1) >> 1) > e) --q;
-    return q;
-}
+//  3. The unpivoted factorisation runs right-looking with the matrix in registers: wave w holds columns c = 4 j + w
+//     (j < 32) of P S P^T, lane l rows l and l + 64. The oracle forms column k as acc = L(i, k) - L(i, 0) t_0 -
+//     L(i, 1) t_1 - ... (t_j = D(j) L(k, j)) and D(k) = L(k, k) - (L(k, 0) t_0 + ...); step j here applies term j of
+//     every such chain (L(i, c) -= L(i, j) t_j(c), t_j(c) = D(j) L(c, j); dot_i += L(i, j) t_j(i)), the same operations
+//     in the same order per entry. Column k is finalised by the wave that holds it (D(k), the rows divided by it) and
+//     published: L(., k) into the column store (kept for the solves), t_k(.) into a ring of kLdltRing slots, then a
+//     per-slot flag (workgroup-scope release / acquire). At step k a wave waits for column k's flag; the wave that
+//     holds column k + 1 first applies term k to it, finalises and publishes it (a switch on its slot), so the critical
+//     path per column is one LDS hand-off, one update and one division; then every wave applies term k to all 32 of
+//     its slots without a branch (a finalised column's registers are dead, so updating them again is harmless, and
+//     straight-line code keeps the FP64 pipe busy). A slot is rewritten kLdltRing columns later, which needs every
+//     wave to have read it (a wave owns one of any four consecutive columns, so none can run more than four columns
+//     ahead of another). Wave 0 also runs the forward solve v(i) -= L(i, k) v(k) at step k, in the oracle's order.
+//     (Round 4 kept the packed triangle in LDS with one workgroup barrier per column step: 139 us per factorisation
+//     at n = 120 in the configs[2] sequence.)
+//  4. The diagonal and backward solves run on wave 0: the vector in registers (two entries per lane), broadcasts by
+//     v_readlane, L read by row from the column store (stride 129 doubles: conflict-free by rows and by columns),
+//     eight columns' loads ahead of the dependent chain.
+constexpr int kLdltRegN = 128;   // n <= 128: lane l holds rows l and l + 64
+constexpr int kLdltSlots = 32;   // columns per wave: c = 4 j + w
+constexpr int kLdltLs = 129;     // column stride of the L store (doubles)
+constexpr int kLdltRing = 8;     // t_k slots (>= 5 needed)
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
     const long long b = __double_as_longlong(v);
@@ -412,37 +523,98 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// t_k(r) of one ring slot is stored at [(r & 3) * 32 + (r >> 2)]: wave w reads its 32 columns' values contiguously
+__device__ __forceinline__ int tq_index(int r) { return ((r & 3) << 5) + (r >> 2); }
+
 #ifdef YAVO_LM_PROFILE
-// profiling builds: cycles of lane 0 of every wave in the LDLT's phases, summed over the launches
-__device__ unsigned long long g_ldlt_prof[kLdltThreads / 64][8];
+// profiling builds: shader cycles of lane 0 of each wave in the phases of the LDLT, summed over launches
+__device__ unsigned long long g_ldlt_prof[4][8];
 #define LDP_DECL unsigned long long ldp_t = __builtin_readcyclecounter(), ldp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define LDP_MARK(k) do { const unsigned long long t_ = __builtin_readcyclecounter(); ldp_acc[k] += t_ - ldp_t; ldp_t = t_; } while (0)
-#define LDP_STORE() do { if ((threadIdx.x & 63) == 0) for (int q_ = 0; q_ < 8; ++q_) atomicAdd(&g_ldlt_prof[threadIdx.x >> 6][q_], ldp_acc[q_]); } while (0)
+#define LDP_MARK(q) do { const unsigned long long t_ = __builtin_readcyclecounter(); ldp_acc[q] += t_ - ldp_t; ldp_t = t_; } while (0)
+#define LDP_STORE() do { if (l == 0) for (int q_ = 0; q_ < 8; ++q_) atomicAdd(&g_ldlt_prof[w][q_], ldp_acc[q_]); } while (0)
 #else
 #define LDP_DECL
-#define LDP_MARK(k) do {} while (0)
+#define LDP_MARK(q) do {} while (0)
 #define LDP_STORE() do {} while (0)
 #endif
-__global__ __launch_bounds__(kLdltThreads) void ba_ldlt_lds_kernel(BaParams P) {
+
+// step k's update of slot J (its column 4 J + w), and, when that column is k + 1, its finalisation and publication
+#define LDLT_UPD(J)                                                                            \
+    do {                                                                                       \
+        if ((J) < kLdltSlots / 2) Al[(J) < kLdltSlots / 2 ? (J) : 0] -= lk0 * tv[J];           \
+        Ah[J] -= lk1 * tv[J];                                                                  \
+    } while (0)
+#define LDLT_FIN(J)                                                                            \
+    case J: {                                                                                  \
+        /* read-only on the slot's registers (the bulk update below writes them): no copies */ \
+        const double dk = dkn - readlane_f64((J) < kLdltSlots / 2 ? dot0 : dot1, kn & 63);     \
+        const bool valid = fabs(dk) > 0;                                                       \
+        if ((J) < kLdltSlots / 2) {                                                            \
+            const double a_ = Al[(J) < kLdltSlots / 2 ? (J) : 0] - lk0 * tkn;                  \
+            const double L0 = valid ? a_ / dk : a_;                                            \
+            Lcn[r0] = L0;                                                                      \
+            tqn[tq0] = dk * L0;                                                                \
+        }                                                                                      \
+        const double b_ = Ah[J] - lk1 * tkn;                                                   \
+        const double L1 = valid ? b_ / dk : b_;                                                \
+        Lcn[r1] = L1;                                                                          \
+        tqn[tq1] = dk * L1;                                                                    \
+        if (l == 0) Dv[kn] = dk;                                                               \
+        __hip_atomic_store(&flag[kn & (kLdltRing - 1)], kn, __ATOMIC_RELEASE,                  \
+                           __HIP_MEMORY_SCOPE_WORKGROUP);                                      \
+    } break;
+
+__global__ __launch_bounds__(256) void ba_ldlt_reg_kernel(BaParams P) {
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    __shared__ double Ls[kLdltMaxN * (kLdltMaxN + 1) / 2];  // the factor, for the solves
-    __shared__ double tv[2][kLdltMaxN];  // t_i = D(k) L(i, k) of step k in tv[k & 1]
-    __shared__ double dor[kLdltMaxN];    // the diagonal of P S P^T
-    __shared__ double dotp[kLdltMaxN];   // row i's diagonal chain L(i, 0) t_i(0) + ... through the last step
-    __shared__ double dg[kLdltMaxN];    // |diagonal|, permuted as the pivots are taken
-    __shared__ int perm[kLdltMaxN];     // position -> original index: (P S P^T)(i, j) = S(perm[i], perm[j])
+    __shared__ double Lc[kLdltRegN * kLdltLs];      // S row-major (n x n) first, then L(r, c) at Lc[c * 129 + r]
+    __shared__ double tq[kLdltRing][kLdltRegN];     // t_k(r) = D(k) L(r, k) of column k in slot k % kLdltRing
+    __shared__ double Dv[kLdltRegN];                // D(k)
+    __shared__ double dor[kLdltRegN];               // the diagonal of P S P^T
+    __shared__ double dg[kLdltRegN];                // |diagonal|, permuted as the pivots are taken
+    __shared__ int perm[kLdltRegN];                 // position -> original index: (P S P^T)(i, j) = S(perm[i], perm[j])
+    __shared__ int flag[kLdltRing];                 // the column a slot holds (-1: none yet)
     __shared__ int s_slow;
-    const int n = P.ns, t = threadIdx.x;
+    const int n = P.ns, t = threadIdx.x, l = t & 63;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int r0 = l, r1 = l + 64;
     LDP_DECL
+    {
+        // S staged row-major, sixteen 16-B loads per thread in flight
+        const int nh = (n * n) >> 1;
+        const double2* src = reinterpret_cast<const double2*>(P.S);
+        double2* dst = reinterpret_cast<double2*>(Lc);
+        for (int e0 = t; e0 < nh; e0 += 16 * 256) {
+            double2 v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = e0 + 256 * u < nh ? src[e0 + 256 * u] : make_double2(0.0, 0.0);
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (e0 + 256 * u < nh) dst[e0 + 256 * u] = v[u];
+        }
+        if (((n * n) & 1) && t == 0) Lc[n * n - 1] = P.S[n * n - 1];
+    }
+    if (t < kLdltRing) flag[t] = -1;
     if (t == 0) s_slow = 0;
-    for (int i = t; i < n; i += kLdltThreads) dg[i] = fabs(P.S[(int64_t)i * n + i]);
+    __syncthreads();
+    if (t < n) dg[t] = fabs(Lc[t * n + t]);
     __syncthreads();
     // 1. ranks by (|d| descending, index ascending); a tie or a NaN sends the sequence to the replay
     if (t < n) {
         const double d = dg[t];
         int rank = 0;
         bool tie = isnan(d);
-        for (int j = 0; j < n; ++j) {
+        int j = 0;
+        for (; j + 8 <= n; j += 8) {
+            double o[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) o[u] = dg[j + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                rank += o[u] > d;
+                tie |= (o[u] == d && j + u != t);
+            }
+        }
+        for (; j < n; ++j) {
             const double o = dg[j];
             rank += o > d;
             tie |= (o == d && j != t);
@@ -493,132 +665,178 @@ __global__ __launch_bounds__(kLdltThreads) void ba_ldlt_lds_kernel(BaParams P) {
     // the oracle's first step: a zero (or NaN) pivot ends the factorisation with only its own transposition applied
     // to the matrix and none to the vector
     const int big0 = perm[0];
-    const double a00 = P.S[(int64_t)big0 * n + big0];
+    const double a00 = Lc[big0 * n + big0];
     const bool brk = !(fabs(a00) > 0);
     __syncthreads();
     if (brk) {
-        for (int i = t; i < n; i += kLdltThreads) perm[i] = i == 0 ? big0 : (i == big0 ? 0 : i);
+        if (t < n) perm[t] = t == 0 ? big0 : (t == big0 ? 0 : t);
         __syncthreads();
     }
-    // 2. P S P^T (lower triangle and diagonal) into LDS, packed by rows: Ls[tri(i, j)] = S(perm[i], perm[j])
-    const int ntri = n * (n + 1) / 2;
-    for (int e = t; e < ntri; e += kLdltThreads) {
-        const int i = tri_row(e);
-        Ls[e] = P.S[(int64_t)perm[i] * n + perm[e - tri(i, 0)]];
-    }
-    __syncthreads();
-    for (int i = t; i < n; i += kLdltThreads) dor[i] = Ls[tri(i, i)];
-    // column 0: L(i, 0) = S(i, 0) / D(0), t_i = D(0) L(i, 0), the diagonal chains' first terms
-    if (!brk) {
-        for (int i = t + 1; i < n; i += kLdltThreads) {
-            const double l = Ls[tri(i, 0)] / a00;
-            Ls[tri(i, 0)] = l;
-            const double tt = a00 * l;
-            tv[0][i] = tt;
-            dotp[i] = l * tt;
+    // 2. P S P^T into registers: Al[j] = entry (r0, 4 j + w) for the columns below 64, Ah[j] = (r1, 4 j + w); only the
+    // strict lower triangle is read (the rest is never used)
+    double Al[kLdltSlots / 2], Ah[kLdltSlots];
+    const int tq0 = tq_index(r0), tq1 = tq_index(r1);
+    {
+        const int p0 = r0 < n ? perm[r0] : 0, p1 = r1 < n ? perm[r1] : 0;
+#pragma unroll
+        for (int j = 0; j < kLdltSlots; ++j) {
+            const int c = 4 * j + w;
+            const int pc = c < n ? perm[c] : 0;
+            if (j < kLdltSlots / 2) Al[j] = (r0 > c && r0 < n) ? Lc[p0 * n + pc] : 0.0;
+            Ah[j] = (r1 > c && r1 < n) ? Lc[p1 * n + pc] : 0.0;
         }
+        if (t < n) dor[t] = Lc[perm[t] * n + perm[t]];
     }
-    __syncthreads();
-    LDP_MARK(0);
-    // 3. right-looking, unpivoted, one barrier per step.  At step k column k is final (L(i, k), t_i = D(k) L(i, k)
-    // in tv[k & 1]) and dotp[i] holds row i's diagonal chain through term k.  Every thread forms D(k + 1) = S(k+1,
-    // k+1) - dotp[k + 1]; the rows of column k + 1 apply term k to that entry, divide by D(k + 1) and publish it (the
-    // next step's input, and term k + 1 of their diagonal chain); the rest of the trailing triangle (k + 2 <= c < i)
-    // applies term k, its entries dealt to the threads in row-major order.
-    int sign = 0;
-    double akk = a00;
-    for (int k = 0; k < n && !brk; ++k) {
-        const int buf = k & 1;
-        const double* tk = tv[buf];
-        if (t == 0) {
-            Ls[tri(k, k)] = akk;
-            if (sign == 1) { if (akk < 0) sign = 3; }
-            else if (sign == 2) { if (akk > 0) sign = 3; }
-            else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+    // the right-hand side, permuted (a zero first pivot: not permuted) -- wave 0 solves
+    double v0 = 0.0, v1 = 0.0;
+    if (w == 0) {
+        v0 = r0 < n ? P.bs[brk ? r0 : perm[r0]] : 0.0;
+        v1 = r1 < n ? P.bs[brk ? r1 : perm[r1]] : 0.0;
+    }
+    __syncthreads();  // the staged S is dead: Lc becomes the column store
+    int err = 0;
+    if (brk) {
+        // the solves read P S P^T as it stands
+#pragma unroll
+        for (int j = 0; j < kLdltSlots; ++j) {
+            const int c = 4 * j + w;
+            if (c < n) {
+                if (j < kLdltSlots / 2) Lc[c * kLdltLs + r0] = Al[j];
+                Lc[c * kLdltLs + r1] = Ah[j];
+            }
         }
-        if (k + 1 < n) {
-            // column k + 1: row k + 2 + j on thread t with j = (t % NW) 64 + t / NW (NW waves), so the rows, and the
-            // latency of their divisions, are spread over every wave; the row's loads are issued before D(k + 1)
-            constexpr int NW = kLdltThreads / 64;
-            const int i1 = k + 2 + (t % NW) * 64 + t / NW;
-            double cx = 0.0, lk = 0.0, dp = 0.0;
-            if (i1 < n) {
-                cx = Ls[tri(i1, k + 1)];
-                lk = Ls[tri(i1, k)];
-                dp = dotp[i1];
+        if (t < n) Dv[t] = dor[t];
+        __syncthreads();
+        if (w == 0)
+            for (int j = 0; j < n; ++j) {
+                const double vj = readlane_f64(j < 64 ? v0 : v1, j & 63);
+                const double a0 = Lc[j * kLdltLs + r0], a1 = Lc[j * kLdltLs + r1];
+                if (r0 > j && r0 < n) v0 = v0 - a0 * vj;
+                if (r1 > j && r1 < n) v1 = v1 - a1 * vj;
             }
-            const double akk1 = dor[k + 1] - dotp[k + 1];
-            const bool v1 = fabs(akk1) > 0;
-            const double t1 = tk[k + 1];
-            LDP_MARK(1);
-            if (i1 < n) {
-                const double acc = cx - lk * t1;
-                const double l = v1 ? acc / akk1 : acc;
-                Ls[tri(i1, k + 1)] = l;
-                const double tt = akk1 * l;
-                tv[buf ^ 1][i1] = tt;
-                dotp[i1] = dp + l * tt;
-            }
-            LDP_MARK(2);
-            // the rest of the trailing triangle, k + 2 <= c < i: thread (row group t >> 4, column lane t & 15) takes
-            // rows k + 3 + (t >> 4) + (kLdltThreads / 16) m and, in each, columns k + 2 + (t & 15) + 16 j (no index
-            // decode; a wave's 16 column lanes read consecutive entries)
-            {
-                const int rg = t >> 4, cl = t & 15;
-                for (int i = k + 3 + rg; i < n; i += kLdltThreads / 16) {
-                    const int rb = tri(i, 0);
-                    const double li = Ls[rb + k];
-                    for (int c = k + 2 + cl; c < i; c += 16) Ls[rb + c] = Ls[rb + c] - li * tk[c];
+    } else {
+        // 3. column 0 (wave 0): D(0) = a00, nonzero here
+        if (w == 0) {
+            const double L0 = Al[0] / a00, L1 = Ah[0] / a00;
+            Lc[r0] = L0;
+            Lc[r1] = L1;
+            tq[0][tq0] = a00 * L0;
+            tq[0][tq1] = a00 * L1;
+            if (l == 0) Dv[0] = a00;
+            __hip_atomic_store(&flag[0], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        double dot0 = 0.0, dot1 = 0.0;  // rows r0, r1: L(r, 0) t_0(r) + L(r, 1) t_1(r) + ... (term 0 assigns)
+        LDP_MARK(0);
+        for (int k = 0; k < n; ++k) {
+            const int s = k & (kLdltRing - 1);
+            for (int spin = 0; __hip_atomic_load(&flag[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != k;) {
+                if (++spin > (1 << 24)) {  // never expected: a bounded wait, reported as a failed solve
+                    err = 1;
+                    break;
                 }
             }
-            akk = akk1;
-            LDP_MARK(3);
+            if (err) break;
+            LDP_MARK(1);
+            const int kn = k + 1;
+            // the loads the critical path needs first (this wave's rows of column k and their t values, D's source),
+            // then, after the column k + 1 hand-off, the t values of all 32 columns for the bulk update
+            const double dkn = dor[kn < n ? kn : 0];
+            const double lk0 = Lc[k * kLdltLs + r0], lk1 = Lc[k * kLdltLs + r1];
+            const double tk0 = tq[s][tq0], tk1 = tq[s][tq1];
+            dot0 = k == 0 ? lk0 * tk0 : dot0 + lk0 * tk0;
+            dot1 = k == 0 ? lk1 * tk1 : dot1 + lk1 * tk1;
+            LDP_MARK(2);
+            if (kn < n && (kn & 3) == w) {  // this wave holds column k + 1 (wave-uniform)
+                double* const Lcn = &Lc[kn * kLdltLs];
+                double* const tqn = &tq[kn & (kLdltRing - 1)][0];
+                const double tkn = readlane_f64(kn < 64 ? tk0 : tk1, kn & 63);  // t_k(k + 1): row k + 1's t value
+                switch (kn >> 2) {
+                    LDLT_FIN(0) LDLT_FIN(1) LDLT_FIN(2) LDLT_FIN(3) LDLT_FIN(4) LDLT_FIN(5) LDLT_FIN(6) LDLT_FIN(7)
+                    LDLT_FIN(8) LDLT_FIN(9) LDLT_FIN(10) LDLT_FIN(11) LDLT_FIN(12) LDLT_FIN(13) LDLT_FIN(14)
+                    LDLT_FIN(15) LDLT_FIN(16) LDLT_FIN(17) LDLT_FIN(18) LDLT_FIN(19) LDLT_FIN(20) LDLT_FIN(21)
+                    LDLT_FIN(22) LDLT_FIN(23) LDLT_FIN(24) LDLT_FIN(25) LDLT_FIN(26) LDLT_FIN(27) LDLT_FIN(28)
+                    LDLT_FIN(29) LDLT_FIN(30) LDLT_FIN(31)
+                    default: break;
+                }
+                LDP_MARK(3);
+            }
+            double tv[kLdltSlots];
+            {
+                const double2* tw = reinterpret_cast<const double2*>(&tq[s][w << 5]);  // t_k(4 j + w) at [j]
+#pragma unroll
+                for (int q = 0; q < kLdltSlots / 2; ++q) {
+                    const double2 v = tw[q];
+                    tv[2 * q] = v.x;
+                    tv[2 * q + 1] = v.y;
+                }
+            }
+            // term k on every slot, branch-free (finalised columns' registers are dead)
+#pragma unroll
+            for (int j = 0; j < kLdltSlots; ++j) LDLT_UPD(j);
+            if (w == 0) {  // the forward solve's step k: rows below k
+                const double vk = readlane_f64(k < 64 ? v0 : v1, k & 63);
+                if (r0 > k && r0 < n) v0 = v0 - lk0 * vk;
+                if (r1 > k && r1 < n) v1 = v1 - lk1 * vk;
+            }
+            LDP_MARK(4);
         }
-        __syncthreads();
-        LDP_MARK(4);
     }
-    if (brk) sign = 0;  // the solves read the untouched P S P^T
-    if (t >= 64) {
+    __syncthreads();
+    LDP_MARK(5);
+    if (w != 0) {
         LDP_STORE();
         return;  // no barrier below
     }
-    // the solves on wave 0: lane l holds positions l and l + 64
-    const int q0 = t, q1 = t + 64;
-    double v0 = 0.0, v1 = 0.0;
-    if (q0 < n) v0 = P.bs[brk ? q0 : perm[q0]];
-    if (q1 < n) v1 = P.bs[brk ? q1 : perm[q1]];
-#pragma unroll 4
-    for (int j = 0; j < n; ++j) {
-        const double vj = readlane_f64(j < 64 ? v0 : v1, j & 63);
-        const double a0 = q0 > j && q0 < n ? Ls[tri(q0, j)] : 0.0;
-        const double a1 = q1 > j && q1 < n ? Ls[tri(q1, j)] : 0.0;
-        if (q0 > j && q0 < n) v0 = v0 - a0 * vj;
-        if (q1 > j && q1 < n) v1 = v1 - a1 * vj;
+    // 4. diagonal and backward solves on wave 0: lane l holds positions r0 and r1
+    const double d0 = r0 < n ? Dv[r0] : 1.0, d1 = r1 < n ? Dv[r1] : 1.0;
+    if (r0 < n) v0 = fabs(d0) > DBL_MIN ? v0 / d0 : 0.0;
+    if (r1 < n) v1 = fabs(d1) > DBL_MIN ? v1 / d1 : 0.0;
+    // backward, eight columns a block: (a) the block's own rows take their terms one column after the other (the
+    // dependent chain: v(j) final, broadcast, the rows above j in the block), (b) the rows above the block take the
+    // block's eight terms, still in descending j -- every row's terms in the oracle's order
+    for (int j0 = n - 1; j0 >= 0; j0 -= 8) {
+        const int jb = j0 - 7 < 0 ? 0 : j0 - 7;
+        double a0[8], a1[8], vj[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = j0 - u < 0 ? 0 : j0 - u;
+            a0[u] = Lc[r0 * kLdltLs + j];
+            a1[u] = Lc[r1 * kLdltLs + j];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = j0 - u;
+            vj[u] = 0.0;
+            if (j >= jb) {
+                vj[u] = readlane_f64(j < 64 ? v0 : v1, j & 63);
+                const double n0 = v0 - a0[u] * vj[u], n1 = v1 - a1[u] * vj[u];
+                v0 = (r0 >= jb && r0 < j) ? n0 : v0;
+                v1 = (r1 >= jb && r1 < j) ? n1 : v1;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (j0 - u >= jb) {
+                const double n0 = v0 - a0[u] * vj[u], n1 = v1 - a1[u] * vj[u];
+                v0 = r0 < jb ? n0 : v0;
+                v1 = r1 < jb ? n1 : v1;
+            }
+        }
     }
-    if (q0 < n) {
-        const double d = Ls[tri(q0, q0)];
-        if (fabs(d) > DBL_MIN) v0 /= d;
-        else v0 = 0;
+    if (r0 < n) P.xp[brk ? r0 : perm[r0]] = v0;
+    if (r1 < n) P.xp[brk ? r1 : perm[r1]] = v1;
+    // isPositive: the oracle's sign state ends in {0, 1} exactly when no D(k) is negative (a zero first pivot: 0)
+    const bool neg = !brk && ((r0 < n && d0 < 0) || (r1 < n && d1 < 0));
+    const bool any_neg = __ballot(neg) != 0;
+    if (l == 0) {
+        P.scal[2] = (any_neg || err) ? 0.0 : 1.0;
+        P.scal[3] = err ? 1.0 : 0.0;
     }
-    if (q1 < n) {
-        const double d = Ls[tri(q1, q1)];
-        if (fabs(d) > DBL_MIN) v1 /= d;
-        else v1 = 0;
-    }
-#pragma unroll 4
-    for (int j = n - 1; j >= 0; --j) {
-        const double vj = readlane_f64(j < 64 ? v0 : v1, j & 63);
-        const double a0 = q0 < j ? Ls[tri(j, q0)] : 0.0;
-        const double a1 = q1 < j ? Ls[tri(j, q1)] : 0.0;
-        if (q0 < j) v0 = v0 - a0 * vj;
-        if (q1 < j) v1 = v1 - a1 * vj;
-    }
-    if (q0 < n) P.xp[brk ? q0 : perm[q0]] = v0;
-    if (q1 < n) P.xp[brk ? q1 : perm[q1]] = v1;
-    if (t == 0) P.scal[2] = (sign == 1 || sign == 0) ? 1.0 : 0.0;
-    LDP_MARK(5);
+    LDP_MARK(6);
     LDP_STORE();
 }
+#undef LDLT_FIN
+#undef LDLT_UPD
 
 // larger systems: the same steps on S in global memory
 __global__ __launch_bounds__(256) void ba_ldlt_kernel(BaParams P) {
@@ -763,12 +981,43 @@ __global__ __launch_bounds__(256) void ba_ldlt_kernel(BaParams P) {
 #undef LL
 }
 
-__global__ __launch_bounds__(256) void ba_backsub_kernel(BaParams P) {
+// The trial step in one launch (g2o's back-substitution, oplus and the trial chi2's per-edge terms): every workgroup
+// first forms all poses of the trial state in LDS (free: exp(x_p) T, fixed: T); one lane per landmark then runs
+// x_l = Dinv (b_l - sum_e H_pl^T x_p) sequentially over its edges, writes X + x_l into the trial state and |e|^2 of
+// each of its edges at the trial state. The trial state is the other buffer: a rejected trial leaves the current
+// one untouched (no backup / restore copies); an accepted one flips P.cur (ba_chi2_kernel's last workgroup).
+__global__ __launch_bounds__(256) void ba_step_kernel(BaParams P, BaMat3 K) {
+    extern __shared__ double sT[];  // [P][7]
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    const int cur = ba_cur(P);
+    const double* T0 = cur ? P.poses2 : P.poses;
+    const double* X0 = cur ? P.X2 : P.X;
+    double* T1 = cur ? P.poses : P.poses2;
+    double* X1 = cur ? P.X : P.X2;
+    const int t = threadIdx.x;
+    for (int p = t; p < P.P; p += kNT) {
+        double Tn[7];
+        if (p < P.nf) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) Tn[i] = T0[7 * p + i];
+        } else {
+            double dT[7];
+            se3_exp(P.xp + 6 * (p - P.nf), dT);
+            se3_mul(dT, T0 + 7 * p, Tn);
+        }
+#pragma unroll
+        for (int i = 0; i < 7; ++i) sT[7 * p + i] = Tn[i];
+        if (blockIdx.x == 0) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) T1[7 * p + i] = Tn[i];
+        }
+    }
+    __syncthreads();
+    const int l = blockIdx.x * kNT + t;
     if (l >= P.L) return;
+    const int k0 = P.le_off[l], k1 = P.le_off[l + 1];
     double tv[3] = {P.bl[3 * l], P.bl[3 * l + 1], P.bl[3 * l + 2]};
-    for (int k = P.le_off[l]; k < P.le_off[l + 1]; ++k) {
+    for (int k = k0; k < k1; ++k) {
         const int e = P.le[k], p = P.ep[e];
         if (p < P.nf) continue;
         const double* xpp = P.xp + 6 * (p - P.nf);
@@ -782,92 +1031,37 @@ __global__ __launch_bounds__(256) void ba_backsub_kernel(BaParams P) {
         }
     }
     const double* D = P.Dinv + 9 * l;
+    double Xn[3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) P.xl[3 * l + c] = D[3 * c] * tv[0] + D[3 * c + 1] * tv[1] + D[3 * c + 2] * tv[2];
-}
-
-// lanes [0, np): free poses; [np, np + 3 L): landmark coordinates
-__global__ __launch_bounds__(256) void ba_update_kernel(BaParams P) {
-    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    const int id = blockIdx.x * blockDim.x + threadIdx.x;
-    if (id < P.np) {
-        const int p = P.nf + id;
-        double dT[7], Tn[7];
-        se3_exp(P.xp + 6 * id, dT);
-        se3_mul(dT, P.poses + 7 * p, Tn);
-#pragma unroll
-        for (int i = 0; i < 7; ++i) P.poses[7 * p + i] = Tn[i];
-    } else if (id < P.np + 3 * P.L) {
-        const int i = id - P.np;
-        P.X[i] = P.X[i] + P.xl[i];
+    for (int c = 0; c < 3; ++c) {
+        const double x = D[3 * c] * tv[0] + D[3 * c + 1] * tv[1] + D[3 * c + 2] * tv[2];
+        P.xl[3 * l + c] = x;
+        Xn[c] = X0[3 * l + c] + x;
+        X1[3 * l + c] = Xn[c];
+    }
+    for (int k = k0; k < k1; ++k) {
+        const int e = P.le[k];
+        double r[2];
+        ba_error(sT + 7 * P.ep[e], K.v, Xn, P.meas + 2 * e, r);
+        P.e2[e] = r[0] * r[0] + r[1] * r[1];
     }
 }
 
-// one lane per edge: its squared error at the current estimate (summed by ba_chi2_kernel)
+// one lane per edge: its squared error at the current estimate (the solve's first chi2)
 __global__ __launch_bounds__(256) void ba_edge_chi2_kernel(BaParams P, BaMat3 K) {
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= P.E) return;
+    const int cur = ba_cur(P);
     double r[2];
-    ba_error(P.poses + 7 * P.ep[e], K.v, P.X + 3 * P.el[e], P.meas + 2 * e, r);
+    ba_error((cur ? P.poses2 : P.poses) + 7 * P.ep[e], K.v, (cur ? P.X2 : P.X) + 3 * P.el[e], P.meas + 2 * e, r);
     P.e2[e] = r[0] * r[0] + r[1] * r[1];
 }
 
-// block 0: chi2 over the edges at the current estimate -> scal[0]; block 1 (when lambda >= 0): the LM scale
-// x.(lambda x + b) over the variables (free poses, then landmarks) -> scal[1]
-__global__ __launch_bounds__(256) void ba_chi2_kernel(BaParams P, BaMat3 K, double lambda, int with_scale) {
-    __shared__ double red[kNT];
-    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    if (P.lam) lambda = *P.lam;
-    const int t = threadIdx.x;
-    double acc = 0.0;
-    if (blockIdx.x == 0) {
-        int e = t;
-        for (; e + 7 * kNT < P.E; e += 8 * kNT) {
-            double q[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) q[u] = P.e2[e + u * kNT];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) acc = acc + q[u];
-        }
-        for (; e < P.E; e += kNT) acc = acc + P.e2[e];
-        const double v = tree256(acc, red);
-        if (t == 0) P.scal[0] = v;
-    } else if (with_scale) {
-        const int ns = P.ns, nv = ns + 3 * P.L;
-        const double* bpf = P.bp + 6 * P.nf;
-        int j = t;
-        for (; j + 7 * kNT < nv; j += 8 * kNT) {
-            double x[8], b[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int q = j + u * kNT;
-                x[u] = q < ns ? P.xp[q] : P.xl[q - ns];
-                b[u] = q < ns ? bpf[q] : P.bl[q - ns];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) acc = acc + x[u] * (lambda * x[u] + b[u]);
-        }
-        for (; j < nv; j += kNT) {
-            double x, b;
-            if (j < ns) {
-                x = P.xp[j];
-                b = bpf[j];
-            } else {
-                x = P.xl[j - ns];
-                b = P.bl[j - ns];
-            }
-            acc = acc + x * (lambda * x + b);
-        }
-        const double v = tree256(acc, red);
-        if (t == 0) P.scal[1] = v;
-    }
-}
-
-// ---- device-driven LM control (one lane each; the host loop of yv_ba_solve's host form, operation for operation) ----
-__global__ void ba_ctl_init_kernel(BaCtl* c, const double* scal, double* log) {
-    c->currentChi = scal[0];
-    log[0] = scal[0];
+// ---- device-driven LM control (the host loop of yv_ba_solve's host form, operation for operation) ----
+__device__ void ba_ctl_init(BaCtl* c, double chi2, double* log, unsigned long long* maxdiag) {
+    c->currentChi = chi2;
+    log[0] = chi2;
     c->lambda = 0;
     c->ni = 2;
     c->rho = 0;
@@ -877,36 +1071,18 @@ __global__ void ba_ctl_init_kernel(BaCtl* c, const double* scal, double* log) {
     c->iters = 0;
     c->skip_iter = 0;
     c->skip_trial = 1;
-    c->skip_restore = 1;
     c->suspended = 0;
     c->iter_done = 0;
+    *maxdiag = 0;
 }
 
-// an iteration's trial loop starts (after its linearisation); the first one sets lambda = tau max|H_ii|
-__global__ void ba_ctl_iter_begin_kernel(BaCtl* c, const unsigned long long* maxdiag) {
-    if (c->skip_iter) return;
-    if (maxdiag) {
-        const double maxd = __longlong_as_double((long long)*maxdiag);
-        c->lambda = 1e-5 * maxd;
-        c->ni = 2;
-    }
-    c->q = 0;
-    c->iter_done = 0;
-    c->skip_trial = 0;
-}
-
-// after a trial: rho, accept (lambda *= max(1/3, min(2/3, 1 - (2 rho - 1)^3))) or reject (lambda *= ni, ni *= 2,
-// restore); the trial loop ends when !(rho < 0 && q < 10)
-__global__ void ba_ctl_decide_kernel(BaCtl* c, const double* scal, int has_ns) {
-    if (c->skip_trial) {
-        c->skip_restore = 1;
-        return;
-    }
-    double tempChi = scal[0];
-    const bool ok2 = has_ns ? scal[2] != 0.0 : true;
+// after a trial: rho, accept (lambda *= max(1/3, min(2/3, 1 - (2 rho - 1)^3)), the trial state becomes current) or
+// reject (lambda *= ni, ni *= 2); the trial loop ends when !(rho < 0 && q < 10). Then the iteration's end: its chi2
+// is logged; stop on q == 10 / rho == 0 / non-finite lambda. A trial loop still running after the one trial slot the
+// host enqueued per iteration suspends the solve (every later kernel skips) until the host resumes it.
+__device__ void ba_ctl_decide(BaCtl* c, double tempChi, double scale, bool ok2, int* cur, double* log) {
     if (!ok2) tempChi = DBL_MAX;
     double rho = c->currentChi - tempChi;
-    double scale = scal[1];
     scale += 1e-3;
     rho /= scale;
     if (rho > 0 && isfinite(tempChi)) {
@@ -916,11 +1092,10 @@ __global__ void ba_ctl_decide_kernel(BaCtl* c, const double* scal, int has_ns) {
         c->lambda *= sf;
         c->ni = 2;
         c->currentChi = tempChi;
-        c->skip_restore = 1;
+        *cur ^= 1;
     } else {
         c->lambda *= c->ni;
         c->ni *= 2;
-        c->skip_restore = 0;
     }
     c->rho = rho;
     c->q += 1;
@@ -928,12 +1103,6 @@ __global__ void ba_ctl_decide_kernel(BaCtl* c, const double* scal, int has_ns) {
         c->iter_done = 1;
         c->skip_trial = 1;
     }
-}
-
-// an iteration ends: its chi2 is logged; stop on q == 10 / rho == 0 / non-finite lambda.  A trial loop still running
-// after the trial slots the host enqueued suspends the solve (every later kernel skips) until the host resumes it.
-__global__ void ba_ctl_iter_end_kernel(BaCtl* c, double* log) {
-    if (c->skip_iter) return;
     if (!c->iter_done) {
         c->suspended = 1;
         c->skip_iter = 1;
@@ -958,67 +1127,137 @@ __global__ void ba_ctl_resume_kernel(BaCtl* c) {
     c->skip_trial = 0;
 }
 
-__global__ __launch_bounds__(256) void ba_copy2_kernel(const int* gate, double* d1, const double* s1, int n1, double* d2,
-                                                       const double* s2, int n2) {
-    if (*gate) return;
+// chi2 over the edges (sum 0) and, for a trial, the LM scale x.(lambda x + b) over the variables (free poses, then
+// landmarks; sum 1) in the oracle's tree256 order: chain t = 0..255 adds items t, t + 256, ... from 0.0, then the
+// halving tree. kChi2Groups workgroups per sum, each running 16 chains over items staged in LDS a block of rows at a
+// time; the last workgroup to finish forms both trees and then (device control) decides the trial or starts the
+// solve, or (host control) leaves chi2 / scale in scal[0] / scal[1].  mode 0: the solve's first chi2; 1: a trial.
+constexpr int kChi2Groups = 16;
+constexpr int kChi2Rows = 128;
+__global__ __launch_bounds__(256) void ba_chi2_kernel(BaParams P, double lambda, int mode) {
+    __shared__ double st[kChi2Rows * 17];
+    __shared__ double red[2][kNT];
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
+    if (P.lam) lambda = *P.lam;
+    const int t = threadIdx.x;
+    const int sum = blockIdx.x / kChi2Groups, g = blockIdx.x - sum * kChi2Groups;
+    const int ns = P.ns;
+    const int N = sum == 0 ? P.E : ns + 3 * P.L;
+    const double* bpf = P.bp + 6 * P.nf;
+    double acc = 0.0;
+    for (int r0 = 0; r0 * kNT < N; r0 += kChi2Rows) {
+#pragma unroll 4
+        for (int i = t; i < kChi2Rows * 16; i += kNT) {
+            const int k = (r0 + (i >> 4)) * kNT + 16 * g + (i & 15);
+            double v = 0.0;
+            if (k < N) {
+                if (sum == 0) {
+                    v = P.e2[k];
+                } else {
+                    const double x = k < ns ? P.xp[k] : P.xl[k - ns];
+                    const double b = k < ns ? bpf[k] : P.bl[k - ns];
+                    v = x * (lambda * x + b);
+                }
+            }
+            st[(i >> 4) * 17 + (i & 15)] = v;
+        }
+        __syncthreads();
+        if (t < 16) {
+            // this chain's rows in the block: item (r0 + i) * 256 + kc < N; eight LDS loads ahead of the adds
+            const int kc = 16 * g + t;
+            const int rows = kc < N ? min(kChi2Rows, (N - 1 - kc) / kNT + 1 - r0) : 0;
+            int i = 0;
+            if (rows >= 8) {
+                double d[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) d[u] = st[u * 17 + t];
+                for (; i + 16 <= rows; i += 8) {
+                    double e[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) e[u] = st[(i + 8 + u) * 17 + t];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) acc = acc + d[u];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) d[u] = e[u];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc = acc + d[u];
+                i += 8;
+            }
+            for (; i < rows; ++i) acc = acc + st[i * 17 + t];
+        }
+        __syncthreads();
+    }
+    if (t < 16) P.part[sum * kNT + 16 * g + t] = acc;
+    if (!ba_last_block(P.ticket + 1)) return;
+    red[0][t] = P.part[t];
+    red[1][t] = mode ? P.part[kNT + t] : 0.0;
+    __syncthreads();
+    for (int off = kNT / 2; off > 0; off >>= 1) {
+        if (t < off) {
+            red[0][t] = red[0][t] + red[0][t + off];
+            red[1][t] = red[1][t] + red[1][t + off];
+        }
+        __syncthreads();
+    }
+    if (t != 0) return;
+    const double chi2 = red[0][0], scale = red[1][0];
+    if (!P.ctl) {
+        P.scal[0] = chi2;
+        if (mode) P.scal[1] = scale;
+    } else if (mode == 0) {
+        ba_ctl_init(P.ctl, chi2, P.log, P.maxdiag);
+    } else {
+        ba_ctl_decide(P.ctl, chi2, scale, P.ns > 0 ? P.scal[2] != 0.0 : true, P.cur, P.log);
+    }
+}
+
+// after the solve: the estimate into P.poses / P.X when it ended in the other buffer
+__global__ __launch_bounds__(256) void ba_finish_kernel(BaParams P) {
+    if (!P.cur || !*P.cur) return;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n1) d1[i] = s1[i];
-    else if (i - n1 < n2) d2[i - n1] = s2[i - n1];
+    if (i < 7 * P.P) P.poses[i] = P.poses2[i];
+    if (i < 3 * P.L) P.X[i] = P.X2[i];
 }
 
 }  // namespace ba
 
-void launch_ba_ctl_init(BaCtl* c, const double* scal, double* log, hipStream_t s) {
-    hipLaunchKernelGGL(ba::ba_ctl_init_kernel, dim3(1), dim3(1), 0, s, c, scal, log);
-}
-void launch_ba_ctl_iter_begin(BaCtl* c, const unsigned long long* maxdiag, hipStream_t s) {
-    hipLaunchKernelGGL(ba::ba_ctl_iter_begin_kernel, dim3(1), dim3(1), 0, s, c, maxdiag);
-}
-void launch_ba_ctl_decide(BaCtl* c, const double* scal, int has_ns, hipStream_t s) {
-    hipLaunchKernelGGL(ba::ba_ctl_decide_kernel, dim3(1), dim3(1), 0, s, c, scal, has_ns);
-}
-void launch_ba_ctl_iter_end(BaCtl* c, double* log, hipStream_t s) {
-    hipLaunchKernelGGL(ba::ba_ctl_iter_end_kernel, dim3(1), dim3(1), 0, s, c, log);
-}
 void launch_ba_ctl_resume(BaCtl* c, hipStream_t s) {
     hipLaunchKernelGGL(ba::ba_ctl_resume_kernel, dim3(1), dim3(1), 0, s, c);
 }
-void launch_ba_copy2(const int* gate, double* d1, const double* s1, int n1, double* d2, const double* s2, int n2,
-                     hipStream_t s) {
-    if (n1 + n2 > 0)
-        hipLaunchKernelGGL(ba::ba_copy2_kernel, dim3((n1 + n2 + 255) / 256), dim3(256), 0, s, gate, d1, s1, n1, d2, s2,
-                           n2);
-}
 
-void launch_ba_linearize(const BaParams& P, const BaMat3& K, hipStream_t s) {
+void launch_ba_linearize(const BaParams& P, const BaMat3& K, int first, hipStream_t s) {
     if (P.E > 0) hipLaunchKernelGGL(ba::ba_linearize_kernel, dim3((P.E + 255) / 256), dim3(256), 0, s, P, K);
-    if (P.np > 0) hipLaunchKernelGGL(ba::ba_pose_reduce_kernel, dim3(P.np), dim3(256), 0, s, P);
+    const int nb = std::max(1, P.np + (P.L + 255) / 256);
+    hipLaunchKernelGGL(ba::ba_reduce_kernel, dim3(nb), dim3(256), 0, s, P, first);
 }
 
-void launch_ba_landmark_reduce(const BaParams& P, unsigned long long* maxdiag, hipStream_t s) {
-    const int n = std::max(P.L, P.np);
-    if (n > 0) hipLaunchKernelGGL(ba::ba_landmark_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, P, maxdiag);
+void launch_ba_ldlt(const BaParams& P, hipStream_t s) {
+    if (P.ns > 0 && P.ns <= ba::kLdltRegN)
+        hipLaunchKernelGGL(ba::ba_ldlt_reg_kernel, dim3(1), dim3(256), 0, s, P);
+    else if (P.ns > 0)
+        hipLaunchKernelGGL(ba::ba_ldlt_kernel, dim3(1), dim3(256), sizeof(double) * 2 * P.ns, s, P);
 }
 
 void launch_ba_trial(const BaParams& P, const BaMat3& K, double lambda, hipStream_t s) {
     const int nl = std::max(P.L, P.E);
     if (nl > 0) hipLaunchKernelGGL(ba::ba_landmark_trial_kernel, dim3((nl + 255) / 256), dim3(256), 0, s, P, lambda);
     const int nb = P.np * (P.np + 1) / 2;
-    if (nb > 0) hipLaunchKernelGGL(ba::ba_schur_kernel, dim3(nb + P.np), dim3(ba::kSchurChunk), 0, s, P, lambda);
-    if (P.ns > 0 && P.ns <= ba::kLdltMaxN)
-        hipLaunchKernelGGL(ba::ba_ldlt_lds_kernel, dim3(1), dim3(ba::kLdltThreads), 0, s, P);
-    else if (P.ns > 0)
-        hipLaunchKernelGGL(ba::ba_ldlt_kernel, dim3(1), dim3(256), sizeof(double) * 2 * P.ns, s, P);
-    if (P.L > 0) hipLaunchKernelGGL(ba::ba_backsub_kernel, dim3((P.L + 255) / 256), dim3(256), 0, s, P);
-    const int nu = P.np + 3 * P.L;
-    if (nu > 0) hipLaunchKernelGGL(ba::ba_update_kernel, dim3((nu + 255) / 256), dim3(256), 0, s, P);
-    if (P.E > 0) hipLaunchKernelGGL(ba::ba_edge_chi2_kernel, dim3((P.E + 255) / 256), dim3(256), 0, s, P, K);
-    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(2), dim3(256), 0, s, P, K, lambda, 1);
+    if (nb > 0) hipLaunchKernelGGL(ba::ba_schur_kernel, dim3(nb + P.np), dim3(ba::kSchurThreads), 0, s, P, lambda);
+    launch_ba_ldlt(P, s);
+    hipLaunchKernelGGL(ba::ba_step_kernel, dim3(std::max(1, (P.L + 255) / 256)), dim3(256),
+                       sizeof(double) * 7 * P.P, s, P, K);
+    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(2 * ba::kChi2Groups), dim3(256), 0, s, P, lambda, 1);
 }
 
 void launch_ba_chi2(const BaParams& P, const BaMat3& K, hipStream_t s) {
     if (P.E > 0) hipLaunchKernelGGL(ba::ba_edge_chi2_kernel, dim3((P.E + 255) / 256), dim3(256), 0, s, P, K);
-    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(1), dim3(256), 0, s, P, K, 0.0, 0);
+    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(ba::kChi2Groups), dim3(256), 0, s, P, 0.0, 0);
+}
+
+void launch_ba_finish(const BaParams& P, hipStream_t s) {
+    const int n = std::max(7 * P.P, 3 * P.L);
+    if (n > 0) hipLaunchKernelGGL(ba::ba_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, s, P);
 }
 
 }  // namespace yavo
@@ -1038,7 +1277,8 @@ struct yv_ba {
     int32_t *d_ep = nullptr, *d_el = nullptr, *d_pe_off = nullptr, *d_pe = nullptr, *d_le_off = nullptr,
             *d_le = nullptr, *d_cv_off = nullptr, *d_cv_e1 = nullptr, *d_cv_e2 = nullptr;
     double* d_meas = nullptr;
-    double *bak_poses = nullptr, *bak_X = nullptr;
+    int* d_cur = nullptr;          // the state the estimate is in (BaParams::cur)
+    unsigned* d_ticket = nullptr;  // last-workgroup counters
     unsigned long long* d_maxdiag = nullptr;
     double* h_scal = nullptr;  // pinned [4]
     yavo::BaCtl* d_ctl = nullptr;  // the device-driven LM's control block
@@ -1108,8 +1348,11 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
     rc |= ba_alloc(b, &b->d_cv_off, P * P + 1);
     rc |= ba_alloc(b, &Q.poses, 7 * P);
     rc |= ba_alloc(b, &Q.X, 3 * L);
-    rc |= ba_alloc(b, &b->bak_poses, 7 * P);
-    rc |= ba_alloc(b, &b->bak_X, 3 * L);
+    rc |= ba_alloc(b, &Q.poses2, 7 * P);
+    rc |= ba_alloc(b, &Q.X2, 3 * L);
+    rc |= ba_alloc(b, &b->d_cur, 1);
+    rc |= ba_alloc(b, &b->d_ticket, 4);
+    rc |= ba_alloc(b, &Q.part, 2 * 256);
     rc |= ba_alloc(b, &Q.err, 2 * E);
     rc |= ba_alloc(b, &Q.Jp, 12 * E);
     rc |= ba_alloc(b, &Q.Jl, 6 * E);
@@ -1133,10 +1376,17 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
         rc = YV_ERR_HIP;
     if (rc == YV_OK && hipHostMalloc(reinterpret_cast<void**>(&b->h_ctl), sizeof(yavo::BaCtl)) != hipSuccess)
         rc = YV_ERR_HIP;
+    if (rc == YV_OK && (hipMemsetAsync(b->d_ticket, 0, 4 * sizeof(unsigned), b->st) != hipSuccess ||
+                        hipMemsetAsync(b->d_cur, 0, sizeof(int), b->st) != hipSuccess ||
+                        hipStreamSynchronize(b->st) != hipSuccess))
+        rc = YV_ERR_HIP;
     if (rc != YV_OK) {
         yv_ba_destroy(b);
         return YV_ERR_HIP;
     }
+    Q.cur = b->d_cur;
+    Q.ticket = b->d_ticket;
+    Q.maxdiag = b->d_maxdiag;
     *out = b;
     return YV_OK;
 }
@@ -1258,14 +1508,12 @@ extern "C" int yv_ba_set_problem(yv_ba* b, int n_poses, int n_fixed, int n_landm
 // and scale (bit-identical double arithmetic), the device everything per edge / landmark / pose
 namespace {
 
-// Trial slots the device-driven solve enqueues per iteration: g2o's trial loop usually accepts its first trial; an
-// iteration that needs more suspends the solve and the host enqueues the rest.
-int ba_trial_slots() { return 1; }
-
 // The LM of yv_ba_solve with its control on the device (default): the host enqueues every iteration's kernels
-// without waiting -- linearise, (iteration begin), per trial slot {backup, trial, decide, restore}, (iteration end)
-// -- and the one-lane ba_ctl_* kernels carry lambda, ni, currentChi and the stop / accept decisions in a device
-// control block that gates the other kernels.  One read-back per solve, plus one per suspended trial loop.
+// without waiting -- linearise + H / b (whose last workgroup begins the iteration), one damping trial (Dinv / W,
+// Schur, LDLT, step into the trial state, chi2 + scale, whose last workgroup decides and ends the iteration) -- and
+// the control block (lambda, ni, currentChi, stop / accept) gates the kernels. g2o's trial loop usually accepts its
+// first trial; an iteration that needs more suspends the solve (every later kernel skips) and the host resumes it.
+// One read-back per solve, plus one per suspended trial loop.
 // poses / landmarks: host in / out; both nullptr: the problem's poses and landmarks are already in Q.poses / Q.X on
 // the device (yv_ba_window_solve) and stay there.
 int ba_solve_device(yv_ba* b, double* poses, double* landmarks, int max_iters, double* chi2_log, int* iters) {
@@ -1282,37 +1530,24 @@ int ba_solve_device(yv_ba* b, double* poses, double* landmarks, int max_iters, d
         b->log_cap = max_iters + 1;
     }
     yavo::BaCtl* c = b->d_ctl;
-    yavo::BaParams Pit = Q, Ptr = Q;
+    yavo::BaParams Pc = Q;
+    Pc.ctl = c;
+    Pc.log = b->d_log;
+    yavo::BaParams Pit = Pc, Ptr = Pc;
     Pit.gate = &c->skip_iter;
     Ptr.gate = &c->skip_trial;
     Ptr.lam = &c->lambda;
+    if (hipMemsetAsync(b->d_cur, 0, sizeof(int), st) != hipSuccess) return YV_ERR_HIP;
     if (host_io && (hipMemcpyAsync(Q.poses, poses, pb, hipMemcpyHostToDevice, st) != hipSuccess ||
                     (xb && hipMemcpyAsync(Q.X, landmarks, xb, hipMemcpyHostToDevice, st) != hipSuccess)))
         return YV_ERR_HIP;
-    yavo::launch_ba_chi2(Q, b->K, st);
-    yavo::launch_ba_ctl_init(c, Q.scal, b->d_log, st);
-    const int slots = ba_trial_slots();
+    yavo::launch_ba_chi2(Pc, b->K, st);
     int first = 0;
     bool resume = false;
     for (;;) {
         for (int it = first; it < max_iters; ++it) {
-            if (!(resume && it == first)) {
-                yavo::launch_ba_linearize(Pit, b->K, st);
-                if (it == 0) {
-                    if (hipMemsetAsync(b->d_maxdiag, 0, sizeof(unsigned long long), st) != hipSuccess) return YV_ERR_HIP;
-                    yavo::launch_ba_landmark_reduce(Pit, b->d_maxdiag, st);
-                } else {
-                    yavo::launch_ba_landmark_reduce(Pit, nullptr, st);
-                }
-                yavo::launch_ba_ctl_iter_begin(c, it == 0 ? b->d_maxdiag : nullptr, st);
-            }
-            for (int q = 0; q < slots; ++q) {
-                yavo::launch_ba_copy2(&c->skip_trial, b->bak_poses, Q.poses, 7 * Q.P, b->bak_X, Q.X, 3 * Q.L, st);
-                yavo::launch_ba_trial(Ptr, b->K, 0.0, st);
-                yavo::launch_ba_ctl_decide(c, Q.scal, Q.ns > 0 ? 1 : 0, st);
-                yavo::launch_ba_copy2(&c->skip_restore, Q.poses, b->bak_poses, 7 * Q.P, Q.X, b->bak_X, 3 * Q.L, st);
-            }
-            yavo::launch_ba_ctl_iter_end(c, b->d_log, st);
+            if (!(resume && it == first)) yavo::launch_ba_linearize(Pit, b->K, it == 0 ? 1 : 0, st);
+            yavo::launch_ba_trial(Ptr, b->K, 0.0, st);
         }
         if (hipGetLastError() != hipSuccess ||
             hipMemcpyAsync(b->h_ctl, c, sizeof(yavo::BaCtl), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -1323,6 +1558,7 @@ int ba_solve_device(yv_ba* b, double* poses, double* landmarks, int max_iters, d
         first = b->h_ctl->it;
         resume = true;
     }
+    yavo::launch_ba_finish(Q, st);
     const int n_it = max_iters > 0 ? b->h_ctl->iters : 0;
     if ((host_io && (hipMemcpyAsync(poses, Q.poses, pb, hipMemcpyDeviceToHost, st) != hipSuccess ||
                      (xb && hipMemcpyAsync(landmarks, Q.X, xb, hipMemcpyDeviceToHost, st) != hipSuccess))) ||
@@ -1348,7 +1584,9 @@ extern "C" int yv_ba_solve(yv_ba* b, double* poses, double* landmarks, int max_i
     yavo::BaParams& Q = b->P;
     const size_t pb = sizeof(double) * 7 * Q.P, xb = sizeof(double) * 3 * Q.L;
     hipStream_t st = b->st;
-    if (hipMemcpyAsync(Q.poses, poses, pb, hipMemcpyHostToDevice, st) != hipSuccess ||
+    int cur = 0;  // the state the estimate is in (the device's *Q.cur, which the host sets)
+    if (hipMemsetAsync(b->d_cur, 0, sizeof(int), st) != hipSuccess ||
+        hipMemcpyAsync(Q.poses, poses, pb, hipMemcpyHostToDevice, st) != hipSuccess ||
         (xb && hipMemcpyAsync(Q.X, landmarks, xb, hipMemcpyHostToDevice, st) != hipSuccess))
         return YV_ERR_HIP;
     yavo::launch_ba_chi2(Q, b->K, st);
@@ -1358,10 +1596,9 @@ extern "C" int yv_ba_solve(yv_ba* b, double* poses, double* landmarks, int max_i
     double lambda = 0, ni = 2;
     int it;
     for (it = 0; it < max_iters; ++it) {
-        yavo::launch_ba_linearize(Q, b->K, st);
+        if (it == 0 && hipMemsetAsync(b->d_maxdiag, 0, sizeof(unsigned long long), st) != hipSuccess) return YV_ERR_HIP;
+        yavo::launch_ba_linearize(Q, b->K, it == 0 ? 1 : 0, st);
         if (it == 0) {
-            if (hipMemsetAsync(b->d_maxdiag, 0, sizeof(unsigned long long), st) != hipSuccess) return YV_ERR_HIP;
-            yavo::launch_ba_landmark_reduce(Q, b->d_maxdiag, st);
             unsigned long long bits = 0;
             if (hipMemcpyAsync(&bits, b->d_maxdiag, sizeof bits, hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess)
@@ -1370,15 +1607,10 @@ extern "C" int yv_ba_solve(yv_ba* b, double* poses, double* landmarks, int max_i
             std::memcpy(&maxd, &bits, sizeof maxd);
             lambda = 1e-5 * maxd;
             ni = 2;
-        } else {
-            yavo::launch_ba_landmark_reduce(Q, nullptr, st);
         }
         double rho = 0;
         int q = 0;
         do {
-            if (hipMemcpyAsync(b->bak_poses, Q.poses, pb, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-                (xb && hipMemcpyAsync(b->bak_X, Q.X, xb, hipMemcpyDeviceToDevice, st) != hipSuccess))
-                return YV_ERR_HIP;
             yavo::launch_ba_trial(Q, b->K, lambda, st);
             if (hipGetLastError() != hipSuccess || ba_sync_scal(b, 3) != YV_OK) return YV_ERR_HIP;
             double tempChi = b->h_scal[0];
@@ -1395,12 +1627,12 @@ extern "C" int yv_ba_solve(yv_ba* b, double* poses, double* landmarks, int max_i
                 lambda *= sf;
                 ni = 2;
                 currentChi = tempChi;
+                cur ^= 1;  // the trial state becomes the estimate
+                if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b->d_cur), cur, 1, st) != hipSuccess)
+                    return YV_ERR_HIP;
             } else {
                 lambda *= ni;
                 ni *= 2;
-                if (hipMemcpyAsync(Q.poses, b->bak_poses, pb, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-                    (xb && hipMemcpyAsync(Q.X, b->bak_X, xb, hipMemcpyDeviceToDevice, st) != hipSuccess))
-                    return YV_ERR_HIP;
             }
             q++;
         } while (rho < 0 && q < 10);
@@ -1410,6 +1642,7 @@ extern "C" int yv_ba_solve(yv_ba* b, double* poses, double* landmarks, int max_i
             break;
         }
     }
+    yavo::launch_ba_finish(Q, st);
     if (hipMemcpyAsync(poses, Q.poses, pb, hipMemcpyDeviceToHost, st) != hipSuccess ||
         (xb && hipMemcpyAsync(landmarks, Q.X, xb, hipMemcpyDeviceToHost, st) != hipSuccess) ||
         hipStreamSynchronize(st) != hipSuccess)
@@ -1434,10 +1667,11 @@ extern "C" int yv_ba_debug_read(yv_ba* b, int which, double* dst, int64_t count)
     return YV_OK;
 }
 
+
 #ifdef YAVO_LM_PROFILE
-// profiling builds only (lib/libyavo_prof.so): LDLT phase cycles per wave [8][8], summed since the last call (reset)
+// profiling builds only (lib/libyavo_prof.so): LDLT phase cycles per wave [4][8], summed since the last call (reset)
 extern "C" int yv_debug_ldlt_prof(unsigned long long* out) {
-    unsigned long long z[yavo::ba::kLdltThreads / 64 * 8] = {};
+    unsigned long long z[4 * 8] = {};
     if (hipDeviceSynchronize() != hipSuccess ||
         hipMemcpyFromSymbol(out, HIP_SYMBOL(yavo::ba::g_ldlt_prof), sizeof z) != hipSuccess ||
         hipMemcpyToSymbol(HIP_SYMBOL(yavo::ba::g_ldlt_prof), z, sizeof z) != hipSuccess)
@@ -1445,6 +1679,48 @@ extern "C" int yv_debug_ldlt_prof(unsigned long long* out) {
     return 0;
 }
 #endif
+
+extern "C" int yv_ba_debug_ldlt(yv_ctx* ctx, const double* S, int n, const double* b, double* x, int* ok) {
+    if (!ctx || !S || !b || !x || !ok || n < 1 || n > 4096) return YV_ERR_INVALID;
+    if (hipSetDevice(yavo::ctx_device(ctx)) != hipSuccess) return YV_ERR_HIP;
+    hipStream_t st = yavo::ctx_stream(ctx);
+    double *dS = nullptr, *db = nullptr, *dx = nullptr, *ds = nullptr;
+    int32_t* dtr = nullptr;
+    const size_t nn = (size_t)n * n;
+    int rc = YV_OK;
+    if (hipMalloc(reinterpret_cast<void**>(&dS), sizeof(double) * nn) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&db), sizeof(double) * n) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dx), sizeof(double) * n) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&ds), sizeof(double) * 16) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dtr), sizeof(int32_t) * n) != hipSuccess)
+        rc = YV_ERR_HIP;
+    double scal[4] = {0, 0, 0, 0};
+    if (rc == YV_OK) {
+        yavo::BaParams Q{};
+        Q.ns = n;
+        Q.S = dS;
+        Q.bs = db;
+        Q.xp = dx;
+        Q.scal = ds;
+        Q.tr = dtr;
+        if (hipMemcpyAsync(dS, S, sizeof(double) * nn, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(db, b, sizeof(double) * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemsetAsync(ds, 0, sizeof(double) * 16, st) != hipSuccess)
+            rc = YV_ERR_HIP;
+        if (rc == YV_OK) {
+            yavo::launch_ba_ldlt(Q, st);
+            if (hipGetLastError() != hipSuccess ||
+                hipMemcpyAsync(x, dx, sizeof(double) * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(scal, ds, sizeof scal, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                rc = YV_ERR_HIP;
+        }
+    }
+    for (void* p : {(void*)dS, (void*)db, (void*)dx, (void*)ds, (void*)dtr})
+        if (p) (void)hipFree(p);
+    if (rc == YV_OK) *ok = scal[2] != 0.0 ? 1 : 0;
+    return rc;
+}
 
 // ------------------------------------------------------------------------------------------------
 // The sliding BA window of the chained stereo front end, assembled on the device (ya_vo_amd/sequence.py

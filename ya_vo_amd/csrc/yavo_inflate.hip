@@ -698,11 +698,13 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t* __restrict__
     const uint32_t nbytes = (uint32_t)len[img];
     int32_t st = kPngOk;
     uint32_t op = 0, flushed = 0, seg = kSegMax;
-    // an IDAT chunk whose CRC failed (gather_kernel): libpng stops at it (a critical chunk's CRC error is fatal)
-    if (uni((uint32_t)crc_bad[img]) != 0u) {
+    // an IDAT chunk whose CRC failed (gather_kernel, flag 1): libpng stops at it (a critical chunk's CRC error is
+    // fatal); a file the host could not read or parse arrives flagged with its status (kPngErrFile) and no stream
+    const int32_t flagged = (int32_t)uni((uint32_t)crc_bad[img]);
+    if (flagged != 0) {
         if (lane == 0) {
             crc_bad[img] = 0;  // the flag is read (readfirstlane waited for it) before it is cleared for the slot's reuse
-            status[img] = kPngErrCrc;
+            status[img] = flagged == 1 ? kPngErrCrc : flagged;
         }
         return;
     }

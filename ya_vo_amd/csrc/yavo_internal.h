@@ -219,29 +219,35 @@ struct BaParams {
     // kernels read lambda from *lam; both nullptr under host control
     const int* gate = nullptr;
     const double* lam = nullptr;
+    // the trial state: ba_step_kernel writes the trial estimate into the other buffer (poses2 / X2 when *cur == 0),
+    // an accepted trial flips *cur; ba_finish_kernel leaves the result in poses / X
+    double* poses2 = nullptr;          // [P][7]
+    double* X2 = nullptr;              // [L][3]
+    int* cur = nullptr;
+    struct BaCtl* ctl = nullptr;        // device control block (nullptr: host control)
+    double* log = nullptr;             // [max_iters + 1] chi2 per iteration (device control)
+    unsigned long long* maxdiag = nullptr;
+    unsigned* ticket = nullptr;        // [4] last-workgroup counters (0 between launches)
+    double* part = nullptr;            // [2][256] chi2 / scale chains
 };
 // The device-side Levenberg-Marquardt control of one solve (g2o OptimizationAlgorithmLevenberg::solve, the
-// host loop's arithmetic): written by the one-lane ba_ctl_* kernels, read by the gates of the others.
+// host loop's arithmetic): written by the last workgroups of ba_reduce_kernel / ba_chi2_kernel, read by the gates.
 struct BaCtl {
     double currentChi, lambda, ni, rho;
     int q, it, stop, iters;
-    int skip_iter, skip_trial, skip_restore, suspended, iter_done, pad[3];
+    int skip_iter, skip_trial, suspended, iter_done;
 };
 struct BaMat3 {
     double v[9];
 };
-void launch_ba_linearize(const BaParams& P, const BaMat3& K, hipStream_t s);
-void launch_ba_landmark_reduce(const BaParams& P, unsigned long long* maxdiag, hipStream_t s);
+// linearise + the H / b blocks (first: the largest diagonal into *P.maxdiag; device control: the iteration begins)
+void launch_ba_linearize(const BaParams& P, const BaMat3& K, int first, hipStream_t s);
+// one damping trial: Dinv / W, Schur, LDLT, step into the trial state, chi2 + scale (device control: the decision)
 void launch_ba_trial(const BaParams& P, const BaMat3& K, double lambda, hipStream_t s);
+// the solve's first chi2 (device control: the control block's initialisation)
 void launch_ba_chi2(const BaParams& P, const BaMat3& K, hipStream_t s);
-// device control: init after the first chi2, per iteration begin / end, per trial decide, backup / restore copies
-void launch_ba_ctl_init(BaCtl* c, const double* scal, double* log, hipStream_t s);
-void launch_ba_ctl_iter_begin(BaCtl* c, const unsigned long long* maxdiag, hipStream_t s);
-void launch_ba_ctl_decide(BaCtl* c, const double* scal, int has_ns, hipStream_t s);
-void launch_ba_ctl_iter_end(BaCtl* c, double* log, hipStream_t s);
+void launch_ba_finish(const BaParams& P, hipStream_t s);
 void launch_ba_ctl_resume(BaCtl* c, hipStream_t s);
-void launch_ba_copy2(const int* gate, double* d1, const double* s1, int n1, double* d2, const double* s2, int n2,
-                     hipStream_t s);
 
 // the shared map (yavo_map.hip): one chunk's block after its pose LM
 void launch_map_chunk(const double* rel, int n, int64_t first_frame, int kf_every, const int32_t* edge_count,
@@ -251,7 +257,8 @@ void launch_map_chunk(const double* rel, int n, int64_t first_frame, int kf_ever
 // PNG decoding on the GPU (yavo_inflate.hip): per-image status codes and the two kernels
 enum : int32_t {
     kPngOk = 0, kPngErrHeader = 1, kPngErrBlock = 2, kPngErrCode = 3, kPngErrOverrun = 4, kPngErrShort = 5,
-    kPngErrFilter = 6, kPngErrCrc = 7, kPngErrAdler = 8
+    kPngErrFilter = 6, kPngErrCrc = 7, kPngErrAdler = 8,
+    kPngErrFile = 9  // missing, unreadable, truncated or not an 8-bit grey PNG of the decoder's size (host side)
 };
 // one IDAT payload of a PNG file staged on the device: len bytes from src to dst (byte offsets in the staging buffers);
 // the chunk's type is the 4 bytes before src, its CRC the 4 after src + len; img = the payload's image in the call

@@ -495,6 +495,8 @@ struct yv_pngdec {
         int64_t* d_off = nullptr;
         int32_t* d_len = nullptr;
         int32_t* d_crc = nullptr;     // [max_images] a payload CRC failed (gather -> inflate, cleared by the inflate)
+        int32_t* h_pre = nullptr;     // pinned [max_images]: kPngErrFile for a file the host could not read / parse
+        bool any_pre = false;
         hipEvent_t copied = nullptr;  // the pinned streams are on the device: the host may refill the slot
         hipEvent_t done = nullptr;    // the slot's inflate completed: the device copy may be overwritten
         bool pending = false;
@@ -599,11 +601,13 @@ int pngdec_launch(yv_pngdec* d, yv_pngdec::Slot& sl, size_t bytes, int n, int np
     if (hipMemcpyAsync(sl.d, sl.h, bytes, hipMemcpyHostToDevice, cs) != hipSuccess ||
         hipMemcpyAsync(sl.d_off, sl.h_off, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, cs) != hipSuccess ||
         hipMemcpyAsync(sl.d_len, sl.h_len, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, cs) != hipSuccess ||
-        hipMemcpyAsync(sl.d_pc, sl.h_pc, sizeof(yavo::PngPiece) * (size_t)npc, hipMemcpyHostToDevice, cs) !=
-            hipSuccess ||
+        (npc && hipMemcpyAsync(sl.d_pc, sl.h_pc, sizeof(yavo::PngPiece) * (size_t)npc, hipMemcpyHostToDevice, cs) !=
+                    hipSuccess) ||
+        (sl.any_pre &&
+         hipMemcpyAsync(sl.d_crc, sl.h_pre, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, cs) != hipSuccess) ||
         hipEventRecord(sl.copied, cs) != hipSuccess)
         return YV_ERR_HIP;
-    yavo::launch_png_gather(sl.d, sl.dg, sl.d_pc, npc, d->check_crc ? sl.d_crc : nullptr, cs);
+    if (npc) yavo::launch_png_gather(sl.d, sl.dg, sl.d_pc, npc, d->check_crc ? sl.d_crc : nullptr, cs);
     if (hipGetLastError() != hipSuccess || hipEventRecord(sl.gathered, cs) != hipSuccess ||
         hipStreamWaitEvent(st, sl.gathered, 0) != hipSuccess ||
         (d->n_last && hipStreamWaitEvent(st, d->last_done, 0) != hipSuccess))
@@ -651,6 +655,7 @@ int yv_pngdec_create(yv_ctx* ctx, int max_images, int H, int W, yv_pngdec** out)
     for (auto& sl : d->slot) {
         ok = ok && hipHostMalloc(reinterpret_cast<void**>(&sl.h_off), sizeof(int64_t) * (size_t)max_images) == hipSuccess &&
              hipHostMalloc(reinterpret_cast<void**>(&sl.h_len), sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
+             hipHostMalloc(reinterpret_cast<void**>(&sl.h_pre), sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
              hipMalloc(reinterpret_cast<void**>(&sl.d_off), sizeof(int64_t) * (size_t)max_images) == hipSuccess &&
              hipMalloc(reinterpret_cast<void**>(&sl.d_len), sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
              hipMalloc(reinterpret_cast<void**>(&sl.d_crc), sizeof(int32_t) * (size_t)max_images) == hipSuccess &&
@@ -686,6 +691,7 @@ void yv_pngdec_destroy(yv_pngdec* d) {
         if (sl.h) (void)hipHostFree(sl.h);
         if (sl.h_off) (void)hipHostFree(sl.h_off);
         if (sl.h_len) (void)hipHostFree(sl.h_len);
+        if (sl.h_pre) (void)hipHostFree(sl.h_pre);
         if (sl.d) (void)hipFree(sl.d);
         if (sl.d_off) (void)hipFree(sl.d_off);
         if (sl.d_len) (void)hipFree(sl.d_len);
@@ -715,10 +721,17 @@ int yv_pngdec_decode(yv_pngdec* d, const uint8_t* const* files, const size_t* si
     if (slot_reserve(*sl, bytes, n) != YV_OK) return YV_ERR_HIP;
     size_t off = 0;
     std::vector<std::vector<yavo::PngPiece>> pcs((size_t)n);
+    sl->any_pre = false;
     for (int i = 0; i < n; ++i) {
         std::memcpy(sl->h + off, files[i], sizes[i]);
-        const int64_t len = png_idat_pieces(sl->h + off, sizes[i], d->H, d->W, (int64_t)off, i, pcs[(size_t)i]);
-        if (len < 0 || len > INT32_MAX) return YV_ERR_INVALID;
+        int64_t len = png_idat_pieces(sl->h + off, sizes[i], d->H, d->W, (int64_t)off, i, pcs[(size_t)i]);
+        sl->h_pre[i] = 0;
+        if (len < 0 || len > INT32_MAX) {  // this image fails (kPngErrFile, zero-filled), the others decode
+            pcs[(size_t)i].clear();
+            len = 0;
+            sl->h_pre[i] = yavo::kPngErrFile;
+            sl->any_pre = true;
+        }
         sl->h_off[i] = (int64_t)off;
         sl->h_len[i] = (int32_t)len;
         off += (sizes[i] + 63) & ~(size_t)63;
@@ -781,7 +794,7 @@ int yv_seq_upload_gpu_frames(yv_seq* s, yv_pngdec* d, const int* frames, int n, 
         return (k % per) ? s->right[frames[k / per]] : s->left[frames[k / per]];
     };
     std::vector<size_t> size((size_t)total), off((size_t)total);
-    std::atomic<int> next{0}, status{YV_OK};
+    std::atomic<int> next{0};
     auto run = [&](auto&& job) {
         next = 0;
         auto work = [&]() {
@@ -792,16 +805,19 @@ int yv_seq_upload_gpu_frames(yv_seq* s, yv_pngdec* d, const int* frames, int n, 
         work();
         for (auto& t : pool) t.join();
     };
+    // a file that is missing, unreadable, truncated or not an 8-bit grey PNG of the decoder's size fails alone
+    // (kPngErrFile, zero-filled, counted by yv_pngdec_status) as cv::imread fails per file; the batch's other images
+    // decode
+    std::vector<int32_t> pre((size_t)total, 0);
     run([&](int k) {
         struct stat sb;
         if (::stat(path_of(k).c_str(), &sb) != 0 || sb.st_size <= 0) {
-            status = YV_ERR_INVALID;
+            pre[k] = yavo::kPngErrFile;
             size[k] = 0;
             return;
         }
         size[k] = (size_t)sb.st_size;
     });
-    if (status.load() != YV_OK) return status.load();
     size_t bytes = 0;
     for (int k = 0; k < total; ++k) {
         off[k] = bytes;
@@ -810,6 +826,9 @@ int yv_seq_upload_gpu_frames(yv_seq* s, yv_pngdec* d, const int* frames, int n, 
     if (slot_reserve(*sl, bytes, total) != YV_OK) return YV_ERR_HIP;
     std::vector<std::vector<yavo::PngPiece>> pcs((size_t)total);
     run([&](int k) {
+        sl->h_off[k] = (int64_t)off[k];
+        sl->h_len[k] = 0;
+        if (pre[k]) return;
         const int fd = ::open(path_of(k).c_str(), O_RDONLY);
         size_t got = 0;
         if (fd >= 0) {
@@ -824,13 +843,17 @@ int yv_seq_upload_gpu_frames(yv_seq* s, yv_pngdec* d, const int* frames, int n, 
             got == size[k] ? png_idat_pieces(sl->h + off[k], size[k], d->H, d->W, (int64_t)off[k], k, pcs[(size_t)k])
                            : -1;
         if (len < 0 || len > INT32_MAX) {
-            status = YV_ERR_INVALID;
+            pcs[(size_t)k].clear();
+            pre[k] = yavo::kPngErrFile;
             return;
         }
-        sl->h_off[k] = (int64_t)off[k];
         sl->h_len[k] = (int32_t)len;
     });
-    if (status.load() != YV_OK) return status.load();
+    sl->any_pre = false;
+    for (int k = 0; k < total; ++k) {
+        sl->h_pre[k] = pre[k];
+        sl->any_pre |= pre[k] != 0;
+    }
     int npc = 0;
     if (slot_set_pieces(*sl, pcs, npc) != YV_OK) return YV_ERR_HIP;
     hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : yavo::ctx_stream(d->ctx);

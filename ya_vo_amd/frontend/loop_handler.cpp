@@ -4,6 +4,7 @@
 
 #include <chrono>
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 #include <condition_variable>
 #include <deque>
@@ -626,6 +627,7 @@ public:
         if (st_ == YV_OK) st_ = yv_host_alloc(ctx_, B_ * img, reinterpret_cast<void**>(&h_img_));
         if (st_ == YV_OK) st_ = yv_host_alloc(ctx_, (size_t)B_ * kMaxKp * sizeof(KeyPoint), reinterpret_cast<void**>(&h_kp_));
         if (st_ == YV_OK) st_ = yv_host_alloc(ctx_, sizeof(int32_t) * (B_ + 1), reinterpret_cast<void**>(&h_cnt_));
+        if (st_ == YV_OK) st_ = yv_host_alloc(ctx_, sizeof(uint32_t) * (B_ + 1), reinterpret_cast<void**>(&h_cand_));
     }
     ~GpuLookahead() {
         if (dec_) yv_pngdec_destroy(dec_);
@@ -635,6 +637,7 @@ public:
         yv_host_free(ctx_, h_img_);
         yv_host_free(ctx_, h_kp_);
         yv_host_free(ctx_, h_cnt_);
+        yv_host_free(ctx_, h_cand_);
     }
     int status() const { return st_; }
     int H() const { return H_; }
@@ -664,6 +667,7 @@ public:
         int st = yv_pngdec_status(dec_, codes.data(), &bad);
         const size_t img = (size_t)H_ * W_;
         if (st == YV_OK) st = yv_download(ctx_, h_cnt_, view_.kp_count, sizeof(int32_t) * n);
+        if (st == YV_OK) st = yv_download(ctx_, h_cand_, view_.cand_count, sizeof(uint32_t) * n);
         if (st == YV_OK) st = yv_download(ctx_, h_kp_, view_.keypoints, sizeof(KeyPoint) * (size_t)n * kMaxKp);
         if (st == YV_OK) st = yv_download(ctx_, h_img_, d_img_, img * n);
         if (st != YV_OK) return st;
@@ -674,7 +678,8 @@ public:
             f->cols = W_;
             f->data.assign(h_img_ + img * i, h_img_ + img * (i + 1));
             const int nk = h_cnt_[i];
-            if (nk == 0) std::cout << "No corners found" << std::endl;  // src/FastDetector.cc:364-366
+            // the FAST candidate count, as getFastFeatures prints it (src/FastDetector.cc:364-366, frontend.cpp)
+            if (h_cand_[i] == 0) std::cout << "No corners found" << std::endl;
             f->keypoints.assign(h_kp_ + (size_t)i * kMaxKp, h_kp_ + (size_t)i * kMaxKp + nk);
             frames[(size_t)i] = f;
         }
@@ -693,6 +698,7 @@ private:
     uint8_t* h_img_ = nullptr;
     KeyPoint* h_kp_ = nullptr;
     int32_t* h_cnt_ = nullptr;
+    uint32_t* h_cand_ = nullptr;
 };
 
 }  // namespace
@@ -700,6 +706,9 @@ private:
 // takeVOStep split over two threads: the worker runs getNextFrame + insertFrameFeatures on its own context for
 // frame k + 1 while this thread runs addFrame(frame k).  Frames leave the worker in path-train order, so ids,
 // keypoints and every later result are the serial loop's.
+// the tracking thread's bound on waiting for the pipeline worker's next frame
+constexpr int kPipelineStallSeconds = 60;
+
 void LoopHandler::runVOPipelined(int max_frames) {
     struct Item {
         Frame::ptr frame;  // nullptr: the end of the train (or a failure, with status != YV_OK)
@@ -775,6 +784,15 @@ void LoopHandler::runVOPipelined(int max_frames) {
                 for (auto& f : frames) {
                     Item it;
                     it.status = st;
+                    if (f && train_it_ >= limit) {
+                        // never more frames than the train holds: a look-ahead that hands a batch over twice (the
+                        // round-4 r04c6 hang: collect() returned the last batch again once nothing was launched, and
+                        // the loop never ended) fails the run instead
+                        std::cerr << "yavo: GPU look-ahead handed over frame " << train_it_ << " of a " << limit
+                                  << "-frame train" << std::endl;
+                        it.status = YV_ERR_INVALID;
+                        f = nullptr;
+                    }
                     if (f) {
                         it.index = (int)train_it_;
                         train_it_++;
@@ -853,12 +871,18 @@ void LoopHandler::runVOPipelined(int max_frames) {
         }
         for (auto& f : ahead) f.wait();  // no decode outlives the loop
     });
+    bool stalled = false;
     while (true) {
         Item it;
         {
             const double t0 = now_s();
             std::unique_lock<std::mutex> lk(mu);
-            cv_get.wait(lk, [&]() { return !q.empty(); });
+            // a bounded wait: no frame's read + detect + describe takes this long, so a worker that delivers nothing
+            // is reported and the run ends non-zero instead of blocking
+            if (!cv_get.wait_for(lk, std::chrono::seconds(kPipelineStallSeconds), [&]() { return !q.empty(); })) {
+                stalled = true;
+                break;
+            }
             it = std::move(q.front());
             q.pop_front();
             t_wait += now_s() - t0;
@@ -877,6 +901,13 @@ void LoopHandler::runVOPipelined(int max_frames) {
         stop = true;
     }
     cv_put.notify_all();
+    if (stalled) {
+        std::cerr << "yavo: the pipeline worker delivered no frame for " << kPipelineStallSeconds << " s" << std::endl;
+        gpu_status_ = YV_ERR_HIP;
+        std::cout.flush();
+        std::cerr.flush();
+        std::_Exit(3);  // the worker may be inside a call that never returns: do not wait for it
+    }
     worker.join();
     peek_next_ = nullptr;
     dropLKAhead(lk_ahead_);

@@ -79,6 +79,21 @@ def shard_images(stereo, halo_left=None, halo_right=None):
     return np.ascontiguousarray(np.concatenate([s] + extra))
 
 
+def exchange_summary(gather_ms, place_ms, slack_ms):
+    """Summary of a run's shared-map exchanges (FrameShard.collective_stats): per exchange the all-gather's and the
+    placement's device time and the slack from the gather's end to the end of the context-stream run it overlapped
+    (>= 0: the collective was hidden behind the image kernels)."""
+    import numpy as np
+    g, pl, sl = (np.asarray(x, np.float64) for x in (gather_ms, place_ms, slack_ms))
+    if not len(g):
+        return None
+    return {"exchanges": int(len(g)), "allgather_ms_mean": round(float(g.mean()), 4),
+            "allgather_ms_max": round(float(g.max()), 4), "place_ms_mean": round(float(pl.mean()), 4),
+            "hidden_fraction": round(float(np.mean(sl >= 0)), 4), "min_slack_ms": round(float(sl.min()), 4),
+            "how": "HIP events on the communication stream around all_gather_into_tensor and map_place; slack = time "
+                   "from the gather's end to the end of the context-stream run it overlaps (>= 0: hidden)"}
+
+
 class FrameShard:
     """One rank's share of a frame-sharded stereo sequence on its GPU: frames
     [first_frame, first_frame + n_frames) and, with `halo`, the predecessor frame first_frame - 1 whose left image is
@@ -159,19 +174,53 @@ class FrameShard:
             self.d_base = torch.from_numpy(identity.copy()).to(dev)
             self.d_anchors = torch.zeros((world, 7), dtype=torch.float64, device=dev)
             self.comm = torch.cuda.Stream(device=dev)
+        # collective timing (set_collective_timing): per exchange, events around the all-gather and the placement on
+        # the communication stream and one on the context stream after the run it overlaps
+        self._timing = False
+        self._ev = []
+        self._ctx_stream = None
+
+    def set_collective_timing(self, on: bool) -> None:
+        """Record HIP events around every exchange from now on (collective_stats reads them); off drops them."""
+        import torch
+        self._timing = bool(on) and self.use_map
+        self._ev = []
+        if self._timing and self._ctx_stream is None:
+            self._ctx_stream = torch.cuda.ExternalStream(self.ctx.stream, device=self.d_prior.device)
+
+    def collective_stats(self):
+        """Device times of the recorded exchanges (after drain): the all-gather (comm stream, events around the
+        collective call), the placement after it, and whether the gather had finished by the time the context stream
+        finished the run it was exchanged beside (the next step's image kernels: then it is off the critical path)."""
+        if not self._ev:
+            return None
+        g = [e0.elapsed_time(e1) for e0, e1, _, _ in self._ev]
+        pl = [e1.elapsed_time(e2) for _, e1, e2, _ in self._ev]
+        slack = [e1.elapsed_time(er) for _, e1, _, er in self._ev]  # > 0: the run ended after the gather
+        return exchange_summary(g, pl, slack)
 
     def _exchange(self) -> None:
         import torch
         import torch.distributed as dist
         # the last track_map's block: all-gathered and placed on the communication stream once it is written
         self.batch.map_wait(self.comm.cuda_stream)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if self._timing else None
         with torch.cuda.stream(self.comm):
+            if ev:
+                ev[0].record(self.comm)
             if self.collective and self.backend == "nccl":
                 dist.all_gather_into_tensor(self.d_gathered, self.d_block)
             elif self.collective:  # gloo: list form
                 dist.all_gather(list(self.d_gathered.unbind(0)), self.d_block)
+            if ev:
+                ev[1].record(self.comm)
             self.ctx.map_place(self.d_gathered.data_ptr(), self.world, self.bb, self.d_base.data_ptr(),
                                self.d_anchors.data_ptr(), stream=self.comm.cuda_stream)
+            if ev:
+                ev[2].record(self.comm)
+        if ev:
+            ev[3].record(self._ctx_stream)  # the run this exchange was issued beside
+            self._ev.append(tuple(ev))
         self.batch.map_release(self.comm.cuda_stream)
         self._pending = False
 
