@@ -65,7 +65,10 @@ int yv_pose_lm_sum_mode(int n_problems);
 int yv_pose_gn_batch(struct yv_ctx* ctx, int n_problems, const int32_t* d_offsets, const double* d_X,
                      const double* d_uv, const double* d_K, double* d_poses, int32_t* d_iterations, void* stream);
 /* F-RANSAC over n_lists match lists: list l = d_matches + l*list_stride, d_counts[l] entries, samples
- * d_samples + l*sample_stride ([iters][8]). */
+ * d_samples + l*sample_stride ([iters][8]).  The hypothesis F / inlier-count workspace belongs to the context
+ * (one per yv_ctx), so calls on one context must be serialised even when they name different streams: run
+ * concurrent F-RANSAC batches on separate contexts (the LoopHandler's side lane does).  Growing the workspace
+ * synchronises the device. */
 int yv_f_ransac_batch(struct yv_ctx* ctx, const yv_match* d_matches, int64_t list_stride, const int32_t* d_counts,
                       int n_lists, const int32_t* d_samples, int64_t sample_stride, int iters, double thr,
                       double* d_F, int32_t* d_max_inliers, int32_t* d_found, void* stream);

@@ -20,10 +20,15 @@
  * Summation orders (the GPU kernels, yavo_ba.hip, follow them bit for bit; g2o's own orders are not exposed, so
  * parity with a g2o build is unpinned):
  *   tree256   values indexed k = 0 .. n-1: partial[t] = sum of items k = t mod 256 in ascending k (from 0.0), then
- *             p[t] += p[t + off], off = 128 .. 1; used for each pose's H_pp / b_p over its edges (edge order), for
- *             chi2 over all edges and for the LM scale over all variables (poses, then landmarks)
- *   sequential per landmark over its edges (edge order) for H_ll / b_l and the back-substitution; per Schur block
- *             entry over the landmarks the two poses share (ascending); per pose for b_schur over its edges
+ *             p[t] += p[t + off], off = 128 .. 1; used for chi2 over all edges and for the LM scale over all
+ *             variables (poses, then landmarks)
+ *   tree4096  the same with 4096 leaves (t = k mod 4096, off = 2048 .. 1); used for each pose's H_pp / b_p over its
+ *             edges (edge order), for each Schur block entry's sum over the co-visible pairs of its two poses
+ *             (landmark order), v = base - total, and for each b_schur entry's sum over the pose's edges (edge order)
+ *   sequential per landmark over its edges (edge order) for H_ll / b_l and the back-substitution
+ * (Rounds 1-4 summed the Schur and b_schur entries as one sequential chain each and H_pp / b_p in tree256 order. A
+ * 3,800-term chain is latency-bound on one GPU lane, and 256 leaves leave each GPU lane ~15 dependent loads; with
+ * 4096 leaves a configs[2] window's sums have at most one item per leaf, so every load is in flight at once.)
  */
 #include "yavo_oracle.h"
 
@@ -46,6 +51,30 @@ static double t_total(const tree256* t) {
     for (int off = BA_NT / 2; off > 0; off >>= 1)
         for (int i = 0; i < off; ++i) p[i] = p[i] + p[i + off];
     return p[0];
+}
+
+#define BA_NW 4096
+typedef struct {
+    double part[BA_NW];
+    int used;  /* leaves [used, BA_NW) are still 0.0 */
+} tree4096;
+static void w_reset(tree4096* t) { t->used = 0; }
+static void w_add(tree4096* t, int k, double v) {
+    const int i = k % BA_NW;
+    while (t->used <= i) t->part[t->used++] = 0.0;
+    t->part[i] = t->part[i] + v;
+}
+/* the halving tree over all 4096 leaves; the untouched leaves are 0.0 (x + 0.0 is x except -0.0 + 0.0 = 0.0, so a
+ * level that adds a zero leaf is applied as an addition, not skipped) */
+static double w_total(tree4096* t) {
+    double* p = t->part;
+    int n = t->used;  /* p[i] for i >= n is 0.0 */
+    for (int off = BA_NW / 2; off > 0; off >>= 1) {
+        const int m = n < off ? n : off;  /* p[i], i < m, are the live leaves this level adds to */
+        for (int i = 0; i < m; ++i) p[i] = p[i] + (i + off < n ? p[i + off] : 0.0);
+        n = m;
+    }
+    return n > 0 ? p[0] : 0.0;
 }
 
 /* e = meas - (K (T X)).xy / z  (or_se3_act = Sophus T * X) */
@@ -262,6 +291,7 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
     double* xl = (double*)malloc(sizeof(double) * 3 * (size_t)L);
     double* bak_p = (double*)malloc(sizeof(double) * 7 * (size_t)P);
     double* bak_X = (double*)malloc(sizeof(double) * 3 * (size_t)L);
+    tree4096* wt = (tree4096*)malloc(sizeof(tree4096));
     double currentChi = ba_chi2(&s, poses, X);
     if (chi2_log) chi2_log[0] = currentChi;
     double lambda = 0, ni = 2;
@@ -281,23 +311,21 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
         for (int p = n_fixed; p < P; ++p) {
             for (int a = 0; a < 6; ++a)
                 for (int b = a; b < 6; ++b) {
-                    tree256 t;
-                    t_reset(&t);
+                    w_reset(wt);
                     for (int k = s.pe_off[p]; k < s.pe_off[p + 1]; ++k) {
                         const double* jp = Jp + 12 * s.pe[k];
-                        t_add(&t, k - s.pe_off[p], jp[a] * jp[b] + jp[6 + a] * jp[6 + b]);
+                        w_add(wt, k - s.pe_off[p], jp[a] * jp[b] + jp[6 + a] * jp[6 + b]);
                     }
-                    Hpp[36 * p + 6 * a + b] = Hpp[36 * p + 6 * b + a] = t_total(&t);
+                    Hpp[36 * p + 6 * a + b] = Hpp[36 * p + 6 * b + a] = w_total(wt);
                 }
             for (int a = 0; a < 6; ++a) {
-                tree256 t;
-                t_reset(&t);
+                w_reset(wt);
                 for (int k = s.pe_off[p]; k < s.pe_off[p + 1]; ++k) {
                     const int e = s.pe[k];
                     const double* jp = Jp + 12 * e;
-                    t_add(&t, k - s.pe_off[p], jp[a] * err[2 * e] + jp[6 + a] * err[2 * e + 1]);
+                    w_add(wt, k - s.pe_off[p], jp[a] * err[2 * e] + jp[6 + a] * err[2 * e + 1]);
                 }
-                bp[6 * p + a] = -t_total(&t);
+                bp[6 * p + a] = -w_total(wt);
             }
         }
         for (int l = 0; l < L; ++l) {
@@ -349,26 +377,29 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
                 for (int p2 = p1; p2 < P; ++p2)
                     for (int a = 0; a < 6; ++a)
                         for (int b = 0; b < 6; ++b) {
-                            double v = p1 == p2 ? Hpp[36 * p1 + 6 * a + b] + (a == b ? lambda : 0.0) : 0.0;
-                            for (int k = s.cv_off[p1 * P + p2]; k < s.cv_off[p1 * P + p2 + 1]; ++k) {
+                            const double base = p1 == p2 ? Hpp[36 * p1 + 6 * a + b] + (a == b ? lambda : 0.0) : 0.0;
+                            const int k0 = s.cv_off[p1 * P + p2];
+                            w_reset(wt);
+                            for (int k = k0; k < s.cv_off[p1 * P + p2 + 1]; ++k) {
                                 const double* w = W + 18 * s.cv_e1[k] + 3 * a;
                                 const double* h = Hpl + 18 * s.cv_e2[k] + 3 * b;
-                                v = v - (w[0] * h[0] + w[1] * h[1] + w[2] * h[2]);
+                                w_add(wt, k - k0, w[0] * h[0] + w[1] * h[1] + w[2] * h[2]);
                             }
+                            const double v = base - w_total(wt);
                             const int r = 6 * (p1 - n_fixed) + a, c = 6 * (p2 - n_fixed) + b;
                             S[(size_t)r * ns + c] = v;
                             S[(size_t)c * ns + r] = v;
                         }
             for (int p = n_fixed; p < P; ++p)
                 for (int a = 0; a < 6; ++a) {
-                    double v = bp[6 * p + a];
+                    w_reset(wt);
                     for (int k = s.pe_off[p]; k < s.pe_off[p + 1]; ++k) {
                         const int e = s.pe[k];
                         const double* w = W + 18 * e + 3 * a;
                         const double* g = bl + 3 * el[e];
-                        v = v - (w[0] * g[0] + w[1] * g[1] + w[2] * g[2]);
+                        w_add(wt, k - s.pe_off[p], w[0] * g[0] + w[1] * g[1] + w[2] * g[2]);
                     }
-                    bs[6 * (p - n_fixed) + a] = v;
+                    bs[6 * (p - n_fixed) + a] = bp[6 * p + a] - w_total(wt);
                 }
             const int ok2 = ns > 0 ? or_ldlt_solve(S, ns, bs, xp) : 1;
             const int dump = it == or_ba_dump_iter && q == 0;
@@ -439,7 +470,7 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
         }
     }
     free(Jp); free(Jl); free(err); free(Hpl); free(W); free(Hpp); free(bp); free(Hll); free(bl); free(Dinv);
-    free(S); free(bs); free(xp); free(xl); free(bak_p); free(bak_X);
+    free(S); free(bs); free(xp); free(xl); free(bak_p); free(bak_X); free(wt);
     ba_free_struct(&s);
     return it;
 }

@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 import ya_vo_amd as yv  # noqa: E402
 
 PHASES = ["preamble (stage S, ranks, registers)", "wait for column k", "step loads + diagonal chain",
-          "owner: slot loop through publish of k + 1", "slot loop (rest)", "final barrier", "solves (wave 0)", "-"]
+          "owner: pair q + 1 finalised and published", "bulk update (+ wave 0 forward solve)", "final barrier", "solves (wave 0)", "-"]
 
 
 def window_system(nb, seed):
@@ -43,15 +43,15 @@ def main():
     S = window_system(args.n // 6, 1)
     b = np.random.default_rng(2).normal(size=args.n)
     ctx.ba_ldlt(S, b)
-    prof = np.zeros((4, 8), np.uint64)
+    prof = np.zeros((8, 8), np.uint64)
     lib.yv_debug_ldlt_prof(prof.ctypes.data)
     for _ in range(args.calls):
         ctx.ba_ldlt(S, b)
     assert lib.yv_debug_ldlt_prof(prof.ctypes.data) == 0
     per = prof.astype(np.float64) / args.calls
     out = {"n": args.n, "calls": args.calls, "cycles_per_call_per_wave": {
-        PHASES[q]: [round(float(per[w, q])) for w in range(4)] for q in range(7)},
-        "total_per_wave": [round(float(per[w].sum())) for w in range(4)]}
+        PHASES[q]: [round(float(per[w, q])) for w in range(8)] for q in range(7)},
+        "total_per_wave": [round(float(per[w].sum())) for w in range(8)]}
     print(json.dumps(out, indent=1))
     ctx.close()
 

@@ -1283,6 +1283,7 @@ struct Arena {
         size_t off, bytes;
     };
     std::vector<Out> outs;
+    std::vector<std::pair<size_t, size_t>> host_spans;  // [off, off + bytes) of every add_host region
     template <class T>
     void add(T** p, size_t count) {
         reqs.push_back({reinterpret_cast<void**>(p), count * sizeof(T), false});
@@ -1317,8 +1318,10 @@ struct Arena {
         }
         char* base = reinterpret_cast<char*>(ctx->scratch);
         size_t off = 0;
+        host_spans.clear();
         for (auto& r : reqs) {
             *r.p = r.host ? static_cast<void*>(ctx->scratch_hd + off) : static_cast<void*>(base + off);
+            if (r.host) host_spans.push_back({off, off + r.bytes});
             off += (r.bytes + 255) & ~(size_t)255;
         }
         return YV_OK;
@@ -1363,10 +1366,24 @@ struct Arena {
         return hipMemcpyAsync(static_cast<char*>(ctx->scratch) + in_lo, ctx->scratch_h + in_lo, in_hi - in_lo,
                               hipMemcpyHostToDevice, s);
     }
+    // one DMA over the span of the device outputs, unless a host region (written in place by the kernel) lies inside
+    // it: then one DMA per device output, so the span's stale device bytes never land on those host results
     hipError_t download(hipStream_t s) {
         if (out_hi <= out_lo) return hipSuccess;
-        return hipMemcpyAsync(ctx->scratch_h + out_lo, static_cast<char*>(ctx->scratch) + out_lo, out_hi - out_lo,
-                              hipMemcpyDeviceToHost, s);
+        bool split = false;
+        for (const auto& h : host_spans) split |= h.first < out_hi && h.second > out_lo;
+        if (!split)
+            return hipMemcpyAsync(ctx->scratch_h + out_lo, static_cast<char*>(ctx->scratch) + out_lo,
+                                  out_hi - out_lo, hipMemcpyDeviceToHost, s);
+        for (const auto& o : outs) {
+            bool host = false;
+            for (const auto& h : host_spans) host |= o.off >= h.first && o.off < h.second;
+            if (host) continue;
+            hipError_t e = hipMemcpyAsync(ctx->scratch_h + o.off, static_cast<char*>(ctx->scratch) + o.off, o.bytes,
+                                          hipMemcpyDeviceToHost, s);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
     }
     // after the stream drained: the outputs into the caller's buffers
     void finish() {

@@ -99,12 +99,9 @@ __global__ __launch_bounds__(256) void ba_linearize_kernel(BaParams P, BaMat3 K)
 #pragma unroll
         for (int c = 0; c < 3; ++c)
             Jl[r * 3 + c] = Jp[r * 6 + 0] * R[0 * 3 + c] + Jp[r * 6 + 1] * R[1 * 3 + c] + Jp[r * 6 + 2] * R[2 * 3 + c];
-    double H[18];
-#pragma unroll
-    for (int a = 0; a < 6; ++a)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) H[3 * a + c] = Jp[a] * Jl[c] + Jp[6 + a] * Jl[3 + c];
-    // 16-B stores (every per-edge block is 16-B aligned)
+    // 16-B stores (every per-edge block is 16-B aligned). H_pl = J_pose^T J_point (6 x 3) is not stored: its readers
+    // form it from these 144 B (hpl_load), which is what storing it would cost them to read, and the 144 B/edge write
+    // is saved
     reinterpret_cast<double2*>(P.err)[e] = make_double2(err[0], err[1]);
     double2* jp2 = reinterpret_cast<double2*>(P.Jp + 12 * (int64_t)e);
 #pragma unroll
@@ -112,25 +109,69 @@ __global__ __launch_bounds__(256) void ba_linearize_kernel(BaParams P, BaMat3 K)
     double2* jl2 = reinterpret_cast<double2*>(P.Jl + 6 * (int64_t)e);
 #pragma unroll
     for (int i = 0; i < 3; ++i) jl2[i] = make_double2(Jl[2 * i], Jl[2 * i + 1]);
-    double2* h2 = reinterpret_cast<double2*>(P.Hpl + 18 * (int64_t)e);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) h2[i] = make_double2(H[2 * i], H[2 * i + 1]);
 }
 
-// last-block-done: every workgroup of the launch arrives once, after its global stores; true in the workgroup that
-// arrived last, after an agent-scope acquire, so it reads what every other workgroup stored (release: each
-// arriving workgroup's fence before its ticket; per-XCD L2s are not coherent, the agent-scope fences write back and
-// invalidate). The counter is left at 0 for the next launch. Every thread of the workgroup must call it.
+// H_pl(e) = J_pose^T J_point, the expression of the oracle's buildSystem, from the edge's stored Jacobians
+__device__ __forceinline__ void hpl_load(const BaParams& P, int64_t e, double* h) {
+    double J[12], L[6];
+    const double2* jp = reinterpret_cast<const double2*>(P.Jp + 12 * e);
+    const double2* jl = reinterpret_cast<const double2*>(P.Jl + 6 * e);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const double2 v = jp[i];
+        J[2 * i] = v.x;
+        J[2 * i + 1] = v.y;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double2 v = jl[i];
+        L[2 * i] = v.x;
+        L[2 * i + 1] = v.y;
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) h[3 * a + c] = J[a] * L[c] + J[6 + a] * L[3 + c];
+}
+
+// last-block-done: every workgroup of the launch arrives once; true in the workgroup that arrived last. What the
+// last workgroup reads from the others is published write-through (agent-scope atomic stores, or atomics), drained
+// (s_waitcnt vmcnt(0) in every storing wave) before the workgroup's barrier and ticket, and read back with agent-scope
+// atomic loads: no cache maintenance fences (MI355X guide, Guideline 16's sc1 form). The counter is left at 0 for the
+// next launch. Every thread of the workgroup must call it.
 __device__ bool ba_last_block(unsigned* ticket) {
     __shared__ unsigned s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence();
-        const unsigned tk = atomicAdd(ticket, 1u);
+        const unsigned tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const bool last = tk == gridDim.x - 1;
-        if (last) {
-            __threadfence();
-            atomicExch(ticket, 0u);
+        if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = last ? 1u : 0u;
+    }
+    __syncthreads();
+    return s_last != 0;
+}
+
+// the same over a large grid: consecutive workgroups in groups of gs = max(16, ceil(grid / 64)), counted per group
+// (groups[0 .. 63]); the last of a group counts at *top. Same-address atomics serialise at the cache (a 512-way
+// single counter cost ~10 us), so no counter takes more than 64 arrivals.
+constexpr int kTicketGroups = 64;
+__device__ bool ba_last_block_h(unsigned* top, unsigned* groups) {
+    __shared__ unsigned s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned G = gridDim.x;
+        const unsigned gs = max(16u, (G + kTicketGroups - 1) / kTicketGroups);
+        const unsigned gi = blockIdx.x / gs, ng = (G + gs - 1) / gs, gsize = min(gs, G - gi * gs);
+        bool last = false;
+        if (__hip_atomic_fetch_add(&groups[gi], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+            __hip_atomic_store(&groups[gi], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1) {
+                __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = true;
+            }
         }
         s_last = last ? 1u : 0u;
     }
@@ -138,10 +179,35 @@ __device__ bool ba_last_block(unsigned* ticket) {
     return s_last != 0;
 }
 
+// last of `count` workgroups to arrive at a per-task counter (see ba_last_block)
+__device__ bool ba_last_of(unsigned* ticket, unsigned count) {
+    __shared__ unsigned s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = tk == count - 1;
+        if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = last ? 1u : 0u;
+    }
+    __syncthreads();
+    return s_last != 0;
+}
+
+__device__ __forceinline__ double ld_agent(const double* p) {
+    return __longlong_as_double(
+        __hip_atomic_load(reinterpret_cast<const long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_agent(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<long long*>(p), __double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // an iteration's trial loop starts (after its linearisation); the first one sets lambda = tau max|H_ii|
 __device__ void ba_ctl_iter_begin(BaCtl* c, const unsigned long long* maxdiag) {
     if (maxdiag) {
-        const double maxd = __longlong_as_double((long long)*maxdiag);
+        const double maxd = __longlong_as_double(
+            (long long)__hip_atomic_load(maxdiag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         c->lambda = 1e-5 * maxd;
         c->ni = 2;
     }
@@ -150,31 +216,67 @@ __device__ void ba_ctl_iter_begin(BaCtl* c, const unsigned long long* maxdiag) {
     c->skip_trial = 0;
 }
 
-__device__ __forceinline__ void atomic_max_abs(unsigned long long* m, double v) {
-    if (v > 0.0) atomicMax(m, (unsigned long long)__double_as_longlong(v));  // NaN never, as fmax ignores it
+// tree4096 (the oracle's order for H_pp / b_p, the Schur blocks and b_schur): leaf t sums items k = t mod 4096 in
+// ascending k from 0.0, then p[t] += p[t + off], off = 2048 .. 1. A sum runs on kWG workgroups of kWLanes lanes:
+// lane u of workgroup g holds leaf g + kWG u. Levels off = 2048 .. kWG add leaves of one residue class mod kWG, so
+// each workgroup runs them on its own leaves (off / kWG lanes apart, nv trees at once) and publishes its class totals;
+// the last workgroup runs levels kWG / 2 .. 1 over the kWG totals.
+constexpr int kWLeaves = 4096;
+constexpr int kWG = 32;
+constexpr int kWLanes = kWLeaves / kWG;  // 128
+
+template <int NV>
+__device__ __forceinline__ void wide_local_tree(double* red) {  // red[q * kWLanes + u]; totals end in red[q * kWLanes]
+    const int t = threadIdx.x;
+    __syncthreads();
+    for (int off = kWLanes / 2; off > 0; off >>= 1) {
+        for (int idx = t; idx < NV * off; idx += kWLanes) {
+            const int q = idx / off, u = idx - q * off;
+            red[q * kWLanes + u] = red[q * kWLanes + u] + red[q * kWLanes + u + off];
+        }
+        __syncthreads();
+    }
 }
 
-// One launch for the iteration's blocks of H and b:
-//  blocks [0, np)      one per free pose: 21 upper H_pp entries + 6 b_p entries in tree256 order over the pose's
-//                      edges (each thread's strided chain, two edges' loads in flight, then the 27 halving trees)
-//  blocks [np, ...)    one lane per landmark: H_ll, b_l sequential over its edges
+// levels kWG / 2 .. 1 over the class totals part[u * stride], u < kWG (published write-through)
+__device__ __forceinline__ double wide_top_tree(const double* part, int stride) {
+    double v[kWG];
+#pragma unroll
+    for (int u = 0; u < kWG; ++u) v[u] = ld_agent(&part[u * stride]);
+#pragma unroll
+    for (int off = kWG / 2; off > 0; off >>= 1)
+#pragma unroll
+        for (int i = 0; i < off; ++i) v[i] = v[i] + v[i + off];
+    return v[0];
+}
+
+__device__ __forceinline__ void atomic_max_abs(unsigned long long* m, double v) {
+    if (v > 0.0)  // NaN never, as fmax ignores it
+        __hip_atomic_fetch_max(m, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One launch for the iteration's blocks of H and b (kWLanes threads per workgroup):
+//  blocks [0, np kWG)  kWG per free pose: 21 upper H_pp entries + 6 b_p entries in tree4096 order over the pose's
+//                      edges (a lane's items k = leaf + 4096 m: one per lane up to 4096 edges, all loads in flight),
+//                      the 27 local trees at once, class totals published; the pose's last workgroup writes H_pp, b_p
+//  blocks beyond:      one lane per landmark: H_ll, b_l sequential over its edges
 // first: the largest |diagonal| (free poses and landmarks) into *P.maxdiag (uint64 bits of a non-negative double).
 // Device control: the last workgroup starts the iteration's trial loop (lambda on the first iteration).
-__global__ __launch_bounds__(256) void ba_reduce_kernel(BaParams P, int first) {
-    __shared__ double red[27 * kNT];
+__global__ __launch_bounds__(kWLanes) void ba_reduce_kernel(BaParams P, int first) {
+    __shared__ double red[27 * kWLanes];
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     const int t = threadIdx.x;
-    if ((int)blockIdx.x < P.np) {
-        const int p = P.nf + blockIdx.x;
+    if ((int)blockIdx.x < P.np * kWG) {
+        const int j = blockIdx.x / kWG, g = blockIdx.x - j * kWG, p = P.nf + j;
         const int k0 = P.pe_off[p], k1 = P.pe_off[p + 1];
-        double h[21], g[6];
+        double h[21], gv[6];
 #pragma unroll
         for (int i = 0; i < 21; ++i) h[i] = 0.0;
 #pragma unroll
-        for (int i = 0; i < 6; ++i) g[i] = 0.0;
-        // this thread's edges k0 + t, k0 + t + 256, ...: the next edge's J and e are loaded (and the one after's index)
-        // while this edge's terms are added
-        auto load_edge = [&](int e, double (&J)[12], double (&er)[2]) {
+        for (int i = 0; i < 6; ++i) gv[i] = 0.0;
+        for (int k = k0 + g + kWG * t; k < k1; k += kWLeaves) {
+            const int e = P.pe[k];
+            double J[12];
             const double2* jp = reinterpret_cast<const double2*>(P.Jp + 12 * (int64_t)e);
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
@@ -183,63 +285,39 @@ __global__ __launch_bounds__(256) void ba_reduce_kernel(BaParams P, int first) {
                 J[2 * i + 1] = v.y;
             }
             const double2 ev = reinterpret_cast<const double2*>(P.err)[e];
-            er[0] = ev.x;
-            er[1] = ev.y;
-        };
-        int k = k0 + t;
-        double Jc[12], ec[2];
-        if (k < k1) load_edge(P.pe[k], Jc, ec);
-        int e_next = k + kNT < k1 ? P.pe[k + kNT] : 0;
-        while (k < k1) {
-            double Jn[12], en[2];
-            const bool more = k + kNT < k1;
-            if (more) load_edge(e_next, Jn, en);
-            if (k + 2 * kNT < k1) e_next = P.pe[k + 2 * kNT];
             int q = 0;
 #pragma unroll
             for (int a = 0; a < 6; ++a)
 #pragma unroll
-                for (int b = a; b < 6; ++b, ++q) h[q] = h[q] + (Jc[a] * Jc[b] + Jc[6 + a] * Jc[6 + b]);
+                for (int b = a; b < 6; ++b, ++q) h[q] = h[q] + (J[a] * J[b] + J[6 + a] * J[6 + b]);
 #pragma unroll
-            for (int a = 0; a < 6; ++a) g[a] = g[a] + (Jc[a] * ec[0] + Jc[6 + a] * ec[1]);
-            k += kNT;
-            if (more) {
-#pragma unroll
-                for (int i = 0; i < 12; ++i) Jc[i] = Jn[i];
-                ec[0] = en[0];
-                ec[1] = en[1];
-            }
+            for (int a = 0; a < 6; ++a) gv[a] = gv[a] + (J[a] * ev.x + J[6 + a] * ev.y);
         }
-        // the 27 halving trees at once: level `off` has 27 * off independent additions p[t] = p[t] + p[t + off],
-        // spread over all 256 threads (each tree's order is the one tree256 uses)
 #pragma unroll
-        for (int i = 0; i < 21; ++i) red[i * kNT + t] = h[i];
+        for (int i = 0; i < 21; ++i) red[i * kWLanes + t] = h[i];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) red[(21 + i) * kNT + t] = g[i];
-        __syncthreads();
-        for (int off = kNT / 2; off > 0; off >>= 1) {
-            for (int idx = t; idx < 27 * off; idx += kNT) {
-                const int q = idx / off, u = idx - q * off;
-                red[q * kNT + u] = red[q * kNT + u] + red[q * kNT + u + off];
+        for (int i = 0; i < 6; ++i) red[(21 + i) * kWLanes + t] = gv[i];
+        wide_local_tree<27>(red);
+        double* part = P.rpart + (int64_t)j * kWG * 27;
+        if (t < 27) st_agent(&part[g * 27 + t], red[t * kWLanes]);
+        if (ba_last_of(P.rticket + j, kWG) && t < 27) {
+            const double v = wide_top_tree(part + t, 27);
+            double* H = P.Hpp + 36 * p;
+            if (t < 21) {
+                int a = 0, q = t;
+                while (q >= 6 - a) {
+                    q -= 6 - a;
+                    ++a;
+                }
+                const int b = a + q;
+                H[6 * a + b] = H[6 * b + a] = v;
+                if (first && a == b) atomic_max_abs(P.maxdiag, fabs(v));
+            } else {
+                P.bp[6 * p + t - 21] = -v;
             }
-            __syncthreads();
-        }
-        double* H = P.Hpp + 36 * p;
-        if (t < 21) {
-            int a = 0, q = t;
-            while (q >= 6 - a) {
-                q -= 6 - a;
-                ++a;
-            }
-            const int b = a + q;
-            const double v = red[t * kNT];
-            H[6 * a + b] = H[6 * b + a] = v;
-            if (first && a == b) atomic_max_abs(P.maxdiag, fabs(v));
-        } else if (t < 27) {
-            P.bp[6 * p + t - 21] = -red[t * kNT];
         }
     } else {
-        const int l = (blockIdx.x - P.np) * kNT + t;
+        const int l = (blockIdx.x - P.np * kWG) * kWLanes + t;
         if (l < P.L) {
             double h[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
             for (int k = P.le_off[l]; k < P.le_off[l + 1]; ++k) {
@@ -267,7 +345,8 @@ __global__ __launch_bounds__(256) void ba_reduce_kernel(BaParams P, int first) {
             if (first) atomic_max_abs(P.maxdiag, m);
         }
     }
-    if (P.ctl && ba_last_block(P.ticket + 0) && t == 0) ba_ctl_iter_begin(P.ctl, first ? P.maxdiag : nullptr);
+    if (P.ctl && ba_last_block_h(P.ticket + 0, P.ticket + 4) && t == 0)
+        ba_ctl_iter_begin(P.ctl, first ? P.maxdiag : nullptr);
 }
 
 __device__ __forceinline__ void inv3(const double* a, double* o) {
@@ -303,13 +382,7 @@ __global__ __launch_bounds__(256) void ba_landmark_trial_kernel(BaParams P, doub
 #pragma unroll
         for (int a = 0; a < 3; ++a) d[4 * a] = d[4 * a] + lambda;
         inv3(d, Di);
-        const double2* h2 = reinterpret_cast<const double2*>(P.Hpl + 18 * (int64_t)id);
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            const double2 v = h2[i];
-            h[2 * i] = v.x;
-            h[2 * i + 1] = v.y;
-        }
+        hpl_load(P, id, h);
         double w[18];
 #pragma unroll
         for (int a = 0; a < 6; ++a)
@@ -322,163 +395,124 @@ __global__ __launch_bounds__(256) void ba_landmark_trial_kernel(BaParams P, doub
     }
 }
 
-constexpr int kSchurPass = 128;   // pairs per pass
-constexpr int kSchurStride = 37;  // doubles per staged pair: 36 products + 1 (2-way instead of 8-way bank conflicts)
-constexpr int kSchurThreads = 256;
-
-// 18 doubles (one 6 x 3 block, 144 B, 16-B aligned) into registers
-__device__ __forceinline__ void load18(const double* src, double* r) {
-    const double2* s2 = reinterpret_cast<const double2*>(src);
+// The Schur complement in the oracle's tree4096 order. Task = an upper block (p1 <= p2) of the free poses, or one
+// pose's b_schur; kWG workgroups per task (see wide_local_tree). A lane's items (pair k = leaf + 4096 m) are loaded as
+// W_e1 (9 16-B loads) and H_pl(e2) (formed from its Jacobians: 9 16-B loads), the next one's already in flight; a configs[2]
+// window has at most one per lane, so a block's ~3,700 pairs are read by 32 CUs with every load in flight at once.
+// grid: (nb + np) kWG workgroups; task = blockIdx / kWG, g = blockIdx % kWG.
+//  tasks [0, nb): S(a, b) = base - tree4096 over the co-visible pairs k of (W_e1(k)[a] . H_pl(e2(k))[b]); on a
+//    diagonal block only a >= b is written, to both mirrored entries (the oracle's loop leaves that value)
+//  tasks [nb, nb + np): b_schur(a) = b_p[a] - tree4096 over the pose's edges of W_e[a] . b_l(e)
+__device__ __forceinline__ void load18(const double* blk, double* r) {
+    const double2* v2 = reinterpret_cast<const double2*>(blk);
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
-        const double2 v = s2[i];
+        const double2 v = v2[i];
         r[2 * i] = v.x;
         r[2 * i + 1] = v.y;
     }
 }
 
-// the sequential chain v = v - d_0 - d_1 - ... over n staged products: the LDS loads of the next eight are issued
-// before this eight's subtractions (double-buffered), so the chain waits on FP64 latency, not on LDS
-__device__ __forceinline__ double schur_chain(double v, const double* sd, int n, int col) {
-    int j = 0;
-    if (n >= 8) {
-        double d[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) d[u] = sd[u * kSchurStride + col];
-        for (; j + 16 <= n; j += 8) {
-            double e[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) e[u] = sd[(j + 8 + u) * kSchurStride + col];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v = v - d[u];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) d[u] = e[u];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v = v - d[u];
-        j += 8;
-    }
-    for (; j < n; ++j) v = v - sd[j * kSchurStride + col];
-    return v;
-}
-
-// One 256-thread workgroup per upper Schur block (p1 <= p2) of the free poses, then one per free pose for b_schur.
-// Block: entry (a, b) is the oracle's sequential chain over the landmarks the two poses share,
-// v = v - (W_e1[a] . H_pl(e2)[b]). The waves are specialised: waves 1-3 produce, wave 0 consumes. In pass q the
-// producers form pass q's 128 pairs' 36 products from their registers into one half of a double-buffered LDS stage
-// (and start loading pass q + 2's blocks), while lanes a * 6 + b (< 36) of wave 0 run their chains over pass q - 1's
-// products in the other half (one LDS load and one subtraction per pair); one barrier per pass. On a diagonal block
-// only a >= b writes (the oracle's loop leaves the (max, min) value in both mirrored entries). b_schur: lanes a < 6
-// run v = b_p[a] - sum_e W_e[a] . b_l(e) over the pose's edges, the products formed the same way.
-__global__ __launch_bounds__(kSchurThreads) void ba_schur_kernel(BaParams P, double lambda) {
-    __shared__ double sd[2][kSchurPass * kSchurStride];
+__global__ __launch_bounds__(kWLanes) void ba_schur_kernel(BaParams P, double lambda) {
+    __shared__ double red[36 * kWLanes];
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     if (P.lam) lambda = *P.lam;
     const int np = P.np, nb = np * (np + 1) / 2;
-    const int t = threadIdx.x;
-    const int pi = t - 64;  // producer index (waves 1-3), < kSchurPass for the producing lanes
-    const bool prod = pi >= 0 && pi < kSchurPass;
-    const int a = t / 6, b = t - 6 * (t / 6);
-    if ((int)blockIdx.x < nb) {
-        int blk = blockIdx.x, i1 = 0;
+    const int task = blockIdx.x / kWG, g = blockIdx.x - task * kWG;
+    const int t = threadIdx.x, leaf = g + kWG * t;
+    if (task < nb) {
+        int blk = task, i1 = 0;
         while (blk >= np - i1) {
             blk -= np - i1;
             ++i1;
         }
         const int i2 = i1 + blk;
         const int p1 = P.nf + i1, p2 = P.nf + i2;
-        const bool active = t < 36 && !(i1 == i2 && a < b);
-        double v = 0.0;
-        if (active) v = p1 == p2 ? P.Hpp[36 * p1 + 6 * a + b] + (a == b ? lambda : 0.0) : 0.0;
         const int c0 = P.cv_off[p1 * P.P + p2], c1 = P.cv_off[p1 * P.P + p2 + 1];
-        const int npass = (c1 - c0 + kSchurPass - 1) / kSchurPass;
-        double rw[2][18], rh[2][18];  // the blocks of passes q (slot q & 1) and q + 1
-        if (prod) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-                if (c0 + u * kSchurPass + pi < c1) {
-                    load18(P.W + 18 * (int64_t)P.cv_e1[c0 + u * kSchurPass + pi], rw[u]);
-                    load18(P.Hpl + 18 * (int64_t)P.cv_e2[c0 + u * kSchurPass + pi], rh[u]);
+        if (c1 == c0) {  // no shared landmark: base - (the tree of 0.0 leaves = 0.0)
+            if (g == 0)
+                for (int q = t; q < 36; q += kWLanes) {
+                    const int a = q / 6, b = q % 6;
+                    if (i1 == i2 && a < b) continue;
+                    const double base = p1 == p2 ? P.Hpp[36 * p1 + 6 * a + b] + (a == b ? lambda : 0.0) : 0.0;
+                    const double v = base - 0.0;
+                    const int r = 6 * i1 + a, c = 6 * i2 + b, ns = P.ns;
+                    P.S[(int64_t)r * ns + c] = v;
+                    P.S[(int64_t)c * ns + r] = v;
                 }
+            return;
         }
-        // passes in pairs so the register slot (q & 1) is a compile-time index
-        auto pass = [&](const int q, double (&w_)[18], double (&h_)[18], double* buf, const double* prev) {
-            if (prod && q < npass) {
-                if (c0 + q * kSchurPass + pi < c1) {
-                    double* dst = &buf[pi * kSchurStride];
+        double acc[36];
 #pragma unroll
-                    for (int x = 0; x < 6; ++x)
+        for (int i = 0; i < 36; ++i) acc[i] = 0.0;
+        int i = c0 + leaf;
+        double w[18], h[18];
+        if (i < c1) {
+            load18(P.W + 18 * (int64_t)P.cv_e1[i], w);
+            hpl_load(P, P.cv_e2[i], h);
+        }
+        while (i < c1) {
+            const int nx = i + kWLeaves;
+            double wn[18], hn[18];
+            if (nx < c1) {
+                load18(P.W + 18 * (int64_t)P.cv_e1[nx], wn);
+                hpl_load(P, P.cv_e2[nx], hn);
+            }
 #pragma unroll
-                        for (int y = 0; y < 6; ++y)
-                            dst[6 * x + y] = w_[3 * x] * h_[3 * y] + w_[3 * x + 1] * h_[3 * y + 1] + w_[3 * x + 2] * h_[3 * y + 2];
-                }
-                const int nx = c0 + (q + 2) * kSchurPass + pi;
-                if (nx < c1) {
-                    load18(P.W + 18 * (int64_t)P.cv_e1[nx], w_);
-                    load18(P.Hpl + 18 * (int64_t)P.cv_e2[nx], h_);
+            for (int a = 0; a < 6; ++a)
+#pragma unroll
+                for (int b = 0; b < 6; ++b)
+                    acc[6 * a + b] = acc[6 * a + b] + (w[3 * a] * h[3 * b] + w[3 * a + 1] * h[3 * b + 1] + w[3 * a + 2] * h[3 * b + 2]);
+            i = nx;
+            if (i < c1) {
+#pragma unroll
+                for (int u = 0; u < 18; ++u) {
+                    w[u] = wn[u];
+                    h[u] = hn[u];
                 }
             }
-            if (active && q > 0) v = schur_chain(v, prev, min(kSchurPass, c1 - c0 - (q - 1) * kSchurPass), t);
-            __syncthreads();
-        };
-        for (int q = 0; q <= npass; q += 2) {
-            pass(q, rw[0], rh[0], sd[0], sd[1]);
-            if (q + 1 <= npass) pass(q + 1, rw[1], rh[1], sd[1], sd[0]);
         }
-        if (active) {
-            const int r = 6 * i1 + a, c = 6 * i2 + b, ns = P.ns;
-            P.S[(int64_t)r * ns + c] = v;
-            P.S[(int64_t)c * ns + r] = v;
+#pragma unroll
+        for (int q = 0; q < 36; ++q) red[q * kWLanes + t] = acc[q];
+        wide_local_tree<36>(red);
+        double* part = P.spart + (int64_t)task * kWG * 36;
+        if (t < 36) st_agent(&part[g * 36 + t], red[t * kWLanes]);
+        if (!ba_last_of(P.sticket + task, kWG)) return;
+        if (t < 36) {
+            const int a = t / 6, b = t % 6;
+            if (!(i1 == i2 && a < b)) {
+                const double base = p1 == p2 ? P.Hpp[36 * p1 + 6 * a + b] + (a == b ? lambda : 0.0) : 0.0;
+                const double v = base - wide_top_tree(part + t, 36);
+                const int r = 6 * i1 + a, c = 6 * i2 + b, ns = P.ns;
+                P.S[(int64_t)r * ns + c] = v;
+                P.S[(int64_t)c * ns + r] = v;
+            }
         }
     } else {
-        const int j = blockIdx.x - nb, p = P.nf + j;
-        const bool active = t < 6;
-        double v = active ? P.bp[6 * p + t] : 0.0;
+        const int j = task - nb, p = P.nf + j;
         const int k0 = P.pe_off[p], k1 = P.pe_off[p + 1];
-        const int npass = (k1 - k0 + kSchurPass - 1) / kSchurPass;
-        double rw[2][18], rg[2][3];
-        if (prod) {
+        double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int i = k0 + leaf; i < k1; i += kWLeaves) {
+            const int e = P.pe[i];
+            double w[18];
+            load18(P.W + 18 * (int64_t)e, w);
+            const double* gl = P.bl + 3 * P.el[e];
+            const double g0 = gl[0], g1 = gl[1], g2 = gl[2];
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
-                if (k0 + u * kSchurPass + pi < k1) {
-                    const int e = P.pe[k0 + u * kSchurPass + pi];
-                    load18(P.W + 18 * (int64_t)e, rw[u]);
-                    const double* g = P.bl + 3 * P.el[e];
-                    rg[u][0] = g[0];
-                    rg[u][1] = g[1];
-                    rg[u][2] = g[2];
-                }
+            for (int a = 0; a < 6; ++a) acc[a] = acc[a] + (w[3 * a] * g0 + w[3 * a + 1] * g1 + w[3 * a + 2] * g2);
         }
-        auto pass = [&](const int q, double (&w_)[18], double (&g_)[3], double* buf, const double* prev) {
-            if (prod && q < npass) {
-                if (k0 + q * kSchurPass + pi < k1) {
-                    double* dst = &buf[pi * kSchurStride];
 #pragma unroll
-                    for (int x = 0; x < 6; ++x) dst[x] = w_[3 * x] * g_[0] + w_[3 * x + 1] * g_[1] + w_[3 * x + 2] * g_[2];
-                }
-                const int nx = k0 + (q + 2) * kSchurPass + pi;
-                if (nx < k1) {
-                    const int e = P.pe[nx];
-                    load18(P.W + 18 * (int64_t)e, w_);
-                    const double* g = P.bl + 3 * P.el[e];
-                    g_[0] = g[0];
-                    g_[1] = g[1];
-                    g_[2] = g[2];
-                }
-            }
-            if (active && q > 0) v = schur_chain(v, prev, min(kSchurPass, k1 - k0 - (q - 1) * kSchurPass), t);
-            __syncthreads();
-        };
-        for (int q = 0; q <= npass; q += 2) {
-            pass(q, rw[0], rg[0], sd[0], sd[1]);
-            if (q + 1 <= npass) pass(q + 1, rw[1], rg[1], sd[1], sd[0]);
-        }
-        if (active) P.bs[6 * j + t] = v;
+        for (int q = 0; q < 6; ++q) red[q * kWLanes + t] = acc[q];
+        wide_local_tree<6>(red);
+        double* part = P.spart + (int64_t)task * kWG * 36;
+        if (t < 6) st_agent(&part[g * 36 + t], red[t * kWLanes]);
+        if (!ba_last_of(P.sticket + task, kWG)) return;
+        if (t < 6) P.bs[6 * j + t] = P.bp[6 * p + t] - wide_top_tree(part + t, 36);
     }
 }
 
 // Eigen LDLT on the reduced system (n <= kLdltRegN = 128), bit-identical to the oracle's left-looking
-// or_ldlt_solve (diagonal pivoting), in one 256-thread workgroup with no workgroup barrier inside the factorisation:
+// or_ldlt_solve (diagonal pivoting), in one 512-thread workgroup with no workgroup barrier inside the factorisation:
 //  1. The pivot sequence. At step k the oracle takes the first position of the largest |L(i, i)|, i >= k, and L(i, i)
 //     for i >= k still holds an original diagonal entry (it is only updated at its own step), so the sequence follows
 //     from the diagonal alone. Distinct values (the usual case): it is the descending order, by ranks. Any tie or NaN:
@@ -486,28 +520,28 @@ __global__ __launch_bounds__(kSchurThreads) void ba_schur_kernel(BaParams P, dou
 //  2. Pivoting commutes with the left-looking factorisation: the oracle swaps untouched original entries in the
 //     trailing part and the finished rows of L, so its result equals the unpivoted factorisation of P S P^T (S is
 //     bitwise symmetric: each Schur entry is stored to both halves from one value).
-//  3. The unpivoted factorisation runs right-looking with the matrix in registers: wave w holds columns c = 4 j + w
-//     (j < 32) of P S P^T, lane l rows l and l + 64. The oracle forms column k as acc = L(i, k) - L(i, 0) t_0 -
-//     L(i, 1) t_1 - ... (t_j = D(j) L(k, j)) and D(k) = L(k, k) - (L(k, 0) t_0 + ...); step j here applies term j of
-//     every such chain (L(i, c) -= L(i, j) t_j(c), t_j(c) = D(j) L(c, j); dot_i += L(i, j) t_j(i)), the same operations
-//     in the same order per entry. Column k is finalised by the wave that holds it (D(k), the rows divided by it) and
-//     published: L(., k) into the column store (kept for the solves), t_k(.) into a ring of kLdltRing slots, then a
-//     per-slot flag (workgroup-scope release / acquire). At step k a wave waits for column k's flag; the wave that
-//     holds column k + 1 first applies term k to it, finalises and publishes it (a switch on its slot), so the critical
-//     path per column is one LDS hand-off, one update and one division; then every wave applies term k to all 32 of
-//     its slots without a branch (a finalised column's registers are dead, so updating them again is harmless, and
-//     straight-line code keeps the FP64 pipe busy). A slot is rewritten kLdltRing columns later, which needs every
-//     wave to have read it (a wave owns one of any four consecutive columns, so none can run more than four columns
-//     ahead of another). Wave 0 also runs the forward solve v(i) -= L(i, k) v(k) at step k, in the oracle's order.
+//  3. The unpivoted factorisation runs right-looking with the matrix in registers, two columns at a time. The oracle
+//     forms column k as acc = L(i, k) - L(i, 0) t_0 - L(i, 1) t_1 - ... (t_j = D(j) L(k, j)) and D(k) = L(k, k) -
+//     (L(k, 0) t_0 + ...); a term j applied to every such chain (L(i, c) -= L(i, j) t_j(c), t_j(c) = D(j) L(c, j);
+//     dot_i += L(i, j) t_j(i)) in ascending j gives the same operations in the same order per entry. Wave w (of 8, two
+//     per SIMD) holds the column pairs q = 8 j + w (columns 2q, 2q + 1) of P S P^T, lane l rows l and l + 64. The wave
+//     that holds pair q + 1 finalises both its columns as soon as pair q is published: column 2q + 2 from terms 2q,
+//     2q + 1 and its division, then column 2q + 3 with term 2q + 2 taken from its own lanes by v_readlane (no LDS
+//     round trip inside the pair) -- at raised wave priority, before its share of the bulk update. A published pair
+//     is L(., c) in the column store (kept for the solves), t_c(.) in a ring of kLdltRing pair slots and a per-slot
+//     flag (workgroup-scope release / acquire). Every wave then applies the pair's two terms to its live pairs'
+//     registers (a finalised pair's registers are dead). A slot is rewritten kLdltRing pairs later, which needs every
+//     wave to have read it: a wave owns one of any eight consecutive pairs, so none runs more than eight ahead.
+//     Wave 0 also runs the forward solve v(i) -= L(i, k) v(k), in the oracle's order.
 //     (Round 4 kept the packed triangle in LDS with one workgroup barrier per column step: 139 us per factorisation
-//     at n = 120 in the configs[2] sequence.)
+//     at n = 120 in the configs[2] sequence; one column per hand-off with four waves: 84 us.)
 //  4. The diagonal and backward solves run on wave 0: the vector in registers (two entries per lane), broadcasts by
-//     v_readlane, L read by row from the column store (stride 129 doubles: conflict-free by rows and by columns),
-//     eight columns' loads ahead of the dependent chain.
+//     v_readlane, L read by row from the column store (stride 129 doubles: conflict-free by rows and by columns).
 constexpr int kLdltRegN = 128;   // n <= 128: lane l holds rows l and l + 64
-constexpr int kLdltSlots = 32;   // columns per wave: c = 4 j + w
+constexpr int kLdltWaves = 8;    // 512 threads: two waves per SIMD
+constexpr int kLdltPairs = 8;    // column pairs per wave: pair 8 j + w holds columns 16 j + 2 w, 16 j + 2 w + 1
 constexpr int kLdltLs = 129;     // column stride of the L store (doubles)
-constexpr int kLdltRing = 8;     // t_k slots (>= 5 needed)
+constexpr int kLdltRing = 8;     // published pairs in flight
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
     const long long b = __double_as_longlong(v);
@@ -523,12 +557,12 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// t_k(r) of one ring slot is stored at [(r & 3) * 32 + (r >> 2)]: wave w reads its 32 columns' values contiguously
-__device__ __forceinline__ int tq_index(int r) { return ((r & 3) << 5) + (r >> 2); }
+// t_c(r) of a ring slot's term h at [h][tq_index(r)] (row order: each wave loads them lane-distributed)
+__device__ __forceinline__ int tq_index(int r) { return r; }
 
 #ifdef YAVO_LM_PROFILE
 // profiling builds: shader cycles of lane 0 of each wave in the phases of the LDLT, summed over launches
-__device__ unsigned long long g_ldlt_prof[4][8];
+__device__ unsigned long long g_ldlt_prof[kLdltWaves][8];
 #define LDP_DECL unsigned long long ldp_t = __builtin_readcyclecounter(), ldp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define LDP_MARK(q) do { const unsigned long long t_ = __builtin_readcyclecounter(); ldp_acc[q] += t_ - ldp_t; ldp_t = t_; } while (0)
 #define LDP_STORE() do { if (l == 0) for (int q_ = 0; q_ < 8; ++q_) atomicAdd(&g_ldlt_prof[w][q_], ldp_acc[q_]); } while (0)
@@ -538,58 +572,73 @@ __device__ unsigned long long g_ldlt_prof[4][8];
 #define LDP_STORE() do {} while (0)
 #endif
 
-// step k's update of slot J (its column 4 J + w), and, when that column is k + 1, its finalisation and publication
-#define LDLT_UPD(J)                                                                            \
-    do {                                                                                       \
-        if ((J) < kLdltSlots / 2) Al[(J) < kLdltSlots / 2 ? (J) : 0] -= lk0 * tv[J];           \
-        Ah[J] -= lk1 * tv[J];                                                                  \
-    } while (0)
-#define LDLT_FIN(J)                                                                            \
-    case J: {                                                                                  \
-        /* read-only on the slot's registers (the bulk update below writes them): no copies */ \
-        const double dk = dkn - readlane_f64((J) < kLdltSlots / 2 ? dot0 : dot1, kn & 63);     \
-        const bool valid = fabs(dk) > 0;                                                       \
-        if ((J) < kLdltSlots / 2) {                                                            \
-            const double a_ = Al[(J) < kLdltSlots / 2 ? (J) : 0] - lk0 * tkn;                  \
-            const double L0 = valid ? a_ / dk : a_;                                            \
-            Lcn[r0] = L0;                                                                      \
-            tqn[tq0] = dk * L0;                                                                \
-        }                                                                                      \
-        const double b_ = Ah[J] - lk1 * tkn;                                                   \
-        const double L1 = valid ? b_ / dk : b_;                                                \
-        Lcn[r1] = L1;                                                                          \
-        tqn[tq1] = dk * L1;                                                                    \
-        if (l == 0) Dv[kn] = dk;                                                               \
-        __hip_atomic_store(&flag[kn & (kLdltRing - 1)], kn, __ATOMIC_RELEASE,                  \
-                           __HIP_MEMORY_SCOPE_WORKGROUP);                                      \
+// pair q + 1 = 8 J + w of this wave: both columns finalised and published (read-only on the registers)
+#define LDLT_FIN(J)                                                                                            \
+    case J: {                                                                                                  \
+        constexpr int jl_ = (J) < kLdltPairs / 2 ? (J) : 0;                                                    \
+        /* column an: terms ca, cb, then D(an) and the division */                                             \
+        double aa0 = 0.0;                                                                                      \
+        if ((J) < kLdltPairs / 2) aa0 = (Al[jl_][0] - lka0 * ta_a) - lkb0 * tb_a;                              \
+        const double aa1 = (Ah[J][0] - lka1 * ta_a) - lkb1 * tb_a;                                             \
+        const bool va = fabs(da) > 0;                                                                          \
+        const double La0 = (J) < kLdltPairs / 2 ? (va ? aa0 / da : aa0) : 0.0;                                 \
+        const double La1 = va ? aa1 / da : aa1;                                                                \
+        const double ua0 = (J) < kLdltPairs / 2 ? da * La0 : 0.0, ua1 = da * La1;                              \
+        if ((J) < kLdltPairs / 2) {                                                                            \
+            Lc[an * kLdltLs + r0] = La0;                                                                       \
+            tqn[tq0] = ua0;                                                                                    \
+        }                                                                                                      \
+        Lc[an * kLdltLs + r1] = La1;                                                                           \
+        tqn[tq1] = ua1;                                                                                        \
+        if (l == 0) Dv[an] = da;                                                                               \
+        if (bn < n) {                                                                                          \
+            /* column bn: terms ca, cb, an (t_an(bn) from row bn's lane), D(bn) = S(bn, bn) - (dot + L t) */   \
+            const double ta_b = readlane_f64(bn < 64 ? ua0 : ua1, bn & 63);                                    \
+            const double db = dorb - readlane_f64(bn < 64 ? dot0 + La0 * ua0 : dot1 + La1 * ua1, bn & 63);   \
+            double ab0 = 0.0;                                                                                  \
+            if ((J) < kLdltPairs / 2) ab0 = ((Al[jl_][1] - lka0 * tc_b) - lkb0 * td_b) - La0 * ta_b;           \
+            const double ab1 = ((Ah[J][1] - lka1 * tc_b) - lkb1 * td_b) - La1 * ta_b;                          \
+            const bool vb = fabs(db) > 0;                                                                      \
+            const double Lb0 = (J) < kLdltPairs / 2 ? (vb ? ab0 / db : ab0) : 0.0;                             \
+            const double Lb1 = vb ? ab1 / db : ab1;                                                            \
+            if ((J) < kLdltPairs / 2) {                                                                        \
+                Lc[bn * kLdltLs + r0] = Lb0;                                                                   \
+                tqn[kLdltRegN + tq0] = db * Lb0;                                                               \
+            }                                                                                                  \
+            Lc[bn * kLdltLs + r1] = Lb1;                                                                       \
+            tqn[kLdltRegN + tq1] = db * Lb1;                                                                   \
+            if (l == 0) Dv[bn] = db;                                                                           \
+        }                                                                                                      \
+        __hip_atomic_store(&flag[qn & (kLdltRing - 1)], qn, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);   \
     } break;
 
-__global__ __launch_bounds__(256) void ba_ldlt_reg_kernel(BaParams P) {
+__global__ __launch_bounds__(64 * kLdltWaves) void ba_ldlt_reg_kernel(BaParams P) {
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    __shared__ double Lc[kLdltRegN * kLdltLs];      // S row-major (n x n) first, then L(r, c) at Lc[c * 129 + r]
-    __shared__ double tq[kLdltRing][kLdltRegN];     // t_k(r) = D(k) L(r, k) of column k in slot k % kLdltRing
-    __shared__ double Dv[kLdltRegN];                // D(k)
-    __shared__ double dor[kLdltRegN];               // the diagonal of P S P^T
-    __shared__ double dg[kLdltRegN];                // |diagonal|, permuted as the pivots are taken
-    __shared__ int perm[kLdltRegN];                 // position -> original index: (P S P^T)(i, j) = S(perm[i], perm[j])
-    __shared__ int flag[kLdltRing];                 // the column a slot holds (-1: none yet)
+    constexpr int NT = 64 * kLdltWaves;
+    __shared__ double Lc[kLdltRegN * kLdltLs];       // S row-major (n x n) first, then L(r, c) at Lc[c * 129 + r]
+    __shared__ double tq[kLdltRing][2][kLdltRegN];   // pair q's t_2q(.), t_2q+1(.) in slot q % kLdltRing
+    __shared__ double Dv[kLdltRegN];                 // D(k)
+    __shared__ double dor[kLdltRegN];                // the diagonal of P S P^T
+    __shared__ double dg[kLdltRegN];                 // |diagonal|, permuted as the pivots are taken
+    __shared__ int perm[kLdltRegN];                  // position -> original index: (P S P^T)(i, j) = S(perm[i], perm[j])
+    __shared__ int flag[kLdltRing];                  // the pair a slot holds (-1: none yet)
     __shared__ int s_slow;
     const int n = P.ns, t = threadIdx.x, l = t & 63;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int r0 = l, r1 = l + 64;
     LDP_DECL
     {
-        // S staged row-major, sixteen 16-B loads per thread in flight
+        // S staged row-major, eight 16-B loads per thread in flight
         const int nh = (n * n) >> 1;
         const double2* src = reinterpret_cast<const double2*>(P.S);
         double2* dst = reinterpret_cast<double2*>(Lc);
-        for (int e0 = t; e0 < nh; e0 += 16 * 256) {
-            double2 v[16];
+        for (int e0 = t; e0 < nh; e0 += 8 * NT) {
+            double2 v[8];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) v[u] = e0 + 256 * u < nh ? src[e0 + 256 * u] : make_double2(0.0, 0.0);
+            for (int u = 0; u < 8; ++u) v[u] = e0 + NT * u < nh ? src[e0 + NT * u] : make_double2(0.0, 0.0);
 #pragma unroll
-            for (int u = 0; u < 16; ++u)
-                if (e0 + 256 * u < nh) dst[e0 + 256 * u] = v[u];
+            for (int u = 0; u < 8; ++u)
+                if (e0 + NT * u < nh) dst[e0 + NT * u] = v[u];
         }
         if (((n * n) & 1) && t == 0) Lc[n * n - 1] = P.S[n * n - 1];
     }
@@ -672,19 +721,21 @@ __global__ __launch_bounds__(256) void ba_ldlt_reg_kernel(BaParams P) {
         if (t < n) perm[t] = t == 0 ? big0 : (t == big0 ? 0 : t);
         __syncthreads();
     }
-    // 2. P S P^T into registers: Al[j] = entry (r0, 4 j + w) for the columns below 64, Ah[j] = (r1, 4 j + w); only the
-    // strict lower triangle is read (the rest is never used)
-    double Al[kLdltSlots / 2], Ah[kLdltSlots];
+    // 2. P S P^T into registers: Al[j][h] = entry (r0, 16 j + 2 w + h) for the columns below 64, Ah[j][h] = (r1, ...);
+    // only the strict lower triangle is read (the rest is never used)
+    double Al[kLdltPairs / 2][2], Ah[kLdltPairs][2];
     const int tq0 = tq_index(r0), tq1 = tq_index(r1);
     {
         const int p0 = r0 < n ? perm[r0] : 0, p1 = r1 < n ? perm[r1] : 0;
 #pragma unroll
-        for (int j = 0; j < kLdltSlots; ++j) {
-            const int c = 4 * j + w;
-            const int pc = c < n ? perm[c] : 0;
-            if (j < kLdltSlots / 2) Al[j] = (r0 > c && r0 < n) ? Lc[p0 * n + pc] : 0.0;
-            Ah[j] = (r1 > c && r1 < n) ? Lc[p1 * n + pc] : 0.0;
-        }
+        for (int j = 0; j < kLdltPairs; ++j)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = 16 * j + 2 * w + h;
+                const int pc = c < n ? perm[c] : 0;
+                if (j < kLdltPairs / 2) Al[j < kLdltPairs / 2 ? j : 0][h] = (r0 > c && r0 < n) ? Lc[p0 * n + pc] : 0.0;
+                Ah[j][h] = (r1 > c && r1 < n) ? Lc[p1 * n + pc] : 0.0;
+            }
         if (t < n) dor[t] = Lc[perm[t] * n + perm[t]];
     }
     // the right-hand side, permuted (a zero first pivot: not permuted) -- wave 0 solves
@@ -698,13 +749,15 @@ __global__ __launch_bounds__(256) void ba_ldlt_reg_kernel(BaParams P) {
     if (brk) {
         // the solves read P S P^T as it stands
 #pragma unroll
-        for (int j = 0; j < kLdltSlots; ++j) {
-            const int c = 4 * j + w;
-            if (c < n) {
-                if (j < kLdltSlots / 2) Lc[c * kLdltLs + r0] = Al[j];
-                Lc[c * kLdltLs + r1] = Ah[j];
+        for (int j = 0; j < kLdltPairs; ++j)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = 16 * j + 2 * w + h;
+                if (c < n) {
+                    if (j < kLdltPairs / 2) Lc[c * kLdltLs + r0] = Al[j < kLdltPairs / 2 ? j : 0][h];
+                    Lc[c * kLdltLs + r1] = Ah[j][h];
+                }
             }
-        }
         if (t < n) Dv[t] = dor[t];
         __syncthreads();
         if (w == 0)
@@ -715,21 +768,35 @@ __global__ __launch_bounds__(256) void ba_ldlt_reg_kernel(BaParams P) {
                 if (r1 > j && r1 < n) v1 = v1 - a1 * vj;
             }
     } else {
-        // 3. column 0 (wave 0): D(0) = a00, nonzero here
+        // 3. pair 0 (wave 0): column 0 with D(0) = a00 (nonzero here); column 1 from term 0 alone, dot_1 = L(1, 0) t_0(1)
         if (w == 0) {
-            const double L0 = Al[0] / a00, L1 = Ah[0] / a00;
-            Lc[r0] = L0;
-            Lc[r1] = L1;
-            tq[0][tq0] = a00 * L0;
-            tq[0][tq1] = a00 * L1;
+            const double L00 = Al[0][0] / a00, L01 = Ah[0][0] / a00;
+            const double u00 = a00 * L00, u01 = a00 * L01;
+            Lc[r0] = L00;
+            Lc[r1] = L01;
+            tq[0][0][tq0] = u00;
+            tq[0][0][tq1] = u01;
             if (l == 0) Dv[0] = a00;
+            if (n > 1) {
+                const double t01 = readlane_f64(u00, 1);
+                const double d1 = dor[1] - readlane_f64(L00 * u00, 1);
+                const bool v1ok = fabs(d1) > 0;
+                const double b0 = Al[0][1] - L00 * t01, b1 = Ah[0][1] - L01 * t01;
+                const double L10 = v1ok ? b0 / d1 : b0, L11 = v1ok ? b1 / d1 : b1;
+                Lc[kLdltLs + r0] = L10;
+                Lc[kLdltLs + r1] = L11;
+                tq[0][1][tq0] = d1 * L10;
+                tq[0][1][tq1] = d1 * L11;
+                if (l == 0) Dv[1] = d1;
+            }
             __hip_atomic_store(&flag[0], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         double dot0 = 0.0, dot1 = 0.0;  // rows r0, r1: L(r, 0) t_0(r) + L(r, 1) t_1(r) + ... (term 0 assigns)
+        const int NP = (n + 1) >> 1;
         LDP_MARK(0);
-        for (int k = 0; k < n; ++k) {
-            const int s = k & (kLdltRing - 1);
-            for (int spin = 0; __hip_atomic_load(&flag[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != k;) {
+        for (int q = 0; q < NP; ++q) {
+            const int s = q & (kLdltRing - 1);
+            for (int spin = 0; __hip_atomic_load(&flag[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != q;) {
                 if (++spin > (1 << 24)) {  // never expected: a bounded wait, reported as a failed solve
                     err = 1;
                     break;
@@ -737,46 +804,75 @@ __global__ __launch_bounds__(256) void ba_ldlt_reg_kernel(BaParams P) {
             }
             if (err) break;
             LDP_MARK(1);
-            const int kn = k + 1;
-            // the loads the critical path needs first (this wave's rows of column k and their t values, D's source),
-            // then, after the column k + 1 hand-off, the t values of all 32 columns for the bulk update
-            const double dkn = dor[kn < n ? kn : 0];
-            const double lk0 = Lc[k * kLdltLs + r0], lk1 = Lc[k * kLdltLs + r1];
-            const double tk0 = tq[s][tq0], tk1 = tq[s][tq1];
-            dot0 = k == 0 ? lk0 * tk0 : dot0 + lk0 * tk0;
-            dot1 = k == 0 ? lk1 * tk1 : dot1 + lk1 * tk1;
+            const int ca = 2 * q, cb = 2 * q + 1;  // this step's terms (cb == n: absent, odd n)
+            const bool hb = cb < n;
+            const int qn = q + 1, an = 2 * qn, bn = 2 * qn + 1;
+            // the loads the critical path needs first: this wave's rows of columns ca, cb and their t values
+            const double lka0 = Lc[ca * kLdltLs + r0], lka1 = Lc[ca * kLdltLs + r1];
+            const double lkb0 = Lc[cb * kLdltLs + r0], lkb1 = Lc[cb * kLdltLs + r1];
+            const double tka0 = tq[s][0][tq0], tka1 = tq[s][0][tq1];
+            const double tkb0 = tq[s][1][tq0], tkb1 = tq[s][1][tq1];
+            const double dora = dor[an < n ? an : 0], dorb = dor[bn < n ? bn : 0];
+            dot0 = ca == 0 ? lka0 * tka0 : dot0 + lka0 * tka0;
+            dot1 = ca == 0 ? lka1 * tka1 : dot1 + lka1 * tka1;
+            if (hb) {
+                dot0 = dot0 + lkb0 * tkb0;
+                dot1 = dot1 + lkb1 * tkb1;
+            }
             LDP_MARK(2);
-            if (kn < n && (kn & 3) == w) {  // this wave holds column k + 1 (wave-uniform)
-                double* const Lcn = &Lc[kn * kLdltLs];
-                double* const tqn = &tq[kn & (kLdltRing - 1)][0];
-                const double tkn = readlane_f64(kn < 64 ? tk0 : tk1, kn & 63);  // t_k(k + 1): row k + 1's t value
-                switch (kn >> 2) {
+            if (qn < NP && (qn & (kLdltWaves - 1)) == w) {  // this wave holds pair q + 1 (wave-uniform; hb holds)
+                __builtin_amdgcn_s_setprio(3);
+                double* const tqn = &tq[qn & (kLdltRing - 1)][0][0];
+                const double ta_a = readlane_f64(an < 64 ? tka0 : tka1, an & 63);  // t_ca(an)
+                const double tb_a = readlane_f64(an < 64 ? tkb0 : tkb1, an & 63);  // t_cb(an)
+                const double tc_b = readlane_f64(bn < 64 ? tka0 : tka1, bn & 63);  // t_ca(bn)
+                const double td_b = readlane_f64(bn < 64 ? tkb0 : tkb1, bn & 63);  // t_cb(bn)
+                const double da = dora - readlane_f64(an < 64 ? dot0 : dot1, an & 63);
+                switch (qn >> 3) {
                     LDLT_FIN(0) LDLT_FIN(1) LDLT_FIN(2) LDLT_FIN(3) LDLT_FIN(4) LDLT_FIN(5) LDLT_FIN(6) LDLT_FIN(7)
-                    LDLT_FIN(8) LDLT_FIN(9) LDLT_FIN(10) LDLT_FIN(11) LDLT_FIN(12) LDLT_FIN(13) LDLT_FIN(14)
-                    LDLT_FIN(15) LDLT_FIN(16) LDLT_FIN(17) LDLT_FIN(18) LDLT_FIN(19) LDLT_FIN(20) LDLT_FIN(21)
-                    LDLT_FIN(22) LDLT_FIN(23) LDLT_FIN(24) LDLT_FIN(25) LDLT_FIN(26) LDLT_FIN(27) LDLT_FIN(28)
-                    LDLT_FIN(29) LDLT_FIN(30) LDLT_FIN(31)
                     default: break;
                 }
+                __builtin_amdgcn_s_setprio(0);
                 LDP_MARK(3);
             }
-            double tv[kLdltSlots];
-            {
-                const double2* tw = reinterpret_cast<const double2*>(&tq[s][w << 5]);  // t_k(4 j + w) at [j]
+            // terms ca, cb on this wave's live pairs (pair 8 j + w > q). The t values of a pair's columns c are
+            // v_readlane broadcasts of the lane-distributed t_ca(.), t_cb(.) loaded above (lane c & 63 of the half
+            // holding c): LDS broadcast loads of them cost eight waves' worth of LDS return bandwidth every step
 #pragma unroll
-                for (int q = 0; q < kLdltSlots / 2; ++q) {
-                    const double2 v = tw[q];
-                    tv[2 * q] = v.x;
-                    tv[2 * q + 1] = v.y;
+            for (int j = 0; j < kLdltPairs; ++j) {
+                if (8 * j + w > q) {
+                    const int cl = (16 * j + 2 * w) & 63;  // wave-uniform lane of this pair's first column
+                    const double tax = readlane_f64(j < kLdltPairs / 2 ? tka0 : tka1, cl);
+                    const double tay = readlane_f64(j < kLdltPairs / 2 ? tka0 : tka1, cl + 1);
+                    if (j < kLdltPairs / 2) {
+                        double (&a)[2] = Al[j < kLdltPairs / 2 ? j : 0];
+                        a[0] = a[0] - lka0 * tax;
+                        a[1] = a[1] - lka0 * tay;
+                    }
+                    Ah[j][0] = Ah[j][0] - lka1 * tax;
+                    Ah[j][1] = Ah[j][1] - lka1 * tay;
+                    if (hb) {
+                        const double tbx = readlane_f64(j < kLdltPairs / 2 ? tkb0 : tkb1, cl);
+                        const double tby = readlane_f64(j < kLdltPairs / 2 ? tkb0 : tkb1, cl + 1);
+                        if (j < kLdltPairs / 2) {
+                            double (&a)[2] = Al[j < kLdltPairs / 2 ? j : 0];
+                            a[0] = a[0] - lkb0 * tbx;
+                            a[1] = a[1] - lkb0 * tby;
+                        }
+                        Ah[j][0] = Ah[j][0] - lkb1 * tbx;
+                        Ah[j][1] = Ah[j][1] - lkb1 * tby;
+                    }
                 }
             }
-            // term k on every slot, branch-free (finalised columns' registers are dead)
-#pragma unroll
-            for (int j = 0; j < kLdltSlots; ++j) LDLT_UPD(j);
-            if (w == 0) {  // the forward solve's step k: rows below k
-                const double vk = readlane_f64(k < 64 ? v0 : v1, k & 63);
-                if (r0 > k && r0 < n) v0 = v0 - lk0 * vk;
-                if (r1 > k && r1 < n) v1 = v1 - lk1 * vk;
+            if (w == 0) {  // the forward solve's terms ca, cb: rows below each
+                const double va = readlane_f64(ca < 64 ? v0 : v1, ca & 63);
+                if (r0 > ca && r0 < n) v0 = v0 - lka0 * va;
+                if (r1 > ca && r1 < n) v1 = v1 - lka1 * va;
+                if (hb) {
+                    const double vb = readlane_f64(cb < 64 ? v0 : v1, cb & 63);
+                    if (r0 > cb && r0 < n) v0 = v0 - lkb0 * vb;
+                    if (r1 > cb && r1 < n) v1 = v1 - lkb1 * vb;
+                }
             }
             LDP_MARK(4);
         }
@@ -791,36 +887,42 @@ __global__ __launch_bounds__(256) void ba_ldlt_reg_kernel(BaParams P) {
     const double d0 = r0 < n ? Dv[r0] : 1.0, d1 = r1 < n ? Dv[r1] : 1.0;
     if (r0 < n) v0 = fabs(d0) > DBL_MIN ? v0 / d0 : 0.0;
     if (r1 < n) v1 = fabs(d1) > DBL_MIN ? v1 / d1 : 0.0;
-    // backward, eight columns a block: (a) the block's own rows take their terms one column after the other (the
-    // dependent chain: v(j) final, broadcast, the rows above j in the block), (b) the rows above the block take the
-    // block's eight terms, still in descending j -- every row's terms in the oracle's order
-    for (int j0 = n - 1; j0 >= 0; j0 -= 8) {
-        const int jb = j0 - 7 < 0 ? 0 : j0 - 7;
-        double a0[8], a1[8], vj[8];
+    // backward, v(i) -= L(j, i) v(j) for j descending: while j >= 64 every row below 64 takes the term (v(j) in the
+    // upper half), then only rows below j of the lower half; loads four columns ahead
+    {
+        int j = n - 1;
+        for (; j >= 67; j -= 4) {
+            double a0[4], a1[4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int j = j0 - u < 0 ? 0 : j0 - u;
-            a0[u] = Lc[r0 * kLdltLs + j];
-            a1[u] = Lc[r1 * kLdltLs + j];
-        }
+            for (int u = 0; u < 4; ++u) {
+                a0[u] = Lc[r0 * kLdltLs + j - u];
+                a1[u] = Lc[r1 * kLdltLs + j - u];
+            }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int j = j0 - u;
-            vj[u] = 0.0;
-            if (j >= jb) {
-                vj[u] = readlane_f64(j < 64 ? v0 : v1, j & 63);
-                const double n0 = v0 - a0[u] * vj[u], n1 = v1 - a1[u] * vj[u];
-                v0 = (r0 >= jb && r0 < j) ? n0 : v0;
-                v1 = (r1 >= jb && r1 < j) ? n1 : v1;
+            for (int u = 0; u < 4; ++u) {
+                const double vj = readlane_f64(v1, (j - u) & 63);
+                v0 = v0 - a0[u] * vj;
+                if (r1 < j - u) v1 = v1 - a1[u] * vj;
             }
         }
+        for (; j >= 64; --j) {
+            const double vj = readlane_f64(v1, j & 63);
+            v0 = v0 - Lc[r0 * kLdltLs + j] * vj;
+            if (r1 < j) v1 = v1 - Lc[r1 * kLdltLs + j] * vj;
+        }
+        for (; j >= 3; j -= 4) {
+            double a0[4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            if (j0 - u >= jb) {
-                const double n0 = v0 - a0[u] * vj[u], n1 = v1 - a1[u] * vj[u];
-                v0 = r0 < jb ? n0 : v0;
-                v1 = r1 < jb ? n1 : v1;
+            for (int u = 0; u < 4; ++u) a0[u] = Lc[r0 * kLdltLs + j - u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double vj = readlane_f64(v0, j - u);
+                if (r0 < j - u) v0 = v0 - a0[u] * vj;
             }
+        }
+        for (; j >= 0; --j) {
+            const double vj = readlane_f64(v0, j);
+            if (r0 < j) v0 = v0 - Lc[r0 * kLdltLs + j] * vj;
         }
     }
     if (r0 < n) P.xp[brk ? r0 : perm[r0]] = v0;
@@ -836,7 +938,7 @@ __global__ __launch_bounds__(256) void ba_ldlt_reg_kernel(BaParams P) {
     LDP_STORE();
 }
 #undef LDLT_FIN
-#undef LDLT_UPD
+
 
 // larger systems: the same steps on S in global memory
 __global__ __launch_bounds__(256) void ba_ldlt_kernel(BaParams P) {
@@ -981,14 +1083,22 @@ __global__ __launch_bounds__(256) void ba_ldlt_kernel(BaParams P) {
 #undef LL
 }
 
+// the position of item k of a tree256 sum over N items in its chain-major copy: chain k mod 256, then k / 256, so
+// that ba_chi2_kernel reads each chain's items contiguously (the item-major order gave every 128-B line to 16
+// workgroups: ~30 MB of line traffic for a 1.5 MB sum)
+__device__ __forceinline__ int chain_pos(int k, int N) { return (k & (kNT - 1)) * ((N + kNT - 1) / kNT) + k / kNT; }
+
 // The trial step in one launch (g2o's back-substitution, oplus and the trial chi2's per-edge terms): every workgroup
 // first forms all poses of the trial state in LDS (free: exp(x_p) T, fixed: T); one lane per landmark then runs
 // x_l = Dinv (b_l - sum_e H_pl^T x_p) sequentially over its edges, writes X + x_l into the trial state and |e|^2 of
 // each of its edges at the trial state. The trial state is the other buffer: a rejected trial leaves the current
 // one untouched (no backup / restore copies); an accepted one flips P.cur (ba_chi2_kernel's last workgroup).
-__global__ __launch_bounds__(256) void ba_step_kernel(BaParams P, BaMat3 K) {
+// It also writes the LM scale's items x (lambda x + b) (free poses' components, then the landmarks') chain-major.
+__global__ __launch_bounds__(256) void ba_step_kernel(BaParams P, BaMat3 K, double lambda) {
     extern __shared__ double sT[];  // [P][7]
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
+    if (P.lam) lambda = *P.lam;
+    const int ns = P.ns, N1 = ns + 3 * P.L;
     const int cur = ba_cur(P);
     const double* T0 = cur ? P.poses2 : P.poses;
     const double* X0 = cur ? P.X2 : P.X;
@@ -1012,6 +1122,11 @@ __global__ __launch_bounds__(256) void ba_step_kernel(BaParams P, BaMat3 K) {
             for (int i = 0; i < 7; ++i) T1[7 * p + i] = Tn[i];
         }
     }
+    if (blockIdx.x == 0)
+        for (int k = t; k < ns; k += kNT) {
+            const double x = P.xp[k];
+            P.sc1[chain_pos(k, N1)] = x * (lambda * x + P.bp[6 * P.nf + k]);
+        }
     __syncthreads();
     const int l = blockIdx.x * kNT + t;
     if (l >= P.L) return;
@@ -1021,7 +1136,8 @@ __global__ __launch_bounds__(256) void ba_step_kernel(BaParams P, BaMat3 K) {
         const int e = P.le[k], p = P.ep[e];
         if (p < P.nf) continue;
         const double* xpp = P.xp + 6 * (p - P.nf);
-        const double* h = P.Hpl + 18 * (int64_t)e;
+        double h[18];
+        hpl_load(P, e, h);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             double d = h[c] * xpp[0];
@@ -1036,6 +1152,7 @@ __global__ __launch_bounds__(256) void ba_step_kernel(BaParams P, BaMat3 K) {
     for (int c = 0; c < 3; ++c) {
         const double x = D[3 * c] * tv[0] + D[3 * c + 1] * tv[1] + D[3 * c + 2] * tv[2];
         P.xl[3 * l + c] = x;
+        P.sc1[chain_pos(ns + 3 * l + c, N1)] = x * (lambda * x + P.bl[3 * l + c]);
         Xn[c] = X0[3 * l + c] + x;
         X1[3 * l + c] = Xn[c];
     }
@@ -1043,7 +1160,7 @@ __global__ __launch_bounds__(256) void ba_step_kernel(BaParams P, BaMat3 K) {
         const int e = P.le[k];
         double r[2];
         ba_error(sT + 7 * P.ep[e], K.v, Xn, P.meas + 2 * e, r);
-        P.e2[e] = r[0] * r[0] + r[1] * r[1];
+        P.e2[chain_pos(e, P.E)] = r[0] * r[0] + r[1] * r[1];
     }
 }
 
@@ -1055,7 +1172,7 @@ __global__ __launch_bounds__(256) void ba_edge_chi2_kernel(BaParams P, BaMat3 K)
     const int cur = ba_cur(P);
     double r[2];
     ba_error((cur ? P.poses2 : P.poses) + 7 * P.ep[e], K.v, (cur ? P.X2 : P.X) + 3 * P.el[e], P.meas + 2 * e, r);
-    P.e2[e] = r[0] * r[0] + r[1] * r[1];
+    P.e2[chain_pos(e, P.E)] = r[0] * r[0] + r[1] * r[1];
 }
 
 // ---- device-driven LM control (the host loop of yv_ba_solve's host form, operation for operation) ----
@@ -1129,52 +1246,48 @@ __global__ void ba_ctl_resume_kernel(BaCtl* c) {
 
 // chi2 over the edges (sum 0) and, for a trial, the LM scale x.(lambda x + b) over the variables (free poses, then
 // landmarks; sum 1) in the oracle's tree256 order: chain t = 0..255 adds items t, t + 256, ... from 0.0, then the
-// halving tree. kChi2Groups workgroups per sum, each running 16 chains over items staged in LDS a block of rows at a
-// time; the last workgroup to finish forms both trees and then (device control) decides the trial or starts the
-// solve, or (host control) leaves chi2 / scale in scal[0] / scal[1].  mode 0: the solve's first chi2; 1: a trial.
-constexpr int kChi2Groups = 16;
-constexpr int kChi2Rows = 128;
-__global__ __launch_bounds__(256) void ba_chi2_kernel(BaParams P, double lambda, int mode) {
-    __shared__ double st[kChi2Rows * 17];
+// halving tree. One 64-lane workgroup per chain and sum (256 or 512 workgroups): its lanes load the chain's items (up
+// to 8 each) into LDS at once, lane 0 adds them in order, and publishes the chain's sum write-through; the last
+// workgroup to finish forms both trees and then (device control) decides the trial or starts the solve, or (host
+// control) leaves chi2 / scale in scal[0] / scal[1].  mode 0: the solve's first chi2; 1: a trial.
+constexpr int kChi2Lanes = 64;
+constexpr int kChi2MaxItems = 8 * kChi2Lanes;  // items per chain held at once (chains longer than this loop)
+__global__ __launch_bounds__(kChi2Lanes) void ba_chi2_kernel(BaParams P, double lambda, int mode) {
+    __shared__ double st[kChi2MaxItems];
     __shared__ double red[2][kNT];
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     if (P.lam) lambda = *P.lam;
     const int t = threadIdx.x;
-    const int sum = blockIdx.x / kChi2Groups, g = blockIdx.x - sum * kChi2Groups;
+    const int sum = blockIdx.x / kNT, c = blockIdx.x - sum * kNT;
     const int ns = P.ns;
     const int N = sum == 0 ? P.E : ns + 3 * P.L;
-    const double* bpf = P.bp + 6 * P.nf;
+    const int R = c < N ? (N - 1 - c) / kNT + 1 : 0;  // this chain's items: c + 256 r, r < R
+    // chain c's items, contiguous (chain_pos): |e|^2 per edge (ba_step_kernel / ba_edge_chi2_kernel) or the LM
+    // scale's x (lambda x + b) per variable (ba_step_kernel)
+    const double* src = (sum == 0 ? P.e2 : P.sc1) + (int64_t)c * ((N + kNT - 1) / kNT);
     double acc = 0.0;
-    for (int r0 = 0; r0 * kNT < N; r0 += kChi2Rows) {
-#pragma unroll 4
-        for (int i = t; i < kChi2Rows * 16; i += kNT) {
-            const int k = (r0 + (i >> 4)) * kNT + 16 * g + (i & 15);
-            double v = 0.0;
-            if (k < N) {
-                if (sum == 0) {
-                    v = P.e2[k];
-                } else {
-                    const double x = k < ns ? P.xp[k] : P.xl[k - ns];
-                    const double b = k < ns ? bpf[k] : P.bl[k - ns];
-                    v = x * (lambda * x + b);
-                }
-            }
-            st[(i >> 4) * 17 + (i & 15)] = v;
+    for (int r0 = 0; r0 < R; r0 += kChi2MaxItems) {
+        const int m = min(kChi2MaxItems, R - r0);
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = t + kChi2Lanes * u;
+            v[u] = 0.0;
+            if (i < m) v[u] = src[r0 + i];
         }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) st[t + kChi2Lanes * u] = v[u];
         __syncthreads();
-        if (t < 16) {
-            // this chain's rows in the block: item (r0 + i) * 256 + kc < N; eight LDS loads ahead of the adds
-            const int kc = 16 * g + t;
-            const int rows = kc < N ? min(kChi2Rows, (N - 1 - kc) / kNT + 1 - r0) : 0;
+        if (t == 0) {
             int i = 0;
-            if (rows >= 8) {
+            if (m >= 8) {
                 double d[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) d[u] = st[u * 17 + t];
-                for (; i + 16 <= rows; i += 8) {
+                for (int u = 0; u < 8; ++u) d[u] = st[u];
+                for (; i + 16 <= m; i += 8) {
                     double e[8];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) e[u] = st[(i + 8 + u) * 17 + t];
+                    for (int u = 0; u < 8; ++u) e[u] = st[i + 8 + u];
 #pragma unroll
                     for (int u = 0; u < 8; ++u) acc = acc + d[u];
 #pragma unroll
@@ -1184,19 +1297,22 @@ __global__ __launch_bounds__(256) void ba_chi2_kernel(BaParams P, double lambda,
                 for (int u = 0; u < 8; ++u) acc = acc + d[u];
                 i += 8;
             }
-            for (; i < rows; ++i) acc = acc + st[i * 17 + t];
+            for (; i < m; ++i) acc = acc + st[i];
         }
         __syncthreads();
     }
-    if (t < 16) P.part[sum * kNT + 16 * g + t] = acc;
-    if (!ba_last_block(P.ticket + 1)) return;
-    red[0][t] = P.part[t];
-    red[1][t] = mode ? P.part[kNT + t] : 0.0;
+    if (t == 0) st_agent(&P.part[sum * kNT + c], acc);
+    if (!ba_last_block_h(P.ticket + 1, P.ticket + 4 + kTicketGroups)) return;
+#pragma unroll
+    for (int u = 0; u < kNT / kChi2Lanes; ++u) {
+        red[0][t + kChi2Lanes * u] = ld_agent(&P.part[t + kChi2Lanes * u]);
+        red[1][t + kChi2Lanes * u] = mode ? ld_agent(&P.part[kNT + t + kChi2Lanes * u]) : 0.0;
+    }
     __syncthreads();
     for (int off = kNT / 2; off > 0; off >>= 1) {
-        if (t < off) {
-            red[0][t] = red[0][t] + red[0][t + off];
-            red[1][t] = red[1][t] + red[1][t + off];
+        for (int i = t; i < off; i += kChi2Lanes) {
+            red[0][i] = red[0][i] + red[0][i + off];
+            red[1][i] = red[1][i] + red[1][i + off];
         }
         __syncthreads();
     }
@@ -1228,13 +1344,13 @@ void launch_ba_ctl_resume(BaCtl* c, hipStream_t s) {
 
 void launch_ba_linearize(const BaParams& P, const BaMat3& K, int first, hipStream_t s) {
     if (P.E > 0) hipLaunchKernelGGL(ba::ba_linearize_kernel, dim3((P.E + 255) / 256), dim3(256), 0, s, P, K);
-    const int nb = std::max(1, P.np + (P.L + 255) / 256);
-    hipLaunchKernelGGL(ba::ba_reduce_kernel, dim3(nb), dim3(256), 0, s, P, first);
+    const int nb = std::max(1, P.np * ba::kWG + (P.L + ba::kWLanes - 1) / ba::kWLanes);
+    hipLaunchKernelGGL(ba::ba_reduce_kernel, dim3(nb), dim3(ba::kWLanes), 0, s, P, first);
 }
 
 void launch_ba_ldlt(const BaParams& P, hipStream_t s) {
     if (P.ns > 0 && P.ns <= ba::kLdltRegN)
-        hipLaunchKernelGGL(ba::ba_ldlt_reg_kernel, dim3(1), dim3(256), 0, s, P);
+        hipLaunchKernelGGL(ba::ba_ldlt_reg_kernel, dim3(1), dim3(64 * ba::kLdltWaves), 0, s, P);
     else if (P.ns > 0)
         hipLaunchKernelGGL(ba::ba_ldlt_kernel, dim3(1), dim3(256), sizeof(double) * 2 * P.ns, s, P);
 }
@@ -1243,16 +1359,17 @@ void launch_ba_trial(const BaParams& P, const BaMat3& K, double lambda, hipStrea
     const int nl = std::max(P.L, P.E);
     if (nl > 0) hipLaunchKernelGGL(ba::ba_landmark_trial_kernel, dim3((nl + 255) / 256), dim3(256), 0, s, P, lambda);
     const int nb = P.np * (P.np + 1) / 2;
-    if (nb > 0) hipLaunchKernelGGL(ba::ba_schur_kernel, dim3(nb + P.np), dim3(ba::kSchurThreads), 0, s, P, lambda);
+    if (nb > 0)
+        hipLaunchKernelGGL(ba::ba_schur_kernel, dim3((nb + P.np) * ba::kWG), dim3(ba::kWLanes), 0, s, P, lambda);
     launch_ba_ldlt(P, s);
     hipLaunchKernelGGL(ba::ba_step_kernel, dim3(std::max(1, (P.L + 255) / 256)), dim3(256),
-                       sizeof(double) * 7 * P.P, s, P, K);
-    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(2 * ba::kChi2Groups), dim3(256), 0, s, P, lambda, 1);
+                       sizeof(double) * 7 * P.P, s, P, K, lambda);
+    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(2 * ba::kNT), dim3(ba::kChi2Lanes), 0, s, P, lambda, 1);
 }
 
 void launch_ba_chi2(const BaParams& P, const BaMat3& K, hipStream_t s) {
     if (P.E > 0) hipLaunchKernelGGL(ba::ba_edge_chi2_kernel, dim3((P.E + 255) / 256), dim3(256), 0, s, P, K);
-    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(ba::kChi2Groups), dim3(256), 0, s, P, 0.0, 0);
+    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(ba::kNT), dim3(ba::kChi2Lanes), 0, s, P, 0.0, 0);
 }
 
 void launch_ba_finish(const BaParams& P, hipStream_t s) {
@@ -1278,7 +1395,8 @@ struct yv_ba {
             *d_le = nullptr, *d_cv_off = nullptr, *d_cv_e1 = nullptr, *d_cv_e2 = nullptr;
     double* d_meas = nullptr;
     int* d_cur = nullptr;          // the state the estimate is in (BaParams::cur)
-    unsigned* d_ticket = nullptr;  // last-workgroup counters
+    unsigned* d_ticket = nullptr;  // last-workgroup counters [kBaTickets]
+    int64_t schur_cap = 0;         // Schur tasks P.spart / P.sticket hold
     unsigned long long* d_maxdiag = nullptr;
     double* h_scal = nullptr;  // pinned [4]
     yavo::BaCtl* d_ctl = nullptr;  // the device-driven LM's control block
@@ -1290,6 +1408,9 @@ struct yv_ba {
 };
 
 namespace {
+
+// [0] reduce, [1] chi2 (the last-workgroup tops); [4, 68) the reduce's groups, [68, 132) chi2's
+constexpr int kBaTickets = 4 + 2 * yavo::ba::kTicketGroups;
 
 template <class T>
 int ba_alloc(yv_ba* b, T** p, size_t count) {
@@ -1307,6 +1428,31 @@ void ba_free_one(yv_ba* b, void* p) {
     if (!p) return;
     (void)hipFree(p);
     b->owned.erase(std::remove(b->owned.begin(), b->owned.end(), p), b->owned.end());
+}
+
+// the tree4096 class totals and per-sum counters of np free poses: P.spart / P.sticket for the Schur tasks (nb upper
+// blocks + np b_schur rows), P.rpart / P.rticket for the pose reduce; grown on demand
+int ba_ensure_schur(yv_ba* b, int np, hipStream_t st) {
+    const int64_t tasks = (int64_t)np * (np + 1) / 2 + np;
+    if (tasks <= b->schur_cap) return YV_OK;
+    if (hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
+    yavo::BaParams& Q = b->P;
+    ba_free_one(b, Q.spart);
+    ba_free_one(b, Q.sticket);
+    ba_free_one(b, Q.rpart);
+    ba_free_one(b, Q.rticket);
+    Q.spart = Q.rpart = nullptr;
+    Q.sticket = Q.rticket = nullptr;
+    b->schur_cap = 0;
+    if (ba_alloc(b, &Q.spart, (size_t)tasks * yavo::ba::kWG * 36) != YV_OK ||
+        ba_alloc(b, &Q.sticket, (size_t)tasks) != YV_OK ||
+        ba_alloc(b, &Q.rpart, (size_t)np * yavo::ba::kWG * 27) != YV_OK ||
+        ba_alloc(b, &Q.rticket, (size_t)np) != YV_OK ||
+        hipMemsetAsync(Q.sticket, 0, sizeof(unsigned) * tasks, st) != hipSuccess ||
+        hipMemsetAsync(Q.rticket, 0, sizeof(unsigned) * (np > 0 ? np : 1), st) != hipSuccess)
+        return YV_ERR_HIP;
+    b->schur_cap = tasks;
+    return YV_OK;
 }
 
 int ba_sync_scal(yv_ba* b, int n) {
@@ -1351,12 +1497,11 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
     rc |= ba_alloc(b, &Q.poses2, 7 * P);
     rc |= ba_alloc(b, &Q.X2, 3 * L);
     rc |= ba_alloc(b, &b->d_cur, 1);
-    rc |= ba_alloc(b, &b->d_ticket, 4);
+    rc |= ba_alloc(b, &b->d_ticket, kBaTickets);
     rc |= ba_alloc(b, &Q.part, 2 * 256);
     rc |= ba_alloc(b, &Q.err, 2 * E);
     rc |= ba_alloc(b, &Q.Jp, 12 * E);
     rc |= ba_alloc(b, &Q.Jl, 6 * E);
-    rc |= ba_alloc(b, &Q.Hpl, 18 * E);
     rc |= ba_alloc(b, &Q.W, 18 * E);
     rc |= ba_alloc(b, &Q.Hpp, 36 * P);
     rc |= ba_alloc(b, &Q.bp, 6 * P);
@@ -1369,14 +1514,15 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
     rc |= ba_alloc(b, &Q.xl, 3 * L);
     rc |= ba_alloc(b, &Q.tr, ns);
     rc |= ba_alloc(b, &Q.scal, 16);
-    rc |= ba_alloc(b, &Q.e2, E);
+    rc |= ba_alloc(b, &Q.e2, E + 256);        // chain-major: 256 x ceil(E / 256)
+    rc |= ba_alloc(b, &Q.sc1, ns + 3 * L + 256);
     rc |= ba_alloc(b, &b->d_maxdiag, 1);
     rc |= ba_alloc(b, &b->d_ctl, 1);
     if (rc == YV_OK && hipHostMalloc(reinterpret_cast<void**>(&b->h_scal), 4 * sizeof(double)) != hipSuccess)
         rc = YV_ERR_HIP;
     if (rc == YV_OK && hipHostMalloc(reinterpret_cast<void**>(&b->h_ctl), sizeof(yavo::BaCtl)) != hipSuccess)
         rc = YV_ERR_HIP;
-    if (rc == YV_OK && (hipMemsetAsync(b->d_ticket, 0, 4 * sizeof(unsigned), b->st) != hipSuccess ||
+    if (rc == YV_OK && (hipMemsetAsync(b->d_ticket, 0, kBaTickets * sizeof(unsigned), b->st) != hipSuccess ||
                         hipMemsetAsync(b->d_cur, 0, sizeof(int), b->st) != hipSuccess ||
                         hipStreamSynchronize(b->st) != hipSuccess))
         rc = YV_ERR_HIP;
@@ -1487,6 +1633,7 @@ extern "C" int yv_ba_set_problem(yv_ba* b, int n_poses, int n_fixed, int n_landm
     Q.nf = n_fixed;
     Q.np = P - n_fixed;
     Q.ns = 6 * Q.np;
+    if (ba_ensure_schur(b, Q.np, b->st) != YV_OK) return YV_ERR_HIP;
     Q.L = L;
     Q.E = E;
     Q.ep = b->d_ep;
@@ -1655,7 +1802,9 @@ extern "C" int yv_ba_solve(yv_ba* b, double* poses, double* landmarks, int max_i
 extern "C" int yv_ba_debug_read(yv_ba* b, int which, double* dst, int64_t count) {
     if (!b || !b->ready || !dst || count < 0) return YV_ERR_INVALID;
     const yavo::BaParams& Q = b->P;
-    double* const bufs[] = {Q.err, Q.Jp, Q.Jl, Q.Hpl, Q.W, Q.Hpp, Q.bp, Q.Hll, Q.bl, Q.Dinv, Q.S, Q.bs, Q.xp, Q.xl,
+    // which = 3 (H_pl) is no longer stored (formed from Jp / Jl where it is read): YV_ERR_INVALID
+    if (which == 3) return YV_ERR_INVALID;
+    double* const bufs[] = {Q.err, Q.Jp, Q.Jl, nullptr, Q.W, Q.Hpp, Q.bp, Q.Hll, Q.bl, Q.Dinv, Q.S, Q.bs, Q.xp, Q.xl,
                             Q.poses, Q.X, Q.scal};
     const int64_t sizes[] = {2LL * Q.E, 12LL * Q.E, 6LL * Q.E, 18LL * Q.E, 18LL * Q.E, 36LL * Q.P, 6LL * Q.P,
                              9LL * Q.L, 3LL * Q.L, 9LL * Q.L, (int64_t)Q.ns * Q.ns, Q.ns, Q.ns, 3LL * Q.L,
@@ -1669,9 +1818,9 @@ extern "C" int yv_ba_debug_read(yv_ba* b, int which, double* dst, int64_t count)
 
 
 #ifdef YAVO_LM_PROFILE
-// profiling builds only (lib/libyavo_prof.so): LDLT phase cycles per wave [4][8], summed since the last call (reset)
+// profiling builds only (lib/libyavo_prof.so): LDLT phase cycles per wave [8][8], summed since the last call (reset)
 extern "C" int yv_debug_ldlt_prof(unsigned long long* out) {
-    unsigned long long z[4 * 8] = {};
+    unsigned long long z[yavo::ba::kLdltWaves * 8] = {};
     if (hipDeviceSynchronize() != hipSuccess ||
         hipMemcpyFromSymbol(out, HIP_SYMBOL(yavo::ba::g_ldlt_prof), sizeof z) != hipSuccess ||
         hipMemcpyToSymbol(HIP_SYMBOL(yavo::ba::g_ldlt_prof), z, sizeof z) != hipSuccess)
@@ -2116,6 +2265,7 @@ extern "C" int yv_ba_window_solve(yv_ba_window* w, int64_t first, int n, int n_f
     Q.nf = n_fixed;
     Q.np = n - n_fixed;
     Q.ns = 6 * Q.np;
+    if (ba_ensure_schur(b, Q.np, st) != YV_OK) return YV_ERR_HIP;
     Q.L = L;
     Q.E = E;
     Q.ep = b->d_ep;

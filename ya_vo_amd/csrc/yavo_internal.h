@@ -201,7 +201,6 @@ struct BaParams {
     double* err = nullptr;            // [E][2]
     double* Jp = nullptr;             // [E][12]
     double* Jl = nullptr;             // [E][6]
-    double* Hpl = nullptr;            // [E][18]
     double* W = nullptr;              // [E][18]
     double* Hpp = nullptr;            // [P][36]
     double* bp = nullptr;             // [P][6]
@@ -214,7 +213,7 @@ struct BaParams {
     double* xl = nullptr;             // [L][3]
     int32_t* tr = nullptr;            // [ns] LDLT transpositions
     double* scal = nullptr;           // [4]: chi2, scale, LDLT ok
-    double* e2 = nullptr;             // [E] squared error per edge
+    double* e2 = nullptr;             // [E] squared error per edge, chain-major (ba_step_kernel's chain_pos)
     // device-driven LM (yv_ba_solve): a kernel returns at once when *gate != 0 (its phase is skipped), and the trial
     // kernels read lambda from *lam; both nullptr under host control
     const int* gate = nullptr;
@@ -227,8 +226,13 @@ struct BaParams {
     struct BaCtl* ctl = nullptr;        // device control block (nullptr: host control)
     double* log = nullptr;             // [max_iters + 1] chi2 per iteration (device control)
     unsigned long long* maxdiag = nullptr;
-    unsigned* ticket = nullptr;        // [4] last-workgroup counters (0 between launches)
+    unsigned* ticket = nullptr;        // [kBaTickets] last-workgroup counters (0 between launches)
     double* part = nullptr;            // [2][256] chi2 / scale chains
+    double* sc1 = nullptr;             // the LM scale's items, chain-major (ba_step_kernel -> ba_chi2_kernel)
+    double* spart = nullptr;           // [Schur task][kWG][36] tree4096 class totals of the Schur workgroups
+    unsigned* sticket = nullptr;       // [Schur task] last-workgroup counters (0 between launches)
+    double* rpart = nullptr;           // [free pose][kWG][27] class totals of the H_pp / b_p reduce
+    unsigned* rticket = nullptr;       // [free pose] last-workgroup counters
 };
 // The device-side Levenberg-Marquardt control of one solve (g2o OptimizationAlgorithmLevenberg::solve, the
 // host loop's arithmetic): written by the last workgroups of ba_reduce_kernel / ba_chi2_kernel, read by the gates.

@@ -254,7 +254,8 @@ private:
 // _3DHandler::getFRANSAC(filterMatches, F, 400, 0.1) (src/3DHandler.cc:145-195): 400 hypotheses of 8 indices drawn
 // uniformly from [0, n) with replacement.  The reference's F is never used after the call (:222, :562), and neither is
 // the count: with a side lane (the pipelined loop) the call is handed to it with its samples (drawn here, in loop
-// order) and its count lands in the frame's event later (resolvePendingF); F stays zero.
+// order) and its count lands in the frame's event later (resolvePendingF: finished calls are folded in at the next
+// getFRANSAC, the rest at the end of the run); F stays zero.
 int LoopHandler::getFRANSAC(const std::vector<Matches>& m, double F[9]) {
     const int n = (int)m.size();
     for (int i = 0; i < 9; ++i) F[i] = 0;
@@ -264,6 +265,8 @@ int LoopHandler::getFRANSAC(const std::vector<Matches>& m, double F[9]) {
     std::uniform_int_distribution<int> dist(0, n - 1);
     for (auto& s : samples) s = dist(ransac_rng_);
     if (side_) {
+        resolvePendingF(false);
+        if (gpu_status_ != YV_OK) return 0;
         auto task = std::make_shared<std::packaged_task<FResult(Device&)>>(
             [m, samples = std::move(samples), n, iters](Device& d) {
                 FResult r;
@@ -914,19 +917,28 @@ void LoopHandler::runVOPipelined(int max_frames) {
     dropLKAhead(lk_cur_);
     side_ = nullptr;
     side_lane_.reset();  // runs what is still queued
-    resolvePendingF();
+    resolvePendingF(true);
     t_features += worker_features;
     t_read += worker_read;  // in the pipelined loop: the worker waiting for the next decoded frame
 }
 
-void LoopHandler::resolvePendingF() {
-    for (auto& p : pending_f_) {
+// wait = false: only the side-lane calls that have finished (polled at every getFRANSAC, so a failing side lane stops
+// tracking at the next reinit frame as a failure on the tracking context does); wait = true: all of them (end of run)
+void LoopHandler::resolvePendingF(bool wait) {
+    size_t keep = 0;
+    for (size_t i = 0; i < pending_f_.size(); ++i) {
+        auto& p = pending_f_[i];
+        if (!wait && p.second.wait_for(std::chrono::seconds(0)) != std::future_status::ready) {
+            if (keep != i) pending_f_[keep] = std::move(p);
+            ++keep;
+            continue;
+        }
         const FResult r = p.second.get();
         prim_.f_ransac += r.seconds;  // on the side lane, beside the tracking thread
         if (!gpu(r.status, "getFRANSAC (side lane)")) continue;
         if (p.first < events_.size()) events_[p.first].f_inliers = r.inliers;
     }
-    pending_f_.clear();
+    pending_f_.resize(keep);
 }
 
 }  // namespace yavo_fe

@@ -183,7 +183,7 @@ private:
     std::unique_ptr<Device> worker_dev_;
     std::unique_ptr<SideLane> side_lane_;
     std::vector<std::pair<size_t, std::future<FResult>>> pending_f_;
-    void resolvePendingF();
+    void resolvePendingF(bool wait);
     // pipelined loop: frame k + 1's pyramidal LK runs on the side lane during frame k's pose LM, over every frame-k
     // feature holding a map point at that moment (a superset of what trackLastFrame(k + 1) tracks: the LM only drops
     // map points, world2Camera only drops points).  LK tracks each point on its own, so the rows trackLastFrame(k + 1)
