@@ -196,6 +196,14 @@ int yv_ba_window_add_block(yv_ba_window* w, const void* d_block, int64_t first_f
  * *solved = 0 when there is nothing to solve (n <= n_fixed or no landmark): the records stay, the anchor is set. */
 int yv_ba_window_solve(yv_ba_window* w, int64_t first, int n, int n_fixed, const double K[9], int max_iters,
                        double* d_anchor, double* chi2_log, int* iters, int* solved);
+/* yv_ba_window_solve in two halves, so the host can enqueue other work (the next chunk's front end on the context
+ * stream) while the solve runs: _begin builds the graph and enqueues every LM iteration on the yv_ba's stream and
+ * returns; _end waits, resumes a suspended trial loop if needed, writes the records back and returns the log.
+ * Between the two, the window's add_block / read / trajectory and a second _begin return YV_ERR_INVALID, and the
+ * yv_ba must not be used by anything else. */
+int yv_ba_window_solve_begin(yv_ba_window* w, int64_t first, int n, int n_fixed, const double K[9], int max_iters,
+                             double* d_anchor);
+int yv_ba_window_solve_end(yv_ba_window* w, double* chi2_log, int* iters, int* solved);
 /* one frame's record (host, blocking): T_wc[7], *n landmarks, up to cap of edge ids / X [3] / uv_own [2] /
  * uv_prev [2] (any may be NULL) */
 int yv_ba_window_read(yv_ba_window* w, int64_t frame, double* T_wc, int* n, int32_t* edge, double* X, double* uv_own,

@@ -14,6 +14,7 @@ from ya_vo_amd import scene  # noqa: E402
 import oracle_bind  # noqa: E402
 
 NAMES = ["err", "Jp", "Jl", "Hpl", "W", "Hpp", "bp", "Hll", "bl", "Dinv", "S", "bs", "xp", "xl", "poses", "X"]
+NOT_STORED = {"Hpl", "W", "Dinv"}  # formed where they are read since round 5 (yv_ba_debug_read refuses them)
 
 
 def main():
@@ -36,7 +37,10 @@ def main():
         gbuf = []
         for k, n in enumerate(sizes):
             a = np.zeros(n)
-            assert ctx.lib.yv_ba_debug_read(ba.handle, k, a.ctypes.data, n) == 0
+            if NAMES[k] in NOT_STORED:
+                a = None
+            else:
+                assert ctx.lib.yv_ba_debug_read(ba.handle, k, a.ctypes.data, n) == 0
             gbuf.append(a)
         obuf = [np.zeros(n) for n in sizes]
         for k in range(16):
@@ -47,6 +51,8 @@ def main():
         print(f"iteration {it}: log gpu {log.tolist()} oracle {olog.tolist()}")
         for k, name in enumerate(NAMES):
             g, o = gbuf[k], obuf[k]
+            if g is None:
+                continue
             if name in ("Hpp", "bp"):  # fixed poses are not assembled on the GPU
                 m = 36 if name == "Hpp" else 6
                 g, o = g[nf * m:], o[nf * m:]

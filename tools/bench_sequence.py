@@ -25,7 +25,7 @@ T_RIGHT = np.array([0, 0, 0, 1, 0, -0.54, 0], np.float64)
 
 
 def measure(frames=200, chunk=20, n_fixed=2, ba_iters=10, repeats=3, cpu_threads=16, cpu=True, kitti="",
-            host_window=False, ctx=None):
+            host_window=False, ctx=None, ba_priority=0):
     """Run the configs[2] front end `repeats` times on frames resident in HBM (after one warm-up run) and return the
     result dict of the best run; cpu: also run tests/sequence_chain.py (the same loop over the CPU oracle) on the same
     frames and compare the trajectories (after the timed runs)."""
@@ -63,7 +63,7 @@ def measure(frames=200, chunk=20, n_fixed=2, ba_iters=10, repeats=3, cpu_threads
 
     def run():
         fe = SequenceFrontend(ctx, chunk, K, t_right, n_fixed=n_fixed, ba_iters=ba_iters, H=H, W=W,
-                              device_window=not host_window)
+                              device_window=not host_window, ba_priority=ba_priority)
         sec = {}
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -138,11 +138,12 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--host-window", action="store_true",
                     help="assemble the BA window on the host (the round-2 path) instead of on the device")
+    ap.add_argument("--ba-priority", type=int, default=0, help="the BA stream's priority (-1 high, 0 default)")
     args = ap.parse_args()
     from ya_vo_amd import io as yio
     from ya_vo_amd.sequence import se3_inverse
     out = measure(args.frames, args.chunk, args.n_fixed, args.ba_iters, args.repeats, args.cpu_threads,
-                  not args.no_cpu, args.kitti, args.host_window)
+                  not args.no_cpu, args.kitti, args.host_window, ba_priority=args.ba_priority)
     traj = out.pop("_trajectory")
     if args.out:
         yio.write_kitti_poses(os.path.splitext(args.out)[0] + "_poses.txt", np.stack([se3_inverse(T) for T in traj]))

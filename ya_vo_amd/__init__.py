@@ -133,6 +133,8 @@ GEOM_SIGNATURES = {
     "yv_ba_window_destroy": (None, [_P]),
     "yv_ba_window_add_block": (_I, [_P, _P, ctypes.c_int64, _I, _P, _P, _P, _I, _P]),
     "yv_ba_window_solve": (_I, [_P, ctypes.c_int64, _I, _I, _P, _I, _P, _P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "yv_ba_window_solve_begin": (_I, [_P, ctypes.c_int64, _I, _I, _P, _I, _P]),
+    "yv_ba_window_solve_end": (_I, [_P, _P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "yv_ba_window_read": (_I, [_P, ctypes.c_int64, _P, ctypes.POINTER(_I), _P, _P, _P, _P, _I]),
     "yv_ba_window_trajectory": (_I, [_P, ctypes.c_int64, _I, _P]),
     "yv_lm_sum_mode": (_I, []),
@@ -726,6 +728,21 @@ class BaWindow:
         _check(self.lib.yv_ba_window_solve(self.handle, first, n, n_fixed, _ptr(K), max_iters,
                                            ctypes.c_void_p(d_anchor) if d_anchor else None, _ptr(log),
                                            ctypes.byref(it), ctypes.byref(ok)), "yv_ba_window_solve")
+        return bool(ok.value), log[: it.value + 1], it.value
+
+    def solve_begin(self, first: int, n: int, n_fixed: int, K, max_iters: int, d_anchor: int = 0) -> None:
+        """Enqueue the solve (yv_ba_window_solve_begin) and return; solve_end collects it."""
+        self._iters = max_iters
+        _check(self.lib.yv_ba_window_solve_begin(self.handle, first, n, n_fixed, _ptr(_f64(K, (9,))), max_iters,
+                                                 ctypes.c_void_p(d_anchor) if d_anchor else None),
+               "yv_ba_window_solve_begin")
+
+    def solve_end(self):
+        """-> (solved, chi2 log [iters + 1], iterations run) of the solve solve_begin enqueued"""
+        log = np.zeros(self._iters + 1)
+        it, ok = ctypes.c_int(0), ctypes.c_int(0)
+        _check(self.lib.yv_ba_window_solve_end(self.handle, _ptr(log), ctypes.byref(it), ctypes.byref(ok)),
+               "yv_ba_window_solve_end")
         return bool(ok.value), log[: it.value + 1], it.value
 
     def read(self, frame: int):

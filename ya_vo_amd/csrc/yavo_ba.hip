@@ -3,22 +3,24 @@
 // extended to pose-landmark edges, restated like oracle/yavo_oracle_ba.c, expression for expression, in its
 // summation orders (built with -ffp-contract=off):
 //
-//   ba_linearize_kernel   one lane per edge: e, J_pose (the reference's linearizeOplus), J_point = J_pose[:, :3] R,
-//                         H_pl = J_pose^T J_point (6 x 3)
-//   ba_pose_reduce_kernel one 256-thread workgroup per free pose: H_pp (21) and b_p (6) over the pose's edges,
-//                         strided partials then a halving tree (tree256)
-//   ba_landmark_*_kernel  one lane per landmark: H_ll, b_l (sequential over its edges); per trial the damped 3 x 3
-//                         inverse per landmark and W = H_pl Dinv per edge
-//   ba_schur_kernel       one 64-lane workgroup per upper Schur block (p1 <= p2), a lane per entry, and one per pose
-//                         for b_schur: sequential over the landmarks the two poses share, pairs staged in LDS
+//   ba_linearize_kernel   one lane per edge: e, J_pose (the reference's linearizeOplus), J_point = J_pose[:, :3] R
+//                         (H_pl = J_pose^T J_point is formed from these where it is read)
+//   ba_reduce_kernel      H_pp (21) + b_p (6) per free pose in tree4096 order (32 workgroups per pose), and one lane
+//                         per landmark for H_ll, b_l (sequential over its edges); its last workgroup starts the
+//                         iteration's trial loop (device control)
+//   ba_schur_kernel       per trial: the reduced pose system S = H_pp + lambda I - sum W H_pl^T and b_schur in tree4096
+//                         order (32 workgroups per upper 6 x 6 block or b_schur row), W = H_pl (H_ll + lambda I)^-1
+//                         formed per co-visible pair
 //   ba_ldlt_reg_kernel    one workgroup: Eigen's LDLT (diagonal pivoting) on the reduced pose system, the matrix in
-//                         registers, columns handed between waves through LDS (n <= 128; ba_ldlt_kernel on global
-//                         memory above), then the solve
-//   ba_backsub_kernel     one lane per landmark: x_l = Dinv (b_l - sum_e H_pl^T x_p)
-//   ba_update_kernel      T <- exp(x_p) T per free pose, X <- X + x_l per landmark
-//   ba_edge_chi2_kernel   one lane per edge: |e|^2 at the current estimate
-//   ba_chi2_kernel        one workgroup: chi2 over all edges and the LM scale x.(lambda x + b), tree256
-// The LM control (lambda, rho, accept / reject, restore) runs on the host in the oracle's arithmetic.
+//                         registers, four-column groups handed between waves through LDS (n <= 128; ba_ldlt_kernel on
+//                         global memory above), then the solve
+//   ba_step_kernel        the trial state: T <- exp(x_p) T, x_l = Dinv (b_l - sum_e H_pl^T x_p), X <- X + x_l, the
+//                         trial's |e|^2 per edge and the LM scale's items (into the other state buffer)
+//   ba_edge_chi2_kernel   one lane per edge: |e|^2 at the current estimate (the solve's first chi2)
+//   ba_chi2_kernel        chi2 and the LM scale x.(lambda x + b) in tree256 order; its last workgroup decides the
+//                         trial (device control) or leaves both for the host
+// The LM control (lambda, rho, accept / reject) runs on the device by default (ba_ctl_*), in the host loop's
+// arithmetic; yv_ba_set_control(b, 0) runs it on the host.
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <math.h>
@@ -358,61 +360,36 @@ __device__ __forceinline__ void inv3(const double* a, double* o) {
     o[6] = c02 * id; o[7] = (a[1] * a[6] - a[0] * a[7]) * id; o[8] = (a[0] * a[4] - a[1] * a[3]) * id;
 }
 
-// lanes [0, L): D^-1 of landmark l (H_ll + lambda I)^-1; lanes [0, E): W_e = H_pl(e) D^-1 of its landmark, with that
-// inverse recomputed in the lane (the same expressions, so the same bits as the landmark lane's)
-__global__ __launch_bounds__(256) void ba_landmark_trial_kernel(BaParams P, double lambda) {
-    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    if (P.lam) lambda = *P.lam;
-    const int id = blockIdx.x * blockDim.x + threadIdx.x;
-    if (id < P.L) {
-        double d[9], Di[9];
+// (H_ll + lambda I)^-1 of landmark l, the oracle's expressions (its Dinv)
+__device__ __forceinline__ void landmark_dinv(const BaParams& P, int l, double lambda, double* Di) {
+    double d[9];
 #pragma unroll
-        for (int i = 0; i < 9; ++i) d[i] = P.Hll[9 * id + i];
+    for (int i = 0; i < 9; ++i) d[i] = P.Hll[9 * (int64_t)l + i];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) d[4 * a] = d[4 * a] + lambda;
-        inv3(d, Di);
-#pragma unroll
-        for (int i = 0; i < 9; ++i) P.Dinv[9 * id + i] = Di[i];
-    }
-    if (id < P.E) {
-        const int l = P.el[id];
-        double d[9], Di[9], h[18];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) d[i] = P.Hll[9 * l + i];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) d[4 * a] = d[4 * a] + lambda;
-        inv3(d, Di);
-        hpl_load(P, id, h);
-        double w[18];
-#pragma unroll
-        for (int a = 0; a < 6; ++a)
-#pragma unroll
-            for (int c = 0; c < 3; ++c)
-                w[3 * a + c] = h[3 * a + 0] * Di[0 * 3 + c] + h[3 * a + 1] * Di[1 * 3 + c] + h[3 * a + 2] * Di[2 * 3 + c];
-        double2* w2 = reinterpret_cast<double2*>(P.W + 18 * (int64_t)id);
-#pragma unroll
-        for (int i = 0; i < 9; ++i) w2[i] = make_double2(w[2 * i], w[2 * i + 1]);
-    }
+    for (int a = 0; a < 3; ++a) d[4 * a] = d[4 * a] + lambda;
+    inv3(d, Di);
 }
 
+// W_e = H_pl(e) Dinv (6 x 3), the oracle's expression
+__device__ __forceinline__ void w_block(const double* h, const double* Di, double* w) {
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            w[3 * a + c] = h[3 * a + 0] * Di[0 * 3 + c] + h[3 * a + 1] * Di[1 * 3 + c] + h[3 * a + 2] * Di[2 * 3 + c];
+}
+
+
 // The Schur complement in the oracle's tree4096 order. Task = an upper block (p1 <= p2) of the free poses, or one
-// pose's b_schur; kWG workgroups per task (see wide_local_tree). A lane's items (pair k = leaf + 4096 m) are loaded as
-// W_e1 (9 16-B loads) and H_pl(e2) (formed from its Jacobians: 9 16-B loads), the next one's already in flight; a configs[2]
-// window has at most one per lane, so a block's ~3,700 pairs are read by 32 CUs with every load in flight at once.
+// pose's b_schur; kWG workgroups per task (see wide_local_tree). A lane's items (pair k = leaf + 4096 m) form what the
+// oracle's trial step stores: Dinv of the pair's landmark from H_ll + lambda I, H_pl of both edges from their
+// Jacobians, W_e1 = H_pl(e1) Dinv -- the same expressions, so the same bits, with no W / Dinv round trip through
+// HBM and no trial kernel (216 B read per diagonal pair, 360 B per off-diagonal one). A configs[2] window has at most
+// one item per lane, so a block's ~3,700 pairs are spread over 32 CUs with every load in flight at once.
 // grid: (nb + np) kWG workgroups; task = blockIdx / kWG, g = blockIdx % kWG.
 //  tasks [0, nb): S(a, b) = base - tree4096 over the co-visible pairs k of (W_e1(k)[a] . H_pl(e2(k))[b]); on a
 //    diagonal block only a >= b is written, to both mirrored entries (the oracle's loop leaves that value)
 //  tasks [nb, nb + np): b_schur(a) = b_p[a] - tree4096 over the pose's edges of W_e[a] . b_l(e)
-__device__ __forceinline__ void load18(const double* blk, double* r) {
-    const double2* v2 = reinterpret_cast<const double2*>(blk);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-        const double2 v = v2[i];
-        r[2 * i] = v.x;
-        r[2 * i + 1] = v.y;
-    }
-}
-
 __global__ __launch_bounds__(kWLanes) void ba_schur_kernel(BaParams P, double lambda) {
     __shared__ double red[36 * kWLanes];
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
@@ -445,32 +422,18 @@ __global__ __launch_bounds__(kWLanes) void ba_schur_kernel(BaParams P, double la
         double acc[36];
 #pragma unroll
         for (int i = 0; i < 36; ++i) acc[i] = 0.0;
-        int i = c0 + leaf;
-        double w[18], h[18];
-        if (i < c1) {
-            load18(P.W + 18 * (int64_t)P.cv_e1[i], w);
-            hpl_load(P, P.cv_e2[i], h);
-        }
-        while (i < c1) {
-            const int nx = i + kWLeaves;
-            double wn[18], hn[18];
-            if (nx < c1) {
-                load18(P.W + 18 * (int64_t)P.cv_e1[nx], wn);
-                hpl_load(P, P.cv_e2[nx], hn);
-            }
+        for (int i = c0 + leaf; i < c1; i += kWLeaves) {
+            const int e1 = P.cv_e1[i], e2 = P.cv_e2[i];
+            double Di[9], h[18], w[18];
+            landmark_dinv(P, P.el[e1], lambda, Di);
+            hpl_load(P, e1, h);
+            w_block(h, Di, w);  // W_e1 = H_pl(e1) Dinv: the trial kernel's product, formed here
+            if (e2 != e1) hpl_load(P, e2, h);
 #pragma unroll
             for (int a = 0; a < 6; ++a)
 #pragma unroll
                 for (int b = 0; b < 6; ++b)
                     acc[6 * a + b] = acc[6 * a + b] + (w[3 * a] * h[3 * b] + w[3 * a + 1] * h[3 * b + 1] + w[3 * a + 2] * h[3 * b + 2]);
-            i = nx;
-            if (i < c1) {
-#pragma unroll
-                for (int u = 0; u < 18; ++u) {
-                    w[u] = wn[u];
-                    h[u] = hn[u];
-                }
-            }
         }
 #pragma unroll
         for (int q = 0; q < 36; ++q) red[q * kWLanes + t] = acc[q];
@@ -493,10 +456,12 @@ __global__ __launch_bounds__(kWLanes) void ba_schur_kernel(BaParams P, double la
         const int k0 = P.pe_off[p], k1 = P.pe_off[p + 1];
         double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         for (int i = k0 + leaf; i < k1; i += kWLeaves) {
-            const int e = P.pe[i];
-            double w[18];
-            load18(P.W + 18 * (int64_t)e, w);
-            const double* gl = P.bl + 3 * P.el[e];
+            const int e = P.pe[i], l = P.el[e];
+            double Di[9], h[18], w[18];
+            landmark_dinv(P, l, lambda, Di);
+            hpl_load(P, e, h);
+            w_block(h, Di, w);
+            const double* gl = P.bl + 3 * l;
             const double g0 = gl[0], g1 = gl[1], g2 = gl[2];
 #pragma unroll
             for (int a = 0; a < 6; ++a) acc[a] = acc[a] + (w[3 * a] * g0 + w[3 * a + 1] * g1 + w[3 * a + 2] * g2);
@@ -1146,7 +1111,8 @@ __global__ __launch_bounds__(256) void ba_step_kernel(BaParams P, BaMat3 K, doub
             tv[c] = tv[c] - d;
         }
     }
-    const double* D = P.Dinv + 9 * l;
+    double D[9];
+    landmark_dinv(P, l, lambda, D);
     double Xn[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -1356,8 +1322,6 @@ void launch_ba_ldlt(const BaParams& P, hipStream_t s) {
 }
 
 void launch_ba_trial(const BaParams& P, const BaMat3& K, double lambda, hipStream_t s) {
-    const int nl = std::max(P.L, P.E);
-    if (nl > 0) hipLaunchKernelGGL(ba::ba_landmark_trial_kernel, dim3((nl + 255) / 256), dim3(256), 0, s, P, lambda);
     const int nb = P.np * (P.np + 1) / 2;
     if (nb > 0)
         hipLaunchKernelGGL(ba::ba_schur_kernel, dim3((nb + P.np) * ba::kWG), dim3(ba::kWLanes), 0, s, P, lambda);
@@ -1502,12 +1466,10 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
     rc |= ba_alloc(b, &Q.err, 2 * E);
     rc |= ba_alloc(b, &Q.Jp, 12 * E);
     rc |= ba_alloc(b, &Q.Jl, 6 * E);
-    rc |= ba_alloc(b, &Q.W, 18 * E);
     rc |= ba_alloc(b, &Q.Hpp, 36 * P);
     rc |= ba_alloc(b, &Q.bp, 6 * P);
     rc |= ba_alloc(b, &Q.Hll, 9 * L);
     rc |= ba_alloc(b, &Q.bl, 3 * L);
-    rc |= ba_alloc(b, &Q.Dinv, 9 * L);
     rc |= ba_alloc(b, &Q.S, ns * ns);
     rc |= ba_alloc(b, &Q.bs, ns);
     rc |= ba_alloc(b, &Q.xp, ns);
@@ -1663,8 +1625,9 @@ namespace {
 // One read-back per solve, plus one per suspended trial loop.
 // poses / landmarks: host in / out; both nullptr: the problem's poses and landmarks are already in Q.poses / Q.X on
 // the device (yv_ba_window_solve) and stay there.
-int ba_solve_device(yv_ba* b, double* poses, double* landmarks, int max_iters, double* chi2_log, int* iters) {
-    const bool host_io = poses != nullptr;
+// the enqueue half: chi2 at the start, then every iteration with one trial slot, then the control block's read-back
+// (asynchronous: ba_solve_wait collects it)
+int ba_solve_enqueue(yv_ba* b, const double* poses, const double* landmarks, int max_iters) {
     yavo::BaParams& Q = b->P;
     const size_t pb = sizeof(double) * 7 * Q.P, xb = sizeof(double) * 3 * Q.L;
     hipStream_t st = b->st;
@@ -1685,35 +1648,70 @@ int ba_solve_device(yv_ba* b, double* poses, double* landmarks, int max_iters, d
     Ptr.gate = &c->skip_trial;
     Ptr.lam = &c->lambda;
     if (hipMemsetAsync(b->d_cur, 0, sizeof(int), st) != hipSuccess) return YV_ERR_HIP;
-    if (host_io && (hipMemcpyAsync(Q.poses, poses, pb, hipMemcpyHostToDevice, st) != hipSuccess ||
-                    (xb && hipMemcpyAsync(Q.X, landmarks, xb, hipMemcpyHostToDevice, st) != hipSuccess)))
+    if (poses && (hipMemcpyAsync(Q.poses, poses, pb, hipMemcpyHostToDevice, st) != hipSuccess ||
+                  (xb && hipMemcpyAsync(Q.X, landmarks, xb, hipMemcpyHostToDevice, st) != hipSuccess)))
         return YV_ERR_HIP;
     yavo::launch_ba_chi2(Pc, b->K, st);
-    int first = 0;
-    bool resume = false;
+    for (int it = 0; it < max_iters; ++it) {
+        yavo::launch_ba_linearize(Pit, b->K, it == 0 ? 1 : 0, st);
+        yavo::launch_ba_trial(Ptr, b->K, 0.0, st);
+    }
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(b->h_ctl, c, sizeof(yavo::BaCtl), hipMemcpyDeviceToHost, st) != hipSuccess)
+        return YV_ERR_HIP;
+    return YV_OK;
+}
+
+// the collecting half: waits for the control block, resumes a suspended trial loop (one read-back each) until the
+// solve ends, then the estimate into Q.poses / Q.X (host copies when poses != nullptr) and the chi2 log
+int ba_solve_wait(yv_ba* b, double* poses, double* landmarks, int max_iters, double* chi2_log, int* iters) {
+    yavo::BaParams& Q = b->P;
+    const size_t pb = sizeof(double) * 7 * Q.P, xb = sizeof(double) * 3 * Q.L;
+    hipStream_t st = b->st;
+    yavo::BaCtl* c = b->d_ctl;
+    yavo::BaParams Pc = Q;
+    Pc.ctl = c;
+    Pc.log = b->d_log;
+    yavo::BaParams Pit = Pc, Ptr = Pc;
+    Pit.gate = &c->skip_iter;
+    Ptr.gate = &c->skip_trial;
+    Ptr.lam = &c->lambda;
     for (;;) {
+        if (hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
+        if (!b->h_ctl->suspended) break;
+        yavo::launch_ba_ctl_resume(c, st);  // the suspended iteration's trial loop continues at its trial q
+        const int first = b->h_ctl->it;
         for (int it = first; it < max_iters; ++it) {
-            if (!(resume && it == first)) yavo::launch_ba_linearize(Pit, b->K, it == 0 ? 1 : 0, st);
+            if (it != first) yavo::launch_ba_linearize(Pit, b->K, 0, st);
             yavo::launch_ba_trial(Ptr, b->K, 0.0, st);
         }
         if (hipGetLastError() != hipSuccess ||
-            hipMemcpyAsync(b->h_ctl, c, sizeof(yavo::BaCtl), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
+            hipMemcpyAsync(b->h_ctl, c, sizeof(yavo::BaCtl), hipMemcpyDeviceToHost, st) != hipSuccess)
             return YV_ERR_HIP;
-        if (!b->h_ctl->suspended) break;
-        yavo::launch_ba_ctl_resume(c, st);  // the suspended iteration's trial loop continues at its trial q
-        first = b->h_ctl->it;
-        resume = true;
     }
     yavo::launch_ba_finish(Q, st);
     const int n_it = max_iters > 0 ? b->h_ctl->iters : 0;
-    if ((host_io && (hipMemcpyAsync(poses, Q.poses, pb, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                     (xb && hipMemcpyAsync(landmarks, Q.X, xb, hipMemcpyDeviceToHost, st) != hipSuccess))) ||
+    if ((poses && (hipMemcpyAsync(poses, Q.poses, pb, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                   (xb && hipMemcpyAsync(landmarks, Q.X, xb, hipMemcpyDeviceToHost, st) != hipSuccess))) ||
         (chi2_log && hipMemcpyAsync(chi2_log, b->d_log, sizeof(double) * (n_it + 1), hipMemcpyDeviceToHost, st) != hipSuccess) ||
         hipStreamSynchronize(st) != hipSuccess)
         return YV_ERR_HIP;
     if (iters) *iters = n_it;
     return YV_OK;
+}
+
+// The LM of yv_ba_solve with its control on the device (default): the host enqueues every iteration's kernels
+// without waiting -- linearise + H / b (whose last workgroup begins the iteration), one damping trial (Schur, LDLT,
+// step into the trial state, chi2 + scale, whose last workgroup decides and ends the iteration) -- and the control
+// block (lambda, ni, currentChi, stop / accept) gates the kernels. g2o's trial loop usually accepts its first trial;
+// an iteration that needs more suspends the solve (every later kernel skips) and the host resumes it. One read-back
+// per solve, plus one per suspended trial loop.
+// poses / landmarks: host in / out; both nullptr: the problem's poses and landmarks are already in Q.poses / Q.X on
+// the device (yv_ba_window_solve) and stay there.
+int ba_solve_device(yv_ba* b, double* poses, double* landmarks, int max_iters, double* chi2_log, int* iters) {
+    const int rc = ba_solve_enqueue(b, poses, landmarks, max_iters);
+    if (rc != YV_OK) return rc;
+    return ba_solve_wait(b, poses, landmarks, max_iters, chi2_log, iters);
 }
 
 }  // namespace
@@ -1802,9 +1800,9 @@ extern "C" int yv_ba_solve(yv_ba* b, double* poses, double* landmarks, int max_i
 extern "C" int yv_ba_debug_read(yv_ba* b, int which, double* dst, int64_t count) {
     if (!b || !b->ready || !dst || count < 0) return YV_ERR_INVALID;
     const yavo::BaParams& Q = b->P;
-    // which = 3 (H_pl) is no longer stored (formed from Jp / Jl where it is read): YV_ERR_INVALID
-    if (which == 3) return YV_ERR_INVALID;
-    double* const bufs[] = {Q.err, Q.Jp, Q.Jl, nullptr, Q.W, Q.Hpp, Q.bp, Q.Hll, Q.bl, Q.Dinv, Q.S, Q.bs, Q.xp, Q.xl,
+    // which = 3 (H_pl), 4 (W) and 9 (Dinv) are no longer stored (formed where they are read): YV_ERR_INVALID
+    if (which == 3 || which == 4 || which == 9) return YV_ERR_INVALID;
+    double* const bufs[] = {Q.err, Q.Jp, Q.Jl, nullptr, nullptr, Q.Hpp, Q.bp, Q.Hll, Q.bl, nullptr, Q.S, Q.bs, Q.xp, Q.xl,
                             Q.poses, Q.X, Q.scal};
     const int64_t sizes[] = {2LL * Q.E, 12LL * Q.E, 6LL * Q.E, 18LL * Q.E, 18LL * Q.E, 36LL * Q.P, 6LL * Q.P,
                              9LL * Q.L, 3LL * Q.L, 9LL * Q.L, (int64_t)Q.ns * Q.ns, Q.ns, Q.ns, 3LL * Q.L,
@@ -2048,6 +2046,12 @@ struct yv_ba_window {
     std::vector<int32_t> h_cnt;  // per store index, -1 = not recorded
     int32_t* h_struct = nullptr;  // pinned: pe_off [P + 1], cv_off [P P + 1]
     size_t h_struct_cap = 0;
+    // a solve enqueued by yv_ba_window_solve_begin, collected by yv_ba_window_solve_end
+    bool solving = false;
+    int solve_kind = 0;  // 1: the LM runs; 2: nothing to solve (only the anchor kernel)
+    int solve_iters = 0, solve_nb = 0, solve_L = 0;
+    double* solve_anchor = nullptr;
+    WinFrames solve_F{};
 };
 
 namespace {
@@ -2155,7 +2159,7 @@ extern "C" int yv_ba_window_add_block(yv_ba_window* w, const void* d_block, int6
                                       const double* d_edge_uv, const int32_t* d_edge_query, const void* d_matches,
                                       int max_kp, void* stream) {
     if (!w || !d_block || !d_edge_uv || !d_edge_query || !d_matches || n_frames < 1 || first_frame < 0 ||
-        max_kp < 1 || max_kp > 65536)
+        max_kp < 1 || max_kp > 65536 || w->solving)  // a pending solve reads the store: collect it first
         return YV_ERR_INVALID;
     if (hipSetDevice(w->ba->dev) != hipSuccess) return YV_ERR_HIP;
     hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : yavo::ctx_stream(w->ba->ctx);
@@ -2175,9 +2179,9 @@ extern "C" int yv_ba_window_add_block(yv_ba_window* w, const void* d_block, int6
     return YV_OK;
 }
 
-extern "C" int yv_ba_window_solve(yv_ba_window* w, int64_t first, int n, int n_fixed, const double K[9], int max_iters,
-                                  double* d_anchor, double* chi2_log, int* iters, int* solved) {
-    if (!w || !K || n < 1 || n > kWinMaxPoses || n_fixed < 0 || max_iters < 0) return YV_ERR_INVALID;
+extern "C" int yv_ba_window_solve_begin(yv_ba_window* w, int64_t first, int n, int n_fixed, const double K[9],
+                                        int max_iters, double* d_anchor) {
+    if (!w || !K || n < 1 || n > kWinMaxPoses || n_fixed < 0 || max_iters < 0 || w->solving) return YV_ERR_INVALID;
     for (int i = 0; i < 9; ++i)
         if (!std::isfinite(K[i])) return YV_ERR_INVALID;
     yv_ba* b = w->ba;
@@ -2194,14 +2198,14 @@ extern "C" int yv_ba_window_solve(yv_ba_window* w, int64_t first, int n, int n_f
         F.base[i] = L;
         L += F.c[i];
     }
-    if (iters) *iters = 0;
-    if (solved) *solved = 0;
     hipStream_t st = b->st;
     if (n <= n_fixed || L == 0) {  // nothing to solve: the anchor is the last frame's pose as recorded
         if (d_anchor) {
             hipLaunchKernelGGL(win_anchor_kernel, dim3(1), dim3(64), 0, st, w->d_T + (F.s0 + n - 1) * 7, d_anchor);
-            if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
+            if (hipGetLastError() != hipSuccess) return YV_ERR_HIP;
         }
+        w->solving = true;
+        w->solve_kind = 2;
         return YV_OK;
     }
     const int E = 2 * L;
@@ -2280,20 +2284,51 @@ extern "C" int yv_ba_window_solve(yv_ba_window* w, int64_t first, int n, int n_f
     Q.cv_e2 = b->d_cv_e2;
     std::memcpy(b->K.v, K, sizeof b->K.v);
     b->ready = true;
-    int it = 0;
-    const int rc = ba_solve_device(b, nullptr, nullptr, max_iters, chi2_log, &it);
+    const int rc = ba_solve_enqueue(b, nullptr, nullptr, max_iters);
     if (rc != YV_OK) return rc;
-    hipLaunchKernelGGL(win_scatter_kernel, dim3(nb), dim3(256), 0, st, F, L, w->max_lm, Q.poses, Q.X, w->d_T, w->d_X,
-                       d_anchor);
+    w->solving = true;
+    w->solve_kind = 1;
+    w->solve_iters = max_iters;
+    w->solve_nb = nb;
+    w->solve_L = L;
+    w->solve_anchor = d_anchor;
+    w->solve_F = F;
+    return YV_OK;
+}
+
+extern "C" int yv_ba_window_solve_end(yv_ba_window* w, double* chi2_log, int* iters, int* solved) {
+    if (!w || !w->solving) return YV_ERR_INVALID;
+    yv_ba* b = w->ba;
+    if (hipSetDevice(b->dev) != hipSuccess) return YV_ERR_HIP;
+    hipStream_t st = b->st;
+    const int kind = w->solve_kind;
+    w->solving = false;
+    w->solve_kind = 0;
+    if (iters) *iters = 0;
+    if (solved) *solved = 0;
+    if (kind == 2) return hipStreamSynchronize(st) == hipSuccess ? YV_OK : YV_ERR_HIP;
+    int it = 0;
+    const int rc = ba_solve_wait(b, nullptr, nullptr, w->solve_iters, chi2_log, &it);
+    if (rc != YV_OK) return rc;
+    yavo::BaParams& Q = b->P;
+    hipLaunchKernelGGL(win_scatter_kernel, dim3(w->solve_nb), dim3(256), 0, st, w->solve_F, w->solve_L, w->max_lm,
+                       Q.poses, Q.X, w->d_T, w->d_X, w->solve_anchor);
     if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
     if (iters) *iters = it;
     if (solved) *solved = 1;
     return YV_OK;
 }
 
+extern "C" int yv_ba_window_solve(yv_ba_window* w, int64_t first, int n, int n_fixed, const double K[9], int max_iters,
+                                  double* d_anchor, double* chi2_log, int* iters, int* solved) {
+    const int rc = yv_ba_window_solve_begin(w, first, n, n_fixed, K, max_iters, d_anchor);
+    if (rc != YV_OK) return rc;
+    return yv_ba_window_solve_end(w, chi2_log, iters, solved);
+}
+
 extern "C" int yv_ba_window_read(yv_ba_window* w, int64_t frame, double* T_wc, int* n, int32_t* edge, double* X,
                                  double* uv_own, double* uv_prev, int cap) {
-    if (!w || !n) return YV_ERR_INVALID;
+    if (!w || !n || w->solving) return YV_ERR_INVALID;
     if (hipSetDevice(w->ba->dev) != hipSuccess || win_collect(w) != YV_OK) return YV_ERR_HIP;
     const int64_t s = frame - w->g0;
     if (w->g0 < 0 || s < 0 || s >= w->cap || w->h_cnt[(size_t)s] < 0) return YV_ERR_INVALID;
@@ -2314,7 +2349,7 @@ extern "C" int yv_ba_window_read(yv_ba_window* w, int64_t frame, double* T_wc, i
 }
 
 extern "C" int yv_ba_window_trajectory(yv_ba_window* w, int64_t first, int n, double* T_wc) {
-    if (!w || !T_wc || n < 0) return YV_ERR_INVALID;
+    if (!w || !T_wc || n < 0 || w->solving) return YV_ERR_INVALID;
     if (hipSetDevice(w->ba->dev) != hipSuccess || win_collect(w) != YV_OK) return YV_ERR_HIP;
     if (n == 0) return YV_OK;
     if (first < w->g0 || first + n > w->g0 + w->cap) return YV_ERR_INVALID;

@@ -201,12 +201,10 @@ struct BaParams {
     double* err = nullptr;            // [E][2]
     double* Jp = nullptr;             // [E][12]
     double* Jl = nullptr;             // [E][6]
-    double* W = nullptr;              // [E][18]
     double* Hpp = nullptr;            // [P][36]
     double* bp = nullptr;             // [P][6]
     double* Hll = nullptr;            // [L][9]
     double* bl = nullptr;             // [L][3]
-    double* Dinv = nullptr;           // [L][9]
     double* S = nullptr;              // [ns][ns]
     double* bs = nullptr;             // [ns]
     double* xp = nullptr;             // [ns]

@@ -116,10 +116,12 @@ class SequenceFrontend:
     """The device front end over a stereo sequence in chunks of `chunk` frames (module docstring)."""
 
     def __init__(self, ctx, chunk: int, K, T_right, n_fixed: int = 2, ba_iters: int = 10,
-                 H: int = 376, W: int = 1241, max_kp: int = 2000, match_thr: int = 20, device_window: bool = True):
+                 H: int = 376, W: int = 1241, max_kp: int = 2000, match_thr: int = 20, device_window: bool = True,
+                 ba_priority: int = 0):
         """device_window: the BA window is recorded, assembled and written back on the device (yv_ba_window_*,
         no per-chunk read-back); False: the host assembly below (window_problem / apply_window), kept as the
-        restatement the device path is checked against."""
+        restatement the device path is checked against. ba_priority: the BA stream's priority (torch's convention:
+        -1 high, 0 default) against the context stream the next chunk's kernels run on."""
         import torch
         from . import Batch, BaWindow, BundleAdjuster
         if chunk < 2 or n_fixed < 1:
@@ -155,7 +157,7 @@ class SequenceFrontend:
         self._h_q = pinned(chunk * max_kp * 4)
         self._h_m = pinned(2 * chunk * max_kp * 100)
         self.ba = BundleAdjuster(ctx, window, window * max_kp, 2 * window * max_kp)
-        self.ba_stream = torch.cuda.Stream(device=dev)  # the BA beside the next chunk's kernels
+        self.ba_stream = torch.cuda.Stream(device=dev, priority=ba_priority)  # the BA beside the next chunk's kernels
         self.ba.set_stream(self.ba_stream.cuda_stream)
         self._ba_pending = False
         self.device_window = device_window
@@ -222,40 +224,45 @@ class SequenceFrontend:
                 seconds[key] = seconds.get(key, 0.0) + dt
 
     def _process_chunk_device(self, first: int, t0: float, seconds) -> None:
-        """process_chunk with the device window: the previous window's BA (its stream; the host waits for its result,
-        the anchor lands in d_base), this chunk's placement after it, then the chunk's frames recorded from the placed
-        block -- no read-back."""
+        """process_chunk with the device window: collect the previous window's BA (begun one call earlier, it ran
+        beside this chunk's kernels; the anchor lands in d_base), place and record this chunk after it, and begin this
+        chunk's window at once, so it runs while the host issues the next chunk -- no read-back but the counts."""
         import time
         ctx, n = self.ctx, self.chunk
         t1 = time.perf_counter()
         if self._ba_pending:
-            self._local_ba_device()
+            self._local_ba_device_end()
         t2 = time.perf_counter()
         ctx.map_place(self.d_block.data_ptr(), 1, self.bb, self.d_base.data_ptr(), self.d_anchors.data_ptr())
         v = self.batch.view()
         self.win.add_block(self.d_block.data_ptr(), first, n, v.edge_uv, v.edge_query, v.matches, self.max_kp)
         self.next_frame = first + n
-        self._ba_pending = True
         t3 = time.perf_counter()
+        self._local_ba_device_begin()
+        t4 = time.perf_counter()
         if seconds is not None:
-            for key, dt in (("issue", t1 - t0), ("ba", t2 - t1), ("place_record", t3 - t2)):
+            for key, dt in (("issue", t1 - t0), ("ba", t2 - t1), ("place_record", t3 - t2), ("ba_begin", t4 - t3)):
                 seconds[key] = seconds.get(key, 0.0) + dt
 
-    def _local_ba_device(self) -> None:
-        self._ba_pending = False
+    def _local_ba_device_begin(self) -> None:
         last = self.next_frame - 1
         lo = max(0, last - self.window + 1)
-        solved, log, it = self.win.solve(lo, last + 1 - lo, self.n_fixed, self.K, self.ba_iters,
-                                         self.d_base.data_ptr())
+        self._ba_last = last
+        self.win.solve_begin(lo, last + 1 - lo, self.n_fixed, self.K, self.ba_iters, self.d_base.data_ptr())
+        self._ba_pending = True
+
+    def _local_ba_device_end(self) -> None:
+        self._ba_pending = False
+        solved, log, it = self.win.solve_end()
         if solved:
-            self.ba_log.append((last, it, float(log[0]), float(log[-1])))
+            self.ba_log.append((self._ba_last, it, float(log[0]), float(log[-1])))
 
     def flush(self, seconds: Dict[str, float] = None) -> None:
         """The last chunk's BA window (process_chunk runs each window one chunk late)."""
         import time
         if self._ba_pending and self.win is not None:
             t0 = time.perf_counter()
-            self._local_ba_device()
+            self._local_ba_device_end()
             if seconds is not None:
                 seconds["ba"] = seconds.get("ba", 0.0) + time.perf_counter() - t0
         elif self._ba_pending:
