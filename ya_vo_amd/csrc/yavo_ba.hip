@@ -579,12 +579,12 @@ __device__ unsigned long long g_ldlt_prof[kLdltWaves][8];
 
 __global__ __launch_bounds__(64 * kLdltWaves) void ba_ldlt_reg_kernel(BaParams P) {
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    constexpr int NT = 64 * kLdltWaves;
-    __shared__ double Lc[kLdltRegN * kLdltLs];       // S row-major (n x n) first, then L(r, c) at Lc[c * 129 + r]
+    __shared__ double Lc[kLdltRegN * kLdltLs];       // L(r, c) at Lc[c * 129 + r]
     __shared__ double tq[kLdltRing][2][kLdltRegN];   // pair q's t_2q(.), t_2q+1(.) in slot q % kLdltRing
     __shared__ double Dv[kLdltRegN];                 // D(k)
     __shared__ double dor[kLdltRegN];                // the diagonal of P S P^T
     __shared__ double dg[kLdltRegN];                 // |diagonal|, permuted as the pivots are taken
+    __shared__ double dsv[kLdltRegN];                // the diagonal of S
     __shared__ int perm[kLdltRegN];                  // position -> original index: (P S P^T)(i, j) = S(perm[i], perm[j])
     __shared__ int flag[kLdltRing];                  // the pair a slot holds (-1: none yet)
     __shared__ int s_slow;
@@ -592,25 +592,15 @@ __global__ __launch_bounds__(64 * kLdltWaves) void ba_ldlt_reg_kernel(BaParams P
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int r0 = l, r1 = l + 64;
     LDP_DECL
-    {
-        // S staged row-major, eight 16-B loads per thread in flight
-        const int nh = (n * n) >> 1;
-        const double2* src = reinterpret_cast<const double2*>(P.S);
-        double2* dst = reinterpret_cast<double2*>(Lc);
-        for (int e0 = t; e0 < nh; e0 += 8 * NT) {
-            double2 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = e0 + NT * u < nh ? src[e0 + NT * u] : make_double2(0.0, 0.0);
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (e0 + NT * u < nh) dst[e0 + NT * u] = v[u];
-        }
-        if (((n * n) & 1) && t == 0) Lc[n * n - 1] = P.S[n * n - 1];
+    // S is read straight from global memory (L2-resident: the Schur kernel just wrote it): its diagonal here, the
+    // registers' entries once the permutation is known (round 4 staged all of S in LDS first: ~4 us more)
+    if (t < n) {
+        const double d = P.S[(int64_t)t * n + t];
+        dg[t] = fabs(d);
+        dsv[t] = d;
     }
     if (t < kLdltRing) flag[t] = -1;
     if (t == 0) s_slow = 0;
-    __syncthreads();
-    if (t < n) dg[t] = fabs(Lc[t * n + t]);
     __syncthreads();
     // 1. ranks by (|d| descending, index ascending); a tie or a NaN sends the sequence to the replay
     if (t < n) {
@@ -679,7 +669,7 @@ __global__ __launch_bounds__(64 * kLdltWaves) void ba_ldlt_reg_kernel(BaParams P
     // the oracle's first step: a zero (or NaN) pivot ends the factorisation with only its own transposition applied
     // to the matrix and none to the vector
     const int big0 = perm[0];
-    const double a00 = Lc[big0 * n + big0];
+    const double a00 = dsv[big0];
     const bool brk = !(fabs(a00) > 0);
     __syncthreads();
     if (brk) {
@@ -687,7 +677,8 @@ __global__ __launch_bounds__(64 * kLdltWaves) void ba_ldlt_reg_kernel(BaParams P
         __syncthreads();
     }
     // 2. P S P^T into registers: Al[j][h] = entry (r0, 16 j + 2 w + h) for the columns below 64, Ah[j][h] = (r1, ...);
-    // only the strict lower triangle is read (the rest is never used)
+    // only the strict lower triangle is read (the rest is never used). S is bitwise symmetric, so entry (r, c) is read
+    // as S(perm[c], perm[r]): one row of S per load instruction, all 24 loads of a lane in flight together
     double Al[kLdltPairs / 2][2], Ah[kLdltPairs][2];
     const int tq0 = tq_index(r0), tq1 = tq_index(r1);
     {
@@ -698,10 +689,11 @@ __global__ __launch_bounds__(64 * kLdltWaves) void ba_ldlt_reg_kernel(BaParams P
             for (int h = 0; h < 2; ++h) {
                 const int c = 16 * j + 2 * w + h;
                 const int pc = c < n ? perm[c] : 0;
-                if (j < kLdltPairs / 2) Al[j < kLdltPairs / 2 ? j : 0][h] = (r0 > c && r0 < n) ? Lc[p0 * n + pc] : 0.0;
-                Ah[j][h] = (r1 > c && r1 < n) ? Lc[p1 * n + pc] : 0.0;
+                const double* row = P.S + (int64_t)pc * n;
+                if (j < kLdltPairs / 2) Al[j < kLdltPairs / 2 ? j : 0][h] = (r0 > c && r0 < n) ? row[p0] : 0.0;
+                Ah[j][h] = (r1 > c && r1 < n) ? row[p1] : 0.0;
             }
-        if (t < n) dor[t] = Lc[perm[t] * n + perm[t]];
+        if (t < n) dor[t] = dsv[perm[t]];
     }
     // the right-hand side, permuted (a zero first pivot: not permuted) -- wave 0 solves
     double v0 = 0.0, v1 = 0.0;
@@ -709,7 +701,7 @@ __global__ __launch_bounds__(64 * kLdltWaves) void ba_ldlt_reg_kernel(BaParams P
         v0 = r0 < n ? P.bs[brk ? r0 : perm[r0]] : 0.0;
         v1 = r1 < n ? P.bs[brk ? r1 : perm[r1]] : 0.0;
     }
-    __syncthreads();  // the staged S is dead: Lc becomes the column store
+    __syncthreads();
     int err = 0;
     if (brk) {
         // the solves read P S P^T as it stands
