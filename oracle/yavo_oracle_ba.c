@@ -19,16 +19,16 @@
  *                   landmark back-substitution
  * Summation orders (the GPU kernels, yavo_ba.hip, follow them bit for bit; g2o's own orders are not exposed, so
  * parity with a g2o build is unpinned):
- *   tree256   values indexed k = 0 .. n-1: partial[t] = sum of items k = t mod 256 in ascending k (from 0.0), then
- *             p[t] += p[t + off], off = 128 .. 1; used for chi2 over all edges and for the LM scale over all
- *             variables (poses, then landmarks)
- *   tree4096  the same with 4096 leaves (t = k mod 4096, off = 2048 .. 1); used for each pose's H_pp / b_p over its
- *             edges (edge order), for each Schur block entry's sum over the co-visible pairs of its two poses
- *             (landmark order), v = base - total, and for each b_schur entry's sum over the pose's edges (edge order)
+ *   tree4096  values indexed k = 0 .. n-1: partial[t] = sum of items k = t mod 4096 in ascending k (from 0.0), then
+ *             p[t] += p[t + off], off = 2048 .. 1; used for each pose's H_pp / b_p over its edges (edge order), for
+ *             each Schur block entry's sum over the co-visible pairs of its two poses (landmark order), v = base -
+ *             total, for each b_schur entry's sum over the pose's edges (edge order), for chi2 over all edges and for
+ *             the LM scale over all variables (poses, then landmarks)
  *   sequential per landmark over its edges (edge order) for H_ll / b_l and the back-substitution
- * (Rounds 1-4 summed the Schur and b_schur entries as one sequential chain each and H_pp / b_p in tree256 order. A
- * 3,800-term chain is latency-bound on one GPU lane, and 256 leaves leave each GPU lane ~15 dependent loads; with
- * 4096 leaves a configs[2] window's sums have at most one item per leaf, so every load is in flight at once.)
+ * (Rounds 1-4 summed the Schur and b_schur entries as one sequential chain each, and H_pp / b_p, chi2 and the scale
+ * in a 256-leaf tree. A 3,800-term chain is latency-bound on one GPU lane, and 256 leaves leave each GPU lane ~15
+ * dependent loads (and chi2's chains 300-450 dependent additions); with 4096 leaves a configs[2] window's sums have
+ * at most one item per leaf for the blocks and ~28 for chi2, so the loads are in flight at once.)
  */
 #include "yavo_oracle.h"
 
@@ -37,21 +37,6 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
-
-#define BA_NT 256
-
-typedef struct {
-    double part[BA_NT];
-} tree256;
-static void t_reset(tree256* t) { memset(t->part, 0, sizeof t->part); }
-static void t_add(tree256* t, int k, double v) { t->part[k % BA_NT] = t->part[k % BA_NT] + v; }
-static double t_total(const tree256* t) {
-    double p[BA_NT];
-    memcpy(p, t->part, sizeof p);
-    for (int off = BA_NT / 2; off > 0; off >>= 1)
-        for (int i = 0; i < off; ++i) p[i] = p[i] + p[i + off];
-    return p[0];
-}
 
 #define BA_NW 4096
 typedef struct {
@@ -248,14 +233,16 @@ static void ba_free_struct(ba_struct* s) {
 }
 
 static double ba_chi2(const ba_struct* s, const double* poses, const double* X) {
-    tree256 t;
-    t_reset(&t);
+    tree4096* t = (tree4096*)malloc(sizeof(tree4096));
+    w_reset(t);
     for (int e = 0; e < s->E; ++e) {
         double r[2];
         ba_error(poses + 7 * s->ep[e], s->K, X + 3 * s->el[e], s->meas + 2 * e, r);
-        t_add(&t, e, r[0] * r[0] + r[1] * r[1]);
+        w_add(t, e, r[0] * r[0] + r[1] * r[1]);
     }
-    return t_total(&t);
+    const double v = w_total(t);
+    free(t);
+    return v;
 }
 
 /* diagnostics (tests only): when or_ba_dump_iter >= 0, the first damping trial of that iteration copies its
@@ -440,12 +427,11 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
             double tempChi = ba_chi2(&s, poses, X);
             if (!ok2) tempChi = DBL_MAX;
             rho = currentChi - tempChi;
-            /* computeScale over the variables (poses, then landmarks), tree256 order */
-            tree256 t;
-            t_reset(&t);
-            for (int j = 0; j < ns; ++j) t_add(&t, j, xp[j] * (lambda * xp[j] + bp[6 * n_fixed + j]));
-            for (int j = 0; j < 3 * L; ++j) t_add(&t, ns + j, xl[j] * (lambda * xl[j] + bl[j]));
-            double scale = t_total(&t);
+            /* computeScale over the variables (poses, then landmarks), tree4096 order */
+            w_reset(wt);
+            for (int j = 0; j < ns; ++j) w_add(wt, j, xp[j] * (lambda * xp[j] + bp[6 * n_fixed + j]));
+            for (int j = 0; j < 3 * L; ++j) w_add(wt, ns + j, xl[j] * (lambda * xl[j] + bl[j]));
+            double scale = w_total(wt);
             scale += 1e-3;
             rho /= scale;
             if (rho > 0 && isfinite(tempChi)) {
