@@ -59,20 +59,6 @@ __device__ __forceinline__ void ba_error(const double* T, const double* K, const
     e[1] = meas[1] - u1 / u2;
 }
 
-// the 256-lane halving tree over one value per thread (LDS), result valid in thread 0
-__device__ __forceinline__ double tree256(double v, double* red) {
-    const int t = threadIdx.x;
-    red[t] = v;
-    __syncthreads();
-    for (int off = kNT / 2; off > 0; off >>= 1) {
-        if (t < off) red[t] = red[t] + red[t + off];
-        __syncthreads();
-    }
-    const double r = red[0];
-    __syncthreads();
-    return r;
-}
-
 // the state (poses, landmarks) the current estimate is in: 0 = P.poses / P.X, 1 = P.poses2 / P.X2
 __device__ __forceinline__ int ba_cur(const BaParams& P) { return P.cur ? *P.cur : 0; }
 
@@ -322,15 +308,39 @@ __global__ __launch_bounds__(kWLanes) void ba_reduce_kernel(BaParams P, int firs
         const int l = (blockIdx.x - P.np * kWG) * kWLanes + t;
         if (l < P.L) {
             double h[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-            for (int k = P.le_off[l]; k < P.le_off[l + 1]; ++k) {
-                const int e = P.le[k];
-                const double* jl = P.Jl + 6 * (int64_t)e;
-                const double e0 = P.err[2 * e], e1 = P.err[2 * e + 1];
+            const int k0 = P.le_off[l], k1 = P.le_off[l + 1];
+            // the landmark's edges four at a time: indices, then every edge's J_point and error loaded before the
+            // additions (in edge order), so a batch costs one dependent load round, not one per edge
+            for (int kb = k0; kb < k1; kb += 4) {
+                int eb[4];
 #pragma unroll
-                for (int a = 0; a < 3; ++a) {
+                for (int u = 0; u < 4; ++u) eb[u] = kb + u < k1 ? P.le[kb + u] : 0;
+                double jl[4][6], er[4][2];
 #pragma unroll
-                    for (int b = a; b < 3; ++b) h[3 * a + b] = h[3 * a + b] + (jl[a] * jl[b] + jl[3 + a] * jl[3 + b]);
-                    g[a] = g[a] + (jl[a] * e0 + jl[3 + a] * e1);
+                for (int u = 0; u < 4; ++u) {
+                    if (kb + u < k1) {
+                        const double2* j2 = reinterpret_cast<const double2*>(P.Jl + 6 * (int64_t)eb[u]);
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) {
+                            const double2 v = j2[i];
+                            jl[u][2 * i] = v.x;
+                            jl[u][2 * i + 1] = v.y;
+                        }
+                        const double2 ev = reinterpret_cast<const double2*>(P.err)[eb[u]];
+                        er[u][0] = ev.x;
+                        er[u][1] = ev.y;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (kb + u >= k1) break;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+#pragma unroll
+                        for (int b = a; b < 3; ++b)
+                            h[3 * a + b] = h[3 * a + b] + (jl[u][a] * jl[u][b] + jl[u][3 + a] * jl[u][3 + b]);
+                        g[a] = g[a] + (jl[u][a] * er[u][0] + jl[u][3 + a] * er[u][1]);
+                    }
                 }
             }
             double m = 0.0;
@@ -1040,22 +1050,17 @@ __global__ __launch_bounds__(256) void ba_ldlt_kernel(BaParams P) {
 #undef LL
 }
 
-// the position of item k of a tree256 sum over N items in its chain-major copy: chain k mod 256, then k / 256, so
-// that ba_chi2_kernel reads each chain's items contiguously (the item-major order gave every 128-B line to 16
-// workgroups: ~30 MB of line traffic for a 1.5 MB sum)
-__device__ __forceinline__ int chain_pos(int k, int N) { return (k & (kNT - 1)) * ((N + kNT - 1) / kNT) + k / kNT; }
-
 // The trial step in one launch (g2o's back-substitution, oplus and the trial chi2's per-edge terms): every workgroup
 // first forms all poses of the trial state in LDS (free: exp(x_p) T, fixed: T); one lane per landmark then runs
 // x_l = Dinv (b_l - sum_e H_pl^T x_p) sequentially over its edges, writes X + x_l into the trial state and |e|^2 of
 // each of its edges at the trial state. The trial state is the other buffer: a rejected trial leaves the current
 // one untouched (no backup / restore copies); an accepted one flips P.cur (ba_chi2_kernel's last workgroup).
-// It also writes the LM scale's items x (lambda x + b) (free poses' components, then the landmarks') chain-major.
+// It also writes the LM scale's items x (lambda x + b) (free poses' components, then the landmarks').
 __global__ __launch_bounds__(256) void ba_step_kernel(BaParams P, BaMat3 K, double lambda) {
     extern __shared__ double sT[];  // [P][7]
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     if (P.lam) lambda = *P.lam;
-    const int ns = P.ns, N1 = ns + 3 * P.L;
+    const int ns = P.ns;
     const int cur = ba_cur(P);
     const double* T0 = cur ? P.poses2 : P.poses;
     const double* X0 = cur ? P.X2 : P.X;
@@ -1082,43 +1087,66 @@ __global__ __launch_bounds__(256) void ba_step_kernel(BaParams P, BaMat3 K, doub
     if (blockIdx.x == 0)
         for (int k = t; k < ns; k += kNT) {
             const double x = P.xp[k];
-            P.sc1[chain_pos(k, N1)] = x * (lambda * x + P.bp[6 * P.nf + k]);
+            P.sc1[k] = x * (lambda * x + P.bp[6 * P.nf + k]);
         }
     __syncthreads();
     const int l = blockIdx.x * kNT + t;
     if (l >= P.L) return;
     const int k0 = P.le_off[l], k1 = P.le_off[l + 1];
     double tv[3] = {P.bl[3 * l], P.bl[3 * l + 1], P.bl[3 * l + 2]};
-    for (int k = k0; k < k1; ++k) {
-        const int e = P.le[k], p = P.ep[e];
-        if (p < P.nf) continue;
-        const double* xpp = P.xp + 6 * (p - P.nf);
-        double h[18];
-        hpl_load(P, e, h);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            double d = h[c] * xpp[0];
-#pragma unroll
-            for (int a = 1; a < 6; ++a) d = d + h[3 * a + c] * xpp[a];
-            tv[c] = tv[c] - d;
-        }
-    }
     double D[9];
     landmark_dinv(P, l, lambda, D);
+    // the landmark's edges two at a time: indices and poses, then both edges' Jacobians and x_p loaded before the
+    // subtractions (in edge order), one dependent load round per pair of edges
+    for (int kb = k0; kb < k1; kb += 2) {
+        int eb[2], pb[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) eb[u] = kb + u < k1 ? P.le[kb + u] : 0;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) pb[u] = kb + u < k1 ? P.ep[eb[u]] : 0;
+        double h[2][18], xv[2][6];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (kb + u < k1 && pb[u] >= P.nf) {
+                hpl_load(P, eb[u], h[u]);
+                const double* xpp = P.xp + 6 * (pb[u] - P.nf);
+#pragma unroll
+                for (int a = 0; a < 6; ++a) xv[u][a] = xpp[a];
+            }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (kb + u >= k1 || pb[u] < P.nf) continue;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                double d = h[u][c] * xv[u][0];
+#pragma unroll
+                for (int a = 1; a < 6; ++a) d = d + h[u][3 * a + c] * xv[u][a];
+                tv[c] = tv[c] - d;
+            }
+        }
+    }
     double Xn[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const double x = D[3 * c] * tv[0] + D[3 * c + 1] * tv[1] + D[3 * c + 2] * tv[2];
         P.xl[3 * l + c] = x;
-        P.sc1[chain_pos(ns + 3 * l + c, N1)] = x * (lambda * x + P.bl[3 * l + c]);
+        P.sc1[ns + 3 * l + c] = x * (lambda * x + P.bl[3 * l + c]);
         Xn[c] = X0[3 * l + c] + x;
         X1[3 * l + c] = Xn[c];
     }
-    for (int k = k0; k < k1; ++k) {
-        const int e = P.le[k];
-        double r[2];
-        ba_error(sT + 7 * P.ep[e], K.v, Xn, P.meas + 2 * e, r);
-        P.e2[chain_pos(e, P.E)] = r[0] * r[0] + r[1] * r[1];
+    for (int kb = k0; kb < k1; kb += 2) {
+        int eb[2], pb[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) eb[u] = kb + u < k1 ? P.le[kb + u] : 0;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) pb[u] = kb + u < k1 ? P.ep[eb[u]] : 0;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (kb + u >= k1) break;
+            double r[2];
+            ba_error(sT + 7 * pb[u], K.v, Xn, P.meas + 2 * eb[u], r);
+            P.e2[eb[u]] = r[0] * r[0] + r[1] * r[1];
+        }
     }
 }
 
@@ -1130,7 +1158,7 @@ __global__ __launch_bounds__(256) void ba_edge_chi2_kernel(BaParams P, BaMat3 K)
     const int cur = ba_cur(P);
     double r[2];
     ba_error((cur ? P.poses2 : P.poses) + 7 * P.ep[e], K.v, (cur ? P.X2 : P.X) + 3 * P.el[e], P.meas + 2 * e, r);
-    P.e2[chain_pos(e, P.E)] = r[0] * r[0] + r[1] * r[1];
+    P.e2[e] = r[0] * r[0] + r[1] * r[1];
 }
 
 // ---- device-driven LM control (the host loop of yv_ba_solve's host form, operation for operation) ----
@@ -1203,79 +1231,37 @@ __global__ void ba_ctl_resume_kernel(BaCtl* c) {
 }
 
 // chi2 over the edges (sum 0) and, for a trial, the LM scale x.(lambda x + b) over the variables (free poses, then
-// landmarks; sum 1) in the oracle's tree256 order: chain t = 0..255 adds items t, t + 256, ... from 0.0, then the
-// halving tree. One 64-lane workgroup per chain and sum (256 or 512 workgroups): its lanes load the chain's items (up
-// to 8 each) into LDS at once, lane 0 adds them in order, and publishes the chain's sum write-through; the last
-// workgroup to finish forms both trees and then (device control) decides the trial or starts the solve, or (host
-// control) leaves chi2 / scale in scal[0] / scal[1].  mode 0: the solve's first chi2; 1: a trial.
-constexpr int kChi2Lanes = 64;
-constexpr int kChi2MaxItems = 8 * kChi2Lanes;  // items per chain held at once (chains longer than this loop)
-__global__ __launch_bounds__(kChi2Lanes) void ba_chi2_kernel(BaParams P, double lambda, int mode) {
-    __shared__ double st[kChi2MaxItems];
-    __shared__ double red[2][kNT];
+// landmarks; sum 1) in the oracle's tree4096 order: kWG workgroups per sum, lane u of workgroup g holds leaf
+// g + kWG u and adds its items k = leaf + 4096 m in order (~19 / ~28 per lane for a configs[2] window, all loaded
+// before the additions; consecutive lanes read consecutive items), the local levels run in the workgroup and its class total is
+// published; the last workgroup of the launch (grouped counters) runs both sums' top levels and then (device control)
+// decides the trial or starts the solve, or (host control) leaves chi2 / scale in scal[0] / scal[1].
+// mode 0: the solve's first chi2; 1: a trial. (Rounds 4-5 used 256 chains of 300-450 dependent additions: 14 us.)
+__global__ __launch_bounds__(kWLanes) void ba_chi2_kernel(BaParams P, double lambda, int mode) {
+    __shared__ double red[kWLanes];
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    if (P.lam) lambda = *P.lam;
     const int t = threadIdx.x;
-    const int sum = blockIdx.x / kNT, c = blockIdx.x - sum * kNT;
-    const int ns = P.ns;
-    const int N = sum == 0 ? P.E : ns + 3 * P.L;
-    const int R = c < N ? (N - 1 - c) / kNT + 1 : 0;  // this chain's items: c + 256 r, r < R
-    // chain c's items, contiguous (chain_pos): |e|^2 per edge (ba_step_kernel / ba_edge_chi2_kernel) or the LM
-    // scale's x (lambda x + b) per variable (ba_step_kernel)
-    const double* src = (sum == 0 ? P.e2 : P.sc1) + (int64_t)c * ((N + kNT - 1) / kNT);
+    const int sum = blockIdx.x / kWG, g = blockIdx.x - sum * kWG;
+    const int N = sum == 0 ? P.E : P.ns + 3 * P.L;
+    const double* src = sum == 0 ? P.e2 : P.sc1;  // |e|^2 per edge / the scale's item per variable (ba_step_kernel)
     double acc = 0.0;
-    for (int r0 = 0; r0 < R; r0 += kChi2MaxItems) {
-        const int m = min(kChi2MaxItems, R - r0);
-        double v[8];
+    // a lane's items in batches of 32, every load of a batch issued before its additions (one latency per batch:
+    // a configs[2] window's sums need one)
+    for (int k0 = g + kWG * t; k0 < N; k0 += 32 * kWLeaves) {
+        double v[32];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = t + kChi2Lanes * u;
-            v[u] = 0.0;
-            if (i < m) v[u] = src[r0 + i];
-        }
+        for (int u = 0; u < 32; ++u) v[u] = k0 + u * kWLeaves < N ? src[k0 + u * kWLeaves] : 0.0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) st[t + kChi2Lanes * u] = v[u];
-        __syncthreads();
-        if (t == 0) {
-            int i = 0;
-            if (m >= 8) {
-                double d[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) d[u] = st[u];
-                for (; i + 16 <= m; i += 8) {
-                    double e[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) e[u] = st[i + 8 + u];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) acc = acc + d[u];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) d[u] = e[u];
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) acc = acc + d[u];
-                i += 8;
-            }
-            for (; i < m; ++i) acc = acc + st[i];
-        }
-        __syncthreads();
+        for (int u = 0; u < 32; ++u)
+            if (k0 + u * kWLeaves < N) acc = acc + v[u];
     }
-    if (t == 0) st_agent(&P.part[sum * kNT + c], acc);
+    red[t] = acc;
+    wide_local_tree<1>(red);
+    if (t == 0) st_agent(&P.part[sum * kWG + g], red[0]);
     if (!ba_last_block_h(P.ticket + 1, P.ticket + 4 + kTicketGroups)) return;
-#pragma unroll
-    for (int u = 0; u < kNT / kChi2Lanes; ++u) {
-        red[0][t + kChi2Lanes * u] = ld_agent(&P.part[t + kChi2Lanes * u]);
-        red[1][t + kChi2Lanes * u] = mode ? ld_agent(&P.part[kNT + t + kChi2Lanes * u]) : 0.0;
-    }
-    __syncthreads();
-    for (int off = kNT / 2; off > 0; off >>= 1) {
-        for (int i = t; i < off; i += kChi2Lanes) {
-            red[0][i] = red[0][i] + red[0][i + off];
-            red[1][i] = red[1][i] + red[1][i + off];
-        }
-        __syncthreads();
-    }
     if (t != 0) return;
-    const double chi2 = red[0][0], scale = red[1][0];
+    const double chi2 = wide_top_tree(P.part, 1);
+    const double scale = mode ? wide_top_tree(P.part + kWG, 1) : 0.0;
     if (!P.ctl) {
         P.scal[0] = chi2;
         if (mode) P.scal[1] = scale;
@@ -1320,12 +1306,12 @@ void launch_ba_trial(const BaParams& P, const BaMat3& K, double lambda, hipStrea
     launch_ba_ldlt(P, s);
     hipLaunchKernelGGL(ba::ba_step_kernel, dim3(std::max(1, (P.L + 255) / 256)), dim3(256),
                        sizeof(double) * 7 * P.P, s, P, K, lambda);
-    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(2 * ba::kNT), dim3(ba::kChi2Lanes), 0, s, P, lambda, 1);
+    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(2 * ba::kWG), dim3(ba::kWLanes), 0, s, P, lambda, 1);
 }
 
 void launch_ba_chi2(const BaParams& P, const BaMat3& K, hipStream_t s) {
     if (P.E > 0) hipLaunchKernelGGL(ba::ba_edge_chi2_kernel, dim3((P.E + 255) / 256), dim3(256), 0, s, P, K);
-    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(ba::kNT), dim3(ba::kChi2Lanes), 0, s, P, 0.0, 0);
+    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(ba::kWG), dim3(ba::kWLanes), 0, s, P, 0.0, 0);
 }
 
 void launch_ba_finish(const BaParams& P, hipStream_t s) {
@@ -1468,7 +1454,7 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
     rc |= ba_alloc(b, &Q.xl, 3 * L);
     rc |= ba_alloc(b, &Q.tr, ns);
     rc |= ba_alloc(b, &Q.scal, 16);
-    rc |= ba_alloc(b, &Q.e2, E + 256);        // chain-major: 256 x ceil(E / 256)
+    rc |= ba_alloc(b, &Q.e2, E);
     rc |= ba_alloc(b, &Q.sc1, ns + 3 * L + 256);
     rc |= ba_alloc(b, &b->d_maxdiag, 1);
     rc |= ba_alloc(b, &b->d_ctl, 1);
