@@ -97,3 +97,31 @@ def test_sequence_device_window_equals_host_assembly(ctx):
         np.testing.assert_array_equal(r_dev[g].X, r_host[g].X)
         np.testing.assert_array_equal(r_dev[g].uv_own, r_host[g].uv_own)
         np.testing.assert_array_equal(r_dev[g].uv_prev, r_host[g].uv_prev)
+
+
+@pytest.mark.gpu
+def test_window_solve_begin_end_guards(ctx):
+    """yv_ba_window_solve_begin / _end (the sequence's asynchronous window solve): while a solve is pending the window
+    refuses reads, records, a second begin and a second end (YV_ERR_INVALID), and after the end it reads the refined
+    records."""
+    import torch
+    n, chunk = 40, 20
+    frames = synth_sequence(73, n, stereo=True)
+    d = torch.from_numpy(frames.reshape(2 * n, *frames.shape[2:])).to("cuda:0")
+    fe = SequenceFrontend(ctx, chunk, scene.K_KITTI, T_RIGHT, device_window=True)
+    try:
+        fe.process_chunk(d[:2 * chunk])
+        assert fe._ba_pending  # the chunk's window solve was begun and not collected
+        with pytest.raises(RuntimeError):
+            fe.win.read(0)
+        with pytest.raises(RuntimeError):
+            fe.win.solve_begin(0, chunk, 2, scene.K_KITTI, 10)
+        solved, log, it = fe.win.solve_end()
+        fe._ba_pending = False
+        assert solved and it >= 1 and len(log) == it + 1
+        with pytest.raises(RuntimeError):
+            fe.win.solve_end()
+        T, e, X, uo, up = fe.win.read(chunk - 1)
+        assert np.all(np.isfinite(T))
+    finally:
+        fe.close()

@@ -175,9 +175,11 @@ class SequenceFrontend:
 
     @property
     def records(self) -> Dict[int, FrameRecord]:
-        """frame -> FrameRecord (device window: read back from the records in HBM, as they stand)."""
+        """frame -> FrameRecord (device window: read back from the records in HBM after the pending window solve,
+        which the window refuses to be read during)."""
         if self.win is None:
             return self._records
+        self.flush()
         out = {}
         for g in range(self.next_frame):
             T, e, X, uo, up = self.win.read(g)
