@@ -374,7 +374,7 @@ def cpu_baseline(kind, threads, offsets, images, B, gpu_poses, edges, literal_fr
 
     def both_orders(k):
         X, uv = eX[k, :ec[k]], euv[k, :ec[k]]
-        return (orc.pose_lm(X, uv, scene.K_KITTI, prior, yv.lm_sum_mode())[0],
+        return (orc.pose_lm(X, uv, scene.K_KITTI, prior, yv.track_lm_sum_mode(len(ec)))[0],
                 orc.pose_lm(X, uv, scene.K_KITTI, prior, 0)[0])
 
     with ThreadPoolExecutor(threads) as ex:
@@ -388,7 +388,7 @@ def cpu_baseline(kind, threads, offsets, images, B, gpu_poses, edges, literal_fr
     try:
         with ThreadPoolExecutor(threads) as ex:
             libm = np.array(list(ex.map(
-                lambda k: orc.pose_lm(eX[k, :ec[k]], euv[k, :ec[k]], scene.K_KITTI, prior, yv.lm_sum_mode())[0],
+                lambda k: orc.pose_lm(eX[k, :ec[k]], euv[k, :ec[k]], scene.K_KITTI, prior, yv.track_lm_sum_mode(len(ec)))[0],
                 range(len(ec)))))
     finally:
         orc.set_libm_flavour(0)

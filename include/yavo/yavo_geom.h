@@ -56,11 +56,13 @@ int yv_pose_lm_batch(struct yv_ctx* ctx, int n_problems, const int32_t* d_offset
                      const double* d_uv, const double* d_K, double* d_poses, uint8_t* d_outlier,
                      int32_t* d_inliers, void* stream);
 /* The order in which the pose-LM kernel sums over edges, as the oracle's sum_mode (oracle/yavo_oracle.h:
- * 4 / 5 / 6 / 7 = 64- / 128- / 256- / 512-thread workgroups). yv_lm_sum_mode: the batch's track LM (256 threads).
- * yv_pose_lm_sum_mode(n): yv_pose_lm (n = 1) and yv_pose_lm_batch with n problems (512 threads up to 256 problems,
- * where the call's latency is set by one problem per CU; 256 above). Results are bit-identical to the oracle in
- * that order and within 1e-9 of the reference's sequential order. */
+ * 4 / 5 / 6 / 7 = 64- / 128- / 256- / 512-thread workgroups). yv_lm_sum_mode: the track LM of a batch of more than
+ * 256 tracks (256 threads). yv_track_lm_sum_mode(n): the track LM of a batch of n tracks (yv_batch_create's
+ * n_tracks; 512 threads up to 256 tracks, 256 above). yv_pose_lm_sum_mode(n): yv_pose_lm (n = 1) and
+ * yv_pose_lm_batch with n problems (the same rule: with few problems the call's latency is set by one problem per
+ * CU). Results are bit-identical to the oracle in that order and within 1e-9 of the reference's sequential order. */
 int yv_lm_sum_mode(void);
+int yv_track_lm_sum_mode(int n_tracks);
 int yv_pose_lm_sum_mode(int n_problems);
 int yv_pose_gn_batch(struct yv_ctx* ctx, int n_problems, const int32_t* d_offsets, const double* d_X,
                      const double* d_uv, const double* d_K, double* d_poses, int32_t* d_iterations, void* stream);
@@ -183,6 +185,9 @@ typedef struct yv_ba_window yv_ba_window;
 /* max_lm: landmark slots per frame (the batch's max_kp); max_kf: keyframes per added block */
 int yv_ba_window_create(yv_ba* ba, int max_lm, int max_kf, yv_ba_window** out);
 void yv_ba_window_destroy(yv_ba_window* w);
+/* size the record store for n_frames frames from the first recorded one (it grows by doubling from 64 otherwise, and
+ * each growth allocates, copies and synchronises the device inside the frame loop) */
+int yv_ba_window_reserve(yv_ba_window* w, int64_t n_frames);
 /* record the frames [first_frame, first_frame + n_frames) of a placed map block (yv_map_place; every frame a
  * keyframe) on `stream` (NULL: the context's): T_wc, landmarks, uv_prev = edge_uv[k][e], uv_own =
  * matches[2 k][edge_query[k][e]].pt2 with e = landmark id & 0xFFFF and k the frame's track (device pointers of

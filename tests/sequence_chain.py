@@ -28,7 +28,7 @@ def oracle_sequence(orc, frames, chunk, K, T_right, offsets, n_fixed=2, ba_iters
 
     def track(g):
         kq = kl[g - 1] if g > 0 else empty
-        X, uv, q, T, out, inl = track_pose(orc, kq, kl[g], kr[g], K, T_right)
+        X, uv, q, T, out, inl = track_pose(orc, kq, kl[g], kr[g], K, T_right, n_tracks=chunk)  # chunk tracks per batch
         own = np.zeros((max_kp, 2), np.int32)
         if len(kq):
             mt = orc.match(kq, kl[g])

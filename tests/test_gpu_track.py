@@ -58,7 +58,8 @@ def test_track_matches_oracle(ctx, oracle, offsets, overlap):
         P = d_pose.cpu().numpy()
         for k in range(n_frames):
             kq = (prev_left if prev_left is not None else kps[0][:0]) if k == 0 else kps[2 * (k - 1)]
-            X, uv, q, T, out, oinl = track_pose(oracle, kq, kps[2 * k], kps[2 * k + 1], scene.K_KITTI, T_RIGHT)
+            X, uv, q, T, out, oinl = track_pose(oracle, kq, kps[2 * k], kps[2 * k + 1], scene.K_KITTI, T_RIGHT,
+                                                n_tracks=n_frames)
             assert cnt[k] == len(X), (run, k)
             base = k * 2000
             gX = ctx.download(v.edge_X + base * 24, np.float64, 3 * cnt[k]).reshape(-1, 3)
@@ -123,7 +124,7 @@ def test_track_overlap_pipelined(ctx, oracle, offsets, monkeypatch, build_async)
                 kq = kp[i - 1][2 * (n_frames - 1)] if i > 0 else kp[0][0][:0]
             else:
                 kq = kp[i][2 * (k - 1)]
-            T = track_pose(oracle, kq, kp[i][2 * k], kp[i][2 * k + 1], scene.K_KITTI, T_RIGHT)[3]
+            T = track_pose(oracle, kq, kp[i][2 * k], kp[i][2 * k + 1], scene.K_KITTI, T_RIGHT, n_tracks=n_frames)[3]
             np.testing.assert_array_equal(P[k], T)
     b.close()
 
@@ -159,7 +160,7 @@ def test_track_lk_mode_matches_oracle(ctx, oracle, offsets):
     P = d_pose.cpu().numpy()
     for t, k in enumerate(range(1, n_frames)):
         X, uv, q, T, out, inl = lk_track_pose(oracle, frames[2 * (k - 1)], frames[2 * k], kps[2 * (k - 1)],
-                                              kps[2 * (k - 1) + 1], scene.K_KITTI, T_RIGHT)
+                                              kps[2 * (k - 1) + 1], scene.K_KITTI, T_RIGHT, n_tracks=nt)
         assert cnt[t] == len(X) > 500
         base = t * 2000
         np.testing.assert_array_equal(ctx.download(v.edge_X + base * 24, np.float64, 3 * cnt[t]).reshape(-1, 3), X)
@@ -193,7 +194,8 @@ def test_frame_shard_lk_halo_tracks_the_boundary_pair(ctx, oracle, offsets):
     kps = [(oracle.brief(L, oracle.fast(L, 2000)[0], offsets), oracle.brief(R, oracle.fast(R, 2000)[0], offsets))
            for L, R in seq]
     for k in range(B):  # track k: frame first + k - 1 (seq[k]) -> frame first + k (seq[k + 1])
-        T = lk_track_pose(oracle, seq[k][0], seq[k + 1][0], kps[k][0], kps[k][1], scene.K_KITTI, T_RIGHT)[3]
+        T = lk_track_pose(oracle, seq[k][0], seq[k + 1][0], kps[k][0], kps[k][1], scene.K_KITTI, T_RIGHT,
+                          n_tracks=shard.n_tracks)[3]
         np.testing.assert_array_equal(P[k], T, err_msg=f"track {k}")
     shard.close()
 

@@ -11,9 +11,13 @@ import time
 
 import numpy as np
 
-from ya_vo_amd import MATCH_DTYPE, lm_sum_mode
+from ya_vo_amd import MATCH_DTYPE, lm_sum_mode, track_lm_sum_mode
 
-lm_sum_mode_default = lm_sum_mode  # the pose-LM kernel's edge-sum order (yv_lm_sum_mode)
+
+def lm_sum_mode_default(n_tracks=None):
+    """The batch track LM's edge-sum order for a batch of n_tracks tracks (yv_track_lm_sum_mode: 512-thread
+    workgroups up to 256 tracks); None: a batch of more than 256 (yv_lm_sum_mode)."""
+    return lm_sum_mode() if n_tracks is None else track_lm_sum_mode(n_tracks)
 
 IDENTITY = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
 
@@ -80,11 +84,13 @@ def track_edges(orc, kq, kl, kr, K, T_right, thr=20, timers=None, init_timers=No
     return X[ok], uv, q
 
 
-def track_pose(orc, kq, kl, kr, K, T_right, prior=IDENTITY, thr=20, sum_mode=None, timers=None, init_timers=None):
-    """track_edges + optimizePoseOnly in `sum_mode` (None: the GPU kernel's order; 0: the reference's sequential
-    order).  timers: as track_edges, plus "pose_lm"; init_timers: as track_edges."""
+def track_pose(orc, kq, kl, kr, K, T_right, prior=IDENTITY, thr=20, sum_mode=None, timers=None, init_timers=None,
+               n_tracks=None):
+    """track_edges + optimizePoseOnly in `sum_mode` (None: the GPU kernel's order for a batch of n_tracks tracks,
+    lm_sum_mode_default; 0: the reference's sequential order).  timers: as track_edges, plus "pose_lm"; init_timers:
+    as track_edges."""
     if sum_mode is None:
-        sum_mode = lm_sum_mode()
+        sum_mode = lm_sum_mode_default(n_tracks)
     X, uv, q = track_edges(orc, kq, kl, kr, K, T_right, thr, timers, init_timers)
     t0 = time.perf_counter()
     T, out, inl = orc.pose_lm(X, uv, K, prior, sum_mode)
@@ -93,13 +99,14 @@ def track_pose(orc, kq, kl, kr, K, T_right, prior=IDENTITY, thr=20, sum_mode=Non
 
 
 def lk_track_pose(orc, img_prev, img_next, kl, kr, K, T_right, prior=IDENTITY, thr=20, lk_sum_mode=1,
-                  lm_sum_mode=None):
+                  lm_sum_mode=None, n_tracks=None):
     """The reference's trackLastFrame + optimizePoseOnly (src/LoopHandler.cc:298-454, 730-861) with frame k-1's
     map points from its stereo pair: kept stereo matches triangulated (left camera = world), tracked by
     calcOpticalFlowPyrLK into frame k, status-1 points at cv::Point2i(next.y, next.x) (truncation).
+    lm_sum_mode None: the GPU kernel's order for a batch of n_tracks tracks (lm_sum_mode_default).
     -> (X [n,3], uv [n,2], query index [n], T, outlier, inliers)."""
     if lm_sum_mode is None:
-        lm_sum_mode = lm_sum_mode_default()
+        lm_sum_mode = lm_sum_mode_default(n_tracks)
     if len(kl) == 0:
         e = np.zeros((0, 3)), np.zeros((0, 2)), np.zeros(0, np.int32)
         return (*e, *orc.pose_lm(e[0], e[1], K, prior, lm_sum_mode))

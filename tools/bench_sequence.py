@@ -63,7 +63,7 @@ def measure(frames=200, chunk=20, n_fixed=2, ba_iters=10, repeats=3, cpu_threads
 
     def run():
         fe = SequenceFrontend(ctx, chunk, K, t_right, n_fixed=n_fixed, ba_iters=ba_iters, H=H, W=W,
-                              device_window=not host_window, ba_priority=ba_priority)
+                              device_window=not host_window, ba_priority=ba_priority, expected_frames=n)
         sec = {}
         torch.cuda.synchronize()
         t0 = time.perf_counter()

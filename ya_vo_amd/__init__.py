@@ -131,6 +131,7 @@ GEOM_SIGNATURES = {
     "yv_ba_set_control": (_I, [_P, _I]),
     "yv_ba_window_create": (_I, [_P, _I, _I, ctypes.POINTER(_P)]),
     "yv_ba_window_destroy": (None, [_P]),
+    "yv_ba_window_reserve": (_I, [_P, ctypes.c_int64]),
     "yv_ba_window_add_block": (_I, [_P, _P, ctypes.c_int64, _I, _P, _P, _P, _I, _P]),
     "yv_ba_window_solve": (_I, [_P, ctypes.c_int64, _I, _I, _P, _I, _P, _P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "yv_ba_window_solve_begin": (_I, [_P, ctypes.c_int64, _I, _I, _P, _I, _P]),
@@ -139,6 +140,7 @@ GEOM_SIGNATURES = {
     "yv_ba_window_trajectory": (_I, [_P, ctypes.c_int64, _I, _P]),
     "yv_lm_sum_mode": (_I, []),
     "yv_pose_lm_sum_mode": (_I, [_I]),
+    "yv_track_lm_sum_mode": (_I, [_I]),
 }
 
 # include/yavo/yavo_map.h (the shared map; ya_vo_amd/map.py wraps the block layout)
@@ -209,6 +211,11 @@ def lm_sum_mode(n_problems=None) -> int:
     (yv_pose_lm_sum_mode)."""
     lib = load_library()
     return int(lib.yv_lm_sum_mode() if n_problems is None else lib.yv_pose_lm_sum_mode(int(n_problems)))
+
+
+def track_lm_sum_mode(n_tracks) -> int:
+    """The batch track LM's edge-sum order (oracle sum_mode) for a batch of n_tracks tracks (yv_track_lm_sum_mode)."""
+    return int(load_library().yv_track_lm_sum_mode(int(n_tracks)))
 
 
 def _check(status: int, what: str) -> None:
@@ -712,6 +719,10 @@ class BaWindow:
             self.close()
         except Exception:
             pass
+
+    def reserve(self, n_frames: int) -> None:
+        """Size the record store for n_frames frames up front (yv_ba_window_reserve: no growth inside the loop)."""
+        _check(self.lib.yv_ba_window_reserve(self.handle, int(n_frames)), "yv_ba_window_reserve")
 
     def add_block(self, d_block: int, first_frame: int, n_frames: int, d_edge_uv: int, d_edge_query: int,
                   d_matches: int, max_kp: int, stream: int = 0) -> None:

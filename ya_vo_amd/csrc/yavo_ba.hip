@@ -1462,6 +1462,19 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
         rc = YV_ERR_HIP;
     if (rc == YV_OK && hipHostMalloc(reinterpret_cast<void**>(&b->h_ctl), sizeof(yavo::BaCtl)) != hipSuccess)
         rc = YV_ERR_HIP;
+    // sized up front where that is small, so a solve loop's first iterations do not allocate (each growth
+    // synchronises the stream and frees device memory, which synchronises the device): the Schur partials of up to 64
+    // free poses, the window graph's co-visibility lists (3 per landmark) and a 64-iteration chi2 log
+    if (rc == YV_OK && max_poses <= 64) rc |= ba_ensure_schur(b, max_poses, b->st);
+    if (rc == YV_OK && max_landmarks > 0) {
+        rc |= ba_alloc(b, &b->d_cv_e1, 3 * L);
+        rc |= ba_alloc(b, &b->d_cv_e2, 3 * L);
+        if (rc == YV_OK) b->cv_cap = 3 * (int64_t)L;
+    }
+    if (rc == YV_OK) {
+        rc |= ba_alloc(b, &b->d_log, 65);
+        if (rc == YV_OK) b->log_cap = 65;
+    }
     if (rc == YV_OK && (hipMemsetAsync(b->d_ticket, 0, kBaTickets * sizeof(unsigned), b->st) != hipSuccess ||
                         hipMemsetAsync(b->d_cur, 0, sizeof(int), b->st) != hipSuccess ||
                         hipStreamSynchronize(b->st) != hipSuccess))
@@ -2015,6 +2028,7 @@ struct yv_ba_window {
     yv_ba* ba = nullptr;
     int max_lm = 0, max_kf = 0;
     int64_t g0 = -1, cap = 0;  // store index 0 = frame g0; frames [g0, g0 + cap) fit
+    int64_t hint = 0;          // yv_ba_window_reserve: frames the store is first sized for
     double *d_T = nullptr, *d_X = nullptr, *d_uvo = nullptr, *d_uvp = nullptr;
     int32_t *d_cnt = nullptr, *d_edge = nullptr;
     int64_t* d_info = nullptr;  // [1 + 2 max_kf]: n_kf, (frame, count) per keyframe of the last block
@@ -2046,7 +2060,7 @@ int win_reserve(yv_ba_window* w, int64_t first, int64_t end, hipStream_t st) {
     if (w->g0 < 0) w->g0 = first;
     if (first < w->g0) return YV_ERR_INVALID;
     if (end - w->g0 <= w->cap) return YV_OK;
-    int64_t cap = std::max<int64_t>(64, w->cap);
+    int64_t cap = std::max<int64_t>(std::max<int64_t>(64, w->hint), w->cap);
     while (cap < end - w->g0) cap *= 2;
     const int64_t M = w->max_lm;
     double *T = nullptr, *X = nullptr, *uvo = nullptr, *uvp = nullptr;
@@ -2108,12 +2122,16 @@ extern "C" int yv_ba_window_create(yv_ba* ba, int max_lm, int max_kf, yv_ba_wind
     w->ba = ba;
     w->max_lm = max_lm;
     w->max_kf = max_kf;
+    // the graph offsets of the largest window the yv_ba takes: pe_off [P + 1], cv_off [P P + 1]
+    const size_t P = (size_t)std::min(ba->max_poses, kWinMaxPoses), need = (P + 1) + P * P + 1;
     if (hipMalloc(reinterpret_cast<void**>(&w->d_info), sizeof(int64_t) * (1 + 2 * (size_t)max_kf)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&w->h_info), sizeof(int64_t) * (1 + 2 * (size_t)max_kf)) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&w->h_struct), sizeof(int32_t) * need) != hipSuccess ||
         hipEventCreateWithFlags(&w->added, hipEventDisableTiming) != hipSuccess) {
         yv_ba_window_destroy(w);
         return YV_ERR_HIP;
     }
+    w->h_struct_cap = need;
     *out = w;
     return YV_OK;
 }
@@ -2131,6 +2149,14 @@ extern "C" void yv_ba_window_destroy(yv_ba_window* w) {
     if (w->h_info) (void)hipHostFree(w->h_info);
     if (w->h_struct) (void)hipHostFree(w->h_struct);
     delete w;
+}
+
+extern "C" int yv_ba_window_reserve(yv_ba_window* w, int64_t n_frames) {
+    if (!w || n_frames < 0 || n_frames > (int64_t)1 << 24 || w->solving) return YV_ERR_INVALID;
+    w->hint = n_frames;
+    if (w->g0 < 0 || n_frames <= w->cap) return YV_OK;  // sized at the first add_block
+    if (hipSetDevice(w->ba->dev) != hipSuccess) return YV_ERR_HIP;
+    return win_reserve(w, w->g0, w->g0 + n_frames, yavo::ctx_stream(w->ba->ctx));
 }
 
 extern "C" int yv_ba_window_add_block(yv_ba_window* w, const void* d_block, int64_t first_frame, int n_frames,

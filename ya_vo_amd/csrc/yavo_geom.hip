@@ -1630,9 +1630,10 @@ __global__ __launch_bounds__(kNT) void pose_gn_kernel(const int32_t* __restrict_
 // (DESIGN.md 4.3, 10): fewer workgroups looping over the problems, LDS padding to one workgroup per CU, and a form
 // holding each problem's edges in LDS.
 constexpr int kLMThreads = 256;
-// A few problems (the host-pointer yv_pose_lm of the LoopHandler, small yv_pose_lm_batch calls) leave most CUs idle,
-// so their latency is what counts: 512 threads, two waves per SIMD of the problem's own CU, halve each thread's edge
-// share (sum order 7, yv_pose_lm_sum_mode).  The batch's tracks keep 256 (two problems per CU interleave there).
+// A few problems (the host-pointer yv_pose_lm of the LoopHandler, small yv_pose_lm_batch calls, the tracks of a small
+// batch such as the sequence front end's 20-frame chunks) leave most CUs idle, so their latency is what counts: 512
+// threads, two waves per SIMD of the problem's own CU, halve each thread's edge share (sum order 7,
+// yv_pose_lm_sum_mode / yv_track_lm_sum_mode).  Larger batches keep 256 (two problems per CU interleave there).
 constexpr int kLMThreadsWide = 512;
 constexpr int kLMWideMaxProblems = 256;
 
@@ -1724,8 +1725,12 @@ void launch_track_pose(int n_tracks, const int32_t* edge_count, int stride, cons
                        const double* edge_uv, const double* K, const double* priors, double* poses,
                        uint8_t* edge_outlier, int32_t* inliers, hipStream_t s) {
     if (n_tracks <= 0) return;
-    geom::launch_lm(n_tracks, s, static_cast<const int32_t*>(nullptr), edge_count, stride, edge_X, edge_uv, K, priors,
-                    poses, edge_outlier, inliers);
+    if (n_tracks <= geom::kLMWideMaxProblems)
+        geom::launch_lm<geom::kLMThreadsWide>(n_tracks, s, static_cast<const int32_t*>(nullptr), edge_count, stride,
+                                              edge_X, edge_uv, K, priors, poses, edge_outlier, inliers);
+    else
+        geom::launch_lm(n_tracks, s, static_cast<const int32_t*>(nullptr), edge_count, stride, edge_X, edge_uv, K,
+                        priors, poses, edge_outlier, inliers);
 }
 
 void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, const double* uv, const double* K,
@@ -1736,6 +1741,11 @@ void launch_pose_gn(const int32_t* offsets, int n_problems, const double* X, con
 }  // namespace yavo
 
 extern "C" int yv_lm_sum_mode(void) { return yavo::geom::lm_mode_of(yavo::geom::kLMThreads); }
+
+extern "C" int yv_track_lm_sum_mode(int n_tracks) {
+    return yavo::geom::lm_mode_of(n_tracks <= yavo::geom::kLMWideMaxProblems ? yavo::geom::kLMThreadsWide
+                                                                             : yavo::geom::kLMThreads);
+}
 
 extern "C" int yv_pose_lm_sum_mode(int n_problems) {
     return yavo::geom::lm_mode_of(n_problems <= yavo::geom::kLMWideMaxProblems ? yavo::geom::kLMThreadsWide

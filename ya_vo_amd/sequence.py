@@ -117,11 +117,13 @@ class SequenceFrontend:
 
     def __init__(self, ctx, chunk: int, K, T_right, n_fixed: int = 2, ba_iters: int = 10,
                  H: int = 376, W: int = 1241, max_kp: int = 2000, match_thr: int = 20, device_window: bool = True,
-                 ba_priority: int = 0):
+                 ba_priority: int = 0, expected_frames: int = 0):
         """device_window: the BA window is recorded, assembled and written back on the device (yv_ba_window_*,
         no per-chunk read-back); False: the host assembly below (window_problem / apply_window), kept as the
         restatement the device path is checked against. ba_priority: the BA stream's priority (torch's convention:
-        -1 high, 0 default) against the context stream the next chunk's kernels run on."""
+        -1 high, 0 default) against the context stream the next chunk's kernels run on. expected_frames: the
+        sequence length when known (the device window's record store is sized for it up front instead of growing by
+        doubling, which synchronises the device inside the loop)."""
         import torch
         from . import Batch, BaWindow, BundleAdjuster
         if chunk < 2 or n_fixed < 1:
@@ -162,6 +164,8 @@ class SequenceFrontend:
         self._ba_pending = False
         self.device_window = device_window
         self.win = BaWindow(self.ba, max_kp, chunk) if device_window else None
+        if self.win is not None and expected_frames > 0:
+            self.win.reserve(expected_frames)
         self._records: Dict[int, FrameRecord] = {}
         self.next_frame = 0
         self.ba_log: List[Tuple[int, int, float, float]] = []  # (last frame, iterations, chi2 first, chi2 last)
