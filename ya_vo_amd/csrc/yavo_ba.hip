@@ -3,21 +3,23 @@
 // extended to pose-landmark edges, restated like oracle/yavo_oracle_ba.c, expression for expression, in its
 // summation orders (built with -ffp-contract=off):
 //
-//   ba_linearize_kernel   one lane per edge: e, J_pose (the reference's linearizeOplus), J_point = J_pose[:, :3] R
-//                         (H_pl = J_pose^T J_point is formed from these where it is read)
-//   ba_reduce_kernel      H_pp (21) + b_p (6) per free pose in tree4096 order (32 workgroups per pose), and one lane
-//                         per landmark for H_ll, b_l (sequential over its edges); its last workgroup starts the
-//                         iteration's trial loop (device control)
+//   ba_reduce_kernel      the iteration's linearisation and blocks: H_pp (21) + b_p (6) per free pose in tree4096
+//                         order (32 workgroups per pose, each edge's e and J_pose formed on the fly), and one lane per
+//                         landmark that linearises its edges -- e, J_pose (the reference's linearizeOplus), J_point =
+//                         J_pose[:, :3] R, stored for the later kernels (H_pl = J_pose^T J_point is formed from them
+//                         where it is read) -- for H_ll, b_l (sequential over its edges); its last workgroup starts
+//                         the iteration's trial loop (device control). (Until round 5 a separate linearisation
+//                         kernel stored e / J first: 10.5 us per iteration on a configs[2] window.)
 //   ba_schur_kernel       per trial: the reduced pose system S = H_pp + lambda I - sum W H_pl^T and b_schur in tree4096
 //                         order (32 workgroups per upper 6 x 6 block or b_schur row), W = H_pl (H_ll + lambda I)^-1
 //                         formed per co-visible pair
 //   ba_ldlt_reg_kernel    one workgroup: Eigen's LDLT (diagonal pivoting) on the reduced pose system, the matrix in
-//                         registers, four-column groups handed between waves through LDS (n <= 128; ba_ldlt_kernel on
+//                         registers, column pairs handed between waves through LDS (n <= 128; ba_ldlt_kernel on
 //                         global memory above), then the solve
 //   ba_step_kernel        the trial state: T <- exp(x_p) T, x_l = Dinv (b_l - sum_e H_pl^T x_p), X <- X + x_l, the
 //                         trial's |e|^2 per edge and the LM scale's items (into the other state buffer)
 //   ba_edge_chi2_kernel   one lane per edge: |e|^2 at the current estimate (the solve's first chi2)
-//   ba_chi2_kernel        chi2 and the LM scale x.(lambda x + b) in tree256 order; its last workgroup decides the
+//   ba_chi2_kernel        chi2 and the LM scale x.(lambda x + b) in tree4096 order; its last workgroup decides the
 //                         trial (device control) or leaves both for the host
 // The LM control (lambda, rho, accept / reject) runs on the device by default (ba_ctl_*), in the host loop's
 // arithmetic; yv_ba_set_control(b, 0) runs it on the host.
@@ -62,19 +64,15 @@ __device__ __forceinline__ void ba_error(const double* T, const double* K, const
 // the state (poses, landmarks) the current estimate is in: 0 = P.poses / P.X, 1 = P.poses2 / P.X2
 __device__ __forceinline__ int ba_cur(const BaParams& P) { return P.cur ? *P.cur : 0; }
 
-__global__ __launch_bounds__(256) void ba_linearize_kernel(BaParams P, BaMat3 K) {
-    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= P.E) return;
-    const int cur = ba_cur(P);
-    const double* T = (cur ? P.poses2 : P.poses) + 7 * P.ep[e];
-    const double* X = (cur ? P.X2 : P.X) + 3 * P.el[e];
-    double err[2];
-    ba_error(T, K.v, X, P.meas + 2 * e, err);
-    double pc[3], R[9], Jp[12], Jl[6];
+// One edge's linearisation at pose T, point X: the error e = meas - proj(T X), J_pose (the reference's
+// linearizeOplus) and J_point = J_pose[:, :3] R. Every reader that needs them forms them with this function, so
+// they are the same bits wherever they are formed.
+__device__ __forceinline__ void edge_linearize(const double* T, const double* K, const double* X, const double* meas,
+                                               double* err, double* Jp, double* Jl) {
+    ba_error(T, K, X, meas, err);
+    double pc[3];
     se3_act(T, X, pc);
-    quat_to_R(T, R);
-    const double fx = K.v[0], fy = K.v[4];
+    const double fx = K[0], fy = K[4];
     const double x = pc[0], y = pc[1], z = pc[2];
     const double zinv = 1.0 / (z + 1e-18);
     const double zinv2 = zinv * zinv;
@@ -82,21 +80,16 @@ __global__ __launch_bounds__(256) void ba_linearize_kernel(BaParams P, BaMat3 K)
     Jp[4] = -fx - fx * x * x * zinv2; Jp[5] = fx * y * zinv;
     Jp[6] = 0; Jp[7] = -fy * zinv; Jp[8] = fy * y * zinv2; Jp[9] = fy + fy * y * y * zinv2;
     Jp[10] = -fy * x * y * zinv2; Jp[11] = -fy * x * zinv;
+    if (Jl) {
+        double R[9];
+        quat_to_R(T, R);
 #pragma unroll
-    for (int r = 0; r < 2; ++r)
+        for (int r = 0; r < 2; ++r)
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-            Jl[r * 3 + c] = Jp[r * 6 + 0] * R[0 * 3 + c] + Jp[r * 6 + 1] * R[1 * 3 + c] + Jp[r * 6 + 2] * R[2 * 3 + c];
-    // 16-B stores (every per-edge block is 16-B aligned). H_pl = J_pose^T J_point (6 x 3) is not stored: its readers
-    // form it from these 144 B (hpl_load), which is what storing it would cost them to read, and the 144 B/edge write
-    // is saved
-    reinterpret_cast<double2*>(P.err)[e] = make_double2(err[0], err[1]);
-    double2* jp2 = reinterpret_cast<double2*>(P.Jp + 12 * (int64_t)e);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) jp2[i] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
-    double2* jl2 = reinterpret_cast<double2*>(P.Jl + 6 * (int64_t)e);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) jl2[i] = make_double2(Jl[2 * i], Jl[2 * i + 1]);
+            for (int c = 0; c < 3; ++c)
+                Jl[r * 3 + c] =
+                    Jp[r * 6 + 0] * R[0 * 3 + c] + Jp[r * 6 + 1] * R[1 * 3 + c] + Jp[r * 6 + 2] * R[2 * 3 + c];
+    }
 }
 
 // H_pl(e) = J_pose^T J_point, the expression of the oracle's buildSystem, from the edge's stored Jacobians
@@ -250,36 +243,36 @@ __device__ __forceinline__ void atomic_max_abs(unsigned long long* m, double v) 
 //  blocks beyond:      one lane per landmark: H_ll, b_l sequential over its edges
 // first: the largest |diagonal| (free poses and landmarks) into *P.maxdiag (uint64 bits of a non-negative double).
 // Device control: the last workgroup starts the iteration's trial loop (lambda on the first iteration).
-__global__ __launch_bounds__(kWLanes) void ba_reduce_kernel(BaParams P, int first) {
+__global__ __launch_bounds__(kWLanes) void ba_reduce_kernel(BaParams P, BaMat3 K, int first) {
     __shared__ double red[27 * kWLanes];
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
     const int t = threadIdx.x;
+    const int cur = ba_cur(P);
+    const double* Tc = cur ? P.poses2 : P.poses;
+    const double* Xc = cur ? P.X2 : P.X;
     if ((int)blockIdx.x < P.np * kWG) {
         const int j = blockIdx.x / kWG, g = blockIdx.x - j * kWG, p = P.nf + j;
         const int k0 = P.pe_off[p], k1 = P.pe_off[p + 1];
+        double T[7];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) T[i] = Tc[7 * p + i];
         double h[21], gv[6];
 #pragma unroll
         for (int i = 0; i < 21; ++i) h[i] = 0.0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) gv[i] = 0.0;
+        // the pose's edges linearised here (the landmark lanes below store the same bits for the later kernels)
         for (int k = k0 + g + kWG * t; k < k1; k += kWLeaves) {
             const int e = P.pe[k];
-            double J[12];
-            const double2* jp = reinterpret_cast<const double2*>(P.Jp + 12 * (int64_t)e);
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                const double2 v = jp[i];
-                J[2 * i] = v.x;
-                J[2 * i + 1] = v.y;
-            }
-            const double2 ev = reinterpret_cast<const double2*>(P.err)[e];
+            double J[12], ev[2];
+            edge_linearize(T, K.v, Xc + 3 * (int64_t)P.el[e], P.meas + 2 * (int64_t)e, ev, J, nullptr);
             int q = 0;
 #pragma unroll
             for (int a = 0; a < 6; ++a)
 #pragma unroll
                 for (int b = a; b < 6; ++b, ++q) h[q] = h[q] + (J[a] * J[b] + J[6 + a] * J[6 + b]);
 #pragma unroll
-            for (int a = 0; a < 6; ++a) gv[a] = gv[a] + (J[a] * ev.x + J[6 + a] * ev.y);
+            for (int a = 0; a < 6; ++a) gv[a] = gv[a] + (J[a] * ev[0] + J[6 + a] * ev[1]);
         }
 #pragma unroll
         for (int i = 0; i < 21; ++i) red[i * kWLanes + t] = h[i];
@@ -309,30 +302,34 @@ __global__ __launch_bounds__(kWLanes) void ba_reduce_kernel(BaParams P, int firs
         if (l < P.L) {
             double h[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
             const int k0 = P.le_off[l], k1 = P.le_off[l + 1];
-            // the landmark's edges four at a time: indices, then every edge's J_point and error loaded before the
-            // additions (in edge order), so a batch costs one dependent load round, not one per edge
-            for (int kb = k0; kb < k1; kb += 4) {
-                int eb[4];
+            double X[3];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) eb[u] = kb + u < k1 ? P.le[kb + u] : 0;
-                double jl[4][6], er[4][2];
+            for (int c = 0; c < 3; ++c) X[c] = Xc[3 * (int64_t)l + c];
+            // the landmark's edges two at a time: indices and poses, then both linearised (error, J_pose, J_point:
+            // stored for the Schur and step kernels, 16-B stores) and added in edge order
+            for (int kb = k0; kb < k1; kb += 2) {
+                int eb[2], pb[2];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < 2; ++u) eb[u] = kb + u < k1 ? P.le[kb + u] : 0;
+#pragma unroll
+                for (int u = 0; u < 2; ++u) pb[u] = kb + u < k1 ? P.ep[eb[u]] : 0;
+                double jl[2][6], er[2][2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
                     if (kb + u < k1) {
-                        const double2* j2 = reinterpret_cast<const double2*>(P.Jl + 6 * (int64_t)eb[u]);
+                        double Jp[12];
+                        edge_linearize(Tc + 7 * (int64_t)pb[u], K.v, X, P.meas + 2 * (int64_t)eb[u], er[u], Jp, jl[u]);
+                        reinterpret_cast<double2*>(P.err)[eb[u]] = make_double2(er[u][0], er[u][1]);
+                        double2* jp2 = reinterpret_cast<double2*>(P.Jp + 12 * (int64_t)eb[u]);
 #pragma unroll
-                        for (int i = 0; i < 3; ++i) {
-                            const double2 v = j2[i];
-                            jl[u][2 * i] = v.x;
-                            jl[u][2 * i + 1] = v.y;
-                        }
-                        const double2 ev = reinterpret_cast<const double2*>(P.err)[eb[u]];
-                        er[u][0] = ev.x;
-                        er[u][1] = ev.y;
+                        for (int i = 0; i < 6; ++i) jp2[i] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
+                        double2* jl2 = reinterpret_cast<double2*>(P.Jl + 6 * (int64_t)eb[u]);
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) jl2[i] = make_double2(jl[u][2 * i], jl[u][2 * i + 1]);
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < 2; ++u) {
                     if (kb + u >= k1) break;
 #pragma unroll
                     for (int a = 0; a < 3; ++a) {
@@ -1287,9 +1284,8 @@ void launch_ba_ctl_resume(BaCtl* c, hipStream_t s) {
 }
 
 void launch_ba_linearize(const BaParams& P, const BaMat3& K, int first, hipStream_t s) {
-    if (P.E > 0) hipLaunchKernelGGL(ba::ba_linearize_kernel, dim3((P.E + 255) / 256), dim3(256), 0, s, P, K);
     const int nb = std::max(1, P.np * ba::kWG + (P.L + ba::kWLanes - 1) / ba::kWLanes);
-    hipLaunchKernelGGL(ba::ba_reduce_kernel, dim3(nb), dim3(ba::kWLanes), 0, s, P, first);
+    hipLaunchKernelGGL(ba::ba_reduce_kernel, dim3(nb), dim3(ba::kWLanes), 0, s, P, K, first);
 }
 
 void launch_ba_ldlt(const BaParams& P, hipStream_t s) {
