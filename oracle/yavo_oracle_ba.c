@@ -22,13 +22,19 @@
  *   tree4096  values indexed k = 0 .. n-1: partial[t] = sum of items k = t mod 4096 in ascending k (from 0.0), then
  *             p[t] += p[t + off], off = 2048 .. 1; used for each pose's H_pp / b_p over its edges (edge order), for
  *             each Schur block entry's sum over the co-visible pairs of its two poses (landmark order), v = base -
- *             total, for each b_schur entry's sum over the pose's edges (edge order), for chi2 over all edges and for
- *             the LM scale over all variables (poses, then landmarks)
+ *             total, for each b_schur entry's sum over the pose's edges (edge order)
+ *   landmark blocks  chi2 and the landmarks' part of the LM scale: per landmark a sequential sum from 0.0 (|e|^2 over
+ *             its edges in edge order / its three x (lambda x + b) items), blocks of 256 landmarks as a halving tree
+ *             over 256 slots (0.0 past L), block totals into 256 leaves (block b into leaf b mod 256, ascending b,
+ *             from 0.0), a halving tree over the leaves; the scale = (the free poses' items in tree256 order: leaf
+ *             t = items j = t mod 256 ascending, halving tree) + (the landmark part)
  *   sequential per landmark over its edges (edge order) for H_ll / b_l and the back-substitution
  * (Rounds 1-4 summed the Schur and b_schur entries as one sequential chain each, and H_pp / b_p, chi2 and the scale
  * in a 256-leaf tree. A 3,800-term chain is latency-bound on one GPU lane, and 256 leaves leave each GPU lane ~15
  * dependent loads (and chi2's chains 300-450 dependent additions); with 4096 leaves a configs[2] window's sums have
- * at most one item per leaf for the blocks and ~28 for chi2, so the loads are in flight at once.)
+ * at most one item per leaf for the blocks and ~28 for chi2, so the loads are in flight at once. Round 5 then moved
+ * chi2 and the scale to the landmark-block order: the GPU's step kernel, one lane per landmark, sums them where it
+ * forms the trial state, without a separate pass over the stored |e|^2 and scale items.)
  */
 #include "yavo_oracle.h"
 
@@ -232,17 +238,38 @@ static void ba_free_struct(ba_struct* s) {
     free(s->cv_off); free(s->cv_l); free(s->cv_e1); free(s->cv_e2);
 }
 
-static double ba_chi2(const ba_struct* s, const double* poses, const double* X) {
-    tree4096* t = (tree4096*)malloc(sizeof(tree4096));
-    w_reset(t);
-    for (int e = 0; e < s->E; ++e) {
-        double r[2];
-        ba_error(poses + 7 * s->ep[e], s->K, X + 3 * s->el[e], s->meas + 2 * e, r);
-        w_add(t, e, r[0] * r[0] + r[1] * r[1]);
+/* the halving tree over 256 values: v[t] += v[t + off], off = 128 .. 1 */
+static double tree256(double* v) {
+    for (int off = 128; off > 0; off >>= 1)
+        for (int t = 0; t < off; ++t) v[t] = v[t] + v[t + off];
+    return v[0];
+}
+
+/* landmark-block order: c[l] per landmark; block b = landmarks [256 b, 256 b + 256) summed as tree256 over its slots
+ * (0.0 past L); leaf t = the block totals b = t mod 256 in ascending b (from 0.0); tree256 over the leaves */
+static double lblock_total(const double* c, int L) {
+    double leaf[256], v[256];
+    for (int t = 0; t < 256; ++t) leaf[t] = 0.0;
+    for (int b = 0; 256 * b < L; ++b) {
+        for (int t = 0; t < 256; ++t) v[t] = 256 * b + t < L ? c[256 * b + t] : 0.0;
+        leaf[b % 256] = leaf[b % 256] + tree256(v);
     }
-    const double v = w_total(t);
-    free(t);
-    return v;
+    return tree256(leaf);
+}
+
+/* chi2 in the landmark-block order of c[l] = 0.0 + |e|^2 over the landmark's edges (edge order); c: [L] scratch */
+static double ba_chi2(const ba_struct* s, const double* poses, const double* X, double* c) {
+    for (int l = 0; l < s->L; ++l) {
+        double acc = 0.0;
+        for (int k = s->le_off[l]; k < s->le_off[l + 1]; ++k) {
+            const int e = s->le[k];
+            double r[2];
+            ba_error(poses + 7 * s->ep[e], s->K, X + 3 * l, s->meas + 2 * e, r);
+            acc = acc + (r[0] * r[0] + r[1] * r[1]);
+        }
+        c[l] = acc;
+    }
+    return lblock_total(c, s->L);
 }
 
 /* diagnostics (tests only): when or_ba_dump_iter >= 0, the first damping trial of that iteration copies its
@@ -279,7 +306,8 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
     double* bak_p = (double*)malloc(sizeof(double) * 7 * (size_t)P);
     double* bak_X = (double*)malloc(sizeof(double) * 3 * (size_t)L);
     tree4096* wt = (tree4096*)malloc(sizeof(tree4096));
-    double currentChi = ba_chi2(&s, poses, X);
+    double* lsum = (double*)malloc(sizeof(double) * (size_t)(L > 0 ? L : 1));
+    double currentChi = ba_chi2(&s, poses, X, lsum);
     if (chi2_log) chi2_log[0] = currentChi;
     double lambda = 0, ni = 2;
     int it;
@@ -424,14 +452,21 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
             if (dump) {
                 ba_dump(13, xl, 3 * (size_t)L); ba_dump(14, poses, 7 * (size_t)P); ba_dump(15, X, 3 * (size_t)L);
             }
-            double tempChi = ba_chi2(&s, poses, X);
+            double tempChi = ba_chi2(&s, poses, X, lsum);
             if (!ok2) tempChi = DBL_MAX;
             rho = currentChi - tempChi;
-            /* computeScale over the variables (poses, then landmarks), tree4096 order */
-            w_reset(wt);
-            for (int j = 0; j < ns; ++j) w_add(wt, j, xp[j] * (lambda * xp[j] + bp[6 * n_fixed + j]));
-            for (int j = 0; j < 3 * L; ++j) w_add(wt, ns + j, xl[j] * (lambda * xl[j] + bl[j]));
-            double scale = w_total(wt);
+            /* computeScale over the variables: the free poses' items in tree256 order (leaf t = items j = t mod 256
+             * ascending from 0.0), plus the landmarks' in the landmark-block order of 0.0 + their three items */
+            double leaf[256];
+            for (int t = 0; t < 256; ++t) leaf[t] = 0.0;
+            for (int j = 0; j < ns; ++j) leaf[j % 256] = leaf[j % 256] + xp[j] * (lambda * xp[j] + bp[6 * n_fixed + j]);
+            const double pose_part = tree256(leaf);
+            for (int l = 0; l < L; ++l) {
+                double acc = 0.0;
+                for (int c = 0; c < 3; ++c) acc = acc + xl[3 * l + c] * (lambda * xl[3 * l + c] + bl[3 * l + c]);
+                lsum[l] = acc;
+            }
+            double scale = pose_part + lblock_total(lsum, L);
             scale += 1e-3;
             rho /= scale;
             if (rho > 0 && isfinite(tempChi)) {
@@ -456,7 +491,7 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
         }
     }
     free(Jp); free(Jl); free(err); free(Hpl); free(W); free(Hpp); free(bp); free(Hll); free(bl); free(Dinv);
-    free(S); free(bs); free(xp); free(xl); free(bak_p); free(bak_X); free(wt);
+    free(S); free(bs); free(xp); free(xl); free(bak_p); free(bak_X); free(wt); free(lsum);
     ba_free_struct(&s);
     return it;
 }

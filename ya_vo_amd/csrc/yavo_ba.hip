@@ -16,11 +16,11 @@
 //   ba_ldlt_reg_kernel    one workgroup: Eigen's LDLT (diagonal pivoting) on the reduced pose system, the matrix in
 //                         registers, column pairs handed between waves through LDS (n <= 128; ba_ldlt_kernel on
 //                         global memory above), then the solve
-//   ba_step_kernel        the trial state: T <- exp(x_p) T, x_l = Dinv (b_l - sum_e H_pl^T x_p), X <- X + x_l, the
-//                         trial's |e|^2 per edge and the LM scale's items (into the other state buffer)
-//   ba_edge_chi2_kernel   one lane per edge: |e|^2 at the current estimate (the solve's first chi2)
-//   ba_chi2_kernel        chi2 and the LM scale x.(lambda x + b) in tree4096 order; its last workgroup decides the
-//                         trial (device control) or leaves both for the host
+//   ba_step_kernel        the trial state: T <- exp(x_p) T, x_l = Dinv (b_l - sum_e H_pl^T x_p), X <- X + x_l (into
+//                         the other state buffer), and the trial's chi2 and LM scale x.(lambda x + b) in the
+//                         landmark-block order (one lane per landmark); its last workgroup decides the trial (device
+//                         control) or leaves both for the host
+//   ba_chi2_kernel        the solve's first chi2 in the same order
 // The LM control (lambda, rho, accept / reject) runs on the device by default (ba_ctl_*), in the host loop's
 // arithmetic; yv_ba_set_control(b, 0) runs it on the host.
 #include <hip/hip_runtime.h>
@@ -1047,117 +1047,6 @@ __global__ __launch_bounds__(256) void ba_ldlt_kernel(BaParams P) {
 #undef LL
 }
 
-// The trial step in one launch (g2o's back-substitution, oplus and the trial chi2's per-edge terms): every workgroup
-// first forms all poses of the trial state in LDS (free: exp(x_p) T, fixed: T); one lane per landmark then runs
-// x_l = Dinv (b_l - sum_e H_pl^T x_p) sequentially over its edges, writes X + x_l into the trial state and |e|^2 of
-// each of its edges at the trial state. The trial state is the other buffer: a rejected trial leaves the current
-// one untouched (no backup / restore copies); an accepted one flips P.cur (ba_chi2_kernel's last workgroup).
-// It also writes the LM scale's items x (lambda x + b) (free poses' components, then the landmarks').
-__global__ __launch_bounds__(256) void ba_step_kernel(BaParams P, BaMat3 K, double lambda) {
-    extern __shared__ double sT[];  // [P][7]
-    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    if (P.lam) lambda = *P.lam;
-    const int ns = P.ns;
-    const int cur = ba_cur(P);
-    const double* T0 = cur ? P.poses2 : P.poses;
-    const double* X0 = cur ? P.X2 : P.X;
-    double* T1 = cur ? P.poses : P.poses2;
-    double* X1 = cur ? P.X : P.X2;
-    const int t = threadIdx.x;
-    for (int p = t; p < P.P; p += kNT) {
-        double Tn[7];
-        if (p < P.nf) {
-#pragma unroll
-            for (int i = 0; i < 7; ++i) Tn[i] = T0[7 * p + i];
-        } else {
-            double dT[7];
-            se3_exp(P.xp + 6 * (p - P.nf), dT);
-            se3_mul(dT, T0 + 7 * p, Tn);
-        }
-#pragma unroll
-        for (int i = 0; i < 7; ++i) sT[7 * p + i] = Tn[i];
-        if (blockIdx.x == 0) {
-#pragma unroll
-            for (int i = 0; i < 7; ++i) T1[7 * p + i] = Tn[i];
-        }
-    }
-    if (blockIdx.x == 0)
-        for (int k = t; k < ns; k += kNT) {
-            const double x = P.xp[k];
-            P.sc1[k] = x * (lambda * x + P.bp[6 * P.nf + k]);
-        }
-    __syncthreads();
-    const int l = blockIdx.x * kNT + t;
-    if (l >= P.L) return;
-    const int k0 = P.le_off[l], k1 = P.le_off[l + 1];
-    double tv[3] = {P.bl[3 * l], P.bl[3 * l + 1], P.bl[3 * l + 2]};
-    double D[9];
-    landmark_dinv(P, l, lambda, D);
-    // the landmark's edges two at a time: indices and poses, then both edges' Jacobians and x_p loaded before the
-    // subtractions (in edge order), one dependent load round per pair of edges
-    for (int kb = k0; kb < k1; kb += 2) {
-        int eb[2], pb[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) eb[u] = kb + u < k1 ? P.le[kb + u] : 0;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) pb[u] = kb + u < k1 ? P.ep[eb[u]] : 0;
-        double h[2][18], xv[2][6];
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-            if (kb + u < k1 && pb[u] >= P.nf) {
-                hpl_load(P, eb[u], h[u]);
-                const double* xpp = P.xp + 6 * (pb[u] - P.nf);
-#pragma unroll
-                for (int a = 0; a < 6; ++a) xv[u][a] = xpp[a];
-            }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (kb + u >= k1 || pb[u] < P.nf) continue;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                double d = h[u][c] * xv[u][0];
-#pragma unroll
-                for (int a = 1; a < 6; ++a) d = d + h[u][3 * a + c] * xv[u][a];
-                tv[c] = tv[c] - d;
-            }
-        }
-    }
-    double Xn[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const double x = D[3 * c] * tv[0] + D[3 * c + 1] * tv[1] + D[3 * c + 2] * tv[2];
-        P.xl[3 * l + c] = x;
-        P.sc1[ns + 3 * l + c] = x * (lambda * x + P.bl[3 * l + c]);
-        Xn[c] = X0[3 * l + c] + x;
-        X1[3 * l + c] = Xn[c];
-    }
-    for (int kb = k0; kb < k1; kb += 2) {
-        int eb[2], pb[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) eb[u] = kb + u < k1 ? P.le[kb + u] : 0;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) pb[u] = kb + u < k1 ? P.ep[eb[u]] : 0;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (kb + u >= k1) break;
-            double r[2];
-            ba_error(sT + 7 * pb[u], K.v, Xn, P.meas + 2 * eb[u], r);
-            P.e2[eb[u]] = r[0] * r[0] + r[1] * r[1];
-        }
-    }
-}
-
-// one lane per edge: its squared error at the current estimate (the solve's first chi2)
-__global__ __launch_bounds__(256) void ba_edge_chi2_kernel(BaParams P, BaMat3 K) {
-    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= P.E) return;
-    const int cur = ba_cur(P);
-    double r[2];
-    ba_error((cur ? P.poses2 : P.poses) + 7 * P.ep[e], K.v, (cur ? P.X2 : P.X) + 3 * P.el[e], P.meas + 2 * e, r);
-    P.e2[e] = r[0] * r[0] + r[1] * r[1];
-}
-
 // ---- device-driven LM control (the host loop of yv_ba_solve's host form, operation for operation) ----
 __device__ void ba_ctl_init(BaCtl* c, double chi2, double* log, unsigned long long* maxdiag) {
     c->currentChi = chi2;
@@ -1227,46 +1116,193 @@ __global__ void ba_ctl_resume_kernel(BaCtl* c) {
     c->skip_trial = 0;
 }
 
-// chi2 over the edges (sum 0) and, for a trial, the LM scale x.(lambda x + b) over the variables (free poses, then
-// landmarks; sum 1) in the oracle's tree4096 order: kWG workgroups per sum, lane u of workgroup g holds leaf
-// g + kWG u and adds its items k = leaf + 4096 m in order (~19 / ~28 per lane for a configs[2] window, all loaded
-// before the additions; consecutive lanes read consecutive items), the local levels run in the workgroup and its class total is
-// published; the last workgroup of the launch (grouped counters) runs both sums' top levels and then (device control)
-// decides the trial or starts the solve, or (host control) leaves chi2 / scale in scal[0] / scal[1].
-// mode 0: the solve's first chi2; 1: a trial. (Rounds 4-5 used 256 chains of 300-450 dependent additions: 14 us.)
-__global__ __launch_bounds__(kWLanes) void ba_chi2_kernel(BaParams P, double lambda, int mode) {
-    __shared__ double red[kWLanes];
-    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
+// chi2 and the LM scale in the oracle's landmark-block order (oracle/yavo_oracle_ba.c lblock_total): a workgroup of
+// kNT lanes holds one block of 256 landmarks, lane t landmark 256 b + t (0.0 past L). Each workgroup runs the block's
+// halving trees in LDS and publishes the totals write-through (P.part[1 + 2 b] chi2, [2 + 2 b] the landmarks' scale
+// part; workgroup 0 also the free poses' scale part, tree256 over their items, at [0]); the last workgroup folds the
+// block totals into 256 leaves (block b into leaf b mod 256, ascending b), runs the trees over the leaves and then
+// decides the trial (device control), starts the solve (trial false), or leaves chi2 / scale in scal[0] / scal[1].
+template <bool kTrial>
+__device__ __forceinline__ void lblock_reduce(const BaParams& P, double chi, double sl, double sp) {
+    __shared__ double red[3][kNT];
     const int t = threadIdx.x;
-    const int sum = blockIdx.x / kWG, g = blockIdx.x - sum * kWG;
-    const int N = sum == 0 ? P.E : P.ns + 3 * P.L;
-    const double* src = sum == 0 ? P.e2 : P.sc1;  // |e|^2 per edge / the scale's item per variable (ba_step_kernel)
-    double acc = 0.0;
-    // a lane's items in batches of 32, every load of a batch issued before its additions (one latency per batch:
-    // a configs[2] window's sums need one)
-    for (int k0 = g + kWG * t; k0 < N; k0 += 32 * kWLeaves) {
-        double v[32];
-#pragma unroll
-        for (int u = 0; u < 32; ++u) v[u] = k0 + u * kWLeaves < N ? src[k0 + u * kWLeaves] : 0.0;
-#pragma unroll
-        for (int u = 0; u < 32; ++u)
-            if (k0 + u * kWLeaves < N) acc = acc + v[u];
+    red[0][t] = chi;
+    red[1][t] = sl;
+    red[2][t] = sp;
+    __syncthreads();
+    for (int off = kNT / 2; off > 0; off >>= 1) {
+        if (t < off) {
+            red[0][t] = red[0][t] + red[0][t + off];
+            if (kTrial) {
+                red[1][t] = red[1][t] + red[1][t + off];
+                red[2][t] = red[2][t] + red[2][t + off];
+            }
+        }
+        __syncthreads();
     }
-    red[t] = acc;
-    wide_local_tree<1>(red);
-    if (t == 0) st_agent(&P.part[sum * kWG + g], red[0]);
+    if (t == 0) {
+        st_agent(&P.part[1 + 2 * blockIdx.x], red[0][0]);
+        if (kTrial) st_agent(&P.part[2 + 2 * blockIdx.x], red[1][0]);
+        if (kTrial && blockIdx.x == 0) st_agent(&P.part[0], red[2][0]);
+    }
     if (!ba_last_block_h(P.ticket + 1, P.ticket + 4 + kTicketGroups)) return;
+    const int nb = (P.L + kNT - 1) / kNT;
+    double lc = 0.0, ls = 0.0;
+    for (int b = t; b < nb; b += kNT) {
+        lc = lc + ld_agent(&P.part[1 + 2 * b]);
+        if (kTrial) ls = ls + ld_agent(&P.part[2 + 2 * b]);
+    }
+    __syncthreads();  // this workgroup's own block trees are read
+    red[0][t] = lc;
+    red[1][t] = ls;
+    __syncthreads();
+    for (int off = kNT / 2; off > 0; off >>= 1) {
+        if (t < off) {
+            red[0][t] = red[0][t] + red[0][t + off];
+            if (kTrial) red[1][t] = red[1][t] + red[1][t + off];
+        }
+        __syncthreads();
+    }
     if (t != 0) return;
-    const double chi2 = wide_top_tree(P.part, 1);
-    const double scale = mode ? wide_top_tree(P.part + kWG, 1) : 0.0;
+    const double chi2 = red[0][0];
+    if (!kTrial) {
+        if (!P.ctl) P.scal[0] = chi2;
+        else ba_ctl_init(P.ctl, chi2, P.log, P.maxdiag);
+        return;
+    }
+    const double scale = ld_agent(&P.part[0]) + red[1][0];
     if (!P.ctl) {
         P.scal[0] = chi2;
-        if (mode) P.scal[1] = scale;
-    } else if (mode == 0) {
-        ba_ctl_init(P.ctl, chi2, P.log, P.maxdiag);
+        P.scal[1] = scale;
     } else {
         ba_ctl_decide(P.ctl, chi2, scale, P.ns > 0 ? P.scal[2] != 0.0 : true, P.cur, P.log);
     }
+}
+
+// The trial step in one launch (g2o's back-substitution, oplus, the trial chi2 and the LM scale): every workgroup
+// first forms all poses of the trial state in LDS (free: exp(x_p) T, fixed: T); one lane per landmark then runs
+// x_l = Dinv (b_l - sum_e H_pl^T x_p) sequentially over its edges, writes X + x_l into the trial state, and sums |e|^2
+// of its edges at the trial state and its three scale items x (lambda x + b) (each from 0.0, in order) for
+// lblock_reduce, whose last workgroup decides the trial. The trial state is the other buffer: a rejected trial leaves
+// the current one untouched (no backup / restore copies); an accepted one flips P.cur. (Until round 5 the per-edge
+// |e|^2 and the scale items went through HBM to a separate tree4096 chi2 kernel: 11 us per trial.)
+__global__ __launch_bounds__(kNT) void ba_step_kernel(BaParams P, BaMat3 K, double lambda) {
+    extern __shared__ double sT[];  // [P][7]
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
+    if (P.lam) lambda = *P.lam;
+    const int ns = P.ns;
+    const int cur = ba_cur(P);
+    const double* T0 = cur ? P.poses2 : P.poses;
+    const double* X0 = cur ? P.X2 : P.X;
+    double* T1 = cur ? P.poses : P.poses2;
+    double* X1 = cur ? P.X : P.X2;
+    const int t = threadIdx.x;
+    for (int p = t; p < P.P; p += kNT) {
+        double Tn[7];
+        if (p < P.nf) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) Tn[i] = T0[7 * p + i];
+        } else {
+            double dT[7];
+            se3_exp(P.xp + 6 * (p - P.nf), dT);
+            se3_mul(dT, T0 + 7 * p, Tn);
+        }
+#pragma unroll
+        for (int i = 0; i < 7; ++i) sT[7 * p + i] = Tn[i];
+        if (blockIdx.x == 0) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) T1[7 * p + i] = Tn[i];
+        }
+    }
+    // the free poses' scale items, leaf t = items k = t mod kNT in ascending k (workgroup 0)
+    double sp = 0.0;
+    if (blockIdx.x == 0)
+        for (int k = t; k < ns; k += kNT) {
+            const double x = P.xp[k];
+            sp = sp + x * (lambda * x + P.bp[6 * P.nf + k]);
+        }
+    __syncthreads();
+    const int l = blockIdx.x * kNT + t;
+    double chi = 0.0, sl = 0.0;
+    if (l < P.L) {
+        const int k0 = P.le_off[l], k1 = P.le_off[l + 1];
+        double tv[3] = {P.bl[3 * l], P.bl[3 * l + 1], P.bl[3 * l + 2]};
+        double D[9];
+        landmark_dinv(P, l, lambda, D);
+        // the landmark's edges two at a time: indices and poses, then both edges' Jacobians and x_p loaded before
+        // the subtractions (in edge order), one dependent load round per pair of edges
+        for (int kb = k0; kb < k1; kb += 2) {
+            int eb[2], pb[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) eb[u] = kb + u < k1 ? P.le[kb + u] : 0;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) pb[u] = kb + u < k1 ? P.ep[eb[u]] : 0;
+            double h[2][18], xv[2][6];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                if (kb + u < k1 && pb[u] >= P.nf) {
+                    hpl_load(P, eb[u], h[u]);
+                    const double* xpp = P.xp + 6 * (pb[u] - P.nf);
+#pragma unroll
+                    for (int a = 0; a < 6; ++a) xv[u][a] = xpp[a];
+                }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                if (kb + u >= k1 || pb[u] < P.nf) continue;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    double d = h[u][c] * xv[u][0];
+#pragma unroll
+                    for (int a = 1; a < 6; ++a) d = d + h[u][3 * a + c] * xv[u][a];
+                    tv[c] = tv[c] - d;
+                }
+            }
+        }
+        double Xn[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double x = D[3 * c] * tv[0] + D[3 * c + 1] * tv[1] + D[3 * c + 2] * tv[2];
+            P.xl[3 * l + c] = x;
+            sl = sl + x * (lambda * x + P.bl[3 * l + c]);
+            Xn[c] = X0[3 * l + c] + x;
+            X1[3 * l + c] = Xn[c];
+        }
+        for (int kb = k0; kb < k1; kb += 2) {
+            int eb[2], pb[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) eb[u] = kb + u < k1 ? P.le[kb + u] : 0;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) pb[u] = kb + u < k1 ? P.ep[eb[u]] : 0;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                if (kb + u >= k1) break;
+                double r[2];
+                ba_error(sT + 7 * pb[u], K.v, Xn, P.meas + 2 * eb[u], r);
+                chi = chi + (r[0] * r[0] + r[1] * r[1]);
+            }
+        }
+    }
+    lblock_reduce<true>(P, chi, sl, sp);
+}
+
+// the solve's first chi2 at the current estimate, in the same order: one lane per landmark over its edges
+__global__ __launch_bounds__(kNT) void ba_chi2_kernel(BaParams P, BaMat3 K) {
+    if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
+    const int cur = ba_cur(P);
+    const double* T = cur ? P.poses2 : P.poses;
+    const double* X = cur ? P.X2 : P.X;
+    const int l = blockIdx.x * kNT + threadIdx.x;
+    double chi = 0.0;
+    if (l < P.L) {
+        const double Xl[3] = {X[3 * l], X[3 * l + 1], X[3 * l + 2]};
+        for (int k = P.le_off[l]; k < P.le_off[l + 1]; ++k) {
+            const int e = P.le[k];
+            double r[2];
+            ba_error(T + 7 * P.ep[e], K.v, Xl, P.meas + 2 * e, r);
+            chi = chi + (r[0] * r[0] + r[1] * r[1]);
+        }
+    }
+    lblock_reduce<false>(P, chi, 0.0, 0.0);
 }
 
 // after the solve: the estimate into P.poses / P.X when it ended in the other buffer
@@ -1302,12 +1338,10 @@ void launch_ba_trial(const BaParams& P, const BaMat3& K, double lambda, hipStrea
     launch_ba_ldlt(P, s);
     hipLaunchKernelGGL(ba::ba_step_kernel, dim3(std::max(1, (P.L + 255) / 256)), dim3(256),
                        sizeof(double) * 7 * P.P, s, P, K, lambda);
-    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(2 * ba::kWG), dim3(ba::kWLanes), 0, s, P, lambda, 1);
 }
 
 void launch_ba_chi2(const BaParams& P, const BaMat3& K, hipStream_t s) {
-    if (P.E > 0) hipLaunchKernelGGL(ba::ba_edge_chi2_kernel, dim3((P.E + 255) / 256), dim3(256), 0, s, P, K);
-    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(ba::kWG), dim3(ba::kWLanes), 0, s, P, 0.0, 0);
+    hipLaunchKernelGGL(ba::ba_chi2_kernel, dim3(std::max(1, (P.L + ba::kNT - 1) / ba::kNT)), dim3(ba::kNT), 0, s, P, K);
 }
 
 void launch_ba_finish(const BaParams& P, hipStream_t s) {
@@ -1436,7 +1470,7 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
     rc |= ba_alloc(b, &Q.X2, 3 * L);
     rc |= ba_alloc(b, &b->d_cur, 1);
     rc |= ba_alloc(b, &b->d_ticket, kBaTickets);
-    rc |= ba_alloc(b, &Q.part, 2 * 256);
+    rc |= ba_alloc(b, &Q.part, 1 + 2 * std::max<size_t>(1, (L + yavo::ba::kNT - 1) / yavo::ba::kNT));
     rc |= ba_alloc(b, &Q.err, 2 * E);
     rc |= ba_alloc(b, &Q.Jp, 12 * E);
     rc |= ba_alloc(b, &Q.Jl, 6 * E);
@@ -1450,8 +1484,6 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
     rc |= ba_alloc(b, &Q.xl, 3 * L);
     rc |= ba_alloc(b, &Q.tr, ns);
     rc |= ba_alloc(b, &Q.scal, 16);
-    rc |= ba_alloc(b, &Q.e2, E);
-    rc |= ba_alloc(b, &Q.sc1, ns + 3 * L + 256);
     rc |= ba_alloc(b, &b->d_maxdiag, 1);
     rc |= ba_alloc(b, &b->d_ctl, 1);
     if (rc == YV_OK && hipHostMalloc(reinterpret_cast<void**>(&b->h_scal), 4 * sizeof(double)) != hipSuccess)

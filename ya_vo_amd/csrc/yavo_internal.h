@@ -211,7 +211,6 @@ struct BaParams {
     double* xl = nullptr;             // [L][3]
     int32_t* tr = nullptr;            // [ns] LDLT transpositions
     double* scal = nullptr;           // [4]: chi2, scale, LDLT ok
-    double* e2 = nullptr;             // [E] squared error per edge
     // device-driven LM (yv_ba_solve): a kernel returns at once when *gate != 0 (its phase is skipped), and the trial
     // kernels read lambda from *lam; both nullptr under host control
     const int* gate = nullptr;
@@ -225,8 +224,8 @@ struct BaParams {
     double* log = nullptr;             // [max_iters + 1] chi2 per iteration (device control)
     unsigned long long* maxdiag = nullptr;
     unsigned* ticket = nullptr;        // [kBaTickets] last-workgroup counters (0 between launches)
-    double* part = nullptr;            // [2][kWG] chi2 / scale class totals
-    double* sc1 = nullptr;             // the LM scale's items (ba_step_kernel -> ba_chi2_kernel)
+    double* part = nullptr;            // [1 + 2 blocks]: the free poses' scale part, then per block of 256
+                                       // landmarks its chi2 and scale totals (ba_step_kernel)
     double* spart = nullptr;           // [Schur task][kWG][36] tree4096 class totals of the Schur workgroups
     unsigned* sticket = nullptr;       // [Schur task] last-workgroup counters (0 between launches)
     double* rpart = nullptr;           // [free pose][kWG][27] class totals of the H_pp / b_p reduce
