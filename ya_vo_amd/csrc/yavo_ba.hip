@@ -1307,6 +1307,7 @@ __global__ __launch_bounds__(kNT) void ba_chi2_kernel(BaParams P, BaMat3 K) {
 
 // after the solve: the estimate into P.poses / P.X when it ended in the other buffer
 __global__ __launch_bounds__(256) void ba_finish_kernel(BaParams P) {
+    if (P.gate && *P.gate) return;  // enqueued with the solve: skipped when it was suspended (the host reruns it)
     if (!P.cur || !*P.cur) return;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < 7 * P.P) P.poses[i] = P.poses2[i];
@@ -1373,6 +1374,8 @@ struct yv_ba {
     double* h_scal = nullptr;  // pinned [4]
     yavo::BaCtl* d_ctl = nullptr;  // the device-driven LM's control block
     yavo::BaCtl* h_ctl = nullptr;  // pinned copy
+    double* h_log = nullptr;       // pinned copy of d_log [log_cap]
+    bool resumed = false;          // the last ba_solve_wait resumed a suspended solve
     double* d_log = nullptr;       // [log_cap] chi2 per iteration
     int log_cap = 0;
     int device_control = 1;        // yv_ba_set_control
@@ -1490,6 +1493,8 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
         rc = YV_ERR_HIP;
     if (rc == YV_OK && hipHostMalloc(reinterpret_cast<void**>(&b->h_ctl), sizeof(yavo::BaCtl)) != hipSuccess)
         rc = YV_ERR_HIP;
+    if (rc == YV_OK && hipHostMalloc(reinterpret_cast<void**>(&b->h_log), sizeof(double) * 65) != hipSuccess)
+        rc = YV_ERR_HIP;
     // sized up front where that is small, so a solve loop's first iterations do not allocate (each growth
     // synchronises the stream and frees device memory, which synchronises the device): the Schur partials of up to 64
     // free poses, the window graph's co-visibility lists (3 per landmark) and a 64-iteration chi2 log
@@ -1525,6 +1530,7 @@ extern "C" void yv_ba_destroy(yv_ba* b) {
     for (void* p : b->owned) (void)hipFree(p);
     if (b->h_scal) (void)hipHostFree(b->h_scal);
     if (b->h_ctl) (void)hipHostFree(b->h_ctl);
+    if (b->h_log) (void)hipHostFree(b->h_log);
     delete b;
 }
 
@@ -1656,6 +1662,10 @@ int ba_solve_enqueue(yv_ba* b, const double* poses, const double* landmarks, int
         b->d_log = nullptr;
         b->log_cap = 0;
         if (ba_alloc(b, &b->d_log, (size_t)max_iters + 1) != YV_OK) return YV_ERR_HIP;
+        if (b->h_log) (void)hipHostFree(b->h_log);
+        b->h_log = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void**>(&b->h_log), sizeof(double) * (max_iters + 1)) != hipSuccess)
+            return YV_ERR_HIP;
         b->log_cap = max_iters + 1;
     }
     yavo::BaCtl* c = b->d_ctl;
@@ -1675,7 +1685,13 @@ int ba_solve_enqueue(yv_ba* b, const double* poses, const double* landmarks, int
         yavo::launch_ba_linearize(Pit, b->K, it == 0 ? 1 : 0, st);
         yavo::launch_ba_trial(Ptr, b->K, 0.0, st);
     }
+    // the end of the solve in the same submission (skipped on the device when it was suspended; ba_solve_wait then
+    // resumes it and reruns these), so an unsuspended solve is collected with one wait
+    yavo::BaParams Pf = Q;
+    Pf.gate = &c->suspended;
+    yavo::launch_ba_finish(Pf, st);
     if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(b->h_log, b->d_log, sizeof(double) * (max_iters + 1), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemcpyAsync(b->h_ctl, c, sizeof(yavo::BaCtl), hipMemcpyDeviceToHost, st) != hipSuccess)
         return YV_ERR_HIP;
     return YV_OK;
@@ -1695,9 +1711,11 @@ int ba_solve_wait(yv_ba* b, double* poses, double* landmarks, int max_iters, dou
     Pit.gate = &c->skip_iter;
     Ptr.gate = &c->skip_trial;
     Ptr.lam = &c->lambda;
+    b->resumed = false;
     for (;;) {
         if (hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
         if (!b->h_ctl->suspended) break;
+        b->resumed = true;
         yavo::launch_ba_ctl_resume(c, st);  // the suspended iteration's trial loop continues at its trial q
         const int first = b->h_ctl->it;
         for (int it = first; it < max_iters; ++it) {
@@ -1708,13 +1726,18 @@ int ba_solve_wait(yv_ba* b, double* poses, double* landmarks, int max_iters, dou
             hipMemcpyAsync(b->h_ctl, c, sizeof(yavo::BaCtl), hipMemcpyDeviceToHost, st) != hipSuccess)
             return YV_ERR_HIP;
     }
-    yavo::launch_ba_finish(Q, st);
     const int n_it = max_iters > 0 ? b->h_ctl->iters : 0;
-    if ((poses && (hipMemcpyAsync(poses, Q.poses, pb, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                   (xb && hipMemcpyAsync(landmarks, Q.X, xb, hipMemcpyDeviceToHost, st) != hipSuccess))) ||
-        (chi2_log && hipMemcpyAsync(chi2_log, b->d_log, sizeof(double) * (n_it + 1), hipMemcpyDeviceToHost, st) != hipSuccess) ||
-        hipStreamSynchronize(st) != hipSuccess)
+    if (b->resumed) {
+        yavo::launch_ba_finish(Q, st);
+        if (hipMemcpyAsync(b->h_log, b->d_log, sizeof(double) * (max_iters + 1), hipMemcpyDeviceToHost, st) !=
+            hipSuccess)
+            return YV_ERR_HIP;
+    }
+    if (poses && (hipMemcpyAsync(poses, Q.poses, pb, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                  (xb && hipMemcpyAsync(landmarks, Q.X, xb, hipMemcpyDeviceToHost, st) != hipSuccess)))
         return YV_ERR_HIP;
+    if ((b->resumed || poses) && hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
+    if (chi2_log) std::memcpy(chi2_log, b->h_log, sizeof(double) * (n_it + 1));
     if (iters) *iters = n_it;
     return YV_OK;
 }
@@ -2027,7 +2050,9 @@ __global__ __launch_bounds__(256) void win_build_kernel(WinFrames F, int L, int 
 // apply_window: T_wc = inverse(T_cw) for every window frame, refined landmarks back to their frames, the anchor
 __global__ __launch_bounds__(256) void win_scatter_kernel(WinFrames F, int L, int max_lm, const double* __restrict__ poses,
                                                           const double* __restrict__ X, double* __restrict__ T,
-                                                          double* __restrict__ Xs, double* __restrict__ anchor) {
+                                                          double* __restrict__ Xs, double* __restrict__ anchor,
+                                                          const int* gate) {
+    if (gate && *gate) return;  // enqueued with the solve: skipped when it was suspended (solve_end reruns it)
     const int t = blockIdx.x * 256 + threadIdx.x;
     if (t < F.P) {
         double o[7];
@@ -2318,6 +2343,10 @@ extern "C" int yv_ba_window_solve_begin(yv_ba_window* w, int64_t first, int n, i
     b->ready = true;
     const int rc = ba_solve_enqueue(b, nullptr, nullptr, max_iters);
     if (rc != YV_OK) return rc;
+    // the write-back in the same submission (skipped on the device if the solve suspends; _end reruns it then)
+    hipLaunchKernelGGL(win_scatter_kernel, dim3(nb), dim3(256), 0, st, F, L, w->max_lm, Q.poses, Q.X, w->d_T, w->d_X,
+                       d_anchor, static_cast<const int*>(&b->d_ctl->suspended));
+    if (hipGetLastError() != hipSuccess) return YV_ERR_HIP;
     w->solving = true;
     w->solve_kind = 1;
     w->solve_iters = max_iters;
@@ -2342,10 +2371,12 @@ extern "C" int yv_ba_window_solve_end(yv_ba_window* w, double* chi2_log, int* it
     int it = 0;
     const int rc = ba_solve_wait(b, nullptr, nullptr, w->solve_iters, chi2_log, &it);
     if (rc != YV_OK) return rc;
-    yavo::BaParams& Q = b->P;
-    hipLaunchKernelGGL(win_scatter_kernel, dim3(w->solve_nb), dim3(256), 0, st, w->solve_F, w->solve_L, w->max_lm,
-                       Q.poses, Q.X, w->d_T, w->d_X, w->solve_anchor);
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
+    if (b->resumed) {  // the write-back enqueued by _begin was skipped: the solve finished only now
+        yavo::BaParams& Q = b->P;
+        hipLaunchKernelGGL(win_scatter_kernel, dim3(w->solve_nb), dim3(256), 0, st, w->solve_F, w->solve_L, w->max_lm,
+                           Q.poses, Q.X, w->d_T, w->d_X, w->solve_anchor, static_cast<const int*>(nullptr));
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
+    }
     if (iters) *iters = it;
     if (solved) *solved = 1;
     return YV_OK;
