@@ -510,11 +510,8 @@ __global__ __launch_bounds__(kWLanes) void ba_schur_kernel(BaParams P, double la
 //  4. The diagonal and backward solves run on wave 0: the vector in registers (two entries per lane), broadcasts by
 //     v_readlane, L read by row from the column store (stride 129 doubles: conflict-free by rows and by columns).
 constexpr int kLdltRegN = 128;   // n <= 128: lane l holds rows l and l + 64
-#ifndef YAVO_LDLT_WAVES
-#define YAVO_LDLT_WAVES 8
-#endif
-constexpr int kLdltWaves = YAVO_LDLT_WAVES;  // 8: 512 threads, two waves per SIMD
-constexpr int kLdltPairs = 64 / kLdltWaves;  // column pairs per wave: pair W j + w holds columns 2 W j + 2 w, + 1
+constexpr int kLdltWaves = 8;    // 512 threads: two waves per SIMD
+constexpr int kLdltPairs = 8;    // column pairs per wave: pair 8 j + w holds columns 16 j + 2 w, 16 j + 2 w + 1
 constexpr int kLdltLs = 129;     // column stride of the L store (doubles)
 constexpr int kLdltRing = 8;     // published pairs in flight
 
@@ -697,7 +694,7 @@ __global__ __launch_bounds__(64 * kLdltWaves) void ba_ldlt_reg_kernel(BaParams P
         for (int j = 0; j < kLdltPairs; ++j)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int c = 2 * kLdltWaves * j + 2 * w + h;
+                const int c = 16 * j + 2 * w + h;
                 const int pc = c < n ? perm[c] : 0;
                 const double* row = P.S + (int64_t)pc * n;
                 if (j < kLdltPairs / 2) Al[j < kLdltPairs / 2 ? j : 0][h] = (r0 > c && r0 < n) ? row[p0] : 0.0;
@@ -719,7 +716,7 @@ __global__ __launch_bounds__(64 * kLdltWaves) void ba_ldlt_reg_kernel(BaParams P
         for (int j = 0; j < kLdltPairs; ++j)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int c = 2 * kLdltWaves * j + 2 * w + h;
+                const int c = 16 * j + 2 * w + h;
                 if (c < n) {
                     if (j < kLdltPairs / 2) Lc[c * kLdltLs + r0] = Al[j < kLdltPairs / 2 ? j : 0][h];
                     Lc[c * kLdltLs + r1] = Ah[j][h];
@@ -795,11 +792,8 @@ __global__ __launch_bounds__(64 * kLdltWaves) void ba_ldlt_reg_kernel(BaParams P
                 const double tc_b = readlane_f64(bn < 64 ? tka0 : tka1, bn & 63);  // t_ca(bn)
                 const double td_b = readlane_f64(bn < 64 ? tkb0 : tkb1, bn & 63);  // t_cb(bn)
                 const double da = dora - readlane_f64(an < 64 ? dot0 : dot1, an & 63);
-                switch (qn / kLdltWaves) {
+                switch (qn >> 3) {
                     LDLT_FIN(0) LDLT_FIN(1) LDLT_FIN(2) LDLT_FIN(3) LDLT_FIN(4) LDLT_FIN(5) LDLT_FIN(6) LDLT_FIN(7)
-#if YAVO_LDLT_WAVES == 4
-                    LDLT_FIN(8) LDLT_FIN(9) LDLT_FIN(10) LDLT_FIN(11) LDLT_FIN(12) LDLT_FIN(13) LDLT_FIN(14) LDLT_FIN(15)
-#endif
                     default: break;
                 }
                 __builtin_amdgcn_s_setprio(0);
@@ -810,8 +804,8 @@ __global__ __launch_bounds__(64 * kLdltWaves) void ba_ldlt_reg_kernel(BaParams P
             // holding c): LDS broadcast loads of them cost eight waves' worth of LDS return bandwidth every step
 #pragma unroll
             for (int j = 0; j < kLdltPairs; ++j) {
-                if (kLdltWaves * j + w > q) {
-                    const int cl = (2 * kLdltWaves * j + 2 * w) & 63;  // wave-uniform lane of this pair's first column
+                if (8 * j + w > q) {
+                    const int cl = (16 * j + 2 * w) & 63;  // wave-uniform lane of this pair's first column
                     const double tax = readlane_f64(j < kLdltPairs / 2 ? tka0 : tka1, cl);
                     const double tay = readlane_f64(j < kLdltPairs / 2 ? tka0 : tka1, cl + 1);
                     if (j < kLdltPairs / 2) {
