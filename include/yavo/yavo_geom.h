@@ -174,6 +174,9 @@ int yv_ba_debug_read(yv_ba* ba, int which, double* dst, int64_t count);
  * or_ldlt_solve computes it; *ok = its isPositive flag.  The same kernels the solve launches (n <= 128: the
  * register form, above: the global-memory form). */
 int yv_ba_debug_ldlt(yv_ctx* ctx, const double* S, int n, const double* b, double* x, int* ok);
+/* Diagnostics: how many suspended trial loops (an iteration whose first damping trial was rejected) the device LM of
+ * this yv_ba has resumed from the host since it was created (tests use it to show the resume path ran). */
+int yv_ba_debug_resumes(yv_ba* ba);
 
 /* ---- the sliding BA window of the chained stereo front end, on the device (BASELINE configs[2]) ----
  * The window LoopHandler's loop would hand Optimizer (src/LoopHandler.cc:60-165, src/Optimizer.cc:17-70), as

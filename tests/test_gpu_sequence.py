@@ -73,6 +73,31 @@ def test_sequence_200_frames_matches_oracle(ctx, oracle, offsets):
     assert rmse_translation(traj, ground_truth(n, scene.K_KITTI)) < 0.02
 
 
+@pytest.mark.timeout(600)
+def test_sequence_window_solves_that_suspend_match_oracle(ctx, oracle, offsets):
+    """Window solves whose device LM suspends (an iteration's first damping trial rejected: at 40 iterations the
+    synthetic windows get there) and is resumed from the host: the finish and write-back enqueued with the solve are
+    skipped on the device and rerun after the resume, and the result is still the oracle loop's bit for bit."""
+    import torch
+    n, chunk, iters = 60, 20, 40
+    frames = synth_sequence(71, n, stereo=True)
+    fe = SequenceFrontend(ctx, chunk, scene.K_KITTI, T_RIGHT, ba_iters=iters)
+    d = torch.from_numpy(frames.reshape(2 * n, *frames.shape[2:])).to("cuda:0")
+    for c in range(n // chunk):
+        fe.process_chunk(d[2 * c * chunk:2 * (c + 1) * chunk])
+    traj = fe.trajectory()
+    ba_log = list(fe.ba_log)
+    resumes = fe.ba.resumes()
+    fe.close()
+    del d
+    assert resumes > 0  # the resume path ran (2 on this sequence, tools/ba_resume_probe.py)
+    ref, _, log = oracle_sequence(oracle, frames, chunk, scene.K_KITTI, T_RIGHT, offsets, ba_iters=iters,
+                                  threads=_threads())
+    assert [x[:2] for x in ba_log] == [x[:2] for x in log]
+    np.testing.assert_array_equal(np.array([x[2:] for x in ba_log]), np.array([x[2:] for x in log]))
+    np.testing.assert_array_equal(traj, ref)
+
+
 def test_sequence_device_window_equals_host_assembly(ctx):
     """The BA window recorded, assembled and written back on the device (yv_ba_window_*) gives the host assembly's
     (window_problem / yv_ba_set_problem / apply_window) trajectory, BA logs and frame records bit for bit."""

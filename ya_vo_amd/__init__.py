@@ -126,6 +126,7 @@ GEOM_SIGNATURES = {
     "yv_ba_set_problem": (_I, [_P, _I, _I, _I, _P, _P, _P, _I, _P]),
     "yv_ba_solve": (_I, [_P, _P, _P, _I, _P, ctypes.POINTER(_I)]),
     "yv_ba_debug_read": (_I, [_P, _I, _P, ctypes.c_int64]),
+    "yv_ba_debug_resumes": (_I, [_P]),
     "yv_ba_debug_ldlt": (_I, [_P, _P, _I, _P, _P, ctypes.POINTER(_I)]),
     "yv_ba_set_stream": (_I, [_P, _P]),
     "yv_ba_set_control": (_I, [_P, _I]),
@@ -674,6 +675,10 @@ class BundleAdjuster:
     def set_control(self, on_device: bool = True) -> None:
         """LM control on the device (default: no read-back per trial) or on the host (yv_ba_set_control)."""
         _check(self.lib.yv_ba_set_control(self.handle, 1 if on_device else 0), "yv_ba_set_control")
+
+    def resumes(self) -> int:
+        """Suspended trial loops the device LM resumed from the host so far (yv_ba_debug_resumes)."""
+        return int(self.lib.yv_ba_debug_resumes(self.handle))
 
     def set_problem(self, n_poses: int, n_fixed: int, n_landmarks: int, edge_pose, edge_landmark, meas, K) -> None:
         self._ep = np.ascontiguousarray(edge_pose, np.int32).reshape(-1)

@@ -1376,6 +1376,7 @@ struct yv_ba {
     yavo::BaCtl* h_ctl = nullptr;  // pinned copy
     double* h_log = nullptr;       // pinned copy of d_log [log_cap]
     bool resumed = false;          // the last ba_solve_wait resumed a suspended solve
+    int resumes = 0;               // suspended trial loops resumed since creation (yv_ba_debug_resumes)
     double* d_log = nullptr;       // [log_cap] chi2 per iteration
     int log_cap = 0;
     int device_control = 1;        // yv_ba_set_control
@@ -1716,6 +1717,7 @@ int ba_solve_wait(yv_ba* b, double* poses, double* landmarks, int max_iters, dou
         if (hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
         if (!b->h_ctl->suspended) break;
         b->resumed = true;
+        ++b->resumes;
         yavo::launch_ba_ctl_resume(c, st);  // the suspended iteration's trial loop continues at its trial q
         const int first = b->h_ctl->it;
         for (int it = first; it < max_iters; ++it) {
@@ -1839,6 +1841,8 @@ extern "C" int yv_ba_solve(yv_ba* b, double* poses, double* landmarks, int max_i
 }
 
 // diagnostics: copy one of the workspace's device buffers (as left by the last yv_ba_solve) to the host
+extern "C" int yv_ba_debug_resumes(yv_ba* b) { return b ? b->resumes : -1; }
+
 extern "C" int yv_ba_debug_read(yv_ba* b, int which, double* dst, int64_t count) {
     if (!b || !b->ready || !dst || count < 0) return YV_ERR_INVALID;
     const yavo::BaParams& Q = b->P;
