@@ -4,14 +4,14 @@
 // summation orders (built with -ffp-contract=off):
 //
 //   ba_reduce_kernel      the iteration's linearisation and blocks: H_pp (21) + b_p (6) per free pose in tree4096
-//                         order (32 workgroups per pose, each edge's e and J_pose formed on the fly), and one lane per
+//                         order (16 workgroups per pose, each edge's e and J_pose formed on the fly), and one lane per
 //                         landmark that linearises its edges -- e, J_pose (the reference's linearizeOplus), J_point =
 //                         J_pose[:, :3] R, stored for the later kernels (H_pl = J_pose^T J_point is formed from them
 //                         where it is read) -- for H_ll, b_l (sequential over its edges); its last workgroup starts
 //                         the iteration's trial loop (device control). (Until round 5 a separate linearisation
 //                         kernel stored e / J first: 10.5 us per iteration on a configs[2] window.)
 //   ba_schur_kernel       per trial: the reduced pose system S = H_pp + lambda I - sum W H_pl^T and b_schur in tree4096
-//                         order (32 workgroups per upper 6 x 6 block or b_schur row), W = H_pl (H_ll + lambda I)^-1
+//                         order (16 workgroups per upper 6 x 6 block or b_schur row), W = H_pl (H_ll + lambda I)^-1
 //                         formed per co-visible pair
 //   ba_ldlt_reg_kernel    one workgroup: Eigen's LDLT (diagonal pivoting) on the reduced pose system, the matrix in
 //                         registers, column pairs handed between waves through LDS (n <= 128; ba_ldlt_kernel on
@@ -203,8 +203,10 @@ __device__ void ba_ctl_iter_begin(BaCtl* c, const unsigned long long* maxdiag) {
 // each workgroup runs them on its own leaves (off / kWG lanes apart, nv trees at once) and publishes its class totals;
 // the last workgroup runs levels kWG / 2 .. 1 over the kWG totals.
 constexpr int kWLeaves = 4096;
-constexpr int kWG = 32;
-constexpr int kWLanes = kWLeaves / kWG;  // 128
+// 16 workgroups of 256 lanes per sum (32 x 128 until c49: the reduce kernel 19.4 -> 17.3 us, the Schur kernel the same;
+// 8 x 512: Schur 33 us, profiles/r05/c49)
+constexpr int kWG = 16;
+constexpr int kWLanes = kWLeaves / kWG;  // 256
 
 template <int NV>
 __device__ __forceinline__ void wide_local_tree(double* red) {  // red[q * kWLanes + u]; totals end in red[q * kWLanes]
@@ -392,7 +394,7 @@ __device__ __forceinline__ void w_block(const double* h, const double* Di, doubl
 // oracle's trial step stores: Dinv of the pair's landmark from H_ll + lambda I, H_pl of both edges from their
 // Jacobians, W_e1 = H_pl(e1) Dinv -- the same expressions, so the same bits, with no W / Dinv round trip through
 // HBM and no trial kernel (216 B read per diagonal pair, 360 B per off-diagonal one). A configs[2] window has at most
-// one item per lane, so a block's ~3,700 pairs are spread over 32 CUs with every load in flight at once.
+// one item per lane, so a block's ~3,700 pairs are spread over 16 CUs with every load in flight at once.
 // grid: (nb + np) kWG workgroups; task = blockIdx / kWG, g = blockIdx % kWG.
 //  tasks [0, nb): S(a, b) = base - tree4096 over the co-visible pairs k of (W_e1(k)[a] . H_pl(e2(k))[b]); on a
 //    diagonal block only a >= b is written, to both mirrored entries (the oracle's loop leaves that value)
