@@ -36,8 +36,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=120)
     ap.add_argument("--calls", type=int, default=50)
+    ap.add_argument("--lib", default=os.path.join(ROOT, "ya_vo_amd", "lib", "libyavo_prof.so"),
+                    help="a YAVO_LM_PROFILE build (experiment builds of the kernel too)")
     args = ap.parse_args()
-    lib = yv.load_library(os.path.join(ROOT, "ya_vo_amd", "lib", "libyavo_prof.so"))
+    lib = yv.load_library(args.lib)
     lib.yv_debug_ldlt_prof.argtypes = [ctypes.c_void_p]
     ctx = yv.Context(0)
     S = window_system(args.n // 6, 1)
