@@ -1290,12 +1290,13 @@ __global__ __launch_bounds__(kNT) void ba_step_kernel(BaParams P, BaMat3 K, doub
     lblock_reduce<true>(P, chi, sl, sp);
 }
 
-// the solve's first chi2 at the current estimate, in the same order: one lane per landmark over its edges
+// the solve's first chi2 at the current estimate, in the same order: one lane per landmark over its edges. A solve
+// starts in state 0 (P.poses / P.X); workgroup 0 also resets *P.cur for the kernels after it (no separate memset)
 __global__ __launch_bounds__(kNT) void ba_chi2_kernel(BaParams P, BaMat3 K) {
     if (P.gate && *P.gate) return;  // a skipped phase of the device-driven LM
-    const int cur = ba_cur(P);
-    const double* T = cur ? P.poses2 : P.poses;
-    const double* X = cur ? P.X2 : P.X;
+    if (P.cur && blockIdx.x == 0 && threadIdx.x == 0) *P.cur = 0;
+    const double* T = P.poses;
+    const double* X = P.X;
     const int l = blockIdx.x * kNT + threadIdx.x;
     double chi = 0.0;
     if (l < P.L) {
@@ -1682,7 +1683,7 @@ int ba_solve_enqueue(yv_ba* b, const double* poses, const double* landmarks, int
     Pit.gate = &c->skip_iter;
     Ptr.gate = &c->skip_trial;
     Ptr.lam = &c->lambda;
-    if (hipMemsetAsync(b->d_cur, 0, sizeof(int), st) != hipSuccess) return YV_ERR_HIP;
+    // (*Q.cur is reset by the first kernel, ba_chi2_kernel)
     if (poses && (hipMemcpyAsync(Q.poses, poses, pb, hipMemcpyHostToDevice, st) != hipSuccess ||
                   (xb && hipMemcpyAsync(Q.X, landmarks, xb, hipMemcpyHostToDevice, st) != hipSuccess)))
         return YV_ERR_HIP;
@@ -2017,10 +2018,24 @@ __global__ __launch_bounds__(256) void win_build_kernel(WinFrames F, int L, int 
                                                         int32_t* __restrict__ el, double* __restrict__ meas,
                                                         int32_t* __restrict__ le_off, int32_t* __restrict__ le,
                                                         int32_t* __restrict__ pe, int32_t* __restrict__ cv1,
-                                                        int32_t* __restrict__ cv2) {
+                                                        int32_t* __restrict__ cv2, int32_t* __restrict__ pe_off,
+                                                        int32_t* __restrict__ cv_off) {
     const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t < F.P) se3_inverse_dev(T + (F.s0 + t) * 7, poses + 7 * t);
+    const int n = F.P;
+    if (t < n) se3_inverse_dev(T + (F.s0 + t) * 7, poses + 7 * t);
     if (t == 0) le_off[L] = 2 * L;
+    // the offsets (closed form in the counts): pose p's edges start at pe0[p]; the co-visibility lists of row p1 hold
+    // (p1, p1): c[p1] + c[p1 + 1] entries and (p1, p1 + 1): c[p1 + 1], after F.row[p1]
+    if (t <= n) pe_off[t] = t < n ? F.pe0[t] : 2 * L;
+    for (int i = t; i <= n * n; i += gridDim.x * 256) {
+        if (i == 0) {
+            cv_off[0] = 0;
+            continue;
+        }
+        const int p1 = (i - 1) / n, p2 = (i - 1) - p1 * n;
+        const int cn = p1 + 1 < n ? F.c[p1 + 1] : 0;
+        cv_off[i] = F.row[p1] + (p2 >= p1 ? F.c[p1] + cn : 0) + (p2 >= p1 + 1 ? cn : 0);
+    }
     if (t >= L) return;
     int i = 1;  // the owning pose: base[i] <= t < base[i] + c[i]
     while (i + 1 < F.P && t >= F.base[i + 1]) ++i;
@@ -2098,8 +2113,6 @@ struct yv_ba_window {
     hipEvent_t added = nullptr;
     bool add_pending = false;
     std::vector<int32_t> h_cnt;  // per store index, -1 = not recorded
-    int32_t* h_struct = nullptr;  // pinned: pe_off [P + 1], cv_off [P P + 1]
-    size_t h_struct_cap = 0;
     // a solve enqueued by yv_ba_window_solve_begin, collected by yv_ba_window_solve_end
     bool solving = false;
     int solve_kind = 0;  // 1: the LM runs; 2: nothing to solve (only the anchor kernel)
@@ -2184,16 +2197,12 @@ extern "C" int yv_ba_window_create(yv_ba* ba, int max_lm, int max_kf, yv_ba_wind
     w->ba = ba;
     w->max_lm = max_lm;
     w->max_kf = max_kf;
-    // the graph offsets of the largest window the yv_ba takes: pe_off [P + 1], cv_off [P P + 1]
-    const size_t P = (size_t)std::min(ba->max_poses, kWinMaxPoses), need = (P + 1) + P * P + 1;
     if (hipMalloc(reinterpret_cast<void**>(&w->d_info), sizeof(int64_t) * (1 + 2 * (size_t)max_kf)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&w->h_info), sizeof(int64_t) * (1 + 2 * (size_t)max_kf)) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&w->h_struct), sizeof(int32_t) * need) != hipSuccess ||
         hipEventCreateWithFlags(&w->added, hipEventDisableTiming) != hipSuccess) {
         yv_ba_window_destroy(w);
         return YV_ERR_HIP;
     }
-    w->h_struct_cap = need;
     *out = w;
     return YV_OK;
 }
@@ -2209,7 +2218,6 @@ extern "C" void yv_ba_window_destroy(yv_ba_window* w) {
     win_free_store(w);
     if (w->d_info) (void)hipFree(w->d_info);
     if (w->h_info) (void)hipHostFree(w->h_info);
-    if (w->h_struct) (void)hipHostFree(w->h_struct);
     delete w;
 }
 
@@ -2277,39 +2285,16 @@ extern "C" int yv_ba_window_solve_begin(yv_ba_window* w, int64_t first, int n, i
     const int E = 2 * L;
     const int64_t nc = 3 * (int64_t)L;
     if (n > b->max_poses || L > b->max_landmarks || E > b->max_edges) return YV_ERR_CAPACITY;
-    // per pose: pe_off (own edges of frame p, then the prev edges of frame p + 1); per row p1 of the co-visibility
-    // buckets: (p1, p1) = c[p1] + c[p1 + 1] entries, (p1, p1 + 1) = c[p1 + 1]
-    const size_t need = (size_t)(n + 1) + (size_t)n * n + 1;
-    if (need > w->h_struct_cap) {
-        if (hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
-        if (w->h_struct) (void)hipHostFree(w->h_struct);
-        w->h_struct = nullptr;
-        w->h_struct_cap = 0;
-        if (hipHostMalloc(reinterpret_cast<void**>(&w->h_struct), sizeof(int32_t) * need) != hipSuccess)
-            return YV_ERR_HIP;
-        w->h_struct_cap = need;
-    }
-    int32_t* pe_off = w->h_struct;
-    int32_t* cv_off = w->h_struct + n + 1;
+    // per pose: its edges start (own edges of frame p, then the prev edges of frame p + 1); per row p1 of the
+    // co-visibility buckets: (p1, p1) = c[p1] + c[p1 + 1] entries, (p1, p1 + 1) = c[p1 + 1]. win_build_kernel writes
+    // pe_off / cv_off from these (until c59 the host wrote them and copied them over: two copies per solve)
     int32_t acc = 0, racc = 0;
     for (int p = 0; p < n; ++p) {
         const int32_t cn = p + 1 < n ? F.c[p + 1] : 0;
-        pe_off[p] = acc;
         F.pe0[p] = acc;
         acc += F.c[p] + cn;
         F.row[p] = racc;
         racc += F.c[p] + 2 * cn;
-    }
-    pe_off[n] = acc;
-    cv_off[0] = 0;
-    for (int p1 = 0; p1 < n; ++p1) {
-        const int32_t cn = p1 + 1 < n ? F.c[p1 + 1] : 0;
-        int32_t r = F.row[p1];
-        for (int p2 = 0; p2 < n; ++p2) {
-            if (p2 == p1) r += F.c[p1] + cn;
-            else if (p2 == p1 + 1) r += cn;
-            cv_off[(int64_t)p1 * n + p2 + 1] = r;
-        }
     }
     if (nc > b->cv_cap) {
         if (hipStreamSynchronize(st) != hipSuccess) return YV_ERR_HIP;
@@ -2322,14 +2307,10 @@ extern "C" int yv_ba_window_solve_begin(yv_ba_window* w, int64_t first, int n, i
     }
     b->ready = false;
     yavo::BaParams& Q = b->P;
-    if (hipMemcpyAsync(b->d_pe_off, pe_off, sizeof(int32_t) * (n + 1), hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(b->d_cv_off, cv_off, sizeof(int32_t) * ((size_t)n * n + 1), hipMemcpyHostToDevice, st) !=
-            hipSuccess)
-        return YV_ERR_HIP;
     const int nb = (std::max(L, n) + 255) / 256;
     hipLaunchKernelGGL(win_build_kernel, dim3(nb), dim3(256), 0, st, F, L, w->max_lm, w->d_T, w->d_X, w->d_uvo,
                        w->d_uvp, Q.poses, Q.X, b->d_ep, b->d_el, b->d_meas, b->d_le_off, b->d_le, b->d_pe, b->d_cv_e1,
-                       b->d_cv_e2);
+                       b->d_cv_e2, b->d_pe_off, b->d_cv_off);
     if (hipGetLastError() != hipSuccess) return YV_ERR_HIP;
     Q.P = n;
     Q.nf = n_fixed;
