@@ -93,10 +93,10 @@ def parse():
                          "skips it")
     ap.add_argument("--collective-world1", action="store_true",
                     help="at N=1, still run the shared-map exchange through a 1-rank process group (RCCL)")
-    ap.add_argument("--sequence-frames", type=int, default=200,
-                    help="frames of the configs[2] leg (rank 0, N=1): the full front end with the local BA window "
-                         "(tools/bench_sequence.py), its trajectory compared with the CPU oracle loop after the timed "
-                         "runs; 0 skips it")
+    ap.add_argument("--sequence-frames", type=int, default=1000,
+                    help="frames of the configs[2] leg's timed runs (rank 0, N=1; median of 5): the full front end "
+                         "with the local BA window (tools/bench_sequence.py); after them the first 200 frames are "
+                         "compared with the CPU oracle loop; 0 skips it")
     ap.add_argument("--sequence-cpu", type=int, default=1,
                     help="1: run tests/sequence_chain.py (the same loop over the CPU oracle) for the sequence leg's "
                          "trajectory check; 0: skip it")
@@ -649,8 +649,8 @@ def main():
             sys.path.insert(0, os.path.join(ROOT, "tools"))
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             import bench_sequence
-            seq = bench_sequence.measure(args.sequence_frames, 20, repeats=3, cpu=bool(args.sequence_cpu),
-                                         cpu_threads=min(16, cpu_threads_available()), ctx=ctx)
+            seq = bench_sequence.measure(args.sequence_frames, 20, repeats=5, cpu=bool(args.sequence_cpu),
+                                         cpu_threads=min(16, cpu_threads_available()), ctx=ctx, check_frames=200)
             seq.pop("_trajectory", None)
         except Exception as e:  # reported, never fatal to the headline
             seq = {"error": repr(e)[:300]}

@@ -192,6 +192,10 @@ int or_ldlt_solve(const double* H, int n, const double* b, double* x);
  * poses [P][7] / X [L][3] in / out; chi2_log [max_iters + 1] optional.  Returns the iterations run. */
 int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t* ep, const int32_t* el,
              const double* meas, int E, const double* K, int max_iters, double* chi2_log);
+/* mode 0 = the kernel order above (bit-exact with yavo_ba.hip); mode 1 = g2o's own loop orders as sequential chains
+ * (yavo_oracle_ba.c header): the order the trajectory tolerance is measured against */
+int or_ba_lm_mode(double* poses, int P, int n_fixed, double* X, int L, const int32_t* ep, const int32_t* el,
+                  const double* meas, int E, const double* K, int max_iters, double* chi2_log, int mode);
 extern int or_ba_dump_iter;
 extern double* or_ba_dump[16];
 

@@ -29,6 +29,20 @@
  *             from 0.0), a halving tree over the leaves; the scale = (the free poses' items in tree256 order: leaf
  *             t = items j = t mod 256 ascending, halving tree) + (the landmark part)
  *   sequential per landmark over its edges (edge order) for H_ll / b_l and the back-substitution
+ * g2o order (or_ba_lm_mode(..., mode 1), the check the kernel order is measured against, never the GPU's order):
+ *   g2o's own loops restated as sequential chains (g2o BlockSolver<Traits>::buildSystem / solve, SparseOptimizer::
+ *   activeRobustChi2, OptimizationAlgorithmLevenberg::computeScale; g2o is not vendored by the reference, its version
+ *   unpinned, CMakeLists.txt:22-23): H_pp / b_p accumulated edge by edge in edge (id) order from 0.0 (each edge's
+ *   constructQuadraticForm, `from->A() += AtO * A`, `b += A^T omega_r` with omega_r = -e); the Schur block of poses
+ *   (p1 <= p2) starts at H_pp + lambda I (or 0) and each co-visible landmark, ascending, subtracts its
+ *   BDinv * B_j^T term (`(*Hi1i2).noalias() -= BDinv * Bj->transpose()`, BDinv = B_i Dinv); LinearSolverDense
+ *   copies each upper block and then its transpose, so a diagonal block enters the dense matrix transposed (its
+ *   lower triangle, the one Eigen's LDLT reads, holds block(b, a)); b_schur = b_p - coefficients, where the
+ *   coefficients accumulate B_i (Dinv b_l) landmark by landmark (ascending; poses of a landmark ascending);
+ *   the landmark update cl = b_l + B^T (-x_p) over the landmark's poses ascending (SparseBlockMatrixCCS::
+ *   rightMultiply), x_l = Dinv cl; chi2 = sum over edges in edge order from 0.0 of e.(Omega e); the scale =
+ *   sum over x = [x_p; x_l] in vector order from 0.0.  Small fixed-size products (3- and 6-term inner products)
+ *   are left to right, as in the kernel order (Eigen's SIMD association of them is build-dependent).
  * (Rounds 1-4 summed the Schur and b_schur entries as one sequential chain each, and H_pp / b_p, chi2 and the scale
  * in a 256-leaf tree. A 3,800-term chain is latency-bound on one GPU lane, and 256 leaves leave each GPU lane ~15
  * dependent loads (and chi2's chains 300-450 dependent additions); with 4096 leaves a configs[2] window's sums have
@@ -284,8 +298,25 @@ static void ba_dump(int which, const double* src, size_t n) {
 /* or_ba_lm: g2o LM with BlockSolver_6_3 (see the header); poses [P][7] (T_cw, SE3d::data()), X [L][3] in / out.
  * chi2_log [max_iters + 1] (may be NULL): chi2 before iteration 0 and after each iteration.  Returns the
  * iterations run (an iteration that fails 10 trials ends the run, as g2o's Terminate). */
+/* chi2 in g2o's order: activeRobustChi2, sequential over the edges in edge order from 0.0 */
+static double ba_chi2_g2o(const ba_struct* s, const double* poses, const double* X) {
+    double chi = 0.0;
+    for (int e = 0; e < s->E; ++e) {
+        double r[2];
+        ba_error(poses + 7 * s->ep[e], s->K, X + 3 * s->el[e], s->meas + 2 * e, r);
+        chi = chi + (r[0] * r[0] + r[1] * r[1]);
+    }
+    return chi;
+}
+
 int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t* ep, const int32_t* el,
              const double* meas, int E, const double* K, int max_iters, double* chi2_log) {
+    return or_ba_lm_mode(poses, P, n_fixed, X, L, ep, el, meas, E, K, max_iters, chi2_log, 0);
+}
+
+int or_ba_lm_mode(double* poses, int P, int n_fixed, double* X, int L, const int32_t* ep, const int32_t* el,
+                  const double* meas, int E, const double* K, int max_iters, double* chi2_log, int mode) {
+    const int g2o = mode == 1;
     ba_struct s = {P, L, E, n_fixed, K, ep, el, meas, 0, 0, 0, 0, 0, 0, 0, 0};
     ba_build_struct(&s);
     const int np = P - n_fixed, ns = 6 * np;
@@ -307,7 +338,8 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
     double* bak_X = (double*)malloc(sizeof(double) * 3 * (size_t)L);
     tree4096* wt = (tree4096*)malloc(sizeof(tree4096));
     double* lsum = (double*)malloc(sizeof(double) * (size_t)(L > 0 ? L : 1));
-    double currentChi = ba_chi2(&s, poses, X, lsum);
+    double* coef = (double*)malloc(sizeof(double) * (size_t)ns + 1);
+    double currentChi = g2o ? ba_chi2_g2o(&s, poses, X) : ba_chi2(&s, poses, X, lsum);
     if (chi2_log) chi2_log[0] = currentChi;
     double lambda = 0, ni = 2;
     int it;
@@ -323,7 +355,24 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
             for (int a = 0; a < 6; ++a)
                 for (int c = 0; c < 3; ++c) Hpl[18 * e + 3 * a + c] = jp[a] * jl[c] + jp[6 + a] * jl[3 + c];
         }
-        for (int p = n_fixed; p < P; ++p) {
+        for (int p = n_fixed; p < P && g2o; ++p) {
+            /* g2o buildSystem: edge by edge in edge order, from 0.0 */
+            double h[36], g[6];
+            for (int i = 0; i < 36; ++i) h[i] = 0.0;
+            for (int a = 0; a < 6; ++a) g[a] = 0.0;
+            for (int k = s.pe_off[p]; k < s.pe_off[p + 1]; ++k) {
+                const int e = s.pe[k];
+                const double* jp = Jp + 12 * e;
+                const double o0 = -err[2 * e], o1 = -err[2 * e + 1];
+                for (int a = 0; a < 6; ++a) {
+                    for (int b = 0; b < 6; ++b) h[6 * a + b] = h[6 * a + b] + (jp[a] * jp[b] + jp[6 + a] * jp[6 + b]);
+                    g[a] = g[a] + (jp[a] * o0 + jp[6 + a] * o1);
+                }
+            }
+            memcpy(Hpp + 36 * p, h, sizeof h);
+            memcpy(bp + 6 * p, g, sizeof g);
+        }
+        for (int p = n_fixed; p < P && !g2o; ++p) {
             for (int a = 0; a < 6; ++a)
                 for (int b = a; b < 6; ++b) {
                     w_reset(wt);
@@ -388,7 +437,25 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
                 }
             }
             /* Schur: S(p1, p2) = [p1 == p2] (H_pp + lambda I) - sum_l W_e1 H_pl(e2)^T ; upper blocks, mirrored */
-            for (int p1 = n_fixed; p1 < P; ++p1)
+            for (int p1 = n_fixed; p1 < P && g2o; ++p1)
+                for (int p2 = p1; p2 < P; ++p2)
+                    for (int a = 0; a < 6; ++a)
+                        for (int b = 0; b < 6; ++b) {
+                            /* g2o solve(): the block starts at H_pp + lambda I (or 0); each co-visible landmark,
+                             * ascending, subtracts its term */
+                            double v = p1 == p2 ? Hpp[36 * p1 + 6 * a + b] + (a == b ? lambda : 0.0) : 0.0;
+                            for (int k = s.cv_off[p1 * P + p2]; k < s.cv_off[p1 * P + p2 + 1]; ++k) {
+                                const double* w = W + 18 * s.cv_e1[k] + 3 * a;
+                                const double* h = Hpl + 18 * s.cv_e2[k] + 3 * b;
+                                v = v - (w[0] * h[0] + w[1] * h[1] + w[2] * h[2]);
+                            }
+                            const int r = 6 * (p1 - n_fixed) + a, c = 6 * (p2 - n_fixed) + b;
+                            /* LinearSolverDense: H.block(r, c) = block, then H.block(c, r) = block^T -- a diagonal
+                             * block ends up transposed */
+                            if (p1 != p2) S[(size_t)r * ns + c] = v;
+                            S[(size_t)c * ns + r] = v;
+                        }
+            for (int p1 = n_fixed; p1 < P && !g2o; ++p1)
                 for (int p2 = p1; p2 < P; ++p2)
                     for (int a = 0; a < 6; ++a)
                         for (int b = 0; b < 6; ++b) {
@@ -405,7 +472,27 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
                             S[(size_t)r * ns + c] = v;
                             S[(size_t)c * ns + r] = v;
                         }
-            for (int p = n_fixed; p < P; ++p)
+            if (g2o) {
+                /* coefficients += B_i (Dinv b_l), landmark by landmark; b_schur = b_p - coefficients */
+                for (int i = 0; i < ns; ++i) coef[i] = 0.0;
+                for (int l = 0; l < L; ++l) {
+                    const double* D = Dinv + 9 * l;
+                    const double* g = bl + 3 * l;
+                    double db[3];
+                    for (int c = 0; c < 3; ++c) db[c] = D[3 * c] * g[0] + D[3 * c + 1] * g[1] + D[3 * c + 2] * g[2];
+                    for (int k = s.le_off[l]; k < s.le_off[l + 1]; ++k) {
+                        const int e = s.le[k], p = ep[e];
+                        if (p < n_fixed) continue;
+                        const double* h = Hpl + 18 * e;
+                        for (int a = 0; a < 6; ++a)
+                            coef[6 * (p - n_fixed) + a] = coef[6 * (p - n_fixed) + a] +
+                                                          (h[3 * a] * db[0] + h[3 * a + 1] * db[1] + h[3 * a + 2] * db[2]);
+                    }
+                }
+                for (int p = n_fixed; p < P; ++p)
+                    for (int a = 0; a < 6; ++a) bs[6 * (p - n_fixed) + a] = bp[6 * p + a] - coef[6 * (p - n_fixed) + a];
+            }
+            for (int p = n_fixed; p < P && !g2o; ++p)
                 for (int a = 0; a < 6; ++a) {
                     w_reset(wt);
                     for (int k = s.pe_off[p]; k < s.pe_off[p + 1]; ++k) {
@@ -428,7 +515,21 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
             /* landmarks: x_l = Dinv (b_l - sum_e H_pl(e)^T x_p(e)) */
             for (int l = 0; l < L; ++l) {
                 double t[3] = {bl[3 * l], bl[3 * l + 1], bl[3 * l + 2]};
-                for (int k = s.le_off[l]; k < s.le_off[l + 1]; ++k) {
+                const int k0 = s.le_off[l], k1 = s.le_off[l + 1];
+                for (int kk = k0; kk < k1; ++kk) {
+                    int k = kk;
+                    if (g2o) {
+                        /* rightMultiply walks the landmark's column in pose order: the (kk - k0)-th smallest pose
+                         * (ties in edge order) */
+                        int best = -1;
+                        for (int j = k0; j < k1; ++j) {
+                            int rank = 0;
+                            for (int i = k0; i < k1; ++i)
+                                rank += ep[s.le[i]] < ep[s.le[j]] || (ep[s.le[i]] == ep[s.le[j]] && i < j);
+                            if (rank == kk - k0) best = j;
+                        }
+                        k = best;
+                    }
                     const int e = s.le[k], p = ep[e];
                     if (p < n_fixed) continue;
                     const double* xpp = xp + 6 * (p - n_fixed);
@@ -452,11 +553,17 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
             if (dump) {
                 ba_dump(13, xl, 3 * (size_t)L); ba_dump(14, poses, 7 * (size_t)P); ba_dump(15, X, 3 * (size_t)L);
             }
-            double tempChi = ba_chi2(&s, poses, X, lsum);
+            double tempChi = g2o ? ba_chi2_g2o(&s, poses, X) : ba_chi2(&s, poses, X, lsum);
             if (!ok2) tempChi = DBL_MAX;
             rho = currentChi - tempChi;
             /* computeScale over the variables: the free poses' items in tree256 order (leaf t = items j = t mod 256
              * ascending from 0.0), plus the landmarks' in the landmark-block order of 0.0 + their three items */
+            double scale;
+            if (g2o) {
+                scale = 0.0;  /* computeScale: x = [x_p; x_l] in vector order */
+                for (int j = 0; j < ns; ++j) scale += xp[j] * (lambda * xp[j] + bp[6 * n_fixed + j]);
+                for (int i = 0; i < 3 * L; ++i) scale += xl[i] * (lambda * xl[i] + bl[i]);
+            } else {
             double leaf[256];
             for (int t = 0; t < 256; ++t) leaf[t] = 0.0;
             for (int j = 0; j < ns; ++j) leaf[j % 256] = leaf[j % 256] + xp[j] * (lambda * xp[j] + bp[6 * n_fixed + j]);
@@ -466,7 +573,8 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
                 for (int c = 0; c < 3; ++c) acc = acc + xl[3 * l + c] * (lambda * xl[3 * l + c] + bl[3 * l + c]);
                 lsum[l] = acc;
             }
-            double scale = pose_part + lblock_total(lsum, L);
+            scale = pose_part + lblock_total(lsum, L);
+            }
             scale += 1e-3;
             rho /= scale;
             if (rho > 0 && isfinite(tempChi)) {
@@ -491,7 +599,7 @@ int or_ba_lm(double* poses, int P, int n_fixed, double* X, int L, const int32_t*
         }
     }
     free(Jp); free(Jl); free(err); free(Hpl); free(W); free(Hpp); free(bp); free(Hll); free(bl); free(Dinv);
-    free(S); free(bs); free(xp); free(xl); free(bak_p); free(bak_X); free(wt); free(lsum);
+    free(S); free(bs); free(xp); free(xl); free(bak_p); free(bak_X); free(wt); free(lsum); free(coef);
     ba_free_struct(&s);
     return it;
 }

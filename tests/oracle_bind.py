@@ -83,6 +83,7 @@ class Oracle:
             "or_recover_pose": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
             "or_ldlt_solve": (_I, [_P, _I, _P, _P]),
             "or_ba_lm": (_I, [_P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P]),
+            "or_ba_lm_mode": (_I, [_P, _I, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _I]),
             "or_map_block_bytes": (ctypes.c_int64, [_I, _I]),
             "or_map_chunk": (None, [_P, _I, ctypes.c_int64, _I, _P, _P, _P, _I, _I, _P]),
             "or_map_place": (None, [_P, _I, ctypes.c_int64, _P, _P]),
@@ -424,8 +425,9 @@ class Oracle:
         pos = self.lib.or_ldlt_solve(_p(H), len(b), _p(b), _p(x))
         return x, bool(pos)
 
-    def ba_lm(self, poses, n_fixed, X, ep, el, meas, K, max_iters=10):
-        """-> (poses [P, 7], X [L, 3], iterations, chi2 log)."""
+    def ba_lm(self, poses, n_fixed, X, ep, el, meas, K, max_iters=10, mode=0):
+        """-> (poses [P, 7], X [L, 3], iterations, chi2 log). mode 0: the kernel's summation order (bit-exact with
+        yv_ba); 1: g2o's own loop orders (BlockSolver::buildSystem / solve, activeRobustChi2, computeScale)."""
         T = np.ascontiguousarray(poses, np.float64).copy()
         Xo = np.ascontiguousarray(X, np.float64).copy()
         ep = np.ascontiguousarray(ep, np.int32)
@@ -433,8 +435,8 @@ class Oracle:
         meas = np.ascontiguousarray(meas, np.float64)
         K = np.ascontiguousarray(K, np.float64).reshape(9)
         log = np.zeros(max_iters + 1)
-        it = self.lib.or_ba_lm(_p(T), len(T), n_fixed, _p(Xo), len(Xo), _p(ep), _p(el), _p(meas), len(ep), _p(K),
-                               max_iters, _p(log))
+        it = self.lib.or_ba_lm_mode(_p(T), len(T), n_fixed, _p(Xo), len(Xo), _p(ep), _p(el), _p(meas), len(ep),
+                                    _p(K), max_iters, _p(log), int(mode))
         return T, Xo, it, log[:it + 1]
 
     # ---- shared map blocks (include/yavo/yavo_map.h) ----

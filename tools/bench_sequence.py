@@ -7,7 +7,8 @@ KITTI seq 00 is used when --kitti <sequence dir> is given and present (it is not
 otherwise 200 synthetic stereo frames with a known trajectory (ya_vo_amd/synth.py: frame k = crop at (k, 3k) of one
 textured fronto-parallel plane, right image +8 columns).
 
-    python tools/bench_sequence.py [--frames 200] [--chunk 20] [--repeats 3] [--cpu-threads 16] [--out f.json]
+    python tools/bench_sequence.py [--frames 1000] [--check-frames 200] [--chunk 20] [--repeats 5]
+                                   [--cpu-threads 16] [--out f.json]
 """
 import argparse
 import json
@@ -24,11 +25,21 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 T_RIGHT = np.array([0, 0, 0, 1, 0, -0.54, 0], np.float64)
 
 
-def measure(frames=200, chunk=20, n_fixed=2, ba_iters=10, repeats=3, cpu_threads=16, cpu=True, kitti="",
-            host_window=False, ctx=None, ba_priority=0):
-    """Run the configs[2] front end `repeats` times on frames resident in HBM (after one warm-up run) and return the
-    result dict of the best run; cpu: also run tests/sequence_chain.py (the same loop over the CPU oracle) on the same
-    frames and compare the trajectories (after the timed runs)."""
+def _pose_diff(A, B):
+    """max |translation difference| (m) and max |quaternion component difference| over two [n, 7] trajectories."""
+    A, B = np.asarray(A), np.asarray(B)
+    return float(np.max(np.abs(A[:, 4:] - B[:, 4:]))), float(np.max(np.abs(A[:, :4] - B[:, :4])))
+
+
+def measure(frames=1000, chunk=20, n_fixed=2, ba_iters=10, repeats=5, cpu_threads=16, cpu=True, kitti="",
+            host_window=False, ctx=None, ba_priority=0, check_frames=200, host_libm=True):
+    """Run the configs[2] front end `repeats` times over `frames` frames resident in HBM (after one warm-up run) and
+    report the median rate (min / max beside it). cpu: after the timed runs, one more device run over the first
+    `check_frames` frames (BASELINE configs[2]'s 200) is compared with tests/sequence_chain.py, the same loop over
+    the CPU oracle: bit for bit in the kernel's BA summation order, and as trajectory RMSE / pose / chi2-log
+    differences against the BA in g2o's own loop order (oracle or_ba_lm mode 1) -- with the restated libm the device
+    shares and, host_libm, with the host C library's pow / sin / cos as the reference's build links them. The timed
+    run's first `check_frames` poses must equal the check run's (a window holds its earlier frames fixed)."""
     import torch
     import ya_vo_amd as yv
     from ya_vo_amd import io as yio
@@ -37,8 +48,9 @@ def measure(frames=200, chunk=20, n_fixed=2, ba_iters=10, repeats=3, cpu_threads
     from ya_vo_amd.synth import synth_sequence
 
     n = frames
-    if n % chunk:
-        raise ValueError("frames must be a multiple of chunk")
+    check = min(check_frames, n) if cpu else 0
+    if n % chunk or check % chunk:
+        raise ValueError("frames and check_frames must be multiples of chunk")
     K = scene.K_KITTI
     if kitti and os.path.isdir(kitti):
         seq = yio.Sequence(kitti, stereo=True)
@@ -61,64 +73,99 @@ def measure(frames=200, chunk=20, n_fixed=2, ba_iters=10, repeats=3, cpu_threads
     d = torch.from_numpy(fr.reshape(2 * n, H, W)).to(torch.device("cuda", ctx.device))
     torch.cuda.synchronize()
 
-    def run():
+    def run(m):
         fe = SequenceFrontend(ctx, chunk, K, t_right, n_fixed=n_fixed, ba_iters=ba_iters, H=H, W=W,
-                              device_window=not host_window, ba_priority=ba_priority, expected_frames=n)
+                              device_window=not host_window, ba_priority=ba_priority, expected_frames=m)
         sec = {}
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for c in range(n // chunk):
+        for c in range(m // chunk):
             fe.process_chunk(d[2 * c * chunk:2 * (c + 1) * chunk], sec)
         fe.flush(sec)
         torch.cuda.synchronize()
         return fe, time.perf_counter() - t0, sec
 
-    fe, _, _ = run()  # warm-up (first launches, allocations)
+    fe, _, _ = run(n)  # warm-up (first launches, allocations)
     fe.close()
     times, secs = [], []
     traj = ba_log = records = None
     for _ in range(repeats):
-        fe, dt, sec = run()
+        fe, dt, sec = run(n)
         times.append(dt)
         secs.append(sec)
         traj, ba_log = fe.trajectory(), fe.ba_log
         records = fe.records
         fe.close()
-    best = int(np.argmin(times))
+    med = int(np.argsort(times)[len(times) // 2])  # the median run (odd repeats) or the upper middle one
+    t_med = float(np.median(times))
     out = {
         "workload": "BASELINE configs[2]: full front end (detect+describe+match+PnP + shared map + local BA), "
-                    f"first {n} frames, 1 x MI355X",
+                    f"{n} frames timed, the first {check} checked against the CPU oracle loop, 1 x MI355X",
         "data": data, "frames": n, "chunk_frames": chunk, "ba_window": chunk + n_fixed,
         "ba_fixed": n_fixed, "ba_iters": ba_iters,
         "ba_window_assembly": "host (window_problem / apply_window, per-chunk read-back)" if host_window else
         "device (yv_ba_window_*: records in HBM, graph built on the device, no per-chunk read-back)",
-        "frames_per_s": round(n / times[best], 2), "seconds": round(times[best], 4),
+        "frames_per_s": round(n / t_med, 2), "statistic": f"median of {repeats} repeats after a warm-up run",
+        "frames_per_s_min": round(n / max(times), 2), "frames_per_s_max": round(n / min(times), 2),
+        "spread": round((max(times) - min(times)) / t_med, 4), "seconds": round(t_med, 4),
         "seconds_all_repeats": [round(t, 4) for t in times],
-        "phase_seconds": {k: round(v, 4) for k, v in secs[best].items()},
+        "phase_seconds": {k: round(v, 4) for k, v in secs[med].items()},
         "ba_solves": len(ba_log),
-        "ba_ms_per_solve": round(1e3 * secs[best].get("ba", 0.0) / max(len(ba_log), 1), 4),
-        "ba_chi2_first_last": [[round(a, 3), round(b, 3)] for _, _, a, b in ba_log],
+        "ba_ms_per_solve": round(1e3 * secs[med].get("ba", 0.0) / max(len(ba_log), 1), 4),
         "landmarks": int(sum(len(r.edge) for r in records.values())),
         "inputs": "frames resident in HBM before the timed region (PCIe excluded)",
     }
-    from sequence_chain import ground_truth, oracle_sequence, rmse_translation
+    from sequence_chain import front_end, ground_truth, rmse_translation, sequence_from_tracks
     if not kitti:
         out["rmse_vs_ground_truth_m"] = rmse_translation(traj, ground_truth(n, K))
-    if cpu:
+    if check:
+        fe, _, _ = run(check)
+        traj_c, log_c = fe.trajectory(), list(fe.ba_log)
+        fe.close()
         import oracle_bind
         orc = oracle_bind.Oracle()
         t0 = time.perf_counter()
-        ref, _, ref_log = oracle_sequence(orc, fr, chunk, K, t_right, offsets.reshape(256, 4),
-                                          n_fixed=n_fixed, ba_iters=ba_iters, threads=cpu_threads)
+        tracks = front_end(orc, fr[:check], chunk, K, t_right, offsets.reshape(256, 4), threads=cpu_threads)
+        ref, _, ref_log = sequence_from_tracks(orc, tracks, chunk, K, n_fixed, ba_iters)
         cpu_s = time.perf_counter() - t0
-        out["cpu_reference"] = {"frames_per_s": round(n / cpu_s, 3), "seconds": round(cpu_s, 2),
+        c = {"frames": check,
+             "timed_run_prefix_identical": bool(np.array_equal(traj[:check], traj_c)),
+             "trajectory_rmse_vs_cpu_ref_m": rmse_translation(traj_c, ref),
+             "trajectory_bit_identical": bool(np.array_equal(traj_c, ref)),
+             "ba_log_identical": ref_log == log_c}
+        if not kitti:
+            c["rmse_vs_ground_truth_m"] = rmse_translation(traj_c, ground_truth(check, K))
+        out["cpu_reference"] = {"frames_per_s": round(check / cpu_s, 3), "seconds": round(cpu_s, 2),
                                 "cores": cpu_threads, "kind": "port",
-                                "sample": f"the same {n} frames through tests/sequence_chain.py (oracle FAST/BRIEF/"
-                                          "match/triangulation/pose LM/map/BA), ref-efficient costs, threads over "
-                                          "frames for the per-frame stages"}
-        out["trajectory_rmse_vs_cpu_ref_m"] = rmse_translation(traj, ref)
-        out["trajectory_bit_identical"] = bool(np.array_equal(traj, ref))
-        out["ba_log_identical"] = ref_log == ba_log
+                                "sample": f"the first {check} frames through tests/sequence_chain.py (oracle FAST/"
+                                          "BRIEF/match/triangulation/pose LM/map/BA), ref-efficient costs, threads "
+                                          "over frames for the per-frame stages"}
+
+        def versus(g_traj, g_log, how):
+            dt, dq = _pose_diff(traj_c, g_traj)
+            chi_d = [abs(a[3] - b[3]) / max(abs(b[3]), 1e-300) for a, b in zip(log_c, g_log)]
+            return {"how": how, "trajectory_rmse_m": rmse_translation(traj_c, g_traj),
+                    "max_translation_diff_m": dt, "max_quaternion_diff": dq,
+                    "ba_final_chi2_max_rel_diff": float(max(chi_d)) if chi_d else 0.0,
+                    "ba_iterations_equal": [x[:2] for x in log_c] == [x[:2] for x in g_log],
+                    "within_1e-4": rmse_translation(traj_c, g_traj) <= 1e-4}
+
+        g_traj, _, g_log = sequence_from_tracks(orc, tracks, chunk, K, n_fixed, ba_iters, ba_mode=1)
+        c["vs_g2o_order"] = versus(g_traj, g_log, "oracle BA in g2o's loop orders (BlockSolver::buildSystem / "
+                                                  "solve, activeRobustChi2, computeScale as sequential chains), the "
+                                                  "same front end; restated pow / sin / cos as on the device")
+        if host_libm:
+            orc.set_libm_flavour(1)
+            try:
+                tracks_h = front_end(orc, fr[:check], chunk, K, t_right, offsets.reshape(256, 4),
+                                     threads=cpu_threads)
+                h_traj, _, h_log = sequence_from_tracks(orc, tracks_h, chunk, K, n_fixed, ba_iters, ba_mode=1)
+            finally:
+                orc.set_libm_flavour(0)
+            c["vs_g2o_order_host_libm"] = versus(h_traj, h_log, "the whole oracle loop (pose LM and BA) with the "
+                                                                "host C library's pow / sin / cos as g2o / Sophus "
+                                                                "call them, BA in g2o's loop orders")
+        out["check"] = c
     out["_trajectory"] = traj
     if own_ctx:
         ctx.close()
@@ -127,11 +174,12 @@ def measure(frames=200, chunk=20, n_fixed=2, ba_iters=10, repeats=3, cpu_threads
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--frames", type=int, default=200)
+    ap.add_argument("--frames", type=int, default=1000)
+    ap.add_argument("--check-frames", type=int, default=200)
     ap.add_argument("--chunk", type=int, default=20)
     ap.add_argument("--n-fixed", type=int, default=2)
     ap.add_argument("--ba-iters", type=int, default=10)
-    ap.add_argument("--repeats", type=int, default=3)
+    ap.add_argument("--repeats", type=int, default=5)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kitti", default="")
@@ -143,7 +191,8 @@ def main():
     from ya_vo_amd import io as yio
     from ya_vo_amd.sequence import se3_inverse
     out = measure(args.frames, args.chunk, args.n_fixed, args.ba_iters, args.repeats, args.cpu_threads,
-                  not args.no_cpu, args.kitti, args.host_window, ba_priority=args.ba_priority)
+                  not args.no_cpu, args.kitti, args.host_window, ba_priority=args.ba_priority,
+                  check_frames=args.check_frames)
     traj = out.pop("_trajectory")
     if args.out:
         yio.write_kitti_poses(os.path.splitext(args.out)[0] + "_poses.txt", np.stack([se3_inverse(T) for T in traj]))
