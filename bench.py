@@ -299,7 +299,7 @@ def cpu_baseline(kind, threads, offsets, images, B, gpu_poses, edges, literal_fr
             timers["fast_harris"] = timers.get("fast_harris", 0.0) + t1 - t0
             timers["blur_brief"] = timers.get("blur_brief", 0.0) + t2 - t1
         T = track_pose(orc, prev_left_kp, kps[0], kps[1], scene.K_KITTI, T_RIGHT, timers=timers,
-                       init_timers=init_timers)[3]
+                       init_timers=init_timers, n_tracks=B)[3]  # the batch's LM order for B tracks
         timers.update({"f_ransac_init": init_timers.get("f_ransac", 0.0)})
         return T, time.perf_counter() - t_start - timers["f_ransac_init"], timers
 

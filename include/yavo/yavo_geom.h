@@ -147,6 +147,10 @@ int yv_recover_pose(struct yv_ctx* ctx, const double E[9], const float* pts1, co
  * BlockSolver_6_3 (Schur complement on the landmarks, dense LDLT on the poses).  The first n_fixed poses are held
  * fixed.  Restated in oracle/yavo_oracle_ba.c (or_ba_lm); results are bit-identical to it. */
 typedef struct yv_ba yv_ba;
+/* max_poses <= 640: the reduced pose system (6 max_poses <= 3840 rows) is factorised by one workgroup whose two
+ * vectors sit in LDS (16 B per row of a 64 KB workgroup allocation).  Device memory besides the problem arrays: the
+ * tree4096 Schur partials of np free poses, (np (np + 1) / 2 + np) x 4.6 KB (24 MB at np = 100, 0.95 GB at 640),
+ * allocated by the first problem that needs them. */
 int yv_ba_create(struct yv_ctx* ctx, int max_poses, int max_landmarks, int max_edges, yv_ba** out);
 void yv_ba_destroy(yv_ba* ba);
 /* The graph: edge e joins pose edge_pose[e] and landmark edge_landmark[e] with measurement meas[e][2] (pixels, x
@@ -172,7 +176,7 @@ int yv_ba_debug_read(yv_ba* ba, int which, double* dst, int64_t count);
 /* Diagnostics: the reduced-system solver of yv_ba_solve on its own -- Eigen LDLT with diagonal pivoting of the
  * symmetric n x n S (row-major, bitwise symmetric as the Schur kernel writes it), then x = S^-1 b as
  * or_ldlt_solve computes it; *ok = its isPositive flag.  The same kernels the solve launches (n <= 128: the
- * register form, above: the global-memory form). */
+ * register form, above: the global-memory form); 1 <= n <= 3840 (the solve's own limit, 6 x 640 poses). */
 int yv_ba_debug_ldlt(yv_ctx* ctx, const double* S, int n, const double* b, double* x, int* ok);
 /* Diagnostics: how many suspended trial loops (an iteration whose first damping trial was rejected) the device LM of
  * this yv_ba has resumed from the host since it was created (tests use it to show the resume path ran). */

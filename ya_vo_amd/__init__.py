@@ -371,11 +371,19 @@ class Context(_GeomMixin):
 
     def close(self) -> None:
         if self.handle:
-            # a yv_batch holds its context: destroy the batches first (never a batch after its context)
-            for b in list(getattr(self, "_batches", ())):
-                b.close()
+            # batches, LK / essential workspaces, bundle adjusters and their windows hold this context (its stream
+            # and device state): destroy them first, windows before their adjusters, never one after the context
+            owned = list(getattr(self, "_owned", ()))
+            for o in sorted(owned, key=lambda o: o._close_rank):
+                o.close()
             self.lib.yv_destroy(self.handle)
             self.handle = None
+
+    def _own(self, obj) -> None:
+        """Register a workspace that holds this context, so close() destroys it first."""
+        if not hasattr(self, "_owned"):
+            self._owned = weakref.WeakSet()
+        self._owned.add(obj)
 
     def __del__(self):
         try:
@@ -469,6 +477,8 @@ class Context(_GeomMixin):
 class Batch:
     """Device-resident batched pipeline (yv_batch): detect -> describe -> match -> removeOutliers."""
 
+    _close_rank = 2
+
     def __init__(self, ctx: Context, max_images: int, H: int, W: int, max_kp: int = 2000, max_pairs: int = 0):
         self.ctx = ctx
         self.lib = ctx.lib
@@ -477,9 +487,7 @@ class Batch:
                "yv_batch_create")
         self.handle = h
         self.max_images, self.H, self.W, self.max_kp, self.max_pairs = max_images, H, W, max_kp, max_pairs
-        if not hasattr(ctx, "_batches"):
-            ctx._batches = weakref.WeakSet()
-        ctx._batches.add(self)
+        ctx._own(self)
 
     def close(self) -> None:
         if self.handle:
@@ -564,11 +572,14 @@ class Batch:
 class Lk:
     """Batched pyramidal LK workspace (yv_lk): build pyramids of device images, track point lists per pair."""
 
+    _close_rank = 2
+
     def __init__(self, ctx: "Context", max_images: int, H: int, W: int, win: int = 11, max_level: int = 3):
         self.ctx, self.lib = ctx, ctx.lib
         h = ctypes.c_void_p()
         _check(self.lib.yv_lk_create(ctx.handle, max_images, H, W, win, max_level, ctypes.byref(h)), "yv_lk_create")
         self.handle = h
+        ctx._own(self)
         self.levels = self.lib.yv_lk_levels(h)
 
     def close(self) -> None:
@@ -606,12 +617,15 @@ class Lk:
 class Essential:
     """Batched cv::findEssentialMat (RANSAC) + cv::recoverPose workspace (yv_essential)."""
 
+    _close_rank = 2
+
     def __init__(self, ctx: "Context", max_pairs: int, max_points: int, max_iters: int = 1000):
         self.ctx, self.lib = ctx, ctx.lib
         h = ctypes.c_void_p()
         _check(self.lib.yv_essential_create(ctx.handle, max_pairs, max_points, max_iters, ctypes.byref(h)),
                "yv_essential_create")
         self.handle = h
+        ctx._own(self)
 
     def close(self) -> None:
         if self.handle:
@@ -649,16 +663,20 @@ class BundleAdjuster:
     projection edge (include/Optimizer.hpp:64-126) between keyframe poses and landmarks; poses SE3d::data() of T_cw,
     the first n_fixed held fixed."""
 
+    _close_rank = 1
+
     def __init__(self, ctx: "Context", max_poses: int, max_landmarks: int, max_edges: int):
         self.ctx, self.lib = ctx, ctx.lib
         h = ctypes.c_void_p()
         _check(self.lib.yv_ba_create(ctx.handle, max_poses, max_landmarks, max_edges, ctypes.byref(h)), "yv_ba_create")
         self.handle = h
+        ctx._own(self)  # Context.close destroys it (and its windows) before the context: no leaked workspace
 
     def close(self) -> None:
         if self.handle:
-            if getattr(self.ctx, "handle", None):  # a closed context took its stream (and the device state) with it
-                self.lib.yv_ba_destroy(self.handle)
+            for w in list(getattr(self, "_windows", ())):  # a window holds its adjuster
+                w.close()
+            self.lib.yv_ba_destroy(self.handle)
             self.handle = None
 
     def __del__(self):
@@ -708,11 +726,17 @@ class BaWindow:
     """The chained front end's sliding BA window on the device (yv_ba_window_*; include/yavo/yavo_geom.h): frame
     records from placed map blocks, the window graph built and solved by `ba` and written back in HBM."""
 
+    _close_rank = 0
+
     def __init__(self, ba: "BundleAdjuster", max_lm: int, max_kf: int):
         self.ba, self.lib = ba, ba.lib
         h = ctypes.c_void_p()
         _check(self.lib.yv_ba_window_create(ba.handle, max_lm, max_kf, ctypes.byref(h)), "yv_ba_window_create")
         self.handle, self.max_lm = h, max_lm
+        if not hasattr(ba, "_windows"):
+            ba._windows = weakref.WeakSet()
+        ba._windows.add(self)
+        ba.ctx._own(self)
 
     def close(self) -> None:
         if self.handle:

@@ -1393,6 +1393,8 @@ namespace {
 
 // [0] reduce, [1] chi2 (the last-workgroup tops); [4, 68) the reduce's groups, [68, 132) chi2's
 constexpr int kBaTickets = 4 + 2 * yavo::ba::kTicketGroups;
+// the global-memory LDLT keeps 2 x 6 np doubles in dynamic LDS beside ~3 KB of its own: 6 x 640 rows fit 64 KB
+constexpr int kBaMaxPoses = 640;
 
 template <class T>
 int ba_alloc(yv_ba* b, T** p, size_t count) {
@@ -1437,6 +1439,18 @@ int ba_ensure_schur(yv_ba* b, int np, hipStream_t st) {
     return YV_OK;
 }
 
+// the last-workgroup counters return to 0 at the end of every launch that uses them; a launch that never finished
+// (an error, a fault) could leave one non-zero, and every later solve would then skip that launch's last-workgroup
+// work silently -- so a new problem, and every failed enqueue, starts from zeroed counters (a few hundred bytes)
+int ba_reset_tickets(yv_ba* b, hipStream_t st) {
+    const yavo::BaParams& Q = b->P;
+    if (hipMemsetAsync(b->d_ticket, 0, kBaTickets * sizeof(unsigned), st) != hipSuccess) return YV_ERR_HIP;
+    if (b->schur_cap > 0 && (hipMemsetAsync(Q.sticket, 0, sizeof(unsigned) * b->schur_cap, st) != hipSuccess ||
+                             hipMemsetAsync(Q.rticket, 0, sizeof(unsigned) * std::max(1, Q.np), st) != hipSuccess))
+        return YV_ERR_HIP;
+    return YV_OK;
+}
+
 int ba_sync_scal(yv_ba* b, int n) {
     if (hipMemcpyAsync(b->h_scal, b->P.scal, sizeof(double) * n, hipMemcpyDeviceToHost, b->st) != hipSuccess ||
         hipStreamSynchronize(b->st) != hipSuccess)
@@ -1450,7 +1464,7 @@ extern "C" int yv_ba_create(yv_ctx* ctx, int max_poses, int max_landmarks, int m
     if (!out) return YV_ERR_INVALID;
     *out = nullptr;
     // the reduced pose system (6 max_poses)^2 doubles is factorised by one workgroup with its vectors in LDS
-    if (!ctx || max_poses < 1 || max_poses > 1024 || max_landmarks < 0 || max_edges < 0) return YV_ERR_INVALID;
+    if (!ctx || max_poses < 1 || max_poses > kBaMaxPoses || max_landmarks < 0 || max_edges < 0) return YV_ERR_INVALID;
     yv_ba* b = new yv_ba();
     b->ctx = ctx;
     b->dev = yavo::ctx_device(ctx);
@@ -1627,7 +1641,7 @@ extern "C" int yv_ba_set_problem(yv_ba* b, int n_poses, int n_fixed, int n_landm
     Q.nf = n_fixed;
     Q.np = P - n_fixed;
     Q.ns = 6 * Q.np;
-    if (ba_ensure_schur(b, Q.np, b->st) != YV_OK) return YV_ERR_HIP;
+    if (ba_ensure_schur(b, Q.np, b->st) != YV_OK || ba_reset_tickets(b, b->st) != YV_OK) return YV_ERR_HIP;
     Q.L = L;
     Q.E = E;
     Q.ep = b->d_ep;
@@ -1659,7 +1673,15 @@ namespace {
 // the device (yv_ba_window_solve) and stay there.
 // the enqueue half: chi2 at the start, then every iteration with one trial slot, then the control block's read-back
 // (asynchronous: ba_solve_wait collects it)
+int ba_solve_enqueue_(yv_ba* b, const double* poses, const double* landmarks, int max_iters);
+
 int ba_solve_enqueue(yv_ba* b, const double* poses, const double* landmarks, int max_iters) {
+    const int rc = ba_solve_enqueue_(b, poses, landmarks, max_iters);
+    if (rc != YV_OK) (void)ba_reset_tickets(b, b->st);
+    return rc;
+}
+
+int ba_solve_enqueue_(yv_ba* b, const double* poses, const double* landmarks, int max_iters) {
     yavo::BaParams& Q = b->P;
     const size_t pb = sizeof(double) * 7 * Q.P, xb = sizeof(double) * 3 * Q.L;
     hipStream_t st = b->st;
@@ -1880,7 +1902,7 @@ extern "C" int yv_debug_ldlt_prof(unsigned long long* out) {
 #endif
 
 extern "C" int yv_ba_debug_ldlt(yv_ctx* ctx, const double* S, int n, const double* b, double* x, int* ok) {
-    if (!ctx || !S || !b || !x || !ok || n < 1 || n > 4096) return YV_ERR_INVALID;
+    if (!ctx || !S || !b || !x || !ok || n < 1 || n > 6 * kBaMaxPoses) return YV_ERR_INVALID;
     if (hipSetDevice(yavo::ctx_device(ctx)) != hipSuccess) return YV_ERR_HIP;
     hipStream_t st = yavo::ctx_stream(ctx);
     double *dS = nullptr, *db = nullptr, *dx = nullptr, *ds = nullptr;

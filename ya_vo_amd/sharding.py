@@ -191,7 +191,8 @@ class FrameShard:
     def collective_stats(self):
         """Device times of the recorded exchanges (after drain): the all-gather (comm stream, events around the
         collective call), the placement after it, and whether the gather had finished by the time the context stream
-        finished the run it was exchanged beside (the next step's image kernels: then it is off the critical path)."""
+        finished the run it was exchanged beside (the next step's image kernels: then it is off the critical path).
+        Only exchanges issued beside a run are recorded (drain's last one has no run to hide behind)."""
         if not self._ev:
             return None
         g = [e0.elapsed_time(e1) for e0, e1, _, _ in self._ev]
@@ -199,12 +200,14 @@ class FrameShard:
         slack = [e1.elapsed_time(er) for _, e1, _, er in self._ev]  # > 0: the run ended after the gather
         return exchange_summary(g, pl, slack)
 
-    def _exchange(self) -> None:
+    def _exchange(self, overlapped: bool = True) -> None:
+        """overlapped: issued right after a run, which it overlaps (step); drain's final exchange overlaps nothing,
+        so it is not timed -- its slack would be measured against a run that had already finished."""
         import torch
         import torch.distributed as dist
         # the last track_map's block: all-gathered and placed on the communication stream once it is written
         self.batch.map_wait(self.comm.cuda_stream)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if self._timing else None
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if self._timing and overlapped else None
         with torch.cuda.stream(self.comm):
             if ev:
                 ev[0].record(self.comm)
@@ -244,7 +247,7 @@ class FrameShard:
         """Exchange the last block, then wait for every stream of the shard."""
         import torch
         if self._pending:
-            self._exchange()
+            self._exchange(overlapped=False)
         self.ctx.sync()
         self.batch.track_sync()
         torch.cuda.synchronize(self.d_prior.device)
