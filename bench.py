@@ -643,6 +643,15 @@ def main():
         except Exception as e:
             png_e2e["host_decode"] = {"error": repr(e)[:300]}
     seq = None
+    if args.sequence_frames > 0 and world > 1 and args.tracker == "match":
+        # configs[2]'s front end frame-sharded over the ranks (every rank; SequenceShard)
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import bench_sequence
+            seq = bench_sequence.measure_sharded(ctx, rank, world, args.sequence_frames, 20, repeats=5)
+        except Exception as e:  # reported, never fatal to the headline
+            seq = {"error": repr(e)[:300]}
     if args.sequence_frames > 0 and world == 1 and rank == 0 and args.tracker == "match":
         # BASELINE configs[2]: the full front end + local BA over the first 200 frames (tools/bench_sequence.py)
         try:

@@ -192,8 +192,8 @@ typedef struct yv_ba_window yv_ba_window;
 /* max_lm: landmark slots per frame (the batch's max_kp); max_kf: keyframes per added block */
 int yv_ba_window_create(yv_ba* ba, int max_lm, int max_kf, yv_ba_window** out);
 void yv_ba_window_destroy(yv_ba_window* w);
-/* size the record store for n_frames frames from the first recorded one (it grows by doubling from 64 otherwise, and
- * each growth allocates, copies and synchronises the device inside the frame loop) */
+/* size the record store for n_frames frames from the first recorded one, allocated by this call (it grows by doubling
+ * from 64 otherwise, and each growth allocates, copies and synchronises the device inside the frame loop) */
 int yv_ba_window_reserve(yv_ba_window* w, int64_t n_frames);
 /* record the frames [first_frame, first_frame + n_frames) of a placed map block (yv_map_place; every frame a
  * keyframe) on `stream` (NULL: the context's): T_wc, landmarks, uv_prev = edge_uv[k][e], uv_own =
@@ -222,6 +222,15 @@ int yv_ba_window_read(yv_ba_window* w, int64_t frame, double* T_wc, int* n, int3
                       double* uv_prev, int cap);
 /* T_wc [n][7] of the recorded frames [first, first + n) (host, blocking) */
 int yv_ba_window_trajectory(yv_ba_window* w, int64_t first, int n, double* T_wc);
+/* The recorded frames [first, first + n) as one map block (yavo_map.h, placed = 2) of a sequence shard, written on
+ * `stream` (NULL: the context's) after the records' writers finished (host wait): keyframe j = frame first + j with
+ * frame_id first + j + frame_id_offset, its T_wc and landmarks (ptID = frame_id << 16 | edge, X_w) as recorded, i.e.
+ * relative to the shard's first frame; header C = T_wc of chunk_frame (the shard's last frame), n_frames = n_kf = n.
+ * yv_map_place then places the gathered shards after each other (A_{r+1} = A_r C_r): T_wc = A_r T, X_w = A_r X.
+ * d_block holds yv_map_block_bytes(max_kf, lm_stride) bytes; n <= max_kf, lm_stride >= the window's max_lm.  The
+ * sequence's frame-sharded form (ya_vo_amd.sequence.SequenceShard). */
+int yv_ba_window_export_block(yv_ba_window* w, int64_t first, int n, int64_t chunk_frame, int64_t frame_id_offset,
+                              void* d_block, int max_kf, int lm_stride, void* stream);
 
 #ifdef __cplusplus
 }

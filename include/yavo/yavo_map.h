@@ -31,7 +31,9 @@ typedef struct yv_map_header {
     int32_t kf_every;    /* keyframe policy: global index % kf_every == 0 */
     int32_t lm_stride;   /* landmark slots per keyframe */
     int32_t max_kf;
-    int32_t placed;      /* 0: block-local (L_k, camera X); 1: world (T_wc, X_w) */
+    int32_t placed;      /* 0: block-local (L_k, camera X); 1: world (T_wc, X_w); 2: a sequence shard's export
+                          * (yv_ba_window_export_block: the shard's own T_wc and X_w, relative to its first frame);
+                          * 3: such an export placed in world coordinates */
     double pad[5];
 } yv_map_header; /* 128 B */
 

@@ -98,6 +98,7 @@ void or_map_place(void* blocks, int world, int64_t bb, double* base, double* anc
         yv_map_header* h = (yv_map_header*)b;
         yv_keyframe* kf = (yv_keyframe*)(b + sizeof(yv_map_header));
         yv_landmark* lm = (yv_landmark*)(b + lm_offset(h->max_kf));
+        const int shard_world = h->placed >= 2;  /* a sequence shard's export: local T_wc, local-world X */
         for (int j = 0; j < h->n_kf; ++j) {
             double T[7];
             or_se3_mul(anchors + 7 * r, kf[j].T, T);
@@ -105,10 +106,10 @@ void or_map_place(void* blocks, int world, int64_t bb, double* base, double* anc
             yv_landmark* l = lm + (int64_t)j * h->lm_stride;
             for (int q = 0; q < kf[j].n_landmarks; ++q) {
                 double Xw[3];
-                or_se3_act(T, l[q].X, Xw);
+                or_se3_act(shard_world ? anchors + 7 * r : T, l[q].X, Xw);
                 memcpy(l[q].X, Xw, sizeof Xw);
             }
         }
-        if (h->n_kf > 0) h->placed = 1;
+        if (h->n_kf > 0) h->placed = shard_world ? 3 : 1;
     }
 }

@@ -205,3 +205,53 @@ def test_parse_block_views_are_read_only(oracle):
     blk[128:136] = 0xFF  # the caller reuses its buffer: the view follows it
     assert kfs["frame_id"][0] != before[0]
     assert blk.flags.writeable  # the caller's own array stays writable
+
+
+def _shard_block(rng, oracle, first, n, max_kf, stride):
+    """A sequence shard's export (yv_ba_window_export_block layout, placed = 2) built on the host: its own T_wc per
+    frame (frame 0 of the shard at identity), X_w in the shard's frame, C = its last T_wc."""
+    bb = ymap.block_bytes(max_kf, stride)
+    raw = np.zeros(bb, np.uint8)
+    T = [np.array([0, 0, 0, 1, 0, 0, 0], np.float64)]
+    for _ in range(n - 1):
+        T.append(oracle.se3_mul(T[-1], oracle.se3_exp(rng.normal(0, 0.05, 6))))
+    h = raw[:128].view(ymap.HEADER_DTYPE)
+    h["chunk"], h["first_frame"], h["n_frames"], h["n_kf"] = T[-1], first, n, n
+    h["kf_every"], h["lm_stride"], h["max_kf"], h["placed"] = 1, stride, max_kf, 2
+    kfs = raw[128:128 + 72 * max_kf].view(ymap.KEYFRAME_DTYPE)
+    lmo = ymap.landmark_offset(max_kf)
+    for j in range(n):
+        c = int(rng.integers(0, stride))
+        kfs[j]["frame_id"], kfs[j]["T"], kfs[j]["n_landmarks"] = first + j, T[j], c
+        lm = raw[lmo + 32 * j * stride:lmo + 32 * (j * stride + c)].view(ymap.LANDMARK_DTYPE)
+        lm["id"] = ((first + j) << 16) + np.arange(c)
+        lm["X"] = rng.normal(0, 10, (c, 3))
+    return raw
+
+
+def test_place_sequence_shards(oracle):
+    """yv_map_place on sequence-shard exports (placed = 2, SequenceShard): A_0 = base, A_{r+1} = A_r C_r, keyframes
+    T_wc = A_r T, landmarks X_w = A_r X (the shard's own world frame, not a camera frame); placed becomes 3."""
+    rng = np.random.default_rng(8)
+    max_kf, stride = 6, 9
+    blocks = [_shard_block(rng, oracle, 0, 6, max_kf, stride), _shard_block(rng, oracle, 6, 5, max_kf, stride),
+              _shard_block(rng, oracle, 11, 4, max_kf, stride)]
+    bb = len(blocks[0])
+    base = oracle.se3_exp(rng.normal(0, 0.3, 6))
+    placed, new_base, anchors = oracle.map_place(np.concatenate(blocks), 3, bb, base)
+    A = base
+    for r, raw in enumerate(blocks):
+        h0, kf0, lm0 = ymap.parse_block(raw)
+        h1, kf1, lm1 = ymap.parse_block(placed[r * bb:(r + 1) * bb])
+        np.testing.assert_array_equal(anchors[r], A)
+        assert int(h1["placed"]) == 3
+        for j in range(int(h0["n_kf"])):
+            np.testing.assert_array_equal(kf1[j]["T"], oracle.se3_mul(A, kf0[j]["T"]))
+            np.testing.assert_array_equal(lm1[j]["id"], lm0[j]["id"])
+            for a, b in zip(lm0[j]["X"], lm1[j]["X"]):
+                np.testing.assert_array_equal(b, oracle.se3_act(A, a))
+        A = oracle.se3_mul(A, h0["chunk"])
+    np.testing.assert_array_equal(new_base, A)
+    m = ymap.Map()
+    m.insert_blocks(placed, 3, bb)  # a placed shard export reads as placed
+    assert sorted(m.frames) == list(range(15))

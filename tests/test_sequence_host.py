@@ -145,3 +145,12 @@ def test_device_window_cap_is_checked_up_front():
     from ya_vo_amd import sequence
     with pytest.raises(ValueError, match="at most 128 poses"):
         sequence.SequenceFrontend(None, 127, np.eye(3), np.array([0, 0, 0, 1, 0, -0.54, 0.0]), n_fixed=2)
+
+
+def test_shard_range_overlaps_by_one_frame():
+    from ya_vo_amd.sequence import shard_range
+    assert [shard_range(r, 4, 100) for r in range(4)] == [(0, 100), (99, 199), (198, 298), (297, 397)]
+    with pytest.raises(ValueError):
+        shard_range(2, 2, 100)
+    with pytest.raises(ValueError):
+        shard_range(0, 1, 1)

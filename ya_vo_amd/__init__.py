@@ -139,6 +139,7 @@ GEOM_SIGNATURES = {
     "yv_ba_window_solve_end": (_I, [_P, _P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "yv_ba_window_read": (_I, [_P, ctypes.c_int64, _P, ctypes.POINTER(_I), _P, _P, _P, _P, _I]),
     "yv_ba_window_trajectory": (_I, [_P, ctypes.c_int64, _I, _P]),
+    "yv_ba_window_export_block": (_I, [_P, ctypes.c_int64, _I, ctypes.c_int64, ctypes.c_int64, _P, _I, _I, _P]),
     "yv_lm_sum_mode": (_I, []),
     "yv_pose_lm_sum_mode": (_I, [_I]),
     "yv_track_lm_sum_mode": (_I, [_I]),
@@ -802,3 +803,11 @@ class BaWindow:
         T = np.zeros((n, 7))
         _check(self.lib.yv_ba_window_trajectory(self.handle, first, n, _ptr(T)), "yv_ba_window_trajectory")
         return T
+
+    def export_block(self, first: int, n: int, chunk_frame: int, frame_id_offset: int, d_block: int, max_kf: int,
+                     lm_stride: int, stream: int = 0) -> None:
+        """Recorded frames [first, first + n) as a sequence shard's map block (yv_ba_window_export_block)."""
+        _check(self.lib.yv_ba_window_export_block(self.handle, first, n, chunk_frame, frame_id_offset,
+                                                  ctypes.c_void_p(d_block), max_kf, lm_stride,
+                                                  ctypes.c_void_p(stream) if stream else None),
+               "yv_ba_window_export_block")

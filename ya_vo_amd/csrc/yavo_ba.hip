@@ -2022,6 +2022,46 @@ __global__ __launch_bounds__(256) void win_add_kernel(const uint8_t* __restrict_
     }
 }
 
+// one workgroup per exported frame: the record's T_wc and landmarks as a map block of a sequence shard (yavo_map.h
+// placed = 2: the shard's own T_wc / X_w, placed after the shards before it by yv_map_place)
+__global__ __launch_bounds__(256) void win_export_kernel(const double* __restrict__ T, const int32_t* __restrict__ cnt,
+                                                         const int32_t* __restrict__ edge, const double* __restrict__ X,
+                                                         int64_t s_first, int n, int64_t s_chunk, int64_t id0,
+                                                         int max_lm, int max_kf, int lm_stride, uint8_t* __restrict__ block) {
+    yv_map_header* h = reinterpret_cast<yv_map_header*>(block);
+    const int j = blockIdx.x;
+    if (j == 0 && threadIdx.x == 0) {
+        for (int i = 0; i < 7; ++i) h->chunk[i] = T[7 * s_chunk + i];
+        h->first_frame = id0;
+        h->n_frames = n;
+        h->n_kf = n;
+        h->kf_every = 1;
+        h->lm_stride = lm_stride;
+        h->max_kf = max_kf;
+        h->placed = 2;
+        for (int i = 0; i < 5; ++i) h->pad[i] = 0.0;
+    }
+    if (j >= n) return;
+    const int64_t s = s_first + j, g = id0 + j;
+    yv_keyframe* kf = reinterpret_cast<yv_keyframe*>(block + sizeof(yv_map_header)) + j;
+    const int64_t lmo = ((int64_t)sizeof(yv_map_header) + (int64_t)max_kf * (int64_t)sizeof(yv_keyframe) + 255) & ~255ll;
+    yv_landmark* lm = reinterpret_cast<yv_landmark*>(block + lmo) + (int64_t)j * lm_stride;
+    const int c = min(max(cnt[s], 0), lm_stride);
+    if (threadIdx.x < 7) kf->T[threadIdx.x] = T[7 * s + threadIdx.x];
+    if (threadIdx.x == 0) {
+        kf->frame_id = g;
+        kf->n_landmarks = c;
+        kf->pad = 0;
+    }
+    for (int l = threadIdx.x; l < c; l += 256) {
+        const int64_t o = s * max_lm + l;
+        lm[l].id = (g << 16) | (int64_t)edge[o];
+        lm[l].X[0] = X[3 * o];
+        lm[l].X[1] = X[3 * o + 1];
+        lm[l].X[2] = X[3 * o + 2];
+    }
+}
+
 struct WinFrames {
     int P;
     int64_t s0;                   // store index of the window's first frame
@@ -2246,8 +2286,16 @@ extern "C" void yv_ba_window_destroy(yv_ba_window* w) {
 extern "C" int yv_ba_window_reserve(yv_ba_window* w, int64_t n_frames) {
     if (!w || n_frames < 0 || n_frames > (int64_t)1 << 24 || w->solving) return YV_ERR_INVALID;
     w->hint = n_frames;
-    if (w->g0 < 0 || n_frames <= w->cap) return YV_OK;  // sized at the first add_block
+    if (n_frames <= w->cap) return YV_OK;
     if (hipSetDevice(w->ba->dev) != hipSuccess) return YV_ERR_HIP;
+    if (w->g0 < 0) {
+        // nothing recorded yet: allocate the store now, not at the first add_block, which runs inside the caller's
+        // frame loop (the store is ~150 MB per 1000 frames at 2000 landmark slots); its origin stays unset
+        w->g0 = 0;
+        const int rc = win_reserve(w, 0, n_frames, yavo::ctx_stream(w->ba->ctx));
+        w->g0 = -1;
+        return rc;
+    }
     return win_reserve(w, w->g0, w->g0 + n_frames, yavo::ctx_stream(w->ba->ctx));
 }
 
@@ -2421,6 +2469,30 @@ extern "C" int yv_ba_window_read(yv_ba_window* w, int64_t frame, double* T_wc, i
         (uv_prev && k && hipMemcpy(uv_prev, w->d_uvp + 2 * o, sizeof(double) * 2 * k, hipMemcpyDeviceToHost) != hipSuccess))
         return YV_ERR_HIP;
     return YV_OK;
+}
+
+extern "C" int yv_ba_window_export_block(yv_ba_window* w, int64_t first, int n, int64_t chunk_frame,
+                                         int64_t frame_id_offset, void* d_block, int max_kf, int lm_stride,
+                                         void* stream) {
+    if (!w || !d_block || n < 0 || n > max_kf || max_kf < 1 || lm_stride < w->max_lm || w->solving ||
+        frame_id_offset < 0 || first + frame_id_offset < 0 || first + frame_id_offset + n > ((int64_t)1 << 47))
+        return YV_ERR_INVALID;
+    if (hipSetDevice(w->ba->dev) != hipSuccess || win_collect(w) != YV_OK) return YV_ERR_HIP;
+    if ((n > 0 && (first < w->g0 || first + n > w->g0 + w->cap)) || chunk_frame < w->g0 ||
+        chunk_frame >= w->g0 + w->cap)
+        return YV_ERR_INVALID;
+    for (int64_t g = first; g < first + n; ++g)
+        if (w->h_cnt[(size_t)(g - w->g0)] < 0) return YV_ERR_INVALID;  // not recorded
+    if (w->h_cnt[(size_t)(chunk_frame - w->g0)] < 0) return YV_ERR_INVALID;
+    // the records' last writers (add_block on its stream, the window write-back on the BA stream) are finished
+    if (hipStreamSynchronize(yavo::ctx_stream(w->ba->ctx)) != hipSuccess ||
+        hipStreamSynchronize(w->ba->st) != hipSuccess)
+        return YV_ERR_HIP;
+    hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : yavo::ctx_stream(w->ba->ctx);
+    hipLaunchKernelGGL(win_export_kernel, dim3(std::max(n, 1)), dim3(256), 0, st, w->d_T, w->d_cnt,
+                       w->d_edge, w->d_X, first - w->g0, n, chunk_frame - w->g0, first + frame_id_offset, w->max_lm,
+                       max_kf, lm_stride, static_cast<uint8_t*>(d_block));
+    return hipGetLastError() == hipSuccess ? YV_OK : YV_ERR_HIP;
 }
 
 extern "C" int yv_ba_window_trajectory(yv_ba_window* w, int64_t first, int n, double* T_wc) {

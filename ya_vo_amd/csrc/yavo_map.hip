@@ -7,7 +7,8 @@
 //                         keyframe records (global index % kf_every == 0)
 //   map_landmarks_kernel  one 256-thread workgroup per keyframe: its LM inliers in edge order (ballot compaction)
 //   map_anchor_kernel     one lane: A_0 = base, A_{r+1} = A_r * C_r over the gathered blocks; base <- A_world
-//   map_place_kernel      one workgroup per (block, keyframe): T_wc = A_r * L_k, X_w = T_wc * X
+//   map_place_kernel      one workgroup per (block, keyframe): T_wc = A_r * L_k, X_w = T_wc * X (a sequence shard's
+//                         export, placed = 2: T_wc = A_r * T, X_w = A_r * X)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -137,18 +138,22 @@ __global__ __launch_bounds__(kNT) void map_place_kernel(uint8_t* blocks, int64_t
     for (int j = blockIdx.x; j < n_kf; j += gridDim.x) {
         yv_keyframe* kf = reinterpret_cast<yv_keyframe*>(block + kf_offset()) + j;
         yv_landmark* lm = reinterpret_cast<yv_landmark*>(block + lm_offset(h->max_kf)) + (int64_t)j * h->lm_stride;
-        double Lk[7], T[7];
+        double Lk[7], T[7], A[7];
         for (int i = 0; i < 7; ++i) Lk[i] = kf->T[i];
-        se3_mul(anchors + 7 * r, Lk, T);
+        for (int i = 0; i < 7; ++i) A[i] = anchors[7 * r + i];
+        se3_mul(A, Lk, T);
         const int n = kf->n_landmarks;
+        // a sequence shard's export (2, or 3 once a workgroup placed it -- other workgroups may read it after that
+        // write): X_w = A_r X (the shard's own world frame)
+        const bool shard_world = h->placed >= 2;
         __syncthreads();  // every lane has read L_k
         if (threadIdx.x == 0) {
             for (int i = 0; i < 7; ++i) kf->T[i] = T[i];
-            if (j == 0) h->placed = 1;
+            if (j == 0) h->placed = shard_world ? 3 : 1;
         }
         for (int q = threadIdx.x; q < n; q += kNT) {
             double Xc[3] = {lm[q].X[0], lm[q].X[1], lm[q].X[2]}, Xw[3];
-            se3_act(T, Xc, Xw);
+            se3_act(shard_world ? A : T, Xc, Xw);
             lm[q].X[0] = Xw[0];
             lm[q].X[1] = Xw[1];
             lm[q].X[2] = Xw[2];

@@ -87,7 +87,7 @@ class Map:
         raw = np.ascontiguousarray(blocks).view(np.uint8).reshape(-1)
         for r in range(world):
             h, kfs, lms = parse_block(raw[r * block_bytes_:(r + 1) * block_bytes_])
-            if int(h["n_kf"]) and not int(h["placed"]):
+            if int(h["n_kf"]) and int(h["placed"]) not in (1, 3):  # 1 / 3: placed (a frame chunk / a sequence shard)
                 raise ValueError(f"block {r} is not placed in world coordinates")
             for kf, lm in zip(kfs, lms):
                 self.insert_keyframe(int(kf["frame_id"]), kf["T"])

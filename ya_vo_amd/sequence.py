@@ -310,3 +310,99 @@ class SequenceFrontend:
         if self.win is not None:
             return self.win.trajectory(0, self.next_frame)
         return np.stack([self._records[g].T_wc for g in sorted(self._records)])
+
+
+def shard_range(rank: int, world: int, frames_per_rank: int) -> Tuple[int, int]:
+    """[first, end) of the frames rank r runs: contiguous shards of `frames_per_rank` frames overlapping by one frame
+    (the 1-frame halo: shard r starts at shard r - 1's last frame, so its first temporal pair is the sequence's own and
+    its trajectory can be placed after shard r - 1's). A world of W ranks covers W (n - 1) + 1 frames."""
+    if not 0 <= rank < world or frames_per_rank < 2:
+        raise ValueError("bad rank / world / frames_per_rank")
+    first = rank * (frames_per_rank - 1)
+    return first, first + frames_per_rank
+
+
+class SequenceShard:
+    """The frame-sharded form of the sequence front end (BASELINE configs[3] / [4] on N GPUs; SURVEY.md 8e: the
+    front end shards with a 1-frame halo, pose chaining is serial): ONE sequence split over `world` ranks
+    (shard_range). Rank r runs its frames through its own SequenceFrontend -- detect .. pose LM, the shared map, the
+    local BA windows -- with its trajectory starting at identity at its first frame; no collective on the data path.
+    finish() exports the shard's frames (rank r > 0 without its first frame, which shard r - 1 owns) as one map block
+    (yv_ba_window_export_block), all-gathers the blocks (RCCL over xGMI; gloo for the CPU / shared-GPU rehearsal) and
+    places them after each other on every rank (yv_map_place: A_0 = I, A_{r+1} = A_r C_r with C_r the shard's last
+    pose; T_wc = A_r T, X_w = A_r X). Each shard's local result is what a one-rank SequenceFrontend run over the same
+    frames gives, bit for bit; the BA windows do not straddle shards (replicas)."""
+
+    def __init__(self, ctx, rank: int, world: int, frames_per_rank: int, chunk: int, K, T_right, n_fixed: int = 2,
+                 ba_iters: int = 10, H: int = 376, W: int = 1241, max_kp: int = 2000, match_thr: int = 20):
+        import torch
+        if frames_per_rank % chunk:
+            raise ValueError("frames_per_rank must be a multiple of chunk")
+        self.ctx, self.rank, self.world, self.n, self.max_kp = ctx, rank, world, frames_per_rank, max_kp
+        self.first, self.end = shard_range(rank, world, frames_per_rank)
+        self.fe = SequenceFrontend(ctx, chunk, K, T_right, n_fixed=n_fixed, ba_iters=ba_iters, H=H, W=W,
+                                   max_kp=max_kp, match_thr=match_thr, expected_frames=frames_per_rank)
+        dev = torch.device("cuda", ctx.device)
+        self.bb = ymap.block_bytes(frames_per_rank, max_kp)
+        self.d_block = torch.zeros(self.bb, dtype=torch.uint8, device=dev)
+        import torch.distributed as dist
+        self.collective = dist.is_available() and dist.is_initialized()
+        if (self.collective and dist.get_world_size() != world) or (world > 1 and not self.collective):
+            raise ValueError("world must match the process group (and N > 1 needs one)")
+        self.d_gathered = torch.zeros((world, self.bb), dtype=torch.uint8, device=dev) if self.collective \
+            else self.d_block.view(1, self.bb)
+        self.d_base = torch.zeros(7, dtype=torch.float64, device=dev)
+        self.d_anchors = torch.zeros((world, 7), dtype=torch.float64, device=dev)
+        self.seconds_exchange = 0.0
+
+    def process_chunk(self, d_images, seconds: Dict[str, float] = None) -> None:
+        """d_images: device uint8 [2 * chunk, H, W] of the shard's next chunk (SequenceFrontend.process_chunk)."""
+        self.fe.process_chunk(d_images, seconds)
+
+    def finish(self) -> None:
+        """The last BA window, the shard's block, the all-gather and the placement (every rank)."""
+        import time
+        import torch
+        import torch.distributed as dist
+        fe = self.fe
+        if fe.next_frame != self.n:
+            raise RuntimeError(f"shard holds {fe.next_frame} of its {self.n} frames")
+        fe.flush()
+        lo = 0 if self.rank == 0 else 1
+        t0 = time.perf_counter()
+        fe.win.export_block(lo, self.n - lo, self.n - 1, self.first, self.d_block.data_ptr(), self.n, self.max_kp)
+        self.ctx.sync()
+        if self.collective and dist.get_backend() == "nccl":
+            dist.all_gather_into_tensor(self.d_gathered, self.d_block)
+        elif self.collective:  # gloo: list form
+            dist.all_gather(list(self.d_gathered.unbind(0)), self.d_block)
+        self.d_base.copy_(torch.from_numpy(IDENTITY.copy()))
+        stream = torch.cuda.current_stream(self.d_block.device)
+        self.ctx.map_place(self.d_gathered.data_ptr(), self.world, self.bb, self.d_base.data_ptr(),
+                           self.d_anchors.data_ptr(), stream=stream.cuda_stream)
+        stream.synchronize()
+        self.seconds_exchange = time.perf_counter() - t0
+
+    def local_trajectory(self) -> np.ndarray:
+        """[n, 7] T_wc of the shard's frames relative to its first frame (the one-rank run's trajectory)."""
+        return self.fe.trajectory()
+
+    def placed_blocks(self) -> np.ndarray:
+        """[world, block_bytes] uint8: every shard's block in world coordinates (the same on every rank)."""
+        return self.d_gathered.cpu().numpy().reshape(self.world, self.bb)
+
+    def trajectory(self) -> np.ndarray:
+        """[world (n - 1) + 1, 7] T_wc of the whole sequence from the placed blocks."""
+        out = []
+        for blk in self.placed_blocks():
+            _, kfs, _ = ymap.parse_block(blk)
+            out.append(np.array(kfs["T"], np.float64))
+        return np.concatenate(out)
+
+    def map(self) -> "ymap.Map":
+        m = ymap.Map()
+        m.insert_blocks(self.placed_blocks(), self.world, self.bb)
+        return m
+
+    def close(self) -> None:
+        self.fe.close()
