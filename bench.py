@@ -751,7 +751,7 @@ def main():
                 a = mops / (t_ms / 1e3) / 1e12
                 per_stage[st] = {"bound": "mfma_fp4", "achieved": round(a, 1), "peak": FP4_MFMA_PEAK_TOPS,
                                  "unit": "T op/s", "frac": round(a / FP4_MFMA_PEAK_TOPS, 4)}
-            elif st == "track_pose":
+            elif st in ("track_pose", "track_edges"):
                 # FP64 VALU: the launch's FP64 wave-instructions from the PMC pass (tools/pmc_traffic.sh,
                 # profiles/pmc_traffic.json) over this run's per-launch time.  SQ_INSTS_VALU_FLOPS_FP64 counts per
                 # wave-instruction (ADD + MUL + 2 FMA), so lane-FLOPs = 64 x it, an upper bound (the LM's lane-0 LDLT
@@ -764,10 +764,14 @@ def main():
                                      "issue_frac": round(4 * f["wave_instructions"] / (SIMD_CYCLES_PER_S * t_ms / 1e3), 4),
                                      "fp64_wave_flops_per_launch": f["flops"],
                                      "fp64_wave_instructions_per_launch": f["wave_instructions"],
-                                     "note": "serial LM per problem, beside the next step's image kernels (DESIGN.md "
-                                             "4.2, 4.4); achieved = 64 lanes x PMC FP64 wave-FLOPs / launch time"}
+                                     "note": ("serial LM per problem, beside the next step's image kernels (DESIGN.md "
+                                              "4.2, 4.4)" if st == "track_pose" else
+                                              "one 4 x 4 Jacobi SVD triangulation per stereo edge, beside the next "
+                                              "step's detect (DESIGN.md 4.3, 7.1)") +
+                                             "; achieved = 64 lanes x PMC FP64 wave-FLOPs / launch time"}
                 else:
-                    per_stage[st] = {"bound": "latency", "note": "serial LM per problem (DESIGN.md 4.2)",
+                    per_stage[st] = {"bound": "latency" if st == "track_pose" else "fp64_valu",
+                                     "note": "FP64 counters not taken at this code (profiles/pmc_traffic.json)",
                                      "ms": round(t_ms, 4)}
             else:
                 a = nbytes[st] / (t_ms / 1e3) / 1e9

@@ -28,7 +28,8 @@ def main():
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = rank % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev)
-    dist.init_process_group(backend, rank=rank, world_size=world,
+    import datetime
+    dist.init_process_group(backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120),
                             **({"device_id": torch.device("cuda", dev)} if backend == "nccl" else {}))
     ctx = yv.Context(dev)
     ctx.set_brief_offsets(np.fromfile(os.path.join(ROOT, "tests", "golden", "brief_offsets_mt19937_42.bin"),

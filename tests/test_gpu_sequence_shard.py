@@ -37,8 +37,14 @@ def _spawn(world, n, chunk, seed, tmp_path, backend="gloo"):
     procs = [subprocess.Popen([sys.executable, os.path.join(TESTS, "sequence_shard_worker.py"), str(r), str(world),
                                str(port), str(n), str(chunk), str(seed), str(tmp_path / f"rank{r}.npz"), backend],
                               env=env) for r in range(world)]
-    for p in procs:
-        assert p.wait(timeout=240) == 0
+    try:
+        for p in procs:
+            assert p.wait(timeout=240) == 0
+    finally:
+        for p in procs:  # a rank that failed leaves its peer inside a collective: end both
+            if p.poll() is None:
+                p.kill()
+                p.wait()
     return [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
 
 

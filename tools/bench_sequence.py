@@ -11,6 +11,7 @@ textured fronto-parallel plane, right image +8 columns).
                                    [--cpu-threads 16] [--out f.json]
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -77,24 +78,34 @@ def measure(frames=1000, chunk=20, n_fixed=2, ba_iters=10, repeats=5, cpu_thread
         fe = SequenceFrontend(ctx, chunk, K, t_right, n_fixed=n_fixed, ba_iters=ba_iters, H=H, W=W,
                               device_window=not host_window, ba_priority=ba_priority, expected_frames=m)
         sec = {}
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for c in range(m // chunk):
-            fe.process_chunk(d[2 * c * chunk:2 * (c + 1) * chunk], sec)
-        fe.flush(sec)
-        torch.cuda.synchronize()
-        return fe, time.perf_counter() - t0, sec
+        # Python's cyclic collector stays out of the timed loop: a full collection is a host stall of its own, and
+        # the loop issues the GPU work from this thread
+        gc.collect()
+        gc.disable()
+        try:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for c in range(m // chunk):
+                fe.process_chunk(d[2 * c * chunk:2 * (c + 1) * chunk], sec)
+            fe.flush(sec)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+        finally:
+            gc.enable()
+        return fe, dt, sec
 
     fe, _, _ = run(n)  # warm-up (first launches, allocations)
     fe.close()
     times, secs = [], []
-    traj = ba_log = records = None
-    for _ in range(repeats):
+    traj = ba_log = None
+    n_landmarks = 0
+    for r in range(repeats):
         fe, dt, sec = run(n)
         times.append(dt)
         secs.append(sec)
         traj, ba_log = fe.trajectory(), fe.ba_log
-        records = fe.records
+        if r == repeats - 1:
+            n_landmarks = int(sum(len(rec.edge) for rec in fe.records.values()))
         fe.close()
     med = int(np.argsort(times)[len(times) // 2])  # the median run (odd repeats) or the upper middle one
     t_med = float(np.median(times))
@@ -112,7 +123,7 @@ def measure(frames=1000, chunk=20, n_fixed=2, ba_iters=10, repeats=5, cpu_thread
         "phase_seconds": {k: round(v, 4) for k, v in secs[med].items()},
         "ba_solves": len(ba_log),
         "ba_ms_per_solve": round(1e3 * secs[med].get("ba", 0.0) / max(len(ba_log), 1), 4),
-        "landmarks": int(sum(len(r.edge) for r in records.values())),
+        "landmarks": n_landmarks,
         "inputs": "frames resident in HBM before the timed region (PCIe excluded)",
     }
     from sequence_chain import front_end, ground_truth, rmse_translation, sequence_from_tracks
@@ -199,14 +210,19 @@ def measure_sharded(ctx, rank, world, frames=1000, chunk=20, n_fixed=2, ba_iters
 
     def run():
         sh = SequenceShard(ctx, rank, world, frames, chunk, K, T_RIGHT, n_fixed=n_fixed, ba_iters=ba_iters, H=H, W=W)
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for c in range(frames // chunk):
-            sh.process_chunk(d[2 * c * chunk:2 * (c + 1) * chunk])
-        sh.finish()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
+        gc.collect()
+        gc.disable()
+        try:
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for c in range(frames // chunk):
+                sh.process_chunk(d[2 * c * chunk:2 * (c + 1) * chunk])
+            sh.finish()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+        finally:
+            gc.enable()
         t = torch.tensor([dt, sh.seconds_exchange], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return sh, float(t[0].item()), float(t[1].item())

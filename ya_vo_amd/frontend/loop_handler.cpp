@@ -2,6 +2,7 @@
 // /root/reference/src/LoopHandler.cc unless noted.
 #include "loop_handler.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <climits>
 #include <cstdlib>
@@ -32,6 +33,96 @@ double now_s() {
 int trunc_int(double v) {
     if (!(v > -2147483649.0 && v < 2147483648.0)) return INT_MIN;
     return (int)v;
+}
+
+// One call of every host-pointer primitive a context serves in the loop, on synthetic data of the sequence's size
+// (an H x W noise image and a copy shifted by (1, 3) pixels; its 2000 keypoints, matches, points and edges).  The
+// first call of each primitive on a context loads its kernels and sizes its workspaces and pinned staging (the
+// essential-matrix workspace, the LK image slots and pyramids, the call arenas); done here, at construction, that
+// one-time cost stays out of the per-frame loop.  No state that a later call reads survives it (the BRIEF offsets
+// are the caller's; the LK image slots are overwritten by the first real call, which finds no match).
+struct WarmParts {
+    bool features = false, matching = false, geometry = false, ransac = false, lk = false;
+};
+
+int warm_context(yv_ctx* ctx, int H, int W, const double K[9], const WarmParts& w) {
+    if (!ctx || H < 32 || W < 32) return YV_OK;
+    std::vector<uint8_t> a((size_t)H * W), b((size_t)H * W);
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (auto& v : a) {
+        x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+        v = (uint8_t)(x >> 56);
+    }
+    for (int r = 0; r < H; ++r)
+        for (int c = 0; c < W; ++c) b[(size_t)r * W + c] = a[(size_t)std::min(r + 1, H - 1) * W + std::min(c + 3, W - 1)];
+    const int max_kp = 2000;
+    std::vector<int32_t> rc(2 * max_kp);
+    std::vector<float> resp(max_kp);
+    int n = 0, nc = 0, st = YV_OK;
+    if ((st = yv_detect(ctx, a.data(), H, W, W, max_kp, rc.data(), resp.data(), &n, &nc)) != YV_OK) return st;
+    std::vector<yv_keypoint> kp(std::max(n, 1));
+    int nk = 0;
+    if ((w.features || w.matching) &&
+        (st = yv_describe(ctx, a.data(), H, W, W, rc.data(), n, kp.data(), &nk)) != YV_OK)
+        return st;
+    std::vector<yv_match> m(std::max(nk, 1)), f(std::max(nk, 1));
+    int nf = 0;
+    if (w.matching && ((st = yv_match_features(ctx, kp.data(), nk, kp.data(), nk, m.data())) != YV_OK ||
+                       (st = yv_filter_matches(ctx, m.data(), nk, 20, f.data(), &nf)) != YV_OK))
+        return st;
+    for (int i = 0; i < nk; ++i) {  // the second view: the keypoint moved by (1, 3)
+        m[i].pt1 = kp[i];
+        m[i].pt2 = kp[i];
+        m[i].pt2.x = kp[i].x + 1;
+        m[i].pt2.y = kp[i].y + 3;
+        m[i].distance = 0;
+    }
+    if (w.ransac && nk >= 8) {
+        std::vector<int32_t> samples(8 * 400);
+        for (size_t i = 0; i < samples.size(); ++i) samples[i] = (int32_t)((i * 7919u) % (unsigned)nk);
+        double F[9];
+        int inl = 0, found = 0;
+        if ((st = yv_f_ransac(ctx, m.data(), nk, samples.data(), 400, 0.1, F, &inl, &found)) != YV_OK) return st;
+    }
+    if (w.geometry && nk >= 5) {
+        std::vector<float> p1(2 * (size_t)nk), p2(2 * (size_t)nk);
+        for (int i = 0; i < nk; ++i) {
+            p1[2 * i] = (float)m[i].pt1.x, p1[2 * i + 1] = (float)m[i].pt1.y;
+            p2[2 * i] = (float)m[i].pt2.x, p2[2 * i + 1] = (float)m[i].pt2.y;
+        }
+        double E[9], R[9], t[3];
+        std::vector<uint8_t> mask(nk);
+        int found = 0, good = 0;
+        if ((st = yv_find_essential(ctx, p2.data(), p1.data(), nk, K[0], K[2], K[5], 0.999, 1.0, E, mask.data(),
+                                    &found)) != YV_OK ||
+            (st = yv_recover_pose(ctx, E, p2.data(), p1.data(), nk, K, R, t, &good)) != YV_OK)
+            return st;
+        const double Ta[7] = {0, 0, 0, 1, 0, 0, 0}, Tb[7] = {0, 0, 0, 1, -0.5, 0, 0};
+        std::vector<double> X(3 * (size_t)nk), proj(3 * (size_t)nk), uv(2 * (size_t)nk);
+        std::vector<uint8_t> ok(nk), outl(nk);
+        int n_ok = 0, inl = 0;
+        if ((st = yv_triangulate(ctx, Ta, Tb, K, m.data(), nk, X.data(), ok.data(), &n_ok)) != YV_OK) return st;
+        for (int i = 0; i < nk; ++i) {  // points in front of the camera, measured where they project
+            X[3 * i] = (m[i].pt1.y - K[2]) / K[0] * 10.0;
+            X[3 * i + 1] = (m[i].pt1.x - K[5]) / K[4] * 10.0;
+            X[3 * i + 2] = 10.0;
+            uv[2 * i] = m[i].pt1.x;
+            uv[2 * i + 1] = m[i].pt1.y;
+        }
+        double pose[7] = {0, 0, 0, 1, 0.01, 0, 0};
+        if ((st = yv_world2camera(ctx, X.data(), nk, pose, K, proj.data())) != YV_OK ||
+            (st = yv_pose_lm(ctx, X.data(), uv.data(), nk, K, pose, outl.data(), &inl)) != YV_OK)
+            return st;
+    }
+    if (w.lk && nk > 0) {
+        std::vector<float> pts(2 * (size_t)nk), nxt(2 * (size_t)nk), err(nk);
+        std::vector<uint8_t> status(nk);
+        for (int i = 0; i < nk; ++i) pts[2 * i] = (float)kp[i].y, pts[2 * i + 1] = (float)kp[i].x;
+        if ((st = yv_calc_optical_flow_pyr_lk(ctx, a.data(), b.data(), H, W, W, pts.data(), nk, 11, 3, 30, 0.01,
+                                              0.001, nxt.data(), status.data(), err.data())) != YV_OK)
+            return st;
+    }
+    return yv_sync(ctx);
 }
 
 }  // namespace
@@ -83,6 +174,7 @@ LoopHandler::LoopHandler(const std::string& config, Device* dev) : dev_(dev) {
         if (isStereo_ && yv_seq_path(seq, i, 1, buf, sizeof buf) > 0) rightPathTrain.emplace_back(buf);
     }
     double P0[16], P1[16], K1[9];
+    if (yv_seq_size(seq, &H_, &W_) != YV_OK) H_ = W_ = 0;  // the first image's size (warmup)
     st = yv_seq_calib(seq, P0, P1, K_, K1);
     yv_seq_close(seq);
     if (st != YV_OK) {
@@ -597,6 +689,17 @@ void LoopHandler::runVO(int max_frames) {
     }
 }
 
+// the tracking thread's context: every primitive addFrame calls (and detect / describe of the serial loop)
+bool LoopHandler::warmup() {
+    if (!dev_ || !dev_->ok()) return false;
+    const double t0 = now_s();
+    WarmParts w;
+    w.features = w.matching = w.geometry = w.ransac = w.lk = true;
+    const bool ok = gpu(warm_context(dev_->ctx(), H_, W_, K_, w), "warmup");
+    t_warmup += now_s() - t0;
+    return ok;
+}
+
 void LoopHandler::setPipeline(int depth, int device, const std::vector<int8_t>& briefOffsets, int readers,
                               int gpu_batch) {
     pipeline_readers_ = readers;
@@ -605,8 +708,27 @@ void LoopHandler::setPipeline(int depth, int device, const std::vector<int8_t>& 
     pipeline_device_ = device;
     pipeline_offsets_ = briefOffsets;
     if (pipeline_depth_ > 0) {
+        const double t0 = now_s();
         worker_dev_ = std::make_unique<Device>(device);
         side_lane_ = std::make_unique<SideLane>(device);  // its thread makes its own context meanwhile
+        // warm both: the worker's detect / describe (its offsets are set again by the worker thread) and the side
+        // lane's getFRANSAC / LK, on the side lane's own thread
+        std::promise<int> side_done;
+        auto side_st = side_done.get_future();
+        const int H = H_, W = W_;
+        const double* K = K_;
+        side_lane_->submit([&side_done, H, W, K](Device& d) {
+            WarmParts w;
+            w.ransac = w.lk = true;
+            side_done.set_value(d.ok() ? warm_context(d.ctx(), H, W, K, w) : d.status());
+        });
+        if (worker_dev_->ok() && yv_set_brief_offsets(worker_dev_->ctx(), pipeline_offsets_.data()) == YV_OK) {
+            WarmParts w;
+            w.features = true;
+            gpu(warm_context(worker_dev_->ctx(), H_, W_, K_, w), "warmup (pipeline worker)");
+        }
+        gpu(side_st.get(), "warmup (side lane)");
+        t_warmup += now_s() - t0;
     }
 }
 

@@ -128,6 +128,11 @@ public:
     // batch is decoded while this one's frames are handed over.
     void setPipeline(int depth, int device, const std::vector<int8_t>& briefOffsets, int readers = 4,
                      int gpu_batch = 0);
+    // One call of every primitive on this context with synthetic data of the sequence's size, before the loop: the
+    // first call of a primitive loads its kernels and sizes its workspaces (setPipeline does the same for the worker
+    // context and the side lane).  Results are unchanged; t_warmup has the time.
+    bool warmup();
+    double t_warmup = 0;
     static Frame::ptr readFrame(const std::string& path);  // cv::imread(path, IMREAD_GRAYSCALE)
 
     // every added frame's pose (T_cw, SE3d::data()) in order, and what happened to it
@@ -154,6 +159,7 @@ private:
     bool ok_ = false;
     std::string error_;
     double K_[9] = {0, 0, 0, 0, 0, 0, 0, 0, 1};
+    int H_ = 0, W_ = 0;  // the sequence's image size (yv_seq_size)
     Device* dev_ = nullptr;
     std::unique_ptr<FastDetector> fd_;
     std::unique_ptr<Brief> brief_;

@@ -13,6 +13,7 @@
 //   --pipeline       DEPTH > 0: frame k + 1's read + detect + describe on a worker thread (own GPU context) while
 //                    frame k is tracked (LoopHandler::setPipeline); the results are the serial loop's
 //   --readers        pipelined: frames read + PNG-decoded ahead on their own threads (default 4)
+//   --no-warmup      skip LoopHandler::warmup (every context's primitives called once before runVO)
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -41,7 +42,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     const std::string config = argv[1];
-    int frames = -1, device = 0, pipeline = 0, readers = 4, gpu_decode = 0;
+    int frames = -1, device = 0, pipeline = 0, readers = 4, gpu_decode = 0, warm = 1;
     uint32_t seed = 42;
     bool check = false;
     std::string poses_txt, poses_bin, events_bin;
@@ -58,6 +59,7 @@ int main(int argc, char** argv) {
         else if (a == "--readers") readers = std::atoi(next().c_str());
         else if (a == "--gpu-decode") gpu_decode = std::atoi(next().c_str());
         else if (a == "--check-config") check = true;
+        else if (a == "--no-warmup") warm = 0;
         else {
             std::cerr << "unknown option " << a << std::endl;
             return 2;
@@ -97,7 +99,10 @@ int main(int argc, char** argv) {
     Brief offsets_setter(dev, 256);
     const std::vector<int8_t> offsets = Brief::preComputeOffsets(seed);
     if (!offsets_setter.setOffsets(offsets)) return 3;
+    // every context is warmed before the loop (LoopHandler::warmup): kernels loaded, workspaces sized
+    if (warm && !lh.warmup()) return 3;
     if (pipeline > 0) lh.setPipeline(pipeline, device, offsets, readers, gpu_decode);
+    if (lh.gpuStatus() != YV_OK) return 3;
 
     const auto t0 = std::chrono::steady_clock::now();
     lh.runVO(frames);
@@ -135,6 +140,7 @@ int main(int argc, char** argv) {
               << ", \"seconds_features\": " << lh.t_features << ", \"seconds_init\": " << lh.t_init
               << ", \"seconds_track\": " << lh.t_track << ", \"seconds_reinit\": " << lh.t_reinit
               << ", \"seconds_read\": " << lh.t_read << ", \"seconds_wait\": " << lh.t_wait
+              << ", \"seconds_warmup\": " << lh.t_warmup
               << ", \"pipeline\": " << pipeline << ", \"readers\": " << (pipeline > 0 ? readers : 0)
               << ", \"gpu_decode_batch\": " << (pipeline > 0 ? gpu_decode : 0) << ", \"primitives_s\": {"
               << "\"world2camera\": " << lh.primitiveTimes().world2camera << ", \"lk\": " << lh.primitiveTimes().lk

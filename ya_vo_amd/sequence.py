@@ -377,10 +377,10 @@ class SequenceShard:
         elif self.collective:  # gloo: list form
             dist.all_gather(list(self.d_gathered.unbind(0)), self.d_block)
         self.d_base.copy_(torch.from_numpy(IDENTITY.copy()))
-        stream = torch.cuda.current_stream(self.d_block.device)
+        torch.cuda.synchronize(self.d_block.device)  # the gathered blocks and the base are in place
         self.ctx.map_place(self.d_gathered.data_ptr(), self.world, self.bb, self.d_base.data_ptr(),
-                           self.d_anchors.data_ptr(), stream=stream.cuda_stream)
-        stream.synchronize()
+                           self.d_anchors.data_ptr())  # on the context stream
+        self.ctx.sync()
         self.seconds_exchange = time.perf_counter() - t0
 
     def local_trajectory(self) -> np.ndarray:
