@@ -98,3 +98,39 @@ def test_sequence_shard_rccl_world1_equals_one_rank(ctx, tmp_path):
     fe.close()
     np.testing.assert_array_equal(res[0]["local"], traj)
     np.testing.assert_array_equal(res[0]["trajectory"], traj)
+
+
+def test_window_export_block_guards(ctx):
+    """yv_ba_window_export_block refuses what it cannot write: frames never recorded, a landmark stride below the
+    window's, more frames than keyframe slots, and an export while a window solve is pending."""
+    import torch
+    from ya_vo_amd import map as ymap
+    from ya_vo_amd.sequence import SequenceFrontend
+    n, chunk = 40, 20
+    frames = synth_sequence(73, n, stereo=True)
+    d = torch.from_numpy(frames.reshape(2 * n, *frames.shape[2:])).to("cuda:0")
+    fe = SequenceFrontend(ctx, chunk, scene.K_KITTI, T_RIGHT, expected_frames=n)
+    blk = torch.zeros(ymap.block_bytes(n, 2000), dtype=torch.uint8, device="cuda:0")
+    try:
+        fe.process_chunk(d[:2 * chunk])
+        with pytest.raises(RuntimeError):  # the chunk's window solve is pending
+            fe.win.export_block(0, chunk, chunk - 1, 0, blk.data_ptr(), n, 2000)
+        fe.flush()
+        with pytest.raises(RuntimeError):  # frames 20 .. 39 are not recorded yet
+            fe.win.export_block(0, n, n - 1, 0, blk.data_ptr(), n, 2000)
+        with pytest.raises(RuntimeError):  # landmark stride below the window's 2000 slots
+            fe.win.export_block(0, chunk, chunk - 1, 0, blk.data_ptr(), n, 1000)
+        with pytest.raises(RuntimeError):  # more frames than keyframe slots
+            fe.win.export_block(0, chunk, chunk - 1, 0, blk.data_ptr(), chunk - 1, 2000)
+        fe.win.export_block(0, chunk, chunk - 1, 100, blk.data_ptr(), n, 2000)
+        ctx.sync()
+        h, kfs, lms = ymap.parse_block(blk.cpu().numpy())
+        assert int(h["placed"]) == 2 and int(h["n_kf"]) == chunk and int(h["first_frame"]) == 100
+        traj = fe.trajectory()
+        np.testing.assert_array_equal(np.array(kfs["T"]), traj)
+        np.testing.assert_array_equal(np.array(h["chunk"]), traj[-1])
+        for j, lm in enumerate(lms):
+            assert np.all((lm["id"] >> 16) == 100 + j)
+            np.testing.assert_array_equal(lm["X"], fe.records[j].X)
+    finally:
+        fe.close()

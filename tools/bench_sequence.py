@@ -121,6 +121,7 @@ def measure(frames=1000, chunk=20, n_fixed=2, ba_iters=10, repeats=5, cpu_thread
         "spread": round((max(times) - min(times)) / t_med, 4), "seconds": round(t_med, 4),
         "seconds_all_repeats": [round(t, 4) for t in times],
         "phase_seconds": {k: round(v, 4) for k, v in secs[med].items()},
+        "phase_seconds_all_repeats": [{k: round(v, 4) for k, v in sc.items()} for sc in secs],
         "ba_solves": len(ba_log),
         "ba_ms_per_solve": round(1e3 * secs[med].get("ba", 0.0) / max(len(ba_log), 1), 4),
         "landmarks": n_landmarks,

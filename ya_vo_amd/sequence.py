@@ -117,7 +117,7 @@ class SequenceFrontend:
 
     def __init__(self, ctx, chunk: int, K, T_right, n_fixed: int = 2, ba_iters: int = 10,
                  H: int = 376, W: int = 1241, max_kp: int = 2000, match_thr: int = 20, device_window: bool = True,
-                 ba_priority: int = 0, expected_frames: int = 0):
+                 ba_priority: int = 0, expected_frames: int = 0, ba_stream=None):
         """device_window: the BA window is recorded, assembled and written back on the device (yv_ba_window_*,
         no per-chunk read-back); False: the host assembly below (window_problem / apply_window), kept as the
         restatement the device path is checked against. ba_priority: the BA stream's priority (torch's convention:
@@ -159,7 +159,8 @@ class SequenceFrontend:
         self._h_q = pinned(chunk * max_kp * 4)
         self._h_m = pinned(2 * chunk * max_kp * 100)
         self.ba = BundleAdjuster(ctx, window, window * max_kp, 2 * window * max_kp)
-        self.ba_stream = torch.cuda.Stream(device=dev, priority=ba_priority)  # the BA beside the next chunk's kernels
+        # the BA beside the next chunk's kernels (ba_stream: a caller's torch stream, e.g. one kept per context)
+        self.ba_stream = ba_stream if ba_stream is not None else torch.cuda.Stream(device=dev, priority=ba_priority)
         self.ba.set_stream(self.ba_stream.cuda_stream)
         self._ba_pending = False
         self.device_window = device_window
