@@ -51,6 +51,9 @@ void yv_destroy(yv_ctx* ctx);
 /* The stream all yv_* calls on this context use (hipStream_t as void*). */
 void* yv_stream(yv_ctx* ctx);
 /* Block until all work queued on the context stream has finished. */
+/* A second stream of the context on a hardware queue of its own (never the context stream's), made on first use and
+ * kept until yv_destroy: work issued on it overlaps the context stream's (the sequence's BA windows). */
+void* yv_side_stream(yv_ctx* ctx);
 int yv_sync(yv_ctx* ctx);
 /* Synchronous copies between host memory and device memory (e.g. a yv_batch_view array) on the
  * context stream. */

@@ -24,7 +24,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=1000)
     ap.add_argument("--repeats", type=int, default=9)
-    ap.add_argument("--mode", default="new", choices=("new", "precreate", "fixedstream"))
+    ap.add_argument("--mode", default="new", choices=("new", "precreate", "fixedstream", "torchnew"))
+    ap.add_argument("--stress", type=int, default=0, help="torch streams made (and kept) before the frontends")
     ap.add_argument("--priority", type=int, default=0, help="the BA stream's priority (-1 high)")
     ap.add_argument("--gap-ms", type=float, default=0.0)
     a = ap.parse_args()
@@ -39,11 +40,15 @@ def main():
     ctx.set_brief_offsets(np.fromfile(os.path.join(ROOT, "tests", "golden", "brief_offsets_mt19937_42.bin"), np.int8))
     d = torch.from_numpy(fr.reshape(2 * n, *fr.shape[2:])).to("cuda:0")
 
+    keep = [torch.cuda.Stream(device="cuda:0") for _ in range(a.stress)]
     fixed = torch.cuda.Stream(device="cuda:0", priority=a.priority) if a.mode == "fixedstream" else None
 
     def make():
+        # new / precreate: the frontend's default BA stream (the context's side stream); torchnew: a fresh torch stream
+        # per frontend (the round-5 default)
+        s = torch.cuda.Stream(device="cuda:0", priority=a.priority) if a.mode == "torchnew" else fixed
         return SequenceFrontend(ctx, chunk, scene.K_KITTI, T_RIGHT, expected_frames=n, ba_priority=a.priority,
-                                ba_stream=fixed)
+                                ba_stream=s)
 
     def timed(fe):
         sec = {}
@@ -75,7 +80,9 @@ def main():
     if pre:
         for fe in pre:
             fe.close()
-    print(json.dumps({"mode": a.mode, "gap_ms": a.gap_ms, "priority": a.priority, "repeats": out}))
+    print(json.dumps({"mode": a.mode, "gap_ms": a.gap_ms, "priority": a.priority, "stress": a.stress,
+                      "repeats": out}))
+    del keep
     ctx.close()
 
 

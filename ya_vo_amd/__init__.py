@@ -67,6 +67,7 @@ SIGNATURES = {
     "yv_create": (_I, [_I, ctypes.POINTER(_P)]),
     "yv_destroy": (None, [_P]),
     "yv_stream": (_P, [_P]),
+    "yv_side_stream": (_P, [_P]),
     "yv_sync": (_I, [_P]),
     "yv_download": (_I, [_P, _P, _P, ctypes.c_size_t]),
     "yv_upload": (_I, [_P, _P, _P, ctypes.c_size_t]),
@@ -395,6 +396,14 @@ class Context(_GeomMixin):
     @property
     def stream(self) -> int:
         return self.lib.yv_stream(self.handle) or 0
+
+    @property
+    def side_stream(self) -> int:
+        """The context's second stream, on a hardware queue of its own (yv_side_stream)."""
+        s = self.lib.yv_side_stream(self.handle)
+        if not s:
+            raise YavoError("yv_side_stream failed")
+        return s
 
     def sync(self) -> None:
         _check(self.lib.yv_sync(self.handle), "yv_sync")

@@ -159,7 +159,11 @@ class SequenceFrontend:
         self._h_q = pinned(chunk * max_kp * 4)
         self._h_m = pinned(2 * chunk * max_kp * 100)
         self.ba = BundleAdjuster(ctx, window, window * max_kp, 2 * window * max_kp)
-        # the BA beside the next chunk's kernels (ba_stream: a caller's torch stream, e.g. one kept per context)
+        # the BA beside the next chunk's kernels: by default the context's side stream, whose hardware queue is never
+        # the context stream's (a fresh torch stream shares it one time in four and the two serialise: yv_side_stream);
+        # ba_priority != 0 or ba_stream: a stream of the caller's
+        if ba_stream is None and ba_priority == 0:
+            ba_stream = torch.cuda.ExternalStream(ctx.side_stream, device=dev)
         self.ba_stream = ba_stream if ba_stream is not None else torch.cuda.Stream(device=dev, priority=ba_priority)
         self.ba.set_stream(self.ba_stream.cuda_stream)
         self._ba_pending = False
