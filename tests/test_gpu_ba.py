@@ -90,6 +90,23 @@ def test_ba_rejects_bad_graph(ctx):
         ba.set_problem(4, 5, 10, np.array([0, 1], np.int32), el, np.zeros((2, 2)), scene.K_KITTI)
 
 
+@pytest.mark.timeout(300)
+def test_ba_size_limits(ctx):
+    """640 poses is the largest window (6 x 640 rows of the reduced system fit the LDLT's 64 KB of LDS): 641 is refused
+    up front, and so is a debug LDLT above 3840 rows; 3840 itself still launches and solves."""
+    with pytest.raises(yv.YavoError):
+        yv.BundleAdjuster(ctx, 641, 10, 20)
+    yv.BundleAdjuster(ctx, 640, 10, 20).close()
+    with pytest.raises(yv.YavoError):
+        ctx.ba_ldlt(np.eye(3841), np.ones(3841))
+    n = 3840  # a diagonal system: the pivoted LDLT's L is I and D the diagonal, so x = b / d, each one division
+    d = np.linspace(1.0, 2.0, n)
+    b = np.arange(n, dtype=np.float64) + 0.5
+    x, ok = ctx.ba_ldlt(np.diag(d), b)
+    assert ok
+    np.testing.assert_array_equal(x, b / d)
+
+
 def _spd(n, seed, cond=1e3):
     rng = np.random.default_rng(seed)
     Q, _ = np.linalg.qr(rng.normal(size=(n, n)))
