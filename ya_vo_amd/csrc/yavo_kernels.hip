@@ -1295,19 +1295,26 @@ __global__ __launch_bounds__(256) void match_kernel(const Desc* __restrict__ des
 // ------------------------------------------------------------------------------------------------
 // The same matcher on the FP4 matrix cores (train lists <= 2048)
 // ------------------------------------------------------------------------------------------------
-// v_mfma_scale_f32_16x16x128_f8f6f4 with both operands FP4 (e2m1) runs a 16 x 16 x 128 tile in the cycles the
-// int8 form needs for 16 x 16 x 64, so a 256-bit descriptor is two K-steps instead of four and an expanded
-// descriptor is 128 B instead of 256 B (half the LDS staging and fragment reads per distance).  Every bit b
-// becomes the FP4 value b (nibble 0b0010 = 1.0, 0b0000 = 0), and both E8M0 block scales are 2^6, so every
-// product is 4096 * a_k * b_k: exact.  The accumulator is f32 and every partial sum an integer of magnitude
-// < 2^22 (the chain starts from c_j = (2047 - j) - 2048 * popcount(b_j), adds 4096 * popcount(a & b) <= 2^20),
-// so every sum is exact in any order and the chain ends at the int8 kernel's key plus 2^21 exactly:
+// v_mfma_scale_f32_32x32x64_f8f6f4 with both operands FP4 (e2m1): every descriptor bit becomes the FP4 value b
+// (nibble 0b0010 = 1.0, 0b0000 = 0) and both E8M0 block scales are 2^6, so every product is 4096 * a_k * b_k: exact.
+// The accumulator is f32 and every partial sum an integer of magnitude < 2^22 (the chain starts from
+// c_j = (2047 - j) - 2048 * popcount(b_j) + 2^21 and adds 4096 * popcount(a & b) <= 2^20), so every sum is exact in
+// any order and the chain ends at the int8 kernel's key plus 2^21 exactly:
 //   key' = 2048 * (pa - Hamming) + (2047 - j) + 2^21 >= 2^21 - 2^19.
-// Every key' is a positive float (a column past the list starts at 0 and, its staged descriptor being zero, stays
+// Every key' is a positive float (a train row past the list starts at 0 and, its staged descriptor being zero, stays
 // 0), and positive floats order as their bit patterns, so the running maximum is v_max3_u32 on the raw bits (a float
-// max would first canonicalise both MFMA results: three VALU ops per pair of distances instead of one).  Descriptor dword w (32 bits) of lane group g
-// is K-block g of K-step w >> 2 for both operands alike; inside a dword the nibble order is a fixed permutation
-// of the bits (the same for A and B), so the products pair matching bits.
+// max would first canonicalise both MFMA results).
+//
+// Train descriptors are the A operand (rows), queries B (columns).  A 32 x 32 x 64 tile takes 32 cycles and holds
+// the SIMD's vector issue for 8 of them, where the 16 x 16 x 128 form holds 8 of 16 (MI355X_MICROARCH.md), so the
+// running maxima and the staging get 24 free issue cycles per MFMA instead of 8 (tools/mfma_fp4_probe.hip: both
+// forms alone 0.91-0.96 of the FP4 peak at 3 waves per SIMD, their matcher loops without LDS 0.83-0.84; the kernel
+// 1.48 -> 1.43 ms per 4096-pair step, profiles/r06/c12, c14).  With the train list on the rows, a lane's 16
+// accumulators are 16 train descriptors of ONE query, so each query tile keeps one running maximum per lane (the two
+// lane halves merge at the end), and the chain start C(row) = c_j is four ds_read_b128 of the staged c row per
+// 32-train block, shared by every query tile of the wave (no broadcast moves).  Lane (n, h = lane >> 5) of a K-step s
+// holds descriptor dword 2 s + h of its train row / query column, for A and B alike; inside a dword the nibble order
+// is a fixed permutation of the bits (the same for A and B), so the products pair matching bits.
 constexpr int MF_TC = 128;               // train descriptors per LDS chunk
 constexpr int MF_ROW = 9;                // uint4 per expanded train row (8 + 1 pad)
 
@@ -1320,21 +1327,30 @@ __device__ __forceinline__ uint4 expand32_fp4(uint32_t w) {
 }
 
 typedef int mf_v8i __attribute__((ext_vector_type(8)));
-typedef float mf_v4f __attribute__((ext_vector_type(4)));
+typedef float mf_v16f __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ mf_v4f mfma_fp4(const mm_v4i& a, const mm_v4i& b, const mf_v4f& c) {
+__device__ __forceinline__ mf_v16f mfma_fp4_32(const mm_v4i& a, const mm_v4i& b, const mf_v16f& c) {
     // FP4 operands use 4 of the 8 operand registers (the backend narrows them); scales 133 = 2^(133-127) = 64
     const mf_v8i a8 = __builtin_shufflevector(a, a, 0, 1, 2, 3, -1, -1, -1, -1);
     const mf_v8i b8 = __builtin_shufflevector(b, b, 0, 1, 2, 3, -1, -1, -1, -1);
-    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, c, 4, 4, 0, 133, 0, 133);
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, 133, 0, 133);
+}
+
+// running maximum of the 16 keys' of one accumulator (positive floats: bit patterns order as the values)
+__device__ __forceinline__ uint32_t max16_u32(uint32_t best, const mf_v16f& a) {
+    auto u = [&](int i) { return __float_as_uint(a[i]); };
+    const uint32_t m0 = max(u(0), max(u(1), u(2))), m1 = max(u(3), max(u(4), u(5)));
+    const uint32_t m2 = max(u(6), max(u(7), u(8))), m3 = max(u(9), max(u(10), u(11)));
+    const uint32_t m4 = max(u(12), max(u(13), u(14)));
+    const uint32_t m5 = max(m0, max(m1, m2)), m6 = max(m3, max(m4, u(15)));
+    return max(best, max(m5, m6));
 }
 
 template <int QT, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void match_fp4_kernel(const Desc* __restrict__ desc,
-                                                        const int32_t* __restrict__ kp_count,
-                                                        const int32_t* __restrict__ pairs, int max_kp,
-                                                        uint32_t* __restrict__ match_key) {
-    constexpr int QB = 4 * QT * 16;  // queries per workgroup
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void match_fp4_kernel(
+    const Desc* __restrict__ desc, const int32_t* __restrict__ kp_count, const int32_t* __restrict__ pairs, int max_kp,
+    uint32_t* __restrict__ match_key) {
+    constexpr int QB = 4 * QT * 32;  // queries per workgroup
     __shared__ uint4 s_t[2][MF_TC * MF_ROW];
     __shared__ float s_c[2][MF_TC];  // c_j = (2047 - j) - 2048 popcount(b_j) + 2^21, 0 past the list
     const int pair = blockIdx.y;
@@ -1343,38 +1359,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     const int q0 = blockIdx.x * QB;
     if (q0 >= nq) return;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int col = lane & 15, g = lane >> 4;
-    const Desc* qd = desc + (int64_t)qi * max_kp;
+    const int n = lane & 31, h = lane >> 5;
+    const uint32_t* qw = reinterpret_cast<const uint32_t*>(desc + (int64_t)qi * max_kp);
     const uint32_t* tw = reinterpret_cast<const uint32_t*>(desc + (int64_t)ti * max_kp);
-    const Desc* td = desc + (int64_t)ti * max_kp;
 
-    // query fragments: tile qt row (lane & 15) = query q0 + 16 QT wave + 16 qt + (lane & 15); K-step s, lane
-    // group g holds descriptor dword 4 s + g
-    mm_v4i A[QT][2];
+    // query fragments: tile qt column n = query q0 + 32 QT wave + 32 qt + n; the lane loads only its own four dwords
+    // (a whole-descriptor load with a lane-dependent pick went through scratch)
+    mm_v4i B[QT][4];
+    uint32_t raw[QT][4];
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
-        const int q = q0 + 16 * QT * wave + 16 * qt + col;
-        const Desc d = qd[q < nq ? q : 0];
+        const int q = q0 + 32 * QT * wave + 32 * qt + n;
+        const uint32_t* w = qw + (int64_t)(q < nq ? q : 0) * 8 + h;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            // blend, not an index: keeps d in registers
-            const uint32_t w01 = (g & 1) ? d.w[4 * s + 1] : d.w[4 * s];
-            const uint32_t w23 = (g & 1) ? d.w[4 * s + 3] : d.w[4 * s + 2];
-            const uint4 e = expand32_fp4((g & 2) ? w23 : w01);
-            A[qt][s] = mm_v4i{(int)e.x, (int)e.y, (int)e.z, (int)e.w};
-        }
+        for (int s = 0; s < 4; ++s) raw[qt][s] = w[2 * s];
     }
-    uint32_t best[QT][4];  // bits of the largest key' so far (0 = +0.0: at most every key')
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) best[qt][r] = 0u;
+        for (int s = 0; s < 4; ++s) {
+            const uint4 e = expand32_fp4(raw[qt][s]);
+            B[qt][s] = mm_v4i{(int)e.x, (int)e.y, (int)e.z, (int)e.w};
+        }
+    uint32_t best[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) best[qt] = 0u;
 
-    // staging: thread -> (train tt = idx >> 3, descriptor dword u = idx & 7), kF dwords per thread per chunk; the
-    // first MF_TC threads also form train tt = tid's chain start
+    // staging: thread -> (train tt = idx >> 3, descriptor dword u = idx & 7), kF dwords per thread per chunk; train
+    // tt's chain start c_j from the popcounts of its 8 dwords, summed over their 8 consecutive lanes by DPP (waves 0-1
+    // re-reading the chunk's descriptors for it stalled the workgroup on those loads at every chunk)
     constexpr int kF = MF_TC * 8 / 256;
     uint32_t pre[kF];
-    float pre_c = 0.f;
     auto fetch = [&](int t0) {
 #pragma unroll
         for (int k = 0; k < kF; ++k) {
@@ -1382,96 +1397,87 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
             const int t = t0 + tt;
             pre[k] = t < nt ? tw[(int64_t)t * 8 + u] : 0u;
         }
-        // (c_j from the staged dwords by DPP popcount sums over each descriptor's 8 lanes, instead of waves 0-1
-        // re-reading 128 descriptors here, measured slower: match 1.64 -> 1.70 ms per 2048-frame step, r03/c56)
-        if (tid < MF_TC) {
-            const int t = t0 + tid;
-            pre_c = t < nt ? (float)((2047 - t) - 2048 * desc_popcount(td[t]) + (1 << 21)) : 0.f;
-        }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, int t0) {
 #pragma unroll
         for (int k = 0; k < kF; ++k) {
             const int idx = tid + 256 * k, tt = idx >> 3, u = idx & 7;
             s_t[buf][tt * MF_ROW + u] = expand32_fp4(pre[k]);
+            uint32_t pc = __builtin_popcount(pre[k]);
+            pc += xl::dpp<0xB1>(pc);
+            pc += xl::dpp<0x4E>(pc);
+            pc += xl::dpp<0x141>(pc);
+            const int t = t0 + tt;
+            if (u == 0) s_c[buf][tt] = t < nt ? (float)((2047 - t) - 2048 * (int)pc + (1 << 21)) : 0.f;
         }
-        if (tid < MF_TC) s_c[buf][tid] = pre_c;
     };
     if (nt > 0) {
         fetch(0);
-        store(0);
+        store(0, 0);
     }
     int buf = 0;
     for (int t0 = 0; t0 < nt; t0 += MF_TC) {
         const bool more = t0 + MF_TC < nt;
         if (more) fetch(t0 + MF_TC);
         __syncthreads();
-        // two 16-column train tiles per pass: four independent MFMA chains, one v_max3 folds both tiles' keys into
-        // the running maximum; a column past nt starts at 0 (below every real key'), so no select is needed
 #pragma unroll
         for (int tt0 = 0; tt0 < MF_TC; tt0 += 32) {
             if (t0 + tt0 >= nt) break;
-            mm_v4i Ba[2], Bb[2];
+            mm_v4i A[4];
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const uint4 va = s_t[buf][(tt0 + col) * MF_ROW + 4 * s + g];
-                const uint4 vb = s_t[buf][(tt0 + 16 + col) * MF_ROW + 4 * s + g];
-                Ba[s] = mm_v4i{(int)va.x, (int)va.y, (int)va.z, (int)va.w};
-                Bb[s] = mm_v4i{(int)vb.x, (int)vb.y, (int)vb.z, (int)vb.w};
+            for (int s = 0; s < 4; ++s) {
+                const uint4 v = s_t[buf][(tt0 + n) * MF_ROW + 2 * s + h];
+                A[s] = mm_v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
             }
-            const float ca = s_c[buf][tt0 + col], cb = s_c[buf][tt0 + 16 + col];
-            const mf_v4f Ca = {ca, ca, ca, ca}, Cb = {cb, cb, cb, cb};
+            // C(row, :) = c of train tt0 + row; accumulator i is row 8 (i >> 2) + 4 h + (i & 3)
+            mf_v16f C;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 c4 = *reinterpret_cast<const float4*>(&s_c[buf][tt0 + 8 * k + 4 * h]);
+                C[4 * k] = c4.x;
+                C[4 * k + 1] = c4.y;
+                C[4 * k + 2] = c4.z;
+                C[4 * k + 3] = c4.w;
+            }
 #pragma unroll
             for (int qt = 0; qt < QT; qt += 2) {
-                mf_v4f a0 = mfma_fp4(A[qt][0], Ba[0], Ca);
-                mf_v4f b0 = mfma_fp4(A[qt][0], Bb[0], Cb);
-                mf_v4f a1 = mfma_fp4(A[qt + 1][0], Ba[0], Ca);
-                mf_v4f b1 = mfma_fp4(A[qt + 1][0], Bb[0], Cb);
-                a0 = mfma_fp4(A[qt][1], Ba[1], a0);
-                b0 = mfma_fp4(A[qt][1], Bb[1], b0);
-                a1 = mfma_fp4(A[qt + 1][1], Ba[1], a1);
-                b1 = mfma_fp4(A[qt + 1][1], Bb[1], b1);
+                mf_v16f a0 = mfma_fp4_32(A[0], B[qt][0], C);
+                mf_v16f a1 = mfma_fp4_32(A[0], B[qt + 1][0], C);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    best[qt][r] = max(best[qt][r], max(__float_as_uint(a0[r]), __float_as_uint(b0[r])));
-                    best[qt + 1][r] = max(best[qt + 1][r], max(__float_as_uint(a1[r]), __float_as_uint(b1[r])));
+                for (int s = 1; s < 4; ++s) {
+                    a0 = mfma_fp4_32(A[s], B[qt][s], a0);
+                    a1 = mfma_fp4_32(A[s], B[qt + 1][s], a1);
                 }
+                best[qt] = max16_u32(best[qt], a0);
+                best[qt + 1] = max16_u32(best[qt + 1], a1);
             }
         }
         if (more) {
-            store(buf ^ 1);  // the other buffer: last read before the barrier at the top of this chunk
+            store(buf ^ 1, t0 + MF_TC);  // the other buffer: last read before the barrier at the top of this chunk
             buf ^= 1;
         }
     }
-    // the popcount of the query each lane writes (row 4g + (col & 3) of every tile; lanes col >= 4 repeat one of
-    // those), its descriptor loads all issued here at once: read inside the 32 writer branches below, each load was
-    // waited for before its branch joined (match 1.74 -> 1.64 ms per 2048-frame step, profiles/r03/c56)
-    int pa_q[QT];
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt)
-        pa_q[qt] = desc_popcount(qd[min(q0 + 16 * QT * wave + 16 * qt + 4 * g + (col & 3), nq - 1)]);
-    // per query row: max over the 16 lanes (train columns) of its lane group
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
+        uint32_t v = best[qt];
+        v = max(v, (uint32_t)__shfl_xor((int)v, 32, 64));  // the other lane half's 16 rows of each train block
+        // the query's popcount: its expanded fragments hold one set bit per descriptor bit, half in each lane half
+        int pa = 0;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            uint32_t v = best[qt][r];
-            v = max(v, (uint32_t)xl::xor_row_i32<8>((int)v));
-            v = max(v, (uint32_t)xl::xor_row_i32<4>((int)v));
-            v = max(v, (uint32_t)xl::xor_row_i32<2>((int)v));
-            v = max(v, (uint32_t)xl::xor_row_i32<1>((int)v));
-            const int q = q0 + 16 * QT * wave + 16 * qt + 4 * g + r;
-            if (col == r && q < nq) {
-                uint32_t key = 0xFFFFFFFFu;  // empty train set (nt >= 1 always leaves a real key in the row max)
-                if (nt > 0) {
-                    const int iv = (int)__uint_as_float(v) - (1 << 21);
-                    const int pa = pa_q[qt];
-                    const uint32_t d = (uint32_t)(pa - (iv >> 11));
-                    const uint32_t jj = 2047u - ((uint32_t)iv & 2047u);
-                    key = (d << 16) | jj;
-                }
-                match_key[(int64_t)pair * max_kp + q] = key;
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pa += __popc((uint32_t)B[qt][s][r]);
+        pa += __shfl_xor(pa, 32, 64);
+        const int q = q0 + 32 * QT * wave + 32 * qt + n;
+        if (h == 0 && q < nq) {
+            uint32_t key = 0xFFFFFFFFu;  // empty train set
+            if (nt > 0) {
+                const int iv = (int)__uint_as_float(v) - (1 << 21);
+                const uint32_t d = (uint32_t)(pa - (iv >> 11));
+                const uint32_t jj = 2047u - ((uint32_t)iv & 2047u);
+                key = (d << 16) | jj;
             }
+            match_key[(int64_t)pair * max_kp + q] = key;
         }
     }
 }
@@ -1480,7 +1486,7 @@ namespace {
 template <int QT, int WPE>
 void launch_fp4(const Desc* desc, const int32_t* kp_count, const int32_t* pairs, int n_pairs, int max_kp,
                 uint32_t* match_key, hipStream_t s) {
-    constexpr int QB = 4 * QT * 16;
+    constexpr int QB = 4 * QT * 32;
     dim3 grid((max_kp + QB - 1) / QB, n_pairs);
     hipLaunchKernelGGL((match_fp4_kernel<QT, WPE>), grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
 }
@@ -1493,8 +1499,9 @@ void launch_match(const Desc* desc, const int32_t* kp_count, const int32_t* pair
         hipLaunchKernelGGL(match_kernel, grid, dim3(256), 0, s, desc, kp_count, pairs, max_kp, match_key);
         return;
     }
-    // FP4: 8 query tiles per wave, 3 waves per SIMD (measured against 2 / 4 waves and 4 / 16 tiles)
-    launch_fp4<8, 3>(desc, kp_count, pairs, n_pairs, max_kp, match_key, s);
+    // FP4: 4 query tiles of 32 per wave, 3 waves per SIMD (168 VGPRs; 2 tiles at 4 waves per SIMD: 1.60 ms vs 1.43,
+    // profiles/r06/c14)
+    launch_fp4<4, 3>(desc, kp_count, pairs, n_pairs, max_kp, match_key, s);
 }
 
 // ------------------------------------------------------------------------------------------------
