@@ -139,6 +139,66 @@ def test_pose_lm_batch(ctx, oracle):
         np.testing.assert_array_equal(out[offs[i]:offs[i + 1]], oout)
 
 
+def _non_finite_scene(n, seed):
+    """A scene whose prior puts some points exactly in the camera plane (pc_z = 0: u / 0 = inf, 0 / 0 = NaN errors),
+    so the LM's passes meet non-finite operands (the literal J^T Omega J form, lm_pass)."""
+    rng = np.random.default_rng(seed)
+    T = scene.pose([0.0, 0.0, 0.0, 1.0], [0.25, -0.5, -5.0])  # identity rotation: pc = X + t exactly
+    z = rng.uniform(9.0, 40.0, n)
+    X = np.stack([rng.uniform(-0.6, 0.6, n) * z, rng.uniform(-0.25, 0.25, n) * z, z], 1)
+    X[:3, 2] = 5.0                                  # pc_z = 0 under the prior
+    X[3] = [-0.25, 0.5, 5.0]                        # pc = 0: 0 / 0
+    uv = scene.project(T, X) + rng.normal(scale=0.4, size=(n, 2))
+    uv[:4] = [[600.0, 180.0], [10.0, 20.0], [1200.0, 300.0], [607.0, 185.0]]
+    return np.ascontiguousarray(X), np.ascontiguousarray(uv), T
+
+
+def test_pose_lm_non_finite_matches_oracle(ctx, oracle):
+    X, uv, prior = _non_finite_scene(800, 5)
+    T, out, inl = ctx.pose_lm(X, uv, scene.K_KITTI, prior)
+    oT, oout, oinl = oracle.pose_lm(X, uv, scene.K_KITTI, prior, LM_ORDER)
+    assert inl == oinl
+    np.testing.assert_array_equal(out, oout)
+    np.testing.assert_array_equal(T, oT)
+
+
+def test_pose_lm_batch_non_finite_matches_oracle(ctx, oracle):
+    """300 problems (the 256-thread kernel), every 3rd with non-finite operands."""
+    import torch
+    count = 300
+    probs, priors = [], []
+    for i in range(count):
+        if i % 3 == 0:
+            X, uv, prior = _non_finite_scene(600 + i, 100 + i)
+        else:
+            X, uv, T_true, _ = scene.random_scene(600 + i, seed=100 + i, noise_px=0.4)
+            prior = scene.perturb(T_true, np.random.default_rng(i))
+        probs.append((X, uv))
+        priors.append(prior)
+    offs = np.cumsum([0] + [len(p[0]) for p in probs]).astype(np.int32)
+    dev = "cuda:0"
+    d_off = torch.from_numpy(offs).to(dev)
+    d_X = torch.from_numpy(np.ascontiguousarray(np.concatenate([p[0] for p in probs]))).to(dev)
+    d_uv = torch.from_numpy(np.ascontiguousarray(np.concatenate([p[1] for p in probs]))).to(dev)
+    d_K = torch.from_numpy(np.tile(scene.K_KITTI.reshape(1, 9), (count, 1))).to(dev)
+    d_P = torch.from_numpy(np.stack(priors)).to(dev)
+    d_out = torch.zeros(int(offs[-1]), dtype=torch.uint8, device=dev)
+    d_inl = torch.zeros(count, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    assert ctx.lib.yv_pose_lm_batch(ctx.handle, count, d_off.data_ptr(), d_X.data_ptr(), d_uv.data_ptr(),
+                                    d_K.data_ptr(), d_P.data_ptr(), d_out.data_ptr(), d_inl.data_ptr(), None) == 0
+    ctx.sync()
+    P = d_P.cpu().numpy()
+    inl = d_inl.cpu().numpy()
+    out = d_out.cpu().numpy().astype(bool)
+    mode = yv.lm_sum_mode(count)
+    for i in range(count):
+        oT, oout, oinl = oracle.pose_lm(probs[i][0], probs[i][1], scene.K_KITTI, priors[i], mode)
+        assert inl[i] == oinl, i
+        np.testing.assert_array_equal(P[i], oT, err_msg=str(i))
+        np.testing.assert_array_equal(out[offs[i]:offs[i + 1]], oout, err_msg=str(i))
+
+
 @pytest.mark.parametrize("count", [256, 512])
 def test_pose_lm_batch_many_repeatable(ctx, oracle, count):
     """256 / 512 bench-sized problems (the 512- and the 256-thread kernel), launched three times: every launch

@@ -1051,10 +1051,51 @@ __device__ __forceinline__ void lm_accumulate_short(double (&part)[28], const do
     for (int r = 2; r < 6; ++r) part[21 + r] = part[21 + r] + (-(a[r] * e[0] + b[r] * e[1]));
 }
 
+// The literal form of one edge's contributions (rho' Omega with Omega = I spelt out: every product with the literal
+// 0.0 / 1.0), added to partials held in a stack array: only the rare pass that meets a non-finite operand runs it
+// (lm_pass), so its temporaries do not count against the hot loop's registers.
+__device__ __noinline__ void lm_accumulate_literal(double* part, const double* J, double w, const double* e) {
+#pragma unroll 1
+    for (int r = 0; r < 6; ++r) {
+        const double t0 = J[r] * w + J[6 + r] * 0.0;
+        const double t1 = J[r] * 0.0 + J[6 + r] * w;
+#pragma unroll 1
+        for (int c = 0; c <= r; ++c) part[r * (r + 1) / 2 + c] = part[r * (r + 1) / 2 + c] + (t0 * J[c] + t1 * J[6 + c]);
+        const double s0 = (w * J[r]) * 1.0 + (w * J[6 + r]) * 0.0;
+        const double s1 = (w * J[r]) * 0.0 + (w * J[6 + r]) * 1.0;
+        part[21 + r] = part[21 + r] + (-(s0 * e[0] + s1 * e[1]));
+    }
+}
+
+// One edge at T: its error, robust chi2 and weight, and J.  Returns c2 > delta^2 on a robust edge (a Huber weight).
+__device__ __forceinline__ void lm_edge(const double* T, const double* K, const double* xi, const double* mi, int rob,
+                                        double* e, double& chi, double& w, double* J, bool& hub) {
+    double pc[3];
+    se3_act(T, xi, pc);
+    edge_error_pc(pc, K, mi, e);
+    const double c2 = e[0] * e[0] + e[1] * e[1];
+    w = 1.0;
+    chi = c2;
+    // Huber only past delta: skipped by the whole wave when no lane needs it (a per-lane branch is if-converted
+    // into an unconditional sqrt + division)
+    hub = rob && c2 > 1.0;
+    if (__any(hub)) {
+        if (rob) chi = huber_rho(c2, &w);
+    }
+    edge_jacobian_pc(pc, K, J);
+}
+
 // One pass over the active edges at S.T: computeActiveErrors + activeRobustChi2 + buildSystem of g2o's
 // BlockSolver (Huber-weighted J^T J lower triangle, -J^T W e, robust chi2), summed in the oracle's tree
 // order into S.vals[0..28).  Also records S.Tlast (the estimate the active edges' errors refer to).
-
+//
+// g2o forms J^T (rho' Omega) J and -J^T (rho' Omega) e with Omega = I, i.e. products with the literal 0.0 / 1.0 of
+// Omega, and J[1] = J[6] = 0 structurally.  With finite operands those products only contribute signed zeros, which
+// cannot change a partial sum (a partial that starts at +0.0 never becomes -0.0, and p + (+-0) = p for p != 0), so the
+// short form gives bit-identical sums.  A pass in which some edge has a non-finite operand is run again by the whole
+// workgroup in the literal form (for every edge: bit-identical to the short form on the finite ones), with the
+// partials on the stack; the hot loop carries only the short form (the literal form inside it raised the kernel's
+// register demand by ~50 VGPRs).
 template <int NT, typename UV>
 __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, int na, const uint8_t* s_robust,
                                         const double* X, const UV* uv, double* s_red,
@@ -1074,6 +1115,7 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
     double part[kLMVals];
 #pragma unroll
     for (int v = 0; v < kLMVals; ++v) part[v] = 0.0;
+    bool literal = false;
     // the next edge's point / measurement / robust flag are loaded while this one is evaluated (the gathers
     // hit L2: their latency would otherwise be paid once per edge)
     double nx[5] = {0, 0, 0, 0, 0};
@@ -1091,47 +1133,30 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
             nx[0] = X[3 * i]; nx[1] = X[3 * i + 1]; nx[2] = X[3 * i + 2]; nx[3] = (double)uv[2 * i]; nx[4] = (double)uv[2 * i + 1];
             nrob = s_robust[i];
         }
-        double e[2], pc[3];
-        se3_act(T, xi, pc);
-        edge_error_pc(pc, K, mi, e);
-        const double c2 = e[0] * e[0] + e[1] * e[1];
-        double w = 1.0;
-        double chi = c2;
-        // Huber only past delta: skipped by the whole wave when no lane needs it (a per-lane branch is if-converted
-        // into an unconditional sqrt + division)
-        const bool hub = rob && c2 > 1.0;
-        if (__any(hub)) {
-            if ((tid & 63) == 0) S.hub = 1;
-            if (rob) chi = huber_rho(c2, &w);
-        }
+        double e[2], J[12], chi, w;
+        bool hub;
+        lm_edge(T, K, xi, mi, rob, e, chi, w, J, hub);
+        if (__any(hub) && (tid & 63) == 0) S.hub = 1;
         part[27] = part[27] + chi;
-        double J[12];
-        edge_jacobian_pc(pc, K, J);
-        // g2o forms J^T (rho' Omega) J and -J^T (rho' Omega) e with Omega = I, i.e. products with the literal
-        // 0.0 / 1.0 of Omega, and J[1] = J[6] = 0 structurally.  With finite operands those products only
-        // contribute signed zeros, which cannot change a partial sum (a partial that starts at +0.0 never
-        // becomes -0.0, and p + (+-0) = p for p != 0), so the short form below gives bit-identical sums; an
-        // edge with a non-finite operand takes the literal form.
         const double fin = J[0] + J[2] + J[3] + J[4] + J[5] + J[7] + J[8] + J[9] + J[10] + J[11] + w + e[0] + e[1];
-        const bool fin_ok = isfinite(fin);
-        // wave-uniform branch: a per-lane one is if-converted, i.e. both forms computed and selected (+100 FP64 ops)
-        if (__builtin_expect(__all(fin_ok), 1)) {
-            lm_accumulate_short(part, J, w, e);
-        } else if (fin_ok) {
-            lm_accumulate_short(part, J, w, e);
-        } else {
-#pragma unroll
-            for (int r = 0; r < 6; ++r) {
-                const double t0 = J[r] * w + J[6 + r] * 0.0;
-                const double t1 = J[r] * 0.0 + J[6 + r] * w;
-#pragma unroll
-                for (int c = 0; c <= r; ++c)
-                    part[r * (r + 1) / 2 + c] = part[r * (r + 1) / 2 + c] + (t0 * J[c] + t1 * J[6 + c]);
-                const double s0 = (w * J[r]) * 1.0 + (w * J[6 + r]) * 0.0;
-                const double s1 = (w * J[r]) * 0.0 + (w * J[6 + r]) * 1.0;
-                part[21 + r] = part[21 + r] + (-(s0 * e[0] + s1 * e[1]));
-            }
+        literal |= !isfinite(fin);
+        lm_accumulate_short(part, J, w, e);
+    }
+    if (__syncthreads_or(literal)) {
+        // the rare pass: every edge again in the literal form, partials on the stack, in the same order
+        double lp[kLMVals];
+        for (int v = 0; v < kLMVals; ++v) lp[v] = 0.0;
+        for (int a = tid; a < na; a += NT) {
+            const int i = s_active[a];
+            const double xi[3] = {X[3 * i], X[3 * i + 1], X[3 * i + 2]}, mi[2] = {(double)uv[2 * i], (double)uv[2 * i + 1]};
+            double e[2], J[12], chi, w;
+            bool hub;
+            lm_edge(T, K, xi, mi, s_robust[i], e, chi, w, J, hub);
+            lp[27] = lp[27] + chi;
+            lm_accumulate_literal(lp, J, w, e);
         }
+#pragma unroll
+        for (int v = 0; v < kLMVals; ++v) part[v] = lp[v];
     }
 #ifdef YAVO_LM_PROFILE
     const unsigned long long p1 = __builtin_readcyclecounter();
@@ -1154,10 +1179,15 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
 // Problem p owns edges [offsets[p], offsets[p+1]) (CSR) or, with counts != nullptr, [p*stride, p*stride +
 // counts[p]) (the batch's fixed-stride track layout).  The prior is read from priors[p] and the estimate
 // written to poses[p] (the two may alias).
-// Register budget of the LM: 2 waves per SIMD = 256 VGPRs and no AGPRs (36 B of scratch), so a SIMD running an LM
-// wave keeps 256 registers for the image kernels beside it (4 detect waves instead of 3): 125k -> 131k frames/s.
-// 3 / 4 (168 / 128 VGPRs) spill 400-600 B per lane in the lane-0 LDLT and triple the LM's latency.
-#define YAVO_LM_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+// Register budget of the LM: 3 waves per SIMD = 168 VGPRs.  With the literal J^T Omega J form out of the edge loop
+// (lm_pass) the hot loop fits without spills (the stack partials and the call of the rare literal pass are the
+// kernel's only scratch), and two LM waves leave a SIMD 176 registers for BRIEF / top-K beside them instead of 48:
+// 230.1 k -> 233.7 k frames/s, the LM itself 2.29 -> 2.12 ms per launch in the step (profiles/r06/c19).  (At 256
+// VGPRs, before the literal form moved out, the kernel took 229-241 and the edge loop spilled at 168.)
+#ifndef YAVO_LM_WPE
+#define YAVO_LM_WPE 3
+#endif
+#define YAVO_LM_ATTR __attribute__((amdgpu_waves_per_eu(YAVO_LM_WPE)))
 template <int NT>
 __device__ __forceinline__ void pose_lm_body(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
                                                       int stride, const double* __restrict__ Xall,
