@@ -942,15 +942,19 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
     const int32_t* bo = band_off + (int64_t)img * (kMaxBands + 1);
     const int lo = bo[band], nbk = bo[band + 1] - lo;
     const int4* kb = reinterpret_cast<const int4*>(kp_band) + (int64_t)img * max_kp + lo;
-    // Every global load of the workgroup is issued up front, in this order: the band's keypoint records (<= 4096 = 4
-    // per thread), then the band (<= 4 16-B words per thread).  vmcnt retires loads in order, so the list packing
-    // below waits only for the records while the band's loads stay in flight behind it.
+    // Every global load of the workgroup is issued up front: the band's keypoint records (<= 4096 = 4 per thread),
+    // then the band itself by LDS-DMA (global_load_lds_dwordx4: word k of the band lands at s4[k] with no VGPR
+    // destination; the LDS address is the wave's base + 16 x lane, and word k = tid + u BR_NT is lane-linear).  Staging
+    // the band through registers held 16 VGPRs per thread across the loads: the kernel took 46, and beside two pose-LM
+    // waves on a SIMD (2 x 168 of 512 registers) a 16-wave BRIEF workgroup fits only at <= 40.
+    // (unconditional loads from a valid record -- the image's first when the band has none -- so no branch merge
+    // waits for them before the band's loads are issued; lanes past nbk ignore theirs)
     int4 kq[4];
+    const int4* kbv = nbk > 0 ? kb : reinterpret_cast<const int4*>(kp_band) + (int64_t)img * max_kp;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int j = u * BR_NT + tid;
-        kq[u] = make_int4(0, 0, 0, 0);
-        if (j < nbk) kq[u] = kb[j];
+        kq[u] = kbv[j < nbk ? j : 0];
     }
     // band: rows rb .. rb + BR_ROWS - 1 (rb = r0 - 8) of the pitched blurred image as 16-B words, LS bytes per row
     // (LS <= the pitch: inside the row); column W of row r is patched with pixel (r + 1, 0) (0 past the image), rows
@@ -960,21 +964,34 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
     const int rb = r0 - 8;
     const int wpr = LS >> 4;              // 16-B words per LDS row
     const int nw = BR_ROWS * wpr;
-    const int kw_fix = W >> 4, sh_fix = 8 * (W & 3), dw_fix = (W >> 2) & 3;
-    uint4 v[4];
+    const int kw_fix = W >> 4;
+    uint4* s4 = reinterpret_cast<uint4*>(s_band);
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    const int wbase = tid & ~63;
+    // the zero words first: an LDS store issued while LDS-DMA loads are in flight waits for them all
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int k = tid + u * BR_NT;
+        const int r = rb + k / wpr;
+        if (k < nw && (r < 0 || r >= H)) s4[k] = make_uint4(0, 0, 0, 0);
+    }
     uint32_t nx[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int k = tid + u * BR_NT;
         const int j = k / wpr, q = k - j * wpr;
         const int r = rb + j;
-        v[u] = make_uint4(0, 0, 0, 0);
         nx[u] = 0u;
         if (k < nw && r >= 0 && r < H) {
-            v[u] = reinterpret_cast<const uint4*>(b + (int64_t)r * bp)[q];
+            __builtin_amdgcn_global_load_lds(b + (int64_t)r * bp + 16 * q, (lds_ptr_t)(s4 + wbase + u * BR_NT), 16, 0,
+                                             0);
             if (q == kw_fix && r + 1 < H) nx[u] = (uint32_t)b[(int64_t)(r + 1) * bp];
         }
     }
+    // every load is in flight: one wait for all of them (consumed earlier, the records were waited for one by one)
+    __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) asm volatile("" : "+v"(kq[u].x), "+v"(kq[u].y), "+v"(kq[u].w), "+v"(nx[u]));
     // 1. this band's keypoints (any order: each keypoint's outputs go to its own slot)
     if (tid == 0) s_n = nbk;
 #pragma unroll
@@ -983,24 +1000,17 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
         if (j < nbk)
             s_list[j] = ((uint32_t)kq[u].w << 16) | ((uint32_t)kq[u].y << 5) | (uint32_t)(kq[u].x - r0);
     }
-    // 2. the band to LDS (the word holding column W takes the next row's first pixel)
-    uint4* s4 = reinterpret_cast<uint4*>(s_band);
+    // 2. column W of each row: the byte after the row's last pixel takes the next row's first pixel, written by the
+    // lane whose LDS-DMA word holds it, after its own loads have landed
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int k = tid + u * BR_NT;
-        if (k < nw) {
-            uint4 w = v[u];
-            if (k - (k / wpr) * wpr == kw_fix) {
-                const uint32_t m = ~(0xFFu << sh_fix);
-                if (dw_fix == 0) w.x = (w.x & m) | (nx[u] << sh_fix);
-                else if (dw_fix == 1) w.y = (w.y & m) | (nx[u] << sh_fix);
-                else if (dw_fix == 2) w.z = (w.z & m) | (nx[u] << sh_fix);
-                else w.w = (w.w & m) | (nx[u] << sh_fix);
-            }
-            s4[k] = w;
-        }
+        const int j = k / wpr, q = k - j * wpr;
+        const int r = rb + j;
+        if (k < nw && q == kw_fix && r >= 0 && r < H) s_band[16 * k + (W & 15)] = (uint8_t)nx[u];
     }
-    // wide images (W > 1320): the rest of the band, word by word
+    // wide images (W > 1320): the rest of the band, word by word through registers
+    const int sh_fix = 8 * (W & 3), dw_fix = (W >> 2) & 3;
     for (int k = tid + 4 * BR_NT; k < nw; k += BR_NT) {
         const int j = k / wpr, q = k - j * wpr;
         const int r = rb + j;
