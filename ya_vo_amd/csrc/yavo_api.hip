@@ -25,6 +25,7 @@ struct yv_ctx {
     int max_corners = 2000;    // include/FastDetector.hpp:36
     uint16_t k9[9] = {12, 22, 31, 41, 44, 41, 31, 22, 12};  // cv::GaussianBlur 9x9, sigma 2.5, 8U
     int8_t* d_offsets = nullptr;                              // [256*4]
+    int offsets_version = 0;                                  // bumped by yv_set_brief_offsets
     yv_batch* single = nullptr;                               // workspace of the host-pointer API
     int32_t* h_pinned = nullptr;                              // small pinned scratch for counts
     void* scratch = nullptr;                                  // device arena of the geometry host calls
@@ -86,6 +87,8 @@ struct yv_batch {
     int32_t* kp_band = nullptr;     // [slot][max_kp] int4 {row, col, id, slot}: the kept keypoints by BRIEF band
     int32_t* band_off = nullptr;    // [slot][kMaxBands + 1]
     int32_t* brief_loff = nullptr;  // [256][2] BRIEF test offsets in the band's LDS layout (launch_brief)
+    int loff_version = -1;          // the ctx offsets_version brief_loff was formed from (-1: never)
+    bool counts_copied = false;     // this run's finalize wrote kp_count_build (the asynchronous build's copy)
     yv_keypoint* keypoints = nullptr;
     Desc* desc = nullptr;
     uint8_t* blur = nullptr;
@@ -541,6 +544,7 @@ int yv_set_brief_offsets(yv_ctx* ctx, const int8_t* offsets) {
     if (set_device(ctx) != YV_OK) return YV_ERR_HIP;
     YV_HIP(hipMemcpyAsync(ctx->d_offsets, offsets, 1024, hipMemcpyHostToDevice, ctx->stream));
     YV_HIP(hipStreamSynchronize(ctx->stream));
+    ++ctx->offsets_version;
     return YV_OK;
 }
 
@@ -737,18 +741,27 @@ int yv_batch_run(yv_batch* b, const uint8_t* d_images, int n_images, int stride,
     // the previous track's build (beside detect and top-K) reads keypoints / matches: BRIEF and finalize rewrite them
     // (its keypoint counts are a copy, kp_count_build, so top-K need not wait)
     rc |= join_build(b, s);
+    // the tests' LDS offsets depend on the offsets table and W only: formed again only when the table changed (a
+    // 256-thread launch in the step waited ~15-50 us for a CU behind the side stream's LM, profiles/r06/c17)
+    const bool new_loff = b->loff_version != ctx->offsets_version;
+    b->loff_version = ctx->offsets_version;
     yavo::launch_brief(b->blur, n_images, H, W, ctx->d_offsets, b->kp_src, b->kp_band, b->band_off, K, b->keypoints,
-                       b->desc, b->brief_loff, s);
+                       b->desc, b->brief_loff, new_loff, s);
     rc |= record_stage(b, s, run, 3);
     if (b->overlap_mode == 3) rc |= launch_deferred_after(b, s);  // after describe
     if (b->n_pairs > 0) {
         yavo::launch_match(b->desc, b->kp_count, b->pairs, b->n_pairs, K, K, b->match_key, s);
         rc |= record_stage(b, s, run, 4);
+        // the asynchronous edge build reads a copy of the keypoint counts (the next run's top-K rewrites them):
+        // the finalize kernel writes it, where a separate device copy waited ~50 us for a CU at the end of the step
+        const bool copy_counts = b->overlap && b->build_async && b->lk_step == 0;
         yavo::launch_match_finalize(b->match_key, b->keypoints, b->kp_count, b->pairs, b->n_pairs, K, match_thr,
                                     b->matches, b->match_count, b->filtered, b->filt_count, b->match_dj,
-                                    b->match_lim, s);
+                                    b->match_lim, s, copy_counts ? b->kp_count_build : nullptr, b->nslots);
+        b->counts_copied = copy_counts;
     } else {
         rc |= record_stage(b, s, run, 4);
+        b->counts_copied = false;
     }
     rc |= record_stage(b, s, run, 5);
     if (rc != YV_OK) return YV_ERR_HIP;
@@ -1028,8 +1041,9 @@ int batch_track(yv_batch* b, const double* d_priors, double* d_poses, void* stre
         // the build (match: edges from the run's matches; LK: pyramids, flow, edges) waits for the run on s and
         // leaves s free for the next run's detect; the match build reads a copy of the keypoint counts
         if (b->lk_step == 0) {
-            YV_HIP(hipMemcpyAsync(b->kp_count_build, b->kp_count, sizeof(int32_t) * (size_t)b->nslots,
-                                  hipMemcpyDeviceToDevice, s_run));
+            if (!b->counts_copied)
+                YV_HIP(hipMemcpyAsync(b->kp_count_build, b->kp_count, sizeof(int32_t) * (size_t)b->nslots,
+                                      hipMemcpyDeviceToDevice, s_run));
             build_counts = b->kp_count_build;
         }
         YV_HIP(hipEventRecord(b->ev_fin, s_run));
@@ -1211,8 +1225,10 @@ int yv_describe(yv_ctx* ctx, const uint8_t* img, int H, int W, int stride, const
     yavo::launch_blur9(b->staging, 1, H, W, W, (int64_t)H * W, ctx->k9, b->blur, s);
     yavo::launch_kp_boundary(b->det_rc, b->det_count, 1, H, W, b->max_kp, b->kp_src, b->kp_count, b->kp_band,
                              b->band_off, s);
+    const bool new_loff = b->loff_version != ctx->offsets_version;
+    b->loff_version = ctx->offsets_version;
     yavo::launch_brief(b->blur, 1, H, W, ctx->d_offsets, b->kp_src, b->kp_band, b->band_off, b->max_kp, b->keypoints,
-                       b->desc, b->brief_loff, s);
+                       b->desc, b->brief_loff, new_loff, s);
     if (check_launch() != YV_OK) return YV_ERR_HIP;
     YV_HIP(stage_d2h(ctx, ctx->h_pinned + 2, b->kp_count, sizeof(int32_t), s));
     YV_HIP(stage_sync(ctx, s));

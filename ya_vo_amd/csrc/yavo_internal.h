@@ -69,11 +69,11 @@ void launch_topk(const uint64_t* cand_keys, int64_t cap, uint32_t* cand_count, u
 void launch_kp_boundary(const int32_t* det_rc, const int32_t* det_count, int n_images, int H, int W,
                         int max_kp, int32_t* kp_src, int32_t* kp_count, int32_t* kp_band, int32_t* band_off,
                         hipStream_t s);
-// BRIEF: writes KeyPoint records + packed descriptors.  loff: a 2 KB device scratch of the caller (the tests' LDS
-// offsets for this W, rewritten by every launch on stream s).
+// BRIEF: writes KeyPoint records + packed descriptors.  loff: a 2 KB device scratch of the caller holding the tests'
+// LDS offsets for this W, formed on stream s first when new_loff (the offsets table or W changed since it was formed).
 void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t* offsets,
                   const int32_t* kp_src, const int32_t* kp_band, const int32_t* band_off, int max_kp,
-                  yv_keypoint* keypoints, Desc* desc, int32_t* loff, hipStream_t s);
+                  yv_keypoint* keypoints, Desc* desc, int32_t* loff, bool new_loff, hipStream_t s);
 // Pack KeyPoint records -> descriptors (host-supplied keypoints).
 void launch_pack_desc(const yv_keypoint* keypoints, const int32_t* kp_count, int n_slots, int max_kp,
                       Desc* desc, hipStream_t s);
@@ -86,7 +86,8 @@ void launch_match(const Desc* desc, const int32_t* kp_count, const int32_t* pair
 void launch_match_finalize(uint32_t* match_key, const yv_keypoint* keypoints,
                            const int32_t* kp_count, const int32_t* pairs, int n_pairs, int max_kp,
                            int thr, yv_match* matches, int32_t* match_count, yv_match* filtered,
-                           int32_t* filt_count, int2* match_dj, int32_t* match_lim, hipStream_t s);
+                           int32_t* filt_count, int2* match_dj, int32_t* match_lim, hipStream_t s,
+                           int32_t* kp_count_copy = nullptr, int n_slots = 0);  // + kp_count[0, n_slots) -> copy
 // removeOutliers on externally supplied Matches records (one list).
 void launch_filter_records(const yv_match* in, int n, int thr, yv_match* out, int32_t* out_count,
                            hipStream_t s);

@@ -1101,11 +1101,11 @@ __global__ void brief_loff_kernel(const int8_t* __restrict__ offsets, int LS, in
 
 void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t* offsets, const int32_t* kp_src,
                   const int32_t* kp_band, const int32_t* band_off, int max_kp, yv_keypoint* keypoints, Desc* desc,
-                  int32_t* loff, hipStream_t s) {
+                  int32_t* loff, bool new_loff, hipStream_t s) {
     dim3 grid(((H + BR_BAND - 1) / BR_BAND) * n_images);
     const size_t lds = (size_t)BR_ROWS * brief_lds_stride(W);
     int2* lo = reinterpret_cast<int2*>(loff);
-    hipLaunchKernelGGL(brief_loff_kernel, dim3(1), dim3(256), 0, s, offsets, brief_lds_stride(W), lo);
+    if (new_loff) hipLaunchKernelGGL(brief_loff_kernel, dim3(1), dim3(256), 0, s, offsets, brief_lds_stride(W), lo);
     hipLaunchKernelGGL(brief_kernel, grid, dim3(BR_NT), lds, s, blur, H, W, kp_src, kp_band, band_off, max_kp,
                        keypoints, desc, lo);
 }
@@ -1541,8 +1541,12 @@ __global__ __launch_bounds__(FZ_NT) void match_finalize_kernel(
     uint32_t* __restrict__ match_key, const yv_keypoint* __restrict__ keypoints,
     const int32_t* __restrict__ kp_count, const int32_t* __restrict__ pairs, int max_kp, int thr,
     yv_match* __restrict__ matches, int32_t* __restrict__ match_count, yv_match* __restrict__ filtered,
-    int32_t* __restrict__ filt_count, int2* __restrict__ match_dj, int32_t* __restrict__ match_lim) {
+    int32_t* __restrict__ filt_count, int2* __restrict__ match_dj, int32_t* __restrict__ match_lim,
+    int32_t* __restrict__ kp_count_copy, int n_slots) {
     __shared__ int s_dist[kMaxKp];
+    // the edge build's copy of the run's keypoint counts (the last writer of kp_count, top-K, ran before this kernel)
+    if (kp_count_copy && blockIdx.x == 0)
+        for (int i = (int)threadIdx.x; i < n_slots; i += FZ_NT) kp_count_copy[i] = kp_count[i];
     __shared__ int s_j[kMaxKp];
     __shared__ int s_pos[kMaxKp];
     __shared__ int s_tmp[40];
@@ -1631,9 +1635,10 @@ __global__ __launch_bounds__(FZ_NT) void match_finalize_kernel(
 void launch_match_finalize(uint32_t* match_key, const yv_keypoint* keypoints, const int32_t* kp_count,
                            const int32_t* pairs, int n_pairs, int max_kp, int thr, yv_match* matches,
                            int32_t* match_count, yv_match* filtered, int32_t* filt_count, int2* match_dj,
-                           int32_t* match_lim, hipStream_t s) {
+                           int32_t* match_lim, hipStream_t s, int32_t* kp_count_copy, int n_slots) {
     hipLaunchKernelGGL(match_finalize_kernel, dim3(n_pairs), dim3(FZ_NT), 0, s, match_key, keypoints, kp_count,
-                       pairs, max_kp, thr, matches, match_count, filtered, filt_count, match_dj, match_lim);
+                       pairs, max_kp, thr, matches, match_count, filtered, filt_count, match_dj, match_lim,
+                       kp_count_copy, n_slots);
 }
 
 // removeOutliers over a caller-supplied Matches list (n <= kMaxKp), one workgroup.
