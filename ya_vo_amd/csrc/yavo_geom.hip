@@ -982,11 +982,14 @@ __device__ __forceinline__ void rs_level(const double* in, double* out, int lane
     if (up) v += h;
 }
 
+// flag (optional): read by every thread after the reduction's first barrier and returned (the pass's literal-form
+// flag rides on the reduction's barriers instead of a barrier of its own); thread 0 clears it after the last one.
 template <int NV, int NT>
-__device__ void lm_reduce(double (&part)[NV], double* red /* >= NV * NT / 64 */, double* out,
-                          unsigned long long* t_sync = nullptr) {
+__device__ int lm_reduce(double (&part)[NV], double* red /* >= NV * NT / 64 */, double* out,
+                         unsigned long long* t_sync = nullptr, int* flag = nullptr) {
     static_assert(NV == 28, "the reduce-scatter schedule is written for 28 values");
     constexpr int W = NT / 64;
+    static_assert(W >= 2, "the flag hand-off needs the two barriers of the multi-wave form");
 #ifdef YAVO_LM_PROFILE
     if (t_sync) *t_sync = __builtin_readcyclecounter();
 #endif
@@ -1000,13 +1003,9 @@ __device__ void lm_reduce(double (&part)[NV], double* red /* >= NV * NT / 64 */,
     rs_level<2, 2>(a2, a1, lane, v);
     const double tot = a1[0] + xl::xor_row_f64<1>(a1[0]);
     const bool owner = v < NV && (lane & 1) == 0;
-    if (W == 1) {
-        if (owner) out[v] = tot;
-        __syncthreads();
-        return;
-    }
     if (owner) red[(tid >> 6) * NV + v] = tot;
     __syncthreads();
+    const int f = flag ? *flag : 0;
     if (tid < NV) {
         double q = red[tid];
 #pragma unroll
@@ -1014,6 +1013,8 @@ __device__ void lm_reduce(double (&part)[NV], double* red /* >= NV * NT / 64 */,
         out[tid] = q;
     }
     __syncthreads();
+    if (flag && tid == 0 && f) *flag = 0;  // every thread read it before the barrier above; set again next pass
+    return f;
 }
 
 struct LMShared {
@@ -1023,6 +1024,7 @@ struct LMShared {
     double lambda, ni, currentChi, tempChi, rho;
     int flag;  // control broadcast from lane 0
     int hub;   // a Huber weight (c2 > delta^2 on a robust edge) was applied in some pass of the current round
+    int lit;   // some edge of the current pass had a non-finite operand (lm_pass: the pass is redone literally)
 };
 
 constexpr int kLMVals = 28;  // 21 lower-triangle H entries + 6 b + 1 chi2
@@ -1142,7 +1144,22 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
         literal |= !isfinite(fin);
         lm_accumulate_short(part, J, w, e);
     }
-    if (__syncthreads_or(literal)) {
+    if (literal) S.lit = 1;
+#ifdef YAVO_LM_PROFILE
+    const unsigned long long p1 = __builtin_readcyclecounter();
+    unsigned long long ps = 0;
+    const int lit = lm_reduce<kLMVals, NT>(part, s_red, S.vals, &ps, &S.lit);
+    if (lmp) {
+        const unsigned long long p2 = __builtin_readcyclecounter();
+        lmp[0] += p1 - p0;
+        lmp[1] += p2 - ps;  // the reduction proper
+        lmp[8] += ps - p1;  // waiting at the first barrier for the other waves' edges
+        lmp[9] += 1;        // passes (error + system evaluations)
+    }
+#else
+    const int lit = lm_reduce<kLMVals, NT>(part, s_red, S.vals, nullptr, &S.lit);
+#endif
+    if (lit) {
         // the rare pass: every edge again in the literal form, partials on the stack, in the same order
         double lp[kLMVals];
         for (int v = 0; v < kLMVals; ++v) lp[v] = 0.0;
@@ -1157,37 +1174,29 @@ __device__ __forceinline__ void lm_pass(LMShared& S, const int16_t* s_active, in
         }
 #pragma unroll
         for (int v = 0; v < kLMVals; ++v) part[v] = lp[v];
+        lm_reduce<kLMVals, NT>(part, s_red, S.vals);
     }
-#ifdef YAVO_LM_PROFILE
-    const unsigned long long p1 = __builtin_readcyclecounter();
-#endif
-#ifdef YAVO_LM_PROFILE
-    unsigned long long ps = 0;
-    lm_reduce<kLMVals, NT>(part, s_red, S.vals, &ps);
-    if (lmp) {
-        const unsigned long long p2 = __builtin_readcyclecounter();
-        lmp[0] += p1 - p0;
-        lmp[1] += p2 - ps;  // the reduction proper
-        lmp[8] += ps - p1;  // waiting at the first barrier for the other waves' edges
-        lmp[9] += 1;        // passes (error + system evaluations)
-    }
-#else
-    lm_reduce<kLMVals, NT>(part, s_red, S.vals);
-#endif
 }
 
 // Problem p owns edges [offsets[p], offsets[p+1]) (CSR) or, with counts != nullptr, [p*stride, p*stride +
 // counts[p]) (the batch's fixed-stride track layout).  The prior is read from priors[p] and the estimate
 // written to poses[p] (the two may alias).
-// Register budget of the LM: 3 waves per SIMD = 168 VGPRs.  With the literal J^T Omega J form out of the edge loop
-// (lm_pass) the hot loop fits without spills (the stack partials and the call of the rare literal pass are the
-// kernel's only scratch), and two LM waves leave a SIMD 176 registers for BRIEF / top-K beside them instead of 48:
-// 230.1 k -> 233.7 k frames/s, the LM itself 2.29 -> 2.12 ms per launch in the step (profiles/r06/c19).  (At 256
-// VGPRs, before the literal form moved out, the kernel took 229-241 and the edge loop spilled at 168.)
-#ifndef YAVO_LM_WPE
-#define YAVO_LM_WPE 3
-#endif
+// Register budget of the LM.  The 256-thread form (the batch of a step's 2048 tracks, beside top-K and BRIEF): 3 waves
+// per SIMD = 168 VGPRs.  With the literal J^T Omega J form out of the edge loop (lm_pass) the hot loop fits without
+// spills (the stack partials and the call of the rare literal pass are the kernel's only scratch), and two LM waves
+// leave a SIMD 176 registers for BRIEF / top-K beside them instead of 48: 230.1 k -> 233.7 k frames/s, the LM itself
+// 2.29 -> 2.12 ms per launch in the step (profiles/r06/c19).  The 512-thread form (one problem of the LoopHandler, the
+// sequence's 20-track batches) keeps 2 waves per SIMD = 256: at 168 its single-problem latency rose ~9% (the pose LM
+// 54 -> 60 ms of a 200-frame LoopHandler run, profiles/r06/c27).
+template <int NT>
+struct LMWaves {
+    static constexpr int value = NT >= 512 ? 2 : 3;
+};
+#ifdef YAVO_LM_WPE
 #define YAVO_LM_ATTR __attribute__((amdgpu_waves_per_eu(YAVO_LM_WPE)))
+#else
+#define YAVO_LM_ATTR __attribute__((amdgpu_waves_per_eu(LMWaves<NT>::value)))
+#endif
 template <int NT>
 __device__ __forceinline__ void pose_lm_body(const int32_t* __restrict__ offsets, const int32_t* __restrict__ counts,
                                                       int stride, const double* __restrict__ Xall,
@@ -1213,6 +1222,7 @@ __device__ __forceinline__ void pose_lm_body(const int32_t* __restrict__ offsets
     const double* uv = uvall + 2 * e0;
     if (tid < 9) S.K[tid] = Kall[9 * prob + tid];
     if (tid < 7) S.T[tid] = priors[7 * prob + tid];
+    if (tid == 0) S.lit = 0;
     for (int i = tid; i < n; i += NT) {
         s_level[i] = 0;
         s_out[i] = 0;
