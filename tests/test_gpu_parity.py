@@ -141,6 +141,21 @@ def test_describe_boundary_and_out_of_buffer(ctx, oracle, offsets):
     assert len(ctx.describe(img, np.zeros((0, 2), np.int32))) == 0
 
 
+def test_describe_after_new_offsets(ctx, oracle, offsets):
+    """The batch forms the tests' LDS offsets once per offsets table: a new table (yv_set_brief_offsets) between two
+    calls on the same workspace must take effect, and restoring the first one must too."""
+    img = _images()["synth_kitti_1234"]
+    orc, _, _ = oracle.fast(img, 2000)
+    other = np.random.default_rng(5).integers(-8, 9, offsets.shape).astype(np.int8)
+    try:
+        np.testing.assert_array_equal(ctx.describe(img, orc), oracle.brief(img, orc, offsets))
+        ctx.set_brief_offsets(other)
+        np.testing.assert_array_equal(ctx.describe(img, orc), oracle.brief(img, orc, other))
+    finally:
+        ctx.set_brief_offsets(offsets)
+    np.testing.assert_array_equal(ctx.describe(img, orc), oracle.brief(img, orc, offsets))
+
+
 def test_describe_golden(ctx):
     b = np.load(os.path.join(GOLDEN, "brief_golden.npz"))
     g = np.load(os.path.join(GOLDEN, "fast_golden.npz"))
