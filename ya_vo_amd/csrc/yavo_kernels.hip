@@ -215,6 +215,10 @@ struct K9 {
     // sum of the taps <= 256: every rounded output (acc + 2^15) >> 16 is <= 255 and acc < 2^24, so the output byte
     // is byte 2 of the accumulator and needs no clamp (OpenCV's bit-exact kernels sum to exactly 256)
     int byte2;
+    // horizontal pass on the int8 matrix cores (every tap <= 127): pixels enter as p - 128, so the sums are offset by
+    // 128 * (sum of the taps), the accumulators' start value
+    int mfma;
+    int hbias;
 };
 
 static K9 make_k9(const uint16_t* k9) {
@@ -233,6 +237,10 @@ static K9 make_k9(const uint16_t* k9) {
         kw.kvo[t] = tap(2 * t - 1) | (tap(2 * t) << 16);
     }
     kw.byte2 = sum <= 256 ? 1 : 0;
+    uint32_t mx = 0;
+    for (int i = 0; i < 9; ++i) mx = k9[i] > mx ? k9[i] : mx;
+    kw.mfma = mx <= 127 ? 1 : 0;
+    kw.hbias = (int)(128 * sum);
     return kw;
 }
 
@@ -302,6 +310,7 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
     uint32_t* hbuf = s_share;
     __shared__ uint16_t s_pos[FT_W * FT_H];
     __shared__ uint32_t s_n, s_npre, s_base;
+    __shared__ uint32_t s_band[4 * 9];  // kh[r][M] at r * 9 + M + 3 for M in -3 .. 5 (0 outside 0 .. 2): the B operand
     DP_DECL
     // 1-D grid, XCD-aware: an image's tiles (and the halo rows neighbouring tiles share) stay in one XCD's L2
     const int ntx = (W + FT_W - 1) / FT_W, nty = (H + FT_H - 1) / FT_H;
@@ -315,6 +324,16 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
     if (tid == 0) {
         s_n = 0;
         s_npre = 0;
+    }
+    if (kBlur && tid < 4 * 9) {
+        const int r = tid / 9, M = tid - 9 * r - 3;
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int m = 0; m < 3; ++m)
+                if (r == j && M == m) v = kw.kh[j][m];
+        s_band[tid] = v;
     }
 
     // stage (FT_H + 8) x (FT_W + 8) = 64 x 72 bytes, one LDS dword per load: 5 per thread, all in flight before the
@@ -474,7 +493,43 @@ __global__ __launch_bounds__(256) void detect_kernel(const uint8_t* __restrict__
     const uint32_t n = s_n;
     // one global atomic per workgroup reserves the output range of this tile's corners
     if (tid == 0 && n > 0) s_base = atomicAdd(&cand_count[img], n);
-    if (kBlur) {
+    if (kBlur && kw.mfma) {
+        // horizontal pass on the int8 matrix cores: the 64 x 64 h of the tile (all 64 LDS rows, the 64 output
+        // columns) is 4 x 4 blocks of 16 x 16, block (rb, cb) = A (tile rows 16 rb .., LDS columns 16 cb .. 16 cb + 63,
+        // as p - 128) x B (the banded taps: B[k][n] = tap(k - n)), one v_mfma_i32_16x16x64_i8 each, wave rb taking
+        // row block rb.  Exact: |products| and sums are integers far inside i32, and the accumulators start at
+        // 128 * sum(taps), so acc = sum_t tap(t) p[x + t] (<= 65280: 16 bits).  A lane (n, g) of K-block g holds
+        // bytes 16 g .. 16 g + 15 of its row / column for A and B alike (the pairing is by K index, the same for
+        // both); B's dword jj is kh[n & 3][4 g + jj - (n >> 2)] (0 outside 0 .. 2), read from s_band.  LDS columns
+        // past 71 (cb = 3) meet zero taps.  Output lane (n, g) holds rows 4 g .. 4 g + 3 of column n: rows 4g, 4g + 1
+        // pack into h row pair 8 rb + 2 g, as the vertical pass reads them.  VALU per wave: 4 x (4 xor + 2 packs)
+        // where the v_dot4 form took ~60: detect alone 2.766 -> 2.743 ms (profiles/r06/c41).  The four lane groups'
+        // row pairs share banks (4-way conflicts on these 8 stores); a 72-dword row-pair stride cost 1 KB of LDS and
+        // the 8th workgroup per CU (2.92 ms), an XOR swizzle of the column groups cost the vertical pass more VALU than
+        // the conflicts (2.82 ms; c42-c44).
+        typedef int dt_v4i __attribute__((ext_vector_type(4)));
+        const int n = lane & 15, g = lane >> 4;
+        dt_v4i B;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int M = 4 * g + jj - (n >> 2);
+            B[jj] = (M >= -3 && M <= 5) ? (int)s_band[(n & 3) * 9 + M + 3] : 0;
+        }
+        const dt_v4i C = {kw.hbias, kw.hbias, kw.hbias, kw.hbias};
+        const int rb = ty;
+        const uint8_t* arow = &tile[(16 * rb + n) * FT_LW + 16 * g];
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+            const uint2 lo = *reinterpret_cast<const uint2*>(arow + 16 * cb);
+            const uint2 hi = *reinterpret_cast<const uint2*>(arow + 16 * cb + 8);
+            const dt_v4i A = {(int)(lo.x ^ 0x80808080u), (int)(lo.y ^ 0x80808080u), (int)(hi.x ^ 0x80808080u),
+                              (int)(hi.y ^ 0x80808080u)};
+            const dt_v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B, C, 0, 0, 0);
+            const int q = 8 * rb + 2 * g, x = 16 * cb + n;
+            hbuf[q * FT_W + x] = (uint32_t)acc[0] | ((uint32_t)acc[1] << 16);
+            hbuf[(q + 1) * FT_W + x] = (uint32_t)acc[2] | ((uint32_t)acc[3] << 16);
+        }
+    } else if (kBlur) {
         // horizontal pass, exact: h = sum_j k_j * p[x + j] as two v_dot4_u32_u8 + one mad on the byte row
         // (rows start 4-byte aligned: FT_LW = 72).  h <= 255 * 256 fits 16 bits; rows 2q and 2q+1 are
         // packed into one dword so the vertical pass can use v_dot2_u32_u16.  One item = 4 adjacent
