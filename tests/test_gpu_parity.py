@@ -216,6 +216,31 @@ def _device_frames(ctx, frames):
     return t
 
 
+@pytest.mark.parametrize("k9", [[2, 9, 25, 44, 96, 44, 25, 9, 2], [0, 0, 0, 28, 200, 28, 0, 0, 0]])
+def test_batch_blur_custom_taps(ctx, oracle, k9):
+    """The detect kernel's fused blur with other tap sets (yv_set_blur_kernel): taps <= 127 take the int8
+    matrix-core horizontal pass (its accumulator bias is 128 x the taps' sum), a tap above 127 the v_dot4 form; both
+    byte-equal to the oracle's blur with the same taps, a border image shape included."""
+    import torch  # noqa: F401
+    default = np.array(yv.DEFAULT_BLUR_KERNEL, np.uint16)
+    for H, W in ((376, 1241), (77, 150)):
+        frames = np.stack([synth_frame(5 + i, i, 2 * i, H, W) for i in range(2)])
+        b = yv.Batch(ctx, 2, H, W, 2000, 0)
+        try:
+            ctx.set_blur_kernel(np.array(k9, np.uint16))
+            d = _device_frames(ctx, frames)
+            b.run(d.data_ptr(), 2, W, H * W, 20)
+            ctx.sync()
+            v = b.view()
+            bp = v.blur_pitch
+            for i in range(2):
+                blur = ctx.download(v.blurred + i * H * bp, np.uint8, H * bp).reshape(H, bp)[:, :W]
+                np.testing.assert_array_equal(blur, oracle.blur(frames[i], np.array(k9, np.uint16)))
+        finally:
+            ctx.set_blur_kernel(default)
+            b.close()
+
+
 def test_batch_pipeline_matches_oracle(ctx, oracle, offsets):
     """Stereo sequence through the device pipeline: images [L0, R0, L1, R1, ...], pairs temporal
     (L_{k-1} -> L_k, as buildInitMap / reinitialize) and stereo (L_k -> R_k); two runs chained through the
