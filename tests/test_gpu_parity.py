@@ -141,6 +141,16 @@ def test_describe_boundary_and_out_of_buffer(ctx, oracle, offsets):
     assert len(ctx.describe(img, np.zeros((0, 2), np.int32))) == 0
 
 
+@pytest.mark.parametrize("W", [1321, 1700])
+def test_describe_wide_image(ctx, oracle, offsets, W):
+    """Rows wider than 1320 px: the band has more 16-B words than four per thread, so its first 4 x 1024 words come
+    by LDS-DMA and the rest through registers (brief_kernel), each with its own column-W patch."""
+    img = synth_frame(3, 0, 0, 120, W)
+    orc, _, _ = oracle.fast(img, 2000)
+    assert len(orc) > 100
+    np.testing.assert_array_equal(ctx.describe(img, orc), oracle.brief(img, orc, offsets))
+
+
 def test_describe_after_new_offsets(ctx, oracle, offsets):
     """The batch forms the tests' LDS offsets once per offsets table: a new table (yv_set_brief_offsets) between two
     calls on the same workspace must take effect, and restoring the first one must too."""
