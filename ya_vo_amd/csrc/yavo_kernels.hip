@@ -979,10 +979,14 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
                                                     const int32_t* __restrict__ band_off, int max_kp,
                                                     yv_keypoint* __restrict__ keypoints, Desc* __restrict__ desc,
                                                     const int2* __restrict__ loff) {
-    extern __shared__ uint8_t s_band[];  // BR_ROWS * brief_lds_stride(W) bytes
-    // this band's keypoints, packed (index << 16) | (col << 5) | (row - r0): index < 4096, col < 2048, 32-row band
-    __shared__ uint32_t s_list[kMaxKp];
-    __shared__ int s_n;
+    // All of the workgroup's LDS is dynamic, from a 16-B aligned base: static __shared__ variables would precede the
+    // dynamic region unpadded (16,388 B of them put the band at 4 mod 16), and the band's 16-B LDS-DMA and zero-word
+    // stores then run off their natural alignment.  Layout: the band (BR_ROWS * LS bytes, LS a multiple of 16), this
+    // band's keypoints packed (index << 16) | (col << 5) | (row - r0) (index < 4096, col < 2048, 32-row band), the
+    // count (launch_brief sizes the region).
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_band[];
+    uint32_t* s_list = reinterpret_cast<uint32_t*>(s_band + BR_ROWS * brief_lds_stride(W));
+    int& s_n = *reinterpret_cast<int*>(s_list + kMaxKp);
     BP_DECL
     // 1-D grid, XCD-aware: neighbouring bands of an image (17 shared rows) stay in one XCD's L2
     const int nbands = (H + BR_BAND - 1) / BR_BAND;
@@ -1158,7 +1162,7 @@ void launch_brief(const uint8_t* blur, int n_images, int H, int W, const int8_t*
                   const int32_t* kp_band, const int32_t* band_off, int max_kp, yv_keypoint* keypoints, Desc* desc,
                   int32_t* loff, bool new_loff, hipStream_t s) {
     dim3 grid(((H + BR_BAND - 1) / BR_BAND) * n_images);
-    const size_t lds = (size_t)BR_ROWS * brief_lds_stride(W);
+    const size_t lds = (size_t)BR_ROWS * brief_lds_stride(W) + sizeof(uint32_t) * kMaxKp + 16;
     int2* lo = reinterpret_cast<int2*>(loff);
     if (new_loff) hipLaunchKernelGGL(brief_loff_kernel, dim3(1), dim3(256), 0, s, offsets, brief_lds_stride(W), lo);
     hipLaunchKernelGGL(brief_kernel, grid, dim3(BR_NT), lds, s, blur, H, W, kp_src, kp_band, band_off, max_kp,
