@@ -25,6 +25,7 @@ constexpr int kMaxWidth = 2048;  // image width limit (BRIEF keeps 49 rows of th
 // BRIEF workgroup reads its band's keypoints only; H <= kBandRows * kMaxBands.
 constexpr int kBandRows = 32;
 constexpr int kMaxBands = 256;
+constexpr int kBandCounters = 1024;  // top-K's (band, bank class) counters: 32 classes up to 32 bands, else 1
 constexpr int kFastTileW = 64;     // FAST / blur output tile: one wave per tile row
 constexpr int kFastTileH = 56;
 // The blurred image (detect's second output, BRIEF's input) is stored with a 128-B aligned row pitch, so the

@@ -727,15 +727,27 @@ __device__ __forceinline__ bool brief_boundary(int row, int col, int H, int W) {
 
 // Compacts points 0..K-1 (rc_at(i) -> int2 {row, col}) to those inside checkBoundry, keeping order;
 // kp_src[slot] = {row, col, id = input index, 0}.  Chunks of 4 * NT points, 4 consecutive per thread.  The kept
-// points are also bucketed by BRIEF band (row / kBandRows): kp_band = {row, col, id, slot} grouped by band (any order
-// inside a band), band_off[b] = the first entry of band b, band_off[nb] = the count (nb = bands of H rows).  A second
-// pass recomputes the same flags and slots and places each point after its band's counter.
+// points are also bucketed by BRIEF band (row / kBandRows): kp_band = {row, col, id, slot} grouped by band,
+// band_off[b] = the first entry of band b, band_off[nb] = the count (nb = bands of H rows).  Inside a band the points
+// are grouped by the LDS bank of their patch centre in brief_kernel's band layout (bank_classes(nb) classes), which
+// deals each 32-lane group of its descriptor waves keypoints of distinct banks (any order inside a class).  A second
+// pass recomputes the same flags and slots and places each point after its (band, class) counter.
+__host__ __device__ constexpr int bank_classes(int nb) { return nb <= kBandCounters / 32 ? 32 : 1; }
+
 template <int NT, class RcAt>
 __device__ void boundary_compact(RcAt rc_at, int K, int H, int W, int32_t* kp_src, int32_t* kp_count,
                                  int32_t* kp_band, int32_t* band_off, int* s_tmp, int* s_band) {
     const int tid = threadIdx.x;
     const int nb = (H + kBandRows - 1) / kBandRows;
-    for (int b = tid; b < nb; b += NT) s_band[b] = 0;
+    const int C = bank_classes(nb), nbc = nb * C;
+    const int LS = brief_lds_stride(W);
+    // (band, class) of a point: the dword bank of its centre byte (row - r0 + 8) * LS + col in the band's LDS copy
+    auto bucket = [&](int row, int col) -> int {
+        const int band = row / kBandRows;
+        const int cls = C == 1 ? 0 : ((((row - band * kBandRows + 8) * LS + col) >> 2) & 31);
+        return band * C + cls;
+    };
+    for (int b = tid; b < nbc; b += NT) s_band[b] = 0;
     __syncthreads();
     int base = 0;
     for (int pass = 0; pass < 2; ++pass) {
@@ -761,12 +773,12 @@ __device__ void boundary_compact(RcAt rc_at, int K, int H, int W, int32_t* kp_sr
             for (int u = 0; u < 4; ++u) {
                 const int i = c0 + tid * 4 + u;
                 if (flags[u]) {
-                    const int band = rcs[u].x / kBandRows;
+                    const int bk = bucket(rcs[u].x, rcs[u].y);
                     if (pass == 0) {
                         reinterpret_cast<int4*>(kp_src)[off] = make_int4(rcs[u].x, rcs[u].y, i, 0);
-                        atomicAdd(&s_band[band], 1);
+                        atomicAdd(&s_band[bk], 1);
                     } else {
-                        const int pos = atomicAdd(&s_band[band], 1);
+                        const int pos = atomicAdd(&s_band[bk], 1);
                         reinterpret_cast<int4*>(kp_band)[pos] = make_int4(rcs[u].x, rcs[u].y, i, off);
                     }
                     off++;
@@ -775,16 +787,21 @@ __device__ void boundary_compact(RcAt rc_at, int K, int H, int W, int32_t* kp_sr
             base += total;
         }
         __syncthreads();
-        if (pass == 0 && tid == 0) {
-            // band counts -> first entries (the second pass's cursors) and the offsets table
+        if (pass == 0) {
+            // (band, class) counts -> first entries (the second pass's cursors) and the band offsets table
             int acc = 0;
-            for (int b = 0; b < nb; ++b) {
-                const int c = s_band[b];
-                s_band[b] = acc;
-                band_off[b] = acc;
-                acc += c;
+            for (int b0 = 0; b0 < nbc; b0 += NT) {
+                const int j = b0 + tid;
+                const int c = j < nbc ? s_band[j] : 0;
+                int tot = 0;
+                const int first = acc + block_excl_scan<NT>(c, s_tmp, &tot);
+                if (j < nbc) {
+                    s_band[j] = first;
+                    if (j % C == 0) band_off[j / C] = first;
+                }
+                acc += tot;
             }
-            band_off[nb] = acc;
+            if (tid == 0) band_off[nb] = acc;
         }
         __syncthreads();
     }
@@ -806,7 +823,7 @@ __global__ __launch_bounds__(NT) void topk_kernel(const uint64_t* __restrict__ c
     __shared__ uint64_t s_keys[kMaxKp];
     __shared__ uint32_t s_hist[256];
     __shared__ int s_tmp[40];
-    __shared__ int s_band[kMaxBands];
+    __shared__ int s_band[kBandCounters];
     __shared__ uint64_t s_prefix, s_mask;
     __shared__ int s_krem, s_done, s_n;
 
@@ -924,7 +941,7 @@ __global__ __launch_bounds__(TK_NT) void kp_boundary_kernel(const int32_t* __res
                                                             int32_t* __restrict__ kp_count, int32_t* __restrict__ kp_band,
                                                             int32_t* __restrict__ band_off) {
     __shared__ int s_tmp[40];
-    __shared__ int s_band[kMaxBands];
+    __shared__ int s_band[kBandCounters];
     const int img = blockIdx.x;
     int K = det_count[img];
     if (K > max_kp) K = max_kp;
@@ -1100,11 +1117,16 @@ __global__ __launch_bounds__(BR_NT) void brief_kernel(const uint8_t* __restrict_
     // VALU of per-keypoint ballot / emit work per wave in the lanes = tests form.
     uint8_t* rec_b = reinterpret_cast<uint8_t*>(keypoints + (int64_t)img * max_kp);
     Desc* d_base = desc + (int64_t)img * max_kp;
-    const int nitems = ((nb + 63) >> 6) * 4;
+    // s_list is grouped by the bank of the patch centre (boundary_compact's classes, ~G entries each): lane kd of the
+    // dealt order takes entry (kd % 32) * G + kd / 32, so the 32 lanes of a group take entries G apart, about one per
+    // class -- distinct banks for every test's uniform offset, up to a carry -- where neighbouring entries share one
+    const int G = (nb + 31) >> 5;
+    const int nitems = ((32 * G + 63) >> 6) * 4;
     // the item index in an SGPR (tid >> 6 is not known to be wave-uniform): loff then comes by scalar loads
     for (int item = __builtin_amdgcn_readfirstlane(wave); item < nitems; item += BR_NW) {
-        const int g = item & 3, k = (item >> 2) * 64 + lane;
-        const bool act = k < nb;
+        const int g = item & 3, kd = (item >> 2) * 64 + lane;
+        const int k = (kd & 31) * G + (kd >> 5);
+        const bool act = (kd >> 5) < G && k < nb;
         const uint32_t e = s_list[act ? k : nb - 1];
         const int i = (int)(e >> 16), row = r0 + (int)(e & 31u), col = (int)((e >> 5) & 2047u);
         const int id = (act && g == 0) ? src[i].z : 0;
